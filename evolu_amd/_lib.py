@@ -1,0 +1,104 @@
+"""ctypes binding of the C ABI in include/evm.h (libevm.so, built in-tree).
+
+There is no fallback: if the HIP library is missing or cannot be loaded the
+import of anything that computes raises, by design.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libevm.so")
+
+EVM_OK = 0
+EVM_EINVAL = 1
+EVM_ENONCANON = 2
+EVM_ECOLLISION = 3
+EVM_ERANGE = 4
+EVM_ETREE = 5
+EVM_EDEVICE = 6
+EVM_ENOMEM = 7
+EVM_ECAPACITY = 8
+
+META_CASEMASK = 0x0000FFFF
+META_VALID = 0x00010000
+META_NONCANON = 0x00020000
+META_RANGE = 0x00040000
+
+MSG_UPS = 0x01
+MSG_XOR = 0x02
+MSG_INS = 0x04
+MSG_BAD = 0x80
+
+DIFF_NONE = -1
+DIFF_RANGE_ERROR = -2
+
+REC_BYTES = 32  # sizeof(evm_rec)
+
+_vp = C.c_void_p
+_sz = C.c_size_t
+_u32 = C.c_uint32
+_i = C.c_int
+
+# name -> (restype, argtypes); every symbol include/evm.h declares.
+SIGNATURES = {
+    "evm_create": (_i, [_i, C.POINTER(_vp)]),
+    "evm_destroy": (None, [_vp]),
+    "evm_strerror": (C.c_char_p, [_i]),
+    "evm_set_stream": (_i, [_vp, _vp]),
+    "evm_get_stream": (_vp, [_vp]),
+    "evm_sync": (_i, [_vp]),
+    "evm_dev_alloc": (_i, [_vp, _sz, C.POINTER(_vp)]),
+    "evm_dev_free": (_i, [_vp, _vp]),
+    "evm_copy_h2d": (_i, [_vp, _vp, _vp, _sz]),
+    "evm_copy_d2h": (_i, [_vp, _vp, _vp, _sz]),
+    "evm_pack": (_i, [_vp, _vp, _sz, _sz, _vp, _vp]),
+    "evm_tree_new": (_i, [_vp, _u32, C.POINTER(_vp)]),
+    "evm_tree_from_leaves": (_i, [_vp, _u32, _vp, _vp, _vp, C.POINTER(_vp)]),
+    "evm_tree_free": (_i, [_vp, _vp]),
+    "evm_tree_info": (_i, [_vp, C.POINTER(_u32), C.POINTER(C.c_uint64)]),
+    "evm_tree_device": (_i, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)]),
+    "evm_tree_leaves": (_i, [_vp, _vp, _vp, _vp, _vp]),
+    "evm_tree_roots": (_i, [_vp, _vp, _vp, _vp]),
+    "evm_tree_to_json": (_i, [_vp, _vp, _u32, _vp, _sz, C.POINTER(_sz)]),
+    "evm_tree_from_json": (_i, [_vp, _u32, C.POINTER(C.c_char_p), C.POINTER(_sz), C.POINTER(_vp)]),
+    "evm_merkle_insert": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, C.POINTER(_vp)]),
+    "evm_merkle_diff": (_i, [_vp, _vp, _vp, _vp]),
+    "evm_apply_batch": (
+        _i,
+        [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _vp, C.POINTER(_vp)],
+    ),
+}
+
+_LIB = None
+
+
+class EngineError(RuntimeError):
+    def __init__(self, status: int, where: str):
+        self.status = status
+        msg = _LIB.evm_strerror(status).decode() if _LIB is not None else str(status)
+        super().__init__("%s: %s (status %d)" % (where, msg, status))
+
+
+def load(path: str = LIB_PATH):
+    """Loads libevm.so (raises if absent: there is no CPU fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise RuntimeError(
+            "libevm.so not built (%s); run `python -c 'import __graft_entry__ as g; g.build()'`" % path
+        )
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(status: int, where: str):
+    if status != EVM_OK:
+        raise EngineError(status, where)

@@ -1,0 +1,932 @@
+// MI355X (gfx950) batch-merge engine for Evolu's CRDT sync path: kernels +
+// the C ABI declared in include/evm.h.
+//
+// Reference semantics restated here (harrywebdev/evolu @ 2025-01-31):
+//   applyMessages.ts:26-131   LWW decisions per message, in batch order
+//   merkleTree.ts:8-50        XOR of murmur3(ts) along the base-3 minute key
+//   merkleTree.ts:52-91       greedy diff descent
+//   apps/server/src/index.ts  per-owner INSERT OR IGNORE + XOR (see evm_server.hip)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "evm_device.hpp"
+#include "evm_internal.hpp"
+#include "evm_prims.hpp"
+
+using namespace evm;
+
+// ============================================================================
+// K1: pack
+// ============================================================================
+constexpr int PACK_THREADS = 256;
+
+__global__ __launch_bounds__(PACK_THREADS) void k_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
+                                                       const u32* __restrict__ aux, u32 aux_limit,
+                                                       evm_rec* __restrict__ out, Info* __restrict__ info) {
+  u32 bad = 0, bad_aux = 0, mn = 0xffffffffu, mx = 0u;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    u32 w[12];
+    load_ts(ts, stride, i, w);
+    const Parsed p = parse_ts46(w);
+    evm_rec r;
+    r.tc = p.tc;
+    r.node = p.node;
+    r.meta = p.meta;
+    r.hash = p.hash;
+    r.minute = p.minute;
+    r.aux = aux ? aux[i] : 0u;
+    if (aux_limit && r.aux >= aux_limit) bad_aux = 1;
+    out[i] = r;
+    if (p.meta & EVM_META_VALID) {
+      mn = min(mn, p.minute);
+      mx = max(mx, p.minute);
+    } else {
+      bad = 1;
+    }
+  }
+  // wave reduce then one atomic per wave
+  for (int d = 32; d >= 1; d >>= 1) {
+    bad |= __shfl_xor(bad, d, 64);
+    bad_aux |= __shfl_xor(bad_aux, d, 64);
+    mn = min(mn, (u32)__shfl_xor(mn, d, 64));
+    mx = max(mx, (u32)__shfl_xor(mx, d, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (bad) atomicOr(&info->bad, 1u);
+    if (bad_aux) atomicOr(&info->bad_aux, 1u);
+    if (mn != 0xffffffffu) {
+      atomicMin(&info->minute_min, mn);
+      atomicMax(&info->minute_max, mx);
+    }
+  }
+}
+
+static int grid_for(size_t n, int threads, int cap = 8192) {
+  size_t g = (n + threads - 1) / threads;
+  if (g < 1) g = 1;
+  if (g > (size_t)cap) g = cap;
+  return (int)g;
+}
+
+int evm::launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,
+                     Info* info) {
+  if (n == 0) return EVM_OK;
+  hipLaunchKernelGGL(k_pack, dim3(grid_for(n, PACK_THREADS, 4096)), dim3(PACK_THREADS), 0, ctx->stream,
+                     (const uint8_t*)ts, stride, n, aux, aux_limit, out, info);
+  return hip_ok(hipGetLastError());
+}
+
+// ============================================================================
+// Scans and sorts (host drivers for evm_prims.hpp)
+// ============================================================================
+template <typename T, template <typename> class Op>
+int evm::scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out, T* total_dev) {
+  if (n == 0) {
+    if (total_dev) HIPR(hipMemsetAsync(total_dev, 0, sizeof(T), ctx->stream));
+    return EVM_OK;
+  }
+  const size_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+  T* part = S.alloc<T>(nt);
+  if (!part) return EVM_ENOMEM;
+  hipLaunchKernelGGL((k_scan_reduce<T, Op<T>>), dim3(nt), dim3(SCAN_THREADS), 0, ctx->stream, in, n, part);
+  hipLaunchKernelGGL((k_scan_partials<T, Op<T>>), dim3(1), dim3(1024), 0, ctx->stream, part, nt, total_dev);
+  hipLaunchKernelGGL((k_scan_down<T, Op<T>>), dim3(nt), dim3(SCAN_THREADS), 0, ctx->stream, in, n, part, out);
+  return hip_ok(hipGetLastError());
+}
+template int evm::scan_exclusive<u32, OpAdd>(evm_ctx*, Scratch&, const u32*, size_t, u32*, u32*);
+template int evm::scan_exclusive<int32_t, OpXor>(evm_ctx*, Scratch&, const int32_t*, size_t, int32_t*, int32_t*);
+
+template <typename K>
+int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t n, int lo_bit, int hi_bit) {
+  if (n <= 1 || hi_bit <= lo_bit) return EVM_OK;
+  const int B = hi_bit - lo_bit;
+  const int passes = (B + RADIX_BITS - 1) / RADIX_BITS;
+  const int width = (B + passes - 1) / passes;
+  const u32 ntiles = (u32)((n + SORT_TILE - 1) / SORT_TILE);
+  K* k2 = S.alloc<K>(n);
+  u32* v2 = S.alloc<u32>(n);
+  u32* counts = S.alloc<u32>((size_t)RADIX_BINS * ntiles);
+  u32* offs = S.alloc<u32>((size_t)RADIX_BINS * ntiles);
+  if (!k2 || !v2 || !counts || !offs) return EVM_ENOMEM;
+  int shift = lo_bit;
+  for (int p = 0; p < passes; ++p) {
+    const int bits = std::min(width, hi_bit - shift);
+    hipLaunchKernelGGL((k_radix_hist<K>), dim3(ntiles), dim3(SORT_THREADS), 0, ctx->stream, keys, n, shift, bits, counts,
+                       ntiles);
+    int st = scan_exclusive<u32, OpAdd>(ctx, S, counts, (size_t)(1u << bits) * ntiles, offs, (u32*)nullptr);
+    if (st) return st;
+    hipLaunchKernelGGL((k_radix_scatter<K>), dim3(ntiles), dim3(SORT_THREADS), 0, ctx->stream, keys, vals, k2, v2, n,
+                       shift, bits, offs, ntiles);
+    std::swap(keys, k2);
+    std::swap(vals, v2);
+    shift += bits;
+  }
+  return hip_ok(hipGetLastError());
+}
+template int evm::radix_sort_pairs<u32>(evm_ctx*, Scratch&, u32*&, u32*&, size_t, int, int);
+template int evm::radix_sort_pairs<u64>(evm_ctx*, Scratch&, u64*&, u32*&, size_t, int, int);
+
+// ============================================================================
+// Trees: leaf lists keyed by ck = owner << 40 | code, sorted, unique.
+// ============================================================================
+__global__ void k_iota(u32* __restrict__ v, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) v[i] = (u32)i;
+}
+
+// Fold input: for every selected message, (owner << 40 | code(minute), hash).
+__global__ void k_fold_prep(const evm_rec* __restrict__ rec, const uint8_t* __restrict__ flags, uint8_t sel_mask,
+                            const u32* __restrict__ pos, int owner_mode, const u32* __restrict__ cell_owner, size_t n,
+                            u64* __restrict__ ck, u32* __restrict__ h, Info* __restrict__ info) {
+  u64 mn = ~0ull, mx = 0ull;
+  u32 maxlen = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    if (flags && !(flags[i] & sel_mask)) continue;
+    const evm_rec r = rec[i];
+    const u32 owner = owner_mode == OWNER_CELL ? cell_owner[r.aux] : (owner_mode == OWNER_AUX ? r.aux : 0u);
+    const u64 c = ((u64)owner << 40) | minute_code(r.minute);
+    const size_t o = pos ? pos[i] : i;
+    ck[o] = c;
+    h[o] = r.hash;
+    mn = min(mn, c);
+    mx = max(mx, c);
+    maxlen = max(maxlen, (u32)base3_len(r.minute));
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    mn = min(mn, (u64)__shfl_xor(mn, d, 64));
+    mx = max(mx, (u64)__shfl_xor(mx, d, 64));
+    maxlen = max(maxlen, (u32)__shfl_xor(maxlen, d, 64));
+  }
+  if ((threadIdx.x & 63) == 0 && mx >= mn) {
+    atomicMin(&info->ck_min, mn);
+    atomicMax(&info->ck_max, mx);
+    atomicMax(&info->maxlen, maxlen);
+  }
+}
+
+__global__ void k_sel_u32(const uint8_t* __restrict__ flags, uint8_t mask, size_t n, u32* __restrict__ sel) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    sel[i] = (flags[i] & mask) ? 1u : 0u;
+}
+
+__global__ void k_heads(const u64* __restrict__ ck, size_t m, u32* __restrict__ head) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < m; p += (size_t)gridDim.x * blockDim.x)
+    head[p] = (p == 0 || ck[p] != ck[p - 1]) ? 1u : 0u;
+}
+
+__global__ void k_run_starts(const u64* __restrict__ ck, const u32* __restrict__ head, const u32* __restrict__ lid,
+                             size_t m, u32* __restrict__ start, u64* __restrict__ out_ck) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < m; p += (size_t)gridDim.x * blockDim.x)
+    if (head[p]) {
+      start[lid[p]] = (u32)p;
+      out_ck[lid[p]] = ck[p];
+    }
+}
+
+__global__ void k_run_xor(const u32* __restrict__ start, const int32_t* __restrict__ pfx, const u32* __restrict__ nrun,
+                          size_t m, int32_t* __restrict__ out_xr) {
+  const u32 L = *nrun;
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < L; r += (size_t)gridDim.x * blockDim.x) {
+    const u32 a = start[r], b = (r + 1 < L) ? start[r + 1] : (u32)m;
+    out_xr[r] = pfx[b] ^ pfx[a];
+  }
+}
+
+// Reduces sorted (ck, h) runs of equal ck to unique leaves (ck, xor).
+// Returns the leaf count (host sync).
+int evm::reduce_runs(evm_ctx* ctx, Scratch& S, const u64* ck, const int32_t* h, size_t m, u64* out_ck, int32_t* out_xr,
+                     uint64_t* out_count) {
+  if (m == 0) {
+    *out_count = 0;
+    return EVM_OK;
+  }
+  u32* head = S.alloc<u32>(m);
+  u32* lid = S.alloc<u32>(m);
+  u32* start = S.alloc<u32>(m);
+  int32_t* pfx = S.alloc<int32_t>(m + 1);
+  u32* nrun = S.alloc<u32>(1);
+  if (!head || !lid || !start || !pfx || !nrun) return EVM_ENOMEM;
+  const int g = grid_for(m, 256);
+  hipLaunchKernelGGL(k_heads, dim3(g), dim3(256), 0, ctx->stream, ck, m, head);
+  int st = scan_exclusive<u32, OpAdd>(ctx, S, head, m, lid, nrun);
+  if (st) return st;
+  st = scan_exclusive<int32_t, OpXor>(ctx, S, h, m, pfx, pfx + m);
+  if (st) return st;
+  hipLaunchKernelGGL(k_run_starts, dim3(g), dim3(256), 0, ctx->stream, ck, head, lid, m, start, out_ck);
+  hipLaunchKernelGGL(k_run_xor, dim3(g), dim3(256), 0, ctx->stream, start, pfx, nrun, m, out_xr);
+  u32 L = 0;
+  HIPR(hipMemcpyAsync(&L, nrun, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  *out_count = L;
+  return hip_ok(hipGetLastError());
+}
+
+__device__ __forceinline__ size_t lower_bound_u64(const u64* a, size_t lo, size_t hi, u64 x) {
+  while (lo < hi) {
+    const size_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ size_t upper_bound_u64(const u64* a, size_t lo, size_t hi, u64 x) {
+  while (lo < hi) {
+    const size_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Merge of two sorted unique leaf lists; equal keys land adjacent (A first).
+__global__ void k_merge_a(const u64* __restrict__ ack, const int32_t* __restrict__ axr, size_t na, const u64* __restrict__ bck,
+                          size_t nb, u64* __restrict__ ock, int32_t* __restrict__ oxr) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t j = lower_bound_u64(bck, 0, nb, ack[i]);
+    ock[i + j] = ack[i];
+    oxr[i + j] = axr[i];
+  }
+}
+__global__ void k_merge_b(const u64* __restrict__ bck, const int32_t* __restrict__ bxr, size_t nb, const u64* __restrict__ ack,
+                          size_t na, u64* __restrict__ ock, int32_t* __restrict__ oxr) {
+  for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = upper_bound_u64(ack, 0, na, bck[j]);
+    ock[i + j] = bck[j];
+    oxr[i + j] = bxr[j];
+  }
+}
+
+__global__ void k_owner_off(const u64* __restrict__ ck, size_t L, u32 n_owners, u64* __restrict__ off) {
+  for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o <= n_owners; o += (size_t)gridDim.x * blockDim.x)
+    off[o] = (o == n_owners) ? (u64)L : (u64)lower_bound_u64(ck, 0, L, (u64)o << 40);
+}
+
+static int tree_alloc(evm_tree* t, u32 n_owners, uint64_t L) {
+  t->n_owners = n_owners;
+  t->n_leaves = L;
+  t->off = nullptr;
+  t->ck = nullptr;
+  t->xr = nullptr;
+  t->pfx = nullptr;
+  if (hipMalloc(&t->off, sizeof(u64) * (n_owners + 1)) != hipSuccess) return EVM_ENOMEM;
+  if (hipMalloc(&t->ck, sizeof(u64) * std::max<uint64_t>(L, 1)) != hipSuccess) return EVM_ENOMEM;
+  if (hipMalloc(&t->xr, sizeof(int32_t) * std::max<uint64_t>(L, 1)) != hipSuccess) return EVM_ENOMEM;
+  if (hipMalloc(&t->pfx, sizeof(int32_t) * (L + 1)) != hipSuccess) return EVM_ENOMEM;
+  return EVM_OK;
+}
+
+static void tree_release(evm_tree* t) {
+  if (!t) return;
+  (void)hipFree(t->off);
+  (void)hipFree(t->ck);
+  (void)hipFree(t->xr);
+  (void)hipFree(t->pfx);
+  delete t;
+}
+
+// Builds a tree object from device leaves (ck sorted unique, xr); copies them.
+int evm::tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, const int32_t* xr, uint64_t L,
+                       evm_tree** out) {
+  evm_tree* t = new evm_tree;
+  int st = tree_alloc(t, n_owners, L);
+  if (st) {
+    tree_release(t);
+    return st;
+  }
+  if (L) {
+    HIPR(hipMemcpyAsync(t->ck, ck, sizeof(u64) * L, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPR(hipMemcpyAsync(t->xr, xr, sizeof(int32_t) * L, hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  hipLaunchKernelGGL(k_owner_off, dim3(grid_for(n_owners + 1, 256)), dim3(256), 0, ctx->stream, t->ck, (size_t)L,
+                     n_owners, t->off);
+  st = scan_exclusive<int32_t, OpXor>(ctx, S, t->xr, L, t->pfx, t->pfx + L);
+  if (st) {
+    tree_release(t);
+    return st;
+  }
+  *out = t;
+  return hip_ok(hipGetLastError());
+}
+
+// Folds m selected (ck, hash) pairs into `in` (may be null = empty trees).
+int evm::fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u64* ck, u32* h, size_t m,
+                        const Info& host_info, evm_tree** out) {
+  // sort by the bits that vary
+  int lo = 0, hi = 0;
+  if (m > 1) {
+    const u64 diff = host_info.ck_min ^ host_info.ck_max;
+    hi = diff ? 64 - __builtin_clzll(diff) : 0;
+    lo = 2 * (CODE_DIGITS - (int)host_info.maxlen);
+    if (lo > hi) lo = hi;
+  }
+  int st = radix_sort_pairs<u64>(ctx, S, ck, h, m, lo, hi);
+  if (st) return st;
+  u64* nck = S.alloc<u64>(std::max<size_t>(m, 1));
+  int32_t* nxr = S.alloc<int32_t>(std::max<size_t>(m, 1));
+  if (!nck || !nxr) return EVM_ENOMEM;
+  uint64_t L1 = 0;
+  st = reduce_runs(ctx, S, ck, (const int32_t*)h, m, nck, nxr, &L1);
+  if (st) return st;
+  const uint64_t L0 = in ? in->n_leaves : 0;
+  if (L0 == 0) return tree_finalize(ctx, S, n_owners, nck, nxr, L1, out);
+  if (L1 == 0) return tree_finalize(ctx, S, n_owners, in->ck, in->xr, L0, out);
+  const size_t tot = L0 + L1;
+  u64* mck = S.alloc<u64>(tot);
+  int32_t* mxr = S.alloc<int32_t>(tot);
+  u64* rck = S.alloc<u64>(tot);
+  int32_t* rxr = S.alloc<int32_t>(tot);
+  if (!mck || !mxr || !rck || !rxr) return EVM_ENOMEM;
+  hipLaunchKernelGGL(k_merge_a, dim3(grid_for(L0, 256)), dim3(256), 0, ctx->stream, in->ck, in->xr, (size_t)L0, nck,
+                     (size_t)L1, mck, mxr);
+  hipLaunchKernelGGL(k_merge_b, dim3(grid_for(L1, 256)), dim3(256), 0, ctx->stream, nck, nxr, (size_t)L1, in->ck,
+                     (size_t)L0, mck, mxr);
+  uint64_t L = 0;
+  st = reduce_runs(ctx, S, mck, mxr, tot, rck, rxr, &L);
+  if (st) return st;
+  return tree_finalize(ctx, S, n_owners, rck, rxr, L, out);
+}
+
+// ============================================================================
+// Diff (merkleTree.ts:63-91), one thread per owner.
+// ============================================================================
+struct TreeView {
+  const u64* off;
+  const u64* ck;
+  const int32_t* pfx;
+};
+
+__device__ __forceinline__ int32_t range_hash(const TreeView& t, size_t lo, size_t hi) { return t.pfx[hi] ^ t.pfx[lo]; }
+
+__global__ void k_diff(TreeView A, TreeView B, u32 n_owners, int64_t* __restrict__ millis) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
+    size_t alo = A.off[o], ahi = A.off[o + 1], blo = B.off[o], bhi = B.off[o + 1];
+    // root: tree1.hash === tree2.hash (undefined for {})
+    const bool ae = ahi > alo, be = bhi > blo;
+    if (ae == be && (!ae || range_hash(A, alo, ahi) == range_hash(B, blo, bhi))) {
+      millis[o] = EVM_DIFF_NONE;
+      continue;
+    }
+    u64 prefix = (u64)o << 40;
+    int depth = 0;
+    u64 kval = 0;  // base-3 value of the key string k so far
+    for (;;) {
+      int pick = -1;
+      size_t na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
+      if (depth < CODE_DIGITS) {
+        const int sh = 2 * (CODE_DIGITS - 1 - depth);
+        size_t ab = lower_bound_u64(A.ck, alo, ahi, prefix | (1ull << sh));
+        size_t bb = lower_bound_u64(B.ck, blo, bhi, prefix | (1ull << sh));
+        for (int c = 0; c < 3; ++c) {
+          const u64 end = prefix + ((u64)(c + 2) << sh);  // child c covers [prefix|(c+1)<<sh, prefix|(c+2)<<sh)
+          const size_t ae2 = lower_bound_u64(A.ck, ab, ahi, end);
+          const size_t be2 = lower_bound_u64(B.ck, bb, bhi, end);
+          const bool ea = ae2 > ab, eb = be2 > bb;
+          if (ea || eb) {
+            const bool differ = ea != eb || range_hash(A, ab, ae2) != range_hash(B, bb, be2);
+            if (differ) {
+              pick = c;
+              na0 = ab; na1 = ae2; nb0 = bb; nb1 = be2;
+              break;
+            }
+          }
+          ab = ae2;
+          bb = be2;
+        }
+      }
+      if (pick < 0) break;
+      const int sh = 2 * (CODE_DIGITS - 1 - depth);
+      prefix |= (u64)(pick + 1) << sh;
+      kval = kval * 3 + (u64)pick;
+      ++depth;
+      alo = na0; ahi = na1; blo = nb0; bhi = nb1;
+    }
+    if (depth > 16) {
+      millis[o] = EVM_DIFF_RANGE_ERROR;  // "0".repeat(16 - k.length) throws (merkleTree.ts:58)
+    } else {
+      u64 v = kval;
+      for (int i = depth; i < 16; ++i) v *= 3;  // padEnd(16, "0")
+      millis[o] = (int64_t)(v * 60000ull);
+    }
+  }
+}
+
+__global__ void k_roots(const u64* __restrict__ off, const int32_t* __restrict__ pfx, u32 n_owners,
+                        int32_t* __restrict__ root, uint8_t* __restrict__ present) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
+    const u64 a = off[o], b = off[o + 1];
+    root[o] = pfx[b] ^ pfx[a];
+    present[o] = b > a;
+  }
+}
+
+// ============================================================================
+// applyMessages (applyMessages.ts:26-131)
+// ============================================================================
+
+// (1) Global __message PK: the same timestamp in two different cells of one
+// batch makes the reference's INSERT fail silently for the later one and
+// stops that cell's running max from advancing.  That interleaving is
+// inherently sequential, so it is detected exactly and reported.
+__global__ void k_xcell(const evm_rec* __restrict__ rec, size_t n, u64* __restrict__ table, u32 log2size,
+                        Info* __restrict__ info) {
+  const u64 mask = (1ull << log2size) - 1;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const evm_rec r = rec[i];
+    if (!(r.meta & EVM_META_VALID)) continue;
+    const u64 mine = ((u64)r.hash << 32) | (u64)(i + 1);
+    u64 pos = ((u64)(r.hash * 2654435761u) ^ (r.node * 0x9E3779B97F4A7C15ull >> 20)) & mask;
+    for (u64 probe = 0; probe <= mask; ++probe) {
+      u64 s = __hip_atomic_load(&table[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s == 0) {
+        const u64 prev = atomicCAS(&table[pos], 0ull, mine);
+        if (prev == 0) break;  // inserted
+        s = prev;
+      }
+      if ((u32)(s >> 32) == r.hash) {
+        const evm_rec o = rec[(size_t)(s & 0xffffffffu) - 1];
+        if (o.tc == r.tc && o.node == r.node && (o.meta & EVM_META_CASEMASK) == (r.meta & EVM_META_CASEMASK)) {
+          if (o.aux != r.aux) atomicOr(&info->collision, 1u);
+          break;
+        }
+      }
+      pos = (pos + 1) & mask;
+    }
+  }
+}
+
+// (2) Segmented (per cell) running max in batch order over the cell-sorted
+// order.  Aggregate = (segment head seen, max since the last head).
+struct SegAgg {
+  u32 head;
+  Key key;
+};
+__device__ __forceinline__ SegAgg seg_combine(const SegAgg& a, const SegAgg& b) {
+  SegAgg r;
+  r.head = a.head | b.head;
+  r.key = b.head ? b.key : key_max(a.key, b.key);
+  return r;
+}
+
+constexpr int LWW_THREADS = 256;
+constexpr int LWW_ITEMS = 8;
+constexpr int LWW_TILE = LWW_THREADS * LWW_ITEMS;
+
+__device__ __forceinline__ SegAgg lww_elem(const evm_rec* rec, const u32* cell_s, const u32* idx_s, size_t p) {
+  SegAgg e;
+  e.head = (p == 0 || cell_s[p] != cell_s[p - 1]) ? 1u : 0u;
+  e.key = key_of(rec[idx_s[p]]);
+  return e;
+}
+
+struct SegLds {
+  u32 head[LWW_THREADS];
+  u64 tc[LWW_THREADS];
+  u64 node[LWW_THREADS];
+  u32 mask[LWW_THREADS];
+};
+__device__ __forceinline__ void seg_put(SegLds& L, int t, const SegAgg& a) {
+  L.head[t] = a.head;
+  L.tc[t] = a.key.tc;
+  L.node[t] = a.key.node;
+  L.mask[t] = a.key.mask;
+}
+__device__ __forceinline__ SegAgg seg_get(const SegLds& L, int t) {
+  SegAgg a;
+  a.head = L.head[t];
+  a.key = Key{L.tc[t], L.node[t], L.mask[t]};
+  return a;
+}
+
+// Block inclusive scan (Hillis-Steele over LDS) of one SegAgg per thread.
+__device__ SegAgg seg_block_inclusive(SegLds& L, SegAgg v) {
+  const int t = threadIdx.x;
+  seg_put(L, t, v);
+  __syncthreads();
+  for (int d = 1; d < LWW_THREADS; d <<= 1) {
+    SegAgg o;
+    const bool has = t >= d;
+    if (has) o = seg_get(L, t - d);
+    __syncthreads();
+    if (has) v = seg_combine(o, v);
+    seg_put(L, t, v);
+    __syncthreads();
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(LWW_THREADS) void k_lww_reduce(const evm_rec* __restrict__ rec, const u32* __restrict__ cell_s,
+                                                            const u32* __restrict__ idx_s, size_t n,
+                                                            u32* __restrict__ t_head, Key* __restrict__ t_key) {
+  __shared__ SegLds L;
+  const size_t base = (size_t)blockIdx.x * LWW_TILE + (size_t)threadIdx.x * LWW_ITEMS;
+  SegAgg acc{0u, key_none()};
+  for (int k = 0; k < LWW_ITEMS; ++k) {
+    const size_t p = base + k;
+    if (p < n) acc = seg_combine(acc, lww_elem(rec, cell_s, idx_s, p));
+  }
+  const SegAgg inc = seg_block_inclusive(L, acc);
+  if (threadIdx.x == LWW_THREADS - 1) {
+    t_head[blockIdx.x] = inc.head;
+    t_key[blockIdx.x] = inc.key;
+  }
+}
+
+// Exclusive scan of the tile aggregates, in one block.
+__global__ __launch_bounds__(LWW_THREADS) void k_lww_tiles(u32* __restrict__ t_head, Key* __restrict__ t_key, size_t nt) {
+  __shared__ SegLds L;
+  const size_t per = (nt + LWW_THREADS - 1) / LWW_THREADS;
+  const size_t b = (size_t)threadIdx.x * per;
+  SegAgg acc{0u, key_none()};
+  for (size_t i = b; i < b + per && i < nt; ++i) acc = seg_combine(acc, SegAgg{t_head[i], t_key[i]});
+  const SegAgg inc = seg_block_inclusive(L, acc);
+  // exclusive for this thread = inclusive of thread-1
+  __syncthreads();
+  seg_put(L, threadIdx.x, inc);
+  __syncthreads();
+  SegAgg run = threadIdx.x ? seg_get(L, threadIdx.x - 1) : SegAgg{0u, key_none()};
+  for (size_t i = b; i < b + per && i < nt; ++i) {
+    const SegAgg here{t_head[i], t_key[i]};
+    t_head[i] = run.head;
+    t_key[i] = run.key;
+    run = seg_combine(run, here);
+  }
+}
+
+__global__ __launch_bounds__(LWW_THREADS) void k_lww_apply(const evm_rec* __restrict__ rec, const u32* __restrict__ cell_s,
+                                                           const u32* __restrict__ idx_s, size_t n,
+                                                           const u32* __restrict__ t_head, const Key* __restrict__ t_key,
+                                                           const evm_rec* __restrict__ prior,
+                                                           const uint8_t* __restrict__ prior_present,
+                                                           uint8_t* __restrict__ flags, int32_t* __restrict__ winner) {
+  __shared__ SegLds L;
+  const size_t base = (size_t)blockIdx.x * LWW_TILE + (size_t)threadIdx.x * LWW_ITEMS;
+  SegAgg e[LWW_ITEMS];
+  SegAgg acc{0u, key_none()};
+#pragma unroll
+  for (int k = 0; k < LWW_ITEMS; ++k) {
+    const size_t p = base + k;
+    e[k] = p < n ? lww_elem(rec, cell_s, idx_s, p) : SegAgg{0u, key_none()};
+    acc = seg_combine(acc, e[k]);
+  }
+  const SegAgg inc = seg_block_inclusive(L, acc);
+  __syncthreads();
+  seg_put(L, threadIdx.x, inc);
+  __syncthreads();
+  SegAgg run = SegAgg{t_head[blockIdx.x], t_key[blockIdx.x]};
+  if (threadIdx.x) run = seg_combine(run, seg_get(L, threadIdx.x - 1));
+#pragma unroll
+  for (int k = 0; k < LWW_ITEMS; ++k) {
+    const size_t p = base + k;
+    if (p >= n) break;
+    const Key excl = e[k].head ? key_none() : run.key;
+    run = seg_combine(run, e[k]);
+    const u32 c = cell_s[p];
+    const u32 i = idx_s[p];
+    Key t = excl;
+    if (prior_present && prior_present[c]) t = key_max(t, key_of(prior[c]));
+    const Key ts = e[k].key;
+    // applyMessages.ts:93  t == null || t < message.timestamp
+    const bool ups = key_cmp(t, ts) < 0;
+    // applyMessages.ts:105 t == null || t !== message.timestamp
+    const bool xr = !((t.mask & KEY_PRESENT) && key_eq(t, ts));
+    flags[i] = (ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u);
+    if (ups) atomicMax(&winner[c], (int32_t)i);
+  }
+}
+
+__global__ void k_mark_bad(const evm_rec* __restrict__ rec, size_t n, uint8_t* __restrict__ flags) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    flags[i] = (rec[i].meta & EVM_META_VALID) ? 0u : EVM_MSG_BAD;
+}
+
+__global__ void k_fill_i32(int32_t* __restrict__ p, size_t n, int32_t v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+static int ceil_log2(size_t x) {
+  int k = 0;
+  while (((size_t)1 << k) < x) ++k;
+  return k;
+}
+
+static int read_info(evm_ctx* ctx, const Info* dev, Info* host) {
+  HIPR(hipMemcpyAsync(host, dev, sizeof(Info), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  return EVM_OK;
+}
+
+static int new_info(evm_ctx* ctx, Scratch& S, Info** out) {
+  Info* d = S.alloc<Info>(1);
+  if (!d) return EVM_ENOMEM;
+  Info h = info_init();
+  HIPR(hipMemcpyAsync(d, &h, sizeof(Info), hipMemcpyHostToDevice, ctx->stream));
+  *out = d;
+  return EVM_OK;
+}
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+const char* evm_strerror(int s) {
+  switch (s) {
+    case EVM_OK: return "ok";
+    case EVM_EINVAL: return "invalid argument";
+    case EVM_ENONCANON: return "timestamp outside the native domain";
+    case EVM_ECOLLISION: return "same timestamp in two cells of one batch";
+    case EVM_ERANGE: return "diff reached a 17-digit key (RangeError)";
+    case EVM_ETREE: return "tree is not a MerkleTree insertIntoMerkleTree can produce";
+    case EVM_EDEVICE: return "HIP error";
+    case EVM_ENOMEM: return "device out of memory";
+    case EVM_ECAPACITY: return "output buffer too small";
+  }
+  return "unknown status";
+}
+
+int evm_create(int device, evm_ctx** out) {
+  if (!out) return EVM_EINVAL;
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return EVM_EDEVICE;
+  if (hipSetDevice(device) != hipSuccess) return EVM_EDEVICE;
+  evm_ctx* c = new evm_ctx;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return EVM_EDEVICE;
+  }
+  c->stream = c->own;
+  *out = c;
+  return EVM_OK;
+}
+
+void evm_destroy(evm_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamDestroy(ctx->own);
+  delete ctx;
+}
+
+int evm_set_stream(evm_ctx* ctx, void* s) {
+  if (!ctx) return EVM_EINVAL;
+  ctx->stream = (hipStream_t)s;  // NULL: the HIP default (null) stream
+  return EVM_OK;
+}
+void* evm_get_stream(evm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int evm_sync(evm_ctx* ctx) {
+  if (!ctx) return EVM_EINVAL;
+  return hip_ok(hipStreamSynchronize(ctx->stream));
+}
+
+int evm_dev_alloc(evm_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !out) return EVM_EINVAL;
+  return hipMalloc(out, bytes ? bytes : 1) == hipSuccess ? EVM_OK : EVM_ENOMEM;
+}
+int evm_dev_free(evm_ctx* ctx, void* p) {
+  if (!ctx) return EVM_EINVAL;
+  return hip_ok(hipFree(p));
+}
+int evm_copy_h2d(evm_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return EVM_EINVAL;
+  if (!bytes) return EVM_OK;
+  HIPR(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return hip_ok(hipStreamSynchronize(ctx->stream));
+}
+int evm_copy_d2h(evm_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return EVM_EINVAL;
+  if (!bytes) return EVM_OK;
+  HIPR(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return hip_ok(hipStreamSynchronize(ctx->stream));
+}
+
+int evm_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const uint32_t* aux, evm_rec* out) {
+  if (!ctx || (n && (!ts || !out)) || stride < 46) return EVM_EINVAL;
+  Scratch S(ctx);
+  Info* info = nullptr;
+  int st = new_info(ctx, S, &info);
+  if (st) return st;
+  st = launch_pack(ctx, ts, stride, n, aux, 0, out, info);
+  if (st) return st;
+  Info h;
+  st = read_info(ctx, info, &h);
+  if (st) return st;
+  return h.bad ? EVM_ENONCANON : EVM_OK;
+}
+
+int evm_tree_new(evm_ctx* ctx, uint32_t n_owners, evm_tree** out) {
+  if (!ctx || !out) return EVM_EINVAL;
+  Scratch S(ctx);
+  int st = tree_finalize(ctx, S, n_owners, nullptr, nullptr, 0, out);
+  if (st) return st;
+  return evm_sync(ctx);
+}
+
+int evm_tree_from_leaves(evm_ctx* ctx, uint32_t n_owners, const uint64_t* off_h, const uint64_t* code_h,
+                         const int32_t* xr_h, evm_tree** out) {
+  if (!ctx || !out || !off_h) return EVM_EINVAL;
+  const uint64_t L = off_h[n_owners];
+  std::vector<u64> ck(L);
+  for (u32 o = 0; o < n_owners; ++o) {
+    if (off_h[o + 1] < off_h[o]) return EVM_EINVAL;
+    for (uint64_t k = off_h[o]; k < off_h[o + 1]; ++k) {
+      if (code_h[k] >> 40) return EVM_EINVAL;
+      ck[k] = ((u64)o << 40) | code_h[k];
+      if (k > off_h[o] && code_h[k] <= code_h[k - 1]) return EVM_EINVAL;  // sorted, unique
+    }
+  }
+  Scratch S(ctx);
+  u64* dck = S.alloc<u64>(std::max<uint64_t>(L, 1));
+  int32_t* dxr = S.alloc<int32_t>(std::max<uint64_t>(L, 1));
+  if (!dck || !dxr) return EVM_ENOMEM;
+  if (L) {
+    HIPR(hipMemcpyAsync(dck, ck.data(), sizeof(u64) * L, hipMemcpyHostToDevice, ctx->stream));
+    HIPR(hipMemcpyAsync(dxr, xr_h, sizeof(int32_t) * L, hipMemcpyHostToDevice, ctx->stream));
+  }
+  int st = tree_finalize(ctx, S, n_owners, dck, dxr, L, out);
+  if (st) return st;
+  return evm_sync(ctx);
+}
+
+int evm_tree_free(evm_ctx* ctx, evm_tree* t) {
+  if (!ctx) return EVM_EINVAL;
+  if (t) {
+    (void)hipStreamSynchronize(ctx->stream);
+    tree_release(t);
+  }
+  return EVM_OK;
+}
+
+int evm_tree_info(const evm_tree* t, uint32_t* n_owners, uint64_t* n_leaves) {
+  if (!t) return EVM_EINVAL;
+  if (n_owners) *n_owners = t->n_owners;
+  if (n_leaves) *n_leaves = t->n_leaves;
+  return EVM_OK;
+}
+
+int evm_tree_device(const evm_tree* t, const uint64_t** off, const uint64_t** code, const int32_t** xr) {
+  if (!t) return EVM_EINVAL;
+  if (off) *off = (const uint64_t*)t->off;
+  if (code) *code = (const uint64_t*)t->ck;
+  if (xr) *xr = t->xr;
+  return EVM_OK;
+}
+
+int evm_tree_leaves(evm_ctx* ctx, const evm_tree* t, uint64_t* off, uint64_t* code, int32_t* xr) {
+  if (!ctx || !t) return EVM_EINVAL;
+  if (off) HIPR(hipMemcpyAsync(off, t->off, sizeof(u64) * (t->n_owners + 1), hipMemcpyDeviceToHost, ctx->stream));
+  if (code && t->n_leaves)
+    HIPR(hipMemcpyAsync(code, t->ck, sizeof(u64) * t->n_leaves, hipMemcpyDeviceToHost, ctx->stream));
+  if (xr && t->n_leaves)
+    HIPR(hipMemcpyAsync(xr, t->xr, sizeof(int32_t) * t->n_leaves, hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if (code)
+    for (uint64_t k = 0; k < t->n_leaves; ++k) code[k] &= (1ull << 40) - 1;
+  return EVM_OK;
+}
+
+int evm_tree_roots(evm_ctx* ctx, const evm_tree* t, int32_t* root, uint8_t* present) {
+  if (!ctx || !t || !root || !present) return EVM_EINVAL;
+  Scratch S(ctx);
+  int32_t* dr = S.alloc<int32_t>(std::max<u32>(t->n_owners, 1));
+  uint8_t* dp = S.alloc<uint8_t>(std::max<u32>(t->n_owners, 1));
+  if (!dr || !dp) return EVM_ENOMEM;
+  if (t->n_owners == 0) return EVM_OK;
+  hipLaunchKernelGGL(k_roots, dim3(grid_for(t->n_owners, 256)), dim3(256), 0, ctx->stream, t->off, t->pfx, t->n_owners,
+                     dr, dp);
+  HIPR(hipMemcpyAsync(root, dr, sizeof(int32_t) * t->n_owners, hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipMemcpyAsync(present, dp, t->n_owners, hipMemcpyDeviceToHost, ctx->stream));
+  return hip_ok(hipStreamSynchronize(ctx->stream));
+}
+
+int evm_merkle_insert(evm_ctx* ctx, const evm_tree* in, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                      evm_tree** out) {
+  if (!ctx || !in || !out || stride < 46 || (n && !ts)) return EVM_EINVAL;
+  Scratch S(ctx);
+  Info* info = nullptr;
+  int st = new_info(ctx, S, &info);
+  if (st) return st;
+  evm_rec* rec = S.alloc<evm_rec>(std::max<size_t>(n, 1));
+  u64* ck = S.alloc<u64>(std::max<size_t>(n, 1));
+  u32* h = S.alloc<u32>(std::max<size_t>(n, 1));
+  if (!rec || !ck || !h) return EVM_ENOMEM;
+  st = launch_pack(ctx, ts, stride, n, owner, in->n_owners, rec, info);
+  if (st) return st;
+  if (n)
+    hipLaunchKernelGGL(k_fold_prep, dim3(grid_for(n, 256, 4096)), dim3(256), 0, ctx->stream, rec, (const uint8_t*)nullptr,
+                       (uint8_t)0, (const u32*)nullptr, (int)(owner ? OWNER_AUX : OWNER_ZERO), (const u32*)nullptr, n, ck,
+                       h, info);
+  Info hi;
+  st = read_info(ctx, info, &hi);
+  if (st) return st;
+  if (hi.bad_aux) return EVM_EINVAL;
+  if (hi.bad) return EVM_ENONCANON;
+  st = fold_into_tree(ctx, S, in, in->n_owners, ck, h, n, hi, out);
+  if (st) return st;
+  return evm_sync(ctx);
+}
+
+int evm_merkle_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* millis) {
+  if (!ctx || !a || !b || !millis || a->n_owners != b->n_owners) return EVM_EINVAL;
+  if (a->n_owners == 0) return EVM_OK;
+  TreeView A{a->off, a->ck, a->pfx}, B{b->off, b->ck, b->pfx};
+  hipLaunchKernelGGL(k_diff, dim3(grid_for(a->n_owners, 64, 1 << 16)), dim3(64), 0, ctx->stream, A, B, a->n_owners,
+                     millis);
+  HIPR(hipGetLastError());
+  return evm_sync(ctx);
+}
+
+int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n, const uint32_t* cell,
+                    uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts, size_t prior_stride,
+                    const uint8_t* prior_present, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+  if (!ctx || !tree_in || !tree_out || stride < 46 || (n && (!ts || !cell || !flags))) return EVM_EINVAL;
+  if (n_cells && !winner) return EVM_EINVAL;
+  if (prior_present && (!prior_ts || prior_stride < 46)) return EVM_EINVAL;
+  if (n >= 0x7fffffffu) return EVM_EINVAL;
+  Scratch S(ctx);
+  Info* info = nullptr;
+  int st = new_info(ctx, S, &info);
+  if (st) return st;
+  evm_rec* rec = S.alloc<evm_rec>(std::max<size_t>(n, 1));
+  evm_rec* prior = S.alloc<evm_rec>(std::max<size_t>(n_cells, 1));
+  if (!rec || !prior) return EVM_ENOMEM;
+  // K1 on the batch and on the prior per-cell maxima
+  st = launch_pack(ctx, ts, stride, n, cell, n_cells, rec, info);
+  if (st) return st;
+  if (prior_present && n_cells) {
+    Info* pinfo = nullptr;
+    if ((st = new_info(ctx, S, &pinfo))) return st;
+    if ((st = launch_pack(ctx, prior_ts, prior_stride, n_cells, nullptr, 0, prior, pinfo))) return st;
+    Info hp;
+    if ((st = read_info(ctx, pinfo, &hp))) return st;
+    // a prior row outside the native domain only matters where it is present
+    if (hp.bad) {
+      std::vector<evm_rec> pr(n_cells);
+      std::vector<uint8_t> pp(n_cells);
+      HIPR(hipMemcpyAsync(pr.data(), prior, sizeof(evm_rec) * n_cells, hipMemcpyDeviceToHost, ctx->stream));
+      HIPR(hipMemcpyAsync(pp.data(), prior_present, n_cells, hipMemcpyDeviceToHost, ctx->stream));
+      HIPR(hipStreamSynchronize(ctx->stream));
+      for (u32 c = 0; c < n_cells; ++c)
+        if (pp[c] && !(pr[c].meta & EVM_META_VALID)) return EVM_ENONCANON;
+    }
+  }
+  if (n_cells)
+    hipLaunchKernelGGL(k_fill_i32, dim3(grid_for(n_cells, 256)), dim3(256), 0, ctx->stream, winner, (size_t)n_cells, -1);
+  if (n == 0) {
+    st = tree_finalize(ctx, S, tree_in->n_owners, tree_in->ck, tree_in->xr, tree_in->n_leaves, tree_out);
+    return st ? st : evm_sync(ctx);
+  }
+  // (1) cross-cell PK collisions
+  const int lg = ceil_log2(2 * n);
+  u64* table = S.alloc<u64>((size_t)1 << lg);
+  if (!table) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(table, 0, sizeof(u64) << lg, ctx->stream));
+  hipLaunchKernelGGL(k_xcell, dim3(grid_for(n, 256, 8192)), dim3(256), 0, ctx->stream, rec, n, table, (u32)lg, info);
+  // (2) stable sort (cell, index)
+  u32* cell_s = S.alloc<u32>(n);
+  u32* idx_s = S.alloc<u32>(n);
+  if (!cell_s || !idx_s) return EVM_ENOMEM;
+  HIPR(hipMemcpyAsync(cell_s, cell, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, idx_s, n);
+  const int cbits = n_cells > 1 ? 32 - __builtin_clz(n_cells - 1) : 0;
+  if ((st = radix_sort_pairs<u32>(ctx, S, cell_s, idx_s, n, 0, cbits))) return st;
+  // (3) segmented running max + decisions
+  const size_t nt = (n + LWW_TILE - 1) / LWW_TILE;
+  u32* t_head = S.alloc<u32>(nt);
+  Key* t_key = S.alloc<Key>(nt);
+  if (!t_head || !t_key) return EVM_ENOMEM;
+  hipLaunchKernelGGL(k_lww_reduce, dim3(nt), dim3(LWW_THREADS), 0, ctx->stream, rec, cell_s, idx_s, n, t_head, t_key);
+  hipLaunchKernelGGL(k_lww_tiles, dim3(1), dim3(LWW_THREADS), 0, ctx->stream, t_head, t_key, nt);
+  hipLaunchKernelGGL(k_lww_apply, dim3(nt), dim3(LWW_THREADS), 0, ctx->stream, rec, cell_s, idx_s, n, t_head, t_key,
+                     prior, prior_present, flags, winner);
+  // (4) Merkle fold of the XOR messages
+  u32* sel = S.alloc<u32>(n);
+  u32* pos = S.alloc<u32>(n);
+  u32* cnt = S.alloc<u32>(1);
+  u64* ck = S.alloc<u64>(n);
+  u32* h = S.alloc<u32>(n);
+  if (!sel || !pos || !cnt || !ck || !h) return EVM_ENOMEM;
+  hipLaunchKernelGGL(k_sel_u32, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, flags, (uint8_t)EVM_MSG_XOR, n, sel);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, pos, cnt))) return st;
+  hipLaunchKernelGGL(k_fold_prep, dim3(grid_for(n, 256, 4096)), dim3(256), 0, ctx->stream, rec, flags,
+                     (uint8_t)EVM_MSG_XOR, pos, (int)(cell_owner ? OWNER_CELL : OWNER_ZERO), cell_owner, n, ck, h, info);
+  Info hi;
+  if ((st = read_info(ctx, info, &hi))) return st;
+  if (hi.bad) {
+    hipLaunchKernelGGL(k_mark_bad, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, rec, n, flags);
+    (void)evm_sync(ctx);
+    return EVM_ENONCANON;
+  }
+  if (hi.bad_aux) return EVM_EINVAL;
+  if (hi.collision) return EVM_ECOLLISION;
+  u32 m = 0;
+  HIPR(hipMemcpyAsync(&m, cnt, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if ((st = fold_into_tree(ctx, S, tree_in, tree_in->n_owners, ck, h, m, hi, tree_out))) return st;
+  return evm_sync(ctx);
+}
+
+}  // extern "C"

@@ -1,0 +1,101 @@
+// Host-side internals shared by the engine's translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/evm.h"
+
+struct evm_ctx {
+  int device;
+  hipStream_t own;
+  hipStream_t stream;
+};
+
+// One MerkleTree per owner, as sorted unique leaves keyed by
+// ck = owner << 40 | code (code: 20 base-4 digits, see evm_device.hpp).
+struct evm_tree {
+  uint32_t n_owners;
+  uint64_t n_leaves;
+  unsigned long long* off;  // [n_owners + 1] leaf range of each owner
+  unsigned long long* ck;   // [n_leaves]
+  int32_t* xr;    // [n_leaves] XOR of the hashes whose key ends at the leaf
+  int32_t* pfx;   // [n_leaves + 1] exclusive prefix XOR of xr (node hash = range XOR)
+};
+
+namespace evm {
+
+typedef unsigned long long u64;
+typedef uint32_t u32;
+
+// Per-call device status block.
+struct Info {
+  u32 bad;        // some record lacks EVM_META_VALID
+  u32 collision;  // cross-cell duplicate timestamp
+  u32 minute_min;
+  u32 minute_max;
+  u64 ck_min;
+  u64 ck_max;
+  u32 maxlen;  // longest base-3 key
+  u32 bad_aux; // an aux id out of range
+};
+
+inline Info info_init() {
+  Info h;
+  h.bad = 0;
+  h.collision = 0;
+  h.minute_min = 0xffffffffu;
+  h.minute_max = 0;
+  h.ck_min = ~0ull;
+  h.ck_max = 0;
+  h.maxlen = 0;
+  h.bad_aux = 0;
+  return h;
+}
+
+inline int hip_ok(hipError_t e) {
+  if (e == hipSuccess) return EVM_OK;
+  return e == hipErrorOutOfMemory ? EVM_ENOMEM : EVM_EDEVICE;
+}
+#define HIPR(expr)                          \
+  do {                                      \
+    hipError_t e_ = (expr);                 \
+    if (e_ != hipSuccess) return evm::hip_ok(e_); \
+  } while (0)
+
+// Stream-ordered scratch, released at scope exit.
+class Scratch {
+ public:
+  explicit Scratch(evm_ctx* c) : ctx_(c) {}
+  ~Scratch() {
+    for (void* p : ptrs_) (void)hipFreeAsync(p, ctx_->stream);
+  }
+  template <typename T>
+  T* alloc(size_t n) {
+    void* p = nullptr;
+    if (hipMallocAsync(&p, sizeof(T) * (n ? n : 1), ctx_->stream) != hipSuccess) return nullptr;
+    ptrs_.push_back(p);
+    return static_cast<T*>(p);
+  }
+
+ private:
+  evm_ctx* ctx_;
+  std::vector<void*> ptrs_;
+};
+
+enum OwnerMode { OWNER_ZERO = 0, OWNER_AUX = 1, OWNER_CELL = 2 };
+
+int launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,
+                Info* info);
+template <typename T, template <typename> class Op>
+int scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out, T* total_dev);
+template <typename K>
+int radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t n, int lo_bit, int hi_bit);
+int reduce_runs(evm_ctx* ctx, Scratch& S, const u64* ck, const int32_t* h, size_t m, u64* out_ck, int32_t* out_xr,
+                uint64_t* out_count);
+int tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, const int32_t* xr, uint64_t L, evm_tree** out);
+int fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u64* ck, u32* h, size_t m,
+                   const Info& host_info, evm_tree** out);
+
+}  // namespace evm

@@ -1,0 +1,235 @@
+// Data-parallel primitives for the engine, written for CDNA4 (wave64, LDS).
+//
+//   * exclusive scan (add / xor) over u32 / u64 ............ reduce-then-scan, 3 launches
+//   * stable LSD radix sort of (key, u32 value) pairs ........ per pass: tile histogram,
+//     scan of the digit-major count matrix, stable scatter ranked with 64-lane ballots
+//
+// Nothing here is reference code: the reference is single-threaded JS.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace evm {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ u64 lanemask_lt() {
+  const u32 lane = __lane_id();
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// ----------------------------------------------------------------------------
+// Exclusive scan.  Op is a functor with `static T id()` and `T operator()(T,T)`.
+// ----------------------------------------------------------------------------
+template <typename T>
+struct OpAdd {
+  __device__ static T id() { return T(0); }
+  __device__ T operator()(T a, T b) const { return a + b; }
+};
+template <typename T>
+struct OpXor {
+  __device__ static T id() { return T(0); }
+  __device__ T operator()(T a, T b) const { return a ^ b; }
+};
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+
+// Block-wide inclusive scan of one value per thread (ordered, any associative op).
+template <typename T, typename Op>
+__device__ __forceinline__ T block_inclusive_scan(T v, T* lds /* >= blockDim.x/64 */, Op op, T* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T o = __shfl_up(v, d, 64);
+    if (lane >= d) v = op(o, v);
+  }
+  if (lane == 63) lds[wid] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T acc = Op::id();
+    for (int w = 0; w < nw; ++w) {
+      const T t = lds[w];
+      lds[w] = acc;
+      acc = op(acc, t);
+    }
+    lds[nw] = acc;
+  }
+  __syncthreads();
+  v = op(lds[wid], v);
+  if (total) *total = lds[nw];
+  __syncthreads();
+  return v;
+}
+
+template <typename T, typename Op>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const T* __restrict__ in, size_t n, T* __restrict__ part) {
+  __shared__ T lds[SCAN_THREADS / 64 + 1];
+  Op op;
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+  T acc = Op::id();
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const size_t i = base + (size_t)k * SCAN_THREADS + threadIdx.x;
+    if (i < n) acc = op(acc, in[i]);
+  }
+  T tot;
+  block_inclusive_scan<T, Op>(acc, lds, op, &tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// One block scans the partials in place (exclusive); *total_out = grand total.
+template <typename T, typename Op>
+__global__ __launch_bounds__(1024) void k_scan_partials(T* __restrict__ part, size_t np, T* __restrict__ total_out) {
+  __shared__ T lds[1024 / 64 + 1];
+  Op op;
+  const size_t per = (np + blockDim.x - 1) / blockDim.x;
+  const size_t b = threadIdx.x * per;
+  T acc = Op::id();
+  for (size_t i = b; i < b + per && i < np; ++i) acc = op(acc, part[i]);
+  T tot;
+  T incl = block_inclusive_scan<T, Op>(acc, lds, op, &tot);
+  // exclusive prefix for this thread = incl minus own contribution: recompute serially
+  T run = Op::id();
+  {
+    // exclusive of thread = inclusive of previous thread; get via shuffle over LDS
+    __shared__ T ex[1024];
+    ex[threadIdx.x] = incl;
+    __syncthreads();
+    run = threadIdx.x == 0 ? Op::id() : ex[threadIdx.x - 1];
+  }
+  for (size_t i = b; i < b + per && i < np; ++i) {
+    const T t = part[i];
+    part[i] = run;
+    run = op(run, t);
+  }
+  if (threadIdx.x == 0 && total_out) *total_out = tot;
+}
+
+// Tile-local exclusive scan with the tile's carry from the scanned partials.
+template <typename T, typename Op>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_down(const T* __restrict__ in, size_t n, const T* __restrict__ part,
+                                                            T* __restrict__ out) {
+  __shared__ T lds[SCAN_THREADS / 64 + 1];
+  Op op;
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+  T v[SCAN_ITEMS];
+  T acc = Op::id();
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const size_t i = base + k;
+    v[k] = i < n ? in[i] : Op::id();
+    acc = op(acc, v[k]);
+  }
+  T incl = block_inclusive_scan<T, Op>(acc, lds, op, nullptr);
+  // exclusive start of this thread = incl - acc (need inverse-free form): shift via LDS
+  __shared__ T ex[SCAN_THREADS];
+  ex[threadIdx.x] = incl;
+  __syncthreads();
+  T run = op(part[blockIdx.x], threadIdx.x == 0 ? Op::id() : ex[threadIdx.x - 1]);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const size_t i = base + k;
+    if (i < n) out[i] = run;
+    run = op(run, v[k]);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Stable LSD radix sort of (key, value) pairs, RADIX_BITS per pass.
+// Tile = 256 threads x 16 items.  Wave w owns items [w*64*16, (w+1)*64*16) of
+// the tile, processed in 16 rounds of 64 consecutive items, so (round, lane)
+// order == input order: ranks from per-wave running digit counters plus a
+// 64-lane ballot match are stable.
+// ----------------------------------------------------------------------------
+constexpr int RADIX_BITS = 8;
+constexpr int RADIX_BINS = 1 << RADIX_BITS;
+constexpr int SORT_THREADS = 256;
+constexpr int SORT_ITEMS = 16;
+constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
+
+template <typename K>
+__device__ __forceinline__ u32 digit_of(K k, int shift, u32 mask) {
+  return (u32)(k >> shift) & mask;
+}
+
+template <typename K>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_hist(const K* __restrict__ keys, size_t n, int shift, int bits,
+                                                             u32* __restrict__ counts, u32 ntiles) {
+  __shared__ u32 hist[RADIX_BINS];
+  for (int d = threadIdx.x; d < RADIX_BINS; d += SORT_THREADS) hist[d] = 0;
+  __syncthreads();
+  const u32 mask = (1u << bits) - 1u;
+  const size_t base = (size_t)blockIdx.x * SORT_TILE;
+#pragma unroll 4
+  for (int k = 0; k < SORT_ITEMS; ++k) {
+    const size_t i = base + (size_t)k * SORT_THREADS + threadIdx.x;
+    if (i < n) atomicAdd(&hist[digit_of(keys[i], shift, mask)], 1u);
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < (1 << bits); d += SORT_THREADS) counts[(size_t)d * ntiles + blockIdx.x] = hist[d];
+}
+
+template <typename K>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(const K* __restrict__ kin, const u32* __restrict__ vin,
+                                                                K* __restrict__ kout, u32* __restrict__ vout, size_t n,
+                                                                int shift, int bits, const u32* __restrict__ offsets,
+                                                                u32 ntiles) {
+  __shared__ u32 wcnt[SORT_THREADS / WAVE][RADIX_BINS];
+  __shared__ u32 toff[RADIX_BINS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const u32 nbins = 1u << bits, mask = nbins - 1u;
+  for (u32 d = threadIdx.x; d < nbins; d += SORT_THREADS) {
+    toff[d] = offsets[(size_t)d * ntiles + blockIdx.x];
+#pragma unroll
+    for (int ww = 0; ww < SORT_THREADS / WAVE; ++ww) wcnt[ww][d] = 0;
+  }
+  __syncthreads();
+  const size_t wbase = (size_t)blockIdx.x * SORT_TILE + (size_t)w * WAVE * SORT_ITEMS;
+  K key[SORT_ITEMS];
+  u32 val[SORT_ITEMS], dig[SORT_ITEMS], rank[SORT_ITEMS];
+  const u64 lt = lanemask_lt();
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; ++r) {
+    const size_t i = wbase + (size_t)r * WAVE + lane;
+    const bool ok = i < n;
+    key[r] = ok ? kin[i] : K(0);
+    val[r] = ok ? vin[i] : 0u;
+    const u32 d = digit_of(key[r], shift, mask);
+    dig[r] = d;
+    u64 peers = __ballot(ok);
+    for (int b = 0; b < bits; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const u64 bal = __ballot(bit);
+      peers &= bit ? bal : ~bal;
+    }
+    if (ok) {
+      const u32 pre = wcnt[w][d];
+      rank[r] = pre + (u32)__popcll(peers & lt);
+      // highest lane of the peer group publishes the new running count
+      if ((peers >> lane) == 1ull) wcnt[w][d] = pre + (u32)__popcll(peers);
+    }
+  }
+  __syncthreads();
+  for (u32 d = threadIdx.x; d < nbins; d += SORT_THREADS) {
+    u32 acc = toff[d];
+#pragma unroll
+    for (int ww = 0; ww < SORT_THREADS / WAVE; ++ww) {
+      const u32 t = wcnt[ww][d];
+      wcnt[ww][d] = acc;
+      acc += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; ++r) {
+    const size_t i = wbase + (size_t)r * WAVE + lane;
+    if (i < n) {
+      const u32 dst = wcnt[w][dig[r]] + rank[r];
+      kout[dst] = key[r];
+      vout[dst] = val[r];
+    }
+  }
+}
+
+}  // namespace evm

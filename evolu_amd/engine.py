@@ -1,0 +1,219 @@
+"""Device-level host wrapper of libevm (torch tensors as device buffers).
+
+torch is plumbing here (device memory, streams, torch.distributed); every
+computation runs in libevm's HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+TS_LEN = 46
+TS_STRIDE = 48  # native coalesced layout: 46 bytes + 2 pad
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def encode_timestamps(strings: Sequence[str], stride: int = TS_STRIDE) -> np.ndarray:
+    """Packs timestamp strings into a (n, stride) uint8 arena.
+
+    Strings that are not exactly 46 ASCII bytes cannot be canonical: their
+    slot is filled with 0xFF bytes so the engine flags them (EVM_META_NONCANON).
+    """
+    n = len(strings)
+    arena = np.zeros((n, stride), dtype=np.uint8)
+    if n == 0:
+        return arena
+    try:
+        raw = "".join(strings).encode("ascii")
+        ok = len(raw) == TS_LEN * n and all(len(s) == TS_LEN for s in strings)
+    except UnicodeEncodeError:
+        ok = False
+    if ok:
+        arena[:, :TS_LEN] = np.frombuffer(raw, dtype=np.uint8).reshape(n, TS_LEN)
+        return arena
+    for i, s in enumerate(strings):
+        b = s.encode("utf-8", "replace")
+        if len(b) == TS_LEN and len(s) == TS_LEN:
+            arena[i, :TS_LEN] = np.frombuffer(b, dtype=np.uint8)
+        else:
+            arena[i, :TS_LEN] = 0xFF
+    return arena
+
+
+class Engine:
+    """One libevm context bound to one GPU (one per thread)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        self.device = device
+        torch.cuda.set_device(device)
+        h = C.c_void_p()
+        check(self.lib.evm_create(device, C.byref(h)), "evm_create")
+        self.h = h
+        self.bind_stream(torch.cuda.current_stream(device))
+
+    def bind_stream(self, stream: torch.cuda.Stream):
+        check(self.lib.evm_set_stream(self.h, C.c_void_p(stream.cuda_stream)), "evm_set_stream")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.evm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --------------------------------------------------------------- buffers
+    def dev(self, a: np.ndarray) -> torch.Tensor:
+        return torch.from_numpy(np.ascontiguousarray(a)).to(f"cuda:{self.device}")
+
+    def timestamps(self, strings: Sequence[str], stride: int = TS_STRIDE) -> torch.Tensor:
+        return self.dev(encode_timestamps(strings, stride))
+
+    # ------------------------------------------------------------------- K1
+    def pack(self, ts: torch.Tensor, aux: Optional[torch.Tensor] = None):
+        """-> (records int64 tensor view [n,4], status)."""
+        n, stride = ts.shape
+        out = torch.empty((n, 4), dtype=torch.int64, device=ts.device)
+        st = self.lib.evm_pack(self.h, _ptr(ts), stride, n, _ptr(aux), _ptr(out))
+        if st not in (_lib.EVM_OK, _lib.EVM_ENONCANON):
+            check(st, "evm_pack")
+        return out, st
+
+    # ----------------------------------------------------------------- trees
+    def tree_new(self, n_owners: int = 1) -> "Trees":
+        h = C.c_void_p()
+        check(self.lib.evm_tree_new(self.h, n_owners, C.byref(h)), "evm_tree_new")
+        return Trees(self, h)
+
+    def tree_from_json(self, texts: Sequence[str]) -> "Trees":
+        bs = [t.encode() for t in texts]
+        arr = (C.c_char_p * len(bs))(*bs)
+        lens = (C.c_size_t * len(bs))(*[len(b) for b in bs])
+        h = C.c_void_p()
+        check(self.lib.evm_tree_from_json(self.h, len(bs), arr, lens, C.byref(h)), "evm_tree_from_json")
+        return Trees(self, h)
+
+    def tree_from_leaves(self, off: np.ndarray, code: np.ndarray, xr: np.ndarray) -> "Trees":
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        code = np.ascontiguousarray(code, dtype=np.uint64)
+        xr = np.ascontiguousarray(xr, dtype=np.int32)
+        h = C.c_void_p()
+        check(
+            self.lib.evm_tree_from_leaves(
+                self.h, len(off) - 1, off.ctypes.data_as(C.c_void_p), code.ctypes.data_as(C.c_void_p),
+                xr.ctypes.data_as(C.c_void_p), C.byref(h)),
+            "evm_tree_from_leaves",
+        )
+        return Trees(self, h)
+
+    def merkle_insert(self, trees: "Trees", ts: torch.Tensor, owner: Optional[torch.Tensor] = None) -> "Trees":
+        n, stride = ts.shape
+        h = C.c_void_p()
+        check(self.lib.evm_merkle_insert(self.h, trees.h, _ptr(ts), stride, n, _ptr(owner), C.byref(h)),
+              "evm_merkle_insert")
+        return Trees(self, h)
+
+    def merkle_diff(self, a: "Trees", b: "Trees") -> torch.Tensor:
+        out = torch.empty(a.n_owners, dtype=torch.int64, device=f"cuda:{self.device}")
+        check(self.lib.evm_merkle_diff(self.h, a.h, b.h, _ptr(out)), "evm_merkle_diff")
+        return out
+
+    # ---------------------------------------------------------------- client
+    def apply_batch(self, trees: "Trees", ts: torch.Tensor, cell: torch.Tensor, n_cells: int,
+                    cell_owner: Optional[torch.Tensor] = None, prior_ts: Optional[torch.Tensor] = None,
+                    prior_present: Optional[torch.Tensor] = None, flags: Optional[torch.Tensor] = None,
+                    winner: Optional[torch.Tensor] = None, raise_on_error: bool = True):
+        """applyMessages for one batch -> (flags u8[n], winner i32[n_cells], Trees, status)."""
+        n, stride = ts.shape
+        dev = ts.device
+        if flags is None:
+            flags = torch.empty(n, dtype=torch.uint8, device=dev)
+        if winner is None:
+            winner = torch.empty(max(n_cells, 1), dtype=torch.int32, device=dev)
+        pstride = prior_ts.shape[1] if prior_ts is not None else 48
+        h = C.c_void_p()
+        st = self.lib.evm_apply_batch(self.h, trees.h, _ptr(ts), stride, n, _ptr(cell), n_cells, _ptr(cell_owner),
+                                      _ptr(prior_ts), pstride, _ptr(prior_present), _ptr(flags), _ptr(winner),
+                                      C.byref(h))
+        if raise_on_error:
+            check(st, "evm_apply_batch")
+        return flags, winner[:n_cells], (Trees(self, h) if st == _lib.EVM_OK else None), st
+
+
+class Trees:
+    """A device-resident set of per-owner MerkleTrees (owns its evm_tree)."""
+
+    def __init__(self, eng: Engine, h):
+        self.eng = eng
+        self.h = h
+        no = C.c_uint32()
+        nl = C.c_uint64()
+        check(eng.lib.evm_tree_info(h, C.byref(no), C.byref(nl)), "evm_tree_info")
+        self.n_owners = no.value
+        self.n_leaves = nl.value
+
+    def free(self):
+        if self.h:
+            self.eng.lib.evm_tree_free(self.eng.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def leaves(self):
+        off = np.zeros(self.n_owners + 1, dtype=np.uint64)
+        code = np.zeros(max(self.n_leaves, 1), dtype=np.uint64)
+        xr = np.zeros(max(self.n_leaves, 1), dtype=np.int32)
+        check(self.eng.lib.evm_tree_leaves(self.eng.h, self.h, off.ctypes.data_as(C.c_void_p),
+                                           code.ctypes.data_as(C.c_void_p), xr.ctypes.data_as(C.c_void_p)),
+              "evm_tree_leaves")
+        return off, code[: self.n_leaves], xr[: self.n_leaves]
+
+    def roots(self):
+        r = np.zeros(max(self.n_owners, 1), dtype=np.int32)
+        p = np.zeros(max(self.n_owners, 1), dtype=np.uint8)
+        check(self.eng.lib.evm_tree_roots(self.eng.h, self.h, r.ctypes.data_as(C.c_void_p),
+                                          p.ctypes.data_as(C.c_void_p)), "evm_tree_roots")
+        return r[: self.n_owners], p[: self.n_owners].astype(bool)
+
+    def to_json(self, owner: int = 0) -> str:
+        ln = C.c_size_t()
+        check(self.eng.lib.evm_tree_to_json(self.eng.h, self.h, owner, None, 0, C.byref(ln)), "evm_tree_to_json")
+        buf = C.create_string_buffer(ln.value)
+        check(self.eng.lib.evm_tree_to_json(self.eng.h, self.h, owner, buf, ln.value, C.byref(ln)),
+              "evm_tree_to_json")
+        return buf.raw[: ln.value].decode()
+
+
+def key_string(code: int) -> str:
+    """Leaf code -> base-3 key string (inverse of the engine's path code)."""
+    out = []
+    for i in range(20):
+        d = (code >> (2 * (19 - i))) & 3
+        if d == 0:
+            break
+        out.append(str(d - 1))
+    return "".join(out)
+
+
+def key_code(key: str) -> int:
+    code = 0
+    for i, ch in enumerate(key):
+        code |= (int(ch) + 1) << (2 * (19 - i))
+    return code

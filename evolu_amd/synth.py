@@ -1,0 +1,136 @@
+"""Seeded synthetic message streams for the BASELINE configs (numpy, vectorised).
+
+Generator spec: SURVEY.md section 8(d).  Every timestamp is canonical and is
+produced by per-node HLC sends (timestamp.ts:97-123 rules: millis = max(last,
+now); counter increments when millis repeats), so (millis, counter, node)
+triples are unique per node.  seed = 0xE7010000 + config number.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+BENCH_T0 = 1704067200000  # 2024-01-01T00:00:00.000Z
+DAY_MS = 86400000
+HEX = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)
+HEXU = np.frombuffer(b"0123456789ABCDEF", dtype=np.uint8)
+
+
+def rng_for(config: int) -> np.random.Generator:
+    return np.random.default_rng(0xE7010000 + config)
+
+
+def civil_from_days(z: np.ndarray):
+    z = z + 719468
+    era = np.floor_divide(z, 146097)
+    doe = z - era * 146097
+    yoe = (doe - doe // 1460 + doe // 36524 - doe // 146096) // 365
+    y = yoe + era * 400
+    doy = doe - (365 * yoe + yoe // 4 - yoe // 100)
+    mp = (5 * doy + 2) // 153
+    d = doy - (153 * mp + 2) // 5 + 1
+    m = np.where(mp < 10, mp + 3, mp - 9)
+    return y + (m <= 2), m, d
+
+
+def format_timestamps(millis: np.ndarray, counter: np.ndarray, node_bytes: np.ndarray, stride: int = 48) -> np.ndarray:
+    """(n,) millis, (n,) counter, (n,16) uint8 node -> (n, stride) uint8 arena of
+    timestamp.ts:43-48 strings (4-digit years only)."""
+    n = millis.shape[0]
+    millis = millis.astype(np.int64)
+    days = millis // DAY_MS
+    ms = millis - days * DAY_MS
+    y, mo, d = civil_from_days(days)
+    if n and (y.min() < 0 or y.max() > 9999):
+        raise ValueError("year outside 0000-9999")
+    hh = ms // 3600000
+    mi = (ms // 60000) % 60
+    ss = (ms // 1000) % 60
+    sss = ms % 1000
+    out = np.zeros((n, stride), dtype=np.uint8)
+
+    def put(col, val, width):
+        v = val.astype(np.int64)
+        for k in range(width - 1, -1, -1):
+            out[:, col + k] = 48 + (v % 10)
+            v = v // 10
+
+    put(0, y, 4)
+    out[:, 4] = ord("-")
+    put(5, mo, 2)
+    out[:, 7] = ord("-")
+    put(8, d, 2)
+    out[:, 10] = ord("T")
+    put(11, hh, 2)
+    out[:, 13] = ord(":")
+    put(14, mi, 2)
+    out[:, 16] = ord(":")
+    put(17, ss, 2)
+    out[:, 19] = ord(".")
+    put(20, sss, 3)
+    out[:, 23] = ord("Z")
+    out[:, 24] = ord("-")
+    c = counter.astype(np.int64)
+    for k in range(3, -1, -1):
+        out[:, 25 + k] = HEXU[c % 16]
+        c = c // 16
+    out[:, 29] = ord("-")
+    out[:, 30:46] = node_bytes
+    return out
+
+
+def random_nodes(rng, count: int, upper_frac: float = 0.0) -> np.ndarray:
+    nodes = HEX[rng.integers(0, 16, size=(count, 16))]
+    if upper_frac > 0:
+        up = (rng.random(count) < upper_frac)[:, None] & (nodes >= ord("a"))
+        nodes = np.where(up, nodes - 32, nodes).astype(np.uint8)
+    return nodes
+
+
+def hlc_stream(rng, n_per_node: np.ndarray, t0: int, span_ms: int, zero_gap_frac: float = 0.05):
+    """Per-node HLC sends.  Returns (millis, counter, node_index) in node-major order."""
+    total = int(n_per_node.sum())
+    node_idx = np.repeat(np.arange(len(n_per_node)), n_per_node)
+    mean_gap = max(1, span_ms // max(1, int(n_per_node.max())))
+    gaps = rng.integers(1, 2 * mean_gap + 1, size=total)
+    gaps[rng.random(total) < zero_gap_frac] = 0
+    starts = np.concatenate([[0], np.cumsum(n_per_node)[:-1]])
+    gaps[starts] = rng.integers(0, mean_gap + 1, size=len(n_per_node))
+    cs = np.cumsum(gaps)
+    millis = t0 + cs - np.repeat(cs[starts], n_per_node) + np.repeat(gaps[starts], n_per_node)
+    # counter: position inside each run of equal millis of one node
+    new_run = np.ones(total, dtype=bool)
+    new_run[1:] = (millis[1:] != millis[:-1]) | (node_idx[1:] != node_idx[:-1])
+    run_start = np.maximum.accumulate(np.where(new_run, np.arange(total), 0))
+    counter = np.arange(total) - run_start
+    if counter.max(initial=0) > 65535:
+        raise ValueError("counter overflow in synthetic stream")
+    return millis, counter, node_idx
+
+
+def config2(n: int = 10_000_000, n_cells: int = 1000, n_nodes: int = 64, stride: int = 48, seed_config: int = 2):
+    """1 owner, n messages over n_cells cells (10x10x10), n_nodes nodes, shuffled."""
+    rng = rng_for(seed_config)
+    per = np.full(n_nodes, n // n_nodes, dtype=np.int64)
+    per[: n - per.sum()] += 1
+    millis, counter, nidx = hlc_stream(rng, per, BENCH_T0, 30 * DAY_MS)
+    nodes = random_nodes(rng, n_nodes)
+    perm = rng.permutation(n)
+    ts = format_timestamps(millis[perm], counter[perm], nodes[nidx[perm]], stride)
+    cell = rng.integers(0, n_cells, size=n, dtype=np.uint32)
+    return ts, cell
+
+
+def config3(n_owners: int = 100_000, per_owner: int = 1000, nodes_per_owner: int = 4, stride: int = 48,
+            seed_config: int = 3):
+    """Server ingest: n_owners x per_owner messages, messages grouped by owner request,
+    owners interleaved; returns (ts arena, owner ids, client-prefix mask)."""
+    rng = rng_for(seed_config)
+    n = n_owners * per_owner
+    per = np.full(n_owners * nodes_per_owner, per_owner // nodes_per_owner, dtype=np.int64)
+    per[:: nodes_per_owner] += per_owner - per.reshape(n_owners, nodes_per_owner).sum(1)
+    millis, counter, nidx = hlc_stream(rng, per, BENCH_T0, 30 * DAY_MS)
+    nodes = random_nodes(rng, n_owners * nodes_per_owner)
+    owner = (nidx // nodes_per_owner).astype(np.uint32)
+    perm = rng.permutation(n)
+    ts = format_timestamps(millis[perm], counter[perm], nodes[nidx[perm]], stride)
+    return ts, owner[perm], millis[perm]

@@ -1,0 +1,148 @@
+/*
+ * evm.h -- C ABI of the MI355X batch-merge engine for Evolu's CRDT sync path.
+ *
+ * Plain C, plain pointers and sizes.  Every compute entry point takes DEVICE
+ * pointers and runs on the context's HIP stream; `evm_copy_*` / `evm_dev_*`
+ * let a caller without its own allocator (the N-API addon) stage host
+ * buffers.  Every call returns an int status (EVM_OK == 0).  One context per
+ * thread; the library keeps no global state.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to harrywebdev/evolu @ 2025-01-31):
+ *
+ *   evm_pack ............ timestamp.ts:50-55 timestampFromString +
+ *                         timestamp.ts:87-88 timestampToHash (batched)
+ *   evm_merkle_insert ... merkleTree.ts:31-50 insertIntoMerkleTree (batched,
+ *                         many owners)
+ *   evm_merkle_diff ..... merkleTree.ts:63-91 diffMerkleTrees (batched over
+ *                         owners)
+ *   evm_apply_batch ..... applyMessages.ts:26-131 applyMessages (LWW decisions
+ *                         + Merkle fold; the SQL writes stay with the caller)
+ *   evm_server_ingest ... apps/server/src/index.ts:138-171 addMessages
+ *   evm_server_select ... apps/server/src/index.ts:173-202 getMessages
+ *   evm_tree_to_json /
+ *   evm_tree_from_json .. types.ts:80-84 merkleTreeToString / FromString
+ */
+#ifndef EVM_H
+#define EVM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+enum evm_status {
+  EVM_OK = 0,
+  EVM_EINVAL = 1,     /* bad argument */
+  EVM_ENONCANON = 2,  /* >= 1 timestamp outside the native domain (see EVM_META_*); nothing applied */
+  EVM_ECOLLISION = 3, /* one timestamp in two cells of a batch (global __message PK); nothing applied */
+  EVM_ERANGE = 4,     /* a diff reached a 17-digit key: the reference throws RangeError */
+  EVM_ETREE = 5,      /* tree JSON is not a tree insertIntoMerkleTree can produce */
+  EVM_EDEVICE = 6,    /* HIP error */
+  EVM_ENOMEM = 7,     /* device allocation failed */
+  EVM_ECAPACITY = 8   /* output buffer too small */
+};
+
+/* ---- packed timestamp record (32 bytes, device) -------------------------
+ * tc    = millis << 16 | counter
+ * node  = the 16 node hex digits as a 64-bit value (case folded)
+ * meta  = EVM_META_* bits; low 16 bits: bit i set <=> node char i is 'A'-'F'
+ * hash  = murmur3 of the canonical string (uint32; timestampToHash)
+ * minute= floor(millis / 60000) == (millis/1000/60)|0 on the native domain
+ * aux   = caller's per-message id copied through (cell or owner)          */
+typedef struct evm_rec {
+  uint64_t tc;
+  uint64_t node;
+  uint32_t meta;
+  uint32_t hash;
+  uint32_t minute;
+  uint32_t aux;
+} evm_rec;
+
+#define EVM_META_CASEMASK 0x0000FFFFu
+#define EVM_META_VALID 0x00010000u    /* canonical and 1970 <= t < 2^31 minutes */
+#define EVM_META_NONCANON 0x00020000u /* not canonical: V8's lenient Date.parse forms etc. */
+#define EVM_META_RANGE 0x00040000u    /* canonical, but before 1970 or at/after 2^31 minutes */
+
+/* ---- per-message flag bits (uint8, device) ----------------------------- */
+#define EVM_MSG_UPS 0x01u /* applyMessages.ts:93  upsert of the user-table cell executed */
+#define EVM_MSG_XOR 0x02u /* applyMessages.ts:105 __message INSERT attempted + Merkle XOR */
+#define EVM_MSG_INS 0x04u /* index.ts:154         INSERT OR IGNORE changed a row (+ XOR) */
+#define EVM_MSG_BAD 0x80u /* timestamp outside the native domain */
+
+/* ---- context ----------------------------------------------------------- */
+typedef struct evm_ctx evm_ctx;
+
+int evm_create(int device, evm_ctx** out);
+void evm_destroy(evm_ctx* ctx);
+const char* evm_strerror(int status);
+int evm_set_stream(evm_ctx* ctx, void* hip_stream); /* NULL: the HIP default stream; initially the context's own */
+void* evm_get_stream(evm_ctx* ctx);
+int evm_sync(evm_ctx* ctx);
+int evm_dev_alloc(evm_ctx* ctx, size_t bytes, void** out);
+int evm_dev_free(evm_ctx* ctx, void* p);
+int evm_copy_h2d(evm_ctx* ctx, void* dst_dev, const void* src_host, size_t bytes);
+int evm_copy_d2h(evm_ctx* ctx, void* dst_host, const void* src_dev, size_t bytes);
+
+/* ---- K1: parse + canonical check + murmur3 + minute (timestamp.ts) -------
+ * ts: n timestamps of 46 significant bytes at `stride` bytes (46 or more;
+ * 48 is the coalesced native layout).  aux may be NULL.  Writes out[n].
+ * Returns EVM_ENONCANON if any record lacks EVM_META_VALID (out still full). */
+int evm_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const uint32_t* aux, evm_rec* out);
+
+/* ---- Merkle trees: per-owner leaf maps, device resident -----------------
+ * A tree set holds one MerkleTree per owner as the sorted list of its leaves:
+ * every key path that received >= 1 insert, with the XOR of the hashes that
+ * ended there.  Node hashes, node presence and JSON all derive from it.
+ * Leaf code = sum (digit_i + 1) * 4^(19 - i) over the base-3 key digits.   */
+typedef struct evm_tree evm_tree;
+
+int evm_tree_new(evm_ctx* ctx, uint32_t n_owners, evm_tree** out); /* all trees {} */
+int evm_tree_from_leaves(evm_ctx* ctx, uint32_t n_owners, const uint64_t* owner_off_host,
+                         const uint64_t* code_host, const int32_t* xor_host, evm_tree** out);
+int evm_tree_free(evm_ctx* ctx, evm_tree* t);
+int evm_tree_info(const evm_tree* t, uint32_t* n_owners, uint64_t* n_leaves);
+/* device views (valid until the tree is freed) */
+int evm_tree_device(const evm_tree* t, const uint64_t** owner_off, const uint64_t** code, const int32_t** xr);
+/* host copies: owner_off[n_owners+1], code[n_leaves], xr[n_leaves] (any may be NULL) */
+int evm_tree_leaves(evm_ctx* ctx, const evm_tree* t, uint64_t* owner_off, uint64_t* code, int32_t* xr);
+/* per owner root: hash (int32) and present (0: the tree is {}) -- host arrays */
+int evm_tree_roots(evm_ctx* ctx, const evm_tree* t, int32_t* root_hash, uint8_t* present);
+/* types.ts:80-81 JSON.stringify(tree of `owner`); *len = bytes needed (no NUL) */
+int evm_tree_to_json(evm_ctx* ctx, const evm_tree* t, uint32_t owner, char* buf, size_t cap, size_t* len);
+/* types.ts:83-84, one JSON text per owner (host strings) */
+int evm_tree_from_json(evm_ctx* ctx, uint32_t n_owners, const char* const* json, const size_t* lens, evm_tree** out);
+
+/* merkleTree.ts:31-50, batched: XOR every timestamp into its owner's tree.
+ * owner: device [n] (NULL: all owner 0).  *out is a new tree set.          */
+int evm_merkle_insert(evm_ctx* ctx, const evm_tree* in, const char* ts, size_t stride, size_t n,
+                      const uint32_t* owner, evm_tree** out);
+
+/* merkleTree.ts:63-91 for every owner o: diffMerkleTrees(a[o], b[o]).
+ * millis: device int64[n_owners]; -1 = option.none, -2 = RangeError.       */
+#define EVM_DIFF_NONE (-1)
+#define EVM_DIFF_RANGE_ERROR (-2)
+int evm_merkle_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* millis);
+
+/* ---- client: applyMessages.ts:26-131 -------------------------------------
+ * Batch order is message order.  cell: device [n], dense ids < n_cells of
+ * (table,row,column) per owner.  cell_owner: device [n_cells] or NULL (one
+ * owner).  prior_ts: device, n_cells timestamps at prior_stride = the cell's
+ * current max in __message (SELECT ... ORDER BY timestamp DESC LIMIT 1);
+ * prior_present: device uint8 [n_cells] (NULL: no prior rows).
+ * Outputs: flags[n] (EVM_MSG_UPS / EVM_MSG_XOR), winner[n_cells] (index of
+ * the message whose upsert is final, -1 if none), *tree_out.
+ * The caller then runs the upsert of each winner and
+ * INSERT ... ON CONFLICT DO NOTHING of each XOR message, in batch order.   */
+int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n,
+                    const uint32_t* cell, uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts,
+                    size_t prior_stride, const uint8_t* prior_present, uint8_t* flags, int32_t* winner,
+                    evm_tree** tree_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EVM_H */

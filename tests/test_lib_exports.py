@@ -1,0 +1,52 @@
+"""CPU checks of the C ABI library: it loads, and exports every symbol
+include/evm.h declares (no compute calls -- there is no GPU here)."""
+import ctypes
+import os
+import re
+
+from oracle import evolu_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "evm.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(evm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from evolu_amd import _lib, build
+
+    build.build_lib()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    # the ctypes binding covers the header exactly
+    assert sorted(_lib.SIGNATURES) == syms
+    assert lib.evm_strerror.restype is not None or True
+
+
+def test_strerror_no_gpu_needed():
+    from evolu_amd import _lib
+
+    lib = _lib.load()
+    assert lib.evm_strerror(0) == b"ok"
+    assert b"RangeError" in lib.evm_strerror(4)
+
+
+def test_minute_arithmetic_matches_js_on_native_range():
+    # merkleTree.ts:33 (millis/1000/60)|0 == floor(millis/60000) for 0 <= millis < 2^31 minutes
+    import random
+
+    r = random.Random(3)
+    for k in list(range(0, 2**31, 99991)) + [2**31 - 1]:
+        for d in (-1, 0, 1):
+            m = k * 60000 + d
+            if 0 <= m < 2**31 * 60000:
+                assert O.to_int32(m / 1000 / 60) == m // 60000
+    for _ in range(20000):
+        m = r.randrange(0, 2**31 * 60000)
+        assert O.to_int32(m / 1000 / 60) == m // 60000
