@@ -1,0 +1,190 @@
+"""Headline benchmark: CRDT messages merged/sec (LWW + Merkle) on MI355X.
+
+Workload (BASELINE.json configs[1]): one
+owner, 10M synthetic CrdtMessages over 1,000 cells (10 tables x 10 rows x 10
+columns), 64 HLC nodes, shuffled batch order.  One step = one
+applyMessages batch (evm_apply_batch: pack + canonical check + murmur3,
+cross-cell PK check, stable cell sort, segmented LWW scan, Merkle fold) with
+the inputs already resident in HBM, starting from an empty tree.
+
+Multi-GPU (torchrun, one rank per GPU): weak scaling -- every rank merges its
+own owner's 10M-message batch (owners are independent in applyMessages: each is
+its own client DB), no data-path collective; the elapsed time is the max over
+ranks.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "CRDT messages merged/sec (LWW+Merkle) and % HBM roofline at 1/2/4/8 GPUs"
+HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
+
+# Algorithmic (compulsory) bytes per message of each kernel on the client path,
+# SURVEY.md section 8(d) accounting, restated per kernel in DESIGN.md.
+ALG_BYTES_PER_MSG = {
+    "k_pack": 46 + 4 + 32,  # ts string + cell in, 32-B record out
+    "k_xcell": 24 + 8,  # key + hash read, one 8-B hash-set slot
+    "(k_radix_scatter<K>)": 16,  # (cell, idx) in and out, per pass
+    "(k_radix_hist<K>)": 4,
+    "k_lww_reduce": 4 + 4 + 20,  # cell + idx + gathered key
+    "k_lww_apply": 4 + 4 + 20 + 1,  # + flag out
+    "k_fold_prep": 1 + 4 + 12 + 12,  # flag, pos, (minute, hash, aux) in; (ck, hash) out
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--messages", type=int, default=10_000_000)
+    ap.add_argument("--cells", type=int, default=1000)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0: skip)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch per kernel (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def cpu_baseline(ts_arena, cells, budget_s):
+    """The oracle (Python restatement, sqlite3 running the reference SQL) on
+    the first S messages of the same workload, single-threaded."""
+    from oracle import evolu_oracle as O
+
+    def msgs(a, b):
+        out = []
+        for i in range(a, b):
+            s = ts_arena[i, :46].tobytes().decode()
+            c = int(cells[i])
+            out.append({"timestamp": s, "table": "t%d" % (c // 100), "row": "r%d" % (c // 10 % 10),
+                        "column": "c%d" % (c % 10), "value": i})
+        return out
+
+    pilot = msgs(0, 2000)
+    db = O.ClientDb()
+    t0 = time.perf_counter()
+    tree = O.apply_messages(db, {}, pilot)
+    rate = len(pilot) / (time.perf_counter() - t0)
+    s = int(min(len(cells) - 2000, max(2000, rate * budget_s)))
+    sample = msgs(2000, 2000 + s)
+    t0 = time.perf_counter()
+    O.apply_messages(db, tree, sample)
+    dt = time.perf_counter() - t0
+    return {
+        "value": len(sample) / dt,
+        "unit": "msgs/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "messages 2000..%d of the config-2 stream applied by oracle/evolu_oracle.py "
+        "(applyMessages.ts control flow, reference SQL verbatim in sqlite3, persistent-spread trie), "
+        "1 thread, %.1f s" % (2000 + s, dt),
+    }
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from evolu_amd import synth
+    from evolu_amd.engine import Engine
+
+    # each rank: its own owner (seed per rank), same shape
+    ts_np, cell_np = synth.config2(a.messages, a.cells, seed_config=2 + 1000 * rank)
+    eng = Engine(local)
+    ts = eng.dev(ts_np)
+    cell = eng.dev(cell_np)
+    empty = eng.tree_new(1)
+    flags = torch.empty(a.messages, dtype=torch.uint8, device=ts.device)
+    winner = torch.empty(a.cells, dtype=torch.int32, device=ts.device)
+
+    def step():
+        _, _, tree, _ = eng.apply_batch(empty, ts, cell, a.cells, flags=flags, winner=winner)
+        return tree
+
+    for _ in range(a.warmup):
+        step().free()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.prof_reset()
+    eng.prof_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tree = step()
+        tree.free()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    eng.prof_enable(False)
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=ts.device)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    prof = eng.prof_report()
+
+    if rank == 0:
+        ms_step = elapsed / a.steps * 1e3
+        value = world * a.messages * a.steps / elapsed
+        # dominant kernel and its roofline
+        known = {k: v for k, v in prof.items() if k in ALG_BYTES_PER_MSG}
+        dom = max(known, key=lambda k: known[k][0])
+        tot_ms, launches = known[dom]
+        avg_s = tot_ms / launches / 1e3
+        alg = ALG_BYTES_PER_MSG[dom] * a.messages
+        achieved = alg / avg_s
+        traffic = None
+        if os.path.exists(a.traffic):
+            t = json.load(open(a.traffic)).get(dom)
+            if t is not None:
+                traffic = t
+        roof = {"bound": "hbm", "kernel": dom, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK, "traffic": traffic,
+                "kernel_ms_avg": avg_s * 1e3, "alg_bytes_per_launch": alg,
+                "kernel_share_of_step": tot_ms / (ms_step * a.steps)}
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "msgs/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (seeded HLC streams, SURVEY 8(d) config 2)",
+            "config": {"workload": "config2: applyMessages, 1 owner per GPU, %d msgs, %d cells, 64 nodes, shuffled"
+                       % (a.messages, a.cells), "messages_per_gpu": a.messages, "cells": a.cells,
+                       "parallelism": "owner-sharded, %d rank(s)" % world},
+            "roofline": roof,
+            "pipeline": {"alg_bytes_per_msg": 120, "pipeline_hbm_frac": 120 * a.messages * world / (elapsed / a.steps) / world / HBM_PEAK,
+                         "kernels_ms_per_step": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}},
+            "cpu_baseline": None,
+        }
+        if world == 1 and a.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(ts_np, cell_np, a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -49,6 +49,9 @@ SIGNATURES = {
     "evm_set_stream": (_i, [_vp, _vp]),
     "evm_get_stream": (_vp, [_vp]),
     "evm_sync": (_i, [_vp]),
+    "evm_prof_enable": (_i, [_vp, _i]),
+    "evm_prof_reset": (_i, [_vp]),
+    "evm_prof_report": (_i, [_vp, _vp, _sz, C.POINTER(_sz)]),
     "evm_dev_alloc": (_i, [_vp, _sz, C.POINTER(_vp)]),
     "evm_dev_free": (_i, [_vp, _vp]),
     "evm_copy_h2d": (_i, [_vp, _vp, _vp, _sz]),
@@ -90,6 +93,10 @@ def load(path: str = LIB_PATH):
         raise RuntimeError(
             "libevm.so not built (%s); run `python -c 'import __graft_entry__ as g; g.build()'`" % path
         )
+    # torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's): load
+    # it first so the process holds ONE HIP runtime, shared with libevm.
+    import torch  # noqa: F401
+
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -10,7 +10,10 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdio.h>
+
 #include <algorithm>
+#include <string>
 #include <vector>
 
 #include "evm_device.hpp"
@@ -75,7 +78,7 @@ static int grid_for(size_t n, int threads, int cap = 8192) {
 int evm::launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,
                      Info* info) {
   if (n == 0) return EVM_OK;
-  hipLaunchKernelGGL(k_pack, dim3(grid_for(n, PACK_THREADS, 4096)), dim3(PACK_THREADS), 0, ctx->stream,
+  KLAUNCH(k_pack, dim3(grid_for(n, PACK_THREADS, 4096)), dim3(PACK_THREADS),
                      (const uint8_t*)ts, stride, n, aux, aux_limit, out, info);
   return hip_ok(hipGetLastError());
 }
@@ -92,9 +95,9 @@ int evm::scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out,
   const size_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
   T* part = S.alloc<T>(nt);
   if (!part) return EVM_ENOMEM;
-  hipLaunchKernelGGL((k_scan_reduce<T, Op<T>>), dim3(nt), dim3(SCAN_THREADS), 0, ctx->stream, in, n, part);
-  hipLaunchKernelGGL((k_scan_partials<T, Op<T>>), dim3(1), dim3(1024), 0, ctx->stream, part, nt, total_dev);
-  hipLaunchKernelGGL((k_scan_down<T, Op<T>>), dim3(nt), dim3(SCAN_THREADS), 0, ctx->stream, in, n, part, out);
+  KLAUNCH((k_scan_reduce<T, Op<T>>), dim3(nt), dim3(SCAN_THREADS), in, n, part);
+  KLAUNCH((k_scan_partials<T, Op<T>>), dim3(1), dim3(1024), part, nt, total_dev);
+  KLAUNCH((k_scan_down<T, Op<T>>), dim3(nt), dim3(SCAN_THREADS), in, n, part, out);
   return hip_ok(hipGetLastError());
 }
 template int evm::scan_exclusive<u32, OpAdd>(evm_ctx*, Scratch&, const u32*, size_t, u32*, u32*);
@@ -115,11 +118,11 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
   int shift = lo_bit;
   for (int p = 0; p < passes; ++p) {
     const int bits = std::min(width, hi_bit - shift);
-    hipLaunchKernelGGL((k_radix_hist<K>), dim3(ntiles), dim3(SORT_THREADS), 0, ctx->stream, keys, n, shift, bits, counts,
+    KLAUNCH((k_radix_hist<K>), dim3(ntiles), dim3(SORT_THREADS), keys, n, shift, bits, counts,
                        ntiles);
     int st = scan_exclusive<u32, OpAdd>(ctx, S, counts, (size_t)(1u << bits) * ntiles, offs, (u32*)nullptr);
     if (st) return st;
-    hipLaunchKernelGGL((k_radix_scatter<K>), dim3(ntiles), dim3(SORT_THREADS), 0, ctx->stream, keys, vals, k2, v2, n,
+    KLAUNCH((k_radix_scatter<K>), dim3(ntiles), dim3(SORT_THREADS), keys, vals, k2, v2, n,
                        shift, bits, offs, ntiles);
     std::swap(keys, k2);
     std::swap(vals, v2);
@@ -210,13 +213,13 @@ int evm::reduce_runs(evm_ctx* ctx, Scratch& S, const u64* ck, const int32_t* h, 
   u32* nrun = S.alloc<u32>(1);
   if (!head || !lid || !start || !pfx || !nrun) return EVM_ENOMEM;
   const int g = grid_for(m, 256);
-  hipLaunchKernelGGL(k_heads, dim3(g), dim3(256), 0, ctx->stream, ck, m, head);
+  KLAUNCH(k_heads, dim3(g), dim3(256), ck, m, head);
   int st = scan_exclusive<u32, OpAdd>(ctx, S, head, m, lid, nrun);
   if (st) return st;
   st = scan_exclusive<int32_t, OpXor>(ctx, S, h, m, pfx, pfx + m);
   if (st) return st;
-  hipLaunchKernelGGL(k_run_starts, dim3(g), dim3(256), 0, ctx->stream, ck, head, lid, m, start, out_ck);
-  hipLaunchKernelGGL(k_run_xor, dim3(g), dim3(256), 0, ctx->stream, start, pfx, nrun, m, out_xr);
+  KLAUNCH(k_run_starts, dim3(g), dim3(256), ck, head, lid, m, start, out_ck);
+  KLAUNCH(k_run_xor, dim3(g), dim3(256), start, pfx, nrun, m, out_xr);
   u32 L = 0;
   HIPR(hipMemcpyAsync(&L, nrun, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
@@ -300,7 +303,7 @@ int evm::tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, co
     HIPR(hipMemcpyAsync(t->ck, ck, sizeof(u64) * L, hipMemcpyDeviceToDevice, ctx->stream));
     HIPR(hipMemcpyAsync(t->xr, xr, sizeof(int32_t) * L, hipMemcpyDeviceToDevice, ctx->stream));
   }
-  hipLaunchKernelGGL(k_owner_off, dim3(grid_for(n_owners + 1, 256)), dim3(256), 0, ctx->stream, t->ck, (size_t)L,
+  KLAUNCH(k_owner_off, dim3(grid_for(n_owners + 1, 256)), dim3(256), t->ck, (size_t)L,
                      n_owners, t->off);
   st = scan_exclusive<int32_t, OpXor>(ctx, S, t->xr, L, t->pfx, t->pfx + L);
   if (st) {
@@ -339,9 +342,9 @@ int evm::fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owne
   u64* rck = S.alloc<u64>(tot);
   int32_t* rxr = S.alloc<int32_t>(tot);
   if (!mck || !mxr || !rck || !rxr) return EVM_ENOMEM;
-  hipLaunchKernelGGL(k_merge_a, dim3(grid_for(L0, 256)), dim3(256), 0, ctx->stream, in->ck, in->xr, (size_t)L0, nck,
+  KLAUNCH(k_merge_a, dim3(grid_for(L0, 256)), dim3(256), in->ck, in->xr, (size_t)L0, nck,
                      (size_t)L1, mck, mxr);
-  hipLaunchKernelGGL(k_merge_b, dim3(grid_for(L1, 256)), dim3(256), 0, ctx->stream, nck, nxr, (size_t)L1, in->ck,
+  KLAUNCH(k_merge_b, dim3(grid_for(L1, 256)), dim3(256), nck, nxr, (size_t)L1, in->ck,
                      (size_t)L0, mck, mxr);
   uint64_t L = 0;
   st = reduce_runs(ctx, S, mck, mxr, tot, rck, rxr, &L);
@@ -630,6 +633,8 @@ static int new_info(evm_ctx* ctx, Scratch& S, Info** out) {
 // ============================================================================
 // C ABI
 // ============================================================================
+static void prof_drain(evm_ctx* ctx);
+
 extern "C" {
 
 const char* evm_strerror(int s) {
@@ -665,7 +670,7 @@ int evm_create(int device, evm_ctx** out) {
 
 void evm_destroy(evm_ctx* ctx) {
   if (!ctx) return;
-  (void)hipStreamSynchronize(ctx->stream);
+  prof_drain(ctx);
   (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -680,6 +685,58 @@ void* evm_get_stream(evm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; 
 int evm_sync(evm_ctx* ctx) {
   if (!ctx) return EVM_EINVAL;
   return hip_ok(hipStreamSynchronize(ctx->stream));
+}
+
+int evm_prof_enable(evm_ctx* ctx, int on) {
+  if (!ctx) return EVM_EINVAL;
+  ctx->prof = on != 0;
+  return EVM_OK;
+}
+
+}  // extern "C"
+static void prof_drain(evm_ctx* ctx) {
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->prof_events) {
+    auto& tot = ctx->prof_total[kv.first];
+    for (auto& ev : kv.second) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, ev.first, ev.second) == hipSuccess) tot.first += ms;
+      tot.second += 1;
+      (void)hipEventDestroy(ev.first);
+      (void)hipEventDestroy(ev.second);
+    }
+  }
+  ctx->prof_events.clear();
+}
+extern "C" {
+
+int evm_prof_reset(evm_ctx* ctx) {
+  if (!ctx) return EVM_EINVAL;
+  prof_drain(ctx);
+  ctx->prof_total.clear();
+  return EVM_OK;
+}
+
+int evm_prof_report(evm_ctx* ctx, char* buf, size_t cap, size_t* len) {
+  if (!ctx || !len) return EVM_EINVAL;
+  prof_drain(ctx);
+  std::string js = "{";
+  bool first = true;
+  char tmp[128];
+  for (auto& kv : ctx->prof_total) {
+    if (!first) js += ",";
+    first = false;
+    js += "\"" + kv.first + "\":";
+    snprintf(tmp, sizeof tmp, "[%.6f,%llu]", kv.second.first, (unsigned long long)kv.second.second);
+    js += tmp;
+  }
+  js += "}";
+  *len = js.size();
+  if (buf) {
+    if (cap < js.size()) return EVM_ECAPACITY;
+    memcpy(buf, js.data(), js.size());
+  }
+  return EVM_OK;
 }
 
 int evm_dev_alloc(evm_ctx* ctx, size_t bytes, void** out) {
@@ -795,7 +852,7 @@ int evm_tree_roots(evm_ctx* ctx, const evm_tree* t, int32_t* root, uint8_t* pres
   uint8_t* dp = S.alloc<uint8_t>(std::max<u32>(t->n_owners, 1));
   if (!dr || !dp) return EVM_ENOMEM;
   if (t->n_owners == 0) return EVM_OK;
-  hipLaunchKernelGGL(k_roots, dim3(grid_for(t->n_owners, 256)), dim3(256), 0, ctx->stream, t->off, t->pfx, t->n_owners,
+  KLAUNCH(k_roots, dim3(grid_for(t->n_owners, 256)), dim3(256), t->off, t->pfx, t->n_owners,
                      dr, dp);
   HIPR(hipMemcpyAsync(root, dr, sizeof(int32_t) * t->n_owners, hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipMemcpyAsync(present, dp, t->n_owners, hipMemcpyDeviceToHost, ctx->stream));
@@ -816,7 +873,7 @@ int evm_merkle_insert(evm_ctx* ctx, const evm_tree* in, const char* ts, size_t s
   st = launch_pack(ctx, ts, stride, n, owner, in->n_owners, rec, info);
   if (st) return st;
   if (n)
-    hipLaunchKernelGGL(k_fold_prep, dim3(grid_for(n, 256, 4096)), dim3(256), 0, ctx->stream, rec, (const uint8_t*)nullptr,
+    KLAUNCH(k_fold_prep, dim3(grid_for(n, 256, 4096)), dim3(256), rec, (const uint8_t*)nullptr,
                        (uint8_t)0, (const u32*)nullptr, (int)(owner ? OWNER_AUX : OWNER_ZERO), (const u32*)nullptr, n, ck,
                        h, info);
   Info hi;
@@ -833,7 +890,7 @@ int evm_merkle_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t*
   if (!ctx || !a || !b || !millis || a->n_owners != b->n_owners) return EVM_EINVAL;
   if (a->n_owners == 0) return EVM_OK;
   TreeView A{a->off, a->ck, a->pfx}, B{b->off, b->ck, b->pfx};
-  hipLaunchKernelGGL(k_diff, dim3(grid_for(a->n_owners, 64, 1 << 16)), dim3(64), 0, ctx->stream, A, B, a->n_owners,
+  KLAUNCH(k_diff, dim3(grid_for(a->n_owners, 64, 1 << 16)), dim3(64), A, B, a->n_owners,
                      millis);
   HIPR(hipGetLastError());
   return evm_sync(ctx);
@@ -874,7 +931,7 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
     }
   }
   if (n_cells)
-    hipLaunchKernelGGL(k_fill_i32, dim3(grid_for(n_cells, 256)), dim3(256), 0, ctx->stream, winner, (size_t)n_cells, -1);
+    KLAUNCH(k_fill_i32, dim3(grid_for(n_cells, 256)), dim3(256), winner, (size_t)n_cells, -1);
   if (n == 0) {
     st = tree_finalize(ctx, S, tree_in->n_owners, tree_in->ck, tree_in->xr, tree_in->n_leaves, tree_out);
     return st ? st : evm_sync(ctx);
@@ -884,13 +941,13 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
   u64* table = S.alloc<u64>((size_t)1 << lg);
   if (!table) return EVM_ENOMEM;
   HIPR(hipMemsetAsync(table, 0, sizeof(u64) << lg, ctx->stream));
-  hipLaunchKernelGGL(k_xcell, dim3(grid_for(n, 256, 8192)), dim3(256), 0, ctx->stream, rec, n, table, (u32)lg, info);
+  KLAUNCH(k_xcell, dim3(grid_for(n, 256, 8192)), dim3(256), rec, n, table, (u32)lg, info);
   // (2) stable sort (cell, index)
   u32* cell_s = S.alloc<u32>(n);
   u32* idx_s = S.alloc<u32>(n);
   if (!cell_s || !idx_s) return EVM_ENOMEM;
   HIPR(hipMemcpyAsync(cell_s, cell, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
-  hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, idx_s, n);
+  KLAUNCH(k_iota, dim3(grid_for(n, 256)), dim3(256), idx_s, n);
   const int cbits = n_cells > 1 ? 32 - __builtin_clz(n_cells - 1) : 0;
   if ((st = radix_sort_pairs<u32>(ctx, S, cell_s, idx_s, n, 0, cbits))) return st;
   // (3) segmented running max + decisions
@@ -898,9 +955,9 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
   u32* t_head = S.alloc<u32>(nt);
   Key* t_key = S.alloc<Key>(nt);
   if (!t_head || !t_key) return EVM_ENOMEM;
-  hipLaunchKernelGGL(k_lww_reduce, dim3(nt), dim3(LWW_THREADS), 0, ctx->stream, rec, cell_s, idx_s, n, t_head, t_key);
-  hipLaunchKernelGGL(k_lww_tiles, dim3(1), dim3(LWW_THREADS), 0, ctx->stream, t_head, t_key, nt);
-  hipLaunchKernelGGL(k_lww_apply, dim3(nt), dim3(LWW_THREADS), 0, ctx->stream, rec, cell_s, idx_s, n, t_head, t_key,
+  KLAUNCH(k_lww_reduce, dim3(nt), dim3(LWW_THREADS), rec, cell_s, idx_s, n, t_head, t_key);
+  KLAUNCH(k_lww_tiles, dim3(1), dim3(LWW_THREADS), t_head, t_key, nt);
+  KLAUNCH(k_lww_apply, dim3(nt), dim3(LWW_THREADS), rec, cell_s, idx_s, n, t_head, t_key,
                      prior, prior_present, flags, winner);
   // (4) Merkle fold of the XOR messages
   u32* sel = S.alloc<u32>(n);
@@ -909,14 +966,14 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
   u64* ck = S.alloc<u64>(n);
   u32* h = S.alloc<u32>(n);
   if (!sel || !pos || !cnt || !ck || !h) return EVM_ENOMEM;
-  hipLaunchKernelGGL(k_sel_u32, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, flags, (uint8_t)EVM_MSG_XOR, n, sel);
+  KLAUNCH(k_sel_u32, dim3(grid_for(n, 256)), dim3(256), flags, (uint8_t)EVM_MSG_XOR, n, sel);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, pos, cnt))) return st;
-  hipLaunchKernelGGL(k_fold_prep, dim3(grid_for(n, 256, 4096)), dim3(256), 0, ctx->stream, rec, flags,
+  KLAUNCH(k_fold_prep, dim3(grid_for(n, 256, 4096)), dim3(256), rec, flags,
                      (uint8_t)EVM_MSG_XOR, pos, (int)(cell_owner ? OWNER_CELL : OWNER_ZERO), cell_owner, n, ck, h, info);
   Info hi;
   if ((st = read_info(ctx, info, &hi))) return st;
   if (hi.bad) {
-    hipLaunchKernelGGL(k_mark_bad, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, rec, n, flags);
+    KLAUNCH(k_mark_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
     (void)evm_sync(ctx);
     return EVM_ENONCANON;
   }

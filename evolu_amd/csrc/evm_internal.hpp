@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/evm.h"
@@ -11,6 +14,10 @@ struct evm_ctx {
   int device;
   hipStream_t own;
   hipStream_t stream;
+  // kernel timing (evm_prof_*): HIP event pairs per kernel name, on `stream`
+  bool prof = false;
+  std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> prof_events;
+  std::map<std::string, std::pair<double, uint64_t>> prof_total;  // ms, launches (drained)
 };
 
 // One MerkleTree per owner, as sorted unique leaves keyed by
@@ -83,6 +90,35 @@ class Scratch {
   evm_ctx* ctx_;
   std::vector<void*> ptrs_;
 };
+
+// Records a start/stop event pair around one launch when profiling is on.
+class ProfScope {
+ public:
+  ProfScope(evm_ctx* c, const char* name) : ctx_(c), name_(name) {
+    if (ctx_->prof && hipEventCreate(&a_) == hipSuccess && hipEventCreate(&b_) == hipSuccess)
+      (void)hipEventRecord(a_, ctx_->stream);
+    else
+      a_ = b_ = nullptr;
+  }
+  ~ProfScope() {
+    if (a_ && b_) {
+      (void)hipEventRecord(b_, ctx_->stream);
+      ctx_->prof_events[name_].push_back({a_, b_});
+    }
+  }
+
+ private:
+  evm_ctx* ctx_;
+  const char* name_;
+  hipEvent_t a_ = nullptr, b_ = nullptr;
+};
+
+// Every kernel launch goes through KLAUNCH (needs `ctx` in scope).
+#define KLAUNCH(kern, grid, block, ...)                                  \
+  do {                                                                   \
+    evm::ProfScope ps_(ctx, #kern);                                      \
+    hipLaunchKernelGGL(kern, grid, block, 0, ctx->stream, __VA_ARGS__); \
+  } while (0)
 
 enum OwnerMode { OWNER_ZERO = 0, OWNER_AUX = 1, OWNER_CELL = 2 };
 

@@ -75,6 +75,23 @@ class Engine:
         except Exception:
             pass
 
+    # ------------------------------------------------------------- profiling
+    def prof_enable(self, on: bool = True):
+        check(self.lib.evm_prof_enable(self.h, 1 if on else 0), "evm_prof_enable")
+
+    def prof_reset(self):
+        check(self.lib.evm_prof_reset(self.h), "evm_prof_reset")
+
+    def prof_report(self) -> dict:
+        """{kernel name: (total ms, launches)} from HIP events on the engine stream."""
+        import json
+
+        ln = C.c_size_t()
+        check(self.lib.evm_prof_report(self.h, None, 0, C.byref(ln)), "evm_prof_report")
+        buf = C.create_string_buffer(ln.value + 64)
+        check(self.lib.evm_prof_report(self.h, buf, ln.value + 64, C.byref(ln)), "evm_prof_report")
+        return {k: (v[0], int(v[1])) for k, v in json.loads(buf.raw[: ln.value].decode()).items()}
+
     # --------------------------------------------------------------- buffers
     def dev(self, a: np.ndarray) -> torch.Tensor:
         return torch.from_numpy(np.ascontiguousarray(a)).to(f"cuda:{self.device}")

@@ -82,6 +82,11 @@ const char* evm_strerror(int status);
 int evm_set_stream(evm_ctx* ctx, void* hip_stream); /* NULL: the HIP default stream; initially the context's own */
 void* evm_get_stream(evm_ctx* ctx);
 int evm_sync(evm_ctx* ctx);
+/* kernel timing with HIP events on the context stream (for roofline reports) */
+int evm_prof_enable(evm_ctx* ctx, int on);
+int evm_prof_reset(evm_ctx* ctx);
+/* JSON {"kernel": [total_ms, launches], ...}; *len = bytes needed */
+int evm_prof_report(evm_ctx* ctx, char* buf, size_t cap, size_t* len);
 int evm_dev_alloc(evm_ctx* ctx, size_t bytes, void** out);
 int evm_dev_free(evm_ctx* ctx, void* p);
 int evm_copy_h2d(evm_ctx* ctx, void* dst_dev, const void* src_host, size_t bytes);
