@@ -31,6 +31,8 @@ MSG_XOR = 0x02
 MSG_INS = 0x04
 MSG_BAD = 0x80
 
+OPT_CLIENT_PATH = 1
+
 DIFF_NONE = -1
 DIFF_RANGE_ERROR = -2
 
@@ -49,6 +51,7 @@ SIGNATURES = {
     "evm_set_stream": (_i, [_vp, _vp]),
     "evm_get_stream": (_vp, [_vp]),
     "evm_sync": (_i, [_vp]),
+    "evm_set_option": (_i, [_vp, _i, C.c_int64]),
     "evm_prof_enable": (_i, [_vp, _i]),
     "evm_prof_reset": (_i, [_vp]),
     "evm_prof_report": (_i, [_vp, _vp, _sz, C.POINTER(_sz)]),

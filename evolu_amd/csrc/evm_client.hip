@@ -1,0 +1,773 @@
+// applyMessages (packages/evolu/src/applyMessages.ts:26-131) on MI355X.
+//
+// Sequential reference semantics, per message i of the batch, in cell c:
+//   t_i = max timestamp of c in __message before i  (prior rows + earlier batch rows)
+//   ups_i = t_i == null || t_i < ts_i     (:93  upsert the user-table cell)
+//   xor_i = t_i == null || t_i !== ts_i   (:105 INSERT ... ON CONFLICT DO NOTHING + Merkle XOR)
+// With no timestamp repeated across cells (checked exactly, k_xcell), t_i is the
+// exclusive running max of c in batch order seeded with the prior max, because a
+// repeat of an older timestamp of c never moves the max.  Two device paths:
+//   * fast path (one owner, <= CL_MAX_CELLS cells): wave-ranges stream the batch
+//     twice, per-cell state in LDS, no global sort (evm_client.hip: k_cl_*);
+//   * general path: stable radix sort by cell + segmented scan (k_lww_*).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "evm_device.hpp"
+#include "evm_internal.hpp"
+#include "evm_prims.hpp"
+
+using namespace evm;
+// ============================================================================
+// applyMessages (applyMessages.ts:26-131)
+// ============================================================================
+
+// (1) Global __message PK: the same timestamp in two different cells of one
+// batch makes the reference's INSERT fail silently for the later one and
+// stops that cell's running max from advancing.  That interleaving is
+// inherently sequential, so it is detected exactly and reported.
+__global__ void k_xcell(const evm_rec* __restrict__ rec, size_t n, u64* __restrict__ table, u32 log2size,
+                        Info* __restrict__ info) {
+  const u64 mask = (1ull << log2size) - 1;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const evm_rec r = rec[i];
+    if (!(r.meta & EVM_META_VALID)) continue;
+    const u64 mine = ((u64)r.hash << 32) | (u64)(i + 1);
+    u64 pos = ((u64)(r.hash * 2654435761u) ^ (r.node * 0x9E3779B97F4A7C15ull >> 20)) & mask;
+    for (u64 probe = 0; probe <= mask; ++probe) {
+      u64 s = __hip_atomic_load(&table[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s == 0) {
+        const u64 prev = atomicCAS(&table[pos], 0ull, mine);
+        if (prev == 0) break;  // inserted
+        s = prev;
+      }
+      if ((u32)(s >> 32) == r.hash) {
+        const evm_rec o = rec[(size_t)(s & 0xffffffffu) - 1];
+        if (o.tc == r.tc && o.node == r.node && (o.meta & EVM_META_CASEMASK) == (r.meta & EVM_META_CASEMASK)) {
+          if (o.aux != r.aux) atomicOr(&info->collision, 1u);
+          break;
+        }
+      }
+      pos = (pos + 1) & mask;
+    }
+  }
+}
+
+// (2) Segmented (per cell) running max in batch order over the cell-sorted
+// order.  Aggregate = (segment head seen, max since the last head).
+struct SegAgg {
+  u32 head;
+  Key key;
+};
+__device__ __forceinline__ SegAgg seg_combine(const SegAgg& a, const SegAgg& b) {
+  SegAgg r;
+  r.head = a.head | b.head;
+  r.key = b.head ? b.key : key_max(a.key, b.key);
+  return r;
+}
+
+constexpr int LWW_THREADS = 256;
+constexpr int LWW_ITEMS = 8;
+constexpr int LWW_TILE = LWW_THREADS * LWW_ITEMS;
+
+__device__ __forceinline__ SegAgg lww_elem(const evm_rec* rec, const u32* cell_s, const u32* idx_s, size_t p) {
+  SegAgg e;
+  e.head = (p == 0 || cell_s[p] != cell_s[p - 1]) ? 1u : 0u;
+  e.key = key_of(rec[idx_s[p]]);
+  return e;
+}
+
+struct SegLds {
+  u32 head[LWW_THREADS];
+  u64 tc[LWW_THREADS];
+  u64 node[LWW_THREADS];
+  u32 mask[LWW_THREADS];
+};
+__device__ __forceinline__ void seg_put(SegLds& L, int t, const SegAgg& a) {
+  L.head[t] = a.head;
+  L.tc[t] = a.key.tc;
+  L.node[t] = a.key.node;
+  L.mask[t] = a.key.mask;
+}
+__device__ __forceinline__ SegAgg seg_get(const SegLds& L, int t) {
+  SegAgg a;
+  a.head = L.head[t];
+  a.key = Key{L.tc[t], L.node[t], L.mask[t]};
+  return a;
+}
+
+// Block inclusive scan (Hillis-Steele over LDS) of one SegAgg per thread.
+__device__ SegAgg seg_block_inclusive(SegLds& L, SegAgg v) {
+  const int t = threadIdx.x;
+  seg_put(L, t, v);
+  __syncthreads();
+  for (int d = 1; d < LWW_THREADS; d <<= 1) {
+    SegAgg o;
+    const bool has = t >= d;
+    if (has) o = seg_get(L, t - d);
+    __syncthreads();
+    if (has) v = seg_combine(o, v);
+    seg_put(L, t, v);
+    __syncthreads();
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(LWW_THREADS) void k_lww_reduce(const evm_rec* __restrict__ rec, const u32* __restrict__ cell_s,
+                                                            const u32* __restrict__ idx_s, size_t n,
+                                                            u32* __restrict__ t_head, Key* __restrict__ t_key) {
+  __shared__ SegLds L;
+  const size_t base = (size_t)blockIdx.x * LWW_TILE + (size_t)threadIdx.x * LWW_ITEMS;
+  SegAgg acc{0u, key_none()};
+  for (int k = 0; k < LWW_ITEMS; ++k) {
+    const size_t p = base + k;
+    if (p < n) acc = seg_combine(acc, lww_elem(rec, cell_s, idx_s, p));
+  }
+  const SegAgg inc = seg_block_inclusive(L, acc);
+  if (threadIdx.x == LWW_THREADS - 1) {
+    t_head[blockIdx.x] = inc.head;
+    t_key[blockIdx.x] = inc.key;
+  }
+}
+
+// Exclusive scan of the tile aggregates, in one block.
+__global__ __launch_bounds__(LWW_THREADS) void k_lww_tiles(u32* __restrict__ t_head, Key* __restrict__ t_key, size_t nt) {
+  __shared__ SegLds L;
+  const size_t per = (nt + LWW_THREADS - 1) / LWW_THREADS;
+  const size_t b = (size_t)threadIdx.x * per;
+  SegAgg acc{0u, key_none()};
+  for (size_t i = b; i < b + per && i < nt; ++i) acc = seg_combine(acc, SegAgg{t_head[i], t_key[i]});
+  const SegAgg inc = seg_block_inclusive(L, acc);
+  // exclusive for this thread = inclusive of thread-1
+  __syncthreads();
+  seg_put(L, threadIdx.x, inc);
+  __syncthreads();
+  SegAgg run = threadIdx.x ? seg_get(L, threadIdx.x - 1) : SegAgg{0u, key_none()};
+  for (size_t i = b; i < b + per && i < nt; ++i) {
+    const SegAgg here{t_head[i], t_key[i]};
+    t_head[i] = run.head;
+    t_key[i] = run.key;
+    run = seg_combine(run, here);
+  }
+}
+
+__global__ __launch_bounds__(LWW_THREADS) void k_lww_apply(const evm_rec* __restrict__ rec, const u32* __restrict__ cell_s,
+                                                           const u32* __restrict__ idx_s, size_t n,
+                                                           const u32* __restrict__ t_head, const Key* __restrict__ t_key,
+                                                           const evm_rec* __restrict__ prior,
+                                                           const uint8_t* __restrict__ prior_present,
+                                                           uint8_t* __restrict__ flags, int32_t* __restrict__ winner) {
+  __shared__ SegLds L;
+  const size_t base = (size_t)blockIdx.x * LWW_TILE + (size_t)threadIdx.x * LWW_ITEMS;
+  SegAgg e[LWW_ITEMS];
+  SegAgg acc{0u, key_none()};
+#pragma unroll
+  for (int k = 0; k < LWW_ITEMS; ++k) {
+    const size_t p = base + k;
+    e[k] = p < n ? lww_elem(rec, cell_s, idx_s, p) : SegAgg{0u, key_none()};
+    acc = seg_combine(acc, e[k]);
+  }
+  const SegAgg inc = seg_block_inclusive(L, acc);
+  __syncthreads();
+  seg_put(L, threadIdx.x, inc);
+  __syncthreads();
+  SegAgg run = SegAgg{t_head[blockIdx.x], t_key[blockIdx.x]};
+  if (threadIdx.x) run = seg_combine(run, seg_get(L, threadIdx.x - 1));
+#pragma unroll
+  for (int k = 0; k < LWW_ITEMS; ++k) {
+    const size_t p = base + k;
+    if (p >= n) break;
+    const Key excl = e[k].head ? key_none() : run.key;
+    run = seg_combine(run, e[k]);
+    const u32 c = cell_s[p];
+    const u32 i = idx_s[p];
+    Key t = excl;
+    if (prior_present && prior_present[c]) t = key_max(t, key_of(prior[c]));
+    const Key ts = e[k].key;
+    // applyMessages.ts:93  t == null || t < message.timestamp
+    const bool ups = key_cmp(t, ts) < 0;
+    // applyMessages.ts:105 t == null || t !== message.timestamp
+    const bool xr = !((t.mask & KEY_PRESENT) && key_eq(t, ts));
+    flags[i] = (ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u);
+    if (ups) atomicMax(&winner[c], (int32_t)i);
+  }
+}
+
+__global__ void k_mark_bad(const evm_rec* __restrict__ rec, size_t n, uint8_t* __restrict__ flags) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    flags[i] = (rec[i].meta & EVM_META_VALID) ? 0u : EVM_MSG_BAD;
+}
+
+__global__ void k_fill_i32(int32_t* __restrict__ p, size_t n, int32_t v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+
+
+// ============================================================================
+// Fast path: one owner, n_cells <= CL_MAX_CELLS.
+//
+// The batch is cut into G contiguous wave-ranges (one 64-lane workgroup each).
+// A range keeps per-cell state in LDS and walks its messages 64 at a time; the
+// lanes of one round that hit the same cell are matched with ballots and
+// combined in lane (= batch) order.
+//   pass 1: per range and cell, the max timestamp and its first index
+//   carry : per cell, exclusive scan over ranges (seeded with the prior max);
+//           the final winner is the first index of the cell's overall max
+//   pass 2: re-walk with the carried state: exclusive max t_i -> flags; write
+//           (minute, hash) of every XOR message for the Merkle fold
+// The timestamp bytes are streamed twice (re-parsing is cheaper than a round
+// trip of a packed record), never sorted, never gathered.
+// ============================================================================
+constexpr u32 CL_MAX_CELLS = 2048;
+constexpr int CL_RANGE_TARGET = 1280;  // ~5 ranges per CU
+constexpr u32 FOLD_WIN = 32768;        // minutes per LDS histogram window (128 KiB)
+constexpr u32 FOLD_MAXWIN = 4;
+constexpr u32 FOLD_CHUNKS = 64;
+constexpr int FOLD_THREADS = 1024;
+
+struct ClMsg {
+  Key key;
+  u32 hash;
+  u32 minute;
+  u32 cell;
+  u32 meta;
+};
+
+// Loads and parses message `i` of the wave's 64-message block starting at
+// `first`.  For stride 48 the block (3 KiB) is read with fully coalesced
+// 16-B loads and re-distributed through LDS.
+__device__ __forceinline__ ClMsg cl_load(const uint8_t* __restrict__ ts, size_t stride, const u32* __restrict__ cell,
+                                         size_t first, size_t n, uint4* __restrict__ stage) {
+  const int lane = threadIdx.x & 63;
+  const size_t i = first + lane;
+  u32 w[12];
+  if (stride == 48) {
+    const uint4* src = reinterpret_cast<const uint4*>(ts + first * 48);
+    const size_t nq = (n - first) * 3;  // 16-B quads left in the arena from `first`
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const size_t q = (size_t)lane + 64 * k;
+      stage[q] = q < nq ? src[q] : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    const uint4 a = stage[3 * lane], b = stage[3 * lane + 1], c = stage[3 * lane + 2];
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
+    __syncthreads();
+  } else if (i < n) {
+    load_ts(ts, stride, i, w);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) w[k] = 0;
+  }
+  const Parsed p = parse_ts46(w);
+  ClMsg m;
+  m.key = Key{p.tc, p.node, (p.meta & EVM_META_CASEMASK) | KEY_PRESENT};
+  m.hash = p.hash;
+  m.minute = p.minute;
+  m.meta = p.meta;
+  m.cell = i < n ? cell[i] : 0xffffffffu;
+  return m;
+}
+
+__device__ __forceinline__ Key shfl_key(const Key& k, int src) {
+  Key o;
+  o.tc = ((u64)(u32)__shfl((int)(u32)(k.tc >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)k.tc, src, 64);
+  o.node = ((u64)(u32)__shfl((int)(u32)(k.node >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)k.node, src, 64);
+  o.mask = (u32)__shfl((int)k.mask, src, 64);
+  return o;
+}
+
+// Lanes whose `cell` equals this lane's (among `active`), by ballots on the bits.
+__device__ __forceinline__ u64 match_cell(u32 c, bool active, int bits) {
+  u64 peers = __ballot(active);
+  for (int b = 0; b < bits; ++b) {
+    const bool bit = (c >> b) & 1u;
+    const u64 bal = __ballot(bit);
+    peers &= bit ? bal : ~bal;
+  }
+  return active ? peers : 0ull;
+}
+
+template <int PASS>
+__global__ __launch_bounds__(64) void k_cl_pass(const uint8_t* __restrict__ ts, size_t stride,
+                                                const u32* __restrict__ cell, size_t n, u32 C, int cbits,
+                                                size_t range_len, u64* __restrict__ agg_tc, u64* __restrict__ agg_node,
+                                                u32* __restrict__ agg_mask, u32* __restrict__ agg_first,
+                                                u32* __restrict__ hash_out, uint8_t* __restrict__ flags,
+                                                u64* __restrict__ pairs, Info* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* stage = reinterpret_cast<uint4*>(smem);                  // 3 KiB
+  u64* s_tc = reinterpret_cast<u64*>(smem + 3072);                // C
+  u64* s_node = s_tc + C;                                         // C
+  u32* s_mask = reinterpret_cast<u32*>(s_node + C);               // C
+  u32* s_first = s_mask + C;                                      // C (pass 1)
+  const int lane = threadIdx.x;
+  const size_t g = blockIdx.x;
+  const size_t beg = g * range_len;
+  const size_t end = min(n, beg + range_len);
+  for (u32 c = lane; c < C; c += 64) {
+    if (PASS == 1) {
+      s_tc[c] = 0;
+      s_node[c] = 0;
+      s_mask[c] = 0;
+      s_first[c] = 0xffffffffu;
+    } else {
+      s_tc[c] = agg_tc[g * C + c];
+      s_node[c] = agg_node[g * C + c];
+      s_mask[c] = agg_mask[g * C + c];
+    }
+  }
+  __syncthreads();
+  const u64 lt = lanemask_lt();
+  u32 bad = 0, bad_aux = 0, mn = 0xffffffffu, mx = 0;
+  for (size_t first = beg; first < end; first += 64) {
+    const ClMsg m = cl_load(ts, stride, cell, first, end, stage);
+    const size_t i = first + lane;
+    const bool live = i < end;
+    const bool valid = (m.meta & EVM_META_VALID) != 0;
+    const bool ok = live && valid && m.cell < C;
+    if (PASS == 1) {
+      bad |= (live && !valid) ? 1u : 0u;
+      bad_aux |= (live && m.cell >= C) ? 1u : 0u;
+      if (live) hash_out[i] = m.hash;
+      if (ok) {
+        mn = min(mn, m.minute);
+        mx = max(mx, m.minute);
+      }
+    }
+    const u64 peers = match_cell(m.cell, ok, cbits);
+    const bool last_peer = ok && (peers >> lane) == 1ull;
+    u64 rem = peers & lt;
+    if (PASS == 1) {
+      // round max of this lane's cell over peers up to this lane, first index wins ties
+      Key acc = key_none();
+      u32 acc_i = 0xffffffffu;
+      while (__any(rem != 0)) {
+        const int src = rem ? (int)__builtin_ctzll(rem) : lane;
+        const Key kp = shfl_key(m.key, src);
+        if (rem) {
+          if (key_cmp(kp, acc) > 0) {
+            acc = kp;
+            acc_i = (u32)(first + src);
+          }
+          rem &= rem - 1;
+        }
+      }
+      if (ok && key_cmp(m.key, acc) > 0) {
+        acc = m.key;
+        acc_i = (u32)i;
+      }
+      if (last_peer) {
+        const Key st{s_tc[m.cell], s_node[m.cell], s_mask[m.cell]};
+        if (key_cmp(acc, st) > 0) {
+          s_tc[m.cell] = acc.tc;
+          s_node[m.cell] = acc.node;
+          s_mask[m.cell] = acc.mask;
+          s_first[m.cell] = acc_i;
+        }
+      }
+    } else {
+      Key acc = ok ? Key{s_tc[m.cell], s_node[m.cell], s_mask[m.cell]} : key_none();
+      while (__any(rem != 0)) {
+        const int src = rem ? (int)__builtin_ctzll(rem) : lane;
+        const Key kp = shfl_key(m.key, src);
+        if (rem) {
+          acc = key_max(acc, kp);
+          rem &= rem - 1;
+        }
+      }
+      if (live) {
+        // applyMessages.ts:93 / :105 with t = acc
+        const bool ups = ok && key_cmp(acc, m.key) < 0;
+        const bool xr = ok && !((acc.mask & KEY_PRESENT) && key_eq(acc, m.key));
+        flags[i] = ok ? (uint8_t)((ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u)) : (uint8_t)EVM_MSG_BAD;
+        pairs[i] = xr ? ((u64)m.hash << 32 | (u64)m.minute) : ~0ull;
+      }
+      if (last_peer) {
+        const Key inc = key_max(acc, m.key);
+        s_tc[m.cell] = inc.tc;
+        s_node[m.cell] = inc.node;
+        s_mask[m.cell] = inc.mask;
+      }
+    }
+  }
+  if (PASS == 1) {
+    __syncthreads();
+    for (u32 c = lane; c < C; c += 64) {
+      agg_tc[g * C + c] = s_tc[c];
+      agg_node[g * C + c] = s_node[c];
+      agg_mask[g * C + c] = s_mask[c];
+      agg_first[g * C + c] = s_first[c];
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+      bad |= __shfl_xor(bad, d, 64);
+      bad_aux |= __shfl_xor(bad_aux, d, 64);
+      mn = min(mn, (u32)__shfl_xor(mn, d, 64));
+      mx = max(mx, (u32)__shfl_xor(mx, d, 64));
+    }
+    if (lane == 0) {
+      if (bad) atomicOr(&info->bad, 1u);
+      if (bad_aux) atomicOr(&info->bad_aux, 1u);
+      if (mn != 0xffffffffu) {
+        atomicMin(&info->minute_min, mn);
+        atomicMax(&info->minute_max, mx);
+      }
+    }
+  }
+}
+
+// Per cell: exclusive scan of the range aggregates in batch order, seeded with
+// the prior max.  Rewrites agg_* in place into the carry-in of every range.
+__global__ void k_cl_carry(u32 C, size_t G, u64* __restrict__ agg_tc, u64* __restrict__ agg_node,
+                           u32* __restrict__ agg_mask, const u32* __restrict__ agg_first,
+                           const evm_rec* __restrict__ prior, const uint8_t* __restrict__ prior_present,
+                           int32_t* __restrict__ winner) {
+  const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  Key run = (prior_present && prior_present[c]) ? key_of(prior[c]) : key_none();
+  int32_t first = -1;
+  for (size_t g = 0; g < G; ++g) {
+    const size_t k = g * C + c;
+    const Key a{agg_tc[k], agg_node[k], agg_mask[k]};
+    const u32 ai = agg_first[k];
+    agg_tc[k] = run.tc;
+    agg_node[k] = run.node;
+    agg_mask[k] = run.mask;
+    if (key_cmp(a, run) > 0) {
+      run = a;
+      first = (int32_t)ai;
+    }
+  }
+  winner[c] = first;
+}
+
+// Exact cross-cell check over a persistent epoch-tagged hash set:
+// slot = epoch:8 | hash low 24 bits:24 | (index + 1):32.  Equal fingerprints
+// compare the raw 46 timestamp bytes.
+__device__ __forceinline__ bool ts_bytes_equal(const uint8_t* ts, size_t stride, size_t a, size_t b) {
+  u32 wa[12], wb[12];
+  load_ts(ts, stride, a, wa);
+  load_ts(ts, stride, b, wb);
+  bool eq = true;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) eq &= wa[k] == wb[k];
+  return eq;
+}
+
+__global__ void k_cl_xcell(const uint8_t* __restrict__ ts, size_t stride, const u32* __restrict__ cell,
+                           const u32* __restrict__ hash, size_t n, u64* __restrict__ table, u32 lg, u32 epoch,
+                           Info* __restrict__ info) {
+  const u64 mask = (1ull << lg) - 1;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const u32 h = hash[i];
+    const u64 mine = ((u64)epoch << 56) | ((u64)(h & 0xffffffu) << 32) | (u64)(i + 1);
+    u64 pos = ((u64)(h * 2654435761u) << 32 | (u64)(h * 0x85ebca6bu)) >> (64 - lg);
+    for (u64 probe = 0; probe <= mask; ++probe) {
+      u64 s = __hip_atomic_load(&table[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((u32)(s >> 56) != epoch) {
+        const u64 prev = atomicCAS(&table[pos], s, mine);
+        if (prev == s) break;  // inserted
+        s = prev;
+        if ((u32)(s >> 56) != epoch) continue;  // lost to a stale rewrite? retry this slot
+      }
+      if ((u32)(s >> 32 & 0xffffffu) == (h & 0xffffffu)) {
+        const size_t j = (size_t)(s & 0xffffffffu) - 1;
+        if (ts_bytes_equal(ts, stride, i, j)) {
+          if (cell[i] != cell[j]) atomicOr(&info->collision, 1u);
+          break;
+        }
+      }
+      pos = (pos + 1) & mask;
+    }
+  }
+}
+
+// Dense Merkle fold over [minute_min, minute_min + FOLD_MAXWIN * FOLD_WIN):
+// per (window, chunk) an LDS XOR histogram + presence bitmap.
+__global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const u64* __restrict__ pairs, size_t n,
+                                                              u32* __restrict__ px, u32* __restrict__ pp,
+                                                              Info* __restrict__ info) {
+  __shared__ u32 hist[FOLD_WIN];
+  __shared__ u32 pres[FOLD_WIN / 32];
+  const u32 mlo = info->minute_min, mhi = info->minute_max;
+  if (mlo > mhi) return;  // no valid message
+  const u32 nwin = (mhi - mlo) / FOLD_WIN + 1;
+  if (nwin > FOLD_MAXWIN || base3_len(mlo) != base3_len(mhi)) {
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicOr(&info->fold_overflow, 1u);
+    return;
+  }
+  const u32 w = blockIdx.y;
+  if (w >= nwin) return;
+  for (u32 b = threadIdx.x; b < FOLD_WIN; b += FOLD_THREADS) hist[b] = 0;
+  for (u32 b = threadIdx.x; b < FOLD_WIN / 32; b += FOLD_THREADS) pres[b] = 0;
+  __syncthreads();
+  const u32 base = mlo + w * FOLD_WIN;
+  const size_t per = (n + FOLD_CHUNKS - 1) / FOLD_CHUNKS;
+  const size_t a = (size_t)blockIdx.x * per, e = min(n, a + per);
+  for (size_t i = a + threadIdx.x; i < e; i += FOLD_THREADS) {
+    const u64 p = pairs[i];
+    const u32 off = (u32)p - base;
+    if ((u32)p != 0xffffffffu && off < FOLD_WIN) {
+      atomicXor(&hist[off], (u32)(p >> 32));
+      atomicOr(&pres[off >> 5], 1u << (off & 31));
+    }
+  }
+  __syncthreads();
+  const size_t slot = (size_t)w * FOLD_CHUNKS + blockIdx.x;
+  for (u32 b = threadIdx.x; b < FOLD_WIN; b += FOLD_THREADS) px[slot * FOLD_WIN + b] = hist[b];
+  for (u32 b = threadIdx.x; b < FOLD_WIN / 32; b += FOLD_THREADS) pp[slot * (FOLD_WIN / 32) + b] = pres[b];
+}
+
+__global__ void k_cl_fold_reduce(const u32* __restrict__ px, const u32* __restrict__ pp, const Info* __restrict__ info,
+                                 u32* __restrict__ dx, u32* __restrict__ dp) {
+  const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= FOLD_MAXWIN * FOLD_WIN) return;
+  const u32 mlo = info->minute_min, mhi = info->minute_max;
+  const bool usable = mlo <= mhi && !info->fold_overflow;
+  const u32 w = b / FOLD_WIN, o = b % FOLD_WIN;
+  u32 x = 0, p = 0;
+  if (usable && w < (mhi - mlo) / FOLD_WIN + 1) {
+    for (u32 k = 0; k < FOLD_CHUNKS; ++k) {
+      const size_t slot = (size_t)w * FOLD_CHUNKS + k;
+      x ^= px[slot * FOLD_WIN + o];
+      p |= (pp[slot * (FOLD_WIN / 32) + (o >> 5)] >> (o & 31)) & 1u;
+    }
+  }
+  dx[b] = x;
+  dp[b] = p;
+}
+
+__global__ void k_cl_leaves(const u32* __restrict__ dx, const u32* __restrict__ dp, const u32* __restrict__ pos,
+                            const Info* __restrict__ info, u64* __restrict__ ck, int32_t* __restrict__ xr) {
+  const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= FOLD_MAXWIN * FOLD_WIN || !dp[b]) return;
+  ck[pos[b]] = minute_code(info->minute_min + b);  // owner 0
+  xr[pos[b]] = (int32_t)dx[b];
+}
+
+// Fallback fold input from the pass-2 pairs (rare: wide minute range).
+__global__ void k_cl_pairs_sel(const u64* __restrict__ pairs, size_t n, u32* __restrict__ sel) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    sel[i] = (u32)pairs[i] != 0xffffffffu;
+}
+__global__ void k_cl_pairs_ck(const u64* __restrict__ pairs, const u32* __restrict__ pos, size_t n, u64* __restrict__ ck,
+                              u32* __restrict__ h, Info* __restrict__ info) {
+  u64 mn = ~0ull, mx = 0;
+  u32 ml = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const u64 p = pairs[i];
+    if ((u32)p == 0xffffffffu) continue;
+    const u64 c = minute_code((u32)p);
+    ck[pos[i]] = c;
+    h[pos[i]] = (u32)(p >> 32);
+    mn = min(mn, c);
+    mx = max(mx, c);
+    ml = max(ml, (u32)base3_len((u32)p));
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    mn = min(mn, (u64)__shfl_xor(mn, d, 64));
+    mx = max(mx, (u64)__shfl_xor(mx, d, 64));
+    ml = max(ml, (u32)__shfl_xor(ml, d, 64));
+  }
+  if ((threadIdx.x & 63) == 0 && mx >= mn) {
+    atomicMin(&info->ck_min, mn);
+    atomicMax(&info->ck_max, mx);
+    atomicMax(&info->maxlen, ml);
+  }
+}
+
+__global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* __restrict__ present, u32 C,
+                              Info* __restrict__ info) {
+  const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C && present[c] && !(prior[c].meta & EVM_META_VALID)) atomicOr(&info->bad, 1u);
+}
+
+// ============================================================================
+// Host drivers
+// ============================================================================
+static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree_in, const char* ts, size_t stride,
+                      size_t n, const u32* cell, u32 C, const evm_rec* prior, const uint8_t* prior_present,
+                      uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+  int st;
+  size_t range = (n + CL_RANGE_TARGET - 1) / CL_RANGE_TARGET;
+  range = std::max<size_t>(2048, (range + 63) / 64 * 64);
+  const size_t G = (n + range - 1) / range;
+  const int cbits = C > 1 ? 32 - __builtin_clz(C - 1) : 0;
+  u64* a_tc = S.alloc<u64>(G * C);
+  u64* a_node = S.alloc<u64>(G * C);
+  u32* a_mask = S.alloc<u32>(G * C);
+  u32* a_first = S.alloc<u32>(G * C);
+  u32* hash = S.alloc<u32>(n);
+  u64* pairs = S.alloc<u64>(n);
+  if (!a_tc || !a_node || !a_mask || !a_first || !hash || !pairs) return EVM_ENOMEM;
+  const size_t lds = 3072 + (size_t)C * 24;
+  {
+    evm::ProfScope ps_(ctx, "k_cl_pass<1>");
+    hipLaunchKernelGGL((k_cl_pass<1>), dim3(G), dim3(64), lds, ctx->stream, (const uint8_t*)ts, stride, cell, n, C,
+                       cbits, range, a_tc, a_node, a_mask, a_first, hash, (uint8_t*)nullptr, (u64*)nullptr, info);
+  }
+  // cross-cell PK check on a persistent hash set (epoch-tagged: no clearing)
+  const int lg = std::max(ceil_log2(n + n / 2 + 1), 10);
+  if (!ctx->xtab || ctx->xtab_lg < lg) {
+    if (ctx->xtab) HIPR(hipFree(ctx->xtab));
+    ctx->xtab = nullptr;
+    HIPR(hipMalloc(&ctx->xtab, sizeof(u64) << lg));
+    HIPR(hipMemsetAsync(ctx->xtab, 0, sizeof(u64) << lg, ctx->stream));
+    ctx->xtab_lg = lg;
+    ctx->xepoch = 0;
+  }
+  if (++ctx->xepoch == 256) {
+    HIPR(hipMemsetAsync(ctx->xtab, 0, sizeof(u64) << ctx->xtab_lg, ctx->stream));
+    ctx->xepoch = 1;
+  }
+  KLAUNCH(k_cl_xcell, dim3(grid_for(n, 256, 16384)), dim3(256), (const uint8_t*)ts, stride, cell, hash, n, ctx->xtab,
+          (u32)ctx->xtab_lg, ctx->xepoch, info);
+  KLAUNCH(k_cl_carry, dim3((C + 255) / 256), dim3(256), C, G, a_tc, a_node, a_mask, a_first, prior, prior_present,
+          winner);
+  {
+    evm::ProfScope ps_(ctx, "k_cl_pass<2>");
+    hipLaunchKernelGGL((k_cl_pass<2>), dim3(G), dim3(64), lds, ctx->stream, (const uint8_t*)ts, stride, cell, n, C,
+                       cbits, range, a_tc, a_node, a_mask, a_first, (u32*)nullptr, flags, pairs, info);
+  }
+  // Merkle fold
+  u32* px = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN);
+  u32* pp = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32));
+  const size_t B = (size_t)FOLD_MAXWIN * FOLD_WIN;
+  u32* dx = S.alloc<u32>(B);
+  u32* dp = S.alloc<u32>(B);
+  u32* pos = S.alloc<u32>(B);
+  u64* lck = S.alloc<u64>(B);
+  int32_t* lxr = S.alloc<int32_t>(B);
+  if (!px || !pp || !dx || !dp || !pos || !lck || !lxr) return EVM_ENOMEM;
+  KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), pairs, n, px, pp, info);
+  KLAUNCH(k_cl_fold_reduce, dim3((B + 255) / 256), dim3(256), px, pp, info, dx, dp);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, dp, B, pos, &info->n_leaves))) return st;
+  KLAUNCH(k_cl_leaves, dim3((B + 255) / 256), dim3(256), dx, dp, pos, info, lck, lxr);
+  Info hi;
+  if ((st = read_info(ctx, info, &hi))) return st;
+  if (hi.bad) return EVM_ENONCANON;
+  if (hi.bad_aux) return EVM_EINVAL;
+  if (hi.collision) return EVM_ECOLLISION;
+  if (!hi.fold_overflow) return merge_into_tree(ctx, S, tree_in, tree_in->n_owners, lck, lxr, hi.n_leaves, tree_out);
+  // wide minute range or mixed key lengths: sort-based fold
+  u32* sel = S.alloc<u32>(n);
+  u32* spos = S.alloc<u32>(n);
+  u32* cnt = S.alloc<u32>(1);
+  u64* ck = S.alloc<u64>(n);
+  u32* h = S.alloc<u32>(n);
+  if (!sel || !spos || !cnt || !ck || !h) return EVM_ENOMEM;
+  KLAUNCH(k_cl_pairs_sel, dim3(grid_for(n, 256)), dim3(256), pairs, n, sel);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, spos, cnt))) return st;
+  KLAUNCH(k_cl_pairs_ck, dim3(grid_for(n, 256, 4096)), dim3(256), pairs, spos, n, ck, h, info);
+  u32 m = 0;
+  HIPR(hipMemcpyAsync(&m, cnt, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  if ((st = read_info(ctx, info, &hi))) return st;
+  return fold_into_tree(ctx, S, tree_in, tree_in->n_owners, ck, h, m, hi, tree_out);
+}
+
+static int apply_general(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree_in, const char* ts, size_t stride,
+                         size_t n, const u32* cell, u32 n_cells, const u32* cell_owner, const evm_rec* prior,
+                         const uint8_t* prior_present, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+  int st;
+  evm_rec* rec = S.alloc<evm_rec>(n);
+  if (!rec) return EVM_ENOMEM;
+  if ((st = launch_pack(ctx, ts, stride, n, cell, n_cells, rec, info))) return st;
+  // (1) cross-cell PK collisions
+  const int lg = ceil_log2(2 * n);
+  u64* table = S.alloc<u64>((size_t)1 << lg);
+  if (!table) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(table, 0, sizeof(u64) << lg, ctx->stream));
+  KLAUNCH(k_xcell, dim3(grid_for(n, 256, 8192)), dim3(256), rec, n, table, (u32)lg, info);
+  // (2) stable sort (cell, index)
+  u32* cell_s = S.alloc<u32>(n);
+  u32* idx_s = S.alloc<u32>(n);
+  if (!cell_s || !idx_s) return EVM_ENOMEM;
+  HIPR(hipMemcpyAsync(cell_s, cell, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
+  if ((st = launch_iota(ctx, idx_s, n))) return st;
+  const int cbits = n_cells > 1 ? 32 - __builtin_clz(n_cells - 1) : 0;
+  if ((st = radix_sort_pairs<u32>(ctx, S, cell_s, idx_s, n, 0, cbits))) return st;
+  // (3) segmented running max + decisions
+  const size_t nt = (n + LWW_TILE - 1) / LWW_TILE;
+  u32* t_head = S.alloc<u32>(nt);
+  Key* t_key = S.alloc<Key>(nt);
+  if (!t_head || !t_key) return EVM_ENOMEM;
+  KLAUNCH(k_lww_reduce, dim3(nt), dim3(LWW_THREADS), rec, cell_s, idx_s, n, t_head, t_key);
+  KLAUNCH(k_lww_tiles, dim3(1), dim3(LWW_THREADS), t_head, t_key, nt);
+  KLAUNCH(k_lww_apply, dim3(nt), dim3(LWW_THREADS), rec, cell_s, idx_s, n, t_head, t_key, prior, prior_present, flags,
+          winner);
+  // (4) Merkle fold of the XOR messages
+  u32* sel = S.alloc<u32>(n);
+  u32* pos = S.alloc<u32>(n);
+  u32* cnt = S.alloc<u32>(1);
+  u64* ck = S.alloc<u64>(n);
+  u32* h = S.alloc<u32>(n);
+  if (!sel || !pos || !cnt || !ck || !h) return EVM_ENOMEM;
+  if ((st = launch_sel(ctx, flags, (uint8_t)EVM_MSG_XOR, n, sel))) return st;
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, pos, cnt))) return st;
+  if ((st = launch_fold_prep(ctx, rec, flags, (uint8_t)EVM_MSG_XOR, pos, (int)(cell_owner ? OWNER_CELL : OWNER_ZERO),
+                              cell_owner, n, ck, h, info)))
+    return st;
+  Info hi;
+  if ((st = read_info(ctx, info, &hi))) return st;
+  if (hi.bad) {
+    KLAUNCH(k_mark_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
+    return EVM_ENONCANON;
+  }
+  if (hi.bad_aux) return EVM_EINVAL;
+  if (hi.collision) return EVM_ECOLLISION;
+  u32 m = 0;
+  HIPR(hipMemcpyAsync(&m, cnt, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  return fold_into_tree(ctx, S, tree_in, tree_in->n_owners, ck, h, m, hi, tree_out);
+}
+
+extern "C" {
+
+int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n, const uint32_t* cell,
+                    uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts, size_t prior_stride,
+                    const uint8_t* prior_present, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+  if (!ctx || !tree_in || !tree_out || stride < 46 || (n && (!ts || !cell || !flags))) return EVM_EINVAL;
+  if (n_cells && !winner) return EVM_EINVAL;
+  if (prior_present && (!prior_ts || prior_stride < 46)) return EVM_EINVAL;
+  if (n >= 0x7fffffffu) return EVM_EINVAL;
+  *tree_out = nullptr;
+  int st;
+  {
+    Scratch S(ctx);
+    Info* info = nullptr;
+    if ((st = new_info(ctx, S, &info))) return st;
+    evm_rec* prior = S.alloc<evm_rec>(std::max<size_t>(n_cells, 1));
+    if (!prior) return EVM_ENOMEM;
+    if (prior_present && n_cells) {
+      // the cells' current maxima (SELECT ... ORDER BY timestamp DESC LIMIT 1)
+      if ((st = launch_pack(ctx, prior_ts, prior_stride, n_cells, nullptr, 0, prior, nullptr))) return st;
+      KLAUNCH(k_prior_check, dim3((n_cells + 255) / 256), dim3(256), prior, prior_present, n_cells, info);
+    }
+    if (n_cells) KLAUNCH(k_fill_i32, dim3(grid_for(n_cells, 256)), dim3(256), winner, (size_t)n_cells, -1);
+    if (n == 0) {
+      Info hi;
+      if ((st = read_info(ctx, info, &hi))) return st;
+      if (hi.bad) return EVM_ENONCANON;
+      st = merge_into_tree(ctx, S, tree_in, tree_in->n_owners, nullptr, nullptr, 0, tree_out);
+    } else if (ctx->client_path == 1 ||
+               (ctx->client_path == 0 && !cell_owner && n_cells <= CL_MAX_CELLS)) {
+      if (cell_owner || n_cells > CL_MAX_CELLS) return EVM_EINVAL;
+      st = apply_fast(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, prior, prior_present, flags, winner,
+                      tree_out);
+    } else {
+      st = apply_general(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, cell_owner, prior, prior_present, flags,
+                         winner, tree_out);
+    }
+  }
+  if (st) return st;
+  return evm_sync(ctx);
+}
+
+}  // extern "C"

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack(const uint8_t* __restrict
     mn = min(mn, (u32)__shfl_xor(mn, d, 64));
     mx = max(mx, (u32)__shfl_xor(mx, d, 64));
   }
-  if ((threadIdx.x & 63) == 0) {
+  if ((threadIdx.x & 63) == 0 && info) {
     if (bad) atomicOr(&info->bad, 1u);
     if (bad_aux) atomicOr(&info->bad_aux, 1u);
     if (mn != 0xffffffffu) {
@@ -66,13 +66,6 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack(const uint8_t* __restrict
       atomicMax(&info->minute_max, mx);
     }
   }
-}
-
-static int grid_for(size_t n, int threads, int cap = 8192) {
-  size_t g = (n + threads - 1) / threads;
-  if (g < 1) g = 1;
-  if (g > (size_t)cap) g = cap;
-  return (int)g;
 }
 
 int evm::launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,
@@ -175,6 +168,22 @@ __global__ void k_sel_u32(const uint8_t* __restrict__ flags, uint8_t mask, size_
     sel[i] = (flags[i] & mask) ? 1u : 0u;
 }
 
+int evm::launch_iota(evm_ctx* ctx, u32* v, size_t n) {
+  KLAUNCH(k_iota, dim3(grid_for(n, 256)), dim3(256), v, n);
+  return hip_ok(hipGetLastError());
+}
+int evm::launch_sel(evm_ctx* ctx, const uint8_t* flags, uint8_t mask, size_t n, u32* sel) {
+  KLAUNCH(k_sel_u32, dim3(grid_for(n, 256)), dim3(256), flags, mask, n, sel);
+  return hip_ok(hipGetLastError());
+}
+int evm::launch_fold_prep(evm_ctx* ctx, const evm_rec* rec, const uint8_t* flags, uint8_t sel_mask, const u32* pos,
+                          int owner_mode, const u32* cell_owner, size_t n, u64* ck, u32* h, Info* info) {
+  if (n == 0) return EVM_OK;
+  KLAUNCH(k_fold_prep, dim3(grid_for(n, 256, 4096)), dim3(256), rec, flags, sel_mask, pos, owner_mode, cell_owner, n, ck,
+          h, info);
+  return hip_ok(hipGetLastError());
+}
+
 __global__ void k_heads(const u64* __restrict__ ck, size_t m, u32* __restrict__ head) {
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < m; p += (size_t)gridDim.x * blockDim.x)
     head[p] = (p == 0 || ck[p] != ck[p - 1]) ? 1u : 0u;
@@ -267,26 +276,26 @@ __global__ void k_owner_off(const u64* __restrict__ ck, size_t L, u32 n_owners, 
     off[o] = (o == n_owners) ? (u64)L : (u64)lower_bound_u64(ck, 0, L, (u64)o << 40);
 }
 
-static int tree_alloc(evm_tree* t, u32 n_owners, uint64_t L) {
+static int tree_alloc(evm_ctx* ctx, evm_tree* t, u32 n_owners, uint64_t L) {
   t->n_owners = n_owners;
   t->n_leaves = L;
   t->off = nullptr;
   t->ck = nullptr;
   t->xr = nullptr;
   t->pfx = nullptr;
-  if (hipMalloc(&t->off, sizeof(u64) * (n_owners + 1)) != hipSuccess) return EVM_ENOMEM;
-  if (hipMalloc(&t->ck, sizeof(u64) * std::max<uint64_t>(L, 1)) != hipSuccess) return EVM_ENOMEM;
-  if (hipMalloc(&t->xr, sizeof(int32_t) * std::max<uint64_t>(L, 1)) != hipSuccess) return EVM_ENOMEM;
-  if (hipMalloc(&t->pfx, sizeof(int32_t) * (L + 1)) != hipSuccess) return EVM_ENOMEM;
+  if (hipMallocAsync((void**)&t->off, sizeof(u64) * (n_owners + 1), ctx->stream) != hipSuccess) return EVM_ENOMEM;
+  if (hipMallocAsync((void**)&t->ck, sizeof(u64) * std::max<uint64_t>(L, 1), ctx->stream) != hipSuccess) return EVM_ENOMEM;
+  if (hipMallocAsync((void**)&t->xr, sizeof(int32_t) * std::max<uint64_t>(L, 1), ctx->stream) != hipSuccess) return EVM_ENOMEM;
+  if (hipMallocAsync((void**)&t->pfx, sizeof(int32_t) * (L + 1), ctx->stream) != hipSuccess) return EVM_ENOMEM;
   return EVM_OK;
 }
 
-static void tree_release(evm_tree* t) {
+static void tree_release(evm_ctx* ctx, evm_tree* t) {
   if (!t) return;
-  (void)hipFree(t->off);
-  (void)hipFree(t->ck);
-  (void)hipFree(t->xr);
-  (void)hipFree(t->pfx);
+  if (t->off) (void)hipFreeAsync(t->off, ctx->stream);
+  if (t->ck) (void)hipFreeAsync(t->ck, ctx->stream);
+  if (t->xr) (void)hipFreeAsync(t->xr, ctx->stream);
+  if (t->pfx) (void)hipFreeAsync(t->pfx, ctx->stream);
   delete t;
 }
 
@@ -294,9 +303,9 @@ static void tree_release(evm_tree* t) {
 int evm::tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, const int32_t* xr, uint64_t L,
                        evm_tree** out) {
   evm_tree* t = new evm_tree;
-  int st = tree_alloc(t, n_owners, L);
+  int st = tree_alloc(ctx, t, n_owners, L);
   if (st) {
-    tree_release(t);
+    tree_release(ctx, t);
     return st;
   }
   if (L) {
@@ -307,7 +316,7 @@ int evm::tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, co
                      n_owners, t->off);
   st = scan_exclusive<int32_t, OpXor>(ctx, S, t->xr, L, t->pfx, t->pfx + L);
   if (st) {
-    tree_release(t);
+    tree_release(ctx, t);
     return st;
   }
   *out = t;
@@ -333,6 +342,13 @@ int evm::fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owne
   uint64_t L1 = 0;
   st = reduce_runs(ctx, S, ck, (const int32_t*)h, m, nck, nxr, &L1);
   if (st) return st;
+  return merge_into_tree(ctx, S, in, n_owners, nck, nxr, L1, out);
+}
+
+// Merges sorted unique leaves (nck, nxr) into `in`; equal keys XOR-combine.
+int evm::merge_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, const u64* nck,
+                         const int32_t* nxr, uint64_t L1, evm_tree** out) {
+  int st = EVM_OK;
   const uint64_t L0 = in ? in->n_leaves : 0;
   if (L0 == 0) return tree_finalize(ctx, S, n_owners, nck, nxr, L1, out);
   if (L1 == 0) return tree_finalize(ctx, S, n_owners, in->ck, in->xr, L0, out);
@@ -425,210 +441,6 @@ __global__ void k_roots(const u64* __restrict__ off, const int32_t* __restrict__
   }
 }
 
-// ============================================================================
-// applyMessages (applyMessages.ts:26-131)
-// ============================================================================
-
-// (1) Global __message PK: the same timestamp in two different cells of one
-// batch makes the reference's INSERT fail silently for the later one and
-// stops that cell's running max from advancing.  That interleaving is
-// inherently sequential, so it is detected exactly and reported.
-__global__ void k_xcell(const evm_rec* __restrict__ rec, size_t n, u64* __restrict__ table, u32 log2size,
-                        Info* __restrict__ info) {
-  const u64 mask = (1ull << log2size) - 1;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const evm_rec r = rec[i];
-    if (!(r.meta & EVM_META_VALID)) continue;
-    const u64 mine = ((u64)r.hash << 32) | (u64)(i + 1);
-    u64 pos = ((u64)(r.hash * 2654435761u) ^ (r.node * 0x9E3779B97F4A7C15ull >> 20)) & mask;
-    for (u64 probe = 0; probe <= mask; ++probe) {
-      u64 s = __hip_atomic_load(&table[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (s == 0) {
-        const u64 prev = atomicCAS(&table[pos], 0ull, mine);
-        if (prev == 0) break;  // inserted
-        s = prev;
-      }
-      if ((u32)(s >> 32) == r.hash) {
-        const evm_rec o = rec[(size_t)(s & 0xffffffffu) - 1];
-        if (o.tc == r.tc && o.node == r.node && (o.meta & EVM_META_CASEMASK) == (r.meta & EVM_META_CASEMASK)) {
-          if (o.aux != r.aux) atomicOr(&info->collision, 1u);
-          break;
-        }
-      }
-      pos = (pos + 1) & mask;
-    }
-  }
-}
-
-// (2) Segmented (per cell) running max in batch order over the cell-sorted
-// order.  Aggregate = (segment head seen, max since the last head).
-struct SegAgg {
-  u32 head;
-  Key key;
-};
-__device__ __forceinline__ SegAgg seg_combine(const SegAgg& a, const SegAgg& b) {
-  SegAgg r;
-  r.head = a.head | b.head;
-  r.key = b.head ? b.key : key_max(a.key, b.key);
-  return r;
-}
-
-constexpr int LWW_THREADS = 256;
-constexpr int LWW_ITEMS = 8;
-constexpr int LWW_TILE = LWW_THREADS * LWW_ITEMS;
-
-__device__ __forceinline__ SegAgg lww_elem(const evm_rec* rec, const u32* cell_s, const u32* idx_s, size_t p) {
-  SegAgg e;
-  e.head = (p == 0 || cell_s[p] != cell_s[p - 1]) ? 1u : 0u;
-  e.key = key_of(rec[idx_s[p]]);
-  return e;
-}
-
-struct SegLds {
-  u32 head[LWW_THREADS];
-  u64 tc[LWW_THREADS];
-  u64 node[LWW_THREADS];
-  u32 mask[LWW_THREADS];
-};
-__device__ __forceinline__ void seg_put(SegLds& L, int t, const SegAgg& a) {
-  L.head[t] = a.head;
-  L.tc[t] = a.key.tc;
-  L.node[t] = a.key.node;
-  L.mask[t] = a.key.mask;
-}
-__device__ __forceinline__ SegAgg seg_get(const SegLds& L, int t) {
-  SegAgg a;
-  a.head = L.head[t];
-  a.key = Key{L.tc[t], L.node[t], L.mask[t]};
-  return a;
-}
-
-// Block inclusive scan (Hillis-Steele over LDS) of one SegAgg per thread.
-__device__ SegAgg seg_block_inclusive(SegLds& L, SegAgg v) {
-  const int t = threadIdx.x;
-  seg_put(L, t, v);
-  __syncthreads();
-  for (int d = 1; d < LWW_THREADS; d <<= 1) {
-    SegAgg o;
-    const bool has = t >= d;
-    if (has) o = seg_get(L, t - d);
-    __syncthreads();
-    if (has) v = seg_combine(o, v);
-    seg_put(L, t, v);
-    __syncthreads();
-  }
-  return v;
-}
-
-__global__ __launch_bounds__(LWW_THREADS) void k_lww_reduce(const evm_rec* __restrict__ rec, const u32* __restrict__ cell_s,
-                                                            const u32* __restrict__ idx_s, size_t n,
-                                                            u32* __restrict__ t_head, Key* __restrict__ t_key) {
-  __shared__ SegLds L;
-  const size_t base = (size_t)blockIdx.x * LWW_TILE + (size_t)threadIdx.x * LWW_ITEMS;
-  SegAgg acc{0u, key_none()};
-  for (int k = 0; k < LWW_ITEMS; ++k) {
-    const size_t p = base + k;
-    if (p < n) acc = seg_combine(acc, lww_elem(rec, cell_s, idx_s, p));
-  }
-  const SegAgg inc = seg_block_inclusive(L, acc);
-  if (threadIdx.x == LWW_THREADS - 1) {
-    t_head[blockIdx.x] = inc.head;
-    t_key[blockIdx.x] = inc.key;
-  }
-}
-
-// Exclusive scan of the tile aggregates, in one block.
-__global__ __launch_bounds__(LWW_THREADS) void k_lww_tiles(u32* __restrict__ t_head, Key* __restrict__ t_key, size_t nt) {
-  __shared__ SegLds L;
-  const size_t per = (nt + LWW_THREADS - 1) / LWW_THREADS;
-  const size_t b = (size_t)threadIdx.x * per;
-  SegAgg acc{0u, key_none()};
-  for (size_t i = b; i < b + per && i < nt; ++i) acc = seg_combine(acc, SegAgg{t_head[i], t_key[i]});
-  const SegAgg inc = seg_block_inclusive(L, acc);
-  // exclusive for this thread = inclusive of thread-1
-  __syncthreads();
-  seg_put(L, threadIdx.x, inc);
-  __syncthreads();
-  SegAgg run = threadIdx.x ? seg_get(L, threadIdx.x - 1) : SegAgg{0u, key_none()};
-  for (size_t i = b; i < b + per && i < nt; ++i) {
-    const SegAgg here{t_head[i], t_key[i]};
-    t_head[i] = run.head;
-    t_key[i] = run.key;
-    run = seg_combine(run, here);
-  }
-}
-
-__global__ __launch_bounds__(LWW_THREADS) void k_lww_apply(const evm_rec* __restrict__ rec, const u32* __restrict__ cell_s,
-                                                           const u32* __restrict__ idx_s, size_t n,
-                                                           const u32* __restrict__ t_head, const Key* __restrict__ t_key,
-                                                           const evm_rec* __restrict__ prior,
-                                                           const uint8_t* __restrict__ prior_present,
-                                                           uint8_t* __restrict__ flags, int32_t* __restrict__ winner) {
-  __shared__ SegLds L;
-  const size_t base = (size_t)blockIdx.x * LWW_TILE + (size_t)threadIdx.x * LWW_ITEMS;
-  SegAgg e[LWW_ITEMS];
-  SegAgg acc{0u, key_none()};
-#pragma unroll
-  for (int k = 0; k < LWW_ITEMS; ++k) {
-    const size_t p = base + k;
-    e[k] = p < n ? lww_elem(rec, cell_s, idx_s, p) : SegAgg{0u, key_none()};
-    acc = seg_combine(acc, e[k]);
-  }
-  const SegAgg inc = seg_block_inclusive(L, acc);
-  __syncthreads();
-  seg_put(L, threadIdx.x, inc);
-  __syncthreads();
-  SegAgg run = SegAgg{t_head[blockIdx.x], t_key[blockIdx.x]};
-  if (threadIdx.x) run = seg_combine(run, seg_get(L, threadIdx.x - 1));
-#pragma unroll
-  for (int k = 0; k < LWW_ITEMS; ++k) {
-    const size_t p = base + k;
-    if (p >= n) break;
-    const Key excl = e[k].head ? key_none() : run.key;
-    run = seg_combine(run, e[k]);
-    const u32 c = cell_s[p];
-    const u32 i = idx_s[p];
-    Key t = excl;
-    if (prior_present && prior_present[c]) t = key_max(t, key_of(prior[c]));
-    const Key ts = e[k].key;
-    // applyMessages.ts:93  t == null || t < message.timestamp
-    const bool ups = key_cmp(t, ts) < 0;
-    // applyMessages.ts:105 t == null || t !== message.timestamp
-    const bool xr = !((t.mask & KEY_PRESENT) && key_eq(t, ts));
-    flags[i] = (ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u);
-    if (ups) atomicMax(&winner[c], (int32_t)i);
-  }
-}
-
-__global__ void k_mark_bad(const evm_rec* __restrict__ rec, size_t n, uint8_t* __restrict__ flags) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    flags[i] = (rec[i].meta & EVM_META_VALID) ? 0u : EVM_MSG_BAD;
-}
-
-__global__ void k_fill_i32(int32_t* __restrict__ p, size_t n, int32_t v) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
-}
-
-static int ceil_log2(size_t x) {
-  int k = 0;
-  while (((size_t)1 << k) < x) ++k;
-  return k;
-}
-
-static int read_info(evm_ctx* ctx, const Info* dev, Info* host) {
-  HIPR(hipMemcpyAsync(host, dev, sizeof(Info), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
-  return EVM_OK;
-}
-
-static int new_info(evm_ctx* ctx, Scratch& S, Info** out) {
-  Info* d = S.alloc<Info>(1);
-  if (!d) return EVM_ENOMEM;
-  Info h = info_init();
-  HIPR(hipMemcpyAsync(d, &h, sizeof(Info), hipMemcpyHostToDevice, ctx->stream));
-  *out = d;
-  return EVM_OK;
-}
 
 // ============================================================================
 // C ABI
@@ -664,6 +476,12 @@ int evm_create(int device, evm_ctx** out) {
     return EVM_EDEVICE;
   }
   c->stream = c->own;
+  // keep freed scratch in the stream-ordered pool between calls
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+    uint64_t thr = ~0ull;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  }
   *out = c;
   return EVM_OK;
 }
@@ -671,6 +489,8 @@ int evm_create(int device, evm_ctx** out) {
 void evm_destroy(evm_ctx* ctx) {
   if (!ctx) return;
   prof_drain(ctx);
+  if (ctx->xtab) (void)hipFree(ctx->xtab);
+  if (ctx->ws) (void)hipFree(ctx->ws);
   (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -685,6 +505,15 @@ void* evm_get_stream(evm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; 
 int evm_sync(evm_ctx* ctx) {
   if (!ctx) return EVM_EINVAL;
   return hip_ok(hipStreamSynchronize(ctx->stream));
+}
+
+int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
+  if (!ctx) return EVM_EINVAL;
+  if (option == EVM_OPT_CLIENT_PATH && value >= 0 && value <= 2) {
+    ctx->client_path = (int)value;
+    return EVM_OK;
+  }
+  return EVM_EINVAL;
 }
 
 int evm_prof_enable(evm_ctx* ctx, int on) {
@@ -810,10 +639,7 @@ int evm_tree_from_leaves(evm_ctx* ctx, uint32_t n_owners, const uint64_t* off_h,
 
 int evm_tree_free(evm_ctx* ctx, evm_tree* t) {
   if (!ctx) return EVM_EINVAL;
-  if (t) {
-    (void)hipStreamSynchronize(ctx->stream);
-    tree_release(t);
-  }
+  if (t) tree_release(ctx, t);  // stream-ordered: safe behind queued readers
   return EVM_OK;
 }
 
@@ -893,96 +719,6 @@ int evm_merkle_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t*
   KLAUNCH(k_diff, dim3(grid_for(a->n_owners, 64, 1 << 16)), dim3(64), A, B, a->n_owners,
                      millis);
   HIPR(hipGetLastError());
-  return evm_sync(ctx);
-}
-
-int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n, const uint32_t* cell,
-                    uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts, size_t prior_stride,
-                    const uint8_t* prior_present, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
-  if (!ctx || !tree_in || !tree_out || stride < 46 || (n && (!ts || !cell || !flags))) return EVM_EINVAL;
-  if (n_cells && !winner) return EVM_EINVAL;
-  if (prior_present && (!prior_ts || prior_stride < 46)) return EVM_EINVAL;
-  if (n >= 0x7fffffffu) return EVM_EINVAL;
-  Scratch S(ctx);
-  Info* info = nullptr;
-  int st = new_info(ctx, S, &info);
-  if (st) return st;
-  evm_rec* rec = S.alloc<evm_rec>(std::max<size_t>(n, 1));
-  evm_rec* prior = S.alloc<evm_rec>(std::max<size_t>(n_cells, 1));
-  if (!rec || !prior) return EVM_ENOMEM;
-  // K1 on the batch and on the prior per-cell maxima
-  st = launch_pack(ctx, ts, stride, n, cell, n_cells, rec, info);
-  if (st) return st;
-  if (prior_present && n_cells) {
-    Info* pinfo = nullptr;
-    if ((st = new_info(ctx, S, &pinfo))) return st;
-    if ((st = launch_pack(ctx, prior_ts, prior_stride, n_cells, nullptr, 0, prior, pinfo))) return st;
-    Info hp;
-    if ((st = read_info(ctx, pinfo, &hp))) return st;
-    // a prior row outside the native domain only matters where it is present
-    if (hp.bad) {
-      std::vector<evm_rec> pr(n_cells);
-      std::vector<uint8_t> pp(n_cells);
-      HIPR(hipMemcpyAsync(pr.data(), prior, sizeof(evm_rec) * n_cells, hipMemcpyDeviceToHost, ctx->stream));
-      HIPR(hipMemcpyAsync(pp.data(), prior_present, n_cells, hipMemcpyDeviceToHost, ctx->stream));
-      HIPR(hipStreamSynchronize(ctx->stream));
-      for (u32 c = 0; c < n_cells; ++c)
-        if (pp[c] && !(pr[c].meta & EVM_META_VALID)) return EVM_ENONCANON;
-    }
-  }
-  if (n_cells)
-    KLAUNCH(k_fill_i32, dim3(grid_for(n_cells, 256)), dim3(256), winner, (size_t)n_cells, -1);
-  if (n == 0) {
-    st = tree_finalize(ctx, S, tree_in->n_owners, tree_in->ck, tree_in->xr, tree_in->n_leaves, tree_out);
-    return st ? st : evm_sync(ctx);
-  }
-  // (1) cross-cell PK collisions
-  const int lg = ceil_log2(2 * n);
-  u64* table = S.alloc<u64>((size_t)1 << lg);
-  if (!table) return EVM_ENOMEM;
-  HIPR(hipMemsetAsync(table, 0, sizeof(u64) << lg, ctx->stream));
-  KLAUNCH(k_xcell, dim3(grid_for(n, 256, 8192)), dim3(256), rec, n, table, (u32)lg, info);
-  // (2) stable sort (cell, index)
-  u32* cell_s = S.alloc<u32>(n);
-  u32* idx_s = S.alloc<u32>(n);
-  if (!cell_s || !idx_s) return EVM_ENOMEM;
-  HIPR(hipMemcpyAsync(cell_s, cell, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
-  KLAUNCH(k_iota, dim3(grid_for(n, 256)), dim3(256), idx_s, n);
-  const int cbits = n_cells > 1 ? 32 - __builtin_clz(n_cells - 1) : 0;
-  if ((st = radix_sort_pairs<u32>(ctx, S, cell_s, idx_s, n, 0, cbits))) return st;
-  // (3) segmented running max + decisions
-  const size_t nt = (n + LWW_TILE - 1) / LWW_TILE;
-  u32* t_head = S.alloc<u32>(nt);
-  Key* t_key = S.alloc<Key>(nt);
-  if (!t_head || !t_key) return EVM_ENOMEM;
-  KLAUNCH(k_lww_reduce, dim3(nt), dim3(LWW_THREADS), rec, cell_s, idx_s, n, t_head, t_key);
-  KLAUNCH(k_lww_tiles, dim3(1), dim3(LWW_THREADS), t_head, t_key, nt);
-  KLAUNCH(k_lww_apply, dim3(nt), dim3(LWW_THREADS), rec, cell_s, idx_s, n, t_head, t_key,
-                     prior, prior_present, flags, winner);
-  // (4) Merkle fold of the XOR messages
-  u32* sel = S.alloc<u32>(n);
-  u32* pos = S.alloc<u32>(n);
-  u32* cnt = S.alloc<u32>(1);
-  u64* ck = S.alloc<u64>(n);
-  u32* h = S.alloc<u32>(n);
-  if (!sel || !pos || !cnt || !ck || !h) return EVM_ENOMEM;
-  KLAUNCH(k_sel_u32, dim3(grid_for(n, 256)), dim3(256), flags, (uint8_t)EVM_MSG_XOR, n, sel);
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, pos, cnt))) return st;
-  KLAUNCH(k_fold_prep, dim3(grid_for(n, 256, 4096)), dim3(256), rec, flags,
-                     (uint8_t)EVM_MSG_XOR, pos, (int)(cell_owner ? OWNER_CELL : OWNER_ZERO), cell_owner, n, ck, h, info);
-  Info hi;
-  if ((st = read_info(ctx, info, &hi))) return st;
-  if (hi.bad) {
-    KLAUNCH(k_mark_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
-    (void)evm_sync(ctx);
-    return EVM_ENONCANON;
-  }
-  if (hi.bad_aux) return EVM_EINVAL;
-  if (hi.collision) return EVM_ECOLLISION;
-  u32 m = 0;
-  HIPR(hipMemcpyAsync(&m, cnt, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
-  if ((st = fold_into_tree(ctx, S, tree_in, tree_in->n_owners, ck, h, m, hi, tree_out))) return st;
   return evm_sync(ctx);
 }
 

@@ -16,8 +16,16 @@ struct evm_ctx {
   hipStream_t stream;
   // kernel timing (evm_prof_*): HIP event pairs per kernel name, on `stream`
   bool prof = false;
+  int client_path = 0;  // EVM_OPT_CLIENT_PATH
   std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> prof_events;
   std::map<std::string, std::pair<double, uint64_t>> prof_total;  // ms, launches (drained)
+  // persistent hash set for the cross-cell timestamp check (epoch-tagged slots)
+  unsigned long long* xtab = nullptr;
+  int xtab_lg = 0;
+  unsigned xepoch = 0;
+  // persistent workspace for the client fast path
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
 };
 
 // One MerkleTree per owner, as sorted unique leaves keyed by
@@ -46,6 +54,8 @@ struct Info {
   u64 ck_max;
   u32 maxlen;  // longest base-3 key
   u32 bad_aux; // an aux id out of range
+  u32 fold_overflow;  // dense minute fold not applicable (range too wide / mixed key lengths)
+  u32 n_leaves;       // leaves produced by the dense fold
 };
 
 inline Info info_init() {
@@ -58,6 +68,8 @@ inline Info info_init() {
   h.ck_max = 0;
   h.maxlen = 0;
   h.bad_aux = 0;
+  h.fold_overflow = 0;
+  h.n_leaves = 0;
   return h;
 }
 
@@ -122,6 +134,41 @@ class ProfScope {
 
 enum OwnerMode { OWNER_ZERO = 0, OWNER_AUX = 1, OWNER_CELL = 2 };
 
+inline int grid_for(size_t n, int threads, int cap = 8192) {
+  size_t g = (n + threads - 1) / threads;
+  if (g < 1) g = 1;
+  if (g > (size_t)cap) g = cap;
+  return (int)g;
+}
+
+inline int ceil_log2(size_t x) {
+  int k = 0;
+  while (((size_t)1 << k) < x) ++k;
+  return k;
+}
+
+inline int read_info(evm_ctx* ctx, const Info* dev, Info* host) {
+  HIPR(hipMemcpyAsync(host, dev, sizeof(Info), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  return EVM_OK;
+}
+
+inline int new_info(evm_ctx* ctx, Scratch& S, Info** out) {
+  Info* d = S.alloc<Info>(1);
+  if (!d) return EVM_ENOMEM;
+  Info h = info_init();
+  HIPR(hipMemcpyAsync(d, &h, sizeof(Info), hipMemcpyHostToDevice, ctx->stream));
+  *out = d;
+  return EVM_OK;
+}
+
+// shared launchers (evm_engine.hip)
+int launch_iota(evm_ctx* ctx, u32* v, size_t n);
+int launch_sel(evm_ctx* ctx, const uint8_t* flags, uint8_t mask, size_t n, u32* sel);
+int launch_fold_prep(evm_ctx* ctx, const evm_rec* rec, const uint8_t* flags, uint8_t sel_mask, const u32* pos,
+                     int owner_mode, const u32* cell_owner, size_t n, u64* ck, u32* h, Info* info);
+int tree_from_device(evm_ctx* ctx, const evm_tree* src, evm_tree** out);  // copy of a tree set
+
 int launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,
                 Info* info);
 template <typename T, template <typename> class Op>
@@ -131,6 +178,8 @@ int radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t n, i
 int reduce_runs(evm_ctx* ctx, Scratch& S, const u64* ck, const int32_t* h, size_t m, u64* out_ck, int32_t* out_xr,
                 uint64_t* out_count);
 int tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, const int32_t* xr, uint64_t L, evm_tree** out);
+int merge_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, const u64* nck, const int32_t* nxr,
+                    uint64_t L1, evm_tree** out);
 int fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u64* ck, u32* h, size_t m,
                    const Info& host_info, evm_tree** out);
 

@@ -75,6 +75,9 @@ class Engine:
         except Exception:
             pass
 
+    def set_option(self, option: int, value: int):
+        check(self.lib.evm_set_option(self.h, option, value), "evm_set_option")
+
     # ------------------------------------------------------------- profiling
     def prof_enable(self, on: bool = True):
         check(self.lib.evm_prof_enable(self.h, 1 if on else 0), "evm_prof_enable")

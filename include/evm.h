@@ -82,6 +82,9 @@ const char* evm_strerror(int status);
 int evm_set_stream(evm_ctx* ctx, void* hip_stream); /* NULL: the HIP default stream; initially the context's own */
 void* evm_get_stream(evm_ctx* ctx);
 int evm_sync(evm_ctx* ctx);
+/* tuning / test knobs */
+#define EVM_OPT_CLIENT_PATH 1 /* evm_apply_batch: 0 auto, 1 force the streaming path, 2 force the sort path */
+int evm_set_option(evm_ctx* ctx, int option, int64_t value);
 /* kernel timing with HIP events on the context stream (for roofline reports) */
 int evm_prof_enable(evm_ctx* ctx, int on);
 int evm_prof_reset(evm_ctx* ctx);
