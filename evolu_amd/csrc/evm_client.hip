@@ -583,6 +583,11 @@ __global__ void k_cl_pairs_ck(const u64* __restrict__ pairs, const u32* __restri
   }
 }
 
+__global__ void k_keep_bad(uint8_t* __restrict__ flags, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    flags[i] &= (uint8_t)EVM_MSG_BAD;
+}
+
 __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* __restrict__ present, u32 C,
                               Info* __restrict__ info) {
   const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -652,7 +657,10 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   KLAUNCH(k_cl_leaves, dim3((B + 255) / 256), dim3(256), dx, dp, pos, info, lck, lxr);
   Info hi;
   if ((st = read_info(ctx, info, &hi))) return st;
-  if (hi.bad) return EVM_ENONCANON;
+  if (hi.bad) {
+    KLAUNCH(k_keep_bad, dim3(grid_for(n, 256)), dim3(256), flags, n);  // nothing applied: only the culprits
+    return EVM_ENONCANON;
+  }
   if (hi.bad_aux) return EVM_EINVAL;
   if (hi.collision) return EVM_ECOLLISION;
   if (!hi.fold_overflow) return merge_into_tree(ctx, S, tree_in, tree_in->n_owners, lck, lxr, hi.n_leaves, tree_out);
