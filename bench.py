@@ -29,6 +29,12 @@ HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 # Algorithmic (compulsory) bytes per message of each kernel on the client path,
 # SURVEY.md section 8(d) accounting, restated per kernel in DESIGN.md.
 ALG_BYTES_PER_MSG = {
+    # streaming fast path (evm_client.hip)
+    "k_cl_pass<1>": 46 + 4 + 4,  # ts + cell in, hash out (per-range aggregates amortised away)
+    "k_cl_pass<2>": 46 + 4 + 1 + 8,  # ts + cell in, flag + (minute, hash) out
+    "k_cl_xcell": 4 + 8,  # hash in, one 8-B hash-set slot
+    "k_cl_fold_hist": 8,  # (minute, hash) pair in
+    # sort path
     "k_pack": 46 + 4 + 32,  # ts string + cell in, 32-B record out
     "k_xcell": 24 + 8,  # key + hash read, one 8-B hash-set slot
     "(k_radix_scatter<K>)": 16,  # (cell, idx) in and out, per pass

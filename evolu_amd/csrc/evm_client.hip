@@ -238,33 +238,61 @@ struct ClMsg {
   u32 meta;
 };
 
-// Loads and parses message `i` of the wave's 64-message block starting at
-// `first`.  For stride 48 the block (3 KiB) is read with fully coalesced
-// 16-B loads and re-distributed through LDS.
-__device__ __forceinline__ ClMsg cl_load(const uint8_t* __restrict__ ts, size_t stride, const u32* __restrict__ cell,
-                                         size_t first, size_t n, uint4* __restrict__ stage) {
+// Raw bytes of one 64-message round, as loaded (not yet redistributed).
+struct ClRaw {
+  uint4 a, b, c;
+  u32 cell;
+};
+
+// Issues the loads of the round starting at `first` (no wait).  For stride 48
+// lane l loads 16-B quads l, l+64, l+128 of the round's 3 KiB block (fully
+// coalesced); other strides load the lane's own timestamp.
+__device__ __forceinline__ ClRaw cl_fetch(const uint8_t* __restrict__ ts, size_t stride, const u32* __restrict__ cell,
+                                          size_t first, size_t end) {
   const int lane = threadIdx.x & 63;
+  ClRaw r;
   const size_t i = first + lane;
-  u32 w[12];
+  r.cell = i < end ? cell[i] : 0xffffffffu;
   if (stride == 48) {
     const uint4* src = reinterpret_cast<const uint4*>(ts + first * 48);
-    const size_t nq = (n - first) * 3;  // 16-B quads left in the arena from `first`
+    const size_t nq = first < end ? (end - first) * 3 : 0;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    r.a = (size_t)lane < nq ? src[lane] : z;
+    r.b = (size_t)lane + 64 < nq ? src[lane + 64] : z;
+    r.c = (size_t)lane + 128 < nq ? src[lane + 128] : z;
+  } else {
+    u32 w[12];
+    if (i < end) {
+      load_ts(ts, stride, i, w);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const size_t q = (size_t)lane + 64 * k;
-      stage[q] = q < nq ? src[q] : make_uint4(0, 0, 0, 0);
+      for (int k = 0; k < 12; ++k) w[k] = 0;
     }
+    r.a = make_uint4(w[0], w[1], w[2], w[3]);
+    r.b = make_uint4(w[4], w[5], w[6], w[7]);
+    r.c = make_uint4(w[8], w[9], w[10], w[11]);
+  }
+  return r;
+}
+
+// Redistributes (stride 48: through the wave's LDS stage) and parses.
+__device__ __forceinline__ ClMsg cl_decode(const ClRaw& r, size_t stride, uint4* __restrict__ stage) {
+  const int lane = threadIdx.x & 63;
+  u32 w[12];
+  if (stride == 48) {
+    stage[lane] = r.a;
+    stage[lane + 64] = r.b;
+    stage[lane + 128] = r.c;
     __syncthreads();
     const uint4 a = stage[3 * lane], b = stage[3 * lane + 1], c = stage[3 * lane + 2];
+    __syncthreads();
     w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
     w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
     w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
-    __syncthreads();
-  } else if (i < n) {
-    load_ts(ts, stride, i, w);
   } else {
-#pragma unroll
-    for (int k = 0; k < 12; ++k) w[k] = 0;
+    w[0] = r.a.x; w[1] = r.a.y; w[2] = r.a.z; w[3] = r.a.w;
+    w[4] = r.b.x; w[5] = r.b.y; w[6] = r.b.z; w[7] = r.b.w;
+    w[8] = r.c.x; w[9] = r.c.y; w[10] = r.c.z; w[11] = r.c.w & 0xffffu;
   }
   const Parsed p = parse_ts46(w);
   ClMsg m;
@@ -272,7 +300,7 @@ __device__ __forceinline__ ClMsg cl_load(const uint8_t* __restrict__ ts, size_t 
   m.hash = p.hash;
   m.minute = p.minute;
   m.meta = p.meta;
-  m.cell = i < n ? cell[i] : 0xffffffffu;
+  m.cell = r.cell;
   return m;
 }
 
@@ -295,6 +323,93 @@ __device__ __forceinline__ u64 match_cell(u32 c, bool active, int bits) {
   return active ? peers : 0ull;
 }
 
+struct ClState {
+  u64* tc;
+  u64* node;
+  u32* mask;
+  u32* first;
+};
+
+struct ClAcc {
+  u32 bad, bad_aux, mn, mx;
+};
+
+// One round of 64 messages (lane order == batch order).
+template <int PASS>
+__device__ __forceinline__ void cl_round(const ClMsg& m, size_t first, size_t end, u32 C, int cbits, const ClState& S,
+                                         u32* __restrict__ hash_out, uint8_t* __restrict__ flags,
+                                         u64* __restrict__ pairs, ClAcc& A) {
+  const int lane = threadIdx.x & 63;
+  const size_t i = first + lane;
+  const bool live = i < end;
+  const bool valid = (m.meta & EVM_META_VALID) != 0;
+  const bool ok = live && valid && m.cell < C;
+  if (PASS == 1) {
+    A.bad |= (live && !valid) ? 1u : 0u;
+    A.bad_aux |= (live && m.cell >= C) ? 1u : 0u;
+    if (live) hash_out[i] = m.hash;
+    if (ok) {
+      A.mn = min(A.mn, m.minute);
+      A.mx = max(A.mx, m.minute);
+    }
+  }
+  const u64 peers = match_cell(m.cell, ok, cbits);
+  const bool last_peer = ok && (peers >> lane) == 1ull;
+  u64 rem = peers & lanemask_lt();
+  if (PASS == 1) {
+    // round max of this lane's cell over peers up to this lane; first index wins ties
+    Key acc = key_none();
+    u32 acc_i = 0xffffffffu;
+    while (__any(rem != 0)) {
+      const int src = rem ? (int)__builtin_ctzll(rem) : lane;
+      const Key kp = shfl_key(m.key, src);
+      if (rem) {
+        if (key_cmp(kp, acc) > 0) {
+          acc = kp;
+          acc_i = (u32)(first + src);
+        }
+        rem &= rem - 1;
+      }
+    }
+    if (ok && key_cmp(m.key, acc) > 0) {
+      acc = m.key;
+      acc_i = (u32)i;
+    }
+    if (last_peer) {
+      const Key st{S.tc[m.cell], S.node[m.cell], S.mask[m.cell]};
+      if (key_cmp(acc, st) > 0) {
+        S.tc[m.cell] = acc.tc;
+        S.node[m.cell] = acc.node;
+        S.mask[m.cell] = acc.mask;
+        S.first[m.cell] = acc_i;
+      }
+    }
+  } else {
+    Key acc = ok ? Key{S.tc[m.cell], S.node[m.cell], S.mask[m.cell]} : key_none();
+    while (__any(rem != 0)) {
+      const int src = rem ? (int)__builtin_ctzll(rem) : lane;
+      const Key kp = shfl_key(m.key, src);
+      if (rem) {
+        acc = key_max(acc, kp);
+        rem &= rem - 1;
+      }
+    }
+    if (live) {
+      // applyMessages.ts:93 / :105 with t = acc
+      const bool ups = ok && key_cmp(acc, m.key) < 0;
+      const bool xr = ok && !((acc.mask & KEY_PRESENT) && key_eq(acc, m.key));
+      flags[i] = ok ? (uint8_t)((ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u)) : (uint8_t)EVM_MSG_BAD;
+      pairs[i] = xr ? ((u64)m.hash << 32 | (u64)m.minute) : ~0ull;
+    }
+    if (last_peer) {
+      const Key inc = key_max(acc, m.key);
+      S.tc[m.cell] = inc.tc;
+      S.node[m.cell] = inc.node;
+      S.mask[m.cell] = inc.mask;
+    }
+  }
+}
+
 template <int PASS>
 __global__ __launch_bounds__(64) void k_cl_pass(const uint8_t* __restrict__ ts, size_t stride,
                                                 const u32* __restrict__ cell, size_t n, u32 C, int cbits,
@@ -303,149 +418,141 @@ __global__ __launch_bounds__(64) void k_cl_pass(const uint8_t* __restrict__ ts, 
                                                 u32* __restrict__ hash_out, uint8_t* __restrict__ flags,
                                                 u64* __restrict__ pairs, Info* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint4* stage = reinterpret_cast<uint4*>(smem);                  // 3 KiB
-  u64* s_tc = reinterpret_cast<u64*>(smem + 3072);                // C
-  u64* s_node = s_tc + C;                                         // C
-  u32* s_mask = reinterpret_cast<u32*>(s_node + C);               // C
-  u32* s_first = s_mask + C;                                      // C (pass 1)
+  uint4* stage = reinterpret_cast<uint4*>(smem);  // 3 KiB
+  ClState S;
+  S.tc = reinterpret_cast<u64*>(smem + 3072);
+  S.node = S.tc + C;
+  S.mask = reinterpret_cast<u32*>(S.node + C);
+  S.first = S.mask + C;
   const int lane = threadIdx.x;
   const size_t g = blockIdx.x;
   const size_t beg = g * range_len;
   const size_t end = min(n, beg + range_len);
   for (u32 c = lane; c < C; c += 64) {
     if (PASS == 1) {
-      s_tc[c] = 0;
-      s_node[c] = 0;
-      s_mask[c] = 0;
-      s_first[c] = 0xffffffffu;
+      S.tc[c] = 0;
+      S.node[c] = 0;
+      S.mask[c] = 0;
+      S.first[c] = 0xffffffffu;
     } else {
-      s_tc[c] = agg_tc[g * C + c];
-      s_node[c] = agg_node[g * C + c];
-      s_mask[c] = agg_mask[g * C + c];
+      S.tc[c] = agg_tc[g * C + c];
+      S.node[c] = agg_node[g * C + c];
+      S.mask[c] = agg_mask[g * C + c];
     }
   }
   __syncthreads();
-  const u64 lt = lanemask_lt();
-  u32 bad = 0, bad_aux = 0, mn = 0xffffffffu, mx = 0;
-  for (size_t first = beg; first < end; first += 64) {
-    const ClMsg m = cl_load(ts, stride, cell, first, end, stage);
-    const size_t i = first + lane;
-    const bool live = i < end;
-    const bool valid = (m.meta & EVM_META_VALID) != 0;
-    const bool ok = live && valid && m.cell < C;
-    if (PASS == 1) {
-      bad |= (live && !valid) ? 1u : 0u;
-      bad_aux |= (live && m.cell >= C) ? 1u : 0u;
-      if (live) hash_out[i] = m.hash;
-      if (ok) {
-        mn = min(mn, m.minute);
-        mx = max(mx, m.minute);
-      }
+  ClAcc A{0u, 0u, 0xffffffffu, 0u};
+  // software pipeline: rounds are fetched two ahead of the one being decoded
+  size_t first = beg;
+  ClRaw r0 = cl_fetch(ts, stride, cell, first, end);
+  ClRaw r1 = cl_fetch(ts, stride, cell, first + 64, end);
+  for (; first < end; first += 128) {
+    const ClRaw r2 = cl_fetch(ts, stride, cell, first + 128, end);
+    const ClRaw r3 = cl_fetch(ts, stride, cell, first + 192, end);
+    {
+      const ClMsg m = cl_decode(r0, stride, stage);
+      cl_round<PASS>(m, first, end, C, cbits, S, hash_out, flags, pairs, A);
     }
-    const u64 peers = match_cell(m.cell, ok, cbits);
-    const bool last_peer = ok && (peers >> lane) == 1ull;
-    u64 rem = peers & lt;
-    if (PASS == 1) {
-      // round max of this lane's cell over peers up to this lane, first index wins ties
-      Key acc = key_none();
-      u32 acc_i = 0xffffffffu;
-      while (__any(rem != 0)) {
-        const int src = rem ? (int)__builtin_ctzll(rem) : lane;
-        const Key kp = shfl_key(m.key, src);
-        if (rem) {
-          if (key_cmp(kp, acc) > 0) {
-            acc = kp;
-            acc_i = (u32)(first + src);
-          }
-          rem &= rem - 1;
-        }
-      }
-      if (ok && key_cmp(m.key, acc) > 0) {
-        acc = m.key;
-        acc_i = (u32)i;
-      }
-      if (last_peer) {
-        const Key st{s_tc[m.cell], s_node[m.cell], s_mask[m.cell]};
-        if (key_cmp(acc, st) > 0) {
-          s_tc[m.cell] = acc.tc;
-          s_node[m.cell] = acc.node;
-          s_mask[m.cell] = acc.mask;
-          s_first[m.cell] = acc_i;
-        }
-      }
-    } else {
-      Key acc = ok ? Key{s_tc[m.cell], s_node[m.cell], s_mask[m.cell]} : key_none();
-      while (__any(rem != 0)) {
-        const int src = rem ? (int)__builtin_ctzll(rem) : lane;
-        const Key kp = shfl_key(m.key, src);
-        if (rem) {
-          acc = key_max(acc, kp);
-          rem &= rem - 1;
-        }
-      }
-      if (live) {
-        // applyMessages.ts:93 / :105 with t = acc
-        const bool ups = ok && key_cmp(acc, m.key) < 0;
-        const bool xr = ok && !((acc.mask & KEY_PRESENT) && key_eq(acc, m.key));
-        flags[i] = ok ? (uint8_t)((ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u)) : (uint8_t)EVM_MSG_BAD;
-        pairs[i] = xr ? ((u64)m.hash << 32 | (u64)m.minute) : ~0ull;
-      }
-      if (last_peer) {
-        const Key inc = key_max(acc, m.key);
-        s_tc[m.cell] = inc.tc;
-        s_node[m.cell] = inc.node;
-        s_mask[m.cell] = inc.mask;
-      }
+    if (first + 64 < end) {
+      const ClMsg m = cl_decode(r1, stride, stage);
+      cl_round<PASS>(m, first + 64, end, C, cbits, S, hash_out, flags, pairs, A);
     }
+    r0 = r2;
+    r1 = r3;
   }
   if (PASS == 1) {
     __syncthreads();
     for (u32 c = lane; c < C; c += 64) {
-      agg_tc[g * C + c] = s_tc[c];
-      agg_node[g * C + c] = s_node[c];
-      agg_mask[g * C + c] = s_mask[c];
-      agg_first[g * C + c] = s_first[c];
+      agg_tc[g * C + c] = S.tc[c];
+      agg_node[g * C + c] = S.node[c];
+      agg_mask[g * C + c] = S.mask[c];
+      agg_first[g * C + c] = S.first[c];
     }
     for (int d = 32; d >= 1; d >>= 1) {
-      bad |= __shfl_xor(bad, d, 64);
-      bad_aux |= __shfl_xor(bad_aux, d, 64);
-      mn = min(mn, (u32)__shfl_xor(mn, d, 64));
-      mx = max(mx, (u32)__shfl_xor(mx, d, 64));
+      A.bad |= __shfl_xor(A.bad, d, 64);
+      A.bad_aux |= __shfl_xor(A.bad_aux, d, 64);
+      A.mn = min(A.mn, (u32)__shfl_xor(A.mn, d, 64));
+      A.mx = max(A.mx, (u32)__shfl_xor(A.mx, d, 64));
     }
     if (lane == 0) {
-      if (bad) atomicOr(&info->bad, 1u);
-      if (bad_aux) atomicOr(&info->bad_aux, 1u);
-      if (mn != 0xffffffffu) {
-        atomicMin(&info->minute_min, mn);
-        atomicMax(&info->minute_max, mx);
+      if (A.bad) atomicOr(&info->bad, 1u);
+      if (A.bad_aux) atomicOr(&info->bad_aux, 1u);
+      if (A.mn != 0xffffffffu) {
+        atomicMin(&info->minute_min, A.mn);
+        atomicMax(&info->minute_max, A.mx);
       }
     }
   }
 }
 
-// Per cell: exclusive scan of the range aggregates in batch order, seeded with
-// the prior max.  Rewrites agg_* in place into the carry-in of every range.
-__global__ void k_cl_carry(u32 C, size_t G, u64* __restrict__ agg_tc, u64* __restrict__ agg_node,
-                           u32* __restrict__ agg_mask, const u32* __restrict__ agg_first,
-                           const evm_rec* __restrict__ prior, const uint8_t* __restrict__ prior_present,
-                           int32_t* __restrict__ winner) {
+// Carry: per cell, exclusive scan of the range aggregates in batch order,
+// seeded with the prior max, as a 3-phase scan over SEG range segments.
+// (max, first index) with ties kept left is associative.
+constexpr u32 CARRY_SEGS = 64;
+
+struct Agg {
+  Key key;
+  u32 first;
+};
+__device__ __forceinline__ Agg agg_merge(const Agg& a, const Agg& b) { return key_cmp(b.key, a.key) > 0 ? b : a; }
+
+__global__ void k_cl_carry_reduce(u32 C, size_t G, const u64* __restrict__ tc, const u64* __restrict__ node,
+                                  const u32* __restrict__ mask, const u32* __restrict__ firsti, u64* __restrict__ s_tc,
+                                  u64* __restrict__ s_node, u32* __restrict__ s_mask, u32* __restrict__ s_first) {
+  const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
+  if (c >= C) return;
+  const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
+  const size_t a = p * per, e = min(G, a + per);
+  Agg run{key_none(), 0xffffffffu};
+#pragma unroll 4
+  for (size_t g = a; g < e; ++g) {
+    const size_t k = g * C + c;
+    run = agg_merge(run, Agg{Key{tc[k], node[k], mask[k]}, firsti[k]});
+  }
+  const size_t o = (size_t)p * C + c;
+  s_tc[o] = run.key.tc;
+  s_node[o] = run.key.node;
+  s_mask[o] = run.key.mask;
+  s_first[o] = run.first;
+}
+
+__global__ void k_cl_carry_segs(u32 C, u64* __restrict__ s_tc, u64* __restrict__ s_node, u32* __restrict__ s_mask,
+                                u32* __restrict__ s_first, const evm_rec* __restrict__ prior,
+                                const uint8_t* __restrict__ prior_present, int32_t* __restrict__ winner) {
   const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  Key run = (prior_present && prior_present[c]) ? key_of(prior[c]) : key_none();
-  int32_t first = -1;
-  for (size_t g = 0; g < G; ++g) {
-    const size_t k = g * C + c;
-    const Key a{agg_tc[k], agg_node[k], agg_mask[k]};
-    const u32 ai = agg_first[k];
-    agg_tc[k] = run.tc;
-    agg_node[k] = run.node;
-    agg_mask[k] = run.mask;
-    if (key_cmp(a, run) > 0) {
-      run = a;
-      first = (int32_t)ai;
-    }
+  // the prior max has no batch index: it wins ties (an equal batch copy is a no-op)
+  Agg run{(prior_present && prior_present[c]) ? key_of(prior[c]) : key_none(), 0xffffffffu};
+  for (u32 p = 0; p < CARRY_SEGS; ++p) {
+    const size_t o = (size_t)p * C + c;
+    const Agg t{Key{s_tc[o], s_node[o], s_mask[o]}, s_first[o]};
+    s_tc[o] = run.key.tc;
+    s_node[o] = run.key.node;
+    s_mask[o] = run.key.mask;
+    s_first[o] = run.first;
+    run = agg_merge(run, t);
   }
-  winner[c] = first;
+  winner[c] = (int32_t)run.first;  // 0xffffffff -> -1: no upsert survives
+}
+
+__global__ void k_cl_carry_down(u32 C, size_t G, u64* __restrict__ tc, u64* __restrict__ node, u32* __restrict__ mask,
+                                const u32* __restrict__ firsti, const u64* __restrict__ s_tc,
+                                const u64* __restrict__ s_node, const u32* __restrict__ s_mask) {
+  const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
+  if (c >= C) return;
+  const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
+  const size_t a = p * per, e = min(G, a + per);
+  const size_t o = (size_t)p * C + c;
+  Key run{s_tc[o], s_node[o], s_mask[o]};
+#pragma unroll 4
+  for (size_t g = a; g < e; ++g) {
+    const size_t k = g * C + c;
+    const Key here{tc[k], node[k], mask[k]};
+    tc[k] = run.tc;
+    node[k] = run.node;
+    mask[k] = run.mask;
+    run = key_max(run, here);
+  }
 }
 
 // Exact cross-cell check over a persistent epoch-tagged hash set:
@@ -485,6 +592,86 @@ __global__ void k_cl_xcell(const uint8_t* __restrict__ ts, size_t stride, const 
         }
       }
       pos = (pos + 1) & mask;
+    }
+  }
+}
+
+// Partitioned cross-cell check (the default): messages are bucketed by the top
+// bits of their hash (one counting-sort pass), then every bucket is checked in
+// an LDS hash set.  Equal timestamps always share a bucket.  A bucket too big
+// for LDS flags `xc_oversize` and the host reruns the global-table check.
+constexpr int XP_THREADS = 1024;
+constexpr int XP_ITEMS = 32;
+constexpr int XP_TILE = XP_THREADS * XP_ITEMS;
+constexpr u32 XP_MAX_BUCKET = 8192;  // entries a bucket may hold for the LDS set
+constexpr u32 XP_SLOTS = 16384;      // LDS set slots, 128 KiB
+
+__global__ __launch_bounds__(XP_THREADS) void k_xp_hist(const u32* __restrict__ hash, size_t n, int kb,
+                                                       u32* __restrict__ counts, u32 ntiles) {
+  extern __shared__ u32 hist[];
+  const u32 B = 1u << kb;
+  for (u32 b = threadIdx.x; b < B; b += XP_THREADS) hist[b] = 0;
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * XP_TILE;
+  for (int k = 0; k < XP_ITEMS; ++k) {
+    const size_t i = base + (size_t)k * XP_THREADS + threadIdx.x;
+    if (i < n) atomicAdd(&hist[hash[i] >> (32 - kb)], 1u);
+  }
+  __syncthreads();
+  for (u32 b = threadIdx.x; b < B; b += XP_THREADS) counts[(size_t)b * ntiles + blockIdx.x] = hist[b];
+}
+
+__global__ __launch_bounds__(XP_THREADS) void k_xp_scatter(const u32* __restrict__ hash, size_t n, int kb,
+                                                          const u32* __restrict__ offs, u32 ntiles,
+                                                          u64* __restrict__ out) {
+  extern __shared__ u32 cnt[];
+  const u32 B = 1u << kb;
+  for (u32 b = threadIdx.x; b < B; b += XP_THREADS) cnt[b] = offs[(size_t)b * ntiles + blockIdx.x];
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * XP_TILE;
+  for (int k = 0; k < XP_ITEMS; ++k) {
+    const size_t i = base + (size_t)k * XP_THREADS + threadIdx.x;
+    if (i < n) {
+      const u32 h = hash[i];
+      const u32 dst = atomicAdd(&cnt[h >> (32 - kb)], 1u);  // order inside a bucket is irrelevant
+      out[dst] = ((u64)h << 32) | (u64)i;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_xp_dedup(const u64* __restrict__ pairs, const u32* __restrict__ offs, u32 ntiles,
+                                                  int kb, size_t n, const uint8_t* __restrict__ ts, size_t stride,
+                                                  const u32* __restrict__ cell, Info* __restrict__ info) {
+  __shared__ u64 tab[XP_SLOTS];  // hash:32 | (index + 1):32, 0 = empty
+  const u32 b = blockIdx.x, B = 1u << kb;
+  const size_t a = offs[(size_t)b * ntiles];
+  const size_t e = (b + 1 < B) ? offs[(size_t)(b + 1) * ntiles] : n;
+  const size_t cnt = e - a;
+  if (cnt < 2) return;
+  if (cnt > XP_MAX_BUCKET) {
+    if (threadIdx.x == 0) atomicOr(&info->fold_overflow, 2u);  // bit 1: bucket too big for LDS
+    return;
+  }
+  u32 slots = 64;
+  while (slots < 2 * cnt) slots <<= 1;
+  for (u32 s = threadIdx.x; s < slots; s += 256) tab[s] = 0;
+  __syncthreads();
+  for (size_t k = a + threadIdx.x; k < e; k += 256) {
+    const u64 p = pairs[k];
+    const u32 h = (u32)(p >> 32), i = (u32)p;
+    const u64 mine = ((u64)h << 32) | (u64)(i + 1);
+    u32 pos = (h * 2654435761u) & (slots - 1);
+    for (u32 probe = 0; probe < slots; ++probe) {
+      const u64 prev = atomicCAS(&tab[pos], 0ull, mine);
+      if (prev == 0) break;  // inserted
+      if ((u32)(prev >> 32) == h) {
+        const u32 j = (u32)prev - 1;
+        if (ts_bytes_equal(ts, stride, i, j)) {  // equal strings <=> equal keys (both canonical)
+          if (cell[i] != cell[j]) atomicOr(&info->collision, 1u);
+          break;
+        }
+      }
+      pos = (pos + 1) & (slots - 1);
     }
   }
 }
@@ -618,24 +805,39 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
     hipLaunchKernelGGL((k_cl_pass<1>), dim3(G), dim3(64), lds, ctx->stream, (const uint8_t*)ts, stride, cell, n, C,
                        cbits, range, a_tc, a_node, a_mask, a_first, hash, (uint8_t*)nullptr, (u64*)nullptr, info);
   }
-  // cross-cell PK check on a persistent hash set (epoch-tagged: no clearing)
-  const int lg = std::max(ceil_log2(n + n / 2 + 1), 10);
-  if (!ctx->xtab || ctx->xtab_lg < lg) {
-    if (ctx->xtab) HIPR(hipFree(ctx->xtab));
-    ctx->xtab = nullptr;
-    HIPR(hipMalloc(&ctx->xtab, sizeof(u64) << lg));
-    HIPR(hipMemsetAsync(ctx->xtab, 0, sizeof(u64) << lg, ctx->stream));
-    ctx->xtab_lg = lg;
-    ctx->xepoch = 0;
+  // cross-cell PK check: partition by hash, LDS hash set per bucket
+  int kb = 1;
+  while (kb < 14 && ((size_t)2048 << kb) < n) ++kb;
+  const u32 xt = (u32)((n + XP_TILE - 1) / XP_TILE);
+  const size_t nbt = ((size_t)1 << kb) * xt;
+  u32* xcnt = S.alloc<u32>(nbt);
+  u32* xoff = S.alloc<u32>(nbt);
+  u64* xpairs = S.alloc<u64>(n);
+  if (!xcnt || !xoff || !xpairs) return EVM_ENOMEM;
+  {
+    evm::ProfScope ps_(ctx, "k_xp_hist");
+    hipLaunchKernelGGL(k_xp_hist, dim3(xt), dim3(XP_THREADS), sizeof(u32) << kb, ctx->stream, hash, n, kb, xcnt, xt);
   }
-  if (++ctx->xepoch == 256) {
-    HIPR(hipMemsetAsync(ctx->xtab, 0, sizeof(u64) << ctx->xtab_lg, ctx->stream));
-    ctx->xepoch = 1;
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, xcnt, nbt, xoff, (u32*)nullptr))) return st;
+  {
+    evm::ProfScope ps_(ctx, "k_xp_scatter");
+    hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), sizeof(u32) << kb, ctx->stream, hash, n, kb, xoff, xt,
+                       xpairs);
   }
-  KLAUNCH(k_cl_xcell, dim3(grid_for(n, 256, 16384)), dim3(256), (const uint8_t*)ts, stride, cell, hash, n, ctx->xtab,
-          (u32)ctx->xtab_lg, ctx->xepoch, info);
-  KLAUNCH(k_cl_carry, dim3((C + 255) / 256), dim3(256), C, G, a_tc, a_node, a_mask, a_first, prior, prior_present,
-          winner);
+  KLAUNCH(k_xp_dedup, dim3(1u << kb), dim3(256), xpairs, xoff, xt, kb, n, (const uint8_t*)ts, stride, cell, info);
+  {
+    u64* s_tc = S.alloc<u64>((size_t)CARRY_SEGS * C);
+    u64* s_node = S.alloc<u64>((size_t)CARRY_SEGS * C);
+    u32* s_mask = S.alloc<u32>((size_t)CARRY_SEGS * C);
+    u32* s_first = S.alloc<u32>((size_t)CARRY_SEGS * C);
+    if (!s_tc || !s_node || !s_mask || !s_first) return EVM_ENOMEM;
+    const u32 cb = (C + 63) / 64;
+    KLAUNCH(k_cl_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_node, a_mask, a_first, s_tc, s_node, s_mask,
+            s_first);
+    KLAUNCH(k_cl_carry_segs, dim3(cb), dim3(64), C, s_tc, s_node, s_mask, s_first, prior, prior_present, winner);
+    KLAUNCH(k_cl_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_node, a_mask, a_first, s_tc, s_node,
+            s_mask);
+  }
   {
     evm::ProfScope ps_(ctx, "k_cl_pass<2>");
     hipLaunchKernelGGL((k_cl_pass<2>), dim3(G), dim3(64), lds, ctx->stream, (const uint8_t*)ts, stride, cell, n, C,
@@ -662,7 +864,27 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
     return EVM_ENONCANON;
   }
   if (hi.bad_aux) return EVM_EINVAL;
+  if (!hi.collision && (hi.fold_overflow & 2u)) {
+    // a hash bucket overflowed LDS (heavy skew): exact check on the global epoch-tagged set
+    const int lg = std::max(ceil_log2(n + n / 2 + 1), 10);
+    if (!ctx->xtab || ctx->xtab_lg < lg) {
+      if (ctx->xtab) HIPR(hipFree(ctx->xtab));
+      ctx->xtab = nullptr;
+      HIPR(hipMalloc(&ctx->xtab, sizeof(u64) << lg));
+      HIPR(hipMemsetAsync(ctx->xtab, 0, sizeof(u64) << lg, ctx->stream));
+      ctx->xtab_lg = lg;
+      ctx->xepoch = 0;
+    }
+    if (++ctx->xepoch == 256) {
+      HIPR(hipMemsetAsync(ctx->xtab, 0, sizeof(u64) << ctx->xtab_lg, ctx->stream));
+      ctx->xepoch = 1;
+    }
+    KLAUNCH(k_cl_xcell, dim3(grid_for(n, 256, 16384)), dim3(256), (const uint8_t*)ts, stride, cell, hash, n, ctx->xtab,
+            (u32)ctx->xtab_lg, ctx->xepoch, info);
+    if ((st = read_info(ctx, info, &hi))) return st;
+  }
   if (hi.collision) return EVM_ECOLLISION;
+  hi.fold_overflow &= 1u;
   if (!hi.fold_overflow) return merge_into_tree(ctx, S, tree_in, tree_in->n_owners, lck, lxr, hi.n_leaves, tree_out);
   // wide minute range or mixed key lengths: sort-based fold
   u32* sel = S.alloc<u32>(n);

@@ -497,7 +497,8 @@ void evm_destroy(evm_ctx* ctx) {
 
 int evm_set_stream(evm_ctx* ctx, void* s) {
   if (!ctx) return EVM_EINVAL;
-  ctx->stream = (hipStream_t)s;  // NULL: the HIP default (null) stream
+  (void)hipStreamSynchronize(ctx->stream);  // the workspace is ordered on one stream at a time
+  ctx->stream = (hipStream_t)s;             // NULL: the HIP default (null) stream
   return EVM_OK;
 }
 void* evm_get_stream(evm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }

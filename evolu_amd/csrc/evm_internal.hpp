@@ -23,9 +23,12 @@ struct evm_ctx {
   unsigned long long* xtab = nullptr;
   int xtab_lg = 0;
   unsigned xepoch = 0;
-  // persistent workspace for the client fast path
+  // persistent workspace (Scratch arena)
   void* ws = nullptr;
   size_t ws_bytes = 0;
+  size_t ws_top = 0;   // arena bytes in use
+  size_t ws_vtop = 0;  // bytes the current call would use (arena + pool overflow)
+  size_t ws_need = 0;  // largest ws_vtop seen
 };
 
 // One MerkleTree per owner, as sorted unique leaves keyed by
@@ -83,23 +86,47 @@ inline int hip_ok(hipError_t e) {
     if (e_ != hipSuccess) return evm::hip_ok(e_); \
   } while (0)
 
-// Stream-ordered scratch, released at scope exit.
+// Per-call scratch: a bump arena in the context's persistent workspace,
+// stream-ordered on ctx->stream (calls on one context never overlap on the
+// device).  When the arena is short the pool backs the call and the
+// outermost Scratch of the next call grows the arena to the size seen, so a
+// repeated workload makes no allocation calls at all.
 class Scratch {
  public:
-  explicit Scratch(evm_ctx* c) : ctx_(c) {}
+  explicit Scratch(evm_ctx* c) : ctx_(c), mark_(c->ws_top), vmark_(c->ws_vtop) {
+    if (mark_ == 0 && vmark_ == 0 && ctx_->ws_need > ctx_->ws_bytes) {
+      (void)hipStreamSynchronize(ctx_->stream);
+      if (ctx_->ws) (void)hipFree(ctx_->ws);
+      ctx_->ws = nullptr;
+      ctx_->ws_bytes = 0;
+      const size_t want = ctx_->ws_need + ctx_->ws_need / 8;
+      if (hipMalloc(&ctx_->ws, want) == hipSuccess) ctx_->ws_bytes = want;
+    }
+  }
   ~Scratch() {
+    ctx_->ws_top = mark_;
+    ctx_->ws_vtop = vmark_;
     for (void* p : ptrs_) (void)hipFreeAsync(p, ctx_->stream);
   }
   template <typename T>
   T* alloc(size_t n) {
+    const size_t bytes = (sizeof(T) * (n ? n : 1) + 255) & ~(size_t)255;
+    ctx_->ws_vtop += bytes;
+    if (ctx_->ws_vtop > ctx_->ws_need) ctx_->ws_need = ctx_->ws_vtop;
+    if (ctx_->ws && ctx_->ws_top + bytes <= ctx_->ws_bytes && ctx_->ws_top + bytes == ctx_->ws_vtop) {
+      void* p = static_cast<char*>(ctx_->ws) + ctx_->ws_top;
+      ctx_->ws_top += bytes;
+      return static_cast<T*>(p);
+    }
     void* p = nullptr;
-    if (hipMallocAsync(&p, sizeof(T) * (n ? n : 1), ctx_->stream) != hipSuccess) return nullptr;
+    if (hipMallocAsync(&p, bytes, ctx_->stream) != hipSuccess) return nullptr;
     ptrs_.push_back(p);
     return static_cast<T*>(p);
   }
 
  private:
   evm_ctx* ctx_;
+  size_t mark_, vmark_;
   std::vector<void*> ptrs_;
 };
 

@@ -164,3 +164,35 @@ def test_fast_vs_sort_path_at_scale(eng, n):
     assert (f1 & L.MSG_BAD).sum() == 0
     del ts, cell
     torch.cuda.empty_cache()
+
+
+def test_redelivery_storm_oversize_bucket(eng):
+    """20k copies of one message overflow an LDS hash bucket: the exact global
+    check takes over; a copy in another cell is still a collision."""
+    from evolu_amd import _lib as L
+
+    ts = "2024-03-01T10:00:00.000Z-0000-00000000000000aa"
+    other = "2024-03-01T10:00:00.001Z-0000-00000000000000aa"
+    strings = [other] + [ts] * 20000
+    cell = np.zeros(len(strings), dtype=np.uint32)
+    flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), eng.timestamps(strings), eng.dev(cell), 2)
+    f = flags.cpu().numpy()
+    assert list(f[:3]) == [3, 3, 0] and (f[2:] == 0).all()
+    assert list(winner.cpu().numpy()) == [1, -1]
+    want = O.apply_messages(O.ClientDb(), {}, [{"timestamp": s, "table": "t", "row": "r", "column": "c", "value": 0}
+                                                for s in strings[:50]])
+    assert tree.to_json(0) == O.merkle_tree_to_string(want)
+    cell[-1] = 1
+    _, _, tree, st = eng.apply_batch(eng.tree_new(1), eng.timestamps(strings), eng.dev(cell), 2, raise_on_error=False)
+    assert st == L.EVM_ECOLLISION
+
+
+def test_collision_detected_at_scale(eng):
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    ts_np, cell_np = synth.config2(2_000_000, 1000, seed_config=7)
+    ts_np = np.concatenate([ts_np, ts_np[123456:123457]])
+    cell_np = np.concatenate([cell_np, (cell_np[123456:123457] + 1) % 1000])
+    _, _, _, st = eng.apply_batch(eng.tree_new(1), eng.dev(ts_np), eng.dev(cell_np), 1000, raise_on_error=False)
+    assert st == L.EVM_ECOLLISION
