@@ -172,15 +172,20 @@ def test_redelivery_storm_oversize_bucket(eng):
     from evolu_amd import _lib as L
 
     ts = "2024-03-01T10:00:00.000Z-0000-00000000000000aa"
-    other = "2024-03-01T10:00:00.001Z-0000-00000000000000aa"
-    strings = [other] + [ts] * 20000
+    older = "2024-03-01T09:59:59.999Z-0000-00000000000000aa"
+    newer = "2024-03-01T10:00:00.001Z-0000-00000000000000aa"
+    # exact redeliveries of the cell max are no-ops; a stale one re-XORs (toggles)
+    strings = [older] + [ts] * 20000 + [newer, ts, ts]
     cell = np.zeros(len(strings), dtype=np.uint32)
     flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), eng.timestamps(strings), eng.dev(cell), 2)
     f = flags.cpu().numpy()
-    assert list(f[:3]) == [3, 3, 0] and (f[2:] == 0).all()
-    assert list(winner.cpu().numpy()) == [1, -1]
-    want = O.apply_messages(O.ClientDb(), {}, [{"timestamp": s, "table": "t", "row": "r", "column": "c", "value": 0}
-                                                for s in strings[:50]])
+    db = O.ClientDb()
+    dec = []
+    want = O.apply_messages(db, {}, [{"timestamp": s, "table": "t", "row": "r", "column": "c", "value": 0}
+                                     for s in strings], dec)
+    assert list(f) == [(1 if u else 0) | (2 if x else 0) for u, x, _ in dec]
+    assert list(f[:3]) == [3, 3, 0] and list(f[-3:]) == [3, 2, 2]
+    assert list(winner.cpu().numpy()) == [20001, -1]
     assert tree.to_json(0) == O.merkle_tree_to_string(want)
     cell[-1] = 1
     _, _, tree, st = eng.apply_batch(eng.tree_new(1), eng.timestamps(strings), eng.dev(cell), 2, raise_on_error=False)
