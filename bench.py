@@ -30,10 +30,12 @@ HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 # SURVEY.md section 8(d) accounting, restated per kernel in DESIGN.md.
 ALG_BYTES_PER_MSG = {
     # streaming fast path (evm_client.hip)
-    "k_cl_pass<1>": 46 + 4 + 4,  # ts + cell in, hash out (per-range aggregates amortised away)
-    "k_cl_pass<2>": 46 + 4 + 1 + 8,  # ts + cell in, flag + (minute, hash) out
-    "k_cl_xcell": 4 + 8,  # hash in, one 8-B hash-set slot
-    "k_cl_fold_hist": 8,  # (minute, hash) pair in
+    "k_cl_pack": 46 + 4 + 28,  # ts + cell in; key 16 + meta 4 + hash 4 + minute 4 out
+    "k_cl_pass<1>": 16 + 4 + 4,  # key + meta + cell in (per-range aggregates amortised away)
+    "k_cl_pass<2>": 16 + 4 + 4 + 1,  # key + meta + cell in, flag out
+    "k_xp_scatter": 4 + 8,  # hash in, (hash, index) out
+    "k_xp_dedup": 8,  # (hash, index) in
+    "k_cl_fold_hist": 9,  # flag + minute + hash in (per window)
     # sort path
     "k_pack": 46 + 4 + 32,  # ts string + cell in, 32-B record out
     "k_xcell": 24 + 8,  # key + hash read, one 8-B hash-set slot

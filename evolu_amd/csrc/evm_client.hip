@@ -230,77 +230,106 @@ constexpr u32 FOLD_MAXWIN = 4;
 constexpr u32 FOLD_CHUNKS = 64;
 constexpr int FOLD_THREADS = 1024;
 
+// K1 for the streaming path: parse every timestamp once, at full occupancy,
+// into SoA records: key (tc, node) 16 B, meta 4 B, hash 4 B, minute 4 B.
+// For stride 48 each wave reads its 64 timestamps (3 KiB) with coalesced 16-B
+// loads and redistributes them through LDS.
+constexpr int CLP_THREADS = 256;
+
+__global__ __launch_bounds__(CLP_THREADS) void k_cl_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
+                                                         const u32* __restrict__ cell, u32 C, uint4* __restrict__ key,
+                                                         u32* __restrict__ meta, u32* __restrict__ hash,
+                                                         u32* __restrict__ minute, Info* __restrict__ info) {
+  __shared__ uint4 stage[CLP_THREADS / 64][192];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u32 bad = 0, bad_aux = 0, mn = 0xffffffffu, mx = 0;
+  const size_t nwaves = (size_t)gridDim.x * (CLP_THREADS / 64);
+  for (size_t first = ((size_t)blockIdx.x * (CLP_THREADS / 64) + wv) * 64; first < n; first += nwaves * 64) {
+    const size_t i = first + lane;
+    u32 w[12];
+    if (stride == 48) {
+      const uint4* src = reinterpret_cast<const uint4*>(ts + first * 48);
+      const size_t nq = (min(n, first + 64) - first) * 3;
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      stage[wv][lane] = (size_t)lane < nq ? src[lane] : z;
+      stage[wv][lane + 64] = (size_t)lane + 64 < nq ? src[lane + 64] : z;
+      stage[wv][lane + 128] = (size_t)lane + 128 < nq ? src[lane + 128] : z;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const uint4 a = stage[wv][3 * lane], b = stage[wv][3 * lane + 1], c = stage[wv][3 * lane + 2];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+      w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+      w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
+    } else if (i < n) {
+      load_ts(ts, stride, i, w);
+    }
+    if (i < n) {
+      const Parsed p = parse_ts46(w);
+      key[i] = make_uint4((u32)p.tc, (u32)(p.tc >> 32), (u32)p.node, (u32)(p.node >> 32));
+      meta[i] = p.meta;
+      hash[i] = p.hash;
+      minute[i] = p.minute;
+      const bool valid = (p.meta & EVM_META_VALID) != 0;
+      bad |= valid ? 0u : 1u;
+      if (cell[i] >= C) bad_aux = 1;
+      if (valid) {
+        mn = min(mn, p.minute);
+        mx = max(mx, p.minute);
+      }
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    bad |= __shfl_xor(bad, d, 64);
+    bad_aux |= __shfl_xor(bad_aux, d, 64);
+    mn = min(mn, (u32)__shfl_xor(mn, d, 64));
+    mx = max(mx, (u32)__shfl_xor(mx, d, 64));
+  }
+  if (lane == 0) {
+    if (bad) atomicOr(&info->bad, 1u);
+    if (bad_aux) atomicOr(&info->bad_aux, 1u);
+    if (mn != 0xffffffffu) {
+      atomicMin(&info->minute_min, mn);
+      atomicMax(&info->minute_max, mx);
+    }
+  }
+}
+
 struct ClMsg {
   Key key;
-  u32 hash;
-  u32 minute;
   u32 cell;
-  u32 meta;
+  bool ok;  // valid timestamp, cell in range, inside the range
 };
 
-// Raw bytes of one 64-message round, as loaded (not yet redistributed).
 struct ClRaw {
-  uint4 a, b, c;
+  uint4 key;
+  u32 meta;
   u32 cell;
 };
 
-// Issues the loads of the round starting at `first` (no wait).  For stride 48
-// lane l loads 16-B quads l, l+64, l+128 of the round's 3 KiB block (fully
-// coalesced); other strides load the lane's own timestamp.
-__device__ __forceinline__ ClRaw cl_fetch(const uint8_t* __restrict__ ts, size_t stride, const u32* __restrict__ cell,
-                                          size_t first, size_t end) {
-  const int lane = threadIdx.x & 63;
+__device__ __forceinline__ ClRaw cl_fetch(const uint4* __restrict__ key, const u32* __restrict__ meta,
+                                          const u32* __restrict__ cell, size_t first, size_t end) {
+  const size_t i = first + (threadIdx.x & 63);
   ClRaw r;
-  const size_t i = first + lane;
-  r.cell = i < end ? cell[i] : 0xffffffffu;
-  if (stride == 48) {
-    const uint4* src = reinterpret_cast<const uint4*>(ts + first * 48);
-    const size_t nq = first < end ? (end - first) * 3 : 0;
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    r.a = (size_t)lane < nq ? src[lane] : z;
-    r.b = (size_t)lane + 64 < nq ? src[lane + 64] : z;
-    r.c = (size_t)lane + 128 < nq ? src[lane + 128] : z;
+  if (i < end) {
+    r.key = key[i];
+    r.meta = meta[i];
+    r.cell = cell[i];
   } else {
-    u32 w[12];
-    if (i < end) {
-      load_ts(ts, stride, i, w);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 12; ++k) w[k] = 0;
-    }
-    r.a = make_uint4(w[0], w[1], w[2], w[3]);
-    r.b = make_uint4(w[4], w[5], w[6], w[7]);
-    r.c = make_uint4(w[8], w[9], w[10], w[11]);
+    r.key = make_uint4(0, 0, 0, 0);
+    r.meta = 0;
+    r.cell = 0xffffffffu;
   }
   return r;
 }
 
-// Redistributes (stride 48: through the wave's LDS stage) and parses.
-__device__ __forceinline__ ClMsg cl_decode(const ClRaw& r, size_t stride, uint4* __restrict__ stage) {
-  const int lane = threadIdx.x & 63;
-  u32 w[12];
-  if (stride == 48) {
-    stage[lane] = r.a;
-    stage[lane + 64] = r.b;
-    stage[lane + 128] = r.c;
-    __syncthreads();
-    const uint4 a = stage[3 * lane], b = stage[3 * lane + 1], c = stage[3 * lane + 2];
-    __syncthreads();
-    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
-    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-    w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
-  } else {
-    w[0] = r.a.x; w[1] = r.a.y; w[2] = r.a.z; w[3] = r.a.w;
-    w[4] = r.b.x; w[5] = r.b.y; w[6] = r.b.z; w[7] = r.b.w;
-    w[8] = r.c.x; w[9] = r.c.y; w[10] = r.c.z; w[11] = r.c.w & 0xffffu;
-  }
-  const Parsed p = parse_ts46(w);
+__device__ __forceinline__ ClMsg cl_decode(const ClRaw& r, u32 C) {
   ClMsg m;
-  m.key = Key{p.tc, p.node, (p.meta & EVM_META_CASEMASK) | KEY_PRESENT};
-  m.hash = p.hash;
-  m.minute = p.minute;
-  m.meta = p.meta;
+  m.key = Key{(u64)r.key.x | ((u64)r.key.y << 32), (u64)r.key.z | ((u64)r.key.w << 32),
+              (r.meta & EVM_META_CASEMASK) | KEY_PRESENT};
   m.cell = r.cell;
+  m.ok = (r.meta & EVM_META_VALID) && r.cell < C;
   return m;
 }
 
@@ -330,31 +359,14 @@ struct ClState {
   u32* first;
 };
 
-struct ClAcc {
-  u32 bad, bad_aux, mn, mx;
-};
-
 // One round of 64 messages (lane order == batch order).
 template <int PASS>
-__device__ __forceinline__ void cl_round(const ClMsg& m, size_t first, size_t end, u32 C, int cbits, const ClState& S,
-                                         u32* __restrict__ hash_out, uint8_t* __restrict__ flags,
-                                         u64* __restrict__ pairs, ClAcc& A) {
+__device__ __forceinline__ void cl_round(const ClMsg& m, size_t first, int cbits, const ClState& S,
+                                         uint8_t* __restrict__ flags, size_t end) {
   const int lane = threadIdx.x & 63;
   const size_t i = first + lane;
-  const bool live = i < end;
-  const bool valid = (m.meta & EVM_META_VALID) != 0;
-  const bool ok = live && valid && m.cell < C;
-  if (PASS == 1) {
-    A.bad |= (live && !valid) ? 1u : 0u;
-    A.bad_aux |= (live && m.cell >= C) ? 1u : 0u;
-    if (live) hash_out[i] = m.hash;
-    if (ok) {
-      A.mn = min(A.mn, m.minute);
-      A.mx = max(A.mx, m.minute);
-    }
-  }
-  const u64 peers = match_cell(m.cell, ok, cbits);
-  const bool last_peer = ok && (peers >> lane) == 1ull;
+  const u64 peers = match_cell(m.cell, m.ok, cbits);
+  const bool last_peer = m.ok && (peers >> lane) == 1ull;
   u64 rem = peers & lanemask_lt();
   if (PASS == 1) {
     // round max of this lane's cell over peers up to this lane; first index wins ties
@@ -371,7 +383,7 @@ __device__ __forceinline__ void cl_round(const ClMsg& m, size_t first, size_t en
         rem &= rem - 1;
       }
     }
-    if (ok && key_cmp(m.key, acc) > 0) {
+    if (m.ok && key_cmp(m.key, acc) > 0) {
       acc = m.key;
       acc_i = (u32)i;
     }
@@ -385,7 +397,7 @@ __device__ __forceinline__ void cl_round(const ClMsg& m, size_t first, size_t en
       }
     }
   } else {
-    Key acc = ok ? Key{S.tc[m.cell], S.node[m.cell], S.mask[m.cell]} : key_none();
+    Key acc = m.ok ? Key{S.tc[m.cell], S.node[m.cell], S.mask[m.cell]} : key_none();
     while (__any(rem != 0)) {
       const int src = rem ? (int)__builtin_ctzll(rem) : lane;
       const Key kp = shfl_key(m.key, src);
@@ -394,12 +406,11 @@ __device__ __forceinline__ void cl_round(const ClMsg& m, size_t first, size_t en
         rem &= rem - 1;
       }
     }
-    if (live) {
+    if (i < end) {
       // applyMessages.ts:93 / :105 with t = acc
-      const bool ups = ok && key_cmp(acc, m.key) < 0;
-      const bool xr = ok && !((acc.mask & KEY_PRESENT) && key_eq(acc, m.key));
-      flags[i] = ok ? (uint8_t)((ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u)) : (uint8_t)EVM_MSG_BAD;
-      pairs[i] = xr ? ((u64)m.hash << 32 | (u64)m.minute) : ~0ull;
+      const bool ups = m.ok && key_cmp(acc, m.key) < 0;
+      const bool xr = m.ok && !((acc.mask & KEY_PRESENT) && key_eq(acc, m.key));
+      flags[i] = m.ok ? (uint8_t)((ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u)) : (uint8_t)EVM_MSG_BAD;
     }
     if (last_peer) {
       const Key inc = key_max(acc, m.key);
@@ -411,16 +422,14 @@ __device__ __forceinline__ void cl_round(const ClMsg& m, size_t first, size_t en
 }
 
 template <int PASS>
-__global__ __launch_bounds__(64) void k_cl_pass(const uint8_t* __restrict__ ts, size_t stride,
+__global__ __launch_bounds__(64) void k_cl_pass(const uint4* __restrict__ key, const u32* __restrict__ meta,
                                                 const u32* __restrict__ cell, size_t n, u32 C, int cbits,
                                                 size_t range_len, u64* __restrict__ agg_tc, u64* __restrict__ agg_node,
                                                 u32* __restrict__ agg_mask, u32* __restrict__ agg_first,
-                                                u32* __restrict__ hash_out, uint8_t* __restrict__ flags,
-                                                u64* __restrict__ pairs, Info* __restrict__ info) {
+                                                uint8_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint4* stage = reinterpret_cast<uint4*>(smem);  // 3 KiB
   ClState S;
-  S.tc = reinterpret_cast<u64*>(smem + 3072);
+  S.tc = reinterpret_cast<u64*>(smem);
   S.node = S.tc + C;
   S.mask = reinterpret_cast<u32*>(S.node + C);
   S.first = S.mask + C;
@@ -441,22 +450,14 @@ __global__ __launch_bounds__(64) void k_cl_pass(const uint8_t* __restrict__ ts, 
     }
   }
   __syncthreads();
-  ClAcc A{0u, 0u, 0xffffffffu, 0u};
-  // software pipeline: rounds are fetched two ahead of the one being decoded
-  size_t first = beg;
-  ClRaw r0 = cl_fetch(ts, stride, cell, first, end);
-  ClRaw r1 = cl_fetch(ts, stride, cell, first + 64, end);
-  for (; first < end; first += 128) {
-    const ClRaw r2 = cl_fetch(ts, stride, cell, first + 128, end);
-    const ClRaw r3 = cl_fetch(ts, stride, cell, first + 192, end);
-    {
-      const ClMsg m = cl_decode(r0, stride, stage);
-      cl_round<PASS>(m, first, end, C, cbits, S, hash_out, flags, pairs, A);
-    }
-    if (first + 64 < end) {
-      const ClMsg m = cl_decode(r1, stride, stage);
-      cl_round<PASS>(m, first + 64, end, C, cbits, S, hash_out, flags, pairs, A);
-    }
+  // software pipeline: two rounds in flight ahead of the one being combined
+  ClRaw r0 = cl_fetch(key, meta, cell, beg, end);
+  ClRaw r1 = cl_fetch(key, meta, cell, beg + 64, end);
+  for (size_t first = beg; first < end; first += 128) {
+    const ClRaw r2 = cl_fetch(key, meta, cell, first + 128, end);
+    const ClRaw r3 = cl_fetch(key, meta, cell, first + 192, end);
+    cl_round<PASS>(cl_decode(r0, C), first, cbits, S, flags, end);
+    if (first + 64 < end) cl_round<PASS>(cl_decode(r1, C), first + 64, cbits, S, flags, end);
     r0 = r2;
     r1 = r3;
   }
@@ -467,20 +468,6 @@ __global__ __launch_bounds__(64) void k_cl_pass(const uint8_t* __restrict__ ts, 
       agg_node[g * C + c] = S.node[c];
       agg_mask[g * C + c] = S.mask[c];
       agg_first[g * C + c] = S.first[c];
-    }
-    for (int d = 32; d >= 1; d >>= 1) {
-      A.bad |= __shfl_xor(A.bad, d, 64);
-      A.bad_aux |= __shfl_xor(A.bad_aux, d, 64);
-      A.mn = min(A.mn, (u32)__shfl_xor(A.mn, d, 64));
-      A.mx = max(A.mx, (u32)__shfl_xor(A.mx, d, 64));
-    }
-    if (lane == 0) {
-      if (A.bad) atomicOr(&info->bad, 1u);
-      if (A.bad_aux) atomicOr(&info->bad_aux, 1u);
-      if (A.mn != 0xffffffffu) {
-        atomicMin(&info->minute_min, A.mn);
-        atomicMax(&info->minute_max, A.mx);
-      }
     }
   }
 }
@@ -649,7 +636,7 @@ __global__ __launch_bounds__(256) void k_xp_dedup(const u64* __restrict__ pairs,
   const size_t cnt = e - a;
   if (cnt < 2) return;
   if (cnt > XP_MAX_BUCKET) {
-    if (threadIdx.x == 0) atomicOr(&info->fold_overflow, 2u);  // bit 1: bucket too big for LDS
+    if (threadIdx.x == 0) atomicOr(&info->xc_oversize, 1u);
     return;
   }
   u32 slots = 64;
@@ -678,7 +665,9 @@ __global__ __launch_bounds__(256) void k_xp_dedup(const u64* __restrict__ pairs,
 
 // Dense Merkle fold over [minute_min, minute_min + FOLD_MAXWIN * FOLD_WIN):
 // per (window, chunk) an LDS XOR histogram + presence bitmap.
-__global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const u64* __restrict__ pairs, size_t n,
+__global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __restrict__ flags,
+                                                              const u32* __restrict__ minute,
+                                                              const u32* __restrict__ hash, size_t n,
                                                               u32* __restrict__ px, u32* __restrict__ pp,
                                                               Info* __restrict__ info) {
   __shared__ u32 hist[FOLD_WIN];
@@ -696,14 +685,31 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const u64* __rest
   for (u32 b = threadIdx.x; b < FOLD_WIN / 32; b += FOLD_THREADS) pres[b] = 0;
   __syncthreads();
   const u32 base = mlo + w * FOLD_WIN;
-  const size_t per = (n + FOLD_CHUNKS - 1) / FOLD_CHUNKS;
+  const size_t per = ((n + FOLD_CHUNKS - 1) / FOLD_CHUNKS + 3) & ~(size_t)3;
   const size_t a = (size_t)blockIdx.x * per, e = min(n, a + per);
-  for (size_t i = a + threadIdx.x; i < e; i += FOLD_THREADS) {
-    const u64 p = pairs[i];
-    const u32 off = (u32)p - base;
-    if ((u32)p != 0xffffffffu && off < FOLD_WIN) {
-      atomicXor(&hist[off], (u32)(p >> 32));
-      atomicOr(&pres[off >> 5], 1u << (off & 31));
+  // 4 messages per thread per step: one 32-bit load of flags
+  for (size_t i = a + 4 * (size_t)threadIdx.x; i < e; i += 4 * FOLD_THREADS) {
+    if (i + 4 <= e) {
+      const u32 f4 = *reinterpret_cast<const u32*>(flags + i);
+      const uint4 m4 = *reinterpret_cast<const uint4*>(minute + i);
+      const uint4 h4 = *reinterpret_cast<const uint4*>(hash + i);
+      const u32 mm[4] = {m4.x, m4.y, m4.z, m4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u32 off = mm[k] - base;
+        if (((f4 >> (8 * k)) & EVM_MSG_XOR) && off < FOLD_WIN) {
+          atomicXor(&hist[off], hh[k]);
+          atomicOr(&pres[off >> 5], 1u << (off & 31));
+        }
+      }
+    } else {
+      for (size_t k = i; k < e; ++k) {
+        const u32 off = minute[k] - base;
+        if ((flags[k] & EVM_MSG_XOR) && off < FOLD_WIN) {
+          atomicXor(&hist[off], hash[k]);
+          atomicOr(&pres[off >> 5], 1u << (off & 31));
+        }
+      }
     }
   }
   __syncthreads();
@@ -739,24 +745,20 @@ __global__ void k_cl_leaves(const u32* __restrict__ dx, const u32* __restrict__ 
   xr[pos[b]] = (int32_t)dx[b];
 }
 
-// Fallback fold input from the pass-2 pairs (rare: wide minute range).
-__global__ void k_cl_pairs_sel(const u64* __restrict__ pairs, size_t n, u32* __restrict__ sel) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    sel[i] = (u32)pairs[i] != 0xffffffffu;
-}
-__global__ void k_cl_pairs_ck(const u64* __restrict__ pairs, const u32* __restrict__ pos, size_t n, u64* __restrict__ ck,
-                              u32* __restrict__ h, Info* __restrict__ info) {
+// Fallback fold input (rare: wide minute range or mixed key lengths).
+__global__ void k_cl_fold_ck(const uint8_t* __restrict__ flags, const u32* __restrict__ minute,
+                             const u32* __restrict__ hash, const u32* __restrict__ pos, size_t n, u64* __restrict__ ck,
+                             u32* __restrict__ h, Info* __restrict__ info) {
   u64 mn = ~0ull, mx = 0;
   u32 ml = 0;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const u64 p = pairs[i];
-    if ((u32)p == 0xffffffffu) continue;
-    const u64 c = minute_code((u32)p);
+    if (!(flags[i] & EVM_MSG_XOR)) continue;
+    const u64 c = minute_code(minute[i]);
     ck[pos[i]] = c;
-    h[pos[i]] = (u32)(p >> 32);
+    h[pos[i]] = hash[i];
     mn = min(mn, c);
     mx = max(mx, c);
-    ml = max(ml, (u32)base3_len((u32)p));
+    ml = max(ml, (u32)base3_len(minute[i]));
   }
   for (int d = 32; d >= 1; d >>= 1) {
     mn = min(mn, (u64)__shfl_xor(mn, d, 64));
@@ -792,18 +794,23 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   range = std::max<size_t>(2048, (range + 63) / 64 * 64);
   const size_t G = (n + range - 1) / range;
   const int cbits = C > 1 ? 32 - __builtin_clz(C - 1) : 0;
+  uint4* key = S.alloc<uint4>(n);
+  u32* meta = S.alloc<u32>(n);
+  u32* hash = S.alloc<u32>(n);
+  u32* minute = S.alloc<u32>(n);
   u64* a_tc = S.alloc<u64>(G * C);
   u64* a_node = S.alloc<u64>(G * C);
   u32* a_mask = S.alloc<u32>(G * C);
   u32* a_first = S.alloc<u32>(G * C);
-  u32* hash = S.alloc<u32>(n);
-  u64* pairs = S.alloc<u64>(n);
-  if (!a_tc || !a_node || !a_mask || !a_first || !hash || !pairs) return EVM_ENOMEM;
-  const size_t lds = 3072 + (size_t)C * 24;
+  if (!key || !meta || !hash || !minute || !a_tc || !a_node || !a_mask || !a_first) return EVM_ENOMEM;
+  // K1: parse, canonical check, murmur3, minute -- at full occupancy
+  KLAUNCH(k_cl_pack, dim3(std::min<size_t>((n + 255) / 256, 2048)), dim3(CLP_THREADS), (const uint8_t*)ts, stride, n,
+          cell, C, key, meta, hash, minute, info);
+  const size_t lds = (size_t)C * 24;
   {
     evm::ProfScope ps_(ctx, "k_cl_pass<1>");
-    hipLaunchKernelGGL((k_cl_pass<1>), dim3(G), dim3(64), lds, ctx->stream, (const uint8_t*)ts, stride, cell, n, C,
-                       cbits, range, a_tc, a_node, a_mask, a_first, hash, (uint8_t*)nullptr, (u64*)nullptr, info);
+    hipLaunchKernelGGL((k_cl_pass<1>), dim3(G), dim3(64), lds, ctx->stream, key, meta, cell, n, C, cbits, range, a_tc,
+                       a_node, a_mask, a_first, (uint8_t*)nullptr);
   }
   // cross-cell PK check: partition by hash, LDS hash set per bucket
   int kb = 1;
@@ -825,6 +832,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
                        xpairs);
   }
   KLAUNCH(k_xp_dedup, dim3(1u << kb), dim3(256), xpairs, xoff, xt, kb, n, (const uint8_t*)ts, stride, cell, info);
+  // carry: per cell, exclusive scan over ranges seeded with the prior max
   {
     u64* s_tc = S.alloc<u64>((size_t)CARRY_SEGS * C);
     u64* s_node = S.alloc<u64>((size_t)CARRY_SEGS * C);
@@ -840,8 +848,8 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   }
   {
     evm::ProfScope ps_(ctx, "k_cl_pass<2>");
-    hipLaunchKernelGGL((k_cl_pass<2>), dim3(G), dim3(64), lds, ctx->stream, (const uint8_t*)ts, stride, cell, n, C,
-                       cbits, range, a_tc, a_node, a_mask, a_first, (u32*)nullptr, flags, pairs, info);
+    hipLaunchKernelGGL((k_cl_pass<2>), dim3(G), dim3(64), lds, ctx->stream, key, meta, cell, n, C, cbits, range, a_tc,
+                       a_node, a_mask, a_first, flags);
   }
   // Merkle fold
   u32* px = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN);
@@ -853,7 +861,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   u64* lck = S.alloc<u64>(B);
   int32_t* lxr = S.alloc<int32_t>(B);
   if (!px || !pp || !dx || !dp || !pos || !lck || !lxr) return EVM_ENOMEM;
-  KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), pairs, n, px, pp, info);
+  KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
   KLAUNCH(k_cl_fold_reduce, dim3((B + 255) / 256), dim3(256), px, pp, info, dx, dp);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, dp, B, pos, &info->n_leaves))) return st;
   KLAUNCH(k_cl_leaves, dim3((B + 255) / 256), dim3(256), dx, dp, pos, info, lck, lxr);
@@ -864,7 +872,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
     return EVM_ENONCANON;
   }
   if (hi.bad_aux) return EVM_EINVAL;
-  if (!hi.collision && (hi.fold_overflow & 2u)) {
+  if (!hi.collision && hi.xc_oversize) {
     // a hash bucket overflowed LDS (heavy skew): exact check on the global epoch-tagged set
     const int lg = std::max(ceil_log2(n + n / 2 + 1), 10);
     if (!ctx->xtab || ctx->xtab_lg < lg) {
@@ -884,7 +892,6 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
     if ((st = read_info(ctx, info, &hi))) return st;
   }
   if (hi.collision) return EVM_ECOLLISION;
-  hi.fold_overflow &= 1u;
   if (!hi.fold_overflow) return merge_into_tree(ctx, S, tree_in, tree_in->n_owners, lck, lxr, hi.n_leaves, tree_out);
   // wide minute range or mixed key lengths: sort-based fold
   u32* sel = S.alloc<u32>(n);
@@ -893,9 +900,9 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   u64* ck = S.alloc<u64>(n);
   u32* h = S.alloc<u32>(n);
   if (!sel || !spos || !cnt || !ck || !h) return EVM_ENOMEM;
-  KLAUNCH(k_cl_pairs_sel, dim3(grid_for(n, 256)), dim3(256), pairs, n, sel);
+  if ((st = launch_sel(ctx, flags, (uint8_t)EVM_MSG_XOR, n, sel))) return st;
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, spos, cnt))) return st;
-  KLAUNCH(k_cl_pairs_ck, dim3(grid_for(n, 256, 4096)), dim3(256), pairs, spos, n, ck, h, info);
+  KLAUNCH(k_cl_fold_ck, dim3(grid_for(n, 256, 4096)), dim3(256), flags, minute, hash, spos, n, ck, h, info);
   u32 m = 0;
   HIPR(hipMemcpyAsync(&m, cnt, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
   if ((st = read_info(ctx, info, &hi))) return st;

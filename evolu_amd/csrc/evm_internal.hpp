@@ -59,6 +59,8 @@ struct Info {
   u32 bad_aux; // an aux id out of range
   u32 fold_overflow;  // dense minute fold not applicable (range too wide / mixed key lengths)
   u32 n_leaves;       // leaves produced by the dense fold
+  u32 xc_oversize;    // a hash bucket of the cross-cell check overflowed LDS
+  u32 pad_;
 };
 
 inline Info info_init() {
@@ -73,6 +75,8 @@ inline Info info_init() {
   h.bad_aux = 0;
   h.fold_overflow = 0;
   h.n_leaves = 0;
+  h.xc_oversize = 0;
+  h.pad_ = 0;
   return h;
 }
 
