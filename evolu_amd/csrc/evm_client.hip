@@ -236,6 +236,35 @@ constexpr int FOLD_THREADS = 1024;
 // loads and redistributes them through LDS.
 constexpr int CLP_THREADS = 256;
 
+__device__ __forceinline__ void clp_fetch(const uint8_t* __restrict__ ts, size_t stride, size_t n, size_t first,
+                                          uint4& a, uint4& b, uint4& c) {
+  const int lane = threadIdx.x & 63;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  if (first >= n) {
+    a = b = c = z;
+    return;
+  }
+  if (stride == 48) {
+    const uint4* src = reinterpret_cast<const uint4*>(ts + first * 48);
+    const size_t nq = (min(n, first + 64) - first) * 3;
+    a = (size_t)lane < nq ? src[lane] : z;
+    b = (size_t)lane + 64 < nq ? src[lane + 64] : z;
+    c = (size_t)lane + 128 < nq ? src[lane + 128] : z;
+  } else {
+    u32 w[12];
+    const size_t i = first + lane;
+    if (i < n) {
+      load_ts(ts, stride, i, w);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) w[k] = 0;
+    }
+    a = make_uint4(w[0], w[1], w[2], w[3]);
+    b = make_uint4(w[4], w[5], w[6], w[7]);
+    c = make_uint4(w[8], w[9], w[10], w[11]);
+  }
+}
+
 __global__ __launch_bounds__(CLP_THREADS) void k_cl_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
                                                          const u32* __restrict__ cell, u32 C, uint4* __restrict__ key,
                                                          u32* __restrict__ meta, u32* __restrict__ hash,
@@ -243,27 +272,31 @@ __global__ __launch_bounds__(CLP_THREADS) void k_cl_pack(const uint8_t* __restri
   __shared__ uint4 stage[CLP_THREADS / 64][192];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   u32 bad = 0, bad_aux = 0, mn = 0xffffffffu, mx = 0;
-  const size_t nwaves = (size_t)gridDim.x * (CLP_THREADS / 64);
-  for (size_t first = ((size_t)blockIdx.x * (CLP_THREADS / 64) + wv) * 64; first < n; first += nwaves * 64) {
+  const size_t step = (size_t)gridDim.x * CLP_THREADS;
+  size_t first = ((size_t)blockIdx.x * (CLP_THREADS / 64) + wv) * 64;
+  uint4 a, b, c;
+  clp_fetch(ts, stride, n, first, a, b, c);
+  for (; first < n; first += step) {
+    uint4 na, nb, nc;  // next round in flight while this one is parsed
+    clp_fetch(ts, stride, n, first + step, na, nb, nc);
     const size_t i = first + lane;
     u32 w[12];
     if (stride == 48) {
-      const uint4* src = reinterpret_cast<const uint4*>(ts + first * 48);
-      const size_t nq = (min(n, first + 64) - first) * 3;
-      const uint4 z = make_uint4(0, 0, 0, 0);
-      stage[wv][lane] = (size_t)lane < nq ? src[lane] : z;
-      stage[wv][lane + 64] = (size_t)lane + 64 < nq ? src[lane + 64] : z;
-      stage[wv][lane + 128] = (size_t)lane + 128 < nq ? src[lane + 128] : z;
+      stage[wv][lane] = a;
+      stage[wv][lane + 64] = b;
+      stage[wv][lane + 128] = c;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      const uint4 a = stage[wv][3 * lane], b = stage[wv][3 * lane + 1], c = stage[wv][3 * lane + 2];
+      const uint4 x = stage[wv][3 * lane], y = stage[wv][3 * lane + 1], z = stage[wv][3 * lane + 2];
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+      w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+      w[8] = z.x; w[9] = z.y; w[10] = z.z; w[11] = z.w & 0xffffu;
+    } else {
       w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
       w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
       w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
-    } else if (i < n) {
-      load_ts(ts, stride, i, w);
     }
     if (i < n) {
       const Parsed p = parse_ts46(w);
@@ -279,6 +312,9 @@ __global__ __launch_bounds__(CLP_THREADS) void k_cl_pack(const uint8_t* __restri
         mx = max(mx, p.minute);
       }
     }
+    a = na;
+    b = nb;
+    c = nc;
   }
   for (int d = 32; d >= 1; d >>= 1) {
     bad |= __shfl_xor(bad, d, 64);
@@ -590,8 +626,8 @@ __global__ void k_cl_xcell(const uint8_t* __restrict__ ts, size_t stride, const 
 constexpr int XP_THREADS = 1024;
 constexpr int XP_ITEMS = 32;
 constexpr int XP_TILE = XP_THREADS * XP_ITEMS;
-constexpr u32 XP_MAX_BUCKET = 8192;  // entries a bucket may hold for the LDS set
-constexpr u32 XP_SLOTS = 16384;      // LDS set slots, 128 KiB
+constexpr u32 XP_MAX_BUCKET = 6144;  // entries a bucket may hold for the LDS set
+constexpr u32 XP_SLOTS = 8192;       // LDS set slots, 64 KiB (two workgroups per CU)
 
 __global__ __launch_bounds__(XP_THREADS) void k_xp_hist(const u32* __restrict__ hash, size_t n, int kb,
                                                        u32* __restrict__ counts, u32 ntiles) {
@@ -629,7 +665,7 @@ __global__ __launch_bounds__(XP_THREADS) void k_xp_scatter(const u32* __restrict
 __global__ __launch_bounds__(256) void k_xp_dedup(const u64* __restrict__ pairs, const u32* __restrict__ offs, u32 ntiles,
                                                   int kb, size_t n, const uint8_t* __restrict__ ts, size_t stride,
                                                   const u32* __restrict__ cell, Info* __restrict__ info) {
-  __shared__ u64 tab[XP_SLOTS];  // hash:32 | (index + 1):32, 0 = empty
+  extern __shared__ u64 tab[];  // XP_SLOTS x (hash:32 | (index + 1):32), 0 = empty
   const u32 b = blockIdx.x, B = 1u << kb;
   const size_t a = offs[(size_t)b * ntiles];
   const size_t e = (b + 1 < B) ? offs[(size_t)(b + 1) * ntiles] : n;
@@ -813,8 +849,8 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
                        a_node, a_mask, a_first, (uint8_t*)nullptr);
   }
   // cross-cell PK check: partition by hash, LDS hash set per bucket
-  int kb = 1;
-  while (kb < 14 && ((size_t)2048 << kb) < n) ++kb;
+  int kb = 1;  // ~5k messages per bucket
+  while (kb < 14 && ((size_t)5000 << kb) < n) ++kb;
   const u32 xt = (u32)((n + XP_TILE - 1) / XP_TILE);
   const size_t nbt = ((size_t)1 << kb) * xt;
   u32* xcnt = S.alloc<u32>(nbt);
@@ -831,7 +867,11 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
     hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), sizeof(u32) << kb, ctx->stream, hash, n, kb, xoff, xt,
                        xpairs);
   }
-  KLAUNCH(k_xp_dedup, dim3(1u << kb), dim3(256), xpairs, xoff, xt, kb, n, (const uint8_t*)ts, stride, cell, info);
+  {
+    evm::ProfScope ps_(ctx, "k_xp_dedup");
+    hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(256), sizeof(u64) * XP_SLOTS, ctx->stream, xpairs, xoff, xt, kb,
+                       n, (const uint8_t*)ts, stride, cell, info);
+  }
   // carry: per cell, exclusive scan over ranges seeded with the prior max
   {
     u64* s_tc = S.alloc<u64>((size_t)CARRY_SEGS * C);
