@@ -71,6 +71,13 @@ SIGNATURES = {
     "evm_tree_from_json": (_i, [_vp, _u32, C.POINTER(C.c_char_p), C.POINTER(_sz), C.POINTER(_vp)]),
     "evm_merkle_insert": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, C.POINTER(_vp)]),
     "evm_merkle_diff": (_i, [_vp, _vp, _vp, _vp]),
+    "evm_store_new": (_i, [_vp, _u32, C.POINTER(_vp)]),
+    "evm_store_free": (_i, [_vp, _vp]),
+    "evm_store_info": (_i, [_vp, C.POINTER(_u32), C.POINTER(C.c_uint64)]),
+    "evm_store_tree": (_vp, [_vp]),
+    "evm_store_messages": (_i, [_vp, _vp, _vp, _vp]),
+    "evm_server_ingest": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, C.c_uint64, _vp]),
+    "evm_server_select": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_apply_batch": (
         _i,
         [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _vp, C.POINTER(_vp)],

@@ -644,6 +644,12 @@ int evm_tree_free(evm_ctx* ctx, evm_tree* t) {
   return EVM_OK;
 }
 
+}  // extern "C"
+
+void evm::tree_destroy(evm_ctx* ctx, evm_tree* t) { tree_release(ctx, t); }
+
+extern "C" {
+
 int evm_tree_info(const evm_tree* t, uint32_t* n_owners, uint64_t* n_leaves) {
   if (!t) return EVM_EINVAL;
   if (n_owners) *n_owners = t->n_owners;
@@ -715,12 +721,19 @@ int evm_merkle_insert(evm_ctx* ctx, const evm_tree* in, const char* ts, size_t s
 
 int evm_merkle_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* millis) {
   if (!ctx || !a || !b || !millis || a->n_owners != b->n_owners) return EVM_EINVAL;
+  int st = launch_diff(ctx, a, b, millis);
+  return st ? st : evm_sync(ctx);
+}
+
+}  // extern "C"
+
+int evm::launch_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* millis) {
   if (a->n_owners == 0) return EVM_OK;
   TreeView A{a->off, a->ck, a->pfx}, B{b->off, b->ck, b->pfx};
-  KLAUNCH(k_diff, dim3(grid_for(a->n_owners, 64, 1 << 16)), dim3(64), A, B, a->n_owners,
-                     millis);
-  HIPR(hipGetLastError());
-  return evm_sync(ctx);
+  KLAUNCH(k_diff, dim3(grid_for(a->n_owners, 64, 1 << 16)), dim3(64), A, B, a->n_owners, millis);
+  return hip_ok(hipGetLastError());
 }
+
+extern "C" {
 
 }  // extern "C"

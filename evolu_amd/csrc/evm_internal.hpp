@@ -198,7 +198,8 @@ int launch_iota(evm_ctx* ctx, u32* v, size_t n);
 int launch_sel(evm_ctx* ctx, const uint8_t* flags, uint8_t mask, size_t n, u32* sel);
 int launch_fold_prep(evm_ctx* ctx, const evm_rec* rec, const uint8_t* flags, uint8_t sel_mask, const u32* pos,
                      int owner_mode, const u32* cell_owner, size_t n, u64* ck, u32* h, Info* info);
-int tree_from_device(evm_ctx* ctx, const evm_tree* src, evm_tree** out);  // copy of a tree set
+int launch_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* millis);
+void tree_destroy(evm_ctx* ctx, evm_tree* t);  // stream-ordered release
 
 int launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,
                 Info* info);

@@ -1,0 +1,547 @@
+// Sync server hot path (apps/server/src/index.ts) on MI355X.
+//
+//   addMessages (index.ts:138-171): per message, INSERT OR IGNORE into
+//     message(timestamp, userId) -- PRIMARY KEY(timestamp, userId) -- and
+//     XOR into the owner's tree iff the row was inserted (changes === 1).
+//   getMessages (index.ts:173-202): diff the owner's tree with the client's;
+//     on Some(d) select the owner's rows with timestamp > ISO(d)-0000-0000..0
+//     and timestamp NOT LIKE '%' || nodeId, ORDER BY timestamp.
+//
+// Store layout (device, sorted by (owner, timestamp string order)):
+//   owner u32 | tc u64 = millis << 16 | counter | rk_hi u64, rk_lo u32 = the
+//   node's 16 chars as 5-bit ASCII-order ranks (chars 0-11 / 12-15) | id u64.
+// (tc, rk_hi, rk_lo) is injective and ordered exactly like the strings.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "evm_device.hpp"
+#include "evm_internal.hpp"
+#include "evm_prims.hpp"
+
+using namespace evm;
+
+struct evm_store {
+  uint32_t n_owners;
+  uint64_t n;
+  unsigned long long* off;  // [n_owners + 1]
+  u32* owner;               // [n]
+  unsigned long long* tc;   // [n]
+  unsigned long long* hi;   // [n]
+  u32* lo;                  // [n]
+  unsigned long long* id;   // [n]
+  evm_tree* tree;
+};
+
+namespace {
+
+struct SKey {
+  u32 owner;
+  u64 tc;
+  u64 hi;
+  u32 lo;
+};
+
+__device__ __forceinline__ int skey_cmp(const SKey& a, const SKey& b) {
+  if (a.owner != b.owner) return a.owner < b.owner ? -1 : 1;
+  if (a.tc != b.tc) return a.tc < b.tc ? -1 : 1;
+  if (a.hi != b.hi) return a.hi < b.hi ? -1 : 1;
+  if (a.lo != b.lo) return a.lo < b.lo ? -1 : 1;
+  return 0;
+}
+
+// node (hex value, case mask) -> 5-bit ranks, chars 0..11 in hi, 12..15 in lo
+__device__ __forceinline__ void node_ranks(u64 node, u32 mask, u64* hi, u32* lo) {
+  u64 h = 0;
+  u32 l = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const u32 v = (u32)(node >> (60 - 4 * i)) & 15u;
+    const u32 r = node_char_rank(v, (mask >> i) & 1u);
+    if (i < 12) h = (h << 5) | r;
+    else l = (l << 5) | r;
+  }
+  *hi = h;
+  *lo = l;
+}
+
+__device__ __forceinline__ SKey skey_of(const evm_rec& r) {
+  SKey k;
+  k.owner = r.aux;
+  k.tc = r.tc;
+  node_ranks(r.node, r.meta & EVM_META_CASEMASK, &k.hi, &k.lo);
+  return k;
+}
+
+struct StoreView {
+  const u64* off;
+  const u32* owner;
+  const u64* tc;
+  const u64* hi;
+  const u32* lo;
+};
+
+__device__ __forceinline__ SKey skey_at(const StoreView& s, size_t k) { return SKey{s.owner[k], s.tc[k], s.hi[k], s.lo[k]}; }
+
+// first k in [a, b) with s[k] >= x
+__device__ __forceinline__ size_t store_lower(const StoreView& s, size_t a, size_t b, const SKey& x) {
+  while (a < b) {
+    const size_t m = (a + b) >> 1;
+    if (skey_cmp(skey_at(s, m), x) < 0) a = m + 1;
+    else b = m;
+  }
+  return a;
+}
+
+// ---------------------------------------------------------------- sort fields
+enum Field { F_LO = 0, F_HI = 1, F_TC = 2, F_OWNER = 3 };
+
+__global__ void k_sv_field(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, size_t n, int field,
+                           u64* __restrict__ out) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    const SKey k = skey_of(rec[perm[p]]);
+    out[p] = field == F_LO ? (u64)k.lo : field == F_HI ? k.hi : field == F_TC ? k.tc : (u64)k.owner;
+  }
+}
+
+// min / max of every field over the batch (decides the radix bits per field)
+struct FieldRange {
+  u64 mn[4];
+  u64 mx[4];
+};
+
+__global__ void k_sv_ranges(const evm_rec* __restrict__ rec, size_t n, FieldRange* __restrict__ fr) {
+  u64 mn[4] = {~0ull, ~0ull, ~0ull, ~0ull}, mx[4] = {0, 0, 0, 0};
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const SKey k = skey_of(rec[i]);
+    const u64 v[4] = {(u64)k.lo, k.hi, k.tc, (u64)k.owner};
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      mn[f] = min(mn[f], v[f]);
+      mx[f] = max(mx[f], v[f]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    for (int d = 32; d >= 1; d >>= 1) {
+      mn[f] = min(mn[f], (u64)__shfl_xor(mn[f], d, 64));
+      mx[f] = max(mx[f], (u64)__shfl_xor(mx[f], d, 64));
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      atomicMin(&fr->mn[f], mn[f]);
+      atomicMax(&fr->mx[f], mx[f]);
+    }
+  }
+}
+
+// ------------------------------------------------------------ dedup + marks
+// Sorted order p: first occurrence of (owner, timestamp) in batch order (the
+// sort is stable on the batch index) that the store does not hold yet.
+__global__ void k_sv_mark(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, size_t n, StoreView st,
+                          uint8_t* __restrict__ flags, u32* __restrict__ sel) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    const u32 i = perm[p];
+    const SKey k = skey_of(rec[i]);
+    bool first = true;
+    if (p > 0) first = skey_cmp(skey_of(rec[perm[p - 1]]), k) != 0;
+    bool ins = first;
+    if (ins) {
+      const size_t a = st.off[k.owner], b = st.off[k.owner + 1];
+      const size_t q = store_lower(st, a, b, k);
+      ins = !(q < b && skey_cmp(skey_at(st, q), k) == 0);
+    }
+    flags[i] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
+    sel[p] = ins ? 1u : 0u;
+  }
+}
+
+__global__ void k_sv_compact(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u32* __restrict__ sel,
+                             const u32* __restrict__ pos, size_t n, u64 id_base, u32* __restrict__ o_owner,
+                             u64* __restrict__ o_tc, u64* __restrict__ o_hi, u32* __restrict__ o_lo,
+                             u64* __restrict__ o_id, u64* __restrict__ l_ck, u32* __restrict__ l_h) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    if (!sel[p]) continue;
+    const u32 i = perm[p];
+    const evm_rec r = rec[i];
+    const SKey k = skey_of(r);
+    const u32 q = pos[p];
+    o_owner[q] = k.owner;
+    o_tc[q] = k.tc;
+    o_hi[q] = k.hi;
+    o_lo[q] = k.lo;
+    o_id[q] = id_base + i;
+    // leaves come out sorted by (owner, minute); the codes follow that order
+    // when the owner's key lengths agree (k_sv_sorted_check tells)
+    l_ck[q] = ((u64)k.owner << 40) | minute_code(r.minute);
+    l_h[q] = r.hash;
+  }
+}
+
+__global__ void k_sv_bad(const evm_rec* __restrict__ rec, size_t n, uint8_t* __restrict__ flags) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    flags[i] = (rec[i].meta & EVM_META_VALID) ? 0u : EVM_MSG_BAD;
+}
+
+__global__ void k_sv_sorted_check(const u64* __restrict__ ck, size_t m, u32* __restrict__ unsorted) {
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x + 1; q < m; q += (size_t)gridDim.x * blockDim.x)
+    if (ck[q] < ck[q - 1]) *unsorted = 1u;
+}
+
+// ------------------------------------------------------------------ merge
+struct StoreOut {
+  u32* owner;
+  u64* tc;
+  u64* hi;
+  u32* lo;
+  u64* id;
+};
+
+__global__ void k_sv_merge_old(StoreView a, const u64* __restrict__ a_id, size_t na, StoreView b, size_t nb,
+                               StoreOut o) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += (size_t)gridDim.x * blockDim.x) {
+    const SKey k = skey_at(a, i);
+    const size_t j = store_lower(b, 0, nb, k);
+    const size_t q = i + j;
+    o.owner[q] = k.owner;
+    o.tc[q] = k.tc;
+    o.hi[q] = k.hi;
+    o.lo[q] = k.lo;
+    o.id[q] = a_id[i];
+  }
+}
+
+__global__ void k_sv_merge_new(StoreView b, const u64* __restrict__ b_id, size_t nb, StoreView a, size_t na,
+                               StoreOut o) {
+  for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += (size_t)gridDim.x * blockDim.x) {
+    const SKey k = skey_at(b, j);
+    const size_t i = store_lower(a, 0, na, k);  // keys are disjoint
+    const size_t q = i + j;
+    o.owner[q] = k.owner;
+    o.tc[q] = k.tc;
+    o.hi[q] = k.hi;
+    o.lo[q] = k.lo;
+    o.id[q] = b_id[j];
+  }
+}
+
+__global__ void k_sv_owner_off(const u32* __restrict__ owner, size_t n, u32 n_owners, u64* __restrict__ off) {
+  for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o <= n_owners; o += (size_t)gridDim.x * blockDim.x) {
+    size_t a = 0, b = n;
+    while (a < b) {
+      const size_t m = (a + b) >> 1;
+      if (owner[m] < (u32)o) a = m + 1;
+      else b = m;
+    }
+    off[o] = a;
+  }
+}
+
+// ------------------------------------------------------------------ select
+// rank -> hex value (case folded)
+__device__ __forceinline__ u32 rank_hex(u32 r) { return r >= 16u ? r - 6u : r; }
+
+__device__ __forceinline__ u64 node_hex_of(u64 hi, u32 lo) {
+  u64 v = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) v = (v << 4) | rank_hex((u32)(hi >> (55 - 5 * i)) & 31u);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v = (v << 4) | rank_hex((lo >> (15 - 5 * i)) & 31u);
+  return v;
+}
+
+// the requester's nodeId: 16 hex chars, either case -> folded value (or -1)
+__device__ __forceinline__ bool parse_node16(const uint8_t* s, u64* v) {
+  u64 x = 0;
+  for (int i = 0; i < 16; ++i) {
+    const u32 c = s[i];
+    u32 d;
+    if (c - 0x30u < 10u) d = c - 0x30u;
+    else if (c - 0x41u < 6u) d = c - 0x37u;
+    else if (c - 0x61u < 6u) d = c - 0x57u;
+    else return false;
+    x = (x << 4) | d;
+  }
+  *v = x;
+  return true;
+}
+
+__global__ void k_sv_sel_count(StoreView st, u32 n_owners, const int64_t* __restrict__ diff,
+                               const uint8_t* __restrict__ node, const uint8_t* __restrict__ active,
+                               u64* __restrict__ first, u32* __restrict__ cnt, u32* __restrict__ bad) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
+    cnt[o] = 0;
+    first[o] = 0;
+    if (active && !active[o]) continue;
+    const int64_t d = diff[o];
+    if (d < 0) continue;  // none or RangeError
+    u64 req;
+    if (!parse_node16(node + 16 * (size_t)o, &req)) {
+      atomicOr(bad, 1u);
+      continue;
+    }
+    const size_t a = st.off[o], b = st.off[o + 1];
+    // timestamp > "ISO(d)-0000-0000000000000000": smallest key with tc = d << 16
+    const SKey since{o, (u64)d << 16, 0ull, 0u};
+    size_t q = store_lower(st, a, b, since);
+    if (q < b && skey_cmp(skey_at(st, q), since) == 0) ++q;  // strictly greater
+    first[o] = q;
+    u32 c = 0;
+    for (size_t k = q; k < b; ++k) c += node_hex_of(st.hi[k], st.lo[k]) != req;  // NOT LIKE '%' || nodeId
+    cnt[o] = c;
+  }
+}
+
+__global__ void k_sv_sel_write(StoreView st, const u64* __restrict__ id, u32 n_owners, const u64* __restrict__ first,
+                               const u32* __restrict__ cnt, const u32* __restrict__ pos, const uint8_t* __restrict__ node,
+                               u64* __restrict__ sel_id) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
+    if (!cnt[o]) continue;
+    u64 req;
+    parse_node16(node + 16 * (size_t)o, &req);
+    u64 w = pos[o];
+    for (size_t k = first[o], b = st.off[o + 1]; k < b; ++k)
+      if (node_hex_of(st.hi[k], st.lo[k]) != req) sel_id[w++] = id[k];
+  }
+}
+
+__global__ void k_u32_to_u64(const u32* __restrict__ a, size_t n, const u32* __restrict__ total, u64* __restrict__ out) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = i < n ? (u64)a[i] : (u64)*total;
+}
+
+StoreView view_of(const evm_store* s) { return StoreView{s->off, s->owner, s->tc, s->hi, s->lo}; }
+
+int store_alloc(evm_ctx* ctx, evm_store* s, u32 n_owners, uint64_t n) {
+  s->n_owners = n_owners;
+  s->n = n;
+  const size_t m = std::max<uint64_t>(n, 1);
+  HIPR(hipMallocAsync((void**)&s->off, sizeof(u64) * (n_owners + 1), ctx->stream));
+  HIPR(hipMallocAsync((void**)&s->owner, sizeof(u32) * m, ctx->stream));
+  HIPR(hipMallocAsync((void**)&s->tc, sizeof(u64) * m, ctx->stream));
+  HIPR(hipMallocAsync((void**)&s->hi, sizeof(u64) * m, ctx->stream));
+  HIPR(hipMallocAsync((void**)&s->lo, sizeof(u32) * m, ctx->stream));
+  HIPR(hipMallocAsync((void**)&s->id, sizeof(u64) * m, ctx->stream));
+  return EVM_OK;
+}
+
+void store_release_arrays(evm_ctx* ctx, evm_store* s) {
+  void* ps[] = {s->off, s->owner, s->tc, s->hi, s->lo, s->id};
+  for (void* p : ps)
+    if (p) (void)hipFreeAsync(p, ctx->stream);
+  s->off = nullptr;
+  s->owner = nullptr;
+  s->tc = s->hi = s->id = nullptr;
+  s->lo = nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int evm_store_new(evm_ctx* ctx, uint32_t n_owners, evm_store** out) {
+  if (!ctx || !out) return EVM_EINVAL;
+  evm_store* s = new evm_store();
+  int st = store_alloc(ctx, s, n_owners, 0);
+  if (!st) st = hip_ok(hipMemsetAsync(s->off, 0, sizeof(u64) * (n_owners + 1), ctx->stream));
+  if (!st) st = evm_tree_new(ctx, n_owners, &s->tree);
+  if (st) {
+    store_release_arrays(ctx, s);
+    delete s;
+    return st;
+  }
+  *out = s;
+  return evm_sync(ctx);
+}
+
+int evm_store_free(evm_ctx* ctx, evm_store* s) {
+  if (!ctx) return EVM_EINVAL;
+  if (!s) return EVM_OK;
+  store_release_arrays(ctx, s);
+  if (s->tree) tree_destroy(ctx, s->tree);
+  delete s;
+  return EVM_OK;
+}
+
+int evm_store_info(const evm_store* s, uint32_t* n_owners, uint64_t* n_messages) {
+  if (!s) return EVM_EINVAL;
+  if (n_owners) *n_owners = s->n_owners;
+  if (n_messages) *n_messages = s->n;
+  return EVM_OK;
+}
+
+const evm_tree* evm_store_tree(const evm_store* s) { return s ? s->tree : nullptr; }
+
+int evm_store_messages(evm_ctx* ctx, const evm_store* s, uint64_t* owner_off, uint64_t* id) {
+  if (!ctx || !s) return EVM_EINVAL;
+  if (owner_off)
+    HIPR(hipMemcpyAsync(owner_off, s->off, sizeof(u64) * (s->n_owners + 1), hipMemcpyDeviceToHost, ctx->stream));
+  if (id && s->n) HIPR(hipMemcpyAsync(id, s->id, sizeof(u64) * s->n, hipMemcpyDeviceToHost, ctx->stream));
+  return evm_sync(ctx);
+}
+
+int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                      uint64_t id_base, uint8_t* flags) {
+  if (!ctx || !s || stride < 46 || (n && (!ts || !owner || !flags))) return EVM_EINVAL;
+  if (n == 0) return EVM_OK;  // index.ts:145 `if (req.messages.length === 0) return merkleTree`
+  if (n >= 0xffffffffull) return EVM_EINVAL;
+  int st;
+  evm_store ns{};
+  evm_tree* new_tree = nullptr;
+  {
+    Scratch S(ctx);
+    Info* info = nullptr;
+    if ((st = new_info(ctx, S, &info))) return st;
+    evm_rec* rec = S.alloc<evm_rec>(n);
+    u32* perm = S.alloc<u32>(n);
+    u64* fv = S.alloc<u64>(n);
+    FieldRange* fr = S.alloc<FieldRange>(1);
+    if (!rec || !perm || !fv || !fr) return EVM_ENOMEM;
+    if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) return st;
+    FieldRange h0;
+    for (int f = 0; f < 4; ++f) {
+      h0.mn[f] = ~0ull;
+      h0.mx[f] = 0;
+    }
+    HIPR(hipMemcpyAsync(fr, &h0, sizeof(h0), hipMemcpyHostToDevice, ctx->stream));
+    KLAUNCH(k_sv_ranges, dim3(grid_for(n, 256, 2048)), dim3(256), rec, n, fr);
+    Info hi;
+    FieldRange hr;
+    HIPR(hipMemcpyAsync(&hr, fr, sizeof(hr), hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = read_info(ctx, info, &hi))) return st;
+    if (hi.bad_aux) return EVM_EINVAL;
+    if (hi.bad) {
+      // a timestamp the engine cannot canonicalise (toISOString would differ
+      // or throw): flag the culprits, apply nothing -- the host falls back
+      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
+      (void)evm_sync(ctx);
+      return EVM_ENONCANON;
+    }
+    // stable LSD sort of the batch index by (owner, tc, rank_hi, rank_lo)
+    if ((st = launch_iota(ctx, perm, n))) return st;
+    const int order[4] = {F_LO, F_HI, F_TC, F_OWNER};
+    for (int f : order) {
+      const u64 d = hr.mn[f] ^ hr.mx[f];
+      if (!d) continue;
+      const int hb = 64 - __builtin_clzll(d);
+      KLAUNCH(k_sv_field, dim3(grid_for(n, 256)), dim3(256), rec, perm, n, f, fv);
+      u64* kk = fv;
+      u32* vv = perm;
+      if ((st = radix_sort_pairs<u64>(ctx, S, kk, vv, n, 0, hb))) return st;
+      if (vv != perm) HIPR(hipMemcpyAsync(perm, vv, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    // dedup within the batch and against the store
+    u32* sel = S.alloc<u32>(n);
+    u32* pos = S.alloc<u32>(n);
+    u32* cnt = S.alloc<u32>(2);
+    if (!sel || !pos || !cnt) return EVM_ENOMEM;
+    const StoreView old = view_of(s);
+    KLAUNCH(k_sv_mark, dim3(grid_for(n, 256)), dim3(256), rec, perm, n, old, flags, sel);
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, pos, cnt))) return st;
+    u32 m = 0;
+    HIPR(hipMemcpyAsync(&m, cnt, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    // inserted rows (sorted), and their leaves
+    u32* n_owner = S.alloc<u32>(m);
+    u64* n_tc = S.alloc<u64>(m);
+    u64* n_hi = S.alloc<u64>(m);
+    u32* n_lo = S.alloc<u32>(m);
+    u64* n_id = S.alloc<u64>(m);
+    u64* l_ck = S.alloc<u64>(m);
+    u32* l_h = S.alloc<u32>(m);
+    if (!n_owner || !n_tc || !n_hi || !n_lo || !n_id || !l_ck || !l_h) return EVM_ENOMEM;
+    HIPR(hipMemsetAsync(cnt + 1, 0, sizeof(u32), ctx->stream));
+    KLAUNCH(k_sv_compact, dim3(grid_for(n, 256)), dim3(256), rec, perm, sel, pos, n, (u64)id_base, n_owner, n_tc, n_hi,
+            n_lo, n_id, l_ck, l_h);
+    if (m > 1) KLAUNCH(k_sv_sorted_check, dim3(grid_for(m, 256)), dim3(256), l_ck, (size_t)m, cnt + 1);
+    // merged store
+    if ((st = store_alloc(ctx, &ns, s->n_owners, s->n + m))) return st;
+    const StoreView nv{nullptr, n_owner, n_tc, n_hi, n_lo};
+    const StoreOut so{ns.owner, ns.tc, ns.hi, ns.lo, ns.id};
+    if (s->n)
+      KLAUNCH(k_sv_merge_old, dim3(grid_for(s->n, 256)), dim3(256), old, (const u64*)s->id, (size_t)s->n, nv, (size_t)m,
+              so);
+    if (m)
+      KLAUNCH(k_sv_merge_new, dim3(grid_for(m, 256)), dim3(256), nv, (const u64*)n_id, (size_t)m, old, (size_t)s->n,
+              so);
+    KLAUNCH(k_sv_owner_off, dim3(grid_for(s->n_owners + 1, 256)), dim3(256), ns.owner, (size_t)ns.n, s->n_owners,
+            ns.off);
+    // Merkle: XOR of the inserted rows into their owners' trees
+    u32 unsorted = 0;
+    HIPR(hipMemcpyAsync(&unsorted, cnt + 1, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    if (unsorted) {
+      // mixed key lengths inside one owner's batch: sort the leaf keys
+      Info fi = info_init();
+      fi.ck_min = 0;
+      fi.ck_max = ~0ull;
+      fi.maxlen = CODE_DIGITS;
+      st = fold_into_tree(ctx, S, s->tree, s->n_owners, l_ck, l_h, m, fi, &new_tree);
+    } else {
+      u64* rck = S.alloc<u64>(std::max<size_t>(m, 1));
+      int32_t* rxr = S.alloc<int32_t>(std::max<size_t>(m, 1));
+      if (!rck || !rxr) return EVM_ENOMEM;
+      uint64_t L = 0;
+      if ((st = reduce_runs(ctx, S, l_ck, (const int32_t*)l_h, m, rck, rxr, &L))) return st;
+      st = merge_into_tree(ctx, S, s->tree, s->n_owners, rck, rxr, L, &new_tree);
+    }
+    if (st) {
+      store_release_arrays(ctx, &ns);
+      return st;
+    }
+  }
+  // commit: swap in the new store arrays and tree
+  store_release_arrays(ctx, s);
+  tree_destroy(ctx, s->tree);
+  s->n = ns.n;
+  s->off = ns.off;
+  s->owner = ns.owner;
+  s->tc = ns.tc;
+  s->hi = ns.hi;
+  s->lo = ns.lo;
+  s->id = ns.id;
+  s->tree = new_tree;
+  return evm_sync(ctx);
+}
+
+int evm_server_select(evm_ctx* ctx, const evm_store* s, const evm_tree* client, const char* node,
+                      const uint8_t* active, int64_t* diff, uint64_t* sel_off, uint64_t* sel_id, uint64_t cap,
+                      uint64_t* n_sel) {
+  if (!ctx || !s || !client || !node || !diff || !sel_off || !n_sel) return EVM_EINVAL;
+  if (client->n_owners != s->n_owners) return EVM_EINVAL;
+  const u32 O = s->n_owners;
+  if (O == 0) {
+    *n_sel = 0;
+    return EVM_OK;
+  }
+  int st;
+  Scratch S(ctx);
+  if ((st = launch_diff(ctx, s->tree, client, diff))) return st;
+  u64* first = S.alloc<u64>(O);
+  u32* cnt = S.alloc<u32>(O);
+  u32* pos = S.alloc<u32>(O);
+  u32* tot = S.alloc<u32>(2);
+  if (!first || !cnt || !pos || !tot) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(tot, 0, 2 * sizeof(u32), ctx->stream));
+  const StoreView v = view_of(s);
+  KLAUNCH(k_sv_sel_count, dim3(grid_for(O, 64, 65536)), dim3(64), v, O, diff, (const uint8_t*)node, active, first, cnt,
+          tot + 1);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, cnt, O, pos, tot))) return st;
+  KLAUNCH(k_u32_to_u64, dim3(grid_for(O + 1, 256)), dim3(256), pos, (size_t)O, tot, (u64*)sel_off);
+  u32 h[2];
+  HIPR(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if (h[1]) return EVM_EINVAL;  // a requester nodeId is not 16 hex chars
+  *n_sel = h[0];
+  if (h[0] > cap || (h[0] && !sel_id)) return EVM_ECAPACITY;
+  KLAUNCH(k_sv_sel_write, dim3(grid_for(O, 64, 65536)), dim3(64), v, (const u64*)s->id, O, first, cnt, pos,
+          (const uint8_t*)node, (u64*)sel_id);
+  return evm_sync(ctx);
+}
+
+}  // extern "C"

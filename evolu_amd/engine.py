@@ -126,6 +126,9 @@ class Engine:
         check(self.lib.evm_tree_from_json(self.h, len(bs), arr, lens, C.byref(h)), "evm_tree_from_json")
         return Trees(self, h)
 
+    def store_new(self, n_owners: int) -> "Store":
+        return Store(self, n_owners)
+
     def tree_from_leaves(self, off: np.ndarray, code: np.ndarray, xr: np.ndarray) -> "Trees":
         off = np.ascontiguousarray(off, dtype=np.uint64)
         code = np.ascontiguousarray(code, dtype=np.uint64)
@@ -173,12 +176,76 @@ class Engine:
         return flags, winner[:n_cells], (Trees(self, h) if st == _lib.EVM_OK else None), st
 
 
+class Store:
+    """Server state: per-owner stored messages + MerkleTrees (index.ts tables)."""
+
+    def __init__(self, eng: "Engine", n_owners: int):
+        self.eng = eng
+        h = C.c_void_p()
+        check(eng.lib.evm_store_new(eng.h, n_owners, C.byref(h)), "evm_store_new")
+        self.h = h
+        self.n_owners = n_owners
+
+    def free(self):
+        if self.h:
+            self.eng.lib.evm_store_free(self.eng.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    @property
+    def n_messages(self) -> int:
+        no = C.c_uint32()
+        nm = C.c_uint64()
+        check(self.eng.lib.evm_store_info(self.h, C.byref(no), C.byref(nm)), "evm_store_info")
+        return nm.value
+
+    def tree(self) -> "Trees":
+        """The store's trees (borrowed: valid until the next ingest)."""
+        return Trees(self.eng, C.c_void_p(self.eng.lib.evm_store_tree(self.h)), owned=False)
+
+    def messages(self):
+        off = np.zeros(self.n_owners + 1, dtype=np.uint64)
+        ids = np.zeros(max(self.n_messages, 1), dtype=np.uint64)
+        check(self.eng.lib.evm_store_messages(self.eng.h, self.h, off.ctypes.data_as(C.c_void_p),
+                                              ids.ctypes.data_as(C.c_void_p)), "evm_store_messages")
+        return off, ids[: self.n_messages]
+
+    def ingest(self, ts: torch.Tensor, owner: torch.Tensor, id_base: int = 0, flags: Optional[torch.Tensor] = None,
+               raise_on_error: bool = True):
+        n, stride = ts.shape
+        if flags is None:
+            flags = torch.empty(max(n, 1), dtype=torch.uint8, device=ts.device)
+        st = self.eng.lib.evm_server_ingest(self.eng.h, self.h, _ptr(ts), stride, n, _ptr(owner), id_base, _ptr(flags))
+        if raise_on_error:
+            check(st, "evm_server_ingest")
+        return flags[:n], st
+
+    def select(self, client: "Trees", node: torch.Tensor, active: Optional[torch.Tensor] = None, cap: int = None):
+        """-> (diff int64[n_owners], sel_off uint64[n_owners+1], sel_id uint64[n_sel])."""
+        dev = node.device
+        O = self.n_owners
+        diff = torch.empty(max(O, 1), dtype=torch.int64, device=dev)
+        off = torch.empty(O + 1, dtype=torch.int64, device=dev)
+        cap = self.n_messages if cap is None else cap
+        ids = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        nsel = C.c_uint64()
+        check(self.eng.lib.evm_server_select(self.eng.h, self.h, client.h, _ptr(node), _ptr(active), _ptr(diff),
+                                             _ptr(off), _ptr(ids), cap, C.byref(nsel)), "evm_server_select")
+        return diff[:O], off, ids[: nsel.value]
+
+
 class Trees:
     """A device-resident set of per-owner MerkleTrees (owns its evm_tree)."""
 
-    def __init__(self, eng: Engine, h):
+    def __init__(self, eng: Engine, h, owned: bool = True):
         self.eng = eng
         self.h = h
+        self.owned = owned
         no = C.c_uint32()
         nl = C.c_uint64()
         check(eng.lib.evm_tree_info(h, C.byref(no), C.byref(nl)), "evm_tree_info")
@@ -186,9 +253,9 @@ class Trees:
         self.n_leaves = nl.value
 
     def free(self):
-        if self.h:
+        if self.h and self.owned:
             self.eng.lib.evm_tree_free(self.eng.h, self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:

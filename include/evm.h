@@ -150,6 +150,42 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
                     size_t prior_stride, const uint8_t* prior_present, uint8_t* flags, int32_t* winner,
                     evm_tree** tree_out);
 
+/* ---- server: apps/server/src/index.ts -------------------------------------
+ * A store holds, per owner (userId), the set of stored messages -- the
+ * "message" table's PRIMARY KEY(timestamp, userId) -- sorted by timestamp
+ * (string order), each with the caller's 64-bit message id, plus the owner's
+ * MerkleTree ("merkleTree" table).  Device resident.                       */
+typedef struct evm_store evm_store;
+
+int evm_store_new(evm_ctx* ctx, uint32_t n_owners, evm_store** out);
+int evm_store_free(evm_ctx* ctx, evm_store* s);
+int evm_store_info(const evm_store* s, uint32_t* n_owners, uint64_t* n_messages);
+/* the store's per-owner trees (borrowed; valid until the next ingest/free) */
+const evm_tree* evm_store_tree(const evm_store* s);
+/* host copies: owner_off[n_owners+1], id[n_messages] in (owner, timestamp) order */
+int evm_store_messages(evm_ctx* ctx, const evm_store* s, uint64_t* owner_off, uint64_t* id);
+
+/* index.ts:138-171 addMessages, batched over requests of many owners.
+ * Batch order = index order (requests concatenated in arrival order).
+ * owner: device [n] owner of each message.  Message i gets id id_base + i.
+ * flags: device [n] -> EVM_MSG_INS where INSERT OR IGNORE changed a row
+ * (first occurrence of (timestamp, owner) not already stored); exactly
+ * those messages are XORed into their owner's tree.                        */
+int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                      uint64_t id_base, uint8_t* flags);
+
+/* index.ts:173-202 getMessages for one request per owner:
+ * diff = diffMerkleTrees(store tree, client[o]); if Some(d), the owner's
+ * messages with timestamp > timestampToString(createSyncTimestamp(d)) and
+ * timestamp NOT LIKE '%' || node[o] (ASCII case-insensitive suffix), in
+ * timestamp order.  node: device, 16 bytes per owner (the requester's
+ * nodeId; 16 hex chars); active: device uint8 [n_owners] (NULL: all).
+ * Outputs (device): diff[n_owners] (EVM_DIFF_NONE / millis / RANGE_ERROR),
+ * sel_off[n_owners + 1], sel_id[cap]; *n_sel = total selected.            */
+int evm_server_select(evm_ctx* ctx, const evm_store* s, const evm_tree* client, const char* node,
+                      const uint8_t* active, int64_t* diff, uint64_t* sel_off, uint64_t* sel_id, uint64_t cap,
+                      uint64_t* n_sel);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,162 @@
+"""Server ingest/select parity (apps/server/src/index.ts) against the oracle's
+verbatim-SQL server (sqlite3)."""
+import json
+import random
+
+import numpy as np
+import pytest
+
+from oracle import evolu_oracle as O
+from tests import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from evolu_amd.engine import Engine
+
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def _requests(seed, n_owners=9, n_req=40, t0=W.T0):
+    """Requests (userId, [timestamps]) with duplicates inside and across requests."""
+    rng = random.Random(seed)
+    owners = ["%021x" % rng.getrandbits(84) for _ in range(n_owners)]
+    pools = {}
+    for o in owners:
+        nodes = [W.node_id(rng, upper=rng.random() < 0.3) for _ in range(3)]
+        base = rng.choice([t0, t0, 0, 3 * 60000])  # short keys for some owners
+        pools[o] = W.hlc_timestamps(rng, 80, nodes, t0=base, span=rng.choice([600_000, 3 * 86_400_000]))
+    reqs = []
+    for _ in range(n_req):
+        o = rng.choice(owners)
+        k = rng.randrange(0, 12)
+        msgs = [rng.choice(pools[o]) for _ in range(k)]
+        reqs.append((o, msgs))
+    return owners, pools, reqs
+
+
+def _run_batches(eng, owners, batches):
+    """batches: list of lists of requests.  Returns (store, per-message flags, ids->ts)."""
+    oid = {o: i for i, o in enumerate(owners)}
+    store = eng.store_new(len(owners))
+    flags_all, id_ts = [], {}
+    base = 0
+    for reqs in batches:
+        strings = [t for _, ms in reqs for t in ms]
+        own = [oid[o] for o, ms in reqs for _ in ms]
+        for k, t in enumerate(strings):
+            id_ts[base + k] = t
+        f, st = store.ingest(eng.timestamps(strings), eng.dev(np.array(own, dtype=np.uint32)), base)
+        flags_all.append(f.cpu().numpy()[: len(strings)])
+        base += len(strings)
+    return store, flags_all, id_ts
+
+
+def _oracle(owners, batches):
+    db = O.ServerDb()
+    ins_all = []
+    for reqs in batches:
+        ins = []
+        for o, ms in reqs:
+            got = []
+            db.add_messages(db.get_merkle_tree(o), o, [(t, b"") for t in ms], got)
+            ins += got
+        ins_all.append(ins)
+    return db, ins_all
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_ingest_vs_oracle(eng, seed):
+    from evolu_amd import _lib as L
+
+    owners, pools, reqs = _requests(seed)
+    batches = [reqs[:15], reqs[15:16], reqs[16:]]
+    store, flags, id_ts = _run_batches(eng, owners, batches)
+    db, ins = _oracle(owners, batches)
+    for f, want in zip(flags, ins):
+        assert [bool(x & L.MSG_INS) for x in f] == want
+    tree = store.tree()
+    for i, o in enumerate(owners):
+        assert tree.to_json(i) == O.merkle_tree_to_string(db.get_merkle_tree(o)), o
+    # stored rows in (owner, timestamp) order == the message table
+    off, ids = store.messages()
+    for i, o in enumerate(owners):
+        rows = db.conn.execute('SELECT "timestamp" FROM "message" WHERE "userId" = ? ORDER BY "timestamp"',
+                               (o,)).fetchall()
+        assert [id_ts[int(k)] for k in ids[off[i]:off[i + 1]]] == [r[0] for r in rows]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_select_vs_oracle(eng, seed):
+    owners, pools, reqs = _requests(100 + seed)
+    store, flags, id_ts = _run_batches(eng, owners, [reqs])
+    db, _ = _oracle(owners, [reqs])
+    rng = random.Random(seed)
+    client_json, nodes, want = [], [], []
+    for o in owners:
+        # the client knows a random subset (incl. nothing / everything)
+        mode = rng.random()
+        have = [t for t in pools[o] if (mode > 0.8 or (mode > 0.2 and rng.random() < 0.7))]
+        ct = {}
+        for t in have:
+            ct = O.insert_into_merkle_tree(ct, O.parse_canonical(t))
+        cj = O.merkle_tree_to_string(ct)
+        node = rng.choice([t[30:] for t in pools[o]] + [W.node_id(rng)])
+        if rng.random() < 0.3:
+            node = node.swapcase()  # LIKE is ASCII case-insensitive
+        client_json.append(cj)
+        nodes.append(node)
+        try:
+            d, rows = db.get_messages(db.get_merkle_tree(o), ct, o, node)
+            want.append((-1 if d is None else d, [r[0] for r in rows]))
+        except O.RangeErrorJS:
+            want.append((-2, []))
+    client = eng.tree_from_json(client_json)
+    node_arr = eng.dev(np.frombuffer("".join(nodes).encode(), dtype=np.uint8).copy())
+    diff, off, ids = store.select(client, node_arr)
+    diff, off, ids = diff.cpu().numpy(), off.cpu().numpy(), ids.cpu().numpy()
+    for i in range(len(owners)):
+        assert int(diff[i]) == want[i][0]
+        assert [id_ts[int(k)] for k in ids[off[i]:off[i + 1]]] == want[i][1]
+
+
+def test_ingest_noncanonical_and_empty(eng):
+    from evolu_amd import _lib as L
+
+    store = eng.store_new(2)
+    f, st = store.ingest(eng.timestamps([]), eng.dev(np.zeros(0, dtype=np.uint32)))
+    assert st == 0 and store.n_messages == 0
+    good = "2024-01-01T00:00:00.000Z-0000-0000000000000001"
+    bad = "2022-02-30T00:00:00.000Z-0000-0000000000000001"
+    f, st = store.ingest(eng.timestamps([good, bad]), eng.dev(np.array([0, 1], dtype=np.uint32)), raise_on_error=False)
+    assert st == L.EVM_ENONCANON and list(f.cpu().numpy()) == [0, L.MSG_BAD]
+    assert store.n_messages == 0
+    assert store.tree().to_json(0) == "{}"
+
+
+def test_ingest_many_owners_scale(eng):
+    """config-3 shape at reduced size: every (owner, ts) once, all inserted;
+    roots == XOR of the owners' hashes; a second ingest of the same batch
+    inserts nothing and leaves every tree unchanged."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    ts_np, owner_np, _ = synth.config3(n_owners=2000, per_owner=500)
+    ts, own = eng.dev(ts_np), eng.dev(owner_np)
+    store = eng.store_new(2000)
+    f, _ = store.ingest(ts, own, 0)
+    assert (f.cpu().numpy() == L.MSG_INS).all()
+    r1, p1 = store.tree().roots()
+    recs, _ = eng.pack(ts)
+    h = recs[:, 2].cpu().numpy().view(np.uint32).reshape(-1, 2)[:, 1]
+    want = np.zeros(2000, dtype=np.uint32)
+    np.bitwise_xor.at(want, owner_np, h)
+    assert np.array_equal(r1.view(np.uint32), want) and p1.all()
+    f2, _ = store.ingest(ts, own, len(ts_np))
+    assert (f2.cpu().numpy() == 0).all() and store.n_messages == len(ts_np)
+    r2, _ = store.tree().roots()
+    assert np.array_equal(r1, r2)
