@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--messages", type=int, default=10_000_000)
     ap.add_argument("--cells", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0: skip)")
+    ap.add_argument("--workload", choices=["client", "server"], default="client",
+                    help="client: config 2 applyMessages (headline); server: config 3/4 ingest + diff + select")
+    ap.add_argument("--owners", type=int, default=100_000, help="server workload: owners per GPU")
+    ap.add_argument("--per-owner", type=int, default=1000, help="server workload: messages per owner")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch per kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -111,6 +115,8 @@ def main():
     from evolu_amd import synth
     from evolu_amd.engine import Engine
 
+    if a.workload == "server":
+        return server_main(a, rank, world, local)
     # each rank: its own owner (seed per rank), same shape
     ts_np, cell_np = synth.config2(a.messages, a.cells, seed_config=2 + 1000 * rank)
     eng = Engine(local)
@@ -190,6 +196,94 @@ def main():
         if world == 1 and a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(ts_np, cell_np, a.cpu_seconds)
         print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def server_main(a, rank, world, local):
+    """Config 3 (1 GPU) / config 4 (N GPUs): server ingest of `owners x
+    per_owner` messages per GPU into an empty store, then getMessages for every
+    owner against a client tree built from the owner's first 90% of
+    messages.  With N ranks every rank receives messages for random owners
+    of the whole job and routes them to the owner's rank (all_to_all over
+    RCCL); roots are all-gathered.  One step = route + ingest + select + roots."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from evolu_amd import dist as D
+    from evolu_amd import synth
+    from evolu_amd.engine import Engine
+
+    O_total = a.owners * world
+    ts_np, owner_np, millis = synth.config3(a.owners, a.per_owner, seed_config=3 + 1000 * rank)
+    # this rank's owner o is job owner o*world + (o+rank)%world: every rank
+    # receives messages for owners living on every rank, no owner on two sources
+    o64 = owner_np.astype(np.int64)
+    owner_np = o64 * world + (o64 + rank) % world
+    eng = Engine(local)
+    dev = torch.device("cuda", local)
+    ts = eng.dev(ts_np)
+    owner = torch.from_numpy(owner_np).to(dev)
+    n_local_owners = (O_total + world - 1) // world
+    if world > 1:
+        ts_r, own_r, src_rank, src_idx = D.route_by_owner(ts, owner)
+    else:
+        ts_r, own_r = ts, owner
+    lown = D.local_owner(own_r, world).contiguous()
+    # client trees: each owner's messages minus the newest 10% (the expected diff)
+    keep =torch.rand(len(own_r), device=dev, generator=torch.Generator(device=dev).manual_seed(7)) < 0.9
+    client = eng.merkle_insert(eng.tree_new(n_local_owners), ts_r[keep].contiguous(), lown[keep].contiguous())
+    node = torch.from_numpy(np.frombuffer(b"0123456789abcdef" * n_local_owners, dtype=np.uint8).copy()).to(dev)
+    flags = torch.empty(len(ts_r), dtype=torch.uint8, device=dev)
+
+    def step():
+        if world > 1:
+            t_r, o_r, _, _ = D.route_by_owner(ts, owner)
+            lo = D.local_owner(o_r, world).contiguous()
+        else:
+            t_r, lo = ts_r, lown
+        store = eng.store_new(n_local_owners)
+        store.ingest(t_r, lo, 0, flags=flags)
+        diff, off, ids = store.select(client, node)
+        r, p = store.tree().roots()
+        if world > 1:
+            D.gather_roots(torch.from_numpy(r).to(dev), torch.from_numpy(p).to(dev), O_total)
+        store.free()
+        return int(ids.numel())
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    eng.prof_reset()
+    eng.prof_enable(True)
+    t0 = time.perf_counter()
+    nsel = 0
+    for _ in range(a.steps):
+        nsel = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    eng.prof_enable(False)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    prof = eng.prof_report()
+    if rank == 0:
+        n = a.owners * a.per_owner
+        ms = elapsed / a.steps * 1e3
+        top = sorted(prof.items(), key=lambda kv: -kv[1][0])[:12]
+        print(json.dumps({
+            "metric": METRIC, "value": world * n * a.steps / elapsed, "unit": "msgs/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u64", "data": "synthetic (seeded HLC streams, SURVEY 8(d) config 3/4)",
+            "config": {"workload": "server: addMessages + getMessages, %d owners x %d msgs per GPU, RCCL owner routing"
+                       % (a.owners, a.per_owner), "messages_per_gpu": n, "owners_per_gpu": a.owners,
+                       "selected_rows_rank0": nsel, "parallelism": "owner-sharded, %d rank(s)" % world},
+            "kernels_ms_per_step": {k: v[0] / a.steps for k, v in top},
+        }), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
