@@ -232,8 +232,17 @@ def server_main(a, rank, world, local):
         ts_r, own_r = ts, owner
     lown = D.local_owner(own_r, world).contiguous()
     # client trees: each owner's messages minus the newest 10% (the expected diff)
-    keep =torch.rand(len(own_r), device=dev, generator=torch.Generator(device=dev).manual_seed(7)) < 0.9
-    client = eng.merkle_insert(eng.tree_new(n_local_owners), ts_r[keep].contiguous(), lown[keep].contiguous())
+    # (the client knows each owner's first 90% by timestamp)
+    order = np.lexsort((millis, o64))
+    rank_in_owner = np.empty(len(order), dtype=np.int64)
+    rank_in_owner[order] = np.arange(len(order)) - np.repeat(np.arange(a.owners) * a.per_owner, a.per_owner)
+    keep_np = (rank_in_owner < int(0.9 * a.per_owner)).astype(np.uint8)
+    if world > 1:  # route the flag with its message (an extra 8-byte column)
+        ext = np.concatenate([ts_np, np.repeat(keep_np[:, None], 8, 1)], 1)
+        keep = D.route_by_owner(torch.from_numpy(ext).to(dev), owner)[0][:, ts_np.shape[1]].bool()
+    else:
+        keep = torch.from_numpy(keep_np).to(dev).bool()
+    client =eng.merkle_insert(eng.tree_new(n_local_owners), ts_r[keep].contiguous(), lown[keep].contiguous())
     node = torch.from_numpy(np.frombuffer(b"0123456789abcdef" * n_local_owners, dtype=np.uint8).copy()).to(dev)
     flags = torch.empty(len(ts_r), dtype=torch.uint8, device=dev)
 
