@@ -167,7 +167,7 @@ def main():
         if os.path.exists(a.traffic):
             t = json.load(open(a.traffic)).get(dom)
             if t is not None:
-                traffic = t
+                traffic = t["bytes"] if isinstance(t, dict) else t  # HBM bytes per launch (PMC, corrected)
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK, "traffic": traffic,
                 "kernel_ms_avg": avg_s * 1e3, "alg_bytes_per_launch": alg,

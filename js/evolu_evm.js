@@ -1,0 +1,152 @@
+// evolu_evm.js -- reference-shaped JS entry points over the N-API addon.
+//
+// Drop-in for the hot path of packages/evolu and apps/server (reference @
+// 2025-01-31): the same inputs and outputs as the reference functions, batched.
+//   insertIntoMerkleTree ... merkleTree.ts:31-50   (many timestamps at once)
+//   diffMerkleTrees ........ merkleTree.ts:63-91
+//   applyMessages .......... applyMessages.ts:26-131 (decisions on the GPU; the
+//                            SQL writes stay with the caller's Database)
+//   Server#addMessages ..... apps/server/src/index.ts:138-171
+//   Server#getMessages ..... apps/server/src/index.ts:173-202
+// Trees cross this boundary as MerkleTree JSON (types.ts:80-84), the format
+// the reference persists and sends.  Results the engine does not model
+// (non-canonical timestamps, a timestamp in two cells) return `null` so the
+// caller runs the reference code for that batch.
+"use strict";
+const addon = require("./evm_napi.node");
+
+const STRIDE = 48;
+const EVM_OK = 0;
+const EVM_ENONCANON = 2;
+const EVM_ECOLLISION = 3;
+const MSG_UPS = 1;
+const MSG_XOR = 2;
+const MSG_INS = 4;
+
+function encodeTimestamps(strings) {
+  const out = new Uint8Array(strings.length * STRIDE);
+  strings.forEach((s, i) => {
+    const o = i * STRIDE;
+    if (s.length !== 46) {
+      out.fill(0xff, o, o + 46); // cannot be canonical: the engine flags it
+      return;
+    }
+    for (let k = 0; k < 46; k++) {
+      const c = s.charCodeAt(k);
+      out[o + k] = c < 128 ? c : 0xff;
+    }
+  });
+  return out;
+}
+
+class Engine {
+  constructor(device = 0) {
+    this.ctx = addon.create(device);
+  }
+  close() {
+    if (this.ctx) addon.destroy(this.ctx);
+    this.ctx = null;
+  }
+  _tree(json) {
+    return addon.treeFromJson(this.ctx, [json]);
+  }
+  _json(tree) {
+    const s = addon.treeToJson(this.ctx, tree, 0);
+    addon.treeFree(this.ctx, tree);
+    return s;
+  }
+
+  // merkleTree.ts:31-50, for a list of timestamps (order-independent)
+  insertIntoMerkleTree(treeJson, timestamps) {
+    const t = this._tree(treeJson);
+    const out = addon.insert(this.ctx, t, encodeTimestamps(timestamps), STRIDE, null);
+    addon.treeFree(this.ctx, t);
+    return this._json(out);
+  }
+
+  // merkleTree.ts:63-91 -> null (option.none) | millis; throws RangeError like keyToTimestamp
+  diffMerkleTrees(aJson, bJson) {
+    const a = this._tree(aJson);
+    const b = this._tree(bJson);
+    const d = addon.diff(this.ctx, a, b)[0];
+    addon.treeFree(this.ctx, a);
+    addon.treeFree(this.ctx, b);
+    if (d === -2) throw new RangeError("Invalid count value");
+    return d === -1 ? null : d;
+  }
+
+  // applyMessages.ts:26-131.  db: { cellMax(table, row, column) -> string|null,
+  // upsert(table, row, column, value), insertMessage(message) }.
+  // Returns the new MerkleTree JSON, or null when the batch needs the reference path.
+  applyMessages(db, treeJson, messages) {
+    const ids = new Map();
+    const cells = [];
+    const cell = new Uint32Array(messages.length);
+    messages.forEach((m, i) => {
+      const k = JSON.stringify([m.table, m.row, m.column]);
+      let c = ids.get(k);
+      if (c === undefined) {
+        c = cells.length;
+        ids.set(k, c);
+        cells.push(m);
+      }
+      cell[i] = c;
+    });
+    // the cells' current maxima: SELECT "timestamp" ... ORDER BY "timestamp" DESC LIMIT 1 (applyMessages.ts:34-40)
+    const prior = cells.map((m) => db.cellMax(m.table, m.row, m.column));
+    const priorPresent = Uint8Array.from(prior.map((p) => (p == null ? 0 : 1)));
+    const t = this._tree(treeJson);
+    const r = addon.applyBatch(this.ctx, t, encodeTimestamps(messages.map((m) => m.timestamp)), STRIDE, cell,
+      cells.length, encodeTimestamps(prior.map((p) => (p == null ? "" : p))), priorPresent);
+    addon.treeFree(this.ctx, t);
+    if (r.status === EVM_ENONCANON || r.status === EVM_ECOLLISION) return null;
+    // the same statements the reference runs, in batch order: the final upsert
+    // of every cell, and INSERT ... ON CONFLICT DO NOTHING of every XOR message
+    r.winner.forEach((i) => {
+      if (i >= 0) db.upsert(messages[i].table, messages[i].row, messages[i].column, messages[i].value);
+    });
+    messages.forEach((m, i) => {
+      if (r.flags[i] & MSG_XOR) db.insertMessage(m);
+    });
+    return this._json(r.tree);
+  }
+}
+
+// apps/server/src/index.ts: one store for many owners (userIds)
+class Server {
+  constructor(engine, nOwners) {
+    this.engine = engine;
+    this.store = addon.storeNew(engine.ctx, nOwners);
+    this.nOwners = nOwners;
+    this.nextId = 0;
+  }
+  close() {
+    addon.storeFree(this.engine.ctx, this.store);
+  }
+  // addMessages for a batch of requests: [{owner, messages: [{timestamp}]}] -> per message inserted flags
+  addMessages(requests) {
+    const ts = [];
+    const own = [];
+    requests.forEach((r) => r.messages.forEach((m) => { ts.push(m.timestamp); own.push(r.owner); }));
+    const r = addon.serverIngest(this.engine.ctx, this.store, encodeTimestamps(ts), STRIDE, Uint32Array.from(own),
+      this.nextId);
+    if (r.status !== EVM_OK) return null;
+    this.nextId += ts.length;
+    return Array.from(r.flags, (f) => (f & MSG_INS) !== 0);
+  }
+  merkleTree(owner) {
+    return addon.treeToJson(this.engine.ctx, addon.storeTree(this.store), owner);
+  }
+  // getMessages for every owner: clientTrees[o] JSON, nodeIds[o] -> { diff[o], ids[o][] }
+  getMessages(clientTreesJson, nodeIds) {
+    const c = addon.treeFromJson(this.engine.ctx, clientTreesJson);
+    const node = encodeTimestamps([]).constructor.from(Buffer.from(nodeIds.join(""), "latin1"));
+    const r = addon.serverSelect(this.engine.ctx, this.store, c, node);
+    addon.treeFree(this.engine.ctx, c);
+    const ids = [];
+    for (let o = 0; o < this.nOwners; o++) ids.push(Array.from(r.ids.subarray(r.off[o], r.off[o + 1])));
+    return { diff: Array.from(r.diff, (d) => (d === -1 ? null : d)), ids };
+  }
+}
+
+module.exports = { Engine, Server, encodeTimestamps, MSG_UPS, MSG_XOR, MSG_INS };

@@ -1,0 +1,98 @@
+"""The N-API addon + JS entry points (js/) on the GPU, driven from node 12,
+against the oracle: the reference-side binding works end to end."""
+import json
+import os
+import random
+import shutil
+import subprocess
+
+import pytest
+
+from oracle import evolu_oracle as O
+from tests import workloads as W
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _build_addon():
+    js = os.path.join(ROOT, "js")
+    out = os.path.join(js, "evm_napi.node")
+    if not os.path.exists(out):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-DNODE_GYP_MODULE_NAME=evm_napi",
+                        "-I/usr/include/node", "-I" + os.path.join(ROOT, "include"), os.path.join(js, "evm_napi.cpp"),
+                        "-o", out, "-L" + os.path.join(ROOT, "evolu_amd"), "-levm",
+                        "-Wl,-rpath,$ORIGIN/../evolu_amd"], check=True)
+    return out
+
+
+@pytest.mark.skipif(shutil.which("node") is None or not os.path.exists("/usr/include/node/node_api.h"),
+                    reason="node / N-API headers not present")
+def test_js_entry_points(tmp_path):
+    _build_addon()
+    n1 = "0000000000000001"
+    ts1, ts2 = O.timestamp_to_string(0, 0, n1), O.timestamp_to_string(1656873738591, 0, n1)
+    cases = {"insert": [{"tree": "{}", "timestamps": [ts1]}, {"tree": "{}", "timestamps": [ts2]},
+                        {"tree": O.merkle_tree_to_string(O.insert_into_merkle_tree({}, O.parse_canonical(ts1))),
+                         "timestamps": [ts2]}],
+             "diff": [{"a": "{}", "b": "{}"},
+                      {"a": "{}", "b": O.merkle_tree_to_string(O.insert_into_merkle_tree({}, O.parse_canonical(ts2)))}]}
+    # applyMessages cases with prior rows
+    apply_cases, expects = [], []
+    for seed in range(3):
+        msgs, cells = W.client_batch(500 + seed, n=200, n_cells=6)
+        prior, _ = W.client_batch(600 + seed, n=30, n_cells=6, t0=W.T0 - 600_000)
+        prior = [dict(m, table=cells[i % 6][0], row=cells[i % 6][1], column=cells[i % 6][2])
+                 for i, m in enumerate(prior)]
+        db = O.ClientDb()
+        t0 = O.apply_messages(db, {}, prior)
+        cell_max = {json.dumps([c[0], c[1], c[2]], separators=(",", ":")): db.cell_max(*c) for c in cells}
+        dec = []
+        t1 = O.apply_messages(db, t0, msgs, dec)
+        ups = {}
+        for m, (u, x, _) in zip(msgs, dec):
+            if u:
+                ups[json.dumps([m["table"], m["row"], m["column"]], separators=(",", ":"))] = m["value"]
+        ins = [m["timestamp"] for m, (u, x, _) in zip(msgs, dec) if x]
+        apply_cases.append({"tree": O.merkle_tree_to_string(t0), "messages": msgs,
+                            "cellMax": {k: v for k, v in cell_max.items() if v is not None}})
+        expects.append({"tree": O.merkle_tree_to_string(t1), "upserts": ups, "inserts": ins})
+    cases["apply"] = apply_cases
+    # server
+    rng = random.Random(2)
+    n_owners = 4
+    pools = [W.hlc_timestamps(rng, 40, [W.node_id(rng) for _ in range(2)]) for _ in range(n_owners)]
+    batches = []
+    for _ in range(3):
+        batches.append([{"owner": o, "messages": [{"timestamp": rng.choice(pools[o])} for _ in range(rng.randrange(8))]}
+                        for o in [rng.randrange(n_owners) for _ in range(5)]])
+    sdb = O.ServerDb()
+    want_ins = []
+    for b in batches:
+        got = []
+        for r in b:
+            u = "u%d" % r["owner"]
+            g = []
+            sdb.add_messages(sdb.get_merkle_tree(u), u, [(m["timestamp"], b"") for m in r["messages"]], g)
+            got += g
+        want_ins.append(got)
+    client = [O.merkle_tree_to_string(O.insert_into_merkle_tree({}, O.parse_canonical(p[0]))) for p in pools]
+    node_ids = [p[1][30:] for p in pools]
+    cases["server"] = {"nOwners": n_owners, "batches": batches, "clientTrees": client, "nodeIds": node_ids}
+    f = tmp_path / "cases.json"
+    f.write_text(json.dumps(cases))
+    res = json.loads(subprocess.run(["node", os.path.join(ROOT, "js", "test_evm.js"), str(f)], check=True,
+                                    capture_output=True, text=True, timeout=300).stdout)
+    snap = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_snapshots.json")))["merkleTree.test.ts.snap"]
+    assert [json.loads(t) for t in res["insert"]] == [snap["insertIntoMerkleTree 1"], snap["insertIntoMerkleTree 2"],
+                                                     snap["insertIntoMerkleTree 3"]]
+    assert res["diff"] == [None, 1656873720000]
+    for got, want in zip(res["apply"], expects):
+        assert got == want
+    assert res["server"]["ins"] == want_ins
+    for o in range(n_owners):
+        assert res["server"]["trees"][o] == O.merkle_tree_to_string(sdb.get_merkle_tree("u%d" % o))
+    for o in range(n_owners):
+        d, rows = sdb.get_messages(sdb.get_merkle_tree("u%d" % o), json.loads(client[o]), "u%d" % o, node_ids[o])
+        assert res["server"]["get"]["diff"][o] == d
+        assert len(res["server"]["get"]["ids"][o]) == len(rows)

@@ -1,0 +1,70 @@
+"""HBM traffic per kernel launch from rocprofv3 PMC passes.
+
+Run two separate counter passes (FETCH_SIZE costs 3 TCC slots, WRITE_SIZE 2:
+they cannot share one), each with nothing but --pmc (MI355X_MICROARCH.md
+§rocprofv3 PMC slots / §HBM):
+
+  rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py ...
+  rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py ...
+
+Corrections (MI355X_MICROARCH.md §HBM): both counters are in KiB; on gfx950
+FETCH_SIZE reports exactly half of the bytes of a wide coalesced streaming
+read, so it is doubled here (this kernel family's loads are 16-B-per-lane
+streams); WRITE_SIZE reads exactly for 16-B streaming stores.  The Infinity
+Cache is not excluded by these counters (bench inputs are 0.5 GB, > 256 MiB).
+
+Usage: python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/traffic.json
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+
+def load(d, counter):
+    paths = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    acc = collections.defaultdict(list)
+    for p in paths:
+        for row in csv.DictReader(open(p)):
+            if row.get("Counter_Name") != counter:
+                continue
+            name = row["Kernel_Name"]
+            acc[name].append(float(row["Counter_Value"]))
+    return acc
+
+
+def short(name):
+    """Kernel symbol -> the name bench.py's event profiler uses."""
+    m = re.match(r"(?:void )?(?:evm::)?([A-Za-z_0-9]+)(<[^>(]*>)?", name)
+    if not m:
+        return name
+    base, targs = m.group(1), m.group(2) or ""
+    if base in ("k_cl_pass",):
+        return "%s<%s>" % (base, targs.strip("<>"))
+    if base in ("k_radix_scatter", "k_radix_hist", "k_scan_down", "k_scan_reduce", "k_scan_partials"):
+        return None
+    return base
+
+
+def main():
+    fetch = load(sys.argv[1], "FETCH_SIZE")
+    write = load(sys.argv[2], "WRITE_SIZE")
+    out = {}
+    for name in set(fetch) | set(write):
+        k = short(name)
+        if not k:
+            continue
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        fb = 2.0 * 1024.0 * (sum(f) / len(f)) if f else None
+        wb = 1024.0 * (sum(w) / len(w)) if w else None
+        out[k] = {"fetch_bytes": fb, "write_bytes": wb,
+                  "bytes": (fb or 0.0) + (wb or 0.0), "launches": max(len(f), len(w))}
+    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
