@@ -95,6 +95,7 @@ int evm::scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out,
 }
 template int evm::scan_exclusive<u32, OpAdd>(evm_ctx*, Scratch&, const u32*, size_t, u32*, u32*);
 template int evm::scan_exclusive<int32_t, OpXor>(evm_ctx*, Scratch&, const int32_t*, size_t, int32_t*, int32_t*);
+template int evm::scan_exclusive<u64, OpMax>(evm_ctx*, Scratch&, const u64*, size_t, u64*, u64*);
 
 template <typename K>
 int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t n, int lo_bit, int hi_bit) {

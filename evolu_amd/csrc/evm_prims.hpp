@@ -31,6 +31,11 @@ struct OpXor {
   __device__ static T id() { return T(0); }
   __device__ T operator()(T a, T b) const { return a ^ b; }
 };
+template <typename T>
+struct OpMax {  // unsigned types: identity 0
+  __device__ static T id() { return T(0); }
+  __device__ T operator()(T a, T b) const { return a > b ? a : b; }
+};
 
 constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ITEMS = 16;

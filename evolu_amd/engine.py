@@ -126,6 +126,21 @@ class Engine:
         check(self.lib.evm_tree_from_json(self.h, len(bs), arr, lens, C.byref(h)), "evm_tree_from_json")
         return Trees(self, h)
 
+    def receive_fold(self, ts: torch.Tensor, local: tuple, now: int, max_drift: int = 60000):
+        """receive.ts:45-66 -> ("ok", (millis, counter, node)) or (error kind, info dict)."""
+        class Res(C.Structure):
+            _fields_ = [("error", C.c_int32), ("counter", C.c_uint32), ("millis", C.c_int64),
+                        ("error_index", C.c_int64), ("next", C.c_int64)]
+
+        n, stride = ts.shape
+        r = Res()
+        check(self.lib.evm_receive_fold(self.h, _ptr(ts), stride, n, local[0], local[1], local[2].encode(), now,
+                                        max_drift, C.byref(r)), "evm_receive_fold")
+        kinds = {1: "TimestampDriftError", 2: "TimestampDuplicateNodeError", 3: "TimestampCounterOverflowError"}
+        if r.error == 0:
+            return "ok", (r.millis, r.counter, local[2])
+        return kinds[r.error], {"index": r.error_index, "next": r.next}
+
     def store_new(self, n_owners: int) -> "Store":
         return Store(self, n_owners)
 

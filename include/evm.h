@@ -150,6 +150,26 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
                     size_t prior_stride, const uint8_t* prior_present, uint8_t* flags, int32_t* winner,
                     evm_tree** tree_out);
 
+/* ---- client: receive.ts:45-66 receiveMessages -----------------------------
+ * Folds timestampFromString(m.timestamp) of every message of a batch into
+ * the local clock with timestamp.ts:125-165 receiveTimestamp, `now` fixed
+ * for the batch (db.worker.ts:71), stopping at the first error exactly as
+ * the reference's readerEither.traverseArray does.  ts: device.          */
+#define EVM_CLOCK_OK 0
+#define EVM_CLOCK_DRIFT 1          /* TimestampDriftError {next, now} */
+#define EVM_CLOCK_DUPLICATE_NODE 2 /* TimestampDuplicateNodeError {node} */
+#define EVM_CLOCK_OVERFLOW 3       /* TimestampCounterOverflowError */
+typedef struct evm_clock_result {
+  int32_t error;       /* EVM_CLOCK_* */
+  uint32_t counter;    /* the new clock (when error == 0) */
+  int64_t millis;
+  int64_t error_index; /* message that failed, -1 */
+  int64_t next;        /* TimestampDriftError.next */
+} evm_clock_result;
+int evm_receive_fold(evm_ctx* ctx, const char* ts, size_t stride, size_t n, int64_t local_millis,
+                     uint32_t local_counter, const char* local_node, int64_t now, int64_t max_drift,
+                     evm_clock_result* out);
+
 /* ---- server: apps/server/src/index.ts -------------------------------------
  * A store holds, per owner (userId), the set of stored messages -- the
  * "message" table's PRIMARY KEY(timestamp, userId) -- sorted by timestamp
