@@ -30,9 +30,9 @@ HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 # SURVEY.md section 8(d) accounting, restated per kernel in DESIGN.md.
 ALG_BYTES_PER_MSG = {
     # streaming fast path (evm_client.hip)
-    "k_cl_pack": 46 + 4 + 28,  # ts + cell in; key 16 + meta 4 + hash 4 + minute 4 out
-    "k_cl_pass<1>": 16 + 4 + 4,  # key + meta + cell in (per-range aggregates amortised away)
-    "k_cl_pass<2>": 16 + 4 + 4 + 1,  # key + meta + cell in, flag out
+    "k_cl_pack": 46 + 28,  # ts in; order key 16 + rl 4 + hash 4 + minute 4 out
+    "k_cl_pass<1>": 16 + 4 + 4,  # order key + rl + cell in (per-range aggregates amortised away)
+    "k_cl_pass<2>": 16 + 4 + 4 + 1,  # order key + rl + cell in, flag out
     "k_xp_scatter": 4 + 8,  # hash in, (hash, index) out
     "k_xp_dedup": 8,  # (hash, index) in
     "k_cl_fold_hist": 9,  # flag + minute + hash in (per window)
@@ -130,14 +130,14 @@ def main():
         _, _, tree, _ = eng.apply_batch(empty, ts, cell, a.cells, flags=flags, winner=winner)
         return tree
 
+    eng.prof_enable(True)  # warmup with events on: fills the engine's event pool
     for _ in range(a.warmup):
         step().free()
     torch.cuda.synchronize()
+    eng.prof_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.prof_reset()
-    eng.prof_enable(True)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         tree = step()
@@ -152,6 +152,14 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
     prof = eng.prof_report()
+    # the same steps once more with the per-kernel events off (reported beside
+    # the timed region, never as `value`): what the event markers cost
+    torch.cuda.synchronize()
+    u0 = time.perf_counter()
+    for _ in range(a.steps):
+        step().free()
+    torch.cuda.synchronize()
+    ms_unprof = (time.perf_counter() - u0) / a.steps * 1e3
 
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
@@ -189,7 +197,7 @@ def main():
                        % (a.messages, a.cells), "messages_per_gpu": a.messages, "cells": a.cells,
                        "parallelism": "owner-sharded, %d rank(s)" % world},
             "roofline": roof,
-            "pipeline": {"alg_bytes_per_msg": 120, "pipeline_hbm_frac": 120 * a.messages * world / (elapsed / a.steps) / world / HBM_PEAK,
+            "pipeline": {"alg_bytes_per_msg": 120, "ms_per_step_events_off": ms_unprof, "pipeline_hbm_frac": 120 * a.messages * world / (elapsed / a.steps) / world / HBM_PEAK,
                          "kernels_ms_per_step": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}},
             "cpu_baseline": None,
         }

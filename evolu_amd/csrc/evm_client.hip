@@ -19,6 +19,7 @@
 
 #include "evm_device.hpp"
 #include "evm_internal.hpp"
+#include "evm_pack.hpp"
 #include "evm_prims.hpp"
 
 using namespace evm;
@@ -227,134 +228,34 @@ constexpr u32 CL_MAX_CELLS = 2048;
 constexpr int CL_RANGE_TARGET = 1280;  // ~5 ranges per CU
 constexpr u32 FOLD_WIN = 32768;        // minutes per LDS histogram window (128 KiB)
 constexpr u32 FOLD_MAXWIN = 4;
-constexpr u32 FOLD_CHUNKS = 64;
+constexpr u32 FOLD_CHUNKS = 128;  // x windows: 256+ single-CU blocks for a 2-window batch
 constexpr int FOLD_THREADS = 1024;
 
-// K1 for the streaming path: parse every timestamp once, at full occupancy,
-// into SoA records: key (tc, node) 16 B, meta 4 B, hash 4 B, minute 4 B.
-// For stride 48 each wave reads its 64 timestamps (3 KiB) with coalesced 16-B
-// loads and redistributes them through LDS.
-constexpr int CLP_THREADS = 256;
-
-__device__ __forceinline__ void clp_fetch(const uint8_t* __restrict__ ts, size_t stride, size_t n, size_t first,
-                                          uint4& a, uint4& b, uint4& c) {
-  const int lane = threadIdx.x & 63;
-  const uint4 z = make_uint4(0, 0, 0, 0);
-  if (first >= n) {
-    a = b = c = z;
-    return;
-  }
-  if (stride == 48) {
-    const uint4* src = reinterpret_cast<const uint4*>(ts + first * 48);
-    const size_t nq = (min(n, first + 64) - first) * 3;
-    a = (size_t)lane < nq ? src[lane] : z;
-    b = (size_t)lane + 64 < nq ? src[lane + 64] : z;
-    c = (size_t)lane + 128 < nq ? src[lane + 128] : z;
-  } else {
-    u32 w[12];
-    const size_t i = first + lane;
-    if (i < n) {
-      load_ts(ts, stride, i, w);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 12; ++k) w[k] = 0;
-    }
-    a = make_uint4(w[0], w[1], w[2], w[3]);
-    b = make_uint4(w[4], w[5], w[6], w[7]);
-    c = make_uint4(w[8], w[9], w[10], w[11]);
-  }
-}
-
-__global__ __launch_bounds__(CLP_THREADS) void k_cl_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
-                                                         const u32* __restrict__ cell, u32 C, uint4* __restrict__ key,
-                                                         u32* __restrict__ meta, u32* __restrict__ hash,
-                                                         u32* __restrict__ minute, Info* __restrict__ info) {
-  __shared__ uint4 stage[CLP_THREADS / 64][192];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  u32 bad = 0, bad_aux = 0, mn = 0xffffffffu, mx = 0;
-  const size_t step = (size_t)gridDim.x * CLP_THREADS;
-  size_t first = ((size_t)blockIdx.x * (CLP_THREADS / 64) + wv) * 64;
-  uint4 a, b, c;
-  clp_fetch(ts, stride, n, first, a, b, c);
-  for (; first < n; first += step) {
-    uint4 na, nb, nc;  // next round in flight while this one is parsed
-    clp_fetch(ts, stride, n, first + step, na, nb, nc);
-    const size_t i = first + lane;
-    u32 w[12];
-    if (stride == 48) {
-      stage[wv][lane] = a;
-      stage[wv][lane + 64] = b;
-      stage[wv][lane + 128] = c;
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      const uint4 x = stage[wv][3 * lane], y = stage[wv][3 * lane + 1], z = stage[wv][3 * lane + 2];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
-      w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-      w[8] = z.x; w[9] = z.y; w[10] = z.z; w[11] = z.w & 0xffffu;
-    } else {
-      w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
-      w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-      w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
-    }
-    if (i < n) {
-      const Parsed p = parse_ts46(w);
-      key[i] = make_uint4((u32)p.tc, (u32)(p.tc >> 32), (u32)p.node, (u32)(p.node >> 32));
-      meta[i] = p.meta;
-      hash[i] = p.hash;
-      minute[i] = p.minute;
-      const bool valid = (p.meta & EVM_META_VALID) != 0;
-      bad |= valid ? 0u : 1u;
-      if (cell[i] >= C) bad_aux = 1;
-      if (valid) {
-        mn = min(mn, p.minute);
-        mx = max(mx, p.minute);
-      }
-    }
-    a = na;
-    b = nb;
-    c = nc;
-  }
-  for (int d = 32; d >= 1; d >>= 1) {
-    bad |= __shfl_xor(bad, d, 64);
-    bad_aux |= __shfl_xor(bad_aux, d, 64);
-    mn = min(mn, (u32)__shfl_xor(mn, d, 64));
-    mx = max(mx, (u32)__shfl_xor(mx, d, 64));
-  }
-  if (lane == 0) {
-    if (bad) atomicOr(&info->bad, 1u);
-    if (bad_aux) atomicOr(&info->bad_aux, 1u);
-    if (mn != 0xffffffffu) {
-      atomicMin(&info->minute_min, mn);
-      atomicMax(&info->minute_max, mx);
-    }
-  }
-}
+constexpr int CL_PF = 8;  // rounds of 64 messages a pass wave keeps in flight
 
 struct ClMsg {
-  Key key;
+  OKey key;
   u32 cell;
   bool ok;  // valid timestamp, cell in range, inside the range
 };
 
 struct ClRaw {
-  uint4 key;
-  u32 meta;
+  uint4 key;  // tc, rh
+  u32 rl;
   u32 cell;
 };
 
-__device__ __forceinline__ ClRaw cl_fetch(const uint4* __restrict__ key, const u32* __restrict__ meta,
+__device__ __forceinline__ ClRaw cl_fetch(const uint4* __restrict__ key, const u32* __restrict__ rl,
                                           const u32* __restrict__ cell, size_t first, size_t end) {
   const size_t i = first + (threadIdx.x & 63);
   ClRaw r;
   if (i < end) {
     r.key = key[i];
-    r.meta = meta[i];
+    r.rl = rl[i];
     r.cell = cell[i];
   } else {
     r.key = make_uint4(0, 0, 0, 0);
-    r.meta = 0;
+    r.rl = 0;
     r.cell = 0xffffffffu;
   }
   return r;
@@ -362,18 +263,17 @@ __device__ __forceinline__ ClRaw cl_fetch(const uint4* __restrict__ key, const u
 
 __device__ __forceinline__ ClMsg cl_decode(const ClRaw& r, u32 C) {
   ClMsg m;
-  m.key = Key{(u64)r.key.x | ((u64)r.key.y << 32), (u64)r.key.z | ((u64)r.key.w << 32),
-              (r.meta & EVM_META_CASEMASK) | KEY_PRESENT};
+  m.key = OKey{(u64)r.key.x | ((u64)r.key.y << 32), (u64)r.key.z | ((u64)r.key.w << 32), r.rl};
   m.cell = r.cell;
-  m.ok = (r.meta & EVM_META_VALID) && r.cell < C;
+  m.ok = (r.rl & OKEY_PRESENT) && r.cell < C;
   return m;
 }
 
-__device__ __forceinline__ Key shfl_key(const Key& k, int src) {
-  Key o;
+__device__ __forceinline__ OKey shfl_okey(const OKey& k, int src) {
+  OKey o;
   o.tc = ((u64)(u32)__shfl((int)(u32)(k.tc >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)k.tc, src, 64);
-  o.node = ((u64)(u32)__shfl((int)(u32)(k.node >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)k.node, src, 64);
-  o.mask = (u32)__shfl((int)k.mask, src, 64);
+  o.rh = ((u64)(u32)__shfl((int)(u32)(k.rh >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)k.rh, src, 64);
+  o.rl = (u32)__shfl((int)k.rl, src, 64);
   return o;
 }
 
@@ -390,10 +290,17 @@ __device__ __forceinline__ u64 match_cell(u32 c, bool active, int bits) {
 
 struct ClState {
   u64* tc;
-  u64* node;
-  u32* mask;
+  u64* rh;
+  u32* rl;
   u32* first;
 };
+
+__device__ __forceinline__ OKey cl_load(const ClState& S, u32 c) { return OKey{S.tc[c], S.rh[c], S.rl[c]}; }
+__device__ __forceinline__ void cl_store(const ClState& S, u32 c, const OKey& k) {
+  S.tc[c] = k.tc;
+  S.rh[c] = k.rh;
+  S.rl[c] = k.rl;
+}
 
 // One round of 64 messages (lane order == batch order).
 template <int PASS>
@@ -406,69 +313,61 @@ __device__ __forceinline__ void cl_round(const ClMsg& m, size_t first, int cbits
   u64 rem = peers & lanemask_lt();
   if (PASS == 1) {
     // round max of this lane's cell over peers up to this lane; first index wins ties
-    Key acc = key_none();
+    OKey acc = okey_none();
     u32 acc_i = 0xffffffffu;
     while (__any(rem != 0)) {
       const int src = rem ? (int)__builtin_ctzll(rem) : lane;
-      const Key kp = shfl_key(m.key, src);
+      const OKey kp = shfl_okey(m.key, src);
       if (rem) {
-        if (key_cmp(kp, acc) > 0) {
+        if (okey_gt(kp, acc)) {
           acc = kp;
           acc_i = (u32)(first + src);
         }
         rem &= rem - 1;
       }
     }
-    if (m.ok && key_cmp(m.key, acc) > 0) {
+    if (m.ok && okey_gt(m.key, acc)) {
       acc = m.key;
       acc_i = (u32)i;
     }
     if (last_peer) {
-      const Key st{S.tc[m.cell], S.node[m.cell], S.mask[m.cell]};
-      if (key_cmp(acc, st) > 0) {
-        S.tc[m.cell] = acc.tc;
-        S.node[m.cell] = acc.node;
-        S.mask[m.cell] = acc.mask;
+      if (okey_gt(acc, cl_load(S, m.cell))) {
+        cl_store(S, m.cell, acc);
         S.first[m.cell] = acc_i;
       }
     }
   } else {
-    Key acc = m.ok ? Key{S.tc[m.cell], S.node[m.cell], S.mask[m.cell]} : key_none();
+    OKey acc = m.ok ? cl_load(S, m.cell) : okey_none();
     while (__any(rem != 0)) {
       const int src = rem ? (int)__builtin_ctzll(rem) : lane;
-      const Key kp = shfl_key(m.key, src);
+      const OKey kp = shfl_okey(m.key, src);
       if (rem) {
-        acc = key_max(acc, kp);
+        acc = okey_max(acc, kp);
         rem &= rem - 1;
       }
     }
     if (i < end) {
-      // applyMessages.ts:93 / :105 with t = acc
-      const bool ups = m.ok && key_cmp(acc, m.key) < 0;
-      const bool xr = m.ok && !((acc.mask & KEY_PRESENT) && key_eq(acc, m.key));
+      // applyMessages.ts:93 / :105 with t = acc (NULL is the all-zero key)
+      const bool ups = m.ok && okey_gt(m.key, acc);
+      const bool xr = m.ok && !okey_eq(acc, m.key);
       flags[i] = m.ok ? (uint8_t)((ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u)) : (uint8_t)EVM_MSG_BAD;
     }
-    if (last_peer) {
-      const Key inc = key_max(acc, m.key);
-      S.tc[m.cell] = inc.tc;
-      S.node[m.cell] = inc.node;
-      S.mask[m.cell] = inc.mask;
-    }
+    if (last_peer) cl_store(S, m.cell, okey_max(acc, m.key));
   }
 }
 
 template <int PASS>
-__global__ __launch_bounds__(64) void k_cl_pass(const uint4* __restrict__ key, const u32* __restrict__ meta,
+__global__ __launch_bounds__(64) void k_cl_pass(const uint4* __restrict__ key, const u32* __restrict__ rl,
                                                 const u32* __restrict__ cell, size_t n, u32 C, int cbits,
-                                                size_t range_len, u64* __restrict__ agg_tc, u64* __restrict__ agg_node,
-                                                u32* __restrict__ agg_mask, u32* __restrict__ agg_first,
-                                                uint8_t* __restrict__ flags) {
+                                                size_t range_len, u64* __restrict__ agg_tc, u64* __restrict__ agg_rh,
+                                                u32* __restrict__ agg_rl, u32* __restrict__ agg_first,
+                                                uint8_t* __restrict__ flags, Info* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   ClState S;
   S.tc = reinterpret_cast<u64*>(smem);
-  S.node = S.tc + C;
-  S.mask = reinterpret_cast<u32*>(S.node + C);
-  S.first = S.mask + C;
+  S.rh = S.tc + C;
+  S.rl = reinterpret_cast<u32*>(S.rh + C);
+  S.first = S.rl + C;
   const int lane = threadIdx.x;
   const size_t g = blockIdx.x;
   const size_t beg = g * range_len;
@@ -476,33 +375,41 @@ __global__ __launch_bounds__(64) void k_cl_pass(const uint4* __restrict__ key, c
   for (u32 c = lane; c < C; c += 64) {
     if (PASS == 1) {
       S.tc[c] = 0;
-      S.node[c] = 0;
-      S.mask[c] = 0;
+      S.rh[c] = 0;
+      S.rl[c] = 0;
       S.first[c] = 0xffffffffu;
     } else {
       S.tc[c] = agg_tc[g * C + c];
-      S.node[c] = agg_node[g * C + c];
-      S.mask[c] = agg_mask[g * C + c];
+      S.rh[c] = agg_rh[g * C + c];
+      S.rl[c] = agg_rl[g * C + c];
     }
   }
   __syncthreads();
-  // software pipeline: two rounds in flight ahead of the one being combined
-  ClRaw r0 = cl_fetch(key, meta, cell, beg, end);
-  ClRaw r1 = cl_fetch(key, meta, cell, beg + 64, end);
-  for (size_t first = beg; first < end; first += 128) {
-    const ClRaw r2 = cl_fetch(key, meta, cell, first + 128, end);
-    const ClRaw r3 = cl_fetch(key, meta, cell, first + 192, end);
-    cl_round<PASS>(cl_decode(r0, C), first, cbits, S, flags, end);
-    if (first + 64 < end) cl_round<PASS>(cl_decode(r1, C), first + 64, cbits, S, flags, end);
-    r0 = r2;
-    r1 = r3;
+  // software pipeline: CL_PF rounds in flight (registers; one wave per SIMD
+  // has the VGPRs), so HBM latency hides behind the serial per-round chain
+  ClRaw buf[CL_PF];
+#pragma unroll
+  for (int k = 0; k < CL_PF; ++k) buf[k] = cl_fetch(key, rl, cell, beg + 64 * k, end);
+  bool aux_bad = false;
+  for (size_t first = beg; first < end; first += 64 * CL_PF) {
+#pragma unroll
+    for (int k = 0; k < CL_PF; ++k) {
+      const ClRaw cur = buf[k];
+      buf[k] = cl_fetch(key, rl, cell, first + 64 * (k + CL_PF), end);
+      const size_t f = first + 64 * k;
+      if (f < end) {
+        if (PASS == 1) aux_bad |= f + lane < end && cur.cell >= C;
+        cl_round<PASS>(cl_decode(cur, C), f, cbits, S, flags, end);
+      }
+    }
   }
+  if (PASS == 1 && __ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
   if (PASS == 1) {
     __syncthreads();
     for (u32 c = lane; c < C; c += 64) {
       agg_tc[g * C + c] = S.tc[c];
-      agg_node[g * C + c] = S.node[c];
-      agg_mask[g * C + c] = S.mask[c];
+      agg_rh[g * C + c] = S.rh[c];
+      agg_rl[g * C + c] = S.rl[c];
       agg_first[g * C + c] = S.first[c];
     }
   }
@@ -514,67 +421,82 @@ __global__ __launch_bounds__(64) void k_cl_pass(const uint4* __restrict__ key, c
 constexpr u32 CARRY_SEGS = 64;
 
 struct Agg {
-  Key key;
+  OKey key;
   u32 first;
 };
-__device__ __forceinline__ Agg agg_merge(const Agg& a, const Agg& b) { return key_cmp(b.key, a.key) > 0 ? b : a; }
+__device__ __forceinline__ Agg agg_merge(const Agg& a, const Agg& b) { return okey_gt(b.key, a.key) ? b : a; }
 
-__global__ void k_cl_carry_reduce(u32 C, size_t G, const u64* __restrict__ tc, const u64* __restrict__ node,
-                                  const u32* __restrict__ mask, const u32* __restrict__ firsti, u64* __restrict__ s_tc,
-                                  u64* __restrict__ s_node, u32* __restrict__ s_mask, u32* __restrict__ s_first) {
+__global__ void k_cl_carry_reduce(u32 C, size_t G, const u64* __restrict__ tc, const u64* __restrict__ rh,
+                                  const u32* __restrict__ rl, const u32* __restrict__ firsti, u64* __restrict__ s_tc,
+                                  u64* __restrict__ s_rh, u32* __restrict__ s_rl, u32* __restrict__ s_first) {
   const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
   if (c >= C) return;
   const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
   const size_t a = p * per, e = min(G, a + per);
-  Agg run{key_none(), 0xffffffffu};
+  Agg run{okey_none(), 0xffffffffu};
 #pragma unroll 4
   for (size_t g = a; g < e; ++g) {
     const size_t k = g * C + c;
-    run = agg_merge(run, Agg{Key{tc[k], node[k], mask[k]}, firsti[k]});
+    run = agg_merge(run, Agg{OKey{tc[k], rh[k], rl[k]}, firsti[k]});
   }
   const size_t o = (size_t)p * C + c;
   s_tc[o] = run.key.tc;
-  s_node[o] = run.key.node;
-  s_mask[o] = run.key.mask;
+  s_rh[o] = run.key.rh;
+  s_rl[o] = run.key.rl;
   s_first[o] = run.first;
 }
 
-__global__ void k_cl_carry_segs(u32 C, u64* __restrict__ s_tc, u64* __restrict__ s_node, u32* __restrict__ s_mask,
-                                u32* __restrict__ s_first, const evm_rec* __restrict__ prior,
-                                const uint8_t* __restrict__ prior_present, int32_t* __restrict__ winner) {
-  const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per cell, one lane per segment (CARRY_SEGS == 64): an exclusive
+// wave scan of the segment aggregates seeded with the prior max.
+static_assert(CARRY_SEGS == 64, "k_cl_carry_segs maps one segment per lane");
+__global__ __launch_bounds__(256) void k_cl_carry_segs(u32 C, u64* __restrict__ s_tc, u64* __restrict__ s_rh,
+                                                       u32* __restrict__ s_rl, u32* __restrict__ s_first,
+                                                       const evm_rec* __restrict__ prior,
+                                                       const uint8_t* __restrict__ prior_present,
+                                                       int32_t* __restrict__ winner) {
+  const u32 c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (c >= C) return;
-  // the prior max has no batch index: it wins ties (an equal batch copy is a no-op)
-  Agg run{(prior_present && prior_present[c]) ? key_of(prior[c]) : key_none(), 0xffffffffu};
-  for (u32 p = 0; p < CARRY_SEGS; ++p) {
-    const size_t o = (size_t)p * C + c;
-    const Agg t{Key{s_tc[o], s_node[o], s_mask[o]}, s_first[o]};
-    s_tc[o] = run.key.tc;
-    s_node[o] = run.key.node;
-    s_mask[o] = run.key.mask;
-    s_first[o] = run.first;
-    run = agg_merge(run, t);
+  const size_t o = (size_t)lane * C + c;
+  Agg v{OKey{s_tc[o], s_rh[o], s_rl[o]}, s_first[o]};
+  // inclusive scan over lanes (segments in batch order); ties keep the left one
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    Agg u;
+    u.key = shfl_okey(v.key, (int)lane - d < 0 ? (int)lane : (int)lane - d);
+    u.first = (u32)__shfl((int)v.first, (int)lane - d < 0 ? (int)lane : (int)lane - d, 64);
+    if ((int)lane >= d) v = agg_merge(u, v);
   }
-  winner[c] = (int32_t)run.first;  // 0xffffffff -> -1: no upsert survives
+  // exclusive: shift right by one, lane 0 gets the prior; the prior has no
+  // batch index and wins ties (an equal batch copy is a no-op)
+  const Agg seed{(prior_present && prior_present[c]) ? okey_of(prior[c]) : okey_none(), 0xffffffffu};
+  Agg ex;
+  ex.key = shfl_okey(v.key, lane == 0 ? 0 : (int)lane - 1);
+  ex.first = (u32)__shfl((int)v.first, lane == 0 ? 0 : (int)lane - 1, 64);
+  ex = lane == 0 ? seed : agg_merge(seed, ex);
+  s_tc[o] = ex.key.tc;
+  s_rh[o] = ex.key.rh;
+  s_rl[o] = ex.key.rl;
+  s_first[o] = ex.first;
+  if (lane == 63) winner[c] = (int32_t)agg_merge(seed, v).first;  // 0xffffffff -> -1: no upsert survives
 }
 
-__global__ void k_cl_carry_down(u32 C, size_t G, u64* __restrict__ tc, u64* __restrict__ node, u32* __restrict__ mask,
+__global__ void k_cl_carry_down(u32 C, size_t G, u64* __restrict__ tc, u64* __restrict__ rh, u32* __restrict__ rl,
                                 const u32* __restrict__ firsti, const u64* __restrict__ s_tc,
-                                const u64* __restrict__ s_node, const u32* __restrict__ s_mask) {
+                                const u64* __restrict__ s_rh, const u32* __restrict__ s_rl) {
   const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
   if (c >= C) return;
   const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
   const size_t a = p * per, e = min(G, a + per);
   const size_t o = (size_t)p * C + c;
-  Key run{s_tc[o], s_node[o], s_mask[o]};
+  OKey run{s_tc[o], s_rh[o], s_rl[o]};
 #pragma unroll 4
   for (size_t g = a; g < e; ++g) {
     const size_t k = g * C + c;
-    const Key here{tc[k], node[k], mask[k]};
+    const OKey here{tc[k], rh[k], rl[k]};
     tc[k] = run.tc;
-    node[k] = run.node;
-    mask[k] = run.mask;
-    run = key_max(run, here);
+    rh[k] = run.rh;
+    rl[k] = run.rl;
+    run = okey_max(run, here);
   }
 }
 
@@ -610,7 +532,7 @@ __global__ void k_cl_xcell(const uint8_t* __restrict__ ts, size_t stride, const 
       if ((u32)(s >> 32 & 0xffffffu) == (h & 0xffffffu)) {
         const size_t j = (size_t)(s & 0xffffffffu) - 1;
         if (ts_bytes_equal(ts, stride, i, j)) {
-          if (cell[i] != cell[j]) atomicOr(&info->collision, 1u);
+          if (cell[i] != cell[j]) atomic_or_if(&info->collision, 1u);
           break;
         }
       }
@@ -624,77 +546,115 @@ __global__ void k_cl_xcell(const uint8_t* __restrict__ ts, size_t stride, const 
 // an LDS hash set.  Equal timestamps always share a bucket.  A bucket too big
 // for LDS flags `xc_oversize` and the host reruns the global-table check.
 constexpr int XP_THREADS = 1024;
-constexpr int XP_ITEMS = 32;
-constexpr int XP_TILE = XP_THREADS * XP_ITEMS;
-constexpr u32 XP_MAX_BUCKET = 6144;  // entries a bucket may hold for the LDS set
-constexpr u32 XP_SLOTS = 8192;       // LDS set slots, 64 KiB (two workgroups per CU)
+constexpr int XP_ITEMS = 16;
+constexpr int XP_TILE = XP_THREADS * XP_ITEMS;  // 16384 pairs staged in 128 KiB of LDS
+constexpr u32 XP_SLOTS = 32768;                 // LDS set: u32 slots, 128 KiB
+constexpr u32 XP_MAX_FILL = 24576;              // bucket capacity cap (75 % load)
+constexpr u32 XP_AVG = 20000;                   // target mean bucket size
+constexpr int XP_MAX_KB = 11;                   // 2048 buckets: n > 41M overfills them -> exact fallback
 
-__global__ __launch_bounds__(XP_THREADS) void k_xp_hist(const u32* __restrict__ hash, size_t n, int kb,
-                                                       u32* __restrict__ counts, u32 ntiles) {
-  extern __shared__ u32 hist[];
+// Buckets have a fixed capacity `cap` in `out` (bucket b owns [b*cap, b*cap+cap));
+// each tile reserves its run per bucket with one atomic on cursor[b], so no
+// count matrix and no scan.  The tile is staged in LDS in bucket order and
+// written back with consecutive lanes on consecutive addresses.  Order inside
+// a bucket is irrelevant.  A full bucket flags xc_oversize (exact fallback).
+__global__ __launch_bounds__(XP_THREADS) void k_xp_scatter(const u32* __restrict__ hash, size_t n, int kb, u32 cap,
+                                                          u32* __restrict__ cursor, u64* __restrict__ out,
+                                                          Info* __restrict__ info) {
+  __shared__ u64 stage[XP_TILE];
+  __shared__ u32 cnt[1u << XP_MAX_KB];  // per bucket: count, then local offset
+  __shared__ u32 gb[1u << XP_MAX_KB];   // per bucket: this tile's base inside the bucket
+  __shared__ u32 scan_tmp[XP_THREADS / 64 + 1];
   const u32 B = 1u << kb;
-  for (u32 b = threadIdx.x; b < B; b += XP_THREADS) hist[b] = 0;
+  const int sh = 32 - kb;
+  for (u32 b = threadIdx.x; b < B; b += XP_THREADS) cnt[b] = 0;
   __syncthreads();
   const size_t base = (size_t)blockIdx.x * XP_TILE;
+  u32 h[XP_ITEMS], r[XP_ITEMS];
+#pragma unroll
   for (int k = 0; k < XP_ITEMS; ++k) {
     const size_t i = base + (size_t)k * XP_THREADS + threadIdx.x;
-    if (i < n) atomicAdd(&hist[hash[i] >> (32 - kb)], 1u);
+    h[k] = i < n ? hash[i] : 0u;
+    r[k] = i < n ? atomicAdd(&cnt[kb ? h[k] >> sh : 0u], 1u) : 0u;
   }
   __syncthreads();
-  for (u32 b = threadIdx.x; b < B; b += XP_THREADS) counts[(size_t)b * ntiles + blockIdx.x] = hist[b];
-}
-
-__global__ __launch_bounds__(XP_THREADS) void k_xp_scatter(const u32* __restrict__ hash, size_t n, int kb,
-                                                          const u32* __restrict__ offs, u32 ntiles,
-                                                          u64* __restrict__ out) {
-  extern __shared__ u32 cnt[];
-  const u32 B = 1u << kb;
-  for (u32 b = threadIdx.x; b < B; b += XP_THREADS) cnt[b] = offs[(size_t)b * ntiles + blockIdx.x];
-  __syncthreads();
-  const size_t base = (size_t)blockIdx.x * XP_TILE;
-  for (int k = 0; k < XP_ITEMS; ++k) {
-    const size_t i = base + (size_t)k * XP_THREADS + threadIdx.x;
-    if (i < n) {
-      const u32 h = hash[i];
-      const u32 dst = atomicAdd(&cnt[h >> (32 - kb)], 1u);  // order inside a bucket is irrelevant
-      out[dst] = ((u64)h << 32) | (u64)i;
+  // exclusive scan of the bucket counts (B <= 16 * XP_THREADS), reserve global runs
+  const u32 per = (B + XP_THREADS - 1) / XP_THREADS;
+  u32 loc[(1u << XP_MAX_KB) / XP_THREADS];
+  u32 sum = 0;
+  for (u32 k = 0; k < per; ++k) {
+    const u32 b = threadIdx.x * per + k;
+    loc[k] = b < B ? cnt[b] : 0u;
+    sum += loc[k];
+  }
+  u32 tot;
+  const u32 incl = block_inclusive_scan<u32>(sum, scan_tmp, OpAdd<u32>(), &tot);
+  u32 run = incl - sum;
+  bool full = false;
+  for (u32 k = 0; k < per; ++k) {
+    const u32 b = threadIdx.x * per + k;
+    if (b < B) {
+      const u32 c = loc[k];
+      cnt[b] = run;
+      u32 g = 0;
+      if (c) {
+        g = atomicAdd(&cursor[b], c);
+        full |= g + c > cap;
+      }
+      gb[b] = g;
+      run += c;
     }
   }
+  if (__ballot(full) && (threadIdx.x & 63) == 0) atomic_or_if(&info->xc_oversize, 1u);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < XP_ITEMS; ++k) {
+    const size_t i = base + (size_t)k * XP_THREADS + threadIdx.x;
+    if (i < n) stage[cnt[kb ? h[k] >> sh : 0u] + r[k]] = ((u64)h[k] << 32) | (u64)i;
+  }
+  __syncthreads();
+  const u32 m = (u32)min((size_t)XP_TILE, n - base);
+  for (u32 t = threadIdx.x; t < m; t += XP_THREADS) {
+    const u64 v = stage[t];
+    const u32 b = kb ? (u32)(v >> 32) >> sh : 0u;
+    const u32 slot = gb[b] + (t - cnt[b]);
+    if (slot < cap) out[(size_t)b * cap + slot] = v;
+  }
 }
 
-__global__ __launch_bounds__(256) void k_xp_dedup(const u64* __restrict__ pairs, const u32* __restrict__ offs, u32 ntiles,
-                                                  int kb, size_t n, const uint8_t* __restrict__ ts, size_t stride,
-                                                  const u32* __restrict__ cell, Info* __restrict__ info) {
-  extern __shared__ u64 tab[];  // XP_SLOTS x (hash:32 | (index + 1):32), 0 = empty
-  const u32 b = blockIdx.x, B = 1u << kb;
-  const size_t a = offs[(size_t)b * ntiles];
-  const size_t e = (b + 1 < B) ? offs[(size_t)(b + 1) * ntiles] : n;
-  const size_t cnt = e - a;
+// One bucket per workgroup: insert every (hash, index) into an LDS set of u32
+// slots = tag:17 | (local index + 1):15; a tag match re-reads the other pair's
+// full hash (L2-hot), and equal hashes compare the raw 46 timestamp bytes.
+__global__ __launch_bounds__(XP_THREADS) void k_xp_dedup(const u64* __restrict__ pairs, const u32* __restrict__ cursor,
+                                                        u32 cap, size_t n, const uint8_t* __restrict__ ts,
+                                                        size_t stride, const u32* __restrict__ cell,
+                                                        Info* __restrict__ info) {
+  __shared__ u32 tab[XP_SLOTS];  // 0 = empty
+  const u32 b = blockIdx.x;
+  const u32 cnt = min(cursor[b], cap);
   if (cnt < 2) return;
-  if (cnt > XP_MAX_BUCKET) {
-    if (threadIdx.x == 0) atomicOr(&info->xc_oversize, 1u);
-    return;
-  }
-  u32 slots = 64;
-  while (slots < 2 * cnt) slots <<= 1;
-  for (u32 s = threadIdx.x; s < slots; s += 256) tab[s] = 0;
+  for (u32 s = threadIdx.x; s < XP_SLOTS; s += XP_THREADS) tab[s] = 0;
   __syncthreads();
-  for (size_t k = a + threadIdx.x; k < e; k += 256) {
-    const u64 p = pairs[k];
+  const u64* bp = pairs + (size_t)b * cap;
+  for (u32 k = threadIdx.x; k < cnt; k += XP_THREADS) {
+    const u64 p = bp[k];
     const u32 h = (u32)(p >> 32), i = (u32)p;
-    const u64 mine = ((u64)h << 32) | (u64)(i + 1);
-    u32 pos = (h * 2654435761u) & (slots - 1);
-    for (u32 probe = 0; probe < slots; ++probe) {
-      const u64 prev = atomicCAS(&tab[pos], 0ull, mine);
+    const u32 mine = ((h >> 15) << 15) | (k + 1);
+    u32 pos = (h * 2654435761u) >> 17;  // 15 bits
+    for (u32 probe = 0; probe < XP_SLOTS; ++probe) {
+      const u32 prev = atomicCAS(&tab[pos], 0u, mine);
       if (prev == 0) break;  // inserted
-      if ((u32)(prev >> 32) == h) {
-        const u32 j = (u32)prev - 1;
-        if (ts_bytes_equal(ts, stride, i, j)) {  // equal strings <=> equal keys (both canonical)
-          if (cell[i] != cell[j]) atomicOr(&info->collision, 1u);
-          break;
+      if ((prev >> 15) == (h >> 15)) {
+        const u64 q = bp[(prev & 0x7fffu) - 1];
+        if ((u32)(q >> 32) == h) {
+          const u32 j = (u32)q;
+          if (ts_bytes_equal(ts, stride, i, j)) {  // equal strings <=> equal keys (both canonical)
+            if (cell[i] != cell[j]) atomic_or_if(&info->collision, 1u);
+            break;
+          }
         }
       }
-      pos = (pos + 1) & (slots - 1);
+      pos = (pos + 1) & (XP_SLOTS - 1);
     }
   }
 }
@@ -773,12 +733,43 @@ __global__ void k_cl_fold_reduce(const u32* __restrict__ px, const u32* __restri
   dp[b] = p;
 }
 
-__global__ void k_cl_leaves(const u32* __restrict__ dx, const u32* __restrict__ dp, const u32* __restrict__ pos,
-                            const Info* __restrict__ info, u64* __restrict__ ck, int32_t* __restrict__ xr) {
-  const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= FOLD_MAXWIN * FOLD_WIN || !dp[b]) return;
-  ck[pos[b]] = minute_code(info->minute_min + b);  // owner 0
-  xr[pos[b]] = (int32_t)dx[b];
+// Dense leaves in one workgroup: positions by a block scan of the presence
+// bits (thread t owns bins [t*per, t*per+per)), codes by a base-3 increment
+// from the thread's first minute (all minutes share one key length here).
+constexpr int LEAF_THREADS = 1024;
+__global__ __launch_bounds__(LEAF_THREADS) void k_cl_leaves(const u32* __restrict__ dx, const u32* __restrict__ dp,
+                                                           Info* __restrict__ info, u64* __restrict__ ck,
+                                                           int32_t* __restrict__ xr) {
+  __shared__ u32 tmp[LEAF_THREADS / 64 + 1];
+  constexpr u32 B = FOLD_MAXWIN * FOLD_WIN, per = B / LEAF_THREADS;
+  const u32 a = threadIdx.x * per;
+  u32 c = 0;
+  for (u32 k = 0; k < per; ++k) c += dp[a + k];
+  u32 total;
+  const u32 incl = block_inclusive_scan<u32>(c, tmp, OpAdd<u32>(), &total);
+  if (threadIdx.x == 0) info->n_leaves = total;
+  if (!c) return;
+  u32 pos = incl - c;
+  const u32 m0 = info->minute_min + a;
+  const int L = base3_len(m0);
+  u64 code = minute_code(m0);
+  for (u32 k = 0; k < per; ++k) {
+    if (dp[a + k]) {
+      ck[pos] = code;  // owner 0
+      xr[pos] = (int32_t)dx[a + k];
+      ++pos;
+    }
+    // code of the next minute: base-3 increment on the digit fields (d + 1 in 1..3)
+    for (int i = L - 1; i >= 0; --i) {
+      const int sh = 2 * (CODE_DIGITS - 1 - i);
+      const u64 v = (code >> sh) & 3u;
+      if (v < 3) {
+        code += 1ull << sh;
+        break;
+      }
+      code -= 2ull << sh;  // 3 -> 1, carry on
+    }
+  }
 }
 
 // Fallback fold input (rare: wide minute range or mixed key lengths).
@@ -802,9 +793,9 @@ __global__ void k_cl_fold_ck(const uint8_t* __restrict__ flags, const u32* __res
     ml = max(ml, (u32)__shfl_xor(ml, d, 64));
   }
   if ((threadIdx.x & 63) == 0 && mx >= mn) {
-    atomicMin(&info->ck_min, mn);
-    atomicMax(&info->ck_max, mx);
-    atomicMax(&info->maxlen, ml);
+    atomic_min_if(&info->ck_min, mn);
+    atomic_max_if(&info->ck_max, mx);
+    atomic_max_if(&info->maxlen, ml);
   }
 }
 
@@ -831,65 +822,68 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   const size_t G = (n + range - 1) / range;
   const int cbits = C > 1 ? 32 - __builtin_clz(C - 1) : 0;
   uint4* key = S.alloc<uint4>(n);
-  u32* meta = S.alloc<u32>(n);
+  u32* rl = S.alloc<u32>(n);
   u32* hash = S.alloc<u32>(n);
   u32* minute = S.alloc<u32>(n);
   u64* a_tc = S.alloc<u64>(G * C);
-  u64* a_node = S.alloc<u64>(G * C);
-  u32* a_mask = S.alloc<u32>(G * C);
+  u64* a_rh = S.alloc<u64>(G * C);
+  u32* a_rl = S.alloc<u32>(G * C);
   u32* a_first = S.alloc<u32>(G * C);
-  if (!key || !meta || !hash || !minute || !a_tc || !a_node || !a_mask || !a_first) return EVM_ENOMEM;
+  if (!key || !rl || !hash || !minute || !a_tc || !a_rh || !a_rl || !a_first) return EVM_ENOMEM;
   // K1: parse, canonical check, murmur3, minute -- at full occupancy
-  KLAUNCH(k_cl_pack, dim3(std::min<size_t>((n + 255) / 256, 2048)), dim3(CLP_THREADS), (const uint8_t*)ts, stride, n,
-          cell, C, key, meta, hash, minute, info);
+  {
+    evm::ProfScope ps_(ctx, "k_cl_pack");
+    const dim3 g(std::min<size_t>((n + 255) / 256, 2048));
+    if (stride == 48)
+      hipLaunchKernelGGL(k_cl_pack<true>, g, dim3(CLP_THREADS), 0, ctx->stream, (const uint8_t*)ts, stride, n, key,
+                         rl, hash, minute, info);
+    else
+      hipLaunchKernelGGL(k_cl_pack<false>, g, dim3(CLP_THREADS), 0, ctx->stream, (const uint8_t*)ts, stride, n, key,
+                         rl, hash, minute, info);
+  }
   const size_t lds = (size_t)C * 24;
   {
     evm::ProfScope ps_(ctx, "k_cl_pass<1>");
-    hipLaunchKernelGGL((k_cl_pass<1>), dim3(G), dim3(64), lds, ctx->stream, key, meta, cell, n, C, cbits, range, a_tc,
-                       a_node, a_mask, a_first, (uint8_t*)nullptr);
+    hipLaunchKernelGGL((k_cl_pass<1>), dim3(G), dim3(64), lds, ctx->stream, key, rl, cell, n, C, cbits, range, a_tc,
+                       a_rh, a_rl, a_first, (uint8_t*)nullptr, info);
   }
-  // cross-cell PK check: partition by hash, LDS hash set per bucket
-  int kb = 1;  // ~5k messages per bucket
-  while (kb < 14 && ((size_t)5000 << kb) < n) ++kb;
+  // cross-cell PK check: partition by hash into fixed-capacity buckets, LDS set per bucket
+  int kb = 0;
+  while (kb < XP_MAX_KB && (n >> kb) > XP_AVG) ++kb;
+  const size_t avg = (n >> kb) + 1;
+  const u32 cap = (u32)std::min<size_t>(XP_MAX_FILL, avg + avg / 8 + 1024);
   const u32 xt = (u32)((n + XP_TILE - 1) / XP_TILE);
-  const size_t nbt = ((size_t)1 << kb) * xt;
-  u32* xcnt = S.alloc<u32>(nbt);
-  u32* xoff = S.alloc<u32>(nbt);
-  u64* xpairs = S.alloc<u64>(n);
-  if (!xcnt || !xoff || !xpairs) return EVM_ENOMEM;
-  {
-    evm::ProfScope ps_(ctx, "k_xp_hist");
-    hipLaunchKernelGGL(k_xp_hist, dim3(xt), dim3(XP_THREADS), sizeof(u32) << kb, ctx->stream, hash, n, kb, xcnt, xt);
-  }
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, xcnt, nbt, xoff, (u32*)nullptr))) return st;
+  u32* xcur = S.alloc<u32>((size_t)1 << kb);
+  u64* xpairs = S.alloc<u64>(((size_t)cap) << kb);
+  if (!xcur || !xpairs) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(xcur, 0, sizeof(u32) << kb, ctx->stream));
   {
     evm::ProfScope ps_(ctx, "k_xp_scatter");
-    hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), sizeof(u32) << kb, ctx->stream, hash, n, kb, xoff, xt,
-                       xpairs);
+    hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), 0, ctx->stream, hash, n, kb, cap, xcur, xpairs, info);
   }
   {
     evm::ProfScope ps_(ctx, "k_xp_dedup");
-    hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(256), sizeof(u64) * XP_SLOTS, ctx->stream, xpairs, xoff, xt, kb,
-                       n, (const uint8_t*)ts, stride, cell, info);
+    hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, ctx->stream, xpairs, xcur, cap, n,
+                       (const uint8_t*)ts, stride, cell, info);
   }
   // carry: per cell, exclusive scan over ranges seeded with the prior max
   {
     u64* s_tc = S.alloc<u64>((size_t)CARRY_SEGS * C);
-    u64* s_node = S.alloc<u64>((size_t)CARRY_SEGS * C);
-    u32* s_mask = S.alloc<u32>((size_t)CARRY_SEGS * C);
+    u64* s_rh = S.alloc<u64>((size_t)CARRY_SEGS * C);
+    u32* s_rl = S.alloc<u32>((size_t)CARRY_SEGS * C);
     u32* s_first = S.alloc<u32>((size_t)CARRY_SEGS * C);
-    if (!s_tc || !s_node || !s_mask || !s_first) return EVM_ENOMEM;
+    if (!s_tc || !s_rh || !s_rl || !s_first) return EVM_ENOMEM;
     const u32 cb = (C + 63) / 64;
-    KLAUNCH(k_cl_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_node, a_mask, a_first, s_tc, s_node, s_mask,
+    KLAUNCH(k_cl_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh, s_rl,
             s_first);
-    KLAUNCH(k_cl_carry_segs, dim3(cb), dim3(64), C, s_tc, s_node, s_mask, s_first, prior, prior_present, winner);
-    KLAUNCH(k_cl_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_node, a_mask, a_first, s_tc, s_node,
-            s_mask);
+    KLAUNCH(k_cl_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_tc, s_rh, s_rl, s_first, prior, prior_present, winner);
+    KLAUNCH(k_cl_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh,
+            s_rl);
   }
   {
     evm::ProfScope ps_(ctx, "k_cl_pass<2>");
-    hipLaunchKernelGGL((k_cl_pass<2>), dim3(G), dim3(64), lds, ctx->stream, key, meta, cell, n, C, cbits, range, a_tc,
-                       a_node, a_mask, a_first, flags);
+    hipLaunchKernelGGL((k_cl_pass<2>), dim3(G), dim3(64), lds, ctx->stream, key, rl, cell, n, C, cbits, range, a_tc,
+                       a_rh, a_rl, a_first, flags, info);
   }
   // Merkle fold
   u32* px = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN);
@@ -897,14 +891,12 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   const size_t B = (size_t)FOLD_MAXWIN * FOLD_WIN;
   u32* dx = S.alloc<u32>(B);
   u32* dp = S.alloc<u32>(B);
-  u32* pos = S.alloc<u32>(B);
   u64* lck = S.alloc<u64>(B);
   int32_t* lxr = S.alloc<int32_t>(B);
-  if (!px || !pp || !dx || !dp || !pos || !lck || !lxr) return EVM_ENOMEM;
+  if (!px || !pp || !dx || !dp || !lck || !lxr) return EVM_ENOMEM;
   KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
   KLAUNCH(k_cl_fold_reduce, dim3((B + 255) / 256), dim3(256), px, pp, info, dx, dp);
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, dp, B, pos, &info->n_leaves))) return st;
-  KLAUNCH(k_cl_leaves, dim3((B + 255) / 256), dim3(256), dx, dp, pos, info, lck, lxr);
+  KLAUNCH(k_cl_leaves, dim3(1), dim3(LEAF_THREADS), dx, dp, info, lck, lxr);
   Info hi;
   if ((st = read_info(ctx, info, &hi))) return st;
   if (hi.bad) {

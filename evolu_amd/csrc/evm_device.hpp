@@ -53,6 +53,7 @@ __device__ __forceinline__ int key_cmp_present(const Key& a, const Key& b) {
     return 0;
   }
   // Different case patterns (rare): first differing char decides by rank.
+#pragma unroll 1
   for (int i = 0; i < 16; ++i) {
     const u32 va = (u32)(a.node >> (60 - 4 * i)) & 15u;
     const u32 vb = (u32)(b.node >> (60 - 4 * i)) & 15u;
@@ -75,12 +76,58 @@ __device__ __forceinline__ bool key_eq(const Key& a, const Key& b) {
 __device__ __forceinline__ Key key_max(const Key& a, const Key& b) { return key_cmp(a, b) >= 0 ? a : b; }
 
 // ----------------------------------------------------------------------------
+// Order key: the raw-string order as three unsigned words, no case loop.
+//   tc  = millis << 16 | counter
+//   rh  = ranks of node chars 0..11, 5 bits each (rank: '0'-'9' 0-9,
+//         'A'-'F' 10-15, 'a'-'f' 16-21 = ASCII order of the bytes)
+//   rl  = ranks of node chars 12..15 (20 bits) | OKEY_PRESENT
+// (tc, rh, rl) compare lexicographically exactly as the 46-byte strings, and
+// are equal iff the strings are; the all-zero key is NULL, below every
+// present key.  The streaming client path carries only this.
+// ----------------------------------------------------------------------------
+constexpr u32 OKEY_PRESENT = 0x80000000u;
+struct OKey {
+  u64 tc;
+  u64 rh;
+  u32 rl;
+};
+__device__ __forceinline__ OKey okey_none() { return OKey{0ull, 0ull, 0u}; }
+__device__ __forceinline__ bool okey_gt(const OKey& a, const OKey& b) {
+  return a.tc != b.tc ? a.tc > b.tc : (a.rh != b.rh ? a.rh > b.rh : a.rl > b.rl);
+}
+__device__ __forceinline__ bool okey_eq(const OKey& a, const OKey& b) {
+  return a.tc == b.tc && a.rh == b.rh && a.rl == b.rl;
+}
+__device__ __forceinline__ OKey okey_max(const OKey& a, const OKey& b) { return okey_gt(b, a) ? b : a; }
+
+// (node, case mask) -> (rh, rl without the present bit).
+__host__ __device__ __forceinline__ void node_rank(u64 node, u32 mask, u64* rh, u32* rl) {
+  u64 h = 0;
+  u32 l = 0;
+  for (int i = 0; i < 16; ++i) {
+    const u32 v = (u32)(node >> (60 - 4 * i)) & 15u;
+    const u32 r = v + ((v >= 10u && !((mask >> i) & 1u)) ? 6u : 0u);
+    if (i < 12) h = (h << 5) | r;
+    else l = (l << 5) | r;
+  }
+  *rh = h;
+  *rl = l;
+}
+__device__ __forceinline__ OKey okey_of(const evm_rec& r) {
+  OKey k;
+  k.tc = r.tc;
+  node_rank(r.node, r.meta & EVM_META_CASEMASK, &k.rh, &k.rl);
+  k.rl |= OKEY_PRESENT;
+  return k;
+}
+
+// ----------------------------------------------------------------------------
 // MurmurHash3_x86_32, seed 0, specialised to 46 bytes = 11 blocks + 2-byte tail.
 // w[0..11] are the string's little-endian 32-bit words (w[11] holds bytes 44,45).
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
+__host__ __device__ __forceinline__ u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
 
-__device__ __forceinline__ u32 murmur3_46(const u32 (&w)[12]) {
+__host__ __device__ __forceinline__ u32 murmur3_46(const u32 (&w)[12]) {
   const u32 c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
   u32 h = 0u;
 #pragma unroll
@@ -104,20 +151,45 @@ __device__ __forceinline__ u32 murmur3_46(const u32 (&w)[12]) {
 }
 
 // ----------------------------------------------------------------------------
-// Parse + canonical check of one 46-byte timestamp.
+// Parse + canonical check of one 46-byte timestamp, word-parallel (SWAR).
+//
+// The string is twelve little-endian words; every byte class test runs on a
+// whole word at once, all date arithmetic is 32-bit with multiply-shift
+// division (year <= 9999), and the minute comes straight from the fields, so
+// no 64-bit division is left on the hot path.
+//   w0 YYYY  w1 -MM-  w2 DDTH  w3 H:mm  w4 :ss.  w5 sssZ  w6 -CCC  w7 C-NN
+//   w8..w10 NNNN  w11 NN (low half)
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ u32 byte_at(const u32 (&w)[12], int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xffu; }
+__host__ __device__ __forceinline__ u32 byte_at(const u32 (&w)[12], int k) {
+  return (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+}
 
-__device__ __forceinline__ bool is_digit(u32 c) { return c - 0x30u < 10u; }
+// Per byte: 0x80 where byte >= n, else 0 (every byte < 0x80, n <= 0x80).
+__host__ __device__ __forceinline__ u32 swar_ge(u32 x, u32 n) {
+  return ((x | 0x80808080u) - 0x01010101u * n) & 0x80808080u;
+}
+__host__ __device__ __forceinline__ u32 swar_digit(u32 x) { return swar_ge(x, 0x30) & ~swar_ge(x, 0x3a); }
+__host__ __device__ __forceinline__ u32 swar_upper(u32 x) { return swar_ge(x, 0x41) & ~swar_ge(x, 0x47); }
+__host__ __device__ __forceinline__ u32 swar_lower(u32 x) { return swar_ge(x, 0x61) & ~swar_ge(x, 0x67); }
 
-// Days since 1970-01-01 of a proleptic Gregorian date (y >= 1970 here).
-__device__ __forceinline__ int64_t days_from_civil(int y, int m, int d) {
-  y -= m <= 2;
-  const int era = y / 400;  // y >= 0 on the native path
-  const int yoe = y - era * 400;
-  const int doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
-  const int doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
-  return (int64_t)era * 146097 + doe - 719468;
+// Four hex chars (first char in the low byte) -> their 16-bit value; any case.
+__host__ __device__ __forceinline__ u32 swar_nibbles(u32 x) {  // per byte: hex value of the char
+  return (x & 0x0f0f0f0fu) + ((x >> 6) & 0x01010101u) * 9u;
+}
+__host__ __device__ __forceinline__ u32 swar_hex16(u32 x) {
+  const u32 v = swar_nibbles(x);
+  const u32 t = (v << 4) | (v >> 8);  // byte0 = c0<<4|c1, byte2 = c2<<4|c3
+  return ((t & 0xffu) << 8) | ((t >> 16) & 0xffu);
+}
+// Four node chars -> their four 5-bit ranks, first char most significant.
+__host__ __device__ __forceinline__ u32 swar_rank20(u32 x) {
+  const u32 r = swar_nibbles(x) + (swar_lower(x) >> 7) * 6u;  // lower-case letters rank above upper
+  return ((r & 0xffu) << 15) | (((r >> 8) & 0xffu) << 10) | (((r >> 16) & 0xffu) << 5) | (r >> 24);
+}
+// 0x80-per-byte flags -> 4 bits (byte k -> bit k).
+__host__ __device__ __forceinline__ u32 swar_bits4(u32 f) {
+  const u32 m = f >> 7;
+  return (m | (m >> 7) | (m >> 14) | (m >> 21)) & 0xfu;
 }
 
 // Millis below this bound give an int32 minute, so `(millis/1000/60)|0`
@@ -130,78 +202,88 @@ struct Parsed {
   u32 meta;
   u32 hash;
   u32 minute;
+  u64 rh;  // order key words (OKey); rl without OKEY_PRESENT
+  u32 rl;
 };
 
-__device__ __forceinline__ Parsed parse_ts46(const u32 (&w)[12]) {
-  Parsed p;
-  bool ok = true;
-  // separators
-  ok &= byte_at(w, 4) == '-' && byte_at(w, 7) == '-' && byte_at(w, 10) == 'T' && byte_at(w, 13) == ':' &&
-        byte_at(w, 16) == ':' && byte_at(w, 19) == '.' && byte_at(w, 23) == 'Z' && byte_at(w, 24) == '-' &&
-        byte_at(w, 29) == '-';
-  // decimal fields
-  u32 dig[17];
-  const int dpos[17] = {0, 1, 2, 3, 5, 6, 8, 9, 11, 12, 14, 15, 17, 18, 20, 21, 22};
-#pragma unroll
-  for (int i = 0; i < 17; ++i) {
-    const u32 c = byte_at(w, dpos[i]);
-    ok &= is_digit(c);
-    dig[i] = c - 0x30u;
-  }
-  const int year = dig[0] * 1000 + dig[1] * 100 + dig[2] * 10 + dig[3];
-  const int mon = dig[4] * 10 + dig[5];
-  const int day = dig[6] * 10 + dig[7];
-  const int hh = dig[8] * 10 + dig[9];
-  const int mi = dig[10] * 10 + dig[11];
-  const int ss = dig[12] * 10 + dig[13];
-  const int sss = dig[14] * 100 + dig[15] * 10 + dig[16];
-  const bool leap = (year % 4 == 0 && year % 100 != 0) || year % 400 == 0;
-  int dim = 31;
-  if (mon == 4 || mon == 6 || mon == 9 || mon == 11) dim = 30;
-  if (mon == 2) dim = leap ? 29 : 28;
-  ok &= mon >= 1 && mon <= 12 && day >= 1 && day <= dim && hh <= 23 && mi <= 59 && ss <= 59;
-  // counter: exactly 4 upper-case hex digits (canonical form of toString(16).toUpperCase())
-  u32 counter = 0;
-#pragma unroll
-  for (int i = 25; i < 29; ++i) {
-    const u32 c = byte_at(w, i);
-    const bool d = is_digit(c), u = c - 0x41u < 6u;
-    ok &= d || u;
-    counter = counter * 16u + (d ? c - 0x30u : c - 0x37u);
-  }
+__host__ __device__ __forceinline__ u32 mul24(u32 a, u32 b) { return a * b; }  // a, b < 2^24: v_mul_u32_u24
+
+__host__ __device__ __forceinline__ Parsed parse_ts46(const u32 (&w)[12]) {
+  // byte classes: separators by template, digits / hex by SWAR ranges
+  const u32 hi = (w[0] | w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7] | w[8] | w[9] | w[10] | (w[11] & 0xffffu)) &
+                 0x80808080u;
+  bool ok = hi == 0;
+  ok &= (w[1] & 0xff0000ffu) == 0x2d00002du && (w[2] & 0x00ff0000u) == 0x00540000u &&
+        (w[3] & 0x0000ff00u) == 0x00003a00u && (w[4] & 0xff0000ffu) == 0x2e00003au &&
+        (w[5] & 0xff000000u) == 0x5a000000u && (w[6] & 0xffu) == 0x2du && (w[7] & 0xff00u) == 0x2d00u;
+  ok &= swar_digit(w[0]) == 0x80808080u && (swar_digit(w[1]) & 0x00808000u) == 0x00808000u &&
+        (swar_digit(w[2]) & 0x80008080u) == 0x80008080u && (swar_digit(w[3]) & 0x80800080u) == 0x80800080u &&
+        (swar_digit(w[4]) & 0x00808000u) == 0x00808000u && (swar_digit(w[5]) & 0x00808080u) == 0x00808080u;
+  // counter: exactly 4 upper-case hex digits (canonical toString(16).toUpperCase())
+  const u32 cw = (w[6] >> 8) | (w[7] << 24);
+  ok &= (swar_digit(cw) | swar_upper(cw)) == 0x80808080u;
   // node: 16 hex digits, either case (types.ts:42 /^[0-9a-f]{16}$/i)
-  u64 node = 0;
-  u32 mask = 0;
+  u32 nw[4];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const u32 c = byte_at(w, 30 + i);
-    const bool d = is_digit(c), u = c - 0x41u < 6u, l = c - 0x61u < 6u;
-    ok &= d || u || l;
-    const u32 v = d ? c - 0x30u : (u ? c - 0x37u : c - 0x57u);
-    node = (node << 4) | v;
-    mask |= (u ? 1u : 0u) << i;
+  for (int k = 0; k < 4; ++k) nw[k] = (w[7 + k] >> 16) | (w[8 + k] << 16);
+  u32 mask = 0;
+  u64 node = 0, rh = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const u32 up = swar_upper(nw[k]);
+    ok &= (swar_digit(nw[k]) | up | swar_lower(nw[k])) == 0x80808080u;
+    mask |= swar_bits4(up) << (4 * k);
+    node = (node << 16) | swar_hex16(nw[k]);
+    if (k < 3) rh = (rh << 20) | swar_rank20(nw[k]);
   }
+  const u32 counter = swar_hex16(cw);
+  // decimal fields (digits already checked; garbage values only when !ok)
+  const u32 d0 = w[0] - 0x30303030u;
+  const u32 year = mul24(mul24(d0 & 0xffu, 10u) + ((d0 >> 8) & 0xffu), 100u) +
+                   mul24((d0 >> 16) & 0xffu, 10u) + (d0 >> 24);
+  auto two = [](u32 x, int sh) { return mul24((x >> sh) & 0xffu, 10u) + ((x >> (sh + 8)) & 0xffu) - 528u; };
+  const u32 mon = two(w[1], 8), day = two(w[2], 0), mi = two(w[3], 16), ss = two(w[4], 8);
+  const u32 hh = mul24((w[2] >> 24) - 0x30u, 10u) + (w[3] & 0xffu) - 0x30u;
+  const u32 sss = mul24(mul24(w[5] & 0xffu, 10u) + ((w[5] >> 8) & 0xffu), 10u) + ((w[5] >> 16) & 0xffu) - 5328u;
+  // calendar: leap year and month length without division
+  const u32 cent = mul24(year, 5243u) >> 19;  // year / 100 for year < 43699
+  const bool leap = (year & 3u) == 0 && (year != mul24(cent, 100u) || (cent & 3u) == 0);
+  constexpr u32 MLEN = (3u << 2) | (0u << 4) | (3u << 6) | (2u << 8) | (3u << 10) | (2u << 12) | (3u << 14) |
+                       (3u << 16) | (2u << 18) | (3u << 20) | (2u << 22) | (3u << 24);  // month length - 28, by 2*mon
+  const bool mon_ok = mon - 1u < 12u;
+  const u32 dim = 28u + ((MLEN >> (2u * (mon & 15u))) & 3u) + ((mon == 2u && leap) ? 1u : 0u);
+  ok &= mon_ok && day - 1u < dim && hh <= 23u && mi <= 59u && ss <= 59u;
   u32 meta = mask;
-  u64 millis = 0;
   u32 minute = 0;
+  u64 millis = 0;
   if (!ok) {
     meta |= EVM_META_NONCANON;
-  } else if (year < 1970) {
+  } else if (year < 1970u) {
     meta |= EVM_META_RANGE;
   } else {
-    millis = (u64)(((days_from_civil(year, mon, day) * 24 + hh) * 60 + mi) * 60 + ss) * 1000ull + (u64)sss;
-    if (millis >= NATIVE_MILLIS_END) {
+    // days since 1970-01-01 (March-based year): 365y + y/4 - y/100 + y/400 + doy - 719468
+    const u32 y = year - (mon <= 2u ? 1u : 0u);
+    const u32 yc = mul24(y, 5243u) >> 19;
+    const u32 mp = mon > 2u ? mon - 3u : mon + 9u;
+    const u32 doy = (mul24(mul24(mp, 153u) + 2u, 52429u) >> 18) + day - 1u;  // (153 mp + 2) / 5
+    const u32 days = mul24(y, 365u) + (y >> 2) - yc + (yc >> 2) + doy - 719468u;
+    const u32 m32 = mul24(days, 1440u) + mul24(hh, 60u) + mi;  // < 2^32 for year <= 9999
+    if (m32 >= 0x80000000u) {
       meta |= EVM_META_RANGE;
     } else {
       meta |= EVM_META_VALID;
-      minute = (u32)(millis / 60000ull);
+      minute = m32;
+      millis = (u64)m32 * 60000ull + (mul24(ss, 1000u) + sss);
     }
   }
+  Parsed p;
   p.tc = (millis << 16) | counter;
   p.node = node;
   p.meta = meta;
   p.hash = (meta & EVM_META_VALID) ? murmur3_46(w) : 0u;
   p.minute = minute;
+  p.rh = rh;
+  p.rl = swar_rank20(nw[3]);
   return p;
 }
 

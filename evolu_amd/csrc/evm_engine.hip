@@ -59,11 +59,11 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack(const uint8_t* __restrict
     mx = max(mx, (u32)__shfl_xor(mx, d, 64));
   }
   if ((threadIdx.x & 63) == 0 && info) {
-    if (bad) atomicOr(&info->bad, 1u);
-    if (bad_aux) atomicOr(&info->bad_aux, 1u);
+    if (bad) atomic_or_if(&info->bad, 1u);
+    if (bad_aux) atomic_or_if(&info->bad_aux, 1u);
     if (mn != 0xffffffffu) {
-      atomicMin(&info->minute_min, mn);
-      atomicMax(&info->minute_max, mx);
+      atomic_min_if(&info->minute_min, mn);
+      atomic_max_if(&info->minute_max, mx);
     }
   }
 }
@@ -158,9 +158,9 @@ __global__ void k_fold_prep(const evm_rec* __restrict__ rec, const uint8_t* __re
     maxlen = max(maxlen, (u32)__shfl_xor(maxlen, d, 64));
   }
   if ((threadIdx.x & 63) == 0 && mx >= mn) {
-    atomicMin(&info->ck_min, mn);
-    atomicMax(&info->ck_max, mx);
-    atomicMax(&info->maxlen, maxlen);
+    atomic_min_if(&info->ck_min, mn);
+    atomic_max_if(&info->ck_max, mx);
+    atomic_max_if(&info->maxlen, maxlen);
   }
 }
 
@@ -490,6 +490,7 @@ int evm_create(int device, evm_ctx** out) {
 void evm_destroy(evm_ctx* ctx) {
   if (!ctx) return;
   prof_drain(ctx);
+  for (hipEvent_t e : ctx->prof_pool) (void)hipEventDestroy(e);
   if (ctx->xtab) (void)hipFree(ctx->xtab);
   if (ctx->ws) (void)hipFree(ctx->ws);
   (void)hipStreamDestroy(ctx->own);
@@ -533,8 +534,8 @@ static void prof_drain(evm_ctx* ctx) {
       float ms = 0.f;
       if (hipEventElapsedTime(&ms, ev.first, ev.second) == hipSuccess) tot.first += ms;
       tot.second += 1;
-      (void)hipEventDestroy(ev.first);
-      (void)hipEventDestroy(ev.second);
+      ctx->prof_pool.push_back(ev.first);
+      ctx->prof_pool.push_back(ev.second);
     }
   }
   ctx->prof_events.clear();

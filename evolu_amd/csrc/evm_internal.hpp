@@ -19,6 +19,7 @@ struct evm_ctx {
   int client_path = 0;  // EVM_OPT_CLIENT_PATH
   std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> prof_events;
   std::map<std::string, std::pair<double, uint64_t>> prof_total;  // ms, launches (drained)
+  std::vector<hipEvent_t> prof_pool;  // recycled events: no hipEventCreate inside a timed loop
   // persistent hash set for the cross-cell timestamp check (epoch-tagged slots)
   unsigned long long* xtab = nullptr;
   int xtab_lg = 0;
@@ -138,10 +139,16 @@ class Scratch {
 class ProfScope {
  public:
   ProfScope(evm_ctx* c, const char* name) : ctx_(c), name_(name) {
-    if (ctx_->prof && hipEventCreate(&a_) == hipSuccess && hipEventCreate(&b_) == hipSuccess)
+    if (!ctx_->prof) return;
+    a_ = take();
+    b_ = take();
+    if (a_ && b_) {
       (void)hipEventRecord(a_, ctx_->stream);
-    else
+    } else {
+      if (a_) ctx_->prof_pool.push_back(a_);
+      if (b_) ctx_->prof_pool.push_back(b_);
       a_ = b_ = nullptr;
+    }
   }
   ~ProfScope() {
     if (a_ && b_) {
@@ -151,6 +158,15 @@ class ProfScope {
   }
 
  private:
+  hipEvent_t take() {
+    if (!ctx_->prof_pool.empty()) {
+      hipEvent_t e = ctx_->prof_pool.back();
+      ctx_->prof_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+  }
   evm_ctx* ctx_;
   const char* name_;
   hipEvent_t a_ = nullptr, b_ = nullptr;

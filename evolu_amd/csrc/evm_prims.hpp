@@ -19,6 +19,74 @@ __device__ __forceinline__ u64 lanemask_lt() {
 }
 
 // ----------------------------------------------------------------------------
+// Status bounds (Info.minute_min & co.).  Same-address atomics from every wave
+// serialise at the memory side (a min+max per wave made the pack kernel 2-5x
+// slower at 2-8k blocks): reduce over the block first, then touch the global
+// word only when this block's value improves on what is already stored.
+// ----------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const T o = __shfl_xor(v, d, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const T o = __shfl_xor(v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ void atomic_min_if(T* p, T v) {
+  if (v < __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(p, v);
+}
+template <typename T>
+__device__ __forceinline__ void atomic_max_if(T* p, T v) {
+  if (v > __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(p, v);
+}
+template <typename T>
+__device__ __forceinline__ void atomic_or_if(T* p, T v) {
+  if ((v & ~__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0) atomicOr(p, v);
+}
+
+// Block-wide min / max / or of one (mn, mx, flags) triple per thread, folded
+// into the global words by thread 0.  Every thread of the block must call it.
+template <typename T, int THREADS>
+__device__ __forceinline__ void block_fold_bounds(T mn, T mx, u32 flags, T* gmin, T* gmax, u32* gflags) {
+  __shared__ T s_mn[THREADS / 64], s_mx[THREADS / 64];
+  __shared__ u32 s_fl[THREADS / 64];
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  const bool any = __ballot(flags != 0) != 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_mn[w] = mn;
+    s_mx[w] = mx;
+    s_fl[w] = any ? 1u : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 fl = 0;
+    for (int k = 0; k < THREADS / 64; ++k) {
+      mn = s_mn[k] < mn ? s_mn[k] : mn;
+      mx = s_mx[k] > mx ? s_mx[k] : mx;
+      fl |= s_fl[k];
+    }
+    if (fl && gflags) atomic_or_if(gflags, 1u);
+    if (mx >= mn) {
+      atomic_min_if(gmin, mn);
+      atomic_max_if(gmax, mx);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
 // Exclusive scan.  Op is a functor with `static T id()` and `T operator()(T,T)`.
 // ----------------------------------------------------------------------------
 template <typename T>
@@ -180,8 +248,16 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(const K* __restr
                                                                 K* __restrict__ kout, u32* __restrict__ vout, size_t n,
                                                                 int shift, int bits, const u32* __restrict__ offsets,
                                                                 u32 ntiles) {
+  // ranks: per-wave running digit counters + 64-lane ballot match (stable);
+  // the tile is then staged in LDS in digit order and written back with
+  // consecutive lanes on consecutive addresses inside each digit run.
   __shared__ u32 wcnt[SORT_THREADS / WAVE][RADIX_BINS];
   __shared__ u32 toff[RADIX_BINS];
+  __shared__ u32 lstart[RADIX_BINS];
+  __shared__ u32 scan_tmp[SORT_THREADS / WAVE + 1];
+  __shared__ K skey[SORT_TILE];
+  __shared__ u32 sval[SORT_TILE];
+  static_assert(RADIX_BINS <= SORT_THREADS, "one digit per thread in the tile scan");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const u32 nbins = 1u << bits, mask = nbins - 1u;
   for (u32 d = threadIdx.x; d < nbins; d += SORT_THREADS) {
@@ -190,7 +266,8 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(const K* __restr
     for (int ww = 0; ww < SORT_THREADS / WAVE; ++ww) wcnt[ww][d] = 0;
   }
   __syncthreads();
-  const size_t wbase = (size_t)blockIdx.x * SORT_TILE + (size_t)w * WAVE * SORT_ITEMS;
+  const size_t tbase = (size_t)blockIdx.x * SORT_TILE;
+  const size_t wbase = tbase + (size_t)w * WAVE * SORT_ITEMS;
   K key[SORT_ITEMS];
   u32 val[SORT_ITEMS], dig[SORT_ITEMS], rank[SORT_ITEMS];
   const u64 lt = lanemask_lt();
@@ -216,24 +293,39 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(const K* __restr
     }
   }
   __syncthreads();
-  for (u32 d = threadIdx.x; d < nbins; d += SORT_THREADS) {
-    u32 acc = toff[d];
+  // per digit: exclusive prefix over waves, tile total, then the tile's digit starts
+  u32 tot = 0;
+  {
+    const u32 d = threadIdx.x;
+    if (d < nbins) {
 #pragma unroll
-    for (int ww = 0; ww < SORT_THREADS / WAVE; ++ww) {
-      const u32 t = wcnt[ww][d];
-      wcnt[ww][d] = acc;
-      acc += t;
+      for (int ww = 0; ww < SORT_THREADS / WAVE; ++ww) {
+        const u32 t = wcnt[ww][d];
+        wcnt[ww][d] = tot;
+        tot += t;
+      }
     }
   }
+  const u32 incl = block_inclusive_scan<u32>(tot, scan_tmp, OpAdd<u32>(), (u32*)nullptr);
+  if (threadIdx.x < nbins) lstart[threadIdx.x] = incl - tot;
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {
     const size_t i = wbase + (size_t)r * WAVE + lane;
     if (i < n) {
-      const u32 dst = wcnt[w][dig[r]] + rank[r];
-      kout[dst] = key[r];
-      vout[dst] = val[r];
+      const u32 lp = lstart[dig[r]] + wcnt[w][dig[r]] + rank[r];
+      skey[lp] = key[r];
+      sval[lp] = val[r];
     }
+  }
+  __syncthreads();
+  const u32 m = (u32)min((size_t)SORT_TILE, n - tbase);
+  for (u32 t = threadIdx.x; t < m; t += SORT_THREADS) {
+    const K k = skey[t];
+    const u32 d = digit_of(k, shift, mask);
+    const u32 dst = toff[d] + (t - lstart[d]);
+    kout[dst] = k;
+    vout[dst] = sval[t];
   }
 }
 

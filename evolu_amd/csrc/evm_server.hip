@@ -97,64 +97,130 @@ __device__ __forceinline__ size_t store_lower(const StoreView& s, size_t a, size
 }
 
 // ---------------------------------------------------------------- sort fields
-enum Field { F_LO = 0, F_HI = 1, F_TC = 2, F_OWNER = 3 };
+enum Field { F_LO = 0, F_HI = 1, F_TC = 2, F_OWNER = 3, F_MS = 4, F_CTR = 5, N_FIELDS = 6 };
+
+__device__ __forceinline__ u64 field_of(const SKey& k, int f) {
+  return f == F_LO ? (u64)k.lo : f == F_HI ? k.hi : f == F_TC ? k.tc : f == F_OWNER ? (u64)k.owner
+         : f == F_MS ? k.tc >> 16 : k.tc & 0xffffu;
+}
 
 __global__ void k_sv_field(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, size_t n, int field,
                            u64* __restrict__ out) {
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    const SKey k = skey_of(rec[perm[p]]);
-    out[p] = field == F_LO ? (u64)k.lo : field == F_HI ? k.hi : field == F_TC ? k.tc : (u64)k.owner;
-  }
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
+    out[p] = field_of(skey_of(rec[perm[p]]), field);
 }
 
 // min / max of every field over the batch (decides the radix bits per field)
 struct FieldRange {
-  u64 mn[4];
-  u64 mx[4];
+  u64 mn[N_FIELDS];
+  u64 mx[N_FIELDS];
 };
 
 __global__ void k_sv_ranges(const evm_rec* __restrict__ rec, size_t n, FieldRange* __restrict__ fr) {
-  u64 mn[4] = {~0ull, ~0ull, ~0ull, ~0ull}, mx[4] = {0, 0, 0, 0};
+  u64 mn[N_FIELDS], mx[N_FIELDS];
+#pragma unroll
+  for (int f = 0; f < N_FIELDS; ++f) {
+    mn[f] = ~0ull;
+    mx[f] = 0;
+  }
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const SKey k = skey_of(rec[i]);
-    const u64 v[4] = {(u64)k.lo, k.hi, k.tc, (u64)k.owner};
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      mn[f] = min(mn[f], v[f]);
-      mx[f] = max(mx[f], v[f]);
+    for (int f = 0; f < N_FIELDS; ++f) {
+      const u64 v = field_of(k, f);
+      mn[f] = min(mn[f], v);
+      mx[f] = max(mx[f], v);
     }
   }
 #pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    for (int d = 32; d >= 1; d >>= 1) {
-      mn[f] = min(mn[f], (u64)__shfl_xor(mn[f], d, 64));
-      mx[f] = max(mx[f], (u64)__shfl_xor(mx[f], d, 64));
-    }
+  for (int f = 0; f < N_FIELDS; ++f) {
+    mn[f] = wave_min(mn[f]);
+    mx[f] = wave_max(mx[f]);
   }
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      atomicMin(&fr->mn[f], mn[f]);
-      atomicMax(&fr->mx[f], mx[f]);
+    for (int f = 0; f < N_FIELDS; ++f) {
+      atomic_min_if(&fr->mn[f], mn[f]);
+      atomic_max_if(&fr->mx[f], mx[f]);
     }
+  }
+}
+
+// Compound sort key (owner - omin : ob | millis - mmin : mb | counter : cb),
+// when ob + mb + cb <= 64: one radix sort orders the batch by (owner, tc);
+// equal compound keys (same owner and tc, different node) are then ordered
+// by the node ranks in k_sv_ties.
+struct CKey {
+  u64 omin, mmin;
+  int mb, cb;
+};
+__global__ void k_sv_ckey(const evm_rec* __restrict__ rec, size_t n, CKey ck, u64* __restrict__ key,
+                          u32* __restrict__ perm) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const evm_rec r = rec[i];
+    key[i] = (((u64)r.aux - ck.omin) << (ck.mb + ck.cb)) | (((r.tc >> 16) - ck.mmin) << ck.cb) | (r.tc & 0xffffu);
+    perm[i] = (u32)i;
+  }
+}
+
+constexpr int TIE_MAX = 64;
+// Runs of equal compound keys: stable insertion sort of the run by the node
+// ranks (the batch index order inside the run is the radix sort's).  A run
+// longer than TIE_MAX flags the slow (full-field) sort.
+__global__ void k_sv_ties(const u64* __restrict__ key, u32* __restrict__ perm, const evm_rec* __restrict__ rec,
+                          size_t n, u32* __restrict__ too_long) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x + 1; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    if (key[p] != key[p - 1] || (p >= 2 && key[p - 2] == key[p - 1])) continue;  // not a run start (at p - 1)
+    const size_t s = p - 1;
+    size_t e = p + 1;
+    while (e < n && key[e] == key[s] && e - s <= TIE_MAX) ++e;
+    if (e - s > TIE_MAX) {
+      atomicOr(too_long, 1u);
+      continue;
+    }
+    u32 idx[TIE_MAX];
+    u64 hi[TIE_MAX];
+    u32 lo[TIE_MAX];
+    const int L = (int)(e - s);
+    for (int k = 0; k < L; ++k) {
+      const u32 i = perm[s + k];
+      const SKey sk = skey_of(rec[i]);
+      int j = k;
+      while (j > 0 && (hi[j - 1] > sk.hi || (hi[j - 1] == sk.hi && lo[j - 1] > sk.lo))) {
+        idx[j] = idx[j - 1];
+        hi[j] = hi[j - 1];
+        lo[j] = lo[j - 1];
+        --j;
+      }
+      idx[j] = i;
+      hi[j] = sk.hi;
+      lo[j] = sk.lo;
+    }
+    for (int k = 0; k < L; ++k) perm[s + k] = idx[k];
   }
 }
 
 // ------------------------------------------------------------ dedup + marks
 // Sorted order p: first occurrence of (owner, timestamp) in batch order (the
 // sort is stable on the batch index) that the store does not hold yet.
-__global__ void k_sv_mark(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, size_t n, StoreView st,
-                          uint8_t* __restrict__ flags, u32* __restrict__ sel) {
+__global__ void k_sv_mark(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u64* __restrict__ skeys,
+                          size_t n, StoreView st, uint8_t* __restrict__ flags, u32* __restrict__ sel) {
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
     const u32 i = perm[p];
-    const SKey k = skey_of(rec[i]);
     bool first = true;
-    if (p > 0) first = skey_cmp(skey_of(rec[perm[p - 1]]), k) != 0;
+    if (p > 0) {
+      // sorted compound keys differ => the timestamps differ (no gathers)
+      if (!skeys || skeys[p] == skeys[p - 1]) first = skey_cmp(skey_of(rec[perm[p - 1]]), skey_of(rec[i])) != 0;
+    }
     bool ins = first;
     if (ins) {
-      const size_t a = st.off[k.owner], b = st.off[k.owner + 1];
-      const size_t q = store_lower(st, a, b, k);
-      ins = !(q < b && skey_cmp(skey_at(st, q), k) == 0);
+      const u32 owner = rec[i].aux;
+      const size_t a = st.off[owner], b = st.off[owner + 1];
+      if (a < b) {
+        const SKey k = skey_of(rec[i]);
+        const size_t q = store_lower(st, a, b, k);
+        ins = !(q < b && skey_cmp(skey_at(st, q), k) == 0);
+      }
     }
     flags[i] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
     sel[p] = ins ? 1u : 0u;
@@ -404,7 +470,7 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
     if (!rec || !perm || !fv || !fr) return EVM_ENOMEM;
     if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) return st;
     FieldRange h0;
-    for (int f = 0; f < 4; ++f) {
+    for (int f = 0; f < N_FIELDS; ++f) {
       h0.mn[f] = ~0ull;
       h0.mx[f] = 0;
     }
@@ -422,18 +488,45 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
       (void)evm_sync(ctx);
       return EVM_ENONCANON;
     }
-    // stable LSD sort of the batch index by (owner, tc, rank_hi, rank_lo)
-    if ((st = launch_iota(ctx, perm, n))) return st;
-    const int order[4] = {F_LO, F_HI, F_TC, F_OWNER};
-    for (int f : order) {
-      const u64 d = hr.mn[f] ^ hr.mx[f];
-      if (!d) continue;
-      const int hb = 64 - __builtin_clzll(d);
-      KLAUNCH(k_sv_field, dim3(grid_for(n, 256)), dim3(256), rec, perm, n, f, fv);
+    auto bits_of = [](u64 d) { return d ? 64 - __builtin_clzll(d) : 0; };
+    const int ob = bits_of(hr.mx[F_OWNER] - hr.mn[F_OWNER]), mb = bits_of(hr.mx[F_MS] - hr.mn[F_MS]),
+              cb = bits_of(hr.mx[F_CTR]);
+    const u64* skeys = nullptr;
+    bool sorted = false;
+    if (ob + mb + cb <= 64) {
+      // one radix sort on the compound (owner, millis, counter) key, then node-rank ties
       u64* kk = fv;
       u32* vv = perm;
-      if ((st = radix_sort_pairs<u64>(ctx, S, kk, vv, n, 0, hb))) return st;
-      if (vv != perm) HIPR(hipMemcpyAsync(perm, vv, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
+      const CKey ck{hr.mn[F_OWNER], hr.mn[F_MS], mb, cb};
+      KLAUNCH(k_sv_ckey, dim3(grid_for(n, 256)), dim3(256), rec, n, ck, kk, vv);
+      if ((st = radix_sort_pairs<u64>(ctx, S, kk, vv, n, 0, ob + mb + cb))) return st;
+      u32* tl = S.alloc<u32>(1);
+      if (!tl) return EVM_ENOMEM;
+      HIPR(hipMemsetAsync(tl, 0, sizeof(u32), ctx->stream));
+      KLAUNCH(k_sv_ties, dim3(grid_for(n, 256)), dim3(256), kk, vv, rec, n, tl);
+      u32 too_long = 0;
+      HIPR(hipMemcpyAsync(&too_long, tl, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+      HIPR(hipStreamSynchronize(ctx->stream));
+      if (!too_long) {
+        if (vv != perm) HIPR(hipMemcpyAsync(perm, vv, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
+        skeys = kk;  // sorted compound keys (scratch lives until the end of the call)
+        sorted = true;
+      }
+    }
+    if (!sorted) {
+      // stable LSD sort of the batch index by (owner, tc, rank_hi, rank_lo), field by field
+      if ((st = launch_iota(ctx, perm, n))) return st;
+      const int order[4] = {F_LO, F_HI, F_TC, F_OWNER};
+      for (int f : order) {
+        const u64 d = hr.mn[f] ^ hr.mx[f];
+        if (!d) continue;
+        const int hb = 64 - __builtin_clzll(d);
+        KLAUNCH(k_sv_field, dim3(grid_for(n, 256)), dim3(256), rec, perm, n, f, fv);
+        u64* kk = fv;
+        u32* vv = perm;
+        if ((st = radix_sort_pairs<u64>(ctx, S, kk, vv, n, 0, hb))) return st;
+        if (vv != perm) HIPR(hipMemcpyAsync(perm, vv, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
+      }
     }
     // dedup within the batch and against the store
     u32* sel = S.alloc<u32>(n);
@@ -441,7 +534,7 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
     u32* cnt = S.alloc<u32>(2);
     if (!sel || !pos || !cnt) return EVM_ENOMEM;
     const StoreView old = view_of(s);
-    KLAUNCH(k_sv_mark, dim3(grid_for(n, 256)), dim3(256), rec, perm, n, old, flags, sel);
+    KLAUNCH(k_sv_mark, dim3(grid_for(n, 256)), dim3(256), rec, perm, skeys, n, old, flags, sel);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, pos, cnt))) return st;
     u32 m = 0;
     HIPR(hipMemcpyAsync(&m, cnt, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));

@@ -160,3 +160,32 @@ def test_ingest_many_owners_scale(eng):
     assert (f2.cpu().numpy() == 0).all() and store.n_messages == len(ts_np)
     r2, _ = store.tree().roots()
     assert np.array_equal(r1, r2)
+
+
+@pytest.mark.parametrize("run", [3, 64, 65, 200])
+def test_ingest_tie_runs(eng, run):
+    """Runs of equal (owner, millis, counter) with distinct nodes (mixed case):
+    ordered by the node bytes; runs longer than the tie fix-up's limit take
+    the full-field sort.  Checked against the oracle's message table."""
+    from evolu_amd import _lib as L
+
+    rng = random.Random(run)
+    owners = ["%021x" % rng.getrandbits(84) for _ in range(3)]
+    reqs = []
+    for k, o in enumerate(owners):
+        nodes = {W.node_id(rng, upper=rng.random() < 0.5) for _ in range(run)}
+        ms = [O.timestamp_to_string(W.T0 + 7 * k, 3, nd) for nd in nodes]
+        ms += [O.timestamp_to_string(W.T0 + 7 * k + 1, 0, nd) for nd in list(nodes)[:5]]
+        rng.shuffle(ms)
+        reqs.append((o, ms + ms[:3]))  # in-request duplicates too
+    store, flags, id_ts = _run_batches(eng, owners, [reqs])
+    db, ins = _oracle(owners, [reqs])
+    assert [bool(x & L.MSG_INS) for x in flags[0]] == ins[0]
+    off, ids = store.messages()
+    for i, o in enumerate(owners):
+        rows = db.conn.execute('SELECT "timestamp" FROM "message" WHERE "userId" = ? ORDER BY "timestamp"',
+                               (o,)).fetchall()
+        assert [id_ts[int(k)] for k in ids[off[i]:off[i + 1]]] == [r[0] for r in rows]
+    tree = store.tree()
+    for i, o in enumerate(owners):
+        assert tree.to_json(i) == O.merkle_tree_to_string(db.get_merkle_tree(o))
