@@ -33,6 +33,9 @@ MSG_BAD = 0x80
 
 OPT_CLIENT_PATH = 1
 
+PB_SYNC_REQUEST = 1
+PB_SYNC_RESPONSE = 2
+
 DIFF_NONE = -1
 DIFF_RANGE_ERROR = -2
 
@@ -78,6 +81,10 @@ SIGNATURES = {
     "evm_store_tree": (_vp, [_vp]),
     "evm_store_messages": (_i, [_vp, _vp, _vp, _vp]),
     "evm_server_ingest": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, C.c_uint64, _vp]),
+    "evm_pb_scan": (_i, [_i, _vp, _sz, _vp]),
+    "evm_pb_split": (_i, [_i, _vp, _sz, _vp, _sz, _vp, _vp, _vp]),
+    "evm_pb_encode": (_i, [_i, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _sz, C.POINTER(_sz)]),
+    "evm_store_since": (_i, [_vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_server_select": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_apply_batch": (
         _i,

@@ -346,8 +346,8 @@ __global__ void k_sv_sel_count(StoreView st, u32 n_owners, const int64_t* __rest
     if (active && !active[o]) continue;
     const int64_t d = diff[o];
     if (d < 0) continue;  // none or RangeError
-    u64 req;
-    if (!parse_node16(node + 16 * (size_t)o, &req)) {
+    u64 req = 0;
+    if (node && !parse_node16(node + 16 * (size_t)o, &req)) {
       atomicOr(bad, 1u);
       continue;
     }
@@ -358,7 +358,11 @@ __global__ void k_sv_sel_count(StoreView st, u32 n_owners, const int64_t* __rest
     if (q < b && skey_cmp(skey_at(st, q), since) == 0) ++q;  // strictly greater
     first[o] = q;
     u32 c = 0;
-    for (size_t k = q; k < b; ++k) c += node_hex_of(st.hi[k], st.lo[k]) != req;  // NOT LIKE '%' || nodeId
+    if (node) {
+      for (size_t k = q; k < b; ++k) c += node_hex_of(st.hi[k], st.lo[k]) != req;  // NOT LIKE '%' || nodeId
+    } else {
+      c = (u32)(b - q);
+    }
     cnt[o] = c;
   }
 }
@@ -368,11 +372,11 @@ __global__ void k_sv_sel_write(StoreView st, const u64* __restrict__ id, u32 n_o
                                u64* __restrict__ sel_id) {
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
     if (!cnt[o]) continue;
-    u64 req;
-    parse_node16(node + 16 * (size_t)o, &req);
+    u64 req = 0;
+    if (node) parse_node16(node + 16 * (size_t)o, &req);
     u64 w = pos[o];
     for (size_t k = first[o], b = st.off[o + 1]; k < b; ++k)
-      if (node_hex_of(st.hi[k], st.lo[k]) != req) sel_id[w++] = id[k];
+      if (!node || node_hex_of(st.hi[k], st.lo[k]) != req) sel_id[w++] = id[k];
   }
 }
 
@@ -602,19 +606,14 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
   return evm_sync(ctx);
 }
 
-int evm_server_select(evm_ctx* ctx, const evm_store* s, const evm_tree* client, const char* node,
-                      const uint8_t* active, int64_t* diff, uint64_t* sel_off, uint64_t* sel_id, uint64_t cap,
-                      uint64_t* n_sel) {
-  if (!ctx || !s || !client || !node || !diff || !sel_off || !n_sel) return EVM_EINVAL;
-  if (client->n_owners != s->n_owners) return EVM_EINVAL;
+}  // extern "C"
+
+// Selection of each owner's rows after a per-owner bound (diff/since, < 0 =
+// none), optionally excluding one node (server getMessages).
+static int select_after(evm_ctx* ctx, Scratch& S, const evm_store* s, const int64_t* bound, const char* node,
+                        const uint8_t* active, uint64_t* sel_off, uint64_t* sel_id, uint64_t cap, uint64_t* n_sel) {
   const u32 O = s->n_owners;
-  if (O == 0) {
-    *n_sel = 0;
-    return EVM_OK;
-  }
   int st;
-  Scratch S(ctx);
-  if ((st = launch_diff(ctx, s->tree, client, diff))) return st;
   u64* first = S.alloc<u64>(O);
   u32* cnt = S.alloc<u32>(O);
   u32* pos = S.alloc<u32>(O);
@@ -622,7 +621,7 @@ int evm_server_select(evm_ctx* ctx, const evm_store* s, const evm_tree* client, 
   if (!first || !cnt || !pos || !tot) return EVM_ENOMEM;
   HIPR(hipMemsetAsync(tot, 0, 2 * sizeof(u32), ctx->stream));
   const StoreView v = view_of(s);
-  KLAUNCH(k_sv_sel_count, dim3(grid_for(O, 64, 65536)), dim3(64), v, O, diff, (const uint8_t*)node, active, first, cnt,
+  KLAUNCH(k_sv_sel_count, dim3(grid_for(O, 64, 65536)), dim3(64), v, O, bound, (const uint8_t*)node, active, first, cnt,
           tot + 1);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, cnt, O, pos, tot))) return st;
   KLAUNCH(k_u32_to_u64, dim3(grid_for(O + 1, 256)), dim3(256), pos, (size_t)O, tot, (u64*)sel_off);
@@ -635,6 +634,34 @@ int evm_server_select(evm_ctx* ctx, const evm_store* s, const evm_tree* client, 
   KLAUNCH(k_sv_sel_write, dim3(grid_for(O, 64, 65536)), dim3(64), v, (const u64*)s->id, O, first, cnt, pos,
           (const uint8_t*)node, (u64*)sel_id);
   return evm_sync(ctx);
+}
+
+extern "C" {
+
+int evm_server_select(evm_ctx* ctx, const evm_store* s, const evm_tree* client, const char* node,
+                      const uint8_t* active, int64_t* diff, uint64_t* sel_off, uint64_t* sel_id, uint64_t cap,
+                      uint64_t* n_sel) {
+  if (!ctx || !s || !client || !node || !diff || !sel_off || !n_sel) return EVM_EINVAL;
+  if (client->n_owners != s->n_owners) return EVM_EINVAL;
+  if (s->n_owners == 0) {
+    *n_sel = 0;
+    return EVM_OK;
+  }
+  int st;
+  Scratch S(ctx);
+  if ((st = launch_diff(ctx, s->tree, client, diff))) return st;
+  return select_after(ctx, S, s, diff, node, active, sel_off, sel_id, cap, n_sel);
+}
+
+int evm_store_since(evm_ctx* ctx, const evm_store* s, const int64_t* since, uint64_t* sel_off, uint64_t* sel_id,
+                    uint64_t cap, uint64_t* n_sel) {
+  if (!ctx || !s || !since || !sel_off || !n_sel) return EVM_EINVAL;
+  if (s->n_owners == 0) {
+    *n_sel = 0;
+    return EVM_OK;
+  }
+  Scratch S(ctx);
+  return select_after(ctx, S, s, since, nullptr, nullptr, sel_off, sel_id, cap, n_sel);
 }
 
 }  // extern "C"

@@ -253,6 +253,21 @@ class Store:
                                              _ptr(off), _ptr(ids), cap, C.byref(nsel)), "evm_server_select")
         return diff[:O], off, ids[: nsel.value]
 
+    def since(self, since: torch.Tensor, cap: int = None):
+        """receive.ts:118-124 resend range, batched over owners: for since[o] >= 0
+        the owner's ids with timestamp > syncTs(since[o]), in timestamp order.
+        -> (sel_off uint64[n_owners+1], sel_id uint64[n_sel])."""
+        dev = since.device
+        O = self.n_owners
+        since = since.to(torch.int64).contiguous()
+        off = torch.empty(O + 1, dtype=torch.int64, device=dev)
+        cap = self.n_messages if cap is None else cap
+        ids = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        nsel = C.c_uint64()
+        check(self.eng.lib.evm_store_since(self.eng.h, self.h, _ptr(since), _ptr(off), _ptr(ids), cap,
+                                           C.byref(nsel)), "evm_store_since")
+        return off, ids[: nsel.value]
+
 
 class Trees:
     """A device-resident set of per-owner MerkleTrees (owns its evm_tree)."""

@@ -20,6 +20,11 @@
  *                         + Merkle fold; the SQL writes stay with the caller)
  *   evm_server_ingest ... apps/server/src/index.ts:138-171 addMessages
  *   evm_server_select ... apps/server/src/index.ts:173-202 getMessages
+ *   evm_pb_* ............ protobuf.ts:60-171 SyncRequest / SyncResponse
+ *                         fromBinary / toBinary (host codec)
+ *   evm_store_since ..... receive.ts:106-142 handleMerkleTreesDiff's resend
+ *                         range (SELECT ... "timestamp" > ? ORDER BY
+ *                         "timestamp"), batched over owners
  *   evm_tree_to_json /
  *   evm_tree_from_json .. types.ts:80-84 merkleTreeToString / FromString
  */
@@ -202,9 +207,50 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
  * nodeId; 16 hex chars); active: device uint8 [n_owners] (NULL: all).
  * Outputs (device): diff[n_owners] (EVM_DIFF_NONE / millis / RANGE_ERROR),
  * sel_off[n_owners + 1], sel_id[cap]; *n_sel = total selected.            */
+/* receive.ts:118-124 (client resend after a diff) / index.ts:98-102 without
+ * the node filter: per owner o with since[o] >= 0, the stored messages with
+ * timestamp > timestampToString(createSyncTimestamp(since[o])), in timestamp
+ * order.  A store fed with the client's inserted messages (owner 0) mirrors
+ * its "__message" table.  since: device int64 [n_owners] (< 0: none).
+ * Outputs as evm_server_select: sel_off[n_owners + 1], sel_id[cap], *n_sel.  */
+int evm_store_since(evm_ctx* ctx, const evm_store* s, const int64_t* since, uint64_t* sel_off, uint64_t* sel_id,
+                    uint64_t cap, uint64_t* n_sel);
+
 int evm_server_select(evm_ctx* ctx, const evm_store* s, const evm_tree* client, const char* node,
                       const uint8_t* active, int64_t* diff, uint64_t* sel_off, uint64_t* sel_id, uint64_t cap,
                       uint64_t* n_sel);
+
+/* ---------------------------------------------------------------- wire codec
+ * protobuf.proto SyncRequest / SyncResponse (protobuf.ts:60-171), HOST
+ * buffers (this is the request body the server receives, index.ts:115, and
+ * the response it sends, index.ts:239).  Encoding omits proto3 defaults and
+ * writes fields in number order (protobuf-ts toBinary); decoding skips
+ * unknown fields and rejects truncated / ill-typed input (EVM_EINVAL).     */
+#define EVM_PB_SYNC_REQUEST 1
+#define EVM_PB_SYNC_RESPONSE 2
+typedef struct evm_pb_sync {
+  uint64_t n_messages;
+  uint64_t content_bytes;      /* sum of the messages' content lengths */
+  uint64_t user_off, user_len; /* SyncRequest.userId, as bytes of buf */
+  uint64_t node_off, node_len; /* SyncRequest.nodeId */
+  uint64_t tree_off, tree_len; /* merkleTree (JSON) */
+  uint64_t nonstd_ts;          /* messages whose timestamp is not 46 bytes */
+} evm_pb_sync;
+/* Pass 1: sizes and the string fields' positions. */
+int evm_pb_scan(int kind, const uint8_t* buf, size_t len, evm_pb_sync* info);
+/* Pass 2: timestamps into the engine's arena (ts[n * stride]; a timestamp
+ * that is not 46 bytes is written as 0xFF bytes so the engine flags it;
+ * ts_len[n] optional), contents concatenated (content_off[n + 1], content
+ * may be NULL to get offsets only). */
+int evm_pb_split(int kind, const uint8_t* buf, size_t len, char* ts, size_t stride, uint32_t* ts_len,
+                 uint64_t* content_off, uint8_t* content);
+/* Encode n messages (ts rows of ts_len[i] bytes, NULL: 46; contents by
+ * content_off) + the string fields (user/node only for a request).  out NULL
+ * or too small: *out_len = bytes needed (EVM_ECAPACITY if out was given). */
+int evm_pb_encode(int kind, const char* ts, size_t stride, const uint32_t* ts_len, size_t n,
+                  const uint64_t* content_off, const uint8_t* content, const char* user, size_t user_len,
+                  const char* node, size_t node_len, const char* tree, size_t tree_len, uint8_t* out, size_t cap,
+                  size_t* out_len);
 
 #ifdef __cplusplus
 }

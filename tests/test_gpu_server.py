@@ -189,3 +189,42 @@ def test_ingest_tie_runs(eng, run):
     tree = store.tree()
     for i, o in enumerate(owners):
         assert tree.to_json(i) == O.merkle_tree_to_string(db.get_merkle_tree(o))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_store_since_resend_range(eng, seed):
+    """receive.ts:118-124: SELECT * FROM "__message" WHERE "timestamp" > ?
+    ORDER BY "timestamp", with ? = timestampToString(createSyncTimestamp(d)),
+    on a store mirroring each owner's message table (sqlite3 as the checker)."""
+    import sqlite3
+
+    owners, pools, reqs = _requests(300 + seed)
+    store, flags, id_ts = _run_batches(eng, owners, [reqs])
+    db, _ = _oracle(owners, [reqs])
+    rng = random.Random(seed)
+    since = []
+    for o in owners:
+        ts_o = sorted(t for t in pools[o])
+        pick = rng.random()
+        if pick < 0.15:
+            since.append(-1)
+        elif pick < 0.3:
+            since.append(0)
+        else:
+            since.append(O.parse_canonical(rng.choice(ts_o))[0] + rng.choice([-1, 0, 0, 1]))
+    off, ids = store.since(torch_tensor(eng, since))
+    off, ids = off.cpu().numpy(), ids.cpu().numpy()
+    for i, o in enumerate(owners):
+        if since[i] < 0:
+            assert off[i + 1] == off[i]
+            continue
+        bound = O.timestamp_to_string(since[i], 0, "0000000000000000")
+        rows = db.conn.execute('SELECT "timestamp" FROM "message" WHERE "userId" = ? AND "timestamp" > ? '
+                               'ORDER BY "timestamp"', (o, bound)).fetchall()
+        assert [id_ts[int(k)] for k in ids[off[i]:off[i + 1]]] == [r[0] for r in rows]
+
+
+def torch_tensor(eng, values):
+    import torch
+
+    return torch.tensor(values, dtype=torch.int64, device=eng.device)
