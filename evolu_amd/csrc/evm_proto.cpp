@@ -199,7 +199,7 @@ int evm_pb_scan(int kind, const uint8_t* buf, size_t len, evm_pb_sync* info) {
 }
 
 int evm_pb_split(int kind, const uint8_t* buf, size_t len, char* ts, size_t stride, uint32_t* ts_len,
-                 uint64_t* content_off, uint8_t* content) {
+                 uint64_t* ts_off, uint64_t* content_off, uint8_t* content) {
   if (stride < 46 || !ts || !content_off) return EVM_EINVAL;
   uint64_t coff = 0;
   content_off[0] = 0;
@@ -210,6 +210,7 @@ int evm_pb_split(int kind, const uint8_t* buf, size_t len, char* ts, size_t stri
     else memset(row, 0xff, 46);
     memset(row + 46, 0, stride - 46);
     if (ts_len) ts_len[i] = (uint32_t)(m.ts_len > 0xffffffffu ? 0xffffffffu : m.ts_len);
+    if (ts_off) ts_off[i] = m.ts ? (uint64_t)(m.ts - buf) : 0;
     if (content && m.content_len) memcpy(content + coff, m.content, m.content_len);
     coff += m.content_len;
     content_off[i + 1] = coff;

@@ -31,6 +31,7 @@ class Sync:
     content_off: np.ndarray  # (n + 1,) uint64
     content: bytes
     tree: str
+    raw: Optional[List[str]] = None  # the timestamp strings as sent (any length)
     user: Optional[str] = None
     node: Optional[str] = None
 
@@ -53,11 +54,14 @@ def decode(kind: int, body: bytes, stride: int = TS_STRIDE) -> Sync:
     ts_len = np.zeros(n, dtype=np.uint32)
     off = np.zeros(n + 1, dtype=np.uint64)
     content = np.zeros(max(info.content_bytes, 1), dtype=np.uint8)
+    ts_off = np.zeros(n, dtype=np.uint64)
     check(lib.evm_pb_split(kind, buf, len(body), ts.ctypes.data_as(C.c_void_p), stride,
-                           ts_len.ctypes.data_as(C.c_void_p), off.ctypes.data_as(C.c_void_p),
+                           ts_len.ctypes.data_as(C.c_void_p), ts_off.ctypes.data_as(C.c_void_p),
+                           off.ctypes.data_as(C.c_void_p),
                            content.ctypes.data_as(C.c_void_p)), "evm_pb_split")
     s = lambda o, k: body[o:o + k].decode("utf-8", "replace")  # noqa: E731
-    out = Sync(ts, ts_len, off, content[: info.content_bytes].tobytes(), s(info.tree_off, info.tree_len))
+    out = Sync(ts, ts_len, off, content[: info.content_bytes].tobytes(), s(info.tree_off, info.tree_len),
+               raw=[body[int(o):int(o) + int(k)].decode("utf-8", "replace") for o, k in zip(ts_off, ts_len)])
     if kind == REQUEST:
         out.user = s(info.user_off, info.user_len)
         out.node = s(info.node_off, info.node_len)

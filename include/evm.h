@@ -240,10 +240,11 @@ typedef struct evm_pb_sync {
 int evm_pb_scan(int kind, const uint8_t* buf, size_t len, evm_pb_sync* info);
 /* Pass 2: timestamps into the engine's arena (ts[n * stride]; a timestamp
  * that is not 46 bytes is written as 0xFF bytes so the engine flags it;
- * ts_len[n] optional), contents concatenated (content_off[n + 1], content
- * may be NULL to get offsets only). */
+ * optional ts_len[n] and ts_off[n] = the original string's bytes in buf),
+ * contents concatenated (content_off[n + 1]; content may be NULL to get
+ * offsets only). */
 int evm_pb_split(int kind, const uint8_t* buf, size_t len, char* ts, size_t stride, uint32_t* ts_len,
-                 uint64_t* content_off, uint8_t* content);
+                 uint64_t* ts_off, uint64_t* content_off, uint8_t* content);
 /* Encode n messages (ts rows of ts_len[i] bytes, NULL: 46; contents by
  * content_off) + the string fields (user/node only for a request).  out NULL
  * or too small: *out_len = bytes needed (EVM_ECAPACITY if out was given). */

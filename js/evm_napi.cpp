@@ -344,6 +344,159 @@ napi_value ServerSelect(napi_env env, napi_callback_info info) {
   return res;
 }
 
+// storeSince(ctx, store, since Float64Array(nOwners), -1 = none) -> { off, ids } (Float64Arrays)
+// receive.ts:118-124 resend range over a store that mirrors "__message"
+napi_value StoreSince(napi_env env, napi_callback_info info) {
+  napi_value a[3];
+  if (!get_args(env, info, 3, a)) return nullptr;
+  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
+  const evm_store* s = (const evm_store*)ext(env, a[1]);
+  void* sv;
+  size_t sl;
+  if (!bytes_of(env, a[2], &sv, &sl)) return nullptr;
+  uint32_t no = 0;
+  uint64_t nm = 0;
+  evm_store_info(s, &no, &nm);
+  if (sl != 8ull * no) return throw_status(env, EVM_EINVAL, "storeSince: one since per owner");
+  std::vector<int64_t> since(no);
+  for (uint32_t i = 0; i < no; ++i) since[i] = (int64_t)((const double*)sv)[i];
+  Dev ds(ctx, 8 * (no ? no : 1), since.data()), doff(ctx, 8 * (no + 1)), dids(ctx, 8 * (nm ? nm : 1));
+  uint64_t nsel = 0;
+  const int st = evm_store_since(ctx, s, (const int64_t*)ds.p, (uint64_t*)doff.p, (uint64_t*)dids.p, nm, &nsel);
+  if (st) return throw_status(env, st, "evm_store_since");
+  std::vector<uint64_t> ho(no + 1), hi(nsel);
+  evm_copy_d2h(ctx, ho.data(), doff.p, 8 * (no + 1));
+  evm_copy_d2h(ctx, hi.data(), dids.p, 8 * nsel);
+  napi_value res;
+  napi_create_object(env, &res);
+  double* p;
+  napi_value x = typed(env, napi_float64_array, no + 1, 8, (void**)&p);
+  for (uint32_t i = 0; i <= no; ++i) p[i] = (double)ho[i];
+  napi_set_named_property(env, res, "off", x);
+  x = typed(env, napi_float64_array, nsel, 8, (void**)&p);
+  for (uint64_t i = 0; i < nsel; ++i) p[i] = (double)hi[i];
+  napi_set_named_property(env, res, "ids", x);
+  return res;
+}
+
+// receiveFold(ctx, ts Uint8Array, stride, millis, counter, node string, now, maxDrift)
+//   -> { error, index, next, millis, counter }     (receive.ts:45-66)
+napi_value ReceiveFold(napi_env env, napi_callback_info info) {
+  napi_value a[8];
+  if (!get_args(env, info, 8, a)) return nullptr;
+  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
+  void* ts;
+  size_t tl;
+  if (!bytes_of(env, a[1], &ts, &tl)) return nullptr;
+  const size_t stride = u32(env, a[2]);
+  double millis = 0, now = 0, drift = 0;
+  napi_get_value_double(env, a[3], &millis);
+  napi_get_value_double(env, a[6], &now);
+  napi_get_value_double(env, a[7], &drift);
+  char node[17] = {0};
+  size_t nl = 0;
+  NAPI_OK(env, napi_get_value_string_latin1(env, a[5], node, sizeof node, &nl));
+  if (nl != 16) return throw_status(env, EVM_EINVAL, "receiveFold: nodeId must be 16 chars");
+  Dev dts(ctx, tl, ts);
+  evm_clock_result r;
+  const int st = evm_receive_fold(ctx, (const char*)dts.p, stride, stride ? tl / stride : 0, (int64_t)millis,
+                                  u32(env, a[4]), node, (int64_t)now, (int64_t)drift, &r);
+  if (st) return throw_status(env, st, "evm_receive_fold");
+  napi_value res, v;
+  napi_create_object(env, &res);
+  const double vals[5] = {(double)r.error, (double)r.error_index, (double)r.next, (double)r.millis,
+                          (double)r.counter};
+  const char* names[5] = {"error", "index", "next", "millis", "counter"};
+  for (int k = 0; k < 5; ++k) {
+    napi_create_double(env, vals[k], &v);
+    napi_set_named_property(env, res, names[k], v);
+  }
+  return res;
+}
+
+// pbDecode(kind, body Uint8Array) -> { ts Uint8Array(n * 48), tsLen, contentOff (Float64Array), content,
+//   userId, nodeId, merkleTree }      (SyncRequest / SyncResponse fromBinary)
+napi_value PbDecode(napi_env env, napi_callback_info info) {
+  napi_value a[2];
+  if (!get_args(env, info, 2, a)) return nullptr;
+  const int kind = (int)u32(env, a[0]);
+  void* body;
+  size_t bl;
+  if (!bytes_of(env, a[1], &body, &bl)) return nullptr;
+  evm_pb_sync si;
+  int st = evm_pb_scan(kind, (const uint8_t*)body, bl, &si);
+  if (st) return throw_status(env, st, "evm_pb_scan");
+  const size_t n = si.n_messages;
+  void *tsp, *tlp, *cp;
+  napi_value ts = typed(env, napi_uint8_array, n * 48, 1, &tsp);
+  napi_value tl = typed(env, napi_uint32_array, n, 4, &tlp);
+  napi_value content = typed(env, napi_uint8_array, si.content_bytes, 1, &cp);
+  std::vector<uint64_t> off(n + 1), toff(n);
+  st = evm_pb_split(kind, (const uint8_t*)body, bl, (char*)tsp, 48, (uint32_t*)tlp, toff.data(), off.data(),
+                    (uint8_t*)cp);
+  if (st) return throw_status(env, st, "evm_pb_split");
+  double* op;
+  napi_value co = typed(env, napi_float64_array, n + 1, 8, (void**)&op);
+  for (size_t i = 0; i <= n; ++i) op[i] = (double)off[i];
+  napi_value res, v;
+  napi_create_object(env, &res);
+  napi_set_named_property(env, res, "ts", ts);
+  napi_set_named_property(env, res, "tsLen", tl);
+  napi_set_named_property(env, res, "contentOff", co);
+  {
+    double* tp;
+    napi_value to = typed(env, napi_float64_array, n, 8, (void**)&tp);
+    for (size_t i = 0; i < n; ++i) tp[i] = (double)toff[i];
+    napi_set_named_property(env, res, "tsOff", to);
+  }
+  napi_set_named_property(env, res, "content", content);
+  const char* b = (const char*)body;
+  napi_create_string_utf8(env, b + si.tree_off, si.tree_len, &v);
+  napi_set_named_property(env, res, "merkleTree", v);
+  if (kind == EVM_PB_SYNC_REQUEST) {
+    napi_create_string_utf8(env, b + si.user_off, si.user_len, &v);
+    napi_set_named_property(env, res, "userId", v);
+    napi_create_string_utf8(env, b + si.node_off, si.node_len, &v);
+    napi_set_named_property(env, res, "nodeId", v);
+  }
+  return res;
+}
+
+std::string str_of(napi_env env, napi_value v) {
+  size_t n = 0;
+  napi_get_value_string_utf8(env, v, nullptr, 0, &n);
+  std::string s(n, '\0');
+  if (n) napi_get_value_string_utf8(env, v, &s[0], n + 1, &n);
+  return s;
+}
+
+// pbEncode(kind, ts Uint8Array(n * 48), content Uint8Array, contentOff Float64Array(n + 1),
+//          userId, nodeId, merkleTree) -> Uint8Array   (toBinary; 46-byte timestamps)
+napi_value PbEncode(napi_env env, napi_callback_info info) {
+  napi_value a[7];
+  if (!get_args(env, info, 7, a)) return nullptr;
+  const int kind = (int)u32(env, a[0]);
+  void *ts, *content, *offv;
+  size_t tl, cl, ol;
+  if (!bytes_of(env, a[1], &ts, &tl) || !bytes_of(env, a[2], &content, &cl) || !bytes_of(env, a[3], &offv, &ol))
+    return nullptr;
+  const size_t n = tl / 48;
+  if (ol != 8 * (n + 1)) return throw_status(env, EVM_EINVAL, "pbEncode: contentOff must have n + 1 entries");
+  std::vector<uint64_t> off(n + 1);
+  for (size_t i = 0; i <= n; ++i) off[i] = (uint64_t)((const double*)offv)[i];
+  const std::string user = str_of(env, a[4]), node = str_of(env, a[5]), tree = str_of(env, a[6]);
+  size_t need = 0;
+  int st = evm_pb_encode(kind, (const char*)ts, 48, nullptr, n, off.data(), (const uint8_t*)content, user.data(),
+                         user.size(), node.data(), node.size(), tree.data(), tree.size(), nullptr, 0, &need);
+  if (st) return throw_status(env, st, "evm_pb_encode");
+  void* out;
+  napi_value arr = typed(env, napi_uint8_array, need, 1, &out);
+  st = evm_pb_encode(kind, (const char*)ts, 48, nullptr, n, off.data(), (const uint8_t*)content, user.data(),
+                     user.size(), node.data(), node.size(), tree.data(), tree.size(), (uint8_t*)out, need, &need);
+  if (st) return throw_status(env, st, "evm_pb_encode");
+  return arr;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   const struct {
     const char* name;
@@ -352,7 +505,8 @@ napi_value Init(napi_env env, napi_value exports) {
              {"treeToJson", TreeToJson}, {"treeFree", TreeFree},     {"diff", Diff},
              {"insert", Insert},         {"applyBatch", ApplyBatch}, {"storeNew", StoreNew},
              {"storeFree", StoreFree},   {"storeTree", StoreTree},   {"serverIngest", ServerIngest},
-             {"serverSelect", ServerSelect}};
+             {"serverSelect", ServerSelect}, {"storeSince", StoreSince}, {"receiveFold", ReceiveFold},
+             {"pbDecode", PbDecode},         {"pbEncode", PbEncode}};
   for (const auto& f : fns) {
     napi_value v;
     napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.fn, nullptr, &v);

@@ -8,6 +8,9 @@
 //                            SQL writes stay with the caller's Database)
 //   Server#addMessages ..... apps/server/src/index.ts:138-171
 //   Server#getMessages ..... apps/server/src/index.ts:173-202
+//   Engine#receiveMessages . receive.ts:45-66 (the HLC fold over a batch)
+//   Engine#messagesSince ... receive.ts:118-124 (resend range, via a Server store)
+//   SyncRequest / SyncResponse fromBinary / toBinary .. protobuf.ts:60-171
 // Trees cross this boundary as MerkleTree JSON (types.ts:80-84), the format
 // the reference persists and sends.  Results the engine does not model
 // (non-canonical timestamps, a timestamp in two cells) return `null` so the
@@ -112,6 +115,55 @@ class Engine {
   }
 }
 
+Engine.prototype.receiveMessages = function (clock, timestamps, now, maxDrift = 60000) {
+  // receive.ts:45-66: fold receiveTimestamp over the batch; clock = {millis, counter, node}.
+  // -> { ok: true, clock } | { ok: false, type, index, next }
+  const r = addon.receiveFold(this.ctx, encodeTimestamps(timestamps), STRIDE, clock.millis, clock.counter, clock.node,
+    now, maxDrift);
+  if (r.error === 0) return { ok: true, clock: { millis: r.millis, counter: r.counter, node: clock.node } };
+  const type = ["", "TimestampDriftError", "TimestampDuplicateNodeError", "TimestampCounterOverflowError"][r.error];
+  return { ok: false, type, index: r.index, next: r.next };
+};
+
+// protobuf.ts:60-171 (protobuf-ts MessageType shape): fromBinary / toBinary
+const PB_REQUEST = 1;
+const PB_RESPONSE = 2;
+function pbMessages(r, body) {
+  const dec = new TextDecoder();
+  const out = [];
+  for (let i = 0; i < r.tsLen.length; i++) {
+    out.push({
+      timestamp: dec.decode(body.subarray(r.tsOff[i], r.tsOff[i] + r.tsLen[i])),
+      content: r.content.slice(r.contentOff[i], r.contentOff[i + 1]),
+    });
+  }
+  return out;
+}
+function pbEncode(kind, m) {
+  const msgs = m.messages || [];
+  const ts = encodeTimestamps(msgs.map((x) => x.timestamp));
+  if (msgs.some((x) => x.timestamp.length !== 46)) throw new RangeError("timestamps must be 46 chars");
+  const off = new Float64Array(msgs.length + 1);
+  msgs.forEach((x, i) => { off[i + 1] = off[i] + x.content.length; });
+  const content = new Uint8Array(off[msgs.length]);
+  msgs.forEach((x, i) => content.set(x.content, off[i]));
+  return addon.pbEncode(kind, ts, content, off, m.userId || "", m.nodeId || "", m.merkleTree || "");
+}
+const SyncRequest = {
+  fromBinary(body) {
+    const r = addon.pbDecode(PB_REQUEST, body);
+    return { messages: pbMessages(r, body), userId: r.userId, nodeId: r.nodeId, merkleTree: r.merkleTree };
+  },
+  toBinary(m) { return pbEncode(PB_REQUEST, m); },
+};
+const SyncResponse = {
+  fromBinary(body) {
+    const r = addon.pbDecode(PB_RESPONSE, body);
+    return { messages: pbMessages(r, body), merkleTree: r.merkleTree };
+  },
+  toBinary(m) { return pbEncode(PB_RESPONSE, m); },
+};
+
 // apps/server/src/index.ts: one store for many owners (userIds)
 class Server {
   constructor(engine, nOwners) {
@@ -147,6 +199,14 @@ class Server {
     for (let o = 0; o < this.nOwners; o++) ids.push(Array.from(r.ids.subarray(r.off[o], r.off[o + 1])));
     return { diff: Array.from(r.diff, (d) => (d === -1 ? null : d)), ids };
   }
+  // receive.ts:118-124 over this store as a "__message" mirror: since[o] millis | null -> ids[o][]
+  messagesSince(since) {
+    const s = Float64Array.from(since, (d) => (d == null ? -1 : d));
+    const r = addon.storeSince(this.engine.ctx, this.store, s);
+    const ids = [];
+    for (let o = 0; o < this.nOwners; o++) ids.push(Array.from(r.ids.subarray(r.off[o], r.off[o + 1])));
+    return ids;
+  }
 }
 
-module.exports = { Engine, Server, encodeTimestamps, MSG_UPS, MSG_XOR, MSG_INS };
+module.exports = { Engine, Server, SyncRequest, SyncResponse, encodeTimestamps, MSG_UPS, MSG_XOR, MSG_INS };

@@ -38,6 +38,9 @@ out.server = { ins: cases.server.batches.map((b) => srv.addMessages(b)) };
 out.server.trees = [];
 for (let o = 0; o < cases.server.nOwners; o++) out.server.trees.push(srv.merkleTree(o));
 out.server.get = srv.getMessages(cases.server.clientTrees, cases.server.nodeIds);
+out.server.since = srv.messagesSince(cases.server.since);
+// receive.ts:45-66 clock fold
+out.receive = cases.receive.map((c) => eng.receiveMessages(c.clock, c.timestamps, c.now));
 srv.close();
 eng.close();
 process.stdout.write(JSON.stringify(out));

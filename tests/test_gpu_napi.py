@@ -78,7 +78,31 @@ def test_js_entry_points(tmp_path):
         want_ins.append(got)
     client = [O.merkle_tree_to_string(O.insert_into_merkle_tree({}, O.parse_canonical(p[0]))) for p in pools]
     node_ids = [p[1][30:] for p in pools]
-    cases["server"] = {"nOwners": n_owners, "batches": batches, "clientTrees": client, "nodeIds": node_ids}
+    since = [None, 0, O.parse_canonical(sorted(pools[2])[10])[0], O.parse_canonical(sorted(pools[3])[-1])[0] + 1]
+    cases["server"] = {"nOwners": n_owners, "batches": batches, "clientTrees": client, "nodeIds": node_ids,
+                       "since": since}
+    # receive fold: ok, drift, duplicate node
+    rcases, rwant = [], []
+    for k, mode in enumerate(["ok", "drift", "dup"]):
+        node = "000000000000000%d" % (k + 1)
+        now = W.T0 + 1000
+        ts = W.hlc_timestamps(rng, 50, [W.node_id(rng) for _ in range(3)], t0=W.T0 - 5000, span=4000)
+        if mode == "drift":
+            ts.insert(20, O.timestamp_to_string(now + 60001, 0, W.node_id(rng)))
+        if mode == "dup":
+            ts.insert(30, O.timestamp_to_string(W.T0, 5, node))
+        clock = {"millis": W.T0 - 7000, "counter": 3, "node": node}
+        rcases.append({"clock": clock, "timestamps": ts, "now": now})
+        t = (clock["millis"], clock["counter"], node)
+        want = None
+        for i, s_ in enumerate(ts):
+            try:
+                t = O.receive_timestamp(t, O.parse_canonical(s_), now, 60000)
+            except O.TimestampError as e:
+                want = {"ok": False, "type": e.kind, "index": i}
+                break
+        rwant.append(want or {"ok": True, "clock": {"millis": t[0], "counter": t[1], "node": node}})
+    cases["receive"] = rcases
     f = tmp_path / "cases.json"
     f.write_text(json.dumps(cases))
     res = json.loads(subprocess.run(["node", os.path.join(ROOT, "js", "test_evm.js"), str(f)], check=True,
@@ -96,3 +120,14 @@ def test_js_entry_points(tmp_path):
         d, rows = sdb.get_messages(sdb.get_merkle_tree("u%d" % o), json.loads(client[o]), "u%d" % o, node_ids[o])
         assert res["server"]["get"]["diff"][o] == d
         assert len(res["server"]["get"]["ids"][o]) == len(rows)
+    id_ts = [m["timestamp"] for b in batches for r in b for m in r["messages"]]
+    for o in range(n_owners):
+        rows = [] if since[o] is None else sdb.conn.execute(
+            'SELECT "timestamp" FROM "message" WHERE "userId" = ? AND "timestamp" > ? ORDER BY "timestamp"',
+            ("u%d" % o, O.timestamp_to_string(since[o], 0, "0000000000000000"))).fetchall()
+        assert [id_ts[int(k)] for k in res["server"]["since"][o]] == [r[0] for r in rows]
+    for got, want in zip(res["receive"], rwant):
+        if want["ok"]:
+            assert got == want
+        else:
+            assert (got["ok"], got["type"], got["index"]) == (False, want["type"], want["index"])

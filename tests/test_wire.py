@@ -3,12 +3,18 @@ against google.protobuf built from the same schema: byte-identical encoding
 (proto3: defaults omitted, field-number order -- what protobuf-ts toBinary
 writes) and identical decoding, incl. unknown fields, reordering and
 truncation.  Host code only: runs without a GPU."""
+import json
+import os
 import random
+import shutil
+import subprocess
 
 import numpy as np
 import pytest
 
 from evolu_amd import wire
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _classes():
@@ -75,7 +81,7 @@ def test_encode_matches_protobuf(seed, kind):
     # and back
     d = wire.decode(kind, mine)
     assert d.contents() == contents and d.tree == tree
-    assert list(d.ts_len) == [len(t.encode()) for t in ts]
+    assert list(d.ts_len) == [len(t.encode()) for t in ts] and d.raw == ts
     for i, t in enumerate(ts):
         if len(t) == 46:
             assert bytes(d.ts[i, :46]).decode() == t
@@ -144,3 +150,36 @@ def test_empty_bodies():
     assert wire.encode(wire.RESPONSE, [], []) == b""
     d = wire.decode(wire.REQUEST, b"")
     assert len(d.ts_len) == 0 and d.user == "" and d.tree == ""
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "js", "evm_napi.node")) or shutil.which("node") is None,
+                    reason="N-API addon / node not available")
+def test_js_sync_codec_matches_protobuf(tmp_path):
+    """The JS shim's SyncRequest/SyncResponse.fromBinary/toBinary (N-API) vs google.protobuf."""
+    rng = random.Random(11)
+    ts, contents = _random_messages(rng, 60)
+    ts = [t if len(t) == 46 else "2024-02-02T00:00:00.000Z-0000-00000000000000%02x" % i for i, t in enumerate(ts)]
+    req = REQ(messages=[dict(timestamp=t, content=c) for t, c in zip(ts, contents)], userId="owner-1",
+              nodeId="0123456789abcdef", merkleTree='{"hash":7}')
+    (tmp_path / "req.bin").write_bytes(req.SerializeToString())
+    script = """
+const fs = require('fs');
+const { SyncRequest, SyncResponse } = require(%r);
+const body = new Uint8Array(fs.readFileSync(%r));
+const r = SyncRequest.fromBinary(body);
+const again = SyncRequest.toBinary(r);
+const resp = SyncResponse.toBinary({ messages: r.messages, merkleTree: r.merkleTree });
+fs.writeFileSync(%r, Buffer.from(again));
+fs.writeFileSync(%r, Buffer.from(resp));
+console.log(JSON.stringify({ n: r.messages.length, userId: r.userId, nodeId: r.nodeId, tree: r.merkleTree,
+  ts: r.messages.map((m) => m.timestamp), c: r.messages.map((m) => Buffer.from(m.content).toString('hex')) }));
+""" % (os.path.join(ROOT, "js", "evolu_evm.js"), str(tmp_path / "req.bin"), str(tmp_path / "again.bin"),
+       str(tmp_path / "resp.bin"))
+    out = subprocess.run(["node", "-e", script], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    got = json.loads(out.stdout)
+    assert got["n"] == 60 and got["ts"] == ts and got["c"] == [c.hex() for c in contents]
+    assert (got["userId"], got["nodeId"], got["tree"]) == ("owner-1", "0123456789abcdef", '{"hash":7}')
+    assert (tmp_path / "again.bin").read_bytes() == req.SerializeToString()
+    resp = RESP(messages=req.messages, merkleTree=req.merkleTree)
+    assert (tmp_path / "resp.bin").read_bytes() == resp.SerializeToString()
