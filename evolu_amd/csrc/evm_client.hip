@@ -897,6 +897,17 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
   KLAUNCH(k_cl_fold_reduce, dim3((B + 255) / 256), dim3(256), px, pp, info, dx, dp);
   KLAUNCH(k_cl_leaves, dim3(1), dim3(LEAF_THREADS), dx, dp, info, lck, lxr);
+  // into an empty tree: build the output speculatively, so the call has one host round trip
+  evm_tree* spec = nullptr;
+  if (tree_in->n_leaves == 0 && (st = tree_finalize_dev(ctx, S, tree_in->n_owners, lck, lxr, &info->n_leaves, B, &spec)))
+    return st;
+  struct SpecGuard {
+    evm_ctx* ctx;
+    evm_tree*& t;
+    ~SpecGuard() {
+      if (t) tree_destroy(ctx, t);
+    }
+  } guard{ctx, spec};
   Info hi;
   if ((st = read_info(ctx, info, &hi))) return st;
   if (hi.bad) {
@@ -924,7 +935,15 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
     if ((st = read_info(ctx, info, &hi))) return st;
   }
   if (hi.collision) return EVM_ECOLLISION;
-  if (!hi.fold_overflow) return merge_into_tree(ctx, S, tree_in, tree_in->n_owners, lck, lxr, hi.n_leaves, tree_out);
+  if (!hi.fold_overflow) {
+    if (spec) {
+      spec->n_leaves = hi.n_leaves;
+      *tree_out = spec;
+      spec = nullptr;
+      return EVM_OK;
+    }
+    return merge_into_tree(ctx, S, tree_in, tree_in->n_owners, lck, lxr, hi.n_leaves, tree_out);
+  }
   // wide minute range or mixed key lengths: sort-based fold
   u32* sel = S.alloc<u32>(n);
   u32* spos = S.alloc<u32>(n);

@@ -324,6 +324,42 @@ int evm::tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, co
   return hip_ok(hipGetLastError());
 }
 
+__global__ void k_copy_leaves(const u64* __restrict__ ck, const int32_t* __restrict__ xr, const u32* __restrict__ d_count,
+                              u64* __restrict__ ock, int32_t* __restrict__ oxr) {
+  const size_t L = *d_count;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < L; i += (size_t)gridDim.x * blockDim.x) {
+    ock[i] = ck[i];
+    oxr[i] = xr[i];
+  }
+}
+
+__global__ void k_owner_off_dev(const u64* __restrict__ ck, const u32* __restrict__ d_count, u32 n_owners,
+                                u64* __restrict__ off) {
+  const size_t L = *d_count;
+  for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o <= n_owners; o += (size_t)gridDim.x * blockDim.x)
+    off[o] = (o == n_owners) ? (u64)L : (u64)lower_bound_u64(ck, 0, L, (u64)o << 40);
+}
+
+int evm::tree_finalize_dev(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, const int32_t* xr,
+                           const u32* d_count, uint64_t cap, evm_tree** out) {
+  evm_tree* t = new evm_tree;
+  int st = tree_alloc(ctx, t, n_owners, cap);
+  if (st) {
+    tree_release(ctx, t);
+    return st;
+  }
+  KLAUNCH(k_copy_leaves, dim3(grid_for(cap, 256, 1024)), dim3(256), ck, xr, d_count, t->ck, t->xr);
+  KLAUNCH(k_owner_off_dev, dim3(grid_for(n_owners + 1, 256)), dim3(256), t->ck, d_count, n_owners, t->off);
+  // prefix XOR over the whole capacity: entries past the count never feed pfx[0..count]
+  st = scan_exclusive<int32_t, OpXor>(ctx, S, t->xr, cap, t->pfx, t->pfx + cap);
+  if (st) {
+    tree_release(ctx, t);
+    return st;
+  }
+  *out = t;
+  return hip_ok(hipGetLastError());
+}
+
 // Folds m selected (ck, hash) pairs into `in` (may be null = empty trees).
 int evm::fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u64* ck, u32* h, size_t m,
                         const Info& host_info, evm_tree** out) {

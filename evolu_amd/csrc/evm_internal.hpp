@@ -226,6 +226,11 @@ int radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t n, i
 int reduce_runs(evm_ctx* ctx, Scratch& S, const u64* ck, const int32_t* h, size_t m, u64* out_ck, int32_t* out_xr,
                 uint64_t* out_count);
 int tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, const int32_t* xr, uint64_t L, evm_tree** out);
+// Same, with the leaf count still on the device (*d_count <= cap): the tree is
+// built without a host round trip; the caller sets (*out)->n_leaves after its
+// one synchronisation.
+int tree_finalize_dev(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, const int32_t* xr, const u32* d_count,
+                      uint64_t cap, evm_tree** out);
 int merge_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, const u64* nck, const int32_t* nxr,
                     uint64_t L1, evm_tree** out);
 int fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u64* ck, u32* h, size_t m,
