@@ -31,8 +31,8 @@ HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 ALG_BYTES_PER_MSG = {
     # streaming fast path (evm_client.hip)
     "k_cl_pack": 46 + 28,  # ts in; order key 16 + rl 4 + hash 4 + minute 4 out
-    "k_cl_pass<1>": 16 + 4 + 4,  # order key + rl + cell in (per-range aggregates amortised away)
-    "k_cl_pass<2>": 16 + 4 + 4 + 1,  # order key + rl + cell in, flag out
+    "k_cl_scan1": 16 + 4 + 4,  # order key + rl + cell in (per-range aggregates amortised away)
+    "k_cl_scan2": 16 + 4 + 4 + 1,  # order key + rl + cell in, flag out
     "k_xp_scatter": 4 + 8,  # hash in, (hash, index) out
     "k_xp_dedup": 8,  # (hash, index) in
     "k_cl_fold_hist": 9,  # flag + minute + hash in (per window)

@@ -32,6 +32,7 @@ MSG_INS = 0x04
 MSG_BAD = 0x80
 
 OPT_CLIENT_PATH = 1
+OPT_SERVER_PATH = 2
 
 PB_SYNC_REQUEST = 1
 PB_SYNC_RESPONSE = 2

@@ -231,7 +231,7 @@ constexpr u32 FOLD_MAXWIN = 4;
 constexpr u32 FOLD_CHUNKS = 128;  // x windows: 256+ single-CU blocks for a 2-window batch
 constexpr int FOLD_THREADS = 1024;
 
-constexpr int CL_PF = 8;  // rounds of 64 messages a pass wave keeps in flight
+constexpr int CL_PF = 8;  // rounds of 64 messages a pass wave keeps in flight (24 B each)
 
 struct ClMsg {
   OKey key;
@@ -302,66 +302,81 @@ __device__ __forceinline__ void cl_store(const ClState& S, u32 c, const OKey& k)
   S.rl[c] = k.rl;
 }
 
-// One round of 64 messages (lane order == batch order).
+// Peer aggregate of one round of 64 messages (lane order == batch order):
+// registers and cross-lane ops only, no per-cell state, so the rounds of a
+// prefetch group are independent and only the short LDS read-compare-write
+// (cl_commit*) is serial from round to round.
+//   PASS 1: max key over this lane's same-cell peers up to and including
+//           itself, with its batch index (ties: the earlier lane);
+//   PASS 2: max key over the strictly earlier same-cell peers.
+struct ClPeer {
+  OKey acc;
+  u32 acc_i;
+  bool last;  // highest lane of its cell in the round: publishes the state
+};
+
 template <int PASS>
-__device__ __forceinline__ void cl_round(const ClMsg& m, size_t first, int cbits, const ClState& S,
-                                         uint8_t* __restrict__ flags, size_t end) {
+__device__ __forceinline__ ClPeer cl_peer(const ClMsg& m, size_t first, int cbits) {
   const int lane = threadIdx.x & 63;
-  const size_t i = first + lane;
   const u64 peers = match_cell(m.cell, m.ok, cbits);
-  const bool last_peer = m.ok && (peers >> lane) == 1ull;
+  ClPeer r;
+  r.last = m.ok && (peers >> lane) == 1ull;
+  r.acc = okey_none();
+  r.acc_i = 0xffffffffu;
   u64 rem = peers & lanemask_lt();
-  if (PASS == 1) {
-    // round max of this lane's cell over peers up to this lane; first index wins ties
-    OKey acc = okey_none();
-    u32 acc_i = 0xffffffffu;
-    while (__any(rem != 0)) {
-      const int src = rem ? (int)__builtin_ctzll(rem) : lane;
-      const OKey kp = shfl_okey(m.key, src);
-      if (rem) {
-        if (okey_gt(kp, acc)) {
-          acc = kp;
-          acc_i = (u32)(first + src);
+  while (__any(rem != 0)) {
+    const int src = rem ? (int)__builtin_ctzll(rem) : lane;
+    const OKey kp = shfl_okey(m.key, src);
+    if (rem) {
+      if (PASS == 1) {
+        if (okey_gt(kp, r.acc)) {
+          r.acc = kp;
+          r.acc_i = (u32)(first + src);
         }
-        rem &= rem - 1;
+      } else {
+        r.acc = okey_max(r.acc, kp);
       }
+      rem &= rem - 1;
     }
-    if (m.ok && okey_gt(m.key, acc)) {
-      acc = m.key;
-      acc_i = (u32)i;
-    }
-    if (last_peer) {
-      if (okey_gt(acc, cl_load(S, m.cell))) {
-        cl_store(S, m.cell, acc);
-        S.first[m.cell] = acc_i;
-      }
-    }
-  } else {
-    OKey acc = m.ok ? cl_load(S, m.cell) : okey_none();
-    while (__any(rem != 0)) {
-      const int src = rem ? (int)__builtin_ctzll(rem) : lane;
-      const OKey kp = shfl_okey(m.key, src);
-      if (rem) {
-        acc = okey_max(acc, kp);
-        rem &= rem - 1;
-      }
-    }
-    if (i < end) {
-      // applyMessages.ts:93 / :105 with t = acc (NULL is the all-zero key)
-      const bool ups = m.ok && okey_gt(m.key, acc);
-      const bool xr = m.ok && !okey_eq(acc, m.key);
-      flags[i] = m.ok ? (uint8_t)((ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u)) : (uint8_t)EVM_MSG_BAD;
-    }
-    if (last_peer) cl_store(S, m.cell, okey_max(acc, m.key));
+  }
+  if (PASS == 1 && m.ok && okey_gt(m.key, r.acc)) {
+    r.acc = m.key;
+    r.acc_i = (u32)(first + lane);
+  }
+  return r;
+}
+
+// pass 1: the round's last peer of a cell folds the round max into the range state
+__device__ __forceinline__ void cl_commit1(const ClMsg& m, const ClPeer& p, const ClState& S) {
+  if (p.last && okey_gt(p.acc, cl_load(S, m.cell))) {
+    cl_store(S, m.cell, p.acc);
+    S.first[m.cell] = p.acc_i;
   }
 }
 
-template <int PASS>
-__global__ __launch_bounds__(64) void k_cl_pass(const uint4* __restrict__ key, const u32* __restrict__ rl,
-                                                const u32* __restrict__ cell, size_t n, u32 C, int cbits,
-                                                size_t range_len, u64* __restrict__ agg_tc, u64* __restrict__ agg_rh,
-                                                u32* __restrict__ agg_rl, u32* __restrict__ agg_first,
-                                                uint8_t* __restrict__ flags, Info* __restrict__ info) {
+// pass 2: t_i = max(range state, earlier peers) -> flags; the last peer publishes
+__device__ __forceinline__ void cl_commit2(const ClMsg& m, const ClPeer& p, const ClState& S,
+                                           uint8_t* __restrict__ flags, size_t i, size_t end) {
+  const OKey t = m.ok ? okey_max(cl_load(S, m.cell), p.acc) : okey_none();
+  if (i < end) {
+    // applyMessages.ts:93 / :105 with t (NULL is the all-zero key)
+    const bool ups = m.ok && okey_gt(m.key, t);
+    const bool xr = m.ok && !okey_eq(t, m.key);
+    flags[i] = m.ok ? (uint8_t)((ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u)) : (uint8_t)EVM_MSG_BAD;
+  }
+  if (p.last) cl_store(S, m.cell, okey_max(t, m.key));
+}
+
+// Pass 1: the wave that owns range g walks it in batch order (64 messages a
+// round, CL_PF rounds in flight) and keeps the range's per-cell (max key,
+// first index) in LDS.  (A version fused with K1 ran 1.7x slower than K1 at
+// full occupancy + this walk: the parse then had no other waves to hide
+// behind.)
+__global__ __launch_bounds__(64) void k_cl_scan1(const uint4* __restrict__ key, const u32* __restrict__ rl,
+                                                 const u32* __restrict__ cell, size_t n, u32 C, int cbits,
+                                                 size_t range_len, u64* __restrict__ agg_tc, u64* __restrict__ agg_rh,
+                                                 u32* __restrict__ agg_rl, u32* __restrict__ agg_first,
+                                                 Info* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   ClState S;
   S.tc = reinterpret_cast<u64*>(smem);
@@ -373,45 +388,77 @@ __global__ __launch_bounds__(64) void k_cl_pass(const uint4* __restrict__ key, c
   const size_t beg = g * range_len;
   const size_t end = min(n, beg + range_len);
   for (u32 c = lane; c < C; c += 64) {
-    if (PASS == 1) {
-      S.tc[c] = 0;
-      S.rh[c] = 0;
-      S.rl[c] = 0;
-      S.first[c] = 0xffffffffu;
-    } else {
-      S.tc[c] = agg_tc[g * C + c];
-      S.rh[c] = agg_rh[g * C + c];
-      S.rl[c] = agg_rl[g * C + c];
-    }
+    S.tc[c] = 0;
+    S.rh[c] = 0;
+    S.rl[c] = 0;
+    S.first[c] = 0xffffffffu;
   }
   __syncthreads();
-  // software pipeline: CL_PF rounds in flight (registers; one wave per SIMD
-  // has the VGPRs), so HBM latency hides behind the serial per-round chain
   ClRaw buf[CL_PF];
 #pragma unroll
   for (int k = 0; k < CL_PF; ++k) buf[k] = cl_fetch(key, rl, cell, beg + 64 * k, end);
   bool aux_bad = false;
   for (size_t first = beg; first < end; first += 64 * CL_PF) {
+    ClMsg m[CL_PF];
+    ClPeer p[CL_PF];
 #pragma unroll
     for (int k = 0; k < CL_PF; ++k) {
-      const ClRaw cur = buf[k];
-      buf[k] = cl_fetch(key, rl, cell, first + 64 * (k + CL_PF), end);
       const size_t f = first + 64 * k;
-      if (f < end) {
-        if (PASS == 1) aux_bad |= f + lane < end && cur.cell >= C;
-        cl_round<PASS>(cl_decode(cur, C), f, cbits, S, flags, end);
-      }
+      aux_bad |= f + lane < end && buf[k].cell >= C;
+      m[k] = cl_decode(buf[k], C);  // rounds past the range: cell = ~0, not ok
+      buf[k] = cl_fetch(key, rl, cell, f + 64 * CL_PF, end);
+      p[k] = cl_peer<1>(m[k], f, cbits);
     }
+#pragma unroll
+    for (int k = 0; k < CL_PF; ++k) cl_commit1(m[k], p[k], S);
   }
-  if (PASS == 1 && __ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
-  if (PASS == 1) {
-    __syncthreads();
-    for (u32 c = lane; c < C; c += 64) {
-      agg_tc[g * C + c] = S.tc[c];
-      agg_rh[g * C + c] = S.rh[c];
-      agg_rl[g * C + c] = S.rl[c];
-      agg_first[g * C + c] = S.first[c];
+  if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
+  __syncthreads();
+  for (u32 c = lane; c < C; c += 64) {
+    agg_tc[g * C + c] = S.tc[c];
+    agg_rh[g * C + c] = S.rh[c];
+    agg_rl[g * C + c] = S.rl[c];
+    agg_first[g * C + c] = S.first[c];
+  }
+}
+
+// Pass 2: re-walk the range with the carried state (the cell maxima of all
+// earlier ranges and the prior rows) -> flags.
+__global__ __launch_bounds__(64) void k_cl_scan2(const uint4* __restrict__ key, const u32* __restrict__ rl,
+                                                 const u32* __restrict__ cell, size_t n, u32 C, int cbits,
+                                                 size_t range_len, const u64* __restrict__ agg_tc,
+                                                 const u64* __restrict__ agg_rh, const u32* __restrict__ agg_rl,
+                                                 uint8_t* __restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  ClState S;
+  S.tc = reinterpret_cast<u64*>(smem);
+  S.rh = S.tc + C;
+  S.rl = reinterpret_cast<u32*>(S.rh + C);
+  S.first = nullptr;
+  const int lane = threadIdx.x;
+  const size_t g = blockIdx.x;
+  const size_t beg = g * range_len;
+  const size_t end = min(n, beg + range_len);
+  for (u32 c = lane; c < C; c += 64) {
+    S.tc[c] = agg_tc[g * C + c];
+    S.rh[c] = agg_rh[g * C + c];
+    S.rl[c] = agg_rl[g * C + c];
+  }
+  __syncthreads();
+  ClRaw buf[CL_PF];
+#pragma unroll
+  for (int k = 0; k < CL_PF; ++k) buf[k] = cl_fetch(key, rl, cell, beg + 64 * k, end);
+  for (size_t first = beg; first < end; first += 64 * CL_PF) {
+    ClMsg m[CL_PF];
+    ClPeer p[CL_PF];
+#pragma unroll
+    for (int k = 0; k < CL_PF; ++k) {
+      m[k] = cl_decode(buf[k], C);  // rounds past the range: cell = ~0, not ok
+      buf[k] = cl_fetch(key, rl, cell, first + 64 * (k + CL_PF), end);
+      p[k] = cl_peer<2>(m[k], first + 64 * k, cbits);
     }
+#pragma unroll
+    for (int k = 0; k < CL_PF; ++k) cl_commit2(m[k], p[k], S, flags, first + 64 * k + lane, end);
   }
 }
 
@@ -552,6 +599,7 @@ constexpr u32 XP_SLOTS = 32768;                 // LDS set: u32 slots, 128 KiB
 constexpr u32 XP_MAX_FILL = 24576;              // bucket capacity cap (75 % load)
 constexpr u32 XP_AVG = 20000;                   // target mean bucket size
 constexpr int XP_MAX_KB = 11;                   // 2048 buckets: n > 41M overfills them -> exact fallback
+constexpr int XD_ITEMS = (XP_MAX_FILL + XP_THREADS - 1) / XP_THREADS;  // pairs per thread in k_xp_dedup
 
 // Buckets have a fixed capacity `cap` in `out` (bucket b owns [b*cap, b*cap+cap));
 // each tile reserves its run per bucket with one atomic on cursor[b], so no
@@ -633,11 +681,21 @@ __global__ __launch_bounds__(XP_THREADS) void k_xp_dedup(const u64* __restrict__
   const u32 b = blockIdx.x;
   const u32 cnt = min(cursor[b], cap);
   if (cnt < 2) return;
+  const u64* bp = pairs + (size_t)b * cap;
+  // every pair of this thread in flight at once (cap <= XP_MAX_FILL), then the set
+  u64 it[XD_ITEMS];
+#pragma unroll
+  for (int r = 0; r < XD_ITEMS; ++r) {
+    const u32 k = r * XP_THREADS + threadIdx.x;
+    it[r] = k < cnt ? bp[k] : 0ull;
+  }
   for (u32 s = threadIdx.x; s < XP_SLOTS; s += XP_THREADS) tab[s] = 0;
   __syncthreads();
-  const u64* bp = pairs + (size_t)b * cap;
-  for (u32 k = threadIdx.x; k < cnt; k += XP_THREADS) {
-    const u64 p = bp[k];
+#pragma unroll
+  for (int r = 0; r < XD_ITEMS; ++r) {
+    const u32 k = r * XP_THREADS + threadIdx.x;
+    if (k >= cnt) break;
+    const u64 p = it[r];
     const u32 h = (u32)(p >> 32), i = (u32)p;
     const u32 mine = ((h >> 15) << 15) | (k + 1);
     u32 pos = (h * 2654435761u) >> 17;  // 15 bits
@@ -714,10 +772,17 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __
   for (u32 b = threadIdx.x; b < FOLD_WIN / 32; b += FOLD_THREADS) pp[slot * (FOLD_WIN / 32) + b] = pres[b];
 }
 
-__global__ void k_cl_fold_reduce(const u32* __restrict__ px, const u32* __restrict__ pp, const Info* __restrict__ info,
-                                 u32* __restrict__ dx, u32* __restrict__ dp) {
-  const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= FOLD_MAXWIN * FOLD_WIN) return;
+// Per bin: XOR / OR of the chunk partials; per block of FR_THREADS bins: the
+// number of present bins and the XOR of their hashes (the leaf kernel's
+// output offsets and prefix-XOR carries).
+constexpr int FR_THREADS = 256;
+constexpr u32 FR_BLOCKS = FOLD_MAXWIN * FOLD_WIN / FR_THREADS;
+__global__ __launch_bounds__(FR_THREADS) void k_cl_fold_reduce(const u32* __restrict__ px, const u32* __restrict__ pp,
+                                                              const Info* __restrict__ info, u32* __restrict__ dx,
+                                                              u32* __restrict__ dp, u32* __restrict__ bcnt,
+                                                              u32* __restrict__ bxor) {
+  __shared__ u32 tmp[FR_THREADS / 64 + 1];
+  const u32 b = blockIdx.x * FR_THREADS + threadIdx.x;  // grid = FR_BLOCKS: every b < FOLD_MAXWIN * FOLD_WIN
   const u32 mlo = info->minute_min, mhi = info->minute_max;
   const bool usable = mlo <= mhi && !info->fold_overflow;
   const u32 w = b / FOLD_WIN, o = b % FOLD_WIN;
@@ -729,45 +794,55 @@ __global__ void k_cl_fold_reduce(const u32* __restrict__ px, const u32* __restri
       p |= (pp[slot * (FOLD_WIN / 32) + (o >> 5)] >> (o & 31)) & 1u;
     }
   }
+  x = p ? x : 0u;
   dx[b] = x;
   dp[b] = p;
+  u32 tot, xtot;
+  block_inclusive_scan<u32>(p, tmp, OpAdd<u32>(), &tot);
+  block_inclusive_scan<u32>(x, tmp, OpXor<u32>(), &xtot);
+  if (threadIdx.x == 0) {
+    bcnt[blockIdx.x] = tot;
+    bxor[blockIdx.x] = xtot;
+  }
 }
 
-// Dense leaves in one workgroup: positions by a block scan of the presence
-// bits (thread t owns bins [t*per, t*per+per)), codes by a base-3 increment
-// from the thread's first minute (all minutes share one key length here).
-constexpr int LEAF_THREADS = 1024;
-__global__ __launch_bounds__(LEAF_THREADS) void k_cl_leaves(const u32* __restrict__ dx, const u32* __restrict__ dp,
-                                                           Info* __restrict__ info, u64* __restrict__ ck,
-                                                           int32_t* __restrict__ xr) {
-  __shared__ u32 tmp[LEAF_THREADS / 64 + 1];
-  constexpr u32 B = FOLD_MAXWIN * FOLD_WIN, per = B / LEAF_THREADS;
-  const u32 a = threadIdx.x * per;
-  u32 c = 0;
-  for (u32 k = 0; k < per; ++k) c += dp[a + k];
-  u32 total;
-  const u32 incl = block_inclusive_scan<u32>(c, tmp, OpAdd<u32>(), &total);
-  if (threadIdx.x == 0) info->n_leaves = total;
-  if (!c) return;
-  u32 pos = incl - c;
-  const u32 m0 = info->minute_min + a;
-  const int L = base3_len(m0);
-  u64 code = minute_code(m0);
-  for (u32 k = 0; k < per; ++k) {
-    if (dp[a + k]) {
-      ck[pos] = code;  // owner 0
-      xr[pos] = (int32_t)dx[a + k];
-      ++pos;
-    }
-    // code of the next minute: base-3 increment on the digit fields (d + 1 in 1..3)
-    for (int i = L - 1; i >= 0; --i) {
-      const int sh = 2 * (CODE_DIGITS - 1 - i);
-      const u64 v = (code >> sh) & 3u;
-      if (v < 3) {
-        code += 1ull << sh;
-        break;
-      }
-      code -= 2ull << sh;  // 3 -> 1, carry on
+// Dense leaves, one bin per thread: block k's first output slot is the sum of
+// the earlier blocks' counts and its prefix-XOR carry the XOR of their hashes
+// (< FR_BLOCKS values, L2-resident); block scans place each leaf.  Minute
+// order == code order here (one key length).  With `pfx` the leaves land
+// directly in a one-owner tree: ck, xr, the exclusive prefix XOR and off.
+__global__ __launch_bounds__(FR_THREADS) void k_cl_leaves(const u32* __restrict__ dx, const u32* __restrict__ dp,
+                                                         const u32* __restrict__ bcnt, const u32* __restrict__ bxor,
+                                                         Info* __restrict__ info, u64* __restrict__ ck,
+                                                         int32_t* __restrict__ xr, int32_t* __restrict__ pfx,
+                                                         u64* __restrict__ off) {
+  __shared__ u32 tmp[FR_THREADS / 64 + 1];
+  u32 s = 0, sx = 0;
+  for (u32 k = threadIdx.x; k < blockIdx.x; k += FR_THREADS) {
+    s += bcnt[k];
+    sx ^= bxor[k];
+  }
+  u32 base, xbase;
+  block_inclusive_scan<u32>(s, tmp, OpAdd<u32>(), &base);
+  block_inclusive_scan<u32>(sx, tmp, OpXor<u32>(), &xbase);
+  const u32 b = blockIdx.x * FR_THREADS + threadIdx.x;
+  const u32 p = dp[b], x = dx[b];
+  u32 tot, xtot;
+  const u32 incl = block_inclusive_scan<u32>(p, tmp, OpAdd<u32>(), &tot);
+  const u32 xincl = block_inclusive_scan<u32>(x, tmp, OpXor<u32>(), &xtot);
+  if (p) {
+    const u32 pos = base + incl - 1;
+    ck[pos] = minute_code(info->minute_min + b);  // owner 0
+    xr[pos] = (int32_t)x;
+    if (pfx) pfx[pos] = (int32_t)(xbase ^ xincl ^ x);
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    const u32 L = base + tot;
+    info->n_leaves = L;
+    if (pfx) {
+      pfx[L] = (int32_t)(xbase ^ xtot);
+      off[0] = 0;
+      off[1] = L;
     }
   }
 }
@@ -834,19 +909,16 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   {
     evm::ProfScope ps_(ctx, "k_cl_pack");
     const dim3 g(std::min<size_t>((n + 255) / 256, 2048));
-    if (stride == 48)
+    if (stride == 48 && ((uintptr_t)ts & 15) == 0)
       hipLaunchKernelGGL(k_cl_pack<true>, g, dim3(CLP_THREADS), 0, ctx->stream, (const uint8_t*)ts, stride, n, key,
                          rl, hash, minute, info);
     else
       hipLaunchKernelGGL(k_cl_pack<false>, g, dim3(CLP_THREADS), 0, ctx->stream, (const uint8_t*)ts, stride, n, key,
                          rl, hash, minute, info);
   }
-  const size_t lds = (size_t)C * 24;
-  {
-    evm::ProfScope ps_(ctx, "k_cl_pass<1>");
-    hipLaunchKernelGGL((k_cl_pass<1>), dim3(G), dim3(64), lds, ctx->stream, key, rl, cell, n, C, cbits, range, a_tc,
-                       a_rh, a_rl, a_first, (uint8_t*)nullptr, info);
-  }
+  // pass 1: per range and cell, the max timestamp and its first index
+  KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(64), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
+              a_first, info);
   // cross-cell PK check: partition by hash into fixed-capacity buckets, LDS set per bucket
   int kb = 0;
   while (kb < XP_MAX_KB && (n >> kb) > XP_AVG) ++kb;
@@ -880,27 +952,35 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
     KLAUNCH(k_cl_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh,
             s_rl);
   }
-  {
-    evm::ProfScope ps_(ctx, "k_cl_pass<2>");
-    hipLaunchKernelGGL((k_cl_pass<2>), dim3(G), dim3(64), lds, ctx->stream, key, rl, cell, n, C, cbits, range, a_tc,
-                       a_rh, a_rl, a_first, flags, info);
-  }
+  KLAUNCH_LDS(k_cl_scan2, dim3(G), dim3(64), (size_t)C * 20, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
+              flags);
   // Merkle fold
   u32* px = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN);
   u32* pp = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32));
   const size_t B = (size_t)FOLD_MAXWIN * FOLD_WIN;
   u32* dx = S.alloc<u32>(B);
   u32* dp = S.alloc<u32>(B);
+  u32* bcnt = S.alloc<u32>(FR_BLOCKS);
+  u32* bxor = S.alloc<u32>(FR_BLOCKS);
   u64* lck = S.alloc<u64>(B);
   int32_t* lxr = S.alloc<int32_t>(B);
-  if (!px || !pp || !dx || !dp || !lck || !lxr) return EVM_ENOMEM;
+  if (!px || !pp || !dx || !dp || !bcnt || !bxor || !lck || !lxr) return EVM_ENOMEM;
   KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
-  KLAUNCH(k_cl_fold_reduce, dim3((B + 255) / 256), dim3(256), px, pp, info, dx, dp);
-  KLAUNCH(k_cl_leaves, dim3(1), dim3(LEAF_THREADS), dx, dp, info, lck, lxr);
-  // into an empty tree: build the output speculatively, so the call has one host round trip
+  KLAUNCH(k_cl_fold_reduce, dim3(FR_BLOCKS), dim3(FR_THREADS), px, pp, info, dx, dp, bcnt, bxor);
+  // into an empty tree: build the output speculatively, so the call has one
+  // host round trip; one owner: the leaf kernel writes the tree itself
   evm_tree* spec = nullptr;
-  if (tree_in->n_leaves == 0 && (st = tree_finalize_dev(ctx, S, tree_in->n_owners, lck, lxr, &info->n_leaves, B, &spec)))
-    return st;
+  if (tree_in->n_leaves == 0 && tree_in->n_owners == 1) {
+    if ((st = tree_alloc_cap(ctx, 1, B, &spec))) return st;
+    KLAUNCH(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), dx, dp, bcnt, bxor, info, spec->ck, spec->xr, spec->pfx,
+            spec->off);
+  } else {
+    KLAUNCH(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), dx, dp, bcnt, bxor, info, lck, lxr, (int32_t*)nullptr,
+            (u64*)nullptr);
+    if (tree_in->n_leaves == 0 &&
+        (st = tree_finalize_dev(ctx, S, tree_in->n_owners, lck, lxr, &info->n_leaves, B, &spec)))
+      return st;
+  }
   struct SpecGuard {
     evm_ctx* ctx;
     evm_tree*& t;

@@ -300,6 +300,17 @@ static void tree_release(evm_ctx* ctx, evm_tree* t) {
   delete t;
 }
 
+int evm::tree_alloc_cap(evm_ctx* ctx, u32 n_owners, uint64_t cap, evm_tree** out) {
+  evm_tree* t = new evm_tree;
+  const int st = tree_alloc(ctx, t, n_owners, cap);
+  if (st) {
+    tree_release(ctx, t);
+    return st;
+  }
+  *out = t;
+  return EVM_OK;
+}
+
 // Builds a tree object from device leaves (ck sorted unique, xr); copies them.
 int evm::tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, const int32_t* xr, uint64_t L,
                        evm_tree** out) {
@@ -550,6 +561,10 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
   if (!ctx) return EVM_EINVAL;
   if (option == EVM_OPT_CLIENT_PATH && value >= 0 && value <= 2) {
     ctx->client_path = (int)value;
+    return EVM_OK;
+  }
+  if (option == EVM_OPT_SERVER_PATH && value >= 0 && value <= 2) {
+    ctx->server_path = (int)value;
     return EVM_OK;
   }
   return EVM_EINVAL;

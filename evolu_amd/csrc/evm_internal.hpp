@@ -17,6 +17,7 @@ struct evm_ctx {
   // kernel timing (evm_prof_*): HIP event pairs per kernel name, on `stream`
   bool prof = false;
   int client_path = 0;  // EVM_OPT_CLIENT_PATH
+  int server_path = 0;  // EVM_OPT_SERVER_PATH
   std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> prof_events;
   std::map<std::string, std::pair<double, uint64_t>> prof_total;  // ms, launches (drained)
   std::vector<hipEvent_t> prof_pool;  // recycled events: no hipEventCreate inside a timed loop
@@ -179,6 +180,13 @@ class ProfScope {
     hipLaunchKernelGGL(kern, grid, block, 0, ctx->stream, __VA_ARGS__); \
   } while (0)
 
+// Same, with dynamic LDS bytes.
+#define KLAUNCH_LDS(kern, grid, block, lds, ...)                            \
+  do {                                                                     \
+    evm::ProfScope ps_(ctx, #kern);                                        \
+    hipLaunchKernelGGL(kern, grid, block, lds, ctx->stream, __VA_ARGS__); \
+  } while (0)
+
 enum OwnerMode { OWNER_ZERO = 0, OWNER_AUX = 1, OWNER_CELL = 2 };
 
 inline int grid_for(size_t n, int threads, int cap = 8192) {
@@ -226,6 +234,9 @@ int radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t n, i
 int reduce_runs(evm_ctx* ctx, Scratch& S, const u64* ck, const int32_t* h, size_t m, u64* out_ck, int32_t* out_xr,
                 uint64_t* out_count);
 int tree_finalize(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, const int32_t* xr, uint64_t L, evm_tree** out);
+// An uninitialised tree with room for `cap` leaves (n_leaves = cap until the
+// caller sets it); the caller's kernels fill off, ck, xr and pfx.
+int tree_alloc_cap(evm_ctx* ctx, u32 n_owners, uint64_t cap, evm_tree** out);
 // Same, with the leaf count still on the device (*d_count <= cap): the tree is
 // built without a host round trip; the caller sets (*out)->n_leaves after its
 // one synchronisation.

@@ -308,6 +308,289 @@ __global__ void k_sv_owner_off(const u32* __restrict__ owner, size_t n, u32 n_ow
   }
 }
 
+// ------------------------------------------------------ K5: owner ingest
+// When every owner's share of the batch fits SVO_CAP rows (the common case:
+// a request carries one owner's messages, index.ts:224-248), one workgroup
+// per owner runs that owner's addMessages in LDS, with no global sort by
+// timestamp:
+//   A  gather the owner's records in batch order (the stable owner sort),
+//      bitonic sort by (order key, batch position); the first occurrence of
+//      each timestamp that the store does not hold gets EVM_MSG_INS
+//      (index.ts:154 changes === 1); the inserted rows (sorted) and their
+//      per-minute XOR leaves go to the owner's slice of batch-sized
+//      temporaries; per-owner counts.
+//   B  (after the counts are scanned) merge the owner's stored rows with the
+//      new rows, and its tree leaves with the new leaves -- equal minutes
+//      XOR-combine, as repeated insertIntoMerkleTree calls do -- straight into
+//      the new store and tree.
+constexpr int SVO_THREADS = 256;
+constexpr u32 SVO_CAP = 2048;
+constexpr int SVO_PER = SVO_CAP / SVO_THREADS;  // sorted positions per thread
+constexpr u32 SVO_POS_BITS = 11;
+static_assert((1u << SVO_POS_BITS) == SVO_CAP, "position field");
+
+struct SvoStatus {
+  u32 big;       // an owner's share of the batch exceeds SVO_CAP
+  u32 unsorted;  // an owner's new leaves mix key lengths (code order != minute order)
+};
+
+__device__ __forceinline__ bool svo_less(u64 ta, u64 ha, u32 xa, u64 tb, u64 hb, u32 xb) {
+  return ta != tb ? ta < tb : (ha != hb ? ha < hb : xa < xb);
+}
+
+// first k in [lo, hi) with a[k] >= x
+__device__ __forceinline__ u64 lb_u64(const u64* a, u64 lo, u64 hi, u64 x) {
+  while (lo < hi) {
+    const u64 mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
+    const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u64* __restrict__ seg, StoreView st,
+    const u64* __restrict__ t_off, const u64* __restrict__ t_ck, u64 id_base, uint8_t* __restrict__ flags,
+    u64* __restrict__ n_tc, u64* __restrict__ n_hi, u32* __restrict__ n_lo, u64* __restrict__ n_id,
+    u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
+    u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status) {
+  __shared__ u64 s_tc[SVO_CAP];
+  __shared__ u64 s_hi[SVO_CAP];
+  __shared__ u32 s_x[SVO_CAP];  // rank_lo << SVO_POS_BITS | position in the owner's batch share
+  __shared__ u32 tmp[SVO_THREADS / 64 + 1];
+  const u32 o = blockIdx.x;
+  const u64 a = seg[o];
+  const u64 m = seg[o + 1] - a;  // an unsorted owner column (bad ids) may underflow: "big"
+  const u64 la = t_off[o], lb = t_off[o + 1];
+  if (m > SVO_CAP || m == 0) {
+    if (threadIdx.x == 0) {
+      if (m) atomicOr(&status->big, 1u);
+      cnt_rows[o] = 0;
+      cnt_new[o] = 0;
+      cnt_leaves[o] = (u32)(lb - la);
+    }
+    return;
+  }
+  u32 P = 1;
+  while (P < m) P <<= 1;
+  for (u32 t = threadIdx.x; t < P; t += SVO_THREADS) {
+    if (t < m) {
+      const evm_rec r = rec[perm[a + t]];
+      u64 hi;
+      u32 lo;
+      node_ranks(r.node, r.meta & EVM_META_CASEMASK, &hi, &lo);
+      s_tc[t] = r.tc;
+      s_hi[t] = hi;
+      s_x[t] = (lo << SVO_POS_BITS) | t;
+    } else {
+      s_tc[t] = ~0ull;
+      s_hi[t] = ~0ull;
+      s_x[t] = ~0u;
+    }
+  }
+  __syncthreads();
+  // bitonic sort, ascending by (tc, rank_hi, rank_lo, position)
+  for (u32 k = 2; k <= P; k <<= 1) {
+    for (u32 j = k >> 1; j > 0; j >>= 1) {
+      for (u32 t = threadIdx.x; t < P / 2; t += SVO_THREADS) {
+        const u32 i = 2 * t - (t & (j - 1)), l = i + j;
+        const u64 ta = s_tc[i], tb = s_tc[l], ha = s_hi[i], hb = s_hi[l];
+        const u32 xa = s_x[i], xb = s_x[l];
+        if (svo_less(tb, hb, xb, ta, ha, xa) == ((i & k) == 0)) {
+          s_tc[i] = tb;
+          s_tc[l] = ta;
+          s_hi[i] = hb;
+          s_hi[l] = ha;
+          s_x[i] = xb;
+          s_x[l] = xa;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // first occurrences not yet stored (thread t owns sorted positions t*SVO_PER ..)
+  const u64 sa = st.off[o], sb = st.off[o + 1];
+  u64 mt[SVO_PER], mh[SVO_PER];
+  u32 ml[SVO_PER], mp[SVO_PER];
+  u32 insm = 0, c = 0;
+#pragma unroll
+  for (int r = 0; r < SVO_PER; ++r) {
+    const u32 p = threadIdx.x * SVO_PER + r;
+    mt[r] = 0;
+    mh[r] = 0;
+    ml[r] = 0;
+    mp[r] = 0;
+    if (p < m) {
+      const u32 x = s_x[p];
+      mt[r] = s_tc[p];
+      mh[r] = s_hi[p];
+      ml[r] = x >> SVO_POS_BITS;
+      mp[r] = x & (SVO_CAP - 1);
+      bool ins = p == 0 || s_tc[p - 1] != mt[r] || s_hi[p - 1] != mh[r] || (s_x[p - 1] >> SVO_POS_BITS) != ml[r];
+      if (ins && sb > sa) {
+        const SKey k{o, mt[r], mh[r], ml[r]};
+        const size_t q = store_lower(st, sa, sb, k);
+        ins = !(q < sb && skey_cmp(skey_at(st, q), k) == 0);
+      }
+      if (ins) {
+        insm |= 1u << r;
+        ++c;
+      }
+    }
+  }
+  u32 M;
+  u32 q = block_inclusive_scan<u32>(c, tmp, OpAdd<u32>(), &M) - c;  // (its barriers free the sort arrays)
+  u32* s_min = reinterpret_cast<u32*>(s_tc);  // inserted rows, sorted: minute
+  u32* s_h = s_min + SVO_CAP;                 //                        hash
+  u32* s_lx = reinterpret_cast<u32*>(s_hi);   // per leaf: XOR
+  u32* s_lm = s_lx + SVO_CAP;                 //           minute
+  for (u32 t = threadIdx.x; t < SVO_CAP; t += SVO_THREADS) s_lx[t] = 0;
+#pragma unroll
+  for (int r = 0; r < SVO_PER; ++r) {
+    const u32 p = threadIdx.x * SVO_PER + r;
+    if (p < m) {
+      const u32 bi = perm[a + mp[r]];
+      const bool ins = (insm >> r) & 1u;
+      flags[bi] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
+      if (ins) {
+        const u64 w = a + q;
+        n_tc[w] = mt[r];
+        n_hi[w] = mh[r];
+        n_lo[w] = ml[r];
+        n_id[w] = id_base + bi;
+        s_min[q] = rec[bi].minute;
+        s_h[q] = rec[bi].hash;
+        ++q;
+      }
+    }
+  }
+  __syncthreads();
+  // leaves: runs of one minute among the inserted rows (sorted by millis)
+  u32 hm = 0, hc = 0;
+#pragma unroll
+  for (int r = 0; r < SVO_PER; ++r) {
+    const u32 p = threadIdx.x * SVO_PER + r;
+    if (p < M && (p == 0 || s_min[p] != s_min[p - 1])) {
+      hm |= 1u << r;
+      ++hc;
+    }
+  }
+  u32 NL;
+  int lid = (int)(block_inclusive_scan<u32>(hc, tmp, OpAdd<u32>(), &NL) - hc) - 1;
+#pragma unroll
+  for (int r = 0; r < SVO_PER; ++r) {
+    const u32 p = threadIdx.x * SVO_PER + r;
+    if (p < M) {
+      if ((hm >> r) & 1u) s_lm[++lid] = s_min[p];
+      atomicXor(&s_lx[lid], s_h[p]);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && NL && base3_len(s_lm[0]) != base3_len(s_lm[NL - 1])) atomicOr(&status->unsorted, 1u);
+  u32 dups = 0;
+  for (u32 l = threadIdx.x; l < NL; l += SVO_THREADS) {
+    const u64 code = ((u64)o << 40) | minute_code(s_lm[l]);
+    const u64 k = lb_u64(t_ck, la, lb, code);
+    const bool dup = k < lb && t_ck[k] == code;
+    l_ck[a + l] = code;
+    l_xr[a + l] = (int32_t)s_lx[l];
+    l_dup[a + l] = dup ? 1 : 0;
+    dups += dup ? 1u : 0u;
+  }
+  u32 dtot;
+  block_inclusive_scan<u32>(dups, tmp, OpAdd<u32>(), &dtot);
+  if (threadIdx.x == 0) {
+    cnt_rows[o] = M;
+    cnt_new[o] = NL;
+    cnt_leaves[o] = (u32)(lb - la) + NL - dtot;
+  }
+}
+
+__global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
+    const u64* __restrict__ seg, u32 n_owners, StoreView st, const u64* __restrict__ st_id, const u64* __restrict__ n_tc,
+    const u64* __restrict__ n_hi, const u32* __restrict__ n_lo, const u64* __restrict__ n_id,
+    const u32* __restrict__ cnt_rows, const u32* __restrict__ row_pos, const u64* __restrict__ t_off,
+    const u64* __restrict__ t_ck, const int32_t* __restrict__ t_xr, const u64* __restrict__ l_ck,
+    const int32_t* __restrict__ l_xr, const uint8_t* __restrict__ l_dup, const u32* __restrict__ cnt_new,
+    const u32* __restrict__ leaf_pos, StoreOut so, u64* __restrict__ so_off, u64* __restrict__ to_ck,
+    int32_t* __restrict__ to_xr, u64* __restrict__ to_off) {
+  __shared__ u32 s_dp[SVO_CAP + 1];  // exclusive prefix count of the new leaves already in the tree
+  __shared__ u32 tmp[SVO_THREADS / 64 + 1];
+  const u32 o = blockIdx.x;
+  const u64 a = seg[o];
+  const u32 M = cnt_rows[o], NL = cnt_new[o];
+  const u64 sa = st.off[o], sb = st.off[o + 1];
+  const u64 base = sa + row_pos[o];  // rows of the earlier owners: old + new
+  // rows: the owner's stored and new keys are disjoint sorted lists
+  for (u64 k = sa + threadIdx.x; k < sb; k += SVO_THREADS) {
+    const SKey key = skey_at(st, k);
+    u32 lo = 0, hi = M;
+    while (lo < hi) {
+      const u32 mid = (lo + hi) >> 1;
+      if (skey_cmp(SKey{o, n_tc[a + mid], n_hi[a + mid], n_lo[a + mid]}, key) < 0) lo = mid + 1;
+      else hi = mid;
+    }
+    const u64 w = base + (k - sa) + lo;
+    so.owner[w] = o;
+    so.tc[w] = key.tc;
+    so.hi[w] = key.hi;
+    so.lo[w] = key.lo;
+    so.id[w] = st_id[k];
+  }
+  for (u32 j = threadIdx.x; j < M; j += SVO_THREADS) {
+    const SKey key{o, n_tc[a + j], n_hi[a + j], n_lo[a + j]};
+    const u64 w = base + j + (store_lower(st, sa, sb, key) - sa);
+    so.owner[w] = o;
+    so.tc[w] = key.tc;
+    so.hi[w] = key.hi;
+    so.lo[w] = key.lo;
+    so.id[w] = n_id[a + j];
+  }
+  // leaves: union of the tree's and the new ones by code, equal codes XOR-combined
+  const u64 la = t_off[o], lb = t_off[o + 1];
+  const u64 lbase = leaf_pos[o];
+  u32 d[SVO_PER], c = 0;
+#pragma unroll
+  for (int r = 0; r < SVO_PER; ++r) {
+    const u32 j = threadIdx.x * SVO_PER + r;
+    d[r] = j < NL ? (u32)l_dup[a + j] : 0u;
+    c += d[r];
+  }
+  u32 dtot;
+  u32 run = block_inclusive_scan<u32>(c, tmp, OpAdd<u32>(), &dtot) - c;
+#pragma unroll
+  for (int r = 0; r < SVO_PER; ++r) {
+    const u32 j = threadIdx.x * SVO_PER + r;
+    if (j < NL) s_dp[j] = run;
+    run += d[r];
+  }
+  if (threadIdx.x == 0) s_dp[NL] = dtot;
+  __syncthreads();
+  for (u64 k = la + threadIdx.x; k < lb; k += SVO_THREADS) {
+    const u64 code = t_ck[k];
+    const u32 j = (u32)(lb_u64(l_ck, a, a + NL, code) - a);  // new leaves below this code
+    const bool eq = j < NL && l_ck[a + j] == code;
+    const u64 w = lbase + (k - la) + j - s_dp[j];
+    to_ck[w] = code;
+    to_xr[w] = t_xr[k] ^ (eq ? l_xr[a + j] : 0);
+  }
+  for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) {
+    if (l_dup[a + j]) continue;
+    const u64 code = l_ck[a + j];
+    const u64 w = lbase + (j - s_dp[j]) + (lb_u64(t_ck, la, lb, code) - la);
+    to_ck[w] = code;
+    to_xr[w] = l_xr[a + j];
+  }
+  if (threadIdx.x == 0) {
+    so_off[o] = base;
+    to_off[o] = lbase;
+    if (o == n_owners - 1) {
+      so_off[n_owners] = base + (sb - sa) + M;
+      to_off[n_owners] = lbase + (lb - la) + NL - dtot;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ select
 // rank -> hex value (case folded)
 __device__ __forceinline__ u32 rank_hex(u32 r) { return r >= 16u ? r - 6u : r; }
@@ -410,6 +693,84 @@ void store_release_arrays(evm_ctx* ctx, evm_store* s) {
   s->lo = nullptr;
 }
 
+// K5 driver.  On success *done = true and (*ns, *new_tree) hold the new store
+// arrays and tree; *done = false (status OK) when some owner's share exceeds
+// SVO_CAP or mixes key lengths: the caller takes the global sort path with
+// the same packed records.  Validity of the batch is checked here (one host
+// round trip for the whole ingest).
+int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec* rec, const u32* owner, size_t n,
+                    uint64_t id_base, uint8_t* flags, Info* info, u32* perm, evm_store* ns, evm_tree** new_tree,
+                    bool* done) {
+  *done = false;
+  const u32 O = s->n_owners;
+  int st;
+  // stable sort of the batch index by owner: each owner's share in batch order
+  u32* own = S.alloc<u32>(n);
+  u64* seg = S.alloc<u64>((size_t)O + 1);
+  SvoStatus* status = S.alloc<SvoStatus>(1);
+  u64* n_tc = S.alloc<u64>(n);
+  u64* n_hi = S.alloc<u64>(n);
+  u32* n_lo = S.alloc<u32>(n);
+  u64* n_id = S.alloc<u64>(n);
+  u64* l_ck = S.alloc<u64>(n);
+  int32_t* l_xr = S.alloc<int32_t>(n);
+  uint8_t* l_dup = S.alloc<uint8_t>(n);
+  u32* cnt = S.alloc<u32>(3 * (size_t)O);  // rows, new leaves, merged leaves
+  u32* pos = S.alloc<u32>(2 * (size_t)O);  // row / leaf offsets
+  u32* tot = S.alloc<u32>(2);
+  if (!own || !seg || !status || !n_tc || !n_hi || !n_lo || !n_id || !l_ck || !l_xr || !l_dup || !cnt || !pos || !tot)
+    return EVM_ENOMEM;
+  HIPR(hipMemcpyAsync(own, owner, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
+  if ((st = launch_iota(ctx, perm, n))) return st;
+  u32* ok = own;
+  u32* ov = perm;
+  const int obits = O > 1 ? 32 - __builtin_clz(O - 1) : 0;
+  if ((st = radix_sort_pairs<u32>(ctx, S, ok, ov, n, 0, obits))) return st;
+  KLAUNCH(k_sv_owner_off, dim3(grid_for((size_t)O + 1, 256)), dim3(256), ok, n, O, seg);
+  HIPR(hipMemsetAsync(status, 0, sizeof(SvoStatus), ctx->stream));
+  const evm_tree* t = s->tree;
+  u32 *c_rows = cnt, *c_new = cnt + O, *c_leaves = cnt + 2 * (size_t)O;
+  KLAUNCH(k_svo_a, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off, (const u64*)t->ck,
+          (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves, status);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, O, pos, tot))) return st;
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, O, pos + O, tot + 1))) return st;
+  Info hi;
+  SvoStatus hs;
+  u32 ht[2];
+  HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipMemcpyAsync(ht, tot, sizeof(ht), hipMemcpyDeviceToHost, ctx->stream));
+  if ((st = read_info(ctx, info, &hi))) return st;
+  if (hi.bad_aux) return EVM_EINVAL;
+  if (hi.bad) {
+    KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
+    (void)evm_sync(ctx);
+    return EVM_ENONCANON;
+  }
+  if (hs.big || hs.unsorted) return EVM_OK;  // the sort path redoes the flags
+  // new store and tree, exactly sized
+  if ((st = store_alloc(ctx, ns, O, s->n + ht[0]))) {
+    store_release_arrays(ctx, ns);
+    return st;
+  }
+  evm_tree* nt = nullptr;
+  if ((st = tree_alloc_cap(ctx, O, ht[1], &nt))) {
+    store_release_arrays(ctx, ns);
+    return st;
+  }
+  const StoreOut so{ns->owner, ns->tc, ns->hi, ns->lo, ns->id};
+  KLAUNCH(k_svo_b, dim3(O), dim3(SVO_THREADS), seg, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id, c_rows,
+          pos, (const u64*)t->off, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + O, so, ns->off, nt->ck,
+          nt->xr, nt->off);
+  if ((st = scan_exclusive<int32_t, OpXor>(ctx, S, nt->xr, ht[1], nt->pfx, nt->pfx + ht[1]))) {
+    store_release_arrays(ctx, ns);
+    tree_destroy(ctx, nt);
+    return st;
+  }
+  *new_tree = nt;
+  *done = true;
+  return EVM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -473,6 +834,12 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
     FieldRange* fr = S.alloc<FieldRange>(1);
     if (!rec || !perm || !fv || !fr) return EVM_ENOMEM;
     if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) return st;
+    if (ctx->server_path != 2 && s->n_owners > 0) {
+      bool done = false;
+      if ((st = ingest_by_owner(ctx, S, s, rec, owner, n, id_base, flags, info, perm, &ns, &new_tree, &done)))
+        return st;
+      if (done) goto commit;
+    }
     FieldRange h0;
     for (int f = 0; f < N_FIELDS; ++f) {
       h0.mn[f] = ~0ull;
@@ -592,6 +959,7 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
       return st;
     }
   }
+commit:
   // commit: swap in the new store arrays and tree
   store_release_arrays(ctx, s);
   tree_destroy(ctx, s->tree);

@@ -89,6 +89,7 @@ void* evm_get_stream(evm_ctx* ctx);
 int evm_sync(evm_ctx* ctx);
 /* tuning / test knobs */
 #define EVM_OPT_CLIENT_PATH 1 /* evm_apply_batch: 0 auto, 1 force the streaming path, 2 force the sort path */
+#define EVM_OPT_SERVER_PATH 2 /* evm_server_ingest: 0/1 per-owner LDS path where every owner's share fits, 2 force the sort path */
 int evm_set_option(evm_ctx* ctx, int option, int64_t value);
 /* kernel timing with HIP events on the context stream (for roofline reports) */
 int evm_prof_enable(evm_ctx* ctx, int on);

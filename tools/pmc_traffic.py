@@ -42,8 +42,6 @@ def short(name):
     if not m:
         return name
     base, targs = m.group(1), m.group(2) or ""
-    if base in ("k_cl_pass",):
-        return "%s<%s>" % (base, targs.strip("<>"))
     if base in ("k_radix_scatter", "k_radix_hist", "k_scan_down", "k_scan_reduce", "k_scan_partials"):
         return None
     return base
