@@ -59,6 +59,9 @@ def parse():
                     help="client: config 2 applyMessages (headline); server: config 3/4 ingest + diff + select")
     ap.add_argument("--owners", type=int, default=100_000, help="server workload: owners per GPU")
     ap.add_argument("--per-owner", type=int, default=1000, help="server workload: messages per owner")
+    ap.add_argument("--request", type=int, default=100,
+                    help="server workload: messages per SyncRequest (one owner each, requests in random order); "
+                         "1 = every message shuffled on its own")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch per kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -224,7 +227,7 @@ def server_main(a, rank, world, local):
     from evolu_amd.engine import Engine
 
     O_total = a.owners * world
-    ts_np, owner_np, millis = synth.config3(a.owners, a.per_owner, seed_config=3 + 1000 * rank)
+    ts_np, owner_np, millis = synth.config3(a.owners, a.per_owner, seed_config=3 + 1000 * rank, request=a.request)
     # this rank's owner o is job owner o*world + (o+rank)%world: every rank
     # receives messages for owners living on every rank, no owner on two sources
     o64 = owner_np.astype(np.int64)
@@ -296,8 +299,8 @@ def server_main(a, rank, world, local):
             "metric": METRIC, "value": world * n * a.steps / elapsed, "unit": "msgs/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u64", "data": "synthetic (seeded HLC streams, SURVEY 8(d) config 3/4)",
-            "config": {"workload": "server: addMessages + getMessages, %d owners x %d msgs per GPU, RCCL owner routing"
-                       % (a.owners, a.per_owner), "messages_per_gpu": n, "owners_per_gpu": a.owners,
+            "config": {"workload": "server: addMessages + getMessages, %d owners x %d msgs per GPU in requests of %d, "
+                       "RCCL owner routing" % (a.owners, a.per_owner, a.request), "messages_per_gpu": n, "owners_per_gpu": a.owners,
                        "selected_rows_rank0": nsel, "parallelism": "owner-sharded, %d rank(s)" % world},
             "kernels_ms_per_step": {k: v[0] / a.steps for k, v in top},
         }), flush=True)

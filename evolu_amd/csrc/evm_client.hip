@@ -367,99 +367,94 @@ __device__ __forceinline__ void cl_commit2(const ClMsg& m, const ClPeer& p, cons
   if (p.last) cl_store(S, m.cell, okey_max(t, m.key));
 }
 
-// Pass 1: the wave that owns range g walks it in batch order (64 messages a
-// round, CL_PF rounds in flight) and keeps the range's per-cell (max key,
-// first index) in LDS.  (A version fused with K1 ran 1.7x slower than K1 at
-// full occupancy + this walk: the parse then had no other waves to hide
-// behind.)
-__global__ __launch_bounds__(64) void k_cl_scan1(const uint4* __restrict__ key, const u32* __restrict__ rl,
-                                                 const u32* __restrict__ cell, size_t n, u32 C, int cbits,
-                                                 size_t range_len, u64* __restrict__ agg_tc, u64* __restrict__ agg_rh,
-                                                 u32* __restrict__ agg_rl, u32* __restrict__ agg_first,
-                                                 Info* __restrict__ info) {
+// The walk of one range by a 4-wave workgroup.  The range is cut into
+// groups of 256 messages; wave w takes messages [64w, 64w + 64) of every
+// group.  The peer phase (cl_peer: ballots and shuffles, the bulk of the
+// work) runs in all four waves at once; the commits -- the short LDS
+// read-compare-write on the range's per-cell state -- follow in batch order,
+// wave 0 to 3, separated by barriers.  Other workgroups on the CU fill the
+// SIMDs while one wave commits.
+//   PASS 1: per-cell (max key, first index) of the range -> agg_*
+//   PASS 2: state = the carried maxima (agg_*) -> flags
+constexpr int WK_THREADS = 256;
+constexpr int WK_PF = 3;  // groups in flight per wave
+
+template <int PASS>
+__device__ __forceinline__ void cl_walk(const uint4* __restrict__ key, const u32* __restrict__ rl,
+                                        const u32* __restrict__ cell, size_t n, u32 C, int cbits, size_t range_len,
+                                        u64* __restrict__ agg_tc, u64* __restrict__ agg_rh, u32* __restrict__ agg_rl,
+                                        u32* __restrict__ agg_first, uint8_t* __restrict__ flags,
+                                        Info* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   ClState S;
   S.tc = reinterpret_cast<u64*>(smem);
   S.rh = S.tc + C;
   S.rl = reinterpret_cast<u32*>(S.rh + C);
-  S.first = S.rl + C;
-  const int lane = threadIdx.x;
+  S.first = PASS == 1 ? S.rl + C : nullptr;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const size_t g = blockIdx.x;
   const size_t beg = g * range_len;
   const size_t end = min(n, beg + range_len);
-  for (u32 c = lane; c < C; c += 64) {
-    S.tc[c] = 0;
-    S.rh[c] = 0;
-    S.rl[c] = 0;
-    S.first[c] = 0xffffffffu;
-  }
-  __syncthreads();
-  ClRaw buf[CL_PF];
-#pragma unroll
-  for (int k = 0; k < CL_PF; ++k) buf[k] = cl_fetch(key, rl, cell, beg + 64 * k, end);
-  bool aux_bad = false;
-  for (size_t first = beg; first < end; first += 64 * CL_PF) {
-    ClMsg m[CL_PF];
-    ClPeer p[CL_PF];
-#pragma unroll
-    for (int k = 0; k < CL_PF; ++k) {
-      const size_t f = first + 64 * k;
-      aux_bad |= f + lane < end && buf[k].cell >= C;
-      m[k] = cl_decode(buf[k], C);  // rounds past the range: cell = ~0, not ok
-      buf[k] = cl_fetch(key, rl, cell, f + 64 * CL_PF, end);
-      p[k] = cl_peer<1>(m[k], f, cbits);
+  for (u32 c = threadIdx.x; c < C; c += WK_THREADS) {
+    if (PASS == 1) {
+      S.tc[c] = 0;
+      S.rh[c] = 0;
+      S.rl[c] = 0;
+      S.first[c] = 0xffffffffu;
+    } else {
+      S.tc[c] = agg_tc[g * C + c];
+      S.rh[c] = agg_rh[g * C + c];
+      S.rl[c] = agg_rl[g * C + c];
     }
-#pragma unroll
-    for (int k = 0; k < CL_PF; ++k) cl_commit1(m[k], p[k], S);
   }
-  if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
   __syncthreads();
-  for (u32 c = lane; c < C; c += 64) {
-    agg_tc[g * C + c] = S.tc[c];
-    agg_rh[g * C + c] = S.rh[c];
-    agg_rl[g * C + c] = S.rl[c];
-    agg_first[g * C + c] = S.first[c];
+  ClRaw buf[WK_PF];
+#pragma unroll
+  for (int k = 0; k < WK_PF; ++k) buf[k] = cl_fetch(key, rl, cell, beg + 256 * k + 64 * w, end);
+  bool aux_bad = false;
+  for (size_t gfirst = beg; gfirst < end; gfirst += 256 * WK_PF) {  // uniform over the workgroup
+#pragma unroll
+    for (int k = 0; k < WK_PF; ++k) {
+      const size_t f = gfirst + 256 * k + 64 * w;  // this wave's round
+      if (PASS == 1) aux_bad |= f + lane < end && buf[k].cell >= C;
+      const ClMsg m = cl_decode(buf[k], C);  // past the range: cell = ~0, not ok
+      buf[k] = cl_fetch(key, rl, cell, f + 256 * WK_PF, end);
+      const ClPeer p = cl_peer<PASS>(m, f, cbits);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (w == t) {
+          if (PASS == 1) cl_commit1(m, p, S);
+          else cl_commit2(m, p, S, flags, f + lane, end);
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (PASS == 1) {
+    if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
+    for (u32 c = threadIdx.x; c < C; c += WK_THREADS) {
+      agg_tc[g * C + c] = S.tc[c];
+      agg_rh[g * C + c] = S.rh[c];
+      agg_rl[g * C + c] = S.rl[c];
+      agg_first[g * C + c] = S.first[c];
+    }
   }
 }
 
-// Pass 2: re-walk the range with the carried state (the cell maxima of all
-// earlier ranges and the prior rows) -> flags.
-__global__ __launch_bounds__(64) void k_cl_scan2(const uint4* __restrict__ key, const u32* __restrict__ rl,
-                                                 const u32* __restrict__ cell, size_t n, u32 C, int cbits,
-                                                 size_t range_len, const u64* __restrict__ agg_tc,
-                                                 const u64* __restrict__ agg_rh, const u32* __restrict__ agg_rl,
-                                                 uint8_t* __restrict__ flags) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  ClState S;
-  S.tc = reinterpret_cast<u64*>(smem);
-  S.rh = S.tc + C;
-  S.rl = reinterpret_cast<u32*>(S.rh + C);
-  S.first = nullptr;
-  const int lane = threadIdx.x;
-  const size_t g = blockIdx.x;
-  const size_t beg = g * range_len;
-  const size_t end = min(n, beg + range_len);
-  for (u32 c = lane; c < C; c += 64) {
-    S.tc[c] = agg_tc[g * C + c];
-    S.rh[c] = agg_rh[g * C + c];
-    S.rl[c] = agg_rl[g * C + c];
-  }
-  __syncthreads();
-  ClRaw buf[CL_PF];
-#pragma unroll
-  for (int k = 0; k < CL_PF; ++k) buf[k] = cl_fetch(key, rl, cell, beg + 64 * k, end);
-  for (size_t first = beg; first < end; first += 64 * CL_PF) {
-    ClMsg m[CL_PF];
-    ClPeer p[CL_PF];
-#pragma unroll
-    for (int k = 0; k < CL_PF; ++k) {
-      m[k] = cl_decode(buf[k], C);  // rounds past the range: cell = ~0, not ok
-      buf[k] = cl_fetch(key, rl, cell, first + 64 * (k + CL_PF), end);
-      p[k] = cl_peer<2>(m[k], first + 64 * k, cbits);
-    }
-#pragma unroll
-    for (int k = 0; k < CL_PF; ++k) cl_commit2(m[k], p[k], S, flags, first + 64 * k + lane, end);
-  }
+__global__ __launch_bounds__(WK_THREADS) void k_cl_scan1(const uint4* __restrict__ key, const u32* __restrict__ rl,
+                                                         const u32* __restrict__ cell, size_t n, u32 C, int cbits,
+                                                         size_t range_len, u64* __restrict__ agg_tc,
+                                                         u64* __restrict__ agg_rh, u32* __restrict__ agg_rl,
+                                                         u32* __restrict__ agg_first, Info* __restrict__ info) {
+  cl_walk<1>(key, rl, cell, n, C, cbits, range_len, agg_tc, agg_rh, agg_rl, agg_first, nullptr, info);
+}
+
+__global__ __launch_bounds__(WK_THREADS) void k_cl_scan2(const uint4* __restrict__ key, const u32* __restrict__ rl,
+                                                         const u32* __restrict__ cell, size_t n, u32 C, int cbits,
+                                                         size_t range_len, u64* __restrict__ agg_tc,
+                                                         u64* __restrict__ agg_rh, u32* __restrict__ agg_rl,
+                                                         uint8_t* __restrict__ flags) {
+  cl_walk<2>(key, rl, cell, n, C, cbits, range_len, agg_tc, agg_rh, agg_rl, nullptr, flags, nullptr);
 }
 
 // Carry: per cell, exclusive scan of the range aggregates in batch order,
@@ -597,7 +592,7 @@ constexpr int XP_ITEMS = 16;
 constexpr int XP_TILE = XP_THREADS * XP_ITEMS;  // 16384 pairs staged in 128 KiB of LDS
 constexpr u32 XP_SLOTS = 32768;                 // LDS set: u32 slots, 128 KiB
 constexpr u32 XP_MAX_FILL = 24576;              // bucket capacity cap (75 % load)
-constexpr u32 XP_AVG = 20000;                   // target mean bucket size
+constexpr u32 XP_AVG = 10000;                   // target mean bucket size (LDS set load <= ~0.4: short probe chains)
 constexpr int XP_MAX_KB = 11;                   // 2048 buckets: n > 41M overfills them -> exact fallback
 constexpr int XD_ITEMS = (XP_MAX_FILL + XP_THREADS - 1) / XP_THREADS;  // pairs per thread in k_xp_dedup
 
@@ -893,7 +888,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
                       uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
   int st;
   size_t range = (n + CL_RANGE_TARGET - 1) / CL_RANGE_TARGET;
-  range = std::max<size_t>(2048, (range + 63) / 64 * 64);
+  range = std::max<size_t>(2048, (range + 255) / 256 * 256);
   const size_t G = (n + range - 1) / range;
   const int cbits = C > 1 ? 32 - __builtin_clz(C - 1) : 0;
   uint4* key = S.alloc<uint4>(n);
@@ -908,7 +903,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   // K1: parse, canonical check, murmur3, minute -- at full occupancy
   {
     evm::ProfScope ps_(ctx, "k_cl_pack");
-    const dim3 g(std::min<size_t>((n + 255) / 256, 2048));
+    const dim3 g(std::min<size_t>((n + 255) / 256, 2048));  // (8192 measured 5 % slower inside the pipeline)
     if (stride == 48 && ((uintptr_t)ts & 15) == 0)
       hipLaunchKernelGGL(k_cl_pack<true>, g, dim3(CLP_THREADS), 0, ctx->stream, (const uint8_t*)ts, stride, n, key,
                          rl, hash, minute, info);
@@ -917,7 +912,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
                          rl, hash, minute, info);
   }
   // pass 1: per range and cell, the max timestamp and its first index
-  KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(64), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
+  KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
               a_first, info);
   // cross-cell PK check: partition by hash into fixed-capacity buckets, LDS set per bucket
   int kb = 0;
@@ -952,7 +947,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
     KLAUNCH(k_cl_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh,
             s_rl);
   }
-  KLAUNCH_LDS(k_cl_scan2, dim3(G), dim3(64), (size_t)C * 20, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
+  KLAUNCH_LDS(k_cl_scan2, dim3(G), dim3(WK_THREADS), (size_t)C * 20, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
               flags);
   // Merkle fold
   u32* px = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN);

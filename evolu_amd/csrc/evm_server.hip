@@ -324,19 +324,14 @@ __global__ void k_sv_owner_off(const u32* __restrict__ owner, size_t n, u32 n_ow
 //      XOR-combine, as repeated insertIntoMerkleTree calls do -- straight into
 //      the new store and tree.
 constexpr int SVO_THREADS = 256;
-constexpr u32 SVO_CAP = 2048;
-constexpr int SVO_PER = SVO_CAP / SVO_THREADS;  // sorted positions per thread
-constexpr u32 SVO_POS_BITS = 11;
-static_assert((1u << SVO_POS_BITS) == SVO_CAP, "position field");
+constexpr u32 SVO_CAP = 4096;  // largest share of one owner handled in LDS
+constexpr int SVO_TIE_MAX = 32;  // longest run of one (millis, counter) with distinct nodes
+constexpr u32 SVO_BUCKET_MAX = 16;  // counting-sort bucket size finished by insertion sort
 
 struct SvoStatus {
-  u32 big;       // an owner's share of the batch exceeds SVO_CAP
-  u32 unsorted;  // an owner's new leaves mix key lengths (code order != minute order)
+  u32 big;       // an owner's share exceeds the launch's capacity
+  u32 fallback;  // a share spans > 2^37 ms, a tie run is longer than SVO_TIE_MAX, or new leaves mix key lengths
 };
-
-__device__ __forceinline__ bool svo_less(u64 ta, u64 ha, u32 xa, u64 tb, u64 hb, u32 xb) {
-  return ta != tb ? ta < tb : (ha != hb ? ha < hb : xa < xb);
-}
 
 // first k in [lo, hi) with a[k] >= x
 __device__ __forceinline__ u64 lb_u64(const u64* a, u64 lo, u64 hi, u64 x) {
@@ -348,21 +343,39 @@ __device__ __forceinline__ u64 lb_u64(const u64* a, u64 lo, u64 hi, u64 x) {
   return lo;
 }
 
+template <u32 CAP>
+struct SvoLog2 {
+  static constexpr int v = CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;
+};
+
+// Phase A for owners whose share is <= CAP.  LDS by batch position t (the
+// owner's share in batch order): node ranks, batch index, hash; sort keys
+// (tc - tc_min) << PB | t, sorted by a bitonic network (8-B elements only);
+// runs of one tc (distinct nodes) are then put in node order.
+template <u32 CAP>
 __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u64* __restrict__ seg, StoreView st,
     const u64* __restrict__ t_off, const u64* __restrict__ t_ck, u64 id_base, uint8_t* __restrict__ flags,
     u64* __restrict__ n_tc, u64* __restrict__ n_hi, u32* __restrict__ n_lo, u64* __restrict__ n_id,
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status) {
-  __shared__ u64 s_tc[SVO_CAP];
-  __shared__ u64 s_hi[SVO_CAP];
-  __shared__ u32 s_x[SVO_CAP];  // rank_lo << SVO_POS_BITS | position in the owner's batch share
+  constexpr int PER = CAP / SVO_THREADS;
+  constexpr int PB = SvoLog2<CAP>::v;
+  constexpr u64 PMASK = CAP - 1;
+  __shared__ u64 s_k[CAP];   // sort keys; later: minute / hash of the inserted rows
+  __shared__ u64 s_rh[CAP];  // by position: node ranks 0..11; later: per-leaf XOR / minute
+  __shared__ u32 s_rl[CAP];  //              node ranks 12..15
+  __shared__ u32 s_bi[CAP];  //              batch index
+  __shared__ u32 s_h[CAP];   //              hash
+  __shared__ u32 s_cnt[CAP];  // counting sort: bucket counts, then starts
+  __shared__ u64 s_red[2 * (SVO_THREADS / 64)];
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
   const u32 o = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const u64 a = seg[o];
   const u64 m = seg[o + 1] - a;  // an unsorted owner column (bad ids) may underflow: "big"
   const u64 la = t_off[o], lb = t_off[o + 1];
-  if (m > SVO_CAP || m == 0) {
+  if (m > CAP || m == 0) {
     if (threadIdx.x == 0) {
       if (m) atomicOr(&status->big, 1u);
       cnt_rows[o] = 0;
@@ -373,60 +386,177 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   }
   u32 P = 1;
   while (P < m) P <<= 1;
-  for (u32 t = threadIdx.x; t < P; t += SVO_THREADS) {
+  // gather: all batch indices, then all records (independent loads in flight)
+  u32 bi[PER];
+  u64 tc[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const u32 t = threadIdx.x + k * SVO_THREADS;
+    bi[k] = t < m ? perm[a + t] : 0u;
+  }
+  u64 tmin = ~0ull, tmax = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const u32 t = threadIdx.x + k * SVO_THREADS;
     if (t < m) {
-      const evm_rec r = rec[perm[a + t]];
+      const evm_rec r = rec[bi[k]];
       u64 hi;
       u32 lo;
       node_ranks(r.node, r.meta & EVM_META_CASEMASK, &hi, &lo);
-      s_tc[t] = r.tc;
-      s_hi[t] = hi;
-      s_x[t] = (lo << SVO_POS_BITS) | t;
-    } else {
-      s_tc[t] = ~0ull;
-      s_hi[t] = ~0ull;
-      s_x[t] = ~0u;
+      s_rh[t] = hi;
+      s_rl[t] = lo;
+      s_bi[t] = bi[k];
+      s_h[t] = r.hash;
+      tc[k] = r.tc;
+      tmin = min(tmin, r.tc);
+      tmax = max(tmax, r.tc);
+    }
+  }
+  tmin = wave_min(tmin);
+  tmax = wave_max(tmax);
+  if (lane == 0) {
+    s_red[wv] = tmin;
+    s_red[SVO_THREADS / 64 + wv] = tmax;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < SVO_THREADS / 64; ++w) {
+    tmin = min(tmin, s_red[w]);
+    tmax = max(tmax, s_red[SVO_THREADS / 64 + w]);
+  }
+  if ((tmax - tmin) >> (64 - PB)) {  // span too wide for the 64-bit sort key
+    if (threadIdx.x == 0) atomicOr(&status->fallback, 1u);
+    return;
+  }
+  // order by (tc, position): a counting sort over CAP buckets of the tc span
+  // (shares spread over time land ~1 per bucket), each bucket finished by an
+  // insertion sort; a share with a crowded bucket (bursts) takes the bitonic
+  // network instead.
+  const int sbits = (tmax - tmin) ? 64 - __builtin_clzll(tmax - tmin) : 0;
+  const int shift = sbits > PB ? sbits - PB : 0;
+  for (u32 t = threadIdx.x; t < CAP; t += SVO_THREADS) s_cnt[t] = 0;
+  __syncthreads();
+  u32 bk[PER], rk[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const u32 t = threadIdx.x + k * SVO_THREADS;
+    bk[k] = rk[k] = 0;
+    if (t < m) {
+      bk[k] = (u32)((tc[k] - tmin) >> shift);
+      rk[k] = atomicAdd(&s_cnt[bk[k]], 1u);
     }
   }
   __syncthreads();
-  // bitonic sort, ascending by (tc, rank_hi, rank_lo, position)
-  for (u32 k = 2; k <= P; k <<= 1) {
-    for (u32 j = k >> 1; j > 0; j >>= 1) {
-      for (u32 t = threadIdx.x; t < P / 2; t += SVO_THREADS) {
-        const u32 i = 2 * t - (t & (j - 1)), l = i + j;
-        const u64 ta = s_tc[i], tb = s_tc[l], ha = s_hi[i], hb = s_hi[l];
-        const u32 xa = s_x[i], xb = s_x[l];
-        if (svo_less(tb, hb, xb, ta, ha, xa) == ((i & k) == 0)) {
-          s_tc[i] = tb;
-          s_tc[l] = ta;
-          s_hi[i] = hb;
-          s_hi[l] = ha;
-          s_x[i] = xb;
-          s_x[l] = xa;
-        }
+  {
+    u32 loc[PER], sum = 0, mx = 0;
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      loc[r] = s_cnt[threadIdx.x * PER + r];
+      sum += loc[r];
+      mx = max(mx, loc[r]);
+    }
+    u32 run = block_inclusive_scan<u32>(sum, tmp, OpAdd<u32>(), (u32*)nullptr) - sum;
+    block_inclusive_scan<u32>(mx, tmp, OpMax<u32>(), &mx);
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      s_cnt[threadIdx.x * PER + r] = run;
+      run += loc[r];
+    }
+    __syncthreads();
+    if (mx <= SVO_BUCKET_MAX) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const u32 t = threadIdx.x + k * SVO_THREADS;
+        if (t < m) s_k[s_cnt[bk[k]] + rk[k]] = ((tc[k] - tmin) << PB) | t;
       }
       __syncthreads();
+      for (u32 b = threadIdx.x; b < CAP; b += SVO_THREADS) {
+        const u32 e = b + 1 < CAP ? s_cnt[b + 1] : (u32)m;
+        for (u32 x = s_cnt[b] + 1; x < e; ++x) {
+          const u64 kx = s_k[x];
+          u32 y = x;
+          while (y > s_cnt[b] && s_k[y - 1] > kx) {
+            s_k[y] = s_k[y - 1];
+            --y;
+          }
+          s_k[y] = kx;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const u32 t = threadIdx.x + k * SVO_THREADS;
+        if (t < P) s_k[t] = t < m ? ((tc[k] - tmin) << PB) | t : ~0ull;
+      }
+      __syncthreads();
+      for (u32 k = 2; k <= P; k <<= 1) {
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+          for (u32 t = threadIdx.x; t < P / 2; t += SVO_THREADS) {
+            const u32 i = 2 * t - (t & (j - 1)), l = i + j;
+            const u64 x = s_k[i], y = s_k[l];
+            if ((y < x) == ((i & k) == 0)) {
+              s_k[i] = y;
+              s_k[l] = x;
+            }
+          }
+          __syncthreads();
+        }
+      }
     }
   }
-  // first occurrences not yet stored (thread t owns sorted positions t*SVO_PER ..)
+  __syncthreads();
+  // runs of one tc: order by the node ranks (then position), insertion sort by
+  // the thread that finds the run's start
+  for (u32 p = threadIdx.x; p + 1 < m; p += SVO_THREADS) {
+    const u64 tp = s_k[p] >> PB;
+    if (s_k[p + 1] >> PB != tp || (p > 0 && s_k[p - 1] >> PB == tp)) continue;
+    u32 e = p + 2;
+    while (e < m && s_k[e] >> PB == tp && e - p <= SVO_TIE_MAX) ++e;
+    if (e - p > SVO_TIE_MAX) {
+      atomicOr(&status->fallback, 1u);
+      continue;
+    }
+    for (u32 x = p + 1; x < e; ++x) {
+      const u64 kx = s_k[x];
+      const u32 px = (u32)(kx & PMASK);
+      const u64 hx = s_rh[px];
+      const u32 lx = s_rl[px];
+      u32 y = x;
+      while (y > p) {
+        const u32 py = (u32)(s_k[y - 1] & PMASK);
+        const u64 hy = s_rh[py];
+        if (hy < hx || (hy == hx && s_rl[py] <= lx)) break;  // equal ranks: positions already ascending
+        s_k[y] = s_k[y - 1];
+        --y;
+      }
+      s_k[y] = kx;
+    }
+  }
+  __syncthreads();
+  // first occurrences not yet stored; thread t owns sorted positions t*PER ..
   const u64 sa = st.off[o], sb = st.off[o + 1];
-  u64 mt[SVO_PER], mh[SVO_PER];
-  u32 ml[SVO_PER], mp[SVO_PER];
+  u64 mt[PER], mh[PER];
+  u32 ml[PER], mb[PER], mhash[PER];
   u32 insm = 0, c = 0;
 #pragma unroll
-  for (int r = 0; r < SVO_PER; ++r) {
-    const u32 p = threadIdx.x * SVO_PER + r;
-    mt[r] = 0;
-    mh[r] = 0;
-    ml[r] = 0;
-    mp[r] = 0;
+  for (int r = 0; r < PER; ++r) {
+    const u32 p = threadIdx.x * PER + r;
+    mt[r] = mh[r] = 0;
+    ml[r] = mb[r] = mhash[r] = 0;
     if (p < m) {
-      const u32 x = s_x[p];
-      mt[r] = s_tc[p];
-      mh[r] = s_hi[p];
-      ml[r] = x >> SVO_POS_BITS;
-      mp[r] = x & (SVO_CAP - 1);
-      bool ins = p == 0 || s_tc[p - 1] != mt[r] || s_hi[p - 1] != mh[r] || (s_x[p - 1] >> SVO_POS_BITS) != ml[r];
+      const u64 kp = s_k[p];
+      const u32 pos = (u32)(kp & PMASK);
+      mt[r] = tmin + (kp >> PB);
+      mh[r] = s_rh[pos];
+      ml[r] = s_rl[pos];
+      mb[r] = s_bi[pos];
+      mhash[r] = s_h[pos];
+      bool ins = true;
+      if (p > 0) {
+        const u64 kq = s_k[p - 1];
+        const u32 qp = (u32)(kq & PMASK);
+        ins = (kq >> PB) != (kp >> PB) || s_rh[qp] != mh[r] || s_rl[qp] != ml[r];
+      }
       if (ins && sb > sa) {
         const SKey k{o, mt[r], mh[r], ml[r]};
         const size_t q = store_lower(st, sa, sb, k);
@@ -439,27 +569,26 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     }
   }
   u32 M;
-  u32 q = block_inclusive_scan<u32>(c, tmp, OpAdd<u32>(), &M) - c;  // (its barriers free the sort arrays)
-  u32* s_min = reinterpret_cast<u32*>(s_tc);  // inserted rows, sorted: minute
-  u32* s_h = s_min + SVO_CAP;                 //                        hash
-  u32* s_lx = reinterpret_cast<u32*>(s_hi);   // per leaf: XOR
-  u32* s_lm = s_lx + SVO_CAP;                 //           minute
-  for (u32 t = threadIdx.x; t < SVO_CAP; t += SVO_THREADS) s_lx[t] = 0;
+  u32 q = block_inclusive_scan<u32>(c, tmp, OpAdd<u32>(), &M) - c;  // (its barriers free the LDS arrays)
+  u32* s_min = reinterpret_cast<u32*>(s_k);  // inserted rows, sorted: minute
+  u32* s_hq = s_min + CAP;                   //                        hash
+  u32* s_lx = reinterpret_cast<u32*>(s_rh);  // per leaf: XOR
+  u32* s_lm = s_lx + CAP;                    //           minute
+  for (u32 t = threadIdx.x; t < CAP; t += SVO_THREADS) s_lx[t] = 0;
 #pragma unroll
-  for (int r = 0; r < SVO_PER; ++r) {
-    const u32 p = threadIdx.x * SVO_PER + r;
+  for (int r = 0; r < PER; ++r) {
+    const u32 p = threadIdx.x * PER + r;
     if (p < m) {
-      const u32 bi = perm[a + mp[r]];
       const bool ins = (insm >> r) & 1u;
-      flags[bi] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
+      flags[mb[r]] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
       if (ins) {
         const u64 w = a + q;
         n_tc[w] = mt[r];
         n_hi[w] = mh[r];
         n_lo[w] = ml[r];
-        n_id[w] = id_base + bi;
-        s_min[q] = rec[bi].minute;
-        s_h[q] = rec[bi].hash;
+        n_id[w] = id_base + mb[r];
+        s_min[q] = (u32)((mt[r] >> 16) / 60000ull);  // == rec.minute on the native domain
+        s_hq[q] = mhash[r];
         ++q;
       }
     }
@@ -468,8 +597,8 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   // leaves: runs of one minute among the inserted rows (sorted by millis)
   u32 hm = 0, hc = 0;
 #pragma unroll
-  for (int r = 0; r < SVO_PER; ++r) {
-    const u32 p = threadIdx.x * SVO_PER + r;
+  for (int r = 0; r < PER; ++r) {
+    const u32 p = threadIdx.x * PER + r;
     if (p < M && (p == 0 || s_min[p] != s_min[p - 1])) {
       hm |= 1u << r;
       ++hc;
@@ -478,15 +607,15 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   u32 NL;
   int lid = (int)(block_inclusive_scan<u32>(hc, tmp, OpAdd<u32>(), &NL) - hc) - 1;
 #pragma unroll
-  for (int r = 0; r < SVO_PER; ++r) {
-    const u32 p = threadIdx.x * SVO_PER + r;
+  for (int r = 0; r < PER; ++r) {
+    const u32 p = threadIdx.x * PER + r;
     if (p < M) {
       if ((hm >> r) & 1u) s_lm[++lid] = s_min[p];
-      atomicXor(&s_lx[lid], s_h[p]);
+      atomicXor(&s_lx[lid], s_hq[p]);
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0 && NL && base3_len(s_lm[0]) != base3_len(s_lm[NL - 1])) atomicOr(&status->unsorted, 1u);
+  if (threadIdx.x == 0 && NL && base3_len(s_lm[0]) != base3_len(s_lm[NL - 1])) atomicOr(&status->fallback, 1u);
   u32 dups = 0;
   for (u32 l = threadIdx.x; l < NL; l += SVO_THREADS) {
     const u64 code = ((u64)o << 40) | minute_code(s_lm[l]);
@@ -549,18 +678,19 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   // leaves: union of the tree's and the new ones by code, equal codes XOR-combined
   const u64 la = t_off[o], lb = t_off[o + 1];
   const u64 lbase = leaf_pos[o];
-  u32 d[SVO_PER], c = 0;
+  constexpr int PERB = SVO_CAP / SVO_THREADS;
+  u32 d[PERB], c = 0;
 #pragma unroll
-  for (int r = 0; r < SVO_PER; ++r) {
-    const u32 j = threadIdx.x * SVO_PER + r;
+  for (int r = 0; r < PERB; ++r) {
+    const u32 j = threadIdx.x * PERB + r;
     d[r] = j < NL ? (u32)l_dup[a + j] : 0u;
     c += d[r];
   }
   u32 dtot;
   u32 run = block_inclusive_scan<u32>(c, tmp, OpAdd<u32>(), &dtot) - c;
 #pragma unroll
-  for (int r = 0; r < SVO_PER; ++r) {
-    const u32 j = threadIdx.x * SVO_PER + r;
+  for (int r = 0; r < PERB; ++r) {
+    const u32 j = threadIdx.x * PERB + r;
     if (j < NL) s_dp[j] = run;
     run += d[r];
   }
@@ -727,26 +857,36 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   const int obits = O > 1 ? 32 - __builtin_clz(O - 1) : 0;
   if ((st = radix_sort_pairs<u32>(ctx, S, ok, ov, n, 0, obits))) return st;
   KLAUNCH(k_sv_owner_off, dim3(grid_for((size_t)O + 1, 256)), dim3(256), ok, n, O, seg);
-  HIPR(hipMemsetAsync(status, 0, sizeof(SvoStatus), ctx->stream));
   const evm_tree* t = s->tree;
   u32 *c_rows = cnt, *c_new = cnt + O, *c_leaves = cnt + 2 * (size_t)O;
-  KLAUNCH(k_svo_a, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off, (const u64*)t->ck,
-          (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves, status);
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, O, pos, tot))) return st;
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, O, pos + O, tot + 1))) return st;
   Info hi;
   SvoStatus hs;
   u32 ht[2];
-  HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipMemcpyAsync(ht, tot, sizeof(ht), hipMemcpyDeviceToHost, ctx->stream));
-  if ((st = read_info(ctx, info, &hi))) return st;
-  if (hi.bad_aux) return EVM_EINVAL;
-  if (hi.bad) {
-    KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
-    (void)evm_sync(ctx);
-    return EVM_ENONCANON;
+  // the common share size first (more workgroups per CU); larger shares retry once
+  for (int pass = 0; pass < 2; ++pass) {
+    HIPR(hipMemsetAsync(status, 0, sizeof(SvoStatus), ctx->stream));
+    if (pass == 0)
+      KLAUNCH(k_svo_a<1024>, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off,
+              (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new,
+              c_leaves, status);
+    else
+      KLAUNCH(k_svo_a<SVO_CAP>, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off,
+              (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new,
+              c_leaves, status);
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, O, pos, tot))) return st;
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, O, pos + O, tot + 1))) return st;
+    HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipMemcpyAsync(ht, tot, sizeof(ht), hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = read_info(ctx, info, &hi))) return st;
+    if (hi.bad_aux) return EVM_EINVAL;
+    if (hi.bad) {
+      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
+      (void)evm_sync(ctx);
+      return EVM_ENONCANON;
+    }
+    if (!hs.big || hs.fallback) break;
   }
-  if (hs.big || hs.unsorted) return EVM_OK;  // the sort path redoes the flags
+  if (hs.big || hs.fallback) return EVM_OK;  // the sort path redoes the flags
   // new store and tree, exactly sized
   if ((st = store_alloc(ctx, ns, O, s->n + ht[0]))) {
     store_release_arrays(ctx, ns);

@@ -121,9 +121,13 @@ def config2(n: int = 10_000_000, n_cells: int = 1000, n_nodes: int = 64, stride:
 
 
 def config3(n_owners: int = 100_000, per_owner: int = 1000, nodes_per_owner: int = 4, stride: int = 48,
-            seed_config: int = 3):
-    """Server ingest: n_owners x per_owner messages, messages grouped by owner request,
-    owners interleaved; returns (ts arena, owner ids, client-prefix mask)."""
+            seed_config: int = 3, request: int = 100):
+    """Server ingest: n_owners x per_owner messages, as the server receives
+    them: SyncRequests of one owner each (index.ts:224-248), `request`
+    messages per request (an owner's messages in random order, cut into
+    requests), requests of all owners in random order; request=1 shuffles
+    single messages (no request structure).  Returns (ts arena, owner ids,
+    millis), in batch order."""
     rng = rng_for(seed_config)
     n = n_owners * per_owner
     per = np.full(n_owners * nodes_per_owner, per_owner // nodes_per_owner, dtype=np.int64)
@@ -131,6 +135,20 @@ def config3(n_owners: int = 100_000, per_owner: int = 1000, nodes_per_owner: int
     millis, counter, nidx = hlc_stream(rng, per, BENCH_T0, 30 * DAY_MS)
     nodes = random_nodes(rng, n_owners * nodes_per_owner)
     owner = (nidx // nodes_per_owner).astype(np.uint32)
-    perm = rng.permutation(n)
+    if request <= 1:
+        perm = rng.permutation(n)
+    else:
+        # messages are owner-major here; shuffle inside each owner, cut into requests, shuffle requests
+        key = owner.astype(np.float64) + rng.random(n)  # random order inside each owner
+        inner = np.argsort(key, kind="stable")
+        rank = np.empty(n, dtype=np.int64)
+        rank[inner] = np.arange(n)
+        start = np.searchsorted(owner[inner], np.arange(n_owners))
+        pos_in_owner = rank - start[owner]
+        req_id = owner.astype(np.int64) * ((per_owner + request - 1) // request) + pos_in_owner // request
+        n_req = n_owners * ((per_owner + request - 1) // request)
+        req_order = rng.permutation(n_req)
+        order_key = req_order[req_id] * (request + 1) + pos_in_owner % request
+        perm = np.argsort(order_key, kind="stable")
     ts = format_timestamps(millis[perm], counter[perm], nodes[nidx[perm]], stride)
     return ts, owner[perm], millis[perm]

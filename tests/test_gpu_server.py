@@ -230,7 +230,7 @@ def torch_tensor(eng, values):
     return torch.tensor(values, dtype=torch.int64, device=eng.device)
 
 
-@pytest.mark.parametrize("n_owners,per_owner", [(3000, 300), (20000, 1000)])
+@pytest.mark.parametrize("n_owners,per_owner", [(3000, 300), (20000, 1000), (50, 3000), (3, 5000)])
 def test_owner_lds_path_vs_sort_path(eng, n_owners, per_owner):
     """The per-owner LDS ingest (K5) and the global sort path are independent
     device algorithms: on config-3-shaped batches with redeliveries, fed in
@@ -263,3 +263,42 @@ def test_owner_lds_path_vs_sort_path(eng, n_owners, per_owner):
         assert np.array_equal(x, y)
     # every distinct (owner, timestamp) is inserted exactly once (config-3 nodes are per owner)
     assert (res[0][0] == L.MSG_INS).sum() == len(np.unique(np.ascontiguousarray(ts_np[:, :46]).view("S46")))
+
+
+def test_owner_lds_path_bursts_vs_oracle(eng):
+    """Owners whose timestamps crowd a few milliseconds (plus far outliers):
+    the LDS path's counting sort overflows its buckets and the bitonic
+    network orders the share; equal (millis, counter) with distinct nodes are
+    ordered by the node bytes.  Checked against the verbatim-SQL oracle and
+    against the global sort path."""
+    from evolu_amd import _lib as L
+
+    rng = random.Random(77)
+    owners = ["%021x" % rng.getrandbits(84) for _ in range(12)]
+    reqs = []
+    for o in owners:
+        nodes = [W.node_id(rng, upper=rng.random() < 0.3) for _ in range(8)]
+        ms = [O.timestamp_to_string(W.T0 + rng.randrange(1000), rng.randrange(4), rng.choice(nodes)) for _ in range(300)]
+        ms += [O.timestamp_to_string(W.T0 + 10 * 86_400_000 + k, 0, nodes[0]) for k in range(2)]
+        ms += ms[:20]  # redeliveries
+        rng.shuffle(ms)
+        reqs.append((o, ms))
+    got = []
+    for path in (1, 2):
+        eng.set_option(L.OPT_SERVER_PATH, path)
+        store, flags, id_ts = _run_batches(eng, owners, [reqs[:6], reqs[6:]])
+        off, ids = store.messages()
+        tree = store.tree()
+        got.append(([list(f) for f in flags], [id_ts[int(k)] for k in ids], [tree.to_json(i) for i in range(len(owners))]))
+        store.free()
+    eng.set_option(L.OPT_SERVER_PATH, 0)
+    assert got[0] == got[1]
+    db, ins = _oracle(owners, [reqs[:6], reqs[6:]])
+    assert [[bool(x & L.MSG_INS) for x in f] for f in got[0][0]] == ins
+    for i, o in enumerate(owners):
+        assert got[0][2][i] == O.merkle_tree_to_string(db.get_merkle_tree(o))
+    want_rows = []
+    for o in owners:
+        want_rows += [r[0] for r in db.conn.execute(
+            'SELECT "timestamp" FROM "message" WHERE "userId" = ? ORDER BY "timestamp"', (o,)).fetchall()]
+    assert got[0][1] == want_rows

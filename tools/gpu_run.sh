@@ -22,4 +22,10 @@ timeout -k 10 300 python -u bench.py --workload server --steps 5 --warmup 2 > gp
   2> gpurun_out/bench_server.err
 rc=$?
 echo "bench server rc=$rc"; cat gpurun_out/bench_server.json; tail -3 gpurun_out/bench_server.err
+if fatal $rc; then exit $rc; fi
+
+timeout -k 10 300 python -u bench.py --workload server --steps 5 --warmup 2 --request 1 > gpurun_out/bench_server_shuffled.json \
+  2> gpurun_out/bench_server_shuffled.err
+rc=$?
+echo "bench server (per-message shuffle) rc=$rc"; cat gpurun_out/bench_server_shuffled.json
 exit $rc

@@ -38,6 +38,7 @@ def load(d, counter):
 
 def short(name):
     """Kernel symbol -> the name bench.py's event profiler uses."""
+    name = name.replace("(anonymous namespace)::", "")
     m = re.match(r"(?:void )?(?:evm::)?([A-Za-z_0-9]+)(<[^>(]*>)?", name)
     if not m:
         return name
