@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--messages", type=int, default=10_000_000)
     ap.add_argument("--cells", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0: skip)")
+    ap.add_argument("--overlap", type=int, default=1, help="EVM_OPT_OVERLAP: independent checks on a second stream")
     ap.add_argument("--workload", choices=["client", "server"], default="client",
                     help="client: config 2 applyMessages (headline); server: config 3/4 ingest + diff + select")
     ap.add_argument("--owners", type=int, default=100_000, help="server workload: owners per GPU")
@@ -123,6 +124,7 @@ def main():
     # each rank: its own owner (seed per rank), same shape
     ts_np, cell_np = synth.config2(a.messages, a.cells, seed_config=2 + 1000 * rank)
     eng = Engine(local)
+    eng.set_option(3, a.overlap)  # EVM_OPT_OVERLAP
     ts = eng.dev(ts_np)
     cell = eng.dev(cell_np)
     empty = eng.tree_new(1)
@@ -282,7 +284,11 @@ def server_main(a, rank, world, local):
     t0 = time.perf_counter()
     nsel = 0
     for _ in range(a.steps):
+        s0 = time.perf_counter()
         nsel = step()
+        if os.environ.get("EVM_BENCH_VERBOSE"):
+            torch.cuda.synchronize()
+            print("step %.2f ms" % ((time.perf_counter() - s0) * 1e3), file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     eng.prof_enable(False)

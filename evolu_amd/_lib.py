@@ -33,6 +33,7 @@ MSG_BAD = 0x80
 
 OPT_CLIENT_PATH = 1
 OPT_SERVER_PATH = 2
+OPT_OVERLAP = 3
 
 PB_SYNC_REQUEST = 1
 PB_SYNC_RESPONSE = 2
@@ -75,6 +76,7 @@ SIGNATURES = {
     "evm_tree_from_json": (_i, [_vp, _u32, C.POINTER(C.c_char_p), C.POINTER(_sz), C.POINTER(_vp)]),
     "evm_merkle_insert": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, C.POINTER(_vp)]),
     "evm_merkle_diff": (_i, [_vp, _vp, _vp, _vp]),
+    "evm_tree_merge": (_i, [_vp, _vp, _vp, C.POINTER(_vp)]),
     "evm_receive_fold": (_i, [_vp, _vp, _sz, _sz, C.c_int64, _u32, C.c_char_p, C.c_int64, C.c_int64, _vp]),
     "evm_store_new": (_i, [_vp, _u32, C.POINTER(_vp)]),
     "evm_store_free": (_i, [_vp, _vp]),

@@ -231,7 +231,6 @@ constexpr u32 FOLD_MAXWIN = 4;
 constexpr u32 FOLD_CHUNKS = 128;  // x windows: 256+ single-CU blocks for a 2-window batch
 constexpr int FOLD_THREADS = 1024;
 
-constexpr int CL_PF = 8;  // rounds of 64 messages a pass wave keeps in flight (24 B each)
 
 struct ClMsg {
   OKey key;
@@ -725,17 +724,20 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __
   if (mlo > mhi) return;  // no valid message
   const u32 nwin = (mhi - mlo) / FOLD_WIN + 1;
   if (nwin > FOLD_MAXWIN || base3_len(mlo) != base3_len(mhi)) {
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicOr(&info->fold_overflow, 1u);
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&info->fold_overflow, 1u);
     return;
   }
-  const u32 w = blockIdx.y;
+  // block b -> (chunk, window) with the windows of one chunk on one XCD
+  // (workgroups go round-robin over the 8 XCDs): the chunk's second read is
+  // an L2 hit
+  const u32 b = blockIdx.x, w = (b / 8) % FOLD_MAXWIN, chunk = (b / (8 * FOLD_MAXWIN)) * 8 + b % 8;
   if (w >= nwin) return;
   for (u32 b = threadIdx.x; b < FOLD_WIN; b += FOLD_THREADS) hist[b] = 0;
   for (u32 b = threadIdx.x; b < FOLD_WIN / 32; b += FOLD_THREADS) pres[b] = 0;
   __syncthreads();
   const u32 base = mlo + w * FOLD_WIN;
   const size_t per = ((n + FOLD_CHUNKS - 1) / FOLD_CHUNKS + 3) & ~(size_t)3;
-  const size_t a = (size_t)blockIdx.x * per, e = min(n, a + per);
+  const size_t a = (size_t)chunk * per, e = min(n, a + per);
   // 4 messages per thread per step: one 32-bit load of flags
   for (size_t i = a + 4 * (size_t)threadIdx.x; i < e; i += 4 * FOLD_THREADS) {
     if (i + 4 <= e) {
@@ -762,7 +764,7 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __
     }
   }
   __syncthreads();
-  const size_t slot = (size_t)w * FOLD_CHUNKS + blockIdx.x;
+  const size_t slot = (size_t)w * FOLD_CHUNKS + chunk;
   for (u32 b = threadIdx.x; b < FOLD_WIN; b += FOLD_THREADS) px[slot * FOLD_WIN + b] = hist[b];
   for (u32 b = threadIdx.x; b < FOLD_WIN / 32; b += FOLD_THREADS) pp[slot * (FOLD_WIN / 32) + b] = pres[b];
 }
@@ -923,15 +925,21 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   u32* xcur = S.alloc<u32>((size_t)1 << kb);
   u64* xpairs = S.alloc<u64>(((size_t)cap) << kb);
   if (!xcur || !xpairs) return EVM_ENOMEM;
-  HIPR(hipMemsetAsync(xcur, 0, sizeof(u32) << kb, ctx->stream));
+  // it reads only the timestamps, cells and hashes: a second stream runs it
+  // beside the walks (joined before the status read)
+  SideFork side(ctx);
   {
-    evm::ProfScope ps_(ctx, "k_xp_scatter");
-    hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), 0, ctx->stream, hash, n, kb, cap, xcur, xpairs, info);
-  }
-  {
-    evm::ProfScope ps_(ctx, "k_xp_dedup");
-    hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, ctx->stream, xpairs, xcur, cap, n,
-                       (const uint8_t*)ts, stride, cell, info);
+    const hipStream_t xs = side.stream();
+    HIPR(hipMemsetAsync(xcur, 0, sizeof(u32) << kb, xs));
+    {
+      evm::ProfScope ps_(ctx, "k_xp_scatter", xs);
+      hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), 0, xs, hash, n, kb, cap, xcur, xpairs, info);
+    }
+    {
+      evm::ProfScope ps_(ctx, "k_xp_dedup", xs);
+      hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, xpairs, xcur, cap, n,
+                         (const uint8_t*)ts, stride, cell, info);
+    }
   }
   // carry: per cell, exclusive scan over ranges seeded with the prior max
   {
@@ -960,7 +968,8 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   u64* lck = S.alloc<u64>(B);
   int32_t* lxr = S.alloc<int32_t>(B);
   if (!px || !pp || !dx || !dp || !bcnt || !bxor || !lck || !lxr) return EVM_ENOMEM;
-  KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
+  static_assert(FOLD_CHUNKS % 8 == 0, "chunk <-> XCD mapping");
+  KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS * FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
   KLAUNCH(k_cl_fold_reduce, dim3(FR_BLOCKS), dim3(FR_THREADS), px, pp, info, dx, dp, bcnt, bxor);
   // into an empty tree: build the output speculatively, so the call has one
   // host round trip; one owner: the leaf kernel writes the tree itself
@@ -983,6 +992,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
       if (t) tree_destroy(ctx, t);
     }
   } guard{ctx, spec};
+  side.join();
   Info hi;
   if ((st = read_info(ctx, info, &hi))) return st;
   if (hi.bad) {

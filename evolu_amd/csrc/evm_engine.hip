@@ -524,6 +524,10 @@ int evm_create(int device, evm_ctx** out) {
     return EVM_EDEVICE;
   }
   c->stream = c->own;
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
+    c->overlap = 0;
   // keep freed scratch in the stream-ordered pool between calls
   hipMemPool_t pool;
   if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
@@ -540,6 +544,10 @@ void evm_destroy(evm_ctx* ctx) {
   for (hipEvent_t e : ctx->prof_pool) (void)hipEventDestroy(e);
   if (ctx->xtab) (void)hipFree(ctx->xtab);
   if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -561,6 +569,10 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
   if (!ctx) return EVM_EINVAL;
   if (option == EVM_OPT_CLIENT_PATH && value >= 0 && value <= 2) {
     ctx->client_path = (int)value;
+    return EVM_OK;
+  }
+  if (option == EVM_OPT_OVERLAP && (value == 0 || value == 1)) {
+    ctx->overlap = (int)value;
     return EVM_OK;
   }
   if (option == EVM_OPT_SERVER_PATH && value >= 0 && value <= 2) {
@@ -768,6 +780,15 @@ int evm_merkle_insert(evm_ctx* ctx, const evm_tree* in, const char* ts, size_t s
   if (hi.bad_aux) return EVM_EINVAL;
   if (hi.bad) return EVM_ENONCANON;
   st = fold_into_tree(ctx, S, in, in->n_owners, ck, h, n, hi, out);
+  if (st) return st;
+  return evm_sync(ctx);
+}
+
+int evm_tree_merge(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, evm_tree** out) {
+  if (!ctx || !a || !b || !out || a->n_owners != b->n_owners) return EVM_EINVAL;
+  Scratch S(ctx);
+  // b's leaves are sorted and unique per owner; equal keys XOR-combine
+  const int st = merge_into_tree(ctx, S, a, a->n_owners, (const u64*)b->ck, b->xr, b->n_leaves, out);
   if (st) return st;
   return evm_sync(ctx);
 }

@@ -18,6 +18,9 @@ struct evm_ctx {
   bool prof = false;
   int client_path = 0;  // EVM_OPT_CLIENT_PATH
   int server_path = 0;  // EVM_OPT_SERVER_PATH
+  int overlap = 1;      // EVM_OPT_OVERLAP: independent checks on a second stream
+  hipStream_t side = nullptr;  // second stream (forked from / joined to `stream` inside a call)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> prof_events;
   std::map<std::string, std::pair<double, uint64_t>> prof_total;  // ms, launches (drained)
   std::vector<hipEvent_t> prof_pool;  // recycled events: no hipEventCreate inside a timed loop
@@ -139,12 +142,12 @@ class Scratch {
 // Records a start/stop event pair around one launch when profiling is on.
 class ProfScope {
  public:
-  ProfScope(evm_ctx* c, const char* name) : ctx_(c), name_(name) {
+  ProfScope(evm_ctx* c, const char* name, hipStream_t s = nullptr) : ctx_(c), name_(name), s_(s ? s : c->stream) {
     if (!ctx_->prof) return;
     a_ = take();
     b_ = take();
     if (a_ && b_) {
-      (void)hipEventRecord(a_, ctx_->stream);
+      (void)hipEventRecord(a_, s_);
     } else {
       if (a_) ctx_->prof_pool.push_back(a_);
       if (b_) ctx_->prof_pool.push_back(b_);
@@ -153,7 +156,7 @@ class ProfScope {
   }
   ~ProfScope() {
     if (a_ && b_) {
-      (void)hipEventRecord(b_, ctx_->stream);
+      (void)hipEventRecord(b_, s_);
       ctx_->prof_events[name_].push_back({a_, b_});
     }
   }
@@ -170,7 +173,31 @@ class ProfScope {
   }
   evm_ctx* ctx_;
   const char* name_;
+  hipStream_t s_;
   hipEvent_t a_ = nullptr, b_ = nullptr;
+};
+
+// Work forked onto ctx->side after everything queued on ctx->stream so far;
+// the destructor joins it back (ctx->stream waits for it) on every path out.
+class SideFork {
+ public:
+  explicit SideFork(evm_ctx* c) : ctx_(c) {
+    on_ = ctx_->overlap && ctx_->side && hipEventRecord(ctx_->ev_fork, ctx_->stream) == hipSuccess &&
+          hipStreamWaitEvent(ctx_->side, ctx_->ev_fork, 0) == hipSuccess;
+  }
+  hipStream_t stream() const { return on_ ? ctx_->side : ctx_->stream; }
+  void join() {
+    if (on_) {
+      (void)hipEventRecord(ctx_->ev_join, ctx_->side);
+      (void)hipStreamWaitEvent(ctx_->stream, ctx_->ev_join, 0);
+      on_ = false;
+    }
+  }
+  ~SideFork() { join(); }
+
+ private:
+  evm_ctx* ctx_;
+  bool on_ = false;
 };
 
 // Every kernel launch goes through KLAUNCH (needs `ctx` in scope).

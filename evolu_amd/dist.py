@@ -13,6 +13,17 @@ host assigns, e.g. from murmur3(ownerId)), and
   which the reference's first-occurrence rules depend on;
 * per-owner roots are all-gathered (RCCL has no XOR reduction; nothing needs
   one: every owner lives on exactly one rank).
+
+Hot owners (a skewed owner distribution, BASELINE config 5: Zipf 1.2, the
+top owner ~18 % of all messages) would pin one rank.  `OwnerMap` splits
+them: a hot owner lives on every rank, and each of its messages goes to the
+rank a hash of its timestamp bytes picks.  Every copy of one (owner,
+timestamp) therefore lands on one rank, so the server's INSERT OR IGNORE
+dedup (index.ts:154) stays exact per rank; the owner's Merkle tree is the
+XOR-combination of its per-rank partial trees (insertIntoMerkleTree is
+order-independent, merkleTree.test.ts:30-42): partial roots XOR together
+(`gather_hot_roots`), partial leaf lists merge on the device
+(`merge_hot_trees`, evm_tree_merge).
 """
 from __future__ import annotations
 
@@ -31,20 +42,93 @@ def local_owner(owner: torch.Tensor, world: int) -> torch.Tensor:
     return (owner // world).to(torch.int32)
 
 
-def route_by_owner(ts: torch.Tensor, owner: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor,
-                                                                                  torch.Tensor]:
+def ts_route_hash(ts: torch.Tensor) -> torch.Tensor:
+    """A fixed 63-bit mix of the 46 timestamp bytes of each row (routing only:
+    equal timestamps -> equal hashes)."""
+    n, stride = ts.shape
+    b = ts[:, :46].to(torch.int64)
+    h = torch.zeros(n, dtype=torch.int64, device=ts.device)
+    for k in range(0, 46, 7):  # 7 bytes per step: no sign trouble in int64
+        w = torch.zeros(n, dtype=torch.int64, device=ts.device)
+        for j in range(k, min(k + 7, 46)):
+            w = w | (b[:, j] << (8 * (j - k)))
+        h = ((h * 1000003) ^ w) & 0x7FFFFFFFFFFFFFFF
+    return h
+
+
+class OwnerMap:
+    """Global owner id -> (rank, local owner id).
+
+    A cold owner o lives on rank o % world as local owner o // world.  Hot
+    owner hot[h] lives on every rank as local owner `per + h` (per = the
+    cold slots per rank) and takes the messages whose timestamp hash picks
+    that rank."""
+
+    def __init__(self, n_owners: int, world: int, rank: int, hot: Optional[torch.Tensor] = None):
+        self.n_owners = n_owners
+        self.world = world
+        self.rank = rank
+        self.per = (n_owners + world - 1) // world
+        self.hot = (hot if hot is not None else torch.zeros(0, dtype=torch.int64)).to(torch.int64).sort().values
+        self.n_local = self.per + int(self.hot.numel())
+
+    def is_hot(self, owner: torch.Tensor) -> torch.Tensor:
+        if self.hot.numel() == 0:
+            return torch.zeros_like(owner, dtype=torch.bool)
+        hot = self.hot.to(owner.device)
+        i = torch.searchsorted(hot, owner.to(torch.int64)).clamp(max=hot.numel() - 1)
+        return hot[i] == owner
+
+    def dest(self, owner: torch.Tensor, ts: torch.Tensor) -> torch.Tensor:
+        d = (owner.to(torch.int64) % self.world)
+        hot = self.is_hot(owner)
+        if bool(hot.any()):
+            d = torch.where(hot, ts_route_hash(ts) % self.world, d)
+        return d
+
+    def local(self, owner: torch.Tensor) -> torch.Tensor:
+        """Local owner ids of messages this rank received."""
+        loc = owner.to(torch.int64) // self.world
+        hot = self.is_hot(owner)
+        if bool(hot.any()):
+            h = torch.searchsorted(self.hot.to(owner.device), owner.to(torch.int64))
+            loc = torch.where(hot, self.per + h, loc)
+        return loc.to(torch.int32)
+
+
+def owner_counts(owner: torch.Tensor, n_owners: int, group=None) -> torch.Tensor:
+    """Messages per global owner over all ranks (all_reduce of local counts)."""
+    c = torch.bincount(owner.to(torch.int64), minlength=n_owners)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(c, group=group)
+    return c
+
+
+def hot_owners(counts: torch.Tensor, world: int, share: float = 0.25) -> torch.Tensor:
+    """Owners holding more than `share` of one rank's fair share of messages."""
+    if world <= 1:
+        return torch.zeros(0, dtype=torch.int64)
+    fair = float(counts.sum().item()) / world
+    return torch.nonzero(counts.cpu() > share * fair).flatten()
+
+
+def route_by_owner(ts: torch.Tensor, owner: torch.Tensor, group=None, dest: Optional[torch.Tensor] = None
+                   ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """All-to-all routing of messages to their owner's rank.
 
     ts: (n, stride) uint8 timestamp rows, owner: (n,) int64 global owner ids,
-    both on this rank.  Returns (ts_recv, owner_recv, src_rank, src_index):
-    the messages this rank owns, in global batch order, with where they came
-    from (to send per-message results back with `route_back`).
+    both on this rank; dest: the rank of every message (default owner %
+    world; OwnerMap.dest splits hot owners).  Returns (ts_recv, owner_recv,
+    src_rank, src_index): the messages this rank owns, in global batch
+    order, with where they came from (to send per-message results back with
+    `route_back`).
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = ts.device
     n, stride = ts.shape
-    dest = owner_rank(owner, world)
+    if dest is None:
+        dest = owner_rank(owner, world)
     order = torch.argsort(dest, stable=True)
     send_counts = torch.bincount(dest, minlength=world).to(torch.int64)
     recv_counts = torch.empty_like(send_counts)
@@ -100,3 +184,55 @@ def gather_roots(root: torch.Tensor, present: torch.Tensor, n_owners_global: int
     dist.all_gather(allr, pad_r, group=group)
     g = torch.stack(allr, 1).reshape(-1)[:n_owners_global]  # row j = local owner j of every rank
     return (g & 0xFFFFFFFF).to(torch.int64).to(torch.int32), (g >> 32) != 0
+
+
+def gather_hot_roots(root: torch.Tensor, present: torch.Tensor, omap: OwnerMap, group=None):
+    """Roots of the split owners: the XOR of the per-rank partial roots
+    (present if any part is).  root/present: this rank's local roots."""
+    nh = int(omap.hot.numel())
+    dev = root.device
+    mine = torch.stack([root[omap.per:omap.per + nh].to(torch.int64) & 0xFFFFFFFF,
+                        present[omap.per:omap.per + nh].to(torch.int64)], 1).contiguous()
+    allp = [torch.empty_like(mine) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(allp, mine, group=group)
+    x = torch.zeros(nh, dtype=torch.int64, device=dev)
+    p = torch.zeros(nh, dtype=torch.bool, device=dev)
+    for t in allp:
+        x = x ^ t[:, 0]
+        p = p | (t[:, 1] != 0)
+    x = torch.where(x >= 2 ** 31, x - 2 ** 32, x)
+    return x.to(torch.int32), p
+
+
+def merge_hot_trees(eng, trees, omap: OwnerMap, group=None):
+    """Full trees of the split owners on every rank: the per-rank partial
+    leaf lists of the hot local owners are all-gathered and XOR-merged on the
+    device (evm_tree_merge).  Returns an engine Trees with one owner per hot
+    owner (in omap.hot order)."""
+    import numpy as np
+
+    nh = int(omap.hot.numel())
+    off, code, xr = trees.leaves()
+    lo, hi = int(off[omap.per]), int(off[omap.per + nh])
+    part_off = (off[omap.per:omap.per + nh + 1] - lo).astype(np.int64)
+    payload = np.concatenate([part_off, code[lo:hi].astype(np.int64), xr[lo:hi].astype(np.int64)])
+    dev = torch.device("cuda", eng.device) if torch.cuda.is_available() else torch.device("cpu")
+    t = torch.from_numpy(payload).to(dev)
+    world = dist.get_world_size(group)
+    sizes = torch.tensor([t.numel()], dtype=torch.int64, device=dev)
+    alls = [torch.empty_like(sizes) for _ in range(world)]
+    dist.all_gather(alls, sizes, group=group)
+    cap = int(max(int(x.item()) for x in alls))
+    pad = torch.zeros(cap, dtype=torch.int64, device=dev)
+    pad[: t.numel()] = t
+    allt = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(allt, pad, group=group)
+    merged = None
+    for r in range(world):
+        a = allt[r].cpu().numpy()
+        po = a[: nh + 1]
+        L = int(po[-1])
+        part = eng.tree_from_leaves(po.astype(np.uint64), a[nh + 1:nh + 1 + L].astype(np.uint64),
+                                    a[nh + 1 + L:nh + 1 + 2 * L].astype(np.int32))
+        merged = part if merged is None else eng.tree_merge(merged, part)
+    return merged

@@ -164,6 +164,12 @@ class Engine:
               "evm_merkle_insert")
         return Trees(self, h)
 
+    def tree_merge(self, a: "Trees", b: "Trees") -> "Trees":
+        """Union of two tree sets' inserts (equal leaves XOR-combine)."""
+        h = C.c_void_p()
+        check(self.lib.evm_tree_merge(self.h, a.h, b.h, C.byref(h)), "evm_tree_merge")
+        return Trees(self, h)
+
     def merkle_diff(self, a: "Trees", b: "Trees") -> torch.Tensor:
         out = torch.empty(a.n_owners, dtype=torch.int64, device=f"cuda:{self.device}")
         check(self.lib.evm_merkle_diff(self.h, a.h, b.h, _ptr(out)), "evm_merkle_diff")

@@ -89,6 +89,7 @@ void* evm_get_stream(evm_ctx* ctx);
 int evm_sync(evm_ctx* ctx);
 /* tuning / test knobs */
 #define EVM_OPT_CLIENT_PATH 1 /* evm_apply_batch: 0 auto, 1 force the streaming path, 2 force the sort path */
+#define EVM_OPT_OVERLAP 3     /* 1 (default): independent checks run on a second HIP stream inside a call; 0: one stream */
 #define EVM_OPT_SERVER_PATH 2 /* evm_server_ingest: 0/1 per-owner LDS path where every owner's share fits, 2 force the sort path */
 int evm_set_option(evm_ctx* ctx, int option, int64_t value);
 /* kernel timing with HIP events on the context stream (for roofline reports) */
@@ -134,6 +135,12 @@ int evm_tree_from_json(evm_ctx* ctx, uint32_t n_owners, const char* const* json,
  * owner: device [n] (NULL: all owner 0).  *out is a new tree set.          */
 int evm_merkle_insert(evm_ctx* ctx, const evm_tree* in, const char* ts, size_t stride, size_t n,
                       const uint32_t* owner, evm_tree** out);
+
+/* Per owner: the tree holding the inserts of both a and b (leaf union, equal
+ * keys XOR-combined) -- what insertIntoMerkleTree gives for the two insert
+ * sets together, in any order (merkleTree.test.ts:30-42).  Combines the
+ * partial trees of an owner whose messages were split over GPUs.          */
+int evm_tree_merge(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, evm_tree** out);
 
 /* merkleTree.ts:63-91 for every owner o: diffMerkleTrees(a[o], b[o]).
  * millis: device int64[n_owners]; -1 = option.none, -2 = RangeError.       */

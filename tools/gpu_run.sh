@@ -18,6 +18,12 @@ rc=$?
 echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err
 if fatal $rc; then exit $rc; fi
 
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 0 --overlap 0 > gpurun_out/bench_no_overlap.json \
+  2> gpurun_out/bench_no_overlap.err
+rc=$?
+echo "bench (one stream) rc=$rc"; cat gpurun_out/bench_no_overlap.json
+if fatal $rc; then exit $rc; fi
+
 timeout -k 10 300 python -u bench.py --workload server --steps 5 --warmup 2 > gpurun_out/bench_server.json \
   2> gpurun_out/bench_server.err
 rc=$?
