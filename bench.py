@@ -69,6 +69,41 @@ def parse():
 
 
 def cpu_baseline(ts_arena, cells, budget_s):
+    """The reference merge restated in JavaScript (oracle/js/cpu_merge.js:
+    timestamp.ts / merkleTree.ts / applyMessages.ts decisions, SQLite
+    replaced by Maps) under node on this host, one thread, over the first
+    messages of the same config-2 stream; the Python oracle (verbatim SQL in
+    sqlite3) when node is absent."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    import numpy as np
+
+    node = shutil.which("node")
+    if node is None:
+        return cpu_baseline_python(ts_arena, cells, budget_s)
+    k = min(len(cells), 2_000_000)
+    with tempfile.TemporaryDirectory() as d:
+        tsf, cf = os.path.join(d, "ts.bin"), os.path.join(d, "cell.bin")
+        np.ascontiguousarray(ts_arena[:k, :48]).tofile(tsf)
+        np.ascontiguousarray(cells[:k], dtype="<u4").tofile(cf)
+        out = subprocess.run([node, os.path.join(ROOT, "oracle", "js", "cpu_merge.js"), tsf, cf, str(k),
+                              str(budget_s)], check=True, capture_output=True, text=True, timeout=budget_s + 120).stdout
+    r = json.loads(out)
+    ver = subprocess.run([node, "--version"], capture_output=True, text=True).stdout.strip()
+    return {
+        "value": r["rate"],
+        "unit": "msgs/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "messages 0..%d of the config-2 stream applied by oracle/js/cpu_merge.js under node %s "
+        "(applyMessages.ts decisions with the SQL as Maps, persistent-spread merkleTree.ts trie, murmur3), "
+        "1 thread, %.1f s" % (r["done"], ver, r["seconds"]),
+    }
+
+
+def cpu_baseline_python(ts_arena, cells, budget_s):
     """The oracle (Python restatement, sqlite3 running the reference SQL) on
     the first S messages of the same workload, single-threaded."""
     from oracle import evolu_oracle as O

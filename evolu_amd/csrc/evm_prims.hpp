@@ -180,31 +180,46 @@ __global__ __launch_bounds__(1024) void k_scan_partials(T* __restrict__ part, si
 }
 
 // Tile-local exclusive scan with the tile's carry from the scanned partials.
+// The tile is loaded and stored coalesced (element k*THREADS + t) and
+// transposed through LDS so that thread t scans elements t*ITEMS ..; the LDS
+// index is padded by one word per 32 (conflict-free both ways for 4-B T).
+__device__ __forceinline__ u32 scan_pad(u32 i) { return i + (i >> 5); }
+
 template <typename T, typename Op>
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan_down(const T* __restrict__ in, size_t n, const T* __restrict__ part,
                                                             T* __restrict__ out) {
+  __shared__ T tile[SCAN_TILE + SCAN_TILE / 32];
   __shared__ T lds[SCAN_THREADS / 64 + 1];
+  __shared__ T ex[SCAN_THREADS];
   Op op;
-  const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const u32 i = k * SCAN_THREADS + threadIdx.x;
+    tile[scan_pad(i)] = base + i < n ? in[base + i] : Op::id();
+  }
+  __syncthreads();
   T v[SCAN_ITEMS];
   T acc = Op::id();
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const size_t i = base + k;
-    v[k] = i < n ? in[i] : Op::id();
+    v[k] = tile[scan_pad(threadIdx.x * SCAN_ITEMS + k)];
     acc = op(acc, v[k]);
   }
-  T incl = block_inclusive_scan<T, Op>(acc, lds, op, nullptr);
-  // exclusive start of this thread = incl - acc (need inverse-free form): shift via LDS
-  __shared__ T ex[SCAN_THREADS];
+  const T incl = block_inclusive_scan<T, Op>(acc, lds, op, nullptr);
   ex[threadIdx.x] = incl;
   __syncthreads();
   T run = op(part[blockIdx.x], threadIdx.x == 0 ? Op::id() : ex[threadIdx.x - 1]);
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const size_t i = base + k;
-    if (i < n) out[i] = run;
+    tile[scan_pad(threadIdx.x * SCAN_ITEMS + k)] = run;
     run = op(run, v[k]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const u32 i = k * SCAN_THREADS + threadIdx.x;
+    if (base + i < n) out[base + i] = tile[scan_pad(i)];
   }
 }
 

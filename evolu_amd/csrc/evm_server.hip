@@ -308,6 +308,56 @@ __global__ void k_sv_owner_off(const u32* __restrict__ owner, size_t n, u32 n_ow
   }
 }
 
+// ------------------------------------------------ owner runs (requests)
+__global__ void k_run_heads(const u32* __restrict__ owner, size_t n, u32* __restrict__ head) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    head[i] = (i == 0 || owner[i] != owner[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_run_emit(const u32* __restrict__ owner, const u32* __restrict__ head, const u32* __restrict__ rid,
+                           size_t n, u32* __restrict__ run_start, u32* __restrict__ run_owner) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    if (head[i]) {
+      run_start[rid[i]] = (u32)i;
+      run_owner[rid[i]] = owner[i];
+    }
+}
+
+// lengths of the runs in (owner, batch) order
+__global__ void k_run_len(const u32* __restrict__ run_start, const u32* __restrict__ order, u32 R, size_t n,
+                          u32* __restrict__ len) {
+  for (u32 j = blockIdx.x * blockDim.x + threadIdx.x; j < R; j += gridDim.x * blockDim.x) {
+    const u32 r = order[j];
+    len[j] = (u32)((r + 1 < R ? (size_t)run_start[r + 1] : n) - run_start[r]);
+  }
+}
+
+// first message position of every owner: the position of its first run
+__global__ void k_run_seg(const u32* __restrict__ run_owner_sorted, u32 R, const u32* __restrict__ run_pos, u32 O,
+                          u64* __restrict__ seg) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o <= O; o += gridDim.x * blockDim.x) {
+    u32 a = 0, b = R;
+    while (a < b) {
+      const u32 m = (a + b) >> 1;
+      if (run_owner_sorted[m] < o) a = m + 1;
+      else b = m;
+    }
+    seg[o] = run_pos[a];  // run_pos[R] = n
+  }
+}
+
+// perm over owner-major positions: one wave per run writes the run's batch
+// indices (consecutive lanes, consecutive addresses)
+__global__ __launch_bounds__(256) void k_run_fill(const u32* __restrict__ run_pos, const u32* __restrict__ run_start,
+                                                  const u32* __restrict__ order, u32 R, u32* __restrict__ perm) {
+  const u32 lane = threadIdx.x & 63;
+  const size_t waves = (size_t)gridDim.x * 4;
+  for (size_t j = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < R; j += waves) {
+    const u32 p = run_pos[j], L = run_pos[j + 1] - p, s = run_start[order[j]];
+    for (u32 q = lane; q < L; q += 64) perm[p + q] = s + q;
+  }
+}
+
 // ------------------------------------------------------ K5: owner ingest
 // When every owner's share of the batch fits SVO_CAP rows (the common case:
 // a request carries one owner's messages, index.ts:224-248), one workgroup
@@ -850,13 +900,42 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   u32* tot = S.alloc<u32>(2);
   if (!own || !seg || !status || !n_tc || !n_hi || !n_lo || !n_id || !l_ck || !l_xr || !l_dup || !cnt || !pos || !tot)
     return EVM_ENOMEM;
-  HIPR(hipMemcpyAsync(own, owner, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
-  if ((st = launch_iota(ctx, perm, n))) return st;
-  u32* ok = own;
-  u32* ov = perm;
   const int obits = O > 1 ? 32 - __builtin_clz(O - 1) : 0;
-  if ((st = radix_sort_pairs<u32>(ctx, S, ok, ov, n, 0, obits))) return st;
-  KLAUNCH(k_sv_owner_off, dim3(grid_for((size_t)O + 1, 256)), dim3(256), ok, n, O, seg);
+  // requests arrive as runs of one owner (index.ts:224-248): sort the runs,
+  // not the messages, when they are long enough
+  u32* head = S.alloc<u32>(n);
+  u32* rid = S.alloc<u32>(n);
+  u32* nrun = S.alloc<u32>(1);
+  if (!head || !rid || !nrun) return EVM_ENOMEM;
+  KLAUNCH(k_run_heads, dim3(grid_for(n, 256)), dim3(256), owner, n, head);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, head, n, rid, nrun))) return st;
+  u32 R = 0;
+  HIPR(hipMemcpyAsync(&R, nrun, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  u32* ov = perm;
+  if ((size_t)R * 8 <= n) {
+    u32* run_start = S.alloc<u32>(R);
+    u32* run_owner = S.alloc<u32>(R);
+    u32* order = S.alloc<u32>(R);
+    u32* len = S.alloc<u32>(R);
+    u32* run_pos = S.alloc<u32>((size_t)R + 1);
+    if (!run_start || !run_owner || !order || !len || !run_pos) return EVM_ENOMEM;
+    KLAUNCH(k_run_emit, dim3(grid_for(n, 256)), dim3(256), owner, head, rid, n, run_start, run_owner);
+    if ((st = launch_iota(ctx, order, R))) return st;
+    u32* rk = run_owner;
+    u32* rv = order;
+    if ((st = radix_sort_pairs<u32>(ctx, S, rk, rv, R, 0, obits))) return st;
+    KLAUNCH(k_run_len, dim3(grid_for(R, 256)), dim3(256), run_start, rv, R, n, len);
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, len, R, run_pos, run_pos + R))) return st;
+    KLAUNCH(k_run_seg, dim3(grid_for((size_t)O + 1, 256)), dim3(256), rk, R, run_pos, O, seg);
+    KLAUNCH(k_run_fill, dim3(grid_for(R, 4, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
+  } else {
+    HIPR(hipMemcpyAsync(own, owner, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
+    if ((st = launch_iota(ctx, perm, n))) return st;
+    u32* ok = own;
+    if ((st = radix_sort_pairs<u32>(ctx, S, ok, ov, n, 0, obits))) return st;
+    KLAUNCH(k_sv_owner_off, dim3(grid_for((size_t)O + 1, 256)), dim3(256), ok, n, O, seg);
+  }
   const evm_tree* t = s->tree;
   u32 *c_rows = cnt, *c_new = cnt + O, *c_leaves = cnt + 2 * (size_t)O;
   Info hi;

@@ -230,8 +230,9 @@ def torch_tensor(eng, values):
     return torch.tensor(values, dtype=torch.int64, device=eng.device)
 
 
-@pytest.mark.parametrize("n_owners,per_owner", [(3000, 300), (20000, 1000), (50, 3000), (3, 5000)])
-def test_owner_lds_path_vs_sort_path(eng, n_owners, per_owner):
+@pytest.mark.parametrize("n_owners,per_owner,req_size", [(3000, 300, 1), (3000, 300, 50), (20000, 1000, 100),
+                                                        (50, 3000, 100), (3, 5000, 100)])
+def test_owner_lds_path_vs_sort_path(eng, n_owners, per_owner, req_size):
     """The per-owner LDS ingest (K5) and the global sort path are independent
     device algorithms: on config-3-shaped batches with redeliveries, fed in
     two ingests (the second one against a non-empty store and trees), they
@@ -240,7 +241,7 @@ def test_owner_lds_path_vs_sort_path(eng, n_owners, per_owner):
     from evolu_amd import _lib as L
     from evolu_amd import synth
 
-    ts_np, owner_np, _ = synth.config3(n_owners=n_owners, per_owner=per_owner, seed_config=11)
+    ts_np, owner_np, _ = synth.config3(n_owners=n_owners, per_owner=per_owner, seed_config=11, request=req_size)
     rng = np.random.default_rng(n_owners)
     dup = rng.integers(0, len(ts_np), size=len(ts_np) // 20)
     ts_np = np.concatenate([ts_np, ts_np[dup]])
