@@ -47,6 +47,12 @@ ALG_BYTES_PER_MSG = {
 }
 
 
+# Kernels that run on the engine's second stream beside the walks (EVM_OPT_OVERLAP):
+# their event durations include time spent sharing the chip, so they are not
+# candidates for the roofline line while the overlap is on.
+SIDE_KERNELS = {"k_xp_scatter", "k_xp_dedup"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,7 +211,7 @@ def main():
         ms_step = elapsed / a.steps * 1e3
         value = world * a.messages * a.steps / elapsed
         # dominant kernel and its roofline
-        known = {k: v for k, v in prof.items() if k in ALG_BYTES_PER_MSG}
+        known = {k: v for k, v in prof.items() if k in ALG_BYTES_PER_MSG and not (a.overlap and k in SIDE_KERNELS)}
         dom = max(known, key=lambda k: known[k][0])
         tot_ms, launches = known[dom]
         avg_s = tot_ms / launches / 1e3
