@@ -724,13 +724,12 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __
   if (mlo > mhi) return;  // no valid message
   const u32 nwin = (mhi - mlo) / FOLD_WIN + 1;
   if (nwin > FOLD_MAXWIN || base3_len(mlo) != base3_len(mhi)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&info->fold_overflow, 1u);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicOr(&info->fold_overflow, 1u);
     return;
   }
-  // block b -> (chunk, window) with the windows of one chunk on one XCD
-  // (workgroups go round-robin over the 8 XCDs): the chunk's second read is
-  // an L2 hit
-  const u32 b = blockIdx.x, w = (b / 8) % FOLD_MAXWIN, chunk = (b / (8 * FOLD_MAXWIN)) * 8 + b % 8;
+  // (mapping the windows of one chunk to one XCD, for an L2 hit on the second
+  // read, measured 1.6x slower: chunk-major dispatch order it is)
+  const u32 w = blockIdx.y, chunk = blockIdx.x;
   if (w >= nwin) return;
   for (u32 b = threadIdx.x; b < FOLD_WIN; b += FOLD_THREADS) hist[b] = 0;
   for (u32 b = threadIdx.x; b < FOLD_WIN / 32; b += FOLD_THREADS) pres[b] = 0;
@@ -968,8 +967,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   u64* lck = S.alloc<u64>(B);
   int32_t* lxr = S.alloc<int32_t>(B);
   if (!px || !pp || !dx || !dp || !bcnt || !bxor || !lck || !lxr) return EVM_ENOMEM;
-  static_assert(FOLD_CHUNKS % 8 == 0, "chunk <-> XCD mapping");
-  KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS * FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
+  KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
   KLAUNCH(k_cl_fold_reduce, dim3(FR_BLOCKS), dim3(FR_THREADS), px, pp, info, dx, dp, bcnt, bxor);
   // into an empty tree: build the output speculatively, so the call has one
   // host round trip; one owner: the leaf kernel writes the tree itself
