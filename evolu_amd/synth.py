@@ -152,3 +152,49 @@ def config3(n_owners: int = 100_000, per_owner: int = 1000, nodes_per_owner: int
         perm = np.argsort(order_key, kind="stable")
     ts = format_timestamps(millis[perm], counter[perm], nodes[nidx[perm]], stride)
     return ts, owner[perm], millis[perm]
+
+
+def config5(n_owners: int, n: int, zipf_s: float = 1.2, cells_per_owner: int = 50, nodes_per_owner: int = 4,
+            stride: int = 48, seed_config: int = 5, redelivery: float = 0.10, upper_frac: float = 0.01):
+    """Adversarial stream (BASELINE config 5): owner sizes Zipf(s); per owner
+    its nodes send on a coarse shared time grid, so many messages share millis
+    across nodes (ties broken by counter, then by node bytes) and nodes repeat
+    millis (counter increments); ~1 % of nodes carry upper-case hex; a
+    `redelivery` fraction of messages is re-sent later in the batch (same
+    owner, same cell: half of them after a newer write to that cell -> the
+    stale-redelivery XOR toggle of applyMessages).  Returns (ts arena, owner
+    u32, cell u32 global ids = owner * cells_per_owner + local cell), batch
+    order."""
+    rng = rng_for(seed_config)
+    w = 1.0 / np.arange(1, n_owners + 1, dtype=np.float64) ** zipf_s
+    base = int(n * (1 - redelivery))
+    counts = rng.multinomial(base, w / w.sum())
+    owner = np.repeat(np.arange(n_owners, dtype=np.int64), counts)
+    node_local = rng.integers(0, nodes_per_owner, size=base)
+    gnode = owner * nodes_per_owner + node_local
+    # coarse grid: ~4 messages per slot per owner -> frequent equal millis
+    slots = np.maximum(1, counts // 4)
+    millis = BENCH_T0 + (rng.random(base) * slots[owner]).astype(np.int64) * 1000
+    # per (node, millis): counter = rank of the message among that node's equal-millis sends
+    order = np.lexsort((np.arange(base), millis, gnode))
+    g_s, m_s = gnode[order], millis[order]
+    new_run = np.ones(base, dtype=bool)
+    new_run[1:] = (g_s[1:] != g_s[:-1]) | (m_s[1:] != m_s[:-1])
+    run_start = np.maximum.accumulate(np.where(new_run, np.arange(base), 0))
+    counter = np.empty(base, dtype=np.int64)
+    counter[order] = np.arange(base) - run_start
+    nodes = random_nodes(rng, n_owners * nodes_per_owner, upper_frac=upper_frac)
+    cell = owner * cells_per_owner + rng.integers(0, cells_per_owner, size=base)
+    perm = rng.permutation(base)
+    ts = format_timestamps(millis[perm], counter[perm], nodes[gnode[perm]], stride)
+    owner, cell = owner[perm], cell[perm]
+    # redeliveries: copies of earlier messages appended later in the batch
+    k = n - base
+    src = rng.integers(0, base, size=k)
+    ts = np.concatenate([ts, ts[src]])
+    owner = np.concatenate([owner, owner[src]])
+    cell = np.concatenate([cell, cell[src]])
+    mix = rng.permutation(n - base) + base  # interleave the copies among the tail
+    tail = np.arange(base, n)
+    ts[tail], owner[tail], cell[tail] = ts[mix], owner[mix], cell[mix]
+    return ts, owner.astype(np.uint32), cell.astype(np.uint32)
