@@ -66,6 +66,8 @@ def parse():
                     help="client: config 2 applyMessages (headline); server: config 3/4 ingest + diff + select")
     ap.add_argument("--owners", type=int, default=100_000, help="server workload: owners per GPU")
     ap.add_argument("--per-owner", type=int, default=1000, help="server workload: messages per owner")
+    ap.add_argument("--zipf", type=float, default=0.0,
+                    help="server workload: owner sizes Zipf(s) (BASELINE config 5 skew, s = 1.2); owners x per-owner msgs in total")
     ap.add_argument("--request", type=int, default=100,
                     help="server workload: messages per SyncRequest (one owner each, requests in random order); "
                          "1 = every message shuffled on its own")
@@ -270,7 +272,11 @@ def server_main(a, rank, world, local):
     from evolu_amd.engine import Engine
 
     O_total = a.owners * world
-    ts_np, owner_np, millis = synth.config3(a.owners, a.per_owner, seed_config=3 + 1000 * rank, request=a.request)
+    if a.zipf > 0:
+        ts_np, owner_np, _, millis = synth.config5(a.owners, a.owners * a.per_owner, zipf_s=a.zipf,
+                                                   seed_config=5 + 1000 * rank, with_millis=True)
+    else:
+        ts_np, owner_np, millis = synth.config3(a.owners, a.per_owner, seed_config=3 + 1000 * rank, request=a.request)
     # this rank's owner o is job owner o*world + (o+rank)%world: every rank
     # receives messages for owners living on every rank, no owner on two sources
     o64 = owner_np.astype(np.int64)
@@ -279,31 +285,45 @@ def server_main(a, rank, world, local):
     dev = torch.device("cuda", local)
     ts = eng.dev(ts_np)
     owner = torch.from_numpy(owner_np).to(dev)
-    n_local_owners = (O_total + world - 1) // world
-    if world > 1:
-        ts_r, own_r, src_rank, src_idx = D.route_by_owner(ts, owner)
-    else:
-        ts_r, own_r = ts, owner
-    lown = D.local_owner(own_r, world).contiguous()
+    # owners too big for one rank (Zipf) are split over the ranks by timestamp hash
+    hot = D.hot_owners(D.owner_counts(owner, O_total), world) if (world > 1 and a.zipf > 0) else None
+    omap = D.OwnerMap(O_total, world, rank, hot)
+    n_local_owners = omap.n_local
+    dest = omap.dest(owner, ts) if world > 1 else None
+
+    def route(rows):
+        if world == 1:
+            return rows, owner
+        t_r, o_r, _, _ = D.route_by_owner(rows, owner, dest=dest)
+        return t_r, o_r
+
+    ts_r, own_r = route(ts)
+    lown = omap.local(own_r).contiguous()
     # client trees: each owner's messages minus the newest 10% (the expected diff)
     # (the client knows each owner's first 90% by timestamp)
     order = np.lexsort((millis, o64))
     rank_in_owner = np.empty(len(order), dtype=np.int64)
-    rank_in_owner[order] = np.arange(len(order)) - np.repeat(np.arange(a.owners) * a.per_owner, a.per_owner)
-    keep_np = (rank_in_owner < int(0.9 * a.per_owner)).astype(np.uint8)
+    counts = np.bincount(o64, minlength=a.owners)
+    rank_in_owner[order] = np.arange(len(order)) - (np.cumsum(counts) - counts)[o64[order]]
+    keep_np = (rank_in_owner < (0.9 * counts[o64]).astype(np.int64)).astype(np.uint8)
     if world > 1:  # route the flag with its message (an extra 8-byte column)
         ext = np.concatenate([ts_np, np.repeat(keep_np[:, None], 8, 1)], 1)
-        keep = D.route_by_owner(torch.from_numpy(ext).to(dev), owner)[0][:, ts_np.shape[1]].bool()
+        keep = route(torch.from_numpy(ext).to(dev))[0][:, ts_np.shape[1]].bool()
     else:
         keep = torch.from_numpy(keep_np).to(dev).bool()
-    client =eng.merkle_insert(eng.tree_new(n_local_owners), ts_r[keep].contiguous(), lown[keep].contiguous())
+    if a.zipf > 0:  # redeliveries: the client's tree holds each known message once
+        first = eng.store_new(n_local_owners)
+        ins, _ = first.ingest(ts_r, lown, 0)
+        keep &= (ins[: len(ts_r)] & 0x04) != 0
+        first.free()
+    client = eng.merkle_insert(eng.tree_new(n_local_owners), ts_r[keep].contiguous(), lown[keep].contiguous())
     node = torch.from_numpy(np.frombuffer(b"0123456789abcdef" * n_local_owners, dtype=np.uint8).copy()).to(dev)
     flags = torch.empty(len(ts_r), dtype=torch.uint8, device=dev)
 
     def step():
         if world > 1:
-            t_r, o_r, _, _ = D.route_by_owner(ts, owner)
-            lo = D.local_owner(o_r, world).contiguous()
+            t_r, o_r = route(ts)
+            lo = omap.local(o_r).contiguous()
         else:
             t_r, lo = ts_r, lown
         store = eng.store_new(n_local_owners)
@@ -311,7 +331,10 @@ def server_main(a, rank, world, local):
         diff, off, ids = store.select(client, node)
         r, p = store.tree().roots()
         if world > 1:
-            D.gather_roots(torch.from_numpy(r).to(dev), torch.from_numpy(p).to(dev), O_total)
+            rt, pt = torch.from_numpy(r).to(dev), torch.from_numpy(p).to(dev)
+            D.gather_roots(rt[: omap.per], pt[: omap.per], O_total)
+            if omap.hot.numel():
+                D.gather_hot_roots(rt, pt, omap)
         store.free()
         return int(ids.numel())
 
@@ -346,8 +369,11 @@ def server_main(a, rank, world, local):
             "metric": METRIC, "value": world * n * a.steps / elapsed, "unit": "msgs/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u64", "data": "synthetic (seeded HLC streams, SURVEY 8(d) config 3/4)",
-            "config": {"workload": "server: addMessages + getMessages, %d owners x %d msgs per GPU in requests of %d, "
-                       "RCCL owner routing" % (a.owners, a.per_owner, a.request), "messages_per_gpu": n, "owners_per_gpu": a.owners,
+            "config": {"workload": ("server: addMessages + getMessages, %d owners x %d msgs per GPU in requests of %d, "
+                                    "RCCL owner routing" % (a.owners, a.per_owner, a.request)) if a.zipf <= 0 else
+                       ("server config 5: addMessages + getMessages, %d msgs per GPU over %d owners with Zipf(%.2f) sizes, "
+                        "hot owners split over ranks" % (n, a.owners, a.zipf)),
+                       "messages_per_gpu": n, "owners_per_gpu": a.owners,
                        "selected_rows_rank0": nsel, "parallelism": "owner-sharded, %d rank(s)" % world},
             "kernels_ms_per_step": {k: v[0] / a.steps for k, v in top},
         }), flush=True)

@@ -204,7 +204,8 @@ __global__ void k_sv_ties(const u64* __restrict__ key, u32* __restrict__ perm, c
 // Sorted order p: first occurrence of (owner, timestamp) in batch order (the
 // sort is stable on the batch index) that the store does not hold yet.
 __global__ void k_sv_mark(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u64* __restrict__ skeys,
-                          size_t n, StoreView st, uint8_t* __restrict__ flags, u32* __restrict__ sel) {
+                          size_t n, StoreView st, uint8_t* __restrict__ flags, u32* __restrict__ sel,
+                          const u32* __restrict__ orig) {
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
     const u32 i = perm[p];
     bool first = true;
@@ -222,7 +223,7 @@ __global__ void k_sv_mark(const evm_rec* __restrict__ rec, const u32* __restrict
         ins = !(q < b && skey_cmp(skey_at(st, q), k) == 0);
       }
     }
-    flags[i] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
+    flags[orig ? orig[i] : i] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
     sel[p] = ins ? 1u : 0u;
   }
 }
@@ -230,7 +231,8 @@ __global__ void k_sv_mark(const evm_rec* __restrict__ rec, const u32* __restrict
 __global__ void k_sv_compact(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u32* __restrict__ sel,
                              const u32* __restrict__ pos, size_t n, u64 id_base, u32* __restrict__ o_owner,
                              u64* __restrict__ o_tc, u64* __restrict__ o_hi, u32* __restrict__ o_lo,
-                             u64* __restrict__ o_id, u64* __restrict__ l_ck, u32* __restrict__ l_h) {
+                             u64* __restrict__ o_id, u64* __restrict__ l_ck, u32* __restrict__ l_h,
+                             const u32* __restrict__ orig) {
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
     if (!sel[p]) continue;
     const u32 i = perm[p];
@@ -241,7 +243,7 @@ __global__ void k_sv_compact(const evm_rec* __restrict__ rec, const u32* __restr
     o_tc[q] = k.tc;
     o_hi[q] = k.hi;
     o_lo[q] = k.lo;
-    o_id[q] = id_base + i;
+    o_id[q] = id_base + (orig ? orig[i] : i);
     // leaves come out sorted by (owner, minute); the codes follow that order
     // when the owner's key lengths agree (k_sv_sorted_check tells)
     l_ck[q] = ((u64)k.owner << 40) | minute_code(r.minute);
@@ -249,9 +251,10 @@ __global__ void k_sv_compact(const evm_rec* __restrict__ rec, const u32* __restr
   }
 }
 
-__global__ void k_sv_bad(const evm_rec* __restrict__ rec, size_t n, uint8_t* __restrict__ flags) {
+__global__ void k_sv_bad(const evm_rec* __restrict__ rec, size_t n, uint8_t* __restrict__ flags,
+                         const u32* __restrict__ orig) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    flags[i] = (rec[i].meta & EVM_META_VALID) ? 0u : EVM_MSG_BAD;
+    flags[orig ? orig[i] : i] = (rec[i].meta & EVM_META_VALID) ? 0u : EVM_MSG_BAD;
 }
 
 __global__ void k_sv_sorted_check(const u64* __restrict__ ck, size_t m, u32* __restrict__ unsorted) {
@@ -358,6 +361,51 @@ __global__ __launch_bounds__(256) void k_run_fill(const u32* __restrict__ run_po
   }
 }
 
+// --------------------------------------------- sub-batches (hybrid ingest)
+// Pack of a sub-batch: message k is the caller's message orig[k].
+__global__ void k_sv_pack_sel(const uint8_t* __restrict__ ts, size_t stride, const u32* __restrict__ owner,
+                              const u32* __restrict__ orig, size_t n, evm_rec* __restrict__ out,
+                              u32* __restrict__ owner_out) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const u32 i = orig[k];
+    u32 w[12];
+    load_ts(ts, stride, i, w);
+    const Parsed p = parse_ts46(w);
+    evm_rec r;
+    r.tc = p.tc;
+    r.node = p.node;
+    r.meta = p.meta;
+    r.hash = p.hash;
+    r.minute = p.minute;
+    r.aux = owner[i];
+    out[k] = r;
+    owner_out[k] = r.aux;
+  }
+}
+
+// messages whose owner's share exceeds the LDS capacity
+__global__ void k_big_mask(const evm_rec* __restrict__ rec, size_t n, const u64* __restrict__ seg, u64 cap,
+                           uint8_t* __restrict__ mask) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const u32 o = rec[i].aux;
+    mask[i] = seg[o + 1] - seg[o] > cap ? 1 : 0;
+  }
+}
+
+// stable split of [0, n) by mask: pos = exclusive count of unmasked before i
+__global__ void k_split(const uint8_t* __restrict__ mask, const u32* __restrict__ pos, size_t n, u32* __restrict__ small,
+                        u32* __restrict__ big) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    if (mask[i]) big[i - pos[i]] = (u32)i;
+    else small[pos[i]] = (u32)i;
+  }
+}
+
+__global__ void k_not_u32(const uint8_t* __restrict__ mask, size_t n, u32* __restrict__ out) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = mask[i] ? 0u : 1u;
+}
+
 // ------------------------------------------------------ K5: owner ingest
 // When every owner's share of the batch fits SVO_CAP rows (the common case:
 // a request carries one owner's messages, index.ts:224-248), one workgroup
@@ -408,7 +456,8 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     const u64* __restrict__ t_off, const u64* __restrict__ t_ck, u64 id_base, uint8_t* __restrict__ flags,
     u64* __restrict__ n_tc, u64* __restrict__ n_hi, u32* __restrict__ n_lo, u64* __restrict__ n_id,
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
-    u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status) {
+    u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status,
+    const u32* __restrict__ orig) {
   constexpr int PER = CAP / SVO_THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
   constexpr u64 PMASK = CAP - 1;
@@ -630,13 +679,14 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     const u32 p = threadIdx.x * PER + r;
     if (p < m) {
       const bool ins = (insm >> r) & 1u;
-      flags[mb[r]] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
+      const u32 ob = orig ? orig[mb[r]] : mb[r];  // the message's index in the caller's batch
+      flags[ob] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
       if (ins) {
         const u64 w = a + q;
         n_tc[w] = mt[r];
         n_hi[w] = mh[r];
         n_lo[w] = ml[r];
-        n_id[w] = id_base + mb[r];
+        n_id[w] = id_base + ob;
         s_min[q] = (u32)((mt[r] >> 16) / 60000ull);  // == rec.minute on the native domain
         s_hq[q] = mhash[r];
         ++q;
@@ -800,19 +850,27 @@ __device__ __forceinline__ bool parse_node16(const uint8_t* s, u64* v) {
   return true;
 }
 
-__global__ void k_sv_sel_count(StoreView st, u32 n_owners, const int64_t* __restrict__ diff,
+// getMessages selection, load-balanced over the candidate rows (an owner's
+// rows after its bound) rather than over owners: one Zipf-hot owner's tens of
+// millions of rows spread over the whole chip instead of one thread.
+// Pass 1 (per owner): the first row after the bound and the candidate count.
+__global__ void k_sv_sel_first(StoreView st, u32 n_owners, const int64_t* __restrict__ diff,
                                const uint8_t* __restrict__ node, const uint8_t* __restrict__ active,
-                               u64* __restrict__ first, u32* __restrict__ cnt, u32* __restrict__ bad) {
+                               u64* __restrict__ first, u32* __restrict__ cand, u64* __restrict__ req,
+                               u32* __restrict__ bad) {
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
-    cnt[o] = 0;
+    cand[o] = 0;
     first[o] = 0;
     if (active && !active[o]) continue;
     const int64_t d = diff[o];
     if (d < 0) continue;  // none or RangeError
-    u64 req = 0;
-    if (node && !parse_node16(node + 16 * (size_t)o, &req)) {
-      atomicOr(bad, 1u);
-      continue;
+    if (node) {
+      u64 r = 0;
+      if (!parse_node16(node + 16 * (size_t)o, &r)) {
+        atomicOr(bad, 1u);
+        continue;
+      }
+      req[o] = r;
     }
     const size_t a = st.off[o], b = st.off[o + 1];
     // timestamp > "ISO(d)-0000-0000000000000000": smallest key with tc = d << 16
@@ -820,32 +878,72 @@ __global__ void k_sv_sel_count(StoreView st, u32 n_owners, const int64_t* __rest
     size_t q = store_lower(st, a, b, since);
     if (q < b && skey_cmp(skey_at(st, q), since) == 0) ++q;  // strictly greater
     first[o] = q;
-    u32 c = 0;
-    if (node) {
-      for (size_t k = q; k < b; ++k) c += node_hex_of(st.hi[k], st.lo[k]) != req;  // NOT LIKE '%' || nodeId
-    } else {
-      c = (u32)(b - q);
-    }
-    cnt[o] = c;
+    cand[o] = (u32)(b - q);
   }
 }
 
-__global__ void k_sv_sel_write(StoreView st, const u64* __restrict__ id, u32 n_owners, const u64* __restrict__ first,
-                               const u32* __restrict__ cnt, const u32* __restrict__ pos, const uint8_t* __restrict__ node,
-                               u64* __restrict__ sel_id) {
-  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
-    if (!cnt[o]) continue;
-    u64 req = 0;
-    if (node) parse_node16(node + 16 * (size_t)o, &req);
-    u64 w = pos[o];
-    for (size_t k = first[o], b = st.off[o + 1]; k < b; ++k)
-      if (!node || node_hex_of(st.hi[k], st.lo[k]) != req) sel_id[w++] = id[k];
+constexpr int SEL_THREADS = 256;
+
+// Owner of candidate j: the last owner whose candidate offset is <= j (owners
+// with no candidates share their successor's offset and are skipped).
+__device__ __forceinline__ u32 cand_owner(const u32* __restrict__ cpos, u32 lo, u32 hi, u32 j) {
+  while (lo + 1 < hi) {  // invariant: cpos[lo] <= j < cpos[hi] (cpos[n_owners] = C)
+    const u32 mid = (lo + hi) >> 1;
+    if (cpos[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Pass 2 (per candidate): keep unless the row's node is the requester's
+// (`NOT LIKE '%' || nodeId`).  Each block narrows the owner search to its
+// own tile of candidates.  cpos has n_owners + 1 entries.
+__global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_keep(StoreView st, u32 n_owners, u32 C,
+                                                             const u32* __restrict__ cpos, const u64* __restrict__ first,
+                                                             const u64* __restrict__ req, u32* __restrict__ keep) {
+  __shared__ u32 range[2];
+  for (u32 j0 = blockIdx.x * SEL_THREADS; j0 < C; j0 += gridDim.x * SEL_THREADS) {
+    const u32 j1 = min(C, j0 + SEL_THREADS) - 1;
+    __syncthreads();
+    if (threadIdx.x == 0) range[0] = cand_owner(cpos, 0, n_owners, j0);
+    if (threadIdx.x == 1) range[1] = cand_owner(cpos, 0, n_owners, j1) + 1;
+    __syncthreads();
+    const u32 j = j0 + threadIdx.x;
+    if (j > j1) continue;
+    const u32 o = cand_owner(cpos, range[0], range[1], j);
+    const size_t k = first[o] + (j - cpos[o]);
+    keep[j] = node_hex_of(st.hi[k], st.lo[k]) != req[o];
   }
 }
 
-__global__ void k_u32_to_u64(const u32* __restrict__ a, size_t n, const u32* __restrict__ total, u64* __restrict__ out) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (size_t)gridDim.x * blockDim.x)
-    out[i] = i < n ? (u64)a[i] : (u64)*total;
+// Pass 3 (per candidate): write the kept ids at their selection positions
+// (kpos = exclusive scan of keep, or null when every candidate is kept).
+__global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_emit(u32 n_owners, u32 C, const u32* __restrict__ cpos,
+                                                             const u64* __restrict__ first, const u32* __restrict__ keep,
+                                                             const u32* __restrict__ kpos, const u64* __restrict__ id,
+                                                             u64* __restrict__ sel_id) {
+  __shared__ u32 range[2];
+  for (u32 j0 = blockIdx.x * SEL_THREADS; j0 < C; j0 += gridDim.x * SEL_THREADS) {
+    const u32 j1 = min(C, j0 + SEL_THREADS) - 1;
+    __syncthreads();
+    if (threadIdx.x == 0) range[0] = cand_owner(cpos, 0, n_owners, j0);
+    if (threadIdx.x == 1) range[1] = cand_owner(cpos, 0, n_owners, j1) + 1;
+    __syncthreads();
+    const u32 j = j0 + threadIdx.x;
+    if (j > j1) continue;
+    if (keep && !keep[j]) continue;
+    const u32 o = cand_owner(cpos, range[0], range[1], j);
+    sel_id[kpos ? kpos[j] : j] = id[first[o] + (j - cpos[o])];
+  }
+}
+
+// Per-owner selection offsets: sel_off[o] = kept candidates before owner o.
+__global__ void k_sv_sel_off(u32 n_owners, u32 C, const u32* __restrict__ cpos, const u32* __restrict__ kpos,
+                             const u32* __restrict__ ktot, u64* __restrict__ sel_off) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o <= n_owners; o += gridDim.x * blockDim.x) {
+    const u32 c = cpos[o];
+    sel_off[o] = kpos ? (c < C ? kpos[c] : *ktot) : c;
+  }
 }
 
 StoreView view_of(const evm_store* s) { return StoreView{s->off, s->owner, s->tc, s->hi, s->lo}; }
@@ -879,9 +977,10 @@ void store_release_arrays(evm_ctx* ctx, evm_store* s) {
 // the same packed records.  Validity of the batch is checked here (one host
 // round trip for the whole ingest).
 int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec* rec, const u32* owner, size_t n,
-                    uint64_t id_base, uint8_t* flags, Info* info, u32* perm, evm_store* ns, evm_tree** new_tree,
-                    bool* done) {
+                    const u32* orig, uint64_t id_base, uint8_t* flags, Info* info, u32* perm, evm_store* ns,
+                    evm_tree** new_tree, bool* done, uint8_t* bigmask, bool* big_only) {
   *done = false;
+  *big_only = false;
   const u32 O = s->n_owners;
   int st;
   // stable sort of the batch index by owner: each owner's share in batch order
@@ -947,11 +1046,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if (pass == 0)
       KLAUNCH(k_svo_a<1024>, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off,
               (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new,
-              c_leaves, status);
+              c_leaves, status, orig);
     else
       KLAUNCH(k_svo_a<SVO_CAP>, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off,
               (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new,
-              c_leaves, status);
+              c_leaves, status, orig);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, O, pos, tot))) return st;
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, O, pos + O, tot + 1))) return st;
     HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
@@ -959,11 +1058,16 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if ((st = read_info(ctx, info, &hi))) return st;
     if (hi.bad_aux) return EVM_EINVAL;
     if (hi.bad) {
-      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
+      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
       (void)evm_sync(ctx);
       return EVM_ENONCANON;
     }
     if (!hs.big || hs.fallback) break;
+  }
+  if (hs.big && !hs.fallback && bigmask) {
+    // only some owners are too big for LDS: tell the caller which messages are theirs
+    KLAUNCH(k_big_mask, dim3(grid_for(n, 256)), dim3(256), rec, n, seg, (u64)SVO_CAP, bigmask);
+    *big_only = true;
   }
   if (hs.big || hs.fallback) return EVM_OK;  // the sort path redoes the flags
   // new store and tree, exactly sized
@@ -1035,11 +1139,17 @@ int evm_store_messages(evm_ctx* ctx, const evm_store* s, uint64_t* owner_off, ui
   return evm_sync(ctx);
 }
 
-int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
-                      uint64_t id_base, uint8_t* flags) {
-  if (!ctx || !s || stride < 46 || (n && (!ts || !owner || !flags))) return EVM_EINVAL;
-  if (n == 0) return EVM_OK;  // index.ts:145 `if (req.messages.length === 0) return merkleTree`
-  if (n >= 0xffffffffull) return EVM_EINVAL;
+}  // extern "C"
+
+// One ingest over the caller's batch, or over the sub-batch orig[0..n) of it
+// (message k = the caller's message orig[k]; flags and ids refer to the
+// caller's indices).  mode 0: per-owner LDS path, and when only some owners
+// are too big for it, the batch split in two (their messages through the
+// sort path, the rest through LDS) -- owners are independent, so the result
+// is the one of a single ingest; mode 1: LDS path, else the sort path;
+// mode 2: the sort path.
+static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                       const u32* orig, uint64_t id_base, uint8_t* flags, int mode) {
   int st;
   evm_store ns{};
   evm_tree* new_tree = nullptr;
@@ -1052,12 +1162,43 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
     u64* fv = S.alloc<u64>(n);
     FieldRange* fr = S.alloc<FieldRange>(1);
     if (!rec || !perm || !fv || !fr) return EVM_ENOMEM;
-    if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) return st;
-    if (ctx->server_path != 2 && s->n_owners > 0) {
-      bool done = false;
-      if ((st = ingest_by_owner(ctx, S, s, rec, owner, n, id_base, flags, info, perm, &ns, &new_tree, &done)))
+    const u32* own = owner;
+    if (orig) {
+      u32* own_sub = S.alloc<u32>(n);
+      if (!own_sub) return EVM_ENOMEM;
+      KLAUNCH(k_sv_pack_sel, dim3(grid_for(n, 256, 4096)), dim3(256), (const uint8_t*)ts, stride, owner, orig, n, rec,
+              own_sub);
+      own = own_sub;
+    } else if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) {
+      return st;
+    }
+    if (mode != 2 && s->n_owners > 0) {
+      bool done = false, big_only = false;
+      uint8_t* bigmask = mode == 0 ? S.alloc<uint8_t>(n) : nullptr;
+      if (mode == 0 && !bigmask) return EVM_ENOMEM;
+      if ((st = ingest_by_owner(ctx, S, s, rec, own, n, orig, id_base, flags, info, perm, &ns, &new_tree, &done,
+                                bigmask, &big_only)))
         return st;
       if (done) goto commit;
+      if (big_only) {
+        // split: the big owners' messages through the sort path, the rest through LDS
+        u32* keep = S.alloc<u32>(n);
+        u32* pos = S.alloc<u32>(n);
+        u32* ns_small = S.alloc<u32>(1);
+        u32* sel_small = S.alloc<u32>(n);
+        u32* sel_big = S.alloc<u32>(n);
+        if (!keep || !pos || !ns_small || !sel_small || !sel_big) return EVM_ENOMEM;
+        KLAUNCH(k_not_u32, dim3(grid_for(n, 256)), dim3(256), bigmask, n, keep);
+        if ((st = scan_exclusive<u32, OpAdd>(ctx, S, keep, n, pos, ns_small))) return st;
+        KLAUNCH(k_split, dim3(grid_for(n, 256)), dim3(256), bigmask, pos, n, sel_small, sel_big);
+        u32 hsmall = 0;
+        HIPR(hipMemcpyAsync(&hsmall, ns_small, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+        HIPR(hipStreamSynchronize(ctx->stream));
+        if (hsmall && (st = ingest_impl(ctx, s, ts, stride, hsmall, owner, sel_small, id_base, flags, 1))) return st;
+        if (n - hsmall && (st = ingest_impl(ctx, s, ts, stride, n - hsmall, owner, sel_big, id_base, flags, 2)))
+          return st;
+        return EVM_OK;
+      }
     }
     FieldRange h0;
     for (int f = 0; f < N_FIELDS; ++f) {
@@ -1074,7 +1215,7 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
     if (hi.bad) {
       // a timestamp the engine cannot canonicalise (toISOString would differ
       // or throw): flag the culprits, apply nothing -- the host falls back
-      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
+      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
       (void)evm_sync(ctx);
       return EVM_ENONCANON;
     }
@@ -1124,7 +1265,7 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
     u32* cnt = S.alloc<u32>(2);
     if (!sel || !pos || !cnt) return EVM_ENOMEM;
     const StoreView old = view_of(s);
-    KLAUNCH(k_sv_mark, dim3(grid_for(n, 256)), dim3(256), rec, perm, skeys, n, old, flags, sel);
+    KLAUNCH(k_sv_mark, dim3(grid_for(n, 256)), dim3(256), rec, perm, skeys, n, old, flags, sel, orig);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, pos, cnt))) return st;
     u32 m = 0;
     HIPR(hipMemcpyAsync(&m, cnt, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
@@ -1140,7 +1281,7 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
     if (!n_owner || !n_tc || !n_hi || !n_lo || !n_id || !l_ck || !l_h) return EVM_ENOMEM;
     HIPR(hipMemsetAsync(cnt + 1, 0, sizeof(u32), ctx->stream));
     KLAUNCH(k_sv_compact, dim3(grid_for(n, 256)), dim3(256), rec, perm, sel, pos, n, (u64)id_base, n_owner, n_tc, n_hi,
-            n_lo, n_id, l_ck, l_h);
+            n_lo, n_id, l_ck, l_h, orig);
     if (m > 1) KLAUNCH(k_sv_sorted_check, dim3(grid_for(m, 256)), dim3(256), l_ck, (size_t)m, cnt + 1);
     // merged store
     if ((st = store_alloc(ctx, &ns, s->n_owners, s->n + m))) return st;
@@ -1193,6 +1334,16 @@ commit:
   return evm_sync(ctx);
 }
 
+extern "C" {
+
+int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                      uint64_t id_base, uint8_t* flags) {
+  if (!ctx || !s || stride < 46 || (n && (!ts || !owner || !flags))) return EVM_EINVAL;
+  if (n == 0) return EVM_OK;  // index.ts:145 `if (req.messages.length === 0) return merkleTree`
+  if (n >= 0xffffffffull) return EVM_EINVAL;
+  return ingest_impl(ctx, s, ts, stride, n, owner, nullptr, id_base, flags, ctx->server_path == 2 ? 2 : 0);
+}
+
 }  // extern "C"
 
 // Selection of each owner's rows after a per-owner bound (diff/since, < 0 =
@@ -1202,24 +1353,43 @@ static int select_after(evm_ctx* ctx, Scratch& S, const evm_store* s, const int6
   const u32 O = s->n_owners;
   int st;
   u64* first = S.alloc<u64>(O);
-  u32* cnt = S.alloc<u32>(O);
-  u32* pos = S.alloc<u32>(O);
+  u32* cand = S.alloc<u32>(O);
+  u32* cpos = S.alloc<u32>(O + 1);
+  u64* req = S.alloc<u64>(O);
   u32* tot = S.alloc<u32>(2);
-  if (!first || !cnt || !pos || !tot) return EVM_ENOMEM;
+  if (!first || !cand || !cpos || !req || !tot) return EVM_ENOMEM;
   HIPR(hipMemsetAsync(tot, 0, 2 * sizeof(u32), ctx->stream));
   const StoreView v = view_of(s);
-  KLAUNCH(k_sv_sel_count, dim3(grid_for(O, 64, 65536)), dim3(64), v, O, bound, (const uint8_t*)node, active, first, cnt,
-          tot + 1);
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, cnt, O, pos, tot))) return st;
-  KLAUNCH(k_u32_to_u64, dim3(grid_for(O + 1, 256)), dim3(256), pos, (size_t)O, tot, (u64*)sel_off);
+  KLAUNCH(k_sv_sel_first, dim3(grid_for(O, 64, 65536)), dim3(64), v, O, bound, (const uint8_t*)node, active, first,
+          cand, req, tot + 1);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, cand, O, cpos, cpos + O))) return st;
   u32 h[2];
-  HIPR(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipMemcpyAsync(&h[0], cpos + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipMemcpyAsync(&h[1], tot + 1, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
   if (h[1]) return EVM_EINVAL;  // a requester nodeId is not 16 hex chars
-  *n_sel = h[0];
-  if (h[0] > cap || (h[0] && !sel_id)) return EVM_ECAPACITY;
-  KLAUNCH(k_sv_sel_write, dim3(grid_for(O, 64, 65536)), dim3(64), v, (const u64*)s->id, O, first, cnt, pos,
-          (const uint8_t*)node, (u64*)sel_id);
+  const u32 C = h[0];
+  const int grid = grid_for(C, SEL_THREADS, 16384);
+  u32* keep = nullptr;
+  u32* kpos = nullptr;
+  u32 K = C;
+  if (node && C) {
+    keep = S.alloc<u32>(C);
+    kpos = S.alloc<u32>(C);
+    if (!keep || !kpos) return EVM_ENOMEM;
+    KLAUNCH(k_sv_sel_keep, dim3(grid), dim3(SEL_THREADS), v, O, C, (const u32*)cpos, (const u64*)first,
+            (const u64*)req, keep);
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, keep, C, kpos, tot))) return st;
+    HIPR(hipMemcpyAsync(&K, tot, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+  }
+  KLAUNCH(k_sv_sel_off, dim3(grid_for(O + 1, 256)), dim3(256), O, C, (const u32*)cpos, (const u32*)kpos,
+          (const u32*)tot, (u64*)sel_off);
+  *n_sel = K;
+  if (K > cap || (K && !sel_id)) return EVM_ECAPACITY;
+  if (K)
+    KLAUNCH(k_sv_sel_emit, dim3(grid), dim3(SEL_THREADS), O, C, (const u32*)cpos, (const u64*)first,
+            (const u32*)keep, (const u32*)kpos, (const u64*)s->id, (u64*)sel_id);
   return evm_sync(ctx);
 }
 

@@ -155,7 +155,8 @@ def config3(n_owners: int = 100_000, per_owner: int = 1000, nodes_per_owner: int
 
 
 def config5(n_owners: int, n: int, zipf_s: float = 1.2, cells_per_owner: int = 50, nodes_per_owner: int = 4,
-            stride: int = 48, seed_config: int = 5, redelivery: float = 0.10, upper_frac: float = 0.01):
+            stride: int = 48, seed_config: int = 5, redelivery: float = 0.10, upper_frac: float = 0.01,
+            with_millis: bool = False):
     """Adversarial stream (BASELINE config 5): owner sizes Zipf(s); per owner
     its nodes send on a coarse shared time grid, so many messages share millis
     across nodes (ties broken by counter, then by node bytes) and nodes repeat
@@ -164,7 +165,7 @@ def config5(n_owners: int, n: int, zipf_s: float = 1.2, cells_per_owner: int = 5
     owner, same cell: half of them after a newer write to that cell -> the
     stale-redelivery XOR toggle of applyMessages).  Returns (ts arena, owner
     u32, cell u32 global ids = owner * cells_per_owner + local cell), batch
-    order."""
+    order; with_millis adds each message's millis (int64) as a fourth."""
     rng = rng_for(seed_config)
     w = 1.0 / np.arange(1, n_owners + 1, dtype=np.float64) ** zipf_s
     base = int(n * (1 - redelivery))
@@ -187,14 +188,17 @@ def config5(n_owners: int, n: int, zipf_s: float = 1.2, cells_per_owner: int = 5
     cell = owner * cells_per_owner + rng.integers(0, cells_per_owner, size=base)
     perm = rng.permutation(base)
     ts = format_timestamps(millis[perm], counter[perm], nodes[gnode[perm]], stride)
-    owner, cell = owner[perm], cell[perm]
+    owner, cell, ms = owner[perm], cell[perm], millis[perm]
     # redeliveries: copies of earlier messages appended later in the batch
     k = n - base
     src = rng.integers(0, base, size=k)
     ts = np.concatenate([ts, ts[src]])
     owner = np.concatenate([owner, owner[src]])
     cell = np.concatenate([cell, cell[src]])
+    ms = np.concatenate([ms, ms[src]])
     mix = rng.permutation(n - base) + base  # interleave the copies among the tail
     tail = np.arange(base, n)
-    ts[tail], owner[tail], cell[tail] = ts[mix], owner[mix], cell[mix]
+    ts[tail], owner[tail], cell[tail], ms[tail] = ts[mix], owner[mix], cell[mix], ms[mix]
+    if with_millis:
+        return ts, owner.astype(np.uint32), cell.astype(np.uint32), ms
     return ts, owner.astype(np.uint32), cell.astype(np.uint32)

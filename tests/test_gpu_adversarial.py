@@ -83,3 +83,57 @@ def test_client_streaming_path_hot_owner(eng, stream):
     assert np.array_equal(flags.cpu().numpy(), fw)
     assert np.array_equal(winner.cpu().numpy(), ww)
     assert tree.to_json(0) == js
+
+
+def test_server_select_adversarial(eng):
+    """getMessages over the Zipf store (index.ts:160-187): the diff per owner
+    against a client that knows each owner's first 90 % by millis (the C
+    restatement's diff), and the rows after it minus the requester's node
+    (case-insensitive LIKE), in timestamp order.  The hottest owner's
+    selection spans thousands of candidate tiles, the cold ones one or none."""
+    from evolu_amd import synth
+
+    ts, owner, _, ms = synth.config5(N_OWNERS, N, cells_per_owner=CELLS, seed_config=5, with_millis=True)
+    counts = np.bincount(owner, minlength=N_OWNERS)
+    order = np.lexsort((ms, owner))
+    rank = np.empty(N, dtype=np.int64)
+    rank[order] = np.arange(N) - (np.cumsum(counts) - counts)[owner[order]]
+    know = rank < (0.9 * counts[owner]).astype(np.int64)
+    srv, cli = CO.Server(N_OWNERS, N), CO.Server(N_OWNERS, N)
+    assert srv.ingest(ts, owner)[0] == 0
+    st, ins = cli.ingest(ts[know], owner[know])
+    assert st == 0
+    store = eng.store_new(N_OWNERS)
+    assert store.ingest(eng.dev(ts), eng.dev(owner), 0)[1] == 0
+    # the client's tree holds each known message once (redeliveries deduplicated)
+    uniq = (ins & 0x04) != 0
+    client = eng.merkle_insert(eng.tree_new(N_OWNERS), eng.dev(np.ascontiguousarray(ts[know][uniq])),
+                               eng.dev(np.ascontiguousarray(owner[know][uniq])))
+    rng = np.random.default_rng(7)
+    req = np.empty((N_OWNERS, 16), dtype=np.uint8)
+    for o in range(N_OWNERS):
+        rows = np.nonzero(owner == o)[0]
+        req[o] = ts[rng.choice(rows), 30:46] if len(rows) and rng.random() < 0.8 else synth.random_nodes(rng, 1)[0]
+        if rng.random() < 0.3:  # LIKE is ASCII case-insensitive
+            req[o] = np.where((req[o] >= ord("a")) & (req[o] <= ord("f")), req[o] - 32, req[o])
+    diff, off, ids = store.select(client, eng.dev(req.reshape(-1).copy()))
+    diff, off, ids = diff.cpu().numpy(), off.cpu().numpy(), ids.cpu().numpy()
+    key = ts[:, :46].copy().view("S46").ravel()
+    low = lambda b: np.where((b >= ord("A")) & (b <= ord("F")), b + 32, b)  # noqa: E731
+    hot = np.argsort(-counts)
+    for o in list(hot[:4]) + list(range(0, N_OWNERS, 7)):
+        d = srv.diff(cli, int(o))
+        assert int(diff[o]) == d, o
+        got = key[ids[off[o]:off[o + 1]].astype(np.int64)]
+        if d < 0:
+            assert len(got) == 0
+            continue
+        since = synth.format_timestamps(np.array([d]), np.array([0]), np.full((1, 16), ord("0"), np.uint8))
+        since = since[:, :46].copy().view("S46")[0, 0]
+        mine = np.unique(key[owner == o])
+        mine = mine[mine > since]
+        node = np.frombuffer(b"".join(mine), dtype=np.uint8).reshape(-1, 46)[:, 30:46] if len(mine) else \
+            np.zeros((0, 16), np.uint8)
+        mine = mine[~np.all(low(node) == low(req[o]), axis=1)]
+        assert np.array_equal(got, mine), (o, len(got), len(mine))
+    assert int(off[-1]) == len(ids)

@@ -34,4 +34,10 @@ timeout -k 10 300 python -u bench.py --workload server --steps 5 --warmup 2 --re
   2> gpurun_out/bench_server_shuffled.err
 rc=$?
 echo "bench server (per-message shuffle) rc=$rc"; cat gpurun_out/bench_server_shuffled.json
+if fatal $rc; then exit $rc; fi
+
+timeout -k 10 300 python -u bench.py --workload server --steps 5 --warmup 2 --zipf 1.2 > gpurun_out/bench_server_zipf.json \
+  2> gpurun_out/bench_server_zipf.err
+rc=$?
+echo "bench server (config 5, Zipf owners) rc=$rc"; cat gpurun_out/bench_server_zipf.json; tail -3 gpurun_out/bench_server_zipf.err
 exit $rc
