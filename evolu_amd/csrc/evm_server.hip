@@ -164,81 +164,104 @@ __global__ void k_sv_ckey(const evm_rec* __restrict__ rec, size_t n, CKey ck, u6
 }
 
 constexpr int TIE_MAX = 64;
-// Runs of equal compound keys: stable insertion sort of the run by the node
-// ranks (the batch index order inside the run is the radix sort's).  A run
+
+// The batch's records in sorted order (one gather; the kernels after it read
+// sequentially).
+__global__ void k_sv_gather(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, size_t n,
+                            evm_rec* __restrict__ srec) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
+    srec[p] = rec[perm[p]];
+}
+
+__device__ __forceinline__ bool same_node(const evm_rec& a, const evm_rec& b) {
+  return a.node == b.node && ((a.meta ^ b.meta) & EVM_META_CASEMASK) == 0;
+}
+
+// Runs of equal compound keys (one owner and tc, several nodes): every member
+// counts the members that sort before it by (node ranks, position) -- the
+// positions inside a run are in batch order (the radix sort is stable) -- and
+// records itself as the source of sorted position run start + rank.  A run
 // longer than TIE_MAX flags the slow (full-field) sort.
-__global__ void k_sv_ties(const u64* __restrict__ key, u32* __restrict__ perm, const evm_rec* __restrict__ rec,
-                          size_t n, u32* __restrict__ too_long) {
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x + 1; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    if (key[p] != key[p - 1] || (p >= 2 && key[p - 2] == key[p - 1])) continue;  // not a run start (at p - 1)
-    const size_t s = p - 1;
-    size_t e = p + 1;
-    while (e < n && key[e] == key[s] && e - s <= TIE_MAX) ++e;
-    if (e - s > TIE_MAX) {
+__global__ void k_sv_ties(const u64* __restrict__ key, const evm_rec* __restrict__ srec, size_t n,
+                          u32* __restrict__ src, u32* __restrict__ too_long) {
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    const u64 k = key[p];
+    const bool left = p > 0 && key[p - 1] == k, right = p + 1 < n && key[p + 1] == k;
+    if (!left && !right) {
+      src[p] = (u32)p;
+      continue;
+    }
+    size_t s = p, e = p + 1;
+    while (s > 0 && key[s - 1] == k && p - s < TIE_MAX) --s;
+    while (e < n && key[e] == k && e - s <= TIE_MAX) ++e;
+    if (e - s > TIE_MAX || (s > 0 && key[s - 1] == k)) {
       atomicOr(too_long, 1u);
       continue;
     }
-    u32 idx[TIE_MAX];
-    u64 hi[TIE_MAX];
-    u32 lo[TIE_MAX];
-    const int L = (int)(e - s);
-    for (int k = 0; k < L; ++k) {
-      const u32 i = perm[s + k];
-      const SKey sk = skey_of(rec[i]);
-      int j = k;
-      while (j > 0 && (hi[j - 1] > sk.hi || (hi[j - 1] == sk.hi && lo[j - 1] > sk.lo))) {
-        idx[j] = idx[j - 1];
-        hi[j] = hi[j - 1];
-        lo[j] = lo[j - 1];
-        --j;
-      }
-      idx[j] = i;
-      hi[j] = sk.hi;
-      lo[j] = sk.lo;
+    const evm_rec r = srec[p];
+    u64 hp;
+    u32 lp;
+    node_ranks(r.node, r.meta & EVM_META_CASEMASK, &hp, &lp);
+    u32 rank = 0;
+    for (size_t q = s; q < e; ++q) {
+      if (q == p) continue;
+      const evm_rec x = srec[q];
+      u64 hq;
+      u32 lq;
+      node_ranks(x.node, x.meta & EVM_META_CASEMASK, &hq, &lq);
+      rank += (hq < hp || (hq == hp && (lq < lp || (lq == lp && q < p)))) ? 1u : 0u;
     }
-    for (int k = 0; k < L; ++k) perm[s + k] = idx[k];
+    src[s + rank] = (u32)p;
   }
 }
 
 // ------------------------------------------------------------ dedup + marks
-// Sorted order p: first occurrence of (owner, timestamp) in batch order (the
-// sort is stable on the batch index) that the store does not hold yet.
-__global__ void k_sv_mark(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u64* __restrict__ skeys,
-                          size_t n, StoreView st, uint8_t* __restrict__ flags, u32* __restrict__ sel,
-                          const u32* __restrict__ orig) {
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    const u32 i = perm[p];
+// Sorted order d (record srec[src[d]], or srec[d] without a tie permutation):
+// first occurrence of (owner, timestamp) in batch order (equal timestamps sit
+// in batch order) that the store does not hold yet.
+__global__ void k_sv_mark(const evm_rec* __restrict__ srec, const u32* __restrict__ src, const u32* __restrict__ perm,
+                          const u64* __restrict__ skeys, size_t n, StoreView st, uint8_t* __restrict__ flags,
+                          u32* __restrict__ sel, const u32* __restrict__ orig) {
+  for (size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x; d < n; d += (size_t)gridDim.x * blockDim.x) {
+    const size_t p = src ? src[d] : d;
+    const evm_rec r = srec[p];
     bool first = true;
-    if (p > 0) {
-      // sorted compound keys differ => the timestamps differ (no gathers)
-      if (!skeys || skeys[p] == skeys[p - 1]) first = skey_cmp(skey_of(rec[perm[p - 1]]), skey_of(rec[i])) != 0;
+    if (d > 0) {
+      // sorted compound keys differ => the timestamps differ; equal => same owner and tc
+      if (!skeys) {
+        first = skey_cmp(skey_of(srec[d - 1]), skey_of(r)) != 0;
+      } else if (skeys[d] == skeys[d - 1]) {
+        first = !same_node(srec[src[d - 1]], r);
+      }
     }
     bool ins = first;
     if (ins) {
-      const u32 owner = rec[i].aux;
+      const u32 owner = r.aux;
       const size_t a = st.off[owner], b = st.off[owner + 1];
       if (a < b) {
-        const SKey k = skey_of(rec[i]);
+        const SKey k = skey_of(r);
         const size_t q = store_lower(st, a, b, k);
         ins = !(q < b && skey_cmp(skey_at(st, q), k) == 0);
       }
     }
+    const u32 i = perm[p];
     flags[orig ? orig[i] : i] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
-    sel[p] = ins ? 1u : 0u;
+    sel[d] = ins ? 1u : 0u;
   }
 }
 
-__global__ void k_sv_compact(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u32* __restrict__ sel,
-                             const u32* __restrict__ pos, size_t n, u64 id_base, u32* __restrict__ o_owner,
-                             u64* __restrict__ o_tc, u64* __restrict__ o_hi, u32* __restrict__ o_lo,
-                             u64* __restrict__ o_id, u64* __restrict__ l_ck, u32* __restrict__ l_h,
-                             const u32* __restrict__ orig) {
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    if (!sel[p]) continue;
-    const u32 i = perm[p];
-    const evm_rec r = rec[i];
+__global__ void k_sv_compact(const evm_rec* __restrict__ srec, const u32* __restrict__ src,
+                             const u32* __restrict__ perm, const u32* __restrict__ sel, const u32* __restrict__ pos,
+                             size_t n, u64 id_base, u32* __restrict__ o_owner, u64* __restrict__ o_tc,
+                             u64* __restrict__ o_hi, u32* __restrict__ o_lo, u64* __restrict__ o_id,
+                             u64* __restrict__ l_ck, u32* __restrict__ l_h, const u32* __restrict__ orig) {
+  for (size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x; d < n; d += (size_t)gridDim.x * blockDim.x) {
+    if (!sel[d]) continue;
+    const size_t p = src ? src[d] : d;
+    const evm_rec r = srec[p];
     const SKey k = skey_of(r);
-    const u32 q = pos[p];
+    const u32 q = pos[d];
+    const u32 i = perm[p];
     o_owner[q] = k.owner;
     o_tc[q] = k.tc;
     o_hi[q] = k.hi;
@@ -392,18 +415,25 @@ __global__ void k_big_mask(const evm_rec* __restrict__ rec, size_t n, const u64*
   }
 }
 
-// stable split of [0, n) by mask: pos = exclusive count of unmasked before i
-__global__ void k_split(const uint8_t* __restrict__ mask, const u32* __restrict__ pos, size_t n, u32* __restrict__ small,
-                        u32* __restrict__ big) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    if (mask[i]) big[i - pos[i]] = (u32)i;
-    else small[pos[i]] = (u32)i;
-  }
+__global__ void k_mask_u32(const uint8_t* __restrict__ mask, size_t n, u32* __restrict__ out) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = mask[i];
 }
 
-__global__ void k_not_u32(const uint8_t* __restrict__ mask, size_t n, u32* __restrict__ out) {
+// the masked indices in order: pos = exclusive count of masked before i
+__global__ void k_pick(const uint8_t* __restrict__ mask, const u32* __restrict__ pos, size_t n, u32* __restrict__ out) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    out[i] = mask[i] ? 0u : 1u;
+    if (mask[i]) out[pos[i]] = (u32)i;
+}
+
+// records of a sub-batch from the caller's packed records
+__global__ void k_sv_rec_sel(const evm_rec* __restrict__ prec, const u32* __restrict__ orig, size_t n,
+                             evm_rec* __restrict__ out, u32* __restrict__ owner_out) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const evm_rec r = prec[orig[k]];
+    out[k] = r;
+    owner_out[k] = r.aux;
+  }
 }
 
 // ------------------------------------------------------ K5: owner ingest
@@ -457,7 +487,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     u64* __restrict__ n_tc, u64* __restrict__ n_hi, u32* __restrict__ n_lo, u64* __restrict__ n_id,
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status,
-    const u32* __restrict__ orig) {
+    const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list) {
   constexpr int PER = CAP / SVO_THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
   constexpr u64 PMASK = CAP - 1;
@@ -469,14 +499,15 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   __shared__ u32 s_cnt[CAP];  // counting sort: bucket counts, then starts
   __shared__ u64 s_red[2 * (SVO_THREADS / 64)];
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
-  const u32 o = blockIdx.x;
+  const u32 o = list ? list[blockIdx.x] : blockIdx.x;  // pass 2: only the owners pass 1 deferred
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const u64 a = seg[o];
   const u64 m = seg[o + 1] - a;  // an unsorted owner column (bad ids) may underflow: "big"
   const u64 la = t_off[o], lb = t_off[o + 1];
   if (m > CAP || m == 0) {
     if (threadIdx.x == 0) {
-      if (m) atomicOr(&status->big, 1u);
+      if (m <= SVO_CAP && mid_list) mid_list[1 + atomicAdd(&mid_list[0], 1u)] = o;  // for the SVO_CAP pass
+      else if (m) atomicOr(&status->big, 1u);
       cnt_rows[o] = 0;
       cnt_new[o] = 0;
       cnt_leaves[o] = (u32)(lb - la);
@@ -1037,39 +1068,44 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   }
   const evm_tree* t = s->tree;
   u32 *c_rows = cnt, *c_new = cnt + O, *c_leaves = cnt + 2 * (size_t)O;
+  u32* mid = S.alloc<u32>((size_t)O + 1);  // [count, owners whose share is in (1024, SVO_CAP]]
+  if (!mid) return EVM_ENOMEM;
   Info hi;
   SvoStatus hs;
-  u32 ht[2];
-  // the common share size first (more workgroups per CU); larger shares retry once
-  for (int pass = 0; pass < 2; ++pass) {
-    HIPR(hipMemsetAsync(status, 0, sizeof(SvoStatus), ctx->stream));
-    if (pass == 0)
-      KLAUNCH(k_svo_a<1024>, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off,
-              (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new,
-              c_leaves, status, orig);
-    else
-      KLAUNCH(k_svo_a<SVO_CAP>, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off,
-              (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new,
-              c_leaves, status, orig);
-    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, O, pos, tot))) return st;
-    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, O, pos + O, tot + 1))) return st;
-    HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipMemcpyAsync(ht, tot, sizeof(ht), hipMemcpyDeviceToHost, ctx->stream));
-    if ((st = read_info(ctx, info, &hi))) return st;
-    if (hi.bad_aux) return EVM_EINVAL;
-    if (hi.bad) {
-      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
-      (void)evm_sync(ctx);
-      return EVM_ENONCANON;
-    }
-    if (!hs.big || hs.fallback) break;
+  u32 ht[2], hmid = 0;
+  HIPR(hipMemsetAsync(status, 0, sizeof(SvoStatus), ctx->stream));
+  HIPR(hipMemsetAsync(mid, 0, sizeof(u32), ctx->stream));
+  // the common share size over every owner (more workgroups per CU); larger
+  // shares are listed and take the SVO_CAP kernel over just those owners
+  KLAUNCH(k_svo_a<1024>, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off, (const u64*)t->ck,
+          (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves, status, orig,
+          (const u32*)nullptr, mid);
+  HIPR(hipMemcpyAsync(&hmid, mid, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  if ((st = read_info(ctx, info, &hi))) return st;
+  if (hi.bad_aux) return EVM_EINVAL;
+  if (hi.bad) {
+    KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
+    (void)evm_sync(ctx);
+    return EVM_ENONCANON;
   }
-  if (hs.big && !hs.fallback && bigmask) {
-    // only some owners are too big for LDS: tell the caller which messages are theirs
+  if (hmid)
+    KLAUNCH(k_svo_a<SVO_CAP>, dim3(hmid), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off,
+            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
+            status, orig, (const u32*)(mid + 1), (u32*)nullptr);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, O, pos, tot))) return st;
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, O, pos + O, tot + 1))) return st;
+  HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipMemcpyAsync(ht, tot, sizeof(ht), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if (hs.fallback) return EVM_OK;  // the sort path redoes every flag
+  if (hs.big) {
+    if (!bigmask) return EVM_OK;
+    // only some owners are too big for LDS: the rest commit here (the big
+    // ones contribute no rows or leaves), the caller sends the big owners'
+    // messages through the sort path
     KLAUNCH(k_big_mask, dim3(grid_for(n, 256)), dim3(256), rec, n, seg, (u64)SVO_CAP, bigmask);
     *big_only = true;
   }
-  if (hs.big || hs.fallback) return EVM_OK;  // the sort path redoes the flags
   // new store and tree, exactly sized
   if ((st = store_alloc(ctx, ns, O, s->n + ht[0]))) {
     store_release_arrays(ctx, ns);
@@ -1143,13 +1179,28 @@ int evm_store_messages(evm_ctx* ctx, const evm_store* s, uint64_t* owner_off, ui
 
 // One ingest over the caller's batch, or over the sub-batch orig[0..n) of it
 // (message k = the caller's message orig[k]; flags and ids refer to the
-// caller's indices).  mode 0: per-owner LDS path, and when only some owners
-// are too big for it, the batch split in two (their messages through the
-// sort path, the rest through LDS) -- owners are independent, so the result
-// is the one of a single ingest; mode 1: LDS path, else the sort path;
-// mode 2: the sort path.
+// caller's indices; prec, when given, holds the caller's packed records).
+// mode 0: per-owner LDS path; when only some owners are too big for it, the
+// rest commit and the big owners' messages then go through the sort path --
+// owners are independent, so the result is the one of a single ingest;
+// mode 1: LDS path, else the sort path; mode 2: the sort path.
+// Swap in the new store arrays and tree.
+static int commit_store(evm_ctx* ctx, evm_store* s, evm_store& ns, evm_tree* new_tree) {
+  store_release_arrays(ctx, s);
+  tree_destroy(ctx, s->tree);
+  s->n = ns.n;
+  s->off = ns.off;
+  s->owner = ns.owner;
+  s->tc = ns.tc;
+  s->hi = ns.hi;
+  s->lo = ns.lo;
+  s->id = ns.id;
+  s->tree = new_tree;
+  return evm_sync(ctx);
+}
+
 static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
-                       const u32* orig, uint64_t id_base, uint8_t* flags, int mode) {
+                       const u32* orig, const evm_rec* prec, uint64_t id_base, uint8_t* flags, int mode) {
   int st;
   evm_store ns{};
   evm_tree* new_tree = nullptr;
@@ -1166,39 +1217,39 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     if (orig) {
       u32* own_sub = S.alloc<u32>(n);
       if (!own_sub) return EVM_ENOMEM;
-      KLAUNCH(k_sv_pack_sel, dim3(grid_for(n, 256, 4096)), dim3(256), (const uint8_t*)ts, stride, owner, orig, n, rec,
-              own_sub);
+      if (prec)  // the caller's records, already packed and checked
+        KLAUNCH(k_sv_rec_sel, dim3(grid_for(n, 256, 8192)), dim3(256), prec, orig, n, rec, own_sub);
+      else
+        KLAUNCH(k_sv_pack_sel, dim3(grid_for(n, 256, 4096)), dim3(256), (const uint8_t*)ts, stride, owner, orig, n,
+                rec, own_sub);
       own = own_sub;
     } else if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) {
       return st;
     }
     if (mode != 2 && s->n_owners > 0) {
       bool done = false, big_only = false;
-      uint8_t* bigmask = mode == 0 ? S.alloc<uint8_t>(n) : nullptr;
-      if (mode == 0 && !bigmask) return EVM_ENOMEM;
+      uint8_t* bigmask = (mode == 0 && !orig) ? S.alloc<uint8_t>(n) : nullptr;
+      if (mode == 0 && !orig && !bigmask) return EVM_ENOMEM;
       if ((st = ingest_by_owner(ctx, S, s, rec, own, n, orig, id_base, flags, info, perm, &ns, &new_tree, &done,
                                 bigmask, &big_only)))
         return st;
-      if (done) goto commit;
-      if (big_only) {
-        // split: the big owners' messages through the sort path, the rest through LDS
-        u32* keep = S.alloc<u32>(n);
-        u32* pos = S.alloc<u32>(n);
-        u32* ns_small = S.alloc<u32>(1);
-        u32* sel_small = S.alloc<u32>(n);
+      if (done && big_only && !orig) {
+        // the LDS path took every owner but the big ones: commit that, then
+        // the big owners' messages (in batch order) through the sort path
+        u32* bm = S.alloc<u32>(n);
+        u32* bpos = S.alloc<u32>(n);
+        u32* nbig = S.alloc<u32>(1);
         u32* sel_big = S.alloc<u32>(n);
-        if (!keep || !pos || !ns_small || !sel_small || !sel_big) return EVM_ENOMEM;
-        KLAUNCH(k_not_u32, dim3(grid_for(n, 256)), dim3(256), bigmask, n, keep);
-        if ((st = scan_exclusive<u32, OpAdd>(ctx, S, keep, n, pos, ns_small))) return st;
-        KLAUNCH(k_split, dim3(grid_for(n, 256)), dim3(256), bigmask, pos, n, sel_small, sel_big);
-        u32 hsmall = 0;
-        HIPR(hipMemcpyAsync(&hsmall, ns_small, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-        HIPR(hipStreamSynchronize(ctx->stream));
-        if (hsmall && (st = ingest_impl(ctx, s, ts, stride, hsmall, owner, sel_small, id_base, flags, 1))) return st;
-        if (n - hsmall && (st = ingest_impl(ctx, s, ts, stride, n - hsmall, owner, sel_big, id_base, flags, 2)))
-          return st;
-        return EVM_OK;
+        if (!bm || !bpos || !nbig || !sel_big) return EVM_ENOMEM;
+        KLAUNCH(k_mask_u32, dim3(grid_for(n, 256)), dim3(256), bigmask, n, bm);
+        if ((st = scan_exclusive<u32, OpAdd>(ctx, S, bm, n, bpos, nbig))) return st;
+        KLAUNCH(k_pick, dim3(grid_for(n, 256)), dim3(256), bigmask, bpos, n, sel_big);
+        u32 hbig = 0;
+        HIPR(hipMemcpyAsync(&hbig, nbig, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+        if ((st = commit_store(ctx, s, ns, new_tree))) return st;
+        return ingest_impl(ctx, s, ts, stride, hbig, owner, sel_big, rec, id_base, flags, 2);
       }
+      if (done) goto commit;
     }
     FieldRange h0;
     for (int f = 0; f < N_FIELDS; ++f) {
@@ -1223,6 +1274,8 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     const int ob = bits_of(hr.mx[F_OWNER] - hr.mn[F_OWNER]), mb = bits_of(hr.mx[F_MS] - hr.mn[F_MS]),
               cb = bits_of(hr.mx[F_CTR]);
     const u64* skeys = nullptr;
+    evm_rec* srec = nullptr;  // records in sorted order
+    u32* src = nullptr;       // sorted position -> srec index (tie runs permuted by node)
     bool sorted = false;
     if (ob + mb + cb <= 64) {
       // one radix sort on the compound (owner, millis, counter) key, then node-rank ties
@@ -1232,14 +1285,17 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       KLAUNCH(k_sv_ckey, dim3(grid_for(n, 256)), dim3(256), rec, n, ck, kk, vv);
       if ((st = radix_sort_pairs<u64>(ctx, S, kk, vv, n, 0, ob + mb + cb))) return st;
       u32* tl = S.alloc<u32>(1);
-      if (!tl) return EVM_ENOMEM;
+      srec = S.alloc<evm_rec>(n);
+      src = S.alloc<u32>(n);
+      if (!tl || !srec || !src) return EVM_ENOMEM;
       HIPR(hipMemsetAsync(tl, 0, sizeof(u32), ctx->stream));
-      KLAUNCH(k_sv_ties, dim3(grid_for(n, 256)), dim3(256), kk, vv, rec, n, tl);
+      KLAUNCH(k_sv_gather, dim3(grid_for(n, 256)), dim3(256), rec, vv, n, srec);
+      KLAUNCH(k_sv_ties, dim3(grid_for(n, 256)), dim3(256), kk, srec, n, src, tl);
       u32 too_long = 0;
       HIPR(hipMemcpyAsync(&too_long, tl, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
       HIPR(hipStreamSynchronize(ctx->stream));
       if (!too_long) {
-        if (vv != perm) HIPR(hipMemcpyAsync(perm, vv, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
+        perm = vv;  // (scratch lives until the end of the call)
         skeys = kk;  // sorted compound keys (scratch lives until the end of the call)
         sorted = true;
       }
@@ -1258,6 +1314,9 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
         if ((st = radix_sort_pairs<u64>(ctx, S, kk, vv, n, 0, hb))) return st;
         if (vv != perm) HIPR(hipMemcpyAsync(perm, vv, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
       }
+      if (!srec && !(srec = S.alloc<evm_rec>(n))) return EVM_ENOMEM;
+      src = nullptr;
+      KLAUNCH(k_sv_gather, dim3(grid_for(n, 256)), dim3(256), rec, (const u32*)perm, n, srec);
     }
     // dedup within the batch and against the store
     u32* sel = S.alloc<u32>(n);
@@ -1265,7 +1324,8 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     u32* cnt = S.alloc<u32>(2);
     if (!sel || !pos || !cnt) return EVM_ENOMEM;
     const StoreView old = view_of(s);
-    KLAUNCH(k_sv_mark, dim3(grid_for(n, 256)), dim3(256), rec, perm, skeys, n, old, flags, sel, orig);
+    KLAUNCH(k_sv_mark, dim3(grid_for(n, 256)), dim3(256), (const evm_rec*)srec, (const u32*)src, (const u32*)perm, skeys,
+            n, old, flags, sel, orig);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, sel, n, pos, cnt))) return st;
     u32 m = 0;
     HIPR(hipMemcpyAsync(&m, cnt, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
@@ -1280,8 +1340,8 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     u32* l_h = S.alloc<u32>(m);
     if (!n_owner || !n_tc || !n_hi || !n_lo || !n_id || !l_ck || !l_h) return EVM_ENOMEM;
     HIPR(hipMemsetAsync(cnt + 1, 0, sizeof(u32), ctx->stream));
-    KLAUNCH(k_sv_compact, dim3(grid_for(n, 256)), dim3(256), rec, perm, sel, pos, n, (u64)id_base, n_owner, n_tc, n_hi,
-            n_lo, n_id, l_ck, l_h, orig);
+    KLAUNCH(k_sv_compact, dim3(grid_for(n, 256)), dim3(256), (const evm_rec*)srec, (const u32*)src, (const u32*)perm,
+            sel, pos, n, (u64)id_base, n_owner, n_tc, n_hi, n_lo, n_id, l_ck, l_h, orig);
     if (m > 1) KLAUNCH(k_sv_sorted_check, dim3(grid_for(m, 256)), dim3(256), l_ck, (size_t)m, cnt + 1);
     // merged store
     if ((st = store_alloc(ctx, &ns, s->n_owners, s->n + m))) return st;
@@ -1320,18 +1380,7 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     }
   }
 commit:
-  // commit: swap in the new store arrays and tree
-  store_release_arrays(ctx, s);
-  tree_destroy(ctx, s->tree);
-  s->n = ns.n;
-  s->off = ns.off;
-  s->owner = ns.owner;
-  s->tc = ns.tc;
-  s->hi = ns.hi;
-  s->lo = ns.lo;
-  s->id = ns.id;
-  s->tree = new_tree;
-  return evm_sync(ctx);
+  return commit_store(ctx, s, ns, new_tree);
 }
 
 extern "C" {
@@ -1341,7 +1390,7 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
   if (!ctx || !s || stride < 46 || (n && (!ts || !owner || !flags))) return EVM_EINVAL;
   if (n == 0) return EVM_OK;  // index.ts:145 `if (req.messages.length === 0) return merkleTree`
   if (n >= 0xffffffffull) return EVM_EINVAL;
-  return ingest_impl(ctx, s, ts, stride, n, owner, nullptr, id_base, flags, ctx->server_path == 2 ? 2 : 0);
+  return ingest_impl(ctx, s, ts, stride, n, owner, nullptr, nullptr, id_base, flags, ctx->server_path == 2 ? 2 : 0);
 }
 
 }  // extern "C"
