@@ -588,6 +588,12 @@ int evm_prof_enable(evm_ctx* ctx, int on) {
   return EVM_OK;
 }
 
+int evm_prof_only(evm_ctx* ctx, const char* kernel) {
+  if (!ctx) return EVM_EINVAL;
+  ctx->prof_only = kernel ? kernel : "";
+  return EVM_OK;
+}
+
 }  // extern "C"
 static void prof_drain(evm_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);

@@ -16,6 +16,7 @@ struct evm_ctx {
   hipStream_t stream;
   // kernel timing (evm_prof_*): HIP event pairs per kernel name, on `stream`
   bool prof = false;
+  std::string prof_only;  // evm_prof_only: time just this kernel ("" = all)
   int client_path = 0;  // EVM_OPT_CLIENT_PATH
   int server_path = 0;  // EVM_OPT_SERVER_PATH
   int overlap = 1;      // EVM_OPT_OVERLAP: independent checks on a second stream
@@ -143,7 +144,7 @@ class Scratch {
 class ProfScope {
  public:
   ProfScope(evm_ctx* c, const char* name, hipStream_t s = nullptr) : ctx_(c), name_(name), s_(s ? s : c->stream) {
-    if (!ctx_->prof) return;
+    if (!ctx_->prof || (!ctx_->prof_only.empty() && ctx_->prof_only != name_)) return;
     a_ = take();
     b_ = take();
     if (a_ && b_) {

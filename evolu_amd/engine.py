@@ -82,6 +82,10 @@ class Engine:
     def prof_enable(self, on: bool = True):
         check(self.lib.evm_prof_enable(self.h, 1 if on else 0), "evm_prof_enable")
 
+    def prof_only(self, kernel: Optional[str] = None):
+        """Time only `kernel`'s launches (its report name); None = every kernel."""
+        check(self.lib.evm_prof_only(self.h, (kernel or "").encode()), "evm_prof_only")
+
     def prof_reset(self):
         check(self.lib.evm_prof_reset(self.h), "evm_prof_reset")
 

@@ -95,6 +95,8 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value);
 /* kernel timing with HIP events on the context stream (for roofline reports) */
 int evm_prof_enable(evm_ctx* ctx, int on);
 int evm_prof_reset(evm_ctx* ctx);
+/* time only the launches of one kernel (its report name); null or "" = all */
+int evm_prof_only(evm_ctx* ctx, const char* kernel);
 /* JSON {"kernel": [total_ms, launches], ...}; *len = bytes needed */
 int evm_prof_report(evm_ctx* ctx, char* buf, size_t cap, size_t* len);
 int evm_dev_alloc(evm_ctx* ctx, size_t bytes, void** out);
