@@ -59,6 +59,7 @@ SIGNATURES = {
     "evm_set_option": (_i, [_vp, _i, C.c_int64]),
     "evm_prof_enable": (_i, [_vp, _i]),
     "evm_prof_reset": (_i, [_vp]),
+    "evm_cross_cell_check": (_i, [_vp, _vp, _sz, _sz, _vp, C.c_uint32, C.POINTER(C.c_int32)]),
     "evm_prof_only": (_i, [_vp, C.c_char_p]),
     "evm_prof_report": (_i, [_vp, _vp, _sz, C.POINTER(_sz)]),
     "evm_dev_alloc": (_i, [_vp, _sz, C.POINTER(_vp)]),

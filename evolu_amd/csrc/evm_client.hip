@@ -1141,4 +1141,31 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
   return evm_sync(ctx);
 }
 
+int evm_cross_cell_check(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const uint32_t* cell, uint32_t n_cells,
+                         int32_t* found) {
+  if (!ctx || !found || stride < 46 || (n && (!ts || !cell))) return EVM_EINVAL;
+  if (n >= 0x7fffffffu) return EVM_EINVAL;
+  *found = 0;
+  if (n == 0) return EVM_OK;
+  int st;
+  Info hi;
+  {
+    Scratch S(ctx);
+    Info* info = nullptr;
+    if ((st = new_info(ctx, S, &info))) return st;
+    evm_rec* rec = S.alloc<evm_rec>(n);
+    const int lg = ceil_log2(2 * n);
+    u64* table = S.alloc<u64>((size_t)1 << lg);
+    if (!rec || !table) return EVM_ENOMEM;
+    if ((st = launch_pack(ctx, ts, stride, n, cell, n_cells, rec, info))) return st;
+    HIPR(hipMemsetAsync(table, 0, sizeof(u64) << lg, ctx->stream));
+    KLAUNCH(k_xcell, dim3(grid_for(n, 256, 8192)), dim3(256), rec, n, table, (u32)lg, info);
+    if ((st = read_info(ctx, info, &hi))) return st;
+  }
+  if (hi.bad) return EVM_ENONCANON;
+  if (hi.bad_aux) return EVM_EINVAL;
+  *found = hi.collision ? 1 : 0;
+  return EVM_OK;
+}
+
 }  // extern "C"

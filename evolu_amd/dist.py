@@ -236,3 +236,96 @@ def merge_hot_trees(eng, trees, omap: OwnerMap, group=None):
                                     a[nh + 1 + L:nh + 1 + 2 * L].astype(np.int32))
         merged = part if merged is None else eng.tree_merge(merged, part)
     return merged
+
+
+# ---------------------------------------------------------------------------
+# Client hot-owner split: ONE owner's applyMessages
+# batch over every rank.  The LWW decisions of applyMessages.ts:26-131 are per
+# cell, so sending every message of a cell to one rank (in global batch order)
+# keeps each cell's running max exact; the global __message PK case (one
+# timestamp in two cells) is checked on the rank a hash of the timestamp picks,
+# so every copy of one timestamp meets there; the tree is the XOR-combination
+# of the per-rank partial trees (insertIntoMerkleTree is order-independent).
+# ---------------------------------------------------------------------------
+EVM_OK, EVM_ECOLLISION = 0, 3
+
+
+def cell_dest(cell: torch.Tensor, world: int) -> torch.Tensor:
+    """Rank of each cell of a split owner (a fixed mix of the cell id)."""
+    c = cell.to(torch.int64) & 0xFFFFFFFF
+    return (((c * 0x9E3779B1) & 0xFFFFFFFF) >> 8) % world
+
+
+def split_apply(ts: torch.Tensor, cell: torch.Tensor, n_cells: int, apply_local, check_local, group=None):
+    """applyMessages of one owner's batch split over the ranks by cell.
+
+    ts (n, stride) uint8 / cell (n,) int: this rank's slice of the batch; the
+    batch is the ranks' slices in rank order.
+    apply_local(ts_r, cell_r) -> (flags u8[n_r], winner int[n_cells] index
+        into ts_r or -1, partial, status) -- evm_apply_batch from an empty
+        tree on this rank's cells (the partial tree is the caller's to merge,
+        `merge_partial_tree`);
+    check_local(ts_t, cell_t) -> bool: a timestamp with two cells
+        (evm_cross_cell_check).
+    Returns (flags u8[n] of this rank's slice, winner int64[n_cells] = global
+    batch index or -1, partial, status); status is the same on every rank
+    (EVM_ECOLLISION if any rank found a cross-cell timestamp)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = ts.device
+    n = ts.shape[0]
+    cell64 = cell.to(torch.int64)
+    # the global PK check, by timestamp hash
+    t_t, c_t, _, _ = route_by_owner(ts, cell64, group=group, dest=ts_route_hash(ts) % world)
+    collide = bool(check_local(t_t, c_t)) if t_t.shape[0] else False
+    # the LWW decisions, by cell
+    ts_c, cell_c, src_rank, src_idx = route_by_owner(ts, cell64, group=group, dest=cell_dest(cell64, world))
+    flags_c, win_c, part, st = apply_local(ts_c, cell_c)
+    status = torch.tensor([max(int(st), EVM_ECOLLISION if collide else EVM_OK)], dtype=torch.int64, device=dev)
+    dist.all_reduce(status, op=dist.ReduceOp.MAX, group=group)
+    status = int(status.item())
+    if status != EVM_OK:
+        return torch.zeros(n, dtype=torch.uint8, device=dev), None, None, status
+    flags = route_back(flags_c.to(torch.int64), src_rank, src_idx, n, group=group).to(torch.uint8)
+    # winners: local index -> global batch index (rank-major)
+    sizes = torch.tensor([n], dtype=torch.int64, device=dev)
+    alls = [torch.empty_like(sizes) for _ in range(world)]
+    dist.all_gather(alls, sizes, group=group)
+    base = torch.cumsum(torch.cat(alls), 0) - torch.cat(alls)
+    gidx = base.index_select(0, src_rank) + src_idx
+    w = win_c.to(torch.int64)
+    mine = cell_dest(torch.arange(n_cells, device=dev), world) == rank
+    glob = torch.where((w >= 0) & mine, gidx.index_select(0, w.clamp(min=0)) if gidx.numel() else w, torch.full_like(w, -1))
+    dist.all_reduce(glob, op=dist.ReduceOp.MAX, group=group)
+    return flags, glob, part, status
+
+
+def merge_partial_tree(eng, tree_in, part, group=None):
+    """The owner's new tree on every rank: its prior tree merged with every
+    rank's partial tree (leaf lists all-gathered, XOR-merged on the device by
+    evm_tree_merge)."""
+    import numpy as np
+
+    off, code, xr = part.leaves()
+    L = int(off[-1])
+    payload = np.concatenate([np.array([L], dtype=np.int64), code[:L].astype(np.int64), xr[:L].astype(np.int64)])
+    gloo = dist.get_backend(group) == "gloo"
+    dev = torch.device("cuda", eng.device) if (torch.cuda.is_available() and not gloo) else torch.device("cpu")
+    t = torch.from_numpy(payload).to(dev)
+    world = dist.get_world_size(group)
+    sizes = torch.tensor([t.numel()], dtype=torch.int64, device=dev)
+    alls = [torch.empty_like(sizes) for _ in range(world)]
+    dist.all_gather(alls, sizes, group=group)
+    cap = int(max(int(x.item()) for x in alls))
+    pad = torch.zeros(cap, dtype=torch.int64, device=dev)
+    pad[: t.numel()] = t
+    allt = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(allt, pad, group=group)
+    merged = tree_in
+    for r in range(world):
+        a = allt[r].cpu().numpy()
+        L = int(a[0])
+        p = eng.tree_from_leaves(np.array([0, L], dtype=np.uint64), a[1:1 + L].astype(np.uint64),
+                                 a[1 + L:1 + 2 * L].astype(np.int32))
+        merged = eng.tree_merge(merged, p)
+    return merged

@@ -201,6 +201,16 @@ class Engine:
         return flags, winner[:n_cells], (Trees(self, h) if st == _lib.EVM_OK else None), st
 
 
+    def cross_cell_check(self, ts: torch.Tensor, cell: torch.Tensor, n_cells: int) -> bool:
+        """True iff some timestamp of the batch occurs with two different cells
+        (the global __message PK case evm_apply_batch reports as EVM_ECOLLISION)."""
+        n, stride = ts.shape
+        found = C.c_int32(0)
+        check(self.lib.evm_cross_cell_check(self.h, _ptr(ts), stride, n, _ptr(cell), n_cells, C.byref(found)),
+              "evm_cross_cell_check")
+        return bool(found.value)
+
+
 class Store:
     """Server state: per-owner stored messages + MerkleTrees (index.ts tables)."""
 

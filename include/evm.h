@@ -165,6 +165,14 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
                     size_t prior_stride, const uint8_t* prior_present, uint8_t* flags, int32_t* winner,
                     evm_tree** tree_out);
 
+/* The global __message PK check evm_apply_batch runs (applyMessages.ts:42-45,
+ * 104-113: one timestamp in two cells of a batch), on its own: for a batch
+ * whose cells are split over ranks (evolu_amd/dist.py split_apply), each rank
+ * checks the messages routed to it by timestamp hash.  *found = 1 iff some
+ * timestamp occurs with two different cells.                               */
+int evm_cross_cell_check(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const uint32_t* cell,
+                         uint32_t n_cells, int32_t* found);
+
 /* ---- client: receive.ts:45-66 receiveMessages -----------------------------
  * Folds timestampFromString(m.timestamp) of every message of a batch into
  * the local clock with timestamp.ts:125-165 receiveTimestamp, `now` fixed
