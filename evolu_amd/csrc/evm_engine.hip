@@ -417,7 +417,7 @@ int evm::merge_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_own
 }
 
 // ============================================================================
-// Diff (merkleTree.ts:63-91), one thread per owner.
+// Diff (merkleTree.ts:63-91), a 16-lane group per owner.
 // ============================================================================
 struct TreeView {
   const u64* off;
@@ -427,55 +427,80 @@ struct TreeView {
 
 __device__ __forceinline__ int32_t range_hash(const TreeView& t, size_t lo, size_t hi) { return t.pfx[hi] ^ t.pfx[lo]; }
 
-__global__ void k_diff(TreeView A, TreeView B, u32 n_owners, int64_t* __restrict__ millis) {
-  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
-    size_t alo = A.off[o], ahi = A.off[o + 1], blo = B.off[o], bhi = B.off[o + 1];
+constexpr int DIFF_LANES = 16;
+
+// At each level the three children's leaf ranges in both trees are 8 lower
+// bounds (child starts 1..3 and the end of child 3, in A and in B): lanes
+// 0-3 / 4-7 of the group search them at once and fetch the prefix XOR at their
+// bound, so a level costs one binary search + one load of latency instead of
+// up to eight searches in a row.  The greedy choice (first child whose hash
+// differs, a missing child counting as different) is then made by every lane
+// of the group on the shuffled bounds.
+__global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owners, int64_t* __restrict__ millis) {
+  const int sub = threadIdx.x & (DIFF_LANES - 1);
+  const u32 groups = gridDim.x * (blockDim.x / DIFF_LANES);
+  for (u32 o = (blockIdx.x * blockDim.x + threadIdx.x) / DIFF_LANES; o < n_owners; o += groups) {
+    u64 alo = A.off[o], ahi = A.off[o + 1], blo = B.off[o], bhi = B.off[o + 1];
     // root: tree1.hash === tree2.hash (undefined for {})
     const bool ae = ahi > alo, be = bhi > blo;
     if (ae == be && (!ae || range_hash(A, alo, ahi) == range_hash(B, blo, bhi))) {
-      millis[o] = EVM_DIFF_NONE;
+      if (sub == 0) millis[o] = EVM_DIFF_NONE;
       continue;
     }
     u64 prefix = (u64)o << 40;
     int depth = 0;
     u64 kval = 0;  // base-3 value of the key string k so far
-    for (;;) {
-      int pick = -1;
-      size_t na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
-      if (depth < CODE_DIGITS) {
-        const int sh = 2 * (CODE_DIGITS - 1 - depth);
-        size_t ab = lower_bound_u64(A.ck, alo, ahi, prefix | (1ull << sh));
-        size_t bb = lower_bound_u64(B.ck, blo, bhi, prefix | (1ull << sh));
-        for (int c = 0; c < 3; ++c) {
-          const u64 end = prefix + ((u64)(c + 2) << sh);  // child c covers [prefix|(c+1)<<sh, prefix|(c+2)<<sh)
-          const size_t ae2 = lower_bound_u64(A.ck, ab, ahi, end);
-          const size_t be2 = lower_bound_u64(B.ck, bb, bhi, end);
-          const bool ea = ae2 > ab, eb = be2 > bb;
-          if (ea || eb) {
-            const bool differ = ea != eb || range_hash(A, ab, ae2) != range_hash(B, bb, be2);
-            if (differ) {
-              pick = c;
-              na0 = ab; na1 = ae2; nb0 = bb; nb1 = be2;
-              break;
-            }
-          }
-          ab = ae2;
-          bb = be2;
+    while (depth < CODE_DIGITS) {
+      const int sh = 2 * (CODE_DIGITS - 1 - depth);
+      // lane s < 4: A bound of prefix + (s+1) << sh; lane 4 <= s < 8: B bound of prefix + (s-3) << sh
+      u64 my = 0;
+      int32_t myx = 0;
+      if (sub < 8) {
+        const bool inA = sub < 4;
+        const u64* ck = inA ? A.ck : B.ck;
+        u64 lo = inA ? alo : blo, hi = inA ? ahi : bhi;
+        const u64 x = prefix + ((u64)((sub & 3) + 1) << sh);
+        while (lo < hi) {
+          const u64 mid = (lo + hi) >> 1;
+          if (ck[mid] < x) lo = mid + 1;
+          else hi = mid;
         }
+        my = lo;
+        myx = (inA ? A.pfx : B.pfx)[lo];
+      }
+      const int g0 = threadIdx.x & ~(DIFF_LANES - 1) & 63;
+      u64 a[4], b[4];
+      int32_t xa[4], xb[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k] = __shfl(my, g0 + k, 64);
+        b[k] = __shfl(my, g0 + 4 + k, 64);
+        xa[k] = __shfl(myx, g0 + k, 64);
+        xb[k] = __shfl(myx, g0 + 4 + k, 64);
+      }
+      int pick = -1;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const bool ea = a[c + 1] > a[c], eb = b[c + 1] > b[c];
+        if (pick < 0 && (ea || eb) && (ea != eb || (xa[c + 1] ^ xa[c]) != (xb[c + 1] ^ xb[c]))) pick = c;
       }
       if (pick < 0) break;
-      const int sh = 2 * (CODE_DIGITS - 1 - depth);
       prefix |= (u64)(pick + 1) << sh;
       kval = kval * 3 + (u64)pick;
       ++depth;
-      alo = na0; ahi = na1; blo = nb0; bhi = nb1;
+      alo = a[pick];
+      ahi = a[pick + 1];
+      blo = b[pick];
+      bhi = b[pick + 1];
     }
-    if (depth > 16) {
-      millis[o] = EVM_DIFF_RANGE_ERROR;  // "0".repeat(16 - k.length) throws (merkleTree.ts:58)
-    } else {
-      u64 v = kval;
-      for (int i = depth; i < 16; ++i) v *= 3;  // padEnd(16, "0")
-      millis[o] = (int64_t)(v * 60000ull);
+    if (sub == 0) {
+      if (depth > 16) {
+        millis[o] = EVM_DIFF_RANGE_ERROR;  // "0".repeat(16 - k.length) throws (merkleTree.ts:58)
+      } else {
+        u64 v = kval;
+        for (int i = depth; i < 16; ++i) v *= 3;  // padEnd(16, "0")
+        millis[o] = (int64_t)(v * 60000ull);
+      }
     }
   }
 }
@@ -810,7 +835,7 @@ int evm_merkle_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t*
 int evm::launch_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* millis) {
   if (a->n_owners == 0) return EVM_OK;
   TreeView A{a->off, a->ck, a->pfx}, B{b->off, b->ck, b->pfx};
-  KLAUNCH(k_diff, dim3(grid_for(a->n_owners, 64, 1 << 16)), dim3(64), A, B, a->n_owners, millis);
+  KLAUNCH(k_diff, dim3(grid_for((size_t)a->n_owners * DIFF_LANES, 256, 1 << 16)), dim3(256), A, B, a->n_owners, millis);
   return hip_ok(hipGetLastError());
 }
 
