@@ -154,12 +154,13 @@ struct CKey {
   u64 omin, mmin;
   int mb, cb;
 };
+// perm values: the batch index, or the caller's index orig[i] of a sub-batch
 __global__ void k_sv_ckey(const evm_rec* __restrict__ rec, size_t n, CKey ck, u64* __restrict__ key,
-                          u32* __restrict__ perm) {
+                          u32* __restrict__ perm, const u32* __restrict__ orig) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const evm_rec r = rec[i];
     key[i] = (((u64)r.aux - ck.omin) << (ck.mb + ck.cb)) | (((r.tc >> 16) - ck.mmin) << ck.cb) | (r.tc & 0xffffu);
-    perm[i] = (u32)i;
+    perm[i] = orig ? orig[i] : (u32)i;
   }
 }
 
@@ -199,17 +200,26 @@ __global__ void k_sv_ties(const u64* __restrict__ key, const evm_rec* __restrict
       continue;
     }
     const evm_rec r = srec[p];
-    u64 hp;
-    u32 lp;
-    node_ranks(r.node, r.meta & EVM_META_CASEMASK, &hp, &lp);
+    const u32 cp = r.meta & EVM_META_CASEMASK;
+    u64 hp = 0;
+    u32 lp = 0;
+    node_ranks(r.node, cp, &hp, &lp);
     u32 rank = 0;
     for (size_t q = s; q < e; ++q) {
       if (q == p) continue;
       const evm_rec x = srec[q];
-      u64 hq;
-      u32 lq;
-      node_ranks(x.node, x.meta & EVM_META_CASEMASK, &hq, &lq);
-      rank += (hq < hp || (hq == hp && (lq < lp || (lq == lp && q < p)))) ? 1u : 0u;
+      const u32 cq = x.meta & EVM_META_CASEMASK;
+      bool before;
+      if (!(cp | cq)) {
+        // no upper-case hex on either side: the ranks order like the hex values
+        before = x.node < r.node || (x.node == r.node && q < p);
+      } else {
+        u64 hq;
+        u32 lq;
+        node_ranks(x.node, cq, &hq, &lq);
+        before = hq < hp || (hq == hp && (lq < lp || (lq == lp && q < p)));
+      }
+      rank += before ? 1u : 0u;
     }
     src[s + rank] = (u32)p;
   }
@@ -1282,20 +1292,24 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       u64* kk = fv;
       u32* vv = perm;
       const CKey ck{hr.mn[F_OWNER], hr.mn[F_MS], mb, cb};
-      KLAUNCH(k_sv_ckey, dim3(grid_for(n, 256)), dim3(256), rec, n, ck, kk, vv);
+      // a sub-batch with the caller's packed records: the sort carries the
+      // caller's indices, so nothing below maps through orig again
+      const bool caller_idx = orig && prec;
+      KLAUNCH(k_sv_ckey, dim3(grid_for(n, 256)), dim3(256), rec, n, ck, kk, vv, caller_idx ? orig : (const u32*)nullptr);
       if ((st = radix_sort_pairs<u64>(ctx, S, kk, vv, n, 0, ob + mb + cb))) return st;
       u32* tl = S.alloc<u32>(1);
       srec = S.alloc<evm_rec>(n);
       src = S.alloc<u32>(n);
       if (!tl || !srec || !src) return EVM_ENOMEM;
       HIPR(hipMemsetAsync(tl, 0, sizeof(u32), ctx->stream));
-      KLAUNCH(k_sv_gather, dim3(grid_for(n, 256)), dim3(256), rec, vv, n, srec);
+      KLAUNCH(k_sv_gather, dim3(grid_for(n, 256)), dim3(256), caller_idx ? prec : rec, vv, n, srec);
       KLAUNCH(k_sv_ties, dim3(grid_for(n, 256)), dim3(256), kk, srec, n, src, tl);
       u32 too_long = 0;
       HIPR(hipMemcpyAsync(&too_long, tl, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
       HIPR(hipStreamSynchronize(ctx->stream));
       if (!too_long) {
         perm = vv;  // (scratch lives until the end of the call)
+        if (caller_idx) orig = nullptr;
         skeys = kk;  // sorted compound keys (scratch lives until the end of the call)
         sorted = true;
       }
