@@ -304,11 +304,14 @@ struct StoreOut {
   u64* id;
 };
 
+// Both sides are sorted by (owner, key) and carry per-owner offsets (b.off /
+// a.off): a row's merged position = its index + the other side's rows of
+// lower owners + a search inside the other side's segment of its owner.
 __global__ void k_sv_merge_old(StoreView a, const u64* __restrict__ a_id, size_t na, StoreView b, size_t nb,
                                StoreOut o) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += (size_t)gridDim.x * blockDim.x) {
     const SKey k = skey_at(a, i);
-    const size_t j = store_lower(b, 0, nb, k);
+    const size_t j = store_lower(b, b.off[k.owner], b.off[k.owner + 1], k);
     const size_t q = i + j;
     o.owner[q] = k.owner;
     o.tc[q] = k.tc;
@@ -322,7 +325,7 @@ __global__ void k_sv_merge_new(StoreView b, const u64* __restrict__ b_id, size_t
                                StoreOut o) {
   for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += (size_t)gridDim.x * blockDim.x) {
     const SKey k = skey_at(b, j);
-    const size_t i = store_lower(a, 0, na, k);  // keys are disjoint
+    const size_t i = store_lower(a, a.off[k.owner], a.off[k.owner + 1], k);  // keys are disjoint
     const size_t q = i + j;
     o.owner[q] = k.owner;
     o.tc[q] = k.tc;
@@ -330,6 +333,11 @@ __global__ void k_sv_merge_new(StoreView b, const u64* __restrict__ b_id, size_t
     o.lo[q] = k.lo;
     o.id[q] = b_id[j];
   }
+}
+
+__global__ void k_add_u64(const u64* __restrict__ a, const u64* __restrict__ b, size_t n, u64* __restrict__ out) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = a[i] + b[i];
 }
 
 __global__ void k_sv_owner_off(const u32* __restrict__ owner, size_t n, u32 n_owners, u64* __restrict__ off) {
@@ -1359,7 +1367,11 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     if (m > 1) KLAUNCH(k_sv_sorted_check, dim3(grid_for(m, 256)), dim3(256), l_ck, (size_t)m, cnt + 1);
     // merged store
     if ((st = store_alloc(ctx, &ns, s->n_owners, s->n + m))) return st;
-    const StoreView nv{nullptr, n_owner, n_tc, n_hi, n_lo};
+    u64* noff = S.alloc<u64>((size_t)s->n_owners + 1);  // the new rows' owner offsets
+    if (!noff) return EVM_ENOMEM;
+    KLAUNCH(k_sv_owner_off, dim3(grid_for(s->n_owners + 1, 256)), dim3(256), (const u32*)n_owner, (size_t)m,
+            s->n_owners, noff);
+    const StoreView nv{noff, n_owner, n_tc, n_hi, n_lo};
     const StoreOut so{ns.owner, ns.tc, ns.hi, ns.lo, ns.id};
     if (s->n)
       KLAUNCH(k_sv_merge_old, dim3(grid_for(s->n, 256)), dim3(256), old, (const u64*)s->id, (size_t)s->n, nv, (size_t)m,
@@ -1367,8 +1379,8 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     if (m)
       KLAUNCH(k_sv_merge_new, dim3(grid_for(m, 256)), dim3(256), nv, (const u64*)n_id, (size_t)m, old, (size_t)s->n,
               so);
-    KLAUNCH(k_sv_owner_off, dim3(grid_for(s->n_owners + 1, 256)), dim3(256), ns.owner, (size_t)ns.n, s->n_owners,
-            ns.off);
+    KLAUNCH(k_add_u64, dim3(grid_for(s->n_owners + 1, 256)), dim3(256), (const u64*)s->off, (const u64*)noff,
+            (size_t)s->n_owners + 1, ns.off);
     // Merkle: XOR of the inserted rows into their owners' trees
     u32 unsorted = 0;
     HIPR(hipMemcpyAsync(&unsorted, cnt + 1, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
