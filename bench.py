@@ -214,6 +214,24 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
     prof_dom = eng.prof_report()
+    # host-to-host (never `value`): the batch in pinned host memory, H2D of
+    # timestamps + cells, the step, D2H of flags + winners -- what a caller
+    # that hands over host buffers (the N-API addon) sees
+    ts_h = torch.from_numpy(ts_np).pin_memory()
+    cell_h = torch.from_numpy(np.ascontiguousarray(cell_np).view(np.int32)).pin_memory()
+    flags_h = torch.empty(a.messages, dtype=torch.uint8).pin_memory()
+    win_h = torch.empty(a.cells, dtype=torch.int32).pin_memory()
+    reps = max(1, min(a.steps, 5))
+    torch.cuda.synchronize()
+    h0 = time.perf_counter()
+    for _ in range(reps):
+        ts.copy_(ts_h, non_blocking=True)
+        cell.view(torch.int32).copy_(cell_h, non_blocking=True)
+        step().free()
+        flags_h.copy_(flags, non_blocking=True)
+        win_h.copy_(winner, non_blocking=True)
+    torch.cuda.synchronize()
+    ms_h2h = (time.perf_counter() - h0) / reps * 1e3
 
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
@@ -249,7 +267,8 @@ def main():
                        % (a.messages, a.cells), "messages_per_gpu": a.messages, "cells": a.cells,
                        "parallelism": "owner-sharded, %d rank(s)" % world},
             "roofline": roof,
-            "pipeline": {"alg_bytes_per_msg": 120, "ms_per_step_all_kernel_events": ms_all_events, "pipeline_hbm_frac": 120 * a.messages * world / (elapsed / a.steps) / world / HBM_PEAK,
+            "pipeline": {"alg_bytes_per_msg": 120, "ms_per_step_all_kernel_events": ms_all_events,
+                         "host_to_host_ms_per_step": ms_h2h, "host_to_host_msgs_per_s": a.messages / ms_h2h * 1e3, "pipeline_hbm_frac": 120 * a.messages * world / (elapsed / a.steps) / world / HBM_PEAK,
                          "kernels_ms_per_step": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}},
             "cpu_baseline": None,
         }

@@ -512,8 +512,9 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   __shared__ u64 s_k[CAP];   // sort keys; later: minute / hash of the inserted rows
   __shared__ u64 s_rh[CAP];  // by position: node ranks 0..11; later: per-leaf XOR / minute
   __shared__ u32 s_rl[CAP];  //              node ranks 12..15
-  __shared__ u32 s_bi[CAP];  //              batch index
   __shared__ u32 s_h[CAP];   //              hash
+  // (the batch index of position t is perm[a + t], re-read from L2 in the
+  // dedup phase: without it the 1,024 kernel's LDS fits five workgroups per CU)
   __shared__ u32 s_cnt[CAP];  // counting sort: bucket counts, then starts
   __shared__ u64 s_red[2 * (SVO_THREADS / 64)];
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
@@ -553,7 +554,6 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
       node_ranks(r.node, r.meta & EVM_META_CASEMASK, &hi, &lo);
       s_rh[t] = hi;
       s_rl[t] = lo;
-      s_bi[t] = bi[k];
       s_h[t] = r.hash;
       tc[k] = r.tc;
       tmin = min(tmin, r.tc);
@@ -697,7 +697,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
       mt[r] = tmin + (kp >> PB);
       mh[r] = s_rh[pos];
       ml[r] = s_rl[pos];
-      mb[r] = s_bi[pos];
+      mb[r] = perm[a + pos];
       mhash[r] = s_h[pos];
       bool ins = true;
       if (p > 0) {
