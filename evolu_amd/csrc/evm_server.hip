@@ -403,27 +403,6 @@ __global__ __launch_bounds__(256) void k_run_fill(const u32* __restrict__ run_po
 }
 
 // --------------------------------------------- sub-batches (hybrid ingest)
-// Pack of a sub-batch: message k is the caller's message orig[k].
-__global__ void k_sv_pack_sel(const uint8_t* __restrict__ ts, size_t stride, const u32* __restrict__ owner,
-                              const u32* __restrict__ orig, size_t n, evm_rec* __restrict__ out,
-                              u32* __restrict__ owner_out) {
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    const u32 i = orig[k];
-    u32 w[12];
-    load_ts(ts, stride, i, w);
-    const Parsed p = parse_ts46(w);
-    evm_rec r;
-    r.tc = p.tc;
-    r.node = p.node;
-    r.meta = p.meta;
-    r.hash = p.hash;
-    r.minute = p.minute;
-    r.aux = owner[i];
-    out[k] = r;
-    owner_out[k] = r.aux;
-  }
-}
-
 // messages whose owner's share exceeds the LDS capacity
 __global__ void k_big_mask(const evm_rec* __restrict__ rec, size_t n, const u64* __restrict__ seg, u64 cap,
                            uint8_t* __restrict__ mask) {
@@ -1195,13 +1174,6 @@ int evm_store_messages(evm_ctx* ctx, const evm_store* s, uint64_t* owner_off, ui
 
 }  // extern "C"
 
-// One ingest over the caller's batch, or over the sub-batch orig[0..n) of it
-// (message k = the caller's message orig[k]; flags and ids refer to the
-// caller's indices; prec, when given, holds the caller's packed records).
-// mode 0: per-owner LDS path; when only some owners are too big for it, the
-// rest commit and the big owners' messages then go through the sort path --
-// owners are independent, so the result is the one of a single ingest;
-// mode 1: LDS path, else the sort path; mode 2: the sort path.
 // Swap in the new store arrays and tree.
 static int commit_store(evm_ctx* ctx, evm_store* s, evm_store& ns, evm_tree* new_tree) {
   store_release_arrays(ctx, s);
@@ -1217,8 +1189,16 @@ static int commit_store(evm_ctx* ctx, evm_store* s, evm_store& ns, evm_tree* new
   return evm_sync(ctx);
 }
 
+// One ingest over the caller's batch, or over the sub-batch orig[0..n) of it
+// (message k = the caller's message orig[k], its packed record prec[orig[k]];
+// flags and ids refer to the caller's indices).
+// mode 0: per-owner LDS path; when only some owners are too big for it, the
+// rest commit and the big owners' messages then go through the sort path --
+// owners are independent, so the result is the one of a single ingest;
+// mode 2: the sort path.
 static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
                        const u32* orig, const evm_rec* prec, uint64_t id_base, uint8_t* flags, int mode) {
+  if (orig && !prec) return EVM_EINVAL;
   int st;
   evm_store ns{};
   evm_tree* new_tree = nullptr;
@@ -1235,11 +1215,8 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     if (orig) {
       u32* own_sub = S.alloc<u32>(n);
       if (!own_sub) return EVM_ENOMEM;
-      if (prec)  // the caller's records, already packed and checked
-        KLAUNCH(k_sv_rec_sel, dim3(grid_for(n, 256, 8192)), dim3(256), prec, orig, n, rec, own_sub);
-      else
-        KLAUNCH(k_sv_pack_sel, dim3(grid_for(n, 256, 4096)), dim3(256), (const uint8_t*)ts, stride, owner, orig, n,
-                rec, own_sub);
+      // the caller's records, already packed and checked
+      KLAUNCH(k_sv_rec_sel, dim3(grid_for(n, 256, 8192)), dim3(256), prec, orig, n, rec, own_sub);
       own = own_sub;
     } else if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) {
       return st;
