@@ -169,6 +169,13 @@ __global__ void k_sel_u32(const uint8_t* __restrict__ flags, uint8_t mask, size_
     sel[i] = (flags[i] & mask) ? 1u : 0u;
 }
 
+__global__ void k_info_set(Info* __restrict__ d, Info h) { *d = h; }
+
+int evm::launch_info_set(evm_ctx* ctx, Info* d, const Info& h) {
+  hipLaunchKernelGGL(k_info_set, dim3(1), dim3(1), 0, ctx->stream, d, h);
+  return hip_ok(hipGetLastError());
+}
+
 int evm::launch_iota(evm_ctx* ctx, u32* v, size_t n) {
   KLAUNCH(k_iota, dim3(grid_for(n, 256)), dim3(256), v, n);
   return hip_ok(hipGetLastError());
@@ -284,19 +291,22 @@ static int tree_alloc(evm_ctx* ctx, evm_tree* t, u32 n_owners, uint64_t L) {
   t->ck = nullptr;
   t->xr = nullptr;
   t->pfx = nullptr;
-  if (hipMallocAsync((void**)&t->off, sizeof(u64) * (n_owners + 1), ctx->stream) != hipSuccess) return EVM_ENOMEM;
-  if (hipMallocAsync((void**)&t->ck, sizeof(u64) * std::max<uint64_t>(L, 1), ctx->stream) != hipSuccess) return EVM_ENOMEM;
-  if (hipMallocAsync((void**)&t->xr, sizeof(int32_t) * std::max<uint64_t>(L, 1), ctx->stream) != hipSuccess) return EVM_ENOMEM;
-  if (hipMallocAsync((void**)&t->pfx, sizeof(int32_t) * (L + 1), ctx->stream) != hipSuccess) return EVM_ENOMEM;
+  // one stream-ordered allocation per tree (the arrays 256-B aligned inside it)
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_off = up(sizeof(u64) * (n_owners + 1)), b_ck = up(sizeof(u64) * std::max<uint64_t>(L, 1)),
+               b_xr = up(sizeof(int32_t) * std::max<uint64_t>(L, 1)), b_pfx = up(sizeof(int32_t) * (L + 1));
+  char* base = nullptr;
+  if (hipMallocAsync((void**)&base, b_off + b_ck + b_xr + b_pfx, ctx->stream) != hipSuccess) return EVM_ENOMEM;
+  t->off = reinterpret_cast<unsigned long long*>(base);
+  t->ck = reinterpret_cast<unsigned long long*>(base + b_off);
+  t->xr = reinterpret_cast<int32_t*>(base + b_off + b_ck);
+  t->pfx = reinterpret_cast<int32_t*>(base + b_off + b_ck + b_xr);
   return EVM_OK;
 }
 
 static void tree_release(evm_ctx* ctx, evm_tree* t) {
   if (!t) return;
-  if (t->off) (void)hipFreeAsync(t->off, ctx->stream);
-  if (t->ck) (void)hipFreeAsync(t->ck, ctx->stream);
-  if (t->xr) (void)hipFreeAsync(t->xr, ctx->stream);
-  if (t->pfx) (void)hipFreeAsync(t->pfx, ctx->stream);
+  if (t->off) (void)hipFreeAsync(t->off, ctx->stream);  // the base of the tree's one allocation
   delete t;
 }
 
@@ -553,6 +563,9 @@ int evm_create(int device, evm_ctx** out) {
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
     c->overlap = 0;
+  // pinned landing buffer for the per-call status record (a pageable D2H
+  // copy would stage through a bounce buffer on every call)
+  if (hipHostMalloc((void**)&c->hinfo, sizeof(Info), hipHostMallocDefault) != hipSuccess) c->hinfo = nullptr;
   // keep freed scratch in the stream-ordered pool between calls
   hipMemPool_t pool;
   if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
@@ -574,6 +587,7 @@ void evm_destroy(evm_ctx* ctx) {
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->own);
+  if (ctx->hinfo) (void)hipHostFree(ctx->hinfo);
   delete ctx;
 }
 

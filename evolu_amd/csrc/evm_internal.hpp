@@ -10,12 +10,17 @@
 
 #include "../../include/evm.h"
 
+namespace evm {
+struct Info;
+}
+
 struct evm_ctx {
   int device;
   hipStream_t own;
   hipStream_t stream;
   // kernel timing (evm_prof_*): HIP event pairs per kernel name, on `stream`
   bool prof = false;
+  evm::Info* hinfo = nullptr;  // pinned host copy of a call's status record (read_info)
   std::string prof_only;  // evm_prof_only: time just this kernel ("" = all)
   int client_path = 0;  // EVM_OPT_CLIENT_PATH
   int server_path = 0;  // EVM_OPT_SERVER_PATH
@@ -231,16 +236,22 @@ inline int ceil_log2(size_t x) {
 }
 
 inline int read_info(evm_ctx* ctx, const Info* dev, Info* host) {
-  HIPR(hipMemcpyAsync(host, dev, sizeof(Info), hipMemcpyDeviceToHost, ctx->stream));
+  Info* land = ctx->hinfo ? ctx->hinfo : host;  // pinned when the context has it
+  HIPR(hipMemcpyAsync(land, dev, sizeof(Info), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
+  if (land != host) *host = *land;
   return EVM_OK;
 }
+
+// the initial record is written by a one-thread kernel (launch argument), not
+// copied from pageable host memory
+int launch_info_set(evm_ctx* ctx, Info* d, const Info& h);
 
 inline int new_info(evm_ctx* ctx, Scratch& S, Info** out) {
   Info* d = S.alloc<Info>(1);
   if (!d) return EVM_ENOMEM;
-  Info h = info_init();
-  HIPR(hipMemcpyAsync(d, &h, sizeof(Info), hipMemcpyHostToDevice, ctx->stream));
+  int st = launch_info_set(ctx, d, info_init());
+  if (st) return st;
   *out = d;
   return EVM_OK;
 }
