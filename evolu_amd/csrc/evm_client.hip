@@ -1099,6 +1099,12 @@ static int apply_general(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* t
   return fold_into_tree(ctx, S, tree_in, tree_in->n_owners, ck, h, m, hi, tree_out);
 }
 
+__global__ void k_apply_init(Info* __restrict__ info, Info h, int32_t* __restrict__ winner, size_t n_cells) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *info = h;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_cells; i += (size_t)gridDim.x * blockDim.x)
+    winner[i] = -1;
+}
+
 extern "C" {
 
 int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n, const uint32_t* cell,
@@ -1112,16 +1118,17 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
   int st;
   {
     Scratch S(ctx);
-    Info* info = nullptr;
-    if ((st = new_info(ctx, S, &info))) return st;
+    Info* info = S.alloc<Info>(1);
     evm_rec* prior = S.alloc<evm_rec>(std::max<size_t>(n_cells, 1));
-    if (!prior) return EVM_ENOMEM;
+    if (!info || !prior) return EVM_ENOMEM;
+    // one launch: the status record, and winner = -1 for every cell
+    KLAUNCH(k_apply_init, dim3(grid_for(std::max<size_t>(n_cells, 1), 256)), dim3(256), info, info_init(), winner,
+            (size_t)n_cells);
     if (prior_present && n_cells) {
       // the cells' current maxima (SELECT ... ORDER BY timestamp DESC LIMIT 1)
       if ((st = launch_pack(ctx, prior_ts, prior_stride, n_cells, nullptr, 0, prior, nullptr))) return st;
       KLAUNCH(k_prior_check, dim3((n_cells + 255) / 256), dim3(256), prior, prior_present, n_cells, info);
     }
-    if (n_cells) KLAUNCH(k_fill_i32, dim3(grid_for(n_cells, 256)), dim3(256), winner, (size_t)n_cells, -1);
     if (n == 0) {
       Info hi;
       if ((st = read_info(ctx, info, &hi))) return st;
