@@ -34,6 +34,7 @@ MSG_BAD = 0x80
 OPT_CLIENT_PATH = 1
 OPT_SERVER_PATH = 2
 OPT_OVERLAP = 3
+OPT_RADIX = 4
 
 PB_SYNC_REQUEST = 1
 PB_SYNC_RESPONSE = 2

@@ -106,9 +106,38 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
   const u32 ntiles = (u32)((n + SORT_TILE - 1) / SORT_TILE);
   K* k2 = S.alloc<K>(n);
   u32* v2 = S.alloc<u32>(n);
+  if (!k2 || !v2) return EVM_ENOMEM;
+  if (ctx->radix_onesweep && passes <= RADIX_MAX_PASSES) {
+    // one read for every pass's digit histogram, then one launch per pass
+    u64* status = S.alloc<u64>((size_t)RADIX_BINS * ntiles);
+    u32* small = S.alloc<u32>((size_t)RADIX_MAX_PASSES * RADIX_BINS + RADIX_MAX_PASSES + 1);
+    if (!status || !small) return EVM_ENOMEM;
+    u32* gh = small;
+    u32* ctr = small + RADIX_MAX_PASSES * RADIX_BINS;
+    u32* err = ctr + RADIX_MAX_PASSES;
+    HIPR(hipMemsetAsync(small, 0, sizeof(u32) * ((size_t)RADIX_MAX_PASSES * RADIX_BINS + RADIX_MAX_PASSES + 1),
+                        ctx->stream));
+    HIPR(hipMemsetAsync(status, 0, sizeof(u64) * RADIX_BINS * ntiles, ctx->stream));
+    KLAUNCH((k_radix_ghist<K>), dim3(std::min<u32>(ntiles, 2048)), dim3(SORT_THREADS), keys, n, lo_bit, width, hi_bit,
+            passes, gh);
+    KLAUNCH(k_radix_gscan, dim3(1), dim3(SORT_THREADS), gh, passes);
+    int shift = lo_bit;
+    for (int p = 0; p < passes; ++p) {
+      const int bits = std::min(width, hi_bit - shift);
+      KLAUNCH((k_radix_onesweep<K>), dim3(ntiles), dim3(SORT_THREADS), keys, vals, k2, v2, n, shift, bits,
+              gh + (size_t)p * RADIX_BINS, status, ctr + p, p, err);
+      std::swap(keys, k2);
+      std::swap(vals, v2);
+      shift += bits;
+    }
+    u32 h_err = 0;
+    HIPR(hipMemcpyAsync(&h_err, err, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    return h_err ? EVM_EDEVICE : hip_ok(hipGetLastError());
+  }
   u32* counts = S.alloc<u32>((size_t)RADIX_BINS * ntiles);
   u32* offs = S.alloc<u32>((size_t)RADIX_BINS * ntiles);
-  if (!k2 || !v2 || !counts || !offs) return EVM_ENOMEM;
+  if (!counts || !offs) return EVM_ENOMEM;
   int shift = lo_bit;
   for (int p = 0; p < passes; ++p) {
     const int bits = std::min(width, hi_bit - shift);
@@ -612,6 +641,10 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
   }
   if (option == EVM_OPT_OVERLAP && (value == 0 || value == 1)) {
     ctx->overlap = (int)value;
+    return EVM_OK;
+  }
+  if (option == EVM_OPT_RADIX && (value == 0 || value == 1)) {
+    ctx->radix_onesweep = (int)value;
     return EVM_OK;
   }
   if (option == EVM_OPT_SERVER_PATH && value >= 0 && value <= 2) {

@@ -25,6 +25,7 @@ struct evm_ctx {
   int client_path = 0;  // EVM_OPT_CLIENT_PATH
   int server_path = 0;  // EVM_OPT_SERVER_PATH
   int overlap = 1;      // EVM_OPT_OVERLAP: independent checks on a second stream
+  int radix_onesweep = 1;  // EVM_OPT_RADIX: 1 one-sweep radix passes (look-back), 0 histogram + scan + scatter
   hipStream_t side = nullptr;  // second stream (forked from / joined to `stream` inside a call)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> prof_events;

@@ -344,4 +344,171 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(const K* __restr
   }
 }
 
+// ----------------------------------------------------------------------------
+// One-sweep variant: the digit histograms of every pass come from ONE read of
+// the keys (k_radix_ghist), and each pass is ONE launch whose tiles find their
+// per-digit offsets by decoupled look-back over the tiles before them (tile
+// ids are taken in launch order from a counter, so every tile a tile waits
+// for is already running).  Status word per (tile, digit): flag:2 | pass+1:4
+// | count:58; AGG = this tile's count, PRE = inclusive prefix through this
+// tile; a word tagged with another pass is not ready, so one clear serves
+// every pass of a sort.  A wait that exceeds RADIX_SPIN_MAX polls sets *err
+// and gives up (the host then fails the call) instead of hanging.
+// ----------------------------------------------------------------------------
+constexpr u64 RS_AGG = 1ull << 62, RS_PRE = 2ull << 62, RS_VAL = (1ull << 58) - 1;
+constexpr int RS_TAG_SHIFT = 58;
+constexpr u32 RADIX_SPIN_MAX = 1u << 24;
+constexpr int RADIX_MAX_PASSES = 8;
+
+template <typename K>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_ghist(const K* __restrict__ keys, size_t n, int lo_bit,
+                                                              int width, int hi_bit, int passes,
+                                                              u32* __restrict__ ghist) {
+  __shared__ u32 h[RADIX_MAX_PASSES][RADIX_BINS];
+  for (int i = threadIdx.x; i < RADIX_MAX_PASSES * RADIX_BINS; i += SORT_THREADS) (&h[0][0])[i] = 0;
+  __syncthreads();
+  for (size_t i = (size_t)blockIdx.x * SORT_THREADS + threadIdx.x; i < n; i += (size_t)gridDim.x * SORT_THREADS) {
+    const K k = keys[i];
+    int shift = lo_bit;
+    for (int p = 0; p < passes; ++p) {
+      const int bits = min(width, hi_bit - shift);
+      atomicAdd(&h[p][digit_of(k, shift, (1u << bits) - 1u)], 1u);
+      shift += bits;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < passes * RADIX_BINS; i += SORT_THREADS) {
+    const u32 v = (&h[0][0])[i];
+    if (v) atomicAdd(&ghist[i], v);
+  }
+}
+
+// exclusive scan of each pass's digit counts (one workgroup, digit per thread)
+static __global__ __launch_bounds__(SORT_THREADS) void k_radix_gscan(u32* __restrict__ ghist, int passes) {
+  __shared__ u32 scan_tmp[SORT_THREADS / WAVE + 1];
+  for (int p = 0; p < passes; ++p) {
+    const u32 v = ghist[p * RADIX_BINS + threadIdx.x];
+    const u32 incl = block_inclusive_scan<u32>(v, scan_tmp, OpAdd<u32>(), (u32*)nullptr);
+    ghist[p * RADIX_BINS + threadIdx.x] = incl - v;
+    __syncthreads();
+  }
+}
+
+template <typename K>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_onesweep(const K* __restrict__ kin, const u32* __restrict__ vin,
+                                                                 K* __restrict__ kout, u32* __restrict__ vout, size_t n,
+                                                                 int shift, int bits, const u32* __restrict__ goff,
+                                                                 u64* __restrict__ status, u32* __restrict__ tile_ctr,
+                                                                 int pass, u32* __restrict__ err) {
+  const u64 tag = (u64)(pass + 1) << RS_TAG_SHIFT, tag_mask = 15ull << RS_TAG_SHIFT;
+  __shared__ u32 wcnt[SORT_THREADS / WAVE][RADIX_BINS];
+  __shared__ u32 toff[RADIX_BINS];
+  __shared__ u32 lstart[RADIX_BINS];
+  __shared__ u32 scan_tmp[SORT_THREADS / WAVE + 1];
+  __shared__ u32 tile_s;
+  __shared__ K skey[SORT_TILE];
+  __shared__ u32 sval[SORT_TILE];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const u32 nbins = 1u << bits, mask = nbins - 1u;
+  if (threadIdx.x == 0) tile_s = atomicAdd(tile_ctr, 1u);
+  for (u32 d = threadIdx.x; d < nbins; d += SORT_THREADS) {
+#pragma unroll
+    for (int ww = 0; ww < SORT_THREADS / WAVE; ++ww) wcnt[ww][d] = 0;
+  }
+  __syncthreads();
+  const u32 tile = tile_s;
+  const size_t tbase = (size_t)tile * SORT_TILE;
+  const size_t wbase = tbase + (size_t)w * WAVE * SORT_ITEMS;
+  K key[SORT_ITEMS];
+  u32 val[SORT_ITEMS], dig[SORT_ITEMS], rank[SORT_ITEMS];
+  const u64 lt = lanemask_lt();
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; ++r) {
+    const size_t i = wbase + (size_t)r * WAVE + lane;
+    const bool ok = i < n;
+    key[r] = ok ? kin[i] : K(0);
+    val[r] = ok ? vin[i] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; ++r) {
+    const size_t i = wbase + (size_t)r * WAVE + lane;
+    const bool ok = i < n;
+    const u32 d = digit_of(key[r], shift, mask);
+    dig[r] = d;
+    u64 peers = __ballot(ok);
+    for (int b = 0; b < bits; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const u64 bal = __ballot(bit);
+      peers &= bit ? bal : ~bal;
+    }
+    if (ok) {
+      const u32 pre = wcnt[w][d];
+      rank[r] = pre + (u32)__popcll(peers & lt);
+      if ((peers >> lane) == 1ull) wcnt[w][d] = pre + (u32)__popcll(peers);
+    }
+  }
+  __syncthreads();
+  u32 tot = 0;
+  const u32 d = threadIdx.x;
+  if (d < nbins) {
+#pragma unroll
+    for (int ww = 0; ww < SORT_THREADS / WAVE; ++ww) {
+      const u32 t = wcnt[ww][d];
+      wcnt[ww][d] = tot;
+      tot += t;
+    }
+    // publish this tile's count, then look back for the tiles before it
+    u64* my = status + (size_t)tile * RADIX_BINS + d;
+    u64 excl = 0;
+    if (tile == 0) {
+      __hip_atomic_store(my, RS_PRE | tag | (u64)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(my, RS_AGG | tag | (u64)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      u32 spins = 0;
+      for (int t = (int)tile - 1; t >= 0;) {
+        const u64 s = __hip_atomic_load(status + (size_t)t * RADIX_BINS + d, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+        const bool mine = (s & tag_mask) == tag;
+        if (mine && (s & RS_PRE)) {
+          excl += s & RS_VAL;
+          break;
+        }
+        if (mine && (s & RS_AGG)) {
+          excl += s & RS_VAL;
+          --t;
+          continue;
+        }
+        if (++spins > RADIX_SPIN_MAX) {
+          atomicOr(err, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __hip_atomic_store(my, RS_PRE | tag | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    toff[d] = goff[d] + (u32)excl;
+  }
+  const u32 incl = block_inclusive_scan<u32>(tot, scan_tmp, OpAdd<u32>(), (u32*)nullptr);
+  if (threadIdx.x < nbins) lstart[threadIdx.x] = incl - tot;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; ++r) {
+    const size_t i = wbase + (size_t)r * WAVE + lane;
+    if (i < n) {
+      const u32 lp = lstart[dig[r]] + wcnt[w][dig[r]] + rank[r];
+      skey[lp] = key[r];
+      sval[lp] = val[r];
+    }
+  }
+  __syncthreads();
+  const u32 m = (u32)min((size_t)SORT_TILE, n - tbase);
+  for (u32 t = threadIdx.x; t < m; t += SORT_THREADS) {
+    const K k = skey[t];
+    const u32 dd = digit_of(k, shift, mask);
+    const u32 dst = toff[dd] + (t - lstart[dd]);
+    kout[dst] = k;
+    vout[dst] = sval[t];
+  }
+}
+
 }  // namespace evm

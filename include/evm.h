@@ -91,6 +91,7 @@ int evm_sync(evm_ctx* ctx);
 #define EVM_OPT_CLIENT_PATH 1 /* evm_apply_batch: 0 auto, 1 force the streaming path, 2 force the sort path */
 #define EVM_OPT_OVERLAP 3     /* 1 (default): independent checks run on a second HIP stream inside a call; 0: one stream */
 #define EVM_OPT_SERVER_PATH 2 /* evm_server_ingest: 0/1 per-owner LDS path where every owner's share fits, 2 force the sort path */
+#define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 0 histogram + scan + scatter per pass */
 int evm_set_option(evm_ctx* ctx, int option, int64_t value);
 /* kernel timing with HIP events on the context stream (for roofline reports) */
 int evm_prof_enable(evm_ctx* ctx, int on);
