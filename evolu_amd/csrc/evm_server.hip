@@ -116,7 +116,9 @@ struct FieldRange {
   u64 mx[N_FIELDS];
 };
 
-__global__ void k_sv_ranges(const evm_rec* __restrict__ rec, size_t n, FieldRange* __restrict__ fr) {
+// (idx: message i's record is rec[idx[i]], else rec[i])
+__global__ void k_sv_ranges(const evm_rec* __restrict__ rec, const u32* __restrict__ idx, size_t n,
+                            FieldRange* __restrict__ fr) {
   u64 mn[N_FIELDS], mx[N_FIELDS];
 #pragma unroll
   for (int f = 0; f < N_FIELDS; ++f) {
@@ -124,7 +126,7 @@ __global__ void k_sv_ranges(const evm_rec* __restrict__ rec, size_t n, FieldRang
     mx[f] = 0;
   }
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const SKey k = skey_of(rec[i]);
+    const SKey k = skey_of(rec[idx ? idx[i] : i]);
 #pragma unroll
     for (int f = 0; f < N_FIELDS; ++f) {
       const u64 v = field_of(k, f);
@@ -155,10 +157,11 @@ struct CKey {
   int mb, cb;
 };
 // perm values: the batch index, or the caller's index orig[i] of a sub-batch
-__global__ void k_sv_ckey(const evm_rec* __restrict__ rec, size_t n, CKey ck, u64* __restrict__ key,
-                          u32* __restrict__ perm, const u32* __restrict__ orig) {
+// (idx: message i's record is rec[idx[i]], else rec[i])
+__global__ void k_sv_ckey(const evm_rec* __restrict__ rec, const u32* __restrict__ idx, size_t n, CKey ck,
+                          u64* __restrict__ key, u32* __restrict__ perm, const u32* __restrict__ orig) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const evm_rec r = rec[i];
+    const evm_rec r = rec[idx ? idx[i] : i];
     key[i] = (((u64)r.aux - ck.omin) << (ck.mb + ck.cb)) | (((r.tc >> 16) - ck.mmin) << ck.cb) | (r.tc & 0xffffu);
     perm[i] = orig ? orig[i] : (u32)i;
   }
@@ -1212,16 +1215,24 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     FieldRange* fr = S.alloc<FieldRange>(1);
     if (!rec || !perm || !fv || !fr) return EVM_ENOMEM;
     const u32* own = owner;
-    if (orig) {
-      u32* own_sub = S.alloc<u32>(n);
-      if (!own_sub) return EVM_ENOMEM;
-      // the caller's records, already packed and checked
-      KLAUNCH(k_sv_rec_sel, dim3(grid_for(n, 256, 8192)), dim3(256), prec, orig, n, rec, own_sub);
-      own = own_sub;
-    } else if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) {
-      return st;
+    // a sub-batch reads the caller's packed (and checked) records through
+    // orig; its own copy is made only for the paths that index it directly
+    bool have_rec = false;
+    u32* own_sub = orig ? S.alloc<u32>(n) : nullptr;
+    if (orig && !own_sub) return EVM_ENOMEM;
+    auto materialize = [&]() {
+      if (!have_rec) {
+        KLAUNCH(k_sv_rec_sel, dim3(grid_for(n, 256, 8192)), dim3(256), prec, orig, n, rec, own_sub);
+        own = own_sub;
+        have_rec = true;
+      }
+    };
+    if (!orig) {
+      if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) return st;
+      have_rec = true;
     }
     if (mode != 2 && s->n_owners > 0) {
+      materialize();
       bool done = false, big_only = false;
       uint8_t* bigmask = (mode == 0 && !orig) ? S.alloc<uint8_t>(n) : nullptr;
       if (mode == 0 && !orig && !bigmask) return EVM_ENOMEM;
@@ -1252,7 +1263,8 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       h0.mx[f] = 0;
     }
     HIPR(hipMemcpyAsync(fr, &h0, sizeof(h0), hipMemcpyHostToDevice, ctx->stream));
-    KLAUNCH(k_sv_ranges, dim3(grid_for(n, 256, 2048)), dim3(256), rec, n, fr);
+    KLAUNCH(k_sv_ranges, dim3(grid_for(n, 256, 2048)), dim3(256), have_rec ? rec : prec, have_rec ? nullptr : orig, n,
+            fr);
     Info hi;
     FieldRange hr;
     HIPR(hipMemcpyAsync(&hr, fr, sizeof(hr), hipMemcpyDeviceToHost, ctx->stream));
@@ -1280,7 +1292,8 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       // a sub-batch with the caller's packed records: the sort carries the
       // caller's indices, so nothing below maps through orig again
       const bool caller_idx = orig && prec;
-      KLAUNCH(k_sv_ckey, dim3(grid_for(n, 256)), dim3(256), rec, n, ck, kk, vv, caller_idx ? orig : (const u32*)nullptr);
+      KLAUNCH(k_sv_ckey, dim3(grid_for(n, 256)), dim3(256), have_rec ? rec : prec, have_rec ? nullptr : orig, n, ck, kk,
+              vv, caller_idx ? orig : (const u32*)nullptr);
       if ((st = radix_sort_pairs<u64>(ctx, S, kk, vv, n, 0, ob + mb + cb))) return st;
       u32* tl = S.alloc<u32>(1);
       srec = S.alloc<evm_rec>(n);
@@ -1301,6 +1314,7 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     }
     if (!sorted) {
       // stable LSD sort of the batch index by (owner, tc, rank_hi, rank_lo), field by field
+      materialize();
       if ((st = launch_iota(ctx, perm, n))) return st;
       const int order[4] = {F_LO, F_HI, F_TC, F_OWNER};
       for (int f : order) {

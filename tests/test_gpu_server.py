@@ -303,3 +303,47 @@ def test_owner_lds_path_bursts_vs_oracle(eng):
         want_rows += [r[0] for r in db.conn.execute(
             'SELECT "timestamp" FROM "message" WHERE "userId" = ? ORDER BY "timestamp"', (o,)).fetchall()]
     assert got[0][1] == want_rows
+
+
+@pytest.mark.parametrize("run", [40, 100])
+def test_big_owner_tie_runs(eng, run):
+    """An owner above the LDS capacity (its messages go through the sort path
+    as a sub-batch after the other owners commit) whose batch holds a run of
+    `run` equal (millis, counter) timestamps with distinct mixed-case nodes:
+    a run above the tie ranking's limit takes the full-field sort over the
+    sub-batch.  Flags, row order and trees against the C restatement."""
+    from evolu_amd import _lib as L
+    from oracle import c_oracle as CO
+
+    rng = random.Random(900 + run)
+    strings, owner = [], []
+    nodes = [W.node_id(rng, upper=rng.random() < 0.3) for _ in range(6)]
+    big = W.hlc_timestamps(rng, 5000, nodes, span=600_000)
+    tie = [O.timestamp_to_string(W.T0 + 123_456, 7, W.node_id(rng, upper=rng.random() < 0.5)) for _ in range(run)]
+    mine = big + tie + tie[:5]  # redeliveries inside the batch
+    rng.shuffle(mine)
+    strings += mine
+    owner += [0] * len(mine)
+    for o in (1, 2):
+        small = W.hlc_timestamps(rng, 300, [W.node_id(rng) for _ in range(3)])
+        strings += small
+        owner += [o] * len(small)
+    perm = list(range(len(strings)))
+    rng.shuffle(perm)
+    strings = [strings[i] for i in perm]
+    owner = np.array([owner[i] for i in perm], dtype=np.uint32)
+    ts_np = eng.timestamps(strings).cpu().numpy()
+    srv = CO.Server(3, len(strings))
+    st, want = srv.ingest(ts_np, owner)
+    assert st == 0
+    store = eng.store_new(3)
+    got, st = store.ingest(eng.dev(ts_np), eng.dev(owner), 0)
+    assert st == 0
+    assert np.array_equal(got.cpu().numpy(), want)
+    off, ids = store.messages()
+    for o in range(3):
+        rows = sorted({s for s, w in zip(strings, owner) if w == o})
+        assert [strings[int(k)] for k in ids[off[o]:off[o + 1]]] == rows
+        assert store.tree().to_json(o) == srv.tree_json(o)
+    assert ((got.cpu().numpy() & L.MSG_INS) != 0).sum() == sum(len({s for s, w in zip(strings, owner) if w == o})
+                                                         for o in range(3))
