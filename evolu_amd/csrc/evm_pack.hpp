@@ -89,10 +89,28 @@ __global__ __launch_bounds__(CLP_THREADS) void k_cl_pack(const uint8_t* __restri
     const bool valid = (p.meta & EVM_META_VALID) != 0;
     if (i < n) {
       key[i] = make_uint4((u32)p.tc, (u32)(p.tc >> 32), (u32)p.rh, (u32)(p.rh >> 32));
+      bad |= valid ? 0u : 1u;
+    }
+    if (S48 && first + 64 <= n && (first & 3) == 0) {
+      // rl / hash / minute of the wave's 64 rows: staged in LDS and written
+      // as one 16-B-per-lane store (48 lanes) instead of three 4-B stores
+      u32* st32 = reinterpret_cast<u32*>(&stage[wv][0]);
+      st32[lane] = p.rl | (valid ? OKEY_PRESENT : 0u);
+      st32[64 + lane] = p.hash;
+      st32[128 + lane] = p.minute;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (lane < 48) {
+        const uint4 v = stage[wv][lane];
+        u32* dst = lane < 16 ? rl : lane < 32 ? hash : minute;
+        reinterpret_cast<uint4*>(dst + first)[lane & 15] = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    } else if (i < n) {
       rl[i] = p.rl | (valid ? OKEY_PRESENT : 0u);
       hash[i] = p.hash;
       minute[i] = p.minute;
-      bad |= valid ? 0u : 1u;
     }
     mn = min(mn, valid ? p.minute : 0xffffffffu);
     mx = max(mx, valid ? p.minute : 0u);
