@@ -28,9 +28,14 @@ __device__ __forceinline__ void clp_fetch(const uint8_t* __restrict__ ts, size_t
   if (S48) {
     const uint4* src = reinterpret_cast<const uint4*>(ts + first * 48);
     if (first + 64 <= n) {
-      a = src[lane];
-      b = src[lane + 64];
-      c = src[lane + 128];
+      // read once: non-temporal
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const v4u* s4 = reinterpret_cast<const v4u*>(src);
+      const v4u x = __builtin_nontemporal_load(s4 + lane), y = __builtin_nontemporal_load(s4 + lane + 64),
+                z = __builtin_nontemporal_load(s4 + lane + 128);
+      a = make_uint4(x.x, x.y, x.z, x.w);
+      b = make_uint4(y.x, y.y, y.z, y.w);
+      c = make_uint4(z.x, z.y, z.z, z.w);
     } else {
       const size_t nq = first < n ? (n - first) * 3 : 0;
       a = (size_t)lane < nq ? src[lane] : z;
@@ -88,7 +93,9 @@ __global__ __launch_bounds__(CLP_THREADS) void k_cl_pack(const uint8_t* __restri
     const Parsed p = parse_ts46(w);  // lanes past n parse zeros; only their stores are masked
     const bool valid = (p.meta & EVM_META_VALID) != 0;
     if (i < n) {
-      key[i] = make_uint4((u32)p.tc, (u32)(p.tc >> 32), (u32)p.rh, (u32)(p.rh >> 32));
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const v4u kv = {(u32)p.tc, (u32)(p.tc >> 32), (u32)p.rh, (u32)(p.rh >> 32)};
+      __builtin_nontemporal_store(kv, reinterpret_cast<v4u*>(key) + i);
       bad |= valid ? 0u : 1u;
     }
     if (S48 && first + 64 <= n && (first & 3) == 0) {
@@ -100,7 +107,7 @@ __global__ __launch_bounds__(CLP_THREADS) void k_cl_pack(const uint8_t* __restri
       st32[128 + lane] = p.minute;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (lane < 48) {
+      if (lane < 48) {  // (a non-temporal store here measured slower: 150 vs 139 us)
         const uint4 v = stage[wv][lane];
         u32* dst = lane < 16 ? rl : lane < 32 ? hash : minute;
         reinterpret_cast<uint4*>(dst + first)[lane & 15] = v;
