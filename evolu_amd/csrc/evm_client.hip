@@ -249,9 +249,12 @@ __device__ __forceinline__ ClRaw cl_fetch(const uint4* __restrict__ key, const u
   const size_t i = first + (threadIdx.x & 63);
   ClRaw r;
   if (i < end) {
-    r.key = key[i];
-    r.rl = rl[i];
-    r.cell = cell[i];
+    // non-temporal: shorter issue-to-land latency for the latency-bound walks
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u k = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(key) + i);
+    r.key = make_uint4(k.x, k.y, k.z, k.w);
+    r.rl = __builtin_nontemporal_load(rl + i);
+    r.cell = __builtin_nontemporal_load(cell + i);
   } else {
     r.key = make_uint4(0, 0, 0, 0);
     r.rl = 0;
@@ -616,7 +619,7 @@ __global__ __launch_bounds__(XP_THREADS) void k_xp_scatter(const u32* __restrict
 #pragma unroll
   for (int k = 0; k < XP_ITEMS; ++k) {
     const size_t i = base + (size_t)k * XP_THREADS + threadIdx.x;
-    h[k] = i < n ? hash[i] : 0u;
+    h[k] = i < n ? __builtin_nontemporal_load(hash + i) : 0u;
     r[k] = i < n ? atomicAdd(&cnt[kb ? h[k] >> sh : 0u], 1u) : 0u;
   }
   __syncthreads();
@@ -740,9 +743,10 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __
   // 4 messages per thread per step: one 32-bit load of flags
   for (size_t i = a + 4 * (size_t)threadIdx.x; i < e; i += 4 * FOLD_THREADS) {
     if (i + 4 <= e) {
-      const u32 f4 = *reinterpret_cast<const u32*>(flags + i);
-      const uint4 m4 = *reinterpret_cast<const uint4*>(minute + i);
-      const uint4 h4 = *reinterpret_cast<const uint4*>(hash + i);
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const u32 f4 = __builtin_nontemporal_load(reinterpret_cast<const u32*>(flags + i));
+      const v4u m4 = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(minute + i));
+      const v4u h4 = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(hash + i));
       const u32 mm[4] = {m4.x, m4.y, m4.z, m4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
