@@ -18,6 +18,7 @@
 
 #include "evm_device.hpp"
 #include "evm_internal.hpp"
+#include "evm_pack.hpp"
 #include "evm_prims.hpp"
 
 using namespace evm;
@@ -68,11 +69,72 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack(const uint8_t* __restrict
   }
 }
 
+// The same for 16-B aligned 48-byte rows: a wave reads its 64 rows as three
+// coalesced (non-temporal) 16-B loads per lane and redistributes them through
+// LDS, as the client path's K1 does (evm_pack.hpp).
+__global__ __launch_bounds__(PACK_THREADS) void k_pack48(const uint8_t* __restrict__ ts, size_t n,
+                                                         const u32* __restrict__ aux, u32 aux_limit,
+                                                         evm_rec* __restrict__ out, Info* __restrict__ info) {
+  __shared__ uint4 stage[PACK_THREADS / 64][192];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u32 bad = 0, bad_aux = 0, mn = 0xffffffffu, mx = 0u;
+  const size_t step = (size_t)gridDim.x * PACK_THREADS;
+  for (size_t first = ((size_t)blockIdx.x * (PACK_THREADS / 64) + wv) * 64; first < n; first += step) {
+    uint4 a, b, c;
+    clp_fetch<true>(ts, 48, n, first, a, b, c);
+    stage[wv][lane] = a;
+    stage[wv][lane + 64] = b;
+    stage[wv][lane + 128] = c;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const uint4 x = stage[wv][3 * lane], y = stage[wv][3 * lane + 1], z = stage[wv][3 * lane + 2];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    u32 w[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w & 0xffffu};
+    const size_t i = first + lane;
+    if (i >= n) continue;
+    const Parsed p = parse_ts46(w);
+    evm_rec r;
+    r.tc = p.tc;
+    r.node = p.node;
+    r.meta = p.meta;
+    r.hash = p.hash;
+    r.minute = p.minute;
+    r.aux = aux ? aux[i] : 0u;
+    if (aux_limit && r.aux >= aux_limit) bad_aux = 1;
+    out[i] = r;
+    if (p.meta & EVM_META_VALID) {
+      mn = min(mn, p.minute);
+      mx = max(mx, p.minute);
+    } else {
+      bad = 1;
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    bad |= __shfl_xor(bad, d, 64);
+    bad_aux |= __shfl_xor(bad_aux, d, 64);
+    mn = min(mn, (u32)__shfl_xor(mn, d, 64));
+    mx = max(mx, (u32)__shfl_xor(mx, d, 64));
+  }
+  if ((threadIdx.x & 63) == 0 && info) {
+    if (bad) atomic_or_if(&info->bad, 1u);
+    if (bad_aux) atomic_or_if(&info->bad_aux, 1u);
+    if (mn != 0xffffffffu) {
+      atomic_min_if(&info->minute_min, mn);
+      atomic_max_if(&info->minute_max, mx);
+    }
+  }
+}
+
 int evm::launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,
                      Info* info) {
   if (n == 0) return EVM_OK;
-  KLAUNCH(k_pack, dim3(grid_for(n, PACK_THREADS, 4096)), dim3(PACK_THREADS),
-                     (const uint8_t*)ts, stride, n, aux, aux_limit, out, info);
+  if (stride == 48 && ((uintptr_t)ts & 15) == 0)
+    KLAUNCH(k_pack48, dim3(grid_for(n, PACK_THREADS, 2048)), dim3(PACK_THREADS), (const uint8_t*)ts, n, aux,
+            aux_limit, out, info);
+  else
+    KLAUNCH(k_pack, dim3(grid_for(n, PACK_THREADS, 4096)), dim3(PACK_THREADS), (const uint8_t*)ts, stride, n, aux,
+            aux_limit, out, info);
   return hip_ok(hipGetLastError());
 }
 
