@@ -76,6 +76,21 @@ __device__ __forceinline__ SKey skey_of(const evm_rec& r) {
   return k;
 }
 
+// A record read once (non-temporal: shorter issue-to-land latency).
+__device__ __forceinline__ evm_rec load_rec_nt(const evm_rec* p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u* q = reinterpret_cast<const v4u*>(p);
+  const v4u a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
+  evm_rec r;
+  r.tc = (u64)a.x | ((u64)a.y << 32);
+  r.node = (u64)a.z | ((u64)a.w << 32);
+  r.meta = b.x;
+  r.hash = b.y;
+  r.minute = b.z;
+  r.aux = b.w;
+  return r;
+}
+
 struct StoreView {
   const u64* off;
   const u32* owner;
@@ -174,7 +189,7 @@ constexpr int TIE_MAX = 64;
 __global__ void k_sv_gather(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, size_t n,
                             evm_rec* __restrict__ srec) {
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
-    srec[p] = rec[perm[p]];
+    srec[p] = rec[perm[p]];  // (a non-temporal gather measured slower here: 3.1 vs 2.8 ms)
 }
 
 __device__ __forceinline__ bool same_node(const evm_rec& a, const evm_rec& b) {
@@ -530,7 +545,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   for (int k = 0; k < PER; ++k) {
     const u32 t = threadIdx.x + k * SVO_THREADS;
     if (t < m) {
-      const evm_rec r = rec[bi[k]];
+      const evm_rec r = load_rec_nt(rec + bi[k]);
       u64 hi;
       u32 lo;
       node_ranks(r.node, r.meta & EVM_META_CASEMASK, &hi, &lo);
