@@ -379,7 +379,7 @@ __device__ __forceinline__ void cl_commit2(const ClMsg& m, const ClPeer& p, cons
 //   PASS 1: per-cell (max key, first index) of the range -> agg_*
 //   PASS 2: state = the carried maxima (agg_*) -> flags
 constexpr int WK_THREADS = 256;
-constexpr int WK_PF = 3;  // groups in flight per wave
+constexpr int WK_PF = 4;  // groups in flight per wave
 
 template <int PASS>
 __device__ __forceinline__ void cl_walk(const uint4* __restrict__ key, const u32* __restrict__ rl,
