@@ -998,19 +998,23 @@ int store_alloc(evm_ctx* ctx, evm_store* s, u32 n_owners, uint64_t n) {
   s->n_owners = n_owners;
   s->n = n;
   const size_t m = std::max<uint64_t>(n, 1);
-  HIPR(hipMallocAsync((void**)&s->off, sizeof(u64) * (n_owners + 1), ctx->stream));
-  HIPR(hipMallocAsync((void**)&s->owner, sizeof(u32) * m, ctx->stream));
-  HIPR(hipMallocAsync((void**)&s->tc, sizeof(u64) * m, ctx->stream));
-  HIPR(hipMallocAsync((void**)&s->hi, sizeof(u64) * m, ctx->stream));
-  HIPR(hipMallocAsync((void**)&s->lo, sizeof(u32) * m, ctx->stream));
-  HIPR(hipMallocAsync((void**)&s->id, sizeof(u64) * m, ctx->stream));
+  // one stream-ordered allocation per store (arrays 256-B aligned inside it;
+  // s->off is its base)
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_off = up(sizeof(u64) * (n_owners + 1)), b4 = up(sizeof(u32) * m), b8 = up(sizeof(u64) * m);
+  char* base = nullptr;
+  HIPR(hipMallocAsync((void**)&base, b_off + 2 * b4 + 3 * b8, ctx->stream));
+  s->off = reinterpret_cast<unsigned long long*>(base);
+  s->owner = reinterpret_cast<u32*>(base + b_off);
+  s->lo = reinterpret_cast<u32*>(base + b_off + b4);
+  s->tc = reinterpret_cast<unsigned long long*>(base + b_off + 2 * b4);
+  s->hi = reinterpret_cast<unsigned long long*>(base + b_off + 2 * b4 + b8);
+  s->id = reinterpret_cast<unsigned long long*>(base + b_off + 2 * b4 + 2 * b8);
   return EVM_OK;
 }
 
 void store_release_arrays(evm_ctx* ctx, evm_store* s) {
-  void* ps[] = {s->off, s->owner, s->tc, s->hi, s->lo, s->id};
-  for (void* p : ps)
-    if (p) (void)hipFreeAsync(p, ctx->stream);
+  if (s->off) (void)hipFreeAsync(s->off, ctx->stream);  // the base of the store's one allocation
   s->off = nullptr;
   s->owner = nullptr;
   s->tc = s->hi = s->id = nullptr;
