@@ -916,9 +916,6 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
       hipLaunchKernelGGL(k_cl_pack<false>, g, dim3(CLP_THREADS), 0, ctx->stream, (const uint8_t*)ts, stride, n, key,
                          rl, hash, minute, info);
   }
-  // pass 1: per range and cell, the max timestamp and its first index
-  KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
-              a_first, info);
   // cross-cell PK check: partition by hash into fixed-capacity buckets, LDS set per bucket
   int kb = 0;
   while (kb < XP_MAX_KB && (n >> kb) > XP_AVG) ++kb;
@@ -928,8 +925,9 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
   u32* xcur = S.alloc<u32>((size_t)1 << kb);
   u64* xpairs = S.alloc<u64>(((size_t)cap) << kb);
   if (!xcur || !xpairs) return EVM_ENOMEM;
-  // it reads only the timestamps, cells and hashes: a second stream runs it
-  // beside the walks (joined before the status read)
+  // it reads only the timestamps, cells and K1's hashes: a second stream runs
+  // it beside the walks, forked right after K1 (joined before the status
+  // read; forked after pass 1 instead: 0.502-0.506 vs 0.497 ms per config-2 step)
   SideFork side(ctx);
   {
     const hipStream_t xs = side.stream();
@@ -944,6 +942,9 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
                          (const uint8_t*)ts, stride, cell, info);
     }
   }
+  // pass 1: per range and cell, the max timestamp and its first index
+  KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
+              a_first, info);
   // carry: per cell, exclusive scan over ranges seeded with the prior max
   {
     u64* s_tc = S.alloc<u64>((size_t)CARRY_SEGS * C);
