@@ -371,18 +371,50 @@ __global__ void k_sv_owner_off(const u32* __restrict__ owner, size_t n, u32 n_ow
 }
 
 // ------------------------------------------------ owner runs (requests)
-__global__ void k_run_heads(const u32* __restrict__ owner, size_t n, u32* __restrict__ head) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    head[i] = (i == 0 || owner[i] != owner[i - 1]) ? 1u : 0u;
+// Run heads (owner[i] != owner[i-1]) compacted in two reads of the owner
+// column: a wave owns a tile of RUN_TILE messages, counts its heads
+// (k_run_count), and after a scan of the tile counts writes each head at
+// its rank (k_run_emit).  (Was: a u32 head flag per message and a scan over
+// n -- 32 B/msg of traffic instead of 8.)
+constexpr int RUN_ITEMS = 64;
+constexpr size_t RUN_TILE = 64 * RUN_ITEMS;
+constexpr int RUN_THREADS = 256;
+
+__device__ __forceinline__ bool run_head(const u32* __restrict__ owner, size_t n, size_t i) {
+  return i < n && (i == 0 || owner[i] != owner[i - 1]);
 }
 
-__global__ void k_run_emit(const u32* __restrict__ owner, const u32* __restrict__ head, const u32* __restrict__ rid,
-                           size_t n, u32* __restrict__ run_start, u32* __restrict__ run_owner) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    if (head[i]) {
-      run_start[rid[i]] = (u32)i;
-      run_owner[rid[i]] = owner[i];
+__global__ __launch_bounds__(RUN_THREADS) void k_run_count(const u32* __restrict__ owner, size_t n,
+                                                           u32* __restrict__ tcnt) {
+  const size_t t = (size_t)blockIdx.x * (RUN_THREADS / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const size_t base = t * RUN_TILE;
+  if (base >= n) return;  // uniform per wave
+  u32 c = 0;
+  for (int it = 0; it < RUN_ITEMS; ++it) c += (u32)__popcll(__ballot(run_head(owner, n, base + (size_t)it * 64 + lane)));
+  if (lane == 0) tcnt[t] = c;
+}
+
+__global__ __launch_bounds__(RUN_THREADS) void k_run_emit(const u32* __restrict__ owner, size_t n,
+                                                          const u32* __restrict__ toff, u32* __restrict__ run_start,
+                                                          u32* __restrict__ run_owner) {
+  const size_t t = (size_t)blockIdx.x * (RUN_THREADS / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const size_t base = t * RUN_TILE;
+  if (base >= n) return;
+  const u64 lt = lanemask_lt();
+  u32 r = toff[t];
+  for (int it = 0; it < RUN_ITEMS; ++it) {
+    const size_t i = base + (size_t)it * 64 + lane;
+    const bool h = run_head(owner, n, i);
+    const u64 bal = __ballot(h);
+    if (h) {
+      const u32 k = r + (u32)__popcll(bal & lt);
+      run_start[k] = (u32)i;
+      run_owner[k] = owner[i];
     }
+    r += (u32)__popcll(bal);
+  }
 }
 
 // lengths of the runs in (owner, batch) order
@@ -1052,12 +1084,14 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   const int obits = O > 1 ? 32 - __builtin_clz(O - 1) : 0;
   // requests arrive as runs of one owner (index.ts:224-248): sort the runs,
   // not the messages, when they are long enough
-  u32* head = S.alloc<u32>(n);
-  u32* rid = S.alloc<u32>(n);
+  const size_t n_rt = (n + RUN_TILE - 1) / RUN_TILE;
+  const dim3 rgrid((unsigned)((n_rt + RUN_THREADS / 64 - 1) / (RUN_THREADS / 64)));
+  u32* tcnt = S.alloc<u32>(n_rt);
+  u32* toff = S.alloc<u32>(n_rt);
   u32* nrun = S.alloc<u32>(1);
-  if (!head || !rid || !nrun) return EVM_ENOMEM;
-  KLAUNCH(k_run_heads, dim3(grid_for(n, 256)), dim3(256), owner, n, head);
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, head, n, rid, nrun))) return st;
+  if (!tcnt || !toff || !nrun) return EVM_ENOMEM;
+  KLAUNCH(k_run_count, rgrid, dim3(RUN_THREADS), owner, n, tcnt);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, tcnt, n_rt, toff, nrun))) return st;
   u32 R = 0;
   HIPR(hipMemcpyAsync(&R, nrun, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
@@ -1069,7 +1103,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     u32* len = S.alloc<u32>(R);
     u32* run_pos = S.alloc<u32>((size_t)R + 1);
     if (!run_start || !run_owner || !order || !len || !run_pos) return EVM_ENOMEM;
-    KLAUNCH(k_run_emit, dim3(grid_for(n, 256)), dim3(256), owner, head, rid, n, run_start, run_owner);
+    KLAUNCH(k_run_emit, rgrid, dim3(RUN_THREADS), owner, n, toff, run_start, run_owner);
     if ((st = launch_iota(ctx, order, R))) return st;
     u32* rk = run_owner;
     u32* rv = order;
