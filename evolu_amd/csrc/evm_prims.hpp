@@ -142,9 +142,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const T* __restric
   Op op;
   const size_t base = (size_t)blockIdx.x * SCAN_TILE;
   T acc = Op::id();
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const size_t i = base + (size_t)k * SCAN_THREADS + threadIdx.x;
-    if (i < n) acc = op(acc, in[i]);
+  if (base + SCAN_TILE <= n) {  // full tile: every load in flight at once
+    T v[SCAN_ITEMS];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) v[k] = in[base + (size_t)k * SCAN_THREADS + threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) acc = op(acc, v[k]);
+  } else {
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+      const size_t i = base + (size_t)k * SCAN_THREADS + threadIdx.x;
+      if (i < n) acc = op(acc, in[i]);
+    }
   }
   T tot;
   block_inclusive_scan<T, Op>(acc, lds, op, &tot);
@@ -193,10 +201,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_down(const T* __restrict_
   __shared__ T ex[SCAN_THREADS];
   Op op;
   const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+  const bool full = base + SCAN_TILE <= n;
+  if (full) {
+    T w[SCAN_ITEMS];
 #pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const u32 i = k * SCAN_THREADS + threadIdx.x;
-    tile[scan_pad(i)] = base + i < n ? in[base + i] : Op::id();
+    for (int k = 0; k < SCAN_ITEMS; ++k) w[k] = in[base + k * SCAN_THREADS + threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) tile[scan_pad(k * SCAN_THREADS + threadIdx.x)] = w[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+      const u32 i = k * SCAN_THREADS + threadIdx.x;
+      tile[scan_pad(i)] = base + i < n ? in[base + i] : Op::id();
+    }
   }
   __syncthreads();
   T v[SCAN_ITEMS];
@@ -216,10 +233,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_down(const T* __restrict_
     run = op(run, v[k]);
   }
   __syncthreads();
+  if (full) {
 #pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    const u32 i = k * SCAN_THREADS + threadIdx.x;
-    if (base + i < n) out[base + i] = tile[scan_pad(i)];
+    for (int k = 0; k < SCAN_ITEMS; ++k) out[base + k * SCAN_THREADS + threadIdx.x] = tile[scan_pad(k * SCAN_THREADS + threadIdx.x)];
+  } else {
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+      const u32 i = k * SCAN_THREADS + threadIdx.x;
+      if (base + i < n) out[base + i] = tile[scan_pad(i)];
+    }
   }
 }
 

@@ -391,7 +391,9 @@ __global__ __launch_bounds__(RUN_THREADS) void k_run_count(const u32* __restrict
   const size_t base = t * RUN_TILE;
   if (base >= n) return;  // uniform per wave
   u32 c = 0;
-  for (int it = 0; it < RUN_ITEMS; ++it) c += (u32)__popcll(__ballot(run_head(owner, n, base + (size_t)it * 64 + lane)));
+#pragma unroll 16
+  for (int it = 0; it < RUN_ITEMS; ++it)
+    c += (u32)__popcll(__ballot(run_head(owner, n, base + (size_t)it * 64 + lane)));
   if (lane == 0) tcnt[t] = c;
 }
 
@@ -404,6 +406,7 @@ __global__ __launch_bounds__(RUN_THREADS) void k_run_emit(const u32* __restrict_
   if (base >= n) return;
   const u64 lt = lanemask_lt();
   u32 r = toff[t];
+#pragma unroll 16
   for (int it = 0; it < RUN_ITEMS; ++it) {
     const size_t i = base + (size_t)it * 64 + lane;
     const bool h = run_head(owner, n, i);
