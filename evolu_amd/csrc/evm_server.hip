@@ -384,6 +384,26 @@ __device__ __forceinline__ bool run_head(const u32* __restrict__ owner, size_t n
   return i < n && (i == 0 || owner[i] != owner[i - 1]);
 }
 
+#ifndef EVM_RUN_VEC
+#define EVM_RUN_VEC 1
+#endif
+// Full tiles of a 16-B aligned column: a lane reads 4 consecutive owners per
+// step (a wave step = 1 KiB), the owner before its first one comes from the
+// lane below (lane 0: the previous step's last, or the owner before the tile).
+// Returns the lane's 4 head bits (bit j: message 4 * (step * 64 + lane) + j).
+__device__ __forceinline__ u32 run_heads4(const uint4 v, u32& carry, int lane) {
+  u32 prev = __shfl_up(v.w, 1, 64);
+  if (lane == 0) prev = carry;
+  carry = __shfl(v.w, 63, 64);
+  return (v.x != prev ? 1u : 0u) | (v.y != v.x ? 2u : 0u) | (v.z != v.y ? 4u : 0u) | (v.w != v.z ? 8u : 0u);
+}
+__device__ __forceinline__ bool run_vec_tile(const u32* __restrict__ owner, size_t n, size_t base) {
+  return EVM_RUN_VEC && base + RUN_TILE <= n && ((uintptr_t)owner & 15) == 0;
+}
+__device__ __forceinline__ u32 run_carry0(const u32* __restrict__ owner, size_t base) {
+  return base ? owner[base - 1] : ~owner[0];  // message 0 always starts a run
+}
+
 __global__ __launch_bounds__(RUN_THREADS) void k_run_count(const u32* __restrict__ owner, size_t n,
                                                            u32* __restrict__ tcnt) {
   const size_t t = (size_t)blockIdx.x * (RUN_THREADS / 64) + (threadIdx.x >> 6);
@@ -391,9 +411,21 @@ __global__ __launch_bounds__(RUN_THREADS) void k_run_count(const u32* __restrict
   const size_t base = t * RUN_TILE;
   if (base >= n) return;  // uniform per wave
   u32 c = 0;
+  if (run_vec_tile(owner, n, base)) {
+    const uint4* o4 = reinterpret_cast<const uint4*>(owner + base);
+    u32 carry = run_carry0(owner, base);
+    uint4 v[RUN_TILE / 256];
+#pragma unroll
+    for (int s = 0; s < (int)(RUN_TILE / 256); ++s) v[s] = o4[s * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < (int)(RUN_TILE / 256); ++s) c += (u32)__popc(run_heads4(v[s], carry, lane));
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  } else {
 #pragma unroll 16
-  for (int it = 0; it < RUN_ITEMS; ++it)
-    c += (u32)__popcll(__ballot(run_head(owner, n, base + (size_t)it * 64 + lane)));
+    for (int it = 0; it < RUN_ITEMS; ++it)
+      c += (u32)__popcll(__ballot(run_head(owner, n, base + (size_t)it * 64 + lane)));
+  }
   if (lane == 0) tcnt[t] = c;
 }
 
@@ -406,6 +438,31 @@ __global__ __launch_bounds__(RUN_THREADS) void k_run_emit(const u32* __restrict_
   if (base >= n) return;
   const u64 lt = lanemask_lt();
   u32 r = toff[t];
+  if (run_vec_tile(owner, n, base)) {
+    const uint4* o4 = reinterpret_cast<const uint4*>(owner + base);
+    u32 carry = run_carry0(owner, base);
+    uint4 v[RUN_TILE / 256];
+#pragma unroll
+    for (int s = 0; s < (int)(RUN_TILE / 256); ++s) v[s] = o4[s * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < (int)(RUN_TILE / 256); ++s) {
+      const u32 hm = run_heads4(v[s], carry, lane);
+      const u32 c = (u32)__popc(hm);  // 0..4: its wave prefix from three ballots
+      const u64 b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
+      u32 k = r + (u32)__popcll(b0 & lt) + 2u * (u32)__popcll(b1 & lt) + 4u * (u32)__popcll(b2 & lt);
+      const u32 i0 = (u32)(base + ((size_t)s * 64 + lane) * 4);
+      const u32 ov[4] = {v[s].x, v[s].y, v[s].z, v[s].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (hm & (1u << j)) {
+          run_start[k] = i0 + j;
+          run_owner[k] = ov[j];
+          ++k;
+        }
+      r += (u32)__popcll(b0) + 2u * (u32)__popcll(b1) + 4u * (u32)__popcll(b2);
+    }
+    return;
+  }
 #pragma unroll 16
   for (int it = 0; it < RUN_ITEMS; ++it) {
     const size_t i = base + (size_t)it * 64 + lane;
