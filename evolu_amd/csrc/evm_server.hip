@@ -500,15 +500,36 @@ __global__ void k_run_seg(const u32* __restrict__ run_owner_sorted, u32 R, const
   }
 }
 
-// perm over owner-major positions: one wave per run writes the run's batch
-// indices (consecutive lanes, consecutive addresses)
+// perm over owner-major positions.  Runs j0 .. j0+RF_RUNS-1 (in owner order)
+// fill one contiguous range of perm, so a wave takes RF_RUNS of them: lanes
+// fetch one run's (position, start) each, then the wave writes the whole
+// range coalesced, each element finding its run among the RF_RUNS bounds.
+constexpr int RF_RUNS = 8;
 __global__ __launch_bounds__(256) void k_run_fill(const u32* __restrict__ run_pos, const u32* __restrict__ run_start,
                                                   const u32* __restrict__ order, u32 R, u32* __restrict__ perm) {
   const u32 lane = threadIdx.x & 63;
   const size_t waves = (size_t)gridDim.x * 4;
-  for (size_t j = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < R; j += waves) {
-    const u32 p = run_pos[j], L = run_pos[j + 1] - p, s = run_start[order[j]];
-    for (u32 q = lane; q < L; q += 64) perm[p + q] = s + q;
+  for (size_t j0 = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RF_RUNS; j0 < R; j0 += waves * RF_RUNS) {
+    u32 p = 0, st = 0;
+    if (lane <= (u32)RF_RUNS) {
+      const size_t j = min(j0 + lane, (size_t)R);  // past the last run: its end
+      p = run_pos[j];
+      if (lane < (u32)RF_RUNS && j < R) st = run_start[order[j]];
+    }
+    u32 pr[RF_RUNS], sr[RF_RUNS];
+#pragma unroll
+    for (int r = 0; r < RF_RUNS; ++r) {
+      pr[r] = __shfl(p, r, 64);
+      sr[r] = __shfl(st, r, 64);
+    }
+    const u32 end = __shfl(p, RF_RUNS, 64);
+    for (u32 q = pr[0] + lane; q < end; q += 64) {
+      u32 v = sr[0] + (q - pr[0]);
+#pragma unroll
+      for (int r = 1; r < RF_RUNS; ++r)
+        if (q >= pr[r]) v = sr[r] + (q - pr[r]);
+      perm[q] = v;
+    }
   }
 }
 
@@ -1171,7 +1192,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     KLAUNCH(k_run_len, dim3(grid_for(R, 256)), dim3(256), run_start, rv, R, n, len);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, len, R, run_pos, run_pos + R))) return st;
     KLAUNCH(k_run_seg, dim3(grid_for((size_t)O + 1, 256)), dim3(256), rk, R, run_pos, O, seg);
-    KLAUNCH(k_run_fill, dim3(grid_for(R, 4, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
+    KLAUNCH(k_run_fill, dim3(grid_for(R, 4 * RF_RUNS, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
   } else {
     HIPR(hipMemcpyAsync(own, owner, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
     if ((st = launch_iota(ctx, perm, n))) return st;
