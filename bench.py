@@ -371,10 +371,14 @@ def server_main(a, rank, world, local):
     t0 = time.perf_counter()
     nsel = 0
     step_ms = []  # per-step wall time (a step ends in a host read-back of the roots, so this adds no sync)
+    step_allocs = []  # per-step growth of the engine's allocation counters (steady state: all zero)
     for _ in range(a.steps):
+        c0 = eng.stats()
         s0 = time.perf_counter()
         nsel = step()
         step_ms.append((time.perf_counter() - s0) * 1e3)
+        c1 = eng.stats()
+        step_allocs.append({k: c1[k] - c0[k] for k in ("workspace_regrows", "scratch_pool_allocs", "block_allocs")})
         if os.environ.get("EVM_BENCH_VERBOSE"):
             print("step %.2f ms" % step_ms[-1], file=sys.stderr, flush=True)
     torch.cuda.synchronize()
@@ -400,6 +404,7 @@ def server_main(a, rank, world, local):
                        "messages_per_gpu": n, "owners_per_gpu": a.owners,
                        "selected_rows_rank0": nsel, "parallelism": "owner-sharded, %d rank(s)" % world},
             "step_ms": [round(x, 3) for x in step_ms],
+            "step_allocs": step_allocs, "engine_stats": eng.stats(),
             "kernels_ms_per_step": {k: v[0] / a.steps for k, v in top},
         }), flush=True)
     if world > 1:

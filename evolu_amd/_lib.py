@@ -35,6 +35,7 @@ OPT_CLIENT_PATH = 1
 OPT_SERVER_PATH = 2
 OPT_OVERLAP = 3
 OPT_RADIX = 4
+OPT_TEST_FAIL = 5
 
 PB_SYNC_REQUEST = 1
 PB_SYNC_RESPONSE = 2
@@ -55,6 +56,8 @@ SIGNATURES = {
     "evm_destroy": (None, [_vp]),
     "evm_strerror": (C.c_char_p, [_i]),
     "evm_set_stream": (_i, [_vp, _vp]),
+    "evm_bind_thread": (_i, [_vp]),
+    "evm_get_stats": (_i, [_vp, _vp]),
     "evm_get_stream": (_vp, [_vp]),
     "evm_sync": (_i, [_vp]),
     "evm_set_option": (_i, [_vp, _i, C.c_int64]),
@@ -71,6 +74,8 @@ SIGNATURES = {
     "evm_tree_new": (_i, [_vp, _u32, C.POINTER(_vp)]),
     "evm_tree_from_leaves": (_i, [_vp, _u32, _vp, _vp, _vp, C.POINTER(_vp)]),
     "evm_tree_free": (_i, [_vp, _vp]),
+    "evm_tree_from_device_leaves": (_i, [_vp, _u32, _vp, _vp, _vp, C.POINTER(_vp)]),
+    "evm_tree_slice": (_i, [_vp, _vp, _u32, _u32, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_tree_info": (_i, [_vp, C.POINTER(_u32), C.POINTER(C.c_uint64)]),
     "evm_tree_device": (_i, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)]),
     "evm_tree_leaves": (_i, [_vp, _vp, _vp, _vp, _vp]),
@@ -92,9 +97,14 @@ SIGNATURES = {
     "evm_pb_encode": (_i, [_i, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _sz, C.POINTER(_sz)]),
     "evm_store_since": (_i, [_vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_server_select": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "evm_store_select_after": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_apply_batch": (
         _i,
         [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _vp, C.POINTER(_vp)],
+    ),
+    "evm_apply_batch_ex": (
+        _i,
+        [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _sz, _sz, _vp, _vp, _vp, C.POINTER(_vp)],
     ),
 }
 

@@ -585,6 +585,84 @@ __global__ void k_cl_xcell(const uint8_t* __restrict__ ts, size_t stride, const 
   }
 }
 
+// Rows already in __message (applyMessages.ts:42-45 PRIMARY KEY "timestamp"):
+// the caller hands over the stored rows whose timestamp is in the batch
+// (SELECT "timestamp", "table", "row", "column" FROM "__message" WHERE
+// "timestamp" IN (...)).  A batch message whose timestamp is stored under
+// another cell would have its INSERT ignored (:107-113) and its cell's running
+// max frozen -- the sequential case the engine reports as a collision.  The
+// stored rows go into an open-addressing set (slot = hash:32 | (row + 1):32);
+// every batch message probes it with K1's hash, equal hashes compare the raw
+// bytes.  Stored timestamps are unique (the PK), so one match ends a probe.
+__global__ void k_st_insert(const evm_rec* __restrict__ srec, size_t m, u64* __restrict__ table, u32 lg) {
+  const u64 mask = (1ull << lg) - 1;
+  for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (size_t)gridDim.x * blockDim.x) {
+    const evm_rec r = srec[j];
+    if (!(r.meta & EVM_META_VALID)) continue;  // not canonical: no canonical batch timestamp equals it
+    const u64 mine = ((u64)r.hash << 32) | (u64)(j + 1);
+    u64 pos = (u64)(r.hash * 2654435761u) & mask;
+    for (u64 probe = 0; probe <= mask; ++probe) {
+      if (atomicCAS(&table[pos], 0ull, mine) == 0ull) break;
+      pos = (pos + 1) & mask;
+    }
+  }
+}
+
+__global__ void k_st_probe(const u32* __restrict__ hash, size_t hstride, const uint8_t* __restrict__ ts, size_t stride,
+                           const u32* __restrict__ cell, size_t n, const uint8_t* __restrict__ sts, size_t sstride,
+                           const u32* __restrict__ scell, const u64* __restrict__ table, u32 lg,
+                           Info* __restrict__ info) {
+  const u64 mask = (1ull << lg) - 1;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const u32 h = hash[i * hstride];
+    u64 pos = (u64)(h * 2654435761u) & mask;
+    for (u64 probe = 0; probe <= mask; ++probe) {
+      const u64 s = table[pos];
+      if (s == 0) break;
+      if ((u32)(s >> 32) == h) {
+        const size_t j = (size_t)(s & 0xffffffffu) - 1;
+        u32 wa[12], wb[12];
+        load_ts(ts, stride, i, wa);
+        load_ts(sts, sstride, j, wb);
+        bool eq = true;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) eq &= wa[k] == wb[k];
+        if (eq) {
+          if (cell[i] != scell[j]) atomic_or_if(&info->collision, 1u);
+          break;
+        }
+      }
+      pos = (pos + 1) & mask;
+    }
+  }
+}
+
+// Stored rows of the batch's timestamps (see k_st_insert), checked on the
+// context stream.  hash: K1's hash of batch message i at hash[i * hstride].
+struct Stored {
+  const char* ts;
+  size_t stride;
+  size_t n;
+  const u32* cell;
+};
+
+static int stored_check(evm_ctx* ctx, Scratch& S, const Stored& st, const u32* hash, size_t hstride, const char* ts,
+                        size_t stride, const u32* cell, size_t n, Info* info) {
+  if (!st.n || !n) return EVM_OK;
+  const int lg = std::max(ceil_log2(2 * st.n), 6);
+  evm_rec* srec = S.alloc<evm_rec>(st.n);
+  u64* table = S.alloc<u64>((size_t)1 << lg);
+  if (!srec || !table) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(table, 0, sizeof(u64) << lg, ctx->stream));
+  int e;
+  // the stored strings' murmur3 (their validity only gates the set)
+  if ((e = launch_pack(ctx, st.ts, st.stride, st.n, nullptr, 0, srec, nullptr))) return e;
+  KLAUNCH(k_st_insert, dim3(grid_for(st.n, 256, 2048)), dim3(256), (const evm_rec*)srec, st.n, table, (u32)lg);
+  KLAUNCH(k_st_probe, dim3(grid_for(n, 256, 8192)), dim3(256), hash, hstride, (const uint8_t*)ts, stride, cell, n,
+          (const uint8_t*)st.ts, st.stride, st.cell, (const u64*)table, (u32)lg, info);
+  return EVM_OK;
+}
+
 // Partitioned cross-cell check (the default): messages are bucketed by the top
 // bits of their hash (one counting-sort pass), then every bucket is checked in
 // an LDS hash set.  Equal timestamps always share a bucket.  A bucket too big
@@ -890,7 +968,7 @@ __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* 
 // ============================================================================
 static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree_in, const char* ts, size_t stride,
                       size_t n, const u32* cell, u32 C, const evm_rec* prior, const uint8_t* prior_present,
-                      uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+                      const Stored& stored, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
   int st;
   size_t range = (n + CL_RANGE_TARGET - 1) / CL_RANGE_TARGET;
   range = std::max<size_t>(2048, (range + 255) / 256 * 256);
@@ -916,6 +994,8 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
       hipLaunchKernelGGL(k_cl_pack<false>, g, dim3(CLP_THREADS), 0, ctx->stream, (const uint8_t*)ts, stride, n, key,
                          rl, hash, minute, info);
   }
+  // batch timestamps already stored under another cell (global PK)
+  if ((st = stored_check(ctx, S, stored, hash, 1, ts, stride, cell, n, info))) return st;
   // cross-cell PK check: partition by hash into fixed-capacity buckets, LDS set per bucket
   int kb = 0;
   while (kb < XP_MAX_KB && (n >> kb) > XP_AVG) ++kb;
@@ -1050,7 +1130,8 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
 
 static int apply_general(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree_in, const char* ts, size_t stride,
                          size_t n, const u32* cell, u32 n_cells, const u32* cell_owner, const evm_rec* prior,
-                         const uint8_t* prior_present, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+                         const uint8_t* prior_present, const Stored& stored, uint8_t* flags, int32_t* winner,
+                         evm_tree** tree_out) {
   int st;
   evm_rec* rec = S.alloc<evm_rec>(n);
   if (!rec) return EVM_ENOMEM;
@@ -1061,6 +1142,8 @@ static int apply_general(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* t
   if (!table) return EVM_ENOMEM;
   HIPR(hipMemsetAsync(table, 0, sizeof(u64) << lg, ctx->stream));
   KLAUNCH(k_xcell, dim3(grid_for(n, 256, 8192)), dim3(256), rec, n, table, (u32)lg, info);
+  if ((st = stored_check(ctx, S, stored, &rec->hash, sizeof(evm_rec) / sizeof(u32), ts, stride, cell, n, info)))
+    return st;
   // (2) stable sort (cell, index)
   u32* cell_s = S.alloc<u32>(n);
   u32* idx_s = S.alloc<u32>(n);
@@ -1115,9 +1198,20 @@ extern "C" {
 int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n, const uint32_t* cell,
                     uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts, size_t prior_stride,
                     const uint8_t* prior_present, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+  return evm_apply_batch_ex(ctx, tree_in, ts, stride, n, cell, n_cells, cell_owner, prior_ts, prior_stride,
+                            prior_present, nullptr, 48, 0, nullptr, flags, winner, tree_out);
+}
+
+int evm_apply_batch_ex(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n,
+                       const uint32_t* cell, uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts,
+                       size_t prior_stride, const uint8_t* prior_present, const char* stored_ts, size_t stored_stride,
+                       size_t n_stored, const uint32_t* stored_cell, uint8_t* flags, int32_t* winner,
+                       evm_tree** tree_out) {
   if (!ctx || !tree_in || !tree_out || stride < 46 || (n && (!ts || !cell || !flags))) return EVM_EINVAL;
   if (n_cells && !winner) return EVM_EINVAL;
   if (prior_present && (!prior_ts || prior_stride < 46)) return EVM_EINVAL;
+  if (n_stored && (!stored_ts || !stored_cell || stored_stride < 46)) return EVM_EINVAL;
+  const Stored stored{stored_ts, stored_stride, n_stored, stored_cell};
   if (n >= 0x7fffffffu) return EVM_EINVAL;
   *tree_out = nullptr;
   int st;
@@ -1142,11 +1236,11 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
     } else if (ctx->client_path == 1 ||
                (ctx->client_path == 0 && !cell_owner && n_cells <= CL_MAX_CELLS)) {
       if (cell_owner || n_cells > CL_MAX_CELLS) return EVM_EINVAL;
-      st = apply_fast(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, prior, prior_present, flags, winner,
+      st = apply_fast(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, prior, prior_present, stored, flags, winner,
                       tree_out);
     } else {
-      st = apply_general(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, cell_owner, prior, prior_present, flags,
-                         winner, tree_out);
+      st = apply_general(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, cell_owner, prior, prior_present, stored,
+                         flags, winner, tree_out);
     }
   }
   if (st) return st;

@@ -375,6 +375,38 @@ __global__ void k_owner_off(const u64* __restrict__ ck, size_t L, u32 n_owners, 
     off[o] = (o == n_owners) ? (u64)L : (u64)lower_bound_u64(ck, 0, L, (u64)o << 40);
 }
 
+// Device leaf lists (per-owner offsets + codes without the owner bits) <->
+// tree leaves (ck = owner << 40 | code).  One wave per owner; codes must be
+// valid, sorted and unique per owner.
+__global__ void k_leaves_in(const u64* __restrict__ off, const u64* __restrict__ code, u32 n_owners,
+                            u64* __restrict__ ck, u32* __restrict__ bad) {
+  const u32 lane = threadIdx.x & 63;
+  for (u32 o = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; o < n_owners; o += (gridDim.x * blockDim.x) >> 6) {
+    const u64 a = off[o], b = off[o + 1];
+    if (b < a) {
+      if (lane == 0) atomicOr(bad, 1u);
+      continue;
+    }
+    for (u64 k = a + lane; k < b; k += 64) {
+      const u64 c = code[k];
+      if ((c >> 40) || (k > a && code[k - 1] >= c)) atomicOr(bad, 1u);
+      ck[k] = ((u64)o << 40) | (c & ((1ull << 40) - 1));
+    }
+  }
+}
+
+__global__ void k_leaves_out(const u64* __restrict__ off, const u64* __restrict__ ck, const int32_t* __restrict__ xr,
+                             u32 owner_lo, u32 count, u64 base, u64 L, u64* __restrict__ o_off,
+                             u64* __restrict__ o_code, int32_t* __restrict__ o_xr) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < L || i <= count; i += (u64)gridDim.x * blockDim.x) {
+    if (i < L) {
+      o_code[i] = ck[base + i] & ((1ull << 40) - 1);
+      o_xr[i] = xr[base + i];
+    }
+    if (i <= count) o_off[i] = off[owner_lo + i] - base;
+  }
+}
+
 static int tree_alloc(evm_ctx* ctx, evm_tree* t, u32 n_owners, uint64_t L) {
   t->n_owners = n_owners;
   t->n_leaves = L;
@@ -386,8 +418,10 @@ static int tree_alloc(evm_ctx* ctx, evm_tree* t, u32 n_owners, uint64_t L) {
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t b_off = up(sizeof(u64) * (n_owners + 1)), b_ck = up(sizeof(u64) * std::max<uint64_t>(L, 1)),
                b_xr = up(sizeof(int32_t) * std::max<uint64_t>(L, 1)), b_pfx = up(sizeof(int32_t) * (L + 1));
-  char* base = nullptr;
-  if (hipMallocAsync((void**)&base, b_off + b_ck + b_xr + b_pfx, ctx->stream) != hipSuccess) return EVM_ENOMEM;
+  size_t bytes = b_off + b_ck + b_xr + b_pfx;
+  char* base = static_cast<char*>(block_alloc(ctx, &bytes));
+  if (!base) return EVM_ENOMEM;
+  t->bytes = bytes;
   t->off = reinterpret_cast<unsigned long long*>(base);
   t->ck = reinterpret_cast<unsigned long long*>(base + b_off);
   t->xr = reinterpret_cast<int32_t*>(base + b_off + b_ck);
@@ -397,8 +431,49 @@ static int tree_alloc(evm_ctx* ctx, evm_tree* t, u32 n_owners, uint64_t L) {
 
 static void tree_release(evm_ctx* ctx, evm_tree* t) {
   if (!t) return;
-  if (t->off) (void)hipFreeAsync(t->off, ctx->stream);  // the base of the tree's one allocation
+  if (t->off) block_free(ctx, t->off, t->bytes);  // the base of the tree's one block
   delete t;
+}
+
+constexpr size_t BLOCK_CACHE = 8;
+
+void* evm::block_alloc(evm_ctx* ctx, size_t* bytes) {
+  const size_t need = *bytes;
+  size_t best = ctx->blocks.size();
+  for (size_t k = 0; k < ctx->blocks.size(); ++k)
+    if (ctx->blocks[k].second >= need && (best == ctx->blocks.size() || ctx->blocks[k].second < ctx->blocks[best].second))
+      best = k;
+  if (best < ctx->blocks.size()) {
+    void* p = ctx->blocks[best].first;
+    *bytes = ctx->blocks[best].second;
+    ctx->blocks.erase(ctx->blocks.begin() + best);
+    return p;
+  }
+  // new block, with headroom so a slowly growing workload keeps hitting the cache
+  const size_t want = need + need / 8;
+  void* p = nullptr;
+  if (hipMallocAsync(&p, want, ctx->stream) != hipSuccess) return nullptr;
+  ++ctx->stats.block_allocs;
+  ctx->stats.block_bytes += want;
+  *bytes = want;
+  return p;
+}
+
+void evm::block_free(evm_ctx* ctx, void* p, size_t bytes) {
+  if (!p) return;
+  ctx->blocks.push_back({p, bytes});
+  if (ctx->blocks.size() > BLOCK_CACHE) {  // drop the smallest
+    size_t k = 0;
+    for (size_t j = 1; j < ctx->blocks.size(); ++j)
+      if (ctx->blocks[j].second < ctx->blocks[k].second) k = j;
+    (void)hipFreeAsync(ctx->blocks[k].first, ctx->stream);
+    ctx->blocks.erase(ctx->blocks.begin() + k);
+  }
+}
+
+void evm::block_cache_clear(evm_ctx* ctx) {
+  for (auto& b : ctx->blocks) (void)hipFreeAsync(b.first, ctx->stream);
+  ctx->blocks.clear();
 }
 
 int evm::tree_alloc_cap(evm_ctx* ctx, u32 n_owners, uint64_t cap, evm_tree** out) {
@@ -671,6 +746,7 @@ void evm_destroy(evm_ctx* ctx) {
   if (!ctx) return;
   prof_drain(ctx);
   for (hipEvent_t e : ctx->prof_pool) (void)hipEventDestroy(e);
+  block_cache_clear(ctx);
   if (ctx->xtab) (void)hipFree(ctx->xtab);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
@@ -680,6 +756,18 @@ void evm_destroy(evm_ctx* ctx) {
   (void)hipStreamDestroy(ctx->own);
   if (ctx->hinfo) (void)hipHostFree(ctx->hinfo);
   delete ctx;
+}
+
+int evm_bind_thread(evm_ctx* ctx) {
+  if (!ctx) return EVM_EINVAL;
+  return hipSetDevice(ctx->device) == hipSuccess ? EVM_OK : EVM_EDEVICE;
+}
+
+int evm_get_stats(const evm_ctx* ctx, evm_stats* out) {
+  if (!ctx || !out) return EVM_EINVAL;
+  *out = ctx->stats;
+  out->workspace_bytes = ctx->ws_bytes;
+  return EVM_OK;
 }
 
 int evm_set_stream(evm_ctx* ctx, void* s) {
@@ -707,6 +795,10 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
   }
   if (option == EVM_OPT_RADIX && (value == 0 || value == 1)) {
     ctx->radix_onesweep = (int)value;
+    return EVM_OK;
+  }
+  if (option == EVM_OPT_TEST_FAIL && value >= 0 && value <= 1) {
+    ctx->test_fail = (int)value;
     return EVM_OK;
   }
   if (option == EVM_OPT_SERVER_PATH && value >= 0 && value <= 2) {
@@ -840,6 +932,45 @@ int evm_tree_from_leaves(evm_ctx* ctx, uint32_t n_owners, const uint64_t* off_h,
   }
   int st = tree_finalize(ctx, S, n_owners, dck, dxr, L, out);
   if (st) return st;
+  return evm_sync(ctx);
+}
+
+int evm_tree_from_device_leaves(evm_ctx* ctx, uint32_t n_owners, const uint64_t* off, const uint64_t* code,
+                                const int32_t* xr, evm_tree** out) {
+  if (!ctx || !out || !off) return EVM_EINVAL;
+  uint64_t L = 0;
+  HIPR(hipMemcpyAsync(&L, off + n_owners, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if (L && (!code || !xr)) return EVM_EINVAL;
+  Scratch S(ctx);
+  u64* ck = S.alloc<u64>(std::max<uint64_t>(L, 1));
+  u32* bad = S.alloc<u32>(1);
+  if (!ck || !bad) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
+  if (n_owners)
+    KLAUNCH(k_leaves_in, dim3(grid_for(n_owners, 4, 1 << 16)), dim3(256), (const u64*)off, (const u64*)code, n_owners,
+            ck, bad);
+  u32 hb = 0;
+  HIPR(hipMemcpyAsync(&hb, bad, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if (hb) return EVM_EINVAL;
+  const int st = tree_finalize(ctx, S, n_owners, ck, xr, L, out);
+  return st ? st : evm_sync(ctx);
+}
+
+int evm_tree_slice(evm_ctx* ctx, const evm_tree* t, uint32_t owner_lo, uint32_t count, uint64_t* off, uint64_t* code,
+                   int32_t* xr, uint64_t cap, uint64_t* n_leaves) {
+  if (!ctx || !t || !n_leaves || owner_lo + (uint64_t)count > t->n_owners || (count && !off)) return EVM_EINVAL;
+  u64 ab[2] = {0, 0};
+  HIPR(hipMemcpyAsync(&ab[0], t->off + owner_lo, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipMemcpyAsync(&ab[1], t->off + owner_lo + count, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  *n_leaves = ab[1] - ab[0];
+  if (*n_leaves > cap || (*n_leaves && (!code || !xr))) return EVM_ECAPACITY;
+  if (count)
+    KLAUNCH(k_leaves_out, dim3(grid_for(std::max<uint64_t>(*n_leaves, count + 1), 256, 8192)), dim3(256),
+            (const u64*)t->off, (const u64*)t->ck, (const int32_t*)t->xr, owner_lo, count, ab[0], *n_leaves,
+            (u64*)off, (u64*)code, xr);
   return evm_sync(ctx);
 }
 

@@ -25,6 +25,7 @@ struct evm_ctx {
   int client_path = 0;  // EVM_OPT_CLIENT_PATH
   int server_path = 0;  // EVM_OPT_SERVER_PATH
   int overlap = 1;      // EVM_OPT_OVERLAP: independent checks on a second stream
+  int test_fail = 0;       // EVM_OPT_TEST_FAIL (tests only)
   int radix_onesweep = 1;  // EVM_OPT_RADIX: 1 one-sweep radix passes (look-back), 0 histogram + scan + scatter
   hipStream_t side = nullptr;  // second stream (forked from / joined to `stream` inside a call)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -41,11 +42,16 @@ struct evm_ctx {
   size_t ws_top = 0;   // arena bytes in use
   size_t ws_vtop = 0;  // bytes the current call would use (arena + pool overflow)
   size_t ws_need = 0;  // largest ws_vtop seen
+  evm_stats stats{};   // allocation counters (evm_get_stats)
+  // freed tree / store blocks kept for reuse (stream-ordered on `stream`):
+  // a steady-state loop of ingests / applies makes no allocation calls
+  std::vector<std::pair<void*, size_t>> blocks;
 };
 
 // One MerkleTree per owner, as sorted unique leaves keyed by
 // ck = owner << 40 | code (code: 20 base-4 digits, see evm_device.hpp).
 struct evm_tree {
+  size_t bytes;  // size of the one device block holding the arrays (base = off)
   uint32_t n_owners;
   uint64_t n_leaves;
   unsigned long long* off;  // [n_owners + 1] leaf range of each owner
@@ -117,6 +123,7 @@ class Scratch {
       ctx_->ws_bytes = 0;
       const size_t want = ctx_->ws_need + ctx_->ws_need / 8;
       if (hipMalloc(&ctx_->ws, want) == hipSuccess) ctx_->ws_bytes = want;
+      ++ctx_->stats.workspace_regrows;
     }
   }
   ~Scratch() {
@@ -136,6 +143,8 @@ class Scratch {
     }
     void* p = nullptr;
     if (hipMallocAsync(&p, bytes, ctx_->stream) != hipSuccess) return nullptr;
+    ++ctx_->stats.scratch_pool_allocs;
+    ctx_->stats.scratch_pool_bytes += bytes;
     ptrs_.push_back(p);
     return static_cast<T*>(p);
   }
@@ -256,6 +265,12 @@ inline int new_info(evm_ctx* ctx, Scratch& S, Info** out) {
   *out = d;
   return EVM_OK;
 }
+
+// Device blocks for trees and stores, recycled through ctx->blocks (best fit,
+// at most BLOCK_CACHE kept); *bytes is updated to the block's real size.
+void* block_alloc(evm_ctx* ctx, size_t* bytes);
+void block_free(evm_ctx* ctx, void* p, size_t bytes);
+void block_cache_clear(evm_ctx* ctx);
 
 // shared launchers (evm_engine.hip)
 int launch_iota(evm_ctx* ctx, u32* v, size_t n);

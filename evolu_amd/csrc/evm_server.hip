@@ -25,6 +25,7 @@
 using namespace evm;
 
 struct evm_store {
+  size_t bytes;  // the one device block holding the arrays (base = off)
   uint32_t n_owners;
   uint64_t n;
   unsigned long long* off;  // [n_owners + 1]
@@ -1080,7 +1081,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_keep(StoreView st, u32 n
 __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_emit(u32 n_owners, u32 C, const u32* __restrict__ cpos,
                                                              const u64* __restrict__ first, const u32* __restrict__ keep,
                                                              const u32* __restrict__ kpos, const u64* __restrict__ id,
-                                                             u64* __restrict__ sel_id) {
+                                                             u64* __restrict__ sel_id, StoreView st,
+                                                             u64* __restrict__ sel_key) {
   __shared__ u32 range[2];
   for (u32 j0 = blockIdx.x * SEL_THREADS; j0 < C; j0 += gridDim.x * SEL_THREADS) {
     const u32 j1 = min(C, j0 + SEL_THREADS) - 1;
@@ -1092,7 +1094,14 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_emit(u32 n_owners, u32 C
     if (j > j1) continue;
     if (keep && !keep[j]) continue;
     const u32 o = cand_owner(cpos, range[0], range[1], j);
-    sel_id[kpos ? kpos[j] : j] = id[first[o] + (j - cpos[o])];
+    const size_t k = first[o] + (j - cpos[o]);
+    const u32 q = kpos ? kpos[j] : j;
+    sel_id[q] = id[k];
+    if (sel_key) {  // the row's order key: merges selections of one owner split over ranks
+      sel_key[3 * (size_t)q] = st.tc[k];
+      sel_key[3 * (size_t)q + 1] = st.hi[k];
+      sel_key[3 * (size_t)q + 2] = st.lo[k];
+    }
   }
 }
 
@@ -1115,8 +1124,10 @@ int store_alloc(evm_ctx* ctx, evm_store* s, u32 n_owners, uint64_t n) {
   // s->off is its base)
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t b_off = up(sizeof(u64) * (n_owners + 1)), b4 = up(sizeof(u32) * m), b8 = up(sizeof(u64) * m);
-  char* base = nullptr;
-  HIPR(hipMallocAsync((void**)&base, b_off + 2 * b4 + 3 * b8, ctx->stream));
+  size_t bytes = b_off + 2 * b4 + 3 * b8;
+  char* base = static_cast<char*>(block_alloc(ctx, &bytes));
+  if (!base) return EVM_ENOMEM;
+  s->bytes = bytes;
   s->off = reinterpret_cast<unsigned long long*>(base);
   s->owner = reinterpret_cast<u32*>(base + b_off);
   s->lo = reinterpret_cast<u32*>(base + b_off + b4);
@@ -1127,7 +1138,7 @@ int store_alloc(evm_ctx* ctx, evm_store* s, u32 n_owners, uint64_t n) {
 }
 
 void store_release_arrays(evm_ctx* ctx, evm_store* s) {
-  if (s->off) (void)hipFreeAsync(s->off, ctx->stream);  // the base of the store's one allocation
+  if (s->off) block_free(ctx, s->off, s->bytes);  // the base of the store's one block
   s->off = nullptr;
   s->owner = nullptr;
   s->tc = s->hi = s->id = nullptr;
@@ -1316,6 +1327,7 @@ static int commit_store(evm_ctx* ctx, evm_store* s, evm_store& ns, evm_tree* new
   store_release_arrays(ctx, s);
   tree_destroy(ctx, s->tree);
   s->n = ns.n;
+  s->bytes = ns.bytes;
   s->off = ns.off;
   s->owner = ns.owner;
   s->tc = ns.tc;
@@ -1339,6 +1351,18 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
   int st;
   evm_store ns{};
   evm_tree* new_tree = nullptr;
+  // an error return after the new arrays exist releases them (the store is untouched)
+  struct Pending {
+    evm_ctx* ctx;
+    evm_store& ns;
+    evm_tree*& t;
+    bool armed = true;
+    ~Pending() {
+      if (!armed) return;
+      store_release_arrays(ctx, &ns);
+      if (t) tree_destroy(ctx, t);
+    }
+  } pending{ctx, ns, new_tree};
   {
     Scratch S(ctx);
     Info* info = nullptr;
@@ -1386,8 +1410,24 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
         KLAUNCH(k_pick, dim3(grid_for(n, 256)), dim3(256), bigmask, bpos, n, sel_big);
         u32 hbig = 0;
         HIPR(hipMemcpyAsync(&hbig, nbig, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-        if ((st = commit_store(ctx, s, ns, new_tree))) return st;
-        return ingest_impl(ctx, s, ts, stride, hbig, owner, sel_big, rec, id_base, flags, 2);
+        HIPR(hipStreamSynchronize(ctx->stream));
+        // phase 2 runs on the uncommitted phase-1 result: the caller's store
+        // changes only when both phases succeed (index.ts:147-169 is one
+        // transaction that rolls back on any error)
+        evm_store mid = ns;
+        mid.tree = new_tree;
+        ns = evm_store{};
+        new_tree = nullptr;
+        st = ctx->test_fail == 1 ? EVM_ENOMEM
+                                 : ingest_impl(ctx, &mid, ts, stride, hbig, owner, sel_big, rec, id_base, flags, 2);
+        if (st) {
+          store_release_arrays(ctx, &mid);
+          tree_destroy(ctx, mid.tree);
+          (void)hipMemsetAsync(flags, 0, n, ctx->stream);  // nothing inserted
+          (void)evm_sync(ctx);
+          return st;
+        }
+        return commit_store(ctx, s, mid, mid.tree);
       }
       if (done) goto commit;
     }
@@ -1525,12 +1565,10 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       if ((st = reduce_runs(ctx, S, l_ck, (const int32_t*)l_h, m, rck, rxr, &L))) return st;
       st = merge_into_tree(ctx, S, s->tree, s->n_owners, rck, rxr, L, &new_tree);
     }
-    if (st) {
-      store_release_arrays(ctx, &ns);
-      return st;
-    }
+    if (st) return st;
   }
 commit:
+  pending.armed = false;
   return commit_store(ctx, s, ns, new_tree);
 }
 
@@ -1549,9 +1587,13 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
 // Selection of each owner's rows after a per-owner bound (diff/since, < 0 =
 // none), optionally excluding one node (server getMessages).
 static int select_after(evm_ctx* ctx, Scratch& S, const evm_store* s, const int64_t* bound, const char* node,
-                        const uint8_t* active, uint64_t* sel_off, uint64_t* sel_id, uint64_t cap, uint64_t* n_sel) {
+                        const uint8_t* active, uint64_t* sel_off, uint64_t* sel_id, uint64_t* sel_key, uint64_t cap,
+                        uint64_t* n_sel) {
   const u32 O = s->n_owners;
   int st;
+  // candidate counts and their scans are u32: a store past 2^32 - 1 rows
+  // would wrap them (and silently shorten the selection)
+  if (s->n > 0xffffffffull) return EVM_ECAPACITY;
   u64* first = S.alloc<u64>(O);
   u32* cand = S.alloc<u32>(O);
   u32* cpos = S.alloc<u32>(O + 1);
@@ -1589,7 +1631,7 @@ static int select_after(evm_ctx* ctx, Scratch& S, const evm_store* s, const int6
   if (K > cap || (K && !sel_id)) return EVM_ECAPACITY;
   if (K)
     KLAUNCH(k_sv_sel_emit, dim3(grid), dim3(SEL_THREADS), O, C, (const u32*)cpos, (const u64*)first,
-            (const u32*)keep, (const u32*)kpos, (const u64*)s->id, (u64*)sel_id);
+            (const u32*)keep, (const u32*)kpos, (const u64*)s->id, (u64*)sel_id, v, (u64*)sel_key);
   return evm_sync(ctx);
 }
 
@@ -1607,7 +1649,7 @@ int evm_server_select(evm_ctx* ctx, const evm_store* s, const evm_tree* client, 
   int st;
   Scratch S(ctx);
   if ((st = launch_diff(ctx, s->tree, client, diff))) return st;
-  return select_after(ctx, S, s, diff, node, active, sel_off, sel_id, cap, n_sel);
+  return select_after(ctx, S, s, diff, node, active, sel_off, sel_id, nullptr, cap, n_sel);
 }
 
 int evm_store_since(evm_ctx* ctx, const evm_store* s, const int64_t* since, uint64_t* sel_off, uint64_t* sel_id,
@@ -1618,7 +1660,19 @@ int evm_store_since(evm_ctx* ctx, const evm_store* s, const int64_t* since, uint
     return EVM_OK;
   }
   Scratch S(ctx);
-  return select_after(ctx, S, s, since, nullptr, nullptr, sel_off, sel_id, cap, n_sel);
+  return select_after(ctx, S, s, since, nullptr, nullptr, sel_off, sel_id, nullptr, cap, n_sel);
+}
+
+int evm_store_select_after(evm_ctx* ctx, const evm_store* s, const int64_t* bound, const char* node,
+                           const uint8_t* active, uint64_t* sel_off, uint64_t* sel_id, uint64_t* sel_key,
+                           uint64_t cap, uint64_t* n_sel) {
+  if (!ctx || !s || !bound || !sel_off || !n_sel) return EVM_EINVAL;
+  if (s->n_owners == 0) {
+    *n_sel = 0;
+    return EVM_OK;
+  }
+  Scratch S(ctx);
+  return select_after(ctx, S, s, bound, node, active, sel_off, sel_id, sel_key, cap, n_sel);
 }
 
 }  // extern "C"

@@ -204,38 +204,121 @@ def gather_hot_roots(root: torch.Tensor, present: torch.Tensor, omap: OwnerMap, 
     return x.to(torch.int32), p
 
 
+def all_gather_var(t: torch.Tensor, group=None):
+    """All-gather of a 1-D tensor whose length differs per rank -> list of
+    the ranks' tensors (same device: RCCL device-to-device, gloo on CPU)."""
+    world = dist.get_world_size(group)
+    home = t.device
+    if dist.get_backend(group) == "gloo" and home.type != "cpu":
+        t = t.cpu()  # gloo (the CPU tests, ranks sharing one GPU) gathers host tensors
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    sizes = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sz = [int(x.item()) for x in sizes]
+    cap = max(max(sz), 1)
+    pad = torch.zeros(cap, dtype=t.dtype, device=t.device)
+    pad[: t.numel()] = t
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return [p[:k].to(home) for p, k in zip(parts, sz)]
+
+
+def gather_leaf_parts(off: torch.Tensor, code: torch.Tensor, xr: torch.Tensor, group=None):
+    """Every rank's partial leaf lists of the split owners (off int64[nh+1]
+    from 0, code int64[L], xr int32/int64[L]) -> [(off, code, xr)] per rank,
+    in one variable-size all-gather (device buffers stay on the device)."""
+    nh = off.numel() - 1
+    L = code.numel()
+    payload = torch.cat([off.to(torch.int64), code.to(torch.int64), xr.to(torch.int64)])
+    out = []
+    for a in all_gather_var(payload, group):
+        L = (a.numel() - (nh + 1)) // 2
+        out.append((a[: nh + 1], a[nh + 1: nh + 1 + L], a[nh + 1 + L:].to(torch.int32)))
+    return out
+
+
 def merge_hot_trees(eng, trees, omap: OwnerMap, group=None):
     """Full trees of the split owners on every rank: the per-rank partial
-    leaf lists of the hot local owners are all-gathered and XOR-merged on the
-    device (evm_tree_merge).  Returns an engine Trees with one owner per hot
+    leaf lists of the hot local owners (evm_tree_slice, device) are
+    all-gathered over RCCL and XOR-merged on the device (evm_tree_from_device_
+    leaves + evm_tree_merge).  Returns an engine Trees with one owner per hot
     owner (in omap.hot order)."""
-    import numpy as np
-
     nh = int(omap.hot.numel())
-    off, code, xr = trees.leaves()
-    lo, hi = int(off[omap.per]), int(off[omap.per + nh])
-    part_off = (off[omap.per:omap.per + nh + 1] - lo).astype(np.int64)
-    payload = np.concatenate([part_off, code[lo:hi].astype(np.int64), xr[lo:hi].astype(np.int64)])
-    dev = torch.device("cuda", eng.device) if torch.cuda.is_available() else torch.device("cpu")
-    t = torch.from_numpy(payload).to(dev)
-    world = dist.get_world_size(group)
-    sizes = torch.tensor([t.numel()], dtype=torch.int64, device=dev)
-    alls = [torch.empty_like(sizes) for _ in range(world)]
-    dist.all_gather(alls, sizes, group=group)
-    cap = int(max(int(x.item()) for x in alls))
-    pad = torch.zeros(cap, dtype=torch.int64, device=dev)
-    pad[: t.numel()] = t
-    allt = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(allt, pad, group=group)
+    off, code, xr = trees.slice_device(omap.per, nh)
     merged = None
-    for r in range(world):
-        a = allt[r].cpu().numpy()
-        po = a[: nh + 1]
-        L = int(po[-1])
-        part = eng.tree_from_leaves(po.astype(np.uint64), a[nh + 1:nh + 1 + L].astype(np.uint64),
-                                    a[nh + 1 + L:nh + 1 + 2 * L].astype(np.int32))
+    for po, pc, px in gather_leaf_parts(off, code, xr, group):
+        part = eng.tree_from_device_leaves(po, pc, px)
         merged = part if merged is None else eng.tree_merge(merged, part)
     return merged
+
+
+def lex_order(key: torch.Tensor) -> torch.Tensor:
+    """Permutation sorting rows of an int64 [m, k] key matrix lexicographically
+    (stable passes from the last column)."""
+    order = torch.arange(key.shape[0], device=key.device)
+    for c in range(key.shape[1] - 1, -1, -1):
+        order = order[torch.argsort(key[order, c], stable=True)]
+    return order
+
+
+def gather_selection(sel_off: torch.Tensor, sel_id: torch.Tensor, sel_key: torch.Tensor, group=None):
+    """getMessages rows of owners split over ranks: each rank selected its
+    share (sel_off int64[nh+1], sel_id int64[m], sel_key int64[m, 3] = the
+    rows' order keys); returns (off, ids) of every split owner's rows from all
+    ranks in timestamp order (ORDER BY "timestamp", index.ts:101), the same
+    on every rank."""
+    nh = sel_off.numel() - 1
+    payload = torch.cat([sel_off.to(torch.int64), sel_id.to(torch.int64), sel_key.to(torch.int64).reshape(-1)])
+    owners, ids, keys = [], [], []
+    for a in all_gather_var(payload, group):
+        po = a[: nh + 1]
+        m = int(po[-1].item())
+        ids.append(a[nh + 1: nh + 1 + m])
+        keys.append(a[nh + 1 + m: nh + 1 + 4 * m].reshape(m, 3))
+        counts = po[1:] - po[:-1]
+        owners.append(torch.repeat_interleave(torch.arange(nh, device=a.device), counts))
+    owner = torch.cat(owners)
+    ids = torch.cat(ids)
+    keys = torch.cat(keys)
+    order = lex_order(torch.cat([owner[:, None], keys], 1))
+    counts = torch.bincount(owner, minlength=nh)
+    off = torch.zeros(nh + 1, dtype=torch.int64, device=ids.device)
+    off[1:] = torch.cumsum(counts, 0)
+    return off, ids[order]
+
+
+def split_get_messages(eng, store, client_local, client_hot, node: torch.Tensor, omap: OwnerMap, group=None):
+    """getMessages (index.ts:173-202) for every local owner when hot owners
+    are split over ranks.  A cold owner lives on one rank: its diff is the
+    one of its full tree.  A hot owner's diff must be the diff of its FULL
+    server tree against the client's full tree -- a diff of a partial tree is
+    not the diff of the whole -- so the partial trees are merged first
+    (merge_hot_trees), the diff is computed on the merge (identical on every
+    rank), each rank selects its share after that bound (with the NOT LIKE
+    node filter) and the shares merge in timestamp order.
+
+    client_local: Trees over the local owners (the client trees of the cold
+    owners; the hot slots are ignored); client_hot: Trees of the hot owners'
+    full client trees, omap.hot order; node: uint8 [n_local * 16].
+    Returns (diff int64[n_local] with the hot slots' full-tree diffs,
+    cold (off, ids) over local owners -- hot slots empty -- and hot (off,
+    ids) over omap.hot, all ranks' rows merged)."""
+    nh = int(omap.hot.numel())
+    diff = eng.merkle_diff(store.tree(), client_local)
+    if nh:
+        merged = merge_hot_trees(eng, store.tree(), omap, group)
+        diff[omap.per: omap.per + nh] = eng.merkle_diff(merged, client_hot)
+        merged.free()
+    active = torch.ones(omap.n_local, dtype=torch.uint8, device=diff.device)
+    active[omap.per: omap.per + nh] = 0
+    off_c, ids_c, _ = store.select_after(diff, node, active=active)
+    if not nh:
+        return diff, (off_c, ids_c), None
+    hot_only = torch.zeros_like(active)
+    hot_only[omap.per: omap.per + nh] = 1
+    off_h, ids_h, key_h = store.select_after(diff, node, active=hot_only, keys=True)
+    part_off = off_h[omap.per: omap.per + nh + 1] - off_h[omap.per]
+    return diff, (off_c, ids_c), gather_selection(part_off, ids_h, key_h, group)
 
 
 # ---------------------------------------------------------------------------

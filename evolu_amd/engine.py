@@ -78,6 +78,15 @@ class Engine:
     def set_option(self, option: int, value: int):
         check(self.lib.evm_set_option(self.h, option, value), "evm_set_option")
 
+    STATS_FIELDS = ("workspace_regrows", "workspace_bytes", "scratch_pool_allocs", "scratch_pool_bytes",
+                    "block_allocs", "block_bytes")
+
+    def stats(self) -> dict:
+        """Allocation counters (evm_get_stats)."""
+        buf = (C.c_uint64 * len(self.STATS_FIELDS))()
+        check(self.lib.evm_get_stats(self.h, C.byref(buf)), "evm_get_stats")
+        return dict(zip(self.STATS_FIELDS, [int(x) for x in buf]))
+
     # ------------------------------------------------------------- profiling
     def prof_enable(self, on: bool = True):
         check(self.lib.evm_prof_enable(self.h, 1 if on else 0), "evm_prof_enable")
@@ -168,6 +177,16 @@ class Engine:
               "evm_merkle_insert")
         return Trees(self, h)
 
+    def tree_from_device_leaves(self, off: torch.Tensor, code: torch.Tensor, xr: torch.Tensor) -> "Trees":
+        """Trees from device leaf lists (int64 off[n_owners+1], int64 code, int32 xr)."""
+        off = off.to(torch.int64).contiguous()
+        code = code.to(torch.int64).contiguous()
+        xr = xr.to(torch.int32).contiguous()
+        h = C.c_void_p()
+        check(self.lib.evm_tree_from_device_leaves(self.h, off.numel() - 1, _ptr(off), _ptr(code), _ptr(xr),
+                                                   C.byref(h)), "evm_tree_from_device_leaves")
+        return Trees(self, h)
+
     def tree_merge(self, a: "Trees", b: "Trees") -> "Trees":
         """Union of two tree sets' inserts (equal leaves XOR-combine)."""
         h = C.c_void_p()
@@ -183,8 +202,13 @@ class Engine:
     def apply_batch(self, trees: "Trees", ts: torch.Tensor, cell: torch.Tensor, n_cells: int,
                     cell_owner: Optional[torch.Tensor] = None, prior_ts: Optional[torch.Tensor] = None,
                     prior_present: Optional[torch.Tensor] = None, flags: Optional[torch.Tensor] = None,
-                    winner: Optional[torch.Tensor] = None, raise_on_error: bool = True):
-        """applyMessages for one batch -> (flags u8[n], winner i32[n_cells], Trees, status)."""
+                    winner: Optional[torch.Tensor] = None, raise_on_error: bool = True,
+                    stored_ts: Optional[torch.Tensor] = None, stored_cell: Optional[torch.Tensor] = None):
+        """applyMessages for one batch -> (flags u8[n], winner i32[n_cells], Trees, status).
+
+        stored_ts / stored_cell: the rows already in __message whose timestamp
+        is in the batch (evm_apply_batch_ex; a cell id >= n_cells = a cell the
+        batch does not touch)."""
         n, stride = ts.shape
         dev = ts.device
         if flags is None:
@@ -193,9 +217,15 @@ class Engine:
             winner = torch.empty(max(n_cells, 1), dtype=torch.int32, device=dev)
         pstride = prior_ts.shape[1] if prior_ts is not None else 48
         h = C.c_void_p()
-        st = self.lib.evm_apply_batch(self.h, trees.h, _ptr(ts), stride, n, _ptr(cell), n_cells, _ptr(cell_owner),
-                                      _ptr(prior_ts), pstride, _ptr(prior_present), _ptr(flags), _ptr(winner),
-                                      C.byref(h))
+        if stored_ts is not None and stored_ts.shape[0]:
+            st = self.lib.evm_apply_batch_ex(self.h, trees.h, _ptr(ts), stride, n, _ptr(cell), n_cells,
+                                             _ptr(cell_owner), _ptr(prior_ts), pstride, _ptr(prior_present),
+                                             _ptr(stored_ts), stored_ts.shape[1], stored_ts.shape[0],
+                                             _ptr(stored_cell), _ptr(flags), _ptr(winner), C.byref(h))
+        else:
+            st = self.lib.evm_apply_batch(self.h, trees.h, _ptr(ts), stride, n, _ptr(cell), n_cells,
+                                          _ptr(cell_owner), _ptr(prior_ts), pstride, _ptr(prior_present),
+                                          _ptr(flags), _ptr(winner), C.byref(h))
         if raise_on_error:
             check(st, "evm_apply_batch")
         return flags, winner[:n_cells], (Trees(self, h) if st == _lib.EVM_OK else None), st
@@ -273,6 +303,23 @@ class Store:
                                              _ptr(off), _ptr(ids), cap, C.byref(nsel)), "evm_server_select")
         return diff[:O], off, ids[: nsel.value]
 
+    def select_after(self, bound: torch.Tensor, node: Optional[torch.Tensor] = None,
+                     active: Optional[torch.Tensor] = None, cap: int = None, keys: bool = False):
+        """Selection with given per-owner bounds (evm_store_select_after):
+        -> (sel_off int64[n_owners+1], sel_id int64[n_sel], sel_key int64[n_sel, 3] or None)."""
+        dev = bound.device
+        O = self.n_owners
+        bound = bound.to(torch.int64).contiguous()
+        off = torch.empty(O + 1, dtype=torch.int64, device=dev)
+        cap = self.n_messages if cap is None else cap
+        ids = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        key = torch.empty((max(cap, 1), 3), dtype=torch.int64, device=dev) if keys else None
+        nsel = C.c_uint64()
+        check(self.eng.lib.evm_store_select_after(self.eng.h, self.h, _ptr(bound), _ptr(node), _ptr(active),
+                                                  _ptr(off), _ptr(ids), _ptr(key), cap, C.byref(nsel)),
+              "evm_store_select_after")
+        return off, ids[: nsel.value], (key[: nsel.value] if keys else None)
+
     def since(self, since: torch.Tensor, cap: int = None):
         """receive.ts:118-124 resend range, batched over owners: for since[o] >= 0
         the owner's ids with timestamp > syncTs(since[o]), in timestamp order.
@@ -321,6 +368,22 @@ class Trees:
                                            code.ctypes.data_as(C.c_void_p), xr.ctypes.data_as(C.c_void_p)),
               "evm_tree_leaves")
         return off, code[: self.n_leaves], xr[: self.n_leaves]
+
+    def slice_device(self, owner_lo: int, count: int):
+        """Device copy of owners [owner_lo, owner_lo+count)'s leaves ->
+        (off int64[count+1] from 0, code int64[L], xr int32[L])."""
+        dev = torch.device("cuda", self.eng.device)
+        nl = C.c_uint64()
+        off = torch.empty(count + 1, dtype=torch.int64, device=dev)
+        st = self.eng.lib.evm_tree_slice(self.eng.h, self.h, owner_lo, count, _ptr(off), None, None, 0, C.byref(nl))
+        if st not in (_lib.EVM_OK, _lib.EVM_ECAPACITY):
+            check(st, "evm_tree_slice")
+        L = nl.value
+        code = torch.empty(max(L, 1), dtype=torch.int64, device=dev)
+        xr = torch.empty(max(L, 1), dtype=torch.int32, device=dev)
+        check(self.eng.lib.evm_tree_slice(self.eng.h, self.h, owner_lo, count, _ptr(off), _ptr(code), _ptr(xr), L,
+                                          C.byref(nl)), "evm_tree_slice")
+        return off, code[:L], xr[:L]
 
     def roots(self):
         r = np.zeros(max(self.n_owners, 1), dtype=np.int32)

@@ -84,6 +84,21 @@ typedef struct evm_ctx evm_ctx;
 int evm_create(int device, evm_ctx** out);
 void evm_destroy(evm_ctx* ctx);
 const char* evm_strerror(int status);
+/* Makes the calling thread use the context's GPU (a worker thread -- e.g. the
+ * N-API addon's async work -- driving a context created on another thread).
+ * A context is still used by one thread at a time. */
+int evm_bind_thread(evm_ctx* ctx);
+/* Allocation counters since evm_create: what a steady-state loop should keep
+ * flat (every counter but workspace_bytes only grows). */
+typedef struct evm_stats {
+  uint64_t workspace_regrows;   /* the per-call scratch arena was reallocated (synchronising) */
+  uint64_t workspace_bytes;     /* current arena size */
+  uint64_t scratch_pool_allocs; /* scratch requests the arena could not hold (stream-ordered pool) */
+  uint64_t scratch_pool_bytes;
+  uint64_t block_allocs;        /* device blocks allocated for trees and stores (freed ones are reused) */
+  uint64_t block_bytes;
+} evm_stats;
+int evm_get_stats(const evm_ctx* ctx, evm_stats* out);
 int evm_set_stream(evm_ctx* ctx, void* hip_stream); /* NULL: the HIP default stream; initially the context's own */
 void* evm_get_stream(evm_ctx* ctx);
 int evm_sync(evm_ctx* ctx);
@@ -92,6 +107,7 @@ int evm_sync(evm_ctx* ctx);
 #define EVM_OPT_OVERLAP 3     /* 1 (default): independent checks run on a second HIP stream inside a call; 0: one stream */
 #define EVM_OPT_SERVER_PATH 2 /* evm_server_ingest: 0/1 per-owner LDS path where every owner's share fits, 2 force the sort path */
 #define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 0 histogram + scan + scatter per pass */
+#define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM) */
 int evm_set_option(evm_ctx* ctx, int option, int64_t value);
 /* kernel timing with HIP events on the context stream (for roofline reports) */
 int evm_prof_enable(evm_ctx* ctx, int on);
@@ -122,6 +138,14 @@ int evm_tree_new(evm_ctx* ctx, uint32_t n_owners, evm_tree** out); /* all trees 
 int evm_tree_from_leaves(evm_ctx* ctx, uint32_t n_owners, const uint64_t* owner_off_host,
                          const uint64_t* code_host, const int32_t* xor_host, evm_tree** out);
 int evm_tree_free(evm_ctx* ctx, evm_tree* t);
+/* The same from DEVICE arrays (off[n_owners + 1], code[off[n_owners]], xr):
+ * how leaf lists gathered over RCCL become trees without a host copy.     */
+int evm_tree_from_device_leaves(evm_ctx* ctx, uint32_t n_owners, const uint64_t* off_dev, const uint64_t* code_dev,
+                                const int32_t* xr_dev, evm_tree** out);
+/* Device copy of the leaves of owners [owner_lo, owner_lo + count): off[count
+ * + 1] (rebased to 0), code / xr [*n_leaves <= cap] (EVM_ECAPACITY if not). */
+int evm_tree_slice(evm_ctx* ctx, const evm_tree* t, uint32_t owner_lo, uint32_t count, uint64_t* off_dev,
+                   uint64_t* code_dev, int32_t* xr_dev, uint64_t cap, uint64_t* n_leaves);
 int evm_tree_info(const evm_tree* t, uint32_t* n_owners, uint64_t* n_leaves);
 /* device views (valid until the tree is freed) */
 int evm_tree_device(const evm_tree* t, const uint64_t** owner_off, const uint64_t** code, const int32_t** xr);
@@ -165,6 +189,26 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
                     const uint32_t* cell, uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts,
                     size_t prior_stride, const uint8_t* prior_present, uint8_t* flags, int32_t* winner,
                     evm_tree** tree_out);
+
+/* evm_apply_batch plus the rows ALREADY in __message that hold a batch
+ * timestamp (applyMessages.ts:42-45: "timestamp" is the table's PRIMARY KEY,
+ * initDbModel.ts:44), i.e. the caller's
+ *   SELECT "timestamp", "table", "row", "column" FROM "__message"
+ *   WHERE "timestamp" IN (<the batch's timestamps>)
+ * stored_ts: device, n_stored timestamps at stored_stride; stored_cell:
+ * device [n_stored], the row's cell in the batch's numbering, or any id >=
+ * n_cells for a cell the batch does not touch.  A batch message whose
+ * timestamp is stored under ANOTHER cell has its INSERT ignored and freezes
+ * that cell's running max (applyMessages.ts:104-119): EVM_ECOLLISION, nothing
+ * applied.  A stored row of the message's own cell is covered by prior_ts
+ * (the cell's max is >= it).  n_stored == 0: exactly evm_apply_batch.
+ * (With cell_owner, a stored row matching another owner's message is also
+ * reported, conservatively.)                                               */
+int evm_apply_batch_ex(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n,
+                       const uint32_t* cell, uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts,
+                       size_t prior_stride, const uint8_t* prior_present, const char* stored_ts, size_t stored_stride,
+                       size_t n_stored, const uint32_t* stored_cell, uint8_t* flags, int32_t* winner,
+                       evm_tree** tree_out);
 
 /* The global __message PK check evm_apply_batch runs (applyMessages.ts:42-45,
  * 104-113: one timestamp in two cells of a batch), on its own: for a batch
@@ -238,6 +282,18 @@ int evm_store_since(evm_ctx* ctx, const evm_store* s, const int64_t* since, uint
 int evm_server_select(evm_ctx* ctx, const evm_store* s, const evm_tree* client, const char* node,
                       const uint8_t* active, int64_t* diff, uint64_t* sel_off, uint64_t* sel_id, uint64_t cap,
                       uint64_t* n_sel);
+
+/* The selection half of getMessages (index.ts:189-197, stmt :98-102) with the
+ * bound given: per owner o with bound[o] >= 0, the rows with timestamp >
+ * timestampToString(createSyncTimestamp(bound[o])) and (node != NULL)
+ * timestamp NOT LIKE '%' || node[o], in timestamp order.  For an owner whose
+ * rows are split over GPUs the bound is the diff of its FULL trees (computed
+ * once, on the merged tree), and each GPU selects its share; sel_key
+ * (device, 3 x u64 per selected row, may be NULL) receives each row's order
+ * key (tc, node ranks hi, lo) so the shares merge in timestamp order.      */
+int evm_store_select_after(evm_ctx* ctx, const evm_store* s, const int64_t* bound, const char* node,
+                           const uint8_t* active, uint64_t* sel_off, uint64_t* sel_id, uint64_t* sel_key,
+                           uint64_t cap, uint64_t* n_sel);
 
 /* ---------------------------------------------------------------- wire codec
  * protobuf.proto SyncRequest / SyncResponse (protobuf.ts:60-171), HOST

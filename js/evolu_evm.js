@@ -191,13 +191,22 @@ class Server {
   }
   // getMessages for every owner: clientTrees[o] JSON, nodeIds[o] -> { diff[o], ids[o][] }
   getMessages(clientTreesJson, nodeIds) {
+    if (clientTreesJson.length !== this.nOwners || nodeIds.length !== this.nOwners)
+      throw new RangeError("one client tree and one nodeId per owner slot");
+    nodeIds.forEach((n) => {
+      // a NodeId is 16 hex chars (types.ts:42); any other string would shift every later owner's slice
+      if (typeof n !== "string" || !/^[0-9a-f]{16}$/i.test(n)) throw new RangeError("nodeId must be 16 hex chars");
+    });
     const c = addon.treeFromJson(this.engine.ctx, clientTreesJson);
     const node = encodeTimestamps([]).constructor.from(Buffer.from(nodeIds.join(""), "latin1"));
     const r = addon.serverSelect(this.engine.ctx, this.store, c, node);
     addon.treeFree(this.engine.ctx, c);
     const ids = [];
     for (let o = 0; o < this.nOwners; o++) ids.push(Array.from(r.ids.subarray(r.off[o], r.off[o + 1])));
-    return { diff: Array.from(r.diff, (d) => (d === -1 ? null : d)), ids };
+    // diffMerkleTrees throws RangeError at a 17-digit key (merkleTree.ts:55-61), which fails that
+    // owner's request (index.ts:185 -> 500): errors[o] holds it, and that owner selects nothing
+    const errors = Array.from(r.diff, (d) => (d === -2 ? new RangeError("Invalid count value") : null));
+    return { diff: Array.from(r.diff, (d) => (d === -1 || d === -2 ? null : d)), ids, errors };
   }
   // receive.ts:118-124 over this store as a "__message" mirror: since[o] millis | null -> ids[o][]
   messagesSince(since) {
