@@ -202,3 +202,91 @@ def config5(n_owners: int, n: int, zipf_s: float = 1.2, cells_per_owner: int = 5
     if with_millis:
         return ts, owner.astype(np.uint32), cell.astype(np.uint32), ms
     return ts, owner.astype(np.uint32), cell.astype(np.uint32)
+
+
+NANOID = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789_-", dtype=np.uint8)
+
+# examples/nextjs/pages/index.tsx:23-34 + the common columns (types.ts:194-201)
+TODO_COLUMNS = ("title", "isCompleted", "categoryId", "isDeleted")
+CATEGORY_COLUMNS = ("name", "isDeleted")
+
+
+def config1(n: int = 100_000, n_nodes: int = 3, stride: int = 48, seed_config: int = 1):
+    """BASELINE config 1: one owner's todo app (examples/nextjs schema) as n
+    CrdtMessages, the batch a client merges with applyMessages.
+
+    Mutations (db.ts:268-300 createNewCrdtMessages: an insert appends
+    createdAt + createdBy, an update appends updatedAt), mix 20 % todo insert
+    (title, isCompleted, categoryId), 5 % category insert (name), 75 % update
+    of one column of a random existing row (todo: title / isCompleted /
+    categoryId / isDeleted; category: name / isDeleted).  Each mutation comes
+    from one of n_nodes nodes at `now` += U[0, 20) ms, its messages stamped by
+    that node's sendTimestamp (timestamp.ts:97-123: millis = max(last, now),
+    counter + 1 on a repeat).  Row ids: 21-char nanoid alphabet.  Batch order =
+    send order (the server returns ORDER BY timestamp per sender).
+    Returns (ts arena, cell u32, cells [(table, row, column)], values list)."""
+    rng = rng_for(seed_config)
+    nodes = random_nodes(rng, n_nodes)
+    owner_id = bytes(HEX[rng.integers(0, 16, size=21)]).decode()  # initDbModel.ts:21-22: 21 hex chars
+    node_state = [(0, 0)] * n_nodes
+    todos, cats = [], []
+    cid = {}
+    cells = []
+    millis, counter, nidx, cell, values = [], [], [], [], []
+    now = BENCH_T0
+
+    def rid():
+        return bytes(NANOID[rng.integers(0, 64, size=21)]).decode()
+
+    def iso(ms):
+        return format_timestamps(np.array([ms]), np.array([0]), np.zeros((1, 16), np.uint8) + 48)[0, :24].tobytes().decode()
+
+    while len(millis) < n:
+        now += int(rng.integers(0, 20))
+        node = int(rng.integers(0, n_nodes))
+        u = rng.random()
+        if u < 0.20 or not todos:
+            row = rid()
+            todos.append(row)
+            cat = cats[int(rng.integers(0, len(cats)))] if cats and rng.random() < 0.5 else None
+            msgs = [("todo", row, "title", "todo %d" % len(todos)), ("todo", row, "isCompleted", 0),
+                    ("todo", row, "categoryId", cat), ("todo", row, "createdAt", iso(now)),
+                    ("todo", row, "createdBy", owner_id)]
+        elif u < 0.25:
+            row = rid()
+            cats.append(row)
+            msgs = [("todoCategory", row, "name", "category %d" % len(cats)), ("todoCategory", row, "createdAt", iso(now)),
+                    ("todoCategory", row, "createdBy", owner_id)]
+        else:
+            if cats and rng.random() < 0.2:
+                row, table = cats[int(rng.integers(0, len(cats)))], "todoCategory"
+                col = CATEGORY_COLUMNS[int(rng.integers(0, 2))]
+                val = 1 if col == "isDeleted" else "renamed %d" % len(millis)
+            else:
+                row, table = todos[int(rng.integers(0, len(todos)))], "todo"
+                col = TODO_COLUMNS[int(rng.integers(0, 4))]
+                val = {"title": "edited %d" % len(millis), "isCompleted": int(rng.integers(0, 2)),
+                       "categoryId": cats[int(rng.integers(0, len(cats)))] if cats else None, "isDeleted": 1}[col]
+            msgs = [(table, row, col, val), (table, row, "updatedAt", iso(now))]
+        m, c = node_state[node]
+        for table, row, col, val in msgs:
+            if len(millis) == n:
+                break
+            if now > m:  # sendTimestamp
+                m, c = now, 0
+            else:
+                c += 1
+            key = (table, row, col)
+            k = cid.get(key)
+            if k is None:
+                k = cid[key] = len(cells)
+                cells.append(key)
+            millis.append(m)
+            counter.append(c)
+            nidx.append(node)
+            cell.append(k)
+            values.append(val)
+        node_state[node] = (m, c)
+    ts = format_timestamps(np.array(millis, dtype=np.int64), np.array(counter, dtype=np.int64), nodes[np.array(nidx)],
+                           stride)
+    return ts, np.array(cell, dtype=np.uint32), cells, values
