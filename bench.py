@@ -1,16 +1,25 @@
 """Headline benchmark: CRDT messages merged/sec (LWW + Merkle) on MI355X.
 
-Workload (BASELINE.json configs[1]): one
+Headline (BASELINE.json configs[1]): one
 owner, 10M synthetic CrdtMessages over 1,000 cells (10 tables x 10 rows x 10
-columns), 64 HLC nodes, shuffled batch order.  One step = one
-applyMessages batch (evm_apply_batch: pack + canonical check + murmur3,
-cross-cell PK check, stable cell sort, segmented LWW scan, Merkle fold) with
-the inputs already resident in HBM, starting from an empty tree.
+columns), 64 HLC nodes, shuffled batch order.  One step = one applyMessages
+batch (evm_apply_batch: pack + canonical check + murmur3, cross-cell PK
+check, LWW walks, Merkle fold) with the inputs already resident in HBM,
+starting from an empty tree.
+
+At N = 1 the same line carries two more BASELINE configs under extra keys:
+  "config1": the examples/nextjs todo-schema stream (100k messages, one
+             owner, ~55k cells: the sort path), GPU time + CPU baseline;
+  "config3": the sync server, 100k owners x 1,000 messages, one SyncRequest
+             per owner (apps/server/src/index.ts:204-216: addMessages then
+             getMessages against the client's tree), with its own roofline
+             and CPU baseline (oracle/js/cpu_server.js, 1 and P threads).
 
 Multi-GPU (torchrun, one rank per GPU): weak scaling -- every rank merges its
-own owner's 10M-message batch (owners are independent in applyMessages: each is
-its own client DB), no data-path collective; the elapsed time is the max over
-ranks.  Rank 0 prints one JSON line.
+own owner's 10M-message batch (owners are independent in applyMessages: each
+is its own client DB), no data-path collective; the elapsed time is the max
+over ranks.  `--workload server` runs configs 3/4/5 standalone (RCCL owner
+routing at N > 1).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -46,6 +55,13 @@ ALG_BYTES_PER_MSG = {
     "k_fold_prep": 1 + 4 + 12 + 12,  # flag, pos, (minute, hash, aux) in; (ck, hash) out
 }
 
+# Server path (evm_server.hip), per message N and per new leaf L
+SERVER_ALG = {
+    "k_pack48": (46 + 4 + 32, 0),  # ts + owner in, 32-B record out
+    "k_svo_a<1024>": (4 + 32 + 1 + 28, 8 + 4 + 1),  # perm + record in; flag + new row out; leaf code/xor/dup out
+    "k_svo_b": (28 + 32, 8 + 4 + 1 + 8 + 4),  # new rows in, store rows out; new leaves in, tree leaves out
+}
+SERVER_PIPELINE_BYTES = 127  # the ideal server pipeline, one sort pass
 
 # Kernels that run on the engine's second stream beside the walks (EVM_OPT_OVERLAP):
 # their event durations include time spent sharing the chip, so they are not
@@ -60,35 +76,60 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--messages", type=int, default=10_000_000)
     ap.add_argument("--cells", type=int, default=1000)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0: skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget per leg (0: skip)")
     ap.add_argument("--overlap", type=int, default=1, help="EVM_OPT_OVERLAP: independent checks on a second stream")
     ap.add_argument("--workload", choices=["client", "server"], default="client",
-                    help="client: config 2 applyMessages (headline); server: config 3/4 ingest + diff + select")
+                    help="client: config 2 applyMessages (headline, + config 1 and 3 legs at N=1); "
+                         "server: config 3/4/5 ingest + diff + select alone")
+    ap.add_argument("--extra", type=int, default=1, help="N=1 client run: add the config-1 and config-3 legs")
     ap.add_argument("--owners", type=int, default=100_000, help="server workload: owners per GPU")
     ap.add_argument("--per-owner", type=int, default=1000, help="server workload: messages per owner")
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="server workload: owner sizes Zipf(s) (BASELINE config 5 skew, s = 1.2); owners x per-owner msgs in total")
-    ap.add_argument("--request", type=int, default=100,
+    ap.add_argument("--request", type=int, default=1000,
                     help="server workload: messages per SyncRequest (one owner each, requests in random order); "
+                         ">= per-owner: one request per owner (the reference's per-request sync exactly); "
                          "1 = every message shuffled on its own")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch per kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
-def cpu_baseline(ts_arena, cells, budget_s):
+def host_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    n = os.cpu_count() or 1
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n_aff = n
+    return {"nproc": n, "cpus_usable": n_aff, "cpu_model": model}
+
+
+def node_bin():
+    import shutil
+
+    return shutil.which("node")
+
+
+def cpu_baseline(ts_arena, cells, budget_s, what="config-2"):
     """The reference merge restated in JavaScript (oracle/js/cpu_merge.js:
     timestamp.ts / merkleTree.ts / applyMessages.ts decisions, SQLite
     replaced by Maps) under node on this host, one thread, over the first
-    messages of the same config-2 stream; the Python oracle (verbatim SQL in
-    sqlite3) when node is absent."""
-    import shutil
+    messages of the same stream; the Python oracle (verbatim SQL in sqlite3)
+    when node is absent."""
     import subprocess
     import tempfile
 
     import numpy as np
 
-    node = shutil.which("node")
+    node = node_bin()
     if node is None:
         return cpu_baseline_python(ts_arena, cells, budget_s)
     k = min(len(cells), 2_000_000)
@@ -100,15 +141,15 @@ def cpu_baseline(ts_arena, cells, budget_s):
                               str(budget_s)], check=True, capture_output=True, text=True, timeout=budget_s + 120).stdout
     r = json.loads(out)
     ver = subprocess.run([node, "--version"], capture_output=True, text=True).stdout.strip()
-    return {
+    return dict({
         "value": r["rate"],
         "unit": "msgs/s",
         "cores": 1,
         "kind": "port",
-        "sample": "messages 0..%d of the config-2 stream applied by oracle/js/cpu_merge.js under node %s "
+        "sample": "messages 0..%d of the %s stream applied by oracle/js/cpu_merge.js under node %s "
         "(applyMessages.ts decisions with the SQL as Maps, persistent-spread merkleTree.ts trie, murmur3), "
-        "1 thread, %.1f s" % (r["done"], ver, r["seconds"]),
-    }
+        "1 thread, %.1f s" % (r["done"], what, ver, r["seconds"]),
+    }, **host_info())
 
 
 def cpu_baseline_python(ts_arena, cells, budget_s):
@@ -135,15 +176,73 @@ def cpu_baseline_python(ts_arena, cells, budget_s):
     t0 = time.perf_counter()
     O.apply_messages(db, tree, sample)
     dt = time.perf_counter() - t0
-    return {
+    return dict({
         "value": len(sample) / dt,
         "unit": "msgs/s",
         "cores": 1,
         "kind": "port",
-        "sample": "messages 2000..%d of the config-2 stream applied by oracle/evolu_oracle.py "
+        "sample": "messages 2000..%d of the stream applied by oracle/evolu_oracle.py "
         "(applyMessages.ts control flow, reference SQL verbatim in sqlite3, persistent-spread trie), "
         "1 thread, %.1f s" % (2000 + s, dt),
-    }
+    }, **host_info())
+
+
+def cpu_baseline_server(ts_np, owner_np, budget_s):
+    """apps/server/src/index.ts:121-216 restated in JavaScript
+    (oracle/js/cpu_server.js: per SyncRequest getMerkleTree JSON.parse,
+    INSERT OR IGNORE as a Set + persistent-spread inserts, the tree's
+    JSON.stringify, diffMerkleTrees against the request's tree, the
+    selection) under node: one thread (the reference's one server process)
+    and P worker_threads over disjoint owners.  Sample: the first owners'
+    requests of the same config-3 stream, in batch order."""
+    import subprocess
+    import tempfile
+
+    import numpy as np
+
+    node = node_bin()
+    if node is None:
+        return None
+    hi = host_info()
+    P = max(1, min(hi["cpus_usable"], 16))  # the box's CPU share for one GPU is 16
+    res = {}
+    with tempfile.TemporaryDirectory() as d:
+        for threads in sorted({1, P}):
+            K = 500 * (threads + 1)  # owners in the sample: more than the budget gets through
+            sel = owner_np < K
+            tsf, of = os.path.join(d, "ts%d.bin" % threads), os.path.join(d, "o%d.bin" % threads)
+            np.ascontiguousarray(ts_np[sel, :48]).tofile(tsf)
+            np.ascontiguousarray(owner_np[sel], dtype="<u4").tofile(of)
+            out = subprocess.run([node, os.path.join(ROOT, "oracle", "js", "cpu_server.js"), tsf, of,
+                                  str(int(sel.sum())), str(budget_s), str(threads)], check=True, capture_output=True,
+                                 text=True, timeout=4 * budget_s + 240).stdout
+            res[threads] = json.loads(out)
+    r1 = res[1]
+    out = dict({
+        "value": r1["rate"], "unit": "msgs/s", "cores": 1, "kind": "port",
+        "sample": "the first %d SyncRequests (%d messages, one owner each) of the config-3 stream served by "
+                  "oracle/js/cpu_server.js (index.ts getMerkleTree + addMessages + getMessages; SQL as Maps; "
+                  "persistent-spread trie; murmur3), 1 thread, %.1f s" % (r1["requests"], r1["done"], r1["seconds"]),
+    }, **hi)
+    if P > 1:
+        rp = res[P]
+        out["threads_%d" % P] = {"value": rp["rate"], "cores": P, "requests": rp["requests"], "messages": rp["done"],
+                                 "seconds": rp["seconds"], "sample": "worker_threads over disjoint owners (owner %% %d)" % P}
+    return out
+
+
+def dominant(prof, alg_keys, exclude=()):
+    known = {k: v for k, v in prof.items() if k in alg_keys and k not in exclude}
+    return max(known, key=lambda k: known[k][0])
+
+
+def traffic_of(path, kernel):
+    if not os.path.exists(path):
+        return None
+    t = json.load(open(path)).get(kernel)
+    if t is None:
+        return None
+    return t["bytes"] if isinstance(t, dict) else t  # HBM bytes per launch (PMC, corrected)
 
 
 def main():
@@ -163,7 +262,12 @@ def main():
     from evolu_amd.engine import Engine
 
     if a.workload == "server":
-        return server_main(a, rank, world, local)
+        out = server_run(a, rank, world, local, a.owners, a.per_owner, a.zipf, a.request, cpu=rank == 0 and world == 1)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     # each rank: its own owner (seed per rank), same shape
     ts_np, cell_np = synth.config2(a.messages, a.cells, seed_config=2 + 1000 * rank)
     eng = Engine(local)
@@ -191,8 +295,7 @@ def main():
     torch.cuda.synchronize()
     ms_all_events = (time.perf_counter() - u0) / a.steps * 1e3
     prof = eng.prof_report()
-    known = {k: v for k, v in prof.items() if k in ALG_BYTES_PER_MSG and not (a.overlap and k in SIDE_KERNELS)}
-    dom = max(known, key=lambda k: known[k][0])
+    dom = dominant(prof, ALG_BYTES_PER_MSG, SIDE_KERNELS if a.overlap else ())
     # timed region: events only around the dominant kernel's launches
     eng.prof_only(dom)
     eng.prof_reset()
@@ -241,13 +344,8 @@ def main():
         avg_s = tot_ms / launches / 1e3
         alg = ALG_BYTES_PER_MSG[dom] * a.messages
         achieved = alg / avg_s
-        traffic = None
-        if os.path.exists(a.traffic):
-            t = json.load(open(a.traffic)).get(dom)
-            if t is not None:
-                traffic = t["bytes"] if isinstance(t, dict) else t  # HBM bytes per launch (PMC, corrected)
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "traffic": traffic,
+                "frac": achieved / HBM_PEAK, "traffic": traffic_of(a.traffic, dom),
                 "kernel_ms_avg": avg_s * 1e3, "alg_bytes_per_launch": alg,
                 "kernel_share_of_step": tot_ms / (ms_step * a.steps)}
         out = {
@@ -268,24 +366,75 @@ def main():
                        "parallelism": "owner-sharded, %d rank(s)" % world},
             "roofline": roof,
             "pipeline": {"alg_bytes_per_msg": 120, "ms_per_step_all_kernel_events": ms_all_events,
-                         "host_to_host_ms_per_step": ms_h2h, "host_to_host_msgs_per_s": a.messages / ms_h2h * 1e3, "pipeline_hbm_frac": 120 * a.messages * world / (elapsed / a.steps) / world / HBM_PEAK,
+                         "host_to_host_ms_per_step": ms_h2h, "host_to_host_msgs_per_s": a.messages / ms_h2h * 1e3,
+                         "pipeline_hbm_frac": 120 * a.messages / (elapsed / a.steps) / HBM_PEAK,
                          "kernels_ms_per_step": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}},
             "cpu_baseline": None,
         }
         if world == 1 and a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(ts_np, cell_np, a.cpu_seconds)
+        del ts, cell, flags, ts_h, cell_h
+        if world == 1 and a.extra:
+            out["config1"] = config1_leg(eng, a)
+            eng.close()
+            torch.cuda.empty_cache()
+            out["config3"] = server_run(a, 0, 1, local, 100_000, 1000, 0.0, 1000, cpu=a.cpu_seconds > 0, leg=True)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def server_main(a, rank, world, local):
+def config1_leg(eng, a):
+    """BASELINE config 1: the todo-schema stream (100k messages, one owner),
+    one applyMessages batch from an empty tree, inputs in HBM."""
+    import torch
+
+    from evolu_amd import synth
+
+    ts_np, cell_np, cells, _ = synth.config1(100_000)
+    ts, cell = eng.dev(ts_np), eng.dev(cell_np)
+    empty = eng.tree_new(1)
+    C = len(cells)
+    flags = torch.empty(len(ts_np), dtype=torch.uint8, device=ts.device)
+    winner = torch.empty(C, dtype=torch.int32, device=ts.device)
+
+    def step():
+        eng.apply_batch(empty, ts, cell, C, flags=flags, winner=winner)[2].free()
+
+    for _ in range(a.warmup):
+        step()
+    eng.prof_enable(True)
+    eng.prof_reset()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    prof = eng.prof_report()
+    eng.prof_enable(False)
+    steps = max(a.steps, 20)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    out = {"workload": "config1: examples/nextjs todo schema (index.tsx:23-34, db.ts:268-300 mutation shapes), "
+                       "100000 msgs, 1 owner, %d cells, 3 nodes, send order (evolu_amd/synth.config1)" % C,
+           "value": len(ts_np) / ms * 1e3, "unit": "msgs/s", "ms_per_batch": ms, "steps": steps,
+           "path": "sort path (> 2,048 cells): radix sort by cell + segmented scan",
+           "kernels_ms_per_batch": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:10]},
+           "cpu_baseline": cpu_baseline(ts_np, cell_np, a.cpu_seconds, "config-1") if a.cpu_seconds > 0 else None}
+    return out
+
+
+def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=False, leg=False):
     """Config 3 (1 GPU) / config 4 (N GPUs): server ingest of `owners x
     per_owner` messages per GPU into an empty store, then getMessages for every
     owner against a client tree built from the owner's first 90% of
-    messages.  With N ranks every rank receives messages for random owners
-    of the whole job and routes them to the owner's rank (all_to_all over
-    RCCL); roots are all-gathered.  One step = route + ingest + select + roots."""
+    messages.  With one request per owner per batch (request >= per_owner)
+    this is the reference's per-request sync (index.ts:204-216) exactly.
+    With N ranks every rank receives messages for random owners of the whole
+    job and routes them to the owner's rank (all_to_all over RCCL); roots
+    are all-gathered.  One step = route + ingest + select + roots."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -294,12 +443,13 @@ def server_main(a, rank, world, local):
     from evolu_amd import synth
     from evolu_amd.engine import Engine
 
-    O_total = a.owners * world
-    if a.zipf > 0:
-        ts_np, owner_np, _, millis = synth.config5(a.owners, a.owners * a.per_owner, zipf_s=a.zipf,
+    O_total = owners * world
+    if zipf > 0:
+        ts_np, owner_np, _, millis = synth.config5(owners, owners * per_owner, zipf_s=zipf,
                                                    seed_config=5 + 1000 * rank, with_millis=True)
     else:
-        ts_np, owner_np, millis = synth.config3(a.owners, a.per_owner, seed_config=3 + 1000 * rank, request=a.request)
+        ts_np, owner_np, millis = synth.config3(owners, per_owner, seed_config=3 + 1000 * rank, request=request)
+    ts_local_np, owner_local_np = ts_np, owner_np
     # this rank's owner o is job owner o*world + (o+rank)%world: every rank
     # receives messages for owners living on every rank, no owner on two sources
     o64 = owner_np.astype(np.int64)
@@ -309,7 +459,7 @@ def server_main(a, rank, world, local):
     ts = eng.dev(ts_np)
     owner = torch.from_numpy(owner_np).to(dev)
     # owners too big for one rank (Zipf) are split over the ranks by timestamp hash
-    hot = D.hot_owners(D.owner_counts(owner, O_total), world) if (world > 1 and a.zipf > 0) else None
+    hot = D.hot_owners(D.owner_counts(owner, O_total), world) if (world > 1 and zipf > 0) else None
     omap = D.OwnerMap(O_total, world, rank, hot)
     n_local_owners = omap.n_local
     dest = omap.dest(owner, ts) if world > 1 else None
@@ -326,7 +476,7 @@ def server_main(a, rank, world, local):
     # (the client knows each owner's first 90% by timestamp)
     order = np.lexsort((millis, o64))
     rank_in_owner = np.empty(len(order), dtype=np.int64)
-    counts = np.bincount(o64, minlength=a.owners)
+    counts = np.bincount(o64, minlength=owners)
     rank_in_owner[order] = np.arange(len(order)) - (np.cumsum(counts) - counts)[o64[order]]
     keep_np = (rank_in_owner < (0.9 * counts[o64]).astype(np.int64)).astype(np.uint8)
     if world > 1:  # route the flag with its message (an extra 8-byte column)
@@ -334,14 +484,19 @@ def server_main(a, rank, world, local):
         keep = route(torch.from_numpy(ext).to(dev))[0][:, ts_np.shape[1]].bool()
     else:
         keep = torch.from_numpy(keep_np).to(dev).bool()
-    if a.zipf > 0:  # redeliveries: the client's tree holds each known message once
+    if zipf > 0:  # redeliveries: the client's tree holds each known message once
         first = eng.store_new(n_local_owners)
         ins, _ = first.ingest(ts_r, lown, 0)
         keep &= (ins[: len(ts_r)] & 0x04) != 0
         first.free()
     client = eng.merkle_insert(eng.tree_new(n_local_owners), ts_r[keep].contiguous(), lown[keep].contiguous())
+    client_hot = None
+    if omap.hot.numel():
+        # a split owner's request carries its FULL client tree: merge the ranks' parts
+        client_hot = D.merge_hot_trees(eng, client, omap)
     node = torch.from_numpy(np.frombuffer(b"0123456789abcdef" * n_local_owners, dtype=np.uint8).copy()).to(dev)
     flags = torch.empty(len(ts_r), dtype=torch.uint8, device=dev)
+    id_base = rank << 40  # globally unique message ids (split owners' selections merge across ranks)
 
     def step():
         if world > 1:
@@ -350,32 +505,46 @@ def server_main(a, rank, world, local):
         else:
             t_r, lo = ts_r, lown
         store = eng.store_new(n_local_owners)
-        store.ingest(t_r, lo, 0, flags=flags)
-        diff, off, ids = store.select(client, node)
+        store.ingest(t_r, lo, id_base, flags=flags)
+        if client_hot is None:
+            diff, off, ids = store.select(client, node)
+            nsel = int(ids.numel())
+        else:
+            diff, (off, ids), (hoff, hids) = D.split_get_messages(eng, store, client, client_hot, node, omap)
+            nsel = int(ids.numel()) + int(hids.numel())
         r, p = store.tree().roots()
         if world > 1:
             rt, pt = torch.from_numpy(r).to(dev), torch.from_numpy(p).to(dev)
             D.gather_roots(rt[: omap.per], pt[: omap.per], O_total)
             if omap.hot.numel():
                 D.gather_hot_roots(rt, pt, omap)
+        n_leaves = store.tree().n_leaves
         store.free()
-        return int(ids.numel())
+        return nsel, n_leaves
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    # per-kernel breakdown (untimed): the dominant kernel
+    eng.prof_enable(True)
+    eng.prof_reset()
+    step()
+    torch.cuda.synchronize()
+    prof = eng.prof_report()
+    dom = dominant(prof, SERVER_ALG)
+    eng.prof_only(dom)
+    eng.prof_reset()
     if world > 1:
         dist.barrier()
-    eng.prof_reset()
-    eng.prof_enable(True)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    nsel = 0
+    nsel = n_leaves = 0
     step_ms = []  # per-step wall time (a step ends in a host read-back of the roots, so this adds no sync)
     step_allocs = []  # per-step growth of the engine's allocation counters (steady state: all zero)
     for _ in range(a.steps):
         c0 = eng.stats()
         s0 = time.perf_counter()
-        nsel = step()
+        nsel, n_leaves = step()
         step_ms.append((time.perf_counter() - s0) * 1e3)
         c1 = eng.stats()
         step_allocs.append({k: c1[k] - c0[k] for k in ("workspace_regrows", "scratch_pool_allocs", "block_allocs")})
@@ -383,32 +552,51 @@ def server_main(a, rank, world, local):
             print("step %.2f ms" % step_ms[-1], file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    prof_dom = eng.prof_report()
     eng.prof_enable(False)
+    eng.prof_only(None)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    prof = eng.prof_report()
-    if rank == 0:
-        n = a.owners * a.per_owner
-        ms = elapsed / a.steps * 1e3
-        top = sorted(prof.items(), key=lambda kv: -kv[1][0])[:12]
-        print(json.dumps({
-            "metric": METRIC, "value": world * n * a.steps / elapsed, "unit": "msgs/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u64", "data": "synthetic (seeded HLC streams, SURVEY 8(d) config 3/4)",
-            "config": {"workload": ("server: addMessages + getMessages, %d owners x %d msgs per GPU in requests of %d, "
-                                    "RCCL owner routing" % (a.owners, a.per_owner, a.request)) if a.zipf <= 0 else
-                       ("server config 5: addMessages + getMessages, %d msgs per GPU over %d owners with Zipf(%.2f) sizes, "
-                        "hot owners split over ranks" % (n, a.owners, a.zipf)),
-                       "messages_per_gpu": n, "owners_per_gpu": a.owners,
-                       "selected_rows_rank0": nsel, "parallelism": "owner-sharded, %d rank(s)" % world},
-            "step_ms": [round(x, 3) for x in step_ms],
-            "step_allocs": step_allocs, "engine_stats": eng.stats(),
-            "kernels_ms_per_step": {k: v[0] / a.steps for k, v in top},
-        }), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    n = owners * per_owner
+    ms = elapsed / a.steps * 1e3
+    tot_ms, launches = prof_dom[dom]
+    avg_s = tot_ms / launches / 1e3
+    per_msg, per_leaf = SERVER_ALG[dom]
+    alg = per_msg * n + per_leaf * n_leaves
+    roof = {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(a.traffic, dom), "kernel_ms_avg": avg_s * 1e3,
+            "alg_bytes_per_launch": alg, "alg_bytes": "%d B/msg + %d B/new leaf (%d leaves)" % (per_msg, per_leaf, n_leaves),
+            "kernel_share_of_step": tot_ms / (ms * a.steps)}
+    reqs = "one SyncRequest per owner" if request >= per_owner else "requests of %d" % request
+    out = {
+        "metric": METRIC, "value": world * n * a.steps / elapsed, "unit": "msgs/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic (seeded HLC streams, SURVEY 8(d) config 3/4/5)",
+        "config": {"workload": ("server: addMessages + getMessages, %d owners x %d msgs per GPU, %s, RCCL owner routing"
+                                % (owners, per_owner, reqs)) if zipf <= 0 else
+                   ("server config 5: addMessages + getMessages, %d msgs per GPU over %d owners with Zipf(%.2f) sizes, "
+                    "hot owners split over ranks" % (n, owners, zipf)),
+                   "messages_per_gpu": n, "owners_per_gpu": owners,
+                   "selected_rows_rank0": nsel, "parallelism": "owner-sharded, %d rank(s)" % world},
+        "roofline": roof,
+        "pipeline": {"alg_bytes_per_msg": SERVER_PIPELINE_BYTES,
+                     "pipeline_hbm_frac": SERVER_PIPELINE_BYTES * n / (elapsed / a.steps) / HBM_PEAK,
+                     "kernels_ms_per_step": {k: v[0] for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:14]}},
+        "step_ms": [round(x, 3) for x in step_ms],
+        "step_allocs": step_allocs, "engine_stats": eng.stats(),
+        "cpu_baseline": None,
+    }
+    if leg:
+        for k in ("metric", "n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
+            out.pop(k)
+    eng.close()
+    del ts, owner, ts_r, lown, keep, client, flags
+    torch.cuda.empty_cache()
+    if cpu and a.cpu_seconds > 0 and zipf <= 0:
+        out["cpu_baseline"] = cpu_baseline_server(ts_local_np, owner_local_np, min(a.cpu_seconds, 10.0))
+    return out
 
 
 if __name__ == "__main__":

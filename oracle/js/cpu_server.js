@@ -67,13 +67,19 @@ function diffMerkleTrees(tree1, tree2) {
 }
 const NODE = "0123456789abcdef"; // the requester's nodeId (bench.py's GPU step uses the same)
 
-function load(tsFile, ownerFile, n) {
+// the rows of the owners this thread serves (owner % threads === me), in batch order
+function load(tsFile, ownerFile, n, threads, me) {
   const tsBuf = fs.readFileSync(tsFile);
   const ob = fs.readFileSync(ownerFile);
-  const owner = new Uint32Array(ob.buffer, ob.byteOffset, n);
-  const ts = new Array(n);
-  for (let i = 0; i < n; i++) ts[i] = tsBuf.toString("latin1", 48 * i, 48 * i + 46);
-  return { ts, owner };
+  const all = new Uint32Array(ob.buffer, ob.byteOffset, n);
+  const ts = [];
+  const own = [];
+  for (let i = 0; i < n; i++) {
+    if (all[i] % threads !== me) continue;
+    ts.push(tsBuf.toString("latin1", 48 * i, 48 * i + 46));
+    own.push(all[i]);
+  }
+  return { ts, owner: Uint32Array.from(own) };
 }
 
 // requests (owner runs) of the owners this thread serves; an owner's client
@@ -150,7 +156,7 @@ if (isMainThread) {
   const budget = Number(budgetArg);
   const threads = Math.max(1, Number(thrArg || 1));
   if (threads === 1) {
-    const d = load(tsFile, ownerFile, n);
+    const d = load(tsFile, ownerFile, n, 1, 0);
     const r = serve(d, prepare(d, 1, 0), budget);
     process.stdout.write(JSON.stringify({ ...r, rate: r.done / r.seconds, threads: 1 }) + "\n");
   } else {
@@ -183,7 +189,7 @@ if (isMainThread) {
   }
 } else {
   const w = workerData;
-  const d = load(w.tsFile, w.ownerFile, w.n);
+  const d = load(w.tsFile, w.ownerFile, w.n, w.threads, w.me);
   const p = prepare(d, w.threads, w.me);
   const gate = new Int32Array(w.sab);
   parentPort.postMessage("ready");
