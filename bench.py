@@ -38,7 +38,10 @@ HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 # Algorithmic (compulsory) bytes per message of each kernel on the client path,
 # SURVEY.md section 8(d) accounting, restated per kernel in DESIGN.md.
 ALG_BYTES_PER_MSG = {
-    # streaming fast path (evm_client.hip)
+    # streaming tc path (evm_client.hip TP1-TP3, the default)
+    "k_tp_pack": 46 + 4 + 16,  # ts + cell in; tc 8 + hash 4 + minute 4 out (per-range cell maxima amortised)
+    "k_tp_flags": 8 + 4 + 1,  # tc + cell in, flag out
+    # exact walk path (a batch with a tie)
     "k_cl_pack": 46 + 28,  # ts in; order key 16 + rl 4 + hash 4 + minute 4 out
     "k_cl_scan1": 16 + 4 + 4,  # order key + rl + cell in (per-range aggregates amortised away)
     "k_cl_scan2": 16 + 4 + 4 + 1,  # order key + rl + cell in, flag out

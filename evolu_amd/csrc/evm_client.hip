@@ -964,30 +964,368 @@ __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* 
 }
 
 // ============================================================================
+// tc path (the default streaming path).  Against its cell's running max t, a
+// message's applyMessages decisions need only tc = millis << 16 | counter:
+//     tc_i > tc(t): upsert + XOR        tc_i < tc(t): XOR only
+// and only tc_i == tc(t) needs the node ranks (a tie: equal millis and counter
+// from two nodes, or a redelivery of the cell's current max).  The tc path
+// decides everything from tc and reports ties; a batch with a tie is redone by
+// the exact walk path above (which carries the full order key).
+//   TP1 k_tp_pack : K1 (parse, canonical check, murmur3, minute) + per (range,
+//                   cell) max tc in LDS -- order-free (ds_max_u64), so pass 1
+//                   of the walks disappears into the parse
+//   TP2 carry     : per cell, exclusive max over the ranges seeded with the
+//                   prior max; the cell's final max
+//   TP3 k_tp_flags: per range, in LDS chunks: counting sort of the chunk by
+//                   cell, then each cell's messages in batch order against
+//                   the carried max -> flags; the message that reaches the
+//                   cell's final max is the cell's winner (the last upsert)
+// Bytes per message: TP1 46 + 4 in, 16 out; TP3 12 in, 1 out.
+// ============================================================================
+constexpr u64 TP_INVALID = ~0ull;  // tc of a message the walk skips (invalid timestamp or cell id)
+constexpr int TP_THREADS = 256;
+constexpr int TP_RANGES = 2048;  // ~8 ranges per CU: TP1's occupancy
+constexpr int TPF_CHUNK = 1024;  // rows per TP3 LDS round (4 per thread)
+
+template <bool S48>
+__global__ __launch_bounds__(TP_THREADS) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
+                                                        const u32* __restrict__ cell, u32 C, size_t range_len,
+                                                        u64* __restrict__ tcs, u32* __restrict__ hash,
+                                                        u32* __restrict__ minute, u64* __restrict__ agg,
+                                                        Info* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) u64 cmax[];  // [C] max tc per cell of this range
+  __shared__ uint4 stage[TP_THREADS / 64][192];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const size_t g = blockIdx.x;
+  const size_t beg = g * range_len, end = min(n, beg + range_len);
+  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) cmax[c] = 0;
+  __syncthreads();
+  u32 bad = 0, aux_bad = 0, mn = 0xffffffffu, mx = 0;
+  for (size_t first = beg + 64 * wv; first < end; first += TP_THREADS) {  // wave-uniform
+    uint4 a, b, c;
+    clp_fetch<S48>(ts, stride, end, first, a, b, c);
+    const size_t i = first + lane;
+    u32 w[12];
+    if (S48) {
+      stage[wv][lane] = a;
+      stage[wv][lane + 64] = b;
+      stage[wv][lane + 128] = c;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const uint4 x = stage[wv][3 * lane], y = stage[wv][3 * lane + 1], z = stage[wv][3 * lane + 2];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+      w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+      w[8] = z.x; w[9] = z.y; w[10] = z.z; w[11] = z.w & 0xffffu;
+    } else {
+      w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+      w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+      w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
+    }
+    const Parsed p = parse_ts46(w);  // (the node ranks it can compute are dead here)
+    const bool valid = (p.meta & EVM_META_VALID) != 0;
+    if (i < end) {
+      const u32 ci = __builtin_nontemporal_load(cell + i);
+      const bool ok = valid && ci < C;
+      __builtin_nontemporal_store(ok ? p.tc : TP_INVALID, tcs + i);
+      if (ok) atomicMax(&cmax[ci], p.tc);
+      bad |= valid ? 0u : 1u;
+      aux_bad |= ci < C ? 0u : 1u;
+    }
+    if (S48 && first + 64 <= end && (first & 3) == 0) {
+      // hash / minute of the wave's 64 rows as 16-B-per-lane stores (32 lanes)
+      u32* st32 = reinterpret_cast<u32*>(&stage[wv][0]);
+      st32[lane] = p.hash;
+      st32[64 + lane] = p.minute;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (lane < 32) {
+        const uint4 v = stage[wv][lane];
+        u32* dst = lane < 16 ? hash : minute;
+        reinterpret_cast<uint4*>(dst + first)[lane & 15] = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    } else if (i < end) {
+      hash[i] = p.hash;
+      minute[i] = p.minute;
+    }
+    mn = min(mn, valid ? p.minute : 0xffffffffu);
+    mx = max(mx, valid ? p.minute : 0u);
+  }
+  if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
+  __syncthreads();
+  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) agg[g * C + c] = cmax[c];
+  block_fold_bounds<u32, TP_THREADS>(mn, mx, bad, &info->minute_min, &info->minute_max, &info->bad);
+}
+
+// TP2: per cell, exclusive max over the G range maxima (3 phases over
+// CARRY_SEGS segments), seeded with the prior max; tfinal = the cell's max.
+__global__ void k_tp_carry_reduce(u32 C, size_t G, const u64* __restrict__ agg, u64* __restrict__ s_max) {
+  const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
+  if (c >= C) return;
+  const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
+  const size_t a = p * per, e = min(G, a + per);
+  u64 m = 0;
+#pragma unroll 8
+  for (size_t g = a; g < e; ++g) m = max(m, agg[g * C + c]);
+  s_max[(size_t)p * C + c] = m;
+}
+
+__global__ __launch_bounds__(256) void k_tp_carry_segs(u32 C, u64* __restrict__ s_max,
+                                                       const evm_rec* __restrict__ prior,
+                                                       const uint8_t* __restrict__ prior_present,
+                                                       u64* __restrict__ tfinal) {
+  const u32 c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  const size_t o = (size_t)lane * C + c;
+  u64 v = s_max[o];
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u64 u = __shfl_up(v, d, 64);
+    if ((int)lane >= d) v = max(v, u);
+  }
+  const u64 seed = (prior_present && prior_present[c]) ? prior[c].tc : 0ull;
+  const u64 ex = __shfl_up(v, 1, 64);
+  s_max[o] = max(seed, lane == 0 ? 0ull : ex);
+  if (lane == 63) tfinal[c] = max(seed, v);
+}
+
+__global__ void k_tp_carry_down(u32 C, size_t G, u64* __restrict__ agg, const u64* __restrict__ s_max) {
+  const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
+  if (c >= C) return;
+  const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
+  const size_t a = p * per, e = min(G, a + per);
+  u64 run = s_max[(size_t)p * C + c];
+#pragma unroll 8
+  for (size_t g = a; g < e; ++g) {
+    const u64 here = agg[g * C + c];
+    agg[g * C + c] = run;
+    run = max(run, here);
+  }
+}
+
+// TP3: one workgroup per range, in chunks of TPF_CHUNK rows (wave w takes
+// rows [256w, 256w + 256) of the chunk, 64 per round).
+//   1 stable counting sort by cell: a row's rank among its wave's earlier rows
+//     of the same cell = the wave's count so far (per-wave LDS counters) + the
+//     lower peers of its round (cell ballots); one scan over (cell, wave)
+//     turns the counts into positions: ord = the rows in (cell, batch) order
+//   2 segmented max-scan over ord (segment = cell; value = tc, the segment
+//     head bit in bit 63 -- a valid tc is < 2^63): the exclusive max of each
+//     row's earlier same-cell rows; with the cell's carried max that is tc(t)
+//   3 flags; the carried max of each cell moves to its last row's inclusive max
+// No serial per-cell loop: a hot cell costs what a cold one does.
+struct SegMaxOp {  // (head:1 | max:63), segmented max
+  static __device__ __forceinline__ u64 id() { return 0ull; }
+  __device__ __forceinline__ u64 operator()(u64 a, u64 b) const {
+    constexpr u64 H = 1ull << 63, M = H - 1;
+    return (b & H) ? b : (max(a & M, b & M) | (a & H));
+  }
+};
+
+__global__ __launch_bounds__(TP_THREADS) void k_tp_flags(const u64* __restrict__ tcs, const u32* __restrict__ cell,
+                                                         size_t n, u32 C, int cbits, size_t range_len,
+                                                         const u64* __restrict__ carry, const u64* __restrict__ tfinal,
+                                                         uint8_t* __restrict__ flags, int32_t* __restrict__ winner,
+                                                         Info* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) u64 tp_lds[];
+  constexpr int W = TP_THREADS / 64;
+  u64* T = tp_lds;                                               // [C] running max of each cell
+  u64* ctc = T + C;                                              // [CHUNK] the chunk's tc
+  u32* cntw = reinterpret_cast<u32*>(ctc + TPF_CHUNK);           // [W][C] per-wave counts -> positions
+  uint16_t* ccell = reinterpret_cast<uint16_t*>(cntw + W * C);   // [CHUNK] cell of a row, 0xffff = skip
+  uint16_t* ord = ccell + TPF_CHUNK;                             // [CHUNK] rows in (cell, batch) order
+  uint8_t* fl = reinterpret_cast<uint8_t*>(ord + TPF_CHUNK);     // [CHUNK] flags of the rows
+  __shared__ u64 tmp64[TP_THREADS / 64 + 1];
+  __shared__ u32 tmp32[TP_THREADS / 64 + 1];
+  __shared__ u64 xchg[TP_THREADS];
+  constexpr int PER = TPF_CHUNK / TP_THREADS;  // rows per thread, and ord entries per thread
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const u64 lt = lanemask_lt();
+  const size_t g = blockIdx.x;
+  const size_t beg = g * range_len, end = min(n, beg + range_len);
+  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) T[c] = carry[g * C + c];
+  u32 tie = 0;
+  const u32 cper = (C + TP_THREADS - 1) / TP_THREADS;  // cells per thread in the position scan
+  for (size_t base = beg; base < end; base += TPF_CHUNK) {
+    const u32 m = (u32)min((size_t)TPF_CHUNK, end - base);
+    for (u32 k = threadIdx.x; k < W * C; k += TP_THREADS) cntw[k] = 0;
+    __syncthreads();
+    // 1a: load, stable rank inside the wave's quarter
+    u32 rk[PER], rc[PER];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const u32 j = wv * (TPF_CHUNK / W) + r * 64 + lane;
+      bool ok = false;
+      u32 ci = 0;
+      if (j < m) {
+        const u64 x = __builtin_nontemporal_load(tcs + base + j);
+        ci = __builtin_nontemporal_load(cell + base + j);
+        ok = x != TP_INVALID;
+        ctc[j] = x;
+        ccell[j] = ok ? (uint16_t)ci : (uint16_t)0xffff;
+        fl[j] = ok ? 0 : (uint8_t)EVM_MSG_BAD;
+      }
+      const u64 peers = match_cell(ci, ok, cbits);
+      u32 before = 0;
+      if (ok) before = cntw[wv * C + ci];
+      if (ok && (peers >> lane) == 1ull) cntw[wv * C + ci] = before + (u32)__popcll(peers);  // last peer
+      rk[r] = before + (u32)__popcll(peers & lt);
+      rc[r] = ok ? ci : 0xffffffffu;
+    }
+    __syncthreads();
+    // 1b: positions: exclusive scan over (cell, wave), cell-major
+    u32 mv;
+    {
+      u32 loc = 0;
+      for (u32 k = 0; k < cper; ++k) {
+        const u32 c = threadIdx.x * cper + k;
+        if (c < C)
+          for (int w = 0; w < W; ++w) loc += cntw[w * C + c];
+      }
+      u32 run = block_inclusive_scan<u32>(loc, tmp32, OpAdd<u32>(), &mv) - loc;
+      for (u32 k = 0; k < cper; ++k) {
+        const u32 c = threadIdx.x * cper + k;
+        if (c < C)
+          for (int w = 0; w < W; ++w) {
+            const u32 v = cntw[w * C + c];
+            cntw[w * C + c] = run;
+            run += v;
+          }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const u32 j = wv * (TPF_CHUNK / W) + r * 64 + lane;
+      if (rc[r] != 0xffffffffu) ord[cntw[wv * C + rc[r]] + rk[r]] = (uint16_t)j;
+    }
+    __syncthreads();
+    // 2: segmented max-scan over ord[0, mv); thread t owns entries [PER t, PER t + PER)
+    constexpr u64 HEAD = 1ull << 63;
+    u64 v[PER];
+    u32 cc[PER];
+    u64 agg = 0;
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const u32 k = PER * threadIdx.x + r;
+      cc[r] = 0xffffffffu;
+      v[r] = 0;
+      if (k < mv) {
+        const u32 j = ord[k];
+        cc[r] = ccell[j];
+        const bool head = k == 0 || ccell[ord[k - 1]] != cc[r];
+        v[r] = ctc[j] | (head ? HEAD : 0ull);
+        agg = SegMaxOp()(agg, v[r]);
+      }
+    }
+    xchg[threadIdx.x] = block_inclusive_scan<u64>(agg, tmp64, SegMaxOp(), (u64*)nullptr);
+    __syncthreads();
+    u64 e = threadIdx.x ? xchg[threadIdx.x - 1] : 0ull;  // the entries before this thread's
+    // 3: flags (reads T); each segment end keeps its cell's new max
+    u64 newT[PER];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const u32 k = PER * threadIdx.x + r;
+      newT[r] = 0;
+      if (k >= mv) continue;
+      const u32 c = cc[r];
+      const u64 x = v[r] & ~HEAD;
+      const u64 t = max(T[c], (v[r] & HEAD) ? 0ull : (e & ~HEAD));
+      uint8_t f;
+      if (x > t) {  // applyMessages.ts:93 and :105 both hold
+        f = EVM_MSG_UPS | EVM_MSG_XOR;
+        if (x == tfinal[c]) winner[c] = (int32_t)(base + ord[k]);  // reaches the final max: the last upsert
+      } else if (x < t) {  // :105 only (a stale redelivery re-XORs)
+        f = EVM_MSG_XOR;
+      } else {  // equal tc: the node ranks decide -> the exact path
+        f = 0;
+        tie = 1;
+      }
+      fl[ord[k]] = f;
+      e = SegMaxOp()(e, v[r]);
+      if (k + 1 == mv || ccell[ord[k + 1]] != c) newT[r] = max(t, e & ~HEAD) | HEAD;  // segment end
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < PER; ++r)
+      if (newT[r] & HEAD) T[cc[r]] = newT[r] & ~HEAD;
+    __syncthreads();
+    // flags out: 4 consecutive rows per thread (base is a multiple of 4)
+    const u32 j4 = 4 * threadIdx.x;
+    if (j4 + 4 <= m) {
+      reinterpret_cast<u32*>(flags + base)[threadIdx.x] = reinterpret_cast<const u32*>(fl)[threadIdx.x];
+    } else {
+      for (u32 j = j4; j < m; ++j) flags[base + j] = fl[j];
+    }
+    __syncthreads();
+  }
+  if (__ballot(tie) && lane == 0) atomic_or_if(&info->ties, 1u);
+}
+
+// ============================================================================
 // Host drivers
 // ============================================================================
-static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree_in, const char* ts, size_t stride,
-                      size_t n, const u32* cell, u32 C, const evm_rec* prior, const uint8_t* prior_present,
-                      const Stored& stored, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+// The streaming paths.  TC: the tc path (TP1-TP3); otherwise the exact walk
+// path (K1 + pass 1 + carry + pass 2 over the full order key).  Both share
+// the cross-cell check, the Merkle fold and the status handling.  The tc
+// path returns TP_REDO when it met a tie (the caller reruns the exact path).
+constexpr int TP_REDO = -100;
+
+template <bool TC>
+static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree_in, const char* ts, size_t stride,
+                        size_t n, const u32* cell, u32 C, const evm_rec* prior, const uint8_t* prior_present,
+                        const Stored& stored, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
   int st;
-  size_t range = (n + CL_RANGE_TARGET - 1) / CL_RANGE_TARGET;
-  range = std::max<size_t>(2048, (range + 255) / 256 * 256);
-  const size_t G = (n + range - 1) / range;
   const int cbits = C > 1 ? 32 - __builtin_clz(C - 1) : 0;
-  uint4* key = S.alloc<uint4>(n);
-  u32* rl = S.alloc<u32>(n);
+  const bool s48 = stride == 48 && ((uintptr_t)ts & 15) == 0;
   u32* hash = S.alloc<u32>(n);
   u32* minute = S.alloc<u32>(n);
-  u64* a_tc = S.alloc<u64>(G * C);
-  u64* a_rh = S.alloc<u64>(G * C);
-  u32* a_rl = S.alloc<u32>(G * C);
-  u32* a_first = S.alloc<u32>(G * C);
-  if (!key || !rl || !hash || !minute || !a_tc || !a_rh || !a_rl || !a_first) return EVM_ENOMEM;
-  // K1: parse, canonical check, murmur3, minute -- at full occupancy
-  {
+  if (!hash || !minute) return EVM_ENOMEM;
+  // TC: ranges of TP1/TP3 (multiples of 256 rows); walk path: ranges of the walks
+  size_t range, G;
+  if (TC) {
+    range = std::max<size_t>(1024, ((n + TP_RANGES - 1) / TP_RANGES + 255) / 256 * 256);
+  } else {
+    range = (n + CL_RANGE_TARGET - 1) / CL_RANGE_TARGET;
+    range = std::max<size_t>(2048, (range + 255) / 256 * 256);
+  }
+  G = (n + range - 1) / range;
+  uint4* key = nullptr;
+  u32* rl = nullptr;
+  u64* tcs = nullptr;
+  u64* agg = nullptr;
+  u64* a_tc = nullptr;
+  u64* a_rh = nullptr;
+  u32* a_rl = nullptr;
+  u32* a_first = nullptr;
+  if (TC) {
+    tcs = S.alloc<u64>(n);
+    agg = S.alloc<u64>(G * C);
+    if (!tcs || !agg) return EVM_ENOMEM;
+    // TP1: parse + per (range, cell) max tc, one workgroup per range
+    evm::ProfScope ps_(ctx, "k_tp_pack");
+    const size_t lds = (size_t)C * 8;
+    if (s48)
+      hipLaunchKernelGGL(k_tp_pack<true>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
+                         cell, C, range, tcs, hash, minute, agg, info);
+    else
+      hipLaunchKernelGGL(k_tp_pack<false>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
+                         cell, C, range, tcs, hash, minute, agg, info);
+  } else {
+    key = S.alloc<uint4>(n);
+    rl = S.alloc<u32>(n);
+    a_tc = S.alloc<u64>(G * C);
+    a_rh = S.alloc<u64>(G * C);
+    a_rl = S.alloc<u32>(G * C);
+    a_first = S.alloc<u32>(G * C);
+    if (!key || !rl || !a_tc || !a_rh || !a_rl || !a_first) return EVM_ENOMEM;
+    // K1: parse, canonical check, murmur3, minute -- at full occupancy
     evm::ProfScope ps_(ctx, "k_cl_pack");
     const dim3 g(std::min<size_t>((n + 255) / 256, 2048));  // (8192 measured 5 % slower inside the pipeline)
-    if (stride == 48 && ((uintptr_t)ts & 15) == 0)
+    if (s48)
       hipLaunchKernelGGL(k_cl_pack<true>, g, dim3(CLP_THREADS), 0, ctx->stream, (const uint8_t*)ts, stride, n, key,
                          rl, hash, minute, info);
     else
@@ -1022,25 +1360,40 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
                          (const uint8_t*)ts, stride, cell, info);
     }
   }
-  // pass 1: per range and cell, the max timestamp and its first index
-  KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
-              a_first, info);
-  // carry: per cell, exclusive scan over ranges seeded with the prior max
-  {
-    u64* s_tc = S.alloc<u64>((size_t)CARRY_SEGS * C);
-    u64* s_rh = S.alloc<u64>((size_t)CARRY_SEGS * C);
-    u32* s_rl = S.alloc<u32>((size_t)CARRY_SEGS * C);
-    u32* s_first = S.alloc<u32>((size_t)CARRY_SEGS * C);
-    if (!s_tc || !s_rh || !s_rl || !s_first) return EVM_ENOMEM;
+  if (TC) {
+    // TP2: per cell, exclusive max over the ranges (in place in agg) + final max
+    u64* s_max = S.alloc<u64>((size_t)CARRY_SEGS * C);
+    u64* tfinal = S.alloc<u64>(C);
+    if (!s_max || !tfinal) return EVM_ENOMEM;
     const u32 cb = (C + 63) / 64;
-    KLAUNCH(k_cl_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh, s_rl,
-            s_first);
-    KLAUNCH(k_cl_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_tc, s_rh, s_rl, s_first, prior, prior_present, winner);
-    KLAUNCH(k_cl_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh,
-            s_rl);
+    KLAUNCH(k_tp_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, (const u64*)agg, s_max);
+    KLAUNCH(k_tp_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_max, prior, prior_present, tfinal);
+    KLAUNCH(k_tp_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, agg, (const u64*)s_max);
+    // TP3: flags + winners
+    const size_t lds = (size_t)C * 8 + TPF_CHUNK * 8 + (size_t)(TP_THREADS / 64) * C * 4 + TPF_CHUNK * 5;
+    KLAUNCH_LDS(k_tp_flags, dim3(G), dim3(TP_THREADS), lds, (const u64*)tcs, cell, n, C, cbits, range,
+                (const u64*)agg, (const u64*)tfinal, flags, winner, info);
+  } else {
+    // pass 1: per range and cell, the max timestamp and its first index
+    KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
+                a_first, info);
+    // carry: per cell, exclusive scan over ranges seeded with the prior max
+    {
+      u64* s_tc = S.alloc<u64>((size_t)CARRY_SEGS * C);
+      u64* s_rh = S.alloc<u64>((size_t)CARRY_SEGS * C);
+      u32* s_rl = S.alloc<u32>((size_t)CARRY_SEGS * C);
+      u32* s_first = S.alloc<u32>((size_t)CARRY_SEGS * C);
+      if (!s_tc || !s_rh || !s_rl || !s_first) return EVM_ENOMEM;
+      const u32 cb = (C + 63) / 64;
+      KLAUNCH(k_cl_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh, s_rl,
+              s_first);
+      KLAUNCH(k_cl_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_tc, s_rh, s_rl, s_first, prior, prior_present, winner);
+      KLAUNCH(k_cl_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh,
+              s_rl);
+    }
+    KLAUNCH_LDS(k_cl_scan2, dim3(G), dim3(WK_THREADS), (size_t)C * 20, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
+                flags);
   }
-  KLAUNCH_LDS(k_cl_scan2, dim3(G), dim3(WK_THREADS), (size_t)C * 20, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
-              flags);
   // Merkle fold
   u32* px = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN);
   u32* pp = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32));
@@ -1083,6 +1436,7 @@ static int apply_fast(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree
     return EVM_ENONCANON;
   }
   if (hi.bad_aux) return EVM_EINVAL;
+  if (TC && hi.ties) return TP_REDO;  // a tie: the node ranks decide -- the exact walk path redoes the batch
   if (!hi.collision && hi.xc_oversize) {
     // a hash bucket overflowed LDS (heavy skew): exact check on the global epoch-tagged set
     const int lg = std::max(ceil_log2(n + n / 2 + 1), 10);
@@ -1220,24 +1574,41 @@ int evm_apply_batch_ex(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
     Info* info = S.alloc<Info>(1);
     evm_rec* prior = S.alloc<evm_rec>(std::max<size_t>(n_cells, 1));
     if (!info || !prior) return EVM_ENOMEM;
-    // one launch: the status record, and winner = -1 for every cell
-    KLAUNCH(k_apply_init, dim3(grid_for(std::max<size_t>(n_cells, 1), 256)), dim3(256), info, info_init(), winner,
-            (size_t)n_cells);
-    if (prior_present && n_cells) {
-      // the cells' current maxima (SELECT ... ORDER BY timestamp DESC LIMIT 1)
-      if ((st = launch_pack(ctx, prior_ts, prior_stride, n_cells, nullptr, 0, prior, nullptr))) return st;
-      KLAUNCH(k_prior_check, dim3((n_cells + 255) / 256), dim3(256), prior, prior_present, n_cells, info);
-    }
+    // one launch: the status record, and winner = -1 for every cell; the
+    // cells' current maxima (SELECT ... ORDER BY timestamp DESC LIMIT 1)
+    auto init = [&]() -> int {
+      KLAUNCH(k_apply_init, dim3(grid_for(std::max<size_t>(n_cells, 1), 256)), dim3(256), info, info_init(), winner,
+              (size_t)n_cells);
+      if (prior_present && n_cells) {
+        int e = launch_pack(ctx, prior_ts, prior_stride, n_cells, nullptr, 0, prior, nullptr);
+        if (e) return e;
+        KLAUNCH(k_prior_check, dim3((n_cells + 255) / 256), dim3(256), prior, prior_present, n_cells, info);
+      }
+      return EVM_OK;
+    };
+    if ((st = init())) return st;
+    const int path = ctx->client_path;
     if (n == 0) {
       Info hi;
       if ((st = read_info(ctx, info, &hi))) return st;
       if (hi.bad) return EVM_ENONCANON;
       st = merge_into_tree(ctx, S, tree_in, tree_in->n_owners, nullptr, nullptr, 0, tree_out);
-    } else if (ctx->client_path == 1 ||
-               (ctx->client_path == 0 && !cell_owner && n_cells <= CL_MAX_CELLS)) {
+    } else if (path == 1 || path == 3 || (path == 0 && !cell_owner && n_cells <= CL_MAX_CELLS)) {
       if (cell_owner || n_cells > CL_MAX_CELLS) return EVM_EINVAL;
-      st = apply_fast(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, prior, prior_present, stored, flags, winner,
-                      tree_out);
+      st = TP_REDO;
+      if (path != 1) {
+        Scratch S2(ctx);  // released before a rerun
+        st = apply_stream<true>(ctx, S2, info, tree_in, ts, stride, n, cell, n_cells, prior, prior_present, stored,
+                                flags, winner, tree_out);
+        if (st == TP_REDO) ++ctx->stats.tc_redos;
+        else if (st == EVM_OK) ++ctx->stats.tc_batches;
+      }
+      if (st == TP_REDO) {
+        // a tie (equal millis and counter in one cell): the exact walk path
+        if (path != 1 && (st = init())) return st;
+        st = apply_stream<false>(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, prior, prior_present, stored,
+                                 flags, winner, tree_out);
+      }
     } else {
       st = apply_general(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, cell_owner, prior, prior_present, stored,
                          flags, winner, tree_out);

@@ -785,7 +785,7 @@ int evm_sync(evm_ctx* ctx) {
 
 int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
   if (!ctx) return EVM_EINVAL;
-  if (option == EVM_OPT_CLIENT_PATH && value >= 0 && value <= 2) {
+  if (option == EVM_OPT_CLIENT_PATH && value >= 0 && value <= 3) {
     ctx->client_path = (int)value;
     return EVM_OK;
   }

@@ -78,7 +78,7 @@ struct Info {
   u32 fold_overflow;  // dense minute fold not applicable (range too wide / mixed key lengths)
   u32 n_leaves;       // leaves produced by the dense fold
   u32 xc_oversize;    // a hash bucket of the cross-cell check overflowed LDS
-  u32 pad_;
+  u32 ties;           // tc path: a message's tc equals its cell's running max (node ranks decide)
 };
 
 inline Info info_init() {
@@ -94,7 +94,7 @@ inline Info info_init() {
   h.fold_overflow = 0;
   h.n_leaves = 0;
   h.xc_oversize = 0;
-  h.pad_ = 0;
+  h.ties = 0;
   return h;
 }
 

@@ -97,13 +97,15 @@ typedef struct evm_stats {
   uint64_t scratch_pool_bytes;
   uint64_t block_allocs;        /* device blocks allocated for trees and stores (freed ones are reused) */
   uint64_t block_bytes;
+  uint64_t tc_batches;          /* evm_apply_batch calls the streaming tc path finished */
+  uint64_t tc_redos;            /* ... that met a tie and were redone by the exact walk path */
 } evm_stats;
 int evm_get_stats(const evm_ctx* ctx, evm_stats* out);
 int evm_set_stream(evm_ctx* ctx, void* hip_stream); /* NULL: the HIP default stream; initially the context's own */
 void* evm_get_stream(evm_ctx* ctx);
 int evm_sync(evm_ctx* ctx);
 /* tuning / test knobs */
-#define EVM_OPT_CLIENT_PATH 1 /* evm_apply_batch: 0 auto, 1 force the streaming path, 2 force the sort path */
+#define EVM_OPT_CLIENT_PATH 1 /* evm_apply_batch: 0 auto (streaming tc path, exact walk on a tie), 1 exact walk path, 2 sort path, 3 tc path (exact walk on a tie) */
 #define EVM_OPT_OVERLAP 3     /* 1 (default): independent checks run on a second HIP stream inside a call; 0: one stream */
 #define EVM_OPT_SERVER_PATH 2 /* evm_server_ingest: 0/1 per-owner LDS path where every owner's share fits, 2 force the sort path */
 #define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 0 histogram + scan + scatter per pass */

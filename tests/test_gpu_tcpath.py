@@ -1,0 +1,212 @@
+"""The streaming tc path of applyMessages (evm_client.hip TP1-TP3, the default
+for one owner with <= 2,048 cells): decisions from tc = millis << 16 |
+counter alone, a batch with a tie (equal tc against its cell's running max:
+equal millis + counter from two nodes, or a redelivery of the cell's max) redone
+by the exact walk path.  Checked against the oracle (applyMessages.ts:26-131,
+verbatim SQL) and, at BASELINE sizes, bit for bit against the sort path."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import evolu_oracle as O
+from tests import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from evolu_amd.engine import Engine
+
+    e = Engine(0)
+    yield e
+    e.set_option(1, 0)
+    e.close()
+
+
+def _has_tie(msgs, prior=None):
+    """Some message's tc equals its cell's running max tc (node ranks decide)."""
+    run = dict(prior or {})
+    for m in msgs:
+        c = (m["table"], m["row"], m["column"])
+        ms, ctr, _ = O.parse_canonical(m["timestamp"])
+        tc = (ms << 16) | ctr
+        t = run.get(c)
+        if t is not None and tc == t:
+            return True
+        if t is None or tc > t:
+            run[c] = tc
+    return False
+
+
+def _apply(eng, msgs, cells, path, prior=None, tree_json="{}"):
+    from evolu_amd import _lib as L
+
+    cid = {c: i for i, c in enumerate(cells)}
+    cell = np.array([cid[(m["table"], m["row"], m["column"])] for m in msgs], dtype=np.uint32)
+    kw = {}
+    if prior is not None:
+        kw["prior_ts"] = eng.timestamps([prior.get(c, "") for c in cells])
+        kw["prior_present"] = eng.dev(np.array([c in prior for c in cells], dtype=np.uint8))
+    eng.set_option(L.OPT_CLIENT_PATH, path)
+    s0 = eng.stats()
+    flags, winner, tree, st = eng.apply_batch(eng.tree_from_json([tree_json]),
+                                              eng.timestamps([m["timestamp"] for m in msgs]), eng.dev(cell),
+                                              len(cells), raise_on_error=False, **kw)
+    s1 = eng.stats()
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    ran = {"tc": s1["tc_batches"] - s0["tc_batches"], "redo": s1["tc_redos"] - s0["tc_redos"]}
+    return st, flags.cpu().numpy(), winner.cpu().numpy(), tree, ran
+
+
+def _oracle(msgs, cells, prior=None):
+    db = O.ClientDb()
+    tree = {}
+    if prior:
+        # the prior rows: one message per cell holding that cell's max
+        tree = O.apply_messages(db, {}, [{"timestamp": t, "table": c[0], "row": c[1], "column": c[2], "value": "p"}
+                                         for c, t in prior.items()])
+    dec = []
+    want = O.apply_messages(db, tree, msgs, dec)
+    flags = np.array([(1 if u else 0) | (2 if x else 0) for u, x, _ in dec], dtype=np.uint8)
+    last = {}
+    for i, m in enumerate(msgs):
+        if dec[i][0]:
+            last[(m["table"], m["row"], m["column"])] = i
+    return flags, np.array([last.get(c, -1) for c in cells]), want, tree
+
+
+def _distinct_batch(seed, n=3000, n_cells=40, nodes=6):
+    """Timestamps with distinct (millis, counter): no tie possible."""
+    rng = random.Random(seed)
+    node_ids = [W.node_id(rng, upper=(k % 2 == 1)) for k in range(nodes)]
+    ms = rng.sample(range(W.T0, W.T0 + 3600_000 * 24), n)
+    cells = [("t%d" % (i % 3), "r%d" % (i // 3), "c") for i in range(n_cells)]
+    msgs = [{"timestamp": O.timestamp_to_string(m, rng.randrange(3), rng.choice(node_ids)),
+             "table": cells[k][0], "row": cells[k][1], "column": cells[k][2], "value": i}
+            for i, (m, k) in enumerate(zip(ms, [rng.randrange(n_cells) for _ in range(n)]))]
+    # stale redeliveries (older than the cell's max): XOR toggles, still no tie
+    for _ in range(200):
+        i = rng.randrange(len(msgs))
+        msgs.insert(rng.randrange(i, len(msgs)) + 1, dict(msgs[i]))
+    return msgs, cells
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_tc_path_without_ties_vs_oracle(eng, seed):
+    msgs, cells = _distinct_batch(seed)
+    tie = _has_tie(msgs)
+    st, flags, winner, tree, ran = _apply(eng, msgs, cells, 3)
+    f, w, want, _ = _oracle(msgs, cells)
+    assert st == 0
+    assert np.array_equal(flags, f) and np.array_equal(winner, w)
+    assert tree.to_json(0) == O.merkle_tree_to_string(want)
+    assert ran == ({"tc": 0, "redo": 1} if tie else {"tc": 1, "redo": 0})
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_tc_path_with_ties_and_case_vs_oracle(eng, seed):
+    """Equal millis across nodes, mixed-case node ids, exact + stale
+    redeliveries: the tie is detected and the exact path answers."""
+    msgs, cells = W.client_batch(700 + seed, n=800, n_cells=7)
+    st, flags, winner, tree, ran = _apply(eng, msgs, cells, 0)
+    f, w, want, _ = _oracle(msgs, cells)
+    assert st == 0
+    assert np.array_equal(flags, f) and np.array_equal(winner, w)
+    assert tree.to_json(0) == O.merkle_tree_to_string(want)
+    assert ran["redo"] == (1 if _has_tie(msgs) else 0)
+
+
+def test_tc_path_prior_rows(eng):
+    """Prior maxima: below, above and equal (an exact redelivery of the prior)."""
+    msgs, cells = _distinct_batch(11, n=1500, n_cells=30)
+    rng = random.Random(3)
+    prior = {}
+    for c in cells[:20]:
+        mine = [m["timestamp"] for m in msgs if (m["table"], m["row"], m["column"]) == c]
+        ms, ctr, node = O.parse_canonical(rng.choice(mine))
+        prior[c] = O.timestamp_to_string(ms + rng.choice([-1, 1]) * rng.randrange(1, 5000), ctr, node)
+    ptc = {c: (O.parse_canonical(t)[0] << 16) | O.parse_canonical(t)[1] for c, t in prior.items()}
+    _, _, _, t0 = _oracle([], cells, prior)
+    st, flags, winner, tree, ran = _apply(eng, msgs, cells, 3, prior=prior, tree_json=O.merkle_tree_to_string(t0))
+    f, w, want, _ = _oracle(msgs, cells, prior)
+    assert st == 0 and np.array_equal(flags, f) and np.array_equal(winner, w)
+    assert ran["tc"] + ran["redo"] == 1 and ran["redo"] == int(_has_tie(msgs, ptc))
+    assert tree.to_json(0) == O.merkle_tree_to_string(want)
+    # an exact redelivery of a prior max is a tie
+    c0 = cells[0]
+    msgs2 = msgs + [{"timestamp": prior[c0], "table": c0[0], "row": c0[1], "column": c0[2], "value": "dup"}]
+    st, flags, winner, tree, ran = _apply(eng, msgs2, cells, 3, prior=prior)
+    f, w, _, _ = _oracle(msgs2, cells, prior)
+    assert st == 0 and np.array_equal(flags, f) and np.array_equal(winner, w)
+    assert ran["redo"] == 1
+
+
+@pytest.mark.parametrize("cells", [1, 7, 1000, 2048])
+def test_tc_path_vs_sort_path_at_scale(eng, cells):
+    """2M messages (config-2 generator): the tc path (no ties in these
+    streams) bit for bit against the sort path; one cell is the hot-cell
+    extreme (every row in one segment of the scan)."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    ts_np, cell_np = synth.config2(2_000_000, cells, seed_config=40 + cells)
+    ts, cell = eng.dev(ts_np), eng.dev(cell_np)
+    res = []
+    for path in (3, 2):
+        eng.set_option(L.OPT_CLIENT_PATH, path)
+        s0 = eng.stats()
+        flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), ts, cell, cells)
+        s1 = eng.stats()
+        off, code, xr = tree.leaves()
+        res.append((flags.cpu().numpy(), winner.cpu().numpy(), code, xr, s1["tc_batches"] - s0["tc_batches"],
+                    s1["tc_redos"] - s0["tc_redos"]))
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    (f1, w1, c1, x1, tc1, r1), (f2, w2, c2, x2, _, _) = res
+    assert np.array_equal(f1, f2) and np.array_equal(w1, w2)
+    assert np.array_equal(c1, c2) and np.array_equal(x1, x2)
+    assert tc1 + r1 == 1
+
+
+def test_tc_path_redeliveries_at_scale(eng):
+    """10M messages + 2 % exact/stale redeliveries: whichever way the tc path
+    goes (a redelivered cell max is a tie), the result equals the sort path."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    ts_np, cell_np = synth.config2(10_000_000, 1000, seed_config=2)
+    rng = np.random.default_rng(5)
+    dup = rng.integers(0, len(ts_np), size=len(ts_np) // 50)
+    ts_np = np.concatenate([ts_np, ts_np[dup]])
+    cell_np = np.concatenate([cell_np, cell_np[dup]])
+    ts, cell = eng.dev(ts_np), eng.dev(cell_np)
+    out = []
+    for path in (0, 2):
+        eng.set_option(L.OPT_CLIENT_PATH, path)
+        flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), ts, cell, 1000)
+        out.append((flags.cpu().numpy(), winner.cpu().numpy(), tree.leaves()[1], tree.leaves()[2]))
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
+
+
+def test_tc_path_bad_input(eng):
+    from evolu_amd import _lib as L
+
+    msgs, cells = _distinct_batch(5, n=500, n_cells=10)
+    strings = [m["timestamp"] for m in msgs]
+    strings[17] = strings[17].replace("T", "t")  # not canonical
+    cid = {c: i for i, c in enumerate(cells)}
+    cell = np.array([cid[(m["table"], m["row"], m["column"])] for m in msgs], dtype=np.uint32)
+    eng.set_option(L.OPT_CLIENT_PATH, 3)
+    flags, _, tree, st = eng.apply_batch(eng.tree_new(1), eng.timestamps(strings), eng.dev(cell), len(cells),
+                                         raise_on_error=False)
+    assert st == L.EVM_ENONCANON and tree is None
+    f = flags.cpu().numpy()
+    assert f[17] == L.MSG_BAD and (np.delete(f, 17) == 0).all()
+    cell[3] = len(cells)  # a cell id out of range
+    _, _, tree, st = eng.apply_batch(eng.tree_new(1), eng.timestamps([m["timestamp"] for m in msgs]), eng.dev(cell),
+                                     len(cells), raise_on_error=False)
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    assert st == L.EVM_EINVAL
