@@ -40,7 +40,7 @@ HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 ALG_BYTES_PER_MSG = {
     # streaming tc path (evm_client.hip TP1-TP3, the default)
     "k_tp_pack": 46 + 4 + 16,  # ts + cell in; tc 8 + hash 4 + minute 4 out (per-range cell maxima amortised)
-    "k_tp_flags": 8 + 4 + 1,  # tc + cell in, flag out
+    "k_tp_walk": 8 + 4 + 1,  # tc + cell in, flag out
     # exact walk path (a batch with a tie)
     "k_cl_pack": 46 + 28,  # ts in; order key 16 + rl 4 + hash 4 + minute 4 out
     "k_cl_scan1": 16 + 4 + 4,  # order key + rl + cell in (per-range aggregates amortised away)
@@ -278,16 +278,27 @@ def main():
     ts = eng.dev(ts_np)
     cell = eng.dev(cell_np)
     empty = eng.tree_new(1)
-    flags = torch.empty(a.messages, dtype=torch.uint8, device=ts.device)
-    winner = torch.empty(a.cells, dtype=torch.int32, device=ts.device)
+    # two output sets: batch k + 1 is enqueued (evm_apply_batch_async) before
+    # batch k is waited, so the host's launches and status read overlap the GPU
+    outs = [(torch.empty(a.messages, dtype=torch.uint8, device=ts.device),
+             torch.empty(a.cells, dtype=torch.int32, device=ts.device)) for _ in range(2)]
+    flags, winner = outs[0]
 
     def step():
         _, _, tree, _ = eng.apply_batch(empty, ts, cell, a.cells, flags=flags, winner=winner)
         return tree
 
+    def run_pipelined(k_steps):
+        pend = eng.apply_batch_async(empty, ts, cell, a.cells, *outs[0])
+        for k in range(1, k_steps + 1):
+            nxt = eng.apply_batch_async(empty, ts, cell, a.cells, *outs[k % 2]) if k < k_steps else None
+            pend.wait()[2].free()
+            pend = nxt
+
     eng.prof_enable(True)  # warmup with events on: fills the engine's event pool
     for _ in range(a.warmup):
         step().free()
+    run_pipelined(max(a.warmup, 2))
     torch.cuda.synchronize()
     # per-kernel breakdown (untimed, an event pair around every launch): picks
     # the dominant main-stream kernel
@@ -306,9 +317,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        tree = step()
-        tree.free()
+    run_pipelined(a.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     eng.prof_enable(False)
@@ -369,6 +378,7 @@ def main():
                        "parallelism": "owner-sharded, %d rank(s)" % world},
             "roofline": roof,
             "pipeline": {"alg_bytes_per_msg": 120, "ms_per_step_all_kernel_events": ms_all_events,
+                         "steps_enqueued_ahead": 1,
                          "host_to_host_ms_per_step": ms_h2h, "host_to_host_msgs_per_s": a.messages / ms_h2h * 1e3,
                          "pipeline_hbm_frac": 120 * a.messages / (elapsed / a.steps) / HBM_PEAK,
                          "kernels_ms_per_step": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}},

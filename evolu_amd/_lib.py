@@ -102,6 +102,11 @@ SIGNATURES = {
         _i,
         [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _vp, C.POINTER(_vp)],
     ),
+    "evm_apply_batch_async": (
+        _i,
+        [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _sz, _sz, _vp, _vp, _vp, C.POINTER(_vp)],
+    ),
+    "evm_apply_wait": (_i, [_vp, _vp, C.POINTER(_vp)]),
     "evm_apply_batch_ex": (
         _i,
         [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _sz, _sz, _vp, _vp, _vp, C.POINTER(_vp)],

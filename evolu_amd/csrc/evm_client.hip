@@ -976,19 +976,17 @@ __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* 
 //                   of the walks disappears into the parse
 //   TP2 carry     : per cell, exclusive max over the ranges seeded with the
 //                   prior max; the cell's final max
-//   TP3 k_tp_flags: per range, in LDS chunks: counting sort of the chunk by
-//                   cell, then each cell's messages in batch order against
-//                   the carried max -> flags; the message that reaches the
-//                   cell's final max is the cell's winner (the last upsert)
+//   TP3 k_tp_walk : one wave per range, its rows in batch order against the
+//                   carried max per cell (LDS) -> flags; the message that
+//                   reaches the cell's final max is its winner (the last upsert)
 // Bytes per message: TP1 46 + 4 in, 16 out; TP3 12 in, 1 out.
 // ============================================================================
 constexpr u64 TP_INVALID = ~0ull;  // tc of a message the walk skips (invalid timestamp or cell id)
 constexpr int TP_THREADS = 256;
 constexpr int TP_RANGES = 2048;  // ~8 ranges per CU: TP1's occupancy
-constexpr int TPF_CHUNK = 1024;  // rows per TP3 LDS round (4 per thread)
 
 template <bool S48>
-__global__ __launch_bounds__(TP_THREADS) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
+__global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
                                                         const u32* __restrict__ cell, u32 C, size_t range_len,
                                                         u64* __restrict__ tcs, u32* __restrict__ hash,
                                                         u32* __restrict__ minute, u64* __restrict__ agg,
@@ -1106,161 +1104,93 @@ __global__ void k_tp_carry_down(u32 C, size_t G, u64* __restrict__ agg, const u6
   }
 }
 
-// TP3: one workgroup per range, in chunks of TPF_CHUNK rows (wave w takes
-// rows [256w, 256w + 256) of the chunk, 64 per round).
-//   1 stable counting sort by cell: a row's rank among its wave's earlier rows
-//     of the same cell = the wave's count so far (per-wave LDS counters) + the
-//     lower peers of its round (cell ballots); one scan over (cell, wave)
-//     turns the counts into positions: ord = the rows in (cell, batch) order
-//   2 segmented max-scan over ord (segment = cell; value = tc, the segment
-//     head bit in bit 63 -- a valid tc is < 2^63): the exclusive max of each
-//     row's earlier same-cell rows; with the cell's carried max that is tc(t)
-//   3 flags; the carried max of each cell moves to its last row's inclusive max
-// No serial per-cell loop: a hot cell costs what a cold one does.
-struct SegMaxOp {  // (head:1 | max:63), segmented max
-  static __device__ __forceinline__ u64 id() { return 0ull; }
-  __device__ __forceinline__ u64 operator()(u64 a, u64 b) const {
-    constexpr u64 H = 1ull << 63, M = H - 1;
-    return (b & H) ? b : (max(a & M, b & M) | (a & H));
-  }
-};
+// TP3: one wave per range (four ranges per workgroup), 64 rows per round in
+// batch order, TPW_PF rounds of (tc, cell) in flight.  The wave keeps its
+// range's running max per cell in LDS (seeded with the carried max).  The
+// lanes of one round that share a cell are matched with ballots; each lane
+// takes the max of its lower peers (a wave prefix-max when the whole round is
+// one cell), then t = max(state, that) decides its flags; the round's last
+// peer of a cell writes the new max.  No barrier: the waves are independent.
+constexpr int TPW_PF = 8;
 
-__global__ __launch_bounds__(TP_THREADS) void k_tp_flags(const u64* __restrict__ tcs, const u32* __restrict__ cell,
-                                                         size_t n, u32 C, int cbits, size_t range_len,
-                                                         const u64* __restrict__ carry, const u64* __restrict__ tfinal,
-                                                         uint8_t* __restrict__ flags, int32_t* __restrict__ winner,
-                                                         Info* __restrict__ info) {
-  extern __shared__ __attribute__((aligned(16))) u64 tp_lds[];
-  constexpr int W = TP_THREADS / 64;
-  u64* T = tp_lds;                                               // [C] running max of each cell
-  u64* ctc = T + C;                                              // [CHUNK] the chunk's tc
-  u32* cntw = reinterpret_cast<u32*>(ctc + TPF_CHUNK);           // [W][C] per-wave counts -> positions
-  uint16_t* ccell = reinterpret_cast<uint16_t*>(cntw + W * C);   // [CHUNK] cell of a row, 0xffff = skip
-  uint16_t* ord = ccell + TPF_CHUNK;                             // [CHUNK] rows in (cell, batch) order
-  uint8_t* fl = reinterpret_cast<uint8_t*>(ord + TPF_CHUNK);     // [CHUNK] flags of the rows
-  __shared__ u64 tmp64[TP_THREADS / 64 + 1];
-  __shared__ u32 tmp32[TP_THREADS / 64 + 1];
-  __shared__ u64 xchg[TP_THREADS];
-  constexpr int PER = TPF_CHUNK / TP_THREADS;  // rows per thread, and ord entries per thread
+__global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ tcs, const u32* __restrict__ cell,
+                                                        size_t n, u32 C, int cbits, size_t range_len, size_t G,
+                                                        const u64* __restrict__ carry, const u64* __restrict__ tfinal,
+                                                        uint8_t* __restrict__ flags, int32_t* __restrict__ winner,
+                                                        Info* __restrict__ info) {
+  extern __shared__ __attribute__((aligned(16))) u64 tw_lds[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const size_t g = (size_t)blockIdx.x * (TP_THREADS / 64) + wv;
+  if (g >= G) return;  // (waves never synchronise with each other)
+  u64* T = tw_lds + (size_t)wv * C;
+  for (u32 c = lane; c < C; c += 64) T[c] = carry[g * C + c];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   const u64 lt = lanemask_lt();
-  const size_t g = blockIdx.x;
   const size_t beg = g * range_len, end = min(n, beg + range_len);
-  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) T[c] = carry[g * C + c];
+  u64 px[TPW_PF];
+  u32 pc[TPW_PF];
+#pragma unroll
+  for (int r = 0; r < TPW_PF; ++r) {
+    const size_t i = beg + 64 * r + lane;
+    px[r] = i < end ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
+    pc[r] = i < end ? __builtin_nontemporal_load(cell + i) : 0u;
+  }
   u32 tie = 0;
-  const u32 cper = (C + TP_THREADS - 1) / TP_THREADS;  // cells per thread in the position scan
-  for (size_t base = beg; base < end; base += TPF_CHUNK) {
-    const u32 m = (u32)min((size_t)TPF_CHUNK, end - base);
-    for (u32 k = threadIdx.x; k < W * C; k += TP_THREADS) cntw[k] = 0;
-    __syncthreads();
-    // 1a: load, stable rank inside the wave's quarter
-    u32 rk[PER], rc[PER];
+  for (size_t first = beg; first < end; first += 64 * TPW_PF) {  // uniform
 #pragma unroll
-    for (int r = 0; r < PER; ++r) {
-      const u32 j = wv * (TPF_CHUNK / W) + r * 64 + lane;
-      bool ok = false;
-      u32 ci = 0;
-      if (j < m) {
-        const u64 x = __builtin_nontemporal_load(tcs + base + j);
-        ci = __builtin_nontemporal_load(cell + base + j);
-        ok = x != TP_INVALID;
-        ctc[j] = x;
-        ccell[j] = ok ? (uint16_t)ci : (uint16_t)0xffff;
-        fl[j] = ok ? 0 : (uint8_t)EVM_MSG_BAD;
+    for (int r = 0; r < TPW_PF; ++r) {
+      const size_t f = first + 64 * r;
+      const u64 x = px[r];
+      const u32 c = pc[r];
+      {
+        const size_t i = f + 64 * TPW_PF + lane;
+        px[r] = i < end ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
+        pc[r] = i < end ? __builtin_nontemporal_load(cell + i) : 0u;
       }
-      const u64 peers = match_cell(ci, ok, cbits);
-      u32 before = 0;
-      if (ok) before = cntw[wv * C + ci];
-      if (ok && (peers >> lane) == 1ull) cntw[wv * C + ci] = before + (u32)__popcll(peers);  // last peer
-      rk[r] = before + (u32)__popcll(peers & lt);
-      rc[r] = ok ? ci : 0xffffffffu;
-    }
-    __syncthreads();
-    // 1b: positions: exclusive scan over (cell, wave), cell-major
-    u32 mv;
-    {
-      u32 loc = 0;
-      for (u32 k = 0; k < cper; ++k) {
-        const u32 c = threadIdx.x * cper + k;
-        if (c < C)
-          for (int w = 0; w < W; ++w) loc += cntw[w * C + c];
-      }
-      u32 run = block_inclusive_scan<u32>(loc, tmp32, OpAdd<u32>(), &mv) - loc;
-      for (u32 k = 0; k < cper; ++k) {
-        const u32 c = threadIdx.x * cper + k;
-        if (c < C)
-          for (int w = 0; w < W; ++w) {
-            const u32 v = cntw[w * C + c];
-            cntw[w * C + c] = run;
-            run += v;
+      if (f >= end) continue;  // uniform
+      const bool ok = x != TP_INVALID;
+      const u64 peers = match_cell(c, ok, cbits);
+      const u64 act = __ballot(ok);
+      // max tc of the lower lanes of the same cell
+      u64 pm = 0;
+      if (peers == act && act == ~0ull) {
+        // the whole round is one cell: exclusive wave prefix max
+        u64 v = x;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const u64 u = __shfl_up(v, d, 64);
+          if (lane >= d) v = max(v, u);
+        }
+        pm = __shfl_up(v, 1, 64);
+        if (lane == 0) pm = 0;
+      } else {
+        u64 rem = peers & lt;
+        while (__any(rem != 0)) {
+          const int src = rem ? (int)__builtin_ctzll(rem) : lane;
+          const u64 v = __shfl(x, src, 64);
+          if (rem) {
+            pm = max(pm, v);
+            rem &= rem - 1;
           }
+        }
       }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < PER; ++r) {
-      const u32 j = wv * (TPF_CHUNK / W) + r * 64 + lane;
-      if (rc[r] != 0xffffffffu) ord[cntw[wv * C + rc[r]] + rk[r]] = (uint16_t)j;
-    }
-    __syncthreads();
-    // 2: segmented max-scan over ord[0, mv); thread t owns entries [PER t, PER t + PER)
-    constexpr u64 HEAD = 1ull << 63;
-    u64 v[PER];
-    u32 cc[PER];
-    u64 agg = 0;
-#pragma unroll
-    for (int r = 0; r < PER; ++r) {
-      const u32 k = PER * threadIdx.x + r;
-      cc[r] = 0xffffffffu;
-      v[r] = 0;
-      if (k < mv) {
-        const u32 j = ord[k];
-        cc[r] = ccell[j];
-        const bool head = k == 0 || ccell[ord[k - 1]] != cc[r];
-        v[r] = ctc[j] | (head ? HEAD : 0ull);
-        agg = SegMaxOp()(agg, v[r]);
+      uint8_t fl = EVM_MSG_BAD;
+      if (ok) {
+        const u64 t = max(T[c], pm);
+        if (x > t) {  // applyMessages.ts:93 and :105 both hold
+          fl = EVM_MSG_UPS | EVM_MSG_XOR;
+          if (x == tfinal[c]) winner[c] = (int32_t)(f + lane);  // reaches the final max: the last upsert
+        } else if (x < t) {  // :105 only (a stale redelivery re-XORs)
+          fl = EVM_MSG_XOR;
+        } else {  // equal tc: the node ranks decide -> the exact path
+          fl = 0;
+          tie = 1;
+        }
+        if ((peers >> lane) == 1ull) T[c] = max(t, x);  // the round's last peer of the cell
       }
+      if (f + lane < end) flags[f + lane] = fl;
     }
-    xchg[threadIdx.x] = block_inclusive_scan<u64>(agg, tmp64, SegMaxOp(), (u64*)nullptr);
-    __syncthreads();
-    u64 e = threadIdx.x ? xchg[threadIdx.x - 1] : 0ull;  // the entries before this thread's
-    // 3: flags (reads T); each segment end keeps its cell's new max
-    u64 newT[PER];
-#pragma unroll
-    for (int r = 0; r < PER; ++r) {
-      const u32 k = PER * threadIdx.x + r;
-      newT[r] = 0;
-      if (k >= mv) continue;
-      const u32 c = cc[r];
-      const u64 x = v[r] & ~HEAD;
-      const u64 t = max(T[c], (v[r] & HEAD) ? 0ull : (e & ~HEAD));
-      uint8_t f;
-      if (x > t) {  // applyMessages.ts:93 and :105 both hold
-        f = EVM_MSG_UPS | EVM_MSG_XOR;
-        if (x == tfinal[c]) winner[c] = (int32_t)(base + ord[k]);  // reaches the final max: the last upsert
-      } else if (x < t) {  // :105 only (a stale redelivery re-XORs)
-        f = EVM_MSG_XOR;
-      } else {  // equal tc: the node ranks decide -> the exact path
-        f = 0;
-        tie = 1;
-      }
-      fl[ord[k]] = f;
-      e = SegMaxOp()(e, v[r]);
-      if (k + 1 == mv || ccell[ord[k + 1]] != c) newT[r] = max(t, e & ~HEAD) | HEAD;  // segment end
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < PER; ++r)
-      if (newT[r] & HEAD) T[cc[r]] = newT[r] & ~HEAD;
-    __syncthreads();
-    // flags out: 4 consecutive rows per thread (base is a multiple of 4)
-    const u32 j4 = 4 * threadIdx.x;
-    if (j4 + 4 <= m) {
-      reinterpret_cast<u32*>(flags + base)[threadIdx.x] = reinterpret_cast<const u32*>(fl)[threadIdx.x];
-    } else {
-      for (u32 j = j4; j < m; ++j) flags[base + j] = fl[j];
-    }
-    __syncthreads();
   }
   if (__ballot(tie) && lane == 0) atomic_or_if(&info->ties, 1u);
 }
@@ -1268,16 +1198,46 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_flags(const u64* __restrict__
 // ============================================================================
 // Host drivers
 // ============================================================================
+// An enqueued streaming batch (evm_apply_batch_async): the call's arguments
+// (the caller keeps them valid until evm_apply_wait), the pinned landing slot
+// of its status record, the event after its last kernel, and its outputs.
+struct evm_pending {
+  const evm_tree* tree_in;
+  const char* ts;
+  size_t stride, n;
+  const uint32_t* cell;
+  uint32_t n_cells;
+  const uint32_t* cell_owner;
+  const char* prior_ts;
+  size_t prior_stride;
+  const uint8_t* prior_present;
+  const char* stored_ts;
+  size_t stored_stride, n_stored;
+  const uint32_t* stored_cell;
+  uint8_t* flags;
+  int32_t* winner;
+  bool enqueued = false;  // false: finished synchronously (status, done)
+  int status = EVM_OK;
+  evm_tree* done = nullptr;
+  evm::Info* hinfo = nullptr;  // pinned
+  hipEvent_t ev = nullptr;
+  evm_tree* spec = nullptr;  // the output tree (an empty one-owner tree_in)
+  void* leaves = nullptr;    // the batch's leaves (ck, xr) for a merge at the wait
+  size_t leaves_bytes = 0;
+};
+
 // The streaming paths.  TC: the tc path (TP1-TP3); otherwise the exact walk
 // path (K1 + pass 1 + carry + pass 2 over the full order key).  Both share
 // the cross-cell check, the Merkle fold and the status handling.  The tc
 // path returns TP_REDO when it met a tie (the caller reruns the exact path).
 constexpr int TP_REDO = -100;
+constexpr int ST_PENDING = -101;  // apply_stream enqueued the batch (evm_apply_batch_async)
 
 template <bool TC>
 static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree_in, const char* ts, size_t stride,
                         size_t n, const u32* cell, u32 C, const evm_rec* prior, const uint8_t* prior_present,
-                        const Stored& stored, uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+                        const Stored& stored, uint8_t* flags, int32_t* winner, evm_tree** tree_out,
+                        evm_pending* pend = nullptr) {
   int st;
   const int cbits = C > 1 ? 32 - __builtin_clz(C - 1) : 0;
   const bool s48 = stride == 48 && ((uintptr_t)ts & 15) == 0;
@@ -1369,10 +1329,9 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     KLAUNCH(k_tp_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, (const u64*)agg, s_max);
     KLAUNCH(k_tp_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_max, prior, prior_present, tfinal);
     KLAUNCH(k_tp_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, agg, (const u64*)s_max);
-    // TP3: flags + winners
-    const size_t lds = (size_t)C * 8 + TPF_CHUNK * 8 + (size_t)(TP_THREADS / 64) * C * 4 + TPF_CHUNK * 5;
-    KLAUNCH_LDS(k_tp_flags, dim3(G), dim3(TP_THREADS), lds, (const u64*)tcs, cell, n, C, cbits, range,
-                (const u64*)agg, (const u64*)tfinal, flags, winner, info);
+    // TP3: flags + winners, one wave per range
+    KLAUNCH_LDS(k_tp_walk, dim3((G + 3) / 4), dim3(TP_THREADS), (size_t)4 * C * 8, (const u64*)tcs, cell, n, C, cbits,
+                range, G, (const u64*)agg, (const u64*)tfinal, flags, winner, info);
   } else {
     // pass 1: per range and cell, the max timestamp and its first index
     KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
@@ -1402,22 +1361,34 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   u32* dp = S.alloc<u32>(B);
   u32* bcnt = S.alloc<u32>(FR_BLOCKS);
   u32* bxor = S.alloc<u32>(FR_BLOCKS);
-  u64* lck = S.alloc<u64>(B);
-  int32_t* lxr = S.alloc<int32_t>(B);
+  const bool spec_out = tree_in->n_leaves == 0 && tree_in->n_owners == 1;
+  u64* lck = nullptr;
+  int32_t* lxr = nullptr;
+  if (pend && !spec_out) {
+    // the leaves outlive this call's scratch: the wait merges them
+    pend->leaves_bytes = B * (sizeof(u64) + sizeof(int32_t));
+    pend->leaves = block_alloc(ctx, &pend->leaves_bytes);
+    if (!pend->leaves) return EVM_ENOMEM;
+    lck = static_cast<u64*>(pend->leaves);
+    lxr = reinterpret_cast<int32_t*>(lck + B);
+  } else {
+    lck = S.alloc<u64>(B);
+    lxr = S.alloc<int32_t>(B);
+  }
   if (!px || !pp || !dx || !dp || !bcnt || !bxor || !lck || !lxr) return EVM_ENOMEM;
   KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
   KLAUNCH(k_cl_fold_reduce, dim3(FR_BLOCKS), dim3(FR_THREADS), px, pp, info, dx, dp, bcnt, bxor);
   // into an empty tree: build the output speculatively, so the call has one
   // host round trip; one owner: the leaf kernel writes the tree itself
   evm_tree* spec = nullptr;
-  if (tree_in->n_leaves == 0 && tree_in->n_owners == 1) {
+  if (spec_out) {
     if ((st = tree_alloc_cap(ctx, 1, B, &spec))) return st;
     KLAUNCH(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), dx, dp, bcnt, bxor, info, spec->ck, spec->xr, spec->pfx,
             spec->off);
   } else {
     KLAUNCH(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), dx, dp, bcnt, bxor, info, lck, lxr, (int32_t*)nullptr,
             (u64*)nullptr);
-    if (tree_in->n_leaves == 0 &&
+    if (!pend && tree_in->n_leaves == 0 &&
         (st = tree_finalize_dev(ctx, S, tree_in->n_owners, lck, lxr, &info->n_leaves, B, &spec)))
       return st;
   }
@@ -1429,6 +1400,14 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     }
   } guard{ctx, spec};
   side.join();
+  if (pend) {
+    // asynchronous: the status record lands in pinned memory; evm_apply_wait finishes
+    HIPR(hipMemcpyAsync(pend->hinfo, info, sizeof(Info), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipEventRecord(pend->ev, ctx->stream));
+    pend->spec = spec;
+    spec = nullptr;
+    return ST_PENDING;
+  }
   Info hi;
   if ((st = read_info(ctx, info, &hi))) return st;
   if (hi.bad) {
@@ -1556,11 +1535,15 @@ int evm_apply_batch(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_
                             prior_present, nullptr, 48, 0, nullptr, flags, winner, tree_out);
 }
 
-int evm_apply_batch_ex(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n,
+}  // extern "C"
+
+// evm_apply_batch_ex, or (pend) its asynchronous form: a streaming batch is
+// enqueued and ST_PENDING returned; anything else finishes here.
+static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n,
                        const uint32_t* cell, uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts,
                        size_t prior_stride, const uint8_t* prior_present, const char* stored_ts, size_t stored_stride,
                        size_t n_stored, const uint32_t* stored_cell, uint8_t* flags, int32_t* winner,
-                       evm_tree** tree_out) {
+                       evm_tree** tree_out, int path, evm_pending* pend) {
   if (!ctx || !tree_in || !tree_out || stride < 46 || (n && (!ts || !cell || !flags))) return EVM_EINVAL;
   if (n_cells && !winner) return EVM_EINVAL;
   if (prior_present && (!prior_ts || prior_stride < 46)) return EVM_EINVAL;
@@ -1587,7 +1570,6 @@ int evm_apply_batch_ex(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
       return EVM_OK;
     };
     if ((st = init())) return st;
-    const int path = ctx->client_path;
     if (n == 0) {
       Info hi;
       if ((st = read_info(ctx, info, &hi))) return st;
@@ -1599,7 +1581,8 @@ int evm_apply_batch_ex(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
       if (path != 1) {
         Scratch S2(ctx);  // released before a rerun
         st = apply_stream<true>(ctx, S2, info, tree_in, ts, stride, n, cell, n_cells, prior, prior_present, stored,
-                                flags, winner, tree_out);
+                                flags, winner, tree_out, pend);
+        if (st == ST_PENDING) return st;
         if (st == TP_REDO) ++ctx->stats.tc_redos;
         else if (st == EVM_OK) ++ctx->stats.tc_batches;
       }
@@ -1616,6 +1599,123 @@ int evm_apply_batch_ex(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
   }
   if (st) return st;
   return evm_sync(ctx);
+}
+
+extern "C" {
+
+int evm_apply_batch_ex(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n,
+                       const uint32_t* cell, uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts,
+                       size_t prior_stride, const uint8_t* prior_present, const char* stored_ts, size_t stored_stride,
+                       size_t n_stored, const uint32_t* stored_cell, uint8_t* flags, int32_t* winner,
+                       evm_tree** tree_out) {
+  if (!ctx) return EVM_EINVAL;
+  return apply_entry(ctx, tree_in, ts, stride, n, cell, n_cells, cell_owner, prior_ts, prior_stride, prior_present,
+                     stored_ts, stored_stride, n_stored, stored_cell, flags, winner, tree_out, ctx->client_path,
+                     nullptr);
+}
+
+int evm_apply_batch_async(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n,
+                          const uint32_t* cell, uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts,
+                          size_t prior_stride, const uint8_t* prior_present, const char* stored_ts,
+                          size_t stored_stride, size_t n_stored, const uint32_t* stored_cell, uint8_t* flags,
+                          int32_t* winner, evm_pending** out) {
+  if (!ctx || !out) return EVM_EINVAL;
+  *out = nullptr;
+  evm_pending* p;
+  if (!ctx->pend_pool.empty()) {
+    p = ctx->pend_pool.back();
+    ctx->pend_pool.pop_back();
+  } else {
+    p = new evm_pending();
+    if (hipHostMalloc((void**)&p->hinfo, sizeof(Info), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&p->ev, hipEventDisableTiming) != hipSuccess) {
+      if (p->hinfo) (void)hipHostFree(p->hinfo);
+      delete p;
+      return EVM_EDEVICE;
+    }
+  }
+  *p = evm_pending{tree_in, ts, stride, n, cell, n_cells, cell_owner, prior_ts, prior_stride, prior_present,
+                   stored_ts, stored_stride, n_stored, stored_cell, flags, winner, false, EVM_OK, nullptr,
+                   p->hinfo, p->ev, nullptr, nullptr, 0};
+  const int st = apply_entry(ctx, tree_in, ts, stride, n, cell, n_cells, cell_owner, prior_ts, prior_stride,
+                             prior_present, stored_ts, stored_stride, n_stored, stored_cell, flags, winner, &p->done,
+                             ctx->client_path, p);
+  if (st == ST_PENDING) {
+    p->enqueued = true;
+  } else {
+    // finished (or failed) synchronously
+    if (p->spec) tree_destroy(ctx, p->spec);
+    if (p->leaves) block_free(ctx, p->leaves, p->leaves_bytes);
+    p->spec = nullptr;
+    p->leaves = nullptr;
+    p->status = st;
+  }
+  *out = p;
+  return EVM_OK;
+}
+
+}  // extern "C"
+
+void evm_pending_pool_clear(evm_ctx* ctx) {
+  for (evm_pending* p : ctx->pend_pool) {
+    if (p->hinfo) (void)hipHostFree(p->hinfo);
+    if (p->ev) (void)hipEventDestroy(p->ev);
+    delete p;
+  }
+  ctx->pend_pool.clear();
+}
+
+extern "C" {
+
+int evm_apply_wait(evm_ctx* ctx, evm_pending* p, evm_tree** tree_out) {
+  if (!ctx || !p || !tree_out) return EVM_EINVAL;
+  *tree_out = nullptr;
+  int st = EVM_OK;
+  if (!p->enqueued) {
+    st = p->status;
+    *tree_out = p->done;
+  } else {
+    st = hip_ok(hipEventSynchronize(p->ev));
+    Info hi = *p->hinfo;
+    const bool redo = !st && !hi.bad && !hi.bad_aux &&
+                      (hi.ties || (!hi.collision && (hi.xc_oversize || hi.fold_overflow)));
+    if (st) {
+    } else if (hi.bad) {
+      KLAUNCH(k_keep_bad, dim3(grid_for(p->n, 256)), dim3(256), p->flags, p->n);  // nothing applied: the culprits
+      st = EVM_ENONCANON;
+    } else if (hi.bad_aux) {
+      st = EVM_EINVAL;
+    } else if (redo) {
+      // a tie, an oversized hash bucket or a wide minute range: the synchronous paths redo the batch
+      if (hi.ties) ++ctx->stats.tc_redos;
+      st = apply_entry(ctx, p->tree_in, p->ts, p->stride, p->n, p->cell, p->n_cells, p->cell_owner, p->prior_ts,
+                       p->prior_stride, p->prior_present, p->stored_ts, p->stored_stride, p->n_stored, p->stored_cell,
+                       p->flags, p->winner, tree_out, hi.ties ? 1 : ctx->client_path, nullptr);
+    } else if (hi.collision) {
+      st = EVM_ECOLLISION;
+    } else if (p->spec) {
+      ++ctx->stats.tc_batches;
+      p->spec->n_leaves = hi.n_leaves;
+      *tree_out = p->spec;
+      p->spec = nullptr;
+    } else {
+      ++ctx->stats.tc_batches;
+      Scratch S(ctx);
+      const size_t B = (size_t)FOLD_MAXWIN * FOLD_WIN;
+      const u64* lck = static_cast<const u64*>(p->leaves);
+      st = merge_into_tree(ctx, S, p->tree_in, p->tree_in->n_owners, lck, reinterpret_cast<const int32_t*>(lck + B),
+                           hi.n_leaves, tree_out);
+    }
+    if (p->spec) tree_destroy(ctx, p->spec);
+    if (p->leaves) block_free(ctx, p->leaves, p->leaves_bytes);
+    p->spec = nullptr;
+    p->leaves = nullptr;
+    if (!st) st = evm_sync(ctx);
+  }
+  p->enqueued = false;
+  p->done = nullptr;
+  ctx->pend_pool.push_back(p);
+  return st;
 }
 
 int evm_cross_cell_check(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const uint32_t* cell, uint32_t n_cells,

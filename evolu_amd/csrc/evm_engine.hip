@@ -747,6 +747,7 @@ void evm_destroy(evm_ctx* ctx) {
   prof_drain(ctx);
   for (hipEvent_t e : ctx->prof_pool) (void)hipEventDestroy(e);
   block_cache_clear(ctx);
+  evm_pending_pool_clear(ctx);
   if (ctx->xtab) (void)hipFree(ctx->xtab);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);

@@ -14,6 +14,8 @@ namespace evm {
 struct Info;
 }
 
+struct evm_pending;
+
 struct evm_ctx {
   int device;
   hipStream_t own;
@@ -46,6 +48,7 @@ struct evm_ctx {
   // freed tree / store blocks kept for reuse (stream-ordered on `stream`):
   // a steady-state loop of ingests / applies makes no allocation calls
   std::vector<std::pair<void*, size_t>> blocks;
+  std::vector<evm_pending*> pend_pool;  // finished evm_apply_batch_async handles (pinned slot + event kept)
 };
 
 // One MerkleTree per owner, as sorted unique leaves keyed by
@@ -271,6 +274,9 @@ inline int new_info(evm_ctx* ctx, Scratch& S, Info** out) {
 void* block_alloc(evm_ctx* ctx, size_t* bytes);
 void block_free(evm_ctx* ctx, void* p, size_t bytes);
 void block_cache_clear(evm_ctx* ctx);
+}  // namespace evm
+void evm_pending_pool_clear(evm_ctx* ctx);  // evm_client.hip
+namespace evm {
 
 // shared launchers (evm_engine.hip)
 int launch_iota(evm_ctx* ctx, u32* v, size_t n);

@@ -231,6 +231,24 @@ class Engine:
         return flags, winner[:n_cells], (Trees(self, h) if st == _lib.EVM_OK else None), st
 
 
+    def apply_batch_async(self, trees: "Trees", ts: torch.Tensor, cell: torch.Tensor, n_cells: int,
+                          flags: torch.Tensor, winner: torch.Tensor, prior_ts: Optional[torch.Tensor] = None,
+                          prior_present: Optional[torch.Tensor] = None, stored_ts: Optional[torch.Tensor] = None,
+                          stored_cell: Optional[torch.Tensor] = None) -> "Pending":
+        """evm_apply_batch_async: enqueue; .wait() -> (flags, winner, Trees or None, status).
+        Every tensor passed must stay alive and untouched until the wait."""
+        n, stride = ts.shape
+        pstride = prior_ts.shape[1] if prior_ts is not None else 48
+        sn = 0 if stored_ts is None else stored_ts.shape[0]
+        sstride = 48 if stored_ts is None else stored_ts.shape[1]
+        h = C.c_void_p()
+        check(self.lib.evm_apply_batch_async(self.h, trees.h, _ptr(ts), stride, n, _ptr(cell), n_cells, None,
+                                             _ptr(prior_ts), pstride, _ptr(prior_present), _ptr(stored_ts), sstride,
+                                             sn, _ptr(stored_cell), _ptr(flags), _ptr(winner), C.byref(h)),
+              "evm_apply_batch_async")
+        return Pending(self, h, (trees, ts, cell, flags, winner, prior_ts, prior_present, stored_ts, stored_cell),
+                       n_cells)
+
     def cross_cell_check(self, ts: torch.Tensor, cell: torch.Tensor, n_cells: int) -> bool:
         """True iff some timestamp of the batch occurs with two different cells
         (the global __message PK case evm_apply_batch reports as EVM_ECOLLISION)."""
@@ -239,6 +257,27 @@ class Engine:
         check(self.lib.evm_cross_cell_check(self.h, _ptr(ts), stride, n, _ptr(cell), n_cells, C.byref(found)),
               "evm_cross_cell_check")
         return bool(found.value)
+
+
+class Pending:
+    """An enqueued applyMessages batch (evm_apply_batch_async); keeps its
+    tensors alive until wait()."""
+
+    def __init__(self, eng: "Engine", h, keep, n_cells: int):
+        self.eng = eng
+        self.h = h
+        self.keep = keep
+        self.n_cells = n_cells
+
+    def wait(self, raise_on_error: bool = True):
+        t = C.c_void_p()
+        st = self.eng.lib.evm_apply_wait(self.eng.h, self.h, C.byref(t))
+        self.h = None
+        flags, winner = self.keep[3], self.keep[4]
+        self.keep = None
+        if raise_on_error:
+            check(st, "evm_apply_wait")
+        return flags, winner[: self.n_cells], (Trees(self.eng, t) if st == _lib.EVM_OK else None), st
 
 
 class Store:

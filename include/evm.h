@@ -212,6 +212,24 @@ int evm_apply_batch_ex(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
                        size_t n_stored, const uint32_t* stored_cell, uint8_t* flags, int32_t* winner,
                        evm_tree** tree_out);
 
+/* Asynchronous evm_apply_batch_ex (applyMessages is a ReaderTaskEither,
+ * applyMessages.ts:26-31): the batch is enqueued on the context stream and the
+ * call returns at once, so the host prepares the next batch while the GPU
+ * works; evm_apply_wait collects the status and the new tree.  Every input and
+ * output buffer (and tree_in) must stay valid and untouched until the wait.
+ * Batches the streaming path does not take (many owners, > 2,048 cells, empty)
+ * and the rare redo cases (a tie, an oversized hash bucket, a wide minute
+ * range) finish synchronously -- inside this call or the wait.  Each handle is
+ * waited exactly once.                                                      */
+typedef struct evm_pending evm_pending;
+int evm_apply_batch_async(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, size_t stride, size_t n,
+                          const uint32_t* cell, uint32_t n_cells, const uint32_t* cell_owner, const char* prior_ts,
+                          size_t prior_stride, const uint8_t* prior_present, const char* stored_ts,
+                          size_t stored_stride, size_t n_stored, const uint32_t* stored_cell, uint8_t* flags,
+                          int32_t* winner, evm_pending** out);
+/* -> the batch's status (as evm_apply_batch_ex); *tree_out on EVM_OK */
+int evm_apply_wait(evm_ctx* ctx, evm_pending* p, evm_tree** tree_out);
+
 /* The global __message PK check evm_apply_batch runs (applyMessages.ts:42-45,
  * 104-113: one timestamp in two cells of a batch), on its own: for a batch
  * whose cells are split over ranks (evolu_amd/dist.py split_apply), each rank
