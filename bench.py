@@ -280,8 +280,9 @@ def main():
     empty = eng.tree_new(1)
     # two output sets: batch k + 1 is enqueued (evm_apply_batch_async) before
     # batch k is waited, so the host's launches and status read overlap the GPU
+    DEPTH = 3  # batches enqueued ahead of the one being waited
     outs = [(torch.empty(a.messages, dtype=torch.uint8, device=ts.device),
-             torch.empty(a.cells, dtype=torch.int32, device=ts.device)) for _ in range(2)]
+             torch.empty(a.cells, dtype=torch.int32, device=ts.device)) for _ in range(DEPTH)]
     flags, winner = outs[0]
 
     def step():
@@ -289,11 +290,15 @@ def main():
         return tree
 
     def run_pipelined(k_steps):
-        pend = eng.apply_batch_async(empty, ts, cell, a.cells, *outs[0])
-        for k in range(1, k_steps + 1):
-            nxt = eng.apply_batch_async(empty, ts, cell, a.cells, *outs[k % 2]) if k < k_steps else None
-            pend.wait()[2].free()
-            pend = nxt
+        import collections
+
+        q = collections.deque()
+        for k in range(k_steps):
+            if len(q) == DEPTH:
+                q.popleft().wait()[2].free()
+            q.append(eng.apply_batch_async(empty, ts, cell, a.cells, *outs[k % DEPTH]))
+        while q:
+            q.popleft().wait()[2].free()
 
     eng.prof_enable(True)  # warmup with events on: fills the engine's event pool
     for _ in range(a.warmup):
@@ -378,7 +383,7 @@ def main():
                        "parallelism": "owner-sharded, %d rank(s)" % world},
             "roofline": roof,
             "pipeline": {"alg_bytes_per_msg": 120, "ms_per_step_all_kernel_events": ms_all_events,
-                         "steps_enqueued_ahead": 1,
+                         "batches_in_flight": DEPTH,
                          "host_to_host_ms_per_step": ms_h2h, "host_to_host_msgs_per_s": a.messages / ms_h2h * 1e3,
                          "pipeline_hbm_frac": 120 * a.messages / (elapsed / a.steps) / HBM_PEAK,
                          "kernels_ms_per_step": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}},

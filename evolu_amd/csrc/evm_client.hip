@@ -794,6 +794,11 @@ __global__ __launch_bounds__(XP_THREADS) void k_xp_dedup(const u64* __restrict__
 
 // Dense Merkle fold over [minute_min, minute_min + FOLD_MAXWIN * FOLD_WIN):
 // per (window, chunk) an LDS XOR histogram + presence bitmap.
+// FLAGS: fold the EVM_MSG_XOR messages; otherwise every message whose minute
+// is in range (the tc path: without a tie every valid message is XORed, and
+// K1 puts the others' minute out of range) -- so the fold need not wait for
+// the walk.
+template <bool FLAGS>
 __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __restrict__ flags,
                                                               const u32* __restrict__ minute,
                                                               const u32* __restrict__ hash, size_t n,
@@ -822,7 +827,7 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __
   for (size_t i = a + 4 * (size_t)threadIdx.x; i < e; i += 4 * FOLD_THREADS) {
     if (i + 4 <= e) {
       typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-      const u32 f4 = __builtin_nontemporal_load(reinterpret_cast<const u32*>(flags + i));
+      const u32 f4 = FLAGS ? __builtin_nontemporal_load(reinterpret_cast<const u32*>(flags + i)) : 0x02020202u;
       const v4u m4 = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(minute + i));
       const v4u h4 = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(hash + i));
       const u32 mm[4] = {m4.x, m4.y, m4.z, m4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w};
@@ -837,7 +842,7 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __
     } else {
       for (size_t k = i; k < e; ++k) {
         const u32 off = minute[k] - base;
-        if ((flags[k] & EVM_MSG_XOR) && off < FOLD_WIN) {
+        if ((!FLAGS || (flags[k] & EVM_MSG_XOR)) && off < FOLD_WIN) {
           atomicXor(&hist[off], hash[k]);
           atomicOr(&pres[off >> 5], 1u << (off & 31));
         }
@@ -1021,12 +1026,13 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
       w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
       w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
     }
-    const Parsed p = parse_ts46(w);  // (the node ranks it can compute are dead here)
+    Parsed p = parse_ts46(w);  // (the node ranks it can compute are dead here)
     const bool valid = (p.meta & EVM_META_VALID) != 0;
     if (i < end) {
       const u32 ci = __builtin_nontemporal_load(cell + i);
       const bool ok = valid && ci < C;
       __builtin_nontemporal_store(ok ? p.tc : TP_INVALID, tcs + i);
+      if (!ok) p.minute = 0xffffffffu;  // outside every fold window: the tc path folds without flags
       if (ok) atomicMax(&cmax[ci], p.tc);
       bad |= valid ? 0u : 1u;
       aux_bad |= ci < C ? 0u : 1u;
@@ -1049,8 +1055,8 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
       hash[i] = p.hash;
       minute[i] = p.minute;
     }
-    mn = min(mn, valid ? p.minute : 0xffffffffu);
-    mx = max(mx, valid ? p.minute : 0u);
+    mn = min(mn, p.minute);
+    mx = max(mx, p.minute != 0xffffffffu ? p.minute : 0u);
   }
   if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
   __syncthreads();
@@ -1122,8 +1128,12 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const size_t g = (size_t)blockIdx.x * (TP_THREADS / 64) + wv;
   if (g >= G) return;  // (waves never synchronise with each other)
-  u64* T = tw_lds + (size_t)wv * C;
-  for (u32 c = lane; c < C; c += 64) T[c] = carry[g * C + c];
+  u64* T = tw_lds + (size_t)wv * 2 * C;  // [C] running max per cell
+  u64* M = T + C;                        // [C] lanes of the current round per cell (zero between rounds)
+  for (u32 c = lane; c < C; c += 64) {
+    T[c] = carry[g * C + c];
+    M[c] = 0;
+  }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   const u64 lt = lanemask_lt();
@@ -1150,7 +1160,12 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
       }
       if (f >= end) continue;  // uniform
       const bool ok = x != TP_INVALID;
-      const u64 peers = match_cell(c, ok, cbits);
+      // the round's lanes of each cell: every lane ORs its bit into its cell's
+      // mask and reads the mask back (one wave: the LDS runs its instructions in
+      // order), then clears it -- three LDS operations instead of cbits ballots
+      if (ok) atomicOr(&M[c], 1ull << lane);
+      const u64 peers = ok ? __hip_atomic_load(&M[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0ull;
+      if (ok) __hip_atomic_store(&M[c], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       const u64 act = __ballot(ok);
       // max tc of the lower lanes of the same cell
       u64 pm = 0;
@@ -1306,54 +1321,8 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   // it reads only the timestamps, cells and K1's hashes: a second stream runs
   // it beside the walks, forked right after K1 (joined before the status
   // read; forked after pass 1 instead: 0.502-0.506 vs 0.497 ms per config-2 step)
-  SideFork side(ctx);
-  {
-    const hipStream_t xs = side.stream();
-    HIPR(hipMemsetAsync(xcur, 0, sizeof(u32) << kb, xs));
-    {
-      evm::ProfScope ps_(ctx, "k_xp_scatter", xs);
-      hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), 0, xs, hash, n, kb, cap, xcur, xpairs, info);
-    }
-    {
-      evm::ProfScope ps_(ctx, "k_xp_dedup", xs);
-      hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, xpairs, xcur, cap, n,
-                         (const uint8_t*)ts, stride, cell, info);
-    }
-  }
-  if (TC) {
-    // TP2: per cell, exclusive max over the ranges (in place in agg) + final max
-    u64* s_max = S.alloc<u64>((size_t)CARRY_SEGS * C);
-    u64* tfinal = S.alloc<u64>(C);
-    if (!s_max || !tfinal) return EVM_ENOMEM;
-    const u32 cb = (C + 63) / 64;
-    KLAUNCH(k_tp_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, (const u64*)agg, s_max);
-    KLAUNCH(k_tp_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_max, prior, prior_present, tfinal);
-    KLAUNCH(k_tp_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, agg, (const u64*)s_max);
-    // TP3: flags + winners, one wave per range
-    KLAUNCH_LDS(k_tp_walk, dim3((G + 3) / 4), dim3(TP_THREADS), (size_t)4 * C * 8, (const u64*)tcs, cell, n, C, cbits,
-                range, G, (const u64*)agg, (const u64*)tfinal, flags, winner, info);
-  } else {
-    // pass 1: per range and cell, the max timestamp and its first index
-    KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
-                a_first, info);
-    // carry: per cell, exclusive scan over ranges seeded with the prior max
-    {
-      u64* s_tc = S.alloc<u64>((size_t)CARRY_SEGS * C);
-      u64* s_rh = S.alloc<u64>((size_t)CARRY_SEGS * C);
-      u32* s_rl = S.alloc<u32>((size_t)CARRY_SEGS * C);
-      u32* s_first = S.alloc<u32>((size_t)CARRY_SEGS * C);
-      if (!s_tc || !s_rh || !s_rl || !s_first) return EVM_ENOMEM;
-      const u32 cb = (C + 63) / 64;
-      KLAUNCH(k_cl_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh, s_rl,
-              s_first);
-      KLAUNCH(k_cl_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_tc, s_rh, s_rl, s_first, prior, prior_present, winner);
-      KLAUNCH(k_cl_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh,
-              s_rl);
-    }
-    KLAUNCH_LDS(k_cl_scan2, dim3(G), dim3(WK_THREADS), (size_t)C * 20, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
-                flags);
-  }
-  // Merkle fold
+  // Merkle fold: LDS XOR histograms per (minute window, chunk), reduced into
+  // leaves -- written straight into the output tree when it starts empty
   u32* px = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN);
   u32* pp = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32));
   const size_t B = (size_t)FOLD_MAXWIN * FOLD_WIN;
@@ -1376,22 +1345,8 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     lxr = S.alloc<int32_t>(B);
   }
   if (!px || !pp || !dx || !dp || !bcnt || !bxor || !lck || !lxr) return EVM_ENOMEM;
-  KLAUNCH(k_cl_fold_hist, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), flags, minute, hash, n, px, pp, info);
-  KLAUNCH(k_cl_fold_reduce, dim3(FR_BLOCKS), dim3(FR_THREADS), px, pp, info, dx, dp, bcnt, bxor);
-  // into an empty tree: build the output speculatively, so the call has one
-  // host round trip; one owner: the leaf kernel writes the tree itself
   evm_tree* spec = nullptr;
-  if (spec_out) {
-    if ((st = tree_alloc_cap(ctx, 1, B, &spec))) return st;
-    KLAUNCH(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), dx, dp, bcnt, bxor, info, spec->ck, spec->xr, spec->pfx,
-            spec->off);
-  } else {
-    KLAUNCH(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), dx, dp, bcnt, bxor, info, lck, lxr, (int32_t*)nullptr,
-            (u64*)nullptr);
-    if (!pend && tree_in->n_leaves == 0 &&
-        (st = tree_finalize_dev(ctx, S, tree_in->n_owners, lck, lxr, &info->n_leaves, B, &spec)))
-      return st;
-  }
+  if (spec_out && (st = tree_alloc_cap(ctx, 1, B, &spec))) return st;
   struct SpecGuard {
     evm_ctx* ctx;
     evm_tree*& t;
@@ -1399,6 +1354,77 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       if (t) tree_destroy(ctx, t);
     }
   } guard{ctx, spec};
+  auto fold = [&](hipStream_t fs) {
+    {
+      evm::ProfScope ps_(ctx, "k_cl_fold_hist", fs);
+      hipLaunchKernelGGL(k_cl_fold_hist<!TC>, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), 0, fs, flags, minute,
+                         hash, n, px, pp, info);
+    }
+    {
+      evm::ProfScope ps_(ctx, "k_cl_fold_reduce", fs);
+      hipLaunchKernelGGL(k_cl_fold_reduce, dim3(FR_BLOCKS), dim3(FR_THREADS), 0, fs, px, pp, info, dx, dp, bcnt, bxor);
+    }
+    evm::ProfScope ps_(ctx, "k_cl_leaves", fs);
+    if (spec)  // one owner, empty: the leaf kernel writes the tree itself
+      hipLaunchKernelGGL(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), 0, fs, dx, dp, bcnt, bxor, info, spec->ck,
+                         spec->xr, spec->pfx, spec->off);
+    else
+      hipLaunchKernelGGL(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), 0, fs, dx, dp, bcnt, bxor, info, lck, lxr,
+                         (int32_t*)nullptr, (u64*)nullptr);
+  };
+  SideFork side(ctx);
+  {
+    const hipStream_t xs = side.stream();
+    HIPR(hipMemsetAsync(xcur, 0, sizeof(u32) << kb, xs));
+    {
+      evm::ProfScope ps_(ctx, "k_xp_scatter", xs);
+      hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), 0, xs, hash, n, kb, cap, xcur, xpairs, info);
+    }
+    {
+      evm::ProfScope ps_(ctx, "k_xp_dedup", xs);
+      hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, xpairs, xcur, cap, n,
+                         (const uint8_t*)ts, stride, cell, info);
+    }
+    if (TC) fold(xs);  // needs no flags: beside the walk
+  }
+  if (TC) {
+    // TP2: per cell, exclusive max over the ranges (in place in agg) + final max
+    u64* s_max = S.alloc<u64>((size_t)CARRY_SEGS * C);
+    u64* tfinal = S.alloc<u64>(C);
+    if (!s_max || !tfinal) return EVM_ENOMEM;
+    const u32 cb = (C + 63) / 64;
+    KLAUNCH(k_tp_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, (const u64*)agg, s_max);
+    KLAUNCH(k_tp_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_max, prior, prior_present, tfinal);
+    KLAUNCH(k_tp_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, agg, (const u64*)s_max);
+    // TP3: flags + winners, one wave per range
+    KLAUNCH_LDS(k_tp_walk, dim3((G + 3) / 4), dim3(TP_THREADS), (size_t)4 * C * 16, (const u64*)tcs, cell, n, C, cbits,
+                range, G, (const u64*)agg, (const u64*)tfinal, flags, winner, info);
+  } else {
+    // pass 1: per range and cell, the max timestamp and its first index
+    KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
+                a_first, info);
+    // carry: per cell, exclusive scan over ranges seeded with the prior max
+    {
+      u64* s_tc = S.alloc<u64>((size_t)CARRY_SEGS * C);
+      u64* s_rh = S.alloc<u64>((size_t)CARRY_SEGS * C);
+      u32* s_rl = S.alloc<u32>((size_t)CARRY_SEGS * C);
+      u32* s_first = S.alloc<u32>((size_t)CARRY_SEGS * C);
+      if (!s_tc || !s_rh || !s_rl || !s_first) return EVM_ENOMEM;
+      const u32 cb = (C + 63) / 64;
+      KLAUNCH(k_cl_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh, s_rl,
+              s_first);
+      KLAUNCH(k_cl_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_tc, s_rh, s_rl, s_first, prior, prior_present, winner);
+      KLAUNCH(k_cl_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, a_tc, a_rh, a_rl, a_first, s_tc, s_rh,
+              s_rl);
+    }
+    KLAUNCH_LDS(k_cl_scan2, dim3(G), dim3(WK_THREADS), (size_t)C * 20, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
+                flags);
+  }
+  if (!TC) fold(ctx->stream);
+  if (!spec_out && !pend && tree_in->n_leaves == 0) {
+    side.join();  // (the tc path's fold ran there)
+    if ((st = tree_finalize_dev(ctx, S, tree_in->n_owners, lck, lxr, &info->n_leaves, B, &spec))) return st;
+  }
   side.join();
   if (pend) {
     // asynchronous: the status record lands in pinned memory; evm_apply_wait finishes

@@ -83,8 +83,10 @@ def test_async_redo_merge_bad_and_general(eng):
     assert fo.cpu().numpy()[5] == L.MSG_BAD and (np.delete(fo.cpu().numpy(), 5) == 0).all()
     # > 2,048 cells: the sort path, finished inside the async call
     many = [("t", "r%d" % i, "c") for i in range(3000)]
-    mm = [{"timestamp": m["timestamp"], "table": "t", "row": "r%d" % (i % 3000), "column": "c", "value": i}
-          for i, m in enumerate(msgs)]
+    import zlib
+
+    mm = [{"timestamp": m["timestamp"], "table": "t", "row": "r%d" % (zlib.crc32(m["timestamp"].encode()) % 3000),
+           "column": "c", "value": i} for i, m in enumerate(msgs)]
     ts2, cell2 = _dev_batch(eng, mm, many)
     f = torch.empty(len(mm), dtype=torch.uint8, device="cuda")
     w = torch.empty(len(many), dtype=torch.int32, device="cuda")
