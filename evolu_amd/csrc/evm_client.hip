@@ -981,9 +981,10 @@ __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* 
 //                   of the walks disappears into the parse
 //   TP2 carry     : per cell, exclusive max over the ranges seeded with the
 //                   prior max; the cell's final max
-//   TP3 k_tp_walk : one wave per range, its rows in batch order against the
-//                   carried max per cell (LDS) -> flags; the message that
-//                   reaches the cell's final max is its winner (the last upsert)
+//   TP3 k_tp_walk : a workgroup per range, a wave per quarter of it, the rows
+//                   in batch order against the carried max per cell (LDS) ->
+//                   flags; the message that reaches the cell's final max is its
+//                   winner (the last upsert)
 // Bytes per message: TP1 46 + 4 in, 16 out; TP3 12 in, 1 out.
 // ============================================================================
 constexpr u64 TP_INVALID = ~0ull;  // tc of a message the walk skips (invalid timestamp or cell id)
@@ -1110,41 +1111,61 @@ __global__ void k_tp_carry_down(u32 C, size_t G, u64* __restrict__ agg, const u6
   }
 }
 
-// TP3: one wave per range (four ranges per workgroup), 64 rows per round in
-// batch order, TPW_PF rounds of (tc, cell) in flight.  The wave keeps its
-// range's running max per cell in LDS (seeded with the carried max).  The
-// lanes of one round that share a cell are matched with ballots; each lane
-// takes the max of its lower peers (a wave prefix-max when the whole round is
-// one cell), then t = max(state, that) decides its flags; the round's last
-// peer of a cell writes the new max.  No barrier: the waves are independent.
+// TP3: one workgroup per range, wave w walks the range's w-th quarter.  A
+// pre-pass (order-free: ds_max_u64) gives each quarter's max per cell; the
+// carried max of quarter w is then the range's carry with quarters 0..w-1
+// folded in.  The walk: 64 rows per round in batch order, TPW_PF rounds of
+// (tc, cell) in flight; the running max per cell in LDS; the lanes of one
+// round that share a cell found through an LDS mask per cell (each lane ORs
+// its bit in, reads the mask back, clears it); each lane takes the max of its
+// lower peers (a wave prefix-max when the round is one cell), t = max(state,
+// that) decides its flags, and the round's last peer of the cell writes the
+// new max.  After the pre-pass the waves never synchronise.
 constexpr int TPW_PF = 8;
+constexpr int TPW_WAVES = TP_THREADS / 64;
 
 __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ tcs, const u32* __restrict__ cell,
-                                                        size_t n, u32 C, int cbits, size_t range_len, size_t G,
+                                                        size_t n, u32 C, size_t range_len,
                                                         const u64* __restrict__ carry, const u64* __restrict__ tfinal,
                                                         uint8_t* __restrict__ flags, int32_t* __restrict__ winner,
                                                         Info* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) u64 tw_lds[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const size_t g = (size_t)blockIdx.x * (TP_THREADS / 64) + wv;
-  if (g >= G) return;  // (waves never synchronise with each other)
-  u64* T = tw_lds + (size_t)wv * 2 * C;  // [C] running max per cell
-  u64* M = T + C;                        // [C] lanes of the current round per cell (zero between rounds)
+  const size_t g = blockIdx.x;
+  u64* T = tw_lds + (size_t)wv * C;                 // [C] running max per cell of this wave's quarter
+  u64* M = tw_lds + (size_t)(TPW_WAVES + wv) * C;  // [C] lanes of the current round per cell (zero between rounds)
+  const size_t sub = range_len / TPW_WAVES;         // a multiple of 64
+  const size_t beg = min(n, g * range_len + wv * sub), end = min(n, beg + sub);
   for (u32 c = lane; c < C; c += 64) {
-    T[c] = carry[g * C + c];
+    T[c] = 0;
     M[c] = 0;
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __syncthreads();
+  // pre-pass: the quarter's max per cell
+  for (size_t i = beg + lane; i < end; i += 64) {
+    const u64 x = tcs[i];
+    if (x != TP_INVALID) atomicMax(&T[__builtin_nontemporal_load(cell + i)], x);
+  }
+  __syncthreads();
+  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
+    u64 run = carry[g * C + c];
+#pragma unroll
+    for (int w = 0; w < TPW_WAVES; ++w) {
+      const size_t o = (size_t)w * C + c;
+      const u64 q = tw_lds[o];
+      tw_lds[o] = run;
+      run = max(run, q);
+    }
+  }
+  __syncthreads();
   const u64 lt = lanemask_lt();
-  const size_t beg = g * range_len, end = min(n, beg + range_len);
   u64 px[TPW_PF];
   u32 pc[TPW_PF];
 #pragma unroll
   for (int r = 0; r < TPW_PF; ++r) {
     const size_t i = beg + 64 * r + lane;
-    px[r] = i < end ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
-    pc[r] = i < end ? __builtin_nontemporal_load(cell + i) : 0u;
+    px[r] = i < end ? tcs[i] : TP_INVALID;
+    pc[r] = i < end ? cell[i] : 0u;
   }
   u32 tie = 0;
   for (size_t first = beg; first < end; first += 64 * TPW_PF) {  // uniform
@@ -1155,14 +1176,13 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
       const u32 c = pc[r];
       {
         const size_t i = f + 64 * TPW_PF + lane;
-        px[r] = i < end ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
-        pc[r] = i < end ? __builtin_nontemporal_load(cell + i) : 0u;
+        px[r] = i < end ? tcs[i] : TP_INVALID;
+        pc[r] = i < end ? cell[i] : 0u;
       }
       if (f >= end) continue;  // uniform
       const bool ok = x != TP_INVALID;
-      // the round's lanes of each cell: every lane ORs its bit into its cell's
-      // mask and reads the mask back (one wave: the LDS runs its instructions in
-      // order), then clears it -- three LDS operations instead of cbits ballots
+      // the round's lanes of each cell (one wave: the LDS runs its
+      // instructions in order, so the read sees every lane's OR)
       if (ok) atomicOr(&M[c], 1ull << lane);
       const u64 peers = ok ? __hip_atomic_load(&M[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0ull;
       if (ok) __hip_atomic_store(&M[c], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -1385,7 +1405,6 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, xpairs, xcur, cap, n,
                          (const uint8_t*)ts, stride, cell, info);
     }
-    if (TC) fold(xs);  // needs no flags: beside the walk
   }
   if (TC) {
     // TP2: per cell, exclusive max over the ranges (in place in agg) + final max
@@ -1396,9 +1415,10 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     KLAUNCH(k_tp_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, (const u64*)agg, s_max);
     KLAUNCH(k_tp_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_max, prior, prior_present, tfinal);
     KLAUNCH(k_tp_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, agg, (const u64*)s_max);
-    // TP3: flags + winners, one wave per range
-    KLAUNCH_LDS(k_tp_walk, dim3((G + 3) / 4), dim3(TP_THREADS), (size_t)4 * C * 16, (const u64*)tcs, cell, n, C, cbits,
-                range, G, (const u64*)agg, (const u64*)tfinal, flags, winner, info);
+    // TP3: flags + winners, a workgroup per range
+    KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * TPW_WAVES * C * 8, (const u64*)tcs, cell, n, C,
+                range, (const u64*)agg, (const u64*)tfinal, flags, winner, info);
+    fold(ctx->stream);  // (needs no flags; on the main stream the side stream's check is all that runs beside)
   } else {
     // pass 1: per range and cell, the max timestamp and its first index
     KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
