@@ -981,10 +981,10 @@ __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* 
 //                   of the walks disappears into the parse
 //   TP2 carry     : per cell, exclusive max over the ranges seeded with the
 //                   prior max; the cell's final max
-//   TP3 k_tp_walk : a workgroup per range, a wave per quarter of it, the rows
-//                   in batch order against the carried max per cell (LDS) ->
-//                   flags; the message that reaches the cell's final max is its
-//                   winner (the last upsert)
+//   TP3 k_tp_walk : a workgroup per range: rows below their cell's running max
+//                   decided on the spot; the rest walked in batch order (LDS
+//                   state) -> flags; the message that reaches the cell's final
+//                   max is its winner (the last upsert)
 // Bytes per message: TP1 46 + 4 in, 16 out; TP3 12 in, 1 out.
 // ============================================================================
 constexpr u64 TP_INVALID = ~0ull;  // tc of a message the walk skips (invalid timestamp or cell id)
@@ -1111,18 +1111,20 @@ __global__ void k_tp_carry_down(u32 C, size_t G, u64* __restrict__ agg, const u6
   }
 }
 
-// TP3: one workgroup per range, wave w walks the range's w-th quarter.  A
-// pre-pass (order-free: ds_max_u64) gives each quarter's max per cell; the
-// carried max of quarter w is then the range's carry with quarters 0..w-1
-// folded in.  The walk: 64 rows per round in batch order, TPW_PF rounds of
-// (tc, cell) in flight; the running max per cell in LDS; the lanes of one
-// round that share a cell found through an LDS mask per cell (each lane ORs
-// its bit in, reads the mask back, clears it); each lane takes the max of its
-// lower peers (a wave prefix-max when the round is one cell), t = max(state,
-// that) decides its flags, and the round's last peer of the cell writes the
-// new max.  After the pre-pass the waves never synchronise.
-constexpr int TPW_PF = 8;
-constexpr int TPW_WAVES = TP_THREADS / 64;
+// TP3: one workgroup per range, the range in chunks of TPC_ROWS rows.  A row
+// whose tc is below its cell's running max at the chunk start is decided on
+// the spot (XOR only: applyMessages.ts:105 holds, :93 does not) -- in a
+// shuffled stream that is nearly every row, so the pass streams at HBM speed.
+// The rest (tc >= that max: possible new maxima, ties) are compacted in
+// batch order into LDS and walked by one wave: 64 candidates per round, the
+// round's lanes of each cell found through an LDS mask per cell (each lane
+// ORs its bit in, reads the mask back, clears it), each lane takes the max of
+// its lower peers (a wave prefix-max when the round is one cell), t =
+// max(running max, that) decides its flags, and the round's last peer of the
+// cell writes the new max.  An ascending stream makes every row a candidate
+// and costs one walk.
+constexpr int TP_WAVES = TP_THREADS / 64;
+constexpr u32 TPC_ROWS = 64 * 4 * TP_WAVES;  // 4 rounds per wave per chunk
 
 __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ tcs, const u32* __restrict__ cell,
                                                         size_t n, u32 C, size_t range_len,
@@ -1130,102 +1132,118 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
                                                         uint8_t* __restrict__ flags, int32_t* __restrict__ winner,
                                                         Info* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) u64 tw_lds[];
+  u64* T = tw_lds;                                       // [C] running max per cell
+  u64* M = T + C;                                        // [C] the walk round's lanes per cell (zero between rounds)
+  u64* cx = M + C;                                       // [TPC_ROWS] candidates: tc
+  u32* ci = reinterpret_cast<u32*>(cx + TPC_ROWS);       // [TPC_ROWS] row index
+  uint16_t* cc = reinterpret_cast<uint16_t*>(ci + TPC_ROWS);  // [TPC_ROWS] cell
+  __shared__ u32 seg[TP_WAVES];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const u64 lt = lanemask_lt();
   const size_t g = blockIdx.x;
-  u64* T = tw_lds + (size_t)wv * C;                 // [C] running max per cell of this wave's quarter
-  u64* M = tw_lds + (size_t)(TPW_WAVES + wv) * C;  // [C] lanes of the current round per cell (zero between rounds)
-  const size_t sub = range_len / TPW_WAVES;         // a multiple of 64
-  const size_t beg = min(n, g * range_len + wv * sub), end = min(n, beg + sub);
-  for (u32 c = lane; c < C; c += 64) {
-    T[c] = 0;
+  const size_t beg = g * range_len, end = min(n, beg + range_len);
+  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
+    T[c] = carry[g * C + c];
     M[c] = 0;
   }
   __syncthreads();
-  // pre-pass: the quarter's max per cell
-  for (size_t i = beg + lane; i < end; i += 64) {
-    const u64 x = tcs[i];
-    if (x != TP_INVALID) atomicMax(&T[__builtin_nontemporal_load(cell + i)], x);
-  }
-  __syncthreads();
-  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
-    u64 run = carry[g * C + c];
-#pragma unroll
-    for (int w = 0; w < TPW_WAVES; ++w) {
-      const size_t o = (size_t)w * C + c;
-      const u64 q = tw_lds[o];
-      tw_lds[o] = run;
-      run = max(run, q);
-    }
-  }
-  __syncthreads();
-  const u64 lt = lanemask_lt();
-  u64 px[TPW_PF];
-  u32 pc[TPW_PF];
-#pragma unroll
-  for (int r = 0; r < TPW_PF; ++r) {
-    const size_t i = beg + 64 * r + lane;
-    px[r] = i < end ? tcs[i] : TP_INVALID;
-    pc[r] = i < end ? cell[i] : 0u;
-  }
   u32 tie = 0;
-  for (size_t first = beg; first < end; first += 64 * TPW_PF) {  // uniform
+  for (size_t base = beg; base < end; base += TPC_ROWS) {
+    // classify this wave's 256 rows; compact the candidates in batch order
+    const size_t wb = base + 256 * wv;
+    u64 x[4];
+    u32 c[4];
 #pragma unroll
-    for (int r = 0; r < TPW_PF; ++r) {
-      const size_t f = first + 64 * r;
-      const u64 x = px[r];
-      const u32 c = pc[r];
-      {
-        const size_t i = f + 64 * TPW_PF + lane;
-        px[r] = i < end ? tcs[i] : TP_INVALID;
-        pc[r] = i < end ? cell[i] : 0u;
+    for (int r = 0; r < 4; ++r) {
+      const size_t i = wb + 64 * r + lane;
+      x[r] = i < end ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
+      c[r] = i < end ? __builtin_nontemporal_load(cell + i) : 0u;
+    }
+    u32 wcnt = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const size_t i = wb + 64 * r + lane;
+      const bool ok = x[r] != TP_INVALID;
+      const bool cand = ok && x[r] >= T[c[r]];
+      if (i < end && !cand) flags[i] = ok ? (uint8_t)EVM_MSG_XOR : (uint8_t)EVM_MSG_BAD;
+      const u64 bal = __ballot(cand);
+      if (cand) {
+        const u32 k = 256 * wv + wcnt + (u32)__popcll(bal & lt);
+        cx[k] = x[r];
+        ci[k] = (u32)i;
+        cc[k] = (uint16_t)c[r];
       }
-      if (f >= end) continue;  // uniform
-      const bool ok = x != TP_INVALID;
-      // the round's lanes of each cell (one wave: the LDS runs its
-      // instructions in order, so the read sees every lane's OR)
-      if (ok) atomicOr(&M[c], 1ull << lane);
-      const u64 peers = ok ? __hip_atomic_load(&M[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0ull;
-      if (ok) __hip_atomic_store(&M[c], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      const u64 act = __ballot(ok);
-      // max tc of the lower lanes of the same cell
-      u64 pm = 0;
-      if (peers == act && act == ~0ull) {
-        // the whole round is one cell: exclusive wave prefix max
-        u64 v = x;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const u64 u = __shfl_up(v, d, 64);
-          if (lane >= d) v = max(v, u);
-        }
-        pm = __shfl_up(v, 1, 64);
-        if (lane == 0) pm = 0;
-      } else {
-        u64 rem = peers & lt;
-        while (__any(rem != 0)) {
-          const int src = rem ? (int)__builtin_ctzll(rem) : lane;
-          const u64 v = __shfl(x, src, 64);
-          if (rem) {
-            pm = max(pm, v);
-            rem &= rem - 1;
+      wcnt += (u32)__popcll(bal);
+    }
+    if (lane == 0) seg[wv] = wcnt;
+    __syncthreads();
+    if (wv == 0) {
+      u32 s0 = seg[0], s1 = seg[1], s2 = seg[2], s3 = seg[3];
+      const u32 total = s0 + s1 + s2 + s3;
+      for (u32 k0 = 0; k0 < total; k0 += 64) {  // uniform
+        const u32 k = k0 + lane;
+        // candidate k of the concatenated wave segments
+        u32 q = k;
+        int sg = 0;
+        if (q >= s0) {
+          q -= s0;
+          sg = 1;
+          if (q >= s1) {
+            q -= s1;
+            sg = 2;
+            if (q >= s2) {
+              q -= s2;
+              sg = 3;
+            }
           }
         }
-      }
-      uint8_t fl = EVM_MSG_BAD;
-      if (ok) {
-        const u64 t = max(T[c], pm);
-        if (x > t) {  // applyMessages.ts:93 and :105 both hold
-          fl = EVM_MSG_UPS | EVM_MSG_XOR;
-          if (x == tfinal[c]) winner[c] = (int32_t)(f + lane);  // reaches the final max: the last upsert
-        } else if (x < t) {  // :105 only (a stale redelivery re-XORs)
-          fl = EVM_MSG_XOR;
-        } else {  // equal tc: the node ranks decide -> the exact path
-          fl = 0;
-          tie = 1;
+        const bool ok = k < total;
+        const u32 slot = 256 * sg + q;
+        const u64 xv = ok ? cx[slot] : 0ull;
+        const u32 cv = ok ? cc[slot] : 0u;
+        if (ok) atomicOr(&M[cv], 1ull << lane);
+        const u64 peers = ok ? __hip_atomic_load(&M[cv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0ull;
+        if (ok) __hip_atomic_store(&M[cv], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const u64 act = __ballot(ok);
+        u64 pm = 0;  // max tc of the lower lanes of the same cell
+        if (peers == act && act == ~0ull) {
+          u64 v = xv;  // the round is one cell: exclusive wave prefix max
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const u64 u = __shfl_up(v, d, 64);
+            if (lane >= d) v = max(v, u);
+          }
+          pm = __shfl_up(v, 1, 64);
+          if (lane == 0) pm = 0;
+        } else {
+          u64 rem = peers & lt;
+          while (__any(rem != 0)) {
+            const int src = rem ? (int)__builtin_ctzll(rem) : lane;
+            const u64 v = __shfl(xv, src, 64);
+            if (rem) {
+              pm = max(pm, v);
+              rem &= rem - 1;
+            }
+          }
         }
-        if ((peers >> lane) == 1ull) T[c] = max(t, x);  // the round's last peer of the cell
+        if (ok) {
+          const u64 t = max(T[cv], pm);
+          uint8_t fl;
+          if (xv > t) {  // applyMessages.ts:93 and :105 both hold
+            fl = EVM_MSG_UPS | EVM_MSG_XOR;
+            if (xv == tfinal[cv]) winner[cv] = (int32_t)ci[slot];  // reaches the final max: the last upsert
+          } else if (xv < t) {  // :105 only
+            fl = EVM_MSG_XOR;
+          } else {  // equal tc: the node ranks decide -> the exact path
+            fl = 0;
+            tie = 1;
+          }
+          flags[ci[slot]] = fl;
+          if ((peers >> lane) == 1ull) T[cv] = max(t, xv);  // the round's last peer of the cell
+        }
       }
-      if (f + lane < end) flags[f + lane] = fl;
     }
+    __syncthreads();
   }
   if (__ballot(tie) && lane == 0) atomic_or_if(&info->ties, 1u);
 }
@@ -1416,8 +1434,8 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     KLAUNCH(k_tp_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_max, prior, prior_present, tfinal);
     KLAUNCH(k_tp_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, agg, (const u64*)s_max);
     // TP3: flags + winners, a workgroup per range
-    KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * TPW_WAVES * C * 8, (const u64*)tcs, cell, n, C,
-                range, (const u64*)agg, (const u64*)tfinal, flags, winner, info);
+    KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14, (const u64*)tcs, cell,
+                n, C, range, (const u64*)agg, (const u64*)tfinal, flags, winner, info);
     fold(ctx->stream);  // (needs no flags; on the main stream the side stream's check is all that runs beside)
   } else {
     // pass 1: per range and cell, the max timestamp and its first index

@@ -210,3 +210,26 @@ def test_tc_path_bad_input(eng):
                                      len(cells), raise_on_error=False)
     eng.set_option(L.OPT_CLIENT_PATH, 0)
     assert st == L.EVM_EINVAL
+
+
+@pytest.mark.parametrize("cells", [1, 64, 1000])
+def test_tc_path_ascending_stream(eng, cells):
+    """Batch order = timestamp order (what a client receives: ORDER BY
+    timestamp): every row is a new maximum of its cell, so every row goes
+    through the walk; bit for bit against the sort path."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    ts_np, cell_np = synth.config2(1_000_000, cells, seed_config=70 + cells)
+    order = np.argsort(ts_np[:, :29].copy().view("S29").ravel(), kind="stable")
+    ts_np, cell_np = ts_np[order], cell_np[order]
+    ts, cell = eng.dev(ts_np), eng.dev(cell_np)
+    res = []
+    for path in (3, 2):
+        eng.set_option(L.OPT_CLIENT_PATH, path)
+        flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), ts, cell, cells)
+        res.append((flags.cpu().numpy(), winner.cpu().numpy(), tree.leaves()[1], tree.leaves()[2]))
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
+    assert (res[0][0] & L.MSG_UPS).mean() > 0.5  # mostly new maxima
