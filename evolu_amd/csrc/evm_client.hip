@@ -1277,7 +1277,44 @@ struct evm_pending {
   evm_tree* spec = nullptr;  // the output tree (an empty one-owner tree_in)
   void* leaves = nullptr;    // the batch's leaves (ck, xr) for a merge at the wait
   size_t leaves_bytes = 0;
+  // the buffers the batch's cross-cell check (second stream) reads after the
+  // call returns -- status record, K1's hashes, the check's buckets -- so the
+  // next batch's kernels, which reuse the scratch arena, never touch them
+  void* dev = nullptr;
+  size_t dev_bytes = 0;
 };
+
+// Geometry of the partitioned cross-cell check for n messages.
+struct XpGeom {
+  int kb;
+  u32 cap;
+};
+static XpGeom xp_geom(size_t n) {
+  XpGeom x;
+  x.kb = 0;
+  while (x.kb < XP_MAX_KB && (n >> x.kb) > XP_AVG) ++x.kb;
+  const size_t avg = (n >> x.kb) + 1;
+  x.cap = (u32)std::min<size_t>(XP_MAX_FILL, avg + avg / 8 + 1024);
+  return x;
+}
+// per-pending device block layout: Info | hash[n] | xcur[2^kb] | xpairs[cap << kb]
+static size_t pend_dev_bytes(size_t n) {
+  const XpGeom x = xp_geom(n);
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  return up(sizeof(Info)) + up(4 * n) + up(4ull << x.kb) + up((8ull * x.cap) << x.kb);
+}
+static void pend_dev_views(void* base, size_t n, Info** info, u32** hash, u32** xcur, u64** xpairs) {
+  const XpGeom x = xp_geom(n);
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  char* p = static_cast<char*>(base);
+  *info = reinterpret_cast<Info*>(p);
+  p += up(sizeof(Info));
+  *hash = reinterpret_cast<u32*>(p);
+  p += up(4 * n);
+  *xcur = reinterpret_cast<u32*>(p);
+  p += up(4ull << x.kb);
+  *xpairs = reinterpret_cast<u64*>(p);
+}
 
 // The streaming paths.  TC: the tc path (TP1-TP3); otherwise the exact walk
 // path (K1 + pass 1 + carry + pass 2 over the full order key).  Both share
@@ -1294,7 +1331,12 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   int st;
   const int cbits = C > 1 ? 32 - __builtin_clz(C - 1) : 0;
   const bool s48 = stride == 48 && ((uintptr_t)ts & 15) == 0;
-  u32* hash = S.alloc<u32>(n);
+  Info* pinfo = nullptr;
+  u32* hash = nullptr;
+  u32* xcur = nullptr;
+  u64* xpairs = nullptr;
+  if (pend) pend_dev_views(pend->dev, n, &pinfo, &hash, &xcur, &xpairs);
+  else hash = S.alloc<u32>(n);
   u32* minute = S.alloc<u32>(n);
   if (!hash || !minute) return EVM_ENOMEM;
   // TC: ranges of TP1/TP3 (multiples of 256 rows); walk path: ranges of the walks
@@ -1348,13 +1390,14 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   // batch timestamps already stored under another cell (global PK)
   if ((st = stored_check(ctx, S, stored, hash, 1, ts, stride, cell, n, info))) return st;
   // cross-cell PK check: partition by hash into fixed-capacity buckets, LDS set per bucket
-  int kb = 0;
-  while (kb < XP_MAX_KB && (n >> kb) > XP_AVG) ++kb;
-  const size_t avg = (n >> kb) + 1;
-  const u32 cap = (u32)std::min<size_t>(XP_MAX_FILL, avg + avg / 8 + 1024);
+  const XpGeom xg = xp_geom(n);
+  const int kb = xg.kb;
+  const u32 cap = xg.cap;
   const u32 xt = (u32)((n + XP_TILE - 1) / XP_TILE);
-  u32* xcur = S.alloc<u32>((size_t)1 << kb);
-  u64* xpairs = S.alloc<u64>(((size_t)cap) << kb);
+  if (!pend) {
+    xcur = S.alloc<u32>((size_t)1 << kb);
+    xpairs = S.alloc<u64>(((size_t)cap) << kb);
+  }
   if (!xcur || !xpairs) return EVM_ENOMEM;
   // it reads only the timestamps, cells and K1's hashes: a second stream runs
   // it beside the walks, forked right after K1 (joined before the status
@@ -1463,15 +1506,23 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     side.join();  // (the tc path's fold ran there)
     if ((st = tree_finalize_dev(ctx, S, tree_in->n_owners, lck, lxr, &info->n_leaves, B, &spec))) return st;
   }
-  side.join();
   if (pend) {
-    // asynchronous: the status record lands in pinned memory; evm_apply_wait finishes
-    HIPR(hipMemcpyAsync(pend->hinfo, info, sizeof(Info), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipEventRecord(pend->ev, ctx->stream));
+    // asynchronous: the second stream finishes the cross-cell check beside the
+    // NEXT batch's kernels; after the main stream's last kernel it lands the
+    // status record in pinned memory.  No join: the main stream goes on.
+    const hipStream_t xs = side.stream();
+    if (xs != ctx->stream) {
+      HIPR(hipEventRecord(ctx->ev_join, ctx->stream));
+      HIPR(hipStreamWaitEvent(xs, ctx->ev_join, 0));
+    }
+    HIPR(hipMemcpyAsync(pend->hinfo, info, sizeof(Info), hipMemcpyDeviceToHost, xs));
+    HIPR(hipEventRecord(pend->ev, xs));
+    side.detach();
     pend->spec = spec;
     spec = nullptr;
     return ST_PENDING;
   }
+  side.join();
   Info hi;
   if ((st = read_info(ctx, info, &hi))) return st;
   if (hi.bad) {
@@ -1618,7 +1669,17 @@ static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
   int st;
   {
     Scratch S(ctx);
-    Info* info = S.alloc<Info>(1);
+    Info* info = nullptr;
+    if (pend) {
+      pend->dev_bytes = pend_dev_bytes(n);
+      pend->dev = block_alloc(ctx, &pend->dev_bytes);
+      if (!pend->dev) return EVM_ENOMEM;
+      u32 *h, *xc;
+      u64* xp;
+      pend_dev_views(pend->dev, n, &info, &h, &xc, &xp);
+    } else {
+      info = S.alloc<Info>(1);
+    }
     evm_rec* prior = S.alloc<evm_rec>(std::max<size_t>(n_cells, 1));
     if (!info || !prior) return EVM_ENOMEM;
     // one launch: the status record, and winner = -1 for every cell; the
@@ -1700,7 +1761,7 @@ int evm_apply_batch_async(evm_ctx* ctx, const evm_tree* tree_in, const char* ts,
   }
   *p = evm_pending{tree_in, ts, stride, n, cell, n_cells, cell_owner, prior_ts, prior_stride, prior_present,
                    stored_ts, stored_stride, n_stored, stored_cell, flags, winner, false, EVM_OK, nullptr,
-                   p->hinfo, p->ev, nullptr, nullptr, 0};
+                   p->hinfo, p->ev, nullptr, nullptr, 0, nullptr, 0};
   const int st = apply_entry(ctx, tree_in, ts, stride, n, cell, n_cells, cell_owner, prior_ts, prior_stride,
                              prior_present, stored_ts, stored_stride, n_stored, stored_cell, flags, winner, &p->done,
                              ctx->client_path, p);
@@ -1710,8 +1771,10 @@ int evm_apply_batch_async(evm_ctx* ctx, const evm_tree* tree_in, const char* ts,
     // finished (or failed) synchronously
     if (p->spec) tree_destroy(ctx, p->spec);
     if (p->leaves) block_free(ctx, p->leaves, p->leaves_bytes);
+    if (p->dev) block_free(ctx, p->dev, p->dev_bytes);
     p->spec = nullptr;
     p->leaves = nullptr;
+    p->dev = nullptr;
     p->status = st;
   }
   *out = p;
@@ -1772,8 +1835,10 @@ int evm_apply_wait(evm_ctx* ctx, evm_pending* p, evm_tree** tree_out) {
     }
     if (p->spec) tree_destroy(ctx, p->spec);
     if (p->leaves) block_free(ctx, p->leaves, p->leaves_bytes);
+    if (p->dev) block_free(ctx, p->dev, p->dev_bytes);
     p->spec = nullptr;
     p->leaves = nullptr;
+    p->dev = nullptr;
     if (!st) st = evm_sync(ctx);
   }
   p->enqueued = false;

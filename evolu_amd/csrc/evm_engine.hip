@@ -435,7 +435,7 @@ static void tree_release(evm_ctx* ctx, evm_tree* t) {
   delete t;
 }
 
-constexpr size_t BLOCK_CACHE = 8;
+constexpr size_t BLOCK_CACHE = 16;
 
 void* evm::block_alloc(evm_ctx* ctx, size_t* bytes) {
   const size_t need = *bytes;

@@ -212,6 +212,8 @@ class SideFork {
       on_ = false;
     }
   }
+  // the side work stays unjoined (the caller ordered what depends on it itself)
+  void detach() { on_ = false; }
   ~SideFork() { join(); }
 
  private:
