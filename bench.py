@@ -93,6 +93,9 @@ def parse():
                     help="server workload: messages per SyncRequest (one owner each, requests in random order); "
                          ">= per-owner: one request per owner (the reference's per-request sync exactly); "
                          "1 = every message shuffled on its own")
+    ap.add_argument("--dom-events", type=int, default=1,
+                    help="1: HIP events around the dominant kernel inside the timed region (the roofline's "
+                         "duration); 0: none in the timed region, the duration from an identical pass after it")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch per kernel (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -289,14 +292,20 @@ def main():
         _, _, tree, _ = eng.apply_batch(empty, ts, cell, a.cells, flags=flags, winner=winner)
         return tree
 
+    host_us = {"enqueue": [], "wait": []}
+
     def run_pipelined(k_steps):
         import collections
 
         q = collections.deque()
         for k in range(k_steps):
             if len(q) == DEPTH:
+                w0 = time.perf_counter()
                 q.popleft().wait()[2].free()
+                host_us["wait"].append((time.perf_counter() - w0) * 1e6)
+            e0 = time.perf_counter()
             q.append(eng.apply_batch_async(empty, ts, cell, a.cells, *outs[k % DEPTH]))
+            host_us["enqueue"].append((time.perf_counter() - e0) * 1e6)
         while q:
             q.popleft().wait()[2].free()
 
@@ -318,13 +327,20 @@ def main():
     # timed region: events only around the dominant kernel's launches
     eng.prof_only(dom)
     eng.prof_reset()
+    eng.prof_enable(bool(a.dom_events))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    host_us["enqueue"].clear()
+    host_us["wait"].clear()
     t0 = time.perf_counter()
     run_pipelined(a.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if not a.dom_events:  # the dominant kernel's duration from an identical pass
+        eng.prof_enable(True)
+        run_pipelined(a.steps)
+        torch.cuda.synchronize()
     eng.prof_enable(False)
     eng.prof_only(None)
     if world > 1:
@@ -384,6 +400,8 @@ def main():
             "roofline": roof,
             "pipeline": {"alg_bytes_per_msg": 120, "ms_per_step_all_kernel_events": ms_all_events,
                          "batches_in_flight": DEPTH,
+                         "host_enqueue_us_avg": sum(host_us["enqueue"]) / max(1, len(host_us["enqueue"])),
+                         "host_wait_us_avg": sum(host_us["wait"]) / max(1, len(host_us["wait"])),
                          "host_to_host_ms_per_step": ms_h2h, "host_to_host_msgs_per_s": a.messages / ms_h2h * 1e3,
                          "pipeline_hbm_frac": 120 * a.messages / (elapsed / a.steps) / HBM_PEAK,
                          "kernels_ms_per_step": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}},

@@ -1297,23 +1297,48 @@ static XpGeom xp_geom(size_t n) {
   x.cap = (u32)std::min<size_t>(XP_MAX_FILL, avg + avg / 8 + 1024);
   return x;
 }
-// per-pending device block layout: Info | hash[n] | xcur[2^kb] | xpairs[cap << kb]
-static size_t pend_dev_bytes(size_t n) {
+// The buffers a streaming batch's second-stream work (cross-cell check, and
+// on the tc path the Merkle fold) reads: the status record, K1's hashes and
+// minutes, the check's buckets, the fold's partials.  One block per pending
+// batch (evm_apply_batch_async), so the next batch's kernels -- which reuse
+// the scratch arena -- never touch them; a synchronous call takes the same
+// layout from the scratch arena.
+struct SideBufs {
+  Info* info;
+  u32* hash;
+  u32* minute;
+  u32* xcur;
+  u64* xpairs;
+  u32 *px, *pp, *dx, *dp, *bcnt, *bxor;
+};
+static size_t side_bufs(void* base, size_t n, SideBufs* v) {
   const XpGeom x = xp_geom(n);
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  return up(sizeof(Info)) + up(4 * n) + up(4ull << x.kb) + up((8ull * x.cap) << x.kb);
-}
-static void pend_dev_views(void* base, size_t n, Info** info, u32** hash, u32** xcur, u64** xpairs) {
-  const XpGeom x = xp_geom(n);
-  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  char* p = static_cast<char*>(base);
-  *info = reinterpret_cast<Info*>(p);
-  p += up(sizeof(Info));
-  *hash = reinterpret_cast<u32*>(p);
-  p += up(4 * n);
-  *xcur = reinterpret_cast<u32*>(p);
-  p += up(4ull << x.kb);
-  *xpairs = reinterpret_cast<u64*>(p);
+  const size_t B = (size_t)FOLD_MAXWIN * FOLD_WIN;
+  const size_t sz[] = {up(sizeof(Info)), up(4 * n), up(4 * n), up(4ull << x.kb), up((8ull * x.cap) << x.kb),
+                       up((size_t)4 * FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN),
+                       up((size_t)4 * FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32)), up(4 * B), up(4 * B),
+                       up(4 * FR_BLOCKS), up(4 * FR_BLOCKS)};
+  size_t off[11], tot = 0;
+  for (int k = 0; k < 11; ++k) {
+    off[k] = tot;
+    tot += sz[k];
+  }
+  if (v && base) {
+    char* p = static_cast<char*>(base);
+    v->info = reinterpret_cast<Info*>(p + off[0]);
+    v->hash = reinterpret_cast<u32*>(p + off[1]);
+    v->minute = reinterpret_cast<u32*>(p + off[2]);
+    v->xcur = reinterpret_cast<u32*>(p + off[3]);
+    v->xpairs = reinterpret_cast<u64*>(p + off[4]);
+    v->px = reinterpret_cast<u32*>(p + off[5]);
+    v->pp = reinterpret_cast<u32*>(p + off[6]);
+    v->dx = reinterpret_cast<u32*>(p + off[7]);
+    v->dp = reinterpret_cast<u32*>(p + off[8]);
+    v->bcnt = reinterpret_cast<u32*>(p + off[9]);
+    v->bxor = reinterpret_cast<u32*>(p + off[10]);
+  }
+  return tot;
 }
 
 // The streaming paths.  TC: the tc path (TP1-TP3); otherwise the exact walk
@@ -1331,14 +1356,14 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   int st;
   const int cbits = C > 1 ? 32 - __builtin_clz(C - 1) : 0;
   const bool s48 = stride == 48 && ((uintptr_t)ts & 15) == 0;
-  Info* pinfo = nullptr;
-  u32* hash = nullptr;
-  u32* xcur = nullptr;
-  u64* xpairs = nullptr;
-  if (pend) pend_dev_views(pend->dev, n, &pinfo, &hash, &xcur, &xpairs);
-  else hash = S.alloc<u32>(n);
-  u32* minute = S.alloc<u32>(n);
-  if (!hash || !minute) return EVM_ENOMEM;
+  SideBufs sb;
+  void* sbase = pend ? pend->dev : static_cast<void*>(S.alloc<char>(side_bufs(nullptr, n, nullptr)));
+  if (!sbase) return EVM_ENOMEM;
+  side_bufs(sbase, n, &sb);
+  u32* hash = sb.hash;
+  u32* minute = sb.minute;
+  u32* xcur = sb.xcur;
+  u64* xpairs = sb.xpairs;
   // TC: ranges of TP1/TP3 (multiples of 256 rows); walk path: ranges of the walks
   size_t range, G;
   if (TC) {
@@ -1394,23 +1419,14 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   const int kb = xg.kb;
   const u32 cap = xg.cap;
   const u32 xt = (u32)((n + XP_TILE - 1) / XP_TILE);
-  if (!pend) {
-    xcur = S.alloc<u32>((size_t)1 << kb);
-    xpairs = S.alloc<u64>(((size_t)cap) << kb);
-  }
-  if (!xcur || !xpairs) return EVM_ENOMEM;
+
   // it reads only the timestamps, cells and K1's hashes: a second stream runs
   // it beside the walks, forked right after K1 (joined before the status
   // read; forked after pass 1 instead: 0.502-0.506 vs 0.497 ms per config-2 step)
   // Merkle fold: LDS XOR histograms per (minute window, chunk), reduced into
   // leaves -- written straight into the output tree when it starts empty
-  u32* px = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN);
-  u32* pp = S.alloc<u32>((size_t)FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32));
+  u32 *px = sb.px, *pp = sb.pp, *dx = sb.dx, *dp = sb.dp, *bcnt = sb.bcnt, *bxor = sb.bxor;
   const size_t B = (size_t)FOLD_MAXWIN * FOLD_WIN;
-  u32* dx = S.alloc<u32>(B);
-  u32* dp = S.alloc<u32>(B);
-  u32* bcnt = S.alloc<u32>(FR_BLOCKS);
-  u32* bxor = S.alloc<u32>(FR_BLOCKS);
   const bool spec_out = tree_in->n_leaves == 0 && tree_in->n_owners == 1;
   u64* lck = nullptr;
   int32_t* lxr = nullptr;
@@ -1466,6 +1482,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, xpairs, xcur, cap, n,
                          (const uint8_t*)ts, stride, cell, info);
     }
+    if (TC) fold(xs);  // the tc path's fold needs no flags: beside the walk (and the next batch)
   }
   if (TC) {
     // TP2: per cell, exclusive max over the ranges (in place in agg) + final max
@@ -1479,7 +1496,6 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     // TP3: flags + winners, a workgroup per range
     KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14, (const u64*)tcs, cell,
                 n, C, range, (const u64*)agg, (const u64*)tfinal, flags, winner, info);
-    fold(ctx->stream);  // (needs no flags; on the main stream the side stream's check is all that runs beside)
   } else {
     // pass 1: per range and cell, the max timestamp and its first index
     KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
@@ -1671,12 +1687,12 @@ static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
     Scratch S(ctx);
     Info* info = nullptr;
     if (pend) {
-      pend->dev_bytes = pend_dev_bytes(n);
+      pend->dev_bytes = side_bufs(nullptr, n, nullptr);
       pend->dev = block_alloc(ctx, &pend->dev_bytes);
       if (!pend->dev) return EVM_ENOMEM;
-      u32 *h, *xc;
-      u64* xp;
-      pend_dev_views(pend->dev, n, &info, &h, &xc, &xp);
+      SideBufs v;
+      side_bufs(pend->dev, n, &v);
+      info = v.info;
     } else {
       info = S.alloc<Info>(1);
     }
