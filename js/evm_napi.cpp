@@ -9,6 +9,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <functional>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -44,6 +46,15 @@ void* ext(napi_env env, napi_value v) {
   napi_get_value_external(env, v, &p);
   return p;
 }
+
+// A context handle: the engine context plus a mutex, so calls from the JS
+// thread and async work on libuv's pool never drive the context at once (one
+// context per thread at a time, include/evm.h).
+struct Ctx {
+  evm_ctx* c;
+  std::mutex m;
+};
+Ctx* ctx_of(napi_env env, napi_value v) { return static_cast<Ctx*>(ext(env, v)); }
 
 napi_value make_ext(napi_env env, void* p) {
   napi_value v;
@@ -110,13 +121,20 @@ napi_value Create(napi_env env, napi_callback_info info) {
   evm_ctx* ctx = nullptr;
   const int st = evm_create((int)u32(env, a[0]), &ctx);
   if (st) return throw_status(env, st, "evm_create");
-  return make_ext(env, ctx);
+  Ctx* c = new Ctx();
+  c->c = ctx;
+  return make_ext(env, c);
 }
 
 napi_value Destroy(napi_env env, napi_callback_info info) {
   napi_value a[1];
   if (!get_args(env, info, 1, a)) return nullptr;
-  evm_destroy((evm_ctx*)ext(env, a[0]));
+  Ctx* c = ctx_of(env, a[0]);
+  {
+    std::lock_guard<std::mutex> g(c->m);
+    evm_destroy(c->c);
+  }
+  delete c;
   return nullptr;
 }
 
@@ -124,7 +142,9 @@ napi_value Destroy(napi_env env, napi_callback_info info) {
 napi_value TreeFromJson(napi_env env, napi_callback_info info) {
   napi_value a[2];
   if (!get_args(env, info, 2, a)) return nullptr;
-  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
   uint32_t n = 0;
   NAPI_OK(env, napi_get_array_length(env, a[1], &n));
   std::vector<std::string> s(n);
@@ -150,7 +170,9 @@ napi_value TreeFromJson(napi_env env, napi_callback_info info) {
 napi_value TreeToJson(napi_env env, napi_callback_info info) {
   napi_value a[3];
   if (!get_args(env, info, 3, a)) return nullptr;
-  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
   const evm_tree* t = (const evm_tree*)ext(env, a[1]);
   size_t len = 0;
   int st = evm_tree_to_json(ctx, t, u32(env, a[2]), nullptr, 0, &len);
@@ -166,7 +188,9 @@ napi_value TreeToJson(napi_env env, napi_callback_info info) {
 napi_value TreeFree(napi_env env, napi_callback_info info) {
   napi_value a[2];
   if (!get_args(env, info, 2, a)) return nullptr;
-  evm_tree_free((evm_ctx*)ext(env, a[0]), (evm_tree*)ext(env, a[1]));
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_tree_free(cx->c, (evm_tree*)ext(env, a[1]));
   return nullptr;
 }
 
@@ -174,7 +198,9 @@ napi_value TreeFree(napi_env env, napi_callback_info info) {
 napi_value Diff(napi_env env, napi_callback_info info) {
   napi_value a[3];
   if (!get_args(env, info, 3, a)) return nullptr;
-  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
   const evm_tree* x = (const evm_tree*)ext(env, a[1]);
   const evm_tree* y = (const evm_tree*)ext(env, a[2]);
   uint32_t no = 0;
@@ -194,7 +220,9 @@ napi_value Diff(napi_env env, napi_callback_info info) {
 napi_value Insert(napi_env env, napi_callback_info info) {
   napi_value a[5];
   if (!get_args(env, info, 5, a)) return nullptr;
-  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
   const evm_tree* t = (const evm_tree*)ext(env, a[1]);
   void* ts;
   size_t tl;
@@ -213,46 +241,197 @@ napi_value Insert(napi_env env, napi_callback_info info) {
   return make_ext(env, out);
 }
 
-// ---------------------------------------------------------------- applyMessages.ts:26-131
-// applyBatch(ctx, tree, ts Uint8Array, stride, cell Uint32Array, nCells, priorTs|null, priorPresent|null)
-//   -> { status, flags: Uint8Array, winner: Int32Array, tree }
-napi_value ApplyBatch(napi_env env, napi_callback_info info) {
-  napi_value a[8];
-  if (!get_args(env, info, 8, a)) return nullptr;
-  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
-  const evm_tree* t = (const evm_tree*)ext(env, a[1]);
-  void *ts, *cell, *pts = nullptr, *pp = nullptr;
-  size_t tl, cl, ptl = 0, ppl = 0;
-  if (!bytes_of(env, a[2], &ts, &tl) || !bytes_of(env, a[4], &cell, &cl)) return nullptr;
-  const size_t stride = u32(env, a[3]);
-  const uint32_t nc = u32(env, a[5]);
-  napi_valuetype vt;
-  napi_typeof(env, a[6], &vt);
-  if (vt != napi_null && vt != napi_undefined) {
-    if (!bytes_of(env, a[6], &pts, &ptl) || !bytes_of(env, a[7], &pp, &ppl)) return nullptr;
+// ---------------------------------------------------------------- async work
+// applyMessages is a ReaderTaskEither (applyMessages.ts:26-31): the *Async
+// entry points run the batch on libuv's pool (napi_create_async_work) and
+// return a Promise of an fp-ts Either -- { _tag: "Right", right } or
+// { _tag: "Left", left: UnknownError } (types.ts:358-372) -- so the worker's
+// event loop is never blocked on the GPU.  The caller's typed arrays are
+// held by references until the work completes.
+struct Async {
+  Ctx* cx;
+  napi_deferred deferred = nullptr;
+  napi_async_work work = nullptr;
+  std::vector<napi_ref> refs;
+  std::function<int()> exec;                    // on the pool thread, context locked and bound
+  std::function<napi_value(napi_env, int)> done;  // on the JS thread: the Right value for a status
+  int status = EVM_OK;
+};
+
+napi_value either(napi_env env, bool right, napi_value v) {
+  napi_value o, tag;
+  napi_create_object(env, &o);
+  napi_create_string_utf8(env, right ? "Right" : "Left", NAPI_AUTO_LENGTH, &tag);
+  napi_set_named_property(env, o, "_tag", tag);
+  napi_set_named_property(env, o, right ? "right" : "left", v);
+  return o;
+}
+
+// UnknownError { type, error: { message, stack } } (types.ts:358-372)
+napi_value unknown_error(napi_env env, int st, const char* where) {
+  napi_value err, inner, v;
+  napi_create_object(env, &err);
+  napi_create_string_utf8(env, "UnknownError", NAPI_AUTO_LENGTH, &v);
+  napi_set_named_property(env, err, "type", v);
+  napi_create_object(env, &inner);
+  const std::string m = std::string(where) + ": " + evm_strerror(st);
+  napi_create_string_utf8(env, m.c_str(), m.size(), &v);
+  napi_set_named_property(env, inner, "message", v);
+  napi_get_undefined(env, &v);
+  napi_set_named_property(env, inner, "stack", v);
+  napi_set_named_property(env, err, "error", inner);
+  return err;
+}
+
+void async_execute(napi_env, void* data) {
+  Async* a = static_cast<Async*>(data);
+  std::lock_guard<std::mutex> lock(a->cx->m);
+  a->status = evm_bind_thread(a->cx->c);
+  if (!a->status) a->status = a->exec();
+}
+
+void async_complete(napi_env env, napi_status, void* data) {
+  Async* a = static_cast<Async*>(data);
+  napi_value v = a->done(env, a->status);  // null: a device error
+  if (v) napi_resolve_deferred(env, a->deferred, either(env, true, v));
+  else napi_resolve_deferred(env, a->deferred, either(env, false, unknown_error(env, a->status, "evolu_evm")));
+  for (napi_ref r : a->refs) napi_delete_reference(env, r);
+  napi_delete_async_work(env, a->work);
+  delete a;
+}
+
+// queues `a`, keeping the given values alive; -> the Promise
+napi_value queue(napi_env env, Async* a, napi_value* keep, size_t nkeep) {
+  for (size_t i = 0; i < nkeep; ++i) {
+    napi_valuetype t;
+    napi_typeof(env, keep[i], &t);
+    if (t != napi_object) continue;
+    napi_ref r;
+    if (napi_create_reference(env, keep[i], 1, &r) == napi_ok) a->refs.push_back(r);
   }
-  const size_t n = stride ? tl / stride : 0;
-  Dev dts(ctx, tl, ts), dcell(ctx, cl, cell), dpts(ctx, ptl, pts), dpp(ctx, ppl, pp);
-  Dev dflags(ctx, n), dwin(ctx, sizeof(int32_t) * (nc ? nc : 1));
+  napi_value promise, name;
+  napi_create_promise(env, &a->deferred, &promise);
+  napi_create_string_utf8(env, "evolu_evm", NAPI_AUTO_LENGTH, &name);
+  napi_create_async_work(env, nullptr, name, async_execute, async_complete, a, &a->work);
+  napi_queue_async_work(env, a->work);
+  return promise;
+}
+
+bool is_null(napi_env env, napi_value v) {
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  return t == napi_null || t == napi_undefined;
+}
+
+// ---------------------------------------------------------------- applyMessages.ts:26-131
+// applyBatch(ctx, tree, ts Uint8Array, stride, cell Uint32Array, nCells, priorTs|null, priorPresent|null
+//            [, storedTs|null, storedCell|null])
+//   -> { status, flags: Uint8Array, winner: Int32Array, tree }
+// storedTs / storedCell: the __message rows holding a batch timestamp
+// (SELECT ... WHERE "timestamp" IN (...)), evm_apply_batch_ex.
+struct ApplyJob {
+  evm_ctx* ctx = nullptr;
+  const evm_tree* t = nullptr;
+  void *ts = nullptr, *cell = nullptr, *pts = nullptr, *pp = nullptr, *sts = nullptr, *sc = nullptr;
+  size_t tl = 0, cl = 0, ptl = 0, ppl = 0, stl = 0, scl = 0, stride = 48;
+  uint32_t nc = 0;
+  std::vector<uint8_t> flags;
+  std::vector<int32_t> winner;
   evm_tree* out = nullptr;
-  const int st = evm_apply_batch(ctx, t, (const char*)dts.p, stride, n, (const uint32_t*)dcell.p, nc, nullptr,
-                                 pts ? (const char*)dpts.p : nullptr, nc ? ptl / nc : 48,
-                                 pp ? (const uint8_t*)dpp.p : nullptr, (uint8_t*)dflags.p, (int32_t*)dwin.p, &out);
-  napi_value res, v;
-  napi_create_object(env, &res);
-  napi_create_int32(env, st, &v);
-  napi_set_named_property(env, res, "status", v);
+
+  bool parse(napi_env env, napi_value* a, size_t argc) {
+    if (!bytes_of(env, a[2], &ts, &tl) || !bytes_of(env, a[4], &cell, &cl)) return false;
+    stride = u32(env, a[3]);
+    nc = u32(env, a[5]);
+    if (!is_null(env, a[6]) && (!bytes_of(env, a[6], &pts, &ptl) || !bytes_of(env, a[7], &pp, &ppl))) return false;
+    if (argc >= 10 && !is_null(env, a[8]) && (!bytes_of(env, a[8], &sts, &stl) || !bytes_of(env, a[9], &sc, &scl)))
+      return false;
+    return true;
+  }
+  // H2D, the batch, D2H -- on the calling thread, context locked
+  int run() {
+    const size_t n = stride ? tl / stride : 0;
+    const size_t ns = scl / 4;
+    Dev dts(ctx, tl, ts), dcell(ctx, cl, cell), dpts(ctx, ptl, pts), dpp(ctx, ppl, pp), dsts(ctx, stl, sts),
+        dsc(ctx, scl, sc);
+    Dev dflags(ctx, n), dwin(ctx, sizeof(int32_t) * (nc ? nc : 1));
+    const int st = evm_apply_batch_ex(ctx, t, (const char*)dts.p, stride, n, (const uint32_t*)dcell.p, nc, nullptr,
+                                      pts ? (const char*)dpts.p : nullptr, nc ? ptl / nc : 48,
+                                      pp ? (const uint8_t*)dpp.p : nullptr, ns ? (const char*)dsts.p : nullptr,
+                                      ns ? stl / ns : 48, ns, ns ? (const uint32_t*)dsc.p : nullptr,
+                                      (uint8_t*)dflags.p, (int32_t*)dwin.p, &out);
+    if (st != EVM_OK && st != EVM_ENONCANON && st != EVM_ECOLLISION) return st;
+    flags.resize(n);
+    winner.resize(nc);
+    evm_copy_d2h(ctx, flags.data(), dflags.p, n);
+    evm_copy_d2h(ctx, winner.data(), dwin.p, sizeof(int32_t) * nc);
+    return st;
+  }
+  napi_value result(napi_env env, int st) {
+    napi_value res, v;
+    napi_create_object(env, &res);
+    napi_create_int32(env, st, &v);
+    napi_set_named_property(env, res, "status", v);
+    void* fh;
+    napi_value fl = typed(env, napi_uint8_array, flags.size(), 1, &fh);
+    if (!flags.empty()) memcpy(fh, flags.data(), flags.size());
+    napi_set_named_property(env, res, "flags", fl);
+    void* wh;
+    napi_value win = typed(env, napi_int32_array, winner.size(), 4, &wh);
+    if (!winner.empty()) memcpy(wh, winner.data(), 4 * winner.size());
+    napi_set_named_property(env, res, "winner", win);
+    if (out) napi_set_named_property(env, res, "tree", make_ext(env, out));
+    return res;
+  }
+};
+
+napi_value ApplyBatch(napi_env env, napi_callback_info info) {
+  napi_value a[10];
+  size_t argc = 10;
+  if (napi_get_cb_info(env, info, &argc, a, nullptr, nullptr) != napi_ok || argc < 8) {
+    napi_throw_type_error(env, nullptr, "missing arguments");
+    return nullptr;
+  }
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  ApplyJob j;
+  j.ctx = cx->c;
+  j.t = (const evm_tree*)ext(env, a[1]);
+  if (!j.parse(env, a, argc)) return nullptr;
+  const int st = j.run();
   if (st != EVM_OK && st != EVM_ENONCANON && st != EVM_ECOLLISION) return throw_status(env, st, "evm_apply_batch");
-  void* fh;
-  napi_value flags = typed(env, napi_uint8_array, n, 1, &fh);
-  evm_copy_d2h(ctx, fh, dflags.p, n);
-  napi_set_named_property(env, res, "flags", flags);
-  void* wh;
-  napi_value win = typed(env, napi_int32_array, nc, 4, &wh);
-  evm_copy_d2h(ctx, wh, dwin.p, sizeof(int32_t) * nc);
-  napi_set_named_property(env, res, "winner", win);
-  if (out) napi_set_named_property(env, res, "tree", make_ext(env, out));
-  return res;
+  return j.result(env, st);
+}
+
+// applyBatchAsync(same arguments) -> Promise<Either<UnknownError, { status, flags, winner, tree }>>
+napi_value ApplyBatchAsync(napi_env env, napi_callback_info info) {
+  napi_value a[10];
+  size_t argc = 10;
+  if (napi_get_cb_info(env, info, &argc, a, nullptr, nullptr) != napi_ok || argc < 8) {
+    napi_throw_type_error(env, nullptr, "missing arguments");
+    return nullptr;
+  }
+  auto* j = new ApplyJob();
+  Async* as = new Async();
+  as->cx = ctx_of(env, a[0]);
+  j->ctx = as->cx->c;
+  j->t = (const evm_tree*)ext(env, a[1]);
+  if (!j->parse(env, a, argc)) {
+    delete j;
+    delete as;
+    return nullptr;
+  }
+  as->exec = [j]() {
+    const int st = j->run();
+    return st;
+  };
+  as->done = [j](napi_env e, int st) -> napi_value {
+    napi_value v = nullptr;
+    if (st == EVM_OK || st == EVM_ENONCANON || st == EVM_ECOLLISION) v = j->result(e, st);
+    delete j;
+    return v;
+  };
+  return queue(env, as, a + 1, argc - 1);
 }
 
 // ---------------------------------------------------------------- server (index.ts)
@@ -260,7 +439,9 @@ napi_value StoreNew(napi_env env, napi_callback_info info) {
   napi_value a[2];
   if (!get_args(env, info, 2, a)) return nullptr;
   evm_store* s = nullptr;
-  const int st = evm_store_new((evm_ctx*)ext(env, a[0]), u32(env, a[1]), &s);
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  const int st = evm_store_new(cx->c, u32(env, a[1]), &s);
   if (st) return throw_status(env, st, "evm_store_new");
   return make_ext(env, s);
 }
@@ -268,7 +449,9 @@ napi_value StoreNew(napi_env env, napi_callback_info info) {
 napi_value StoreFree(napi_env env, napi_callback_info info) {
   napi_value a[2];
   if (!get_args(env, info, 2, a)) return nullptr;
-  evm_store_free((evm_ctx*)ext(env, a[0]), (evm_store*)ext(env, a[1]));
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_store_free(cx->c, (evm_store*)ext(env, a[1]));
   return nullptr;
 }
 
@@ -279,69 +462,157 @@ napi_value StoreTree(napi_env env, napi_callback_info info) {
 }
 
 // serverIngest(ctx, store, ts Uint8Array, stride, owner Uint32Array, idBase) -> { status, flags }
+struct IngestJob {
+  evm_ctx* ctx = nullptr;
+  evm_store* s = nullptr;
+  void *ts = nullptr, *ow = nullptr;
+  size_t tl = 0, ol = 0, stride = 48;
+  double base = 0;
+  std::vector<uint8_t> flags;
+  bool parse(napi_env env, napi_value* a) {
+    s = (evm_store*)ext(env, a[1]);
+    if (!bytes_of(env, a[2], &ts, &tl) || !bytes_of(env, a[4], &ow, &ol)) return false;
+    stride = u32(env, a[3]);
+    napi_get_value_double(env, a[5], &base);
+    return true;
+  }
+  int run() {
+    const size_t n = stride ? tl / stride : 0;
+    Dev dts(ctx, tl, ts), dow(ctx, ol, ow), dfl(ctx, n);
+    const int st = evm_server_ingest(ctx, s, (const char*)dts.p, stride, n, (const uint32_t*)dow.p, (uint64_t)base,
+                                     (uint8_t*)dfl.p);
+    if (st != EVM_OK && st != EVM_ENONCANON) return st;
+    flags.resize(n);
+    evm_copy_d2h(ctx, flags.data(), dfl.p, n);
+    return st;
+  }
+  napi_value result(napi_env env, int st) {
+    napi_value res, v;
+    napi_create_object(env, &res);
+    napi_create_int32(env, st, &v);
+    napi_set_named_property(env, res, "status", v);
+    void* fh;
+    napi_value fl = typed(env, napi_uint8_array, flags.size(), 1, &fh);
+    if (!flags.empty()) memcpy(fh, flags.data(), flags.size());
+    napi_set_named_property(env, res, "flags", fl);
+    return res;
+  }
+};
+
 napi_value ServerIngest(napi_env env, napi_callback_info info) {
   napi_value a[6];
   if (!get_args(env, info, 6, a)) return nullptr;
-  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
-  evm_store* s = (evm_store*)ext(env, a[1]);
-  void *ts, *ow;
-  size_t tl, ol;
-  if (!bytes_of(env, a[2], &ts, &tl) || !bytes_of(env, a[4], &ow, &ol)) return nullptr;
-  const size_t stride = u32(env, a[3]);
-  const size_t n = stride ? tl / stride : 0;
-  double base = 0;
-  napi_get_value_double(env, a[5], &base);
-  Dev dts(ctx, tl, ts), dow(ctx, ol, ow), dfl(ctx, n);
-  const int st = evm_server_ingest(ctx, s, (const char*)dts.p, stride, n, (const uint32_t*)dow.p, (uint64_t)base,
-                                   (uint8_t*)dfl.p);
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  IngestJob j;
+  j.ctx = cx->c;
+  if (!j.parse(env, a)) return nullptr;
+  const int st = j.run();
   if (st != EVM_OK && st != EVM_ENONCANON) return throw_status(env, st, "evm_server_ingest");
-  napi_value res, v;
-  napi_create_object(env, &res);
-  napi_create_int32(env, st, &v);
-  napi_set_named_property(env, res, "status", v);
-  void* fh;
-  napi_value flags = typed(env, napi_uint8_array, n, 1, &fh);
-  evm_copy_d2h(ctx, fh, dfl.p, n);
-  napi_set_named_property(env, res, "flags", flags);
-  return res;
+  return j.result(env, st);
+}
+
+napi_value ServerIngestAsync(napi_env env, napi_callback_info info) {
+  napi_value a[6];
+  if (!get_args(env, info, 6, a)) return nullptr;
+  auto* j = new IngestJob();
+  Async* as = new Async();
+  as->cx = ctx_of(env, a[0]);
+  j->ctx = as->cx->c;
+  if (!j->parse(env, a)) {
+    delete j;
+    delete as;
+    return nullptr;
+  }
+  as->exec = [j]() { return j->run(); };
+  as->done = [j](napi_env e, int st) -> napi_value {
+    napi_value v = (st == EVM_OK || st == EVM_ENONCANON) ? j->result(e, st) : nullptr;
+    delete j;
+    return v;
+  };
+  return queue(env, as, a + 1, 5);
 }
 
 // serverSelect(ctx, store, clientTree, node Uint8Array(16 * nOwners)) -> { diff, off, ids } (Float64Arrays)
+struct SelectJob {
+  evm_ctx* ctx = nullptr;
+  const evm_store* s = nullptr;
+  const evm_tree* c = nullptr;
+  void* node = nullptr;
+  size_t nl = 0;
+  std::vector<int64_t> hd;
+  std::vector<uint64_t> ho, hi;
+  bool parse(napi_env env, napi_value* a) {
+    s = (const evm_store*)ext(env, a[1]);
+    c = (const evm_tree*)ext(env, a[2]);
+    return bytes_of(env, a[3], &node, &nl);
+  }
+  int run() {
+    uint32_t no = 0;
+    uint64_t nm = 0;
+    evm_store_info(s, &no, &nm);
+    Dev dn(ctx, nl, node), dd(ctx, 8 * (no ? no : 1)), doff(ctx, 8 * (no + 1)), dids(ctx, 8 * (nm ? nm : 1));
+    uint64_t nsel = 0;
+    const int st = evm_server_select(ctx, s, c, (const char*)dn.p, nullptr, (int64_t*)dd.p, (uint64_t*)doff.p,
+                                     (uint64_t*)dids.p, nm, &nsel);
+    if (st) return st;
+    hd.resize(no);
+    ho.resize(no + 1);
+    hi.resize(nsel);
+    evm_copy_d2h(ctx, hd.data(), dd.p, 8 * no);
+    evm_copy_d2h(ctx, ho.data(), doff.p, 8 * (no + 1));
+    evm_copy_d2h(ctx, hi.data(), dids.p, 8 * nsel);
+    return EVM_OK;
+  }
+  napi_value result(napi_env env) {
+    napi_value res;
+    napi_create_object(env, &res);
+    double* p;
+    napi_value x = typed(env, napi_float64_array, hd.size(), 8, (void**)&p);
+    for (size_t i = 0; i < hd.size(); ++i) p[i] = (double)hd[i];
+    napi_set_named_property(env, res, "diff", x);
+    x = typed(env, napi_float64_array, ho.size(), 8, (void**)&p);
+    for (size_t i = 0; i < ho.size(); ++i) p[i] = (double)ho[i];
+    napi_set_named_property(env, res, "off", x);
+    x = typed(env, napi_float64_array, hi.size(), 8, (void**)&p);
+    for (size_t i = 0; i < hi.size(); ++i) p[i] = (double)hi[i];
+    napi_set_named_property(env, res, "ids", x);
+    return res;
+  }
+};
+
 napi_value ServerSelect(napi_env env, napi_callback_info info) {
   napi_value a[4];
   if (!get_args(env, info, 4, a)) return nullptr;
-  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
-  const evm_store* s = (const evm_store*)ext(env, a[1]);
-  const evm_tree* c = (const evm_tree*)ext(env, a[2]);
-  void* node;
-  size_t nl;
-  if (!bytes_of(env, a[3], &node, &nl)) return nullptr;
-  uint32_t no = 0;
-  uint64_t nm = 0;
-  evm_store_info(s, &no, &nm);
-  Dev dn(ctx, nl, node), dd(ctx, 8 * (no ? no : 1)), doff(ctx, 8 * (no + 1)), dids(ctx, 8 * (nm ? nm : 1));
-  uint64_t nsel = 0;
-  const int st = evm_server_select(ctx, s, c, (const char*)dn.p, nullptr, (int64_t*)dd.p, (uint64_t*)doff.p,
-                                   (uint64_t*)dids.p, nm, &nsel);
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  SelectJob j;
+  j.ctx = cx->c;
+  if (!j.parse(env, a)) return nullptr;
+  const int st = j.run();
   if (st) return throw_status(env, st, "evm_server_select");
-  std::vector<int64_t> hd(no);
-  std::vector<uint64_t> ho(no + 1), hi(nsel);
-  evm_copy_d2h(ctx, hd.data(), dd.p, 8 * no);
-  evm_copy_d2h(ctx, ho.data(), doff.p, 8 * (no + 1));
-  evm_copy_d2h(ctx, hi.data(), dids.p, 8 * nsel);
-  napi_value res;
-  napi_create_object(env, &res);
-  double* p;
-  napi_value x = typed(env, napi_float64_array, no, 8, (void**)&p);
-  for (uint32_t i = 0; i < no; ++i) p[i] = (double)hd[i];
-  napi_set_named_property(env, res, "diff", x);
-  x = typed(env, napi_float64_array, no + 1, 8, (void**)&p);
-  for (uint32_t i = 0; i <= no; ++i) p[i] = (double)ho[i];
-  napi_set_named_property(env, res, "off", x);
-  x = typed(env, napi_float64_array, nsel, 8, (void**)&p);
-  for (uint64_t i = 0; i < nsel; ++i) p[i] = (double)hi[i];
-  napi_set_named_property(env, res, "ids", x);
-  return res;
+  return j.result(env);
+}
+
+napi_value ServerSelectAsync(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  if (!get_args(env, info, 4, a)) return nullptr;
+  auto* j = new SelectJob();
+  Async* as = new Async();
+  as->cx = ctx_of(env, a[0]);
+  j->ctx = as->cx->c;
+  if (!j->parse(env, a)) {
+    delete j;
+    delete as;
+    return nullptr;
+  }
+  as->exec = [j]() { return j->run(); };
+  as->done = [j](napi_env e, int st) -> napi_value {
+    napi_value v = st == EVM_OK ? j->result(e) : nullptr;
+    delete j;
+    return v;
+  };
+  return queue(env, as, a + 1, 3);
 }
 
 // storeSince(ctx, store, since Float64Array(nOwners), -1 = none) -> { off, ids } (Float64Arrays)
@@ -349,7 +620,9 @@ napi_value ServerSelect(napi_env env, napi_callback_info info) {
 napi_value StoreSince(napi_env env, napi_callback_info info) {
   napi_value a[3];
   if (!get_args(env, info, 3, a)) return nullptr;
-  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
   const evm_store* s = (const evm_store*)ext(env, a[1]);
   void* sv;
   size_t sl;
@@ -384,7 +657,9 @@ napi_value StoreSince(napi_env env, napi_callback_info info) {
 napi_value ReceiveFold(napi_env env, napi_callback_info info) {
   napi_value a[8];
   if (!get_args(env, info, 8, a)) return nullptr;
-  evm_ctx* ctx = (evm_ctx*)ext(env, a[0]);
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
   void* ts;
   size_t tl;
   if (!bytes_of(env, a[1], &ts, &tl)) return nullptr;
@@ -504,6 +779,8 @@ napi_value Init(napi_env env, napi_value exports) {
   } fns[] = {{"create", Create},         {"destroy", Destroy},       {"treeFromJson", TreeFromJson},
              {"treeToJson", TreeToJson}, {"treeFree", TreeFree},     {"diff", Diff},
              {"insert", Insert},         {"applyBatch", ApplyBatch}, {"storeNew", StoreNew},
+             {"applyBatchAsync", ApplyBatchAsync}, {"serverIngestAsync", ServerIngestAsync},
+             {"serverSelectAsync", ServerSelectAsync},
              {"storeFree", StoreFree},   {"storeTree", StoreTree},   {"serverIngest", ServerIngest},
              {"serverSelect", ServerSelect}, {"storeSince", StoreSince}, {"receiveFold", ReceiveFold},
              {"pbDecode", PbDecode},         {"pbEncode", PbEncode}};

@@ -79,14 +79,36 @@ class Engine {
   }
 
   // applyMessages.ts:26-131.  db: { cellMax(table, row, column) -> string|null,
-  // upsert(table, row, column, value), insertMessage(message) }.
-  // Returns the new MerkleTree JSON, or null when the batch needs the reference path.
+  // storedRows(timestamps) -> [{timestamp, table, row, column}] (optional: the
+  // "__message" rows holding one of the batch's timestamps, PK "timestamp",
+  // initDbModel.ts:44), upsert(table, row, column, value), insertMessage(message) }.
+  // Returns the new MerkleTree JSON, or null when the batch needs the reference path
+  // (a non-canonical timestamp, or one timestamp under two cells in the batch or
+  // against a stored row: the reference then ignores that INSERT, :104-119).
   applyMessages(db, treeJson, messages) {
+    const args = this._applyArgs(db, treeJson, messages);
+    const r = addon.applyBatch(this.ctx, ...args);
+    addon.treeFree(this.ctx, args[0]);
+    return this._applyWrites(db, messages, r);
+  }
+
+  // the same, the GPU work on a libuv worker thread: Promise<Either<UnknownError, json|null>>
+  // (the reference's Effect-returning shape, types.ts:317-399)
+  async applyMessagesAsync(db, treeJson, messages) {
+    const args = this._applyArgs(db, treeJson, messages);
+    const e = await addon.applyBatchAsync(this.ctx, ...args);
+    addon.treeFree(this.ctx, args[0]);
+    if (e._tag === "Left") return e;
+    return { _tag: "Right", right: this._applyWrites(db, messages, e.right) };
+  }
+
+  _applyArgs(db, treeJson, messages) {
     const ids = new Map();
     const cells = [];
     const cell = new Uint32Array(messages.length);
+    const key = (m) => JSON.stringify([m.table, m.row, m.column]);
     messages.forEach((m, i) => {
-      const k = JSON.stringify([m.table, m.row, m.column]);
+      const k = key(m);
       let c = ids.get(k);
       if (c === undefined) {
         c = cells.length;
@@ -98,10 +120,21 @@ class Engine {
     // the cells' current maxima: SELECT "timestamp" ... ORDER BY "timestamp" DESC LIMIT 1 (applyMessages.ts:34-40)
     const prior = cells.map((m) => db.cellMax(m.table, m.row, m.column));
     const priorPresent = Uint8Array.from(prior.map((p) => (p == null ? 0 : 1)));
-    const t = this._tree(treeJson);
-    const r = addon.applyBatch(this.ctx, t, encodeTimestamps(messages.map((m) => m.timestamp)), STRIDE, cell,
-      cells.length, encodeTimestamps(prior.map((p) => (p == null ? "" : p))), priorPresent);
-    addon.treeFree(this.ctx, t);
+    let storedTs = null;
+    let storedCell = null;
+    if (typeof db.storedRows === "function") {
+      const rows = db.storedRows(Array.from(new Set(messages.map((m) => m.timestamp))));
+      if (rows.length) {
+        storedTs = encodeTimestamps(rows.map((r) => r.timestamp));
+        // a row of a cell the batch does not touch: any id >= the cell count
+        storedCell = Uint32Array.from(rows, (r) => { const c = ids.get(key(r)); return c === undefined ? 0xffffffff : c; });
+      }
+    }
+    return [this._tree(treeJson), encodeTimestamps(messages.map((m) => m.timestamp)), STRIDE, cell, cells.length,
+      encodeTimestamps(prior.map((p) => (p == null ? "" : p))), priorPresent, storedTs, storedCell];
+  }
+
+  _applyWrites(db, messages, r) {
     if (r.status === EVM_ENONCANON || r.status === EVM_ECOLLISION) return null;
     // the same statements the reference runs, in batch order: the final upsert
     // of every cell, and INSERT ... ON CONFLICT DO NOTHING of every XOR message
@@ -177,30 +210,59 @@ class Server {
   }
   // addMessages for a batch of requests: [{owner, messages: [{timestamp}]}] -> per message inserted flags
   addMessages(requests) {
+    const [ts, own] = this._ingestArgs(requests);
+    const r = addon.serverIngest(this.engine.ctx, this.store, ts, STRIDE, own, this.nextId);
+    return this._ingested(r, own.length);
+  }
+  // -> Promise<Either<UnknownError, flags|null>>; the id range is reserved before the await
+  async addMessagesAsync(requests) {
+    const [ts, own] = this._ingestArgs(requests);
+    const base = this.nextId;
+    this.nextId += own.length;
+    const e = await addon.serverIngestAsync(this.engine.ctx, this.store, ts, STRIDE, own, base);
+    if (e._tag === "Left") return e;
+    return { _tag: "Right", right: e.right.status !== EVM_OK ? null : Array.from(e.right.flags, (f) => (f & MSG_INS) !== 0) };
+  }
+  _ingestArgs(requests) {
     const ts = [];
     const own = [];
     requests.forEach((r) => r.messages.forEach((m) => { ts.push(m.timestamp); own.push(r.owner); }));
-    const r = addon.serverIngest(this.engine.ctx, this.store, encodeTimestamps(ts), STRIDE, Uint32Array.from(own),
-      this.nextId);
+    return [encodeTimestamps(ts), Uint32Array.from(own)];
+  }
+  _ingested(r, n) {
     if (r.status !== EVM_OK) return null;
-    this.nextId += ts.length;
+    this.nextId += n;
     return Array.from(r.flags, (f) => (f & MSG_INS) !== 0);
   }
   merkleTree(owner) {
     return addon.treeToJson(this.engine.ctx, addon.storeTree(this.store), owner);
   }
-  // getMessages for every owner: clientTrees[o] JSON, nodeIds[o] -> { diff[o], ids[o][] }
+  // getMessages for every owner: clientTrees[o] JSON, nodeIds[o] -> { diff[o], ids[o][], errors[o] }
   getMessages(clientTreesJson, nodeIds) {
+    const [c, node] = this._selectArgs(clientTreesJson, nodeIds);
+    try {
+      return this._selected(addon.serverSelect(this.engine.ctx, this.store, c, node));
+    } finally {
+      addon.treeFree(this.engine.ctx, c);
+    }
+  }
+  // -> Promise<Either<UnknownError, { diff, ids, errors }>>
+  async getMessagesAsync(clientTreesJson, nodeIds) {
+    const [c, node] = this._selectArgs(clientTreesJson, nodeIds);
+    const e = await addon.serverSelectAsync(this.engine.ctx, this.store, c, node);
+    addon.treeFree(this.engine.ctx, c);
+    return e._tag === "Left" ? e : { _tag: "Right", right: this._selected(e.right) };
+  }
+  _selectArgs(clientTreesJson, nodeIds) {
     if (clientTreesJson.length !== this.nOwners || nodeIds.length !== this.nOwners)
       throw new RangeError("one client tree and one nodeId per owner slot");
     nodeIds.forEach((n) => {
       // a NodeId is 16 hex chars (types.ts:42); any other string would shift every later owner's slice
       if (typeof n !== "string" || !/^[0-9a-f]{16}$/i.test(n)) throw new RangeError("nodeId must be 16 hex chars");
     });
-    const c = addon.treeFromJson(this.engine.ctx, clientTreesJson);
-    const node = encodeTimestamps([]).constructor.from(Buffer.from(nodeIds.join(""), "latin1"));
-    const r = addon.serverSelect(this.engine.ctx, this.store, c, node);
-    addon.treeFree(this.engine.ctx, c);
+    return [addon.treeFromJson(this.engine.ctx, clientTreesJson), Uint8Array.from(Buffer.from(nodeIds.join(""), "latin1"))];
+  }
+  _selected(r) {
     const ids = [];
     for (let o = 0; o < this.nOwners; o++) ids.push(Array.from(r.ids.subarray(r.off[o], r.off[o + 1])));
     // diffMerkleTrees throws RangeError at a 17-digit key (merkleTree.ts:55-61), which fails that

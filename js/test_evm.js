@@ -19,17 +19,23 @@ out.diff = cases.diff.map((c) => {
 });
 
 // applyMessages with an in-memory Database stand-in
-out.apply = cases.apply.map((c) => {
+function fakeDb(c) {
   const max = new Map(Object.entries(c.cellMax));
   const upserts = {};
   const inserts = [];
   const db = {
     cellMax: (t, r, col) => max.get(JSON.stringify([t, r, col])) || null,
+    // SELECT "timestamp", "table", "row", "column" FROM "__message" WHERE "timestamp" IN (...)
+    storedRows: (tss) => { const s = new Set(tss); return c.stored.filter((r) => s.has(r.timestamp)); },
     upsert: (t, r, col, v) => { upserts[JSON.stringify([t, r, col])] = v; },
     insertMessage: (m) => inserts.push(m.timestamp),
   };
-  const tree = eng.applyMessages(db, c.tree, c.messages);
-  return { tree, upserts, inserts };
+  return { db, upserts, inserts };
+}
+out.apply = cases.apply.map((c) => {
+  const f = fakeDb(c);
+  const tree = eng.applyMessages(f.db, c.tree, c.messages);
+  return { tree, upserts: f.upserts, inserts: f.inserts };
 });
 
 // server addMessages / getMessages
@@ -42,5 +48,31 @@ out.server.since = srv.messagesSince(cases.server.since);
 // receive.ts:45-66 clock fold
 out.receive = cases.receive.map((c) => eng.receiveMessages(c.clock, c.timestamps, c.now));
 srv.close();
-eng.close();
-process.stdout.write(JSON.stringify(out));
+
+// the async entry points: Promise<Either<UnknownError, ...>>, all in flight at once
+async function asyncPart() {
+  const fs_ = cases.apply.map((c) => fakeDb(c));
+  const es = await Promise.all(cases.apply.map((c, i) => eng.applyMessagesAsync(fs_[i].db, c.tree, c.messages)));
+  out.applyAsync = es.map((e, i) => (e._tag === "Right" ? { tree: e.right, upserts: fs_[i].upserts, inserts: fs_[i].inserts } : e));
+  const s2 = new Server(eng, cases.server.nOwners);
+  out.server.insAsync = [];
+  for (const b of cases.server.batches) {
+    const e = await s2.addMessagesAsync(b);
+    out.server.insAsync.push(e._tag === "Right" ? e.right : e);
+  }
+  out.server.treesAsync = [];
+  for (let o = 0; o < cases.server.nOwners; o++) out.server.treesAsync.push(s2.merkleTree(o));
+  const g = await s2.getMessagesAsync(cases.server.clientTrees, cases.server.nodeIds);
+  out.server.getAsync = g._tag === "Right" ? g.right : g;
+  // an owner id beyond the store's owner count: the engine refuses the batch -> Left
+  const addon = require("./evm_napi.node");
+  out.leftOnError = await addon.serverIngestAsync(eng.ctx, s2.store, new Uint8Array(48), 48, new Uint32Array([99]), 0);
+  s2.close();
+}
+asyncPart().then(() => {
+  eng.close();
+  process.stdout.write(JSON.stringify(out));
+}, (e) => {
+  process.stderr.write(String(e && e.stack) + "\n");
+  process.exit(1);
+});

@@ -39,14 +39,23 @@ def test_js_entry_points(tmp_path):
                       {"a": "{}", "b": O.merkle_tree_to_string(O.insert_into_merkle_tree({}, O.parse_canonical(ts2)))}]}
     # applyMessages cases with prior rows
     apply_cases, expects = [], []
-    for seed in range(3):
+    for seed in range(4):
         msgs, cells = W.client_batch(500 + seed, n=200, n_cells=6)
         prior, _ = W.client_batch(600 + seed, n=30, n_cells=6, t0=W.T0 - 600_000)
         prior = [dict(m, table=cells[i % 6][0], row=cells[i % 6][1], column=cells[i % 6][2])
                  for i, m in enumerate(prior)]
+        rng = random.Random(seed)
+        # redeliveries of stored rows (their own cells), and in case 3 one stored
+        # timestamp under another cell: the reference ignores that INSERT -> null
+        for m in rng.sample(prior, 8):
+            msgs.insert(rng.randrange(len(msgs) + 1), dict(m))
+        if seed == 3:
+            msgs.insert(50, dict(prior[4], column="otherColumn"))
         db = O.ClientDb()
         t0 = O.apply_messages(db, {}, prior)
         cell_max = {json.dumps([c[0], c[1], c[2]], separators=(",", ":")): db.cell_max(*c) for c in cells}
+        stored = [{"timestamp": r[0], "table": r[1], "row": r[2], "column": r[3]} for r in db.conn.execute(
+            'SELECT "timestamp", "table", "row", "column" FROM "__message"').fetchall()]
         dec = []
         t1 = O.apply_messages(db, t0, msgs, dec)
         ups = {}
@@ -54,9 +63,10 @@ def test_js_entry_points(tmp_path):
             if u:
                 ups[json.dumps([m["table"], m["row"], m["column"]], separators=(",", ":"))] = m["value"]
         ins = [m["timestamp"] for m, (u, x, _) in zip(msgs, dec) if x]
-        apply_cases.append({"tree": O.merkle_tree_to_string(t0), "messages": msgs,
+        apply_cases.append({"tree": O.merkle_tree_to_string(t0), "messages": msgs, "stored": stored,
                             "cellMax": {k: v for k, v in cell_max.items() if v is not None}})
-        expects.append({"tree": O.merkle_tree_to_string(t1), "upserts": ups, "inserts": ins})
+        expects.append({"tree": O.merkle_tree_to_string(t1), "upserts": ups, "inserts": ins} if seed < 3 else
+                       {"tree": None, "upserts": {}, "inserts": []})
     cases["apply"] = apply_cases
     # server
     rng = random.Random(2)
@@ -111,15 +121,23 @@ def test_js_entry_points(tmp_path):
     assert [json.loads(t) for t in res["insert"]] == [snap["insertIntoMerkleTree 1"], snap["insertIntoMerkleTree 2"],
                                                      snap["insertIntoMerkleTree 3"]]
     assert res["diff"] == [None, 1656873720000]
-    for got, want in zip(res["apply"], expects):
+    assert len(res["apply"]) == len(expects) == len(res["applyAsync"])
+    for got, got_async, want in zip(res["apply"], res["applyAsync"], expects):
         assert got == want
+        assert got_async == want  # Promise<Either>: Right, the same writes
     assert res["server"]["ins"] == want_ins
     for o in range(n_owners):
         assert res["server"]["trees"][o] == O.merkle_tree_to_string(sdb.get_merkle_tree("u%d" % o))
-    for o in range(n_owners):
-        d, rows = sdb.get_messages(sdb.get_merkle_tree("u%d" % o), json.loads(client[o]), "u%d" % o, node_ids[o])
-        assert res["server"]["get"]["diff"][o] == d
-        assert len(res["server"]["get"]["ids"][o]) == len(rows)
+    for key in ("get", "getAsync"):
+        for o in range(n_owners):
+            d, rows = sdb.get_messages(sdb.get_merkle_tree("u%d" % o), json.loads(client[o]), "u%d" % o, node_ids[o])
+            assert res["server"][key]["diff"][o] == d
+            assert len(res["server"][key]["ids"][o]) == len(rows)
+    assert res["server"]["insAsync"] == want_ins
+    assert res["server"]["treesAsync"] == res["server"]["trees"]
+    assert res["server"]["getAsync"]["ids"] == res["server"]["get"]["ids"]
+    # a device error reaches the caller as Left(UnknownError), not as a throw
+    assert res["leftOnError"]["_tag"] == "Left" and res["leftOnError"]["left"]["type"] == "UnknownError"
     id_ts = [m["timestamp"] for b in batches for r in b for m in r["messages"]]
     for o in range(n_owners):
         rows = [] if since[o] is None else sdb.conn.execute(
