@@ -42,6 +42,7 @@ def test_js_entry_points(tmp_path):
     for seed in range(4):
         msgs, cells = W.client_batch(500 + seed, n=200, n_cells=6)
         prior, _ = W.client_batch(600 + seed, n=30, n_cells=6, t0=W.T0 - 600_000)
+        prior = list({m["timestamp"]: m for m in prior}.values())  # one cell per stored timestamp
         prior = [dict(m, table=cells[i % 6][0], row=cells[i % 6][1], column=cells[i % 6][2])
                  for i, m in enumerate(prior)]
         rng = random.Random(seed)
