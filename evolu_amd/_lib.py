@@ -20,6 +20,8 @@ EVM_ETREE = 5
 EVM_EDEVICE = 6
 EVM_ENOMEM = 7
 EVM_ECAPACITY = 8
+EVM_EDIST = 9
+DIST_ID_BYTES = 128
 
 META_CASEMASK = 0x0000FFFF
 META_VALID = 0x00010000
@@ -98,6 +100,13 @@ SIGNATURES = {
     "evm_store_since": (_i, [_vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_server_select": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_store_select_after": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "evm_dist_unique_id": (_i, [_vp]),
+    "evm_dist_init": (_i, [_vp, _vp, _i, _i, C.POINTER(_vp)]),
+    "evm_dist_free": (None, [_vp, _vp]),
+    "evm_dist_info": (_i, [_vp, C.POINTER(_i), C.POINTER(_i)]),
+    "evm_dist_route": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, C.POINTER(C.c_uint64)]),
+    "evm_dist_take": (_i, [_vp, _vp, _u32, _vp, _sz, _vp, _vp, _vp, C.c_uint64, _vp]),
+    "evm_dist_gather_roots": (_i, [_vp, _vp, _vp, _u32, _vp, _vp]),
     "evm_apply_batch": (
         _i,
         [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _vp, C.POINTER(_vp)],

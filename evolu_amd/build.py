@@ -12,7 +12,7 @@ LIB = os.path.join(HERE, "libevm.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("EVM_ARCH", "gfx950")
 
-SOURCES = ["evm_engine.hip", "evm_client.hip", "evm_server.hip", "evm_clock.hip", "evm_json.cpp", "evm_proto.cpp"]
+SOURCES = ["evm_engine.hip", "evm_client.hip", "evm_server.hip", "evm_clock.hip", "evm_dist.hip", "evm_json.cpp", "evm_proto.cpp"]
 HEADERS = ["evm_device.hpp", "evm_pack.hpp", "evm_prims.hpp", "evm_internal.hpp"]
 
 
@@ -26,7 +26,7 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest(deps):
         return LIB
     cmd = [HIPCC, "-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function", "-I" + INCLUDE] + srcs + ["-o", LIB + ".tmp"]
+           "-Wno-unused-function", "-I" + INCLUDE] + srcs + ["-ldl", "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -709,6 +709,7 @@ const char* evm_strerror(int s) {
     case EVM_EDEVICE: return "HIP error";
     case EVM_ENOMEM: return "device out of memory";
     case EVM_ECAPACITY: return "output buffer too small";
+    case EVM_EDIST: return "RCCL unavailable or a collective failed";
   }
   return "unknown status";
 }

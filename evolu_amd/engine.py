@@ -456,3 +456,77 @@ def key_code(key: str) -> int:
     for i, ch in enumerate(key):
         code |= (int(ch) + 1) << (2 * (19 - i))
     return code
+
+
+def dist_unique_id() -> bytes:
+    """A new RCCL communicator id (evm_dist_unique_id); rank 0 makes it."""
+    lib = _lib.load()
+    buf = (C.c_uint8 * _lib.DIST_ID_BYTES)()
+    check(lib.evm_dist_unique_id(buf), "evm_dist_unique_id")
+    return bytes(buf)
+
+
+class Dist:
+    """Owner sharding over RCCL (evm_dist_*): one per Engine, collective calls
+    in the same order on every rank."""
+
+    def __init__(self, eng: Engine, uid: bytes, rank: int, world: int):
+        if len(uid) != _lib.DIST_ID_BYTES:
+            raise ValueError("unique id must be %d bytes" % _lib.DIST_ID_BYTES)
+        self.eng = eng
+        self.rank, self.world = rank, world
+        h = C.c_void_p()
+        buf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+        check(eng.lib.evm_dist_init(eng.h, buf, rank, world, C.byref(h)), "evm_dist_init")
+        self.h = h
+        self.n_recv = 0
+        self.stride = TS_STRIDE
+
+    def free(self):
+        if getattr(self, "h", None):
+            self.eng.lib.evm_dist_free(self.eng.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def route(self, ts: torch.Tensor, owner: torch.Tensor, aux: Optional[torch.Tensor] = None,
+              dest: Optional[torch.Tensor] = None) -> int:
+        """Collective: rows to rank dest (default owner % world) -> rows received."""
+        n, stride = ts.shape
+        nr = C.c_uint64()
+        check(self.eng.lib.evm_dist_route(self.eng.h, self.h, _ptr(ts), stride, n, _ptr(owner), _ptr(aux), _ptr(dest),
+                                          C.byref(nr)), "evm_dist_route")
+        self.n_recv = nr.value
+        self.stride = stride
+        return self.n_recv
+
+    def take(self, group: int = 0, aux: bool = True, src: bool = True, out=None):
+        """The last route's rows -> (ts, owner, aux or None, src or None, group_off or None);
+        out: optional preallocated (ts, owner, aux, src) tensors with >= n_recv rows."""
+        n = self.n_recv
+        dev = torch.device("cuda", self.eng.device)
+        if out is None:
+            out = (torch.empty((max(n, 1), self.stride), dtype=torch.uint8, device=dev),
+                   torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                   torch.empty(max(n, 1), dtype=torch.int32, device=dev) if aux else None,
+                   torch.empty(max(n, 1), dtype=torch.int64, device=dev) if src else None)
+        ts, ow, ax, sr = out
+        cap = ts.shape[0]
+        goff = (C.c_uint64 * (group + 1))() if group else None
+        check(self.eng.lib.evm_dist_take(self.eng.h, self.h, group, _ptr(ts), ts.shape[1], _ptr(ow), _ptr(ax), _ptr(sr),
+                                         cap, goff), "evm_dist_take")
+        g = [int(x) for x in goff] if group else None
+        return ts[:n], ow[:n], (ax[:n] if ax is not None else None), (sr[:n] if sr is not None else None), g
+
+    def gather_roots(self, trees: "Trees", n_owners_global: int):
+        """Collective: every global owner's (root int32, present bool) on the device."""
+        dev = torch.device("cuda", self.eng.device)
+        root = torch.empty(max(n_owners_global, 1), dtype=torch.int32, device=dev)
+        present = torch.empty(max(n_owners_global, 1), dtype=torch.uint8, device=dev)
+        check(self.eng.lib.evm_dist_gather_roots(self.eng.h, self.h, trees.h, n_owners_global, _ptr(root),
+                                                 _ptr(present)), "evm_dist_gather_roots")
+        return root[:n_owners_global], present[:n_owners_global].bool()

@@ -48,7 +48,8 @@ enum evm_status {
   EVM_ETREE = 5,      /* tree JSON is not a tree insertIntoMerkleTree can produce */
   EVM_EDEVICE = 6,    /* HIP error */
   EVM_ENOMEM = 7,     /* device allocation failed */
-  EVM_ECAPACITY = 8   /* output buffer too small */
+  EVM_ECAPACITY = 8,  /* output buffer too small */
+  EVM_EDIST = 9       /* RCCL missing or a collective failed (evm_dist_*) */
 };
 
 /* ---- packed timestamp record (32 bytes, device) -------------------------
@@ -347,6 +348,47 @@ int evm_pb_encode(int kind, const char* ts, size_t stride, const uint32_t* ts_le
                   const uint64_t* content_off, const uint8_t* content, const char* user, size_t user_len,
                   const char* node, size_t node_len, const char* tree, size_t tree_len, uint8_t* out, size_t cap,
                   size_t* out_len);
+
+/* ------------------------------------------------------------------------
+ * Multi-GPU owner sharding (evm_dist.hip).  One process per
+ * GPU and one evm_dist per context; every call below is collective (all
+ * ranks call it, in the same order) except evm_dist_take.  Owners are
+ * independent in the whole path, so rank r serves the owners with
+ * owner % world == r (dense owner ids the caller assigns, e.g. from
+ * murmur3(ownerId)); as local owner owner / world.  Replaces nothing in the
+ * reference (one process there); it is what lets the N-API caller run one
+ * addon per GPU of a node.  RCCL (librccl.so.1) is opened at run time.
+ * ------------------------------------------------------------------------ */
+#define EVM_DIST_ID_BYTES 128
+typedef struct evm_dist evm_dist;
+/* a new communicator id (rank 0 makes it and hands it to the others) */
+int evm_dist_unique_id(uint8_t* id);
+/* collective: the communicator of `world` ranks (world <= 64) on ctx's device */
+int evm_dist_init(evm_ctx* ctx, const uint8_t* id, int rank, int world, evm_dist** out);
+void evm_dist_free(evm_ctx* ctx, evm_dist* d);
+int evm_dist_info(const evm_dist* d, int* rank, int* world);
+/* collective: every row (device ts[n * stride], stride % 8 == 0; owner[n]
+ * global owner ids; optional aux[n], e.g. the cell) goes to rank
+ * dest ? dest[i] : owner[i] % world.  The received rows stay in the
+ * context's staging buffer in (source rank, source order) -- the global
+ * batch order when each rank's input is its slice of the batch in rank
+ * order; *n_recv = their count (host).  A dest >= world: that row is
+ * dropped and EVM_EINVAL returned after the exchange completed. */
+int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                   const uint32_t* aux, const uint8_t* dest, uint64_t* n_recv);
+/* local: the last route's rows into caller buffers (device): out_ts rows of
+ * out_stride bytes, out_owner (global ids), optional out_aux and out_src
+ * (source rank << 32 | index in that rank's input).  group == 0: in receive
+ * order; 0 < group <= 64: grouped by local owner (owner / world < group),
+ * receive order inside each group, group_off (host, group + 1) the bounds.
+ * cap < n_recv: EVM_ECAPACITY (the rows stay staged; take again). */
+int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_t out_stride, uint32_t* out_owner,
+                  uint32_t* out_aux, uint64_t* out_src, uint64_t cap, uint64_t* group_off);
+/* collective: every owner's root over all ranks.  t: this rank's trees, local
+ * owner j = global owner j * world + rank (t->n_owners <= ceil(n_global /
+ * world)).  root/present: device [n_owners_global]. */
+int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* t, uint32_t n_owners_global, int32_t* root,
+                          uint8_t* present);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,104 @@
+"""The evm_dist_* C ABI (RCCL) on one GPU (world 1: every row routes to this
+rank through RCCL's self send/recv): the exchange keeps batch order, the
+take groups by local owner stably, the roots gather matches the trees.
+Multi-rank routing order is covered by the gloo tests of the same algorithm
+(tests/test_dist.py); 8-GPU runs are the driver's."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from evolu_amd.engine import Engine
+
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def dist(eng):
+    from evolu_amd.engine import Dist, dist_unique_id
+
+    d = Dist(eng, dist_unique_id(), 0, 1)
+    yield d
+    d.free()
+
+
+def _rows(n, n_owners, seed):
+    from evolu_amd import synth
+
+    ts, _ = synth.config2(n, 1000, seed_config=seed)
+    rng = np.random.default_rng(seed)
+    owner = rng.integers(0, n_owners, n).astype(np.uint32)
+    aux = rng.integers(0, 1 << 31, n).astype(np.uint32)
+    return ts, owner, aux
+
+
+@pytest.mark.parametrize("n", [0, 1, 4095, 4096, 4097, 300_000])
+def test_route_take_keeps_order(eng, dist, n):
+    ts, owner, aux = _rows(max(n, 1000), 37, n + 1)
+    ts, owner, aux = ts[:n], owner[:n], aux[:n]
+    got = dist.route(eng.dev(ts), eng.dev(owner), eng.dev(aux))
+    assert got == n
+    t2, o2, a2, src, g = dist.take()
+    assert g is None
+    assert np.array_equal(t2.cpu().numpy(), ts)
+    assert np.array_equal(o2.cpu().numpy().view(np.uint32), owner)
+    assert np.array_equal(a2.cpu().numpy().view(np.uint32), aux)
+    assert np.array_equal(src.cpu().numpy(), np.arange(n, dtype=np.int64))  # source rank 0, index i
+
+
+@pytest.mark.parametrize("group", [1, 5, 8, 64])
+def test_take_grouped_by_local_owner(eng, dist, group):
+    n = 250_000
+    ts, owner, aux = _rows(n, group, 7 + group)
+    assert dist.route(eng.dev(ts), eng.dev(owner), eng.dev(aux)) == n
+    t2, o2, a2, src, goff = dist.take(group=group)
+    order = np.argsort(owner, kind="stable")
+    assert np.array_equal(src.cpu().numpy(), order)
+    assert np.array_equal(t2.cpu().numpy(), ts[order])
+    assert np.array_equal(a2.cpu().numpy().view(np.uint32), aux[order])
+    want = np.concatenate([[0], np.cumsum(np.bincount(owner, minlength=group))])
+    assert goff == list(want)
+    # the staged rows can be taken again (ungrouped this time)
+    t3, _, _, s3, _ = dist.take()
+    assert np.array_equal(s3.cpu().numpy(), np.arange(n))
+
+
+def test_bad_dest_and_group_overflow(eng, dist):
+    from evolu_amd import _lib as L
+
+    n = 10_000
+    ts, owner, aux = _rows(n, 4, 3)
+    dest = np.zeros(n, dtype=np.uint8)
+    dest[77] = 1  # no rank 1 in a world of 1
+    with pytest.raises(L.EngineError) as e:
+        dist.route(eng.dev(ts), eng.dev(owner), None, dest=eng.dev(dest))
+    assert e.value.status == L.EVM_EINVAL
+    # the exchange completed without the bad row; the next route is clean
+    assert dist.route(eng.dev(ts), eng.dev(owner), dest=eng.dev(np.zeros(n, dtype=np.uint8))) == n
+    with pytest.raises(L.EngineError) as e:
+        dist.take(group=3)  # owners 0..3 do not fit 3 groups
+    assert e.value.status == L.EVM_EINVAL
+    small = (torch.empty((10, 48), dtype=torch.uint8, device="cuda"), torch.empty(10, dtype=torch.int32, device="cuda"),
+             None, None)
+    with pytest.raises(L.EngineError) as e:
+        dist.take(out=small)
+    assert e.value.status == L.EVM_ECAPACITY
+
+
+def test_gather_roots_matches_trees(eng, dist):
+    from evolu_amd import synth
+
+    n_owners = 1000
+    ts, owner = synth.config3(n_owners, 20, seed_config=5)[:2]
+    owner = owner.astype(np.uint32)
+    owner[owner == 17] = 18  # an owner without messages: present = 0
+    trees = eng.merkle_insert(eng.tree_new(n_owners), eng.dev(ts), eng.dev(owner))
+    root, present = dist.gather_roots(trees, n_owners)
+    r, p = trees.roots()
+    assert np.array_equal(root.cpu().numpy(), r) and np.array_equal(present.cpu().numpy(), p)

@@ -50,3 +50,11 @@ def test_minute_arithmetic_matches_js_on_native_range():
     for _ in range(20000):
         m = r.randrange(0, 2**31 * 60000)
         assert O.to_int32(m / 1000 / 60) == m // 60000
+
+
+def test_dist_unique_id_without_gpu():
+    """evm_dist_unique_id needs RCCL's bootstrap only (no device)."""
+    from evolu_amd.engine import dist_unique_id
+
+    a, b = dist_unique_id(), dist_unique_id()
+    assert len(a) == 128 and a != b
