@@ -85,6 +85,11 @@ def parse():
                     help="client: config 2 applyMessages (headline, + config 1 and 3 legs at N=1); "
                          "server: config 3/4/5 ingest + diff + select alone")
     ap.add_argument("--extra", type=int, default=1, help="N=1 client run: add the config-1 and config-3 legs")
+    ap.add_argument("--shape", choices=["auto", "config2", "config4c"], default="auto",
+                    help="client workload: config2 = one owner per GPU, no exchange; config4c = owners_per_rank "
+                         "owners per GPU, every rank's batch holds messages of all the job's owners and routes them "
+                         "to the owner's rank over RCCL (evm_dist_route); auto = config2 at N=1, config4c at N>1")
+    ap.add_argument("--owners-per-rank", type=int, default=8, help="config4c: owners per GPU")
     ap.add_argument("--owners", type=int, default=100_000, help="server workload: owners per GPU")
     ap.add_argument("--per-owner", type=int, default=1000, help="server workload: messages per owner")
     ap.add_argument("--zipf", type=float, default=0.0,
@@ -274,6 +279,14 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    shape = a.shape if a.shape != "auto" else ("config2" if world == 1 else "config4c")
+    if shape == "config4c":
+        out = client_routed(a, rank, world, local)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     # each rank: its own owner (seed per rank), same shape
     ts_np, cell_np = synth.config2(a.messages, a.cells, seed_config=2 + 1000 * rank)
     eng = Engine(local)
@@ -420,6 +433,156 @@ def main():
         dist.destroy_process_group()
 
 
+XGMI_LINK = 153e9  # B/s per xGMI link (one link per peer in an 8-GPU node)
+ROUTE_BYTES = 64  # wire record per routed message (evm_dist.hip: 48-B timestamp row + owner, cell, index)
+DIST_ALG = {
+    "(k_dist_count<MODE>)": 4,  # owner in (send side: caller's owner ids; take side: the records' owner field)
+    "(k_dist_scatter<SEND>)": 48 + 4 + 4 + 64,  # ts row + owner + cell in, record out
+    "(k_dist_scatter<RECV>)": 64 + 48 + 4 + 4,  # record in; ts row + owner + cell out
+}
+
+
+def make_dist(eng, rank, world):
+    """The RCCL communicator of evm_dist_*: rank 0's id broadcast over torch.distributed."""
+    import torch
+    import torch.distributed as dist
+
+    from evolu_amd.engine import Dist, dist_unique_id
+
+    uid = torch.zeros(128, dtype=torch.uint8, device=torch.device("cuda", eng.device))
+    if rank == 0:
+        uid.copy_(torch.frombuffer(bytearray(dist_unique_id()), dtype=torch.uint8))
+    if world > 1:
+        dist.broadcast(uid, 0)
+    return Dist(eng, bytes(uid.cpu().numpy()), rank, world)
+
+
+def client_routed(a, rank, world, local):
+    """Config 4, client side (SURVEY 8(d) "4-C"): owners_per_rank owners per
+    GPU, each with config-2 cell contention (a.cells cells, 64 HLC nodes per
+    source rank).  Every rank's batch slice holds messages of ALL the job's
+    owners in random order; one step = evm_dist_route (RCCL all-to-all by
+    owner % world) + evm_dist_take grouped by local owner + one
+    applyMessages batch per owner (enqueued together) + the owners' roots
+    all-gathered (evm_dist_gather_roots).  Weak scaling: a.messages per GPU."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from evolu_amd import synth
+    from evolu_amd.engine import Engine
+
+    K = a.owners_per_rank
+    G = K * world
+    M = a.messages
+    rng = np.random.default_rng(4000 + rank)
+    owner_np = rng.integers(0, G, M).astype(np.uint32)
+    cnt = np.bincount(owner_np, minlength=G)
+    ts_np = np.empty((M, 48), dtype=np.uint8)
+    cell_np = np.empty(M, dtype=np.uint32)
+    for g in range(G):
+        if cnt[g] == 0:
+            continue
+        t_g, c_g = synth.config2(int(max(cnt[g], 1000)), a.cells, seed_config=40_000 + 64 * g + rank)
+        at = np.nonzero(owner_np == g)[0]
+        ts_np[at] = t_g[: cnt[g]]
+        cell_np[at] = c_g[: cnt[g]]
+    eng = Engine(local)
+    eng.set_option(3, a.overlap)
+    dev = torch.device("cuda", local)
+    dd = make_dist(eng, rank, world)
+    ts, owner, cell = eng.dev(ts_np), eng.dev(owner_np), eng.dev(cell_np)
+    del ts_np
+    cap = int(M * 1.25) + 65536
+    bufs = (torch.empty((cap, 48), dtype=torch.uint8, device=dev), torch.empty(cap, dtype=torch.int32, device=dev),
+            torch.empty(cap, dtype=torch.int32, device=dev), None)
+    flags = torch.empty(cap, dtype=torch.uint8, device=dev)
+    winners = torch.empty((K, a.cells), dtype=torch.int32, device=dev)
+    empty = eng.tree_new(1)
+    route_ms = []
+
+    def step():
+        r0 = time.perf_counter()
+        n_r = dd.route(ts, owner, aux=cell)
+        t2, _, c2, _, goff = dd.take(group=K, src=False, out=bufs)
+        route_ms.append((time.perf_counter() - r0) * 1e3)
+        pend = [eng.apply_batch_async(empty, t2[goff[k]:goff[k + 1]], c2[goff[k]:goff[k + 1]], a.cells,
+                                      flags[goff[k]:goff[k + 1]], winners[k]) for k in range(K)]
+        trees = [p.wait()[2] for p in pend]
+        # the rank's K owners' roots -> every owner's root on every rank
+        root, present = dd.gather_roots(trees, G)
+        for t in trees:
+            t.free()
+        return n_r, root
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.prof_enable(True)
+    eng.prof_reset()
+    step()
+    torch.cuda.synchronize()
+    prof = eng.prof_report()
+    alg_all = dict(ALG_BYTES_PER_MSG, **DIST_ALG)
+    dom = dominant(prof, alg_all, SIDE_KERNELS if a.overlap else ())
+    eng.prof_only(dom)
+    eng.prof_reset()
+    route_ms.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_recv = 0
+    for _ in range(a.steps):
+        n_recv, _ = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    prof_dom = eng.prof_report()
+    eng.prof_enable(False)
+    eng.prof_only(None)
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    route = torch.tensor([sum(route_ms) / max(1, len(route_ms))], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(route, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    route_ms_avg = float(route.item())
+    ms = elapsed / a.steps * 1e3
+    tot_ms, launches = prof_dom[dom]
+    avg_s = tot_ms / launches / 1e3
+    rows = n_recv if "RECV" in dom or dom in ALG_BYTES_PER_MSG else M
+    alg = alg_all[dom] * rows / (K if dom in ALG_BYTES_PER_MSG else 1)  # client kernels run once per owner batch
+    remote = M * (world - 1) / world  # rows leaving this rank (uniform owners)
+    out = {
+        "metric": METRIC, "value": world * M * a.steps / elapsed, "unit": "msgs/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (seeded HLC streams, SURVEY 8(d) config 4, client side)",
+        "config": {"workload": "config4c: applyMessages, %d owners per GPU x %d cells each, %d msgs per GPU from all "
+                               "%d owners of the job, routed by owner %% world over RCCL (evm_dist_route), one batch "
+                               "per owner, roots all-gathered" % (K, a.cells, M, G),
+                   "messages_per_gpu": M, "owners_per_gpu": K, "cells_per_owner": a.cells,
+                   "parallelism": "owner-sharded, %d rank(s), RCCL all-to-all" % world},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(a.traffic, dom),
+                     "kernel_ms_avg": avg_s * 1e3, "alg_bytes_per_launch": alg,
+                     "kernel_share_of_step": tot_ms / (ms * a.steps)},
+        "route": {"ms_per_step": route_ms_avg, "bytes_per_msg": ROUTE_BYTES,
+                  "remote_bytes_per_gpu": remote * ROUTE_BYTES,
+                  "xgmi_frac": (remote * ROUTE_BYTES / (route_ms_avg / 1e3) / ((world - 1) * XGMI_LINK))
+                  if world > 1 else None,
+                  "xgmi_peak_GBps": (world - 1) * XGMI_LINK / 1e9 if world > 1 else None},
+        "pipeline": {"alg_bytes_per_msg": 120,
+                     "kernels_ms_per_step": {k: v[0] for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:14]}},
+        "cpu_baseline": None,
+    }
+    dd.free()
+    eng.close()
+    return out
+
+
 def config1_leg(eng, a):
     """BASELINE config 1: the todo-schema stream (100k messages, one owner),
     one applyMessages batch from an empty tree, inputs in HBM."""
@@ -498,13 +661,17 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
     hot = D.hot_owners(D.owner_counts(owner, O_total), world) if (world > 1 and zipf > 0) else None
     omap = D.OwnerMap(O_total, world, rank, hot)
     n_local_owners = omap.n_local
-    dest = omap.dest(owner, ts) if world > 1 else None
+    dest = omap.dest(owner, ts).to(torch.uint8).contiguous() if world > 1 else None
+    dd = make_dist(eng, rank, world) if world > 1 else None
+    owner32 = owner.to(torch.int32).contiguous()
 
     def route(rows):
+        """evm_dist_route + take: rows to their owner's rank (hot owners: by timestamp hash)."""
         if world == 1:
             return rows, owner
-        t_r, o_r, _, _ = D.route_by_owner(rows, owner, dest=dest)
-        return t_r, o_r
+        dd.route(rows, owner32, dest=dest)
+        t_r, o_r, _, _, _ = dd.take(aux=False, src=False)
+        return t_r, o_r.to(torch.int64)
 
     ts_r, own_r = route(ts)
     lown = omap.local(own_r).contiguous()
@@ -548,12 +715,16 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
         else:
             diff, (off, ids), (hoff, hids) = D.split_get_messages(eng, store, client, client_hot, node, omap)
             nsel = int(ids.numel()) + int(hids.numel())
-        r, p = store.tree().roots()
         if world > 1:
-            rt, pt = torch.from_numpy(r).to(dev), torch.from_numpy(p).to(dev)
-            D.gather_roots(rt[: omap.per], pt[: omap.per], O_total)
             if omap.hot.numel():
+                r, p = store.tree().roots()
+                rt, pt = torch.from_numpy(r).to(dev), torch.from_numpy(p).to(dev)
+                D.gather_roots(rt[: omap.per], pt[: omap.per], O_total)
                 D.gather_hot_roots(rt, pt, omap)
+            else:
+                dd.gather_roots(store.tree(), O_total)  # device to device (RCCL all-gather)
+        else:
+            store.tree().roots()
         n_leaves = store.tree().n_leaves
         store.free()
         return nsel, n_leaves
@@ -627,6 +798,8 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
     if leg:
         for k in ("metric", "n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
             out.pop(k)
+    if dd is not None:
+        dd.free()
     eng.close()
     del ts, owner, ts_r, lown, keep, client, flags
     torch.cuda.empty_cache()

@@ -5,4 +5,4 @@ include/evm.h; this package is its Python host side, mirroring the
 reference's function API (packages/evolu/src/{timestamp,merkleTree,
 applyMessages}.ts and apps/server/src/index.ts).
 """
-__all__ = ["engine", "api"]
+__all__ = ["engine", "dist", "server", "synth", "wire"]

@@ -106,7 +106,7 @@ SIGNATURES = {
     "evm_dist_info": (_i, [_vp, C.POINTER(_i), C.POINTER(_i)]),
     "evm_dist_route": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, C.POINTER(C.c_uint64)]),
     "evm_dist_take": (_i, [_vp, _vp, _u32, _vp, _sz, _vp, _vp, _vp, C.c_uint64, _vp]),
-    "evm_dist_gather_roots": (_i, [_vp, _vp, _vp, _u32, _vp, _vp]),
+    "evm_dist_gather_roots": (_i, [_vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     "evm_apply_batch": (
         _i,
         [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _vp, C.POINTER(_vp)],

@@ -1056,8 +1056,12 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
       hash[i] = p.hash;
       minute[i] = p.minute;
     }
-    mn = min(mn, p.minute);
-    mx = max(mx, p.minute != 0xffffffffu ? p.minute : 0u);
+    // (lanes past the range end parsed zero bytes: their minute must not
+    // widen the bounds, or the dense fold of a batch whose size is not a
+    // multiple of 64 overflows into the sort-based fold)
+    const bool in = i < end;
+    mn = min(mn, in ? p.minute : 0xffffffffu);
+    mx = max(mx, in && p.minute != 0xffffffffu ? p.minute : 0u);
   }
   if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
   __syncthreads();

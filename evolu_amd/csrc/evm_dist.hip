@@ -147,7 +147,16 @@ __device__ __forceinline__ u64 match_bucket(u32 b, bool active, int bits) {
 }
 
 __device__ __forceinline__ void copy_row(char* __restrict__ dst, const char* __restrict__ src, size_t bytes) {
-  // stride % 8 == 0 (checked on the host)
+  // stride % 8 == 0 (checked on the host); 16-B accesses when both ends allow
+  if (bytes == 48 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    const uint4 a = s[0], b = s[1], c = s[2];
+    d[0] = a;
+    d[1] = b;
+    d[2] = c;
+    return;
+  }
   const u64* s = reinterpret_cast<const u64*>(src);
   u64* d = reinterpret_cast<u64*>(dst);
   for (size_t k = 0; k < bytes / 8; ++k) d[k] = s[k];
@@ -476,18 +485,32 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
   return EVM_OK;
 }
 
-int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* t, uint32_t n_owners_global, int32_t* root,
-                          uint8_t* present) {
-  if (!ctx || !d || !t || (n_owners_global && (!root || !present))) return EVM_EINVAL;
+int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* const* trees, uint32_t n_trees,
+                          uint32_t n_owners_global, int32_t* root, uint8_t* present) {
+  if (!ctx || !d || (n_trees && !trees) || (n_owners_global && (!root || !present))) return EVM_EINVAL;
   const u32 G = (u32)d->world;
   const u32 per = (n_owners_global + G - 1) / G;
-  if (t->n_owners > per) return EVM_EINVAL;
+  size_t local = 0;
+  for (u32 k = 0; k < n_trees; ++k) {
+    if (!trees[k]) return EVM_EINVAL;
+    local += trees[k]->n_owners;
+  }
+  if (local > per) return EVM_EINVAL;
   if (!n_owners_global) return EVM_OK;
   Scratch S(ctx);
   u64* mine = S.alloc<u64>(per);
   u64* all = S.alloc<u64>((size_t)per * G);
   if (!mine || !all) return EVM_ENOMEM;
-  KLAUNCH(k_dist_root_pack, dim3(grid_for(per, 256)), dim3(256), t->off, t->pfx, t->n_owners, per, mine);
+  // this rank's local owners: the trees' owners in order, then zeros up to `per`
+  u32 at = 0;
+  for (u32 k = 0; k < n_trees; ++k) {
+    const evm_tree* t = trees[k];
+    const u32 cnt = k + 1 < n_trees ? t->n_owners : per - at;  // the last launch also zero-fills the tail
+    if (cnt)
+      KLAUNCH(k_dist_root_pack, dim3(grid_for(cnt, 256)), dim3(256), t->off, t->pfx, t->n_owners, cnt, mine + at);
+    at += t->n_owners;
+  }
+  if (!n_trees) HIPR(hipMemsetAsync(mine, 0, sizeof(u64) * per, ctx->stream));
   NCCLR(d->r->all_gather(mine, all, per, ncclUint64, d->comm, ctx->stream));
   KLAUNCH(k_dist_root_unpack, dim3(grid_for(n_owners_global, 256)), dim3(256), all, G, per, n_owners_global, root,
           present);

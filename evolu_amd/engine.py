@@ -522,11 +522,14 @@ class Dist:
         g = [int(x) for x in goff] if group else None
         return ts[:n], ow[:n], (ax[:n] if ax is not None else None), (sr[:n] if sr is not None else None), g
 
-    def gather_roots(self, trees: "Trees", n_owners_global: int):
-        """Collective: every global owner's (root int32, present bool) on the device."""
+    def gather_roots(self, trees, n_owners_global: int):
+        """Collective: every global owner's (root int32, present bool) on the device.
+        trees: one Trees (its owners = this rank's local owners) or a list of them."""
         dev = torch.device("cuda", self.eng.device)
+        ts = list(trees) if isinstance(trees, (list, tuple)) else [trees]
+        arr = (C.c_void_p * max(len(ts), 1))(*[t.h.value if isinstance(t.h, C.c_void_p) else t.h for t in ts])
         root = torch.empty(max(n_owners_global, 1), dtype=torch.int32, device=dev)
         present = torch.empty(max(n_owners_global, 1), dtype=torch.uint8, device=dev)
-        check(self.eng.lib.evm_dist_gather_roots(self.eng.h, self.h, trees.h, n_owners_global, _ptr(root),
+        check(self.eng.lib.evm_dist_gather_roots(self.eng.h, self.h, arr, len(ts), n_owners_global, _ptr(root),
                                                  _ptr(present)), "evm_dist_gather_roots")
         return root[:n_owners_global], present[:n_owners_global].bool()

@@ -384,11 +384,13 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
  * cap < n_recv: EVM_ECAPACITY (the rows stay staged; take again). */
 int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_t out_stride, uint32_t* out_owner,
                   uint32_t* out_aux, uint64_t* out_src, uint64_t cap, uint64_t* group_off);
-/* collective: every owner's root over all ranks.  t: this rank's trees, local
- * owner j = global owner j * world + rank (t->n_owners <= ceil(n_global /
- * world)).  root/present: device [n_owners_global]. */
-int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* t, uint32_t n_owners_global, int32_t* root,
-                          uint8_t* present);
+/* collective: every owner's root over all ranks.  This rank's local owners
+ * are the owners of trees[0..n_trees) in order (one tree set for all of
+ * them, or one single-owner tree per owner); local owner j = global owner
+ * j * world + rank, at most ceil(n_global / world) of them.  root/present:
+ * device [n_owners_global]. */
+int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* const* trees, uint32_t n_trees,
+                          uint32_t n_owners_global, int32_t* root, uint8_t* present);
 
 #ifdef __cplusplus
 }

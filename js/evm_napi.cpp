@@ -772,6 +772,112 @@ napi_value PbEncode(napi_env env, napi_callback_info info) {
   return arr;
 }
 
+// ---------------------------------------------------------------- multi-GPU (evm_dist_*)
+// One addon instance per GPU process; rank 0 makes the id and hands it to the others.
+// distUniqueId() -> Uint8Array(128)
+napi_value DistUniqueId(napi_env env, napi_callback_info) {
+  void* p;
+  napi_value arr = typed(env, napi_uint8_array, EVM_DIST_ID_BYTES, 1, &p);
+  const int st = evm_dist_unique_id((uint8_t*)p);
+  if (st) return throw_status(env, st, "evm_dist_unique_id");
+  return arr;
+}
+
+// distInit(ctx, id, rank, world) -> handle   (collective, blocks until every rank joined)
+napi_value DistInit(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  if (!get_args(env, info, 4, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  void* id;
+  size_t il;
+  if (!bytes_of(env, a[1], &id, &il)) return nullptr;
+  if (il != EVM_DIST_ID_BYTES) return throw_status(env, EVM_EINVAL, "distInit: id must be 128 bytes");
+  evm_dist* d = nullptr;
+  const int st = evm_dist_init(cx->c, (const uint8_t*)id, (int)u32(env, a[2]), (int)u32(env, a[3]), &d);
+  if (st) return throw_status(env, st, "evm_dist_init");
+  return make_ext(env, d);
+}
+
+napi_value DistFree(napi_env env, napi_callback_info info) {
+  napi_value a[2];
+  if (!get_args(env, info, 2, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_dist_free(cx->c, (evm_dist*)ext(env, a[1]));
+  return nullptr;
+}
+
+// distRoute(ctx, d, ts Uint8Array(n * stride), stride, owner Uint32Array, aux Uint32Array | null)
+//   -> { ts, owner, aux, src (Float64Array: source rank * 2^32 + index) }   (collective)
+napi_value DistRoute(napi_env env, napi_callback_info info) {
+  napi_value a[6];
+  if (!get_args(env, info, 6, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
+  evm_dist* d = (evm_dist*)ext(env, a[1]);
+  void *ts, *ow, *ax = nullptr;
+  size_t tl, ol, al = 0;
+  if (!bytes_of(env, a[2], &ts, &tl) || !bytes_of(env, a[4], &ow, &ol)) return nullptr;
+  if (!is_null(env, a[5]) && !bytes_of(env, a[5], &ax, &al)) return nullptr;
+  const size_t stride = u32(env, a[3]);
+  const size_t n = ol / 4;
+  if (!stride || tl != n * stride || (ax && al != ol)) return throw_status(env, EVM_EINVAL, "distRoute: sizes");
+  Dev dts(ctx, tl, ts), dow(ctx, ol, ow), dax(ctx, ax ? al : 1, ax);
+  uint64_t nr = 0;
+  int st = evm_dist_route(ctx, d, (const char*)dts.p, stride, n, (const uint32_t*)dow.p,
+                          ax ? (const uint32_t*)dax.p : nullptr, nullptr, &nr);
+  if (st) return throw_status(env, st, "evm_dist_route");
+  Dev rts(ctx, nr * stride), row(ctx, nr * 4), rax(ctx, nr * 4), rsrc(ctx, nr * 8);
+  st = evm_dist_take(ctx, d, 0, (char*)rts.p, stride, (uint32_t*)row.p, (uint32_t*)rax.p, (uint64_t*)rsrc.p, nr,
+                     nullptr);
+  if (st) return throw_status(env, st, "evm_dist_take");
+  void *hts, *how, *hax;
+  napi_value vts = typed(env, napi_uint8_array, nr * stride, 1, &hts);
+  napi_value vow = typed(env, napi_uint32_array, nr, 4, &how);
+  napi_value vax = typed(env, napi_uint32_array, nr, 4, &hax);
+  std::vector<uint64_t> src(nr);
+  evm_copy_d2h(ctx, hts, rts.p, nr * stride);
+  evm_copy_d2h(ctx, how, row.p, nr * 4);
+  evm_copy_d2h(ctx, hax, rax.p, nr * 4);
+  evm_copy_d2h(ctx, src.data(), rsrc.p, nr * 8);
+  double* sp;
+  napi_value vsrc = typed(env, napi_float64_array, nr, 8, (void**)&sp);
+  for (uint64_t i = 0; i < nr; ++i) sp[i] = (double)(src[i] >> 32) * 4294967296.0 + (double)(uint32_t)src[i];
+  napi_value res;
+  napi_create_object(env, &res);
+  napi_set_named_property(env, res, "ts", vts);
+  napi_set_named_property(env, res, "owner", vow);
+  napi_set_named_property(env, res, "aux", vax);
+  napi_set_named_property(env, res, "src", vsrc);
+  return res;
+}
+
+// distGatherRoots(ctx, d, tree, nOwnersGlobal) -> { root Int32Array, present Uint8Array }   (collective)
+napi_value DistGatherRoots(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  if (!get_args(env, info, 4, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
+  const uint32_t ng = u32(env, a[3]);
+  Dev dr(ctx, 4 * (ng ? ng : 1)), dp(ctx, ng ? ng : 1);
+  const evm_tree* t = (const evm_tree*)ext(env, a[2]);
+  const int st = evm_dist_gather_roots(ctx, (evm_dist*)ext(env, a[1]), &t, 1, ng, (int32_t*)dr.p, (uint8_t*)dp.p);
+  if (st) return throw_status(env, st, "evm_dist_gather_roots");
+  void *hr, *hp;
+  napi_value vr = typed(env, napi_int32_array, ng, 4, &hr);
+  napi_value vp = typed(env, napi_uint8_array, ng, 1, &hp);
+  evm_copy_d2h(ctx, hr, dr.p, 4ull * ng);
+  evm_copy_d2h(ctx, hp, dp.p, ng);
+  napi_value res;
+  napi_create_object(env, &res);
+  napi_set_named_property(env, res, "root", vr);
+  napi_set_named_property(env, res, "present", vp);
+  return res;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   const struct {
     const char* name;
@@ -783,7 +889,9 @@ napi_value Init(napi_env env, napi_value exports) {
              {"serverSelectAsync", ServerSelectAsync},
              {"storeFree", StoreFree},   {"storeTree", StoreTree},   {"serverIngest", ServerIngest},
              {"serverSelect", ServerSelect}, {"storeSince", StoreSince}, {"receiveFold", ReceiveFold},
-             {"pbDecode", PbDecode},         {"pbEncode", PbEncode}};
+             {"pbDecode", PbDecode},         {"pbEncode", PbEncode},
+             {"distUniqueId", DistUniqueId}, {"distInit", DistInit},     {"distFree", DistFree},
+             {"distRoute", DistRoute},       {"distGatherRoots", DistGatherRoots}};
   for (const auto& f : fns) {
     napi_value v;
     napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.fn, nullptr, &v);

@@ -280,4 +280,36 @@ class Server {
   }
 }
 
-module.exports = { Engine, Server, SyncRequest, SyncResponse, encodeTimestamps, MSG_UPS, MSG_XOR, MSG_INS };
+// Multi-GPU owner sharding (evm_dist_*): one Engine + Dist per GPU process;
+// rank 0 makes the id (Dist.uniqueId()) and hands it to the other processes.
+// Owners live on rank owner % world (dense owner ids, e.g. from murmur3(userId)).
+class Dist {
+  static uniqueId() {
+    return addon.distUniqueId();
+  }
+  constructor(engine, id, rank, world) {
+    this.engine = engine;
+    this.rank = rank;
+    this.world = world;
+    this.h = addon.distInit(engine.ctx, id, rank, world); // collective
+  }
+  close() {
+    addon.distFree(this.engine.ctx, this.h);
+  }
+  // collective: this rank's slice of a batch -> the rows of the owners this rank
+  // serves, in global batch order: { timestamps, owner, aux, src } (src = rank * 2^32 + index)
+  route(timestamps, owners, aux = null) {
+    const r = addon.distRoute(this.engine.ctx, this.h, encodeTimestamps(timestamps), STRIDE, Uint32Array.from(owners),
+      aux ? Uint32Array.from(aux) : null);
+    const dec = new TextDecoder();
+    const ts = [];
+    for (let i = 0; i < r.owner.length; i++) ts.push(dec.decode(r.ts.subarray(i * STRIDE, i * STRIDE + 46)));
+    return { timestamps: ts, owner: r.owner, aux: r.aux, src: r.src };
+  }
+  // collective: every owner's root (local owner j of rank r = owner j * world + r)
+  gatherRoots(server, nOwnersGlobal) {
+    return addon.distGatherRoots(this.engine.ctx, this.h, addon.storeTree(server.store), nOwnersGlobal);
+  }
+}
+
+module.exports = { Engine, Server, Dist, SyncRequest, SyncResponse, encodeTimestamps, MSG_UPS, MSG_XOR, MSG_INS };

@@ -2,7 +2,7 @@
 // prints the results as JSON (the pytest side compares them with the oracle).
 "use strict";
 const fs = require("fs");
-const { Engine, Server } = require("./evolu_evm.js");
+const { Engine, Server, Dist } = require("./evolu_evm.js");
 
 const cases = JSON.parse(fs.readFileSync(process.argv[2], "utf8"));
 const eng = new Engine(0);
@@ -64,6 +64,20 @@ async function asyncPart() {
   for (let o = 0; o < cases.server.nOwners; o++) out.server.treesAsync.push(s2.merkleTree(o));
   const g = await s2.getMessagesAsync(cases.server.clientTrees, cases.server.nodeIds);
   out.server.getAsync = g._tag === "Right" ? g.right : g;
+  // multi-GPU plumbing at world 1 (RCCL self exchange): rows keep batch order; roots = the trees' hashes
+  const d = new Dist(eng, Dist.uniqueId(), 0, 1);
+  const rts = cases.server.batches.flat().flatMap((r) => r.messages.map((m) => m.timestamp));
+  const rown = cases.server.batches.flat().flatMap((r) => r.messages.map(() => r.owner));
+  const routed = d.route(rts, rown, rown.map((o, i) => i * 7));
+  out.dist = {
+    sameOrder: routed.timestamps.join() === rts.join() && Array.from(routed.owner).join() === rown.join() &&
+      Array.from(routed.src).join() === rts.map((_, i) => i).join() &&
+      Array.from(routed.aux).join() === rown.map((o, i) => i * 7).join(),
+    roots: (({ root, present }) => Array.from(root, (x, i) => (present[i] ? x : null)))(
+      d.gatherRoots(s2, cases.server.nOwners)),
+    treeHashes: out.server.treesAsync.map((t) => { const h = JSON.parse(t).hash; return h === undefined ? null : h; }),
+  };
+  d.close();
   // an owner id beyond the store's owner count: the engine refuses the batch -> Left
   const addon = require("./evm_napi.node");
   out.leftOnError = await addon.serverIngestAsync(eng.ctx, s2.store, new Uint8Array(48), 48, new Uint32Array([99]), 0);
@@ -71,7 +85,7 @@ async function asyncPart() {
 }
 asyncPart().then(() => {
   eng.close();
-  process.stdout.write(JSON.stringify(out));
+  process.stdout.write("\n" + JSON.stringify(out) + "\n");
 }, (e) => {
   process.stderr.write(String(e && e.stack) + "\n");
   process.exit(1);

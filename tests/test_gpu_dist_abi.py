@@ -102,3 +102,15 @@ def test_gather_roots_matches_trees(eng, dist):
     root, present = dist.gather_roots(trees, n_owners)
     r, p = trees.roots()
     assert np.array_equal(root.cpu().numpy(), r) and np.array_equal(present.cpu().numpy(), p)
+
+
+def test_gather_roots_of_single_owner_trees(eng, dist):
+    """One tree per local owner (the client path's per-owner batches): the
+    local owners are the trees' owners in order, the rest absent."""
+    from evolu_amd import synth
+
+    ts, owner = synth.config3(4, 50, seed_config=9)[:2]
+    trees = [eng.merkle_insert(eng.tree_new(1), eng.dev(ts[owner == o])) for o in range(3)]
+    root, present = dist.gather_roots(trees, 5)
+    want = [int(t.roots()[0][0]) for t in trees]
+    assert root.cpu().tolist()[:3] == want and present.cpu().tolist() == [True, True, True, False, False]

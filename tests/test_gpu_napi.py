@@ -116,8 +116,9 @@ def test_js_entry_points(tmp_path):
     cases["receive"] = rcases
     f = tmp_path / "cases.json"
     f.write_text(json.dumps(cases))
-    res = json.loads(subprocess.run(["node", os.path.join(ROOT, "js", "test_evm.js"), str(f)], check=True,
-                                    capture_output=True, text=True, timeout=300).stdout)
+    out = subprocess.run(["node", os.path.join(ROOT, "js", "test_evm.js"), str(f)], check=True,
+                         capture_output=True, text=True, timeout=300).stdout
+    res = json.loads(out.strip().splitlines()[-1])  # (RCCL prints its banner on stdout first)
     snap = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_snapshots.json")))["merkleTree.test.ts.snap"]
     assert [json.loads(t) for t in res["insert"]] == [snap["insertIntoMerkleTree 1"], snap["insertIntoMerkleTree 2"],
                                                      snap["insertIntoMerkleTree 3"]]
@@ -137,6 +138,9 @@ def test_js_entry_points(tmp_path):
     assert res["server"]["insAsync"] == want_ins
     assert res["server"]["treesAsync"] == res["server"]["trees"]
     assert res["server"]["getAsync"]["ids"] == res["server"]["get"]["ids"]
+    # evm_dist_* through the addon at world 1
+    assert res["dist"]["sameOrder"] is True
+    assert res["dist"]["roots"] == res["dist"]["treeHashes"]
     # a device error reaches the caller as Left(UnknownError), not as a throw
     assert res["leftOnError"]["_tag"] == "Left" and res["leftOnError"]["left"]["type"] == "UnknownError"
     id_ts = [m["timestamp"] for b in batches for r in b for m in r["messages"]]

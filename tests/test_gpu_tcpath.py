@@ -7,6 +7,7 @@ verbatim SQL) and, at BASELINE sizes, bit for bit against the sort path."""
 import random
 
 import numpy as np
+import torch
 import pytest
 
 from oracle import evolu_oracle as O
@@ -233,3 +234,30 @@ def test_tc_path_ascending_stream(eng, cells):
     for a, b in zip(res[0], res[1]):
         assert np.array_equal(a, b)
     assert (res[0][0] & L.MSG_UPS).mean() > 0.5  # mostly new maxima
+
+
+@pytest.mark.parametrize("n", [1_250_001, 999_937, 65])
+def test_tc_path_ragged_size_keeps_dense_fold(eng, n):
+    """A batch whose size is not a multiple of 64 takes the dense minute fold
+    (the tail lanes of the last wave must not widen the minute bounds), and
+    equals the sort path."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    ts_np, cell_np = synth.config2(max(n, 1000), 1000, seed_config=77)
+    ts, cell = eng.dev(ts_np[:n]), eng.dev(cell_np[:n])
+    eng.set_option(L.OPT_CLIENT_PATH, 3)
+    eng.prof_enable(True)
+    eng.prof_reset()
+    f1, w1, t1, st = eng.apply_batch(eng.tree_new(1), ts, cell, 1000, raise_on_error=False)
+    rep = eng.prof_report()
+    eng.prof_enable(False)
+    if st == L.EVM_OK:  # (a tie would send the batch to the exact walk path)
+        assert "k_cl_fold_hist<true>" in rep or "k_cl_fold_hist" in rep, sorted(rep)
+        assert "k_cl_fold_ck" not in rep, sorted(rep)
+    eng.set_option(L.OPT_CLIENT_PATH, 2)
+    f2, w2, t2, _ = eng.apply_batch(eng.tree_new(1), ts, cell, 1000)
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    if st == L.EVM_OK:
+        assert torch.equal(f1, f2) and torch.equal(w1, w2)
+        assert t1.to_json(0) == t2.to_json(0)
