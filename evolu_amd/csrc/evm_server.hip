@@ -536,12 +536,10 @@ __global__ __launch_bounds__(256) void k_run_fill(const u32* __restrict__ run_po
 
 // --------------------------------------------- sub-batches (hybrid ingest)
 // messages whose owner's share exceeds the LDS capacity
-__global__ void k_big_mask(const evm_rec* __restrict__ rec, size_t n, const u64* __restrict__ seg, u64 cap,
+__global__ void k_big_mask(const evm_rec* __restrict__ rec, size_t n, const uint8_t* __restrict__ ownbig,
                            uint8_t* __restrict__ mask) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const u32 o = rec[i].aux;
-    mask[i] = seg[o + 1] - seg[o] > cap ? 1 : 0;
-  }
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    mask[i] = ownbig[rec[i].aux];
 }
 
 __global__ void k_mask_u32(const uint8_t* __restrict__ mask, size_t n, u32* __restrict__ out) {
@@ -600,6 +598,25 @@ __device__ __forceinline__ u64 lb_u64(const u64* a, u64 lo, u64 hi, u64 x) {
   return lo;
 }
 
+// A segment: a contiguous piece of one owner's share of the batch and the
+// key range it covers.  Normally one segment per owner (the identity view:
+// owner = s, bounds from the owner offsets).  An owner whose share exceeds
+// SVO_CAP is cut into key-range segments at minute splitters (sampled from
+// its messages): every copy of a timestamp lands in one segment, so the
+// per-segment dedup is the owner's; each segment also owns the owner's
+// stored rows [sa, sb) and tree leaves [la, lb) of its minute range (the
+// first segment from -inf, the last to +inf), so the merge writes every
+// stored row and leaf exactly once.
+struct SegView {
+  const u32* owner;  // [NS] (null: identity)
+  const u64* start;  // [NS + 1] offsets into perm
+  const u64* sa;     // stored rows [sa[s], sb[s])
+  const u64* sb;
+  const u64* la;     // tree leaves [la[s], lb[s])
+  const u64* lb;
+};
+__device__ __forceinline__ u32 seg_owner(const SegView& v, u32 s) { return v.owner ? v.owner[s] : s; }
+
 template <u32 CAP>
 struct SvoLog2 {
   static constexpr int v = CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;
@@ -611,12 +628,13 @@ struct SvoLog2 {
 // runs of one tc (distinct nodes) are then put in node order.
 template <u32 CAP>
 __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
-    const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u64* __restrict__ seg, StoreView st,
-    const u64* __restrict__ t_off, const u64* __restrict__ t_ck, u64 id_base, uint8_t* __restrict__ flags,
+    const evm_rec* __restrict__ rec, const u32* __restrict__ perm, SegView sv, StoreView st,
+    const u64* __restrict__ t_ck, u64 id_base, uint8_t* __restrict__ flags,
     u64* __restrict__ n_tc, u64* __restrict__ n_hi, u32* __restrict__ n_lo, u64* __restrict__ n_id,
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status,
-    const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list) {
+    const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list,
+    uint8_t* __restrict__ ownbig) {
   constexpr int PER = CAP / SVO_THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
   constexpr u64 PMASK = CAP - 1;
@@ -629,18 +647,23 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   __shared__ u32 s_cnt[CAP];  // counting sort: bucket counts, then starts
   __shared__ u64 s_red[2 * (SVO_THREADS / 64)];
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
-  const u32 o = list ? list[blockIdx.x] : blockIdx.x;  // pass 2: only the owners pass 1 deferred
+  const u32 s = list ? list[blockIdx.x] : blockIdx.x;  // pass 2: only the segments pass 1 deferred
+  const u32 o = seg_owner(sv, s);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const u64 a = seg[o];
-  const u64 m = seg[o + 1] - a;  // an unsorted owner column (bad ids) may underflow: "big"
-  const u64 la = t_off[o], lb = t_off[o + 1];
+  const u64 a = sv.start[s];
+  const u64 m = sv.start[s + 1] - a;  // an unsorted owner column (bad ids) may underflow: "big"
+  const u64 la = sv.la[s], lb = sv.lb[s];
   if (m > CAP || m == 0) {
     if (threadIdx.x == 0) {
-      if (m <= SVO_CAP && mid_list) mid_list[1 + atomicAdd(&mid_list[0], 1u)] = o;  // for the SVO_CAP pass
-      else if (m) atomicOr(&status->big, 1u);
-      cnt_rows[o] = 0;
-      cnt_new[o] = 0;
-      cnt_leaves[o] = (u32)(lb - la);
+      if (m <= SVO_CAP && mid_list) {
+        mid_list[1 + atomicAdd(&mid_list[0], 1u)] = s;  // for the SVO_CAP pass
+      } else if (m) {
+        atomicOr(&status->big, 1u);
+        ownbig[o] = 1;  // the owner's messages go to the sort path (k_seg_fix drops its other segments)
+      }
+      cnt_rows[s] = 0;
+      cnt_new[s] = 0;
+      cnt_leaves[s] = (u32)(lb - la);
     }
     return;
   }
@@ -792,8 +815,37 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     }
   }
   __syncthreads();
+  // among equal timestamps the one first in the batch (smallest batch index)
+  // is the candidate insert -- independent of the order the segment's
+  // messages were listed in (key-range segments are gathered unordered).
+  // s_cnt[p] = 1: p is its timestamp's candidate.  A run's first position
+  // decides the whole run (O(run) per run).
+  for (u32 p = threadIdx.x; p < m; p += SVO_THREADS) {
+    const u64 kp = s_k[p];
+    const u32 pp = (u32)(kp & PMASK);
+    auto same = [&](u32 x, u32 y) {
+      const u32 px = (u32)(s_k[x] & PMASK), py = (u32)(s_k[y] & PMASK);
+      return (s_k[x] >> PB) == (s_k[y] >> PB) && s_rh[px] == s_rh[py] && s_rl[px] == s_rl[py];
+    };
+    if (p > 0 && same(p - 1, p)) continue;  // not a run start: the start decides
+    u32 e = p + 1;
+    if (e < m && same(p, e)) {
+      u32 best = p, bb = perm[a + pp];
+      for (; e < m && same(e - 1, e); ++e) {
+        const u32 be = perm[a + (u32)(s_k[e] & PMASK)];
+        if (be < bb) {
+          bb = be;
+          best = e;
+        }
+      }
+      for (u32 q = p; q < e; ++q) s_cnt[q] = q == best ? 1u : 0u;
+    } else {
+      s_cnt[p] = 1u;
+    }
+  }
+  __syncthreads();
   // first occurrences not yet stored; thread t owns sorted positions t*PER ..
-  const u64 sa = st.off[o], sb = st.off[o + 1];
+  const u64 sa = sv.sa[s], sb = sv.sb[s];
   u64 mt[PER], mh[PER];
   u32 ml[PER], mb[PER], mhash[PER];
   u32 insm = 0, c = 0;
@@ -810,12 +862,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
       ml[r] = s_rl[pos];
       mb[r] = perm[a + pos];
       mhash[r] = s_h[pos];
-      bool ins = true;
-      if (p > 0) {
-        const u64 kq = s_k[p - 1];
-        const u32 qp = (u32)(kq & PMASK);
-        ins = (kq >> PB) != (kp >> PB) || s_rh[qp] != mh[r] || s_rl[qp] != ml[r];
-      }
+      bool ins = s_cnt[p] != 0;
       if (ins && sb > sa) {
         const SKey k{o, mt[r], mh[r], ml[r]};
         const size_t q = store_lower(st, sa, sb, k);
@@ -889,27 +936,40 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   u32 dtot;
   block_inclusive_scan<u32>(dups, tmp, OpAdd<u32>(), &dtot);
   if (threadIdx.x == 0) {
-    cnt_rows[o] = M;
-    cnt_new[o] = NL;
-    cnt_leaves[o] = (u32)(lb - la) + NL - dtot;
+    cnt_rows[s] = M;
+    cnt_new[s] = NL;
+    cnt_leaves[s] = (u32)(lb - la) + NL - dtot;
+  }
+}
+
+// segments of an owner sent to the sort path contribute nothing here (its
+// stored rows and leaves are still copied)
+__global__ void k_seg_fix(SegView sv, u32 NS, const uint8_t* __restrict__ ownbig, u32* __restrict__ cnt_rows,
+                          u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves) {
+  for (u32 s = blockIdx.x * blockDim.x + threadIdx.x; s < NS; s += gridDim.x * blockDim.x) {
+    if (!ownbig[seg_owner(sv, s)]) continue;
+    cnt_rows[s] = 0;
+    cnt_new[s] = 0;
+    cnt_leaves[s] = (u32)(sv.lb[s] - sv.la[s]);
   }
 }
 
 __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
-    const u64* __restrict__ seg, u32 n_owners, StoreView st, const u64* __restrict__ st_id, const u64* __restrict__ n_tc,
+    SegView sv, u32 NS, u32 n_owners, StoreView st, const u64* __restrict__ st_id, const u64* __restrict__ n_tc,
     const u64* __restrict__ n_hi, const u32* __restrict__ n_lo, const u64* __restrict__ n_id,
-    const u32* __restrict__ cnt_rows, const u32* __restrict__ row_pos, const u64* __restrict__ t_off,
+    const u32* __restrict__ cnt_rows, const u32* __restrict__ row_pos,
     const u64* __restrict__ t_ck, const int32_t* __restrict__ t_xr, const u64* __restrict__ l_ck,
     const int32_t* __restrict__ l_xr, const uint8_t* __restrict__ l_dup, const u32* __restrict__ cnt_new,
     const u32* __restrict__ leaf_pos, StoreOut so, u64* __restrict__ so_off, u64* __restrict__ to_ck,
     int32_t* __restrict__ to_xr, u64* __restrict__ to_off) {
   __shared__ u32 s_dp[SVO_CAP + 1];  // exclusive prefix count of the new leaves already in the tree
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
-  const u32 o = blockIdx.x;
-  const u64 a = seg[o];
-  const u32 M = cnt_rows[o], NL = cnt_new[o];
-  const u64 sa = st.off[o], sb = st.off[o + 1];
-  const u64 base = sa + row_pos[o];  // rows of the earlier owners: old + new
+  const u32 s = blockIdx.x;
+  const u32 o = seg_owner(sv, s);
+  const u64 a = sv.start[s];
+  const u32 M = cnt_rows[s], NL = cnt_new[s];
+  const u64 sa = sv.sa[s], sb = sv.sb[s];
+  const u64 base = sa + row_pos[s];  // rows of the earlier segments: old + new
   // rows: the owner's stored and new keys are disjoint sorted lists
   for (u64 k = sa + threadIdx.x; k < sb; k += SVO_THREADS) {
     const SKey key = skey_at(st, k);
@@ -936,8 +996,8 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     so.id[w] = n_id[a + j];
   }
   // leaves: union of the tree's and the new ones by code, equal codes XOR-combined
-  const u64 la = t_off[o], lb = t_off[o + 1];
-  const u64 lbase = leaf_pos[o];
+  const u64 la = sv.la[s], lb = sv.lb[s];
+  const u64 lbase = leaf_pos[s];
   constexpr int PERB = SVO_CAP / SVO_THREADS;
   u32 d[PERB], c = 0;
 #pragma unroll
@@ -972,9 +1032,11 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     to_xr[w] = l_xr[a + j];
   }
   if (threadIdx.x == 0) {
-    so_off[o] = base;
-    to_off[o] = lbase;
-    if (o == n_owners - 1) {
+    if (s == 0 || seg_owner(sv, s - 1) != o) {  // the owner's first segment starts its rows and leaves
+      so_off[o] = base;
+      to_off[o] = lbase;
+    }
+    if (s == NS - 1) {
       so_off[n_owners] = base + (sb - sa) + M;
       to_off[n_owners] = lbase + (lb - la) + NL - dtot;
     }
@@ -1145,6 +1207,213 @@ void store_release_arrays(evm_ctx* ctx, evm_store* s) {
   s->lo = nullptr;
 }
 
+// ------------------------------------------- key-range segments (big owners)
+constexpr u32 SEG_TARGET = 720;     // messages per segment of a cut owner (nearly all fit the 1,024 kernel)
+constexpr u32 SEG_SPLIT_MIN = 1024; // shares above this are cut (the 1,024 kernel is the fast one)
+constexpr u32 SAMPLE_STRIDE = 16;   // one sampled minute per 16 messages of a cut owner
+constexpr u32 SEG_TABLE_RATIO = 64; // minute -> segment table when the splitters span <= 64 minutes per segment
+
+__device__ __forceinline__ u32 upper_u32(const u32* a, u32 n, u32 x) {  // first k with a[k] > x
+  u32 lo = 0, hi = n;
+  while (lo < hi) {
+    const u32 mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// per owner: segments (1 unless the share exceeds SVO_CAP), samples, splitters
+__global__ void k_seg_plan(const u64* __restrict__ seg, u32 O, u32* __restrict__ nb, u32* __restrict__ ns,
+                           u32* __restrict__ nsp) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < O; o += gridDim.x * blockDim.x) {
+    const u64 m = seg[o + 1] - seg[o];
+    const bool big = m > SEG_SPLIT_MIN;
+    const u32 b = big ? (u32)((m + SEG_TARGET - 1) / SEG_TARGET) : 1u;
+    nb[o] = b;
+    ns[o] = big ? (u32)((m + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE) : 0u;
+    nsp[o] = b - 1;
+  }
+}
+
+// sample q of owner o: the minute of its share's message at j * SAMPLE_STRIDE
+// (share in batch order: a spread-out sample); key (owner, minute - gmin)
+__global__ void k_seg_sample(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u64* __restrict__ seg,
+                             const u32* __restrict__ soff, u32 O, u32 nsamp, u32 gmin, int mb,
+                             u64* __restrict__ key, u32* __restrict__ val) {
+  for (u32 q = blockIdx.x * blockDim.x + threadIdx.x; q < nsamp; q += gridDim.x * blockDim.x) {
+    const u32 o = upper_u32(soff, O + 1, q) - 1;
+    const u64 p = seg[o] + (u64)(q - soff[o]) * SAMPLE_STRIDE;
+    const u32 mnt = rec[perm[p]].minute;
+    key[q] = ((u64)o << mb) | (u64)(mnt - gmin);
+    val[q] = q;
+  }
+}
+
+// splitter k (1 .. nb-1) of owner o: the sorted sample at rank k * ns / nb
+__global__ void k_seg_split(const u64* __restrict__ skey, const u32* __restrict__ soff, const u32* __restrict__ spoff,
+                            const u32* __restrict__ bbase, u32 O, u32 nsp, u32 gmin, int mb, u32* __restrict__ sp) {
+  const u64 mask = (1ull << mb) - 1;
+  for (u32 q = blockIdx.x * blockDim.x + threadIdx.x; q < nsp; q += gridDim.x * blockDim.x) {
+    const u32 o = upper_u32(spoff, O + 1, q) - 1;
+    const u32 k = q - spoff[o] + 1;
+    const u64 nso = soff[o + 1] - soff[o], nbo = bbase[o + 1] - bbase[o];
+    if (!nso) {  // no sample: one segment takes everything (if it overflows, the owner takes the sort path)
+      sp[q] = 0xffffffffu;
+      continue;
+    }
+    const u64 r = soff[o] + (u64)k * nso / nbo;
+    sp[q] = (u32)(skey[r] & mask) + gmin;
+  }
+}
+
+// per cut owner: the length of its minute -> segment table (the minutes from
+// its first to its last splitter), 0 when that span is too wide (search)
+__global__ void k_seg_tlen(const u32* __restrict__ spoff, const u32* __restrict__ sp, u32 O, u32* __restrict__ tlen) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < O; o += gridDim.x * blockDim.x) {
+    const u32 a = spoff[o], k = spoff[o + 1] - a;
+    u32 len = 0;
+    if (k) {
+      const u64 span = (u64)sp[a + k - 1] - sp[a] + 1;
+      len = span <= (u64)SEG_TABLE_RATIO * (k + 1) ? (u32)span : 0u;
+    }
+    tlen[o] = len;
+  }
+}
+
+// table entry q of owner o: the segment (splitters <= minute) of minute sp_first + j
+__global__ void k_seg_table(const u32* __restrict__ spoff, const u32* __restrict__ sp, const u32* __restrict__ toff,
+                            u32 O, u32 ntab, u32* __restrict__ tab) {
+  for (u32 q = blockIdx.x * blockDim.x + threadIdx.x; q < ntab; q += gridDim.x * blockDim.x) {
+    const u32 o = upper_u32(toff, O + 1, q) - 1;
+    const u32 a = spoff[o], k = spoff[o + 1] - a;
+    tab[q] = upper_u32(sp + a, k, sp[a] + (q - toff[o]));
+  }
+}
+
+// every message's segment: the owner's first, plus the splitters <= its minute
+__global__ void k_seg_key(const evm_rec* __restrict__ rec, const u32* __restrict__ owner, size_t n,
+                          const u32* __restrict__ bbase, const u32* __restrict__ spoff, const u32* __restrict__ sp,
+                          const u32* __restrict__ toff, const u32* __restrict__ tab, u32* __restrict__ key,
+                          u32* __restrict__ val) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const u32 o = owner[i];
+    const u32 b0 = bbase[o], nbo = bbase[o + 1] - b0;
+    u32 k = b0;
+    if (nbo > 1) {
+      const u32 mnt = rec[i].minute, a = spoff[o], t0 = toff[o], tl = toff[o + 1] - t0;
+      if (tl) {
+        const u32 first = sp[a];
+        k += mnt < first ? 0u : mnt - first >= tl ? nbo - 1 : tab[t0 + (mnt - first)];
+      } else {
+        k += upper_u32(sp + a, nbo - 1, mnt);
+      }
+    }
+    key[i] = k;
+    val[i] = (u32)i;
+  }
+}
+
+__global__ void k_seg_start(const u32* __restrict__ skey, size_t n, u32 NS, u64* __restrict__ start) {
+  for (u32 b = blockIdx.x * blockDim.x + threadIdx.x; b <= NS; b += gridDim.x * blockDim.x) {
+    size_t lo = 0, hi = n;
+    while (lo < hi) {
+      const size_t mid = (lo + hi) >> 1;
+      if (skey[mid] < b) lo = mid + 1;
+      else hi = mid;
+    }
+    start[b] = lo;
+  }
+}
+
+// every 16th batch position: (owner, minute - gmin) (mb = 0: owner only)
+__global__ void k_seg_sample_all(const evm_rec* __restrict__ rec, const u32* __restrict__ owner, size_t n, u32 gmin,
+                                 int mb, u64* __restrict__ key, u32* __restrict__ val) {
+  const size_t nq = (n + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = q * SAMPLE_STRIDE;
+    u64 k = (u64)owner[i] << mb;
+    if (mb) k |= (u64)(rec[i].minute - gmin);
+    key[q] = k;
+    val[q] = (u32)q;
+  }
+}
+
+// segments per owner from its sample count (share ~ 16 x samples)
+__global__ void k_seg_plan_est(const u32* __restrict__ soff, u32 O, int cut, u32* __restrict__ nb,
+                               u32* __restrict__ nsp) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < O; o += gridDim.x * blockDim.x) {
+    const u64 est = (u64)(soff[o + 1] - soff[o]) * SAMPLE_STRIDE;
+    const u32 b = cut && est > SEG_SPLIT_MIN ? (u32)((est + SEG_TARGET - 1) / SEG_TARGET) : 1u;
+    nb[o] = b;
+    nsp[o] = b - 1;
+  }
+}
+
+// per owner: its samples' range in the sorted sample keys
+__global__ void k_seg_soff(const u64* __restrict__ skey, u32 nsamp, u32 O, int mb, u32* __restrict__ soff) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o <= O; o += gridDim.x * blockDim.x) {
+    const u64 x = (u64)o << mb;
+    u32 lo = 0, hi = nsamp;
+    while (lo < hi) {
+      const u32 mid = (lo + hi) >> 1;
+      if (skey[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    soff[o] = lo;
+  }
+}
+
+__global__ void k_widen(const u32* __restrict__ a, size_t n, u64* __restrict__ b) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+// segment b's owner and the first stored row / tree leaf of its minute range
+__global__ void k_seg_ranges(const u32* __restrict__ bbase, const u32* __restrict__ spoff, const u32* __restrict__ sp,
+                             u32 O, u32 NS, StoreView st, const u64* __restrict__ t_off, const u64* __restrict__ t_ck,
+                             u32* __restrict__ sowner, u64* __restrict__ sa, u64* __restrict__ la) {
+  for (u32 b = blockIdx.x * blockDim.x + threadIdx.x; b < NS; b += gridDim.x * blockDim.x) {
+    const u32 o = upper_u32(bbase, O + 1, b) - 1;
+    const u32 k = b - bbase[o];
+    sowner[b] = o;
+    u64 r0 = st.off[o], l0 = t_off[o];
+    if (k) {
+      const u32 mlo = sp[spoff[o] + k - 1];
+      const u64 tc0 = ((u64)mlo * 60000ull) << 16;  // rows with minute >= mlo: tc >= this
+      u64 hi = st.off[o + 1];
+      while (r0 < hi) {
+        const u64 mid = (r0 + hi) >> 1;
+        if (st.tc[mid] < tc0) r0 = mid + 1;
+        else hi = mid;
+      }
+      l0 = lb_u64(t_ck, l0, t_off[o + 1], ((u64)o << 40) | minute_code(mlo));
+    }
+    sa[b] = r0;
+    la[b] = l0;
+  }
+}
+
+__global__ void k_seg_ends(const u32* __restrict__ sowner, u32 NS, StoreView st, const u64* __restrict__ t_off,
+                           const u64* __restrict__ sa, const u64* __restrict__ la, u64* __restrict__ sb,
+                           u64* __restrict__ lb) {
+  for (u32 b = blockIdx.x * blockDim.x + threadIdx.x; b < NS; b += gridDim.x * blockDim.x) {
+    const u32 o = sowner[b];
+    const bool next = b + 1 < NS && sowner[b + 1] == o;
+    sb[b] = next ? sa[b + 1] : st.off[o + 1];
+    lb[b] = next ? la[b + 1] : t_off[o + 1];
+  }
+}
+
+static int base3_len_host(uint32_t m) {
+  int L = 1;
+  uint64_t p = 3;
+  while (L < CODE_DIGITS && (uint64_t)m >= p) {
+    p *= 3;
+    ++L;
+  }
+  return L;
+}
+
 // K5 driver.  On success *done = true and (*ns, *new_tree) hold the new store
 // arrays and tree; *done = false (status OK) when some owner's share exceeds
 // SVO_CAP or mixes key lengths: the caller takes the global sort path with
@@ -1158,7 +1427,6 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   const u32 O = s->n_owners;
   int st;
   // stable sort of the batch index by owner: each owner's share in batch order
-  u32* own = S.alloc<u32>(n);
   u64* seg = S.alloc<u64>((size_t)O + 1);
   SvoStatus* status = S.alloc<SvoStatus>(1);
   u64* n_tc = S.alloc<u64>(n);
@@ -1168,10 +1436,9 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   u64* l_ck = S.alloc<u64>(n);
   int32_t* l_xr = S.alloc<int32_t>(n);
   uint8_t* l_dup = S.alloc<uint8_t>(n);
-  u32* cnt = S.alloc<u32>(3 * (size_t)O);  // rows, new leaves, merged leaves
-  u32* pos = S.alloc<u32>(2 * (size_t)O);  // row / leaf offsets
   u32* tot = S.alloc<u32>(2);
-  if (!own || !seg || !status || !n_tc || !n_hi || !n_lo || !n_id || !l_ck || !l_xr || !l_dup || !cnt || !pos || !tot)
+  uint8_t* ownbig = S.alloc<uint8_t>(O);
+  if (!seg || !status || !n_tc || !n_hi || !n_lo || !n_id || !l_ck || !l_xr || !l_dup || !tot || !ownbig)
     return EVM_ENOMEM;
   const int obits = O > 1 ? 32 - __builtin_clz(O - 1) : 0;
   // requests arrive as runs of one owner (index.ts:224-248): sort the runs,
@@ -1188,7 +1455,43 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   HIPR(hipMemcpyAsync(&R, nrun, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
   u32* ov = perm;
-  if ((size_t)R * 8 <= n) {
+  const bool runs = (size_t)R * 8 <= n;
+  const evm_tree* t = s->tree;
+  Info hi;
+  auto check_info = [&]() -> int {
+    int e = read_info(ctx, info, &hi);
+    if (e) return e;
+    if (hi.bad_aux) return EVM_EINVAL;
+    if (hi.bad) {
+      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
+      (void)evm_sync(ctx);
+      return EVM_ENONCANON;
+    }
+    return EVM_OK;
+  };
+  // a batch's minutes all have one base-3 key length: code order = minute
+  // order, so an owner can be cut at minutes (else no owner is cut)
+  auto cuttable = [&]() {
+    return ctx->server_path != 3 && hi.minute_min <= hi.minute_max &&
+           base3_len_host(hi.minute_min) == base3_len_host(hi.minute_max);
+  };
+  u32* nb = S.alloc<u32>((size_t)O + 1);
+  u32* nsm = S.alloc<u32>((size_t)O + 1);
+  u32* nsp = S.alloc<u32>((size_t)O + 1);
+  u32* bbase = S.alloc<u32>((size_t)O + 1);
+  u32* soff = S.alloc<u32>((size_t)O + 1);
+  u32* spoff = S.alloc<u32>((size_t)O + 1);
+  if (!nb || !nsm || !nsp || !bbase || !soff || !spoff) return EVM_ENOMEM;
+  SegView sv{nullptr, seg, s->off, s->off + 1, t->off, t->off + 1};
+  u32 NS = O;
+  const u32* kperm = ov;  // batch indices, segment by segment
+  bool split = false;
+  u64* skey = nullptr;   // sorted samples: owner << mb | minute - gmin
+  u32 gmin = 0;
+  int mb = 1;
+  u32 nspl = 0;
+  if (runs) {
+    // requests arrive as runs of one owner (index.ts:224-248): sort the runs, not the messages
     u32* run_start = S.alloc<u32>(R);
     u32* run_owner = S.alloc<u32>(R);
     u32* order = S.alloc<u32>(R);
@@ -1204,41 +1507,123 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, len, R, run_pos, run_pos + R))) return st;
     KLAUNCH(k_run_seg, dim3(grid_for((size_t)O + 1, 256)), dim3(256), rk, R, run_pos, O, seg);
     KLAUNCH(k_run_fill, dim3(grid_for(R, 4 * RF_RUNS, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
+    // owners above SEG_SPLIT_MIN: key-range segments, splitters from every
+    // 16th message of their share
+    KLAUNCH(k_seg_plan, dim3(grid_for(O, 256)), dim3(256), seg, O, nb, nsm, nsp);
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nb, O, bbase, bbase + O))) return st;
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsm, O, soff, soff + O))) return st;
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsp, O, spoff, spoff + O))) return st;
+    u32 plan[3] = {0, 0, 0};  // segments, samples, splitters
+    HIPR(hipMemcpyAsync(&plan[0], bbase + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipMemcpyAsync(&plan[1], soff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipMemcpyAsync(&plan[2], spoff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = check_info())) return st;
+    split = plan[1] > 0 && cuttable();
+    if (split) {
+      gmin = hi.minute_min;
+      mb = std::max(1, ceil_log2((size_t)(hi.minute_max - gmin) + 1));
+      NS = plan[0];
+      nspl = plan[2];
+      const u32 nsamp = plan[1];
+      skey = S.alloc<u64>(nsamp);
+      u32* sval = S.alloc<u32>(nsamp);
+      if (!skey || !sval) return EVM_ENOMEM;
+      KLAUNCH(k_seg_sample, dim3(grid_for(nsamp, 256)), dim3(256), rec, ov, seg, soff, O, nsamp, gmin, mb, skey, sval);
+      if ((st = radix_sort_pairs<u64>(ctx, S, skey, sval, nsamp, 0, mb + obits))) return st;
+    }
   } else {
-    HIPR(hipMemcpyAsync(own, owner, sizeof(u32) * n, hipMemcpyDeviceToDevice, ctx->stream));
-    if ((st = launch_iota(ctx, perm, n))) return st;
-    u32* ok = own;
-    if ((st = radix_sort_pairs<u32>(ctx, S, ok, ov, n, 0, obits))) return st;
-    KLAUNCH(k_sv_owner_off, dim3(grid_for((size_t)O + 1, 256)), dim3(256), ok, n, O, seg);
+    // messages of many owners interleaved: plan from a sample of every 16th
+    // batch position (each owner's share estimated as 16 x its samples; a
+    // wrong estimate costs speed only -- an overfull segment sends its owner
+    // to the sort path); then ONE sort of the batch by segment, which also
+    // groups the owners (no separate owner sort)
+    if ((st = check_info())) return st;
+    if (cuttable()) {
+      gmin = hi.minute_min;
+      mb = std::max(1, ceil_log2((size_t)(hi.minute_max - gmin) + 1));
+    } else {
+      gmin = 0;
+      mb = 0;  // no minutes in the key: one segment per owner
+    }
+    const u32 nq = (u32)((n + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE);
+    skey = S.alloc<u64>(nq);
+    u32* sval = S.alloc<u32>(nq);
+    if (!skey || !sval) return EVM_ENOMEM;
+    KLAUNCH(k_seg_sample_all, dim3(grid_for(nq, 256)), dim3(256), rec, owner, n, gmin, mb, skey, sval);
+    if ((st = radix_sort_pairs<u64>(ctx, S, skey, sval, nq, 0, mb + obits))) return st;
+    KLAUNCH(k_seg_soff, dim3(grid_for((size_t)O + 1, 256)), dim3(256), skey, nq, O, mb, soff);
+    KLAUNCH(k_seg_plan_est, dim3(grid_for(O, 256)), dim3(256), soff, O, mb > 0 ? 1 : 0, nb, nsp);
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nb, O, bbase, bbase + O))) return st;
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsp, O, spoff, spoff + O))) return st;
+    u32 plan[2] = {0, 0};
+    HIPR(hipMemcpyAsync(&plan[0], bbase + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipMemcpyAsync(&plan[1], spoff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    split = true;  // (possibly one segment per owner)
+    NS = plan[0];
+    nspl = plan[1];
   }
-  const evm_tree* t = s->tree;
-  u32 *c_rows = cnt, *c_new = cnt + O, *c_leaves = cnt + 2 * (size_t)O;
-  u32* mid = S.alloc<u32>((size_t)O + 1);  // [count, owners whose share is in (1024, SVO_CAP]]
-  if (!mid) return EVM_ENOMEM;
-  Info hi;
+  if (split) {
+    u32* sp = S.alloc<u32>(std::max<u32>(nspl, 1));
+    u32* bkey = S.alloc<u32>(n);
+    u32* bval = S.alloc<u32>(n);
+    u64* sstart = S.alloc<u64>((size_t)NS + 1);
+    u32* sown = S.alloc<u32>(NS);
+    u64* ssa = S.alloc<u64>(NS);
+    u64* ssb = S.alloc<u64>(NS);
+    u64* sla = S.alloc<u64>(NS);
+    u64* slb = S.alloc<u64>(NS);
+    if (!sp || !bkey || !bval || !sstart || !sown || !ssa || !ssb || !sla || !slb) return EVM_ENOMEM;
+    if (nspl)
+      KLAUNCH(k_seg_split, dim3(grid_for(nspl, 256)), dim3(256), skey, soff, spoff, bbase, O, nspl, gmin, mb, sp);
+    // minute -> segment tables of the cut owners (a lookup per message instead of a search)
+    u32* tlen = S.alloc<u32>((size_t)O + 1);
+    u32* tboff = S.alloc<u32>((size_t)O + 1);
+    if (!tlen || !tboff) return EVM_ENOMEM;
+    KLAUNCH(k_seg_tlen, dim3(grid_for(O, 256)), dim3(256), spoff, sp, O, tlen);
+    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, tlen, O, tboff, tboff + O))) return st;
+    u32 ntab = 0;
+    HIPR(hipMemcpyAsync(&ntab, tboff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    u32* tab = S.alloc<u32>(std::max<u32>(ntab, 1));
+    if (!tab) return EVM_ENOMEM;
+    if (ntab) KLAUNCH(k_seg_table, dim3(grid_for(ntab, 256)), dim3(256), spoff, sp, tboff, O, ntab, tab);
+    KLAUNCH(k_seg_key, dim3(grid_for(n, 256)), dim3(256), rec, owner, n, bbase, spoff, sp, tboff, tab, bkey, bval);
+    u32* bk = bkey;
+    u32* bv = bval;
+    if ((st = radix_sort_pairs<u32>(ctx, S, bk, bv, n, 0, std::max(1, ceil_log2(NS))))) return st;
+    KLAUNCH(k_seg_start, dim3(grid_for((size_t)NS + 1, 256)), dim3(256), bk, n, NS, sstart);
+    KLAUNCH(k_seg_ranges, dim3(grid_for(NS, 256)), dim3(256), bbase, spoff, sp, O, NS, view_of(s), (const u64*)t->off,
+            (const u64*)t->ck, sown, ssa, sla);
+    KLAUNCH(k_seg_ends, dim3(grid_for(NS, 256)), dim3(256), sown, NS, view_of(s), (const u64*)t->off, ssa, sla, ssb,
+            slb);
+    sv = SegView{sown, sstart, ssa, ssb, sla, slb};
+    kperm = bv;
+  }
+  u32* cnt = S.alloc<u32>(3 * (size_t)NS);  // rows, new leaves, merged leaves (per segment)
+  u32* pos = S.alloc<u32>(2 * (size_t)NS);  // row / leaf offsets
+  u32* mid = S.alloc<u32>((size_t)NS + 1);  // [count, segments whose share is in (1024, SVO_CAP]]
+  if (!cnt || !pos || !mid) return EVM_ENOMEM;
+  u32 *c_rows = cnt, *c_new = cnt + NS, *c_leaves = cnt + 2 * (size_t)NS;
   SvoStatus hs;
   u32 ht[2], hmid = 0;
   HIPR(hipMemsetAsync(status, 0, sizeof(SvoStatus), ctx->stream));
   HIPR(hipMemsetAsync(mid, 0, sizeof(u32), ctx->stream));
-  // the common share size over every owner (more workgroups per CU); larger
-  // shares are listed and take the SVO_CAP kernel over just those owners
-  KLAUNCH(k_svo_a<1024>, dim3(O), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off, (const u64*)t->ck,
-          (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves, status, orig,
-          (const u32*)nullptr, mid);
+  HIPR(hipMemsetAsync(ownbig, 0, O, ctx->stream));
+  // the common share size over every segment (more workgroups per CU); larger
+  // shares are listed and take the SVO_CAP kernel over just those segments
+  KLAUNCH(k_svo_a<1024>, dim3(NS), dim3(SVO_THREADS), rec, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base,
+          flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, (const u32*)nullptr,
+          mid, ownbig);
   HIPR(hipMemcpyAsync(&hmid, mid, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  if ((st = read_info(ctx, info, &hi))) return st;
-  if (hi.bad_aux) return EVM_EINVAL;
-  if (hi.bad) {
-    KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
-    (void)evm_sync(ctx);
-    return EVM_ENONCANON;
-  }
+  HIPR(hipStreamSynchronize(ctx->stream));
   if (hmid)
-    KLAUNCH(k_svo_a<SVO_CAP>, dim3(hmid), dim3(SVO_THREADS), rec, ov, seg, view_of(s), (const u64*)t->off,
-            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)(mid + 1), (u32*)nullptr);
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, O, pos, tot))) return st;
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, O, pos + O, tot + 1))) return st;
+    KLAUNCH(k_svo_a<SVO_CAP>, dim3(hmid), dim3(SVO_THREADS), rec, kperm, sv, view_of(s), (const u64*)t->ck,
+            (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves, status, orig,
+            (const u32*)(mid + 1), (u32*)nullptr, ownbig);
+  KLAUNCH(k_seg_fix, dim3(grid_for(NS, 256)), dim3(256), sv, NS, ownbig, c_rows, c_new, c_leaves);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, NS, pos, tot))) return st;
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, NS, pos + NS, tot + 1))) return st;
   HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipMemcpyAsync(ht, tot, sizeof(ht), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
@@ -1248,7 +1633,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     // only some owners are too big for LDS: the rest commit here (the big
     // ones contribute no rows or leaves), the caller sends the big owners'
     // messages through the sort path
-    KLAUNCH(k_big_mask, dim3(grid_for(n, 256)), dim3(256), rec, n, seg, (u64)SVO_CAP, bigmask);
+    KLAUNCH(k_big_mask, dim3(grid_for(n, 256)), dim3(256), rec, n, ownbig, bigmask);
     *big_only = true;
   }
   // new store and tree, exactly sized
@@ -1262,9 +1647,9 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     return st;
   }
   const StoreOut so{ns->owner, ns->tc, ns->hi, ns->lo, ns->id};
-  KLAUNCH(k_svo_b, dim3(O), dim3(SVO_THREADS), seg, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id, c_rows,
-          pos, (const u64*)t->off, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + O, so, ns->off, nt->ck,
-          nt->xr, nt->off);
+  KLAUNCH(k_svo_b, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
+          c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + NS, so, ns->off, nt->ck, nt->xr,
+          nt->off);
   if ((st = scan_exclusive<int32_t, OpXor>(ctx, S, nt->xr, ht[1], nt->pfx, nt->pfx + ht[1]))) {
     store_release_arrays(ctx, ns);
     tree_destroy(ctx, nt);

@@ -108,7 +108,9 @@ int evm_sync(evm_ctx* ctx);
 /* tuning / test knobs */
 #define EVM_OPT_CLIENT_PATH 1 /* evm_apply_batch: 0 auto (streaming tc path, exact walk on a tie), 1 exact walk path, 2 sort path, 3 tc path (exact walk on a tie) */
 #define EVM_OPT_OVERLAP 3     /* 1 (default): independent checks run on a second HIP stream inside a call; 0: one stream */
-#define EVM_OPT_SERVER_PATH 2 /* evm_server_ingest: 0/1 per-owner LDS path where every owner's share fits, 2 force the sort path */
+#define EVM_OPT_SERVER_PATH 2 /* evm_server_ingest: 0/1 per-owner LDS path, owners above its capacity cut into
+                                 key-range segments; 2 force the sort path; 3 LDS path without the segments (owners
+                                 above the capacity through the sort path) */
 #define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 0 histogram + scan + scatter per pass */
 #define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM) */
 int evm_set_option(evm_ctx* ctx, int option, int64_t value);

@@ -40,6 +40,7 @@ def test_split_ingest_rolls_back_on_phase2_failure(eng):
     ts_a, own_a = _batch(41, n_owners)
     ts_b, own_b = _batch(42, n_owners)
     assert np.bincount(own_b, minlength=n_owners).max() > 4096  # the split path is taken
+    eng.set_option(L.OPT_SERVER_PATH, 3)  # big owners through the sort path (no key-range segments)
     store = eng.store_new(n_owners)
     store.ingest(eng.dev(ts_a), eng.dev(own_a), 0)
     before = _snapshot(store)
@@ -47,6 +48,7 @@ def test_split_ingest_rolls_back_on_phase2_failure(eng):
     eng.set_option(L.OPT_TEST_FAIL, 1)
     _, st = store.ingest(eng.dev(ts_b), eng.dev(own_b), len(ts_a), flags=flags, raise_on_error=False)
     eng.set_option(L.OPT_TEST_FAIL, 0)
+    eng.set_option(L.OPT_SERVER_PATH, 0)
     assert st == L.EVM_ENOMEM
     after = _snapshot(store)
     for x, y in zip(before, after):

@@ -1,0 +1,103 @@
+"""Key-range segments of big owners (evm_server.hip k_seg_*): an owner whose
+share of a batch exceeds the LDS capacity (4,096) is cut at sampled minute
+splitters into segments that each fit the per-owner LDS kernels.  Checked
+bit for bit against the global sort path (EVM_OPT_SERVER_PATH 2) and the
+unsegmented LDS path (3: big owners through the sort path) -- flags, stored
+rows in (owner, timestamp) order, every leaf -- over two ingests (the second
+against a non-empty store, whose rows and leaves the segments must each copy
+exactly once), on Zipf-skewed, bursty and mixed-key-length batches."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import evolu_oracle as O
+from tests import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from evolu_amd.engine import Engine
+
+    e = Engine(0)
+    yield e
+    e.set_option(2, 0)
+    e.close()
+
+
+def _run(eng, path, n_owners, ts_np, owner_np, cut):
+    from evolu_amd import _lib as L
+
+    eng.set_option(L.OPT_SERVER_PATH, path)
+    store = eng.store_new(n_owners)
+    fl = []
+    for a, b in ((0, cut), (cut, len(ts_np))):
+        f, st = store.ingest(eng.dev(ts_np[a:b]), eng.dev(owner_np[a:b]), a)
+        assert st == L.EVM_OK
+        fl.append(f.cpu().numpy().copy())
+    off, ids = store.messages()
+    toff, code, xr = store.tree().leaves()
+    store.free()
+    eng.set_option(L.OPT_SERVER_PATH, 0)
+    return np.concatenate(fl), off, ids, toff, code, xr
+
+
+def _same(a, b):
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("n_owners,n,seed", [(200, 600_000, 1), (2000, 2_000_000, 2), (5, 300_000, 3)])
+def test_zipf_segments_vs_sort_path(eng, n_owners, n, seed):
+    from evolu_amd import synth
+
+    ts_np, owner_np, _ = synth.config5(n_owners, n, seed_config=60 + seed)
+    assert np.bincount(owner_np).max() > 4096
+    cut = len(ts_np) * 3 // 5
+    seg = _run(eng, 0, n_owners, ts_np, owner_np, cut)
+    _same(seg, _run(eng, 2, n_owners, ts_np, owner_np, cut))
+    _same(seg, _run(eng, 3, n_owners, ts_np, owner_np, cut))
+
+
+def test_burst_minute_overflows_to_sort_path(eng):
+    """A big owner with 6,000 messages in one minute: that segment cannot fit,
+    so the owner goes to the sort path while the other owners' segments commit."""
+    rng = random.Random(5)
+    strings, owner = [], []
+    nodes = [W.node_id(rng) for _ in range(8)]
+    burst = [O.timestamp_to_string(W.T0 + 120_000 + rng.randrange(60_000), rng.randrange(3), rng.choice(nodes))
+             for _ in range(6000)]
+    spread = W.hlc_timestamps(rng, 9000, nodes, span=3 * 86_400_000)
+    for o, ms in ((0, burst + spread), (1, W.hlc_timestamps(rng, 8000, nodes[:3], span=86_400_000)),
+                  (2, W.hlc_timestamps(rng, 500, nodes[:2]))):
+        ms = ms + ms[:100]  # redeliveries
+        strings += ms
+        owner += [o] * len(ms)
+    perm = list(range(len(strings)))
+    rng.shuffle(perm)
+    strings = [strings[i] for i in perm]
+    owner_np = np.array([owner[i] for i in perm], dtype=np.uint32)
+    ts_np = eng.timestamps(strings).cpu().numpy()
+    cut = len(strings) // 2
+    seg = _run(eng, 0, 3, ts_np, owner_np, cut)
+    _same(seg, _run(eng, 2, 3, ts_np, owner_np, cut))
+
+
+def test_mixed_key_lengths_disable_segments(eng):
+    """A batch whose minutes have base-3 keys of two lengths (a 1990 timestamp)
+    is not segmented (code order != minute order across lengths): big owners
+    take the sort path, results unchanged."""
+    rng = random.Random(6)
+    nodes = [W.node_id(rng) for _ in range(4)]
+    ms = W.hlc_timestamps(rng, 9000, nodes, span=86_400_000)
+    old = [O.timestamp_to_string(631_152_000_000 + k * 61_000, 0, nodes[0]) for k in range(30)]  # 1990
+    strings = ms + old + ms[:50]
+    rng.shuffle(strings)
+    owner_np = np.zeros(len(strings), dtype=np.uint32)
+    owner_np[::7] = 1
+    ts_np = eng.timestamps(strings).cpu().numpy()
+    cut = len(strings) // 3
+    seg = _run(eng, 0, 2, ts_np, owner_np, cut)
+    _same(seg, _run(eng, 2, 2, ts_np, owner_np, cut))

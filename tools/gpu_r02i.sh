@@ -1,0 +1,16 @@
+#!/bin/bash
+# server segments: tests + zipf bench
+mkdir -p gpurun_out
+fatal() { case "$1" in 124|134|137|139) return 0 ;; *) return 1 ;; esac; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_server_segments.py tests/test_gpu_server.py tests/test_gpu_adversarial.py -x -q \
+  --timeout 200 --timeout-method thread > gpurun_out/pytest_i.log 2>&1
+rc=$?
+echo "tests rc=$rc"; tail -5 gpurun_out/pytest_i.log
+if fatal $rc; then exit $rc; fi
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u bench.py --workload server --zipf 1.2 --steps 5 --warmup 2 --cpu-seconds 0 \
+  > gpurun_out/bench_z.json 2> gpurun_out/bench_z.err
+rc=$?
+echo "bench zipf rc=$rc"; python3 -c "
+import json;d=json.load(open('gpurun_out/bench_z.json'));print(d['ms_per_step'], d['value']/1e9, d['roofline']['kernel'], d['roofline']['frac']); print(list(d['pipeline']['kernels_ms_per_step'].items())[:16])"
+exit $rc
