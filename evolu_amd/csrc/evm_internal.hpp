@@ -289,7 +289,7 @@ int launch_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* mil
 void tree_destroy(evm_ctx* ctx, evm_tree* t);  // stream-ordered release
 
 int launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,
-                Info* info);
+                Info* info, u32* minute_out = nullptr);
 template <typename T, template <typename> class Op>
 int scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out, T* total_dev);
 template <typename K>

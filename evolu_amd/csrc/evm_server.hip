@@ -1208,7 +1208,8 @@ void store_release_arrays(evm_ctx* ctx, evm_store* s) {
 }
 
 // ------------------------------------------- key-range segments (big owners)
-constexpr u32 SEG_TARGET = 720;     // messages per segment of a cut owner (nearly all fit the 1,024 kernel)
+constexpr u32 SEG_TARGET = 560;     // messages per segment of a cut owner: minute-granular splitters and
+                                    // sampling noise keep nearly all below 1,024 (the fast kernel)
 constexpr u32 SEG_SPLIT_MIN = 1024; // shares above this are cut (the 1,024 kernel is the fast one)
 constexpr u32 SAMPLE_STRIDE = 16;   // one sampled minute per 16 messages of a cut owner
 constexpr u32 SEG_TABLE_RATIO = 64; // minute -> segment table when the splitters span <= 64 minutes per segment
@@ -1238,13 +1239,18 @@ __global__ void k_seg_plan(const u64* __restrict__ seg, u32 O, u32* __restrict__
 
 // sample q of owner o: the minute of its share's message at j * SAMPLE_STRIDE
 // (share in batch order: a spread-out sample); key (owner, minute - gmin)
-__global__ void k_seg_sample(const evm_rec* __restrict__ rec, const u32* __restrict__ perm, const u64* __restrict__ seg,
+__device__ __forceinline__ u32 minute_of(const evm_rec* rec, const u32* minute, size_t i) {
+  return minute ? minute[i] : rec[i].minute;
+}
+
+__global__ void k_seg_sample(const evm_rec* __restrict__ rec, const u32* __restrict__ minute,
+                             const u32* __restrict__ perm, const u64* __restrict__ seg,
                              const u32* __restrict__ soff, u32 O, u32 nsamp, u32 gmin, int mb,
                              u64* __restrict__ key, u32* __restrict__ val) {
   for (u32 q = blockIdx.x * blockDim.x + threadIdx.x; q < nsamp; q += gridDim.x * blockDim.x) {
     const u32 o = upper_u32(soff, O + 1, q) - 1;
     const u64 p = seg[o] + (u64)(q - soff[o]) * SAMPLE_STRIDE;
-    const u32 mnt = rec[perm[p]].minute;
+    const u32 mnt = minute_of(rec, minute, perm[p]);
     key[q] = ((u64)o << mb) | (u64)(mnt - gmin);
     val[q] = q;
   }
@@ -1292,7 +1298,8 @@ __global__ void k_seg_table(const u32* __restrict__ spoff, const u32* __restrict
 }
 
 // every message's segment: the owner's first, plus the splitters <= its minute
-__global__ void k_seg_key(const evm_rec* __restrict__ rec, const u32* __restrict__ owner, size_t n,
+__global__ void k_seg_key(const evm_rec* __restrict__ rec, const u32* __restrict__ minute,
+                          const u32* __restrict__ owner, size_t n,
                           const u32* __restrict__ bbase, const u32* __restrict__ spoff, const u32* __restrict__ sp,
                           const u32* __restrict__ toff, const u32* __restrict__ tab, u32* __restrict__ key,
                           u32* __restrict__ val) {
@@ -1301,7 +1308,7 @@ __global__ void k_seg_key(const evm_rec* __restrict__ rec, const u32* __restrict
     const u32 b0 = bbase[o], nbo = bbase[o + 1] - b0;
     u32 k = b0;
     if (nbo > 1) {
-      const u32 mnt = rec[i].minute, a = spoff[o], t0 = toff[o], tl = toff[o + 1] - t0;
+      const u32 mnt = minute_of(rec, minute, i), a = spoff[o], t0 = toff[o], tl = toff[o + 1] - t0;
       if (tl) {
         const u32 first = sp[a];
         k += mnt < first ? 0u : mnt - first >= tl ? nbo - 1 : tab[t0 + (mnt - first)];
@@ -1327,13 +1334,14 @@ __global__ void k_seg_start(const u32* __restrict__ skey, size_t n, u32 NS, u64*
 }
 
 // every 16th batch position: (owner, minute - gmin) (mb = 0: owner only)
-__global__ void k_seg_sample_all(const evm_rec* __restrict__ rec, const u32* __restrict__ owner, size_t n, u32 gmin,
-                                 int mb, u64* __restrict__ key, u32* __restrict__ val) {
+__global__ void k_seg_sample_all(const evm_rec* __restrict__ rec, const u32* __restrict__ minute,
+                                 const u32* __restrict__ owner, size_t n, u32 gmin, int mb, u64* __restrict__ key,
+                                 u32* __restrict__ val) {
   const size_t nq = (n + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE;
   for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (size_t)gridDim.x * blockDim.x) {
     const size_t i = q * SAMPLE_STRIDE;
     u64 k = (u64)owner[i] << mb;
-    if (mb) k |= (u64)(rec[i].minute - gmin);
+    if (mb) k |= (u64)(minute_of(rec, minute, i) - gmin);
     key[q] = k;
     val[q] = (u32)q;
   }
@@ -1344,7 +1352,9 @@ __global__ void k_seg_plan_est(const u32* __restrict__ soff, u32 O, int cut, u32
                                u32* __restrict__ nsp) {
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < O; o += gridDim.x * blockDim.x) {
     const u64 est = (u64)(soff[o + 1] - soff[o]) * SAMPLE_STRIDE;
-    const u32 b = cut && est > SEG_SPLIT_MIN ? (u32)((est + SEG_TARGET - 1) / SEG_TARGET) : 1u;
+    // (estimates above 3/4 of the split size are cut too: a share estimated low
+    // would otherwise exceed 1,024 and take the slower SVO_CAP kernel)
+    const u32 b = cut && est > SEG_SPLIT_MIN * 3 / 4 ? (u32)((est + SEG_TARGET - 1) / SEG_TARGET) : 1u;
     nb[o] = b;
     nsp[o] = b - 1;
   }
@@ -1419,9 +1429,9 @@ static int base3_len_host(uint32_t m) {
 // SVO_CAP or mixes key lengths: the caller takes the global sort path with
 // the same packed records.  Validity of the batch is checked here (one host
 // round trip for the whole ingest).
-int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec* rec, const u32* owner, size_t n,
-                    const u32* orig, uint64_t id_base, uint8_t* flags, Info* info, u32* perm, evm_store* ns,
-                    evm_tree** new_tree, bool* done, uint8_t* bigmask, bool* big_only) {
+int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec* rec, const u32* minute,
+                    const u32* owner, size_t n, const u32* orig, uint64_t id_base, uint8_t* flags, Info* info, u32* perm,
+                    evm_store* ns, evm_tree** new_tree, bool* done, uint8_t* bigmask, bool* big_only) {
   *done = false;
   *big_only = false;
   const u32 O = s->n_owners;
@@ -1528,7 +1538,8 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
       skey = S.alloc<u64>(nsamp);
       u32* sval = S.alloc<u32>(nsamp);
       if (!skey || !sval) return EVM_ENOMEM;
-      KLAUNCH(k_seg_sample, dim3(grid_for(nsamp, 256)), dim3(256), rec, ov, seg, soff, O, nsamp, gmin, mb, skey, sval);
+      KLAUNCH(k_seg_sample, dim3(grid_for(nsamp, 256)), dim3(256), rec, minute, ov, seg, soff, O, nsamp, gmin, mb, skey,
+              sval);
       if ((st = radix_sort_pairs<u64>(ctx, S, skey, sval, nsamp, 0, mb + obits))) return st;
     }
   } else {
@@ -1549,7 +1560,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     skey = S.alloc<u64>(nq);
     u32* sval = S.alloc<u32>(nq);
     if (!skey || !sval) return EVM_ENOMEM;
-    KLAUNCH(k_seg_sample_all, dim3(grid_for(nq, 256)), dim3(256), rec, owner, n, gmin, mb, skey, sval);
+    KLAUNCH(k_seg_sample_all, dim3(grid_for(nq, 256)), dim3(256), rec, minute, owner, n, gmin, mb, skey, sval);
     if ((st = radix_sort_pairs<u64>(ctx, S, skey, sval, nq, 0, mb + obits))) return st;
     KLAUNCH(k_seg_soff, dim3(grid_for((size_t)O + 1, 256)), dim3(256), skey, nq, O, mb, soff);
     KLAUNCH(k_seg_plan_est, dim3(grid_for(O, 256)), dim3(256), soff, O, mb > 0 ? 1 : 0, nb, nsp);
@@ -1588,7 +1599,8 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     u32* tab = S.alloc<u32>(std::max<u32>(ntab, 1));
     if (!tab) return EVM_ENOMEM;
     if (ntab) KLAUNCH(k_seg_table, dim3(grid_for(ntab, 256)), dim3(256), spoff, sp, tboff, O, ntab, tab);
-    KLAUNCH(k_seg_key, dim3(grid_for(n, 256)), dim3(256), rec, owner, n, bbase, spoff, sp, tboff, tab, bkey, bval);
+    KLAUNCH(k_seg_key, dim3(grid_for(n, 256)), dim3(256), rec, minute, owner, n, bbase, spoff, sp, tboff, tab, bkey,
+            bval);
     u32* bk = bkey;
     u32* bv = bval;
     if ((st = radix_sort_pairs<u32>(ctx, S, bk, bv, n, 0, std::max(1, ceil_log2(NS))))) return st;
@@ -1770,8 +1782,11 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
         have_rec = true;
       }
     };
+    u32* minute = nullptr;  // compact minutes (segment keys); a sub-batch reads them from the records
     if (!orig) {
-      if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info))) return st;
+      minute = S.alloc<u32>(n);
+      if (!minute) return EVM_ENOMEM;
+      if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info, minute))) return st;
       have_rec = true;
     }
     if (mode != 2 && s->n_owners > 0) {
@@ -1779,8 +1794,8 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       bool done = false, big_only = false;
       uint8_t* bigmask = (mode == 0 && !orig) ? S.alloc<uint8_t>(n) : nullptr;
       if (mode == 0 && !orig && !bigmask) return EVM_ENOMEM;
-      if ((st = ingest_by_owner(ctx, S, s, rec, own, n, orig, id_base, flags, info, perm, &ns, &new_tree, &done,
-                                bigmask, &big_only)))
+      if ((st = ingest_by_owner(ctx, S, s, rec, minute, own, n, orig, id_base, flags, info, perm, &ns, &new_tree,
+                                &done, bigmask, &big_only)))
         return st;
       if (done && big_only && !orig) {
         // the LDS path took every owner but the big ones: commit that, then
