@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <vector>
 
 #include "evm_device.hpp"
@@ -489,7 +490,8 @@ __global__ void k_run_len(const u32* __restrict__ run_start, const u32* __restri
 
 // first message position of every owner: the position of its first run
 __global__ void k_run_seg(const u32* __restrict__ run_owner_sorted, u32 R, const u32* __restrict__ run_pos, u32 O,
-                          u64* __restrict__ seg) {
+                          u64* __restrict__ seg, Info* __restrict__ info) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && R && run_owner_sorted[R - 1] >= O) atomicOr(&info->bad_aux, 1u);
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o <= O; o += gridDim.x * blockDim.x) {
     u32 a = 0, b = R;
     while (a < b) {
@@ -536,10 +538,10 @@ __global__ __launch_bounds__(256) void k_run_fill(const u32* __restrict__ run_po
 
 // --------------------------------------------- sub-batches (hybrid ingest)
 // messages whose owner's share exceeds the LDS capacity
-__global__ void k_big_mask(const evm_rec* __restrict__ rec, size_t n, const uint8_t* __restrict__ ownbig,
+__global__ void k_big_mask(const u32* __restrict__ owner, size_t n, const uint8_t* __restrict__ ownbig,
                            uint8_t* __restrict__ mask) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    mask[i] = ownbig[rec[i].aux];
+    mask[i] = ownbig[owner[i]];
 }
 
 __global__ void k_mask_u32(const uint8_t* __restrict__ mask, size_t n, u32* __restrict__ out) {
@@ -626,9 +628,10 @@ struct SvoLog2 {
 // owner's share in batch order): node ranks, batch index, hash; sort keys
 // (tc - tc_min) << PB | t, sorted by a bitonic network (8-B elements only);
 // runs of one tc (distinct nodes) are then put in node order.
-template <u32 CAP>
+template <u32 CAP, bool PARSE>
 __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
-    const evm_rec* __restrict__ rec, const u32* __restrict__ perm, SegView sv, StoreView st,
+    const evm_rec* __restrict__ rec, const uint8_t* __restrict__ ts, size_t stride, Info* __restrict__ info,
+    const u32* __restrict__ perm, SegView sv, StoreView st,
     const u64* __restrict__ t_ck, u64 id_base, uint8_t* __restrict__ flags,
     u64* __restrict__ n_tc, u64* __restrict__ n_hi, u32* __restrict__ n_lo, u64* __restrict__ n_id,
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
@@ -678,20 +681,47 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     bi[k] = t < m ? perm[a + t] : 0u;
   }
   u64 tmin = ~0ull, tmax = 0;
+  if (PARSE) {
+    // the timestamp rows themselves (no packed records): parse + murmur3 here
+    u32 bad = 0;
+    for (int k = 0; k < PER; ++k) {
+      const u32 t = threadIdx.x + k * SVO_THREADS;
+      if (t < m) {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const v4u* row = reinterpret_cast<const v4u*>(ts + (size_t)bi[k] * stride);
+        const v4u x = __builtin_nontemporal_load(row), y = __builtin_nontemporal_load(row + 1),
+                  z = __builtin_nontemporal_load(row + 2);
+        const u32 w[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w & 0xffffu};
+        const Parsed p = parse_ts46(w);
+        bad |= (p.meta & EVM_META_VALID) ? 0u : 1u;
+        u64 hi;
+        u32 lo;
+        node_ranks(p.node, p.meta & EVM_META_CASEMASK, &hi, &lo);
+        s_rh[t] = hi;
+        s_rl[t] = lo;
+        s_h[t] = p.hash;
+        tc[k] = p.tc;
+        tmin = min(tmin, p.tc);
+        tmax = max(tmax, p.tc);
+      }
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(&info->bad, 1u);  // nothing is applied: the host re-packs to flag them
+  } else {
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const u32 t = threadIdx.x + k * SVO_THREADS;
-    if (t < m) {
-      const evm_rec r = load_rec_nt(rec + bi[k]);
-      u64 hi;
-      u32 lo;
-      node_ranks(r.node, r.meta & EVM_META_CASEMASK, &hi, &lo);
-      s_rh[t] = hi;
-      s_rl[t] = lo;
-      s_h[t] = r.hash;
-      tc[k] = r.tc;
-      tmin = min(tmin, r.tc);
-      tmax = max(tmax, r.tc);
+    for (int k = 0; k < PER; ++k) {
+      const u32 t = threadIdx.x + k * SVO_THREADS;
+      if (t < m) {
+        const evm_rec r = load_rec_nt(rec + bi[k]);
+        u64 hi;
+        u32 lo;
+        node_ranks(r.node, r.meta & EVM_META_CASEMASK, &hi, &lo);
+        s_rh[t] = hi;
+        s_rl[t] = lo;
+        s_h[t] = r.hash;
+        tc[k] = r.tc;
+        tmin = min(tmin, r.tc);
+        tmax = max(tmax, r.tc);
+      }
     }
   }
   tmin = wave_min(tmin);
@@ -1431,7 +1461,16 @@ static int base3_len_host(uint32_t m) {
 // round trip for the whole ingest).
 int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec* rec, const u32* minute,
                     const u32* owner, size_t n, const u32* orig, uint64_t id_base, uint8_t* flags, Info* info, u32* perm,
-                    evm_store* ns, evm_tree** new_tree, bool* done, uint8_t* bigmask, bool* big_only) {
+                    evm_store* ns, evm_tree** new_tree, bool* done, uint8_t* bigmask, bool* big_only, const char* ts,
+                    size_t stride, const std::function<int()>& pack_now) {
+  // fused: the records are not packed yet; K5 parses the timestamp rows itself
+  // unless a step needs records or minutes (then pack_now() packs them)
+  bool fused = (bool)pack_now;
+  auto unfuse = [&]() -> int {
+    if (!fused) return EVM_OK;
+    fused = false;
+    return pack_now();
+  };
   *done = false;
   *big_only = false;
   const u32 O = s->n_owners;
@@ -1515,7 +1554,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if ((st = radix_sort_pairs<u32>(ctx, S, rk, rv, R, 0, obits))) return st;
     KLAUNCH(k_run_len, dim3(grid_for(R, 256)), dim3(256), run_start, rv, R, n, len);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, len, R, run_pos, run_pos + R))) return st;
-    KLAUNCH(k_run_seg, dim3(grid_for((size_t)O + 1, 256)), dim3(256), rk, R, run_pos, O, seg);
+    KLAUNCH(k_run_seg, dim3(grid_for((size_t)O + 1, 256)), dim3(256), rk, R, run_pos, O, seg, info);
     KLAUNCH(k_run_fill, dim3(grid_for(R, 4 * RF_RUNS, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
     // owners above SEG_SPLIT_MIN: key-range segments, splitters from every
     // 16th message of their share
@@ -1527,6 +1566,8 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     HIPR(hipMemcpyAsync(&plan[0], bbase + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipMemcpyAsync(&plan[1], soff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipMemcpyAsync(&plan[2], spoff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    if (plan[1] > 0 && (st = unfuse())) return st;  // cut owners: the splitters need the minutes
     if ((st = check_info())) return st;
     split = plan[1] > 0 && cuttable();
     if (split) {
@@ -1548,6 +1589,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     // wrong estimate costs speed only -- an overfull segment sends its owner
     // to the sort path); then ONE sort of the batch by segment, which also
     // groups the owners (no separate owner sort)
+    if ((st = unfuse())) return st;
     if ((st = check_info())) return st;
     if (cuttable()) {
       gmin = hi.minute_min;
@@ -1624,28 +1666,49 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   HIPR(hipMemsetAsync(ownbig, 0, O, ctx->stream));
   // the common share size over every segment (more workgroups per CU); larger
   // shares are listed and take the SVO_CAP kernel over just those segments
-  KLAUNCH(k_svo_a<1024>, dim3(NS), dim3(SVO_THREADS), rec, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base,
-          flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, (const u32*)nullptr,
-          mid, ownbig);
+  const uint8_t* tsb = reinterpret_cast<const uint8_t*>(ts);
+  if (fused)
+    KLAUNCH((k_svo_a<1024, true>), dim3(NS), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
+            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
+            status, orig, (const u32*)nullptr, mid, ownbig);
+  else
+    KLAUNCH((k_svo_a<1024, false>), dim3(NS), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
+            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
+            status, orig, (const u32*)nullptr, mid, ownbig);
   HIPR(hipMemcpyAsync(&hmid, mid, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
-  if (hmid)
-    KLAUNCH(k_svo_a<SVO_CAP>, dim3(hmid), dim3(SVO_THREADS), rec, kperm, sv, view_of(s), (const u64*)t->ck,
-            (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves, status, orig,
-            (const u32*)(mid + 1), (u32*)nullptr, ownbig);
+  if (hmid && fused)
+    KLAUNCH((k_svo_a<SVO_CAP, true>), dim3(hmid), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
+            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
+            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig);
+  else if (hmid)
+    KLAUNCH((k_svo_a<SVO_CAP, false>), dim3(hmid), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
+            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
+            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig);
   KLAUNCH(k_seg_fix, dim3(grid_for(NS, 256)), dim3(256), sv, NS, ownbig, c_rows, c_new, c_leaves);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, NS, pos, tot))) return st;
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, NS, pos + NS, tot + 1))) return st;
   HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipMemcpyAsync(ht, tot, sizeof(ht), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
-  if (hs.fallback) return EVM_OK;  // the sort path redoes every flag
+  if (fused) {
+    // the parse's verdict: a row outside the native domain -> pack to flag the culprits
+    if ((st = read_info(ctx, info, &hi))) return st;
+    if (hi.bad) {
+      if ((st = unfuse())) return st;
+      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
+      (void)evm_sync(ctx);
+      return EVM_ENONCANON;
+    }
+  }
+  if (hs.fallback) return unfuse();  // the sort path redoes every flag (from packed records)
+  if (hs.big && bigmask && (st = unfuse())) return st;  // the big owners' sub-batch reads packed records
   if (hs.big) {
     if (!bigmask) return EVM_OK;
     // only some owners are too big for LDS: the rest commit here (the big
     // ones contribute no rows or leaves), the caller sends the big owners'
     // messages through the sort path
-    KLAUNCH(k_big_mask, dim3(grid_for(n, 256)), dim3(256), rec, n, ownbig, bigmask);
+    KLAUNCH(k_big_mask, dim3(grid_for(n, 256)), dim3(256), owner, n, ownbig, bigmask);
     *big_only = true;
   }
   // new store and tree, exactly sized
@@ -1776,18 +1839,31 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     u32* own_sub = orig ? S.alloc<u32>(n) : nullptr;
     if (orig && !own_sub) return EVM_ENOMEM;
     auto materialize = [&]() {
-      if (!have_rec) {
+      if (!have_rec && orig) {
         KLAUNCH(k_sv_rec_sel, dim3(grid_for(n, 256, 8192)), dim3(256), prec, orig, n, rec, own_sub);
         own = own_sub;
         have_rec = true;
       }
     };
     u32* minute = nullptr;  // compact minutes (segment keys); a sub-batch reads them from the records
+    // the per-owner path parses 16-B aligned rows itself; the records are
+    // packed only when a step needs them (cut owners, sort path, culprits)
+    const bool defer = !orig && mode == 0 && s->n_owners > 0 && stride >= 48 && stride % 16 == 0 &&
+                       ((uintptr_t)ts & 15) == 0 && ctx->server_path != 3;
+    std::function<int()> pack_now;
     if (!orig) {
       minute = S.alloc<u32>(n);
       if (!minute) return EVM_ENOMEM;
-      if ((st = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info, minute))) return st;
-      have_rec = true;
+      auto do_pack = [&, minute]() -> int {
+        int e = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info, minute);
+        if (!e) have_rec = true;
+        return e;
+      };
+      if (defer) {
+        pack_now = do_pack;
+      } else if ((st = do_pack())) {
+        return st;
+      }
     }
     if (mode != 2 && s->n_owners > 0) {
       materialize();
@@ -1795,7 +1871,7 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       uint8_t* bigmask = (mode == 0 && !orig) ? S.alloc<uint8_t>(n) : nullptr;
       if (mode == 0 && !orig && !bigmask) return EVM_ENOMEM;
       if ((st = ingest_by_owner(ctx, S, s, rec, minute, own, n, orig, id_base, flags, info, perm, &ns, &new_tree,
-                                &done, bigmask, &big_only)))
+                                &done, bigmask, &big_only, ts, stride, pack_now)))
         return st;
       if (done && big_only && !orig) {
         // the LDS path took every owner but the big ones: commit that, then
@@ -1831,6 +1907,7 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       }
       if (done) goto commit;
     }
+    if (!have_rec && pack_now && (st = pack_now())) return st;  // the sort path reads packed records
     FieldRange h0;
     for (int f = 0; f < N_FIELDS; ++f) {
       h0.mn[f] = ~0ull;
