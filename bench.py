@@ -260,7 +260,30 @@ def traffic_of(path, kernel):
     return t["bytes"] if isinstance(t, dict) else t  # HBM bytes per launch (PMC, corrected)
 
 
+_STDOUT = None  # the real stdout: the one JSON line goes there, everything else to stderr
+
+
+def quiet_stdout():
+    """Libraries print banners on the C-level stdout (RCCL's version lines at
+    communicator creation): route fd 1 to stderr for the whole run and keep
+    the real stdout for the result line only."""
+    global _STDOUT
+    sys.stdout.flush()
+    _STDOUT = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit(obj):
+    line = (json.dumps(obj) + "\n").encode()
+    if _STDOUT is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_STDOUT, line)
+
+
 def main():
+    quiet_stdout()
     a = parse()
     import numpy as np
     import torch
@@ -279,7 +302,7 @@ def main():
     if a.workload == "server":
         out = server_run(a, rank, world, local, a.owners, a.per_owner, a.zipf, a.request, cpu=rank == 0 and world == 1)
         if rank == 0:
-            print(json.dumps(out), flush=True)
+            emit(out)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -287,7 +310,7 @@ def main():
     if shape == "config4c":
         out = client_routed(a, rank, world, local)
         if rank == 0:
-            print(json.dumps(out), flush=True)
+            emit(out)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -432,17 +455,17 @@ def main():
             eng.close()
             torch.cuda.empty_cache()
             out["config3"] = server_run(a, 0, 1, local, 100_000, 1000, 0.0, 1000, cpu=a.cpu_seconds > 0, leg=True)
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
 
 XGMI_LINK = 153e9  # B/s per xGMI link (one link per peer in an 8-GPU node)
-ROUTE_BYTES = 64  # wire record per routed message (evm_dist.hip: 48-B timestamp row + owner, cell, index)
+ROUTE_BYTES = 32  # packed wire record per routed message (evm_dist.hip: tc, node, case mask, owner, cell, index)
 DIST_ALG = {
     "(k_dist_count<MODE>)": 4,  # owner in (send side: caller's owner ids; take side: the records' owner field)
-    "(k_dist_scatter<SEND>)": 48 + 4 + 4 + 64,  # ts row + owner + cell in, record out
-    "(k_dist_scatter<RECV>)": 64 + 48 + 4 + 4,  # record in; ts row + owner + cell out
+    "(k_dist_scatter<SEND>)": 48 + 4 + 4 + 32,  # ts row + owner + cell in, packed record out
+    "(k_dist_scatter<RECV>)": 32 + 48 + 4 + 4,  # packed record in; rebuilt ts row + owner + cell out
 }
 
 

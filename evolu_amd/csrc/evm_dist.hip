@@ -94,27 +94,88 @@ constexpr int DT = 256;               // threads per partition block
 constexpr int DROUNDS = 16;           // rows per thread per block
 constexpr u32 DTILE = DT * DROUNDS;   // rows per block
 constexpr u32 MAX_BUCKETS = 64;
-constexpr size_t META = 16;           // owner u32, aux u32, source index u32, pad
+constexpr size_t META = 16;           // raw records: owner u32, aux u32, source index u32, pad
+constexpr size_t PACKED = 32;         // packed records (48-B timestamp rows): tc, node, owner, aux, index, case|valid
+constexpr u32 PK_VALID = 1u << 16;
 constexpr u32 CNT_WORDS = 4 * MAX_BUCKETS;
 constexpr u32 CNT_BAD = CNT_WORDS - 1;
 
 // bucket of row i: SEND (caller arrays) -> destination rank; RECV (wire
-// records) -> local owner (owner / world)
+// records, owner at byte `ooff`) -> local owner (owner / world)
 enum { SEND = 0, RECV = 1 };
 
 template <int MODE>
 __device__ __forceinline__ u32 bucket_of(size_t i, const u32* owner, const uint8_t* dest, const char* rec, size_t rb,
-                                         size_t stride, u32 world) {
+                                         size_t ooff, u32 world) {
   if (MODE == SEND) return dest ? (u32)dest[i] : owner[i] % world;
-  const u32 o = *reinterpret_cast<const u32*>(rec + i * rb + stride);
+  const u32 o = *reinterpret_cast<const u32*>(rec + i * rb + ooff);
   return o / world;
+}
+
+// Packed wire form of a 48-B timestamp row: the parsed (tc, node, case mask)
+// -- 16 B instead of 46 -- from which the receiver rebuilds the identical
+// string (a canonical timestamp is a function of them, timestamp.ts:43-55).
+// A row outside the native domain travels as "invalid" and is rebuilt as
+// 0xFF bytes, which the engine rejects exactly like the original.
+__device__ __forceinline__ void put_byte(u32 (&w)[12], int i, u32 c) { w[i >> 2] |= (c & 0xffu) << (8 * (i & 3)); }
+__device__ __forceinline__ void put_dec(u32 (&w)[12], int at, u32 v, int digits) {
+  for (int k = digits - 1; k >= 0; --k) {
+    put_byte(w, at + k, 0x30u + v % 10u);
+    v /= 10u;
+  }
+}
+__device__ __forceinline__ void format_ts46(u64 tc, u64 node, u32 cmask, bool valid, u32 (&w)[12]) {
+  for (int k = 0; k < 12; ++k) w[k] = 0;
+  if (!valid) {
+    for (int k = 0; k < 11; ++k) w[k] = 0xffffffffu;
+    w[11] = 0xffffu;
+    return;
+  }
+  const u64 ms = tc >> 16;
+  const u32 ctr = (u32)(tc & 0xffffu);
+  const u64 days = ms / 86400000ull;
+  const u32 rem = (u32)(ms - days * 86400000ull);
+  // civil date of a day count (proleptic Gregorian, days since 1970-01-01)
+  const u64 z = days + 719468ull;
+  const u64 era = z / 146097ull;
+  const u32 doe = (u32)(z - era * 146097ull);
+  const u32 yoe = (doe - doe / 1460u + doe / 36524u - doe / 146096u) / 365u;
+  const u32 doy = doe - (365u * yoe + yoe / 4u - yoe / 100u);
+  const u32 mp = (5u * doy + 2u) / 153u;
+  const u32 d = doy - (153u * mp + 2u) / 5u + 1u;
+  const u32 m = mp < 10u ? mp + 3u : mp - 9u;
+  const u32 y = (u32)(yoe + era * 400ull) + (m <= 2u ? 1u : 0u);
+  put_dec(w, 0, y, 4);
+  put_byte(w, 4, '-');
+  put_dec(w, 5, m, 2);
+  put_byte(w, 7, '-');
+  put_dec(w, 8, d, 2);
+  put_byte(w, 10, 'T');
+  put_dec(w, 11, rem / 3600000u, 2);
+  put_byte(w, 13, ':');
+  put_dec(w, 14, rem / 60000u % 60u, 2);
+  put_byte(w, 16, ':');
+  put_dec(w, 17, rem / 1000u % 60u, 2);
+  put_byte(w, 19, '.');
+  put_dec(w, 20, rem % 1000u, 3);
+  put_byte(w, 23, 'Z');
+  put_byte(w, 24, '-');
+  for (int k = 0; k < 4; ++k) {
+    const u32 v = (ctr >> (12 - 4 * k)) & 15u;
+    put_byte(w, 25 + k, v < 10u ? 0x30u + v : 0x37u + v);  // upper-case hex counter
+  }
+  put_byte(w, 29, '-');
+  for (int k = 0; k < 16; ++k) {
+    const u32 v = (u32)(node >> (60 - 4 * k)) & 15u;
+    put_byte(w, 30 + k, v < 10u ? 0x30u + v : (((cmask >> k) & 1u) ? 0x37u : 0x57u) + v);
+  }
 }
 
 // per-block bucket counts, bucket-major ([b * nblocks + block]): their
 // exclusive scan is every (bucket, block)'s first output slot, stable
 template <int MODE>
 __global__ __launch_bounds__(DT) void k_dist_count(const u32* __restrict__ owner, const uint8_t* __restrict__ dest,
-                                                   const char* __restrict__ rec, size_t rb, size_t stride, size_t n,
+                                                   const char* __restrict__ rec, size_t rb, size_t ooff, size_t n,
                                                    u32 world, u32 B, u32 nblocks, u32* __restrict__ counts,
                                                    u32* __restrict__ bad) {
   __shared__ u32 c[MAX_BUCKETS];
@@ -125,7 +186,7 @@ __global__ __launch_bounds__(DT) void k_dist_count(const u32* __restrict__ owner
   for (int r = 0; r < DROUNDS; ++r) {
     const size_t i = base + (size_t)r * DT + threadIdx.x;
     if (i < n) {
-      const u32 b = bucket_of<MODE>(i, owner, dest, rec, rb, stride, world);
+      const u32 b = bucket_of<MODE>(i, owner, dest, rec, rb, ooff, world);
       if (b < B) atomicAdd(&c[b], 1u);
       else oob = true;
     }
@@ -170,7 +231,8 @@ __device__ __forceinline__ void copy_row(char* __restrict__ dst, const char* __r
 template <int MODE>
 __global__ __launch_bounds__(DT) void k_dist_scatter(
     const char* __restrict__ ts, size_t stride, const u32* __restrict__ owner, const u32* __restrict__ aux,
-    const uint8_t* __restrict__ dest, const char* __restrict__ rec, size_t rb, size_t n, u32 world, u32 B, int bits,
+    const uint8_t* __restrict__ dest, const char* __restrict__ rec, size_t rb, int packed, size_t n, u32 world, u32 B,
+    int bits,
     u32 nblocks, const u32* __restrict__ offs, char* __restrict__ out_rec, char* __restrict__ out_ts,
     size_t out_stride, u32* __restrict__ out_owner, u32* __restrict__ out_aux, u64* __restrict__ out_src,
     const u64* __restrict__ roff, u32 n_src) {
@@ -186,7 +248,7 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
     const bool ok = i < n;
     size_t pos = i;
     if (offs) {
-      const u32 b = ok ? bucket_of<MODE>(i, owner, dest, rec, rb, stride, world) : 0u;
+      const u32 b = ok ? bucket_of<MODE>(i, owner, dest, rec, rb, packed ? 16 : stride, world) : 0u;
       const bool act = ok && b < B;
       u32(*wc)[MAX_BUCKETS] = wcnt[r & 1];
       wc[wv][lane] = 0;
@@ -209,7 +271,16 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
     } else if (!ok) {
       continue;
     }
-    if (MODE == SEND) {
+    if (MODE == SEND && packed) {
+      const uint4* row = reinterpret_cast<const uint4*>(ts + i * stride);
+      const uint4 x = row[0], y = row[1], z = row[2];
+      const u32 w[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w & 0xffffu};
+      const Parsed p = parse_ts46(w);
+      uint4* dst = reinterpret_cast<uint4*>(out_rec + pos * rb);
+      dst[0] = make_uint4((u32)p.tc, (u32)(p.tc >> 32), (u32)p.node, (u32)(p.node >> 32));
+      dst[1] = make_uint4(owner[i], aux ? aux[i] : 0u, (u32)i,
+                          (p.meta & EVM_META_CASEMASK) | ((p.meta & EVM_META_VALID) ? PK_VALID : 0u));
+    } else if (MODE == SEND) {
       char* dst = out_rec + pos * rb;
       copy_row(dst, ts + i * stride, stride);
       uint4 m;
@@ -220,8 +291,21 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
       *reinterpret_cast<uint4*>(dst + stride) = m;
     } else {
       const char* src = rec + i * rb;
-      copy_row(out_ts + pos * out_stride, src, stride);
-      const uint4 m = *reinterpret_cast<const uint4*>(src + stride);
+      uint4 m;
+      if (packed) {
+        const uint4 a = reinterpret_cast<const uint4*>(src)[0];
+        m = reinterpret_cast<const uint4*>(src)[1];
+        u32 w[12];
+        format_ts46((u64)a.x | ((u64)a.y << 32), (u64)a.z | ((u64)a.w << 32), m.w & 0xffffu, (m.w & PK_VALID) != 0,
+                    w);
+        uint4* dst = reinterpret_cast<uint4*>(out_ts + pos * out_stride);
+        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+        dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
+      } else {
+        copy_row(out_ts + pos * out_stride, src, stride);
+        m = *reinterpret_cast<const uint4*>(src + stride);
+      }
       out_owner[pos] = m.x;
       if (out_aux) out_aux[pos] = m.y;
       if (out_src) {
@@ -277,6 +361,7 @@ struct evm_dist {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
   size_t stride = 48, rb = 64;
+  int packed = 0;  // the last route's records: packed (48-B rows) or raw
   char* send = nullptr;  // wire records (send side), device
   size_t send_cap = 0;   // bytes
   char* recv = nullptr;  // received records (staging for evm_dist_take)
@@ -306,13 +391,13 @@ int grow(char** p, size_t* cap, size_t want) {
 // Returns the scanned slot matrix (offs) and the bucket totals (device).
 template <int MODE>
 int partition_offsets(evm_ctx* ctx, Scratch& S, const u32* owner, const uint8_t* dest, const char* rec, size_t rb,
-                      size_t stride, size_t n, u32 world, u32 B, u32** offs_out, u32* nblocks_out, u64* totals,
+                      size_t ooff, size_t n, u32 world, u32 B, u32** offs_out, u32* nblocks_out, u64* totals,
                       u32* bad) {
   const u32 nblocks = (u32)std::max<size_t>(1, (n + DTILE - 1) / DTILE);
   u32* counts = S.alloc<u32>((size_t)B * nblocks);
   u32* offs = S.alloc<u32>((size_t)B * nblocks + 1);
   if (!counts || !offs) return EVM_ENOMEM;
-  KLAUNCH((k_dist_count<MODE>), dim3(nblocks), dim3(DT), owner, dest, rec, rb, stride, n, world, B, nblocks, counts,
+  KLAUNCH((k_dist_count<MODE>), dim3(nblocks), dim3(DT), owner, dest, rec, rb, ooff, n, world, B, nblocks, counts,
           bad);
   int st = scan_exclusive<u32, OpAdd>(ctx, S, counts, (size_t)B * nblocks, offs, offs + (size_t)B * nblocks);
   if (st) return st;
@@ -385,9 +470,12 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   if (!ctx || !d || !n_recv || stride < 46 || stride % 8 || (n && (!ts || !owner))) return EVM_EINVAL;
   if (n >= 0xffffffffull) return EVM_EINVAL;
   const u32 G = (u32)d->world;
-  const size_t rb = stride + META;
+  // 48-B rows, 16-B aligned: packed 32-B records (half the xGMI bytes); other strides travel raw
+  const int packed = stride == 48 && ((uintptr_t)ts & 15) == 0 ? 1 : 0;
+  const size_t rb = packed ? PACKED : stride + META;
   d->stride = stride;
   d->rb = rb;
+  d->packed = packed;
   Scratch S(ctx);
   u32* bad = S.alloc<u32>(1);
   if (!bad) return EVM_ENOMEM;
@@ -401,9 +489,9 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   if (n) {
     if ((st = partition_offsets<SEND>(ctx, S, owner, dest, nullptr, rb, stride, n, G, G, &offs, &nblocks, scnt, bad)))
       return st;
-    KLAUNCH((k_dist_scatter<SEND>), dim3(nblocks), dim3(DT), ts, stride, owner, aux, dest, (const char*)nullptr, rb, n,
-            G, G, ceil_log2(G), nblocks, offs, d->send, (char*)nullptr, (size_t)0, (u32*)nullptr, (u32*)nullptr,
-            (u64*)nullptr, (const u64*)nullptr, 0u);
+    KLAUNCH((k_dist_scatter<SEND>), dim3(nblocks), dim3(DT), ts, stride, owner, aux, dest, (const char*)nullptr, rb,
+            packed, n, G, G, ceil_log2(G), nblocks, offs, d->send, (char*)nullptr, (size_t)0, (u32*)nullptr,
+            (u32*)nullptr, (u64*)nullptr, (const u64*)nullptr, 0u);
   } else {
     HIPR(hipMemsetAsync(scnt, 0, G * sizeof(u64), ctx->stream));
   }
@@ -449,6 +537,7 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
   if (!ctx || !d || group > MAX_BUCKETS || (group && !group_off)) return EVM_EINVAL;
   const size_t n = d->n_recv;
   if (n && (!out_ts || !out_owner || out_stride < d->stride || out_stride % 8)) return EVM_EINVAL;
+  if (n && d->packed && (out_stride % 16 || ((uintptr_t)out_ts & 15))) return EVM_EINVAL;  // rebuilt rows: 16-B stores
   if (n > cap) return EVM_ECAPACITY;
   const u32 G = (u32)d->world;
   const u64* droff = d->cnt + 2 * MAX_BUCKETS;
@@ -456,7 +545,8 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
   if (!group) {
     if (n)
       KLAUNCH((k_dist_scatter<RECV>), dim3((u32)((n + DTILE - 1) / DTILE)), dim3(DT), (const char*)nullptr, d->stride,
-              (const u32*)nullptr, (const u32*)nullptr, (const uint8_t*)nullptr, d->recv, d->rb, n, G, 1u, 0, 1u,
+              (const u32*)nullptr, (const u32*)nullptr, (const uint8_t*)nullptr, d->recv, d->rb, d->packed, n, G, 1u, 0,
+              1u,
               (const u32*)nullptr, (char*)nullptr, out_ts, out_stride, out_owner, out_aux, (u64*)out_src, droff, G + 1);
     return hip_ok(hipGetLastError());
   }
@@ -468,11 +558,12 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
   if (n) {
     u32* offs = nullptr;
     u32 nblocks = 0;
-    int st = partition_offsets<RECV>(ctx, S, nullptr, nullptr, d->recv, d->rb, d->stride, n, G, group, &offs,
-                                     &nblocks, tot, bad);
+    int st = partition_offsets<RECV>(ctx, S, nullptr, nullptr, d->recv, d->rb, d->packed ? 16 : d->stride, n, G,
+                                     group, &offs, &nblocks, tot, bad);
     if (st) return st;
     KLAUNCH((k_dist_scatter<RECV>), dim3(nblocks), dim3(DT), (const char*)nullptr, d->stride, (const u32*)nullptr,
-            (const u32*)nullptr, (const uint8_t*)nullptr, d->recv, d->rb, n, G, group, ceil_log2(group), nblocks, offs,
+            (const u32*)nullptr, (const uint8_t*)nullptr, d->recv, d->rb, d->packed, n, G, group, ceil_log2(group),
+            nblocks, offs,
             (char*)nullptr, out_ts, out_stride, out_owner, out_aux, (u64*)out_src, droff, G + 1);
   }
   HIPR(hipMemcpyAsync(tot + MAX_BUCKETS, bad, sizeof(u32), hipMemcpyDeviceToDevice, ctx->stream));

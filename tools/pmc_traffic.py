@@ -45,6 +45,11 @@ def short(name):
     base, targs = m.group(1), m.group(2) or ""
     if base in ("k_radix_scatter", "k_radix_hist", "k_scan_down", "k_scan_reduce", "k_scan_partials"):
         return None
+    if base == "k_svo_a" and targs:
+        # KLAUNCH names the template launch by its source text: "(k_svo_a<1024, true>)"
+        args = [a.strip().rstrip("u") for a in targs[1:-1].split(",")]
+        args = ["SVO_CAP" if a == "4096" else a for a in args]
+        return "(k_svo_a<%s>)" % ", ".join(args)
     return base
 
 
