@@ -637,7 +637,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status,
     const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list,
-    uint8_t* __restrict__ ownbig) {
+    uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner) {
   constexpr int PER = CAP / SVO_THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
   constexpr u64 PMASK = CAP - 1;
@@ -924,6 +924,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
         n_hi[w] = mh[r];
         n_lo[w] = ml[r];
         n_id[w] = id_base + ob;
+        if (n_owner) n_owner[w] = o;  // (the rows are written into an empty store's own arrays)
         s_min[q] = (u32)((mt[r] >> 16) / 60000ull);  // == rec.minute on the native domain
         s_hq[q] = mhash[r];
         ++q;
@@ -991,7 +992,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     const u64* __restrict__ t_ck, const int32_t* __restrict__ t_xr, const u64* __restrict__ l_ck,
     const int32_t* __restrict__ l_xr, const uint8_t* __restrict__ l_dup, const u32* __restrict__ cnt_new,
     const u32* __restrict__ leaf_pos, StoreOut so, u64* __restrict__ so_off, u64* __restrict__ to_ck,
-    int32_t* __restrict__ to_xr, u64* __restrict__ to_off) {
+    int32_t* __restrict__ to_xr, u64* __restrict__ to_off, int rows_in_place) {
   __shared__ u32 s_dp[SVO_CAP + 1];  // exclusive prefix count of the new leaves already in the tree
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
   const u32 s = blockIdx.x;
@@ -1001,7 +1002,9 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   const u64 sa = sv.sa[s], sb = sv.sb[s];
   const u64 base = sa + row_pos[s];  // rows of the earlier segments: old + new
   // rows: the owner's stored and new keys are disjoint sorted lists
-  for (u64 k = sa + threadIdx.x; k < sb; k += SVO_THREADS) {
+  // rows_in_place: an empty store whose every message was inserted -- the
+  // K5 rows already sit at their final places (position = batch position)
+  for (u64 k = sa + threadIdx.x; !rows_in_place && k < sb; k += SVO_THREADS) {
     const SKey key = skey_at(st, k);
     u32 lo = 0, hi = M;
     while (lo < hi) {
@@ -1016,7 +1019,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     so.lo[w] = key.lo;
     so.id[w] = st_id[k];
   }
-  for (u32 j = threadIdx.x; j < M; j += SVO_THREADS) {
+  for (u32 j = threadIdx.x; !rows_in_place && j < M; j += SVO_THREADS) {
     const SKey key{o, n_tc[a + j], n_hi[a + j], n_lo[a + j]};
     const u64 w = base + j + (store_lower(st, sa, sb, key) - sa);
     so.owner[w] = o;
@@ -1659,6 +1662,27 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   u32* mid = S.alloc<u32>((size_t)NS + 1);  // [count, segments whose share is in (1024, SVO_CAP]]
   if (!cnt || !pos || !mid) return EVM_ENOMEM;
   u32 *c_rows = cnt, *c_new = cnt + NS, *c_leaves = cnt + 2 * (size_t)NS;
+  // an empty store (a new server, config 3): K5 writes its rows straight into
+  // the new store's arrays at their batch positions -- if every message is
+  // inserted that is the final layout and k_svo_b copies no row
+  u32* n_owner = nullptr;
+  evm_store pre{};
+  if (s->n == 0) {
+    if ((st = store_alloc(ctx, &pre, O, n))) {
+      store_release_arrays(ctx, &pre);
+      return st;
+    }
+    n_tc = pre.tc;
+    n_hi = pre.hi;
+    n_lo = pre.lo;
+    n_id = pre.id;
+    n_owner = pre.owner;
+  }
+  struct PreGuard {  // released on every path that does not adopt it
+    evm_ctx* ctx;
+    evm_store* p;
+    ~PreGuard() { store_release_arrays(ctx, p); }
+  } pre_guard{ctx, &pre};
   SvoStatus hs;
   u32 ht[2], hmid = 0;
   HIPR(hipMemsetAsync(status, 0, sizeof(SvoStatus), ctx->stream));
@@ -1670,21 +1694,21 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   if (fused)
     KLAUNCH((k_svo_a<1024, true>), dim3(NS), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
             (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)nullptr, mid, ownbig);
+            status, orig, (const u32*)nullptr, mid, ownbig, n_owner);
   else
     KLAUNCH((k_svo_a<1024, false>), dim3(NS), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
             (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)nullptr, mid, ownbig);
+            status, orig, (const u32*)nullptr, mid, ownbig, n_owner);
   HIPR(hipMemcpyAsync(&hmid, mid, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
   if (hmid && fused)
     KLAUNCH((k_svo_a<SVO_CAP, true>), dim3(hmid), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
             (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig);
+            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig, n_owner);
   else if (hmid)
     KLAUNCH((k_svo_a<SVO_CAP, false>), dim3(hmid), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
             (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig);
+            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig, n_owner);
   KLAUNCH(k_seg_fix, dim3(grid_for(NS, 256)), dim3(256), sv, NS, ownbig, c_rows, c_new, c_leaves);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, NS, pos, tot))) return st;
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, NS, pos + NS, tot + 1))) return st;
@@ -1712,7 +1736,12 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     *big_only = true;
   }
   // new store and tree, exactly sized
-  if ((st = store_alloc(ctx, ns, O, s->n + ht[0]))) {
+  const int in_place = (n_owner && ht[0] == n) ? 1 : 0;
+  if (in_place) {
+    *ns = pre;  // adopt the pre-allocated store (its rows are final)
+    ns->n = n;
+    pre = evm_store{};
+  } else if ((st = store_alloc(ctx, ns, O, s->n + ht[0]))) {
     store_release_arrays(ctx, ns);
     return st;
   }
@@ -1724,7 +1753,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   const StoreOut so{ns->owner, ns->tc, ns->hi, ns->lo, ns->id};
   KLAUNCH(k_svo_b, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
           c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + NS, so, ns->off, nt->ck, nt->xr,
-          nt->off);
+          nt->off, in_place);
   if ((st = scan_exclusive<int32_t, OpXor>(ctx, S, nt->xr, ht[1], nt->pfx, nt->pfx + ht[1]))) {
     store_release_arrays(ctx, ns);
     tree_destroy(ctx, nt);
