@@ -637,7 +637,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status,
     const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list,
-    uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner) {
+    uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner, int flags_preset) {
   constexpr int PER = CAP / SVO_THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
   constexpr u64 PMASK = CAP - 1;
@@ -917,7 +917,9 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     if (p < m) {
       const bool ins = (insm >> r) & 1u;
       const u32 ob = orig ? orig[mb[r]] : mb[r];  // the message's index in the caller's batch
-      flags[ob] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
+      // flags_preset: the batch's flags were set to INS by a coalesced fill;
+      // only the duplicates (the minority) need a random 1-B store
+      if (!ins || !flags_preset) flags[ob] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
       if (ins) {
         const u64 w = a + q;
         n_tc[w] = mt[r];
@@ -1685,6 +1687,8 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   } pre_guard{ctx, &pre};
   SvoStatus hs;
   u32 ht[2], hmid = 0;
+  const int preset = orig ? 0 : 1;
+  if (preset) HIPR(hipMemsetAsync(flags, EVM_MSG_INS, n, ctx->stream));
   HIPR(hipMemsetAsync(status, 0, sizeof(SvoStatus), ctx->stream));
   HIPR(hipMemsetAsync(mid, 0, sizeof(u32), ctx->stream));
   HIPR(hipMemsetAsync(ownbig, 0, O, ctx->stream));
@@ -1694,21 +1698,21 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   if (fused)
     KLAUNCH((k_svo_a<1024, true>), dim3(NS), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
             (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)nullptr, mid, ownbig, n_owner);
+            status, orig, (const u32*)nullptr, mid, ownbig, n_owner, preset);
   else
     KLAUNCH((k_svo_a<1024, false>), dim3(NS), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
             (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)nullptr, mid, ownbig, n_owner);
+            status, orig, (const u32*)nullptr, mid, ownbig, n_owner, preset);
   HIPR(hipMemcpyAsync(&hmid, mid, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
   if (hmid && fused)
     KLAUNCH((k_svo_a<SVO_CAP, true>), dim3(hmid), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
             (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig, n_owner);
+            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig, n_owner, preset);
   else if (hmid)
     KLAUNCH((k_svo_a<SVO_CAP, false>), dim3(hmid), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
             (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig, n_owner);
+            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig, n_owner, preset);
   KLAUNCH(k_seg_fix, dim3(grid_for(NS, 256)), dim3(256), sv, NS, ownbig, c_rows, c_new, c_leaves);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, NS, pos, tot))) return st;
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, NS, pos + NS, tot + 1))) return st;
