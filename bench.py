@@ -85,6 +85,7 @@ def parse():
     ap.add_argument("--cells", type=int, default=1000)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget per leg (0: skip)")
     ap.add_argument("--overlap", type=int, default=1, help="EVM_OPT_OVERLAP: independent checks on a second stream")
+    ap.add_argument("--depth", type=int, default=4, help="config 2: batches in flight (evm_apply_batch_async)")
     ap.add_argument("--workload", choices=["client", "server"], default="client",
                     help="client: config 2 applyMessages (headline, + config 1 and 3 legs at N=1); "
                          "server: config 3/4/5 ingest + diff + select alone")
@@ -323,7 +324,7 @@ def main():
     empty = eng.tree_new(1)
     # two output sets: batch k + 1 is enqueued (evm_apply_batch_async) before
     # batch k is waited, so the host's launches and status read overlap the GPU
-    DEPTH = 3  # batches enqueued ahead of the one being waited
+    DEPTH = max(1, a.depth)  # batches enqueued ahead of the one being waited
     outs = [(torch.empty(a.messages, dtype=torch.uint8, device=ts.device),
              torch.empty(a.cells, dtype=torch.int32, device=ts.device)) for _ in range(DEPTH)]
     flags, winner = outs[0]
