@@ -61,10 +61,14 @@ ALG_BYTES_PER_MSG = {
 # Server path (evm_server.hip), per message N and per new leaf L
 SERVER_ALG = {
     "k_pack48": (46 + 4 + 32 + 4, 0),  # ts + owner in, 32-B record + minute out (only when records are needed)
+    "k_minute48": (46 + 4 + 4, 0),  # ts + owner in, minute out (segment keys when K5 parses the rows)
     # per-owner ingest parsing the timestamp rows itself (requests of one owner, no owner above 1,024)
     "(k_svo_a<1024, true>)": (4 + 46 + 1 + 28, 8 + 4 + 1),  # perm + ts row in; flag + new row out; leaf code/xor/dup out
     # the same over packed records (interleaved owners / key-range segments)
     "(k_svo_a<1024, false>)": (4 + 32 + 1 + 28, 8 + 4 + 1),  # perm + record in; flag + new row out; leaf out
+    # the same with 512-message capacity (first pass when the typical segment is small: Zipf tails)
+    "(k_svo_a<512, true>)": (4 + 46 + 1 + 28, 8 + 4 + 1),
+    "(k_svo_a<512, false>)": (4 + 32 + 1 + 28, 8 + 4 + 1),
     "k_svo_b": (28 + 32, 8 + 4 + 1 + 8 + 4),  # new rows in, store rows out; new leaves in, tree leaves out
     "k_seg_key": (4 + 4 + 8, 0),  # owner + minute in, (segment, index) out
 }

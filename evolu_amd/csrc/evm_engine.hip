@@ -74,10 +74,12 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack(const uint8_t* __restrict
 // The same for 16-B aligned 48-byte rows: a wave reads its 64 rows as three
 // coalesced (non-temporal) 16-B loads per lane and redistributes them through
 // LDS, as the client path's K1 does (evm_pack.hpp).
-__global__ __launch_bounds__(PACK_THREADS) void k_pack48(const uint8_t* __restrict__ ts, size_t n,
-                                                         const u32* __restrict__ aux, u32 aux_limit,
-                                                         evm_rec* __restrict__ out, Info* __restrict__ info,
-                                                         u32* __restrict__ minute_out) {
+// REC = false: the minutes and the checks only (the server's segment keys
+// when K5 parses the rows itself).
+template <bool REC>
+__device__ __forceinline__ void pack48_body(const uint8_t* __restrict__ ts, size_t n, const u32* __restrict__ aux,
+                                            u32 aux_limit, evm_rec* __restrict__ out, Info* __restrict__ info,
+                                            u32* __restrict__ minute_out) {
   __shared__ uint4 stage[PACK_THREADS / 64][192];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   u32 bad = 0, bad_aux = 0, mn = 0xffffffffu, mx = 0u;
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack48(const uint8_t* __restri
     r.minute = p.minute;
     r.aux = aux ? aux[i] : 0u;
     if (aux_limit && r.aux >= aux_limit) bad_aux = 1;
-    out[i] = r;  // (staging the records through LDS for 1-KiB stores measured slower: 1.92 vs 1.68 ms)
+    if (REC) out[i] = r;  // (staging the records through LDS for 1-KiB stores measured slower: 1.92 vs 1.68 ms)
     if (minute_out) minute_out[i] = p.minute;  // compact copy for the server's segment keys
     if (p.meta & EVM_META_VALID) {
       mn = min(mn, p.minute);
@@ -128,6 +130,27 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack48(const uint8_t* __restri
       atomic_max_if(&info->minute_max, mx);
     }
   }
+}
+
+__global__ __launch_bounds__(PACK_THREADS) void k_pack48(const uint8_t* __restrict__ ts, size_t n,
+                                                         const u32* __restrict__ aux, u32 aux_limit,
+                                                         evm_rec* __restrict__ out, Info* __restrict__ info,
+                                                         u32* __restrict__ minute_out) {
+  pack48_body<true>(ts, n, aux, aux_limit, out, info, minute_out);
+}
+__global__ __launch_bounds__(PACK_THREADS) void k_minute48(const uint8_t* __restrict__ ts, size_t n,
+                                                           const u32* __restrict__ aux, u32 aux_limit,
+                                                           Info* __restrict__ info, u32* __restrict__ minute_out) {
+  pack48_body<false>(ts, n, aux, aux_limit, nullptr, info, minute_out);
+}
+
+int evm::launch_minutes(evm_ctx* ctx, const char* ts, size_t n, const u32* aux, u32 aux_limit, Info* info,
+                        u32* minute_out) {
+  if (n == 0) return EVM_OK;
+  if (((uintptr_t)ts & 15) != 0) return EVM_EINVAL;
+  KLAUNCH(k_minute48, dim3(grid_for(n, PACK_THREADS, 2048)), dim3(PACK_THREADS), (const uint8_t*)ts, n, aux, aux_limit,
+          info, minute_out);
+  return hip_ok(hipGetLastError());
 }
 
 int evm::launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,

@@ -290,6 +290,9 @@ void tree_destroy(evm_ctx* ctx, evm_tree* t);  // stream-ordered release
 
 int launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, const u32* aux, u32 aux_limit, evm_rec* out,
                 Info* info, u32* minute_out = nullptr);
+// 48-B rows (16-B aligned): the minutes and the pack's checks, no records
+int launch_minutes(evm_ctx* ctx, const char* ts, size_t n, const u32* aux, u32 aux_limit, Info* info,
+                   u32* minute_out);
 template <typename T, template <typename> class Op>
 int scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out, T* total_dev);
 template <typename K>

@@ -621,7 +621,7 @@ __device__ __forceinline__ u32 seg_owner(const SegView& v, u32 s) { return v.own
 
 template <u32 CAP>
 struct SvoLog2 {
-  static constexpr int v = CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;
+  static constexpr int v = CAP == 512 ? 9 : CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;
 };
 
 // Phase A for owners whose share is <= CAP.  LDS by batch position t (the
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     u64* __restrict__ n_tc, u64* __restrict__ n_hi, u32* __restrict__ n_lo, u64* __restrict__ n_id,
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status,
-    const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list,
+    const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list, u32* __restrict__ mid1,
     uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner, int flags_preset) {
   constexpr int PER = CAP / SVO_THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
@@ -658,7 +658,9 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   const u64 la = sv.la[s], lb = sv.lb[s];
   if (m > CAP || m == 0) {
     if (threadIdx.x == 0) {
-      if (m <= SVO_CAP && mid_list) {
+      if (m <= 1024 && mid1) {
+        mid1[1 + atomicAdd(&mid1[0], 1u)] = s;  // for the 1,024 pass
+      } else if (m <= SVO_CAP && mid_list) {
         mid_list[1 + atomicAdd(&mid_list[0], 1u)] = s;  // for the SVO_CAP pass
       } else if (m) {
         atomicOr(&status->big, 1u);
@@ -782,17 +784,27 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
         if (t < m) s_k[s_cnt[bk[k]] + rk[k]] = ((tc[k] - tmin) << PB) | t;
       }
       __syncthreads();
-      for (u32 b = threadIdx.x; b < CAP; b += SVO_THREADS) {
-        const u32 e = b + 1 < CAP ? s_cnt[b + 1] : (u32)m;
-        for (u32 x = s_cnt[b] + 1; x < e; ++x) {
-          const u64 kx = s_k[x];
-          u32 y = x;
-          while (y > s_cnt[b] && s_k[y - 1] > kx) {
-            s_k[y] = s_k[y - 1];
-            --y;
-          }
-          s_k[y] = kx;
+      // each key's place in its bucket = the bucket's keys below it (keys are
+      // distinct: they carry the position); every key counts in parallel
+      // instead of one thread insertion-sorting a bucket
+      u32 dst[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const u32 t = threadIdx.x + k * SVO_THREADS;
+        dst[k] = 0;
+        if (t < m) {
+          const u32 b0 = s_cnt[bk[k]], b1 = bk[k] + 1 < CAP ? s_cnt[bk[k] + 1] : (u32)m;
+          const u64 key = ((tc[k] - tmin) << PB) | t;
+          u32 r = 0;
+          for (u32 x = b0; x < b1; ++x) r += s_k[x] < key ? 1u : 0u;
+          dst[k] = b0 + r;
         }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const u32 t = threadIdx.x + k * SVO_THREADS;
+        if (t < m) s_k[dst[k]] = ((tc[k] - tmin) << PB) | t;
       }
     } else {
 #pragma unroll
@@ -817,31 +829,48 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     }
   }
   __syncthreads();
-  // runs of one tc: order by the node ranks (then position), insertion sort by
-  // the thread that finds the run's start
-  for (u32 p = threadIdx.x; p + 1 < m; p += SVO_THREADS) {
-    const u64 tp = s_k[p] >> PB;
-    if (s_k[p + 1] >> PB != tp || (p > 0 && s_k[p - 1] >> PB == tp)) continue;
-    u32 e = p + 2;
-    while (e < m && s_k[e] >> PB == tp && e - p <= SVO_TIE_MAX) ++e;
-    if (e - p > SVO_TIE_MAX) {
-      atomicOr(&status->fallback, 1u);
-      continue;
-    }
-    for (u32 x = p + 1; x < e; ++x) {
-      const u64 kx = s_k[x];
-      const u32 px = (u32)(kx & PMASK);
+  // runs of one tc: order by the node ranks (then position).  Each member
+  // finds its run's bounds and counts the members below it, all in parallel
+  // (runs are short: distinct nodes at one (millis, counter))
+  {
+    constexpr int PT = (CAP + SVO_THREADS - 1) / SVO_THREADS;
+    u64 kk[PT];
+    u32 kd[PT];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const u32 p = threadIdx.x + k * SVO_THREADS;
+      kd[k] = p;
+      kk[k] = 0;
+      if (p >= m) continue;
+      const u64 kp = s_k[p];
+      kk[k] = kp;
+      const u64 tp = kp >> PB;
+      const bool lo_eq = p > 0 && s_k[p - 1] >> PB == tp, hi_eq = p + 1 < m && s_k[p + 1] >> PB == tp;
+      if (!lo_eq && !hi_eq) continue;
+      u32 b0 = p, b1 = p + 1;
+      while (b0 > 0 && s_k[b0 - 1] >> PB == tp && p - b0 < SVO_TIE_MAX) --b0;
+      while (b1 < m && s_k[b1] >> PB == tp && b1 - b0 <= SVO_TIE_MAX) ++b1;
+      if (b1 - b0 > SVO_TIE_MAX || (b0 > 0 && s_k[b0 - 1] >> PB == tp)) {
+        atomicOr(&status->fallback, 1u);
+        continue;
+      }
+      const u32 px = (u32)(kp & PMASK);
       const u64 hx = s_rh[px];
       const u32 lx = s_rl[px];
-      u32 y = x;
-      while (y > p) {
-        const u32 py = (u32)(s_k[y - 1] & PMASK);
-        const u64 hy = s_rh[py];
-        if (hy < hx || (hy == hx && s_rl[py] <= lx)) break;  // equal ranks: positions already ascending
-        s_k[y] = s_k[y - 1];
-        --y;
+      u32 r = 0;
+      for (u32 q = b0; q < b1; ++q) {
+        const u32 pq = (u32)(s_k[q] & PMASK);
+        const u64 hq = s_rh[pq];
+        const u32 lq = s_rl[pq];
+        r += (hq < hx || (hq == hx && (lq < lx || (lq == lx && pq < px)))) ? 1u : 0u;
       }
-      s_k[y] = kx;
+      kd[k] = b0 + r;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const u32 p = threadIdx.x + k * SVO_THREADS;
+      if (p < m && kd[k] != p) s_k[kd[k]] = kk[k];
     }
   }
   __syncthreads();
@@ -1476,6 +1505,15 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     fused = false;
     return pack_now();
   };
+  // the segment keys need only the minutes: 48-B rows get them (and the
+  // pack's checks) without the 32-B records, which K5 then does not read
+  bool have_min = false;
+  auto minutes = [&]() -> int {
+    if (!fused || have_min) return EVM_OK;
+    if (stride != 48) return unfuse();
+    have_min = true;
+    return launch_minutes(ctx, ts, n, owner, s->n_owners, info, const_cast<u32*>(minute));
+  };
   *done = false;
   *big_only = false;
   const u32 O = s->n_owners;
@@ -1517,6 +1555,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if (e) return e;
     if (hi.bad_aux) return EVM_EINVAL;
     if (hi.bad) {
+      if ((e = unfuse())) return e;  // the culprits are flagged from packed records
       KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
       (void)evm_sync(ctx);
       return EVM_ENONCANON;
@@ -1572,7 +1611,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     HIPR(hipMemcpyAsync(&plan[1], soff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipMemcpyAsync(&plan[2], spoff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipStreamSynchronize(ctx->stream));
-    if (plan[1] > 0 && (st = unfuse())) return st;  // cut owners: the splitters need the minutes
+    if (plan[1] > 0 && (st = minutes())) return st;  // cut owners: the splitters need the minutes
     if ((st = check_info())) return st;
     split = plan[1] > 0 && cuttable();
     if (split) {
@@ -1594,7 +1633,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     // wrong estimate costs speed only -- an overfull segment sends its owner
     // to the sort path); then ONE sort of the batch by segment, which also
     // groups the owners (no separate owner sort)
-    if ((st = unfuse())) return st;
+    if ((st = minutes())) return st;
     if ((st = check_info())) return st;
     if (cuttable()) {
       gmin = hi.minute_min;
@@ -1695,24 +1734,33 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   // the common share size over every segment (more workgroups per CU); larger
   // shares are listed and take the SVO_CAP kernel over just those segments
   const uint8_t* tsb = reinterpret_cast<const uint8_t*>(ts);
-  if (fused)
-    KLAUNCH((k_svo_a<1024, true>), dim3(NS), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
-            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)nullptr, mid, ownbig, n_owner, preset);
-  else
-    KLAUNCH((k_svo_a<1024, false>), dim3(NS), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
-            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)nullptr, mid, ownbig, n_owner, preset);
+  // pass A over every segment with the capacity that fits the typical share
+  // (small segments -- Zipf tails, cut owners -- take the 512 kernel: half the
+  // per-workgroup fixed work, twice the occupancy); larger shares are listed
+  // for the 1,024 and SVO_CAP passes
+  u32* mid1 = S.alloc<u32>((size_t)NS + 1);
+  if (!mid1) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(mid1, 0, sizeof(u32), ctx->stream));
+  const bool small = NS && n / NS < 400;
+  auto pass = [&](u32 cap, dim3 grid, const u32* list, u32* l1, u32* l2) {
+#define SVO_ARGS                                                                                                      \
+  rec, tsb, stride, info, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, \
+      l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, list, l2, l1, ownbig, n_owner, preset
+    if (cap == 512 && fused) KLAUNCH((k_svo_a<512, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
+    else if (cap == 512) KLAUNCH((k_svo_a<512, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
+    else if (cap == 1024 && fused) KLAUNCH((k_svo_a<1024, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
+    else if (cap == 1024) KLAUNCH((k_svo_a<1024, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
+    else if (fused) KLAUNCH((k_svo_a<SVO_CAP, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
+    else KLAUNCH((k_svo_a<SVO_CAP, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
+#undef SVO_ARGS
+  };
+  pass(small ? 512 : 1024, dim3(NS), (const u32*)nullptr, small ? mid1 : (u32*)nullptr, mid);
+  u32 hm1 = 0;
   HIPR(hipMemcpyAsync(&hmid, mid, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipMemcpyAsync(&hm1, mid1, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
-  if (hmid && fused)
-    KLAUNCH((k_svo_a<SVO_CAP, true>), dim3(hmid), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
-            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig, n_owner, preset);
-  else if (hmid)
-    KLAUNCH((k_svo_a<SVO_CAP, false>), dim3(hmid), dim3(SVO_THREADS), rec, tsb, stride, info, kperm, sv, view_of(s),
-            (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, l_xr, l_dup, c_rows, c_new, c_leaves,
-            status, orig, (const u32*)(mid + 1), (u32*)nullptr, ownbig, n_owner, preset);
+  if (hm1) pass(1024, dim3(hm1), (const u32*)(mid1 + 1), (u32*)nullptr, (u32*)nullptr);
+  if (hmid) pass(SVO_CAP, dim3(hmid), (const u32*)(mid + 1), (u32*)nullptr, (u32*)nullptr);
   KLAUNCH(k_seg_fix, dim3(grid_for(NS, 256)), dim3(256), sv, NS, ownbig, c_rows, c_new, c_leaves);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, NS, pos, tot))) return st;
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, NS, pos + NS, tot + 1))) return st;
