@@ -201,3 +201,38 @@ def test_collision_detected_at_scale(eng):
     cell_np = np.concatenate([cell_np, (cell_np[123456:123457] + 1) % 1000])
     _, _, _, st = eng.apply_batch(eng.tree_new(1), eng.dev(ts_np), eng.dev(cell_np), 1000, raise_on_error=False)
     assert st == L.EVM_ECOLLISION
+
+
+@pytest.mark.parametrize("copies", [2, 7, 30, 60])
+def test_cross_cell_check_hash_classes(eng, copies):
+    """The partitioned cross-cell check settles one pair of a hash class per
+    round: a timestamp redelivered `copies` times in one cell is no collision
+    (the result equals the sort path's); one more copy in another cell, placed
+    last, is found whatever the class size (above XP_MAX_ROUNDS the exact
+    global check takes over)."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    ts_np, cell_np = synth.config2(200_000, 1000, seed_config=11)
+    rng = np.random.default_rng(copies)
+    picks = rng.integers(0, len(ts_np), size=5)
+    extra_ts = np.concatenate([np.repeat(ts_np[p:p + 1], copies, axis=0) for p in picks])
+    extra_cell = np.concatenate([np.repeat(cell_np[p:p + 1], copies) for p in picks])
+    ts2 = np.concatenate([ts_np, extra_ts])
+    cell2 = np.concatenate([cell_np, extra_cell])
+    perm = rng.permutation(len(ts2))
+    ts2, cell2 = ts2[perm], cell2[perm]
+    res = []
+    for path in (1, 2):
+        eng.set_option(L.OPT_CLIENT_PATH, path)
+        flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), eng.dev(ts2), eng.dev(cell2), 1000)
+        off, code, xr = tree.leaves()
+        res.append((flags.cpu().numpy(), winner.cpu().numpy(), code, xr))
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)
+    # one copy of the last class in another cell: a collision
+    ts3 = np.concatenate([ts2, ts_np[picks[-1]:picks[-1] + 1]])
+    cell3 = np.concatenate([cell2, (cell_np[picks[-1]:picks[-1] + 1] + 1) % 1000])
+    _, _, _, st = eng.apply_batch(eng.tree_new(1), eng.dev(ts3), eng.dev(cell3), 1000, raise_on_error=False)
+    assert st == L.EVM_ECOLLISION
