@@ -324,7 +324,7 @@ __device__ __forceinline__ void load_ts(const uint8_t* __restrict__ base, size_t
 // ----------------------------------------------------------------------------
 constexpr int CODE_DIGITS = 20;  // 3^20 > 2^31 > every native minute
 
-__device__ __forceinline__ int base3_len(u32 m) {
+__host__ __device__ __forceinline__ int base3_len(u32 m) {
   int L = 1;
   u64 p = 3;
   while (L < CODE_DIGITS && (u64)m >= p) {
@@ -334,7 +334,42 @@ __device__ __forceinline__ int base3_len(u32 m) {
   return L;
 }
 
-__device__ __forceinline__ u64 minute_code(u32 m) {
+// The five base-3 digits of x < 243 as 2-bit fields, most significant first:
+// f = x / 243 in 16-bit fixed point, rounded up (270 > 2^16 / 243; the error
+// after k steps, < 3^k * 0.0012, stays below the 3^(k-5) gap), then each
+// digit is the integer part of f * 3.
+__host__ __device__ __forceinline__ u32 b3_raw5(u32 x) {
+  u32 f = x * 270u, r = 0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    f *= 3u;
+    r = (r << 2) | (f >> 16);
+    f &= 0xffffu;
+  }
+  return r;
+}
+
+// code of minute m from its 20 raw base-3 digits (R(x): the five digits of
+// x < 243, from a table or b3_raw5): the L significant digits + 1 each, the
+// most significant at the top digit (== the digit loop below, ~8x fewer
+// instructions: three divisions instead of twenty, no 64-bit multiply).
+template <typename R>
+__host__ __device__ __forceinline__ u64 minute_code_from(u32 m, R raw5) {
+  const u32 q1 = m / 59049u, r1 = m - q1 * 59049u;  // 3^10
+  const u32 a = q1 / 243u, b = q1 - a * 243u, c = r1 / 243u, d = r1 - c * 243u;
+  const u64 raw = ((u64)((raw5(a) << 10) | raw5(b)) << 20) | (u64)((raw5(c) << 10) | raw5(d));
+  const int top = raw ? 63 - __builtin_clzll(raw) : 0;  // highest set bit
+  const int L = top / 2 + 1;                            // significant digits (m == 0: one)
+  const u64 ones = 0x5555555555ull >> (2 * (CODE_DIGITS - L));
+  return (raw + ones) << (2 * (CODE_DIGITS - L));
+}
+
+__host__ __device__ __forceinline__ u64 minute_code(u32 m) {
+  return minute_code_from(m, [](u32 x) { return b3_raw5(x); });
+}
+
+// The reference digit loop (tests check minute_code against it).
+__host__ __device__ __forceinline__ u64 minute_code_loop(u32 m) {
   const int L = base3_len(m);
   u64 code = 0;
   // digits least significant first

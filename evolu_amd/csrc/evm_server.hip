@@ -650,6 +650,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   __shared__ u32 s_cnt[CAP];  // counting sort: bucket counts, then starts
   __shared__ u64 s_red[2 * (SVO_THREADS / 64)];
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
+  __shared__ uint16_t s_b3[243];  // base-3 digits of 0..242 (the leaves' key codes)
   const u32 s = list ? list[blockIdx.x] : blockIdx.x;  // pass 2: only the segments pass 1 deferred
   const u32 o = seg_owner(sv, s);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -672,6 +673,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     }
     return;
   }
+  if (threadIdx.x < 243) s_b3[threadIdx.x] = (uint16_t)b3_raw5(threadIdx.x);  // (read after many barriers)
   u32 P = 1;
   while (P < m) P <<= 1;
   // gather: all batch indices, then all records (independent loads in flight)
@@ -696,11 +698,8 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
         const u32 w[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w & 0xffffu};
         const Parsed p = parse_ts46(w);
         bad |= (p.meta & EVM_META_VALID) ? 0u : 1u;
-        u64 hi;
-        u32 lo;
-        node_ranks(p.node, p.meta & EVM_META_CASEMASK, &hi, &lo);
-        s_rh[t] = hi;
-        s_rl[t] = lo;
+        s_rh[t] = p.rh;  // (== node_ranks(p.node, case mask): the parse's SWAR ranks)
+        s_rl[t] = p.rl;
         s_h[t] = p.hash;
         tc[k] = p.tc;
         tmin = min(tmin, p.tc);
@@ -933,6 +932,10 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
       }
     }
   }
+  // minute = millis / 60000: one 64-bit division per segment, then 32-bit
+  // divisions of the offsets from a whole-minute base (spans < 2^32 ms)
+  const u64 base_min = (tmin >> 16) / 60000ull, base_ms = base_min * 60000ull;
+  const bool narrow = ((tmax >> 16) - base_ms) >> 32 == 0;
   u32 M;
   u32 q = block_inclusive_scan<u32>(c, tmp, OpAdd<u32>(), &M) - c;  // (its barriers free the LDS arrays)
   u32* s_min = reinterpret_cast<u32*>(s_k);  // inserted rows, sorted: minute
@@ -956,7 +959,8 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
         n_lo[w] = ml[r];
         n_id[w] = id_base + ob;
         if (n_owner) n_owner[w] = o;  // (the rows are written into an empty store's own arrays)
-        s_min[q] = (u32)((mt[r] >> 16) / 60000ull);  // == rec.minute on the native domain
+        s_min[q] = narrow ? (u32)base_min + (u32)((mt[r] >> 16) - base_ms) / 60000u
+                          : (u32)((mt[r] >> 16) / 60000ull);  // == rec.minute on the native domain
         s_hq[q] = mhash[r];
         ++q;
       }
@@ -987,7 +991,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   if (threadIdx.x == 0 && NL && base3_len(s_lm[0]) != base3_len(s_lm[NL - 1])) atomicOr(&status->fallback, 1u);
   u32 dups = 0;
   for (u32 l = threadIdx.x; l < NL; l += SVO_THREADS) {
-    const u64 code = ((u64)o << 40) | minute_code(s_lm[l]);
+    const u64 code = ((u64)o << 40) | minute_code_from(s_lm[l], [&](u32 x) { return (u32)s_b3[x]; });
     const u64 k = lb_u64(t_ck, la, lb, code);
     const bool dup = k < lb && t_ck[k] == code;
     l_ck[a + l] = code;
