@@ -188,14 +188,23 @@ template int evm::scan_exclusive<u64, OpMax>(evm_ctx*, Scratch&, const u64*, siz
 
 template <typename K>
 int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t n, int lo_bit, int hi_bit) {
-  if (n <= 1 || hi_bit <= lo_bit) return EVM_OK;
+  // vals == nullptr: the values are the identity 0..n-1 (made by the first pass)
+  if (n <= 1 || hi_bit <= lo_bit) {
+    if (!vals) {
+      vals = S.alloc<u32>(std::max<size_t>(n, 1));
+      if (!vals) return EVM_ENOMEM;
+      return launch_iota(ctx, vals, n);
+    }
+    return EVM_OK;
+  }
   const int B = hi_bit - lo_bit;
   const int passes = (B + RADIX_BITS - 1) / RADIX_BITS;
   const int width = (B + passes - 1) / passes;
   const u32 ntiles = (u32)((n + SORT_TILE - 1) / SORT_TILE);
   K* k2 = S.alloc<K>(n);
   u32* v2 = S.alloc<u32>(n);
-  if (!k2 || !v2) return EVM_ENOMEM;
+  u32* v3 = vals ? v2 : S.alloc<u32>(n);  // identity values: a second buffer for the ping-pong
+  if (!k2 || !v2 || !v3) return EVM_ENOMEM;
   if (ctx->radix_onesweep && passes <= RADIX_MAX_PASSES) {
     // one read for every pass's digit histogram, then one launch per pass
     u64* status = S.alloc<u64>((size_t)RADIX_BINS * ntiles);
@@ -217,6 +226,7 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
               gh + (size_t)p * RADIX_BINS, status, ctr + p, p, err);
       std::swap(keys, k2);
       std::swap(vals, v2);
+      if (!v2) v2 = v3;
       shift += bits;
     }
     u32 h_err = 0;
@@ -238,6 +248,7 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
                        shift, bits, offs, ntiles);
     std::swap(keys, k2);
     std::swap(vals, v2);
+    if (!v2) v2 = v3;
     shift += bits;
   }
   return hip_ok(hipGetLastError());

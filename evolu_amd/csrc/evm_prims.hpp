@@ -319,7 +319,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(const K* __restr
     const size_t i = wbase + (size_t)r * WAVE + lane;
     const bool ok = i < n;
     key[r] = ok ? kin[i] : K(0);
-    val[r] = ok ? vin[i] : 0u;
+    val[r] = ok ? (vin ? vin[i] : (u32)i) : 0u;  // no values: the identity
     const u32 d = digit_of(key[r], shift, mask);
     dig[r] = d;
     u64 peers = __ballot(ok);
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_onesweep(const K* __rest
     const size_t i = wbase + (size_t)r * WAVE + lane;
     const bool ok = i < n;
     key[r] = ok ? kin[i] : K(0);
-    val[r] = ok ? vin[i] : 0u;
+    val[r] = ok ? (vin ? vin[i] : (u32)i) : 0u;  // no values: the identity (the first pass of an index sort)
   }
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {

@@ -621,15 +621,15 @@ __device__ __forceinline__ u32 seg_owner(const SegView& v, u32 s) { return v.own
 
 template <u32 CAP>
 struct SvoLog2 {
-  static constexpr int v = CAP == 512 ? 9 : CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;
+  static constexpr int v = CAP == 128 ? 7 : CAP == 512 ? 9 : CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;
 };
 
 // Phase A for owners whose share is <= CAP.  LDS by batch position t (the
 // owner's share in batch order): node ranks, batch index, hash; sort keys
 // (tc - tc_min) << PB | t, sorted by a bitonic network (8-B elements only);
 // runs of one tc (distinct nodes) are then put in node order.
-template <u32 CAP, bool PARSE>
-__global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
+template <u32 CAP, bool PARSE, int THREADS = SVO_THREADS>
+__global__ __launch_bounds__(THREADS) void k_svo_a(
     const evm_rec* __restrict__ rec, const uint8_t* __restrict__ ts, size_t stride, Info* __restrict__ info,
     const u32* __restrict__ perm, SegView sv, StoreView st,
     const u64* __restrict__ t_ck, u64 id_base, uint8_t* __restrict__ flags,
@@ -637,8 +637,8 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status,
     const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list, u32* __restrict__ mid1,
-    uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner, int flags_preset) {
-  constexpr int PER = CAP / SVO_THREADS;
+    uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner, int flags_preset, u32* __restrict__ mid512) {
+  constexpr int PER = CAP / THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
   constexpr u64 PMASK = CAP - 1;
   __shared__ u64 s_k[CAP];   // sort keys; later: minute / hash of the inserted rows
@@ -648,8 +648,8 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   // (the batch index of position t is perm[a + t], re-read from L2 in the
   // dedup phase: without it the 1,024 kernel's LDS fits five workgroups per CU)
   __shared__ u32 s_cnt[CAP];  // counting sort: bucket counts, then starts
-  __shared__ u64 s_red[2 * (SVO_THREADS / 64)];
-  __shared__ u32 tmp[SVO_THREADS / 64 + 1];
+  __shared__ u64 s_red[2 * (THREADS / 64)];
+  __shared__ u32 tmp[THREADS / 64 + 1];
   __shared__ uint16_t s_b3[243];  // base-3 digits of 0..242 (the leaves' key codes)
   const u32 s = list ? list[blockIdx.x] : blockIdx.x;  // pass 2: only the segments pass 1 deferred
   const u32 o = seg_owner(sv, s);
@@ -659,7 +659,9 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   const u64 la = sv.la[s], lb = sv.lb[s];
   if (m > CAP || m == 0) {
     if (threadIdx.x == 0) {
-      if (m <= 1024 && mid1) {
+      if (m <= 512 && mid512) {
+        mid512[1 + atomicAdd(&mid512[0], 1u)] = s;  // for the 512 pass (after the one-wave pass)
+      } else if (m <= 1024 && mid1) {
         mid1[1 + atomicAdd(&mid1[0], 1u)] = s;  // for the 1,024 pass
       } else if (m <= SVO_CAP && mid_list) {
         mid_list[1 + atomicAdd(&mid_list[0], 1u)] = s;  // for the SVO_CAP pass
@@ -673,7 +675,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     }
     return;
   }
-  if (threadIdx.x < 243) s_b3[threadIdx.x] = (uint16_t)b3_raw5(threadIdx.x);  // (read after many barriers)
+  for (u32 t = threadIdx.x; t < 243; t += THREADS) s_b3[t] = (uint16_t)b3_raw5(t);  // (read after many barriers)
   u32 P = 1;
   while (P < m) P <<= 1;
   // gather: all batch indices, then all records (independent loads in flight)
@@ -681,7 +683,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   u64 tc[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const u32 t = threadIdx.x + k * SVO_THREADS;
+    const u32 t = threadIdx.x + k * THREADS;
     bi[k] = t < m ? perm[a + t] : 0u;
   }
   u64 tmin = ~0ull, tmax = 0;
@@ -689,7 +691,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     // the timestamp rows themselves (no packed records): parse + murmur3 here
     u32 bad = 0;
     for (int k = 0; k < PER; ++k) {
-      const u32 t = threadIdx.x + k * SVO_THREADS;
+      const u32 t = threadIdx.x + k * THREADS;
       if (t < m) {
         typedef unsigned int v4u __attribute__((ext_vector_type(4)));
         const v4u* row = reinterpret_cast<const v4u*>(ts + (size_t)bi[k] * stride);
@@ -710,7 +712,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   } else {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const u32 t = threadIdx.x + k * SVO_THREADS;
+      const u32 t = threadIdx.x + k * THREADS;
       if (t < m) {
         const evm_rec r = load_rec_nt(rec + bi[k]);
         u64 hi;
@@ -729,13 +731,13 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   tmax = wave_max(tmax);
   if (lane == 0) {
     s_red[wv] = tmin;
-    s_red[SVO_THREADS / 64 + wv] = tmax;
+    s_red[THREADS / 64 + wv] = tmax;
   }
   __syncthreads();
 #pragma unroll
-  for (int w = 0; w < SVO_THREADS / 64; ++w) {
+  for (int w = 0; w < THREADS / 64; ++w) {
     tmin = min(tmin, s_red[w]);
-    tmax = max(tmax, s_red[SVO_THREADS / 64 + w]);
+    tmax = max(tmax, s_red[THREADS / 64 + w]);
   }
   if ((tmax - tmin) >> (64 - PB)) {  // span too wide for the 64-bit sort key
     if (threadIdx.x == 0) atomicOr(&status->fallback, 1u);
@@ -747,12 +749,12 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   // network instead.
   const int sbits = (tmax - tmin) ? 64 - __builtin_clzll(tmax - tmin) : 0;
   const int shift = sbits > PB ? sbits - PB : 0;
-  for (u32 t = threadIdx.x; t < CAP; t += SVO_THREADS) s_cnt[t] = 0;
+  for (u32 t = threadIdx.x; t < CAP; t += THREADS) s_cnt[t] = 0;
   __syncthreads();
   u32 bk[PER], rk[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const u32 t = threadIdx.x + k * SVO_THREADS;
+    const u32 t = threadIdx.x + k * THREADS;
     bk[k] = rk[k] = 0;
     if (t < m) {
       bk[k] = (u32)((tc[k] - tmin) >> shift);
@@ -779,7 +781,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     if (mx <= SVO_BUCKET_MAX) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
-        const u32 t = threadIdx.x + k * SVO_THREADS;
+        const u32 t = threadIdx.x + k * THREADS;
         if (t < m) s_k[s_cnt[bk[k]] + rk[k]] = ((tc[k] - tmin) << PB) | t;
       }
       __syncthreads();
@@ -789,7 +791,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
       u32 dst[PER];
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
-        const u32 t = threadIdx.x + k * SVO_THREADS;
+        const u32 t = threadIdx.x + k * THREADS;
         dst[k] = 0;
         if (t < m) {
           const u32 b0 = s_cnt[bk[k]], b1 = bk[k] + 1 < CAP ? s_cnt[bk[k] + 1] : (u32)m;
@@ -802,19 +804,19 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
-        const u32 t = threadIdx.x + k * SVO_THREADS;
+        const u32 t = threadIdx.x + k * THREADS;
         if (t < m) s_k[dst[k]] = ((tc[k] - tmin) << PB) | t;
       }
     } else {
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
-        const u32 t = threadIdx.x + k * SVO_THREADS;
+        const u32 t = threadIdx.x + k * THREADS;
         if (t < P) s_k[t] = t < m ? ((tc[k] - tmin) << PB) | t : ~0ull;
       }
       __syncthreads();
       for (u32 k = 2; k <= P; k <<= 1) {
         for (u32 j = k >> 1; j > 0; j >>= 1) {
-          for (u32 t = threadIdx.x; t < P / 2; t += SVO_THREADS) {
+          for (u32 t = threadIdx.x; t < P / 2; t += THREADS) {
             const u32 i = 2 * t - (t & (j - 1)), l = i + j;
             const u64 x = s_k[i], y = s_k[l];
             if ((y < x) == ((i & k) == 0)) {
@@ -832,12 +834,12 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   // finds its run's bounds and counts the members below it, all in parallel
   // (runs are short: distinct nodes at one (millis, counter))
   {
-    constexpr int PT = (CAP + SVO_THREADS - 1) / SVO_THREADS;
+    constexpr int PT = (CAP + THREADS - 1) / THREADS;
     u64 kk[PT];
     u32 kd[PT];
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
-      const u32 p = threadIdx.x + k * SVO_THREADS;
+      const u32 p = threadIdx.x + k * THREADS;
       kd[k] = p;
       kk[k] = 0;
       if (p >= m) continue;
@@ -868,7 +870,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
-      const u32 p = threadIdx.x + k * SVO_THREADS;
+      const u32 p = threadIdx.x + k * THREADS;
       if (p < m && kd[k] != p) s_k[kd[k]] = kk[k];
     }
   }
@@ -878,7 +880,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   // messages were listed in (key-range segments are gathered unordered).
   // s_cnt[p] = 1: p is its timestamp's candidate.  A run's first position
   // decides the whole run (O(run) per run).
-  for (u32 p = threadIdx.x; p < m; p += SVO_THREADS) {
+  for (u32 p = threadIdx.x; p < m; p += THREADS) {
     const u64 kp = s_k[p];
     const u32 pp = (u32)(kp & PMASK);
     auto same = [&](u32 x, u32 y) {
@@ -942,7 +944,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   u32* s_hq = s_min + CAP;                   //                        hash
   u32* s_lx = reinterpret_cast<u32*>(s_rh);  // per leaf: XOR
   u32* s_lm = s_lx + CAP;                    //           minute
-  for (u32 t = threadIdx.x; t < CAP; t += SVO_THREADS) s_lx[t] = 0;
+  for (u32 t = threadIdx.x; t < CAP; t += THREADS) s_lx[t] = 0;
 #pragma unroll
   for (int r = 0; r < PER; ++r) {
     const u32 p = threadIdx.x * PER + r;
@@ -990,7 +992,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
   __syncthreads();
   if (threadIdx.x == 0 && NL && base3_len(s_lm[0]) != base3_len(s_lm[NL - 1])) atomicOr(&status->fallback, 1u);
   u32 dups = 0;
-  for (u32 l = threadIdx.x; l < NL; l += SVO_THREADS) {
+  for (u32 l = threadIdx.x; l < NL; l += THREADS) {
     const u64 code = ((u64)o << 40) | minute_code_from(s_lm[l], [&](u32 x) { return (u32)s_b3[x]; });
     const u64 k = lb_u64(t_ck, la, lb, code);
     const bool dup = k < lb && t_ck[k] == code;
@@ -1005,6 +1007,34 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_a(
     cnt_rows[s] = M;
     cnt_new[s] = NL;
     cnt_leaves[s] = (u32)(lb - la) + NL - dtot;
+  }
+}
+
+// Segments by share size, listed per K5 capacity (<= 128, <= 512, <= 1,024,
+// the rest): each K5 pass then launches exactly its segments -- a workgroup
+// per segment that would only defer itself costs a dispatch all the same.
+// lists[c * (NS + 1)] = count of class c, its segments after it.
+__global__ void k_seg_classes(SegView sv, u32 NS, u32* __restrict__ lists) {
+  const int lane = threadIdx.x & 63;
+  const u64 lt = lanemask_lt();
+  for (u32 s0 = blockIdx.x * blockDim.x; s0 < NS; s0 += gridDim.x * blockDim.x) {  // uniform per wave
+    const u32 s = s0 + threadIdx.x;
+    int cls = -1;
+    if (s < NS) {
+      const u64 m = sv.start[s + 1] - sv.start[s];
+      cls = m <= 128 ? 0 : m <= 512 ? 1 : m <= 1024 ? 2 : 3;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const u64 b = __ballot(cls == c);
+      if (!b) continue;
+      u32* L = lists + (size_t)c * (NS + 1);
+      const int leader = __builtin_ctzll(b);
+      u32 base = 0;
+      if (lane == leader) base = atomicAdd(&L[0], (u32)__popcll(b));
+      base = __shfl(base, leader, 64);
+      if (cls == c) L[1 + base + (u32)__popcll(b & lt)] = s;
+    }
   }
 }
 
@@ -1365,27 +1395,48 @@ __global__ void k_seg_table(const u32* __restrict__ spoff, const u32* __restrict
   }
 }
 
-// every message's segment: the owner's first, plus the splitters <= its minute
-__global__ void k_seg_key(const evm_rec* __restrict__ rec, const u32* __restrict__ minute,
-                          const u32* __restrict__ owner, size_t n,
-                          const u32* __restrict__ bbase, const u32* __restrict__ spoff, const u32* __restrict__ sp,
-                          const u32* __restrict__ toff, const u32* __restrict__ tab, u32* __restrict__ key,
-                          u32* __restrict__ val) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const u32 o = owner[i];
-    const u32 b0 = bbase[o], nbo = bbase[o + 1] - b0;
-    u32 k = b0;
-    if (nbo > 1) {
-      const u32 mnt = minute_of(rec, minute, i), a = spoff[o], t0 = toff[o], tl = toff[o + 1] - t0;
-      if (tl) {
-        const u32 first = sp[a];
-        k += mnt < first ? 0u : mnt - first >= tl ? nbo - 1 : tab[t0 + (mnt - first)];
-      } else {
-        k += upper_u32(sp + a, nbo - 1, mnt);
+// every message's segment: the owner's first, plus the splitters <= its minute.
+// Four messages per thread, their dependent lookups (owner -> segment base ->
+// table) interleaved so the L2 round trips overlap; the batch index is not
+// written (the segment sort's first pass makes the identity values).
+constexpr int SK_ITEMS = 4;
+__global__ __launch_bounds__(256) void k_seg_key(const evm_rec* __restrict__ rec, const u32* __restrict__ minute,
+                                                 const u32* __restrict__ owner, size_t n,
+                                                 const u32* __restrict__ bbase, const u32* __restrict__ spoff,
+                                                 const u32* __restrict__ sp, const u32* __restrict__ toff,
+                                                 const u32* __restrict__ tab, u32* __restrict__ key) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x * SK_ITEMS;
+  for (size_t i0 = (size_t)blockIdx.x * blockDim.x * SK_ITEMS + threadIdx.x; i0 < n; i0 += stride) {
+    u32 o[SK_ITEMS], mnt[SK_ITEMS], b0[SK_ITEMS], nbo[SK_ITEMS], k[SK_ITEMS];
+#pragma unroll
+    for (int r = 0; r < SK_ITEMS; ++r) {
+      const size_t i = i0 + (size_t)r * blockDim.x;
+      o[r] = i < n ? owner[i] : 0u;
+      mnt[r] = i < n ? minute_of(rec, minute, i) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < SK_ITEMS; ++r) {
+      b0[r] = bbase[o[r]];
+      nbo[r] = bbase[o[r] + 1] - b0[r];
+      k[r] = b0[r];
+    }
+#pragma unroll
+    for (int r = 0; r < SK_ITEMS; ++r) {
+      if (nbo[r] > 1) {
+        const u32 a = spoff[o[r]], t0 = toff[o[r]], tl = toff[o[r] + 1] - t0;
+        if (tl) {
+          const u32 first = sp[a];
+          k[r] += mnt[r] < first ? 0u : mnt[r] - first >= tl ? nbo[r] - 1 : tab[t0 + (mnt[r] - first)];
+        } else {
+          k[r] += upper_u32(sp + a, nbo[r] - 1, mnt[r]);
+        }
       }
     }
-    key[i] = k;
-    val[i] = (u32)i;
+#pragma unroll
+    for (int r = 0; r < SK_ITEMS; ++r) {
+      const size_t i = i0 + (size_t)r * blockDim.x;
+      if (i < n) key[i] = k[r];
+    }
   }
 }
 
@@ -1667,14 +1718,13 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   if (split) {
     u32* sp = S.alloc<u32>(std::max<u32>(nspl, 1));
     u32* bkey = S.alloc<u32>(n);
-    u32* bval = S.alloc<u32>(n);
     u64* sstart = S.alloc<u64>((size_t)NS + 1);
     u32* sown = S.alloc<u32>(NS);
     u64* ssa = S.alloc<u64>(NS);
     u64* ssb = S.alloc<u64>(NS);
     u64* sla = S.alloc<u64>(NS);
     u64* slb = S.alloc<u64>(NS);
-    if (!sp || !bkey || !bval || !sstart || !sown || !ssa || !ssb || !sla || !slb) return EVM_ENOMEM;
+    if (!sp || !bkey || !sstart || !sown || !ssa || !ssb || !sla || !slb) return EVM_ENOMEM;
     if (nspl)
       KLAUNCH(k_seg_split, dim3(grid_for(nspl, 256)), dim3(256), skey, soff, spoff, bbase, O, nspl, gmin, mb, sp);
     // minute -> segment tables of the cut owners (a lookup per message instead of a search)
@@ -1689,10 +1739,10 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     u32* tab = S.alloc<u32>(std::max<u32>(ntab, 1));
     if (!tab) return EVM_ENOMEM;
     if (ntab) KLAUNCH(k_seg_table, dim3(grid_for(ntab, 256)), dim3(256), spoff, sp, tboff, O, ntab, tab);
-    KLAUNCH(k_seg_key, dim3(grid_for(n, 256)), dim3(256), rec, minute, owner, n, bbase, spoff, sp, tboff, tab, bkey,
-            bval);
+    KLAUNCH(k_seg_key, dim3(grid_for((n + SK_ITEMS - 1) / SK_ITEMS, 256)), dim3(256), rec, minute, owner, n, bbase,
+            spoff, sp, tboff, tab, bkey);
     u32* bk = bkey;
-    u32* bv = bval;
+    u32* bv = nullptr;  // the batch index: the identity, made by the sort's first pass
     if ((st = radix_sort_pairs<u32>(ctx, S, bk, bv, n, 0, std::max(1, ceil_log2(NS))))) return st;
     KLAUNCH(k_seg_start, dim3(grid_for((size_t)NS + 1, 256)), dim3(256), bk, n, NS, sstart);
     KLAUNCH(k_seg_ranges, dim3(grid_for(NS, 256)), dim3(256), bbase, spoff, sp, O, NS, view_of(s), (const u64*)t->off,
@@ -1742,15 +1792,15 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   // (small segments -- Zipf tails, cut owners -- take the 512 kernel: half the
   // per-workgroup fixed work, twice the occupancy); larger shares are listed
   // for the 1,024 and SVO_CAP passes
-  u32* mid1 = S.alloc<u32>((size_t)NS + 1);
-  if (!mid1) return EVM_ENOMEM;
-  HIPR(hipMemsetAsync(mid1, 0, sizeof(u32), ctx->stream));
   const bool small = NS && n / NS < 400;
-  auto pass = [&](u32 cap, dim3 grid, const u32* list, u32* l1, u32* l2) {
+  auto pass = [&](u32 cap, dim3 grid, const u32* list, u32* l1, u32* l2, u32* l512) {
 #define SVO_ARGS                                                                                                      \
   rec, tsb, stride, info, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, \
-      l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, list, l2, l1, ownbig, n_owner, preset
-    if (cap == 512 && fused) KLAUNCH((k_svo_a<512, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
+      l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, list, l2, l1, ownbig, n_owner, preset, l512
+    // (the one-wave kernel: Zipf-tail owners of <= 128 messages, 32 workgroups per CU)
+    if (cap == 128 && fused) KLAUNCH((k_svo_a<128, true, 64>), grid, dim3(64), SVO_ARGS);
+    else if (cap == 128) KLAUNCH((k_svo_a<128, false, 64>), grid, dim3(64), SVO_ARGS);
+    else if (cap == 512 && fused) KLAUNCH((k_svo_a<512, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
     else if (cap == 512) KLAUNCH((k_svo_a<512, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
     else if (cap == 1024 && fused) KLAUNCH((k_svo_a<1024, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
     else if (cap == 1024) KLAUNCH((k_svo_a<1024, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
@@ -1758,13 +1808,29 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     else KLAUNCH((k_svo_a<SVO_CAP, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
 #undef SVO_ARGS
   };
-  pass(small ? 512 : 1024, dim3(NS), (const u32*)nullptr, small ? mid1 : (u32*)nullptr, mid);
-  u32 hm1 = 0;
-  HIPR(hipMemcpyAsync(&hmid, mid, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipMemcpyAsync(&hm1, mid1, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
-  if (hm1) pass(1024, dim3(hm1), (const u32*)(mid1 + 1), (u32*)nullptr, (u32*)nullptr);
-  if (hmid) pass(SVO_CAP, dim3(hmid), (const u32*)(mid + 1), (u32*)nullptr, (u32*)nullptr);
+  if (small) {
+    // small segments on average (Zipf tails and ~560-message cuts): segments
+    // listed by size class first, then one pass per class over exactly its
+    // segments (the one-wave kernel for <= 128 messages)
+    u32* lists = S.alloc<u32>(4 * ((size_t)NS + 1));
+    if (!lists) return EVM_ENOMEM;
+    for (int c = 0; c < 4; ++c) HIPR(hipMemsetAsync(lists + (size_t)c * (NS + 1), 0, sizeof(u32), ctx->stream));
+    KLAUNCH(k_seg_classes, dim3(grid_for(NS, 256)), dim3(256), sv, NS, lists);
+    u32 hc[4];
+    for (int c = 0; c < 4; ++c)
+      HIPR(hipMemcpyAsync(&hc[c], lists + (size_t)c * (NS + 1), sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    const u32 caps[4] = {128, 512, 1024, SVO_CAP};
+    for (int c = 0; c < 4; ++c)
+      if (hc[c])
+        pass(caps[c], dim3(hc[c]), (const u32*)(lists + (size_t)c * (NS + 1) + 1), (u32*)nullptr, (u32*)nullptr,
+             (u32*)nullptr);
+  } else {
+    pass(1024, dim3(NS), (const u32*)nullptr, (u32*)nullptr, mid, (u32*)nullptr);
+    HIPR(hipMemcpyAsync(&hmid, mid, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    if (hmid) pass(SVO_CAP, dim3(hmid), (const u32*)(mid + 1), (u32*)nullptr, (u32*)nullptr, (u32*)nullptr);
+  }
   KLAUNCH(k_seg_fix, dim3(grid_for(NS, 256)), dim3(256), sv, NS, ownbig, c_rows, c_new, c_leaves);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, NS, pos, tot))) return st;
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, NS, pos + NS, tot + 1))) return st;
