@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <functional>
@@ -1014,6 +1015,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
 // the rest): each K5 pass then launches exactly its segments -- a workgroup
 // per segment that would only defer itself costs a dispatch all the same.
 // lists[c * (NS + 1)] = count of class c, its segments after it.
+constexpr int SEG_CLASSES = 5;
 __global__ void k_seg_classes(SegView sv, u32 NS, u32* __restrict__ lists) {
   const int lane = threadIdx.x & 63;
   const u64 lt = lanemask_lt();
@@ -1022,10 +1024,10 @@ __global__ void k_seg_classes(SegView sv, u32 NS, u32* __restrict__ lists) {
     int cls = -1;
     if (s < NS) {
       const u64 m = sv.start[s + 1] - sv.start[s];
-      cls = m <= 128 ? 0 : m <= 512 ? 1 : m <= 1024 ? 2 : 3;
+      cls = m <= 128 ? 0 : m <= 512 ? 1 : m <= 1024 ? 2 : m <= 2048 ? 3 : 4;
     }
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < SEG_CLASSES; ++c) {
       const u64 b = __ballot(cls == c);
       if (!b) continue;
       u32* L = lists + (size_t)c * (NS + 1);
@@ -1309,6 +1311,15 @@ void store_release_arrays(evm_ctx* ctx, evm_store* s) {
 constexpr u32 SEG_TARGET = 560;     // messages per segment of a cut owner: minute-granular splitters and
                                     // sampling noise keep nearly all below 1,024 (the fast kernel)
 constexpr u32 SEG_SPLIT_MIN = 1024; // shares above this are cut (the 1,024 kernel is the fast one)
+// (EVM_SEG_TARGET overrides SEG_TARGET: tuning experiments only)
+static u32 seg_target() {
+  static const u32 t = [] {
+    const char* e = getenv("EVM_SEG_TARGET");
+    const long v = e ? atol(e) : 0;
+    return v >= 64 && v <= 4096 ? (u32)v : SEG_TARGET;
+  }();
+  return t;
+}
 constexpr u32 SAMPLE_STRIDE = 16;   // one sampled minute per 16 messages of a cut owner
 constexpr u32 SEG_TABLE_RATIO = 64; // minute -> segment table when the splitters span <= 64 minutes per segment
 
@@ -1323,12 +1334,12 @@ __device__ __forceinline__ u32 upper_u32(const u32* a, u32 n, u32 x) {  // first
 }
 
 // per owner: segments (1 unless the share exceeds SVO_CAP), samples, splitters
-__global__ void k_seg_plan(const u64* __restrict__ seg, u32 O, u32* __restrict__ nb, u32* __restrict__ ns,
+__global__ void k_seg_plan(const u64* __restrict__ seg, u32 O, u32 target, u32* __restrict__ nb, u32* __restrict__ ns,
                            u32* __restrict__ nsp) {
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < O; o += gridDim.x * blockDim.x) {
     const u64 m = seg[o + 1] - seg[o];
     const bool big = m > SEG_SPLIT_MIN;
-    const u32 b = big ? (u32)((m + SEG_TARGET - 1) / SEG_TARGET) : 1u;
+    const u32 b = big ? (u32)((m + target - 1) / target) : 1u;
     nb[o] = b;
     ns[o] = big ? (u32)((m + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE) : 0u;
     nsp[o] = b - 1;
@@ -1467,13 +1478,13 @@ __global__ void k_seg_sample_all(const evm_rec* __restrict__ rec, const u32* __r
 }
 
 // segments per owner from its sample count (share ~ 16 x samples)
-__global__ void k_seg_plan_est(const u32* __restrict__ soff, u32 O, int cut, u32* __restrict__ nb,
+__global__ void k_seg_plan_est(const u32* __restrict__ soff, u32 O, int cut, u32 target, u32* __restrict__ nb,
                                u32* __restrict__ nsp) {
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < O; o += gridDim.x * blockDim.x) {
     const u64 est = (u64)(soff[o + 1] - soff[o]) * SAMPLE_STRIDE;
     // (estimates above 3/4 of the split size are cut too: a share estimated low
     // would otherwise exceed 1,024 and take the slower SVO_CAP kernel)
-    const u32 b = cut && est > SEG_SPLIT_MIN * 3 / 4 ? (u32)((est + SEG_TARGET - 1) / SEG_TARGET) : 1u;
+    const u32 b = cut && est > SEG_SPLIT_MIN * 3 / 4 ? (u32)((est + target - 1) / target) : 1u;
     nb[o] = b;
     nsp[o] = b - 1;
   }
@@ -1657,7 +1668,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     KLAUNCH(k_run_fill, dim3(grid_for(R, 4 * RF_RUNS, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
     // owners above SEG_SPLIT_MIN: key-range segments, splitters from every
     // 16th message of their share
-    KLAUNCH(k_seg_plan, dim3(grid_for(O, 256)), dim3(256), seg, O, nb, nsm, nsp);
+    KLAUNCH(k_seg_plan, dim3(grid_for(O, 256)), dim3(256), seg, O, seg_target(), nb, nsm, nsp);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nb, O, bbase, bbase + O))) return st;
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsm, O, soff, soff + O))) return st;
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsp, O, spoff, spoff + O))) return st;
@@ -1704,7 +1715,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     KLAUNCH(k_seg_sample_all, dim3(grid_for(nq, 256)), dim3(256), rec, minute, owner, n, gmin, mb, skey, sval);
     if ((st = radix_sort_pairs<u64>(ctx, S, skey, sval, nq, 0, mb + obits))) return st;
     KLAUNCH(k_seg_soff, dim3(grid_for((size_t)O + 1, 256)), dim3(256), skey, nq, O, mb, soff);
-    KLAUNCH(k_seg_plan_est, dim3(grid_for(O, 256)), dim3(256), soff, O, mb > 0 ? 1 : 0, nb, nsp);
+    KLAUNCH(k_seg_plan_est, dim3(grid_for(O, 256)), dim3(256), soff, O, mb > 0 ? 1 : 0, seg_target(), nb, nsp);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nb, O, bbase, bbase + O))) return st;
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsp, O, spoff, spoff + O))) return st;
     u32 plan[2] = {0, 0};
@@ -1804,6 +1815,8 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     else if (cap == 512) KLAUNCH((k_svo_a<512, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
     else if (cap == 1024 && fused) KLAUNCH((k_svo_a<1024, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
     else if (cap == 1024) KLAUNCH((k_svo_a<1024, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
+    else if (cap == 2048 && fused) KLAUNCH((k_svo_a<2048, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
+    else if (cap == 2048) KLAUNCH((k_svo_a<2048, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
     else if (fused) KLAUNCH((k_svo_a<SVO_CAP, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
     else KLAUNCH((k_svo_a<SVO_CAP, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
 #undef SVO_ARGS
@@ -1812,16 +1825,17 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     // small segments on average (Zipf tails and ~560-message cuts): segments
     // listed by size class first, then one pass per class over exactly its
     // segments (the one-wave kernel for <= 128 messages)
-    u32* lists = S.alloc<u32>(4 * ((size_t)NS + 1));
+    u32* lists = S.alloc<u32>(SEG_CLASSES * ((size_t)NS + 1));
     if (!lists) return EVM_ENOMEM;
-    for (int c = 0; c < 4; ++c) HIPR(hipMemsetAsync(lists + (size_t)c * (NS + 1), 0, sizeof(u32), ctx->stream));
+    for (int c = 0; c < SEG_CLASSES; ++c)
+      HIPR(hipMemsetAsync(lists + (size_t)c * (NS + 1), 0, sizeof(u32), ctx->stream));
     KLAUNCH(k_seg_classes, dim3(grid_for(NS, 256)), dim3(256), sv, NS, lists);
-    u32 hc[4];
-    for (int c = 0; c < 4; ++c)
+    u32 hc[SEG_CLASSES];
+    for (int c = 0; c < SEG_CLASSES; ++c)
       HIPR(hipMemcpyAsync(&hc[c], lists + (size_t)c * (NS + 1), sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipStreamSynchronize(ctx->stream));
-    const u32 caps[4] = {128, 512, 1024, SVO_CAP};
-    for (int c = 0; c < 4; ++c)
+    const u32 caps[SEG_CLASSES] = {128, 512, 1024, 2048, SVO_CAP};
+    for (int c = 0; c < SEG_CLASSES; ++c)
       if (hc[c])
         pass(caps[c], dim3(hc[c]), (const u32*)(lists + (size_t)c * (NS + 1) + 1), (u32*)nullptr, (u32*)nullptr,
              (u32*)nullptr);
