@@ -49,6 +49,8 @@ def short(name):
         # KLAUNCH names the template launch by its source text: "(k_svo_a<1024, true>)"
         args = [a.strip().rstrip("u") for a in targs[1:-1].split(",")]
         args = ["SVO_CAP" if a == "4096" else a for a in args]
+        if len(args) == 3 and args[2] == "256":  # the default workgroup size is not in the launch text
+            args = args[:2]
         return "(k_svo_a<%s>)" % ", ".join(args)
     return base
 
