@@ -648,7 +648,18 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   __shared__ u32 s_h[CAP];   //              hash
   // (the batch index of position t is perm[a + t], re-read from L2 in the
   // dedup phase: without it the 1,024 kernel's LDS fits five workgroups per CU)
-  __shared__ u32 s_cnt[CAP];  // counting sort: bucket counts, then starts
+  // counting sort: bucket counts, then starts; then the candidate flags.  Up
+  // to 2,048 they ride in the top 12 bits of s_rl (20 bits of ranks): 4 KiB
+  // less LDS, six 1,024 workgroups per CU instead of five
+  constexpr bool PACK = CAP <= 2048;
+  constexpr u32 RLM = (1u << 20) - 1u;
+  __shared__ u32 s_cnt[PACK ? 1 : CAP];
+  auto cnt_get = [&](u32 i) -> u32 { return PACK ? s_rl[i] >> 20 : s_cnt[i]; };
+  auto cnt_set = [&](u32 i, u32 v) {
+    if (PACK) s_rl[i] = (s_rl[i] & RLM) | (v << 20);
+    else s_cnt[i] = v;
+  };
+  auto rl_get = [&](u32 i) -> u32 { return s_rl[i] & RLM; };
   __shared__ u64 s_red[2 * (THREADS / 64)];
   __shared__ u32 tmp[THREADS / 64 + 1];
   __shared__ uint16_t s_b3[243];  // base-3 digits of 0..242 (the leaves' key codes)
@@ -750,7 +761,10 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   // network instead.
   const int sbits = (tmax - tmin) ? 64 - __builtin_clzll(tmax - tmin) : 0;
   const int shift = sbits > PB ? sbits - PB : 0;
-  for (u32 t = threadIdx.x; t < CAP; t += THREADS) s_cnt[t] = 0;
+  for (u32 t = threadIdx.x; t < CAP; t += THREADS) {
+    if (PACK) s_rl[t] &= RLM;
+    else s_cnt[t] = 0;
+  }
   __syncthreads();
   u32 bk[PER], rk[PER];
 #pragma unroll
@@ -759,7 +773,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     bk[k] = rk[k] = 0;
     if (t < m) {
       bk[k] = (u32)((tc[k] - tmin) >> shift);
-      rk[k] = atomicAdd(&s_cnt[bk[k]], 1u);
+      rk[k] = PACK ? atomicAdd(&s_rl[bk[k]], 1u << 20) >> 20 : atomicAdd(&s_cnt[bk[k]], 1u);
     }
   }
   __syncthreads();
@@ -767,7 +781,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     u32 loc[PER], sum = 0, mx = 0;
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
-      loc[r] = s_cnt[threadIdx.x * PER + r];
+      loc[r] = cnt_get(threadIdx.x * PER + r);
       sum += loc[r];
       mx = max(mx, loc[r]);
     }
@@ -775,7 +789,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     block_inclusive_scan<u32>(mx, tmp, OpMax<u32>(), &mx);
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
-      s_cnt[threadIdx.x * PER + r] = run;
+      cnt_set(threadIdx.x * PER + r, run);
       run += loc[r];
     }
     __syncthreads();
@@ -783,7 +797,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const u32 t = threadIdx.x + k * THREADS;
-        if (t < m) s_k[s_cnt[bk[k]] + rk[k]] = ((tc[k] - tmin) << PB) | t;
+        if (t < m) s_k[cnt_get(bk[k]) + rk[k]] = ((tc[k] - tmin) << PB) | t;
       }
       __syncthreads();
       // each key's place in its bucket = the bucket's keys below it (keys are
@@ -795,7 +809,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
         const u32 t = threadIdx.x + k * THREADS;
         dst[k] = 0;
         if (t < m) {
-          const u32 b0 = s_cnt[bk[k]], b1 = bk[k] + 1 < CAP ? s_cnt[bk[k] + 1] : (u32)m;
+          const u32 b0 = cnt_get(bk[k]), b1 = bk[k] + 1 < CAP ? cnt_get(bk[k] + 1) : (u32)m;
           const u64 key = ((tc[k] - tmin) << PB) | t;
           u32 r = 0;
           for (u32 x = b0; x < b1; ++x) r += s_k[x] < key ? 1u : 0u;
@@ -858,12 +872,12 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       }
       const u32 px = (u32)(kp & PMASK);
       const u64 hx = s_rh[px];
-      const u32 lx = s_rl[px];
+      const u32 lx = rl_get(px);
       u32 r = 0;
       for (u32 q = b0; q < b1; ++q) {
         const u32 pq = (u32)(s_k[q] & PMASK);
         const u64 hq = s_rh[pq];
-        const u32 lq = s_rl[pq];
+        const u32 lq = rl_get(pq);
         r += (hq < hx || (hq == hx && (lq < lx || (lq == lx && pq < px)))) ? 1u : 0u;
       }
       kd[k] = b0 + r;
@@ -886,7 +900,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     const u32 pp = (u32)(kp & PMASK);
     auto same = [&](u32 x, u32 y) {
       const u32 px = (u32)(s_k[x] & PMASK), py = (u32)(s_k[y] & PMASK);
-      return (s_k[x] >> PB) == (s_k[y] >> PB) && s_rh[px] == s_rh[py] && s_rl[px] == s_rl[py];
+      return (s_k[x] >> PB) == (s_k[y] >> PB) && s_rh[px] == s_rh[py] && rl_get(px) == rl_get(py);
     };
     if (p > 0 && same(p - 1, p)) continue;  // not a run start: the start decides
     u32 e = p + 1;
@@ -899,9 +913,9 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
           best = e;
         }
       }
-      for (u32 q = p; q < e; ++q) s_cnt[q] = q == best ? 1u : 0u;
+      for (u32 q = p; q < e; ++q) cnt_set(q, q == best ? 1u : 0u);
     } else {
-      s_cnt[p] = 1u;
+      cnt_set(p, 1u);
     }
   }
   __syncthreads();
@@ -920,10 +934,10 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       const u32 pos = (u32)(kp & PMASK);
       mt[r] = tmin + (kp >> PB);
       mh[r] = s_rh[pos];
-      ml[r] = s_rl[pos];
+      ml[r] = rl_get(pos);
       mb[r] = perm[a + pos];
       mhash[r] = s_h[pos];
-      bool ins = s_cnt[p] != 0;
+      bool ins = cnt_get(p) != 0;
       if (ins && sb > sa) {
         const SKey k{o, mt[r], mh[r], ml[r]};
         const size_t q = store_lower(st, sa, sb, k);
