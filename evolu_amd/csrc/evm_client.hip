@@ -748,11 +748,42 @@ __global__ __launch_bounds__(XP_THREADS) void k_xp_scatter(const u32* __restrict
 // One bucket per workgroup: insert every (hash, index) into an LDS set of u32
 // slots = tag:17 | (local index + 1):15; a tag match re-reads the other pair's
 // full hash (L2-hot), and equal hashes compare the raw 46 timestamp bytes.
+// A pair gets XP_INLINE_PROBES probes in its wave's round; one still unplaced
+// is queued (its next slot kept) and finished after the rounds, one per lane
+// -- so a long probe chain no longer holds its whole wave at every round.
+// Insertion order does not matter: slots never empty again, so two pairs of
+// one hash (one start slot) always meet whichever goes first.
+constexpr u32 XP_INLINE_PROBES = 2;
+constexpr u32 XQ_CAP = 2048;
+__device__ __forceinline__ bool xp_insert(u32* tab, const u64* bp, u64 p, u32 k, u32& pos, u32 budget,
+                                          const uint8_t* ts, size_t stride, const u32* cell, Info* info) {
+  const u32 h = (u32)(p >> 32), i = (u32)p;
+  const u32 mine = ((h >> 15) << 15) | (k + 1);
+  for (u32 probe = 0; probe < budget; ++probe) {
+    const u32 prev = atomicCAS(&tab[pos], 0u, mine);
+    if (prev == 0) return true;  // inserted
+    if ((prev >> 15) == (h >> 15)) {
+      const u64 q = bp[(prev & 0x7fffu) - 1];
+      if ((u32)(q >> 32) == h) {
+        const u32 j = (u32)q;
+        if (ts_bytes_equal(ts, stride, i, j)) {  // equal strings <=> equal keys (both canonical)
+          if (cell[i] != cell[j]) atomic_or_if(&info->collision, 1u);
+          return true;
+        }
+      }
+    }
+    pos = (pos + 1) & (XP_SLOTS - 1);
+  }
+  return false;
+}
+
 __global__ __launch_bounds__(XP_THREADS) void k_xp_dedup(const u64* __restrict__ pairs, const u32* __restrict__ cursor,
                                                         u32 cap, size_t n, const uint8_t* __restrict__ ts,
                                                         size_t stride, const u32* __restrict__ cell,
                                                         Info* __restrict__ info) {
   __shared__ u32 tab[XP_SLOTS];  // 0 = empty
+  __shared__ u32 q[XQ_CAP];      // queued pairs: next slot:15 | local index:15
+  __shared__ u32 qn;
   const u32 b = blockIdx.x;
   const u32 cnt = min(cursor[b], cap);
   if (cnt < 2) return;
@@ -765,30 +796,26 @@ __global__ __launch_bounds__(XP_THREADS) void k_xp_dedup(const u64* __restrict__
     it[r] = k < cnt ? bp[k] : 0ull;
   }
   for (u32 s = threadIdx.x; s < XP_SLOTS; s += XP_THREADS) tab[s] = 0;
+  if (threadIdx.x == 0) qn = 0;
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < XD_ITEMS; ++r) {
     const u32 k = r * XP_THREADS + threadIdx.x;
     if (k >= cnt) break;
     const u64 p = it[r];
-    const u32 h = (u32)(p >> 32), i = (u32)p;
-    const u32 mine = ((h >> 15) << 15) | (k + 1);
-    u32 pos = (h * 2654435761u) >> 17;  // 15 bits
-    for (u32 probe = 0; probe < XP_SLOTS; ++probe) {
-      const u32 prev = atomicCAS(&tab[pos], 0u, mine);
-      if (prev == 0) break;  // inserted
-      if ((prev >> 15) == (h >> 15)) {
-        const u64 q = bp[(prev & 0x7fffu) - 1];
-        if ((u32)(q >> 32) == h) {
-          const u32 j = (u32)q;
-          if (ts_bytes_equal(ts, stride, i, j)) {  // equal strings <=> equal keys (both canonical)
-            if (cell[i] != cell[j]) atomic_or_if(&info->collision, 1u);
-            break;
-          }
-        }
-      }
-      pos = (pos + 1) & (XP_SLOTS - 1);
+    u32 pos = ((u32)(p >> 32) * 2654435761u) >> 17;  // 15 bits
+    if (!xp_insert(tab, bp, p, k, pos, XP_INLINE_PROBES, ts, stride, cell, info)) {
+      const u32 at = atomicAdd(&qn, 1u);
+      if (at < XQ_CAP) q[at] = (pos << 15) | k;
+      else xp_insert(tab, bp, p, k, pos, XP_SLOTS, ts, stride, cell, info);  // queue full: finish here
     }
+  }
+  __syncthreads();
+  const u32 m = min(qn, XQ_CAP);
+  for (u32 t = threadIdx.x; t < m; t += XP_THREADS) {
+    const u32 e = q[t], k = e & 0x7fffu;
+    u32 pos = e >> 15;
+    xp_insert(tab, bp, bp[k], k, pos, XP_SLOTS, ts, stride, cell, info);
   }
 }
 
