@@ -1420,47 +1420,64 @@ __global__ void k_seg_table(const u32* __restrict__ spoff, const u32* __restrict
   }
 }
 
+// Per owner, everything a message's segment lookup needs in one 32-B record
+// (first segment, segment count, splitter offset, table offset and length,
+// first splitter): one dependent load instead of six.
+struct alignas(16) SegOwn {
+  u32 b0, nbo, a, t0, tl, first, pad0, pad1;
+};
+__global__ void k_seg_own(const u32* __restrict__ bbase, const u32* __restrict__ spoff, const u32* __restrict__ sp,
+                          const u32* __restrict__ toff, u32 O, SegOwn* __restrict__ own) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < O; o += gridDim.x * blockDim.x) {
+    SegOwn r;
+    r.b0 = bbase[o];
+    r.nbo = bbase[o + 1] - r.b0;
+    r.a = spoff[o];
+    r.t0 = toff[o];
+    r.tl = toff[o + 1] - r.t0;
+    r.first = r.nbo > 1 ? sp[r.a] : 0u;
+    r.pad0 = r.pad1 = 0;
+    own[o] = r;
+  }
+}
+
 // every message's segment: the owner's first, plus the splitters <= its minute.
-// Four messages per thread, their dependent lookups (owner -> segment base ->
-// table) interleaved so the L2 round trips overlap; the batch index is not
-// written (the segment sort's first pass makes the identity values).
+// Four messages per thread, their lookups (owner record -> table) interleaved
+// so the L2 round trips overlap; the batch index is not written (the segment
+// sort's first pass makes the identity values).
 constexpr int SK_ITEMS = 4;
 __global__ __launch_bounds__(256) void k_seg_key(const evm_rec* __restrict__ rec, const u32* __restrict__ minute,
                                                  const u32* __restrict__ owner, size_t n,
-                                                 const u32* __restrict__ bbase, const u32* __restrict__ spoff,
-                                                 const u32* __restrict__ sp, const u32* __restrict__ toff,
+                                                 const SegOwn* __restrict__ own, const u32* __restrict__ sp,
                                                  const u32* __restrict__ tab, u32* __restrict__ key) {
   const size_t stride = (size_t)gridDim.x * blockDim.x * SK_ITEMS;
   for (size_t i0 = (size_t)blockIdx.x * blockDim.x * SK_ITEMS + threadIdx.x; i0 < n; i0 += stride) {
-    u32 o[SK_ITEMS], mnt[SK_ITEMS], b0[SK_ITEMS], nbo[SK_ITEMS], k[SK_ITEMS];
+    u32 o[SK_ITEMS], mnt[SK_ITEMS], k[SK_ITEMS];
+    SegOwn r[SK_ITEMS];
 #pragma unroll
-    for (int r = 0; r < SK_ITEMS; ++r) {
-      const size_t i = i0 + (size_t)r * blockDim.x;
-      o[r] = i < n ? owner[i] : 0u;
-      mnt[r] = i < n ? minute_of(rec, minute, i) : 0u;
+    for (int j = 0; j < SK_ITEMS; ++j) {
+      const size_t i = i0 + (size_t)j * blockDim.x;
+      o[j] = i < n ? owner[i] : 0u;
+      mnt[j] = i < n ? minute_of(rec, minute, i) : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < SK_ITEMS; ++r) {
-      b0[r] = bbase[o[r]];
-      nbo[r] = bbase[o[r] + 1] - b0[r];
-      k[r] = b0[r];
-    }
+    for (int j = 0; j < SK_ITEMS; ++j) r[j] = own[o[j]];
 #pragma unroll
-    for (int r = 0; r < SK_ITEMS; ++r) {
-      if (nbo[r] > 1) {
-        const u32 a = spoff[o[r]], t0 = toff[o[r]], tl = toff[o[r] + 1] - t0;
-        if (tl) {
-          const u32 first = sp[a];
-          k[r] += mnt[r] < first ? 0u : mnt[r] - first >= tl ? nbo[r] - 1 : tab[t0 + (mnt[r] - first)];
+    for (int j = 0; j < SK_ITEMS; ++j) {
+      k[j] = r[j].b0;
+      if (r[j].nbo > 1) {
+        if (r[j].tl) {
+          const u32 d = mnt[j] - r[j].first;
+          k[j] += mnt[j] < r[j].first ? 0u : d >= r[j].tl ? r[j].nbo - 1 : tab[r[j].t0 + d];
         } else {
-          k[r] += upper_u32(sp + a, nbo[r] - 1, mnt[r]);
+          k[j] += upper_u32(sp + r[j].a, r[j].nbo - 1, mnt[j]);
         }
       }
     }
 #pragma unroll
-    for (int r = 0; r < SK_ITEMS; ++r) {
-      const size_t i = i0 + (size_t)r * blockDim.x;
-      if (i < n) key[i] = k[r];
+    for (int j = 0; j < SK_ITEMS; ++j) {
+      const size_t i = i0 + (size_t)j * blockDim.x;
+      if (i < n) key[i] = k[j];
     }
   }
 }
@@ -1764,8 +1781,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     u32* tab = S.alloc<u32>(std::max<u32>(ntab, 1));
     if (!tab) return EVM_ENOMEM;
     if (ntab) KLAUNCH(k_seg_table, dim3(grid_for(ntab, 256)), dim3(256), spoff, sp, tboff, O, ntab, tab);
-    KLAUNCH(k_seg_key, dim3(grid_for((n + SK_ITEMS - 1) / SK_ITEMS, 256)), dim3(256), rec, minute, owner, n, bbase,
-            spoff, sp, tboff, tab, bkey);
+    SegOwn* sown_rec = S.alloc<SegOwn>(std::max<u32>(O, 1));
+    if (!sown_rec) return EVM_ENOMEM;
+    KLAUNCH(k_seg_own, dim3(grid_for(O, 256)), dim3(256), bbase, spoff, sp, tboff, O, sown_rec);
+    KLAUNCH(k_seg_key, dim3(grid_for((n + SK_ITEMS - 1) / SK_ITEMS, 256)), dim3(256), rec, minute, owner, n,
+            (const SegOwn*)sown_rec, sp, tab, bkey);
     u32* bk = bkey;
     u32* bv = nullptr;  // the batch index: the identity, made by the sort's first pass
     if ((st = radix_sort_pairs<u32>(ctx, S, bk, bv, n, 0, std::max(1, ceil_log2(NS))))) return st;

@@ -101,3 +101,37 @@ def test_mixed_key_lengths_disable_segments(eng):
     cut = len(strings) // 3
     seg = _run(eng, 0, 2, ts_np, owner_np, cut)
     _same(seg, _run(eng, 2, 2, ts_np, owner_np, cut))
+
+
+@pytest.mark.parametrize("burst", [2600, 5000])
+def test_size_classes_with_burst_segment(eng, burst):
+    """Many small owners (the batch takes the size-class passes: the one-wave
+    128 kernel, 512, 1,024) plus a big owner whose burst minute makes one
+    segment of burst/2+ messages per ingest (the 2,048 or the 4,096 class): equal to the
+    sort path over two ingests."""
+    rng = random.Random(burst)
+    strings, owner = [], []
+    nodes = [W.node_id(rng) for _ in range(8)]
+    burst_ms = [O.timestamp_to_string(W.T0 + 240_000 + rng.randrange(60_000), rng.randrange(3), rng.choice(nodes))
+                for _ in range(burst)]
+    groups = [(0, burst_ms + W.hlc_timestamps(rng, 9000, nodes, span=3 * 86_400_000)),
+              (1, W.hlc_timestamps(rng, 8000, nodes[:3], span=86_400_000))]
+    groups += [(o, W.hlc_timestamps(rng, rng.randrange(5, 300), nodes[:2])) for o in range(2, 302)]
+    for o, ms in groups:
+        ms = ms + ms[: len(ms) // 20]  # redeliveries
+        strings += ms
+        owner += [o] * len(ms)
+    perm = list(range(len(strings)))
+    rng.shuffle(perm)
+    strings = [strings[i] for i in perm]
+    owner_np = np.array([owner[i] for i in perm], dtype=np.uint32)
+    ts_np = eng.timestamps(strings).cpu().numpy()
+    cut = len(strings) // 2
+    eng.prof_enable(True)
+    eng.prof_reset()
+    seg = _run(eng, 0, 302, ts_np, owner_np, cut)
+    ran = set(eng.prof_report())
+    eng.prof_enable(False)
+    assert any("k_svo_a<128" in k for k in ran), ran
+    assert any(("k_svo_a<2048" if burst < 4000 else "k_svo_a<SVO_CAP") in k for k in ran), ran
+    _same(seg, _run(eng, 2, 302, ts_np, owner_np, cut))
