@@ -622,7 +622,7 @@ __device__ __forceinline__ u32 seg_owner(const SegView& v, u32 s) { return v.own
 
 template <u32 CAP>
 struct SvoLog2 {
-  static constexpr int v = CAP == 128 ? 7 : CAP == 512 ? 9 : CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;
+  static constexpr int v = CAP == 128 ? 7 : CAP == 256 ? 8 : CAP == 512 ? 9 : CAP == 1024 ? 10 : CAP == 2048 ? 11 : 12;
 };
 
 // Phase A for owners whose share is <= CAP.  LDS by batch position t (the
@@ -1029,7 +1029,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
 // the rest): each K5 pass then launches exactly its segments -- a workgroup
 // per segment that would only defer itself costs a dispatch all the same.
 // lists[c * (NS + 1)] = count of class c, its segments after it.
-constexpr int SEG_CLASSES = 5;
+constexpr int SEG_CLASSES = 6;
 __global__ void k_seg_classes(SegView sv, u32 NS, u32* __restrict__ lists) {
   const int lane = threadIdx.x & 63;
   const u64 lt = lanemask_lt();
@@ -1038,7 +1038,7 @@ __global__ void k_seg_classes(SegView sv, u32 NS, u32* __restrict__ lists) {
     int cls = -1;
     if (s < NS) {
       const u64 m = sv.start[s + 1] - sv.start[s];
-      cls = m <= 128 ? 0 : m <= 512 ? 1 : m <= 1024 ? 2 : m <= 2048 ? 3 : 4;
+      cls = m <= 128 ? 0 : m <= 256 ? 1 : m <= 512 ? 2 : m <= 1024 ? 3 : m <= 2048 ? 4 : 5;
     }
 #pragma unroll
     for (int c = 0; c < SEG_CLASSES; ++c) {
@@ -1842,9 +1842,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
 #define SVO_ARGS                                                                                                      \
   rec, tsb, stride, info, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, \
       l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, list, l2, l1, ownbig, n_owner, preset, l512
-    // (the one-wave kernel: Zipf-tail owners of <= 128 messages, 32 workgroups per CU)
+    // (the one-wave kernels: Zipf-tail owners of <= 128 / <= 256 messages, no cross-wave barriers)
     if (cap == 128 && fused) KLAUNCH((k_svo_a<128, true, 64>), grid, dim3(64), SVO_ARGS);
     else if (cap == 128) KLAUNCH((k_svo_a<128, false, 64>), grid, dim3(64), SVO_ARGS);
+    else if (cap == 256 && fused) KLAUNCH((k_svo_a<256, true, 64>), grid, dim3(64), SVO_ARGS);
+    else if (cap == 256) KLAUNCH((k_svo_a<256, false, 64>), grid, dim3(64), SVO_ARGS);
     else if (cap == 512 && fused) KLAUNCH((k_svo_a<512, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
     else if (cap == 512) KLAUNCH((k_svo_a<512, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
     else if (cap == 1024 && fused) KLAUNCH((k_svo_a<1024, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
@@ -1868,7 +1870,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     for (int c = 0; c < SEG_CLASSES; ++c)
       HIPR(hipMemcpyAsync(&hc[c], lists + (size_t)c * (NS + 1), sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipStreamSynchronize(ctx->stream));
-    const u32 caps[SEG_CLASSES] = {128, 512, 1024, 2048, SVO_CAP};
+    const u32 caps[SEG_CLASSES] = {128, 256, 512, 1024, 2048, SVO_CAP};
     for (int c = 0; c < SEG_CLASSES; ++c)
       if (hc[c])
         pass(caps[c], dim3(hc[c]), (const u32*)(lists + (size_t)c * (NS + 1) + 1), (u32*)nullptr, (u32*)nullptr,
