@@ -4,7 +4,10 @@ k_cl_pack, starts one) the span from that launch to the next step's, the
 time some kernel is running (union of intervals over all streams), the idle
 rest, and the largest gaps with the kernels on either side.
 
-    python tools/trace_gaps.py gpurun_out/prof/run_kernel_trace.csv k_cl_pack
+    python tools/trace_gaps.py gpurun_out/prof/run_kernel_trace.csv k_cl_pack [first_step last_step]
+
+The optional step window (0-based, end exclusive) isolates one pass of the
+bench, e.g. its timed pipelined region; "spans" prints every step's span.
 """
 import csv
 import re
@@ -17,7 +20,7 @@ def short(name):
     return re.split(r"[(<]", name)[0].replace("evm::", "")
 
 
-def main(path, first):
+def main(path, first, lo=None, hi=None, show=False):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
@@ -27,6 +30,12 @@ def main(path, first):
     if len(starts) < 3:
         print("fewer than 3 steps of", first)
         return
+    if show:
+        for j, (a, b) in enumerate(zip(starts[:-1], starts[1:])):
+            print(j, "%.1f" % ((rows[b][0] - rows[a][0]) / 1e3))
+        return
+    if lo is not None:
+        starts = starts[lo:hi + 1]
     spans, busys = [], []
     gaps_all = []
     # steps much longer than the median carry something else (the bench's
@@ -64,4 +73,10 @@ def main(path, first):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "k_cl_pack")
+    args = sys.argv[1:]
+    if len(args) > 2 and args[2] == "spans":
+        main(args[0], args[1], show=True)
+    elif len(args) > 3:
+        main(args[0], args[1], int(args[2]), int(args[3]))
+    else:
+        main(args[0], args[1] if len(args) > 1 else "k_cl_pack")
