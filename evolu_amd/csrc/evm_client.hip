@@ -1023,8 +1023,13 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                                                         const u32* __restrict__ cell, u32 C, size_t range_len,
                                                         u64* __restrict__ tcs, u32* __restrict__ hash,
                                                         u32* __restrict__ minute, u64* __restrict__ agg,
-                                                        Info* __restrict__ info) {
+                                                        Info* __restrict__ info, u32* __restrict__ zero_buf,
+                                                        u32 zero_n) {
   extern __shared__ __attribute__((aligned(16))) u64 cmax[];  // [C] max tc per cell of this range
+  // (the cross-cell check's bucket cursors, cleared here instead of by a
+  // memset on the second stream, which forks after this kernel)
+  if (blockIdx.x == 0)
+    for (u32 k = threadIdx.x; k < zero_n; k += TP_THREADS) zero_buf[k] = 0u;
   __shared__ uint4 stage[TP_THREADS / 64][192];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const size_t g = blockIdx.x;
@@ -1421,10 +1426,10 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     const size_t lds = (size_t)C * 8;
     if (s48)
       hipLaunchKernelGGL(k_tp_pack<true>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, minute, agg, info);
+                         cell, C, range, tcs, hash, minute, agg, info, xcur, 1u << xp_geom(n).kb);
     else
       hipLaunchKernelGGL(k_tp_pack<false>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, minute, agg, info);
+                         cell, C, range, tcs, hash, minute, agg, info, xcur, 1u << xp_geom(n).kb);
   } else {
     key = S.alloc<uint4>(n);
     rl = S.alloc<u32>(n);
@@ -1503,7 +1508,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   SideFork side(ctx);
   {
     const hipStream_t xs = side.stream();
-    HIPR(hipMemsetAsync(xcur, 0, sizeof(u32) << kb, xs));
+    if (!TC) HIPR(hipMemsetAsync(xcur, 0, sizeof(u32) << kb, xs));  // (the tc path's K1 cleared them)
     {
       evm::ProfScope ps_(ctx, "k_xp_scatter", xs);
       hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), 0, xs, hash, n, kb, cap, xcur, xpairs, info);
