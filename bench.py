@@ -90,9 +90,17 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget per leg (0: skip)")
     ap.add_argument("--overlap", type=int, default=1, help="EVM_OPT_OVERLAP: independent checks on a second stream")
     ap.add_argument("--depth", type=int, default=4, help="config 2: batches in flight (evm_apply_batch_async)")
-    ap.add_argument("--workload", choices=["client", "server"], default="client",
-                    help="client: config 2 applyMessages (headline, + config 1 and 3 legs at N=1); "
-                         "server: config 3/4/5 ingest + diff + select alone")
+    ap.add_argument("--workload", choices=["auto", "client", "server", "config4"], default="auto",
+                    help="auto: client at N=1, config4 at N>1; "
+                         "client: config 2 applyMessages (headline, + config 1, 3 and 4 legs at N=1); "
+                         "server: config 3/5 ingest + diff + select alone; "
+                         "config4: the sharded sync server (1B msgs / 1M owners at 8 GPUs, weak scaling)")
+    ap.add_argument("--c4-owners", type=int, default=125_000, help="config4: owners per GPU")
+    ap.add_argument("--c4-per-owner", type=int, default=1000, help="config4: messages per owner")
+    ap.add_argument("--c4-sample", type=int, default=1000, help="config4: owners per rank in the self-check")
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="config4 rehearsal: N loopback ranks (threads) sharing GPU 0 through evm_dist_hub "
+                         "(not a multi-GPU measurement)")
     ap.add_argument("--extra", type=int, default=1, help="N=1 client run: add the config-1 and config-3 legs")
     ap.add_argument("--shape", choices=["auto", "config2", "config4c"], default="auto",
                     help="client workload: config2 = one owner per GPU, no exchange; config4c = owners_per_rank "
@@ -304,7 +312,30 @@ def main():
     from evolu_amd import synth
     from evolu_amd.engine import Engine
 
-    if a.workload == "server":
+    if a.loopback:
+        emit(config4_loopback(a, a.loopback))
+        return
+    workload = a.workload if a.workload != "auto" else ("client" if world == 1 else "config4")
+    if workload == "config4":
+        eng = Engine(local)
+        dd = make_dist(eng, rank, world)
+        res = config4_rank(eng, dd, TorchComm(world, torch.device("cuda", local)), a.c4_owners, a.c4_per_owner,
+                           a.steps, a.warmup, a.c4_sample)
+        if rank == 0:
+            out = {"metric": METRIC, "value": res.pop("value"), "unit": "msgs/s", "n_gpus": world,
+                   "steps": a.steps, "warmup": a.warmup, "ms_per_step": res.pop("ms_per_step"),
+                   "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+                   "data": "synthetic (seeded HLC streams generated on the device, SURVEY 8(d) config 4)",
+                   "cpu_baseline": None}
+            res.pop("steps"), res.pop("warmup")
+            out.update(res)
+            emit(out)
+        dd.free()
+        eng.close()
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if workload == "server":
         out = server_run(a, rank, world, local, a.owners, a.per_owner, a.zipf, a.request, cpu=rank == 0 and world == 1)
         if rank == 0:
             emit(out)
@@ -460,6 +491,14 @@ def main():
             eng.close()
             torch.cuda.empty_cache()
             out["config3"] = server_run(a, 0, 1, local, 100_000, 1000, 0.0, 1000, cpu=a.cpu_seconds > 0, leg=True)
+            # config 4 at world 1: the per-GPU work of the N-GPU line (its weak-scaling base)
+            eng4 = Engine(local)
+            dd4 = make_dist(eng4, 0, 1)
+            out["config4"] = config4_rank(eng4, dd4, TorchComm(1, torch.device("cuda", local)), a.c4_owners,
+                                          a.c4_per_owner, a.steps, a.warmup, a.c4_sample)
+            dd4.free()
+            eng4.close()
+            torch.cuda.empty_cache()
         emit(out)
     if world > 1:
         dist.destroy_process_group()
@@ -474,6 +513,9 @@ DIST_ALG = {
 }
 
 
+DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
+
+
 def make_dist(eng, rank, world):
     """The RCCL communicator of evm_dist_*: rank 0's id broadcast over torch.distributed."""
     import torch
@@ -486,7 +528,9 @@ def make_dist(eng, rank, world):
         uid.copy_(torch.frombuffer(bytearray(dist_unique_id()), dtype=torch.uint8))
     if world > 1:
         dist.broadcast(uid, 0)
-    return Dist(eng, bytes(uid.cpu().numpy()), rank, world)
+    d = Dist(eng, bytes(uid.cpu().numpy()), rank, world)
+    d.transport = "RCCL"
+    return d
 
 
 def client_routed(a, rank, world, local):
@@ -612,6 +656,298 @@ def client_routed(a, rank, world, local):
     }
     dd.free()
     eng.close()
+    return out
+
+
+class TorchComm:
+    """Rank coordination over torch.distributed (the bench's timing only)."""
+
+    def __init__(self, world, dev):
+        self.world, self.dev = world, dev
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    def _reduce(self, x, dtype, op):
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor([x], dtype=dtype, device=self.dev)
+        if self.world > 1:
+            dist.all_reduce(t, op=op)
+        return t.item()
+
+    def max(self, x: float) -> float:
+        import torch
+        import torch.distributed as dist
+
+        return float(self._reduce(x, torch.float64, dist.ReduceOp.MAX))
+
+    def min(self, x: int) -> int:
+        import torch
+        import torch.distributed as dist
+
+        return int(self._reduce(x, torch.int64, dist.ReduceOp.MIN))
+
+
+class ThreadComm:
+    """The same for loopback ranks (threads of one process, evm_dist_hub)."""
+
+    def __init__(self, world):
+        import threading
+
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.vals = [None] * world
+
+    def barrier(self):
+        self.bar.wait()
+
+    def _reduce(self, rank, x, f):
+        self.bar.wait()
+        self.vals[rank] = x
+        self.bar.wait()
+        r = f(self.vals)
+        self.bar.wait()
+        return r
+
+    def bind(self, rank):
+        comm = self
+
+        class R:
+            def barrier(self):
+                comm.barrier()
+
+            def max(self, x):
+                return comm._reduce(rank, x, max)
+
+            def min(self, x):
+                return comm._reduce(rank, x, min)
+
+        return R()
+
+
+C4_SEED = 0xE7010004  # SURVEY 8(d): seed = 0xE7010000 + config number
+
+
+def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10, warmup=2, sample=1000,
+                 seed=C4_SEED, verbose=False):
+    """BASELINE config 4 on one rank: the sync server (index.ts:138-202,
+    addMessages + getMessages) over owners_per_gpu x world owners of
+    per_owner messages each, sharded by murmur3(userId) mod world.
+
+    Every rank's input is its slice of the job's requests: for every owner of
+    the job one SyncRequest with the messages j = rank, rank + world, ... of
+    that owner, requests in a seeded owner order (evm_synth.hip).  One step
+    = route (RCCL all-to-all of counts + 32-B packed records, evm_dist_route)
+    + take with local owner ids + addMessages into an empty store
+    (evm_server_ingest) + getMessages against each owner's client tree
+    (the client knows ~90 % of the owner's messages; requester = the owner's
+    node 0, excluded by the NOT LIKE filter) + every owner's root all-gathered
+    (evm_dist_gather_roots).  Weak scaling: owners_per_gpu x per_owner
+    messages per GPU (125M: 1B over 1M owners at 8 GPUs).
+
+    After the timed steps every rank re-derives `sample` of its owners on its
+    own -- their messages regenerated in receive order, one unsharded ingest
+    + select on this GPU -- and compares inserted counts, roots (as
+    all-gathered), diffs and the selected rows byte for byte; the result is
+    agreed over the ranks (parity_checked)."""
+    import numpy as np
+    import torch
+
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+    from evolu_amd.sharded import ShardedServer
+
+    rank, world = dd.rank, dd.world
+    dev = torch.device("cuda", eng.device)
+    O = owners_per_gpu * world
+    P = per_owner
+    gen = synth.DeviceSynth()
+    t_setup = time.perf_counter()
+    ids = gen.owner_ids(seed, O, dev)
+    srv = ShardedServer(eng, dd, ids, 21)
+    n_local = srv.n_local
+    ts_in, owner_in, _ = gen.source(seed, O, P, world, rank, dev)
+    # client trees (and requester nodes) of this rank's owners, in chunks
+    client = eng.tree_new(n_local)
+    node = torch.empty((max(n_local, 1), 16), dtype=torch.uint8, device=dev)
+    chunk = max(1, 16_000_000 // P)
+    for c0 in range(0, n_local, chunk):
+        lst = srv.owners_here[c0:c0 + chunk]
+        t_c, li_c, k_c = gen.owners(seed, O, P, 1, lst, dev)
+        node[c0:c0 + lst.numel()] = t_c.view(lst.numel(), P, 48)[:, 0, 30:46]  # message 0 = node 0
+        kb = k_c.bool()
+        nxt = eng.merkle_insert(client, t_c[kb].contiguous(), (li_c[kb] + c0).contiguous())
+        client.free()
+        client = nxt
+        del t_c, li_c, k_c, kb
+    node = node.reshape(-1).contiguous()
+    n_exp = n_local * P  # every message of every local owner arrives exactly once
+    out = (torch.empty((max(n_exp, 1), 48), dtype=torch.uint8, device=dev),
+           torch.empty(max(n_exp, 1), dtype=torch.int32, device=dev), None, None)
+    flags = torch.empty(max(n_exp, 1), dtype=torch.uint8, device=dev)
+    id_base = rank << 40
+    torch.cuda.synchronize(dev)
+    setup_s = time.perf_counter() - t_setup
+    route_ms = []
+    last = {}
+
+    def step():
+        r0 = time.perf_counter()
+        t_r, o_r = srv.route(ts_in, owner_in, out=out)
+        route_ms.append((time.perf_counter() - r0) * 1e3)
+        srv.new_store()
+        srv.store.ingest(t_r, o_r, id_base, flags=flags)
+        diff, off, sel = srv.select(client, node)
+        root, present = srv.roots()
+        last.update(n_r=t_r.shape[0], diff=diff, off=off, sel=sel, root=root, present=present)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    # per-kernel breakdown (untimed): the dominant kernel
+    eng.prof_enable(True)
+    eng.prof_reset()
+    step()
+    torch.cuda.synchronize(dev)
+    prof = eng.prof_report()
+    alg_all = dict(DIST_ALG, **SERVER_ALG)
+    dom = dominant(prof, alg_all)
+    eng.prof_only(dom)
+    eng.prof_reset()
+    route_ms.clear()
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step()
+        if verbose:
+            print("rank %d step %d" % (rank, k), file=sys.stderr, flush=True)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    prof_dom = eng.prof_report()
+    eng.prof_enable(False)
+    eng.prof_only(None)
+    elapsed = comm.max(t1 - t0)
+    route_avg = comm.max(sum(route_ms) / max(1, len(route_ms)))
+
+    # ---- self-check: `sample` owners re-derived unsharded on this GPU
+    n_r = last["n_r"]
+    k = min(sample, n_local)
+    ok = n_r == n_exp
+    detail = {"received": int(n_r), "expected": int(n_exp)}
+    if k:
+        li = torch.unique(torch.linspace(0, n_local - 1, k, device=dev).round().to(torch.int64))
+        k = li.numel()
+        glob = srv.owners_here[li]
+        ts_s, own_s, _ = gen.owners(seed, O, P, world, glob, dev)
+        ref = eng.store_new(k)
+        f_s, _ = ref.ingest(ts_s, own_s, 0)
+        t_c, li_c, k_c = gen.owners(seed, O, P, 1, glob, dev)
+        kb = k_c.bool()
+        client_s = eng.merkle_insert(eng.tree_new(k), t_c[kb].contiguous(), li_c[kb].contiguous())
+        node_s = t_c.view(k, P, 48)[:, 0, 30:46].reshape(-1).contiguous()
+        diff_s, off_s, sel_s = ref.select(client_s, node_s)
+        r_s, p_s = ref.tree().roots()
+        # inserted counts per owner
+        ins_big = torch.bincount(out[1][:n_r][(flags[:n_r] & L.MSG_INS) != 0].to(torch.int64),
+                                 minlength=n_local)[li]
+        ins_ref = torch.bincount(own_s[(f_s & L.MSG_INS) != 0].to(torch.int64), minlength=k)
+        ok_ins = bool(torch.equal(ins_big, ins_ref))
+        # roots as all-gathered (any rank's view of these owners)
+        g64 = glob.to(torch.int64)
+        ok_root = (np.array_equal(last["root"][g64].cpu().numpy(), r_s) and
+                   np.array_equal(last["present"][g64].cpu().numpy(), p_s))
+        ok_diff = bool(torch.equal(last["diff"][li], diff_s))
+        # selected rows, byte for byte, in order
+        off, sel = last["off"], last["sel"]
+        cnt_big = off[li + 1] - off[li]
+        cnt_ref = off_s[1:] - off_s[:-1]
+        ok_sel = bool(torch.equal(cnt_big, cnt_ref))
+        n_sel = int(cnt_ref.sum().item())
+        if ok_sel and n_sel:
+            starts = torch.repeat_interleave(off[li], cnt_big)
+            within = torch.arange(n_sel, device=dev) - torch.repeat_interleave(torch.cumsum(cnt_big, 0) - cnt_big,
+                                                                               cnt_big)
+            rows_big = out[0][(sel[starts + within] - id_base)]
+            rows_ref = ts_s[sel_s]
+            ok_sel = bool(torch.equal(rows_big[:, :46], rows_ref[:, :46]))
+        ok = ok and ok_ins and ok_root and ok_diff and ok_sel
+        detail.update(sample_owners=k, inserted=ok_ins, roots=ok_root, diffs=ok_diff, selections=ok_sel,
+                      selected_rows=n_sel, inserted_rows=int(ins_ref.sum().item()))
+        ref.free()
+        client_s.free()
+    parity = comm.min(1 if ok else 0) == 1
+    n = owners_per_gpu * P  # per GPU (weak scaling)
+    ms = elapsed / steps * 1e3
+    tot_ms, launches = prof_dom[dom]
+    avg_s = tot_ms / launches / 1e3
+    if dom in DIST_ALG:
+        alg = DIST_ALG[dom] * n_r
+    else:
+        per_msg, per_leaf = SERVER_ALG[dom]
+        alg = per_msg * n_r + per_leaf * srv.store.tree().n_leaves
+    remote = n * (world - 1) / world
+    res = {
+        "value": world * n * steps / elapsed, "ms_per_step": ms, "steps": steps, "warmup": warmup,
+        "config": {"workload": "config4: sync server (index.ts:138-202 addMessages + getMessages), %d owners x %d "
+                               "msgs = %d msgs over %d GPU(s) (%d owners x %d msgs per GPU, weak scaling: 1B msgs over "
+                               "1M owners at 8 GPUs), owners sharded by murmur3(userId) mod %d on the device "
+                               "(evm_dist_directory), every rank's slice holds one request per owner of the job, "
+                               "routed over %s (evm_dist_route, 32-B packed records), ingest into an empty store, "
+                               "getMessages vs each owner's client tree (~90 %% known), roots all-gathered"
+                               % (O, P, O * P, world, owners_per_gpu, P, world, dd.transport),
+                   "messages_per_gpu": n, "owners_total": O, "owners_per_gpu": owners_per_gpu,
+                   "owners_this_rank": n_local, "parallelism": "owner-sharded (murmur3 mod %d), %s" % (world, dd.transport)},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(DEFAULT_TRAFFIC, dom),
+                     "kernel_ms_avg": avg_s * 1e3, "alg_bytes_per_launch": alg,
+                     "kernel_share_of_step": tot_ms / (ms * steps)},
+        "pipeline": {"alg_bytes_per_msg": SERVER_PIPELINE_BYTES,
+                     "pipeline_hbm_frac": SERVER_PIPELINE_BYTES * n / (elapsed / steps) / HBM_PEAK,
+                     "kernels_ms_per_step": {kk: v[0] for kk, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:16]}},
+        "route": {"ms_per_step": route_avg, "bytes_per_msg": ROUTE_BYTES, "remote_bytes_per_gpu": remote * ROUTE_BYTES,
+                  "xgmi_frac": (remote * ROUTE_BYTES / (route_avg / 1e3) / ((world - 1) * XGMI_LINK))
+                  if world > 1 else None},
+        "parity_checked": parity, "self_check_rank%d" % rank: detail, "setup_s": setup_s,
+    }
+    srv.close()
+    client.free()
+    del ts_in, owner_in, out, flags
+    return res
+
+
+def config4_loopback(a, world, device=0):
+    """config4_rank on `world` loopback ranks: threads of this process on one
+    GPU, evm_dist over an in-process hub (device-to-device copies instead of
+    RCCL) -- the multi-rank partitions, exchange, directory and gathers run
+    exactly as at N GPUs, at 1/world of the speed.  A correctness rehearsal,
+    never a scaling number."""
+    from evolu_amd.engine import run_loopback
+
+    comm = ThreadComm(world)
+
+    def fn(r, eng, dd):
+        try:
+            return config4_rank(eng, dd, comm.bind(r), a.c4_owners, a.c4_per_owner, a.steps, a.warmup, a.c4_sample)
+        except BaseException:
+            comm.bar.abort()  # the other ranks may wait in a bench barrier, not a collective
+            raise
+
+    results = run_loopback(world, fn, device)
+    res = results[0]
+    for r in range(1, world):
+        res.update({k: v for k, v in results[r].items() if k.startswith("self_check_rank")})
+    out = {"metric": METRIC + " [loopback rehearsal, not a multi-GPU measurement]", "value": res.pop("value"),
+           "unit": "msgs/s", "n_gpus": 1, "loopback_ranks": world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": res.pop("ms_per_step"), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "u64", "data": "synthetic (device generator, SURVEY 8(d) config 4)", "cpu_baseline": None}
+    res.pop("steps"), res.pop("warmup")
+    out.update(res)
     return out
 
 

@@ -104,6 +104,11 @@ SIGNATURES = {
     "evm_dist_init": (_i, [_vp, _vp, _i, _i, C.POINTER(_vp)]),
     "evm_dist_free": (None, [_vp, _vp]),
     "evm_dist_info": (_i, [_vp, C.POINTER(_i), C.POINTER(_i)]),
+    "evm_dist_hub_new": (_i, [_i, C.POINTER(_vp)]),
+    "evm_dist_hub_free": (None, [_vp]),
+    "evm_dist_hub_abort": (None, [_vp]),
+    "evm_dist_init_loopback": (_i, [_vp, _vp, _i, C.POINTER(_vp)]),
+    "evm_dist_directory": (_i, [_vp, _vp, _vp, _sz, _sz, _u32, _vp, _vp, C.POINTER(_u32)]),
     "evm_dist_route": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, C.POINTER(C.c_uint64)]),
     "evm_dist_take": (_i, [_vp, _vp, _u32, _vp, _sz, _vp, _vp, _vp, C.c_uint64, _vp]),
     "evm_dist_gather_roots": (_i, [_vp, _vp, _vp, _u32, _u32, _vp, _vp]),

@@ -20,18 +20,28 @@ def _newest(paths):
     return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
 
 
-def build_lib(force: bool = False, verbose: bool = False) -> str:
-    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "evm.h")]
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest(deps):
-        return LIB
+# synthetic streams on the device (bench / test input; not part of libevm)
+SYNTH_LIB = os.path.join(HERE, "libevmsynth.so")
+SYNTH_SOURCES = ["evm_synth.hip"]
+
+
+def _build(lib, sources, headers, extra, force, verbose):
+    srcs = [os.path.join(CSRC, s) for s in sources]
+    deps = srcs + [os.path.join(CSRC, h) for h in headers] + [os.path.join(INCLUDE, "evm.h")]
+    if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _newest(deps):
+        return lib
     cmd = [HIPCC, "-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function", "-I" + INCLUDE] + srcs + ["-ldl", "-o", LIB + ".tmp"]
+           "-Wno-unused-function", "-I" + INCLUDE] + srcs + extra + ["-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> str:
+    _build(SYNTH_LIB, SYNTH_SOURCES, ["evm_device.hpp"], [], force, verbose)
+    return _build(LIB, SOURCES, HEADERS, ["-ldl"], force, verbose)
 
 
 if __name__ == "__main__":

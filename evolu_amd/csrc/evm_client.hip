@@ -999,42 +999,131 @@ __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* 
 // tc path (the default streaming path).  Against its cell's running max t, a
 // message's applyMessages decisions need only tc = millis << 16 | counter:
 //     tc_i > tc(t): upsert + XOR        tc_i < tc(t): XOR only
-// and only tc_i == tc(t) needs the node ranks (a tie: equal millis and counter
-// from two nodes, or a redelivery of the cell's current max).  The tc path
-// decides everything from tc and reports ties; a batch with a tie is redone by
-// the exact walk path above (which carries the full order key).
+// and only tc_i == tc(t) needs the node chars (a tie: equal millis and counter
+// from two nodes, or a redelivery of the cell's current max).  Every running
+// max is therefore carried as (tc, row) -- the row that holds it, or the
+// prior max, or none -- and a tie compares the two timestamps' node ranks,
+// read from the rows' bytes (applyMessages.ts:93 `t < timestamp`, :105
+// `t !== timestamp`, string order).
 //   TP1 k_tp_pack : K1 (parse, canonical check, murmur3, minute) + per (range,
-//                   cell) max tc in LDS -- order-free (ds_max_u64), so pass 1
-//                   of the walks disappears into the parse
+//                   cell) the max tc in LDS and its row; cells where two rows
+//                   share that max (or the row record raced) are resolved by
+//                   node rank in a short rescan of the range
 //   TP2 carry     : per cell, exclusive max over the ranges seeded with the
-//                   prior max; the cell's final max
+//                   prior max; the cell's final max -> its winner (the first
+//                   occurrence of the final max key, applyMessages.ts:93)
 //   TP3 k_tp_walk : a workgroup per range: rows below their cell's running max
 //                   decided on the spot; the rest walked in batch order (LDS
-//                   state) -> flags; the message that reaches the cell's final
-//                   max is its winner (the last upsert)
+//                   state) -> flags
 // Bytes per message: TP1 46 + 4 in, 16 out; TP3 12 in, 1 out.
 // ============================================================================
 constexpr u64 TP_INVALID = ~0ull;  // tc of a message the walk skips (invalid timestamp or cell id)
 constexpr int TP_THREADS = 256;
 constexpr int TP_RANGES = 2048;  // ~8 ranges per CU: TP1's occupancy
+constexpr u32 TP_RANGE_MAX = 65280;  // rows per range: TP1 keeps a row as a 16-bit offset
+constexpr u32 ROW_NONE = 0xffffffffu;   // no max (SQL NULL: below every timestamp)
+constexpr u32 ROW_PRIOR = 0xfffffffeu;  // the max is the caller's prior row of the cell
+constexpr u32 TP_MATCH_MAX = 512;       // TP1 rescan: rows tied at a cell's range max
+
+// Node ranks (OKey rh, rl) of a batch row: chars 30..45 of its timestamp.
+struct NodeSrc {
+  const uint8_t* ts;
+  size_t stride;
+  const evm_rec* prior;  // per cell (ROW_PRIOR)
+};
+__device__ __forceinline__ void node_ranks_of(const NodeSrc& N, u32 c, u32 row, u64* rh, u32* rl) {
+  if (row == ROW_PRIOR) {
+    const evm_rec& p = N.prior[c];
+    node_rank(p.node, p.meta & EVM_META_CASEMASK, rh, rl);
+    return;
+  }
+  const uint8_t* s = N.ts + (size_t)row * N.stride;
+  u32 w[5];  // words 7..11 of the string (bytes 28..47; 46, 47 unused)
+  if ((N.stride & 3) == 0 && N.stride >= 48) {
+    const u32* p = reinterpret_cast<const u32*>(s + 28);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) w[k] = p[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      u32 x = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (28 + 4 * k + j < 46) x |= (u32)s[28 + 4 * k + j] << (8 * j);
+      w[k] = x;
+    }
+  }
+  u64 h = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) h = (h << 20) | swar_rank20((w[k] >> 16) | (w[k + 1] << 16));
+  *rh = h;
+  *rl = swar_rank20((w[3] >> 16) | (w[4] << 16));
+}
+
+// A carried max: (tc, row).  Order = the timestamps' string order; ROW_NONE
+// below everything; equal timestamps: the earlier one (prior, then the lower
+// row) -- so the carried row of the final max is the first occurrence.
+struct TK {
+  u64 tc;
+  u32 row;
+};
+__device__ __forceinline__ int tk_cmp(const NodeSrc& N, u32 c, const TK& a, const TK& b) {
+  if (a.row == ROW_NONE) return b.row == ROW_NONE ? 0 : -1;
+  if (b.row == ROW_NONE) return 1;
+  if (a.tc != b.tc) return a.tc < b.tc ? -1 : 1;
+  if (a.row == b.row) return 0;
+  u64 ha, hb;
+  u32 la, lb;
+  node_ranks_of(N, c, a.row, &ha, &la);
+  node_ranks_of(N, c, b.row, &hb, &lb);
+  if (ha != hb) return ha < hb ? -1 : 1;
+  if (la != lb) return la < lb ? -1 : 1;
+  return 0;
+}
+__device__ __forceinline__ u32 tk_earlier(u32 a, u32 b) {
+  if (a == ROW_PRIOR || b == ROW_PRIOR) return ROW_PRIOR;
+  return a < b ? a : b;
+}
+__device__ __forceinline__ TK tk_max(const NodeSrc& N, u32 c, const TK& a, const TK& b) {
+  const int k = tk_cmp(N, c, a, b);
+  if (k > 0) return a;
+  if (k < 0) return b;
+  return TK{a.tc, tk_earlier(a.row, b.row)};
+}
+__device__ __forceinline__ TK shfl_tk(const TK& k, int src) {
+  TK o;
+  o.tc = ((u64)(u32)__shfl((int)(u32)(k.tc >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)k.tc, src, 64);
+  o.row = (u32)__shfl((int)k.row, src, 64);
+  return o;
+}
 
 template <bool S48>
-__global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
+__global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
                                                         const u32* __restrict__ cell, u32 C, size_t range_len,
                                                         u64* __restrict__ tcs, u32* __restrict__ hash,
                                                         u32* __restrict__ minute, u64* __restrict__ agg,
-                                                        Info* __restrict__ info, u32* __restrict__ zero_buf,
-                                                        u32 zero_n) {
-  extern __shared__ __attribute__((aligned(16))) u64 cmax[];  // [C] max tc per cell of this range
+                                                        u32* __restrict__ arow, Info* __restrict__ info,
+                                                        u32* __restrict__ zero_buf, u32 zero_n) {
+  // LDS: [C] max tc per cell of this range, [C] its row (16-bit offset),
+  // [ceil(C/32)] cells to resolve (two rows at the max, or a raced row record)
+  extern __shared__ __attribute__((aligned(16))) u64 cmax[];
+  uint16_t* crow = reinterpret_cast<uint16_t*>(cmax + C);
+  u32* cfix = reinterpret_cast<u32*>(crow + ((C + 1) & ~1u));
   // (the cross-cell check's bucket cursors, cleared here instead of by a
   // memset on the second stream, which forks after this kernel)
   if (blockIdx.x == 0)
     for (u32 k = threadIdx.x; k < zero_n; k += TP_THREADS) zero_buf[k] = 0u;
   __shared__ uint4 stage[TP_THREADS / 64][192];
+  __shared__ u32 nmatch;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const size_t g = blockIdx.x;
   const size_t beg = g * range_len, end = min(n, beg + range_len);
-  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) cmax[c] = 0;
+  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
+    cmax[c] = 0;
+    crow[c] = 0xffffu;
+  }
+  for (u32 k = threadIdx.x; k < (C + 31) / 32; k += TP_THREADS) cfix[k] = 0;
+  if (threadIdx.x == 0) nmatch = 0;
   __syncthreads();
   u32 bad = 0, aux_bad = 0, mn = 0xffffffffu, mx = 0;
   for (size_t first = beg + 64 * wv; first < end; first += TP_THREADS) {  // wave-uniform
@@ -1066,7 +1155,18 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
       const bool ok = valid && ci < C;
       __builtin_nontemporal_store(ok ? p.tc : TP_INVALID, tcs + i);
       if (!ok) p.minute = 0xffffffffu;  // outside every fold window: the tc path folds without flags
-      if (ok) atomicMax(&cmax[ci], p.tc);
+      if (ok) {
+        const u64 old = atomicMax(&cmax[ci], p.tc);
+        bool fix = old == p.tc;  // a second row at the max so far (or a tc of 0)
+        if (old < p.tc) {
+          // this row raised the max: record it, then re-read the max -- if a
+          // later raise came in between, this record may have overwritten
+          // that row's, so the cell is resolved by the rescan
+          __hip_atomic_store(&crow[ci], (uint16_t)(i - beg), __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+          fix = __hip_atomic_load(&cmax[ci], __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP) != p.tc;
+        }
+        if (fix) atomicOr(&cfix[ci >> 5], 1u << (ci & 31));
+      }
       bad |= valid ? 0u : 1u;
       aux_bad |= ci < C ? 0u : 1u;
     }
@@ -1097,53 +1197,119 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
   }
   if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
   __syncthreads();
-  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) agg[g * C + c] = cmax[c];
+  bool any_fix = false;
+  for (u32 k = threadIdx.x; k < (C + 31) / 32; k += TP_THREADS) any_fix |= cfix[k] != 0;
+  if (__syncthreads_or(any_fix)) {
+    // rescan (rare): the rows of the cells to resolve that hold the cell's
+    // range max, with their node ranks, into LDS (the stage is free now) ...
+    struct Match {
+      u64 rh;
+      u32 rl, row, cell, pad;
+    };
+    Match* mt = reinterpret_cast<Match*>(&stage[0][0]);
+    static_assert(sizeof(stage) >= TP_MATCH_MAX * sizeof(Match), "match list fits the stage");
+    const NodeSrc N{ts, stride, nullptr};
+    for (size_t i = beg + threadIdx.x; i < end; i += TP_THREADS) {
+      const u64 t = __hip_atomic_load(tcs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // written above
+      if (t == TP_INVALID) continue;
+      const u32 ci = cell[i];
+      if (!((cfix[ci >> 5] >> (ci & 31)) & 1u) || t != cmax[ci]) continue;
+      const u32 k = atomicAdd(&nmatch, 1u);
+      if (k < TP_MATCH_MAX) {
+        Match m;
+        node_ranks_of(N, ci, (u32)i, &m.rh, &m.rl);
+        m.row = (u32)i;
+        m.cell = ci;
+        m.pad = 0;
+        mt[k] = m;
+      }
+    }
+    __syncthreads();
+    const u32 nm = nmatch;
+    if (nm > TP_MATCH_MAX) {
+      if (threadIdx.x == 0) atomicOr(&info->ties, 1u);  // too many: the exact walk path redoes the batch
+    } else {
+      // ... then per cell the best: highest node ranks, the lowest row among equals
+      for (u32 k = threadIdx.x; k < nm; k += TP_THREADS) {
+        const Match e = mt[k];
+        bool best = true;
+        for (u32 f = 0; f < nm && best; ++f) {
+          const Match o = mt[f];
+          if (f == k || o.cell != e.cell) continue;
+          best = !(o.rh > e.rh || (o.rh == e.rh && (o.rl > e.rl || (o.rl == e.rl && o.row < e.row))));
+        }
+        if (best) crow[e.cell] = (uint16_t)(e.row - beg);
+      }
+    }
+    __syncthreads();
+  }
+  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
+    agg[g * C + c] = cmax[c];
+    arow[g * C + c] = crow[c] == 0xffffu ? ROW_NONE : (u32)(beg + crow[c]);
+  }
   block_fold_bounds<u32, TP_THREADS>(mn, mx, bad, &info->minute_min, &info->minute_max, &info->bad);
 }
 
 // TP2: per cell, exclusive max over the G range maxima (3 phases over
-// CARRY_SEGS segments), seeded with the prior max; tfinal = the cell's max.
-__global__ void k_tp_carry_reduce(u32 C, size_t G, const u64* __restrict__ agg, u64* __restrict__ s_max) {
+// CARRY_SEGS segments), seeded with the prior max; the final max -> winner.
+__global__ void k_tp_carry_reduce(u32 C, size_t G, const u64* __restrict__ agg, const u32* __restrict__ arow,
+                                  NodeSrc N, u64* __restrict__ s_max, u32* __restrict__ s_row) {
   const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
   if (c >= C) return;
   const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
   const size_t a = p * per, e = min(G, a + per);
-  u64 m = 0;
+  TK m{0, ROW_NONE};
 #pragma unroll 8
-  for (size_t g = a; g < e; ++g) m = max(m, agg[g * C + c]);
-  s_max[(size_t)p * C + c] = m;
+  for (size_t g = a; g < e; ++g) {
+    const TK x{agg[g * C + c], arow[g * C + c]};
+    if (x.row == ROW_NONE) continue;
+    if (m.row == ROW_NONE || x.tc > m.tc) m = x;
+    else if (x.tc == m.tc) m = tk_max(N, c, m, x);  // (rare: equal tc in two ranges)
+  }
+  s_max[(size_t)p * C + c] = m.tc;
+  s_row[(size_t)p * C + c] = m.row;
 }
 
-__global__ __launch_bounds__(256) void k_tp_carry_segs(u32 C, u64* __restrict__ s_max,
-                                                       const evm_rec* __restrict__ prior,
-                                                       const uint8_t* __restrict__ prior_present,
-                                                       u64* __restrict__ tfinal) {
+__global__ __launch_bounds__(256) void k_tp_carry_segs(u32 C, u64* __restrict__ s_max, u32* __restrict__ s_row,
+                                                       NodeSrc N, const uint8_t* __restrict__ prior_present,
+                                                       int32_t* __restrict__ winner) {
   const u32 c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (c >= C) return;
   const size_t o = (size_t)lane * C + c;
-  u64 v = s_max[o];
+  TK v{s_max[o], s_row[o]};
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const u64 u = __shfl_up(v, d, 64);
-    if ((int)lane >= d) v = max(v, u);
+    const TK u = shfl_tk(v, (int)lane - d < 0 ? (int)lane : (int)lane - d);
+    if ((int)lane >= d) v = tk_max(N, c, u, v);
   }
-  const u64 seed = (prior_present && prior_present[c]) ? prior[c].tc : 0ull;
-  const u64 ex = __shfl_up(v, 1, 64);
-  s_max[o] = max(seed, lane == 0 ? 0ull : ex);
-  if (lane == 63) tfinal[c] = max(seed, v);
+  const TK seed = (prior_present && prior_present[c]) ? TK{N.prior[c].tc, ROW_PRIOR} : TK{0, ROW_NONE};
+  const TK ex = shfl_tk(v, lane == 0 ? 0 : (int)lane - 1);
+  const TK e = lane == 0 ? seed : tk_max(N, c, seed, ex);
+  s_max[o] = e.tc;
+  s_row[o] = e.row;
+  if (lane == 63) {
+    // the last upsert is the first occurrence of the final max (none if the
+    // prior max or nothing holds it)
+    const TK f = tk_max(N, c, seed, v);
+    winner[c] = (f.row == ROW_NONE || f.row == ROW_PRIOR) ? -1 : (int32_t)f.row;
+  }
 }
 
-__global__ void k_tp_carry_down(u32 C, size_t G, u64* __restrict__ agg, const u64* __restrict__ s_max) {
+__global__ void k_tp_carry_down(u32 C, size_t G, u64* __restrict__ agg, u32* __restrict__ arow, NodeSrc N,
+                                const u64* __restrict__ s_max, const u32* __restrict__ s_row) {
   const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
   if (c >= C) return;
   const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
   const size_t a = p * per, e = min(G, a + per);
-  u64 run = s_max[(size_t)p * C + c];
+  TK run{s_max[(size_t)p * C + c], s_row[(size_t)p * C + c]};
 #pragma unroll 8
   for (size_t g = a; g < e; ++g) {
-    const u64 here = agg[g * C + c];
-    agg[g * C + c] = run;
-    run = max(run, here);
+    const TK here{agg[g * C + c], arow[g * C + c]};
+    agg[g * C + c] = run.tc;
+    arow[g * C + c] = run.row;
+    if (here.row == ROW_NONE) continue;
+    if (run.row == ROW_NONE || here.tc > run.tc) run = here;
+    else if (here.tc == run.tc) run = tk_max(N, c, run, here);
   }
 }
 
@@ -1157,22 +1323,23 @@ __global__ void k_tp_carry_down(u32 C, size_t G, u64* __restrict__ agg, const u6
 // ORs its bit in, reads the mask back, clears it), each lane takes the max of
 // its lower peers (a wave prefix-max when the round is one cell), t =
 // max(running max, that) decides its flags, and the round's last peer of the
-// cell writes the new max.  An ascending stream makes every row a candidate
-// and costs one walk.
+// cell writes the new max.  Keys are (tc, row): equal tc compares node ranks
+// (tk_cmp), so a tie costs two 16-byte reads.  An ascending stream makes
+// every row a candidate and costs one walk.
 constexpr int TP_WAVES = TP_THREADS / 64;
 constexpr u32 TPC_ROWS = 64 * 4 * TP_WAVES;  // 4 rounds per wave per chunk
 
 __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ tcs, const u32* __restrict__ cell,
                                                         size_t n, u32 C, size_t range_len,
-                                                        const u64* __restrict__ carry, const u64* __restrict__ tfinal,
-                                                        uint8_t* __restrict__ flags, int32_t* __restrict__ winner,
-                                                        Info* __restrict__ info) {
+                                                        const u64* __restrict__ carry, const u32* __restrict__ crow,
+                                                        NodeSrc N, uint8_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) u64 tw_lds[];
-  u64* T = tw_lds;                                       // [C] running max per cell
+  u64* T = tw_lds;                                       // [C] running max per cell: tc
   u64* M = T + C;                                        // [C] the walk round's lanes per cell (zero between rounds)
   u64* cx = M + C;                                       // [TPC_ROWS] candidates: tc
   u32* ci = reinterpret_cast<u32*>(cx + TPC_ROWS);       // [TPC_ROWS] row index
   uint16_t* cc = reinterpret_cast<uint16_t*>(ci + TPC_ROWS);  // [TPC_ROWS] cell
+  u32* TR = reinterpret_cast<u32*>(cc + TPC_ROWS);       // [C] running max per cell: row
   __shared__ u32 seg[TP_WAVES];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const u64 lt = lanemask_lt();
@@ -1180,10 +1347,10 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
   const size_t beg = g * range_len, end = min(n, beg + range_len);
   for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
     T[c] = carry[g * C + c];
+    TR[c] = crow[g * C + c];
     M[c] = 0;
   }
   __syncthreads();
-  u32 tie = 0;
   for (size_t base = beg; base < end; base += TPC_ROWS) {
     // classify this wave's 256 rows; compact the candidates in batch order
     const size_t wb = base + 256 * wv;
@@ -1200,6 +1367,7 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
     for (int r = 0; r < 4; ++r) {
       const size_t i = wb + 64 * r + lane;
       const bool ok = x[r] != TP_INVALID;
+      // (a cell without a max yet: TR == ROW_NONE and T == 0, every row a candidate)
       const bool cand = ok && x[r] >= T[c[r]];
       if (i < end && !cand) flags[i] = ok ? (uint8_t)EVM_MSG_XOR : (uint8_t)EVM_MSG_BAD;
       const u64 bal = __ballot(cand);
@@ -1235,53 +1403,48 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
         }
         const bool ok = k < total;
         const u32 slot = 256 * sg + q;
-        const u64 xv = ok ? cx[slot] : 0ull;
+        const TK own{ok ? cx[slot] : 0ull, ok ? ci[slot] : ROW_NONE};
         const u32 cv = ok ? cc[slot] : 0u;
         if (ok) atomicOr(&M[cv], 1ull << lane);
         const u64 peers = ok ? __hip_atomic_load(&M[cv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0ull;
         if (ok) __hip_atomic_store(&M[cv], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         const u64 act = __ballot(ok);
-        u64 pm = 0;  // max tc of the lower lanes of the same cell
+        TK pm{0, ROW_NONE};  // max key of the lower lanes of the same cell
         if (peers == act && act == ~0ull) {
-          u64 v = xv;  // the round is one cell: exclusive wave prefix max
+          TK v = own;  // the round is one cell: exclusive wave prefix max
 #pragma unroll
           for (int d = 1; d < 64; d <<= 1) {
-            const u64 u = __shfl_up(v, d, 64);
-            if (lane >= d) v = max(v, u);
+            const TK u = shfl_tk(v, lane >= d ? lane - d : lane);
+            if (lane >= d) v = tk_max(N, cv, u, v);
           }
-          pm = __shfl_up(v, 1, 64);
-          if (lane == 0) pm = 0;
+          pm = shfl_tk(v, lane >= 1 ? lane - 1 : lane);
+          if (lane == 0) pm = TK{0, ROW_NONE};
         } else {
           u64 rem = peers & lt;
           while (__any(rem != 0)) {
             const int src = rem ? (int)__builtin_ctzll(rem) : lane;
-            const u64 v = __shfl(xv, src, 64);
+            const TK v = shfl_tk(own, src);
             if (rem) {
-              pm = max(pm, v);
+              pm = tk_max(N, cv, pm, v);
               rem &= rem - 1;
             }
           }
         }
         if (ok) {
-          const u64 t = max(T[cv], pm);
-          uint8_t fl;
-          if (xv > t) {  // applyMessages.ts:93 and :105 both hold
-            fl = EVM_MSG_UPS | EVM_MSG_XOR;
-            if (xv == tfinal[cv]) winner[cv] = (int32_t)ci[slot];  // reaches the final max: the last upsert
-          } else if (xv < t) {  // :105 only
-            fl = EVM_MSG_XOR;
-          } else {  // equal tc: the node ranks decide -> the exact path
-            fl = 0;
-            tie = 1;
+          const TK t = tk_max(N, cv, TK{T[cv], TR[cv]}, pm);
+          const int k3 = tk_cmp(N, cv, own, t);
+          // applyMessages.ts:93 `t < timestamp` -> upsert; :105 `t !== timestamp` -> INSERT + XOR
+          flags[own.row] = k3 > 0 ? (uint8_t)(EVM_MSG_UPS | EVM_MSG_XOR) : k3 < 0 ? (uint8_t)EVM_MSG_XOR : (uint8_t)0;
+          if ((peers >> lane) == 1ull) {  // the round's last peer of the cell
+            const TK nt = k3 > 0 ? own : t;
+            T[cv] = nt.tc;
+            TR[cv] = nt.row;
           }
-          flags[ci[slot]] = fl;
-          if ((peers >> lane) == 1ull) T[cv] = max(t, xv);  // the round's last peer of the cell
         }
       }
     }
     __syncthreads();
   }
-  if (__ballot(tie) && lane == 0) atomic_or_if(&info->ties, 1u);
 }
 
 // ============================================================================
@@ -1404,6 +1567,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   size_t range, G;
   if (TC) {
     range = std::max<size_t>(1024, ((n + TP_RANGES - 1) / TP_RANGES + 255) / 256 * 256);
+    range = std::min<size_t>(range, TP_RANGE_MAX);  // (TP1 records rows as 16-bit offsets)
   } else {
     range = (n + CL_RANGE_TARGET - 1) / CL_RANGE_TARGET;
     range = std::max<size_t>(2048, (range + 255) / 256 * 256);
@@ -1413,6 +1577,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   u32* rl = nullptr;
   u64* tcs = nullptr;
   u64* agg = nullptr;
+  u32* arow = nullptr;
   u64* a_tc = nullptr;
   u64* a_rh = nullptr;
   u32* a_rl = nullptr;
@@ -1420,16 +1585,17 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   if (TC) {
     tcs = S.alloc<u64>(n);
     agg = S.alloc<u64>(G * C);
-    if (!tcs || !agg) return EVM_ENOMEM;
-    // TP1: parse + per (range, cell) max tc, one workgroup per range
+    arow = S.alloc<u32>(G * C);
+    if (!tcs || !agg || !arow) return EVM_ENOMEM;
+    // TP1: parse + per (range, cell) max tc and its row, one workgroup per range
     evm::ProfScope ps_(ctx, "k_tp_pack");
-    const size_t lds = (size_t)C * 8;
+    const size_t lds = (size_t)C * 8 + (size_t)((C + 1) & ~1u) * 2 + (size_t)((C + 31) / 32) * 4;
     if (s48)
       hipLaunchKernelGGL(k_tp_pack<true>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, minute, agg, info, xcur, 1u << xp_geom(n).kb);
+                         cell, C, range, tcs, hash, minute, agg, arow, info, xcur, 1u << xp_geom(n).kb);
     else
       hipLaunchKernelGGL(k_tp_pack<false>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, minute, agg, info, xcur, 1u << xp_geom(n).kb);
+                         cell, C, range, tcs, hash, minute, agg, arow, info, xcur, 1u << xp_geom(n).kb);
   } else {
     key = S.alloc<uint4>(n);
     rl = S.alloc<u32>(n);
@@ -1523,15 +1689,18 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   if (TC) {
     // TP2: per cell, exclusive max over the ranges (in place in agg) + final max
     u64* s_max = S.alloc<u64>((size_t)CARRY_SEGS * C);
-    u64* tfinal = S.alloc<u64>(C);
-    if (!s_max || !tfinal) return EVM_ENOMEM;
+    u32* s_row = S.alloc<u32>((size_t)CARRY_SEGS * C);
+    if (!s_max || !s_row) return EVM_ENOMEM;
+    const NodeSrc N{(const uint8_t*)ts, stride, prior};
     const u32 cb = (C + 63) / 64;
-    KLAUNCH(k_tp_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, (const u64*)agg, s_max);
-    KLAUNCH(k_tp_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_max, prior, prior_present, tfinal);
-    KLAUNCH(k_tp_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, agg, (const u64*)s_max);
-    // TP3: flags + winners, a workgroup per range
-    KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14, (const u64*)tcs, cell,
-                n, C, range, (const u64*)agg, (const u64*)tfinal, flags, winner, info);
+    KLAUNCH(k_tp_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, (const u64*)agg, (const u32*)arow, N, s_max,
+            s_row);
+    KLAUNCH(k_tp_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_max, s_row, N, prior_present, winner);
+    KLAUNCH(k_tp_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, agg, arow, N, (const u64*)s_max,
+            (const u32*)s_row);
+    // TP3: flags, a workgroup per range
+    KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14 + (size_t)C * 4,
+                (const u64*)tcs, cell, n, C, range, (const u64*)agg, (const u32*)arow, N, flags);
   } else {
     // pass 1: per range and cell, the max timestamp and its first index
     KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,

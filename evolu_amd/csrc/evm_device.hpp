@@ -287,6 +287,59 @@ __host__ __device__ __forceinline__ Parsed parse_ts46(const u32 (&w)[12]) {
   return p;
 }
 
+// The inverse of parse_ts46 on the native domain: timestamp.ts:43-48
+// timestampToString of (tc, node, case mask) as 12 little-endian words
+// (bytes 46-47 zero).  Proleptic Gregorian civil date of the day count.
+__host__ __device__ __forceinline__ void put_byte(u32 (&w)[12], int i, u32 c) {
+  w[i >> 2] |= (c & 0xffu) << (8 * (i & 3));
+}
+__host__ __device__ __forceinline__ void put_dec(u32 (&w)[12], int at, u32 v, int digits) {
+  for (int k = digits - 1; k >= 0; --k) {
+    put_byte(w, at + k, 0x30u + v % 10u);
+    v /= 10u;
+  }
+}
+__host__ __device__ __forceinline__ void format_ts46(u64 tc, u64 node, u32 cmask, u32 (&w)[12]) {
+  for (int k = 0; k < 12; ++k) w[k] = 0;
+  const u64 ms = tc >> 16;
+  const u32 ctr = (u32)(tc & 0xffffu);
+  const u64 days = ms / 86400000ull;
+  const u32 rem = (u32)(ms - days * 86400000ull);
+  const u64 z = days + 719468ull;
+  const u64 era = z / 146097ull;
+  const u32 doe = (u32)(z - era * 146097ull);
+  const u32 yoe = (doe - doe / 1460u + doe / 36524u - doe / 146096u) / 365u;
+  const u32 doy = doe - (365u * yoe + yoe / 4u - yoe / 100u);
+  const u32 mp = (5u * doy + 2u) / 153u;
+  const u32 d = doy - (153u * mp + 2u) / 5u + 1u;
+  const u32 m = mp < 10u ? mp + 3u : mp - 9u;
+  const u32 y = (u32)(yoe + era * 400ull) + (m <= 2u ? 1u : 0u);
+  put_dec(w, 0, y, 4);
+  put_byte(w, 4, '-');
+  put_dec(w, 5, m, 2);
+  put_byte(w, 7, '-');
+  put_dec(w, 8, d, 2);
+  put_byte(w, 10, 'T');
+  put_dec(w, 11, rem / 3600000u, 2);
+  put_byte(w, 13, ':');
+  put_dec(w, 14, rem / 60000u % 60u, 2);
+  put_byte(w, 16, ':');
+  put_dec(w, 17, rem / 1000u % 60u, 2);
+  put_byte(w, 19, '.');
+  put_dec(w, 20, rem % 1000u, 3);
+  put_byte(w, 23, 'Z');
+  put_byte(w, 24, '-');
+  for (int k = 0; k < 4; ++k) {
+    const u32 v = (ctr >> (12 - 4 * k)) & 15u;
+    put_byte(w, 25 + k, v < 10u ? 0x30u + v : 0x37u + v);  // upper-case hex counter
+  }
+  put_byte(w, 29, '-');
+  for (int k = 0; k < 16; ++k) {
+    const u32 v = (u32)(node >> (60 - 4 * k)) & 15u;
+    put_byte(w, 30 + k, v < 10u ? 0x30u + v : (((cmask >> k) & 1u) ? 0x37u : 0x57u) + v);
+  }
+}
+
 // Loads the 46 significant bytes of timestamp i into 12 words.
 __device__ __forceinline__ void load_ts(const uint8_t* __restrict__ base, size_t stride, size_t i, u32 (&w)[12]) {
   const uint8_t* s = base + i * stride;

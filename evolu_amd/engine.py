@@ -269,7 +269,22 @@ class Pending:
         self.keep = keep
         self.n_cells = n_cells
 
+    def __del__(self):
+        # dropped without a wait (e.g. an exception between enqueue and wait):
+        # wait anyway, so the handle is released and no tensor the batch still
+        # reads or writes goes back to the caching allocator early
+        try:
+            if self.h is not None and self.eng.h:
+                t = C.c_void_p()
+                if self.eng.lib.evm_apply_wait(self.eng.h, self.h, C.byref(t)) == _lib.EVM_OK and t.value:
+                    self.eng.lib.evm_tree_free(self.eng.h, t)
+                self.h = None
+        except Exception:
+            pass
+
     def wait(self, raise_on_error: bool = True):
+        if self.h is None:
+            raise RuntimeError("evm_apply_wait: this batch was already waited")
         t = C.c_void_p()
         st = self.eng.lib.evm_apply_wait(self.eng.h, self.h, C.byref(t))
         self.h = None
@@ -466,21 +481,94 @@ def dist_unique_id() -> bytes:
     return bytes(buf)
 
 
-class Dist:
-    """Owner sharding over RCCL (evm_dist_*): one per Engine, collective calls
-    in the same order on every rank."""
+class DistHub:
+    """In-process rendezvous of `world` loopback ranks (evm_dist_hub): one
+    Engine + Dist per rank, each driven by its own host thread."""
 
-    def __init__(self, eng: Engine, uid: bytes, rank: int, world: int):
-        if len(uid) != _lib.DIST_ID_BYTES:
-            raise ValueError("unique id must be %d bytes" % _lib.DIST_ID_BYTES)
+    def __init__(self, world: int):
+        self.lib = _lib.load()
+        self.world = world
+        h = C.c_void_p()
+        check(self.lib.evm_dist_hub_new(world, C.byref(h)), "evm_dist_hub_new")
+        self.h = h
+
+    def abort(self):
+        """A rank failed: its peers' pending and later collectives return EVM_EDIST."""
+        if getattr(self, "h", None):
+            self.lib.evm_dist_hub_abort(self.h)
+
+    def free(self):
+        if getattr(self, "h", None):
+            self.lib.evm_dist_hub_free(self.h)
+            self.h = None
+
+
+def run_loopback(world: int, fn, device: int = 0):
+    """fn(rank, eng, dist) on `world` loopback ranks: one thread, Engine (on its
+    own HIP stream) and Dist per rank over one DistHub on `device`.  Returns
+    the ranks' results; raises if any rank raised (the others' collectives
+    are aborted rather than left waiting)."""
+    import threading
+
+    hub = DistHub(world)
+    results, errors = [None] * world, []
+
+    def run(r):
+        eng = dd = None
+        try:
+            torch.cuda.set_device(device)
+            s = torch.cuda.Stream(device)
+            with torch.cuda.stream(s):
+                eng = Engine(device)
+                dd = Dist(eng, None, r, world, hub=hub)
+                dd.transport = "loopback hub (%d threads, 1 GPU)" % world
+                results[r] = fn(r, eng, dd)
+                torch.cuda.synchronize(device)
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            errors.append((r, e))
+            hub.abort()
+        finally:
+            if dd is not None:
+                dd.free()
+            if eng is not None:
+                eng.close()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    hub.free()
+    if errors:
+        r, e = sorted(errors, key=lambda x: x[0])[0]
+        raise RuntimeError("loopback rank %d failed: %r" % (r, e)) from e
+    return results
+
+
+class Dist:
+    """Owner sharding (evm_dist_*): one per Engine, collective calls in the
+    same order on every rank.  Over RCCL (uid from dist_unique_id), or over a
+    DistHub (loopback ranks in one process)."""
+
+    def __init__(self, eng: Engine, uid: Optional[bytes], rank: int, world: int, hub: Optional[DistHub] = None):
         self.eng = eng
         self.rank, self.world = rank, world
         h = C.c_void_p()
-        buf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
-        check(eng.lib.evm_dist_init(eng.h, buf, rank, world, C.byref(h)), "evm_dist_init")
+        if hub is not None:
+            if hub.world != world:
+                raise ValueError("hub world %d != %d" % (hub.world, world))
+            check(eng.lib.evm_dist_init_loopback(eng.h, hub.h, rank, C.byref(h)), "evm_dist_init_loopback")
+        else:
+            if len(uid) != _lib.DIST_ID_BYTES:
+                raise ValueError("unique id must be %d bytes" % _lib.DIST_ID_BYTES)
+            buf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+            check(eng.lib.evm_dist_init(eng.h, buf, rank, world, C.byref(h)), "evm_dist_init")
         self.h = h
+        self.transport = "loopback hub" if hub is not None else "RCCL"
         self.n_recv = 0
         self.stride = TS_STRIDE
+        self.n_local = None  # owners this rank serves (after directory())
+        self.n_dir = 0
 
     def free(self):
         if getattr(self, "h", None):
@@ -492,6 +580,25 @@ class Dist:
             self.free()
         except Exception:
             pass
+
+    def directory(self, ids: torch.Tensor):
+        """Owner directory from userId strings (uint8 [n_owners, stride] device
+        rows, every id id_len = stride bytes unless given as (rows, id_len)):
+        owner g -> rank murmur3(userId_g) % world, dense local ids.  Returns
+        (dest uint8[n], local int32[n]) on the device; sets self.n_local."""
+        if isinstance(ids, tuple):
+            ids, id_len = ids
+        else:
+            id_len = ids.shape[1]
+        n, stride = ids.shape
+        dest = torch.empty(max(n, 1), dtype=torch.uint8, device=ids.device)
+        local = torch.empty(max(n, 1), dtype=torch.int32, device=ids.device)
+        nl = C.c_uint32()
+        check(self.eng.lib.evm_dist_directory(self.eng.h, self.h, _ptr(ids), stride, id_len, n, _ptr(dest),
+                                              _ptr(local), C.byref(nl)), "evm_dist_directory")
+        self.n_local = nl.value
+        self.n_dir = n
+        return dest[:n], local[:n]
 
     def route(self, ts: torch.Tensor, owner: torch.Tensor, aux: Optional[torch.Tensor] = None,
               dest: Optional[torch.Tensor] = None) -> int:

@@ -204,6 +204,162 @@ def config5(n_owners: int, n: int, zipf_s: float = 1.2, cells_per_owner: int = 5
     return ts, owner.astype(np.uint32), cell.astype(np.uint32)
 
 
+# ---------------------------------------------------------------------------
+# Config 4 (1B messages over 1M owners, sharded by murmur3(userId) mod G):
+# generated on the device by libevmsynth.so (evolu_amd/csrc/evm_synth.hip);
+# this is its numpy twin (same bytes), for tests and small cases.
+# ---------------------------------------------------------------------------
+C4_SPAN = 30 * DAY_MS
+C4_PERM_A = 1000003
+_U = np.uint64
+
+
+def _sm(x):
+    with np.errstate(over="ignore"):
+        z = x + _U(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> _U(30))) * _U(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> _U(27))) * _U(0x94D049BB133111EB)
+        return z ^ (z >> _U(31))
+
+
+def _H(seed, t, x, y):
+    x = np.asarray(x).astype(np.uint64)
+    y = np.asarray(y).astype(np.uint64)
+    s = _sm(np.full(1, seed, dtype=np.uint64) ^ _U(t))
+    return _sm(_sm(s ^ x) ^ y)
+
+
+def config4_shape(P: int):
+    slots = max(1, ((P + 3) // 4 + 1) // 2)
+    return slots, C4_SPAN // slots, slots * 9 // 10
+
+
+def _hex16(v: np.ndarray) -> np.ndarray:
+    sh = np.arange(60, -1, -4, dtype=np.uint64)
+    return HEX[((v[:, None] >> sh[None, :]) & _U(15)).astype(np.int64)]
+
+
+def config4_owner_ids(seed: int, n: int) -> np.ndarray:
+    """userId strings of owners 0..n-1: (n, 21) uint8, lower-case hex."""
+    o = np.arange(n, dtype=np.uint64)
+    a = _H(seed, 1, o, 0)
+    b = _H(seed, 1, o, 1) >> _U(44)
+    tail = HEX[((b[:, None] >> np.arange(16, -1, -4, dtype=np.uint64)[None, :]) & _U(15)).astype(np.int64)]
+    return np.concatenate([_hex16(a), tail], 1)
+
+
+def config4_messages(seed: int, P: int, o: np.ndarray, j: np.ndarray):
+    """Message j of owner o -> (ts rows (n, 48), keep bool)."""
+    slots, gap, keep_slots = config4_shape(P)
+    o = np.asarray(o, dtype=np.int64)
+    j = np.asarray(j, dtype=np.int64)
+    q, k = j & 3, j >> 2
+    slot, ctr = k >> 1, k & 1
+    h = _H(seed, 3, o, (q << 16) | slot)
+    millis = BENCH_T0 + slot * gap + (h % _U(gap)).astype(np.int64)
+    node = _hex16(_H(seed, 2, o, q))
+    return format_timestamps(millis, ctr, node, 48), slot < keep_slots
+
+
+def config4_source(seed: int, O: int, P: int, G: int, s: int):
+    """Source rank s of G: (ts, owner u32, keep) -- twin of evs_config4_source."""
+    m = (P - s + G - 1) // G
+    r = np.arange(O * m, dtype=np.int64)
+    p, t = r // m, r % m
+    o = (p * C4_PERM_A + seed % O) % O
+    ts, keep = config4_messages(seed, P, o, s + t * G)
+    return ts, o.astype(np.uint32), keep
+
+
+def config4_owners(seed: int, P: int, G: int, owners: np.ndarray):
+    """All P messages of each owner, source-major for G sources (the order a
+    rank receives them): (ts, list index u32, keep) -- twin of evs_config4_owners."""
+    owners = np.asarray(owners, dtype=np.int64)
+    js = np.concatenate([np.arange(s, P, G) for s in range(G)])
+    o = np.repeat(owners, P)
+    j = np.tile(js, len(owners))
+    ts, keep = config4_messages(seed, P, o, j)
+    return ts, np.repeat(np.arange(len(owners), dtype=np.uint32), P), keep
+
+
+class DeviceSynth:
+    """libevmsynth.so: the config-4 generator on the device (torch tensors)."""
+
+    def __init__(self):
+        import ctypes as C
+        import os
+
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libevmsynth.so")
+        if not os.path.exists(path):
+            raise RuntimeError("libevmsynth.so not built (%s)" % path)
+        import torch  # noqa: F401  (one HIP runtime in the process)
+
+        self.C = C
+        L = C.CDLL(path)
+        vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+        L.evs_config4_source.argtypes = [vp, u64, u32, u32, u32, u32, vp, vp, vp]
+        L.evs_config4_owners.argtypes = [vp, u64, u32, u32, u32, vp, u32, vp, vp, vp]
+        L.evs_owner_ids.argtypes = [vp, u64, u32, C.c_size_t, vp]
+        self.L = L
+
+    @staticmethod
+    def _p(t):
+        import ctypes as C
+
+        return None if t is None else C.c_void_p(t.data_ptr())
+
+    def _stream(self, dev):
+        import torch
+
+        return self.C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+    def source(self, seed: int, O: int, P: int, G: int, s: int, dev, keep: bool = False):
+        import torch
+
+        m = (P - s + G - 1) // G
+        n = O * m
+        ts = torch.empty((n, 48), dtype=torch.uint8, device=dev)
+        owner = torch.empty(n, dtype=torch.int32, device=dev)
+        kp = torch.empty(n, dtype=torch.uint8, device=dev) if keep else None
+        if self.L.evs_config4_source(self._stream(dev), seed, O, P, G, s, self._p(ts), self._p(owner), self._p(kp)):
+            raise ValueError("evs_config4_source: bad arguments")
+        return ts, owner, kp
+
+    def owners(self, seed: int, O: int, P: int, G: int, owners, dev):
+        import torch
+
+        lst = owners.to(device=dev, dtype=torch.int32).contiguous()
+        n = lst.numel() * P
+        ts = torch.empty((max(n, 1), 48), dtype=torch.uint8, device=dev)
+        li = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        kp = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        if self.L.evs_config4_owners(self._stream(dev), seed, O, P, G, self._p(lst), lst.numel(), self._p(ts),
+                                     self._p(li), self._p(kp)):
+            raise ValueError("evs_config4_owners: bad arguments")
+        return ts[:n], li[:n], kp[:n]
+
+    def owner_ids(self, seed: int, n: int, dev, stride: int = 24):
+        import torch
+
+        out = torch.empty((max(n, 1), stride), dtype=torch.uint8, device=dev)
+        if self.L.evs_owner_ids(self._stream(dev), seed, n, stride, self._p(out)):
+            raise ValueError("evs_owner_ids: bad arguments")
+        return out[:n]
+
+
+def client_adversarial(n: int = 10_000_000, n_cells: int = 1000, n_nodes: int = 64, stride: int = 48,
+                       seed_config: int = 5):
+    """BASELINE config 5 on the client side: ONE owner's applyMessages batch
+    with config 5's adversarial structure (config5 above with one owner):
+    millis on a coarse shared grid (equal-millis bursts across nodes: counter
+    and node tie-breaks), 10 % redeliveries (half after a newer write to the
+    cell: the stale XOR toggle; the rest exact copies of the cell max: ties),
+    ~1 % upper-case nodes.  Returns (ts arena, cell u32)."""
+    ts, _, cell = config5(1, n, cells_per_owner=n_cells, nodes_per_owner=n_nodes, stride=stride,
+                          seed_config=seed_config)
+    return ts, cell
+
+
 NANOID = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789_-", dtype=np.uint8)
 
 # examples/nextjs/pages/index.tsx:23-34 + the common columns (types.ts:194-201)

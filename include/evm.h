@@ -354,43 +354,81 @@ int evm_pb_encode(int kind, const char* ts, size_t stride, const uint32_t* ts_le
 /* ------------------------------------------------------------------------
  * Multi-GPU owner sharding (evm_dist.hip).  One process per
  * GPU and one evm_dist per context; every call below is collective (all
- * ranks call it, in the same order) except evm_dist_take.  Owners are
- * independent in the whole path, so rank r serves the owners with
- * owner % world == r (dense owner ids the caller assigns, e.g. from
- * murmur3(ownerId)); as local owner owner / world.  Replaces nothing in the
- * reference (one process there); it is what lets the N-API caller run one
- * addon per GPU of a node.  RCCL (librccl.so.1) is opened at run time.
+ * ranks call it, in the same order) except evm_dist_take and
+ * evm_dist_directory.  Owners are independent in the whole path, so every
+ * owner lives on one rank: by default rank owner % world as local owner
+ * owner / world (dense owner ids the caller assigns); after
+ * evm_dist_directory, rank murmur3(userId) mod world with
+ * dense local ids.  Replaces nothing in the reference (one process there);
+ * it is what lets the N-API caller run one addon per GPU of a node.
+ *
+ * Failure: a rank that fails locally (bad argument, allocation) still joins
+ * every collective of the call, flagged, and then EVERY rank returns an
+ * error (the failing rank its own code, the others EVM_EDIST) -- no rank is
+ * left waiting in a receive.  Only a NULL ctx / d / n_recv returns at once.
+ *
+ * Transports: RCCL (librccl.so.1, opened at run time; evm_dist_init), or an
+ * in-process loopback hub (evm_dist_init_loopback): `world` contexts, one
+ * host thread each, device-to-device copies instead of xGMI -- the same
+ * partitions, count exchange, grouping and gathers, testable on one GPU.
  * ------------------------------------------------------------------------ */
 #define EVM_DIST_ID_BYTES 128
 typedef struct evm_dist evm_dist;
+typedef struct evm_dist_hub evm_dist_hub;
 /* a new communicator id (rank 0 makes it and hands it to the others) */
 int evm_dist_unique_id(uint8_t* id);
 /* collective: the communicator of `world` ranks (world <= 64) on ctx's device */
 int evm_dist_init(evm_ctx* ctx, const uint8_t* id, int rank, int world, evm_dist** out);
+/* loopback: a hub for `world` in-process ranks; each rank's thread calls
+ * evm_dist_init_loopback with its own context.  Free the hub after every
+ * evm_dist on it. */
+int evm_dist_hub_new(int world, evm_dist_hub** out);
+void evm_dist_hub_free(evm_dist_hub* hub);
+/* a rank's thread failed outside the library: every pending and later
+ * collective on the hub returns EVM_EDIST instead of waiting for it */
+void evm_dist_hub_abort(evm_dist_hub* hub);
+int evm_dist_init_loopback(evm_ctx* ctx, evm_dist_hub* hub, int rank, evm_dist** out);
 void evm_dist_free(evm_ctx* ctx, evm_dist* d);
 int evm_dist_info(const evm_dist* d, int* rank, int* world);
+/* local (every rank computes the same): the owner directory.  ids: device,
+ * n_owners userId strings of id_len bytes at `stride` (index = global owner
+ * id).  Owner g goes to rank murmur3(userId_g) mod world (MurmurHash3_x86_32,
+ * seed 0, the murmurhash@2.0.1 of timestamp.ts:87-88) as local id = its rank
+ * among that rank's owners in global order.  Afterwards evm_dist_route sends
+ * row i to the directory's rank of owner[i], evm_dist_take writes local ids,
+ * and evm_dist_gather_roots maps local roots back to global owners.
+ * Optional outputs (device): dest[n_owners], local[n_owners]; *n_local (host)
+ * = owners this rank serves.  n_owners == 0 removes the directory. */
+int evm_dist_directory(evm_ctx* ctx, evm_dist* d, const char* ids, size_t stride, size_t id_len, uint32_t n_owners,
+                       uint8_t* dest, uint32_t* local, uint32_t* n_local);
 /* collective: every row (device ts[n * stride], stride % 8 == 0; owner[n]
- * global owner ids; optional aux[n], e.g. the cell) goes to rank
- * dest ? dest[i] : owner[i] % world.  The received rows stay in the
- * context's staging buffer in (source rank, source order) -- the global
- * batch order when each rank's input is its slice of the batch in rank
- * order; *n_recv = their count (host).  A dest >= world: that row is
- * dropped and EVM_EINVAL returned after the exchange completed. */
+ * global owner ids; optional aux[n], e.g. the cell) goes to rank dest[i]
+ * (dest given), the directory's rank of owner[i], or owner[i] % world.  The
+ * received rows stay in the context's staging buffer in (source rank,
+ * source order) -- the global batch order when each rank's input is its
+ * slice of the batch in rank order; *n_recv = their count (host).  48-B rows
+ * travel as 32-B packed records (bytes 46-47, padding, arrive as zero)
+ * unless some row anywhere in the job is outside the native domain: then
+ * every rank sends raw records and every byte arrives.  A row whose
+ * destination is out of range is dropped and EVM_EINVAL returned on its
+ * rank after the exchange completed. */
 int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, const uint32_t* owner,
                    const uint32_t* aux, const uint8_t* dest, uint64_t* n_recv);
 /* local: the last route's rows into caller buffers (device): out_ts rows of
- * out_stride bytes, out_owner (global ids), optional out_aux and out_src
- * (source rank << 32 | index in that rank's input).  group == 0: in receive
- * order; 0 < group <= 64: grouped by local owner (owner / world < group),
- * receive order inside each group, group_off (host, group + 1) the bounds.
+ * out_stride bytes, out_owner (global ids; local ids with a directory),
+ * optional out_aux and out_src (source rank << 32 | index in that rank's
+ * input).  group == 0: in receive order; 0 < group <= 64: grouped by local
+ * owner (owner / world, or the directory's local id, < group), receive order
+ * inside each group, group_off (host, group + 1) the bounds.
  * cap < n_recv: EVM_ECAPACITY (the rows stay staged; take again). */
 int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_t out_stride, uint32_t* out_owner,
                   uint32_t* out_aux, uint64_t* out_src, uint64_t cap, uint64_t* group_off);
 /* collective: every owner's root over all ranks.  This rank's local owners
  * are the owners of trees[0..n_trees) in order (one tree set for all of
- * them, or one single-owner tree per owner); local owner j = global owner
- * j * world + rank, at most ceil(n_global / world) of them.  root/present:
- * device [n_owners_global]. */
+ * them, or one single-owner tree per owner): local owner j = global owner
+ * j * world + rank, at most ceil(n_global / world) of them -- or, with a
+ * directory (n_owners_global == its size), the directory's local ids.
+ * root/present: device [n_owners_global]. */
 int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* const* trees, uint32_t n_trees,
                           uint32_t n_owners_global, int32_t* root, uint8_t* present);
 

@@ -1,9 +1,10 @@
 """The streaming tc path of applyMessages (evm_client.hip TP1-TP3, the default
 for one owner with <= 2,048 cells): decisions from tc = millis << 16 |
-counter alone, a batch with a tie (equal tc against its cell's running max:
-equal millis + counter from two nodes, or a redelivery of the cell's max) redone
-by the exact walk path.  Checked against the oracle (applyMessages.ts:26-131,
-verbatim SQL) and, at BASELINE sizes, bit for bit against the sort path."""
+counter, and a tie (equal tc against its cell's running max: equal millis +
+counter from two nodes, or a redelivery of the cell's max) decided inside the
+walk by the two timestamps' node ranks -- no redo.  Checked against the
+oracle (applyMessages.ts:26-131, verbatim SQL), the C restatement at the
+headline's own stream and size, and bit for bit against the sort path."""
 import random
 
 import numpy as np
@@ -103,20 +104,22 @@ def test_tc_path_without_ties_vs_oracle(eng, seed):
     assert st == 0
     assert np.array_equal(flags, f) and np.array_equal(winner, w)
     assert tree.to_json(0) == O.merkle_tree_to_string(want)
-    assert ran == ({"tc": 0, "redo": 1} if tie else {"tc": 1, "redo": 0})
+    assert ran == {"tc": 1, "redo": 0}
 
 
 @pytest.mark.parametrize("seed", range(4))
 def test_tc_path_with_ties_and_case_vs_oracle(eng, seed):
     """Equal millis across nodes, mixed-case node ids, exact + stale
-    redeliveries: the tie is detected and the exact path answers."""
+    redeliveries: the ties are decided by node rank inside the walk."""
     msgs, cells = W.client_batch(700 + seed, n=800, n_cells=7)
-    st, flags, winner, tree, ran = _apply(eng, msgs, cells, 0)
+    st, flags, winner, tree, ran = _apply(eng, msgs, cells, 3)
     f, w, want, _ = _oracle(msgs, cells)
     assert st == 0
     assert np.array_equal(flags, f) and np.array_equal(winner, w)
     assert tree.to_json(0) == O.merkle_tree_to_string(want)
-    assert ran["redo"] == (1 if _has_tie(msgs) else 0)
+    assert ran == {"tc": 1, "redo": 0}
+    if seed == 0:
+        assert _has_tie(msgs)  # (the stream does exercise ties)
 
 
 def test_tc_path_prior_rows(eng):
@@ -133,15 +136,15 @@ def test_tc_path_prior_rows(eng):
     st, flags, winner, tree, ran = _apply(eng, msgs, cells, 3, prior=prior, tree_json=O.merkle_tree_to_string(t0))
     f, w, want, _ = _oracle(msgs, cells, prior)
     assert st == 0 and np.array_equal(flags, f) and np.array_equal(winner, w)
-    assert ran["tc"] + ran["redo"] == 1 and ran["redo"] == int(_has_tie(msgs, ptc))
+    assert ran == {"tc": 1, "redo": 0}
     assert tree.to_json(0) == O.merkle_tree_to_string(want)
-    # an exact redelivery of a prior max is a tie
+    # an exact redelivery of a prior max is a tie against the prior row: a no-op
     c0 = cells[0]
     msgs2 = msgs + [{"timestamp": prior[c0], "table": c0[0], "row": c0[1], "column": c0[2], "value": "dup"}]
     st, flags, winner, tree, ran = _apply(eng, msgs2, cells, 3, prior=prior)
     f, w, _, _ = _oracle(msgs2, cells, prior)
     assert st == 0 and np.array_equal(flags, f) and np.array_equal(winner, w)
-    assert ran["redo"] == 1
+    assert ran == {"tc": 1, "redo": 0} and _has_tie(msgs2, ptc)
 
 
 @pytest.mark.parametrize("cells", [1, 7, 1000, 2048])
@@ -261,3 +264,80 @@ def test_tc_path_ragged_size_keeps_dense_fold(eng, n):
     if st == L.EVM_OK:
         assert torch.equal(f1, f2) and torch.equal(w1, w2)
         assert t1.to_json(0) == t2.to_json(0)
+
+
+def test_tc_path_headline_stream_vs_c_oracle(eng):
+    """The stream and size bench.py times (BASELINE config 2: 10M messages,
+    1,000 cells, 64 nodes, seed 2) through the tc path only, bit for bit
+    against the C restatement of applyMessages: flags, winners, tree JSON."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+    from oracle import c_oracle as CO
+
+    ts_np, cell_np = synth.config2(10_000_000, 1000, seed_config=2)
+    st_w, f_w, w_w, js_w = CO.apply(ts_np, cell_np, 1000)
+    assert st_w == 0
+    eng.set_option(L.OPT_CLIENT_PATH, 3)
+    s0 = eng.stats()
+    flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), eng.dev(ts_np), eng.dev(cell_np), 1000)
+    s1 = eng.stats()
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    assert s1["tc_batches"] - s0["tc_batches"] == 1 and s1["tc_redos"] == s0["tc_redos"]
+    assert np.array_equal(flags.cpu().numpy(), f_w)
+    assert np.array_equal(winner.cpu().numpy(), w_w)
+    assert tree.to_json(0) == js_w
+
+
+@pytest.mark.parametrize("n,cells,nodes", [(2_000_000, 1000, 64), (1_000_000, 50, 4), (300_000, 1, 8)])
+def test_tc_path_adversarial_client_stream_vs_c_oracle(eng, n, cells, nodes):
+    """BASELINE config 5 on the client side: one owner, equal-millis bursts
+    (counter and node tie-breaks), 10 % redeliveries (half after a newer
+    write: the XOR toggle; the rest ties with the cell max), ~1 % upper-case
+    nodes.  Ties are decided inside the walk (no redo), bit for bit against
+    the C restatement."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+    from oracle import c_oracle as CO
+
+    ts_np, cell_np = synth.client_adversarial(n, cells, nodes, seed_config=5)
+    st_w, f_w, w_w, js_w = CO.apply(ts_np, cell_np, cells)
+    assert st_w == 0
+    eng.set_option(L.OPT_CLIENT_PATH, 3)
+    s0 = eng.stats()
+    flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), eng.dev(ts_np), eng.dev(cell_np), cells)
+    s1 = eng.stats()
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    assert s1["tc_batches"] - s0["tc_batches"] == 1 and s1["tc_redos"] == s0["tc_redos"]
+    assert np.array_equal(flags.cpu().numpy(), f_w)
+    assert np.array_equal(winner.cpu().numpy(), w_w)
+    assert tree.to_json(0) == js_w
+    assert ((f_w & L.MSG_XOR) == 0).sum() > 0  # the stream has exact redeliveries of cell maxima (ties)
+
+
+def test_tc_path_tie_list_overflow_redoes_exactly(eng):
+    """More than 512 rows of one range tied at a cell's range max (700 nodes
+    sending at the same millisecond, counter 0): TP1's list overflows and the
+    exact walk path answers -- the result is still exact."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    rng = np.random.default_rng(9)
+    n = 4096
+    ms = synth.BENCH_T0 + rng.integers(0, 10_000, n)
+    ms[100:800] = synth.BENCH_T0 + 50_000  # 700 rows, one millisecond, above everything else
+    nodes = synth.random_nodes(rng, n)
+    ts_np = synth.format_timestamps(ms, np.zeros(n, dtype=np.int64), nodes)
+    cell_np = np.zeros(n, dtype=np.uint32)
+    cell_np[::7] = 1
+    cell_np[100:800] = 0
+    from oracle import c_oracle as CO
+
+    st_w, f_w, w_w, js_w = CO.apply(ts_np, cell_np, 2)
+    eng.set_option(L.OPT_CLIENT_PATH, 3)
+    s0 = eng.stats()
+    flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), eng.dev(ts_np), eng.dev(cell_np), 2)
+    s1 = eng.stats()
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    assert s1["tc_redos"] - s0["tc_redos"] == 1
+    assert np.array_equal(flags.cpu().numpy(), f_w) and np.array_equal(winner.cpu().numpy(), w_w)
+    assert tree.to_json(0) == js_w
