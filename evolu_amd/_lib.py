@@ -94,6 +94,7 @@ SIGNATURES = {
     "evm_store_tree": (_vp, [_vp]),
     "evm_store_messages": (_i, [_vp, _vp, _vp, _vp]),
     "evm_server_ingest": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, C.c_uint64, _vp]),
+    "evm_server_ingest_ex": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, C.c_uint64, _vp, _vp]),
     "evm_pb_scan": (_i, [_i, _vp, _sz, _vp]),
     "evm_pb_split": (_i, [_i, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp]),
     "evm_pb_encode": (_i, [_i, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _sz, C.POINTER(_sz)]),

@@ -821,10 +821,9 @@ __global__ __launch_bounds__(XP_THREADS) void k_xp_dedup(const u64* __restrict__
 
 // Dense Merkle fold over [minute_min, minute_min + FOLD_MAXWIN * FOLD_WIN):
 // per (window, chunk) an LDS XOR histogram + presence bitmap.
-// FLAGS: fold the EVM_MSG_XOR messages; otherwise every message whose minute
-// is in range (the tc path: without a tie every valid message is XORed, and
-// K1 puts the others' minute out of range) -- so the fold need not wait for
-// the walk.
+// FLAGS: fold the EVM_MSG_XOR messages (both streaming paths); otherwise
+// every message whose minute is in range (valid only for a batch in which
+// every valid message is XORed).
 template <bool FLAGS>
 __global__ __launch_bounds__(FOLD_THREADS) void k_cl_fold_hist(const uint8_t* __restrict__ flags,
                                                               const u32* __restrict__ minute,
@@ -1150,23 +1149,13 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(7, 8
     }
     Parsed p = parse_ts46(w);  // (the node ranks it can compute are dead here)
     const bool valid = (p.meta & EVM_META_VALID) != 0;
+    u32 ci = 0;
+    bool ok = false;
     if (i < end) {
-      const u32 ci = __builtin_nontemporal_load(cell + i);
-      const bool ok = valid && ci < C;
+      ci = __builtin_nontemporal_load(cell + i);
+      ok = valid && ci < C;
       __builtin_nontemporal_store(ok ? p.tc : TP_INVALID, tcs + i);
-      if (!ok) p.minute = 0xffffffffu;  // outside every fold window: the tc path folds without flags
-      if (ok) {
-        const u64 old = atomicMax(&cmax[ci], p.tc);
-        bool fix = old == p.tc;  // a second row at the max so far (or a tc of 0)
-        if (old < p.tc) {
-          // this row raised the max: record it, then re-read the max -- if a
-          // later raise came in between, this record may have overwritten
-          // that row's, so the cell is resolved by the rescan
-          __hip_atomic_store(&crow[ci], (uint16_t)(i - beg), __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
-          fix = __hip_atomic_load(&cmax[ci], __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP) != p.tc;
-        }
-        if (fix) atomicOr(&cfix[ci >> 5], 1u << (ci & 31));
-      }
+      if (!ok) p.minute = 0xffffffffu;  // outside every fold window (and the minute bounds)
       bad |= valid ? 0u : 1u;
       aux_bad |= ci < C ? 0u : 1u;
     }
@@ -1194,6 +1183,24 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(7, 8
     const bool in = i < end;
     mn = min(mn, in ? p.minute : 0xffffffffu);
     mx = max(mx, in && p.minute != 0xffffffffu ? p.minute : 0u);
+    // the range's max tc per cell and the row holding it (after the stores:
+    // hash and minute are dead by now)
+    if (ok) {
+      const u64 old = atomicMax(&cmax[ci], p.tc);
+      bool fix = old == p.tc;  // a second row at the max so far (or a tc of 0)
+      if (old < p.tc) {
+        // this row raised the max: record it, then re-read the max -- if a
+        // later raise came in between, this record may have overwritten that
+        // row's, so the cell is resolved by the rescan.  (LDS executes one
+        // wave's operations in order: only the compiler must keep the store
+        // before the load -- no fence, which would also wait for this wave's
+        // outstanding global loads)
+        __hip_atomic_store(&crow[ci], (uint16_t)(i - beg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("" ::: "memory");
+        fix = __hip_atomic_load(&cmax[ci], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != p.tc;
+      }
+      if (fix) atomicOr(&cfix[ci >> 5], 1u << (ci & 31));
+    }
   }
   if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
   __syncthreads();
@@ -1258,13 +1265,14 @@ __global__ void k_tp_carry_reduce(u32 C, size_t G, const u64* __restrict__ agg, 
   if (c >= C) return;
   const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
   const size_t a = p * per, e = min(G, a + per);
+  // (a range without rows holds (0, ROW_NONE); a row of tc 0 ties with it and
+  // takes the rare path, which ranks NONE below every row)
   TK m{0, ROW_NONE};
 #pragma unroll 8
   for (size_t g = a; g < e; ++g) {
     const TK x{agg[g * C + c], arow[g * C + c]};
-    if (x.row == ROW_NONE) continue;
-    if (m.row == ROW_NONE || x.tc > m.tc) m = x;
-    else if (x.tc == m.tc) m = tk_max(N, c, m, x);  // (rare: equal tc in two ranges)
+    if (x.tc > m.tc) m = x;
+    else if (x.tc == m.tc && x.row != m.row) m = tk_max(N, c, m, x);  // (rare: equal tc in two ranges)
   }
   s_max[(size_t)p * C + c] = m.tc;
   s_row[(size_t)p * C + c] = m.row;
@@ -1307,9 +1315,8 @@ __global__ void k_tp_carry_down(u32 C, size_t G, u64* __restrict__ agg, u32* __r
     const TK here{agg[g * C + c], arow[g * C + c]};
     agg[g * C + c] = run.tc;
     arow[g * C + c] = run.row;
-    if (here.row == ROW_NONE) continue;
-    if (run.row == ROW_NONE || here.tc > run.tc) run = here;
-    else if (here.tc == run.tc) run = tk_max(N, c, run, here);
+    if (here.tc > run.tc) run = here;
+    else if (here.tc == run.tc && here.row != run.row) run = tk_max(N, c, run, here);
   }
 }
 
@@ -1656,7 +1663,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   auto fold = [&](hipStream_t fs) {
     {
       evm::ProfScope ps_(ctx, "k_cl_fold_hist", fs);
-      hipLaunchKernelGGL(k_cl_fold_hist<!TC>, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), 0, fs, flags, minute,
+      hipLaunchKernelGGL(k_cl_fold_hist<true>, dim3(FOLD_CHUNKS, FOLD_MAXWIN), dim3(FOLD_THREADS), 0, fs, flags, minute,
                          hash, n, px, pp, info);
     }
     {
@@ -1684,7 +1691,6 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, xpairs, xcur, cap, n,
                          (const uint8_t*)ts, stride, cell, info);
     }
-    if (TC) fold(xs);  // the tc path's fold needs no flags: beside the walk (and the next batch)
   }
   if (TC) {
     // TP2: per cell, exclusive max over the ranges (in place in agg) + final max
@@ -1701,6 +1707,15 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     // TP3: flags, a workgroup per range
     KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14 + (size_t)C * 4,
                 (const u64*)tcs, cell, n, C, range, (const u64*)agg, (const u32*)arow, N, flags);
+    // the Merkle fold reads the walk's flags (an exact redelivery of a cell's
+    // max is not XORed): on the second stream after the walk, beside the
+    // next batch's K1 when batches are pipelined
+    const hipStream_t fs = side.stream();
+    if (fs != ctx->stream) {
+      HIPR(hipEventRecord(ctx->ev_fork, ctx->stream));
+      HIPR(hipStreamWaitEvent(fs, ctx->ev_fork, 0));
+    }
+    fold(fs);
   } else {
     // pass 1: per range and cell, the max timestamp and its first index
     KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,

@@ -127,11 +127,25 @@ struct RcclTransport final : Transport {
   }
   int exchange(const char* sbase, const uint64_t* soff, const uint64_t* slen, char* rbase, const uint64_t* roff,
                const uint64_t* rlen, hipStream_t s) override {
+    // transfers in pieces of at most CHUNK bytes (a 4 GiB self-send arrived
+    // corrupted in one call); both sides cut a peer's bytes alike, and
+    // point-to-point calls to one peer match in issue order
+    constexpr uint64_t CHUNK = 1ull << 29;
     if (r->group_start() != ncclSuccess) return EVM_EDIST;
     int st = EVM_OK;
     for (int p = 0; p < world; ++p) {
-      if (r->send(sbase + soff[p], slen[p], ncclUint8, p, comm, s) != ncclSuccess) st = EVM_EDIST;
-      if (r->recv(rbase + roff[p], rlen[p], ncclUint8, p, comm, s) != ncclSuccess) st = EVM_EDIST;
+      uint64_t o = 0;
+      do {
+        const uint64_t k = std::min<uint64_t>(CHUNK, slen[p] - o);
+        if (r->send(sbase + soff[p] + o, k, ncclUint8, p, comm, s) != ncclSuccess) st = EVM_EDIST;
+        o += k;
+      } while (o < slen[p]);
+      o = 0;
+      do {
+        const uint64_t k = std::min<uint64_t>(CHUNK, rlen[p] - o);
+        if (r->recv(rbase + roff[p] + o, k, ncclUint8, p, comm, s) != ncclSuccess) st = EVM_EDIST;
+        o += k;
+      } while (o < rlen[p]);
     }
     if (r->group_end() != ncclSuccess) st = EVM_EDIST;  // always closed, whatever failed inside
     return st;

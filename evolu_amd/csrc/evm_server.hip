@@ -556,6 +556,22 @@ __global__ void k_pick(const uint8_t* __restrict__ mask, const u32* __restrict__
     if (mask[i]) out[pos[i]] = (u32)i;
 }
 
+// per-owner isolation (evm_server_ingest_ex): an owner with a culprit row
+__global__ void k_owner_bad(const uint8_t* __restrict__ flags, const u32* __restrict__ owner, size_t n, u32 O,
+                            uint8_t* __restrict__ obad) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    if ((flags[i] & EVM_MSG_BAD) && owner[i] < O) obad[owner[i]] = 1;
+}
+// rows of owners without one (mask) and their count (keep as u32 for the scan)
+__global__ void k_owner_keep(const u32* __restrict__ owner, size_t n, const uint8_t* __restrict__ obad,
+                             uint8_t* __restrict__ mask, u32* __restrict__ keep) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const uint8_t k = obad[owner[i]] ? 0 : 1;
+    mask[i] = k;
+    keep[i] = k;
+  }
+}
+
 // records of a sub-batch from the caller's packed records
 __global__ void k_sv_rec_sel(const evm_rec* __restrict__ prec, const u32* __restrict__ orig, size_t n,
                              evm_rec* __restrict__ out, u32* __restrict__ owner_out) {
@@ -2258,6 +2274,45 @@ int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride,
   if (n == 0) return EVM_OK;  // index.ts:145 `if (req.messages.length === 0) return merkleTree`
   if (n >= 0xffffffffull) return EVM_EINVAL;
   return ingest_impl(ctx, s, ts, stride, n, owner, nullptr, nullptr, id_base, flags, ctx->server_path == 2 ? 2 : 0);
+}
+
+int evm_server_ingest_ex(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                         uint64_t id_base, uint8_t* flags, uint8_t* owner_status) {
+  if (!ctx || !s || !owner_status || stride < 46 || (n && (!ts || !owner || !flags))) return EVM_EINVAL;
+  if (n >= 0xffffffffull) return EVM_EINVAL;
+  const u32 O = s->n_owners;
+  if (O) HIPR(hipMemsetAsync(owner_status, 0, O, ctx->stream));
+  if (n == 0) return evm_sync(ctx);
+  const int mode = ctx->server_path == 2 ? 2 : 0;
+  int st = ingest_impl(ctx, s, ts, stride, n, owner, nullptr, nullptr, id_base, flags, mode);
+  if (st != EVM_ENONCANON) return st;
+  // some owners' rows are outside the native domain: nothing was applied and
+  // flags mark the culprits.  Those owners commit nothing (their requests
+  // fail as one transaction, index.ts:147-169); every other owner commits.
+  Scratch S(ctx);
+  uint8_t* mask = S.alloc<uint8_t>(n);
+  u32* keep = S.alloc<u32>(n);
+  u32* pos = S.alloc<u32>(n);
+  u32* nkeep = S.alloc<u32>(1);
+  u32* sel = S.alloc<u32>(n);
+  evm_rec* rec = S.alloc<evm_rec>(n);
+  Info* info = nullptr;
+  if (!mask || !keep || !pos || !nkeep || !sel || !rec) return EVM_ENOMEM;
+  if ((st = new_info(ctx, S, &info))) return st;
+  KLAUNCH(k_owner_bad, dim3(grid_for(n, 256)), dim3(256), flags, owner, n, O, owner_status);
+  KLAUNCH(k_owner_keep, dim3(grid_for(n, 256)), dim3(256), owner, n, (const uint8_t*)owner_status, mask, keep);
+  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, keep, n, pos, nkeep))) return st;
+  KLAUNCH(k_pick, dim3(grid_for(n, 256)), dim3(256), (const uint8_t*)mask, (const u32*)pos, n, sel);
+  if ((st = launch_pack(ctx, ts, stride, n, owner, O, rec, info))) return st;
+  u32 hkeep = 0;
+  HIPR(hipMemcpyAsync(&hkeep, nkeep, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if (hkeep) {
+    // (the sub-batch writes the flags of its rows; the rejected owners' rows
+    // keep the first pass's: EVM_MSG_BAD for the culprits, 0 otherwise)
+    if ((st = ingest_impl(ctx, s, ts, stride, hkeep, owner, sel, rec, id_base, flags, mode))) return st;
+  }
+  return EVM_ENONCANON;
 }
 
 }  // extern "C"

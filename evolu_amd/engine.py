@@ -344,6 +344,19 @@ class Store:
             check(st, "evm_server_ingest")
         return flags[:n], st
 
+    def ingest_ex(self, ts: torch.Tensor, owner: torch.Tensor, id_base: int = 0, flags: Optional[torch.Tensor] = None):
+        """evm_server_ingest_ex: per-owner transactions -> (flags, owner_status
+        uint8[n_owners] (1: that owner committed nothing), status)."""
+        n, stride = ts.shape
+        if flags is None:
+            flags = torch.empty(max(n, 1), dtype=torch.uint8, device=ts.device)
+        ost = torch.empty(max(self.n_owners, 1), dtype=torch.uint8, device=ts.device)
+        st = self.eng.lib.evm_server_ingest_ex(self.eng.h, self.h, _ptr(ts), stride, n, _ptr(owner), id_base,
+                                               _ptr(flags), _ptr(ost))
+        if st not in (_lib.EVM_OK, _lib.EVM_ENONCANON):
+            check(st, "evm_server_ingest_ex")
+        return flags[:n], ost[: self.n_owners], st
+
     def select(self, client: "Trees", node: torch.Tensor, active: Optional[torch.Tensor] = None, cap: int = None):
         """-> (diff int64[n_owners], sel_off uint64[n_owners+1], sel_id uint64[n_sel])."""
         dev = node.device

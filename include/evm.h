@@ -285,6 +285,17 @@ int evm_store_messages(evm_ctx* ctx, const evm_store* s, uint64_t* owner_off, ui
 int evm_server_ingest(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
                       uint64_t id_base, uint8_t* flags);
 
+/* The same with the reference's per-request transactions (index.ts:147-169:
+ * a throw rolls back that request only): an owner with a row outside the
+ * native domain commits NOTHING -- owner_status[o] = 1 (device uint8
+ * [n_owners]), its culprit rows flagged EVM_MSG_BAD, its other rows 0 --
+ * and every other owner commits exactly as evm_server_ingest would.  Returns
+ * EVM_OK (all committed), EVM_ENONCANON (the flagged owners did not, the rest
+ * did), or an error (nothing committed).  A batch carries one request per
+ * owner, as SyncServer's rounds do. */
+int evm_server_ingest_ex(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                         uint64_t id_base, uint8_t* flags, uint8_t* owner_status);
+
 /* index.ts:173-202 getMessages for one request per owner:
  * diff = diffMerkleTrees(store tree, client[o]); if Some(d), the owner's
  * messages with timestamp > timestampToString(createSyncTimestamp(d)) and

@@ -208,6 +208,47 @@ def timestamp_to_hash(millis: int, counter: int, node: str) -> int:
     return murmur3_32(timestamp_to_string(millis, counter, node).encode("utf-8"))
 
 
+_ISO_JS = re.compile(r"^(\d{4})-(\d{2})-(\d{2})[Tt](\d{2}):(\d{2}):(\d{2})\.(\d{3})[Zz]$")
+_PARSE_INT_16 = re.compile(r"^\s*([+-]?)(?:0[xX])?([0-9a-fA-F]+)")
+
+
+def date_parse_js(s: str) -> Optional[int]:
+    """V8 ``Date.parse`` of an ISO-shaped date string (its ES5 ISO parser:
+    fixed-width fields, a day up to 31 rolls over past the month's end (MakeDay),
+    hour 24 only at :00:00.000, 't'/'z' in either case) -> millis, None for
+    NaN.  Other shapes raise NonCanonical (V8's legacy parser: not modelled).
+    Pinned by node: tests/golden/js_lenient.json (oracle/js/gen_lenient.js)."""
+    mt = _ISO_JS.match(s)
+    if not mt:
+        raise NonCanonical(s)
+    y, mo, d, hh, mi, ss, ms = (int(mt.group(i)) for i in range(1, 8))
+    if not (1 <= mo <= 12 and 1 <= d <= 31 and hh <= 24 and mi <= 59 and ss <= 59):
+        return None
+    if hh == 24 and (mi or ss or ms):
+        return None
+    return (_days_from_civil(y, mo, 1) + d - 1) * MS_PER_DAY + ((hh * 60 + mi) * 60 + ss) * 1000 + ms
+
+
+def timestamp_from_string_js(s: str) -> Tuple[Optional[int], int, str]:
+    """timestamp.ts:50-55 as written: ``a = s.split("-")``; millis =
+    ``Date.parse(a.slice(0, 3).join("-"))`` (None for NaN), counter =
+    ``parseInt(a[3], 16)``, node = ``a[4]``.  Canonical strings take
+    parse_canonical; a counter or node JS would turn into NaN / undefined is
+    not modelled (NonCanonical)."""
+    try:
+        return parse_canonical(s)
+    except NonCanonical:
+        pass
+    a = s.split("-")
+    if len(a) < 5:
+        raise NonCanonical(s)
+    mt = _PARSE_INT_16.match(a[3])
+    if not mt:
+        raise NonCanonical(s)
+    counter = int(mt.group(2), 16) * (-1 if mt.group(1) == "-" else 1)
+    return date_parse_js("-".join(a[:3])), counter, a[4]
+
+
 def create_sync_timestamp(millis: int = 0) -> Tuple[int, int, str]:
     """timestamp.ts:35-41."""
     return (millis, 0, "0000000000000000")
@@ -522,7 +563,12 @@ class ServerDb:
                 if inserted is not None:
                     inserted.append(took)
                 if took:
-                    tree = insert_into_merkle_tree(tree, timestamp_from_string(ts))
+                    # the raw string is stored; the tree sees timestampFromString(raw)
+                    # (lenient), whose toISOString throws on an invalid date
+                    t = timestamp_from_string_js(ts)
+                    if t[0] is None:
+                        raise RangeErrorJS("Invalid time value")
+                    tree = insert_into_merkle_tree(tree, t)
             cur.execute(_SQL_SAVE_TREE, (user_id, merkle_tree_to_string(tree)))
             cur.execute("COMMIT")
         except Exception:

@@ -152,3 +152,21 @@ def test_packed_wire_rebuilds_rows_exactly(eng, dist):
     assert dist.route(eng.dev(ext), eng.dev(owner)) == len(strings)
     t3, _, _, _, _ = dist.take()
     assert np.array_equal(t3.cpu().numpy(), ext)
+
+
+def test_route_larger_than_4gib_arrives_whole(eng, dist):
+    """A route whose exchange is > 2^32 bytes (140M rows x 32-B records: the
+    config-4 share of one GPU) arrives byte for byte through RCCL (the
+    transfer is cut into pieces)."""
+    from evolu_amd import synth
+
+    gen = synth.DeviceSynth()
+    dev = torch.device("cuda", 0)
+    ts, owner, _ = gen.source(0xE7010004, 140_000, 1000, 1, 0, dev)
+    n = dist.route(ts, owner)
+    assert n == ts.shape[0]
+    out = (torch.empty_like(ts), torch.empty_like(owner), None, None)
+    t2, o2, _, _, _ = dist.take(aux=False, src=False, out=out)
+    assert torch.equal(t2, ts) and torch.equal(o2, owner)
+    del ts, owner, out, t2, o2
+    torch.cuda.empty_cache()

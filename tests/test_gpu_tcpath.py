@@ -311,7 +311,8 @@ def test_tc_path_adversarial_client_stream_vs_c_oracle(eng, n, cells, nodes):
     assert np.array_equal(flags.cpu().numpy(), f_w)
     assert np.array_equal(winner.cpu().numpy(), w_w)
     assert tree.to_json(0) == js_w
-    assert ((f_w & L.MSG_XOR) == 0).sum() > 0  # the stream has exact redeliveries of cell maxima (ties)
+    if cells > 1:
+        assert ((f_w & L.MSG_XOR) == 0).sum() > 0  # the stream has exact redeliveries of cell maxima (ties)
 
 
 def test_tc_path_tie_list_overflow_redoes_exactly(eng):

@@ -60,7 +60,11 @@ def _expected(bodies):
         except Exception:
             out.append("ParseBodyError")
             continue
-        tree, _, rows = sdb.sync(r.userId, r.nodeId, r.merkleTree, [(m.timestamp, m.content) for m in r.messages])
+        try:
+            tree, _, rows = sdb.sync(r.userId, r.nodeId, r.merkleTree, [(m.timestamp, m.content) for m in r.messages])
+        except O.RangeErrorJS:
+            out.append("500")  # index.ts:224-233: the request rolled back
+            continue
         out.append(RESP(messages=[dict(timestamp=t, content=c) for t, c in rows],
                         merkleTree=O.merkle_tree_to_string(tree)).SerializeToString())
     return out
@@ -102,4 +106,81 @@ def test_empty_requests_and_unknown_user(eng):
               REQ(userId="b", nodeId="0123456789abcdef", merkleTree="{}").SerializeToString()]
     srv = SyncServer(eng, 4)
     assert srv.sync(bodies) == _expected(bodies)
+    srv.close()
+
+
+def test_per_request_failure_and_lenient_timestamps(eng):
+    """index.ts:147-169 / :224-233: a request with an invalid date fails alone
+    (500, nothing of it stored) while the other requests of the round commit;
+    a lenient but valid timestamp (V8 rolls 02-30 into March; a lower-case
+    counter parses) is stored under its raw spelling and XORed in its
+    canonical form -- the responses, including later requests of the same
+    owners, are byte-identical to the reference's."""
+    from evolu_amd.server import RangeError, SyncServer
+
+    rng = random.Random(21)
+    users = ["%021x" % rng.getrandbits(84) for _ in range(5)]
+    nodes = [W.node_id(rng) for _ in range(3)]
+    pools = {u: W.hlc_timestamps(rng, 40, nodes) for u in users}
+
+    def req(u, ts, node=None, tree="{}"):
+        return REQ(messages=[dict(timestamp=t, content=("c%d" % k).encode()) for k, t in enumerate(ts)], userId=u,
+                   nodeId=node or nodes[0], merkleTree=tree).SerializeToString()
+
+    bad_date = "2024-02-32T10:00:00.000Z-0000-" + nodes[1]
+    lenient = ["2024-02-30T23:59:59.999Z-000a-" + nodes[1], "2023-04-31t12:00:00.000z-00FF-" + nodes[2].upper()]
+    # a canonical row right next to a lenient one: raw-string order differs from canonical order
+    near = "2024-03-01T23:59:59.999Z-0000-" + nodes[2]
+    bodies = [
+        req(users[0], pools[users[0]][:10]),
+        req(users[1], pools[users[1]][:5] + [bad_date] + pools[users[1]][5:8]),  # -> 500
+        req(users[2], pools[users[2]][:6] + lenient + [near]),
+        req(users[3], pools[users[3]][:12], node=nodes[1]),
+        # later requests of the same owners
+        req(users[1], pools[users[1]][8:14]),  # the failed request stored nothing
+        req(users[2], pools[users[2]][6:9] + [lenient[0]], node=nodes[2]),  # a redelivered lenient row
+        req(users[2], [], node=nodes[0]),  # getMessages over rows kept under lenient spellings (raw order)
+        req(users[0], pools[users[0]][10:12] + ["2024-13-01T00:00:00.000Z-0000-" + nodes[0]]),  # -> 500
+        req(users[0], pools[users[0]][12:15]),
+    ]
+    want = _expected(bodies)
+    assert want[1] == "500" and want[7] == "500"
+    srv = SyncServer(eng, 8)
+    got = srv.sync(bodies)
+    for i, (g, w) in enumerate(zip(got, want)):
+        if w == "500":
+            assert isinstance(g, RangeError), i
+        else:
+            assert g == w, i
+    assert not srv.detached
+    # one timestamp under two spellings (lenient, then canonical): the reference
+    # stores both; the device keeps one key -> that user is handed to the caller
+    canon = "2024-03-01T23:59:59.999Z-000A-" + nodes[1]
+    more = [req(users[2], [canon]), req(users[2], pools[users[2]][9:11]), req(users[4], pools[users[4]][:3])]
+    got2 = srv.sync(more)
+    want2 = _expected(bodies + more)[len(bodies):]
+    assert got2[0] is None and got2[1] is None and users[2] in srv.detached
+    assert got2[2] == want2[2]
+    srv.close()
+
+
+def test_node_id_not_hex_is_handed_over_unapplied(eng):
+    """A nodeId the engine cannot use in NOT LIKE '%' || nodeId: the request is
+    not applied (None) and the user's later requests are the caller's too."""
+    from evolu_amd.server import SyncServer
+
+    rng = random.Random(5)
+    node = W.node_id(rng)
+    ts = W.hlc_timestamps(rng, 10, [node])
+    b = [REQ(messages=[dict(timestamp=t, content=b"x") for t in ts[:5]], userId="u", nodeId="not-a-node",
+             merkleTree="{}").SerializeToString(),
+         REQ(messages=[dict(timestamp=t, content=b"x") for t in ts[5:]], userId="u", nodeId=node,
+             merkleTree="{}").SerializeToString(),
+         REQ(messages=[dict(timestamp=t, content=b"y") for t in ts[:3]], userId="v", nodeId=node,
+             merkleTree="{}").SerializeToString()]
+    srv = SyncServer(eng, 4)
+    got = srv.sync(b)
+    assert got[0] is None and got[1] is None and "u" in srv.detached
+    assert got[2] == _expected(b[2:])[0]
+    assert srv.store.n_messages == 3  # nothing of "u" was stored
     srv.close()
