@@ -138,11 +138,13 @@ class EngineError(RuntimeError):
         super().__init__("%s: %s (status %d)" % (where, msg, status))
 
 
-def load(path: str = LIB_PATH):
-    """Loads libevm.so (raises if absent: there is no CPU fallback)."""
+def load(path: str = None):
+    """Loads libevm.so (raises if absent: there is no CPU fallback).
+    EVM_LIB_PATH selects another in-tree build (A/B measurements)."""
     global _LIB
     if _LIB is not None:
         return _LIB
+    path = path or os.environ.get("EVM_LIB_PATH") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(
             "libevm.so not built (%s); run `python -c 'import __graft_entry__ as g; g.build()'`" % path

@@ -1019,7 +1019,6 @@ __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* 
 constexpr u64 TP_INVALID = ~0ull;  // tc of a message the walk skips (invalid timestamp or cell id)
 constexpr int TP_THREADS = 256;
 constexpr int TP_RANGES = 2048;  // ~8 ranges per CU: TP1's occupancy
-constexpr u32 TP_RANGE_MAX = 65280;  // rows per range: TP1 keeps a row as a 16-bit offset
 constexpr u32 ROW_NONE = 0xffffffffu;   // no max (SQL NULL: below every timestamp)
 constexpr u32 ROW_PRIOR = 0xfffffffeu;  // the max is the caller's prior row of the cell
 constexpr u32 TP_MATCH_MAX = 512;       // TP1 rescan: rows tied at a cell's range max
@@ -1096,18 +1095,29 @@ __device__ __forceinline__ TK shfl_tk(const TK& k, int src) {
   return o;
 }
 
+// TP1: K1 + per (range, cell) the max tc and the row holding it.  One LDS
+// 64-bit max per row on key = millis << 21 | counter << 13 | (8191 - row
+// offset): exact for millis < 2^41 (until 2039-09), counter < 256 and ranges
+// of <= 8,192 rows -- the largest key is the range's max tc at its first row.
+// A row outside that (far) or a second row at a max tc (ds_max returns the key
+// it replaced: equal tc bits) marks its cell; marked cells are resolved by a
+// rescan of the range (true max tc, then the node ranks of the rows at it).
+#ifndef TP_WPE
+#define TP_WPE 8  // waves per SIMD TP1 is compiled for (7: no spills, measured no faster)
+#endif
+constexpr u32 TP_ROWS_MAX = 8192;  // rows per range (the key's 13-bit row offset)
+constexpr u64 TP_MS_FAST = 1ull << 41;
+
 template <bool S48>
-__global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
+__global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_WPE, 8))) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
                                                         const u32* __restrict__ cell, u32 C, size_t range_len,
                                                         u64* __restrict__ tcs, u32* __restrict__ hash,
                                                         u32* __restrict__ minute, u64* __restrict__ agg,
                                                         u32* __restrict__ arow, Info* __restrict__ info,
                                                         u32* __restrict__ zero_buf, u32 zero_n) {
-  // LDS: [C] max tc per cell of this range, [C] its row (16-bit offset),
-  // [ceil(C/32)] cells to resolve (two rows at the max, or a raced row record)
+  // LDS: [C] max key per cell of this range, [ceil(C/32)] the marked cells
   extern __shared__ __attribute__((aligned(16))) u64 cmax[];
-  uint16_t* crow = reinterpret_cast<uint16_t*>(cmax + C);
-  u32* cfix = reinterpret_cast<u32*>(crow + ((C + 1) & ~1u));
+  u32* cfix = reinterpret_cast<u32*>(cmax + C);
   // (the cross-cell check's bucket cursors, cleared here instead of by a
   // memset on the second stream, which forks after this kernel)
   if (blockIdx.x == 0)
@@ -1117,10 +1127,7 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(7, 8
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const size_t g = blockIdx.x;
   const size_t beg = g * range_len, end = min(n, beg + range_len);
-  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
-    cmax[c] = 0;
-    crow[c] = 0xffffu;
-  }
+  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) cmax[c] = 0;
   for (u32 k = threadIdx.x; k < (C + 31) / 32; k += TP_THREADS) cfix[k] = 0;
   if (threadIdx.x == 0) nmatch = 0;
   __syncthreads();
@@ -1149,13 +1156,21 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(7, 8
     }
     Parsed p = parse_ts46(w);  // (the node ranks it can compute are dead here)
     const bool valid = (p.meta & EVM_META_VALID) != 0;
-    u32 ci = 0;
-    bool ok = false;
     if (i < end) {
-      ci = __builtin_nontemporal_load(cell + i);
-      ok = valid && ci < C;
+      const u32 ci = __builtin_nontemporal_load(cell + i);
+      const bool ok = valid && ci < C;
       __builtin_nontemporal_store(ok ? p.tc : TP_INVALID, tcs + i);
       if (!ok) p.minute = 0xffffffffu;  // outside every fold window (and the minute bounds)
+      if (ok) {
+        const u64 ms = p.tc >> 16;
+        const u32 ctr = (u32)p.tc & 0xffffu;
+        bool mark = true;  // far
+        if (ms < TP_MS_FAST && ctr < 256u) {
+          const u64 key = (ms << 21) | ((u64)ctr << 13) | (u64)(TP_ROWS_MAX - 1u - (u32)(i - beg));
+          mark = (atomicMax(&cmax[ci], key) >> 13) == (key >> 13);  // a second row at this tc (or tc 0)
+        }
+        if (mark) atomicOr(&cfix[ci >> 5], 1u << (ci & 31));
+      }
       bad |= valid ? 0u : 1u;
       aux_bad |= ci < C ? 0u : 1u;
     }
@@ -1183,44 +1198,45 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(7, 8
     const bool in = i < end;
     mn = min(mn, in ? p.minute : 0xffffffffu);
     mx = max(mx, in && p.minute != 0xffffffffu ? p.minute : 0u);
-    // the range's max tc per cell and the row holding it (after the stores:
-    // hash and minute are dead by now)
-    if (ok) {
-      const u64 old = atomicMax(&cmax[ci], p.tc);
-      bool fix = old == p.tc;  // a second row at the max so far (or a tc of 0)
-      if (old < p.tc) {
-        // this row raised the max: record it, then re-read the max -- if a
-        // later raise came in between, this record may have overwritten that
-        // row's, so the cell is resolved by the rescan.  (LDS executes one
-        // wave's operations in order: only the compiler must keep the store
-        // before the load -- no fence, which would also wait for this wave's
-        // outstanding global loads)
-        __hip_atomic_store(&crow[ci], (uint16_t)(i - beg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        asm volatile("" ::: "memory");
-        fix = __hip_atomic_load(&cmax[ci], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != p.tc;
-      }
-      if (fix) atomicOr(&cfix[ci >> 5], 1u << (ci & 31));
-    }
   }
   if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
   __syncthreads();
+  // the unmarked cells: tc and row straight from the key
+  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
+    if ((cfix[c >> 5] >> (c & 31)) & 1u) continue;
+    const u64 k = cmax[c];
+    agg[g * C + c] = k ? (((k >> 21) << 16) | ((k >> 13) & 0xffu)) : 0ull;
+    arow[g * C + c] = k ? (u32)(beg + (TP_ROWS_MAX - 1u - (u32)(k & (TP_ROWS_MAX - 1u)))) : ROW_NONE;
+  }
   bool any_fix = false;
   for (u32 k = threadIdx.x; k < (C + 31) / 32; k += TP_THREADS) any_fix |= cfix[k] != 0;
   if (__syncthreads_or(any_fix)) {
-    // rescan (rare): the rows of the cells to resolve that hold the cell's
-    // range max, with their node ranks, into LDS (the stage is free now) ...
+    // rescan (rare): the marked cells' true max tc, then their rows at it with
+    // their node ranks into LDS (the stage is free now), then per cell the
+    // best: highest node ranks, the lowest row among equals
     struct Match {
       u64 rh;
       u32 rl, row, cell, pad;
     };
     Match* mt = reinterpret_cast<Match*>(&stage[0][0]);
     static_assert(sizeof(stage) >= TP_MATCH_MAX * sizeof(Match), "match list fits the stage");
-    const NodeSrc N{ts, stride, nullptr};
+    auto marked = [&](u32 c) { return ((cfix[c >> 5] >> (c & 31)) & 1u) != 0; };
+    for (u32 c = threadIdx.x; c < C; c += TP_THREADS)
+      if (marked(c)) cmax[c] = 0;
+    __syncthreads();
     for (size_t i = beg + threadIdx.x; i < end; i += TP_THREADS) {
       const u64 t = __hip_atomic_load(tcs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // written above
       if (t == TP_INVALID) continue;
       const u32 ci = cell[i];
-      if (!((cfix[ci >> 5] >> (ci & 31)) & 1u) || t != cmax[ci]) continue;
+      if (marked(ci)) atomicMax(&cmax[ci], t);
+    }
+    __syncthreads();
+    const NodeSrc N{ts, stride, nullptr};
+    for (size_t i = beg + threadIdx.x; i < end; i += TP_THREADS) {
+      const u64 t = __hip_atomic_load(tcs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == TP_INVALID) continue;
+      const u32 ci = cell[i];
+      if (!marked(ci) || t != cmax[ci]) continue;
       const u32 k = atomicAdd(&nmatch, 1u);
       if (k < TP_MATCH_MAX) {
         Match m;
@@ -1236,7 +1252,6 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(7, 8
     if (nm > TP_MATCH_MAX) {
       if (threadIdx.x == 0) atomicOr(&info->ties, 1u);  // too many: the exact walk path redoes the batch
     } else {
-      // ... then per cell the best: highest node ranks, the lowest row among equals
       for (u32 k = threadIdx.x; k < nm; k += TP_THREADS) {
         const Match e = mt[k];
         bool best = true;
@@ -1245,14 +1260,12 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(7, 8
           if (f == k || o.cell != e.cell) continue;
           best = !(o.rh > e.rh || (o.rh == e.rh && (o.rl > e.rl || (o.rl == e.rl && o.row < e.row))));
         }
-        if (best) crow[e.cell] = (uint16_t)(e.row - beg);
+        if (best) {
+          agg[g * C + e.cell] = cmax[e.cell];
+          arow[g * C + e.cell] = e.row;
+        }
       }
     }
-    __syncthreads();
-  }
-  for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
-    agg[g * C + c] = cmax[c];
-    arow[g * C + c] = crow[c] == 0xffffu ? ROW_NONE : (u32)(beg + crow[c]);
   }
   block_fold_bounds<u32, TP_THREADS>(mn, mx, bad, &info->minute_min, &info->minute_max, &info->bad);
 }
@@ -1574,7 +1587,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   size_t range, G;
   if (TC) {
     range = std::max<size_t>(1024, ((n + TP_RANGES - 1) / TP_RANGES + 255) / 256 * 256);
-    range = std::min<size_t>(range, TP_RANGE_MAX);  // (TP1 records rows as 16-bit offsets)
+    range = std::min<size_t>(range, TP_ROWS_MAX);  // (TP1's key holds a 13-bit row offset)
   } else {
     range = (n + CL_RANGE_TARGET - 1) / CL_RANGE_TARGET;
     range = std::max<size_t>(2048, (range + 255) / 256 * 256);
@@ -1596,7 +1609,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     if (!tcs || !agg || !arow) return EVM_ENOMEM;
     // TP1: parse + per (range, cell) max tc and its row, one workgroup per range
     evm::ProfScope ps_(ctx, "k_tp_pack");
-    const size_t lds = (size_t)C * 8 + (size_t)((C + 1) & ~1u) * 2 + (size_t)((C + 31) / 32) * 4;
+    const size_t lds = (size_t)C * 8 + (size_t)((C + 31) / 32) * 4;
     if (s48)
       hipLaunchKernelGGL(k_tp_pack<true>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
                          cell, C, range, tcs, hash, minute, agg, arow, info, xcur, 1u << xp_geom(n).kb);
