@@ -7,19 +7,27 @@ batch (evm_apply_batch: pack + canonical check + murmur3, cross-cell PK
 check, LWW walks, Merkle fold) with the inputs already resident in HBM,
 starting from an empty tree.
 
-At N = 1 the same line carries two more BASELINE configs under extra keys:
+At N = 1 the same line carries the other BASELINE configs under extra keys:
+  "client_adversarial": config 5 on the client side (equal-millis ties,
+             exact and stale redeliveries, upper-case nodes), 10M messages,
+             pipelined like the headline, its own roofline;
   "config1": the examples/nextjs todo-schema stream (100k messages, one
              owner, ~55k cells: the sort path), GPU time + CPU baseline;
   "config3": the sync server, 100k owners x 1,000 messages, one SyncRequest
              per owner (apps/server/src/index.ts:204-216: addMessages then
              getMessages against the client's tree), with its own roofline
-             and CPU baseline (oracle/js/cpu_server.js, 1 and P threads).
+             and CPU baseline (oracle/js/cpu_server.js, 1 and P threads);
+  "config4": the N > 1 workload at world 1 (its weak-scaling base).
 
-Multi-GPU (torchrun, one rank per GPU): weak scaling -- every rank merges its
-own owner's 10M-message batch (owners are independent in applyMessages: each
-is its own client DB), no data-path collective; the elapsed time is the max
-over ranks.  `--workload server` runs configs 3/4/5 standalone (RCCL owner
-routing at N > 1).  Rank 0 prints one JSON line.
+Multi-GPU (torchrun, one rank per GPU): BASELINE config 4 by default -- the
+sync server over 125,000 owners x 1,000 messages per GPU (1B messages over
+1M owners at 8 GPUs), owners sharded by murmur3(userId) mod N on the device,
+every rank's slice routed over RCCL (evm_dist_route), roots all-gathered,
+and an in-run self-check of sampled owners against an unsharded recompute
+(`parity_checked`).  The elapsed time is the max over ranks.  `--workload
+client` runs config 2 per rank, `--workload server` configs 3/5 standalone,
+`--loopback N` rehearses config 4 with N ranks on one GPU.  Rank 0 prints one
+JSON line.
 """
 from __future__ import annotations
 
@@ -487,6 +495,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(ts_np, cell_np, a.cpu_seconds)
         del ts, cell, flags, ts_h, cell_h
         if world == 1 and a.extra:
+            out["client_adversarial"] = adversarial_leg(eng, a)
             out["config1"] = config1_leg(eng, a)
             eng.close()
             torch.cuda.empty_cache()
@@ -949,6 +958,75 @@ def config4_loopback(a, world, device=0):
     res.pop("steps"), res.pop("warmup")
     out.update(res)
     return out
+
+
+def adversarial_leg(eng, a):
+    """BASELINE config 5 on the client side (synth.client_adversarial): one
+    owner, 10M messages over 1,000 cells from 64 nodes, equal-millis bursts
+    (ties broken by counter and node), 10 % redeliveries (half stale: XOR
+    toggles; the rest exact copies of the cell max: no-ops decided by node
+    ranks inside the walk), ~1 % upper-case nodes.  Pipelined exactly like
+    the headline; tc_redos must stay 0 (no batch falls back to the exact walk
+    path)."""
+    import collections
+
+    import torch
+
+    from evolu_amd import synth
+
+    n, C = a.messages, a.cells
+    ts_np, cell_np = synth.client_adversarial(n, C, 64, seed_config=5)
+    ts, cell = eng.dev(ts_np), eng.dev(cell_np)
+    del ts_np
+    empty = eng.tree_new(1)
+    depth = max(1, a.depth)
+    outs = [(torch.empty(n, dtype=torch.uint8, device=ts.device), torch.empty(C, dtype=torch.int32, device=ts.device))
+            for _ in range(depth)]
+
+    def run(k_steps):
+        q = collections.deque()
+        for k in range(k_steps):
+            if len(q) == depth:
+                q.popleft().wait()[2].free()
+            q.append(eng.apply_batch_async(empty, ts, cell, C, *outs[k % depth]))
+        while q:
+            q.popleft().wait()[2].free()
+
+    run(max(a.warmup, 2))
+    torch.cuda.synchronize()
+    eng.prof_enable(True)
+    eng.prof_reset()
+    for _ in range(3):
+        eng.apply_batch(empty, ts, cell, C, flags=outs[0][0], winner=outs[0][1])[2].free()
+    torch.cuda.synchronize()
+    prof = eng.prof_report()
+    dom = dominant(prof, ALG_BYTES_PER_MSG, SIDE_KERNELS)
+    eng.prof_only(dom)
+    eng.prof_reset()
+    s0 = eng.stats()
+    t0 = time.perf_counter()
+    run(a.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    s1 = eng.stats()
+    prof_dom = eng.prof_report()
+    eng.prof_enable(False)
+    eng.prof_only(None)
+    f = outs[0][0].cpu().numpy()
+    tot_ms, launches = prof_dom[dom]
+    avg_s = tot_ms / launches / 1e3
+    alg = ALG_BYTES_PER_MSG[dom] * n
+    ms = dt / a.steps * 1e3
+    return {"workload": "client config 5 (synth.client_adversarial): 1 owner, %d msgs, %d cells, 64 nodes, equal-millis "
+                        "bursts, 10 %% redeliveries, ~1 %% upper-case nodes; %d batches in flight" % (n, C, depth),
+            "value": n / ms * 1e3, "unit": "msgs/s", "ms_per_step": ms, "steps": a.steps,
+            "tc_batches": s1["tc_batches"] - s0["tc_batches"], "tc_redos": s1["tc_redos"] - s0["tc_redos"],
+            "no_op_rows": int((f == 0).sum()), "xor_only_rows": int((f == 2).sum()), "upsert_rows": int((f == 3).sum()),
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "kernel_ms_avg": avg_s * 1e3,
+                         "alg_bytes_per_launch": alg},
+            "pipeline_hbm_frac": 120 * n / (dt / a.steps) / HBM_PEAK,
+            "kernels_ms_per_step": {k: v[0] / 3 for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:12]}}
 
 
 def config1_leg(eng, a):

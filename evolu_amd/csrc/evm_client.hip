@@ -1250,7 +1250,14 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
     __syncthreads();
     const u32 nm = nmatch;
     if (nm > TP_MATCH_MAX) {
-      if (threadIdx.x == 0) atomicOr(&info->ties, 1u);  // too many: the exact walk path redoes the batch
+      // too many: the exact walk path redoes the batch; until then the carry
+      // and the walk must read in-bounds rows (no row: NONE)
+      if (threadIdx.x == 0) atomicOr(&info->ties, 1u);
+      for (u32 c = threadIdx.x; c < C; c += TP_THREADS)
+        if (marked(c)) {
+          agg[g * C + c] = 0;
+          arow[g * C + c] = ROW_NONE;
+        }
     } else {
       for (u32 k = threadIdx.x; k < nm; k += TP_THREADS) {
         const Match e = mt[k];
