@@ -98,7 +98,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget per leg (0: skip)")
     ap.add_argument("--overlap", type=int, default=1, help="EVM_OPT_OVERLAP: independent checks on a second stream")
     ap.add_argument("--depth", type=int, default=4, help="config 2: batches in flight (evm_apply_batch_async)")
-    ap.add_argument("--workload", choices=["auto", "client", "server", "config4"], default="auto",
+    ap.add_argument("--workload", choices=["auto", "client", "server", "config4", "adversarial"], default="auto",
                     help="auto: client at N=1, config4 at N>1; "
                          "client: config 2 applyMessages (headline, + config 1, 3 and 4 legs at N=1); "
                          "server: config 3/5 ingest + diff + select alone; "
@@ -126,8 +126,9 @@ def parse():
     ap.add_argument("--dom-events", type=int, default=1,
                     help="1: HIP events around the dominant kernel inside the timed region (the roofline's "
                          "duration); 0: none in the timed region, the duration from an identical pass after it")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch per kernel (written by tools/pmc_traffic.py)")
+    ap.add_argument("--traffic-dir", default=os.path.join(ROOT, "profiles"),
+                    help="PMC-derived HBM bytes per launch per kernel, traffic_<workload>.json per workload "
+                         "(written by tools/pmc_traffic.py from tools/gpu_prof.sh's passes)")
     return ap.parse_args()
 
 
@@ -272,7 +273,13 @@ def dominant(prof, alg_keys, exclude=()):
     return max(known, key=lambda k: known[k][0])
 
 
-def traffic_of(path, kernel):
+TRAFFIC_DIR = os.path.join(ROOT, "profiles")
+
+
+def traffic_of(kernel, workload):
+    """HBM bytes per launch of `kernel` in `workload` from the PMC passes
+    (profiles/traffic_<workload>.json), or None."""
+    path = os.path.join(TRAFFIC_DIR, "traffic_%s.json" % workload)
     if not os.path.exists(path):
         return None
     t = json.load(open(path)).get(kernel)
@@ -304,8 +311,10 @@ def emit(obj):
 
 
 def main():
+    global TRAFFIC_DIR
     quiet_stdout()
     a = parse()
+    TRAFFIC_DIR = a.traffic_dir
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -342,6 +351,11 @@ def main():
         eng.close()
         if world > 1:
             dist.destroy_process_group()
+        return
+    if workload == "adversarial":  # the client_adversarial leg alone (profiling)
+        eng = Engine(local)
+        emit(dict(adversarial_leg(eng, a), metric=METRIC + " [client config 5 leg]"))
+        eng.close()
         return
     if workload == "server":
         out = server_run(a, rank, world, local, a.owners, a.per_owner, a.zipf, a.request, cpu=rank == 0 and world == 1)
@@ -462,7 +476,7 @@ def main():
         alg = ALG_BYTES_PER_MSG[dom] * a.messages
         achieved = alg / avg_s
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "traffic": traffic_of(a.traffic, dom),
+                "frac": achieved / HBM_PEAK, "traffic": traffic_of(dom, "client"),
                 "kernel_ms_avg": avg_s * 1e3, "alg_bytes_per_launch": alg,
                 "kernel_share_of_step": tot_ms / (ms_step * a.steps)}
         out = {
@@ -520,9 +534,6 @@ DIST_ALG = {
     "(k_dist_scatter<SEND>)": 48 + 4 + 4 + 32,  # ts row + owner + cell in, packed record out
     "(k_dist_scatter<RECV>)": 32 + 48 + 4 + 4,  # packed record in; rebuilt ts row + owner + cell out
 }
-
-
-DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
 
 
 def make_dist(eng, rank, world):
@@ -651,7 +662,7 @@ def client_routed(a, rank, world, local):
                    "messages_per_gpu": M, "owners_per_gpu": K, "cells_per_owner": a.cells,
                    "parallelism": "owner-sharded, %d rank(s), RCCL all-to-all" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9,
-                     "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(a.traffic, dom),
+                     "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(dom, "config4c"),
                      "kernel_ms_avg": avg_s * 1e3, "alg_bytes_per_launch": alg,
                      "kernel_share_of_step": tot_ms / (ms * a.steps)},
         "route": {"ms_per_step": route_ms_avg, "bytes_per_msg": ROUTE_BYTES,
@@ -913,7 +924,7 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
                    "messages_per_gpu": n, "owners_total": O, "owners_per_gpu": owners_per_gpu,
                    "owners_this_rank": n_local, "parallelism": "owner-sharded (murmur3 mod %d), %s" % (world, dd.transport)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9,
-                     "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(DEFAULT_TRAFFIC, dom),
+                     "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(dom, "config4"),
                      "kernel_ms_avg": avg_s * 1e3, "alg_bytes_per_launch": alg,
                      "kernel_share_of_step": tot_ms / (ms * steps)},
         "pipeline": {"alg_bytes_per_msg": SERVER_PIPELINE_BYTES,
@@ -1024,7 +1035,7 @@ def adversarial_leg(eng, a):
             "no_op_rows": int((f == 0).sum()), "xor_only_rows": int((f == 2).sum()), "upsert_rows": int((f == 3).sum()),
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "kernel_ms_avg": avg_s * 1e3,
-                         "alg_bytes_per_launch": alg},
+                         "alg_bytes_per_launch": alg, "traffic": traffic_of(dom, "client_adversarial")},
             "pipeline_hbm_frac": 120 * n / (dt / a.steps) / HBM_PEAK,
             "kernels_ms_per_step": {k: v[0] / 3 for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:12]}}
 
@@ -1032,6 +1043,7 @@ def adversarial_leg(eng, a):
 def config1_leg(eng, a):
     """BASELINE config 1: the todo-schema stream (100k messages, one owner),
     one applyMessages batch from an empty tree, inputs in HBM."""
+    import numpy as np
     import torch
 
     from evolu_amd import synth
@@ -1068,7 +1080,72 @@ def config1_leg(eng, a):
            "path": "sort path (> 2,048 cells): radix sort by cell + segmented scan",
            "kernels_ms_per_batch": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:10]},
            "cpu_baseline": cpu_baseline(ts_np, cell_np, a.cpu_seconds, "config-1") if a.cpu_seconds > 0 else None}
+    # per-batch latency at the sizes a client applies (send.ts:107-111 one
+    # mutation's messages; receive.ts:84-87 one sync's): the first k messages
+    # of the stream, cells renumbered, one synchronous applyMessages each
+    lat = {}
+    for k in (100, 1000, 10_000, 100_000):
+        k = min(k, len(ts_np))
+        used, cid = np.unique(cell_np[:k], return_inverse=True)
+        ts_k, cell_k = eng.dev(ts_np[:k]), eng.dev(cid.astype(np.uint32))
+        fl = torch.empty(k, dtype=torch.uint8, device=ts.device)
+        wn = torch.empty(len(used), dtype=torch.int32, device=ts.device)
+        for _ in range(3):
+            eng.apply_batch(empty, ts_k, cell_k, len(used), flags=fl, winner=wn)[2].free()
+        xs = []
+        for _ in range(30):
+            t0 = time.perf_counter()
+            eng.apply_batch(empty, ts_k, cell_k, len(used), flags=fl, winner=wn)[2].free()
+            xs.append((time.perf_counter() - t0) * 1e3)  # (the call returns after its status read: synchronous)
+        xs.sort()
+        lat[str(k)] = {"p50_ms": xs[len(xs) // 2], "p90_ms": xs[int(len(xs) * 0.9)], "cells": int(len(used))}
+    out["latency_per_batch"] = lat
     return out
+
+
+def reingest(eng, a, ts1, own1, owners, per_owner, request, flags):
+    """The server's steady state: a second round of requests (new messages
+    of the same owners: another seed's stream) ingested into a store that
+    already holds the first round's owners x per_owner rows -- addMessages
+    with the stored rows and trees merged (k_svo_b), then getMessages is not
+    timed here.  Timed per ingest, the first ingest untimed."""
+    import torch
+
+    from evolu_amd import synth
+
+    ts2_np, own2_np, _ = synth.config3(owners, per_owner, seed_config=3 + 7919, request=request)
+    ts2, own2 = eng.dev(ts2_np), eng.dev(own2_np)
+    del ts2_np, own2_np
+    f2 = torch.empty(ts2.shape[0], dtype=torch.uint8, device=ts2.device)
+    reps = max(2, min(a.steps, 5))
+    ms = []
+    prof = None
+    for r in range(reps + 1):
+        st = eng.store_new(owners)
+        st.ingest(ts1, own1, 0, flags=flags)
+        if r == reps:
+            eng.prof_enable(True)
+            eng.prof_reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st.ingest(ts2, own2, 1 << 40, flags=f2)
+        torch.cuda.synchronize()
+        if r == reps:
+            prof = eng.prof_report()
+            eng.prof_enable(False)
+        elif r > 0:
+            ms.append((time.perf_counter() - t0) * 1e3)
+        n_stored = st.n_messages
+        st.free()
+    n = ts2.shape[0]
+    m = sorted(ms)[len(ms) // 2]
+    dom = dominant(prof, SERVER_ALG)
+    tot_ms, launches = prof[dom]
+    return {"workload": "a second round of %d msgs (%d owners, new timestamps) into a store holding %d rows: "
+                        "addMessages with the stored rows and trees merged" % (n, owners, ts1.shape[0]),
+            "value": n / m * 1e3, "unit": "msgs/s", "ms_per_ingest_median": m, "ms_per_ingest": [round(x, 3) for x in ms],
+            "stored_after": int(n_stored), "dominant_kernel": dom, "dominant_kernel_ms": tot_ms / launches,
+            "kernels_ms": {k: v[0] for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:10]}}
 
 
 def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=False, leg=False):
@@ -1219,7 +1296,7 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
     per_msg, per_leaf = SERVER_ALG[dom]
     alg = per_msg * n + per_leaf * n_leaves
     roof = {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(a.traffic, dom), "kernel_ms_avg": avg_s * 1e3,
+            "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(dom, "config3" if zipf <= 0 else "config5"), "kernel_ms_avg": avg_s * 1e3,
             "alg_bytes_per_launch": alg, "alg_bytes": "%d B/msg + %d B/new leaf (%d leaves)" % (per_msg, per_leaf, n_leaves),
             "kernel_share_of_step": tot_ms / (ms * a.steps)}
     reqs = "one SyncRequest per owner" if request >= per_owner else "requests of %d" % request
@@ -1244,6 +1321,8 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
     if leg:
         for k in ("metric", "n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
             out.pop(k)
+    if world == 1 and zipf <= 0:
+        out["reingest"] = reingest(eng, a, ts_r, lown, owners, per_owner, request, flags)
     if dd is not None:
         dd.free()
     eng.close()

@@ -13,7 +13,9 @@ read, so it is doubled here (this kernel family's loads are 16-B-per-lane
 streams); WRITE_SIZE reads exactly for 16-B streaming stores.  The Infinity
 Cache is not excluded by these counters (bench inputs are 0.5 GB, > 256 MiB).
 
-Usage: python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/traffic.json
+Usage: python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/traffic_<workload>.json
+(one pair of passes per workload: a kernel's bytes per launch depend on the
+workload's size, so bench.py reads the file of the leg it reports)
 """
 import collections
 import csv
@@ -45,6 +47,10 @@ def short(name):
     base, targs = m.group(1), m.group(2) or ""
     if base in ("k_radix_scatter", "k_radix_hist", "k_scan_down", "k_scan_reduce", "k_scan_partials"):
         return None
+    if base == "k_dist_scatter" and targs:
+        return "(k_dist_scatter<%s>)" % ("SEND" if targs.strip("<>") == "0" else "RECV")
+    if base == "k_dist_count" and targs:
+        return "(k_dist_count<MODE>)"
     if base == "k_svo_a" and targs:
         # KLAUNCH names the template launch by its source text: "(k_svo_a<1024, true>)"
         args = [a.strip().rstrip("u") for a in targs[1:-1].split(",")]
