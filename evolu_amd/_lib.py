@@ -113,6 +113,15 @@ SIGNATURES = {
     "evm_dist_route": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, C.POINTER(C.c_uint64)]),
     "evm_dist_take": (_i, [_vp, _vp, _u32, _vp, _sz, _vp, _vp, _vp, C.c_uint64, _vp]),
     "evm_dist_gather_roots": (_i, [_vp, _vp, _vp, _u32, _u32, _vp, _vp]),
+    "evm_dist_hot_owners": (_i, [_vp, _vp, _vp, _sz, _u32, C.c_double, _vp, _u32, C.POINTER(_u32)]),
+    "evm_dist_split": (_i, [_vp, _vp, _vp, _u32, _u32, C.POINTER(_u32)]),
+    "evm_dist_merge_trees": (_i, [_vp, _vp, _vp, _u32, _u32, C.POINTER(_vp)]),
+    "evm_dist_merge_select": (_i, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "evm_dist_ts_dest": (_i, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "evm_dist_cell_dest": (_i, [_vp, _vp, _vp, _sz, _vp]),
+    "evm_dist_return": (_i, [_vp, _vp, _vp, _u32, _vp, _sz]),
+    "evm_dist_split_winners": (_i, [_vp, _vp, _vp, _u32, _vp]),
+    "evm_dist_agree_status": (_i, [_vp, _vp, C.c_int32, C.POINTER(C.c_int32)]),
     "evm_apply_batch": (
         _i,
         [_vp, _vp, _vp, _sz, _sz, _vp, _u32, _vp, _vp, _sz, _vp, _vp, _vp, C.POINTER(_vp)],

@@ -748,6 +748,9 @@ __global__ __launch_bounds__(XP_THREADS) void k_xp_scatter(const u32* __restrict
 // One bucket per workgroup: insert every (hash, index) into an LDS set of u32
 // slots = tag:17 | (local index + 1):15; a tag match re-reads the other pair's
 // full hash (L2-hot), and equal hashes compare the raw 46 timestamp bytes.
+// (Probing past same-cell equal hashes to skip the byte reads of redeliveries
+// measured slower: 82 vs 75 us per config-2 batch -- longer chains, and the
+// two cell reads cost what the row reads did.)
 // A pair gets XP_INLINE_PROBES probes in its wave's round; one still unplaced
 // is queued (its next slot kept) and finished after the rounds, one per lane
 // -- so a long probe chain no longer holds its whole wave at every round.
@@ -1277,66 +1280,99 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
   block_fold_bounds<u32, TP_THREADS>(mn, mx, bad, &info->minute_min, &info->minute_max, &info->bad);
 }
 
-// TP2: per cell, exclusive max over the G range maxima (3 phases over
-// CARRY_SEGS segments), seeded with the prior max; the final max -> winner.
-__global__ void k_tp_carry_reduce(u32 C, size_t G, const u64* __restrict__ agg, const u32* __restrict__ arow,
-                                  NodeSrc N, u64* __restrict__ s_max, u32* __restrict__ s_row) {
-  const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
-  if (c >= C) return;
-  const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
-  const size_t a = p * per, e = min(G, a + per);
+// TP2: per cell, the exclusive max over the G range maxima seeded with the
+// prior max, and the final max -> winner.  One workgroup per CT_CELLS cells:
+// each of its CT_GROUPS lane groups reduces a contiguous segment of ranges
+// (CT_CELLS consecutive cells = one 128-B read per range), one wave per cell
+// scans the segment maxima in LDS, and the groups write their segment's
+// running maxima (the second read of the tile hits L2).
+constexpr u32 CT_CELLS = 16, CT_GROUPS = 64, CT_THREADS = CT_CELLS * CT_GROUPS;
+
+__global__ __launch_bounds__(CT_THREADS) void k_tp_carry(u32 C, size_t G, u64* __restrict__ agg,
+                                                         u32* __restrict__ arow, NodeSrc N,
+                                                         const uint8_t* __restrict__ prior_present,
+                                                         int32_t* __restrict__ winner) {
+  __shared__ u64 s_tc[CT_GROUPS][CT_CELLS];
+  __shared__ u32 s_row[CT_GROUPS][CT_CELLS];
+  const u32 cl = threadIdx.x % CT_CELLS, grp = threadIdx.x / CT_CELLS;
+  const u32 c = blockIdx.x * CT_CELLS + cl;
+  const bool ok = c < C;
+  const size_t per = (G + CT_GROUPS - 1) / CT_GROUPS;
+  const size_t a = min(G, grp * per), e = min(G, a + per);
   // (a range without rows holds (0, ROW_NONE); a row of tc 0 ties with it and
   // takes the rare path, which ranks NONE below every row)
+  // (CT_BATCH loads in flight per lane before any compare: the rare tie
+  // compare reads memory and would otherwise serialise the loads)
+  constexpr int CT_BATCH = 8;
   TK m{0, ROW_NONE};
-#pragma unroll 8
-  for (size_t g = a; g < e; ++g) {
-    const TK x{agg[g * C + c], arow[g * C + c]};
-    if (x.tc > m.tc) m = x;
-    else if (x.tc == m.tc && x.row != m.row) m = tk_max(N, c, m, x);  // (rare: equal tc in two ranges)
-  }
-  s_max[(size_t)p * C + c] = m.tc;
-  s_row[(size_t)p * C + c] = m.row;
-}
-
-__global__ __launch_bounds__(256) void k_tp_carry_segs(u32 C, u64* __restrict__ s_max, u32* __restrict__ s_row,
-                                                       NodeSrc N, const uint8_t* __restrict__ prior_present,
-                                                       int32_t* __restrict__ winner) {
-  const u32 c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (c >= C) return;
-  const size_t o = (size_t)lane * C + c;
-  TK v{s_max[o], s_row[o]};
+  if (ok) {
+    for (size_t g0 = a; g0 < e; g0 += CT_BATCH) {
+      u64 t[CT_BATCH];
+      u32 r[CT_BATCH];
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const TK u = shfl_tk(v, (int)lane - d < 0 ? (int)lane : (int)lane - d);
-    if ((int)lane >= d) v = tk_max(N, c, u, v);
+      for (int k = 0; k < CT_BATCH; ++k) {
+        const size_t g = g0 + k;
+        t[k] = g < e ? agg[g * C + c] : 0ull;
+        r[k] = g < e ? arow[g * C + c] : ROW_NONE;
+      }
+#pragma unroll
+      for (int k = 0; k < CT_BATCH; ++k) {
+        const TK x{t[k], r[k]};
+        if (x.tc > m.tc) m = x;
+        else if (x.tc == m.tc && x.row != m.row) m = tk_max(N, c, m, x);  // (rare: equal tc in two ranges)
+      }
+    }
   }
-  const TK seed = (prior_present && prior_present[c]) ? TK{N.prior[c].tc, ROW_PRIOR} : TK{0, ROW_NONE};
-  const TK ex = shfl_tk(v, lane == 0 ? 0 : (int)lane - 1);
-  const TK e = lane == 0 ? seed : tk_max(N, c, seed, ex);
-  s_max[o] = e.tc;
-  s_row[o] = e.row;
-  if (lane == 63) {
-    // the last upsert is the first occurrence of the final max (none if the
-    // prior max or nothing holds it)
-    const TK f = tk_max(N, c, seed, v);
-    winner[c] = (f.row == ROW_NONE || f.row == ROW_PRIOR) ? -1 : (int32_t)f.row;
+  s_tc[grp][cl] = m.tc;
+  s_row[grp][cl] = m.row;
+  __syncthreads();
+  {
+    const u32 w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const u32 cw = blockIdx.x * CT_CELLS + w;
+    static_assert(CT_GROUPS == 64 && CT_THREADS / 64 == CT_CELLS, "one wave per cell, one lane per group");
+    if (cw < C) {
+      TK v{s_tc[lane][w], s_row[lane][w]};
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const TK u = shfl_tk(v, (int)lane - d < 0 ? (int)lane : (int)lane - d);
+        if ((int)lane >= d) v = tk_max(N, cw, u, v);
+      }
+      const TK seed = (prior_present && prior_present[cw]) ? TK{N.prior[cw].tc, ROW_PRIOR} : TK{0, ROW_NONE};
+      const TK ex = shfl_tk(v, lane == 0 ? 0 : (int)lane - 1);
+      const TK x = lane == 0 ? seed : tk_max(N, cw, seed, ex);
+      s_tc[lane][w] = x.tc;
+      s_row[lane][w] = x.row;
+      if (lane == 63) {
+        // the last upsert is the first occurrence of the final max (none if
+        // the prior max or nothing holds it)
+        const TK f = tk_max(N, cw, seed, v);
+        winner[cw] = (f.row == ROW_NONE || f.row == ROW_PRIOR) ? -1 : (int32_t)f.row;
+      }
+    }
   }
-}
-
-__global__ void k_tp_carry_down(u32 C, size_t G, u64* __restrict__ agg, u32* __restrict__ arow, NodeSrc N,
-                                const u64* __restrict__ s_max, const u32* __restrict__ s_row) {
-  const u32 c = blockIdx.x * blockDim.x + threadIdx.x, p = blockIdx.y;
-  if (c >= C) return;
-  const size_t per = (G + CARRY_SEGS - 1) / CARRY_SEGS;
-  const size_t a = p * per, e = min(G, a + per);
-  TK run{s_max[(size_t)p * C + c], s_row[(size_t)p * C + c]};
-#pragma unroll 8
-  for (size_t g = a; g < e; ++g) {
-    const TK here{agg[g * C + c], arow[g * C + c]};
-    agg[g * C + c] = run.tc;
-    arow[g * C + c] = run.row;
-    if (here.tc > run.tc) run = here;
-    else if (here.tc == run.tc && here.row != run.row) run = tk_max(N, c, run, here);
+  __syncthreads();
+  if (!ok) return;
+  TK run{s_tc[grp][cl], s_row[grp][cl]};
+  for (size_t g0 = a; g0 < e; g0 += CT_BATCH) {
+    u64 t[CT_BATCH];
+    u32 r[CT_BATCH];
+#pragma unroll
+    for (int k = 0; k < CT_BATCH; ++k) {
+      const size_t g = g0 + k;
+      t[k] = g < e ? agg[g * C + c] : 0ull;
+      r[k] = g < e ? arow[g * C + c] : ROW_NONE;
+    }
+#pragma unroll
+    for (int k = 0; k < CT_BATCH; ++k) {
+      const size_t g = g0 + k;
+      if (g < e) {
+        agg[g * C + c] = run.tc;
+        arow[g * C + c] = run.row;
+      }
+      const TK here{t[k], r[k]};
+      if (here.tc > run.tc) run = here;
+      else if (here.tc == run.tc && here.row != run.row) run = tk_max(N, c, run, here);
+    }
   }
 }
 
@@ -1714,16 +1750,9 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   }
   if (TC) {
     // TP2: per cell, exclusive max over the ranges (in place in agg) + final max
-    u64* s_max = S.alloc<u64>((size_t)CARRY_SEGS * C);
-    u32* s_row = S.alloc<u32>((size_t)CARRY_SEGS * C);
-    if (!s_max || !s_row) return EVM_ENOMEM;
     const NodeSrc N{(const uint8_t*)ts, stride, prior};
-    const u32 cb = (C + 63) / 64;
-    KLAUNCH(k_tp_carry_reduce, dim3(cb, CARRY_SEGS), dim3(64), C, G, (const u64*)agg, (const u32*)arow, N, s_max,
-            s_row);
-    KLAUNCH(k_tp_carry_segs, dim3((C + 3) / 4), dim3(256), C, s_max, s_row, N, prior_present, winner);
-    KLAUNCH(k_tp_carry_down, dim3(cb, CARRY_SEGS), dim3(64), C, G, agg, arow, N, (const u64*)s_max,
-            (const u32*)s_row);
+    KLAUNCH(k_tp_carry, dim3((C + CT_CELLS - 1) / CT_CELLS), dim3(CT_THREADS), C, G, agg, arow, N, prior_present,
+            winner);
     // TP3: flags, a workgroup per range
     KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14 + (size_t)C * 4,
                 (const u64*)tcs, cell, n, C, range, (const u64*)agg, (const u32*)arow, N, flags);
@@ -1940,9 +1969,11 @@ static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
     if (!info || !prior) return EVM_ENOMEM;
     // one launch: the status record, and winner = -1 for every cell; the
     // cells' current maxima (SELECT ... ORDER BY timestamp DESC LIMIT 1)
-    auto init = [&]() -> int {
-      KLAUNCH(k_apply_init, dim3(grid_for(std::max<size_t>(n_cells, 1), 256)), dim3(256), info, info_init(), winner,
-              (size_t)n_cells);
+    // (the tc path's carry writes every cell's winner itself)
+    const bool tc_path = n && path != 1 && (path == 3 || (path == 0 && !cell_owner && n_cells <= CL_MAX_CELLS));
+    auto init = [&](bool winners) -> int {
+      const size_t nw = winners ? n_cells : 0;
+      KLAUNCH(k_apply_init, dim3(grid_for(std::max<size_t>(nw, 1), 256)), dim3(256), info, info_init(), winner, nw);
       if (prior_present && n_cells) {
         int e = launch_pack(ctx, prior_ts, prior_stride, n_cells, nullptr, 0, prior, nullptr);
         if (e) return e;
@@ -1950,7 +1981,7 @@ static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
       }
       return EVM_OK;
     };
-    if ((st = init())) return st;
+    if ((st = init(!tc_path))) return st;
     if (n == 0) {
       Info hi;
       if ((st = read_info(ctx, info, &hi))) return st;
@@ -1969,7 +2000,7 @@ static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
       }
       if (st == TP_REDO) {
         // a tie (equal millis and counter in one cell): the exact walk path
-        if (path != 1 && (st = init())) return st;
+        if (path != 1 && (st = init(true))) return st;
         st = apply_stream<false>(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, prior, prior_present, stored,
                                  flags, winner, tree_out);
       }

@@ -253,12 +253,16 @@ constexpr u32 W_ROFF = 2 * MAX_BUCKETS;        // [65] receive offsets (rows)
 constexpr u32 W_AGREE_S = 3 * MAX_BUCKETS + 8; // [64] agreement words sent
 constexpr u32 W_AGREE_R = 4 * MAX_BUCKETS + 8; // [64] agreement words received
 constexpr u32 W_BAD = 5 * MAX_BUCKETS + 8;     // the local flags: [0] bad destination, [1] invalid row
-constexpr u32 CNT_WORDS = 5 * MAX_BUCKETS + 16;
+constexpr u32 W_GS = 5 * MAX_BUCKETS + 16;     // [2] (status, value) gathered
+constexpr u32 W_GR = 5 * MAX_BUCKETS + 18;     // [2 * 64] every rank's (status, value)
+constexpr u32 CNT_WORDS = 7 * MAX_BUCKETS + 24;
 
-// Routing of row i.  SEND: the destination rank -- the caller's dest, the
-// directory's rank of the owner, or owner % world.  RECV (wire records, owner
-// at byte `ooff`): the local owner -- the directory's local id, or owner /
-// world.  >= B: out of range (reported, not routed).
+// Routing of row i.  SEND: the destination rank -- the caller's dest, a hash
+// of the row's timestamp for a split (hot) owner, the directory's rank of the
+// owner, or owner % world.  RECV (wire records, owner at byte `ooff`): the
+// local owner -- hot_base + hot index for a split owner, the directory's local
+// id, or owner / world.  >= B: out of range (reported, not routed).
+constexpr u32 HOT_NONE = 0xffffffffu;
 struct Route {
   const u32* owner;
   const uint8_t* dest;
@@ -266,19 +270,50 @@ struct Route {
   const u32* dir_local;      // directory: local id of every global owner on its rank
   u32 n_dir;
   u32 world;
+  const u32* hot;            // split: hot index of every global owner (HOT_NONE: not split)
+  u32 n_hot_tab;             // global owners the table covers
+  u32 hot_base;              // local id of hot owner 0 on every rank
+  const char* ts;            // SEND: the rows (a split owner's rows go by timestamp hash)
+  size_t stride;
 };
+
+// The timestamp-hash rank of a row (murmur3 of its 46 bytes: equal strings,
+// equal ranks -- every copy of one (owner, timestamp) meets on one rank, so
+// INSERT OR IGNORE and the Merkle XOR stay exact per rank).  stride % 8 == 0.
+__device__ __forceinline__ u32 ts_rank(const char* row, u32 world) {
+  const uint2* q = reinterpret_cast<const uint2*>(row);
+  u32 w[12];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint2 v = q[k];
+    w[2 * k] = v.x;
+    w[2 * k + 1] = v.y;
+  }
+  w[11] &= 0xffffu;
+  return murmur3_46(w) % world;
+}
+
+__device__ __forceinline__ bool is_hot(const Route& R, u32 o) {
+  return R.hot && o < R.n_hot_tab && R.hot[o] != HOT_NONE;
+}
+
+__device__ __forceinline__ u32 local_of(const Route& R, u32 o) {
+  if (is_hot(R, o)) return R.hot_base + R.hot[o];
+  if (R.dir_local) return o < R.n_dir ? R.dir_local[o] : 0xffffffffu;
+  return o / R.world;
+}
 
 template <int MODE>
 __device__ __forceinline__ u32 bucket_of(size_t i, const Route& R, const char* rec, size_t rb, size_t ooff) {
   if (MODE == 0) {
     if (R.dest) return R.dest[i];
     const u32 o = R.owner[i];
+    if (is_hot(R, o)) return ts_rank(R.ts + i * R.stride, R.world);
     if (R.dir_dest) return o < R.n_dir ? (u32)R.dir_dest[o] : 0xffffffffu;
     return o % R.world;
   }
   const u32 o = *reinterpret_cast<const u32*>(rec + i * rb + ooff);
-  if (R.dir_local) return o < R.n_dir ? R.dir_local[o] : 0xffffffffu;
-  return o / R.world;
+  return local_of(R, o);
 }
 enum { SEND = 0, RECV = 1 };
 
@@ -435,7 +470,7 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
         copy_row(out_ts + pos * out_stride, src, stride);
         m = *reinterpret_cast<const uint4*>(src + stride);
       }
-      out_owner[pos] = R.dir_local ? (m.x < R.n_dir ? R.dir_local[m.x] : 0xffffffffu) : m.x;
+      out_owner[pos] = (R.dir_local || R.hot) ? local_of(R, m.x) : m.x;
       if (out_aux) out_aux[pos] = m.y;
       if (out_src) {
         // source rank: the last r with roff[r] <= i
@@ -485,12 +520,25 @@ __global__ void k_dist_root_pack(const u64* __restrict__ off, const int32_t* __r
 }
 
 // gathered [rank][per + 1] -> global owner g: local g / world of rank g % world,
-// or the directory's (rank, local) of g
+// or the directory's (rank, local) of g; a split owner: the XOR of every
+// rank's partial root at its hot slot (present if any part is)
 __global__ void k_dist_root_unpack(const u64* __restrict__ all, u32 world, u32 stride, u32 n_global,
                                    const uint8_t* __restrict__ dir_dest, const u32* __restrict__ dir_local,
+                                   const u32* __restrict__ hot, u32 n_hot_tab, u32 hot_base,
                                    int32_t* __restrict__ root, uint8_t* __restrict__ present) {
   for (u32 g = blockIdx.x * blockDim.x + threadIdx.x; g < n_global; g += gridDim.x * blockDim.x) {
-    const u64 v = dir_dest ? all[(size_t)dir_dest[g] * stride + dir_local[g]] : all[(size_t)(g % world) * stride + g / world];
+    u64 v;
+    if (hot && g < n_hot_tab && hot[g] != HOT_NONE) {
+      u32 x = 0, p = 0;
+      for (u32 r = 0; r < world; ++r) {
+        const u64 w = all[(size_t)r * stride + hot_base + hot[g]];
+        x ^= (u32)w;
+        p |= (u32)(w >> 32);
+      }
+      v = (u64)x | ((u64)(p != 0) << 32);
+    } else {
+      v = dir_dest ? all[(size_t)dir_dest[g] * stride + dir_local[g]] : all[(size_t)(g % world) * stride + g / world];
+    }
     root[g] = (int32_t)(uint32_t)v;
     present[g] = (uint8_t)(v >> 32);
   }
@@ -552,6 +600,177 @@ __global__ __launch_bounds__(DT) void k_dir_local(const uint8_t* __restrict__ de
   }
 }
 
+
+// ------------------------------------------------------------------ split kernels
+// Rows per global owner (hot-owner detection).
+__global__ void k_split_hist(const u32* __restrict__ owner, size_t n, u32 n_global, u64* __restrict__ counts,
+                             u32* __restrict__ bad) {
+  bool oob = false;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const u32 o = owner[i];
+    if (o < n_global) atomicAdd(&counts[o], 1ull);
+    else oob = true;
+  }
+  if (__ballot(oob) && __lane_id() == 0) atomicOr(bad, 1u);
+}
+
+// Owners whose row count over all ranks exceeds thr (gathered [rank][per]).
+__global__ void k_split_select(const u64* __restrict__ all, u32 world, size_t per, u32 n_global, u64 thr,
+                               u32* __restrict__ list, u32* __restrict__ n_list, u32 cap) {
+  for (u32 g = blockIdx.x * blockDim.x + threadIdx.x; g < n_global; g += gridDim.x * blockDim.x) {
+    u64 t = 0;
+    for (u32 r = 0; r < world; ++r) t += all[(size_t)r * per + g];
+    if (t > thr) {
+      const u32 k = atomicAdd(n_list, 1u);
+      if (k < cap) list[k] = g;
+    }
+  }
+}
+
+__global__ void k_ts_dest(const char* __restrict__ ts, size_t stride, size_t n, u32 world, uint8_t* __restrict__ dest) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dest[i] = (uint8_t)ts_rank(ts + i * stride, world);
+}
+
+// a fixed mix of the cell id (dist.py cell_dest)
+__global__ void k_cell_dest(const u32* __restrict__ cell, size_t n, u32 world, uint8_t* __restrict__ dest) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dest[i] = (uint8_t)(((cell[i] * 0x9E3779B1u) >> 8) % world);
+}
+
+// Leaves of owners [lo, lo + count) rebased to owner 0: [L][ck x L][xr, two per word]
+__global__ void k_merge_pack(const u64* __restrict__ ck, const int32_t* __restrict__ xr, u64 a, u64 L, u32 lo,
+                             u64* __restrict__ out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = L;
+  u64* oc = out + 1;
+  int32_t* ox = reinterpret_cast<int32_t*>(out + 1 + L);
+  for (u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x; k < L; k += (u64)gridDim.x * blockDim.x) {
+    oc[k] = ck[a + k] - ((u64)lo << 40);
+    ox[k] = xr[a + k];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (L & 1)) ox[L] = 0;
+}
+
+// selection payload: [n + 1 offsets from 0][m ids][3m keys]
+__global__ void k_sel_pack(const uint64_t* __restrict__ off, const uint64_t* __restrict__ id,
+                           const uint64_t* __restrict__ key, u32 n, u64 m, u64* __restrict__ out) {
+  const u64 a = off[0];
+  for (u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x; k < (u64)n + 1 + 4 * m; k += (u64)gridDim.x * blockDim.x) {
+    u64 v;
+    if (k <= n) v = off[k] - a;
+    else if (k <= n + m) v = id[a + (k - n - 1)];
+    else v = key[3 * a + (k - n - 1 - m)];
+    out[k] = v;
+  }
+}
+
+__device__ __forceinline__ bool key_lt3(const u64* a, const u64* b) {
+  return a[0] != b[0] ? a[0] < b[0] : (a[1] != b[1] ? a[1] < b[1] : a[2] < b[2]);
+}
+
+// out_off[g] = sum over ranks of their group offsets
+__global__ void k_sel_off(const u64* __restrict__ all, u32 world, size_t per, u32 n, uint64_t* __restrict__ out_off) {
+  for (u32 g = blockIdx.x * blockDim.x + threadIdx.x; g <= n; g += gridDim.x * blockDim.x) {
+    u64 t = 0;
+    for (u32 r = 0; r < world; ++r) t += all[(size_t)r * per + g];
+    out_off[g] = t;
+  }
+}
+
+// Every gathered row to its place: its group's start + its rank inside its
+// own part + the rows of the other ranks' parts of the group that sort before
+// it (equal keys: the lower rank first).  rbase: [world + 1] row prefix.
+__global__ void k_sel_merge(const u64* __restrict__ all, u32 world, size_t per, u32 n, const u64* __restrict__ rbase,
+                            const uint64_t* __restrict__ out_off, uint64_t* __restrict__ out_id) {
+  const u64 M = rbase[world];
+  for (u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x; t < M; t += (u64)gridDim.x * blockDim.x) {
+    u32 p = 0;
+    while (rbase[p + 1] <= t) ++p;
+    const u64 j = t - rbase[p];
+    const u64* A = all + (size_t)p * per;
+    const u64 mp = A[n];
+    // group of row j: the last g with off[g] <= j
+    u32 lo = 0, hi = n;
+    while (hi - lo > 1) {
+      const u32 mid = (lo + hi) >> 1;
+      if (A[mid] <= j) lo = mid;
+      else hi = mid;
+    }
+    const u32 g = lo;
+    const u64* key = A + n + 1 + mp + 3 * j;
+    u64 pos = out_off[g] + (j - A[g]);
+    for (u32 q = 0; q < world; ++q) {
+      if (q == p) continue;
+      const u64* B = all + (size_t)q * per;
+      const u64 mq = B[n];
+      const u64* kq = B + n + 1 + mq;
+      u64 a = B[g], b = B[g + 1];
+      // rows of q's group g before this key: < key (q > p) or <= key (q < p)
+      while (a < b) {
+        const u64 mid = (a + b) >> 1;
+        const bool before = q < p ? !key_lt3(key, kq + 3 * mid) : key_lt3(kq + 3 * mid, key);
+        if (before) a = mid + 1;
+        else b = mid;
+      }
+      pos += a - B[g];
+    }
+    out_id[pos] = A[n + 1 + j];
+  }
+}
+
+// return path: (source index, value) of every received row, in receive order
+__global__ void k_ret_pack(const char* __restrict__ rec, size_t rb, size_t ooff, size_t n,
+                           const uint8_t* __restrict__ val, u32 elem, u64* __restrict__ out) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const u32 idx = *reinterpret_cast<const u32*>(rec + k * rb + ooff + 8);
+    u64 v = 0;
+    for (u32 b = 0; b < elem; ++b) v |= (u64)val[k * elem + b] << (8 * b);
+    out[2 * k] = idx;
+    out[2 * k + 1] = v;
+  }
+}
+
+__global__ void k_ret_scatter(const u64* __restrict__ in, size_t n, uint8_t* __restrict__ out, size_t n_out, u32 elem,
+                              u32* __restrict__ bad) {
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const u64 idx = in[2 * k], v = in[2 * k + 1];
+    if (idx >= n_out) {
+      atomicOr(bad, 1u);
+      continue;
+    }
+    for (u32 b = 0; b < elem; ++b) out[idx * elem + b] = (uint8_t)(v >> (8 * b));
+  }
+}
+
+// winners: index into the receive order -> global batch index + 1 (0: none)
+__global__ void k_win_map(const int32_t* __restrict__ win, u32 n_cells, const char* __restrict__ rec, size_t rb,
+                          size_t ooff, u64 n_recv, const u64* __restrict__ roff, u32 world,
+                          const u64* __restrict__ base, u64* __restrict__ out, u32* __restrict__ bad) {
+  for (u32 c = blockIdx.x * blockDim.x + threadIdx.x; c < n_cells; c += gridDim.x * blockDim.x) {
+    const int32_t w = win[c];
+    u64 v = 0;
+    if (w >= 0) {
+      if ((u64)w >= n_recv) {
+        atomicOr(bad, 1u);
+      } else {
+        u32 s = 0;
+        while (s + 1 < world && roff[s + 1] <= (u64)w) ++s;
+        const u32 idx = *reinterpret_cast<const u32*>(rec + (size_t)w * rb + ooff + 8);
+        v = base[s] + idx + 1;
+      }
+    }
+    out[c] = v;
+  }
+}
+
+__global__ void k_win_reduce(const u64* __restrict__ all, u32 world, size_t per, u32 n_cells, int64_t* __restrict__ out) {
+  for (u32 c = blockIdx.x * blockDim.x + threadIdx.x; c < n_cells; c += gridDim.x * blockDim.x) {
+    u64 m = 0;
+    for (u32 r = 0; r < world; ++r) m = max(m, all[(size_t)r * per + c]);
+    out[c] = (int64_t)m - 1;
+  }
+}
+
 }  // namespace
 
 struct evm_dist {
@@ -573,6 +792,13 @@ struct evm_dist {
   u32 n_dir = 0;
   u32 dir_per = 0;      // the most owners any rank serves
   u32 dir_n_local = 0;  // owners this rank serves
+  // hot-owner split (evm_dist_split): global owner -> hot index on every rank
+  u32* hot = nullptr;
+  u32 n_hot_tab = 0, n_hot = 0, hot_base = 0;
+  // the last route: rows this rank sent to / received from every peer, and
+  // its input size (evm_dist_return, evm_dist_split_winners)
+  uint64_t sent[MAX_BUCKETS] = {}, recvd[MAX_BUCKETS] = {};
+  uint64_t n_in = 0;
 };
 
 namespace {
@@ -596,6 +822,11 @@ Route route_of(const evm_dist* d, const u32* owner, const uint8_t* dest) {
   R.dir_local = d->dir_local;
   R.n_dir = d->n_dir;
   R.world = (u32)d->world;
+  R.hot = d->hot;
+  R.n_hot_tab = d->n_hot_tab;
+  R.hot_base = d->hot_base;
+  R.ts = nullptr;
+  R.stride = 0;
   return R;
 }
 
@@ -639,6 +870,26 @@ int dist_alloc(evm_ctx* ctx, evm_dist* d) {
     return EVM_ENOMEM;
   memset(d->hcnt, 0, CNT_WORDS * sizeof(u64));
   return hip_ok(hipMemsetAsync(d->cnt, 0, CNT_WORDS * sizeof(u64), ctx->stream));
+}
+
+
+// One all-gather of (status, value) per rank: the peers' values into vals
+// (host, world words); any rank's status set -> every rank fails.
+int gather_status(evm_ctx* ctx, evm_dist* d, int local, u64 value, uint64_t* vals) {
+  const u32 G = (u32)d->world;
+  d->hcnt[W_GS] = (u64)(u32)local;
+  d->hcnt[W_GS + 1] = value;
+  HIPR(hipMemcpyAsync(d->cnt + W_GS, d->hcnt + W_GS, 2 * sizeof(u64), hipMemcpyHostToDevice, ctx->stream));
+  int st = d->tx->all_gather_u64(d->cnt + W_GS, d->cnt + W_GR, 2, ctx->stream);
+  if (st) return st;
+  HIPR(hipMemcpyAsync(d->hcnt + W_GR, d->cnt + W_GR, 2 * G * sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if (local) return local;
+  for (u32 p = 0; p < G; ++p) {
+    if (d->hcnt[W_GR + 2 * p]) return EVM_EDIST;
+    if (vals) vals[p] = d->hcnt[W_GR + 2 * p + 1];
+  }
+  return EVM_OK;
 }
 
 }  // namespace
@@ -730,6 +981,7 @@ void evm_dist_free(evm_ctx* ctx, evm_dist* d) {
   if (d->hcnt) (void)hipHostFree(d->hcnt);
   if (d->dir_dest) (void)hipFree(d->dir_dest);
   if (d->dir_local) (void)hipFree(d->dir_local);
+  if (d->hot) (void)hipFree(d->hot);
   delete d;
 }
 
@@ -745,8 +997,11 @@ int evm_dist_directory(evm_ctx* ctx, evm_dist* d, const char* ids, size_t stride
   if (!ctx || !d || (n_owners && (!ids || id_len == 0 || id_len > stride || id_len > 4096))) return EVM_EINVAL;
   if (d->dir_dest) (void)hipFree(d->dir_dest);
   if (d->dir_local) (void)hipFree(d->dir_local);
+  if (d->hot) (void)hipFree(d->hot);  // (a split's hot slots follow the directory's: set it again)
   d->dir_dest = nullptr;
   d->dir_local = nullptr;
+  d->hot = nullptr;
+  d->n_hot_tab = d->n_hot = d->hot_base = 0;
   d->n_dir = d->dir_per = d->dir_n_local = 0;
   if (n_local) *n_local = 0;
   if (!n_owners) return EVM_OK;
@@ -798,9 +1053,12 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   u32* flags = S.alloc<u32>(2);  // [0] a destination out of range, [1] a row outside the native domain
   u64* scnt = d->cnt + W_SEND;
   u64* rcnt = d->cnt + W_RECV;
-  const Route R = route_of(d, owner, dest);
+  Route R = route_of(d, owner, dest);
+  R.ts = ts;
+  R.stride = stride;
   u32* offs = nullptr;
   u32 nblocks = 0;
+  d->n_in = 0;
   if (!flags) lerr = lerr ? lerr : EVM_ENOMEM;
   if (!lerr) lerr = hip_ok(hipMemsetAsync(flags, 0, 2 * sizeof(u32), ctx->stream));
   if (!lerr) lerr = grow(&d->send, &d->send_cap, std::max<size_t>(n, 1) * rb);
@@ -874,6 +1132,11 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   d->rb = rb;
   d->packed = packed ? 1 : 0;
   d->n_recv = total;
+  d->n_in = n;
+  for (u32 p = 0; p < G; ++p) {
+    d->sent[p] = hs[p] & CNT_MASK;
+    d->recvd[p] = hr[p] & CNT_MASK;
+  }
   *n_recv = total;
   return bad_dest ? EVM_EINVAL : hip_ok(hipGetLastError());
 }
@@ -926,11 +1189,13 @@ int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* const* tree
   if (!ctx || !d) return EVM_EINVAL;  // nothing to join the collective with
   const u32 G = (u32)d->world;
   // every rank sizes the gather alike: from the directory, or ceil(n / world)
-  const u32 per = d->dir_dest ? d->dir_per : (n_owners_global + G - 1) / G;
+  // (a split adds its hot slots after every rank's cold ones)
+  const u32 per = (d->hot ? d->hot_base + d->n_hot : d->dir_dest ? d->dir_per : (n_owners_global + G - 1) / G);
   const u32 stride = per + 1;  // + one status word per rank
   int lerr = EVM_OK;
   if ((n_trees && !trees) || (n_owners_global && (!root || !present))) lerr = EVM_EINVAL;
   if (d->dir_dest && n_owners_global != d->n_dir) lerr = EVM_EINVAL;
+  if (d->hot && n_owners_global != d->n_hot_tab) lerr = EVM_EINVAL;
   size_t local = 0;
   for (u32 k = 0; k < n_trees && !lerr; ++k) {
     if (!trees[k]) lerr = EVM_EINVAL;
@@ -967,8 +1232,305 @@ int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* const* tree
     if (hs[p]) return EVM_EDIST;
   if (!n_owners_global) return EVM_OK;
   KLAUNCH(k_dist_root_unpack, dim3(grid_for(n_owners_global, 256)), dim3(256), all, G, stride, n_owners_global,
-          d->dir_dest, d->dir_local, root, present);
+          d->dir_dest, d->dir_local, (const u32*)d->hot, d->n_hot_tab, d->hot_base, root, present);
   return hip_ok(hipStreamSynchronize(ctx->stream));
+}
+
+// ------------------------------------------------------------------ hot-owner split
+int evm_dist_hot_owners(evm_ctx* ctx, evm_dist* d, const uint32_t* owner, size_t n, uint32_t n_owners_global,
+                        double share, uint32_t* hot, uint32_t cap, uint32_t* n_hot) {
+  if (!ctx || !d || !n_hot) return EVM_EINVAL;
+  *n_hot = 0;
+  const u32 G = (u32)d->world;
+  int lerr = EVM_OK;
+  if ((n && !owner) || (cap && !hot) || !(share > 0.0)) lerr = EVM_EINVAL;
+  // the owner count and the total rows must agree before the count gather
+  uint64_t vals[MAX_BUCKETS];
+  int st = gather_status(ctx, d, lerr, n_owners_global, vals);
+  if (st) return st;
+  for (u32 p = 0; p < G; ++p)
+    if (vals[p] != n_owners_global) lerr = EVM_EINVAL;
+  if ((st = gather_status(ctx, d, lerr, n, vals))) return st;
+  uint64_t total = 0;
+  for (u32 p = 0; p < G; ++p) total += vals[p];
+  if (G == 1 || n_owners_global == 0) return EVM_OK;
+  Scratch S(ctx);
+  u64* counts = S.alloc<u64>(n_owners_global);
+  u64* all = S.alloc<u64>((size_t)n_owners_global * G);
+  u32* list = S.alloc<u32>((size_t)std::max<u32>(cap, 1) + 2);
+  lerr = (!counts || !all || !list) ? EVM_ENOMEM : EVM_OK;
+  if (!lerr) {
+    lerr = hip_ok(hipMemsetAsync(counts, 0, sizeof(u64) * n_owners_global, ctx->stream));
+    if (!lerr) lerr = hip_ok(hipMemsetAsync(list, 0, sizeof(u32) * 2, ctx->stream));
+    if (!lerr && n)
+      KLAUNCH(k_split_hist, dim3(grid_for(n, 256)), dim3(256), owner, n, n_owners_global, counts, list + 1);
+  }
+  if ((st = gather_status(ctx, d, lerr, 0, nullptr))) return st;
+  if ((st = d->tx->all_gather_u64(counts, all, n_owners_global, ctx->stream))) return st;
+  // hot: more than `share` of one rank's fair share of all rows
+  const double fair = (double)total / G;
+  const u64 thr = (u64)(share * fair);
+  KLAUNCH(k_split_select, dim3(grid_for(n_owners_global, 256)), dim3(256), (const u64*)all, G,
+          (size_t)n_owners_global, n_owners_global, thr, list + 2, list, cap);
+  u32 h[2];
+  HIPR(hipMemcpyAsync(h, list, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if (h[1]) return EVM_EINVAL;  // an owner id >= n_owners_global (after the collectives: nobody waits)
+  *n_hot = h[0];
+  if (h[0] > cap) return EVM_ECAPACITY;
+  if (h[0]) {
+    HIPR(hipMemcpyAsync(hot, list + 2, sizeof(u32) * h[0], hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    std::sort(hot, hot + h[0]);  // (the device list is in arrival order)
+  }
+  return EVM_OK;
+}
+
+int evm_dist_split(evm_ctx* ctx, evm_dist* d, const uint32_t* hot, uint32_t n_hot, uint32_t n_owners_global,
+                   uint32_t* hot_base) {
+  if (!ctx || !d || (n_hot && !hot) || n_hot > n_owners_global) return EVM_EINVAL;
+  if (d->dir_dest && n_owners_global != d->n_dir) return EVM_EINVAL;
+  std::vector<u32> tab;
+  if (n_hot) {
+    tab.assign(n_owners_global, HOT_NONE);
+    for (u32 h = 0; h < n_hot; ++h) {
+      if (hot[h] >= n_owners_global || tab[hot[h]] != HOT_NONE) return EVM_EINVAL;  // in range, no repeats
+      tab[hot[h]] = h;
+    }
+  }
+  if (d->hot) (void)hipFree(d->hot);
+  d->hot = nullptr;
+  d->n_hot_tab = d->n_hot = d->hot_base = 0;
+  const u32 G = (u32)d->world;
+  const u32 base = d->dir_dest ? d->dir_per : (n_owners_global + G - 1) / G;
+  if (hot_base) *hot_base = base;
+  if (!n_hot) return EVM_OK;
+  HIPR(hipMalloc(&d->hot, sizeof(u32) * n_owners_global));
+  HIPR(hipMemcpyAsync(d->hot, tab.data(), sizeof(u32) * n_owners_global, hipMemcpyHostToDevice, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  d->n_hot_tab = n_owners_global;
+  d->n_hot = n_hot;
+  d->hot_base = base;
+  return EVM_OK;
+}
+
+int evm_dist_ts_dest(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, uint8_t* dest) {
+  if (!ctx || !d || stride < 48 || stride % 8 || (n && (!ts || !dest))) return EVM_EINVAL;
+  if (n) KLAUNCH(k_ts_dest, dim3(grid_for(n, 256)), dim3(256), ts, stride, n, (u32)d->world, dest);
+  return hip_ok(hipGetLastError());
+}
+
+int evm_dist_cell_dest(evm_ctx* ctx, evm_dist* d, const uint32_t* cell, size_t n, uint8_t* dest) {
+  if (!ctx || !d || (n && (!cell || !dest))) return EVM_EINVAL;
+  if (n) KLAUNCH(k_cell_dest, dim3(grid_for(n, 256)), dim3(256), cell, n, (u32)d->world, dest);
+  return hip_ok(hipGetLastError());
+}
+
+int evm_dist_merge_trees(evm_ctx* ctx, evm_dist* d, const evm_tree* t, uint32_t owner_lo, uint32_t count,
+                         evm_tree** out) {
+  if (!ctx || !d || !out) return EVM_EINVAL;
+  *out = nullptr;
+  const u32 G = (u32)d->world;
+  int lerr = EVM_OK;
+  if (!t || owner_lo + (uint64_t)count > t->n_owners) lerr = EVM_EINVAL;
+  u64 ab[2] = {0, 0};
+  if (!lerr && count) {
+    HIPR(hipMemcpyAsync(&ab[0], t->off + owner_lo, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipMemcpyAsync(&ab[1], t->off + owner_lo + count, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+  }
+  const u64 L = ab[1] - ab[0];
+  const u64 words = 1 + L + (L + 1) / 2;
+  uint64_t sizes[MAX_BUCKETS];
+  // (count must match too: every rank's parts are trees of `count` owners)
+  int st = gather_status(ctx, d, lerr, ((u64)count << 40) | words, sizes);
+  if (st) return st;
+  u64 per = 0;
+  for (u32 p = 0; p < G; ++p) {
+    if ((sizes[p] >> 40) != count) lerr = EVM_EINVAL;
+    per = std::max<u64>(per, sizes[p] & ((1ull << 40) - 1));
+  }
+  Scratch S(ctx);
+  u64* mine = S.alloc<u64>(per);
+  u64* all = S.alloc<u64>(per * G);
+  if (!lerr && (!mine || !all)) lerr = EVM_ENOMEM;
+  if (!lerr)
+    KLAUNCH(k_merge_pack, dim3(grid_for(std::max<u64>(L, 1), 256)), dim3(256), (const u64*)t->ck, t->xr, ab[0], L,
+            owner_lo, mine);
+  if ((st = gather_status(ctx, d, lerr, 0, nullptr))) return st;
+  if ((st = d->tx->all_gather_u64(mine, all, per, ctx->stream))) return st;
+  // XOR-merge the parts in rank order (the same tree on every rank)
+  evm_tree* acc = nullptr;
+  for (u32 p = 0; p < G; ++p) {
+    const u64* A = all + (size_t)p * per;
+    u64 lp = 0;  // (the part's leaf count: its first word)
+    HIPR(hipMemcpyAsync(&lp, A, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    const u64* ckp = A + 1;
+    const int32_t* xrp = reinterpret_cast<const int32_t*>(A + 1 + lp);
+    evm_tree* next = nullptr;
+    st = acc ? merge_into_tree(ctx, S, acc, count, ckp, xrp, lp, &next) : tree_finalize(ctx, S, count, ckp, xrp, lp, &next);
+    if (acc) tree_destroy(ctx, acc);
+    if (st) {
+      if (next) tree_destroy(ctx, next);
+      return st;
+    }
+    acc = next;
+  }
+  *out = acc;
+  return evm_sync(ctx);
+}
+
+int evm_dist_merge_select(evm_ctx* ctx, evm_dist* d, uint32_t n_groups, const uint64_t* off, const uint64_t* id,
+                          const uint64_t* key, uint64_t* out_off, uint64_t* out_id, uint64_t cap, uint64_t* n_out) {
+  if (!ctx || !d || !n_out) return EVM_EINVAL;
+  *n_out = 0;
+  const u32 G = (u32)d->world;
+  int lerr = EVM_OK;
+  if (!off || !out_off) lerr = EVM_EINVAL;
+  u64 ab[2] = {0, 0};
+  if (!lerr) {
+    HIPR(hipMemcpyAsync(&ab[0], off, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipMemcpyAsync(&ab[1], off + n_groups, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    if (ab[1] < ab[0] || (ab[1] > ab[0] && (!id || !key))) lerr = EVM_EINVAL;
+  }
+  const u64 m = lerr ? 0 : ab[1] - ab[0];
+  uint64_t sizes[MAX_BUCKETS];
+  int st = gather_status(ctx, d, lerr, ((u64)n_groups << 40) | m, sizes);
+  if (st) return st;
+  u64 rb[MAX_BUCKETS + 1];
+  rb[0] = 0;
+  u64 mx = 0;
+  for (u32 p = 0; p < G; ++p) {
+    if ((sizes[p] >> 40) != n_groups) lerr = EVM_EINVAL;
+    const u64 mp = sizes[p] & ((1ull << 40) - 1);
+    rb[p + 1] = rb[p] + mp;
+    mx = std::max<u64>(mx, mp);
+  }
+  const u64 per = (u64)n_groups + 1 + 4 * mx;
+  Scratch S(ctx);
+  u64* mine = S.alloc<u64>(per);
+  u64* all = S.alloc<u64>(per * G);
+  u64* drb = S.alloc<u64>(G + 1);
+  if (!lerr && (!mine || !all || !drb)) lerr = EVM_ENOMEM;
+  if (!lerr) {
+    KLAUNCH(k_sel_pack, dim3(grid_for(n_groups + 1 + 4 * m, 256)), dim3(256), off, id, key, n_groups, m, mine);
+    // every rank's row count sits at its word n_groups (its last offset)
+    lerr = hip_ok(hipMemcpyAsync(drb, rb, sizeof(u64) * (G + 1), hipMemcpyHostToDevice, ctx->stream));
+  }
+  if ((st = gather_status(ctx, d, lerr, 0, nullptr))) return st;
+  if ((st = d->tx->all_gather_u64(mine, all, per, ctx->stream))) return st;
+  const u64 M = rb[G];
+  *n_out = M;
+  KLAUNCH(k_sel_off, dim3(grid_for(n_groups + 1, 256)), dim3(256), (const u64*)all, G, (size_t)per, n_groups, out_off);
+  if (M > cap) {
+    HIPR(hipStreamSynchronize(ctx->stream));
+    return EVM_ECAPACITY;
+  }
+  if (M) {
+    if (!out_id) return EVM_EINVAL;
+    KLAUNCH(k_sel_merge, dim3(grid_for(M, 256)), dim3(256), (const u64*)all, G, (size_t)per, n_groups,
+            (const u64*)drb, out_off, out_id);
+  }
+  return evm_sync(ctx);
+}
+
+int evm_dist_return(evm_ctx* ctx, evm_dist* d, const void* val, uint32_t elem, void* out, size_t n_out) {
+  if (!ctx || !d) return EVM_EINVAL;
+  const u32 G = (u32)d->world;
+  const size_t n = d->n_recv;
+  int lerr = EVM_OK;
+  if ((elem != 1 && elem != 2 && elem != 4 && elem != 8) || (n && !val) || (n_out && !out)) lerr = EVM_EINVAL;
+  const size_t ooff = d->packed ? 16 : d->stride;
+  Scratch S(ctx);
+  u32* bad = S.alloc<u32>(1);
+  u64 back = 0;
+  for (u32 p = 0; p < G; ++p) back += d->sent[p];
+  if (!bad) lerr = lerr ? lerr : EVM_ENOMEM;
+  if (!lerr) lerr = grow(&d->send, &d->send_cap, std::max<size_t>(n, 1) * 16);
+  u64* rbuf = S.alloc<u64>(2 * std::max<u64>(back, 1));
+  if (!lerr && !rbuf) lerr = EVM_ENOMEM;
+  if (!lerr) {
+    lerr = hip_ok(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
+    if (!lerr && n)
+      KLAUNCH(k_ret_pack, dim3(grid_for(n, 256)), dim3(256), (const char*)d->recv, d->rb, ooff, n,
+              (const uint8_t*)val, elem, reinterpret_cast<u64*>(d->send));
+  }
+  if (int st = agree(ctx, d, lerr)) return st;
+  // rows go back to the rank they came from: the route's counts reversed
+  uint64_t soff[MAX_BUCKETS], slen[MAX_BUCKETS], roff[MAX_BUCKETS], rlen[MAX_BUCKETS];
+  uint64_t so = 0, ro = 0;
+  for (u32 p = 0; p < G; ++p) {
+    soff[p] = so * 16;
+    slen[p] = d->recvd[p] * 16;
+    roff[p] = ro * 16;
+    rlen[p] = d->sent[p] * 16;
+    so += d->recvd[p];
+    ro += d->sent[p];
+  }
+  int st = d->tx->exchange(d->send, soff, slen, reinterpret_cast<char*>(rbuf), roff, rlen, ctx->stream);
+  if (st) return st;
+  if (back)
+    KLAUNCH(k_ret_scatter, dim3(grid_for(back, 256)), dim3(256), (const u64*)rbuf, (size_t)back, (uint8_t*)out, n_out,
+            elem, bad);
+  u32 hb = 0;
+  HIPR(hipMemcpyAsync(&hb, bad, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  return hb ? EVM_EINVAL : EVM_OK;  // a source index >= n_out
+}
+
+int evm_dist_split_winners(evm_ctx* ctx, evm_dist* d, const int32_t* win, uint32_t n_cells, int64_t* out) {
+  if (!ctx || !d) return EVM_EINVAL;
+  const u32 G = (u32)d->world;
+  int lerr = EVM_OK;
+  if (n_cells && (!win || !out)) lerr = EVM_EINVAL;
+  uint64_t nin[MAX_BUCKETS];
+  int st = gather_status(ctx, d, lerr, ((u64)n_cells << 40) | d->n_in, nin);
+  if (st) return st;
+  u64 base[MAX_BUCKETS + 1];
+  base[0] = 0;
+  for (u32 p = 0; p < G; ++p) {
+    if ((nin[p] >> 40) != n_cells) lerr = EVM_EINVAL;
+    base[p + 1] = base[p] + (nin[p] & ((1ull << 40) - 1));
+  }
+  Scratch S(ctx);
+  u64* mine = S.alloc<u64>(std::max<u32>(n_cells, 1));
+  u64* all = S.alloc<u64>((size_t)std::max<u32>(n_cells, 1) * G);
+  u64* dbase = S.alloc<u64>(G + 1);
+  u32* bad = S.alloc<u32>(1);
+  if (!lerr && (!mine || !all || !dbase || !bad)) lerr = EVM_ENOMEM;
+  if (!lerr) {
+    lerr = hip_ok(hipMemcpyAsync(dbase, base, sizeof(u64) * (G + 1), hipMemcpyHostToDevice, ctx->stream));
+    if (!lerr) lerr = hip_ok(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
+    if (!lerr && n_cells)
+      KLAUNCH(k_win_map, dim3(grid_for(n_cells, 256)), dim3(256), win, n_cells, (const char*)d->recv, d->rb,
+              d->packed ? (size_t)16 : d->stride, (u64)d->n_recv, (const u64*)(d->cnt + W_ROFF), G,
+              (const u64*)dbase, mine, bad);
+    if (!lerr) {
+      u32 hb = 0;
+      lerr = hip_ok(hipMemcpyAsync(&hb, bad, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+      if (!lerr) lerr = hip_ok(hipStreamSynchronize(ctx->stream));
+      if (!lerr && hb) lerr = EVM_EINVAL;  // a winner past the received rows
+    }
+  }
+  if ((st = gather_status(ctx, d, lerr, 0, nullptr))) return st;
+  if (!n_cells) return EVM_OK;
+  if ((st = d->tx->all_gather_u64(mine, all, n_cells, ctx->stream))) return st;
+  KLAUNCH(k_win_reduce, dim3(grid_for(n_cells, 256)), dim3(256), (const u64*)all, G, (size_t)n_cells, n_cells, out);
+  return evm_sync(ctx);
+}
+
+int evm_dist_agree_status(evm_ctx* ctx, evm_dist* d, int32_t local, int32_t* max_status) {
+  if (!ctx || !d || !max_status) return EVM_EINVAL;
+  const u32 G = (u32)d->world;
+  uint64_t v[MAX_BUCKETS];
+  const int st = gather_status(ctx, d, EVM_OK, (u64)(u32)local, v);
+  if (st) return st;
+  int32_t m = 0;
+  for (u32 p = 0; p < G; ++p) m = std::max<int32_t>(m, (int32_t)(u32)v[p]);
+  *max_status = m;
+  return EVM_OK;
 }
 
 }  // extern "C"

@@ -24,6 +24,12 @@ XOR-combination of its per-rank partial trees (insertIntoMerkleTree is
 order-independent, merkleTree.test.ts:30-42): partial roots XOR together
 (`gather_hot_roots`), partial leaf lists merge on the device
 (`merge_hot_trees`, evm_tree_merge).
+
+This module is the torch.distributed formulation (gloo on CPU for the
+multi-process tests, RCCL through torch on GPUs).  The product path for a
+caller without torch is the same plan behind the C ABI: evm_dist_route /
+take / gather_roots / hot_owners / split / merge_trees / merge_select /
+return / split_winners (include/evm.h), driven by evolu_amd/sharded.py.
 """
 from __future__ import annotations
 
@@ -109,7 +115,7 @@ def hot_owners(counts: torch.Tensor, world: int, share: float = 0.25) -> torch.T
     if world <= 1:
         return torch.zeros(0, dtype=torch.int64)
     fair = float(counts.sum().item()) / world
-    return torch.nonzero(counts.cpu() > share * fair).flatten()
+    return torch.nonzero(counts > share * fair).flatten()  # (on the counts' device)
 
 
 def route_by_owner(ts: torch.Tensor, owner: torch.Tensor, group=None, dest: Optional[torch.Tensor] = None
@@ -386,29 +392,10 @@ def split_apply(ts: torch.Tensor, cell: torch.Tensor, n_cells: int, apply_local,
 def merge_partial_tree(eng, tree_in, part, group=None):
     """The owner's new tree on every rank: its prior tree merged with every
     rank's partial tree (leaf lists all-gathered, XOR-merged on the device by
-    evm_tree_merge)."""
-    import numpy as np
-
-    off, code, xr = part.leaves()
-    L = int(off[-1])
-    payload = np.concatenate([np.array([L], dtype=np.int64), code[:L].astype(np.int64), xr[:L].astype(np.int64)])
-    gloo = dist.get_backend(group) == "gloo"
-    dev = torch.device("cuda", eng.device) if (torch.cuda.is_available() and not gloo) else torch.device("cpu")
-    t = torch.from_numpy(payload).to(dev)
-    world = dist.get_world_size(group)
-    sizes = torch.tensor([t.numel()], dtype=torch.int64, device=dev)
-    alls = [torch.empty_like(sizes) for _ in range(world)]
-    dist.all_gather(alls, sizes, group=group)
-    cap = int(max(int(x.item()) for x in alls))
-    pad = torch.zeros(cap, dtype=torch.int64, device=dev)
-    pad[: t.numel()] = t
-    allt = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(allt, pad, group=group)
+    evm_tree_merge; the leaves never leave the device except where gloo
+    itself needs host tensors)."""
     merged = tree_in
-    for r in range(world):
-        a = allt[r].cpu().numpy()
-        L = int(a[0])
-        p = eng.tree_from_leaves(np.array([0, L], dtype=np.uint64), a[1:1 + L].astype(np.uint64),
-                                 a[1 + L:1 + 2 * L].astype(np.int32))
+    for po, pc, px in gather_leaf_parts(*part.slice_device(0, part.n_owners), group):
+        p = eng.tree_from_device_leaves(po, pc, px)
         merged = eng.tree_merge(merged, p)
     return merged

@@ -653,3 +653,94 @@ class Dist:
         check(self.eng.lib.evm_dist_gather_roots(self.eng.h, self.h, arr, len(ts), n_owners_global, _ptr(root),
                                                  _ptr(present)), "evm_dist_gather_roots")
         return root[:n_owners_global], present[:n_owners_global].bool()
+
+    # ------------------------------------------------ hot-owner / cell split
+    def hot_owners(self, owner: torch.Tensor, n_owners_global: int, share: float = 0.25, cap: int = 4096) -> np.ndarray:
+        """Collective: global owners holding more than `share` of one rank's
+        fair share of all rows (evm_dist_hot_owners) -> sorted uint32 array."""
+        buf = np.zeros(max(cap, 1), dtype=np.uint32)
+        nh = C.c_uint32()
+        check(self.eng.lib.evm_dist_hot_owners(self.eng.h, self.h, _ptr(owner), owner.numel(), n_owners_global,
+                                               share, buf.ctypes.data_as(C.c_void_p), cap, C.byref(nh)),
+              "evm_dist_hot_owners")
+        return buf[: nh.value].copy()
+
+    def split(self, hot, n_owners_global: int) -> int:
+        """Split the listed global owners over every rank (evm_dist_split);
+        returns hot_base (hot owner h is local owner hot_base + h)."""
+        hot = np.ascontiguousarray(np.asarray(hot, dtype=np.uint32))
+        base = C.c_uint32()
+        check(self.eng.lib.evm_dist_split(self.eng.h, self.h, hot.ctypes.data_as(C.c_void_p), hot.size,
+                                          n_owners_global, C.byref(base)), "evm_dist_split")
+        self.hot = hot
+        self.n_hot = int(hot.size)
+        self.hot_base = base.value
+        return self.hot_base
+
+    def merge_trees(self, trees: "Trees", owner_lo: int, count: int) -> "Trees":
+        """Collective: the XOR merge over ranks of owners [owner_lo, +count) of
+        every rank's trees (evm_dist_merge_trees) -- the same on every rank."""
+        h = C.c_void_p()
+        check(self.eng.lib.evm_dist_merge_trees(self.eng.h, self.h, trees.h, owner_lo, count, C.byref(h)),
+              "evm_dist_merge_trees")
+        return Trees(self.eng, h)
+
+    def merge_select(self, off: torch.Tensor, ids: torch.Tensor, keys: torch.Tensor, cap: Optional[int] = None):
+        """Collective: per-group selections split over ranks (off: n_groups+1
+        bounds, may start past 0) -> (off int64[n_groups+1], ids int64[m]) in
+        timestamp order, the same on every rank (evm_dist_merge_select)."""
+        dev = off.device
+        ng = off.numel() - 1
+        out_off = torch.empty(ng + 1, dtype=torch.int64, device=dev)
+        nout = C.c_uint64()
+        if cap is None:  # size first (the same total on every rank: both calls stay collective)
+            st = self.eng.lib.evm_dist_merge_select(self.eng.h, self.h, ng, _ptr(off), _ptr(ids), _ptr(keys),
+                                                    _ptr(out_off), None, 0, C.byref(nout))
+            if st not in (_lib.EVM_OK, _lib.EVM_ECAPACITY):
+                check(st, "evm_dist_merge_select")
+            if st == _lib.EVM_OK:
+                return out_off, torch.empty(0, dtype=torch.int64, device=dev)
+            cap = nout.value
+        out_id = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        check(self.eng.lib.evm_dist_merge_select(self.eng.h, self.h, ng, _ptr(off), _ptr(ids), _ptr(keys),
+                                                 _ptr(out_off), _ptr(out_id), cap, C.byref(nout)),
+              "evm_dist_merge_select")
+        return out_off, out_id[: nout.value]
+
+    def ts_dest(self, ts: torch.Tensor) -> torch.Tensor:
+        """Rank of every row by timestamp hash (evm_dist_ts_dest)."""
+        n, stride = ts.shape
+        dest = torch.empty(max(n, 1), dtype=torch.uint8, device=ts.device)
+        check(self.eng.lib.evm_dist_ts_dest(self.eng.h, self.h, _ptr(ts), stride, n, _ptr(dest)), "evm_dist_ts_dest")
+        return dest[:n]
+
+    def cell_dest(self, cell: torch.Tensor) -> torch.Tensor:
+        """Rank of every row's cell (evm_dist_cell_dest)."""
+        n = cell.numel()
+        dest = torch.empty(max(n, 1), dtype=torch.uint8, device=cell.device)
+        check(self.eng.lib.evm_dist_cell_dest(self.eng.h, self.h, _ptr(cell), n, _ptr(dest)), "evm_dist_cell_dest")
+        return dest[:n]
+
+    def send_back(self, val: torch.Tensor, n_out: int) -> torch.Tensor:
+        """Collective: per received row values (receive order) back to their
+        source positions (evm_dist_return) -> tensor [n_out] of val's dtype."""
+        val = val.contiguous()
+        elem = val.element_size()
+        out = torch.zeros(max(n_out, 1), dtype=val.dtype, device=val.device)
+        check(self.eng.lib.evm_dist_return(self.eng.h, self.h, _ptr(val), elem, _ptr(out), n_out), "evm_dist_return")
+        return out[:n_out]
+
+    def split_winners(self, win: torch.Tensor, n_cells: int) -> torch.Tensor:
+        """Collective: winners (index into the last route's receive order or -1)
+        -> global batch indexes int64[n_cells] (evm_dist_split_winners)."""
+        out = torch.empty(max(n_cells, 1), dtype=torch.int64, device=win.device)
+        w = win.to(torch.int32).contiguous()  # (kept alive across the call)
+        check(self.eng.lib.evm_dist_split_winners(self.eng.h, self.h, _ptr(w), n_cells, _ptr(out)),
+              "evm_dist_split_winners")
+        return out[:n_cells]
+
+    def agree_status(self, local: int) -> int:
+        """Collective: the largest status over the ranks."""
+        m = C.c_int32()
+        check(self.eng.lib.evm_dist_agree_status(self.eng.h, self.h, int(local), C.byref(m)), "evm_dist_agree_status")
+        return m.value

@@ -443,6 +443,77 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
 int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* const* trees, uint32_t n_trees,
                           uint32_t n_owners_global, int32_t* root, uint8_t* present);
 
+/* ---- hot owners split over every rank (BASELINE config 5) ----
+ * A skewed owner distribution (Zipf 1.2: the top owner ~18 % of all rows)
+ * would pin one rank.  A split owner lives on EVERY rank, as local id
+ * hot_base + h (h: its index in the hot list), and each of its rows goes to
+ * the rank murmur3(its 46 timestamp bytes) mod world picks -- every copy of
+ * one (owner, timestamp) meets on one rank, so INSERT OR IGNORE (index.ts:154)
+ * and the per-rank Merkle XOR stay exact, and the owner's tree is the XOR
+ * merge of its per-rank partial trees (insertIntoMerkleTree is
+ * order-independent, merkleTree.test.ts:30-42).  getMessages of a split
+ * owner (index.ts:173-202): diff its FULL tree (evm_dist_merge_trees) against
+ * the client's, each rank selects its share after that bound
+ * (evm_store_select_after with sel_key), evm_dist_merge_select merges the
+ * shares in timestamp order.
+ *
+ * collective: owners with more than `share` x (all rows / world) rows over
+ * all ranks -> hot (host, sorted ascending), *n_hot (EVM_ECAPACITY if > cap).
+ * owner: device [n] global ids < n_owners_global. */
+int evm_dist_hot_owners(evm_ctx* ctx, evm_dist* d, const uint32_t* owner, size_t n, uint32_t n_owners_global,
+                        double share, uint32_t* hot, uint32_t cap, uint32_t* n_hot);
+/* local (every rank passes the same list): split the listed global owners
+ * (host, distinct, < n_owners_global; after evm_dist_directory when there is
+ * one, n_owners_global = its size).  Afterwards evm_dist_route sends a split
+ * owner's rows by timestamp hash, evm_dist_take writes local ids for every
+ * row (hot_base + h for a split owner), and evm_dist_gather_roots XORs the
+ * split owners' partial roots (its trees then cover hot_base + n_hot local
+ * owners).  *hot_base (host, may be NULL) = the cold local slots per rank.
+ * n_hot == 0 removes the split. */
+int evm_dist_split(evm_ctx* ctx, evm_dist* d, const uint32_t* hot, uint32_t n_hot, uint32_t n_owners_global,
+                   uint32_t* hot_base);
+/* collective: the full trees of owners [owner_lo, owner_lo + count) of t:
+ * every rank's leaves of them all-gathered on the device and XOR-merged
+ * (evm_tree_merge semantics), rebased to owners 0..count-1 -- the same tree
+ * on every rank.  (count: the same on every rank.) */
+int evm_dist_merge_trees(evm_ctx* ctx, evm_dist* d, const evm_tree* t, uint32_t owner_lo, uint32_t count,
+                         evm_tree** out);
+/* collective: n_groups selections split over ranks -> one per group, every
+ * rank's rows merged in timestamp order (ORDER BY "timestamp", index.ts:101;
+ * equal keys: lower rank first).  off: device [n_groups + 1] row bounds into
+ * id / key (key: 3 x u64 per row, evm_store_select_after's sel_key; off[0]
+ * need not be 0).  Outputs (device, the same on every rank): out_off
+ * [n_groups + 1] from 0, out_id[cap]; *n_out = rows (EVM_ECAPACITY if > cap,
+ * out_off still written). */
+int evm_dist_merge_select(evm_ctx* ctx, evm_dist* d, uint32_t n_groups, const uint64_t* off, const uint64_t* id,
+                          const uint64_t* key, uint64_t* out_off, uint64_t* out_id, uint64_t cap, uint64_t* n_out);
+
+/* ---- one owner's applyMessages batch split over the ranks by cell ----------
+ * (the client side of config 5).  The LWW decisions of applyMessages.ts:26-131
+ * are per cell: route every row with dest = evm_dist_cell_dest (its cell's
+ * rank) and the cell as aux, take in receive order (the global batch order),
+ * apply on this rank's cells; the global __message PK check (one timestamp in
+ * two cells) runs on the rank evm_dist_ts_dest picks (route by it, then
+ * evm_cross_cell_check); evm_dist_agree_status combines the statuses;
+ * evm_dist_return sends the flags back to the rows' source positions,
+ * evm_dist_split_winners maps the winners to global batch indexes, and
+ * evm_dist_merge_trees XOR-merges the per-rank partial trees.
+ * local: dest[i] = murmur3(row i's 46 timestamp bytes) mod world (device) */
+int evm_dist_ts_dest(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, uint8_t* dest);
+/* local: dest[i] = the rank of cell[i] (a fixed mix of the id, mod world) */
+int evm_dist_cell_dest(evm_ctx* ctx, evm_dist* d, const uint32_t* cell, size_t n, uint8_t* dest);
+/* collective: val (device, the last route's received rows in receive order,
+ * elem = 1/2/4/8 bytes each) back to the rows' source ranks: out[source
+ * index] (device, n_out elements) on every rank. */
+int evm_dist_return(evm_ctx* ctx, evm_dist* d, const void* val, uint32_t elem, void* out, size_t n_out);
+/* collective: win (device [n_cells]: an index into the last route's receive
+ * order, or -1) -> out (device int64 [n_cells], every rank): the global batch
+ * index of the winner (the ranks' inputs in rank order) or -1; a cell's
+ * winner comes from the one rank that holds the cell. */
+int evm_dist_split_winners(evm_ctx* ctx, evm_dist* d, const int32_t* win, uint32_t n_cells, int64_t* out);
+/* collective: *max_status = the largest `local` over the ranks */
+int evm_dist_agree_status(evm_ctx* ctx, evm_dist* d, int32_t local, int32_t* max_status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -811,8 +811,13 @@ napi_value DistFree(napi_env env, napi_callback_info info) {
 // distRoute(ctx, d, ts Uint8Array(n * stride), stride, owner Uint32Array, aux Uint32Array | null)
 //   -> { ts, owner, aux, src (Float64Array: source rank * 2^32 + index) }   (collective)
 napi_value DistRoute(napi_env env, napi_callback_info info) {
-  napi_value a[6];
-  if (!get_args(env, info, 6, a)) return nullptr;
+  napi_value a[7];
+  size_t argc = 7;
+  napi_get_undefined(env, &a[6]);
+  if (napi_get_cb_info(env, info, &argc, a, nullptr, nullptr) != napi_ok || argc < 6) {
+    napi_throw_type_error(env, nullptr, "missing arguments");
+    return nullptr;
+  }
   Ctx* cx = ctx_of(env, a[0]);
   std::lock_guard<std::mutex> lock(cx->m);
   evm_ctx* ctx = cx->c;
@@ -824,10 +829,16 @@ napi_value DistRoute(napi_env env, napi_callback_info info) {
   const size_t stride = u32(env, a[3]);
   const size_t n = ol / 4;
   if (!stride || tl != n * stride || (ax && al != ol)) return throw_status(env, EVM_EINVAL, "distRoute: sizes");
-  Dev dts(ctx, tl, ts), dow(ctx, ol, ow), dax(ctx, ax ? al : 1, ax);
+  void* de = nullptr;
+  size_t dl = 0;
+  napi_valuetype t6;
+  napi_typeof(env, a[6], &t6);
+  if (argc >= 7 && t6 != napi_undefined && !is_null(env, a[6]) && !bytes_of(env, a[6], &de, &dl)) return nullptr;
+  if (de && dl != n) return throw_status(env, EVM_EINVAL, "distRoute: dest must have one rank per row");
+  Dev dts(ctx, tl, ts), dow(ctx, ol, ow), dax(ctx, ax ? al : 1, ax), dde(ctx, de ? dl : 1, de);
   uint64_t nr = 0;
   int st = evm_dist_route(ctx, d, (const char*)dts.p, stride, n, (const uint32_t*)dow.p,
-                          ax ? (const uint32_t*)dax.p : nullptr, nullptr, &nr);
+                          ax ? (const uint32_t*)dax.p : nullptr, de ? (const uint8_t*)dde.p : nullptr, &nr);
   if (st) return throw_status(env, st, "evm_dist_route");
   Dev rts(ctx, nr * stride), row(ctx, nr * 4), rax(ctx, nr * 4), rsrc(ctx, nr * 8);
   st = evm_dist_take(ctx, d, 0, (char*)rts.p, stride, (uint32_t*)row.p, (uint32_t*)rax.p, (uint64_t*)rsrc.p, nr,
@@ -878,6 +889,317 @@ napi_value DistGatherRoots(napi_env env, napi_callback_info info) {
   return res;
 }
 
+// ---- loopback ranks (worker threads of one process, one GPU): the hub travels as a BigInt address
+napi_value DistHubNew(napi_env env, napi_callback_info info) {
+  napi_value a[1];
+  if (!get_args(env, info, 1, a)) return nullptr;
+  evm_dist_hub* h = nullptr;
+  const int st = evm_dist_hub_new((int)u32(env, a[0]), &h);
+  if (st) return throw_status(env, st, "evm_dist_hub_new");
+  napi_value v;
+  napi_create_bigint_uint64(env, (uint64_t)(uintptr_t)h, &v);
+  return v;
+}
+
+evm_dist_hub* hub_of(napi_env env, napi_value v) {
+  uint64_t x = 0;
+  bool lossless = false;
+  napi_get_value_bigint_uint64(env, v, &x, &lossless);
+  return (evm_dist_hub*)(uintptr_t)x;
+}
+
+napi_value DistHubFree(napi_env env, napi_callback_info info) {
+  napi_value a[1];
+  if (!get_args(env, info, 1, a)) return nullptr;
+  evm_dist_hub_free(hub_of(env, a[0]));
+  return nullptr;
+}
+
+napi_value DistHubAbort(napi_env env, napi_callback_info info) {
+  napi_value a[1];
+  if (!get_args(env, info, 1, a)) return nullptr;
+  evm_dist_hub_abort(hub_of(env, a[0]));
+  return nullptr;
+}
+
+// distInitLoopback(ctx, hub BigInt, rank) -> handle   (collectives block until every rank's thread joins)
+napi_value DistInitLoopback(napi_env env, napi_callback_info info) {
+  napi_value a[3];
+  if (!get_args(env, info, 3, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_dist* d = nullptr;
+  const int st = evm_dist_init_loopback(cx->c, hub_of(env, a[1]), (int)u32(env, a[2]), &d);
+  if (st) return throw_status(env, st, "evm_dist_init_loopback");
+  return make_ext(env, d);
+}
+
+// distDirectory(ctx, d, ids Uint8Array(n * stride), stride, idLen) -> { dest Uint8Array, local Uint32Array, nLocal }
+napi_value DistDirectory(napi_env env, napi_callback_info info) {
+  napi_value a[5];
+  if (!get_args(env, info, 5, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
+  void* ids;
+  size_t il;
+  if (!bytes_of(env, a[2], &ids, &il)) return nullptr;
+  const size_t stride = u32(env, a[3]), id_len = u32(env, a[4]);
+  if (!stride || il % stride) return throw_status(env, EVM_EINVAL, "distDirectory: sizes");
+  const uint32_t n = (uint32_t)(il / stride);
+  Dev dids(ctx, il, ids), ddest(ctx, n), dloc(ctx, 4ull * n);
+  uint32_t nl = 0;
+  const int st = evm_dist_directory(ctx, (evm_dist*)ext(env, a[1]), (const char*)dids.p, stride, id_len, n,
+                                    (uint8_t*)ddest.p, (uint32_t*)dloc.p, &nl);
+  if (st) return throw_status(env, st, "evm_dist_directory");
+  void *hd, *hl;
+  napi_value vd = typed(env, napi_uint8_array, n, 1, &hd);
+  napi_value vl = typed(env, napi_uint32_array, n, 4, &hl);
+  evm_copy_d2h(ctx, hd, ddest.p, n);
+  evm_copy_d2h(ctx, hl, dloc.p, 4ull * n);
+  napi_value res, v;
+  napi_create_object(env, &res);
+  napi_set_named_property(env, res, "dest", vd);
+  napi_set_named_property(env, res, "local", vl);
+  napi_create_uint32(env, nl, &v);
+  napi_set_named_property(env, res, "nLocal", v);
+  return res;
+}
+
+// distHotOwners(ctx, d, owner Uint32Array, nGlobal, share) -> Uint32Array (sorted)   (collective)
+napi_value DistHotOwners(napi_env env, napi_callback_info info) {
+  napi_value a[5];
+  if (!get_args(env, info, 5, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
+  void* ow;
+  size_t ol;
+  if (!bytes_of(env, a[2], &ow, &ol)) return nullptr;
+  double share = 0.25;
+  napi_get_value_double(env, a[4], &share);
+  const uint32_t ng = u32(env, a[3]);
+  Dev dow(ctx, ol, ow);
+  std::vector<uint32_t> hot(4096);
+  uint32_t nh = 0;
+  const int st = evm_dist_hot_owners(ctx, (evm_dist*)ext(env, a[1]), (const uint32_t*)dow.p, ol / 4, ng, share,
+                                     hot.data(), (uint32_t)hot.size(), &nh);
+  if (st) return throw_status(env, st, "evm_dist_hot_owners");
+  void* hp;
+  napi_value vh = typed(env, napi_uint32_array, nh, 4, &hp);
+  if (nh) memcpy(hp, hot.data(), 4ull * nh);
+  return vh;
+}
+
+// distSplit(ctx, d, hot Uint32Array, nGlobal) -> hotBase
+napi_value DistSplit(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  if (!get_args(env, info, 4, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  void* hot;
+  size_t hl;
+  if (!bytes_of(env, a[2], &hot, &hl)) return nullptr;
+  uint32_t base = 0;
+  const int st = evm_dist_split(cx->c, (evm_dist*)ext(env, a[1]), (const uint32_t*)hot, (uint32_t)(hl / 4),
+                                u32(env, a[3]), &base);
+  if (st) return throw_status(env, st, "evm_dist_split");
+  napi_value v;
+  napi_create_uint32(env, base, &v);
+  return v;
+}
+
+napi_value f64_array(napi_env env, const std::vector<uint64_t>& x) {
+  double* p;
+  napi_value v = typed(env, napi_float64_array, x.size(), 8, (void**)&p);
+  for (size_t i = 0; i < x.size(); ++i) p[i] = (double)x[i];
+  return v;
+}
+
+// distSelectSplit(ctx, d, store, clientTree, node Uint8Array(nLocal * 16), hotBase, nHot)
+//   -> { diff Float64Array(nLocal), off, ids (this rank's rows per local id),
+//        hotOff, hotIds (every rank's rows of the split owners, timestamp order) }   (collective)
+// getMessages (index.ts:173-202) with split owners: their diffs are those of their FULL trees
+napi_value DistSelectSplit(napi_env env, napi_callback_info info) {
+  napi_value a[7];
+  if (!get_args(env, info, 7, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
+  evm_dist* d = (evm_dist*)ext(env, a[1]);
+  const evm_store* s = (const evm_store*)ext(env, a[2]);
+  const evm_tree* client = (const evm_tree*)ext(env, a[3]);
+  void* node;
+  size_t nl;
+  if (!bytes_of(env, a[4], &node, &nl)) return nullptr;
+  const uint32_t base = u32(env, a[5]), nh = u32(env, a[6]);
+  uint32_t n_local = 0;
+  uint64_t n_msg = 0;
+  evm_store_info(s, &n_local, &n_msg);
+  if (nl != 16ull * n_local || base + (uint64_t)nh != n_local)
+    return throw_status(env, EVM_EINVAL, "distSelectSplit: sizes");
+  const evm_tree* tree = evm_store_tree(s);
+  Dev ddiff(ctx, 8ull * n_local), dnode(ctx, nl, node), doff(ctx, 8ull * (n_local + 1)),
+      dids(ctx, 8 * (n_msg ? n_msg : 1)), dkey(ctx, 24 * (n_msg ? n_msg : 1)), dhoff(ctx, 8ull * (nh + 1));
+  // (a local failure still joins every collective, flagged: no peer is left waiting)
+  int st = evm_merkle_diff(ctx, tree, client, (int64_t*)ddiff.p);
+  evm_tree *full = nullptr, *sub = nullptr;
+  const int st_m = evm_dist_merge_trees(ctx, d, st ? nullptr : tree, base, nh, &full);
+  if (!st) st = st_m;
+  // the client's trees of the split owners: its hot slots
+  uint64_t L = 0;
+  std::vector<uint64_t> soff(nh + 1);
+  if (!st) st = evm_tree_slice(ctx, client, base, nh, nullptr, nullptr, nullptr, 0, &L);
+  if (st == EVM_ECAPACITY) st = EVM_OK;
+  Dev dso(ctx, 8ull * (nh + 1)), dsc(ctx, 8 * (L ? L : 1)), dsx(ctx, 4 * (L ? L : 1));
+  if (!st) st = evm_tree_slice(ctx, client, base, nh, (uint64_t*)dso.p, (uint64_t*)dsc.p, (int32_t*)dsx.p, L, &L);
+  if (!st) st = evm_tree_from_device_leaves(ctx, nh, (const uint64_t*)dso.p, (const uint64_t*)dsc.p,
+                                            (const int32_t*)dsx.p, &sub);
+  if (!st && nh) st = evm_merkle_diff(ctx, full, sub, (int64_t*)ddiff.p + base);
+  if (full) evm_tree_free(ctx, full);
+  if (sub) evm_tree_free(ctx, sub);
+  uint64_t nsel = 0, nhot = 0;
+  if (!st)
+    st = evm_store_select_after(ctx, s, (const int64_t*)ddiff.p, (const char*)dnode.p, nullptr, (uint64_t*)doff.p,
+                                (uint64_t*)dids.p, (uint64_t*)dkey.p, n_msg, &nsel);
+  Dev dhids(ctx, 8);
+  {
+    const int st_s = evm_dist_merge_select(ctx, d, nh, st ? nullptr : (const uint64_t*)doff.p + base,
+                                           (const uint64_t*)dids.p, (const uint64_t*)dkey.p, (uint64_t*)dhoff.p,
+                                           nullptr, 0, &nhot);
+    if (!st) st = st_s;
+    if (st == EVM_ECAPACITY) {  // (every rank: the same total)
+      Dev big(ctx, 8 * nhot);
+      st = evm_dist_merge_select(ctx, d, nh, (const uint64_t*)doff.p + base, (const uint64_t*)dids.p,
+                                 (const uint64_t*)dkey.p, (uint64_t*)dhoff.p, (uint64_t*)big.p, nhot, &nhot);
+      std::swap(dhids.p, big.p);
+    }
+  }
+  if (st) return throw_status(env, st, "distSelectSplit");
+  std::vector<int64_t> diff(n_local);
+  std::vector<uint64_t> off(n_local + 1), ids(nsel), hoff(nh + 1), hids(nhot);
+  evm_copy_d2h(ctx, diff.data(), ddiff.p, 8ull * n_local);
+  evm_copy_d2h(ctx, off.data(), doff.p, 8ull * (n_local + 1));
+  if (nsel) evm_copy_d2h(ctx, ids.data(), dids.p, 8 * nsel);
+  evm_copy_d2h(ctx, hoff.data(), dhoff.p, 8ull * (nh + 1));
+  if (nhot) evm_copy_d2h(ctx, hids.data(), dhids.p, 8 * nhot);
+  double* dp;
+  napi_value vdiff = typed(env, napi_float64_array, n_local, 8, (void**)&dp);
+  for (uint32_t i = 0; i < n_local; ++i) dp[i] = (double)diff[i];
+  napi_value res;
+  napi_create_object(env, &res);
+  napi_set_named_property(env, res, "diff", vdiff);
+  napi_set_named_property(env, res, "off", f64_array(env, off));
+  napi_set_named_property(env, res, "ids", f64_array(env, ids));
+  napi_set_named_property(env, res, "hotOff", f64_array(env, hoff));
+  napi_set_named_property(env, res, "hotIds", f64_array(env, hids));
+  return res;
+}
+
+// distSplitApply(ctx, d, ts Uint8Array(n * 48), cell Uint32Array, nCells, treeIn)
+//   -> { status, flags Uint8Array(n), winner Float64Array(nCells) (global batch index, -1), tree | null }
+// applyMessages of ONE owner's batch split over the ranks by cell (collective): each rank passes its
+// slice (the batch = the slices in rank order); winner and tree are the same on every rank
+napi_value DistSplitApply(napi_env env, napi_callback_info info) {
+  napi_value a[6];
+  if (!get_args(env, info, 6, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
+  evm_dist* d = (evm_dist*)ext(env, a[1]);
+  void *ts, *cell;
+  size_t tl, cl;
+  if (!bytes_of(env, a[2], &ts, &tl) || !bytes_of(env, a[3], &cell, &cl)) return nullptr;
+  const uint32_t nc = u32(env, a[4]);
+  const evm_tree* tree_in = (const evm_tree*)ext(env, a[5]);
+  const size_t n = cl / 4;
+  if (tl != n * 48) return throw_status(env, EVM_EINVAL, "distSplitApply: sizes");
+  Dev dts(ctx, tl, ts), dcell(ctx, cl, cell), dzero(ctx, 4 * (n ? n : 1)), ddest(ctx, n ? n : 1);
+  std::vector<uint32_t> zero(n, 0u);
+  if (n) evm_copy_h2d(ctx, dzero.p, zero.data(), 4 * n);
+  uint64_t nr = 0;
+  int local = EVM_OK;
+  // the global PK check (applyMessages.ts:42-45): every copy of a timestamp meets on one rank
+  int st = evm_dist_ts_dest(ctx, d, (const char*)dts.p, 48, n, (uint8_t*)ddest.p);
+  if (!st) st = evm_dist_route(ctx, d, (const char*)dts.p, 48, n, (const uint32_t*)dzero.p,
+                               (const uint32_t*)dcell.p, (const uint8_t*)ddest.p, &nr);
+  if (st) return throw_status(env, st, "distSplitApply: route");
+  {
+    Dev rts(ctx, 48 * (nr ? nr : 1)), row(ctx, 4 * (nr ? nr : 1)), rax(ctx, 4 * (nr ? nr : 1));
+    st = evm_dist_take(ctx, d, 0, (char*)rts.p, 48, (uint32_t*)row.p, (uint32_t*)rax.p, nullptr, nr, nullptr);
+    int32_t found = 0;
+    if (!st && nr) st = evm_cross_cell_check(ctx, (const char*)rts.p, 48, nr, (const uint32_t*)rax.p, nc, &found);
+    if (st) local = st;
+    else if (found) local = EVM_ECOLLISION;
+    st = EVM_OK;
+  }
+  // the LWW decisions (applyMessages.ts:78-124) are per cell: every row of a cell on the cell's rank
+  st = evm_dist_cell_dest(ctx, d, (const uint32_t*)dcell.p, n, (uint8_t*)ddest.p);
+  if (st && !local) local = st;
+  // (a failed dest: route with bad destinations -- the route reports them after the exchange)
+  st = evm_dist_route(ctx, d, (const char*)dts.p, 48, n, (const uint32_t*)dzero.p, (const uint32_t*)dcell.p,
+                      (const uint8_t*)ddest.p, &nr);
+  if (st) return throw_status(env, st, "distSplitApply: route");  // (every rank fails a route together)
+  Dev rts(ctx, 48 * (nr ? nr : 1)), row(ctx, 4 * (nr ? nr : 1)), rax(ctx, 4 * (nr ? nr : 1)),
+      fl(ctx, nr ? nr : 1), win(ctx, 4ull * (nc ? nc : 1)), dflags(ctx, n ? n : 1), dwin(ctx, 8ull * (nc ? nc : 1));
+  // (local failures from here on go into `local`: every rank still reaches the status agreement)
+  st = evm_dist_take(ctx, d, 0, (char*)rts.p, 48, (uint32_t*)row.p, (uint32_t*)rax.p, nullptr, nr, nullptr);
+  if (st && !local) local = st;
+  evm_tree *empty = nullptr, *part = nullptr;
+  st = evm_tree_new(ctx, 1, &empty);
+  if (st && !local) local = st;
+  st = EVM_OK;
+  if (!local) {
+    if (nr) {
+      const int a_st = evm_apply_batch(ctx, empty, (const char*)rts.p, 48, nr, (const uint32_t*)rax.p, nc, nullptr,
+                                       nullptr, 48, nullptr, (uint8_t*)fl.p, (int32_t*)win.p, &part);
+      if (a_st) local = a_st;
+    } else {
+      std::vector<int32_t> none(nc ? nc : 1, -1);
+      st = evm_copy_h2d(ctx, win.p, none.data(), 4ull * (nc ? nc : 1));
+      part = empty;
+      empty = nullptr;
+    }
+  }
+  if (st && !local) local = st;
+  int32_t status = 0;
+  st = evm_dist_agree_status(ctx, d, local, &status);
+  napi_value res, v;
+  napi_create_object(env, &res);
+  if (!st && status == EVM_OK) st = evm_dist_return(ctx, d, fl.p, 1, dflags.p, n);
+  if (!st && status == EVM_OK) st = evm_dist_split_winners(ctx, d, (const int32_t*)win.p, nc, (int64_t*)dwin.p);
+  evm_tree *merged = nullptr, *out = nullptr;
+  if (!st && status == EVM_OK) st = evm_dist_merge_trees(ctx, d, part, 0, 1, &merged);
+  if (!st && status == EVM_OK) st = evm_tree_merge(ctx, tree_in, merged, &out);
+  if (empty) evm_tree_free(ctx, empty);
+  if (part) evm_tree_free(ctx, part);
+  if (merged) evm_tree_free(ctx, merged);
+  if (st) return throw_status(env, st, "distSplitApply");
+  napi_create_int32(env, status, &v);
+  napi_set_named_property(env, res, "status", v);
+  void* hf;
+  napi_value vf = typed(env, napi_uint8_array, n, 1, &hf);
+  double* wp;
+  napi_value vw = typed(env, napi_float64_array, nc, 8, (void**)&wp);
+  if (status == EVM_OK) {
+    if (n) evm_copy_d2h(ctx, hf, dflags.p, n);
+    std::vector<int64_t> w(nc);
+    if (nc) evm_copy_d2h(ctx, w.data(), dwin.p, 8ull * nc);
+    for (uint32_t c = 0; c < nc; ++c) wp[c] = (double)w[c];
+  } else {
+    if (n) memset(hf, 0, n);
+    for (uint32_t c = 0; c < nc; ++c) wp[c] = -1;
+  }
+  napi_set_named_property(env, res, "flags", vf);
+  napi_set_named_property(env, res, "winner", vw);
+  if (out) napi_set_named_property(env, res, "tree", make_ext(env, out));
+  else {
+    napi_get_null(env, &v);
+    napi_set_named_property(env, res, "tree", v);
+  }
+  return res;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   const struct {
     const char* name;
@@ -891,7 +1213,11 @@ napi_value Init(napi_env env, napi_value exports) {
              {"serverSelect", ServerSelect}, {"storeSince", StoreSince}, {"receiveFold", ReceiveFold},
              {"pbDecode", PbDecode},         {"pbEncode", PbEncode},
              {"distUniqueId", DistUniqueId}, {"distInit", DistInit},     {"distFree", DistFree},
-             {"distRoute", DistRoute},       {"distGatherRoots", DistGatherRoots}};
+             {"distRoute", DistRoute},       {"distGatherRoots", DistGatherRoots},
+             {"distHubNew", DistHubNew},     {"distHubFree", DistHubFree},   {"distHubAbort", DistHubAbort},
+             {"distInitLoopback", DistInitLoopback}, {"distDirectory", DistDirectory},
+             {"distHotOwners", DistHotOwners}, {"distSplit", DistSplit},   {"distSelectSplit", DistSelectSplit},
+             {"distSplitApply", DistSplitApply}};
   for (const auto& f : fns) {
     napi_value v;
     napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.fn, nullptr, &v);

@@ -282,33 +282,110 @@ class Server {
 
 // Multi-GPU owner sharding (evm_dist_*): one Engine + Dist per GPU process;
 // rank 0 makes the id (Dist.uniqueId()) and hands it to the other processes.
-// Owners live on rank owner % world (dense owner ids, e.g. from murmur3(userId)).
+// Owners live on rank owner % world, or -- after directory(userIds) -- on rank
+// murmur3(userId) % world with dense local ids (SURVEY 8(e)).  Loopback ranks
+// (Dist.loopbackHub(world), one worker thread each, one GPU) run the same
+// collectives with device copies instead of xGMI.
 class Dist {
   static uniqueId() {
     return addon.distUniqueId();
   }
+  // a hub for `world` loopback ranks (a BigInt: hand it to the worker threads)
+  static loopbackHub(world) {
+    return addon.distHubNew(world);
+  }
+  static freeHub(hub) {
+    addon.distHubFree(hub);
+  }
+  static abortHub(hub) {
+    addon.distHubAbort(hub);
+  }
+  // id: a uniqueId (RCCL), or { hub } for a loopback rank
   constructor(engine, id, rank, world) {
     this.engine = engine;
     this.rank = rank;
     this.world = world;
-    this.h = addon.distInit(engine.ctx, id, rank, world); // collective
+    this.h = id && id.hub !== undefined ? addon.distInitLoopback(engine.ctx, id.hub, rank)
+      : addon.distInit(engine.ctx, id, rank, world); // collective
+    this.hotBase = 0;
+    this.hot = new Uint32Array(0);
   }
   close() {
     addon.distFree(this.engine.ctx, this.h);
   }
+  // owner directory from the userId strings (global owner id = index): -> { dest, local, nLocal }
+  directory(userIds) {
+    const len = userIds.length ? Buffer.byteLength(userIds[0], "latin1") : 1;
+    const stride = (len + 7) & ~7;
+    const ids = new Uint8Array(userIds.length * stride);
+    userIds.forEach((u, i) => {
+      if (Buffer.byteLength(u, "latin1") !== len) throw new RangeError("userIds must have one length");
+      ids.set(Buffer.from(u, "latin1"), i * stride);
+    });
+    const r = addon.distDirectory(this.engine.ctx, this.h, ids, stride, len);
+    this.nOwners = userIds.length;
+    this.nLocal = r.nLocal;
+    return r;
+  }
+  // collective: split the owners holding more than `share` of one rank's fair share of
+  // this round's rows (owners: this rank's rows' global ids) over every rank.
+  // Local ids afterwards: hotBase + h for split owner hot[h].  -> hot (Uint32Array)
+  splitHot(owners, nOwnersGlobal, share = 0.25) {
+    const hot = addon.distHotOwners(this.engine.ctx, this.h, Uint32Array.from(owners), nOwnersGlobal, share);
+    this.hotBase = addon.distSplit(this.engine.ctx, this.h, hot, nOwnersGlobal);
+    this.hot = hot;
+    this.nLocal = this.hotBase + hot.length;
+    return hot;
+  }
   // collective: this rank's slice of a batch -> the rows of the owners this rank
-  // serves, in global batch order: { timestamps, owner, aux, src } (src = rank * 2^32 + index)
-  route(timestamps, owners, aux = null) {
+  // serves, in global batch order: { timestamps, owner, aux, src } (src = rank * 2^32 + index;
+  // owner: local ids once a directory or split is set).  dest (optional): the rank of every row.
+  route(timestamps, owners, aux = null, dest = null) {
     const r = addon.distRoute(this.engine.ctx, this.h, encodeTimestamps(timestamps), STRIDE, Uint32Array.from(owners),
-      aux ? Uint32Array.from(aux) : null);
+      aux ? Uint32Array.from(aux) : null, dest ? Uint8Array.from(dest) : null);
     const dec = new TextDecoder();
     const ts = [];
     for (let i = 0; i < r.owner.length; i++) ts.push(dec.decode(r.ts.subarray(i * STRIDE, i * STRIDE + 46)));
     return { timestamps: ts, owner: r.owner, aux: r.aux, src: r.src };
   }
-  // collective: every owner's root (local owner j of rank r = owner j * world + r)
+  // collective: every owner's root (split owners: the XOR of their partial roots)
   gatherRoots(server, nOwnersGlobal) {
     return addon.distGatherRoots(this.engine.ctx, this.h, addon.storeTree(server.store), nOwnersGlobal);
+  }
+  // collective: getMessages (index.ts:173-202) over a server whose owners are this rank's
+  // local ids, with split owners: clientTreesJson[j] / nodeIds[j] per local id (the hot
+  // slots: the split owner's client tree and requester, the same on every rank).
+  // -> { diff[j], ids[j][] (this rank's rows), hotIds[h][] (every rank's rows, timestamp order) }
+  getMessagesSplit(server, clientTreesJson, nodeIds) {
+    const [c, node] = server._selectArgs(clientTreesJson, nodeIds);
+    try {
+      const r = addon.distSelectSplit(this.engine.ctx, this.h, server.store, c, node, this.hotBase, this.hot.length);
+      const ids = [];
+      for (let j = 0; j < server.nOwners; j++) ids.push(Array.from(r.ids.subarray(r.off[j], r.off[j + 1])));
+      const hotIds = [];
+      for (let h = 0; h < this.hot.length; h++) hotIds.push(Array.from(r.hotIds.subarray(r.hotOff[h], r.hotOff[h + 1])));
+      return { diff: Array.from(r.diff, (d) => (d === -1 || d === -2 ? null : d)), ids, hotIds };
+    } finally {
+      addon.treeFree(this.engine.ctx, c);
+    }
+  }
+  // collective: applyMessages (applyMessages.ts:26-131) of ONE owner's batch split over
+  // the ranks by cell; each rank passes its slice (timestamps, cell ids < nCells).
+  // -> { status, flags (this slice), winner[c] (global batch index or -1), tree JSON | null }
+  applyMessagesSplit(timestamps, cells, nCells, treeJson = "{}") {
+    const t = addon.treeFromJson(this.engine.ctx, [treeJson]);
+    try {
+      const r = addon.distSplitApply(this.engine.ctx, this.h, encodeTimestamps(timestamps), Uint32Array.from(cells),
+        nCells, t);
+      let tree = null;
+      if (r.tree) {
+        tree = addon.treeToJson(this.engine.ctx, r.tree, 0);
+        addon.treeFree(this.engine.ctx, r.tree);
+      }
+      return { status: r.status, flags: r.flags, winner: Array.from(r.winner), tree };
+    } finally {
+      addon.treeFree(this.engine.ctx, t);
+    }
   }
 }
 

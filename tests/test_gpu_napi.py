@@ -154,3 +154,81 @@ def test_js_entry_points(tmp_path):
             assert got == want
         else:
             assert (got["ok"], got["type"], got["index"]) == (False, want["type"], want["index"])
+
+
+@pytest.mark.skipif(shutil.which("node") is None or not os.path.exists("/usr/include/node/node_api.h"),
+                    reason="node / N-API headers not present")
+@pytest.mark.parametrize("world", [2, 3])
+def test_js_dist_split_loopback(tmp_path, world):
+    """js/evolu_evm.js Dist on loopback ranks (worker threads, one GPU):
+    applyMessagesSplit (one owner's batch split by cell) and the server's
+    hot-owner split (directory, splitHot, route, getMessagesSplit,
+    gatherRoots) against the unsharded C restatement."""
+    import numpy as np
+
+    from evolu_amd import synth
+    from oracle import c_oracle as CO
+
+    _build_addon()
+    ts, _, cell = synth.config5(1, 6000, cells_per_owner=120, seed_config=58)
+    st_o, flags_o, win_o, js_o = CO.apply(ts, cell.astype(np.uint32), 120)
+    strs = [bytes(r[:46]).decode() for r in ts]
+    O_ = 24
+    sts, sown, _ = synth.config5(O_, 8000, seed_config=72)
+    sstr = [bytes(r[:46]).decode() for r in sts]
+    rng = np.random.default_rng(9)
+    keep = rng.random(len(sts)) < 0.5
+    srv, cli = CO.Server(O_, len(sts)), CO.Server(O_, len(sts))
+    assert srv.ingest(sts, sown.astype(np.uint32))[0] == 0
+    assert cli.ingest(sts[keep], sown[keep].astype(np.uint32))[0] == 0
+    node_of = ["%016x" % (0xABCD_0000_0000_0000 + g) for g in range(O_)]
+    cases = {"world": world,
+             "apply": {"timestamps": strs, "cells": [int(c) for c in cell], "nCells": 120},
+             "server": {"userIds": ["user%016d" % g for g in range(O_)], "timestamps": sstr,
+                        "owners": [int(o) for o in sown],
+                        "clientTrees": [CO.tree_json(sts[keep & (sown == g)]) for g in range(O_)],
+                        "nodeIds": node_of}}
+    f = tmp_path / "cases.json"
+    f.write_text(json.dumps(cases))
+    out = subprocess.run(["node", os.path.join(ROOT, "js", "test_dist_split.js"), str(f)], check=True,
+                         capture_output=True, text=True, timeout=300).stdout
+    res = json.loads(out.strip().splitlines()[-1])
+    assert st_o == 0
+    assert sum((x["apply"]["flags"] for x in res), []) == [int(v) for v in flags_o]
+    for x in res:
+        assert x["apply"]["status"] == 0 and x["apply"]["winner"] == [int(v) for v in win_o]
+        assert x["apply"]["tree"] == js_o
+    counts = np.bincount(sown, minlength=O_)
+    want_hot = [int(g) for g in np.flatnonzero(counts > 0.25 * len(sts) / world)]
+    assert want_hot and all(x["server"]["hot"] == want_hot for x in res)
+
+    def row(i):
+        q, k = int(i) // 2 ** 40, int(i) % 2 ** 40
+        return res[q]["server"]["rows"][k]
+
+    def expected(g, d):
+        if d is None:
+            return []
+        sync = O.timestamp_to_string(d, 0, "0000000000000000")
+        return [s for s in sorted({sstr[i] for i in np.flatnonzero(sown == g)})
+                if s > sync and not s.lower().endswith(node_of[g])]
+
+    seen = set()
+    for x in res:
+        sv = x["server"]
+        for j, g in enumerate(sv["glob"]):
+            if g < 0:
+                continue
+            d = srv.diff(cli, g)
+            d = None if d == -1 else d
+            assert sv["diff"][j] == d
+            if j >= sv["hotBase"]:
+                got = [row(i) for i in sv["hotIds"][j - sv["hotBase"]]]
+            else:
+                got = [row(i) for i in sv["ids"][j]]
+                seen.add(g)
+            assert got == expected(g, d)
+        for g in range(O_):
+            h = O.merkle_tree_from_string(srv.tree_json(g)).get("hash", 0)
+            assert sv["root"][g] == h
+    assert seen | set(want_hot) == set(range(O_))
