@@ -98,11 +98,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget per leg (0: skip)")
     ap.add_argument("--overlap", type=int, default=1, help="EVM_OPT_OVERLAP: independent checks on a second stream")
     ap.add_argument("--depth", type=int, default=4, help="config 2: batches in flight (evm_apply_batch_async)")
-    ap.add_argument("--workload", choices=["auto", "client", "server", "config4", "adversarial"], default="auto",
+    ap.add_argument("--workload", choices=["auto", "client", "server", "config4", "adversarial", "config5"], default="auto",
                     help="auto: client at N=1, config4 at N>1; "
                          "client: config 2 applyMessages (headline, + config 1, 3 and 4 legs at N=1); "
                          "server: config 3/5 ingest + diff + select alone; "
                          "config4: the sharded sync server (1B msgs / 1M owners at 8 GPUs, weak scaling)")
+    ap.add_argument("--radix", type=int, default=None, help="EVM_OPT_RADIX for --workload config5 (A/B of 10-bit digits)")
     ap.add_argument("--c4-owners", type=int, default=125_000, help="config4: owners per GPU")
     ap.add_argument("--c4-per-owner", type=int, default=1000, help="config4: messages per owner")
     ap.add_argument("--c4-sample", type=int, default=1000, help="config4: owners per rank in the self-check")
@@ -352,6 +353,13 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    if workload == "config5":  # the config-5 shape leg alone (profiling)
+        eng = Engine(local)
+        if a.radix is not None:
+            eng.set_option(4, a.radix)
+        emit(dict(config5_shape_leg(eng, a), metric=METRIC + " [server config 5 shape leg]"))
+        eng.close()
+        return
     if workload == "adversarial":  # the client_adversarial leg alone (profiling)
         eng = Engine(local)
         emit(dict(adversarial_leg(eng, a), metric=METRIC + " [client config 5 leg]"))
@@ -521,6 +529,10 @@ def main():
                                           a.c4_per_owner, a.steps, a.warmup, a.c4_sample)
             dd4.free()
             eng4.close()
+            torch.cuda.empty_cache()
+            eng5 = Engine(local)
+            out["config5_shape"] = config5_shape_leg(eng5, a)
+            eng5.close()
             torch.cuda.empty_cache()
         emit(out)
     if world > 1:
@@ -1040,6 +1052,110 @@ def adversarial_leg(eng, a):
             "kernels_ms_per_step": {k: v[0] / 3 for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:12]}}
 
 
+def config5_shape_leg(eng, a, owners=100_000, n=100_000_000, seed=0xE7010005, sample=200):
+    """BASELINE config 5 shape on the server: 100M messages over 100k owners,
+    owner sizes Zipf(1.2) (the top owner ~18 %), equal-millis bursts on a
+    1-second grid, 1 % upper-case nodes, 10 % exact redeliveries, shuffled
+    (no request runs) -- generated on the device (evs_config5_shape).  One
+    step = new store + addMessages (INSERT OR IGNORE) + getMessages against
+    client trees holding ~90 % + every owner's root.  Self-check: `sample`
+    of the smaller owners recomputed from all their rows alone by the global
+    sort path (inserts and tree JSON; tests pin both paths to the oracle)."""
+    import numpy as np
+    import torch
+
+    from evolu_amd import synth
+
+    dev = torch.device("cuda", eng.device)
+    gen = synth.DeviceSynth()
+    t0 = time.perf_counter()
+    ts, owner, keep = synth.device_config5_shape(gen, seed, owners, n, dev)
+    gen_s = time.perf_counter() - t0
+    first = eng.store_new(owners)
+    ins, _ = first.ingest(ts, owner, 0)
+    known = (keep != 0) & ((ins[:n] & 0x04) != 0)  # the client holds each known message once
+    first.free()
+    client = eng.merkle_insert(eng.tree_new(owners), ts[known].contiguous(), owner[known].contiguous())
+    del known
+    node = torch.from_numpy(np.frombuffer(b"0123456789abcdef" * owners, dtype=np.uint8).copy()).to(dev)
+    flags = torch.empty(n, dtype=torch.uint8, device=dev)
+    keep_store = [None]
+
+    def step(keep_it=False):
+        store = eng.store_new(owners)
+        store.ingest(ts, owner, 0, flags=flags)
+        store.select(client, node)
+        store.tree().roots()
+        if keep_it:
+            keep_store[0] = store
+        else:
+            store.free()
+
+    for _ in range(max(1, a.warmup)):
+        step()
+    torch.cuda.synchronize()
+    eng.prof_enable(True)
+    eng.prof_reset()
+    step()
+    torch.cuda.synchronize()
+    prof = eng.prof_report()
+    dom = dominant(prof, SERVER_ALG)
+    eng.prof_only(dom)
+    eng.prof_reset()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    prof_dom = eng.prof_report()
+    eng.prof_enable(False)
+    eng.prof_only(None)
+    ms = dt / a.steps * 1e3
+    # self-check on the smaller owners (every row of each)
+    step(keep_it=True)
+    store = keep_store[0]
+    counts = torch.bincount(owner.to(torch.int64), minlength=owners).cpu().numpy()
+    rng = np.random.default_rng(seed & 0xFFFF)
+    pool = np.flatnonzero((counts > 0) & (counts < 20_000))
+    pick = np.sort(rng.choice(pool, size=min(sample, len(pool)), replace=False))
+    sel = torch.isin(owner, torch.from_numpy(pick.astype(np.int32)).to(dev))
+    rows = ts[sel].cpu().numpy()
+    own = owner[sel].cpu().numpy().astype(np.uint32)
+    fl = flags[sel].cpu().numpy()
+    local = np.searchsorted(pick, own).astype(np.uint32)
+    # the same owners' rows alone through the other ingest algorithm (the
+    # global sort path, EVM_OPT_SERVER_PATH 2) on a fresh store
+    eng.set_option(2, 2)
+    try:
+        ref = eng.store_new(len(pick))
+        f_ref, st = ref.ingest(eng.dev(rows), eng.dev(local), 0)
+        f_ref = f_ref.cpu().numpy()
+    finally:
+        eng.set_option(2, 0)
+    ok_ins = st == 0 and np.array_equal((fl & 0x04) != 0, (f_ref & 0x04) != 0)
+    ok_tree = all(store.tree().to_json(int(g)) == ref.tree().to_json(j) for j, g in enumerate(pick))
+    ref.free()
+    store.free()
+    tot_ms, launches = prof_dom[dom]
+    avg_s = tot_ms / launches / 1e3
+    per_msg, per_leaf = SERVER_ALG[dom]
+    n_leaves = client.n_leaves
+    alg = per_msg * n + per_leaf * n_leaves
+    return {"workload": "config 5 shape (server): %d msgs over %d owners, Zipf 1.2 (top owner %.1f %%), equal-millis "
+                        "bursts on a 1-s grid, 1 %% upper-case nodes, 10 %% exact redeliveries, shuffled; addMessages "
+                        "into an empty store + getMessages + roots per step" % (n, owners, 100.0 * counts.max() / n),
+            "value": n / ms * 1e3, "unit": "msgs/s", "ms_per_step": ms, "steps": a.steps,
+            "data": "synthetic (device generator evs_config5_shape, %.2f s)" % gen_s,
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "kernel_ms_avg": avg_s * 1e3,
+                         "alg_bytes_per_launch": alg, "traffic": traffic_of(dom, "config5")},
+            "pipeline_hbm_frac": SERVER_PIPELINE_BYTES * n / (dt / a.steps) / HBM_PEAK,
+            "kernels_ms_per_step": {k: v[0] for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:14]},
+            "parity_checked": bool(ok_ins and ok_tree),
+            "self_check": {"owners": int(len(pick)), "rows": int(len(rows)), "inserts": bool(ok_ins),
+                           "trees": bool(ok_tree)}}
+
+
 def config1_leg(eng, a):
     """BASELINE config 1: the todo-schema stream (100k messages, one owner),
     one applyMessages batch from an empty tree, inputs in HBM."""
@@ -1058,8 +1174,21 @@ def config1_leg(eng, a):
     def step():
         eng.apply_batch(empty, ts, cell, C, flags=flags, winner=winner)[2].free()
 
+    def path_taken(fn):
+        s0 = eng.stats()
+        fn()
+        s1 = eng.stats()
+        if s1["small_batches"] > s0["small_batches"]:
+            return "small-batch path: 5 kernels, one status read"
+        if s1["small_fallbacks"] > s0["small_fallbacks"]:
+            return "sort path (the small-batch path handed over)"
+        if s1["tc_batches"] > s0["tc_batches"]:
+            return "tc streaming path"
+        return "sort path: radix sort by cell + segmented scan"
+
     for _ in range(a.warmup):
         step()
+    path = path_taken(step)
     eng.prof_enable(True)
     eng.prof_reset()
     for _ in range(a.steps):
@@ -1077,7 +1206,7 @@ def config1_leg(eng, a):
     out = {"workload": "config1: examples/nextjs todo schema (index.tsx:23-34, db.ts:268-300 mutation shapes), "
                        "100000 msgs, 1 owner, %d cells, 3 nodes, send order (evolu_amd/synth.config1)" % C,
            "value": len(ts_np) / ms * 1e3, "unit": "msgs/s", "ms_per_batch": ms, "steps": steps,
-           "path": "sort path (> 2,048 cells): radix sort by cell + segmented scan",
+           "path": path,
            "kernels_ms_per_batch": {k: v[0] / a.steps for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:10]},
            "cpu_baseline": cpu_baseline(ts_np, cell_np, a.cpu_seconds, "config-1") if a.cpu_seconds > 0 else None}
     # per-batch latency at the sizes a client applies (send.ts:107-111 one
@@ -1090,15 +1219,30 @@ def config1_leg(eng, a):
         ts_k, cell_k = eng.dev(ts_np[:k]), eng.dev(cid.astype(np.uint32))
         fl = torch.empty(k, dtype=torch.uint8, device=ts.device)
         wn = torch.empty(len(used), dtype=torch.int32, device=ts.device)
-        for _ in range(3):
+        def one():
             eng.apply_batch(empty, ts_k, cell_k, len(used), flags=fl, winner=wn)[2].free()
-        xs = []
-        for _ in range(30):
-            t0 = time.perf_counter()
-            eng.apply_batch(empty, ts_k, cell_k, len(used), flags=fl, winner=wn)[2].free()
-            xs.append((time.perf_counter() - t0) * 1e3)  # (the call returns after its status read: synchronous)
-        xs.sort()
-        lat[str(k)] = {"p50_ms": xs[len(xs) // 2], "p90_ms": xs[int(len(xs) * 0.9)], "cells": int(len(used))}
+
+        def timed():
+            for _ in range(3):
+                one()
+            xs = []
+            for _ in range(30):
+                t0 = time.perf_counter()
+                one()
+                xs.append((time.perf_counter() - t0) * 1e3)  # (the call returns after its status read: synchronous)
+            xs.sort()
+            return xs
+
+        xs = timed()
+        lat[str(k)] = {"p50_ms": xs[len(xs) // 2], "p90_ms": xs[int(len(xs) * 0.9)], "cells": int(len(used)),
+                       "path": path_taken(one)}
+        for name, opt in (("small_path", 4), ("sort_path", 2)):  # the paths auto did not take, for comparison
+            eng.set_option(1, opt)
+            try:
+                xs = timed()
+                lat[str(k)][name + "_p50_ms"] = xs[len(xs) // 2]
+            finally:
+                eng.set_option(1, 0)
     out["latency_per_batch"] = lat
     return out
 

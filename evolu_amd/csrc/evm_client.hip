@@ -1861,6 +1861,472 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   return fold_into_tree(ctx, S, tree_in, tree_in->n_owners, ck, h, m, hi, tree_out);
 }
 
+// ============================================================================
+// Small-batch path (send.ts:107-111: a client applies what one sync brings --
+// hundreds to ~100k messages): the sort path's ~25 launches and 4 host
+// synchronisations are latency at this size, so the same decisions run as
+// five kernels and ONE status read:
+//   K1 k_sm_pack    parse + canonical check + murmur3 (rec), rows per cell,
+//                   the cross-cell PK set (raw-byte compare), minute bounds
+//   K2 k_sm_scan    one workgroup: cell offsets (exclusive scan of the counts)
+//   K3 k_sm_scatter rows -> their cell's slots (unordered within the cell)
+//   K4 k_sm_lww     a thread per cell: its rows in batch order (repeated
+//                   selection, <= SM_SEG of them; longer cells: a workgroup
+//                   each, k_sm_long), the running max from the prior
+//                   max -> flags and winner (applyMessages.ts:93,105); the
+//                   XOR rows' hashes into dense minute bins
+//   K5 k_sm_fold    one workgroup: bins -> leaves, merged with tree_in's
+//                   leaves (equal keys XOR-combine), prefix XOR -> the tree
+// A cell with more than SM_SEG rows, minutes wider than SM_BINS or of two
+// base-3 lengths (leaf order != minute order) make the batch take the sort
+// path instead (SM_FALLBACK).
+// ============================================================================
+constexpr size_t SM_MAX_N = 1u << 18;       // rows (the auto choice over > 2,048 cells; EVM_OPT_CLIENT_PATH 4 forces it)
+constexpr size_t SM_AUTO_FEW = 1u << 14;    // rows: the auto choice over <= 2,048 cells too
+constexpr u32 SM_MAX_CELLS = 1u << 22;
+constexpr u32 SM_SEG = 32;                  // rows per cell kept in registers (longer cells: k_sm_long)
+constexpr u32 SM_LONG_MAX = 4096;           // rows of one cell k_sm_long sorts in LDS
+constexpr int SM_LONG_THREADS = 256;
+constexpr u32 SM_BINS = 1u << 16;           // minutes (45 days) of the dense fold
+constexpr int SM_FOLD_THREADS = 1024;
+constexpr int SM_FALLBACK = -102;
+
+__global__ __launch_bounds__(256) void k_sm_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
+                                                 const u32* __restrict__ cell, u32 C, evm_rec* __restrict__ rec,
+                                                 u32* __restrict__ cnt, u64* __restrict__ table, u32 lg,
+                                                 Info* __restrict__ info) {
+  const u64 mask = (1ull << lg) - 1;
+  u32 bad = 0, mn = 0xffffffffu, mx = 0;
+  bool bad_aux = false, coll = false;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    u32 w[12];
+    load_ts(ts, stride, i, w);
+    const Parsed p = parse_ts46(w);
+    const u32 c = cell[i];
+    evm_rec r;
+    r.tc = p.tc;
+    r.node = p.node;
+    r.meta = p.meta;
+    r.hash = p.hash;
+    r.minute = p.minute;
+    r.aux = c;
+    rec[i] = r;
+    if (!(p.meta & EVM_META_VALID)) {
+      bad = 1;
+      continue;
+    }
+    mn = min(mn, p.minute);
+    mx = max(mx, p.minute);
+    if (c >= C) {
+      bad_aux = true;
+      continue;
+    }
+    atomicAdd(&cnt[c], 1u);
+    // the global __message PK (applyMessages.ts:42-45): one timestamp in two cells
+    const u64 mine = ((u64)p.hash << 32) | (u64)(i + 1);
+    u64 pos = ((u64)(p.hash * 2654435761u) ^ (p.node * 0x9E3779B97F4A7C15ull >> 20)) & mask;
+    for (u64 probe = 0; probe <= mask; ++probe) {
+      u64 sl = __hip_atomic_load(&table[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (sl == 0) {
+        const u64 prev = atomicCAS(&table[pos], 0ull, mine);
+        if (prev == 0) break;  // inserted
+        sl = prev;
+      }
+      if ((u32)(sl >> 32) == p.hash) {
+        const size_t j = (size_t)(sl & 0xffffffffu) - 1;
+        if (ts_bytes_equal(ts, stride, i, j)) {
+          coll |= cell[j] != c;
+          break;
+        }
+      }
+      pos = (pos + 1) & mask;
+    }
+  }
+  if (__ballot(bad_aux) && (threadIdx.x & 63) == 0) atomic_or_if(&info->bad_aux, 1u);
+  if (__ballot(coll) && (threadIdx.x & 63) == 0) atomic_or_if(&info->collision, 1u);
+  block_fold_bounds<u32, 256>(mn, mx, bad, &info->minute_min, &info->minute_max, &info->bad);
+}
+
+// cell offsets: off[c] = rows of cells < c (off[C] = all), and cnt[c] = off[c]
+// (K3's cursors).  One workgroup, tiles of 16,384 counts: 16 consecutive per
+// thread (four 16-B loads), a block scan, the running total carried.
+constexpr u32 SM_SCAN_ITEMS = 16;
+__global__ __launch_bounds__(SM_FOLD_THREADS) void k_sm_scan(u32* __restrict__ cnt, u32 C, u32* __restrict__ off) {
+  __shared__ u32 lds[SM_FOLD_THREADS / 64 + 1];
+  constexpr u32 TILE = SM_FOLD_THREADS * SM_SCAN_ITEMS;
+  u32 carry = 0;
+  for (u32 base = 0; base < C; base += TILE) {
+    const u32 a = base + threadIdx.x * SM_SCAN_ITEMS;
+    u32 v[SM_SCAN_ITEMS];
+    if (a + SM_SCAN_ITEMS <= C) {  // (cnt is 256-B aligned scratch: a is a multiple of 16)
+      const uint4* p = reinterpret_cast<const uint4*>(cnt + a);
+#pragma unroll
+      for (u32 q = 0; q < SM_SCAN_ITEMS / 4; ++q) {
+        const uint4 x = p[q];
+        v[4 * q] = x.x;
+        v[4 * q + 1] = x.y;
+        v[4 * q + 2] = x.z;
+        v[4 * q + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) v[q] = a + q < C ? cnt[a + q] : 0u;
+    }
+    u32 sum = 0;
+#pragma unroll
+    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) sum += v[q];
+    u32 tot;
+    u32 run = carry + block_inclusive_scan<u32, OpAdd<u32>>(sum, lds, OpAdd<u32>(), &tot) - sum;
+#pragma unroll
+    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q)
+      if (a + q < C) {
+        off[a + q] = run;
+        cnt[a + q] = run;
+        run += v[q];
+      }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) off[C] = carry;
+}
+
+__global__ void k_sm_scatter(const evm_rec* __restrict__ rec, size_t n, u32 C, u32* __restrict__ cur,
+                             u32* __restrict__ grp) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const evm_rec r = rec[i];
+    if (!(r.meta & EVM_META_VALID) || r.aux >= C) continue;
+    grp[atomicAdd(&cur[r.aux], 1u)] = (u32)i;
+  }
+}
+
+// A thread per cell.  Its rows are taken in batch order by repeated
+// selection (the smallest index above the last one: O(k^2) reads of the
+// cell's L2-hot slots, no per-lane array, k <= SM_SEG).  The XOR rows' hashes
+// go into a per-workgroup LDS copy of the minute bins when the batch's minutes
+// fit it (a client batch spans minutes, not days: thousands of rows hit the
+// same few bins, which global atomics would serialise), flushed once per
+// workgroup; wider batches use the global bins directly.
+constexpr u32 SM_LDS_BINS = 8192;
+__global__ __launch_bounds__(256) void k_sm_lww(const evm_rec* __restrict__ rec, const u32* __restrict__ off,
+                                                const u32* __restrict__ grp, u32 C,
+                                                const evm_rec* __restrict__ prior,
+                                                const uint8_t* __restrict__ prior_present, uint8_t* __restrict__ flags,
+                                                int32_t* __restrict__ winner, u32* __restrict__ bins,
+                                                u32* __restrict__ pres, u32* __restrict__ long_list,
+                                                u32* __restrict__ long_n, Info* __restrict__ info) {
+  __shared__ u32 lbins[SM_LDS_BINS];
+  __shared__ u32 lpres[SM_LDS_BINS / 32];
+  const u32 mlo = info->minute_min, mhi = info->minute_max;
+  const u32 W = mhi >= mlo ? mhi - mlo + 1 : 0u;
+  const bool lds = W <= SM_LDS_BINS;
+  if (lds) {
+    for (u32 k = threadIdx.x; k < W; k += blockDim.x) lbins[k] = 0;
+    for (u32 k = threadIdx.x; k < (W + 31) / 32; k += blockDim.x) lpres[k] = 0;
+  }
+  __syncthreads();
+  for (u32 c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const u32 a = off[c], k = off[c + 1] - a;
+    if (k == 0) continue;  // (winner -1 from the init)
+    if (k > SM_SEG) {  // a long cell (a hot row of the app): a workgroup of k_sm_long takes it
+      if (k > SM_LONG_MAX) atomic_or_if(&info->fold_overflow, 1u);  // (the sort path)
+      else long_list[atomicAdd(long_n, 1u)] = c;
+      continue;
+    }
+    Key run = (prior_present && prior_present[c]) ? key_of(prior[c]) : key_none();
+    int32_t win = -1;
+    u32 last = 0;
+    for (u32 step = 0; step < k; ++step) {
+      u32 i = 0xffffffffu;
+      for (u32 q = 0; q < k; ++q) {
+        const u32 v = grp[a + q];
+        if ((step == 0 || v > last) && v < i) i = v;
+      }
+      last = i;
+      const evm_rec r = rec[i];
+      const Key ts = key_of(r);
+      const bool ups = key_cmp(run, ts) < 0;                            // applyMessages.ts:93
+      const bool xr = !((run.mask & KEY_PRESENT) && key_eq(run, ts));  // applyMessages.ts:105
+      flags[i] = (ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u);
+      if (ups) {
+        win = (int32_t)i;
+        run = ts;
+      }
+      if (xr) {
+        const u32 d = r.minute - mlo;
+        if (lds) {
+          atomicXor(&lbins[d], r.hash);
+          atomicOr(&lpres[d >> 5], 1u << (d & 31));
+        } else if (d >= SM_BINS) {
+          atomic_or_if(&info->fold_overflow, 1u);
+        } else {
+          atomicXor(&bins[d], r.hash);
+          atomicOr(&pres[d >> 5], 1u << (d & 31));
+        }
+      }
+    }
+    winner[c] = win;
+  }
+  if (!lds) return;
+  __syncthreads();
+  for (u32 k = threadIdx.x; k < (W + 31) / 32; k += blockDim.x) {
+    const u32 m = lpres[k];
+    if (!m) continue;
+    atomicOr(&pres[k], m);
+    for (u32 b = 0; b < 32; ++b)
+      if ((m >> b) & 1u) atomicXor(&bins[32 * k + b], lbins[32 * k + b]);
+  }
+}
+
+// The long cells (SM_SEG < rows <= SM_LONG_MAX), a workgroup each: the rows'
+// indices sorted in LDS (bitonic), the exclusive running max in batch order by
+// a blocked scan with key_max (each thread a contiguous run of positions),
+// then flags, the winner (the last upsert) and the XOR rows' bins.
+__global__ __launch_bounds__(SM_LONG_THREADS) void k_sm_long(const evm_rec* __restrict__ rec,
+                                                             const u32* __restrict__ off,
+                                                             const u32* __restrict__ grp,
+                                                             const u32* __restrict__ long_list,
+                                                             const u32* __restrict__ long_n,
+                                                             const evm_rec* __restrict__ prior,
+                                                             const uint8_t* __restrict__ prior_present,
+                                                             uint8_t* __restrict__ flags, int32_t* __restrict__ winner,
+                                                             u32* __restrict__ bins, u32* __restrict__ pres,
+                                                             Info* __restrict__ info) {
+  __shared__ u32 idx[SM_LONG_MAX];
+  __shared__ u64 s_tc[SM_LONG_THREADS], s_node[SM_LONG_THREADS];
+  __shared__ u32 s_mask[SM_LONG_THREADS];
+  __shared__ int32_t s_win;
+  const u32 t = threadIdx.x;
+  const u32 nl = *long_n;
+  const u32 mlo = info->minute_min;
+  for (u32 li = blockIdx.x; li < nl; li += gridDim.x) {
+    const u32 c = long_list[li];
+    const u32 a = off[c], k = off[c + 1] - a;
+    u32 P = 1;
+    while (P < k) P <<= 1;
+    for (u32 q = t; q < P; q += SM_LONG_THREADS) idx[q] = q < k ? grp[a + q] : 0xffffffffu;
+    if (t == 0) s_win = -1;
+    __syncthreads();
+    for (u32 size = 2; size <= P; size <<= 1)  // bitonic sort of the row indices
+      for (u32 stride = size >> 1; stride > 0; stride >>= 1) {
+        for (u32 q = t; q < P; q += SM_LONG_THREADS) {
+          const u32 r = q ^ stride;
+          if (r > q) {
+            const u32 x = idx[q], y = idx[r];
+            const bool up = (q & size) == 0;
+            if ((x > y) == up) {
+              idx[q] = y;
+              idx[r] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    // this thread's positions [p0, p1): their max, then the block's exclusive scan
+    const u32 per = (k + SM_LONG_THREADS - 1) / SM_LONG_THREADS;
+    const u32 p0 = min(k, t * per), p1 = min(k, p0 + per);
+    Key m = key_none();
+    for (u32 q = p0; q < p1; ++q) m = key_max(m, key_of(rec[idx[q]]));
+    s_tc[t] = m.tc;
+    s_node[t] = m.node;
+    s_mask[t] = m.mask;
+    __syncthreads();
+    for (u32 d = 1; d < SM_LONG_THREADS; d <<= 1) {  // inclusive max scan (Hillis-Steele)
+      Key o = key_none();
+      if (t >= d) o = Key{s_tc[t - d], s_node[t - d], s_mask[t - d]};
+      __syncthreads();
+      if (t >= d) {
+        m = key_max(o, m);
+        s_tc[t] = m.tc;
+        s_node[t] = m.node;
+        s_mask[t] = m.mask;
+      }
+      __syncthreads();
+    }
+    Key run = (prior_present && prior_present[c]) ? key_of(prior[c]) : key_none();
+    if (t > 0) run = key_max(run, Key{s_tc[t - 1], s_node[t - 1], s_mask[t - 1]});
+    int32_t win = -1;
+    for (u32 q = p0; q < p1; ++q) {
+      const u32 i = idx[q];
+      const evm_rec r = rec[i];
+      const Key ts = key_of(r);
+      const bool ups = key_cmp(run, ts) < 0;                            // applyMessages.ts:93
+      const bool xr = !((run.mask & KEY_PRESENT) && key_eq(run, ts));  // applyMessages.ts:105
+      flags[i] = (ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u);
+      if (ups) {
+        win = (int32_t)i;
+        run = ts;
+      }
+      if (xr) {
+        const u32 d = r.minute - mlo;
+        if (d >= SM_BINS) {
+          atomic_or_if(&info->fold_overflow, 1u);
+        } else {
+          atomicXor(&bins[d], r.hash);
+          atomicOr(&pres[d >> 5], 1u << (d & 31));
+        }
+      }
+    }
+    if (win >= 0) atomicMax(&s_win, win);
+    __syncthreads();
+    if (t == 0) winner[c] = s_win;
+    __syncthreads();
+  }
+}
+
+// One workgroup: the batch's leaves (present bins, minute order = code order
+// for keys of one base-3 length) merged with tree_in's (ack/axr, L0 sorted
+// unique, one owner) into the output tree's arrays; equal keys XOR-combine
+// (a leaf whose XOR is 0 stays, as in evm_tree_merge).
+__global__ __launch_bounds__(SM_FOLD_THREADS) void k_sm_fold(const u32* __restrict__ bins, const u32* __restrict__ pres,
+                                                             const u64* __restrict__ ack, const int32_t* __restrict__ axr,
+                                                             u32 L0, u64* __restrict__ nck, int32_t* __restrict__ nxr,
+                                                             u64* __restrict__ mck, int32_t* __restrict__ mxr,
+                                                             u64* __restrict__ off, u64* __restrict__ ock,
+                                                             int32_t* __restrict__ oxr, int32_t* __restrict__ opfx,
+                                                             Info* __restrict__ info) {
+  __shared__ u32 lds[SM_FOLD_THREADS / 64 + 1];
+  __shared__ int32_t xlds[SM_FOLD_THREADS / 64 + 1];
+  const u32 t = threadIdx.x;
+  if (info->bad || info->bad_aux || info->collision || info->fold_overflow) return;  // (the host reads why)
+  const u32 mlo = info->minute_min, mhi = info->minute_max;
+  const u32 W = mhi >= mlo ? min(SM_BINS, mhi - mlo + 1) : 0u;
+  if (W && base3_len(mlo) != base3_len(mhi)) {
+    if (t == 0) atomicOr(&info->fold_overflow, 1u);
+    return;
+  }
+  // (1) the batch's leaves
+  const u32 per = (W + SM_FOLD_THREADS - 1) / SM_FOLD_THREADS;
+  const u32 a = min(W, t * per), e = min(W, a + per);
+  u32 k = 0;
+  for (u32 d = a; d < e; ++d) k += (pres[d >> 5] >> (d & 31)) & 1u;
+  u32 L1;
+  u32 pos = block_inclusive_scan<u32, OpAdd<u32>>(k, lds, OpAdd<u32>(), &L1) - k;
+  for (u32 d = a; d < e; ++d)
+    if ((pres[d >> 5] >> (d & 31)) & 1u) {
+      nck[pos] = minute_code(mlo + d);
+      nxr[pos] = (int32_t)bins[d];
+      ++pos;
+    }
+  __syncthreads();
+  // (2) merge positions: A[i] before the B keys >= it, B[j] after the A keys <= it
+  for (u32 i = t; i < L0; i += SM_FOLD_THREADS) {
+    const u64 x = ack[i];
+    u32 lo = 0, hi = L1;
+    while (lo < hi) {
+      const u32 m = (lo + hi) >> 1;
+      if (nck[m] < x) lo = m + 1;
+      else hi = m;
+    }
+    mck[i + lo] = x;
+    mxr[i + lo] = axr[i];
+  }
+  for (u32 j = t; j < L1; j += SM_FOLD_THREADS) {
+    const u64 x = nck[j];
+    u32 lo = 0, hi = L0;
+    while (lo < hi) {
+      const u32 m = (lo + hi) >> 1;
+      if (ack[m] <= x) lo = m + 1;
+      else hi = m;
+    }
+    mck[j + lo] = x;
+    mxr[j + lo] = nxr[j];
+  }
+  __syncthreads();
+  // (3) equal neighbours (one from each side) combine; compact
+  const u32 M = L0 + L1;
+  const u32 per2 = (M + SM_FOLD_THREADS - 1) / SM_FOLD_THREADS;
+  const u32 b0 = min(M, t * per2), b1 = min(M, b0 + per2);
+  u32 h = 0;
+  for (u32 p = b0; p < b1; ++p) h += (p == 0 || mck[p] != mck[p - 1]) ? 1u : 0u;
+  u32 L;
+  const u32 o0 = block_inclusive_scan<u32, OpAdd<u32>>(h, lds, OpAdd<u32>(), &L) - h;
+  u32 o = o0;
+  int32_t xacc = 0;
+  for (u32 p = b0; p < b1; ++p) {
+    if (p != 0 && mck[p] == mck[p - 1]) continue;
+    const int32_t x = mxr[p] ^ ((p + 1 < M && mck[p + 1] == mck[p]) ? mxr[p + 1] : 0);
+    ock[o] = mck[p];
+    oxr[o] = x;
+    xacc ^= x;
+    ++o;
+  }
+  // (4) exclusive prefix XOR of the leaves (node hash = range XOR): this
+  // thread's leaves, after the XOR of every earlier thread's
+  int32_t xtot;
+  int32_t run = block_inclusive_scan<int32_t, OpXor<int32_t>>(xacc, xlds, OpXor<int32_t>(), &xtot) ^ xacc;
+  for (u32 q = o0; q < o0 + h; ++q) {
+    opfx[q] = run;
+    run ^= oxr[q];
+  }
+  if (t == 0) {
+    opfx[L] = xtot;
+    off[0] = 0;
+    off[1] = L;
+    info->n_leaves = L;
+  }
+}
+
+static int apply_small(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree_in, const char* ts, size_t stride,
+                       size_t n, const u32* cell, u32 C, const evm_rec* prior, const uint8_t* prior_present,
+                       uint8_t* flags, int32_t* winner, evm_tree** tree_out) {
+  const int lg = ceil_log2(2 * n);
+  const size_t a_cnt = ((size_t)(C + 1) * 4 + 255) & ~(size_t)255;
+  const size_t a_bins = (size_t)SM_BINS * 4, a_pres = (size_t)SM_BINS / 8;
+  const size_t zero_bytes = a_cnt + a_bins + a_pres + (sizeof(u64) << lg);
+  char* z = S.alloc<char>(zero_bytes);
+  evm_rec* rec = S.alloc<evm_rec>(n);
+  u32* off = S.alloc<u32>(C + 1);
+  u32* grp = S.alloc<u32>(n);
+  const u32 L0 = (u32)tree_in->n_leaves;
+  const size_t nmax = std::min<size_t>(n, SM_BINS);
+  u64* nck = S.alloc<u64>(nmax);
+  int32_t* nxr = S.alloc<int32_t>(nmax);
+  u64* mck = S.alloc<u64>(L0 + nmax);
+  int32_t* mxr = S.alloc<int32_t>(L0 + nmax);
+  if (!z || !rec || !off || !grp || !nck || !nxr || !mck || !mxr) return EVM_ENOMEM;
+  u32* cnt = reinterpret_cast<u32*>(z);  // [C] counts, then the long-cell count at [C]
+  u32* long_n = cnt + C;
+  u32* long_list = S.alloc<u32>(std::max<size_t>(n / SM_SEG + 1, 1));
+  if (!long_list) return EVM_ENOMEM;
+  u32* bins = reinterpret_cast<u32*>(z + a_cnt);
+  u32* pres = reinterpret_cast<u32*>(z + a_cnt + a_bins);
+  u64* table = reinterpret_cast<u64*>(z + a_cnt + a_bins + a_pres);
+  HIPR(hipMemsetAsync(z, 0, zero_bytes, ctx->stream));
+  KLAUNCH(k_sm_pack, dim3(grid_for(n, 256, 1024)), dim3(256), (const uint8_t*)ts, stride, n, cell, C, rec, cnt, table,
+          (u32)lg, info);
+  KLAUNCH(k_sm_scan, dim3(1), dim3(SM_FOLD_THREADS), cnt, C, off);
+  KLAUNCH(k_sm_scatter, dim3(grid_for(n, 256, 1024)), dim3(256), (const evm_rec*)rec, n, C, cnt, grp);
+  KLAUNCH(k_sm_lww, dim3(grid_for(C, 256, 4096)), dim3(256), (const evm_rec*)rec, (const u32*)off, (const u32*)grp, C,
+          prior, prior_present, flags, winner, bins, pres, long_list, long_n, info);
+  KLAUNCH(k_sm_long, dim3(64), dim3(SM_LONG_THREADS), (const evm_rec*)rec, (const u32*)off, (const u32*)grp,
+          (const u32*)long_list, (const u32*)long_n, prior, prior_present, flags, winner, bins, pres, info);
+  evm_tree* t = nullptr;
+  int st = tree_alloc_cap(ctx, 1, (uint64_t)L0 + nmax, &t);
+  if (st) return st;
+  KLAUNCH(k_sm_fold, dim3(1), dim3(SM_FOLD_THREADS), (const u32*)bins, (const u32*)pres, (const u64*)tree_in->ck,
+          (const int32_t*)tree_in->xr, L0, nck, nxr, mck, mxr, t->off, t->ck, t->xr, t->pfx, info);
+  Info hi;
+  if ((st = read_info(ctx, info, &hi))) {
+    tree_destroy(ctx, t);
+    return st;
+  }
+  if (hi.bad) {
+    tree_destroy(ctx, t);
+    KLAUNCH(k_mark_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags);
+    return EVM_ENONCANON;
+  }
+  if (hi.bad_aux || hi.collision) {
+    tree_destroy(ctx, t);
+    return hi.bad_aux ? EVM_EINVAL : EVM_ECOLLISION;
+  }
+  if (hi.fold_overflow) {
+    tree_destroy(ctx, t);
+    return SM_FALLBACK;
+  }
+  t->n_leaves = hi.n_leaves;
+  *tree_out = t;
+  return EVM_OK;
+}
+
 static int apply_general(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tree_in, const char* ts, size_t stride,
                          size_t n, const u32* cell, u32 n_cells, const u32* cell_owner, const evm_rec* prior,
                          const uint8_t* prior_present, const Stored& stored, uint8_t* flags, int32_t* winner,
@@ -1969,8 +2435,15 @@ static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
     if (!info || !prior) return EVM_ENOMEM;
     // one launch: the status record, and winner = -1 for every cell; the
     // cells' current maxima (SELECT ... ORDER BY timestamp DESC LIMIT 1)
+    // the small-batch path: eligible batches up to SM_MAX_N over many cells,
+    // and up to SM_AUTO_FEW over few (measured: 100 msgs 0.060 vs 0.106 ms on
+    // the tc path, 1,000 msgs 0.097 vs 0.122 ms)
+    const bool small_ok = n && !cell_owner && tree_in->n_owners == 1 && n_stored == 0 && n_cells <= SM_MAX_CELLS &&
+                          ((uintptr_t)ts & 15) == 0 && n < 0x7fffffffu;
+    const bool small_auto = small_ok && path == 0 && n <= SM_AUTO_FEW;
     // (the tc path's carry writes every cell's winner itself)
-    const bool tc_path = n && path != 1 && (path == 3 || (path == 0 && !cell_owner && n_cells <= CL_MAX_CELLS));
+    const bool tc_path =
+        n && path != 1 && (path == 3 || (path == 0 && !cell_owner && n_cells <= CL_MAX_CELLS && !small_auto));
     auto init = [&](bool winners) -> int {
       const size_t nw = winners ? n_cells : 0;
       KLAUNCH(k_apply_init, dim3(grid_for(std::max<size_t>(nw, 1), 256)), dim3(256), info, info_init(), winner, nw);
@@ -1987,7 +2460,7 @@ static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
       if ((st = read_info(ctx, info, &hi))) return st;
       if (hi.bad) return EVM_ENONCANON;
       st = merge_into_tree(ctx, S, tree_in, tree_in->n_owners, nullptr, nullptr, 0, tree_out);
-    } else if (path == 1 || path == 3 || (path == 0 && !cell_owner && n_cells <= CL_MAX_CELLS)) {
+    } else if (path == 1 || path == 3 || (path == 0 && !cell_owner && n_cells <= CL_MAX_CELLS && !small_auto)) {
       if (cell_owner || n_cells > CL_MAX_CELLS) return EVM_EINVAL;
       st = TP_REDO;
       if (path != 1) {
@@ -2005,6 +2478,22 @@ static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
                                  flags, winner, tree_out);
       }
     } else {
+      // a small batch (one owner, no stored rows): five kernels and one status read
+      st = SM_FALLBACK;
+      if (small_ok && (path == 4 || small_auto || (path == 0 && n <= SM_MAX_N))) {
+        {
+          Scratch S2(ctx);  // released before a rerun
+          st = apply_small(ctx, S2, info, tree_in, ts, stride, n, cell, n_cells, prior, prior_present, flags, winner,
+                           tree_out);
+        }
+        if (st != SM_FALLBACK) {
+          if (st) return st;
+          ++ctx->stats.small_batches;
+          return evm_sync(ctx);
+        }
+        ++ctx->stats.small_fallbacks;
+        if ((st = init(true))) return st;  // the sort path, from a fresh status record
+      }
       st = apply_general(ctx, S, info, tree_in, ts, stride, n, cell, n_cells, cell_owner, prior, prior_present, stored,
                          flags, winner, tree_out);
     }

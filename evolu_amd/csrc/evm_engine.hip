@@ -198,7 +198,12 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
     return EVM_OK;
   }
   const int B = hi_bit - lo_bit;
-  const int passes = (B + RADIX_BITS - 1) / RADIX_BITS;
+  // 10-bit digits when they save a pass (EVM_OPT_RADIX 2): 1,024 digits per
+  // pass, 4 per thread in the look-back
+  const bool wide = ctx->radix_onesweep == 2 && (B + 9) / 10 < (B + RADIX_BITS - 1) / RADIX_BITS;
+  const int rb = wide ? 10 : RADIX_BITS;
+  const int bins = 1 << rb;
+  const int passes = (B + rb - 1) / rb;
   const int width = (B + passes - 1) / passes;
   const u32 ntiles = (u32)((n + SORT_TILE - 1) / SORT_TILE);
   K* k2 = S.alloc<K>(n);
@@ -207,23 +212,33 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
   if (!k2 || !v2 || !v3) return EVM_ENOMEM;
   if (ctx->radix_onesweep && passes <= RADIX_MAX_PASSES) {
     // one read for every pass's digit histogram, then one launch per pass
-    u64* status = S.alloc<u64>((size_t)RADIX_BINS * ntiles);
-    u32* small = S.alloc<u32>((size_t)RADIX_MAX_PASSES * RADIX_BINS + RADIX_MAX_PASSES + 1);
+    u64* status = S.alloc<u64>((size_t)bins * ntiles);
+    u32* small = S.alloc<u32>((size_t)RADIX_MAX_PASSES * bins + RADIX_MAX_PASSES + 1);
     if (!status || !small) return EVM_ENOMEM;
     u32* gh = small;
-    u32* ctr = small + RADIX_MAX_PASSES * RADIX_BINS;
+    u32* ctr = small + RADIX_MAX_PASSES * bins;
     u32* err = ctr + RADIX_MAX_PASSES;
-    HIPR(hipMemsetAsync(small, 0, sizeof(u32) * ((size_t)RADIX_MAX_PASSES * RADIX_BINS + RADIX_MAX_PASSES + 1),
+    HIPR(hipMemsetAsync(small, 0, sizeof(u32) * ((size_t)RADIX_MAX_PASSES * bins + RADIX_MAX_PASSES + 1),
                         ctx->stream));
-    HIPR(hipMemsetAsync(status, 0, sizeof(u64) * RADIX_BINS * ntiles, ctx->stream));
-    KLAUNCH((k_radix_ghist<K>), dim3(std::min<u32>(ntiles, 2048)), dim3(SORT_THREADS), keys, n, lo_bit, width, hi_bit,
-            passes, gh);
-    KLAUNCH(k_radix_gscan, dim3(1), dim3(SORT_THREADS), gh, passes);
+    HIPR(hipMemsetAsync(status, 0, sizeof(u64) * bins * ntiles, ctx->stream));
+    if (wide) {
+      KLAUNCH((k_radix_ghist<K, 10>), dim3(std::min<u32>(ntiles, 2048)), dim3(SORT_THREADS), keys, n, lo_bit, width,
+              hi_bit, passes, gh);
+      KLAUNCH((k_radix_gscan<10>), dim3(1), dim3(SORT_THREADS), gh, passes);
+    } else {
+      KLAUNCH((k_radix_ghist<K>), dim3(std::min<u32>(ntiles, 2048)), dim3(SORT_THREADS), keys, n, lo_bit, width,
+              hi_bit, passes, gh);
+      KLAUNCH((k_radix_gscan<>), dim3(1), dim3(SORT_THREADS), gh, passes);
+    }
     int shift = lo_bit;
     for (int p = 0; p < passes; ++p) {
       const int bits = std::min(width, hi_bit - shift);
-      KLAUNCH((k_radix_onesweep<K>), dim3(ntiles), dim3(SORT_THREADS), keys, vals, k2, v2, n, shift, bits,
-              gh + (size_t)p * RADIX_BINS, status, ctr + p, p, err);
+      if (wide)
+        KLAUNCH((k_radix_onesweep<K, 10>), dim3(ntiles), dim3(SORT_THREADS), keys, vals, k2, v2, n, shift, bits,
+                gh + (size_t)p * bins, status, ctr + p, p, err);
+      else
+        KLAUNCH((k_radix_onesweep<K>), dim3(ntiles), dim3(SORT_THREADS), keys, vals, k2, v2, n, shift, bits,
+                gh + (size_t)p * bins, status, ctr + p, p, err);
       std::swap(keys, k2);
       std::swap(vals, v2);
       if (!v2) v2 = v3;
@@ -238,6 +253,7 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
   u32* offs = S.alloc<u32>((size_t)RADIX_BINS * ntiles);
   if (!counts || !offs) return EVM_ENOMEM;
   int shift = lo_bit;
+  // (8-bit passes: `wide` needs the one-sweep kernels)
   for (int p = 0; p < passes; ++p) {
     const int bits = std::min(width, hi_bit - shift);
     KLAUNCH((k_radix_hist<K>), dim3(ntiles), dim3(SORT_THREADS), keys, n, shift, bits, counts,
@@ -825,7 +841,7 @@ int evm_sync(evm_ctx* ctx) {
 
 int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
   if (!ctx) return EVM_EINVAL;
-  if (option == EVM_OPT_CLIENT_PATH && value >= 0 && value <= 3) {
+  if (option == EVM_OPT_CLIENT_PATH && value >= 0 && value <= 4) {
     ctx->client_path = (int)value;
     return EVM_OK;
   }
@@ -833,7 +849,7 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
     ctx->overlap = (int)value;
     return EVM_OK;
   }
-  if (option == EVM_OPT_RADIX && (value == 0 || value == 1)) {
+  if (option == EVM_OPT_RADIX && value >= 0 && value <= 2) {
     ctx->radix_onesweep = (int)value;
     return EVM_OK;
   }

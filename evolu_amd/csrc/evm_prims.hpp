@@ -388,12 +388,15 @@ constexpr int RS_TAG_SHIFT = 58;
 constexpr u32 RADIX_SPIN_MAX = 1u << 24;
 constexpr int RADIX_MAX_PASSES = 8;
 
-template <typename K>
+// RB: bits per pass (8, or 10 when that saves a pass: 1,024 digits, each
+// thread owning DPT = 4 consecutive digits in the per-digit phases).
+template <typename K, int RB = RADIX_BITS>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_ghist(const K* __restrict__ keys, size_t n, int lo_bit,
                                                               int width, int hi_bit, int passes,
                                                               u32* __restrict__ ghist) {
-  __shared__ u32 h[RADIX_MAX_PASSES][RADIX_BINS];
-  for (int i = threadIdx.x; i < RADIX_MAX_PASSES * RADIX_BINS; i += SORT_THREADS) (&h[0][0])[i] = 0;
+  constexpr int BINS = 1 << RB;
+  __shared__ u32 h[RADIX_MAX_PASSES][BINS];
+  for (int i = threadIdx.x; i < RADIX_MAX_PASSES * BINS; i += SORT_THREADS) (&h[0][0])[i] = 0;
   __syncthreads();
   for (size_t i = (size_t)blockIdx.x * SORT_THREADS + threadIdx.x; i < n; i += (size_t)gridDim.x * SORT_THREADS) {
     const K k = keys[i];
@@ -405,33 +408,46 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_ghist(const K* __restric
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < passes * RADIX_BINS; i += SORT_THREADS) {
+  for (int i = threadIdx.x; i < passes * BINS; i += SORT_THREADS) {
     const u32 v = (&h[0][0])[i];
     if (v) atomicAdd(&ghist[i], v);
   }
 }
 
-// exclusive scan of each pass's digit counts (one workgroup, digit per thread)
-static __global__ __launch_bounds__(SORT_THREADS) void k_radix_gscan(u32* __restrict__ ghist, int passes) {
+// exclusive scan of each pass's digit counts (one workgroup, DPT digits per thread)
+template <int RB = RADIX_BITS>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_gscan(u32* __restrict__ ghist, int passes) {
+  constexpr int BINS = 1 << RB, DPT = BINS / SORT_THREADS;
+  static_assert(DPT >= 1, "at least one digit per thread");
   __shared__ u32 scan_tmp[SORT_THREADS / WAVE + 1];
   for (int p = 0; p < passes; ++p) {
-    const u32 v = ghist[p * RADIX_BINS + threadIdx.x];
-    const u32 incl = block_inclusive_scan<u32>(v, scan_tmp, OpAdd<u32>(), (u32*)nullptr);
-    ghist[p * RADIX_BINS + threadIdx.x] = incl - v;
+    u32 v[DPT], sum = 0;
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      v[k] = ghist[p * BINS + threadIdx.x * DPT + k];
+      sum += v[k];
+    }
+    u32 run = block_inclusive_scan<u32>(sum, scan_tmp, OpAdd<u32>(), (u32*)nullptr) - sum;
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      ghist[p * BINS + threadIdx.x * DPT + k] = run;
+      run += v[k];
+    }
     __syncthreads();
   }
 }
 
-template <typename K>
+template <typename K, int RB = RADIX_BITS>
 __global__ __launch_bounds__(SORT_THREADS) void k_radix_onesweep(const K* __restrict__ kin, const u32* __restrict__ vin,
                                                                  K* __restrict__ kout, u32* __restrict__ vout, size_t n,
                                                                  int shift, int bits, const u32* __restrict__ goff,
                                                                  u64* __restrict__ status, u32* __restrict__ tile_ctr,
                                                                  int pass, u32* __restrict__ err) {
+  constexpr int BINS = 1 << RB, DPT = BINS / SORT_THREADS;
   const u64 tag = (u64)(pass + 1) << RS_TAG_SHIFT, tag_mask = 15ull << RS_TAG_SHIFT;
-  __shared__ u32 wcnt[SORT_THREADS / WAVE][RADIX_BINS];
-  __shared__ u32 toff[RADIX_BINS];
-  __shared__ u32 lstart[RADIX_BINS];
+  __shared__ u32 wcnt[SORT_THREADS / WAVE][BINS];
+  __shared__ u32 toff[BINS];
+  __shared__ u32 lstart[BINS];
   __shared__ u32 scan_tmp[SORT_THREADS / WAVE + 1];
   __shared__ u32 tile_s;
   __shared__ K skey[SORT_TILE];
@@ -476,48 +492,58 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_onesweep(const K* __rest
     }
   }
   __syncthreads();
-  u32 tot = 0;
-  const u32 d = threadIdx.x;
-  if (d < nbins) {
+  // per digit (DPT consecutive ones per thread): prefix over waves, then
+  // publish this tile's count and look back for the tiles before it
+  u32 tot[DPT], tsum = 0;
 #pragma unroll
-    for (int ww = 0; ww < SORT_THREADS / WAVE; ++ww) {
-      const u32 t = wcnt[ww][d];
-      wcnt[ww][d] = tot;
-      tot += t;
-    }
-    // publish this tile's count, then look back for the tiles before it
-    u64* my = status + (size_t)tile * RADIX_BINS + d;
-    u64 excl = 0;
-    if (tile == 0) {
-      __hip_atomic_store(my, RS_PRE | tag | (u64)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(my, RS_AGG | tag | (u64)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      u32 spins = 0;
-      for (int t = (int)tile - 1; t >= 0;) {
-        const u64 s = __hip_atomic_load(status + (size_t)t * RADIX_BINS + d, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-        const bool mine = (s & tag_mask) == tag;
-        if (mine && (s & RS_PRE)) {
-          excl += s & RS_VAL;
-          break;
-        }
-        if (mine && (s & RS_AGG)) {
-          excl += s & RS_VAL;
-          --t;
-          continue;
-        }
-        if (++spins > RADIX_SPIN_MAX) {
-          atomicOr(err, 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+  for (int k = 0; k < DPT; ++k) {
+    const u32 d = threadIdx.x * DPT + k;
+    tot[k] = 0;
+    if (d < nbins) {
+#pragma unroll
+      for (int ww = 0; ww < SORT_THREADS / WAVE; ++ww) {
+        const u32 t = wcnt[ww][d];
+        wcnt[ww][d] = tot[k];
+        tot[k] += t;
       }
-      __hip_atomic_store(my, RS_PRE | tag | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      u64* my = status + (size_t)tile * BINS + d;
+      u64 excl = 0;
+      if (tile == 0) {
+        __hip_atomic_store(my, RS_PRE | tag | (u64)tot[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_store(my, RS_AGG | tag | (u64)tot[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        u32 spins = 0;
+        for (int t = (int)tile - 1; t >= 0;) {
+          const u64 s = __hip_atomic_load(status + (size_t)t * BINS + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const bool mine = (s & tag_mask) == tag;
+          if (mine && (s & RS_PRE)) {
+            excl += s & RS_VAL;
+            break;
+          }
+          if (mine && (s & RS_AGG)) {
+            excl += s & RS_VAL;
+            --t;
+            continue;
+          }
+          if (++spins > RADIX_SPIN_MAX) {
+            atomicOr(err, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __hip_atomic_store(my, RS_PRE | tag | (excl + tot[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      toff[d] = goff[d] + (u32)excl;
     }
-    toff[d] = goff[d] + (u32)excl;
+    tsum += tot[k];
   }
-  const u32 incl = block_inclusive_scan<u32>(tot, scan_tmp, OpAdd<u32>(), (u32*)nullptr);
-  if (threadIdx.x < nbins) lstart[threadIdx.x] = incl - tot;
+  u32 run = block_inclusive_scan<u32>(tsum, scan_tmp, OpAdd<u32>(), (u32*)nullptr) - tsum;
+#pragma unroll
+  for (int k = 0; k < DPT; ++k) {
+    const u32 d = threadIdx.x * DPT + k;
+    if (d < nbins) lstart[d] = run;
+    run += tot[k];
+  }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; ++r) {

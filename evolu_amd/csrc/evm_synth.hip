@@ -1,5 +1,5 @@
 // Synthetic message streams on the device (bench and test input, not part of
-// libevm): BASELINE config 4 -- O owners x P messages, 4 HLC nodes per owner,
+// libevm).  Config 5 shape at the end of the file.  BASELINE config 4 -- O owners x P messages, 4 HLC nodes per owner,
 // a 30-day span, every timestamp canonical.  Every byte is a
 // pure function of (seed, owner, message index), so any rank can regenerate
 // any owner's messages (the bench's self-check) and evolu_amd/synth.py has a
@@ -146,6 +146,83 @@ u64 gcd(u64 a, u64 b) {
   return a;
 }
 
+// ---------------------------------------------------------------------------
+// BASELINE config 5 shape (the server side): n messages, owners Zipf(s) by
+// the inverse of `cdf` (host-built, cumulative, O doubles), shuffled, the
+// last n / 10 rows exact redeliveries of earlier ones.  Message r (source
+// index src = r, or a redelivery's H(9, r, 0) % base):
+//   owner o = upper_bound(cdf, u) with u = (H(4, src, 0) >> 11) * 2^-53
+//   node    = H(2, o, q), q = H(5, src, 0) & 3 (4 nodes per owner); a node
+//             with H(6, o, q) % 100 == 0 spells its hex letters upper-case
+//   millis  = T0 + (H(7, src, 0) % slots(o)) * 1000: a 1-second grid of
+//             slots(o) = max(1, floor(base * p_o) / 4) -- ~4 messages per slot
+//             per owner, so equal millis across nodes are frequent
+//   counter = H(8, src, 0) % 1024
+//   keep    = H(10, src, 0) % 10 != 0 (the client already holds it)
+// ---------------------------------------------------------------------------
+struct C5 {
+  u64 seed;
+  u32 O;
+  u64 n, base;
+  const double* cdf;
+};
+
+__device__ __forceinline__ void c5_message(const C5& S, u64 src, u32 (&w)[12], u32* owner, bool* keep) {
+  const double u = (double)(H(S.seed, 4, src, 0) >> 11) * (1.0 / 9007199254740992.0);
+  u32 lo = 0, hi = S.O;  // upper_bound
+  while (lo < hi) {
+    const u32 m = (lo + hi) >> 1;
+    if (S.cdf[m] <= u) lo = m + 1;
+    else hi = m;
+  }
+  const u32 o = lo < S.O ? lo : S.O - 1;
+  const u32 q = (u32)(H(S.seed, 5, src, 0) & 3u);
+  const u64 node = H(S.seed, 2, o, q);
+  u32 mask = 0;
+  if (H(S.seed, 6, o, q) % 100u == 0u)
+    for (int k = 0; k < 16; ++k)
+      if (((node >> (60 - 4 * k)) & 15u) >= 10u) mask |= 1u << k;
+  const double p = S.cdf[o] - (o ? S.cdf[o - 1] : 0.0);
+  u64 slots = (u64)((double)S.base * p) / 4u;
+  if (slots < 1) slots = 1;
+  const u64 ms = T0 + (H(S.seed, 7, src, 0) % slots) * 1000ull;
+  const u32 ctr = (u32)(H(S.seed, 8, src, 0) % 1024u);
+  format_ts46((ms << 16) | ctr, node, mask, w);
+  *owner = o;
+  *keep = H(S.seed, 10, src, 0) % 10u != 0u;
+}
+
+__global__ void k_c5(C5 S, char* __restrict__ ts, u32* __restrict__ owner, uint8_t* __restrict__ keep) {
+  for (u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x; r < S.n; r += (u64)gridDim.x * blockDim.x) {
+    const u64 src = r < S.base ? r : H(S.seed, 9, r, 0) % S.base;
+    u32 w[12], o;
+    bool kp;
+    c5_message(S, src, w, &o, &kp);
+    store_row(ts, r, w);
+    if (owner) owner[r] = o;
+    if (keep) keep[r] = kp ? 1 : 0;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// BASELINE config 5 shape: n rows of 48 bytes, owner ids, keep flags (see
+// above); cdf: device, O cumulative owner probabilities.  0, or -1.
+int evs_config5_shape(void* stream, uint64_t seed, uint32_t O, uint64_t n, const double* cdf, char* ts,
+                      uint32_t* owner, uint8_t* keep) {
+  if (!O || !cdf || (n && !ts)) return -1;
+  if (!n) return 0;
+  C5 S{seed, O, n, n - n / 10, cdf};
+  if (S.base == 0) S.base = n;
+  hipLaunchKernelGGL(k_c5, dim3(grid(n)), dim3(256), 0, (hipStream_t)stream, S, ts, owner, keep);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // extern "C"
+
+namespace {
 }  // namespace
 
 extern "C" {

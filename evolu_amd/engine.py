@@ -79,7 +79,7 @@ class Engine:
         check(self.lib.evm_set_option(self.h, option, value), "evm_set_option")
 
     STATS_FIELDS = ("workspace_regrows", "workspace_bytes", "scratch_pool_allocs", "scratch_pool_bytes",
-                    "block_allocs", "block_bytes", "tc_batches", "tc_redos")
+                    "block_allocs", "block_bytes", "tc_batches", "tc_redos", "small_batches", "small_fallbacks")
 
     def stats(self) -> dict:
         """Allocation counters (evm_get_stats)."""

@@ -282,6 +282,36 @@ def config4_owners(seed: int, P: int, G: int, owners: np.ndarray):
     return ts, np.repeat(np.arange(len(owners), dtype=np.uint32), P), keep
 
 
+def config5_cdf(O: int, zipf_s: float = 1.2) -> np.ndarray:
+    """Cumulative Zipf(s) owner probabilities (float64[O]) -- the config-5
+    shape generator's input (the device and the twin search the same array)."""
+    w = 1.0 / np.arange(1, O + 1, dtype=np.float64) ** zipf_s
+    return np.cumsum(w / w.sum())
+
+
+def config5_shape(seed: int, O: int, n: int, cdf: np.ndarray = None):
+    """Twin of evs_config5_shape (evm_synth.hip): (ts (n, 48), owner u32, keep
+    bool) -- Zipf owners, 4 nodes per owner (1 % upper-case), a 1-second
+    grid of ~4 messages per slot per owner, shuffled, the last n / 10 rows
+    exact redeliveries of earlier ones."""
+    cdf = config5_cdf(O) if cdf is None else cdf
+    base = n - n // 10 or n
+    r = np.arange(n, dtype=np.uint64)
+    src = np.where(r < _U(base), r, _H(seed, 9, r, 0) % _U(base)).astype(np.uint64)
+    u = (_H(seed, 4, src, 0) >> _U(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+    o = np.minimum(np.searchsorted(cdf, u, side="right"), O - 1).astype(np.int64)
+    q = (_H(seed, 5, src, 0) & _U(3)).astype(np.int64)
+    node = _hex16(_H(seed, 2, o, q))
+    upper = (_H(seed, 6, o, q) % _U(100)) == 0
+    node = np.where(upper[:, None] & (node >= ord("a")), node - 32, node).astype(np.uint8)
+    p = cdf[o] - np.where(o > 0, cdf[np.maximum(o - 1, 0)], 0.0)
+    slots = np.maximum(1, (np.float64(base) * p).astype(np.uint64) // _U(4)).astype(np.uint64)
+    millis = BENCH_T0 + ((_H(seed, 7, src, 0) % slots).astype(np.int64)) * 1000
+    ctr = (_H(seed, 8, src, 0) % _U(1024)).astype(np.int64)
+    keep = (_H(seed, 10, src, 0) % _U(10)) != 0
+    return format_timestamps(millis, ctr, node, 48), o.astype(np.uint32), keep
+
+
 class DeviceSynth:
     """libevmsynth.so: the config-4 generator on the device (torch tensors)."""
 
@@ -300,6 +330,7 @@ class DeviceSynth:
         L.evs_config4_source.argtypes = [vp, u64, u32, u32, u32, u32, vp, vp, vp]
         L.evs_config4_owners.argtypes = [vp, u64, u32, u32, u32, vp, u32, vp, vp, vp]
         L.evs_owner_ids.argtypes = [vp, u64, u32, C.c_size_t, vp]
+        L.evs_config5_shape.argtypes = [vp, u64, u32, u64, vp, vp, vp, vp]
         self.L = L
 
     @staticmethod
@@ -446,3 +477,17 @@ def config1(n: int = 100_000, n_nodes: int = 3, stride: int = 48, seed_config: i
     ts = format_timestamps(np.array(millis, dtype=np.int64), np.array(counter, dtype=np.int64), nodes[np.array(nidx)],
                            stride)
     return ts, np.array(cell, dtype=np.uint32), cells, values
+
+
+def device_config5_shape(gen: "DeviceSynth", seed: int, O: int, n: int, dev, zipf_s: float = 1.2):
+    """evs_config5_shape on the device -> (ts (n, 48) uint8, owner int32, keep uint8) tensors."""
+    import torch
+
+    cdf = torch.from_numpy(config5_cdf(O, zipf_s)).to(dev)
+    ts = torch.empty((max(n, 1), 48), dtype=torch.uint8, device=dev)
+    owner = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    keep = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    if gen.L.evs_config5_shape(gen._stream(dev), seed, O, n, gen._p(cdf), gen._p(ts), gen._p(owner), gen._p(keep)):
+        raise ValueError("evs_config5_shape: bad arguments")
+    torch.cuda.current_stream(dev).synchronize()  # (cdf is freed on return)
+    return ts[:n], owner[:n], keep[:n]

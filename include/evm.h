@@ -99,19 +99,25 @@ typedef struct evm_stats {
   uint64_t block_allocs;        /* device blocks allocated for trees and stores (freed ones are reused) */
   uint64_t block_bytes;
   uint64_t tc_batches;          /* evm_apply_batch calls the streaming tc path finished */
-  uint64_t tc_redos;            /* ... that met a tie and were redone by the exact walk path */
+  uint64_t tc_redos;            /* ... whose tie list overflowed and were redone by the exact walk path */
+  uint64_t small_batches;       /* evm_apply_batch calls the small-batch path finished */
+  uint64_t small_fallbacks;     /* ... it handed to the sort path (a cell of > 4,096 rows, minutes too wide) */
 } evm_stats;
 int evm_get_stats(const evm_ctx* ctx, evm_stats* out);
 int evm_set_stream(evm_ctx* ctx, void* hip_stream); /* NULL: the HIP default stream; initially the context's own */
 void* evm_get_stream(evm_ctx* ctx);
 int evm_sync(evm_ctx* ctx);
 /* tuning / test knobs */
-#define EVM_OPT_CLIENT_PATH 1 /* evm_apply_batch: 0 auto (streaming tc path, exact walk on a tie), 1 exact walk path, 2 sort path, 3 tc path (exact walk on a tie) */
+#define EVM_OPT_CLIENT_PATH 1 /* evm_apply_batch: 0 auto (<= 2,048 cells: the streaming tc path; more cells: the \
+                                 small-batch path up to 262,144 messages, else the sort path), 1 exact walk path, \
+                                 2 sort path, 3 tc path (the exact walk path only when a range's tie list \
+                                 overflows), 4 small-batch path (the sort path when it does not apply) */
 #define EVM_OPT_OVERLAP 3     /* 1 (default): independent checks run on a second HIP stream inside a call; 0: one stream */
 #define EVM_OPT_SERVER_PATH 2 /* evm_server_ingest: 0/1 per-owner LDS path, owners above its capacity cut into
                                  key-range segments; 2 force the sort path; 3 LDS path without the segments (owners
                                  above the capacity through the sort path) */
-#define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 0 histogram + scan + scatter per pass */
+#define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 2 the same with \
+                                 10-bit digits when that saves a pass; 0 histogram + scan + scatter per pass */
 #define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM) */
 int evm_set_option(evm_ctx* ctx, int option, int64_t value);
 /* kernel timing with HIP events on the context stream (for roofline reports) */

@@ -1048,10 +1048,10 @@ napi_value DistSelectSplit(napi_env env, napi_callback_info info) {
   if (!st) st = st_m;
   // the client's trees of the split owners: its hot slots
   uint64_t L = 0;
-  std::vector<uint64_t> soff(nh + 1);
-  if (!st) st = evm_tree_slice(ctx, client, base, nh, nullptr, nullptr, nullptr, 0, &L);
+  Dev dso(ctx, 8ull * (nh + 1));
+  if (!st) st = evm_tree_slice(ctx, client, base, nh, (uint64_t*)dso.p, nullptr, nullptr, 0, &L);
   if (st == EVM_ECAPACITY) st = EVM_OK;
-  Dev dso(ctx, 8ull * (nh + 1)), dsc(ctx, 8 * (L ? L : 1)), dsx(ctx, 4 * (L ? L : 1));
+  Dev dsc(ctx, 8 * (L ? L : 1)), dsx(ctx, 4 * (L ? L : 1));
   if (!st) st = evm_tree_slice(ctx, client, base, nh, (uint64_t*)dso.p, (uint64_t*)dsc.p, (int32_t*)dsx.p, L, &L);
   if (!st) st = evm_tree_from_device_leaves(ctx, nh, (const uint64_t*)dso.p, (const uint64_t*)dsc.p,
                                             (const int32_t*)dsx.p, &sub);

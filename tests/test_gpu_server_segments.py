@@ -135,3 +135,21 @@ def test_size_classes_with_burst_segment(eng, burst):
     assert any("k_svo_a<128" in k for k in ran), ran
     assert any(("k_svo_a<2048" if burst < 4000 else "k_svo_a<SVO_CAP") in k for k in ran), ran
     _same(seg, _run(eng, 2, 302, ts_np, owner_np, cut))
+
+
+@pytest.mark.parametrize("path", [0, 2])
+def test_ten_bit_radix_digits_give_the_same_store(eng, path):
+    """EVM_OPT_RADIX 2 (10-bit digits where they save a pass: the segment
+    sort's ~19-bit ids in 2 passes instead of 3, the sort path's 40-bit leaf
+    keys in 4 instead of 5) against the 8-bit one-sweep sort, bit for bit."""
+    from evolu_amd import synth
+
+    ts_np, owner_np, _ = synth.config5(3000, 1_500_000, seed_config=64)
+    cut = len(ts_np) // 2
+    base = _run(eng, path, 3000, ts_np, owner_np, cut)
+    eng.set_option(4, 2)
+    try:
+        wide = _run(eng, path, 3000, ts_np, owner_np, cut)
+    finally:
+        eng.set_option(4, 1)
+    _same(base, wide)
