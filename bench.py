@@ -78,6 +78,8 @@ SERVER_ALG = {
     "(k_svo_a<512, true>)": (4 + 46 + 1 + 28, 8 + 4 + 1),
     "(k_svo_a<512, false>)": (4 + 32 + 1 + 28, 8 + 4 + 1),
     "k_svo_b": (28 + 32, 8 + 4 + 1 + 8 + 4),  # new rows in, store rows out; new leaves in, tree leaves out
+    "k_svo_b<true>": (28 + 32, 8 + 4 + 1 + 8 + 4),  # (the merge into a non-empty store: LDS-staged keys)
+    "k_svo_b<false>": (28 + 32, 8 + 4 + 1 + 8 + 4),  # (an empty store)
     "k_seg_key": (4 + 4 + 8, 0),  # owner + minute in, (segment, index) out
 }
 SERVER_PIPELINE_BYTES = 127  # the ideal server pipeline, one sort pass

@@ -12,6 +12,7 @@
 //   * general path: stable radix sort by cell + segmented scan (k_lww_*).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -1629,7 +1630,8 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   // TC: ranges of TP1/TP3 (multiples of 256 rows); walk path: ranges of the walks
   size_t range, G;
   if (TC) {
-    range = std::max<size_t>(1024, ((n + TP_RANGES - 1) / TP_RANGES + 255) / 256 * 256);
+    static const size_t tp_ranges = getenv("EVM_TP_RANGES") ? (size_t)atol(getenv("EVM_TP_RANGES")) : TP_RANGES;
+    range = std::max<size_t>(1024, ((n + tp_ranges - 1) / tp_ranges + 255) / 256 * 256);
     range = std::min<size_t>(range, TP_ROWS_MAX);  // (TP1's key holds a 13-bit row offset)
   } else {
     range = (n + CL_RANGE_TARGET - 1) / CL_RANGE_TARGET;
@@ -1884,7 +1886,8 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
 constexpr size_t SM_MAX_N = 1u << 18;       // rows (the auto choice over > 2,048 cells; EVM_OPT_CLIENT_PATH 4 forces it)
 constexpr size_t SM_AUTO_FEW = 1u << 14;    // rows: the auto choice over <= 2,048 cells too
 constexpr u32 SM_MAX_CELLS = 1u << 22;
-constexpr u32 SM_SEG = 32;                  // rows per cell kept in registers (longer cells: k_sm_long)
+constexpr u32 SM_SEG = 8;                   // rows per cell a thread takes (longer cells: k_sm_long; its
+                                            // O(k^2) selection made 20-32-row cells the kernel's tail at 32)
 constexpr u32 SM_LONG_MAX = 4096;           // rows of one cell k_sm_long sorts in LDS
 constexpr int SM_LONG_THREADS = 256;
 constexpr u32 SM_BINS = 1u << 16;           // minutes (45 days) of the dense fold
@@ -1977,13 +1980,29 @@ __global__ __launch_bounds__(SM_FOLD_THREADS) void k_sm_scan(u32* __restrict__ c
     for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) sum += v[q];
     u32 tot;
     u32 run = carry + block_inclusive_scan<u32, OpAdd<u32>>(sum, lds, OpAdd<u32>(), &tot) - sum;
+    u32 x[SM_SCAN_ITEMS];
 #pragma unroll
-    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q)
-      if (a + q < C) {
-        off[a + q] = run;
-        cnt[a + q] = run;
-        run += v[q];
+    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) {
+      x[q] = run;
+      run += v[q];
+    }
+    if (a + SM_SCAN_ITEMS <= C) {  // 16-B stores (off is 256-B aligned scratch too)
+      uint4* po = reinterpret_cast<uint4*>(off + a);
+      uint4* pc = reinterpret_cast<uint4*>(cnt + a);
+#pragma unroll
+      for (u32 q = 0; q < SM_SCAN_ITEMS / 4; ++q) {
+        const uint4 y = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+        po[q] = y;
+        pc[q] = y;
       }
+    } else {
+#pragma unroll
+      for (u32 q = 0; q < SM_SCAN_ITEMS; ++q)
+        if (a + q < C) {
+          off[a + q] = x[q];
+          cnt[a + q] = x[q];
+        }
+    }
     carry += tot;
   }
   if (threadIdx.x == 0) off[C] = carry;
@@ -2297,7 +2316,7 @@ static int apply_small(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tre
   KLAUNCH(k_sm_scatter, dim3(grid_for(n, 256, 1024)), dim3(256), (const evm_rec*)rec, n, C, cnt, grp);
   KLAUNCH(k_sm_lww, dim3(grid_for(C, 256, 4096)), dim3(256), (const evm_rec*)rec, (const u32*)off, (const u32*)grp, C,
           prior, prior_present, flags, winner, bins, pres, long_list, long_n, info);
-  KLAUNCH(k_sm_long, dim3(64), dim3(SM_LONG_THREADS), (const evm_rec*)rec, (const u32*)off, (const u32*)grp,
+  KLAUNCH(k_sm_long, dim3(1024), dim3(SM_LONG_THREADS), (const evm_rec*)rec, (const u32*)off, (const u32*)grp,
           (const u32*)long_list, (const u32*)long_n, prior, prior_present, flags, winner, bins, pres, info);
   evm_tree* t = nullptr;
   int st = tree_alloc_cap(ctx, 1, (uint64_t)L0 + nmax, &t);

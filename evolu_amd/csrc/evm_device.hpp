@@ -127,6 +127,18 @@ __device__ __forceinline__ OKey okey_of(const evm_rec& r) {
 // ----------------------------------------------------------------------------
 __host__ __device__ __forceinline__ u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
 
+// h * 5 + c as a shift-add: left as a multiply, the compiler folds the
+// rotate, the multiply and the 32-bit constant into a 64-bit multiply-add
+// (v_mad_u64_u32, a quarter-rate instruction) once per block; the empty asm
+// keeps the shifted copy opaque so the add stays two full-rate adds.
+__host__ __device__ __forceinline__ u32 mul5_add(u32 h, u32 c) {
+  u32 t = h << 2;
+#ifdef __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+v"(t));
+#endif
+  return h + t + c;
+}
+
 __host__ __device__ __forceinline__ u32 murmur3_46(const u32 (&w)[12]) {
   const u32 c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
   u32 h = 0u;
@@ -135,7 +147,7 @@ __host__ __device__ __forceinline__ u32 murmur3_46(const u32 (&w)[12]) {
     u32 k = w[i] * c1;
     k = rotl32(k, 15) * c2;
     h ^= k;
-    h = rotl32(h, 13) * 5u + 0xe6546b64u;
+    h = mul5_add(rotl32(h, 13), 0xe6546b64u);
   }
   u32 k = w[11] & 0xffffu;  // tail: bytes 44 (low) and 45
   k *= c1;

@@ -653,6 +653,7 @@ struct TreeView {
   const u64* off;
   const u64* ck;
   const int32_t* pfx;
+  const int32_t* xr;
 };
 
 __device__ __forceinline__ int32_t range_hash(const TreeView& t, size_t lo, size_t hi) { return t.pfx[hi] ^ t.pfx[lo]; }
@@ -665,7 +666,11 @@ constexpr int DIFF_LANES = 16;
 // bound, so a level costs one binary search + one load of latency instead of
 // up to eight searches in a row.  The greedy choice (first child whose hash
 // differs, a missing child counting as different) is then made by every lane
-// of the group on the shuffled bounds.
+// of the group on the shuffled bounds.  Once both ranges hold at most 16
+// leaves (a few levels down: ranges shrink ~3x per level), the group loads
+// them -- one leaf of A and one of B per lane -- and finishes every remaining
+// level in registers: a child's presence is a ballot of the lanes whose digit
+// at this depth selects it, its hash a 16-lane XOR reduction.
 __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owners, int64_t* __restrict__ millis) {
   const int sub = threadIdx.x & (DIFF_LANES - 1);
   const u32 groups = gridDim.x * (blockDim.x / DIFF_LANES);
@@ -680,7 +685,12 @@ __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owne
     u64 prefix = (u64)o << 40;
     int depth = 0;
     u64 kval = 0;  // base-3 value of the key string k so far
+    bool in_regs = false;
     while (depth < CODE_DIGITS) {
+      if (ahi - alo <= DIFF_LANES && bhi - blo <= DIFF_LANES) {
+        in_regs = true;  // the rest in registers
+        break;
+      }
       const int sh = 2 * (CODE_DIGITS - 1 - depth);
       // lane s < 4: A bound of prefix + (s+1) << sh; lane 4 <= s < 8: B bound of prefix + (s-3) << sh
       u64 my = 0;
@@ -722,6 +732,35 @@ __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owne
       ahi = a[pick + 1];
       blo = b[pick];
       bhi = b[pick + 1];
+    }
+    if (in_regs) {
+      const u64 ia = alo + sub, ib = blo + sub;
+      bool va = ia < ahi, vb = ib < bhi;
+      const u64 ca = va ? A.ck[ia] : 0ull, cb = vb ? B.ck[ib] : 0ull;
+      const int32_t xa = va ? A.xr[ia] : 0, xb = vb ? B.xr[ib] : 0;
+      const u64 gmask = 0xFFFFull << (threadIdx.x & 63 & ~(DIFF_LANES - 1));
+      while (depth < CODE_DIGITS) {
+        const int sh = 2 * (CODE_DIGITS - 1 - depth);
+        const u32 da = va ? (u32)(ca >> sh) & 3u : 0u, db = vb ? (u32)(cb >> sh) & 3u : 0u;
+        int pick = -1;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const bool ina = da == (u32)c + 1u, inb = db == (u32)c + 1u;
+          const bool ea = (__ballot(ina) & gmask) != 0, eb = (__ballot(inb) & gmask) != 0;
+          int32_t ha = ina ? xa : 0, hb = inb ? xb : 0;
+#pragma unroll
+          for (int m = DIFF_LANES / 2; m >= 1; m >>= 1) {
+            ha ^= __shfl_xor(ha, m, 64);
+            hb ^= __shfl_xor(hb, m, 64);
+          }
+          if (pick < 0 && (ea || eb) && (ea != eb || ha != hb)) pick = c;
+        }
+        if (pick < 0) break;
+        kval = kval * 3 + (u64)pick;
+        ++depth;
+        va = va && da == (u32)pick + 1u;
+        vb = vb && db == (u32)pick + 1u;
+      }
     }
     if (sub == 0) {
       if (depth > 16) {
@@ -1130,7 +1169,7 @@ int evm_merkle_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t*
 
 int evm::launch_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* millis) {
   if (a->n_owners == 0) return EVM_OK;
-  TreeView A{a->off, a->ck, a->pfx}, B{b->off, b->ck, b->pfx};
+  TreeView A{a->off, a->ck, a->pfx, a->xr}, B{b->off, b->ck, b->pfx, b->xr};
   KLAUNCH(k_diff, dim3(grid_for((size_t)a->n_owners * DIFF_LANES, 256, 1 << 16)), dim3(256), A, B, a->n_owners, millis);
   return hip_ok(hipGetLastError());
 }

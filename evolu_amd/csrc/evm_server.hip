@@ -1082,6 +1082,33 @@ __global__ void k_seg_fix(SegView sv, u32 NS, const uint8_t* __restrict__ ownbig
   }
 }
 
+// The merge of a segment's stored rows / tree leaves with its new ones.  With
+// at most SVB_LDS new keys (nearly every segment) they sit in LDS: a stored
+// row finds its place by a binary search there (#new keys below it), and a
+// new row's place comes from the same searches -- a histogram of those counts,
+// whose inclusive prefix at j is the number of stored rows below new row j
+// (keys are disjoint) -- so no search touches global memory.  Larger
+// segments search the global arrays as before.  Leaves the same way (an equal
+// tree leaf counts one bin higher: it is not below the new code).
+constexpr u32 SVB_LDS = 1024;
+
+__device__ __forceinline__ void svb_inclusive_prefix(u32* h, u32 m, u32* tmp) {
+  // h[0..m) -> inclusive prefix sums in place (m <= SVB_LDS + 1)
+  constexpr u32 PER = (SVB_LDS + 1 + SVO_THREADS - 1) / SVO_THREADS;
+  const u32 b0 = min(m, threadIdx.x * PER), b1 = min(m, b0 + PER);
+  u32 sum = 0;
+  for (u32 q = b0; q < b1; ++q) sum += h[q];
+  u32 run = block_inclusive_scan<u32>(sum, tmp, OpAdd<u32>(), (u32*)nullptr) - sum;
+  for (u32 q = b0; q < b1; ++q) {
+    run += h[q];
+    h[q] = run;
+  }
+  __syncthreads();
+}
+
+// MERGE = false: the store is empty (no stored rows, no tree leaves): no LDS
+// staging (its 24 KiB would cost occupancy for nothing).
+template <bool MERGE>
 __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     SegView sv, u32 NS, u32 n_owners, StoreView st, const u64* __restrict__ st_id, const u64* __restrict__ n_tc,
     const u64* __restrict__ n_hi, const u32* __restrict__ n_lo, const u64* __restrict__ n_id,
@@ -1092,6 +1119,10 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     int32_t* __restrict__ to_xr, u64* __restrict__ to_off, int rows_in_place) {
   __shared__ u32 s_dp[SVO_CAP + 1];  // exclusive prefix count of the new leaves already in the tree
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
+  constexpr u32 LN = MERGE ? SVB_LDS : 1;
+  __shared__ u64 k_tc[LN], k_hi[LN];  // new row keys (then new leaf codes in k_tc)
+  __shared__ u32 k_lo[LN];
+  __shared__ u32 hist[LN + 1];
   const u32 s = blockIdx.x;
   const u32 o = seg_owner(sv, s);
   const u64 a = sv.start[s];
@@ -1101,13 +1132,34 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   // rows: the owner's stored and new keys are disjoint sorted lists
   // rows_in_place: an empty store whose every message was inserted -- the
   // K5 rows already sit at their final places (position = batch position)
+  const bool lds_rows = MERGE && !rows_in_place && M <= SVB_LDS;
+  if (lds_rows) {
+    for (u32 j = threadIdx.x; j < M; j += SVO_THREADS) {
+      k_tc[j] = n_tc[a + j];
+      k_hi[j] = n_hi[a + j];
+      k_lo[j] = n_lo[a + j];
+    }
+    for (u32 j = threadIdx.x; j <= M; j += SVO_THREADS) hist[j] = 0;
+  }
+  __syncthreads();
   for (u64 k = sa + threadIdx.x; !rows_in_place && k < sb; k += SVO_THREADS) {
     const SKey key = skey_at(st, k);
     u32 lo = 0, hi = M;
-    while (lo < hi) {
-      const u32 mid = (lo + hi) >> 1;
-      if (skey_cmp(SKey{o, n_tc[a + mid], n_hi[a + mid], n_lo[a + mid]}, key) < 0) lo = mid + 1;
-      else hi = mid;
+    if (lds_rows) {
+      while (lo < hi) {  // (one owner: compare (tc, hi, lo))
+        const u32 mid = (lo + hi) >> 1;
+        const bool below = k_tc[mid] != key.tc ? k_tc[mid] < key.tc
+                           : k_hi[mid] != key.hi ? k_hi[mid] < key.hi : k_lo[mid] < key.lo;
+        if (below) lo = mid + 1;
+        else hi = mid;
+      }
+      atomicAdd(&hist[lo], 1u);
+    } else {
+      while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (skey_cmp(SKey{o, n_tc[a + mid], n_hi[a + mid], n_lo[a + mid]}, key) < 0) lo = mid + 1;
+        else hi = mid;
+      }
     }
     const u64 w = base + (k - sa) + lo;
     so.owner[w] = o;
@@ -1116,9 +1168,19 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     so.lo[w] = key.lo;
     so.id[w] = st_id[k];
   }
+  __syncthreads();
+  if (lds_rows) svb_inclusive_prefix(hist, M + 1, tmp);  // hist[j] = stored rows below new row j
   for (u32 j = threadIdx.x; !rows_in_place && j < M; j += SVO_THREADS) {
-    const SKey key{o, n_tc[a + j], n_hi[a + j], n_lo[a + j]};
-    const u64 w = base + j + (store_lower(st, sa, sb, key) - sa);
+    SKey key;
+    u64 below;
+    if (lds_rows) {
+      key = SKey{o, k_tc[j], k_hi[j], k_lo[j]};
+      below = hist[j];
+    } else {
+      key = SKey{o, n_tc[a + j], n_hi[a + j], n_lo[a + j]};
+      below = store_lower(st, sa, sb, key) - sa;
+    }
+    const u64 w = base + j + below;
     so.owner[w] = o;
     so.tc[w] = key.tc;
     so.hi[w] = key.hi;
@@ -1145,19 +1207,42 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     run += d[r];
   }
   if (threadIdx.x == 0) s_dp[NL] = dtot;
+  const bool lds_leaves = MERGE && NL <= SVB_LDS;
+  __syncthreads();  // (the rows' LDS keys are dead: the leaf codes take k_tc)
+  if (lds_leaves) {
+    for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) k_tc[j] = l_ck[a + j];
+    for (u32 j = threadIdx.x; j <= NL; j += SVO_THREADS) hist[j] = 0;
+  }
   __syncthreads();
   for (u64 k = la + threadIdx.x; k < lb; k += SVO_THREADS) {
     const u64 code = t_ck[k];
-    const u32 j = (u32)(lb_u64(l_ck, a, a + NL, code) - a);  // new leaves below this code
-    const bool eq = j < NL && l_ck[a + j] == code;
+    u32 j;
+    bool eq;
+    if (lds_leaves) {
+      u32 lo = 0, hi = NL;
+      while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (k_tc[mid] < code) lo = mid + 1;
+        else hi = mid;
+      }
+      j = lo;
+      eq = j < NL && k_tc[j] == code;
+      atomicAdd(&hist[j + (eq ? 1u : 0u)], 1u);  // (an equal tree leaf is not below new leaf j)
+    } else {
+      j = (u32)(lb_u64(l_ck, a, a + NL, code) - a);  // new leaves below this code
+      eq = j < NL && l_ck[a + j] == code;
+    }
     const u64 w = lbase + (k - la) + j - s_dp[j];
     to_ck[w] = code;
     to_xr[w] = t_xr[k] ^ (eq ? l_xr[a + j] : 0);
   }
+  __syncthreads();
+  if (lds_leaves) svb_inclusive_prefix(hist, NL + 1, tmp);  // hist[j] = tree leaves below new leaf j
   for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) {
     if (l_dup[a + j]) continue;
-    const u64 code = l_ck[a + j];
-    const u64 w = lbase + (j - s_dp[j]) + (lb_u64(t_ck, la, lb, code) - la);
+    const u64 code = lds_leaves ? k_tc[j] : l_ck[a + j];
+    const u64 below = lds_leaves ? (u64)hist[j] : lb_u64(t_ck, la, lb, code) - la;
+    const u64 w = lbase + (j - s_dp[j]) + below;
     to_ck[w] = code;
     to_xr[w] = l_xr[a + j];
   }
@@ -1939,7 +2024,12 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     return st;
   }
   const StoreOut so{ns->owner, ns->tc, ns->hi, ns->lo, ns->id};
-  KLAUNCH(k_svo_b, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
+  if (s->n)
+    KLAUNCH(k_svo_b<true>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
+          c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + NS, so, ns->off, nt->ck, nt->xr,
+          nt->off, in_place);
+  else
+    KLAUNCH(k_svo_b<false>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
           c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + NS, so, ns->off, nt->ck, nt->xr,
           nt->off, in_place);
   if ((st = scan_exclusive<int32_t, OpXor>(ctx, S, nt->xr, ht[1], nt->pfx, nt->pfx + ht[1]))) {

@@ -51,6 +51,13 @@ def short(name):
         return "(k_dist_scatter<%s>)" % ("SEND" if targs.strip("<>") == "0" else "RECV")
     if base == "k_dist_count" and targs:
         return "(k_dist_count<MODE>)"
+    if base in ("k_svo_b", "k_tp_pack", "k_cl_fold_hist", "k_radix_onesweep", "k_radix_ghist") and targs:
+        # KLAUNCH names a plain template launch by its text: "k_svo_b<true>"; the
+        # parenthesised launches of the client/sort paths keep their own names
+        t = targs.strip("<>").split(",")[0].strip()
+        if base == "k_svo_b":
+            return "k_svo_b<%s>" % t
+        return base
     if base == "k_svo_a" and targs:
         # KLAUNCH names the template launch by its source text: "(k_svo_a<1024, true>)"
         args = [a.strip().rstrip("u") for a in targs[1:-1].split(",")]
