@@ -1116,7 +1116,7 @@ template <bool S48>
 __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_WPE, 8))) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
                                                         const u32* __restrict__ cell, u32 C, size_t range_len,
                                                         u64* __restrict__ tcs, u32* __restrict__ hash,
-                                                        u32* __restrict__ minute, u64* __restrict__ agg,
+                                                        u64* __restrict__ agg,
                                                         u32* __restrict__ arow, Info* __restrict__ info,
                                                         u32* __restrict__ zero_buf, u32 zero_n) {
   // LDS: [C] max key per cell of this range, [ceil(C/32)] the marked cells
@@ -1179,22 +1179,17 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
       aux_bad |= ci < C ? 0u : 1u;
     }
     if (S48 && first + 64 <= end && (first & 3) == 0) {
-      // hash / minute of the wave's 64 rows as 16-B-per-lane stores (32 lanes)
+      // hashes of the wave's 64 rows as 16-B-per-lane stores (16 lanes); the
+      // minute is not stored: the fused check + fold re-derives it from tc
       u32* st32 = reinterpret_cast<u32*>(&stage[wv][0]);
       st32[lane] = p.hash;
-      st32[64 + lane] = p.minute;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (lane < 32) {
-        const uint4 v = stage[wv][lane];
-        u32* dst = lane < 16 ? hash : minute;
-        reinterpret_cast<uint4*>(dst + first)[lane & 15] = v;
-      }
+      if (lane < 16) reinterpret_cast<uint4*>(hash + first)[lane] = stage[wv][lane];
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     } else if (i < end) {
       hash[i] = p.hash;
-      minute[i] = p.minute;
     }
     // (lanes past the range end parsed zero bytes: their minute must not
     // widen the bounds, or the dense fold of a batch whose size is not a
@@ -1396,7 +1391,8 @@ constexpr u32 TPC_ROWS = 64 * 4 * TP_WAVES;  // 4 rounds per wave per chunk
 __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ tcs, const u32* __restrict__ cell,
                                                         size_t n, u32 C, size_t range_len,
                                                         const u64* __restrict__ carry, const u32* __restrict__ crow,
-                                                        NodeSrc N, uint8_t* __restrict__ flags) {
+                                                        NodeSrc N, uint8_t* __restrict__ flags,
+                                                        u32* __restrict__ noop, Info* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) u64 tw_lds[];
   u64* T = tw_lds;                                       // [C] running max per cell: tc
   u64* M = T + C;                                        // [C] the walk round's lanes per cell (zero between rounds)
@@ -1494,9 +1490,10 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
             }
           }
         }
+        int k3 = 1;
         if (ok) {
           const TK t = tk_max(N, cv, TK{T[cv], TR[cv]}, pm);
-          const int k3 = tk_cmp(N, cv, own, t);
+          k3 = tk_cmp(N, cv, own, t);
           // applyMessages.ts:93 `t < timestamp` -> upsert; :105 `t !== timestamp` -> INSERT + XOR
           flags[own.row] = k3 > 0 ? (uint8_t)(EVM_MSG_UPS | EVM_MSG_XOR) : k3 < 0 ? (uint8_t)EVM_MSG_XOR : (uint8_t)0;
           if ((peers >> lane) == 1ull) {  // the round's last peer of the cell
@@ -1505,9 +1502,300 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
             TR[cv] = nt.row;
           }
         }
+        // exact redeliveries of the cell's max: listed for the fold's correction (k_xf_fix)
+        const u64 nb = __ballot(ok && k3 == 0);
+        if (nb) {
+          u32 at = 0;
+          if (lane == 0) at = atomicAdd(&info->noop_n, (u32)__popcll(nb));
+          at = __shfl(at, 0, 64);
+          if ((nb >> lane) & 1ull) noop[at + (u32)__popcll(nb & lt)] = own.row;
+        }
       }
     }
     __syncthreads();
+  }
+}
+
+// ============================================================================
+// XF: the tc path's cross-cell PK check fused with its Merkle fold.
+//
+// Messages are bucketed by MINUTE (contiguous minute ranges; a batch spanning
+// fewer minutes than buckets splits each minute by hash bits), so one bucket
+// holds every copy of a timestamp AND every message of its minutes: the
+// bucket's workgroup checks the global `__message` PK in an LDS set and XORs
+// the hashes into an LDS histogram of its minutes.  The fold XORs EVERY row;
+// the rows the walk finds to be exact redeliveries of their cell's max (the
+// only rows applyMessages.ts:105 does not XOR) are XORed out again afterwards
+// (k_xf_fix) -- XOR is its own inverse, the presence count drops by one.
+//
+// The LDS set compares 64-bit fingerprints instead of the 46 raw bytes: a
+// pair is hash32 | minute offset | tc bits | cell, so two copies of one
+// timestamp carry equal fingerprints.  Equal fingerprints in two different
+// cells are a *possible* collision: the batch is redone by the exact walk
+// path, whose byte-exact check decides (two distinct timestamps need equal
+// murmur3 AND equal minute AND equal mixed tc bits to get there).  A bucket
+// that overflows, a span above XF_SPAN_MAX or two base-3 key lengths also
+// redo the batch (`xf_redo`).  Bytes per message: scatter 16 in + 8 out,
+// dedup + fold 8 in.
+// ============================================================================
+constexpr u32 XF_SPAN_MAX = FOLD_MAXWIN * FOLD_WIN;  // minutes of the dense leaf arrays (k_cl_leaves)
+constexpr int XF_MIN_KB = 6;                         // >= 64 buckets
+constexpr u32 XF_WMAX = XF_SPAN_MAX / (1u << XF_MIN_KB) + 2;  // minutes one bucket can touch (its LDS histogram)
+
+// A message's place on the minute axis is K = d + hash / 2^32 (d = minute -
+// mlo), and bucket b covers K in [b, b + 1) * span / B: equal lengths of the
+// axis, so a batch spread over its minutes fills the buckets evenly whether
+// it spans many minutes per bucket or many buckets per minute.  Every copy
+// of a timestamp has one K.  floor(K * B) = d << kb | hash >> (32 - kb) is an
+// exact integer below 2^28, divided by span with a multiply-high.
+struct XfGeom {
+  u32 mlo, span, magic;  // minutes [mlo, mlo + span); magic = ceil(2^32 / span) (span > 1)
+  int kb, mb, xb, cb;    // bucket bits, minute-offset bits, tc bits, cell bits of a pair
+  u32 W;                 // minutes a bucket can touch
+  bool ok;
+};
+__device__ __forceinline__ XfGeom xf_geom(const Info* info, int kb, int cbits) {
+  XfGeom g;
+  g.mlo = info->minute_min;
+  const u32 mhi = info->minute_max;
+  g.ok = g.mlo <= mhi;
+  g.span = g.ok ? mhi - g.mlo + 1u : 1u;
+  g.ok = g.ok && g.span <= XF_SPAN_MAX && base3_len(g.mlo) == base3_len(mhi);
+  if (!g.ok) g.span = 1;
+  g.kb = kb;
+  g.magic = g.span > 1 ? (u32)((0x100000000ull + g.span - 1) / g.span) : 0u;
+  g.W = ((g.span + (1u << kb) - 1) >> kb) + 1u;
+  g.mb = 32 - __builtin_clz(g.W - 1);  // W >= 2
+  g.cb = cbits;
+  g.xb = 32 - g.mb - cbits;
+  return g;
+}
+__device__ __forceinline__ u32 xf_first_minute(const XfGeom& g, u32 b) { return (b * g.span) >> g.kb; }
+
+// (d = minute - mlo, hash, tc, cell) -> bucket and pair (hash32 | minute
+// offset in the bucket | mixed tc bits | cell)
+__device__ __forceinline__ u64 xf_pair(const XfGeom& g, u32 d, u32 h, u64 tc, u32 c, u32* bucket) {
+  const u32 N = (d << g.kb) | (g.kb ? h >> (32 - g.kb) : 0u);
+  u32 b = N;
+  if (g.span > 1) {
+    b = __umulhi(N, g.magic);  // floor(N / span) or one above
+    if (b * g.span > N) --b;
+  }
+  *bucket = b;
+  const u32 moff = d - xf_first_minute(g, b);
+  const u32 x = ((u32)tc ^ (u32)(tc >> 32)) * 0x9E3779B1u;  // every tc bit mixed into the top bits
+  const u32 lo = (moff << (32 - g.mb)) | ((x >> (32 - g.xb)) << g.cb) | c;
+  return ((u64)h << 32) | lo;
+}
+
+__device__ __forceinline__ u32 minute_of_tc(u64 tc) { return (u32)((tc >> 16) / 60000ull); }
+
+__global__ __launch_bounds__(XP_THREADS) void k_xf_scatter(const u32* __restrict__ hash, const u64* __restrict__ tcs,
+                                                          const u32* __restrict__ cell, size_t n, int kb, int cbits,
+                                                          u32 cap, u32* __restrict__ cursor, u64* __restrict__ out,
+                                                          u32* __restrict__ dx, u32* __restrict__ dc,
+                                                          Info* __restrict__ info) {
+  __shared__ u64 stage[XP_TILE];
+  __shared__ u32 cnt[1u << XP_MAX_KB];  // per bucket: count, then local offset
+  __shared__ u32 gb[1u << XP_MAX_KB];   // per bucket: this tile's base inside the bucket
+  __shared__ u32 scan_tmp[XP_THREADS / 64 + 1];
+  const XfGeom g = xf_geom(info, kb, cbits);
+  if (!g.ok) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&info->xf_redo, 1u);
+    return;
+  }
+  // the fold's dense minute arrays (the dedup kernel adds into them after this one)
+  for (u32 k = blockIdx.x * XP_THREADS + threadIdx.x; k < g.span; k += gridDim.x * XP_THREADS) {
+    dx[k] = 0;
+    dc[k] = 0;
+  }
+  const u32 B = 1u << kb;
+  for (u32 b = threadIdx.x; b < B; b += XP_THREADS) cnt[b] = 0;
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * XP_TILE;
+  u64 v[XP_ITEMS];
+  u32 bk[XP_ITEMS], r[XP_ITEMS];
+#pragma unroll
+  for (int k = 0; k < XP_ITEMS; ++k) {
+    const size_t i = base + (size_t)k * XP_THREADS + threadIdx.x;
+    const u64 tc = i < n ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
+    const u32 h = i < n ? __builtin_nontemporal_load(hash + i) : 0u;
+    const u32 c = i < n ? __builtin_nontemporal_load(cell + i) : 0u;
+    bk[k] = B;  // none (an invalid row: the batch is rejected anyway)
+    v[k] = 0;
+    if (tc != TP_INVALID) {
+      const u32 d = minute_of_tc(tc) - g.mlo;
+      v[k] = xf_pair(g, d, h, tc, c, &bk[k]);
+    }
+    r[k] = bk[k] < B ? atomicAdd(&cnt[bk[k]], 1u) : 0u;
+  }
+  __syncthreads();
+  const u32 per = (B + XP_THREADS - 1) / XP_THREADS;
+  u32 loc[(1u << XP_MAX_KB) / XP_THREADS];
+  u32 sum = 0;
+  for (u32 k = 0; k < per; ++k) {
+    const u32 b = threadIdx.x * per + k;
+    loc[k] = b < B ? cnt[b] : 0u;
+    sum += loc[k];
+  }
+  u32 tot;
+  const u32 incl = block_inclusive_scan<u32>(sum, scan_tmp, OpAdd<u32>(), &tot);
+  u32 run = incl - sum;
+  bool full = false;
+  for (u32 k = 0; k < per; ++k) {
+    const u32 b = threadIdx.x * per + k;
+    if (b < B) {
+      const u32 c = loc[k];
+      cnt[b] = run;
+      u32 gg = 0;
+      if (c) {
+        gg = atomicAdd(&cursor[b], c);
+        full |= gg + c > cap;
+      }
+      gb[b] = gg;
+      run += c;
+    }
+  }
+  if (__ballot(full) && (threadIdx.x & 63) == 0) atomic_or_if(&info->xf_redo, 1u);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < XP_ITEMS; ++k)
+    if (bk[k] < B) stage[cnt[bk[k]] + r[k]] = v[k];
+  __syncthreads();
+  // write-back in bucket order: the bucket of staged slot t is the last one
+  // whose local offset is <= t (a binary search over the B offsets in LDS)
+  for (u32 t = threadIdx.x; t < tot; t += XP_THREADS) {
+    u32 lo = 0, hi = B - 1;
+    while (lo < hi) {
+      const u32 mid = (lo + hi + 1) >> 1;
+      if (cnt[mid] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const u32 slot = gb[lo] + (t - cnt[lo]);
+    if (slot < cap) out[(size_t)lo * cap + slot] = stage[t];
+  }
+}
+
+// One bucket per workgroup: the PK check on fingerprints (LDS set of u32
+// slots = hash tag:17 | (local index + 1):15; a tag match re-reads the other
+// pair, L2-hot) and the fold of the bucket's minutes in LDS, flushed with one
+// global XOR / add per minute of the bucket.
+__device__ __forceinline__ bool xf_insert(u32* tab, const u64* bp, u64 p, u32 k, u32& pos, u32 budget, u32 cmask,
+                                          Info* info) {
+  const u32 h = (u32)(p >> 32);
+  const u32 mine = ((h >> 15) << 15) | (k + 1);
+  for (u32 probe = 0; probe < budget; ++probe) {
+    const u32 prev = atomicCAS(&tab[pos], 0u, mine);
+    if (prev == 0) return true;  // inserted
+    if ((prev >> 15) == (h >> 15)) {
+      const u64 q = bp[(prev & 0x7fffu) - 1];
+      if ((q | cmask) == (p | cmask)) {  // equal fingerprints: a copy of one timestamp (or a near-impossible twin)
+        if (((u32)q & cmask) != ((u32)p & cmask)) atomic_or_if(&info->xf_redo, 1u);
+        return true;
+      }
+    }
+    pos = (pos + 1) & (XP_SLOTS - 1);
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(XP_THREADS) void k_xf_dedup(const u64* __restrict__ pairs, const u32* __restrict__ cursor,
+                                                        u32 cap, int kb, int cbits, u32* __restrict__ dx,
+                                                        u32* __restrict__ dc, Info* __restrict__ info) {
+  __shared__ u32 tab[XP_SLOTS];  // 0 = empty
+  __shared__ u32 q[XQ_CAP];      // queued pairs: next slot:15 | local index:15
+  __shared__ u32 hx[XF_WMAX], hc[XF_WMAX];
+  __shared__ u32 qn;
+  const u32 b = blockIdx.x;
+  const u32 cnt = min(cursor[b], cap);
+  if (cnt == 0) return;
+  const XfGeom g = xf_geom(info, kb, cbits);
+  if (!g.ok) return;
+  const u32 cmask = (1u << cbits) - 1u;
+  const u64* bp = pairs + (size_t)b * cap;
+  u64 it[XD_ITEMS];
+#pragma unroll
+  for (int r = 0; r < XD_ITEMS; ++r) {
+    const u32 k = r * XP_THREADS + threadIdx.x;
+    it[r] = k < cnt ? bp[k] : 0ull;
+  }
+  for (u32 s = threadIdx.x; s < XP_SLOTS; s += XP_THREADS) tab[s] = 0;
+  for (u32 s = threadIdx.x; s < g.W; s += XP_THREADS) {
+    hx[s] = 0;
+    hc[s] = 0;
+  }
+  if (threadIdx.x == 0) qn = 0;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < XD_ITEMS; ++r) {
+    const u32 k = r * XP_THREADS + threadIdx.x;
+    if (k >= cnt) break;
+    const u64 p = it[r];
+    const u32 moff = (u32)p >> (32 - g.mb);
+    atomicXor(&hx[moff], (u32)(p >> 32));
+    atomicAdd(&hc[moff], 1u);
+    if (cnt < 2) continue;
+    u32 pos = ((u32)(p >> 32) * 2654435761u) >> 17;  // 15 bits
+    if (!xf_insert(tab, bp, p, k, pos, XP_INLINE_PROBES, cmask, info)) {
+      const u32 at = atomicAdd(&qn, 1u);
+      if (at < XQ_CAP) q[at] = (pos << 15) | k;
+      else xf_insert(tab, bp, p, k, pos, XP_SLOTS, cmask, info);  // queue full: finish here
+    }
+  }
+  __syncthreads();
+  const u32 m = min(qn, XQ_CAP);
+  for (u32 t = threadIdx.x; t < m; t += XP_THREADS) {
+    const u32 e = q[t], k = e & 0x7fffu;
+    u32 pos = e >> 15;
+    xf_insert(tab, bp, bp[k], k, pos, XP_SLOTS, cmask, info);
+  }
+  // the bucket's minutes (a minute split over buckets gets one XOR / add from each)
+  const u32 m0 = xf_first_minute(g, b);
+  for (u32 s = threadIdx.x; s < g.W; s += XP_THREADS) {
+    const u32 c = hc[s];
+    if (!c) continue;
+    const u32 d = m0 + s;
+    atomicXor(&dx[d], hx[s]);
+    atomicAdd(&dc[d], c);
+  }
+}
+
+// The walk's exact redeliveries of a cell's max: XORed out of the fold again.
+__global__ void k_xf_fix(const u32* __restrict__ noop, const u32* __restrict__ hash, const u64* __restrict__ tcs,
+                         int kb, int cbits, u32* __restrict__ dx, u32* __restrict__ dc, Info* __restrict__ info) {
+  const u32 m = info->noop_n;
+  if (m == 0 || info->xf_redo) return;
+  const u32 mlo = info->minute_min;
+  for (u32 t = blockIdx.x * blockDim.x + threadIdx.x; t < m; t += gridDim.x * blockDim.x) {
+    const u32 r = noop[t];
+    const u32 d = minute_of_tc(tcs[r]) - mlo;
+    atomicXor(&dx[d], hash[r]);
+    atomicSub(&dc[d], 1u);
+  }
+}
+
+// Per minute: presence (count > 0) and the XOR; per block of FR_THREADS
+// minutes the present count and XOR (k_cl_leaves' offsets and carries).
+__global__ __launch_bounds__(FR_THREADS) void k_xf_blocks(u32* __restrict__ dx, const u32* __restrict__ dc,
+                                                         const Info* __restrict__ info, u32* __restrict__ dp,
+                                                         u32* __restrict__ bcnt, u32* __restrict__ bxor) {
+  __shared__ u32 tmp[FR_THREADS / 64 + 1];
+  const u32 b = blockIdx.x * FR_THREADS + threadIdx.x;  // grid = FR_BLOCKS
+  const u32 mlo = info->minute_min, mhi = info->minute_max;
+  const bool usable = mlo <= mhi && !info->xf_redo && mhi - mlo < XF_SPAN_MAX;
+  u32 x = 0, p = 0;
+  if (usable && b <= mhi - mlo) {
+    p = dc[b] != 0 ? 1u : 0u;
+    x = p ? dx[b] : 0u;
+  }
+  dx[b] = x;
+  dp[b] = p;
+  u32 tot, xtot;
+  block_inclusive_scan<u32>(p, tmp, OpAdd<u32>(), &tot);
+  block_inclusive_scan<u32>(x, tmp, OpXor<u32>(), &xtot);
+  if (threadIdx.x == 0) {
+    bcnt[blockIdx.x] = tot;
+    bxor[blockIdx.x] = xtot;
   }
 }
 
@@ -1554,7 +1842,7 @@ struct XpGeom {
 };
 static XpGeom xp_geom(size_t n) {
   XpGeom x;
-  x.kb = 0;
+  x.kb = XF_MIN_KB;  // (the fused check + fold of the tc path needs >= 64 minute buckets)
   while (x.kb < XP_MAX_KB && (n >> x.kb) > XP_AVG) ++x.kb;
   const size_t avg = (n >> x.kb) + 1;
   x.cap = (u32)std::min<size_t>(XP_MAX_FILL, avg + avg / 8 + 1024);
@@ -1573,6 +1861,7 @@ struct SideBufs {
   u32* xcur;
   u64* xpairs;
   u32 *px, *pp, *dx, *dp, *bcnt, *bxor;
+  u32 *dc, *noop;  // tc path: per-minute row counts of the fused fold, the walk's exact redeliveries
 };
 static size_t side_bufs(void* base, size_t n, SideBufs* v) {
   const XpGeom x = xp_geom(n);
@@ -1581,9 +1870,10 @@ static size_t side_bufs(void* base, size_t n, SideBufs* v) {
   const size_t sz[] = {up(sizeof(Info)), up(4 * n), up(4 * n), up(4ull << x.kb), up((8ull * x.cap) << x.kb),
                        up((size_t)4 * FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN),
                        up((size_t)4 * FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32)), up(4 * B), up(4 * B),
-                       up(4 * FR_BLOCKS), up(4 * FR_BLOCKS)};
-  size_t off[11], tot = 0;
-  for (int k = 0; k < 11; ++k) {
+                       up(4 * FR_BLOCKS), up(4 * FR_BLOCKS), up(4 * B), up(4 * n)};
+  constexpr int NB = sizeof(sz) / sizeof(sz[0]);
+  size_t off[NB], tot = 0;
+  for (int k = 0; k < NB; ++k) {
     off[k] = tot;
     tot += sz[k];
   }
@@ -1600,6 +1890,8 @@ static size_t side_bufs(void* base, size_t n, SideBufs* v) {
     v->dp = reinterpret_cast<u32*>(p + off[8]);
     v->bcnt = reinterpret_cast<u32*>(p + off[9]);
     v->bxor = reinterpret_cast<u32*>(p + off[10]);
+    v->dc = reinterpret_cast<u32*>(p + off[11]);
+    v->noop = reinterpret_cast<u32*>(p + off[12]);
   }
   return tot;
 }
@@ -1657,10 +1949,10 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     const size_t lds = (size_t)C * 8 + (size_t)((C + 31) / 32) * 4;
     if (s48)
       hipLaunchKernelGGL(k_tp_pack<true>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, minute, agg, arow, info, xcur, 1u << xp_geom(n).kb);
+                         cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb);
     else
       hipLaunchKernelGGL(k_tp_pack<false>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, minute, agg, arow, info, xcur, 1u << xp_geom(n).kb);
+                         cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb);
   } else {
     key = S.alloc<uint4>(n);
     rl = S.alloc<u32>(n);
@@ -1718,6 +2010,15 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       if (t) tree_destroy(ctx, t);
     }
   } guard{ctx, spec};
+  auto leaves = [&](hipStream_t fs) {
+    evm::ProfScope ps_(ctx, "k_cl_leaves", fs);
+    if (spec)  // one owner, empty: the leaf kernel writes the tree itself
+      hipLaunchKernelGGL(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), 0, fs, dx, dp, bcnt, bxor, info, spec->ck,
+                         spec->xr, spec->pfx, spec->off);
+    else
+      hipLaunchKernelGGL(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), 0, fs, dx, dp, bcnt, bxor, info, lck, lxr,
+                         (int32_t*)nullptr, (u64*)nullptr);
+  };
   auto fold = [&](hipStream_t fs) {
     {
       evm::ProfScope ps_(ctx, "k_cl_fold_hist", fs);
@@ -1728,23 +2029,28 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       evm::ProfScope ps_(ctx, "k_cl_fold_reduce", fs);
       hipLaunchKernelGGL(k_cl_fold_reduce, dim3(FR_BLOCKS), dim3(FR_THREADS), 0, fs, px, pp, info, dx, dp, bcnt, bxor);
     }
-    evm::ProfScope ps_(ctx, "k_cl_leaves", fs);
-    if (spec)  // one owner, empty: the leaf kernel writes the tree itself
-      hipLaunchKernelGGL(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), 0, fs, dx, dp, bcnt, bxor, info, spec->ck,
-                         spec->xr, spec->pfx, spec->off);
-    else
-      hipLaunchKernelGGL(k_cl_leaves, dim3(FR_BLOCKS), dim3(FR_THREADS), 0, fs, dx, dp, bcnt, bxor, info, lck, lxr,
-                         (int32_t*)nullptr, (u64*)nullptr);
+    leaves(fs);
   };
   SideFork side(ctx);
   {
     const hipStream_t xs = side.stream();
-    if (!TC) HIPR(hipMemsetAsync(xcur, 0, sizeof(u32) << kb, xs));  // (the tc path's K1 cleared them)
-    {
-      evm::ProfScope ps_(ctx, "k_xp_scatter", xs);
-      hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), 0, xs, hash, n, kb, cap, xcur, xpairs, info);
-    }
-    {
+    if (TC) {
+      // the fused cross-cell check + Merkle fold (minute buckets; k_xf_fix
+      // after the walk XORs its exact redeliveries out again)
+      {
+        evm::ProfScope ps_(ctx, "k_xf_scatter", xs);
+        hipLaunchKernelGGL(k_xf_scatter, dim3(xt), dim3(XP_THREADS), 0, xs, hash, (const u64*)tcs, cell, n, kb, cbits,
+                           cap, xcur, xpairs, sb.dx, sb.dc, info);
+      }
+      evm::ProfScope ps_(ctx, "k_xf_dedup", xs);
+      hipLaunchKernelGGL(k_xf_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, (const u64*)xpairs, (const u32*)xcur,
+                         cap, kb, cbits, sb.dx, sb.dc, info);
+    } else {
+      HIPR(hipMemsetAsync(xcur, 0, sizeof(u32) << kb, xs));  // (the tc path's K1 clears them)
+      {
+        evm::ProfScope ps_(ctx, "k_xp_scatter", xs);
+        hipLaunchKernelGGL(k_xp_scatter, dim3(xt), dim3(XP_THREADS), 0, xs, hash, n, kb, cap, xcur, xpairs, info);
+      }
       evm::ProfScope ps_(ctx, "k_xp_dedup", xs);
       hipLaunchKernelGGL(k_xp_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, xpairs, xcur, cap, n,
                          (const uint8_t*)ts, stride, cell, info);
@@ -1757,7 +2063,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
             winner);
     // TP3: flags, a workgroup per range
     KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14 + (size_t)C * 4,
-                (const u64*)tcs, cell, n, C, range, (const u64*)agg, (const u32*)arow, N, flags);
+                (const u64*)tcs, cell, n, C, range, (const u64*)agg, (const u32*)arow, N, flags, sb.noop, info);
     // the Merkle fold reads the walk's flags (an exact redelivery of a cell's
     // max is not XORed): on the second stream after the walk, beside the
     // next batch's K1 when batches are pipelined
@@ -1766,7 +2072,17 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       HIPR(hipEventRecord(ctx->ev_fork, ctx->stream));
       HIPR(hipStreamWaitEvent(fs, ctx->ev_fork, 0));
     }
-    fold(fs);
+    {
+      evm::ProfScope ps_(ctx, "k_xf_fix", fs);
+      hipLaunchKernelGGL(k_xf_fix, dim3(64), dim3(256), 0, fs, (const u32*)sb.noop, (const u32*)hash,
+                         (const u64*)tcs, kb, cbits, sb.dx, sb.dc, info);
+    }
+    {
+      evm::ProfScope ps_(ctx, "k_xf_blocks", fs);
+      hipLaunchKernelGGL(k_xf_blocks, dim3(FR_BLOCKS), dim3(FR_THREADS), 0, fs, sb.dx, (const u32*)sb.dc, info, sb.dp,
+                         sb.bcnt, sb.bxor);
+    }
+    leaves(fs);
   } else {
     // pass 1: per range and cell, the max timestamp and its first index
     KLAUNCH_LDS(k_cl_scan1, dim3(G), dim3(WK_THREADS), (size_t)C * 24, key, rl, cell, n, C, cbits, range, a_tc, a_rh, a_rl,
@@ -1817,7 +2133,9 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     return EVM_ENONCANON;
   }
   if (hi.bad_aux) return EVM_EINVAL;
-  if (TC && hi.ties) return TP_REDO;  // a tie: the node ranks decide -- the exact walk path redoes the batch
+  // an overflowed tie list, or the fused check + fold could not finish (a
+  // possible collision, a full bucket, a wide minute range): the exact walk path redoes the batch
+  if (TC && (hi.ties || hi.xf_redo)) return TP_REDO;
   if (!hi.collision && hi.xc_oversize) {
     // a hash bucket overflowed LDS (heavy skew): exact check on the global epoch-tagged set
     const int lg = std::max(ceil_log2(n + n / 2 + 1), 10);
@@ -2599,8 +2917,9 @@ int evm_apply_wait(evm_ctx* ctx, evm_pending* p, evm_tree** tree_out) {
   } else {
     st = hip_ok(hipEventSynchronize(p->ev));
     Info hi = *p->hinfo;
+    const bool exact = hi.ties || hi.xf_redo;  // (the tc path's redo: the exact walk path)
     const bool redo = !st && !hi.bad && !hi.bad_aux &&
-                      (hi.ties || (!hi.collision && (hi.xc_oversize || hi.fold_overflow)));
+                      (exact || (!hi.collision && (hi.xc_oversize || hi.fold_overflow)));
     if (st) {
     } else if (hi.bad) {
       KLAUNCH(k_keep_bad, dim3(grid_for(p->n, 256)), dim3(256), p->flags, p->n);  // nothing applied: the culprits
@@ -2609,10 +2928,10 @@ int evm_apply_wait(evm_ctx* ctx, evm_pending* p, evm_tree** tree_out) {
       st = EVM_EINVAL;
     } else if (redo) {
       // a tie, an oversized hash bucket or a wide minute range: the synchronous paths redo the batch
-      if (hi.ties) ++ctx->stats.tc_redos;
+      if (exact) ++ctx->stats.tc_redos;
       st = apply_entry(ctx, p->tree_in, p->ts, p->stride, p->n, p->cell, p->n_cells, p->cell_owner, p->prior_ts,
                        p->prior_stride, p->prior_present, p->stored_ts, p->stored_stride, p->n_stored, p->stored_cell,
-                       p->flags, p->winner, tree_out, hi.ties ? 1 : ctx->client_path, nullptr);
+                       p->flags, p->winner, tree_out, exact ? 1 : ctx->client_path, nullptr);
     } else if (hi.collision) {
       st = EVM_ECOLLISION;
     } else if (p->spec) {

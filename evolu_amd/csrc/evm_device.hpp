@@ -221,19 +221,20 @@ struct Parsed {
 __host__ __device__ __forceinline__ u32 mul24(u32 a, u32 b) { return a * b; }  // a, b < 2^24: v_mul_u32_u24
 
 __host__ __device__ __forceinline__ Parsed parse_ts46(const u32 (&w)[12]) {
-  // byte classes: separators by template, digits / hex by SWAR ranges
-  const u32 hi = (w[0] | w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7] | w[8] | w[9] | w[10] | (w[11] & 0xffffu)) &
-                 0x80808080u;
-  bool ok = hi == 0;
-  ok &= (w[1] & 0xff0000ffu) == 0x2d00002du && (w[2] & 0x00ff0000u) == 0x00540000u &&
-        (w[3] & 0x0000ff00u) == 0x00003a00u && (w[4] & 0xff0000ffu) == 0x2e00003au &&
-        (w[5] & 0xff000000u) == 0x5a000000u && (w[6] & 0xffu) == 0x2du && (w[7] & 0xff00u) == 0x2d00u;
-  ok &= swar_digit(w[0]) == 0x80808080u && (swar_digit(w[1]) & 0x00808000u) == 0x00808000u &&
-        (swar_digit(w[2]) & 0x80008080u) == 0x80008080u && (swar_digit(w[3]) & 0x80800080u) == 0x80800080u &&
-        (swar_digit(w[4]) & 0x00808000u) == 0x00808000u && (swar_digit(w[5]) & 0x00808080u) == 0x00808080u;
+  // byte classes: separators by template, digits / hex by SWAR ranges.  Every
+  // failed check sets bits of `err` (no short-circuit `&&`: on the device a
+  // chain of them compiles to one exec-mask branch per test)
+  u32 err = (w[0] | w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7] | w[8] | w[9] | w[10] | (w[11] & 0xffffu)) &
+            0x80808080u;
+  err |= ((w[1] & 0xff0000ffu) ^ 0x2d00002du) | ((w[2] & 0x00ff0000u) ^ 0x00540000u) |
+         ((w[3] & 0x0000ff00u) ^ 0x00003a00u) | ((w[4] & 0xff0000ffu) ^ 0x2e00003au) |
+         ((w[5] & 0xff000000u) ^ 0x5a000000u) | ((w[6] & 0xffu) ^ 0x2du) | ((w[7] & 0xff00u) ^ 0x2d00u);
+  // (swar_digit sets only 0x80 bits: a required digit missing leaves its bit in ~d & m)
+  err |= (~swar_digit(w[0]) & 0x80808080u) | (~swar_digit(w[1]) & 0x00808000u) | (~swar_digit(w[2]) & 0x80008080u) |
+         (~swar_digit(w[3]) & 0x80800080u) | (~swar_digit(w[4]) & 0x00808000u) | (~swar_digit(w[5]) & 0x00808080u);
   // counter: exactly 4 upper-case hex digits (canonical toString(16).toUpperCase())
   const u32 cw = (w[6] >> 8) | (w[7] << 24);
-  ok &= (swar_digit(cw) | swar_upper(cw)) == 0x80808080u;
+  err |= ~(swar_digit(cw) | swar_upper(cw)) & 0x80808080u;
   // node: 16 hex digits, either case (types.ts:42 /^[0-9a-f]{16}$/i)
   u32 nw[4];
 #pragma unroll
@@ -243,11 +244,12 @@ __host__ __device__ __forceinline__ Parsed parse_ts46(const u32 (&w)[12]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const u32 up = swar_upper(nw[k]);
-    ok &= (swar_digit(nw[k]) | up | swar_lower(nw[k])) == 0x80808080u;
+    err |= ~(swar_digit(nw[k]) | up | swar_lower(nw[k])) & 0x80808080u;
     mask |= swar_bits4(up) << (4 * k);
     node = (node << 16) | swar_hex16(nw[k]);
     if (k < 3) rh = (rh << 20) | swar_rank20(nw[k]);
   }
+  bool ok = err == 0;
   const u32 counter = swar_hex16(cw);
   // decimal fields (digits already checked; garbage values only when !ok)
   const u32 d0 = w[0] - 0x30303030u;
@@ -259,40 +261,29 @@ __host__ __device__ __forceinline__ Parsed parse_ts46(const u32 (&w)[12]) {
   const u32 sss = mul24(mul24(w[5] & 0xffu, 10u) + ((w[5] >> 8) & 0xffu), 10u) + ((w[5] >> 16) & 0xffu) - 5328u;
   // calendar: leap year and month length without division
   const u32 cent = mul24(year, 5243u) >> 19;  // year / 100 for year < 43699
-  const bool leap = (year & 3u) == 0 && (year != mul24(cent, 100u) || (cent & 3u) == 0);
+  const bool leap = ((year & 3u) == 0) & ((year != mul24(cent, 100u)) | ((cent & 3u) == 0));
   constexpr u32 MLEN = (3u << 2) | (0u << 4) | (3u << 6) | (2u << 8) | (3u << 10) | (2u << 12) | (3u << 14) |
                        (3u << 16) | (2u << 18) | (3u << 20) | (2u << 22) | (3u << 24);  // month length - 28, by 2*mon
   const bool mon_ok = mon - 1u < 12u;
-  const u32 dim = 28u + ((MLEN >> (2u * (mon & 15u))) & 3u) + ((mon == 2u && leap) ? 1u : 0u);
-  ok &= mon_ok && day - 1u < dim && hh <= 23u && mi <= 59u && ss <= 59u;
-  u32 meta = mask;
-  u32 minute = 0;
-  u64 millis = 0;
-  if (!ok) {
-    meta |= EVM_META_NONCANON;
-  } else if (year < 1970u) {
-    meta |= EVM_META_RANGE;
-  } else {
-    // days since 1970-01-01 (March-based year): 365y + y/4 - y/100 + y/400 + doy - 719468
-    const u32 y = year - (mon <= 2u ? 1u : 0u);
-    const u32 yc = mul24(y, 5243u) >> 19;
-    const u32 mp = mon > 2u ? mon - 3u : mon + 9u;
-    const u32 doy = (mul24(mul24(mp, 153u) + 2u, 52429u) >> 18) + day - 1u;  // (153 mp + 2) / 5
-    const u32 days = mul24(y, 365u) + (y >> 2) - yc + (yc >> 2) + doy - 719468u;
-    const u32 m32 = mul24(days, 1440u) + mul24(hh, 60u) + mi;  // < 2^32 for year <= 9999
-    if (m32 >= 0x80000000u) {
-      meta |= EVM_META_RANGE;
-    } else {
-      meta |= EVM_META_VALID;
-      minute = m32;
-      millis = (u64)m32 * 60000ull + (mul24(ss, 1000u) + sss);
-    }
-  }
+  const u32 dim = 28u + ((MLEN >> (2u * (mon & 15u))) & 3u) + (((mon == 2u) & leap) ? 1u : 0u);
+  ok = ok & mon_ok & (day - 1u < dim) & (hh <= 23u) & (mi <= 59u) & (ss <= 59u);
+  // days since 1970-01-01 (March-based year): 365y + y/4 - y/100 + y/400 + doy - 719468;
+  // computed for every row (garbage when !ok, then unused) -- a select, not a branch
+  const u32 y = year - (mon <= 2u ? 1u : 0u);
+  const u32 yc = mul24(y, 5243u) >> 19;
+  const u32 mp = mon > 2u ? mon - 3u : mon + 9u;
+  const u32 doy = (mul24(mul24(mp & 15u, 153u) + 2u, 52429u) >> 18) + day - 1u;  // (153 mp + 2) / 5
+  const u32 days = mul24(y, 365u) + (y >> 2) - yc + (yc >> 2) + doy - 719468u;
+  const u32 m32 = mul24(days & 0xffffffu, 1440u) + mul24(hh & 0xffu, 60u) + mi;  // < 2^32 for year <= 9999
+  const bool valid = ok & (year >= 1970u) & (m32 < 0x80000000u);
+  u32 meta = mask | (valid ? (u32)EVM_META_VALID : !ok ? (u32)EVM_META_NONCANON : (u32)EVM_META_RANGE);
+  const u32 minute = valid ? m32 : 0u;
+  const u64 millis = valid ? (u64)m32 * 60000ull + (mul24(ss & 0xffu, 1000u) + sss) : 0ull;
   Parsed p;
   p.tc = (millis << 16) | counter;
   p.node = node;
   p.meta = meta;
-  p.hash = (meta & EVM_META_VALID) ? murmur3_46(w) : 0u;
+  p.hash = valid ? murmur3_46(w) : 0u;
   p.minute = minute;
   p.rh = rh;
   p.rl = swar_rank20(nw[3]);

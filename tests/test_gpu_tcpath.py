@@ -255,8 +255,8 @@ def test_tc_path_ragged_size_keeps_dense_fold(eng, n):
     f1, w1, t1, st = eng.apply_batch(eng.tree_new(1), ts, cell, 1000, raise_on_error=False)
     rep = eng.prof_report()
     eng.prof_enable(False)
-    if st == L.EVM_OK:  # (a tie would send the batch to the exact walk path)
-        assert "k_cl_fold_hist<true>" in rep or "k_cl_fold_hist" in rep, sorted(rep)
+    if st == L.EVM_OK:  # (the tc path's fused check + dense fold, not the sort-based fold)
+        assert "k_xf_dedup" in rep and "k_xf_blocks" in rep, sorted(rep)
         assert "k_cl_fold_ck" not in rep, sorted(rep)
     eng.set_option(L.OPT_CLIENT_PATH, 2)
     f2, w2, t2, _ = eng.apply_batch(eng.tree_new(1), ts, cell, 1000)
@@ -342,3 +342,102 @@ def test_tc_path_tie_list_overflow_redoes_exactly(eng):
     assert s1["tc_redos"] - s0["tc_redos"] == 1
     assert np.array_equal(flags.cpu().numpy(), f_w) and np.array_equal(winner.cpu().numpy(), w_w)
     assert tree.to_json(0) == js_w
+
+
+# ---------------------------------------------------------------------------
+# The fused cross-cell check + Merkle fold (k_xf_*): minute buckets, the fold
+# of every row with the walk's exact redeliveries XORed out again, and the
+# batches it hands to the exact walk path (xf_redo) -- each against the C
+# restatement of applyMessages.
+# ---------------------------------------------------------------------------
+def _c_vs_tc(eng, ts_np, cell_np, cells, redo):
+    from evolu_amd import _lib as L
+    from oracle import c_oracle as CO
+
+    st_w, f_w, w_w, js_w = CO.apply(ts_np, cell_np, cells)
+    eng.set_option(L.OPT_CLIENT_PATH, 3)
+    s0 = eng.stats()
+    flags, winner, tree, st = eng.apply_batch(eng.tree_new(1), eng.dev(ts_np), eng.dev(cell_np), cells,
+                                              raise_on_error=False)
+    s1 = eng.stats()
+    eng.set_option(L.OPT_CLIENT_PATH, 0)
+    assert (s1["tc_redos"] - s0["tc_redos"], s1["tc_batches"] - s0["tc_batches"]) == ((1, 0) if redo else (0, 1))
+    if st_w != 0:
+        return st, st_w
+    assert st == 0
+    assert np.array_equal(flags.cpu().numpy(), f_w) and np.array_equal(winner.cpu().numpy(), w_w)
+    assert tree.to_json(0) == js_w
+    return st, st_w
+
+
+@pytest.mark.parametrize("minutes", [1, 3, 700])
+def test_xf_narrow_minute_span(eng, minutes):
+    """A batch over fewer minutes than buckets: each minute is split over
+    buckets by hash bits, its XOR combined from every bucket; with exact and
+    stale redeliveries (the walk's no-op rows XORed out of the fold)."""
+    from evolu_amd import synth
+
+    rng = np.random.default_rng(minutes)
+    n = 1_000_000
+    ms = synth.BENCH_T0 + rng.integers(0, minutes * 60_000, n)
+    nodes = synth.random_nodes(rng, 16)
+    ts_np = synth.format_timestamps(ms, rng.integers(0, 4, n), nodes[rng.integers(0, 16, n)])
+    cell_np = rng.integers(0, 300, n).astype(np.uint32)
+    dup = rng.integers(0, n, n // 20)  # 5 % redeliveries
+    ts_np = np.concatenate([ts_np, ts_np[dup]])
+    cell_np = np.concatenate([cell_np, cell_np[dup]])
+    # (every copy of a timestamp in its first copy's cell: no cross-cell twins)
+    key = ts_np[:, :46].copy().view("S46").ravel()
+    _, first, inv = np.unique(key, return_index=True, return_inverse=True)
+    cell_np = cell_np[first][inv].astype(np.uint32)
+    _c_vs_tc(eng, ts_np, cell_np, 300, redo=False)
+
+
+def test_xf_collision_redoes_exactly(eng):
+    """One timestamp in two different cells (the global __message PK): the
+    fingerprints match across cells, the exact walk path confirms the collision."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    ts_np, cell_np = synth.config2(200_000, 100, seed_config=91)
+    ts_np = np.concatenate([ts_np, ts_np[1234:1235]])
+    cell_np = np.concatenate([cell_np, np.array([(cell_np[1234] + 1) % 100], dtype=np.uint32)])
+    st, st_w = _c_vs_tc(eng, ts_np, cell_np, 100, redo=True)
+    assert st == L.EVM_ECOLLISION and st_w != 0
+
+
+def test_xf_wide_span_redoes_exactly(eng):
+    """A batch over more than XF_SPAN_MAX (131,072) minutes: the exact walk path."""
+    from evolu_amd import synth
+
+    rng = np.random.default_rng(4)
+    n = 300_000
+    ms = synth.BENCH_T0 + rng.integers(0, 200 * 86_400_000, n)
+    ts_np = synth.format_timestamps(ms, np.zeros(n, dtype=np.int64), synth.random_nodes(rng, n))
+    _c_vs_tc(eng, ts_np, rng.integers(0, 64, n).astype(np.uint32), 64, redo=True)
+
+
+def test_xf_skewed_minute_overflows_to_exact(eng):
+    """Half the batch in one minute of a 30-day batch: that minute's bucket
+    overflows its capacity and the exact walk path answers."""
+    from evolu_amd import synth
+
+    rng = np.random.default_rng(6)
+    n = 2_000_000
+    ms = synth.BENCH_T0 + rng.integers(0, 30 * 86_400_000, n)
+    ms[: n // 2] = synth.BENCH_T0 + 5 * 86_400_000 + rng.integers(0, 60_000, n // 2)
+    ts_np = synth.format_timestamps(ms, np.zeros(n, dtype=np.int64), synth.random_nodes(rng, n))
+    _c_vs_tc(eng, ts_np, rng.integers(0, 1000, n).astype(np.uint32), 1000, redo=True)
+
+
+def test_xf_mixed_key_lengths_redo(eng):
+    """Minutes on both sides of 3^16 (2051-11-05): two base-3 key lengths, so
+    leaf order is not minute order -- the exact walk path's sort-based fold."""
+    from evolu_amd import synth
+
+    rng = np.random.default_rng(8)
+    n = 100_000
+    edge = 3 ** 16 * 60_000
+    ms = edge + rng.integers(-3_600_000, 3_600_000, n)
+    ts_np = synth.format_timestamps(ms, np.zeros(n, dtype=np.int64), synth.random_nodes(rng, 32)[rng.integers(0, 32, n)])
+    _c_vs_tc(eng, ts_np, rng.integers(0, 50, n).astype(np.uint32), 50, redo=True)
