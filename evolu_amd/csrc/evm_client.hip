@@ -1129,13 +1129,13 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
   __shared__ uint4 stage[TP_THREADS / 64][192];
   __shared__ u32 nmatch;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u32 bad = 0, aux_bad = 0, mn = 0xffffffffu, mx = 0;
   const size_t g = blockIdx.x;
   const size_t beg = g * range_len, end = min(n, beg + range_len);
   for (u32 c = threadIdx.x; c < C; c += TP_THREADS) cmax[c] = 0;
   for (u32 k = threadIdx.x; k < (C + 31) / 32; k += TP_THREADS) cfix[k] = 0;
   if (threadIdx.x == 0) nmatch = 0;
   __syncthreads();
-  u32 bad = 0, aux_bad = 0, mn = 0xffffffffu, mx = 0;
   for (size_t first = beg + 64 * wv; first < end; first += TP_THREADS) {  // wave-uniform
     uint4 a, b, c;
     clp_fetch<S48>(ts, stride, end, first, a, b, c);
@@ -1158,7 +1158,18 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
       w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
       w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
     }
+#if EVM_ABL_TP == 1  // (ablation builds only: no parse at all)
+    Parsed p{};
+    p.tc = (((u64)w[1] << 32) | w[0]) & 0x00007fffffffffffull;
+    p.hash = w[2];
+    p.minute = w[3] & 0xffffu;
+    p.meta = EVM_META_VALID;
+#else
     Parsed p = parse_ts46(w);  // (the node ranks it can compute are dead here)
+#endif
+#if EVM_ABL_TP == 2  // (ablation: no murmur3)
+    p.hash = w[5];
+#endif
     const bool valid = (p.meta & EVM_META_VALID) != 0;
     if (i < end) {
       const u32 ci = __builtin_nontemporal_load(cell + i);
@@ -1169,7 +1180,12 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
         const u64 ms = p.tc >> 16;
         const u32 ctr = (u32)p.tc & 0xffffu;
         bool mark = true;  // far
+#if EVM_ABL_TP == 3  // (ablation: no per-range LDS max)
+        mark = false;
+        if (false) {
+#else
         if (ms < TP_MS_FAST && ctr < 256u) {
+#endif
           const u64 key = (ms << 21) | ((u64)ctr << 13) | (u64)(TP_ROWS_MAX - 1u - (u32)(i - beg));
           mark = (atomicMax(&cmax[ci], key) >> 13) == (key >> 13);  // a second row at this tc (or tc 0)
         }
@@ -1178,19 +1194,9 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
       bad |= valid ? 0u : 1u;
       aux_bad |= ci < C ? 0u : 1u;
     }
-    if (S48 && first + 64 <= end && (first & 3) == 0) {
-      // hashes of the wave's 64 rows as 16-B-per-lane stores (16 lanes); the
-      // minute is not stored: the fused check + fold re-derives it from tc
-      u32* st32 = reinterpret_cast<u32*>(&stage[wv][0]);
-      st32[lane] = p.hash;
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (lane < 16) reinterpret_cast<uint4*>(hash + first)[lane] = stage[wv][lane];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    } else if (i < end) {
-      hash[i] = p.hash;
-    }
+    // (the wave's 64 hashes are one contiguous 256-B store; the minute is not
+    // stored: the fused check + fold re-derives it from tc)
+    if (i < end) hash[i] = p.hash;
     // (lanes past the range end parsed zero bytes: their minute must not
     // widen the bounds, or the dense fold of a batch whose size is not a
     // multiple of 64 overflows into the sort-based fold)
@@ -1198,7 +1204,6 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
     mn = min(mn, in ? p.minute : 0xffffffffu);
     mx = max(mx, in && p.minute != 0xffffffffu ? p.minute : 0u);
   }
-  if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
   __syncthreads();
   // the unmarked cells: tc and row straight from the key
   for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
@@ -1273,6 +1278,7 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
       }
     }
   }
+  if (__ballot(aux_bad) && lane == 0) atomicOr(&info->bad_aux, 1u);
   block_fold_bounds<u32, TP_THREADS>(mn, mx, bad, &info->minute_min, &info->minute_max, &info->bad);
 }
 
@@ -1590,48 +1596,60 @@ __device__ __forceinline__ u64 xf_pair(const XfGeom& g, u32 d, u32 h, u64 tc, u3
 
 __device__ __forceinline__ u32 minute_of_tc(u64 tc) { return (u32)((tc >> 16) / 60000ull); }
 
-__global__ __launch_bounds__(XP_THREADS) void k_xf_scatter(const u32* __restrict__ hash, const u64* __restrict__ tcs,
+// d = minute(tc) - mlo without a 64-bit division: rel = millis - mlo * 60000
+// fits 32 bits while the span is <= XF_SPAN32 minutes, and (rel >> 5) / 1875
+// is exact as a multiply-high below 2^27 (M = ceil(2^42 / 1875)).
+constexpr u32 XF_SPAN32 = 71582;  // floor(2^32 / 60000)
+__device__ __forceinline__ u32 xf_minute_off(u64 tc, u64 base_ms, u32 mlo, bool narrow) {
+  if (narrow) return __umulhi((u32)(((tc >> 16) - base_ms) >> 5), 2345624806u) >> 10;
+  return minute_of_tc(tc) - mlo;
+}
+
+// A tile of THREADS x ITEMS pairs is staged in LDS with its bucket ids and
+// written back bucket by bucket (EVM_XF_SCATTER picks the shape).
+template <int THREADS, int ITEMS>
+__global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ hash, const u64* __restrict__ tcs,
                                                           const u32* __restrict__ cell, size_t n, int kb, int cbits,
                                                           u32 cap, u32* __restrict__ cursor, u64* __restrict__ out,
                                                           u32* __restrict__ dx, u32* __restrict__ dc,
                                                           Info* __restrict__ info) {
-  __shared__ u64 stage[XP_TILE];
+  __shared__ u64 stage[(THREADS * ITEMS)];
+  __shared__ uint16_t sbk[(THREADS * ITEMS)];      // the bucket of each staged pair
   __shared__ u32 cnt[1u << XP_MAX_KB];  // per bucket: count, then local offset
   __shared__ u32 gb[1u << XP_MAX_KB];   // per bucket: this tile's base inside the bucket
-  __shared__ u32 scan_tmp[XP_THREADS / 64 + 1];
+  __shared__ u32 scan_tmp[THREADS / 64 + 1];
   const XfGeom g = xf_geom(info, kb, cbits);
   if (!g.ok) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&info->xf_redo, 1u);
     return;
   }
   // the fold's dense minute arrays (the dedup kernel adds into them after this one)
-  for (u32 k = blockIdx.x * XP_THREADS + threadIdx.x; k < g.span; k += gridDim.x * XP_THREADS) {
+  for (u32 k = blockIdx.x * THREADS + threadIdx.x; k < g.span; k += gridDim.x * THREADS) {
     dx[k] = 0;
     dc[k] = 0;
   }
   const u32 B = 1u << kb;
-  for (u32 b = threadIdx.x; b < B; b += XP_THREADS) cnt[b] = 0;
+  const bool narrow = g.span <= XF_SPAN32;
+  const u64 base_ms = (u64)g.mlo * 60000ull;
+  for (u32 b = threadIdx.x; b < B; b += THREADS) cnt[b] = 0;
   __syncthreads();
-  const size_t base = (size_t)blockIdx.x * XP_TILE;
-  u64 v[XP_ITEMS];
-  u32 bk[XP_ITEMS], r[XP_ITEMS];
+  const size_t base = (size_t)blockIdx.x * (THREADS * ITEMS);
+  u64 v[ITEMS];
+  u32 bk[ITEMS], r[ITEMS];
 #pragma unroll
-  for (int k = 0; k < XP_ITEMS; ++k) {
-    const size_t i = base + (size_t)k * XP_THREADS + threadIdx.x;
+  for (int k = 0; k < ITEMS; ++k) {
+    const size_t i = base + (size_t)k * THREADS + threadIdx.x;
     const u64 tc = i < n ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
     const u32 h = i < n ? __builtin_nontemporal_load(hash + i) : 0u;
     const u32 c = i < n ? __builtin_nontemporal_load(cell + i) : 0u;
     bk[k] = B;  // none (an invalid row: the batch is rejected anyway)
     v[k] = 0;
-    if (tc != TP_INVALID) {
-      const u32 d = minute_of_tc(tc) - g.mlo;
-      v[k] = xf_pair(g, d, h, tc, c, &bk[k]);
-    }
+    if (tc != TP_INVALID) v[k] = xf_pair(g, xf_minute_off(tc, base_ms, g.mlo, narrow), h, tc, c, &bk[k]);
     r[k] = bk[k] < B ? atomicAdd(&cnt[bk[k]], 1u) : 0u;
   }
   __syncthreads();
-  const u32 per = (B + XP_THREADS - 1) / XP_THREADS;
-  u32 loc[(1u << XP_MAX_KB) / XP_THREADS];
+  const u32 per = (B + THREADS - 1) / THREADS;
+  u32 loc[(1u << XP_MAX_KB) / THREADS];
   u32 sum = 0;
   for (u32 k = 0; k < per; ++k) {
     const u32 b = threadIdx.x * per + k;
@@ -1659,20 +1677,18 @@ __global__ __launch_bounds__(XP_THREADS) void k_xf_scatter(const u32* __restrict
   if (__ballot(full) && (threadIdx.x & 63) == 0) atomic_or_if(&info->xf_redo, 1u);
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < XP_ITEMS; ++k)
-    if (bk[k] < B) stage[cnt[bk[k]] + r[k]] = v[k];
-  __syncthreads();
-  // write-back in bucket order: the bucket of staged slot t is the last one
-  // whose local offset is <= t (a binary search over the B offsets in LDS)
-  for (u32 t = threadIdx.x; t < tot; t += XP_THREADS) {
-    u32 lo = 0, hi = B - 1;
-    while (lo < hi) {
-      const u32 mid = (lo + hi + 1) >> 1;
-      if (cnt[mid] <= t) lo = mid;
-      else hi = mid - 1;
+  for (int k = 0; k < ITEMS; ++k)
+    if (bk[k] < B) {
+      const u32 at = cnt[bk[k]] + r[k];
+      stage[at] = v[k];
+      sbk[at] = (uint16_t)bk[k];
     }
-    const u32 slot = gb[lo] + (t - cnt[lo]);
-    if (slot < cap) out[(size_t)lo * cap + slot] = stage[t];
+  __syncthreads();
+  // write-back in bucket order: consecutive lanes on consecutive slots of a bucket
+  for (u32 t = threadIdx.x; t < tot; t += THREADS) {
+    const u32 b = sbk[t];
+    const u32 slot = gb[b] + (t - cnt[b]);
+    if (slot < cap) out[(size_t)b * cap + slot] = stage[t];
   }
 }
 
@@ -1765,10 +1781,11 @@ __global__ void k_xf_fix(const u32* __restrict__ noop, const u32* __restrict__ h
                          int kb, int cbits, u32* __restrict__ dx, u32* __restrict__ dc, Info* __restrict__ info) {
   const u32 m = info->noop_n;
   if (m == 0 || info->xf_redo) return;
-  const u32 mlo = info->minute_min;
+  const u32 mlo = info->minute_min, span = info->minute_max - mlo + 1u;
   for (u32 t = blockIdx.x * blockDim.x + threadIdx.x; t < m; t += gridDim.x * blockDim.x) {
     const u32 r = noop[t];
     const u32 d = minute_of_tc(tcs[r]) - mlo;
+    if (d >= span) continue;  // (never for a valid row: its minute is inside TP1's bounds)
     atomicXor(&dx[d], hash[r]);
     atomicSub(&dc[d], 1u);
   }
@@ -1947,11 +1964,12 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     // TP1: parse + per (range, cell) max tc and its row, one workgroup per range
     evm::ProfScope ps_(ctx, "k_tp_pack");
     const size_t lds = (size_t)C * 8 + (size_t)((C + 31) / 32) * 4;
+    const dim3 g1((u32)G);
     if (s48)
-      hipLaunchKernelGGL(k_tp_pack<true>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
+      hipLaunchKernelGGL(k_tp_pack<true>, g1, dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
                          cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb);
     else
-      hipLaunchKernelGGL(k_tp_pack<false>, dim3(G), dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
+      hipLaunchKernelGGL(k_tp_pack<false>, g1, dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
                          cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb);
   } else {
     key = S.alloc<uint4>(n);
@@ -1978,6 +1996,9 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   const int kb = xg.kb;
   const u32 cap = xg.cap;
   const u32 xt = (u32)((n + XP_TILE - 1) / XP_TILE);
+  static const int xf_shape = getenv("EVM_XF_SCATTER") ? atoi(getenv("EVM_XF_SCATTER")) : 0;
+  const u32 xf_tile = xf_shape == 0 ? 1024 * 12 : xf_shape == 1 ? 512 * 12 : 512 * 8;
+  const u32 xft = (u32)((n + xf_tile - 1) / xf_tile);
 
   // it reads only the timestamps, cells and K1's hashes: a second stream runs
   // it beside the walks, forked right after K1 (joined before the status
@@ -2039,8 +2060,11 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       // after the walk XORs its exact redeliveries out again)
       {
         evm::ProfScope ps_(ctx, "k_xf_scatter", xs);
-        hipLaunchKernelGGL(k_xf_scatter, dim3(xt), dim3(XP_THREADS), 0, xs, hash, (const u64*)tcs, cell, n, kb, cbits,
-                           cap, xcur, xpairs, sb.dx, sb.dc, info);
+#define XF_SCATTER_ARGS hash, (const u64*)tcs, cell, n, kb, cbits, cap, xcur, xpairs, sb.dx, sb.dc, info
+        if (xf_shape == 0) hipLaunchKernelGGL((k_xf_scatter<1024, 12>), dim3(xft), dim3(1024), 0, xs, XF_SCATTER_ARGS);
+        else if (xf_shape == 1) hipLaunchKernelGGL((k_xf_scatter<512, 12>), dim3(xft), dim3(512), 0, xs, XF_SCATTER_ARGS);
+        else hipLaunchKernelGGL((k_xf_scatter<512, 8>), dim3(xft), dim3(512), 0, xs, XF_SCATTER_ARGS);
+#undef XF_SCATTER_ARGS
       }
       evm::ProfScope ps_(ctx, "k_xf_dedup", xs);
       hipLaunchKernelGGL(k_xf_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, (const u64*)xpairs, (const u32*)xcur,
