@@ -1285,10 +1285,14 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
 // TP2: per cell, the exclusive max over the G range maxima seeded with the
 // prior max, and the final max -> winner.  One workgroup per CT_CELLS cells:
 // each of its CT_GROUPS lane groups reduces a contiguous segment of ranges
-// (CT_CELLS consecutive cells = one 128-B read per range), one wave per cell
-// scans the segment maxima in LDS, and the groups write their segment's
-// running maxima (the second read of the tile hits L2).
-constexpr u32 CT_CELLS = 16, CT_GROUPS = 64, CT_THREADS = CT_CELLS * CT_GROUPS;
+// (CT_CELLS consecutive cells = one 64-B read per range), one wave per cell
+// scans the segment maxima in LDS (two per lane), and the groups write their
+// segment's running maxima.  A segment of <= CT_CACHE ranges (G <= 2,048:
+// the headline) is loaded once, every load in flight at once, and kept in
+// registers for the write-back; equal tc in two ranges (rare: the node ranks
+// decide) sends the lane to the exact loop, which re-reads memory.
+constexpr u32 CT_CELLS = 8, CT_GROUPS = 128, CT_THREADS = CT_CELLS * CT_GROUPS;
+constexpr int CT_BATCH = 8, CT_CACHE = 16;
 
 __global__ __launch_bounds__(CT_THREADS) void k_tp_carry(u32 C, size_t G, u64* __restrict__ agg,
                                                          u32* __restrict__ arow, NodeSrc N,
@@ -1299,15 +1303,34 @@ __global__ __launch_bounds__(CT_THREADS) void k_tp_carry(u32 C, size_t G, u64* _
   const u32 cl = threadIdx.x % CT_CELLS, grp = threadIdx.x / CT_CELLS;
   const u32 c = blockIdx.x * CT_CELLS + cl;
   const bool ok = c < C;
+  const u32 cc = ok ? c : C - 1;  // (loads stay in bounds; the lane writes nothing)
   const size_t per = (G + CT_GROUPS - 1) / CT_GROUPS;
   const size_t a = min(G, grp * per), e = min(G, a + per);
   // (a range without rows holds (0, ROW_NONE); a row of tc 0 ties with it and
-  // takes the rare path, which ranks NONE below every row)
-  // (CT_BATCH loads in flight per lane before any compare: the rare tie
-  // compare reads memory and would otherwise serialise the loads)
-  constexpr int CT_BATCH = 8;
+  // takes the exact loop, which ranks NONE below every row)
+  const bool cached = per <= CT_CACHE;
+  u64 tcache[CT_CACHE];
+  u32 rcache[CT_CACHE];
   TK m{0, ROW_NONE};
-  if (ok) {
+  bool tie = false;
+  if (cached) {
+#pragma unroll
+    for (int k = 0; k < CT_CACHE; ++k) {
+      const size_t g = a + k;
+      const size_t gi = min(g, G - 1) * C + cc;
+      const u64 t = agg[gi];
+      const u32 r = arow[gi];
+      tcache[k] = g < e ? t : 0ull;
+      rcache[k] = g < e ? r : ROW_NONE;
+    }
+#pragma unroll
+    for (int k = 0; k < CT_CACHE; ++k) {
+      if (tcache[k] > m.tc) m = TK{tcache[k], rcache[k]};
+      else if (tcache[k] == m.tc && rcache[k] != m.row) tie = true;
+    }
+  }
+  if (ok && (!cached || tie)) {
+    m = TK{0, ROW_NONE};
     for (size_t g0 = a; g0 < e; g0 += CT_BATCH) {
       u64 t[CT_BATCH];
       u32 r[CT_BATCH];
@@ -1329,11 +1352,13 @@ __global__ __launch_bounds__(CT_THREADS) void k_tp_carry(u32 C, size_t G, u64* _
   s_row[grp][cl] = m.row;
   __syncthreads();
   {
+    // one wave per cell; lane l holds segments 2l and 2l + 1
     const u32 w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const u32 cw = blockIdx.x * CT_CELLS + w;
-    static_assert(CT_GROUPS == 64 && CT_THREADS / 64 == CT_CELLS, "one wave per cell, one lane per group");
-    if (cw < C) {
-      TK v{s_tc[lane][w], s_row[lane][w]};
+    static_assert(CT_GROUPS == 128 && CT_THREADS / 64 >= CT_CELLS, "one wave per cell, two groups per lane");
+    if (w < CT_CELLS && cw < C) {
+      const TK v0{s_tc[2 * lane][w], s_row[2 * lane][w]}, v1{s_tc[2 * lane + 1][w], s_row[2 * lane + 1][w]};
+      TK v = tk_max(N, cw, v0, v1);
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const TK u = shfl_tk(v, (int)lane - d < 0 ? (int)lane : (int)lane - d);
@@ -1341,9 +1366,12 @@ __global__ __launch_bounds__(CT_THREADS) void k_tp_carry(u32 C, size_t G, u64* _
       }
       const TK seed = (prior_present && prior_present[cw]) ? TK{N.prior[cw].tc, ROW_PRIOR} : TK{0, ROW_NONE};
       const TK ex = shfl_tk(v, lane == 0 ? 0 : (int)lane - 1);
-      const TK x = lane == 0 ? seed : tk_max(N, cw, seed, ex);
-      s_tc[lane][w] = x.tc;
-      s_row[lane][w] = x.row;
+      const TK x0 = lane == 0 ? seed : tk_max(N, cw, seed, ex);  // before segment 2l
+      const TK x1 = tk_max(N, cw, x0, v0);                       // before segment 2l + 1
+      s_tc[2 * lane][w] = x0.tc;
+      s_row[2 * lane][w] = x0.row;
+      s_tc[2 * lane + 1][w] = x1.tc;
+      s_row[2 * lane + 1][w] = x1.row;
       if (lane == 63) {
         // the last upsert is the first occurrence of the final max (none if
         // the prior max or nothing holds it)
@@ -1355,6 +1383,33 @@ __global__ __launch_bounds__(CT_THREADS) void k_tp_carry(u32 C, size_t G, u64* _
   __syncthreads();
   if (!ok) return;
   TK run{s_tc[grp][cl], s_row[grp][cl]};
+  if (cached && !tie) {
+    // the running max by tc alone unless it meets an equal tc (then the
+    // exact loop, from memory: nothing is written before this check)
+    u64 rt = run.tc;
+    u32 rr = run.row;
+#pragma unroll
+    for (int k = 0; k < CT_CACHE; ++k) {
+      if (tcache[k] > rt) {
+        rt = tcache[k];
+        rr = rcache[k];
+      } else if (tcache[k] == rt && rcache[k] != rr) {
+        tie = true;
+      }
+    }
+    if (!tie) {
+#pragma unroll
+      for (int k = 0; k < CT_CACHE; ++k) {
+        const size_t g = a + k;
+        if (g < e) {
+          agg[g * C + c] = run.tc;
+          arow[g * C + c] = run.row;
+        }
+        if (tcache[k] > run.tc) run = TK{tcache[k], rcache[k]};
+      }
+      return;
+    }
+  }
   for (size_t g0 = a; g0 < e; g0 += CT_BATCH) {
     u64 t[CT_BATCH];
     u32 r[CT_BATCH];
