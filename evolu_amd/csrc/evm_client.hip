@@ -2475,7 +2475,7 @@ __global__ __launch_bounds__(256) void k_sm_lww(const evm_rec* __restrict__ rec,
           atomic_or_if(&info->fold_overflow, 1u);
         } else {
           atomicXor(&bins[d], r.hash);
-          atomicOr(&pres[d >> 5], 1u << (d & 31));
+          atomic_or_if(&pres[d >> 5], 1u << (d & 31));
         }
       }
     }
@@ -2486,9 +2486,90 @@ __global__ __launch_bounds__(256) void k_sm_lww(const evm_rec* __restrict__ rec,
   for (u32 k = threadIdx.x; k < (W + 31) / 32; k += blockDim.x) {
     const u32 m = lpres[k];
     if (!m) continue;
-    atomicOr(&pres[k], m);
+    atomic_or_if(&pres[k], m);
     for (u32 b = 0; b < 32; ++b)
       if ((m >> b) & 1u) atomicXor(&bins[32 * k + b], lbins[32 * k + b]);
+  }
+}
+
+// The long cells of up to 64 rows (every long cell of the config-1 todo app:
+// hot rows of a few dozen updates), one WAVE each, no barriers: lane l takes
+// the cell's row of batch rank l (ranks by 64 shuffled compares, placed
+// through a per-wave LDS slot array), the exclusive running max is a wave
+// prefix max of the keys seeded with the prior, and the XOR rows' hashes are
+// reduced per minute inside the wave -- one global XOR / OR per distinct
+// minute of the cell instead of one per row (a client batch spans a few
+// minutes: per-row global atomics on the same bins serialise).
+constexpr u32 SM_WAVE_MAX = 64;
+__device__ __forceinline__ Key shfl_key(const Key& k, int src) {
+  Key o;
+  o.tc = ((u64)(u32)__shfl((int)(u32)(k.tc >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)k.tc, src, 64);
+  o.node = ((u64)(u32)__shfl((int)(u32)(k.node >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)k.node, src, 64);
+  o.mask = (u32)__shfl((int)k.mask, src, 64);
+  return o;
+}
+__global__ __launch_bounds__(256) void k_sm_long_wave(const evm_rec* __restrict__ rec, const u32* __restrict__ off,
+                                                      const u32* __restrict__ grp, const u32* __restrict__ long_list,
+                                                      const u32* __restrict__ long_n, const evm_rec* __restrict__ prior,
+                                                      const uint8_t* __restrict__ prior_present,
+                                                      uint8_t* __restrict__ flags, int32_t* __restrict__ winner,
+                                                      u32* __restrict__ bins, u32* __restrict__ pres,
+                                                      Info* __restrict__ info) {
+  __shared__ u32 slot[4][SM_WAVE_MAX];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const u32 nl = *long_n;
+  const u32 mlo = info->minute_min;
+  for (u32 li = blockIdx.x * 4 + wv; li < nl; li += gridDim.x * 4) {  // wave-uniform
+    const u32 c = long_list[li];
+    const u32 a = off[c], k = off[c + 1] - a;
+    if (k > SM_WAVE_MAX) continue;  // (k_sm_long)
+    const bool in = (u32)lane < k;
+    const u32 i = in ? grp[a + lane] : 0xffffffffu;
+    u32 rank = 0;
+    for (u32 j = 0; j < k; ++j) rank += (u32)__shfl((int)i, (int)j, 64) < i ? 1u : 0u;
+    if (in) slot[wv][rank] = i;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const u32 row = in ? slot[wv][lane] : 0u;  // lane = batch rank
+    __builtin_amdgcn_wave_barrier();
+    evm_rec r{};
+    if (in) r = rec[row];
+    const Key ts = in ? key_of(r) : key_none();
+    Key v = ts;  // inclusive prefix max over the lanes (batch order)
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const Key o = shfl_key(v, lane >= d ? lane - d : lane);
+      if (lane >= d) v = key_max(o, v);
+    }
+    Key run = (prior_present && prior_present[c]) ? key_of(prior[c]) : key_none();
+    const Key ex = shfl_key(v, lane > 0 ? lane - 1 : 0);
+    if (lane > 0) run = key_max(run, ex);
+    const bool ups = in && key_cmp(run, ts) < 0;                             // applyMessages.ts:93
+    const bool xr = in && !((run.mask & KEY_PRESENT) && key_eq(run, ts));  // applyMessages.ts:105
+    if (in) flags[row] = (ups ? EVM_MSG_UPS : 0u) | (xr ? EVM_MSG_XOR : 0u);
+    const u64 ub = __ballot(ups);  // the last upsert in batch order wins
+    const u32 wrow = (u32)__shfl((int)row, ub ? 63 - __builtin_clzll(ub) : 0, 64);
+    if (lane == 0) winner[c] = ub ? (int32_t)wrow : -1;
+    // per distinct minute of the XOR rows: one reduction, one global update
+    const u32 d = xr ? r.minute - mlo : 0xffffffffu;
+    u64 left = __ballot(xr);
+    while (left) {
+      const int ld = __builtin_ctzll(left);
+      const u32 dm = (u32)__shfl((int)d, ld, 64);
+      const u64 mem = __ballot(xr && d == dm);
+      u32 h = ((mem >> lane) & 1ull) ? r.hash : 0u;
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) h ^= (u32)__shfl_xor((int)h, m, 64);
+      if (lane == ld) {
+        if (dm >= SM_BINS) {
+          atomic_or_if(&info->fold_overflow, 1u);
+        } else {
+          atomicXor(&bins[dm], h);
+          atomic_or_if(&pres[dm >> 5], 1u << (dm & 31));
+        }
+      }
+      left &= ~mem;
+    }
   }
 }
 
@@ -2516,6 +2597,7 @@ __global__ __launch_bounds__(SM_LONG_THREADS) void k_sm_long(const evm_rec* __re
   for (u32 li = blockIdx.x; li < nl; li += gridDim.x) {
     const u32 c = long_list[li];
     const u32 a = off[c], k = off[c + 1] - a;
+    if (k <= SM_WAVE_MAX) continue;  // (k_sm_long_wave; uniform over the workgroup)
     u32 P = 1;
     while (P < k) P <<= 1;
     for (u32 q = t; q < P; q += SM_LONG_THREADS) idx[q] = q < k ? grp[a + q] : 0xffffffffu;
@@ -2577,7 +2659,7 @@ __global__ __launch_bounds__(SM_LONG_THREADS) void k_sm_long(const evm_rec* __re
           atomic_or_if(&info->fold_overflow, 1u);
         } else {
           atomicXor(&bins[d], r.hash);
-          atomicOr(&pres[d >> 5], 1u << (d & 31));
+          atomic_or_if(&pres[d >> 5], 1u << (d & 31));
         }
       }
     }
@@ -2713,7 +2795,10 @@ static int apply_small(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tre
   KLAUNCH(k_sm_scatter, dim3(grid_for(n, 256, 1024)), dim3(256), (const evm_rec*)rec, n, C, cnt, grp);
   KLAUNCH(k_sm_lww, dim3(grid_for(C, 256, 4096)), dim3(256), (const evm_rec*)rec, (const u32*)off, (const u32*)grp, C,
           prior, prior_present, flags, winner, bins, pres, long_list, long_n, info);
-  KLAUNCH(k_sm_long, dim3(1024), dim3(SM_LONG_THREADS), (const evm_rec*)rec, (const u32*)off, (const u32*)grp,
+  KLAUNCH(k_sm_long_wave, dim3(grid_for(n / SM_SEG + 1, 4, 1024)), dim3(256), (const evm_rec*)rec, (const u32*)off,
+          (const u32*)grp, (const u32*)long_list, (const u32*)long_n, prior, prior_present, flags, winner, bins, pres,
+          info);
+  KLAUNCH(k_sm_long, dim3(256), dim3(SM_LONG_THREADS), (const evm_rec*)rec, (const u32*)off, (const u32*)grp,
           (const u32*)long_list, (const u32*)long_n, prior, prior_present, flags, winner, bins, pres, info);
   evm_tree* t = nullptr;
   int st = tree_alloc_cap(ctx, 1, (uint64_t)L0 + nmax, &t);

@@ -117,8 +117,9 @@ def test_collision_and_noncanonical(eng):
 
 
 def test_long_cells_and_fallbacks_give_the_same_answers(eng):
-    """A cell of 40 rows (a workgroup of k_sm_long sorts it in LDS) stays on
-    the small path; a cell of 5,000 rows (> 4,096) and minutes 60 days apart
+    """A cell of 40 rows (one wave of k_sm_long_wave) and one of 300 rows (a
+    workgroup of k_sm_long sorts it in LDS) stay on the small path; a cell of
+    5,000 rows (> 4,096) and minutes 60 days apart
     hand the batch to the sort path (small_fallbacks counts them); every
     result exact."""
     from evolu_amd import synth
@@ -126,6 +127,7 @@ def test_long_cells_and_fallbacks_give_the_same_answers(eng):
     ts, cell = synth.config2(12_000, 3000, seed_config=11)  # (unique timestamps)
     cell = cell.astype(np.uint32)
     cell[:40] = 5  # a long cell
+    cell[40:340] = 6  # a longer one
     b0, f0 = _stats(eng)
     st_o, f_o, w_o, js_o = CO.apply(ts, cell, 3000)
     st, f, w, js = _apply(eng, ts, cell, 3000, 4)
