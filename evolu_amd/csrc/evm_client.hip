@@ -1021,6 +1021,8 @@ __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* 
 // Bytes per message: TP1 46 + 4 in, 16 out; TP3 12 in, 1 out.
 // ============================================================================
 constexpr u64 TP_INVALID = ~0ull;  // tc of a message the walk skips (invalid timestamp or cell id)
+constexpr u32 XF_SPAN_MAX = FOLD_MAXWIN * FOLD_WIN;  // minutes of the fused fold's dense arrays (k_cl_leaves)
+__device__ __forceinline__ u32 minute_of_tc(u64 tc) { return (u32)((tc >> 16) / 60000ull); }
 constexpr int TP_THREADS = 256;
 constexpr int TP_RANGES = 2048;  // ~8 ranges per CU: TP1's occupancy
 constexpr u32 ROW_NONE = 0xffffffffu;   // no max (SQL NULL: below every timestamp)
@@ -1109,6 +1111,7 @@ __device__ __forceinline__ TK shfl_tk(const TK& k, int src) {
 #ifndef TP_WPE
 #define TP_WPE 8  // waves per SIMD TP1 is compiled for (7: no spills, measured no faster)
 #endif
+
 constexpr u32 TP_ROWS_MAX = 8192;  // rows per range (the key's 13-bit row offset)
 constexpr u64 TP_MS_FAST = 1ull << 41;
 
@@ -1118,7 +1121,8 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
                                                         u64* __restrict__ tcs, u32* __restrict__ hash,
                                                         u64* __restrict__ agg,
                                                         u32* __restrict__ arow, Info* __restrict__ info,
-                                                        u32* __restrict__ zero_buf, u32 zero_n) {
+                                                        u32* __restrict__ zero_buf, u32 zero_n,
+                                                        u32* __restrict__ fold_zero, u32 fold_zero_n) {
   // LDS: [C] max key per cell of this range, [ceil(C/32)] the marked cells
   extern __shared__ __attribute__((aligned(16))) u64 cmax[];
   u32* cfix = reinterpret_cast<u32*>(cmax + C);
@@ -1126,6 +1130,9 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
   // memset on the second stream, which forks after this kernel)
   if (blockIdx.x == 0)
     for (u32 k = threadIdx.x; k < zero_n; k += TP_THREADS) zero_buf[k] = 0u;
+  // (and the fused fold's dense minute arrays, which the dedup kernel and the
+  // walk add into afterwards -- a slice per workgroup)
+  for (u32 k = blockIdx.x * TP_THREADS + threadIdx.x; k < fold_zero_n; k += gridDim.x * TP_THREADS) fold_zero[k] = 0u;
   __shared__ uint4 stage[TP_THREADS / 64][192];
   __shared__ u32 nmatch;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1453,7 +1460,8 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
                                                         size_t n, u32 C, size_t range_len,
                                                         const u64* __restrict__ carry, const u32* __restrict__ crow,
                                                         NodeSrc N, uint8_t* __restrict__ flags,
-                                                        u32* __restrict__ noop, Info* __restrict__ info) {
+                                                        const u32* __restrict__ hash, u32* __restrict__ dx,
+                                                        u32* __restrict__ dc, const Info* __restrict__ info) {
   extern __shared__ __attribute__((aligned(16))) u64 tw_lds[];
   u64* T = tw_lds;                                       // [C] running max per cell: tc
   u64* M = T + C;                                        // [C] the walk round's lanes per cell (zero between rounds)
@@ -1563,13 +1571,16 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
             TR[cv] = nt.row;
           }
         }
-        // exact redeliveries of the cell's max: listed for the fold's correction (k_xf_fix)
-        const u64 nb = __ballot(ok && k3 == 0);
-        if (nb) {
-          u32 at = 0;
-          if (lane == 0) at = atomicAdd(&info->noop_n, (u32)__popcll(nb));
-          at = __shfl(at, 0, 64);
-          if ((nb >> lane) & 1ull) noop[at + (u32)__popcll(nb & lt)] = own.row;
+        // an exact redelivery of the cell's max is the one row applyMessages.ts:105
+        // does not XOR: out of the fused fold again (the dedup kernel XORs every
+        // row; XOR and add commute, so the order against it does not matter)
+        if (ok && k3 == 0) {
+          const u32 mlo = info->minute_min, span = info->minute_max - mlo + 1u;
+          const u32 d = minute_of_tc(own.tc) - mlo;
+          if (span <= XF_SPAN_MAX && d < span) {
+            atomicXor(&dx[d], hash[own.row]);
+            atomicSub(&dc[d], 1u);
+          }
         }
       }
     }
@@ -1599,7 +1610,6 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
 // redo the batch (`xf_redo`).  Bytes per message: scatter 16 in + 8 out,
 // dedup + fold 8 in.
 // ============================================================================
-constexpr u32 XF_SPAN_MAX = FOLD_MAXWIN * FOLD_WIN;  // minutes of the dense leaf arrays (k_cl_leaves)
 constexpr int XF_MIN_KB = 6;                         // >= 64 buckets
 constexpr u32 XF_WMAX = XF_SPAN_MAX / (1u << XF_MIN_KB) + 2;  // minutes one bucket can touch (its LDS histogram)
 
@@ -1649,7 +1659,6 @@ __device__ __forceinline__ u64 xf_pair(const XfGeom& g, u32 d, u32 h, u64 tc, u3
   return ((u64)h << 32) | lo;
 }
 
-__device__ __forceinline__ u32 minute_of_tc(u64 tc) { return (u32)((tc >> 16) / 60000ull); }
 
 // d = minute(tc) - mlo without a 64-bit division: rel = millis - mlo * 60000
 // fits 32 bits while the span is <= XF_SPAN32 minutes, and (rel >> 5) / 1875
@@ -1677,11 +1686,6 @@ __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ 
   if (!g.ok) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&info->xf_redo, 1u);
     return;
-  }
-  // the fold's dense minute arrays (the dedup kernel adds into them after this one)
-  for (u32 k = blockIdx.x * THREADS + threadIdx.x; k < g.span; k += gridDim.x * THREADS) {
-    dx[k] = 0;
-    dc[k] = 0;
   }
   const u32 B = 1u << kb;
   const bool narrow = g.span <= XF_SPAN32;
@@ -1831,21 +1835,6 @@ __global__ __launch_bounds__(XP_THREADS) void k_xf_dedup(const u64* __restrict__
   }
 }
 
-// The walk's exact redeliveries of a cell's max: XORed out of the fold again.
-__global__ void k_xf_fix(const u32* __restrict__ noop, const u32* __restrict__ hash, const u64* __restrict__ tcs,
-                         int kb, int cbits, u32* __restrict__ dx, u32* __restrict__ dc, Info* __restrict__ info) {
-  const u32 m = info->noop_n;
-  if (m == 0 || info->xf_redo) return;
-  const u32 mlo = info->minute_min, span = info->minute_max - mlo + 1u;
-  for (u32 t = blockIdx.x * blockDim.x + threadIdx.x; t < m; t += gridDim.x * blockDim.x) {
-    const u32 r = noop[t];
-    const u32 d = minute_of_tc(tcs[r]) - mlo;
-    if (d >= span) continue;  // (never for a valid row: its minute is inside TP1's bounds)
-    atomicXor(&dx[d], hash[r]);
-    atomicSub(&dc[d], 1u);
-  }
-}
-
 // Per minute: presence (count > 0) and the XOR; per block of FR_THREADS
 // minutes the present count and XOR (k_cl_leaves' offsets and carries).
 __global__ __launch_bounds__(FR_THREADS) void k_xf_blocks(u32* __restrict__ dx, const u32* __restrict__ dc,
@@ -1932,8 +1921,7 @@ struct SideBufs {
   u32* minute;
   u32* xcur;
   u64* xpairs;
-  u32 *px, *pp, *dx, *dp, *bcnt, *bxor;
-  u32 *dc, *noop;  // tc path: per-minute row counts of the fused fold, the walk's exact redeliveries
+  u32 *px, *pp, *dx, *dc, *dp, *bcnt, *bxor;  // (dc, the tc path's per-minute row counts, right after dx)
 };
 static size_t side_bufs(void* base, size_t n, SideBufs* v) {
   const XpGeom x = xp_geom(n);
@@ -1941,8 +1929,8 @@ static size_t side_bufs(void* base, size_t n, SideBufs* v) {
   const size_t B = (size_t)FOLD_MAXWIN * FOLD_WIN;
   const size_t sz[] = {up(sizeof(Info)), up(4 * n), up(4 * n), up(4ull << x.kb), up((8ull * x.cap) << x.kb),
                        up((size_t)4 * FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN),
-                       up((size_t)4 * FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32)), up(4 * B), up(4 * B),
-                       up(4 * FR_BLOCKS), up(4 * FR_BLOCKS), up(4 * B), up(4 * n)};
+                       up((size_t)4 * FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32)), up(4 * B), up(4 * B), up(4 * B),
+                       up(4 * FR_BLOCKS), up(4 * FR_BLOCKS)};
   constexpr int NB = sizeof(sz) / sizeof(sz[0]);
   size_t off[NB], tot = 0;
   for (int k = 0; k < NB; ++k) {
@@ -1959,11 +1947,10 @@ static size_t side_bufs(void* base, size_t n, SideBufs* v) {
     v->px = reinterpret_cast<u32*>(p + off[5]);
     v->pp = reinterpret_cast<u32*>(p + off[6]);
     v->dx = reinterpret_cast<u32*>(p + off[7]);
-    v->dp = reinterpret_cast<u32*>(p + off[8]);
-    v->bcnt = reinterpret_cast<u32*>(p + off[9]);
-    v->bxor = reinterpret_cast<u32*>(p + off[10]);
-    v->dc = reinterpret_cast<u32*>(p + off[11]);
-    v->noop = reinterpret_cast<u32*>(p + off[12]);
+    v->dc = reinterpret_cast<u32*>(p + off[8]);
+    v->dp = reinterpret_cast<u32*>(p + off[9]);
+    v->bcnt = reinterpret_cast<u32*>(p + off[10]);
+    v->bxor = reinterpret_cast<u32*>(p + off[11]);
   }
   return tot;
 }
@@ -2022,10 +2009,10 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     const dim3 g1((u32)G);
     if (s48)
       hipLaunchKernelGGL(k_tp_pack<true>, g1, dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb);
+                         cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
     else
       hipLaunchKernelGGL(k_tp_pack<false>, g1, dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb);
+                         cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
   } else {
     key = S.alloc<uint4>(n);
     rl = S.alloc<u32>(n);
@@ -2142,7 +2129,8 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
             winner);
     // TP3: flags, a workgroup per range
     KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14 + (size_t)C * 4,
-                (const u64*)tcs, cell, n, C, range, (const u64*)agg, (const u32*)arow, N, flags, sb.noop, info);
+                (const u64*)tcs, cell, n, C, range, (const u64*)agg, (const u32*)arow, N, flags, (const u32*)hash,
+                sb.dx, sb.dc, (const Info*)info);
     // the Merkle fold reads the walk's flags (an exact redelivery of a cell's
     // max is not XORed): on the second stream after the walk, beside the
     // next batch's K1 when batches are pipelined
@@ -2150,11 +2138,6 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     if (fs != ctx->stream) {
       HIPR(hipEventRecord(ctx->ev_fork, ctx->stream));
       HIPR(hipStreamWaitEvent(fs, ctx->ev_fork, 0));
-    }
-    {
-      evm::ProfScope ps_(ctx, "k_xf_fix", fs);
-      hipLaunchKernelGGL(k_xf_fix, dim3(64), dim3(256), 0, fs, (const u32*)sb.noop, (const u32*)hash,
-                         (const u64*)tcs, kb, cbits, sb.dx, sb.dc, info);
     }
     {
       evm::ProfScope ps_(ctx, "k_xf_blocks", fs);
@@ -2351,27 +2334,37 @@ __global__ __launch_bounds__(256) void k_sm_pack(const uint8_t* __restrict__ ts,
 // (K3's cursors).  One workgroup, tiles of 16,384 counts: 16 consecutive per
 // thread (four 16-B loads), a block scan, the running total carried.
 constexpr u32 SM_SCAN_ITEMS = 16;
+// One workgroup, tiles of SM_FOLD_THREADS x 16 counts; the next tile's loads
+// are issued before this tile is scanned (a 100k-message batch has ~55k cells:
+// four tiles, one load latency instead of four).
+__device__ __forceinline__ void sm_scan_load(const u32* cnt, u32 C, u32 a, u32 (&v)[SM_SCAN_ITEMS]) {
+  if (a + SM_SCAN_ITEMS <= C) {  // (cnt is 256-B aligned scratch: a is a multiple of 16)
+    const uint4* p = reinterpret_cast<const uint4*>(cnt + a);
+#pragma unroll
+    for (u32 q = 0; q < SM_SCAN_ITEMS / 4; ++q) {
+      const uint4 x = p[q];
+      v[4 * q] = x.x;
+      v[4 * q + 1] = x.y;
+      v[4 * q + 2] = x.z;
+      v[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) v[q] = a + q < C ? cnt[a + q] : 0u;
+  }
+}
 __global__ __launch_bounds__(SM_FOLD_THREADS) void k_sm_scan(u32* __restrict__ cnt, u32 C, u32* __restrict__ off) {
   __shared__ u32 lds[SM_FOLD_THREADS / 64 + 1];
   constexpr u32 TILE = SM_FOLD_THREADS * SM_SCAN_ITEMS;
   u32 carry = 0;
+  u32 nv[SM_SCAN_ITEMS];
+  sm_scan_load(cnt, C, threadIdx.x * SM_SCAN_ITEMS, nv);
   for (u32 base = 0; base < C; base += TILE) {
     const u32 a = base + threadIdx.x * SM_SCAN_ITEMS;
     u32 v[SM_SCAN_ITEMS];
-    if (a + SM_SCAN_ITEMS <= C) {  // (cnt is 256-B aligned scratch: a is a multiple of 16)
-      const uint4* p = reinterpret_cast<const uint4*>(cnt + a);
 #pragma unroll
-      for (u32 q = 0; q < SM_SCAN_ITEMS / 4; ++q) {
-        const uint4 x = p[q];
-        v[4 * q] = x.x;
-        v[4 * q + 1] = x.y;
-        v[4 * q + 2] = x.z;
-        v[4 * q + 3] = x.w;
-      }
-    } else {
-#pragma unroll
-      for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) v[q] = a + q < C ? cnt[a + q] : 0u;
-    }
+    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) v[q] = nv[q];
+    if (base + TILE < C) sm_scan_load(cnt, C, a + TILE, nv);  // (in flight during this tile's scan)
     u32 sum = 0;
 #pragma unroll
     for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) sum += v[q];
@@ -2508,18 +2501,28 @@ __device__ __forceinline__ Key shfl_key(const Key& k, int src) {
   o.mask = (u32)__shfl((int)k.mask, src, 64);
   return o;
 }
-__global__ __launch_bounds__(256) void k_sm_long_wave(const evm_rec* __restrict__ rec, const u32* __restrict__ off,
+constexpr int SM_LW_WAVES = 16;  // waves per workgroup (one cell each at a time; the LDS bins shared)
+__global__ __launch_bounds__(64 * SM_LW_WAVES) void k_sm_long_wave(const evm_rec* __restrict__ rec, const u32* __restrict__ off,
                                                       const u32* __restrict__ grp, const u32* __restrict__ long_list,
                                                       const u32* __restrict__ long_n, const evm_rec* __restrict__ prior,
                                                       const uint8_t* __restrict__ prior_present,
                                                       uint8_t* __restrict__ flags, int32_t* __restrict__ winner,
                                                       u32* __restrict__ bins, u32* __restrict__ pres,
                                                       Info* __restrict__ info) {
-  __shared__ u32 slot[4][SM_WAVE_MAX];
+  __shared__ u32 slot[SM_LW_WAVES][SM_WAVE_MAX];
+  __shared__ u32 lbins[SM_LDS_BINS];  // the workgroup's copy of the minute bins (as k_sm_lww)
+  __shared__ u32 lpres[SM_LDS_BINS / 32];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const u32 nl = *long_n;
-  const u32 mlo = info->minute_min;
-  for (u32 li = blockIdx.x * 4 + wv; li < nl; li += gridDim.x * 4) {  // wave-uniform
+  const u32 mlo = info->minute_min, mhi = info->minute_max;
+  const u32 W = mhi >= mlo ? mhi - mlo + 1 : 0u;
+  const bool lds = W <= SM_LDS_BINS;
+  if (lds) {
+    for (u32 q = threadIdx.x; q < W; q += blockDim.x) lbins[q] = 0;
+    for (u32 q = threadIdx.x; q < (W + 31) / 32; q += blockDim.x) lpres[q] = 0;
+  }
+  __syncthreads();
+  for (u32 li = blockIdx.x * SM_LW_WAVES + wv; li < nl; li += gridDim.x * SM_LW_WAVES) {  // wave-uniform
     const u32 c = long_list[li];
     const u32 a = off[c], k = off[c + 1] - a;
     if (k > SM_WAVE_MAX) continue;  // (k_sm_long)
@@ -2550,8 +2553,15 @@ __global__ __launch_bounds__(256) void k_sm_long_wave(const evm_rec* __restrict_
     const u64 ub = __ballot(ups);  // the last upsert in batch order wins
     const u32 wrow = (u32)__shfl((int)row, ub ? 63 - __builtin_clzll(ub) : 0, 64);
     if (lane == 0) winner[c] = ub ? (int32_t)wrow : -1;
-    // per distinct minute of the XOR rows: one reduction, one global update
     const u32 d = xr ? r.minute - mlo : 0xffffffffu;
+    if (lds) {
+      if (xr) {
+        atomicXor(&lbins[d], r.hash);
+        atomicOr(&lpres[d >> 5], 1u << (d & 31));
+      }
+      continue;
+    }
+    // (wide batches) per distinct minute of the XOR rows: one reduction, one global update
     u64 left = __ballot(xr);
     while (left) {
       const int ld = __builtin_ctzll(left);
@@ -2570,6 +2580,15 @@ __global__ __launch_bounds__(256) void k_sm_long_wave(const evm_rec* __restrict_
       }
       left &= ~mem;
     }
+  }
+  if (!lds) return;
+  __syncthreads();
+  for (u32 q = threadIdx.x; q < (W + 31) / 32; q += blockDim.x) {
+    const u32 m = lpres[q];
+    if (!m) continue;
+    atomic_or_if(&pres[q], m);
+    for (u32 b = 0; b < 32; ++b)
+      if ((m >> b) & 1u) atomicXor(&bins[32 * q + b], lbins[32 * q + b]);
   }
 }
 
@@ -2795,7 +2814,7 @@ static int apply_small(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tre
   KLAUNCH(k_sm_scatter, dim3(grid_for(n, 256, 1024)), dim3(256), (const evm_rec*)rec, n, C, cnt, grp);
   KLAUNCH(k_sm_lww, dim3(grid_for(C, 256, 4096)), dim3(256), (const evm_rec*)rec, (const u32*)off, (const u32*)grp, C,
           prior, prior_present, flags, winner, bins, pres, long_list, long_n, info);
-  KLAUNCH(k_sm_long_wave, dim3(grid_for(n / SM_SEG + 1, 4, 1024)), dim3(256), (const evm_rec*)rec, (const u32*)off,
+  KLAUNCH(k_sm_long_wave, dim3(64), dim3(64 * SM_LW_WAVES), (const evm_rec*)rec, (const u32*)off,
           (const u32*)grp, (const u32*)long_list, (const u32*)long_n, prior, prior_present, flags, winner, bins, pres,
           info);
   KLAUNCH(k_sm_long, dim3(256), dim3(SM_LONG_THREADS), (const evm_rec*)rec, (const u32*)off, (const u32*)grp,

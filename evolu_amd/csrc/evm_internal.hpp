@@ -83,7 +83,6 @@ struct Info {
   u32 xc_oversize;    // a hash bucket of the cross-cell check overflowed LDS
   u32 ties;           // tc path: a message's tc equals its cell's running max (node ranks decide)
   u32 xf_redo;        // tc path: the fused check + fold cannot finish (minute span, full bucket, fingerprint match)
-  u32 noop_n;         // tc path: rows the walk found to be exact redeliveries of their cell's max (not XORed)
 };
 
 inline Info info_init() {
@@ -101,7 +100,6 @@ inline Info info_init() {
   h.xc_oversize = 0;
   h.ties = 0;
   h.xf_redo = 0;
-  h.noop_n = 0;
   return h;
 }
 
