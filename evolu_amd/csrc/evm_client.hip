@@ -1113,11 +1113,33 @@ __device__ __forceinline__ TK shfl_tk(const TK& k, int src) {
 #endif
 
 constexpr u32 TP_ROWS_MAX = 8192;  // rows per range (the key's 13-bit row offset)
+
+// Range g of the tc path.  The batch's first L rows are cut into five
+// geometric sub-ranges (q, q, 2q, 4q, L - 8q; q = L/16 rounded down to 64):
+// in the first rows every row is a candidate of the walk (no earlier maximum
+// of its cell exists), so a full-length first range would hold the walk's
+// longest serial chain; each sub-range starts from the maxima of all earlier
+// ones.  Then ranges of L.  G' = ceil(n / L) + 4.
+struct TpRanges {
+  size_t L, q;
+};
+__host__ __device__ __forceinline__ void tp_range(const TpRanges& R, size_t g, size_t n, size_t* beg, size_t* end) {
+  size_t b, e;
+  if (g < 5) {
+    b = g == 0 ? 0 : R.q << (g - 1);
+    e = g == 4 ? R.L : R.q << g;
+  } else {
+    b = (g - 4) * R.L;
+    e = b + R.L;
+  }
+  *beg = b < n ? b : n;
+  *end = e < n ? e : n;
+}
 constexpr u64 TP_MS_FAST = 1ull << 41;
 
 template <bool S48>
 __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_WPE, 8))) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
-                                                        const u32* __restrict__ cell, u32 C, size_t range_len,
+                                                        const u32* __restrict__ cell, u32 C, TpRanges R,
                                                         u64* __restrict__ tcs, u32* __restrict__ hash,
                                                         u64* __restrict__ agg,
                                                         u32* __restrict__ arow, Info* __restrict__ info,
@@ -1138,7 +1160,8 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   u32 bad = 0, aux_bad = 0, mn = 0xffffffffu, mx = 0;
   const size_t g = blockIdx.x;
-  const size_t beg = g * range_len, end = min(n, beg + range_len);
+  size_t beg, end;
+  tp_range(R, g, n, &beg, &end);
   for (u32 c = threadIdx.x; c < C; c += TP_THREADS) cmax[c] = 0;
   for (u32 k = threadIdx.x; k < (C + 31) / 32; k += TP_THREADS) cfix[k] = 0;
   if (threadIdx.x == 0) nmatch = 0;
@@ -1457,7 +1480,7 @@ constexpr int TP_WAVES = TP_THREADS / 64;
 constexpr u32 TPC_ROWS = 64 * 4 * TP_WAVES;  // 4 rounds per wave per chunk
 
 __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ tcs, const u32* __restrict__ cell,
-                                                        size_t n, u32 C, size_t range_len,
+                                                        size_t n, u32 C, TpRanges R,
                                                         const u64* __restrict__ carry, const u32* __restrict__ crow,
                                                         NodeSrc N, uint8_t* __restrict__ flags,
                                                         const u32* __restrict__ hash, u32* __restrict__ dx,
@@ -1473,7 +1496,8 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const u64 lt = lanemask_lt();
   const size_t g = blockIdx.x;
-  const size_t beg = g * range_len, end = min(n, beg + range_len);
+  size_t beg, end;
+  tp_range(R, g, n, &beg, &end);
   for (u32 c = threadIdx.x; c < C; c += TP_THREADS) {
     T[c] = carry[g * C + c];
     TR[c] = crow[g * C + c];
@@ -1980,15 +2004,18 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   u64* xpairs = sb.xpairs;
   // TC: ranges of TP1/TP3 (multiples of 256 rows); walk path: ranges of the walks
   size_t range, G;
+  TpRanges TR{};
   if (TC) {
     static const size_t tp_ranges = getenv("EVM_TP_RANGES") ? (size_t)atol(getenv("EVM_TP_RANGES")) : TP_RANGES;
     range = std::max<size_t>(1024, ((n + tp_ranges - 1) / tp_ranges + 255) / 256 * 256);
     range = std::min<size_t>(range, TP_ROWS_MAX);  // (TP1's key holds a 13-bit row offset)
+    TR = TpRanges{range, (range / 16) & ~(size_t)63};
+    G = (n + range - 1) / range + 4;  // (the first range in five geometric pieces)
   } else {
     range = (n + CL_RANGE_TARGET - 1) / CL_RANGE_TARGET;
     range = std::max<size_t>(2048, (range + 255) / 256 * 256);
+    G = (n + range - 1) / range;
   }
-  G = (n + range - 1) / range;
   uint4* key = nullptr;
   u32* rl = nullptr;
   u64* tcs = nullptr;
@@ -2009,10 +2036,10 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     const dim3 g1((u32)G);
     if (s48)
       hipLaunchKernelGGL(k_tp_pack<true>, g1, dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
+                         cell, C, TR, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
     else
       hipLaunchKernelGGL(k_tp_pack<false>, g1, dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, range, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
+                         cell, C, TR, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
   } else {
     key = S.alloc<uint4>(n);
     rl = S.alloc<u32>(n);
@@ -2129,7 +2156,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
             winner);
     // TP3: flags, a workgroup per range
     KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14 + (size_t)C * 4,
-                (const u64*)tcs, cell, n, C, range, (const u64*)agg, (const u32*)arow, N, flags, (const u32*)hash,
+                (const u64*)tcs, cell, n, C, TR, (const u64*)agg, (const u32*)arow, N, flags, (const u32*)hash,
                 sb.dx, sb.dc, (const Info*)info);
     // the Merkle fold reads the walk's flags (an exact redelivery of a cell's
     // max is not XORed): on the second stream after the walk, beside the

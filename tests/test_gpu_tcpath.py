@@ -317,20 +317,21 @@ def test_tc_path_adversarial_client_stream_vs_c_oracle(eng, n, cells, nodes):
 
 def test_tc_path_tie_list_overflow_redoes_exactly(eng):
     """More than 512 rows of one range tied at a cell's range max (700 nodes
-    sending at the same millisecond, counter 0): TP1's list overflows and the
-    exact walk path answers -- the result is still exact."""
+    sending at the same millisecond, counter 0, inside the second range of
+    1,024 rows: the first is cut into geometric pieces): TP1's list overflows
+    and the exact walk path answers -- the result is still exact."""
     from evolu_amd import _lib as L
     from evolu_amd import synth
 
     rng = np.random.default_rng(9)
     n = 4096
     ms = synth.BENCH_T0 + rng.integers(0, 10_000, n)
-    ms[100:800] = synth.BENCH_T0 + 50_000  # 700 rows, one millisecond, above everything else
+    ms[1100:1800] = synth.BENCH_T0 + 50_000  # 700 rows, one millisecond, above everything else (one range)
     nodes = synth.random_nodes(rng, n)
     ts_np = synth.format_timestamps(ms, np.zeros(n, dtype=np.int64), nodes)
     cell_np = np.zeros(n, dtype=np.uint32)
     cell_np[::7] = 1
-    cell_np[100:800] = 0
+    cell_np[1100:1800] = 0
     from oracle import c_oracle as CO
 
     st_w, f_w, w_w, js_w = CO.apply(ts_np, cell_np, 2)
