@@ -1022,6 +1022,27 @@ __global__ void k_prior_check(const evm_rec* __restrict__ prior, const uint8_t* 
 // ============================================================================
 constexpr u64 TP_INVALID = ~0ull;  // tc of a message the walk skips (invalid timestamp or cell id)
 constexpr u32 XF_SPAN_MAX = FOLD_MAXWIN * FOLD_WIN;  // minutes of the fused fold's dense arrays (k_cl_leaves)
+// TP1's per-row word for the walk and the fused check: cell << 49 | millis << 8
+// | counter while millis < 2^41 and counter < 256 (every row of a batch before
+// 2039-09 with < 256 sends per node and millisecond), so neither reads the
+// cell column again; any other valid row is TP_FAR with its tc in a side
+// array (and its cell from the column).  The order of (millis, counter) is kept.
+constexpr u64 TP_FAR = ~0ull - 1ull;
+constexpr int TPC_CELL = 49;
+__device__ __forceinline__ u64 tpc_pack(u64 tc, u32 c) {
+  return ((u64)c << TPC_CELL) | ((tc >> 16) << 8) | (tc & 0xffull);
+}
+__device__ __forceinline__ void tpc_unpack(u64 v, const u64* __restrict__ far, const u32* __restrict__ cell, size_t i,
+                                           u64* tc, u32* c) {
+  if (v == TP_FAR) {
+    *tc = far[i];
+    *c = cell[i];
+  } else {
+    const u64 low = v & ((1ull << TPC_CELL) - 1ull);
+    *tc = ((low >> 8) << 16) | (low & 0xffull);
+    *c = (u32)(v >> TPC_CELL);
+  }
+}
 __device__ __forceinline__ u32 minute_of_tc(u64 tc) { return (u32)((tc >> 16) / 60000ull); }
 constexpr int TP_THREADS = 256;
 constexpr int TP_RANGES = 2048;  // ~8 ranges per CU: TP1's occupancy
@@ -1140,8 +1161,8 @@ constexpr u64 TP_MS_FAST = 1ull << 41;
 template <bool S48>
 __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_WPE, 8))) void k_tp_pack(const uint8_t* __restrict__ ts, size_t stride, size_t n,
                                                         const u32* __restrict__ cell, u32 C, TpRanges R,
-                                                        u64* __restrict__ tcs, u32* __restrict__ hash,
-                                                        u64* __restrict__ agg,
+                                                        u64* __restrict__ tcs, u64* __restrict__ tcs_far,
+                                                        u32* __restrict__ hash, u64* __restrict__ agg,
                                                         u32* __restrict__ arow, Info* __restrict__ info,
                                                         u32* __restrict__ zero_buf, u32 zero_n,
                                                         u32* __restrict__ fold_zero, u32 fold_zero_n) {
@@ -1204,7 +1225,9 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
     if (i < end) {
       const u32 ci = __builtin_nontemporal_load(cell + i);
       const bool ok = valid && ci < C;
-      __builtin_nontemporal_store(ok ? p.tc : TP_INVALID, tcs + i);
+      const bool fast = (p.tc >> 16) < TP_MS_FAST && ((u32)p.tc & 0xffffu) < 256u;
+      __builtin_nontemporal_store(!ok ? TP_INVALID : fast ? tpc_pack(p.tc, ci) : TP_FAR, tcs + i);
+      if (ok && !fast) tcs_far[i] = p.tc;
       if (!ok) p.minute = 0xffffffffu;  // outside every fold window (and the minute bounds)
       if (ok) {
         const u64 ms = p.tc >> 16;
@@ -1259,17 +1282,21 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
       if (marked(c)) cmax[c] = 0;
     __syncthreads();
     for (size_t i = beg + threadIdx.x; i < end; i += TP_THREADS) {
-      const u64 t = __hip_atomic_load(tcs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // written above
-      if (t == TP_INVALID) continue;
-      const u32 ci = cell[i];
+      const u64 v = __hip_atomic_load(tcs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // written above
+      if (v == TP_INVALID) continue;
+      u64 t;
+      u32 ci;
+      tpc_unpack(v, tcs_far, cell, i, &t, &ci);
       if (marked(ci)) atomicMax(&cmax[ci], t);
     }
     __syncthreads();
     const NodeSrc N{ts, stride, nullptr};
     for (size_t i = beg + threadIdx.x; i < end; i += TP_THREADS) {
-      const u64 t = __hip_atomic_load(tcs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == TP_INVALID) continue;
-      const u32 ci = cell[i];
+      const u64 v = __hip_atomic_load(tcs + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v == TP_INVALID) continue;
+      u64 t;
+      u32 ci;
+      tpc_unpack(v, tcs_far, cell, i, &t, &ci);
       if (!marked(ci) || t != cmax[ci]) continue;
       const u32 k = atomicAdd(&nmatch, 1u);
       if (k < TP_MATCH_MAX) {
@@ -1479,7 +1506,8 @@ __global__ __launch_bounds__(CT_THREADS) void k_tp_carry(u32 C, size_t G, u64* _
 constexpr int TP_WAVES = TP_THREADS / 64;
 constexpr u32 TPC_ROWS = 64 * 4 * TP_WAVES;  // 4 rounds per wave per chunk
 
-__global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ tcs, const u32* __restrict__ cell,
+__global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ tcs, const u64* __restrict__ tcs_far,
+                                                        const u32* __restrict__ cell,
                                                         size_t n, u32 C, TpRanges R,
                                                         const u64* __restrict__ carry, const u32* __restrict__ crow,
                                                         NodeSrc N, uint8_t* __restrict__ flags,
@@ -1509,11 +1537,22 @@ __global__ __launch_bounds__(TP_THREADS) void k_tp_walk(const u64* __restrict__ 
     const size_t wb = base + 256 * wv;
     u64 x[4];
     u32 c[4];
+    u64 v[4];  // (all four loads in flight before any decode)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const size_t i = wb + 64 * r + lane;
-      x[r] = i < end ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
-      c[r] = i < end ? __builtin_nontemporal_load(cell + i) : 0u;
+      v[r] = i < end ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const u64 low = v[r] & ((1ull << TPC_CELL) - 1ull);
+      x[r] = v[r] == TP_INVALID ? TP_INVALID : ((low >> 8) << 16) | (low & 0xffull);
+      c[r] = v[r] == TP_INVALID ? 0u : (u32)(v[r] >> TPC_CELL);
+    }
+    if (__any(v[0] == TP_FAR || v[1] == TP_FAR || v[2] == TP_FAR || v[3] == TP_FAR)) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (v[r] == TP_FAR) tpc_unpack(v[r], tcs_far, cell, wb + 64 * r + lane, &x[r], &c[r]);
     }
     u32 wcnt = 0;
 #pragma unroll
@@ -1697,6 +1736,7 @@ __device__ __forceinline__ u32 xf_minute_off(u64 tc, u64 base_ms, u32 mlo, bool 
 // written back bucket by bucket (EVM_XF_SCATTER picks the shape).
 template <int THREADS, int ITEMS>
 __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ hash, const u64* __restrict__ tcs,
+                                                          const u64* __restrict__ tcs_far,
                                                           const u32* __restrict__ cell, size_t n, int kb, int cbits,
                                                           u32 cap, u32* __restrict__ cursor, u64* __restrict__ out,
                                                           u32* __restrict__ dx, u32* __restrict__ dc,
@@ -1722,12 +1762,17 @@ __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ 
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
     const size_t i = base + (size_t)k * THREADS + threadIdx.x;
-    const u64 tc = i < n ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
+    const u64 tv = i < n ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
     const u32 h = i < n ? __builtin_nontemporal_load(hash + i) : 0u;
-    const u32 c = i < n ? __builtin_nontemporal_load(cell + i) : 0u;
     bk[k] = B;  // none (an invalid row: the batch is rejected anyway)
     v[k] = 0;
-    if (tc != TP_INVALID) v[k] = xf_pair(g, xf_minute_off(tc, base_ms, g.mlo, narrow), h, tc, c, &bk[k]);
+    if (tv != TP_INVALID) {
+      const u64 low = tv & ((1ull << TPC_CELL) - 1ull);
+      u64 tc = ((low >> 8) << 16) | (low & 0xffull);
+      u32 c = (u32)(tv >> TPC_CELL);
+      if (tv == TP_FAR) tpc_unpack(tv, tcs_far, cell, i, &tc, &c);
+      v[k] = xf_pair(g, xf_minute_off(tc, base_ms, g.mlo, narrow), h, tc, c, &bk[k]);
+    }
     r[k] = bk[k] < B ? atomicAdd(&cnt[bk[k]], 1u) : 0u;
   }
   __syncthreads();
@@ -1946,6 +1991,7 @@ struct SideBufs {
   u32* xcur;
   u64* xpairs;
   u32 *px, *pp, *dx, *dc, *dp, *bcnt, *bxor;  // (dc, the tc path's per-minute row counts, right after dx)
+  u64 *tcs, *tcs_far;  // tc path: TP1's packed (cell, tc) per row (the second stream's scatter reads it) and far rows' tc
 };
 static size_t side_bufs(void* base, size_t n, SideBufs* v) {
   const XpGeom x = xp_geom(n);
@@ -1954,7 +2000,7 @@ static size_t side_bufs(void* base, size_t n, SideBufs* v) {
   const size_t sz[] = {up(sizeof(Info)), up(4 * n), up(4 * n), up(4ull << x.kb), up((8ull * x.cap) << x.kb),
                        up((size_t)4 * FOLD_MAXWIN * FOLD_CHUNKS * FOLD_WIN),
                        up((size_t)4 * FOLD_MAXWIN * FOLD_CHUNKS * (FOLD_WIN / 32)), up(4 * B), up(4 * B), up(4 * B),
-                       up(4 * FR_BLOCKS), up(4 * FR_BLOCKS)};
+                       up(4 * FR_BLOCKS), up(4 * FR_BLOCKS), up(8 * n), up(8 * n)};
   constexpr int NB = sizeof(sz) / sizeof(sz[0]);
   size_t off[NB], tot = 0;
   for (int k = 0; k < NB; ++k) {
@@ -1975,6 +2021,8 @@ static size_t side_bufs(void* base, size_t n, SideBufs* v) {
     v->dp = reinterpret_cast<u32*>(p + off[9]);
     v->bcnt = reinterpret_cast<u32*>(p + off[10]);
     v->bxor = reinterpret_cast<u32*>(p + off[11]);
+    v->tcs = reinterpret_cast<u64*>(p + off[12]);
+    v->tcs_far = reinterpret_cast<u64*>(p + off[13]);
   }
   return tot;
 }
@@ -2026,7 +2074,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   u32* a_rl = nullptr;
   u32* a_first = nullptr;
   if (TC) {
-    tcs = S.alloc<u64>(n);
+    tcs = sb.tcs;  // (in the batch's own block: the second stream reads it after the call returns)
     agg = S.alloc<u64>(G * C);
     arow = S.alloc<u32>(G * C);
     if (!tcs || !agg || !arow) return EVM_ENOMEM;
@@ -2036,10 +2084,10 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
     const dim3 g1((u32)G);
     if (s48)
       hipLaunchKernelGGL(k_tp_pack<true>, g1, dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, TR, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
+                         cell, C, TR, tcs, sb.tcs_far, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
     else
       hipLaunchKernelGGL(k_tp_pack<false>, g1, dim3(TP_THREADS), lds, ctx->stream, (const uint8_t*)ts, stride, n,
-                         cell, C, TR, tcs, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
+                         cell, C, TR, tcs, sb.tcs_far, hash, agg, arow, info, xcur, 1u << xp_geom(n).kb, sb.dx, 2u * XF_SPAN_MAX);
   } else {
     key = S.alloc<uint4>(n);
     rl = S.alloc<u32>(n);
@@ -2129,7 +2177,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       // after the walk XORs its exact redeliveries out again)
       {
         evm::ProfScope ps_(ctx, "k_xf_scatter", xs);
-#define XF_SCATTER_ARGS hash, (const u64*)tcs, cell, n, kb, cbits, cap, xcur, xpairs, sb.dx, sb.dc, info
+#define XF_SCATTER_ARGS hash, (const u64*)tcs, (const u64*)sb.tcs_far, cell, n, kb, cbits, cap, xcur, xpairs, sb.dx, sb.dc, info
         if (xf_shape == 0) hipLaunchKernelGGL((k_xf_scatter<1024, 12>), dim3(xft), dim3(1024), 0, xs, XF_SCATTER_ARGS);
         else if (xf_shape == 1) hipLaunchKernelGGL((k_xf_scatter<512, 12>), dim3(xft), dim3(512), 0, xs, XF_SCATTER_ARGS);
         else hipLaunchKernelGGL((k_xf_scatter<512, 8>), dim3(xft), dim3(512), 0, xs, XF_SCATTER_ARGS);
@@ -2156,7 +2204,8 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
             winner);
     // TP3: flags, a workgroup per range
     KLAUNCH_LDS(k_tp_walk, dim3(G), dim3(TP_THREADS), (size_t)2 * C * 8 + (size_t)TPC_ROWS * 14 + (size_t)C * 4,
-                (const u64*)tcs, cell, n, C, TR, (const u64*)agg, (const u32*)arow, N, flags, (const u32*)hash,
+                (const u64*)tcs, (const u64*)sb.tcs_far, cell, n, C, TR, (const u64*)agg, (const u32*)arow, N, flags,
+                (const u32*)hash,
                 sb.dx, sb.dc, (const Info*)info);
     // the Merkle fold reads the walk's flags (an exact redelivery of a cell's
     // max is not XORed): on the second stream after the walk, beside the

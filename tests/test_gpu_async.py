@@ -37,12 +37,16 @@ def test_pipelined_batches_equal_sync(eng):
 
     from evolu_amd import synth
 
+    # (batches large enough that one batch's second-stream work -- the fused
+    # check + fold reads TP1's per-row words -- still runs while the next
+    # batch's TP1 writes its own: they must not share a buffer)
+    n = 2_000_000
     batches = []
     for k in range(4):
-        ts_np, cell_np = synth.config2(300_000, 500, seed_config=60 + k)
+        ts_np, cell_np = synth.config2(n, 500, seed_config=60 + k)
         batches.append((eng.dev(ts_np), eng.dev(cell_np)))
     trees_in = [eng.tree_new(1) for _ in batches]
-    outs = [(torch.empty(300_000, dtype=torch.uint8, device="cuda"), torch.empty(500, dtype=torch.int32, device="cuda"))
+    outs = [(torch.empty(n, dtype=torch.uint8, device="cuda"), torch.empty(500, dtype=torch.int32, device="cuda"))
             for _ in batches]
     pend = [eng.apply_batch_async(trees_in[k], ts, cell, 500, *outs[k]) for k, (ts, cell) in enumerate(batches)]
     for k, p in enumerate(pend):

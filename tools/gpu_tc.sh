@@ -2,7 +2,7 @@
 # The tc path's tests, then the headline bench line only (no extra legs).
 mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) return 0 ;; *) return 1 ;; esac; }
-timeout -k 10 600 python -u -m pytest tests/test_gpu_tcpath.py tests/test_gpu_apply.py tests/test_gpu_scale.py -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_tc.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_tcpath.py tests/test_gpu_apply.py tests/test_gpu_scale.py tests/test_gpu_async.py -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_tc.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_tc.log
 if fatal $rc; then exit $rc; fi
