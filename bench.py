@@ -47,9 +47,9 @@ HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 # SURVEY.md section 8(d) accounting, restated per kernel in DESIGN.md.
 ALG_BYTES_PER_MSG = {
     # streaming tc path (evm_client.hip TP1-TP3, the default)
-    "k_tp_pack": 46 + 4 + 12,  # ts + cell in; tc 8 + hash 4 out (per-range cell maxima amortised)
-    "k_tp_walk": 8 + 4 + 1,  # tc + cell in, flag out
-    "k_xf_scatter": 4 + 8 + 4 + 8,  # hash + tc + cell in, fingerprint pair out (minute buckets)
+    "k_tp_pack": 46 + 4 + 12,  # ts + cell in; packed (cell, tc) word 8 + hash 4 out (per-range cell maxima amortised)
+    "k_tp_walk": 8 + 1,  # packed (cell, tc) word in, flag out
+    "k_xf_scatter": 8 + 4 + 8,  # packed word + hash in, fingerprint pair out (minute buckets)
     "k_xf_dedup": 8,  # pair in (PK check + fold of the bucket's minutes in LDS)
     # exact walk path (a batch with a tie)
     "k_cl_pack": 46 + 28,  # ts in; order key 16 + rl 4 + hash 4 + minute 4 out

@@ -442,3 +442,31 @@ def test_xf_mixed_key_lengths_redo(eng):
     ms = edge + rng.integers(-3_600_000, 3_600_000, n)
     ts_np = synth.format_timestamps(ms, np.zeros(n, dtype=np.int64), synth.random_nodes(rng, 32)[rng.integers(0, 32, n)])
     _c_vs_tc(eng, ts_np, rng.integers(0, 50, n).astype(np.uint32), 50, redo=True)
+
+
+@pytest.mark.parametrize("case", ["counter", "year2045"])
+def test_tc_path_far_rows_vs_c_oracle(eng, case):
+    """Rows outside TP1's packed word (counter >= 256, or millis >= 2^41:
+    after 2039-09) travel as TP_FAR with their tc in the side array: the
+    walk and the fused check read them from there; still one tc batch, no
+    redo, bit-exact against the C restatement."""
+    from evolu_amd import synth
+
+    rng = np.random.default_rng(12)
+    n = 400_000
+    t0 = synth.BENCH_T0 if case == "counter" else 2_378_000_000_000  # (2045-05: same base-3 key length as 2024)
+    ms = t0 + rng.integers(0, 20 * 86_400_000, n)
+    ctr = np.zeros(n, dtype=np.int64)
+    if case == "counter":
+        far = rng.random(n) < 0.02
+        ctr[far] = rng.integers(256, 0xffff, far.sum())
+    nodes = synth.random_nodes(rng, 32)
+    ts_np = synth.format_timestamps(ms, ctr, nodes[rng.integers(0, 32, n)])
+    # (every far row marks its cell for TP1's rescan, whose match list holds
+    # 512 rows per range: all-far batches over few cells)
+    cells = 700 if case == "counter" else 200
+    cell_np = rng.integers(0, cells, n).astype(np.uint32)
+    key = ts_np[:, :46].copy().view("S46").ravel()
+    _, first, inv = np.unique(key, return_index=True, return_inverse=True)
+    cell_np = cell_np[first][inv].astype(np.uint32)  # (no cross-cell twins)
+    _c_vs_tc(eng, ts_np, cell_np, cells, redo=False)
