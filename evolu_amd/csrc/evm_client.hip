@@ -1740,7 +1740,7 @@ __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ 
                                                           const u32* __restrict__ cell, size_t n, int kb, int cbits,
                                                           u32 cap, u32* __restrict__ cursor, u64* __restrict__ out,
                                                           u32* __restrict__ dx, u32* __restrict__ dc,
-                                                          Info* __restrict__ info) {
+                                                          Info* __restrict__ info, u32 tl) {
   __shared__ u64 stage[(THREADS * ITEMS)];
   __shared__ uint16_t sbk[(THREADS * ITEMS)];      // the bucket of each staged pair
   __shared__ u32 cnt[1u << XP_MAX_KB];  // per bucket: count, then local offset
@@ -1756,12 +1756,13 @@ __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ 
   const u64 base_ms = (u64)g.mlo * 60000ull;
   for (u32 b = threadIdx.x; b < B; b += THREADS) cnt[b] = 0;
   __syncthreads();
-  const size_t base = (size_t)blockIdx.x * (THREADS * ITEMS);
+  const size_t base = (size_t)blockIdx.x * tl;  // (tl <= THREADS * ITEMS rows per tile)
   u64 v[ITEMS];
   u32 bk[ITEMS], r[ITEMS];
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
-    const size_t i = base + (size_t)k * THREADS + threadIdx.x;
+    const u32 t = (u32)k * THREADS + threadIdx.x;
+    const size_t i = t < tl ? base + t : n;
     const u64 tv = i < n ? __builtin_nontemporal_load(tcs + i) : TP_INVALID;
     const u32 h = i < n ? __builtin_nontemporal_load(hash + i) : 0u;
     bk[k] = B;  // none (an invalid row: the batch is rejected anyway)
@@ -2113,9 +2114,11 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   const int kb = xg.kb;
   const u32 cap = xg.cap;
   const u32 xt = (u32)((n + XP_TILE - 1) / XP_TILE);
-  static const int xf_shape = getenv("EVM_XF_SCATTER") ? atoi(getenv("EVM_XF_SCATTER")) : 0;
-  const u32 xf_tile = xf_shape == 0 ? 1024 * 12 : xf_shape == 1 ? 512 * 12 : 512 * 8;
-  const u32 xft = (u32)((n + xf_tile - 1) / xf_tile);
+  // scatter tiles of 12,288 rows (rounding the tile count up to whole rounds
+  // of the chip -- 1,024 tiles of 9,766 rows for 10M -- measured slower, 85
+  // vs 78-81 us: shorter bucket runs cost more than the last round's sliver)
+  const u32 xft = (u32)((n + 12287) / 12288);
+  const u32 xf_tl = 12288;
 
   // it reads only the timestamps, cells and K1's hashes: a second stream runs
   // it beside the walks, forked right after K1 (joined before the status
@@ -2177,11 +2180,8 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       // after the walk XORs its exact redeliveries out again)
       {
         evm::ProfScope ps_(ctx, "k_xf_scatter", xs);
-#define XF_SCATTER_ARGS hash, (const u64*)tcs, (const u64*)sb.tcs_far, cell, n, kb, cbits, cap, xcur, xpairs, sb.dx, sb.dc, info
-        if (xf_shape == 0) hipLaunchKernelGGL((k_xf_scatter<1024, 12>), dim3(xft), dim3(1024), 0, xs, XF_SCATTER_ARGS);
-        else if (xf_shape == 1) hipLaunchKernelGGL((k_xf_scatter<512, 12>), dim3(xft), dim3(512), 0, xs, XF_SCATTER_ARGS);
-        else hipLaunchKernelGGL((k_xf_scatter<512, 8>), dim3(xft), dim3(512), 0, xs, XF_SCATTER_ARGS);
-#undef XF_SCATTER_ARGS
+        hipLaunchKernelGGL((k_xf_scatter<1024, 12>), dim3(xft), dim3(1024), 0, xs, hash, (const u64*)tcs,
+                           (const u64*)sb.tcs_far, cell, n, kb, cbits, cap, xcur, xpairs, sb.dx, sb.dc, info, xf_tl);
       }
       evm::ProfScope ps_(ctx, "k_xf_dedup", xs);
       hipLaunchKernelGGL(k_xf_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, (const u64*)xpairs, (const u32*)xcur,
