@@ -1739,7 +1739,6 @@ __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ 
                                                           const u64* __restrict__ tcs_far,
                                                           const u32* __restrict__ cell, size_t n, int kb, int cbits,
                                                           u32 cap, u32* __restrict__ cursor, u64* __restrict__ out,
-                                                          u32* __restrict__ dx, u32* __restrict__ dc,
                                                           Info* __restrict__ info, u32 tl) {
   __shared__ u64 stage[(THREADS * ITEMS)];
   __shared__ uint16_t sbk[(THREADS * ITEMS)];      // the bucket of each staged pair
@@ -2181,7 +2180,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       {
         evm::ProfScope ps_(ctx, "k_xf_scatter", xs);
         hipLaunchKernelGGL((k_xf_scatter<1024, 12>), dim3(xft), dim3(1024), 0, xs, hash, (const u64*)tcs,
-                           (const u64*)sb.tcs_far, cell, n, kb, cbits, cap, xcur, xpairs, sb.dx, sb.dc, info, xf_tl);
+                           (const u64*)sb.tcs_far, cell, n, kb, cbits, cap, xcur, xpairs, info, xf_tl);
       }
       evm::ProfScope ps_(ctx, "k_xf_dedup", xs);
       hipLaunchKernelGGL(k_xf_dedup, dim3(1u << kb), dim3(XP_THREADS), 0, xs, (const u64*)xpairs, (const u32*)xcur,
