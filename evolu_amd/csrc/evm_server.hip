@@ -726,7 +726,12 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
         const v4u x = __builtin_nontemporal_load(row), y = __builtin_nontemporal_load(row + 1),
                   z = __builtin_nontemporal_load(row + 2);
         const u32 w[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w & 0xffffu};
+#if EVM_ABL_SV == 1  // (ablation builds only: no murmur3)
+        Parsed p = parse_ts46(w);
+        p.hash = w[5];
+#else
         const Parsed p = parse_ts46(w);
+#endif
         bad |= (p.meta & EVM_META_VALID) ? 0u : 1u;
         s_rh[t] = p.rh;  // (== node_ranks(p.node, case mask): the parse's SWAR ranks)
         s_rl[t] = p.rl;
@@ -861,6 +866,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     }
   }
   __syncthreads();
+#if EVM_ABL_SV != 2  // (ablation 2: no tie-run ordering)
   // runs of one tc: order by the node ranks (then position).  Each member
   // finds its run's bounds and counts the members below it, all in parallel
   // (runs are short: distinct nodes at one (millis, counter))
@@ -906,11 +912,16 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     }
   }
   __syncthreads();
+#endif
   // among equal timestamps the one first in the batch (smallest batch index)
   // is the candidate insert -- independent of the order the segment's
   // messages were listed in (key-range segments are gathered unordered).
   // s_cnt[p] = 1: p is its timestamp's candidate.  A run's first position
   // decides the whole run (O(run) per run).
+#if EVM_ABL_SV == 3  // (ablation: every position a candidate)
+  for (u32 p = threadIdx.x; p < m; p += THREADS) cnt_set(p, 1u);
+  if (false)
+#endif
   for (u32 p = threadIdx.x; p < m; p += THREADS) {
     const u64 kp = s_k[p];
     const u32 pp = (u32)(kp & PMASK);
