@@ -102,18 +102,31 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget per leg (0: skip)")
     ap.add_argument("--overlap", type=int, default=1, help="EVM_OPT_OVERLAP: independent checks on a second stream")
     ap.add_argument("--depth", type=int, default=4, help="config 2: batches in flight (evm_apply_batch_async)")
-    ap.add_argument("--workload", choices=["auto", "client", "server", "config4", "adversarial", "config5"], default="auto",
-                    help="auto: client at N=1, config4 at N>1; "
-                         "client: config 2 applyMessages (headline, + config 1, 3 and 4 legs at N=1); "
-                         "server: config 3/5 ingest + diff + select alone; "
-                         "config4: the sharded sync server (1B msgs / 1M owners at 8 GPUs, weak scaling)")
-    ap.add_argument("--radix", type=int, default=None, help="EVM_OPT_RADIX for --workload config5 (A/B of 10-bit digits)")
+    ap.add_argument("--workload", choices=["auto", "client", "server", "config4", "adversarial", "config5",
+                                           "config5c", "config5shape"], default="auto",
+                    help="auto: client at N=1, config4 (+ the config5 and config5c legs) at N>1; "
+                         "client: config 2 applyMessages (headline, + config 1, 3, 4 and 5-shape legs at N=1); "
+                         "server: config 3 (or --zipf) ingest + diff + select alone, one GPU; "
+                         "config4: the sharded sync server (1B msgs / 1M owners at 8 GPUs, weak scaling); "
+                         "config5: the sharded sync server on config 5's stream (Zipf 1.2 owners, hot owners split "
+                         "over every rank), self-checked; config5c: one owner's applyMessages batch split by cell, "
+                         "self-checked; config5shape: the config-5 stream on one GPU, unsharded (profiling)")
+    ap.add_argument("--radix", type=int, default=None,
+                    help="EVM_OPT_RADIX for --workload config5shape (A/B of 10-bit digits)")
+    ap.add_argument("--c5", type=int, default=1, help="N>1 default run: add the config5 and config5c legs")
+    ap.add_argument("--c5-owners", type=int, default=125_000, help="config5: owners per GPU")
+    ap.add_argument("--c5-messages", type=int, default=125_000_000, help="config5: messages per GPU")
+    ap.add_argument("--c5-sample", type=int, default=200, help="config5: cold owners per rank in the self-check")
+    ap.add_argument("--c5-share", type=float, default=0.1,
+                    help="config5: an owner above this share of one rank's fair share of rows is split")
+    ap.add_argument("--c5c-messages", type=int, default=10_000_000, help="config5c: messages per GPU")
+    ap.add_argument("--c5c-cells", type=int, default=1000, help="config5c: cells per GPU")
     ap.add_argument("--c4-owners", type=int, default=125_000, help="config4: owners per GPU")
     ap.add_argument("--c4-per-owner", type=int, default=1000, help="config4: messages per owner")
     ap.add_argument("--c4-sample", type=int, default=1000, help="config4: owners per rank in the self-check")
     ap.add_argument("--loopback", type=int, default=0,
-                    help="config4 rehearsal: N loopback ranks (threads) sharing GPU 0 through evm_dist_hub "
-                         "(not a multi-GPU measurement)")
+                    help="config4 (or --workload config5 / config5c) rehearsal: N loopback ranks (threads) sharing "
+                         "GPU 0 through evm_dist_hub (not a multi-GPU measurement)")
     ap.add_argument("--extra", type=int, default=1, help="N=1 client run: add the config-1 and config-3 legs")
     ap.add_argument("--shape", choices=["auto", "config2", "config4c"], default="auto",
                     help="client workload: config2 = one owner per GPU, no exchange; config4c = owners_per_rank "
@@ -229,7 +242,7 @@ def cpu_baseline_python(ts_arena, cells, budget_s):
     }, **host_info())
 
 
-def cpu_baseline_server(ts_np, owner_np, budget_s):
+def cpu_baseline_server(ts_np, owner_np, budget_s, what="config-3"):
     """apps/server/src/index.ts:121-216 restated in JavaScript
     (oracle/js/cpu_server.js: per SyncRequest getMerkleTree JSON.parse,
     INSERT OR IGNORE as a Set + persistent-spread inserts, the tree's
@@ -246,7 +259,9 @@ def cpu_baseline_server(ts_np, owner_np, budget_s):
     if node is None:
         return None
     hi = host_info()
-    P = max(1, min(hi["cpus_usable"], 16))  # the box's CPU share for one GPU is 16
+    # P = the host's CPU share of ONE GPU (16 on this pool's boxes, OMP_NUM_THREADS): each
+    # worker thread loads the whole sample, so P = nproc (256) would need P copies of it
+    P = max(1, min(hi["cpus_usable"], CPU_SHARE_PER_GPU))
     res = {}
     with tempfile.TemporaryDirectory() as d:
         for threads in sorted({1, P}):
@@ -262,14 +277,43 @@ def cpu_baseline_server(ts_np, owner_np, budget_s):
     r1 = res[1]
     out = dict({
         "value": r1["rate"], "unit": "msgs/s", "cores": 1, "kind": "port",
-        "sample": "the first %d SyncRequests (%d messages, one owner each) of the config-3 stream served by "
+        "sample": "the first %d SyncRequests (%d messages, one owner each) of the %s stream served by "
                   "oracle/js/cpu_server.js (index.ts getMerkleTree + addMessages + getMessages; SQL as Maps; "
-                  "persistent-spread trie; murmur3), 1 thread, %.1f s" % (r1["requests"], r1["done"], r1["seconds"]),
+                  "persistent-spread trie; murmur3), 1 thread, %.1f s" % (r1["requests"], r1["done"], what,
+                                                                          r1["seconds"]),
     }, **hi)
     if P > 1:
         rp = res[P]
         out["threads_%d" % P] = {"value": rp["rate"], "cores": P, "requests": rp["requests"], "messages": rp["done"],
-                                 "seconds": rp["seconds"], "sample": "worker_threads over disjoint owners (owner %% %d)" % P}
+                                 "seconds": rp["seconds"], "sample": "worker_threads over disjoint owners (owner %% %d)" % P,
+                                 "why_%d" % P: "the host's CPU share of one GPU on this pool (OMP_NUM_THREADS=16); "
+                                               "P = nproc is not run: every worker loads the whole sample"}
+    return out
+
+
+CPU_SHARE_PER_GPU = 16
+
+
+def cpu_baseline_server_n(world, budget_s, dev):
+    """The CPU baseline of an N-GPU server line (rank 0, after the timed legs):
+    cpu_server.js on a config-3-shaped stream (evs_config4_source with one
+    source: every message of the first owners, one SyncRequest per owner),
+    1 thread and the per-GPU CPU share; `per_node_share` states what N
+    shares of it would do (linear in threads: owners are disjoint)."""
+    from evolu_amd import synth
+
+    gen = synth.DeviceSynth()
+    K = 500 * (CPU_SHARE_PER_GPU + 1)
+    ts, owner, _ = gen.source(C4_SEED, K, 1000, 1, 0, dev)
+    out = cpu_baseline_server(ts.cpu().numpy(), owner.cpu().numpy().astype("uint32"), budget_s,
+                              what="config-3-shaped (%d owners x 1,000, device generator)" % K)
+    if out is not None:
+        tk = "threads_%d" % CPU_SHARE_PER_GPU
+        if tk in out:
+            out["per_node_share"] = {"gpus": world, "threads": world * CPU_SHARE_PER_GPU,
+                                     "value_extrapolated": world * out[tk]["value"],
+                                     "how": "%d x the %d-thread rate (disjoint owners scale linearly)"
+                                            % (world, CPU_SHARE_PER_GPU)}
     return out
 
 
@@ -335,29 +379,60 @@ def main():
     from evolu_amd.engine import Engine
 
     if a.loopback:
-        emit(config4_loopback(a, a.loopback))
+        if a.workload == "config5":
+            emit(config5_loopback(a, a.loopback))
+        elif a.workload == "config5c":
+            emit(client_split_loopback(a, a.loopback))
+        else:
+            emit(config4_loopback(a, a.loopback))
         return
     workload = a.workload if a.workload != "auto" else ("client" if world == 1 else "config4")
-    if workload == "config4":
-        eng = Engine(local)
-        dd = make_dist(eng, rank, world)
-        res = config4_rank(eng, dd, TorchComm(world, torch.device("cuda", local)), a.c4_owners, a.c4_per_owner,
-                           a.steps, a.warmup, a.c4_sample)
+    dev = torch.device("cuda", local)
+    if workload in ("config4", "config5", "config5c"):
+        comm = TorchComm(world, dev)
+
+        def leg(fn, *args):
+            eng = Engine(local)
+            dd = make_dist(eng, rank, world)
+            try:
+                return fn(eng, dd, comm, *args)
+            finally:
+                dd.free()
+                eng.close()
+                torch.cuda.empty_cache()
+
+        if workload == "config4":
+            res = leg(config4_rank, a.c4_owners, a.c4_per_owner, a.steps, a.warmup, a.c4_sample)
+            data = "synthetic (seeded HLC streams generated on the device, SURVEY 8(d) config 4)"
+        elif workload == "config5":
+            res = leg(config5_rank, a.c5_owners, a.c5_messages, a.steps, a.warmup, a.c5_sample, a.c5_share)
+            data = "synthetic (device generator evs_config5_shape, SURVEY 8(d) config 5)"
+        else:
+            res = leg(client_split_rank, a.c5c_messages, a.c5c_cells, a.steps, a.warmup)
+            data = "synthetic (synth.client_adversarial per slice, SURVEY 8(d) config 5, client side)"
+        extra = {}
+        if workload == "config4" and world > 1 and a.c5:
+            # BASELINE config 5 at the same N: the server on the Zipf stream with hot owners
+            # split, and one owner's client batch split by cell -- both self-checked
+            c5 = leg(config5_rank, a.c5_owners, a.c5_messages, min(a.steps, 5), min(a.warmup, 1), a.c5_sample,
+                     a.c5_share)
+            c5c = leg(client_split_rank, a.c5c_messages, a.c5c_cells, min(a.steps, 5), min(a.warmup, 1))
+            extra = {"config5": c5, "config5c": c5c}
         if rank == 0:
             out = {"metric": METRIC, "value": res.pop("value"), "unit": "msgs/s", "n_gpus": world,
                    "steps": a.steps, "warmup": a.warmup, "ms_per_step": res.pop("ms_per_step"),
                    "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-                   "data": "synthetic (seeded HLC streams generated on the device, SURVEY 8(d) config 4)",
-                   "cpu_baseline": None}
-            res.pop("steps"), res.pop("warmup")
+                   "data": data, "cpu_baseline": None}
+            res.pop("steps"), res.pop("warmup", None)
             out.update(res)
+            out.update(extra)
+            if a.cpu_seconds > 0 and workload != "config5c":
+                out["cpu_baseline"] = cpu_baseline_server_n(world, min(a.cpu_seconds, 10.0), dev)
             emit(out)
-        dd.free()
-        eng.close()
         if world > 1:
             dist.destroy_process_group()
         return
-    if workload == "config5":  # the config-5 shape leg alone (profiling)
+    if workload == "config5shape":  # the config-5 shape leg alone, one GPU (profiling)
         eng = Engine(local)
         if a.radix is not None:
             eng.set_option(4, a.radix)
@@ -728,6 +803,28 @@ class TorchComm:
 
         return int(self._reduce(x, torch.int64, dist.ReduceOp.MIN))
 
+    def sum_vec(self, v):
+        """Element-wise sum over ranks of an int64 vector (numpy in, numpy out)."""
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+
+        t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.int64)).to(self.dev)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.cpu().numpy()
+
+    def all_gather(self, t):
+        """Every rank's tensor (same shape on every rank) -> list in rank order (device to device)."""
+        import torch
+        import torch.distributed as dist
+
+        if self.world == 1:
+            return [t]
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t.contiguous())
+        return out
+
 
 class ThreadComm:
     """The same for loopback ranks (threads of one process, evm_dist_hub)."""
@@ -762,6 +859,23 @@ class ThreadComm:
 
             def min(self, x):
                 return comm._reduce(rank, x, min)
+
+            def sum_vec(self, v):
+                import numpy as np
+
+                return comm._reduce(rank, np.asarray(v, dtype=np.int64), lambda vs: np.sum(vs, axis=0))
+
+            def all_gather(self, t):
+                import torch
+
+                torch.cuda.current_stream().synchronize()  # t is complete before a peer copies it
+
+                def copies(vs):
+                    out = [x.clone() for x in vs]
+                    torch.cuda.current_stream().synchronize()  # (peers may free theirs after the barrier)
+                    return out
+
+                return comm._reduce(rank, t, copies)
 
         return R()
 
@@ -985,6 +1099,403 @@ def config4_loopback(a, world, device=0):
     res.pop("steps"), res.pop("warmup")
     out.update(res)
     return out
+
+
+C5_SEED = 0xE7010005  # seed = 0xE7010000 + config number
+
+
+def c5_nodes(seed, glob):
+    """Requester nodeId of every local slot (global owner ids, -1 unused):
+    rank 0's node q = 0 of the owner in the config-5 generator (evm_synth.hip
+    c5_message: H(seed, 2, owner, 0)), lower-case hex -- the same on every
+    rank, so a split owner's shares are filtered alike (NOT LIKE is
+    case-insensitive, index.ts:98-102).  -> uint8 [n, 16]."""
+    import numpy as np
+
+    from evolu_amd import synth
+
+    g = np.maximum(np.asarray(glob, dtype=np.int64), 0).astype(np.uint64)
+    return synth._hex16(synth._H(seed, 2, g, np.zeros_like(g))).astype(np.uint8)
+
+
+def _leaves_equal(ta, a, tb, b, count=1):
+    """Owners [a, a+count) of trees ta and [b, b+count) of tb hold identical leaf lists."""
+    import torch
+
+    oa, ca, xa = ta.slice_device(a, count)
+    ob, cb, xb = tb.slice_device(b, count)
+    return bool(torch.equal(oa, ob) and torch.equal(ca, cb) and torch.equal(xa, xb))
+
+
+def config5_rank(eng, dd, comm, owners_per_gpu=125_000, n_per_gpu=125_000_000, steps=5, warmup=1, sample=200,
+                 share=0.1, seed=C5_SEED, verbose=False):
+    """BASELINE config 5 on the server at N GPUs, through the C ABI the Node
+    caller uses (evolu_amd/sharded.py ShardedServer):
+    owners_per_gpu x world owners with Zipf(1.2) sizes, n_per_gpu messages
+    per rank's slice (1B over 1M owners at 8 GPUs, weak scaling): equal-millis
+    bursts on a 1-second grid, 1 % upper-case nodes, 10 % exact redeliveries,
+    shuffled (evm_synth.hip evs_config5_shape, seed + rank per slice; the job's
+    batch = the slices in rank order).
+
+    Setup (untimed): the directory murmur3(userId) mod world
+    (evm_dist_directory); the hot owners -- above `share` of one rank's fair
+    share of the job's rows -- found over all ranks (evm_dist_hot_owners) and
+    split over every rank by timestamp hash (evm_dist_split); one round routed
+    and ingested to learn what each owner's client knows (keep flag, first
+    copy); the client trees (a split owner's: every rank's part merged,
+    evm_dist_merge_trees).  One step = route (evm_dist_route + take, local
+    ids) + addMessages into an empty store (evm_server_ingest) + getMessages
+    (evm_server_select; split owners: full-tree diffs, each rank's share after
+    the bound, shares merged in timestamp order by evm_dist_merge_select) +
+    every owner's root all-gathered (evm_dist_gather_roots XORs the split
+    owners' partial roots).
+
+    Self-check (after the timed steps): every rank regenerates every slice,
+    keeps the rows of a sample of its cold owners and of EVERY split owner, in
+    global batch order, and recomputes them unsharded on one store of this
+    GPU: inserted counts (a split owner's summed over ranks), roots (as
+    all-gathered), diffs, the split owners' full trees, and the selected rows
+    byte for byte (a split owner's merged list: each rank checks the entries
+    that came from its own rows, every rank the count) -> parity_checked,
+    agreed over the ranks."""
+    import numpy as np
+    import torch
+
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+    from evolu_amd.sharded import ShardedServer
+
+    rank, world = dd.rank, dd.world
+    dev = torch.device("cuda", eng.device)
+    O = owners_per_gpu * world
+    gen = synth.DeviceSynth()
+    t_setup = time.perf_counter()
+    ids = gen.owner_ids(seed, O, dev)
+    srv = ShardedServer(eng, dd, ids, 21)
+    del ids
+    ts_in, owner_in, keep_in = synth.device_config5_shape(gen, seed + rank, O, n_per_gpu, dev)
+    hot = srv.split_hot(owner_in, share=share)
+    nh, base = int(hot.size), srv.hot_base
+    n_local = srv.n_local
+    # what each owner's client knows: its kept messages, each once (the first copy inserted)
+    n_r = dd.route(ts_in, owner_in, aux=keep_in.to(torch.int32))
+    t_r, o_r, k_r, _, _ = dd.take(src=False)
+    first = eng.store_new(n_local)
+    ins, _ = first.ingest(t_r, o_r, 0)
+    first.free()
+    known = (k_r != 0) & ((ins[:n_r] & L.MSG_INS) != 0)
+    partial = eng.merkle_insert(eng.tree_new(n_local), t_r[known].contiguous(), o_r[known].contiguous())
+    del t_r, o_r, k_r, ins, known, keep_in
+    client = srv.client_trees(partial)
+    if client is not partial:
+        partial.free()
+    glob = srv.local_owners().cpu().numpy()
+    node = torch.from_numpy(c5_nodes(seed, glob).reshape(-1).copy()).to(dev)
+    out = (torch.empty((max(n_r, 1), 48), dtype=torch.uint8, device=dev),
+           torch.empty(max(n_r, 1), dtype=torch.int32, device=dev), None, None)
+    flags = torch.empty(max(n_r, 1), dtype=torch.uint8, device=dev)
+    id_base = rank << 40
+    torch.cuda.synchronize(dev)
+    setup_s = time.perf_counter() - t_setup
+    route_ms = []
+    last = {}
+
+    def step():
+        r0 = time.perf_counter()
+        t, o = srv.route(ts_in, owner_in, out=out)
+        route_ms.append((time.perf_counter() - r0) * 1e3)
+        srv.new_store()
+        srv.store.ingest(t, o, id_base, flags=flags)
+        sel = srv.select(client, node)
+        if nh:
+            diff, (off, sid), (hoff, hid) = sel
+        else:
+            (diff, off, sid), hoff, hid = sel, None, None
+        root, present = srv.roots()
+        last.update(n=t.shape[0], diff=diff, off=off, sid=sid, hoff=hoff, hid=hid, root=root, present=present)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.prof_enable(True)
+    eng.prof_reset()
+    step()
+    torch.cuda.synchronize(dev)
+    prof = eng.prof_report()
+    alg_all = dict(DIST_ALG, **SERVER_ALG)
+    dom = dominant(prof, alg_all)
+    eng.prof_only(dom)
+    eng.prof_reset()
+    route_ms.clear()
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step()
+        if verbose:
+            print("rank %d config5 step %d" % (rank, k), file=sys.stderr, flush=True)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    prof_dom = eng.prof_report()
+    eng.prof_enable(False)
+    eng.prof_only(None)
+    elapsed = comm.max(t1 - t0)
+    route_avg = comm.max(sum(route_ms) / max(1, len(route_ms)))
+    n_recv_max = int(comm.max(float(last["n"])))
+
+    # ---- self-check: sampled cold owners + every split owner, unsharded on this GPU
+    t_chk = time.perf_counter()
+    n = last["n"]
+    cold = np.flatnonzero(glob[:base] >= 0)
+    pick = cold[np.unique(np.linspace(0, len(cold) - 1, min(sample, len(cold))).round().astype(np.int64))] \
+        if len(cold) else np.zeros(0, dtype=np.int64)
+    chk_local = np.concatenate([pick, base + np.arange(nh)]).astype(np.int64)
+    chk_glob = glob[chk_local]
+    order = np.argsort(chk_glob, kind="stable")
+    k = len(order)
+    loc_sorted = chk_local[order]  # local id of ref owner q (ref owners = the checked globals, sorted)
+    g_sorted = torch.from_numpy(chk_glob[order].astype(np.int32)).to(dev)
+    rows, own, kp = [], [], []
+    for s_ in range(world):  # the job's batch: the slices in rank order
+        t_s, o_s, k_s = synth.device_config5_shape(gen, seed + s_, O, n_per_gpu, dev)
+        m = torch.isin(o_s, g_sorted)
+        rows.append(t_s[m])
+        own.append(o_s[m])
+        kp.append(k_s[m])
+        del t_s, o_s, k_s, m
+    rows, own, kp = torch.cat(rows), torch.cat(own), torch.cat(kp)
+    j = torch.searchsorted(g_sorted, own).to(torch.int32).contiguous()
+    ref = eng.store_new(max(k, 1))
+    f_ref, st_ref = ref.ingest(rows, j, 0)
+    known = (kp != 0) & ((f_ref & L.MSG_INS) != 0)
+    client_ref = eng.merkle_insert(eng.tree_new(max(k, 1)), rows[known].contiguous(), j[known].contiguous())
+    node_ref = node.view(-1, 16)[torch.from_numpy(loc_sorted).to(dev)].reshape(-1).contiguous()
+    diff_ref, off_ref, sel_ref = ref.select(client_ref, node_ref)
+    r_ref, p_ref = ref.tree().roots()
+    ins_ref = torch.bincount(j[(f_ref & L.MSG_INS) != 0].to(torch.int64), minlength=max(k, 1)).cpu().numpy()
+    ins_big = torch.bincount(out[1][:n][(flags[:n] & L.MSG_INS) != 0].to(torch.int64),
+                             minlength=n_local).cpu().numpy()
+    ins_hot = comm.sum_vec(ins_big[base:base + nh])  # (collective) a split owner's inserts over every rank
+    ins_big = ins_big.copy()
+    ins_big[base:base + nh] = ins_hot
+    ok_ins = bool(st_ref == 0 and np.array_equal(ins_big[loc_sorted], ins_ref[:k]))
+    g64 = torch.from_numpy(chk_glob[order].astype(np.int64)).to(dev)
+    ok_root = bool(np.array_equal(last["root"][g64].cpu().numpy(), r_ref[:k]) and
+                   np.array_equal(last["present"][g64].cpu().numpy(), p_ref[:k]))
+    ok_diff = bool(torch.equal(last["diff"][torch.from_numpy(loc_sorted).to(dev)], diff_ref[:k]))
+    # the split owners' full trees (collective), leaf for leaf
+    full = dd.merge_trees(srv.store.tree(), base, nh) if nh else None
+    ok_tree = all(_leaves_equal(full, h, ref.tree(), int(np.searchsorted(chk_glob[order], hot[h])))
+                  for h in range(nh))
+    if full is not None:
+        full.free()
+    # selections: a cold owner's rows are all here; a split owner's merged
+    # list holds every rank's rows -- this rank checks the ones it holds
+    off_ref_np = off_ref.cpu().numpy()
+    ok_sel, n_sel = True, 0
+    mask40 = (1 << 40) - 1
+    for q in range(k):
+        lq = int(loc_sorted[q])
+        want = sel_ref[int(off_ref_np[q]):int(off_ref_np[q + 1])]
+        n_sel += int(want.numel())
+        if lq < base:
+            a_, b_ = int(last["off"][lq]), int(last["off"][lq + 1])
+            got = last["sid"][a_:b_]
+            if got.numel() != want.numel():
+                ok_sel = False
+                continue
+            if got.numel() and not torch.equal(out[0][got - id_base][:, :46], rows[want][:, :46]):
+                ok_sel = False
+        else:
+            h = lq - base
+            a_, b_ = int(last["hoff"][h]), int(last["hoff"][h + 1])
+            got = last["hid"][a_:b_]
+            if got.numel() != want.numel():
+                ok_sel = False
+                continue
+            mine = (got >> 40) == rank
+            if bool(mine.any()) and not torch.equal(out[0][got[mine] & mask40][:, :46], rows[want[mine]][:, :46]):
+                ok_sel = False
+    ok = ok_ins and ok_root and ok_diff and ok_tree and ok_sel
+    detail = {"sample_owners": int(len(pick)), "split_owners_checked": nh, "rows_checked": int(rows.shape[0]),
+              "inserted": ok_ins, "roots": ok_root, "diffs": ok_diff, "split_trees": ok_tree, "selections": ok_sel,
+              "selected_rows": n_sel, "check_s": time.perf_counter() - t_chk}
+    ref.free()
+    client_ref.free()
+    del rows, own, kp, j, f_ref, known
+    parity = comm.min(1 if ok else 0) == 1
+    ms = elapsed / steps * 1e3
+    tot_ms, launches = prof_dom[dom]
+    avg_s = tot_ms / launches / 1e3
+    if dom in DIST_ALG:
+        alg = DIST_ALG[dom] * n
+    else:
+        per_msg, per_leaf = SERVER_ALG[dom]
+        alg = per_msg * n + per_leaf * srv.store.tree().n_leaves
+    res = {
+        "value": world * n_per_gpu * steps / elapsed, "ms_per_step": ms, "steps": steps, "warmup": warmup,
+        "config": {"workload": "config5: sync server (index.ts:138-202 addMessages + getMessages), %d msgs over %d "
+                               "owners (%d msgs / %d owners per GPU, weak scaling: 1B over 1M at 8 GPUs), owner sizes "
+                               "Zipf(1.2), equal-millis bursts, 1 %% upper-case nodes, 10 %% exact redeliveries, "
+                               "shuffled; owners by murmur3(userId) mod %d (evm_dist_directory), %d hot owners "
+                               "(> %.2f of a rank's fair share) split over every rank by timestamp hash "
+                               "(evm_dist_hot_owners/split), routed over %s (evm_dist_route), getMessages with "
+                               "full-tree diffs and merged selections (evm_dist_merge_trees/merge_select), roots "
+                               "all-gathered" % (n_per_gpu * world, O, n_per_gpu, owners_per_gpu, world, nh, share,
+                                                 dd.transport),
+                   "messages_per_gpu": n_per_gpu, "owners_total": O, "owners_per_gpu": owners_per_gpu,
+                   "split_owners": [int(x) for x in hot[:16]], "n_split_owners": nh,
+                   "rows_received_this_rank": int(n), "rows_received_max_rank": n_recv_max,
+                   "parallelism": "owner-sharded (murmur3 mod %d) + hot owners split by timestamp hash, %s"
+                                  % (world, dd.transport)},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": alg / avg_s / HBM_PEAK, "traffic": traffic_of(dom, "config5n"),
+                     "kernel_ms_avg": avg_s * 1e3, "alg_bytes_per_launch": alg,
+                     "kernel_share_of_step": tot_ms / (ms * steps)},
+        "pipeline": {"alg_bytes_per_msg": SERVER_PIPELINE_BYTES,
+                     "pipeline_hbm_frac": SERVER_PIPELINE_BYTES * n_per_gpu / (elapsed / steps) / HBM_PEAK,
+                     "kernels_ms_per_step": {kk: v[0] for kk, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:16]}},
+        "route": {"ms_per_step": route_avg, "bytes_per_msg": ROUTE_BYTES,
+                  "imbalance_max_over_mean": n_recv_max / max(1.0, n_per_gpu)},
+        "parity_checked": parity, "self_check_rank%d" % rank: detail, "setup_s": setup_s,
+    }
+    srv.close()
+    client.free()
+    del ts_in, owner_in, out, flags
+    return res
+
+
+def config5_loopback(a, world, device=0):
+    """config5_rank on `world` loopback ranks sharing one GPU (evm_dist_hub):
+    the directory, hot-owner split, exchange, merged selections and gathers
+    run exactly as at N GPUs -- a correctness rehearsal, never a scaling number."""
+    from evolu_amd.engine import run_loopback
+
+    comm = ThreadComm(world)
+
+    def fn(r, eng, dd):
+        try:
+            return config5_rank(eng, dd, comm.bind(r), a.c5_owners, a.c5_messages, a.steps, a.warmup, a.c5_sample,
+                                a.c5_share)
+        except BaseException:
+            comm.bar.abort()
+            raise
+
+    results = run_loopback(world, fn, device)
+    res = results[0]
+    for r in range(1, world):
+        res.update({k: v for k, v in results[r].items() if k.startswith("self_check_rank")})
+    out = {"metric": METRIC + " [loopback rehearsal, not a multi-GPU measurement]", "value": res.pop("value"),
+           "unit": "msgs/s", "n_gpus": 1, "loopback_ranks": world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": res.pop("ms_per_step"), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "u64", "data": "synthetic (device generator evs_config5_shape, SURVEY 8(d) config 5)",
+           "cpu_baseline": None}
+    res.pop("steps"), res.pop("warmup")
+    out.update(res)
+    return out
+
+
+def client_split_rank(eng, dd, comm, n_per_gpu=10_000_000, cells_per_gpu=1000, steps=5, warmup=1, seed=5):
+    """BASELINE config 5 on the client at N GPUs: ONE owner's applyMessages
+    batch (applyMessages.ts:26-131) of world x n_per_gpu messages over
+    world x cells_per_gpu cells with config 5's adversarial structure
+    (synth.client_adversarial per slice: equal-millis bursts, stale and exact
+    redeliveries, upper-case nodes), each rank holding its slice, split over
+    the ranks by cell through the C ABI (sharded.split_apply: the global PK
+    check by timestamp hash, every cell's rows on its rank in batch order,
+    flags back to the source rows, global winners, the partial trees merged).
+    Self-check: the whole batch gathered and applied unsharded on this GPU --
+    this slice's flags, every winner and the tree, leaf for leaf."""
+    import numpy as np
+    import torch
+
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+    from evolu_amd.sharded import split_apply
+
+    rank, world = dd.rank, dd.world
+    dev = torch.device("cuda", eng.device)
+    C = cells_per_gpu * world
+    t_setup = time.perf_counter()
+    ts_np, cell_np = synth.client_adversarial(n_per_gpu, C, seed_config=seed + 1000 * rank)
+    ts, cell = eng.dev(ts_np), eng.dev(cell_np.view(np.int32))
+    del ts_np, cell_np
+    empty = eng.tree_new(1)
+    setup_s = time.perf_counter() - t_setup
+    last = {}
+
+    def step(keep=False):
+        flags, winner, tree, st = split_apply(eng, dd, ts, cell, C, tree_in=empty)
+        if st != L.EVM_OK:
+            raise RuntimeError("split_apply status %d" % st)
+        if keep:
+            last.update(flags=flags, winner=winner, tree=tree)
+        else:
+            tree.free()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.prof_enable(True)
+    eng.prof_reset()
+    step()
+    torch.cuda.synchronize(dev)
+    prof = eng.prof_report()
+    eng.prof_enable(False)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    elapsed = comm.max(time.perf_counter() - t0)
+    step(keep=True)
+    # ---- self-check: the whole batch, unsharded
+    all_ts = torch.cat(comm.all_gather(ts))
+    all_cell = torch.cat(comm.all_gather(cell))
+    f_ref, w_ref, t_ref, st_ref = eng.apply_batch(eng.tree_new(1), all_ts, all_cell, C, raise_on_error=False)
+    ok_st = st_ref == L.EVM_OK
+    ok_flags = ok_st and bool(torch.equal(last["flags"], f_ref[rank * n_per_gpu:(rank + 1) * n_per_gpu]))
+    ok_win = ok_st and bool(torch.equal(last["winner"], w_ref.to(torch.int64)))
+    ok_tree = ok_st and _leaves_equal(last["tree"], 0, t_ref, 0)
+    last["tree"].free()
+    if t_ref is not None:
+        t_ref.free()
+    ok = ok_flags and ok_win and ok_tree
+    parity = comm.min(1 if ok else 0) == 1
+    ms = elapsed / steps * 1e3
+    return {"config": {"workload": "config5-C: applyMessages of ONE owner's batch of %d msgs (%d per GPU) over %d "
+                                   "cells, equal-millis bursts + stale/exact redeliveries + upper-case nodes "
+                                   "(synth.client_adversarial per slice), split over %d rank(s) by cell through "
+                                   "evm_dist_* (global PK check by timestamp hash, flags returned to the source rows, "
+                                   "winners and tree merged)" % (n_per_gpu * world, n_per_gpu, C, world),
+                       "messages_per_gpu": n_per_gpu, "cells_total": C,
+                       "parallelism": "one owner split by cell over %d rank(s), %s" % (world, dd.transport)},
+            "value": world * n_per_gpu * steps / elapsed, "unit": "msgs/s", "ms_per_step": ms, "steps": steps,
+            "setup_s": setup_s,
+            "kernels_ms_per_step": {kk: v[0] for kk, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:12]},
+            "parity_checked": parity,
+            "self_check_rank%d" % rank: {"flags": ok_flags, "winners": ok_win, "tree": ok_tree,
+                                         "batch_rows": int(all_ts.shape[0])}}
+
+
+def client_split_loopback(a, world, device=0):
+    from evolu_amd.engine import run_loopback
+
+    comm = ThreadComm(world)
+
+    def fn(r, eng, dd):
+        try:
+            return client_split_rank(eng, dd, comm.bind(r), a.c5c_messages, a.c5c_cells, a.steps, a.warmup)
+        except BaseException:
+            comm.bar.abort()
+            raise
+
+    results = run_loopback(world, fn, device)
+    res = results[0]
+    for r in range(1, world):
+        res.update({k: v for k, v in results[r].items() if k.startswith("self_check_rank")})
+    return dict(res, metric=METRIC + " [client config 5 split, loopback rehearsal]", loopback_ranks=world)
 
 
 def adversarial_leg(eng, a):
@@ -1297,105 +1808,53 @@ def reingest(eng, a, ts1, own1, owners, per_owner, request, flags):
 
 
 def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=False, leg=False):
-    """Config 3 (1 GPU) / config 4 (N GPUs): server ingest of `owners x
-    per_owner` messages per GPU into an empty store, then getMessages for every
-    owner against a client tree built from the owner's first 90% of
+    """Config 3 (or the Zipf stream with --zipf) on ONE GPU: server ingest of
+    `owners x per_owner` messages into an empty store, then getMessages for
+    every owner against a client tree built from the owner's first 90% of
     messages.  With one request per owner per batch (request >= per_owner)
-    this is the reference's per-request sync (index.ts:204-216) exactly.
-    With N ranks every rank receives messages for random owners of the whole
-    job and routes them to the owner's rank (all_to_all over RCCL); roots
-    are all-gathered.  One step = route + ingest + select + roots."""
+    this is the reference's per-request sync (index.ts:204-216) exactly.  One
+    step = ingest + select + roots.  (N GPUs: --workload config4 / config5,
+    the sharded server through evm_dist_*.)"""
     import numpy as np
     import torch
-    import torch.distributed as dist
 
-    from evolu_amd import dist as D
     from evolu_amd import synth
     from evolu_amd.engine import Engine
 
-    O_total = owners * world
+    if world > 1:
+        raise SystemExit("--workload server runs on one GPU; at N GPUs use --workload config4 or config5")
     if zipf > 0:
         ts_np, owner_np, _, millis = synth.config5(owners, owners * per_owner, zipf_s=zipf,
                                                    seed_config=5 + 1000 * rank, with_millis=True)
     else:
         ts_np, owner_np, millis = synth.config3(owners, per_owner, seed_config=3 + 1000 * rank, request=request)
-    ts_local_np, owner_local_np = ts_np, owner_np
-    # this rank's owner o is job owner o*world + (o+rank)%world: every rank
-    # receives messages for owners living on every rank, no owner on two sources
-    o64 = owner_np.astype(np.int64)
-    owner_np = o64 * world + (o64 + rank) % world
     eng = Engine(local)
     dev = torch.device("cuda", local)
-    ts = eng.dev(ts_np)
-    owner = torch.from_numpy(owner_np).to(dev)
-    # owners too big for one rank (Zipf) are split over the ranks by timestamp hash
-    hot = D.hot_owners(D.owner_counts(owner, O_total), world) if (world > 1 and zipf > 0) else None
-    omap = D.OwnerMap(O_total, world, rank, hot)
-    n_local_owners = omap.n_local
-    dest = omap.dest(owner, ts).to(torch.uint8).contiguous() if world > 1 else None
-    dd = make_dist(eng, rank, world) if world > 1 else None
-    owner32 = owner.to(torch.int32).contiguous()
-
-    def route(rows):
-        """evm_dist_route + take: rows to their owner's rank (hot owners: by timestamp hash)."""
-        if world == 1:
-            return rows, owner
-        dd.route(rows, owner32, dest=dest)
-        t_r, o_r, _, _, _ = dd.take(aux=False, src=False)
-        return t_r, o_r.to(torch.int64)
-
-    ts_r, own_r = route(ts)
-    lown = omap.local(own_r).contiguous()
+    ts_r = eng.dev(ts_np)
+    lown = torch.from_numpy(owner_np.astype(np.int32)).to(dev)
     # client trees: each owner's messages minus the newest 10% (the expected diff)
     # (SURVEY 8(d) config 3: the client knows each owner's first 90% by timestamp)
+    o64 = owner_np.astype(np.int64)
     order = np.lexsort((millis, o64))
     rank_in_owner = np.empty(len(order), dtype=np.int64)
     counts = np.bincount(o64, minlength=owners)
     rank_in_owner[order] = np.arange(len(order)) - (np.cumsum(counts) - counts)[o64[order]]
-    keep_np = (rank_in_owner < (0.9 * counts[o64]).astype(np.int64)).astype(np.uint8)
-    if world > 1:  # route the flag with its message (an extra 8-byte column)
-        ext = np.concatenate([ts_np, np.repeat(keep_np[:, None], 8, 1)], 1)
-        keep = route(torch.from_numpy(ext).to(dev))[0][:, ts_np.shape[1]].bool()
-    else:
-        keep = torch.from_numpy(keep_np).to(dev).bool()
+    keep = torch.from_numpy(rank_in_owner < (0.9 * counts[o64]).astype(np.int64)).to(dev)
     if zipf > 0:  # redeliveries: the client's tree holds each known message once
-        first = eng.store_new(n_local_owners)
+        first = eng.store_new(owners)
         ins, _ = first.ingest(ts_r, lown, 0)
         keep &= (ins[: len(ts_r)] & 0x04) != 0
         first.free()
-    client = eng.merkle_insert(eng.tree_new(n_local_owners), ts_r[keep].contiguous(), lown[keep].contiguous())
-    client_hot = None
-    if omap.hot.numel():
-        # a split owner's request carries its FULL client tree: merge the ranks' parts
-        client_hot = D.merge_hot_trees(eng, client, omap)
-    node = torch.from_numpy(np.frombuffer(b"0123456789abcdef" * n_local_owners, dtype=np.uint8).copy()).to(dev)
+    client = eng.merkle_insert(eng.tree_new(owners), ts_r[keep].contiguous(), lown[keep].contiguous())
+    node = torch.from_numpy(np.frombuffer(b"0123456789abcdef" * owners, dtype=np.uint8).copy()).to(dev)
     flags = torch.empty(len(ts_r), dtype=torch.uint8, device=dev)
-    id_base = rank << 40  # globally unique message ids (split owners' selections merge across ranks)
 
     def step():
-        if world > 1:
-            t_r, o_r = route(ts)
-            lo = omap.local(o_r).contiguous()
-        else:
-            t_r, lo = ts_r, lown
-        store = eng.store_new(n_local_owners)
-        store.ingest(t_r, lo, id_base, flags=flags)
-        if client_hot is None:
-            diff, off, ids = store.select(client, node)
-            nsel = int(ids.numel())
-        else:
-            diff, (off, ids), (hoff, hids) = D.split_get_messages(eng, store, client, client_hot, node, omap)
-            nsel = int(ids.numel()) + int(hids.numel())
-        if world > 1:
-            if omap.hot.numel():
-                r, p = store.tree().roots()
-                rt, pt = torch.from_numpy(r).to(dev), torch.from_numpy(p).to(dev)
-                D.gather_roots(rt[: omap.per], pt[: omap.per], O_total)
-                D.gather_hot_roots(rt, pt, omap)
-            else:
-                dd.gather_roots(store.tree(), O_total)  # device to device (RCCL all-gather)
-        else:
-            store.tree().roots()
+        store = eng.store_new(owners)
+        store.ingest(ts_r, lown, 0, flags=flags)
+        diff, off, ids = store.select(client, node)
+        nsel = int(ids.numel())
+        store.tree().roots()
         n_leaves = store.tree().n_leaves
         store.free()
         return nsel, n_leaves
@@ -1412,8 +1871,6 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
     dom = dominant(prof, SERVER_ALG)
     eng.prof_only(dom)
     eng.prof_reset()
-    if world > 1:
-        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     nsel = n_leaves = 0
@@ -1433,10 +1890,7 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
     prof_dom = eng.prof_report()
     eng.prof_enable(False)
     eng.prof_only(None)
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = t1 - t0
     n = owners * per_owner
     ms = elapsed / a.steps * 1e3
     tot_ms, launches = prof_dom[dom]
@@ -1449,15 +1903,15 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
             "kernel_share_of_step": tot_ms / (ms * a.steps)}
     reqs = "one SyncRequest per owner" if request >= per_owner else "requests of %d" % request
     out = {
-        "metric": METRIC, "value": world * n * a.steps / elapsed, "unit": "msgs/s", "n_gpus": world,
+        "metric": METRIC, "value": n * a.steps / elapsed, "unit": "msgs/s", "n_gpus": 1,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic (seeded HLC streams, SURVEY 8(d) config 3/4/5)",
-        "config": {"workload": ("server: addMessages + getMessages, %d owners x %d msgs per GPU, %s, RCCL owner routing"
+        "config": {"workload": ("server: addMessages + getMessages, %d owners x %d msgs, %s"
                                 % (owners, per_owner, reqs)) if zipf <= 0 else
-                   ("server config 5: addMessages + getMessages, %d msgs per GPU over %d owners with Zipf(%.2f) sizes, "
-                    "hot owners split over ranks" % (n, owners, zipf)),
+                   ("server, Zipf stream: addMessages + getMessages, %d msgs over %d owners with Zipf(%.2f) sizes"
+                    % (n, owners, zipf)),
                    "messages_per_gpu": n, "owners_per_gpu": owners,
-                   "selected_rows_rank0": nsel, "parallelism": "owner-sharded, %d rank(s)" % world},
+                   "selected_rows": nsel, "parallelism": "one GPU"},
         "roofline": roof,
         "pipeline": {"alg_bytes_per_msg": SERVER_PIPELINE_BYTES,
                      "pipeline_hbm_frac": SERVER_PIPELINE_BYTES * n / (elapsed / a.steps) / HBM_PEAK,
@@ -1469,15 +1923,13 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
     if leg:
         for k in ("metric", "n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
             out.pop(k)
-    if world == 1 and zipf <= 0:
+    if zipf <= 0:
         out["reingest"] = reingest(eng, a, ts_r, lown, owners, per_owner, request, flags)
-    if dd is not None:
-        dd.free()
     eng.close()
-    del ts, owner, ts_r, lown, keep, client, flags
+    del ts_r, lown, keep, client, flags
     torch.cuda.empty_cache()
     if cpu and a.cpu_seconds > 0 and zipf <= 0:
-        out["cpu_baseline"] = cpu_baseline_server(ts_local_np, owner_local_np, min(a.cpu_seconds, 10.0))
+        out["cpu_baseline"] = cpu_baseline_server(ts_np, owner_np, min(a.cpu_seconds, 10.0))
     return out
 
 

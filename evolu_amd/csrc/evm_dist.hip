@@ -245,7 +245,10 @@ constexpr u32 PK_VALID = 1u << 16;
 // count words exchanged per route: the row count in the low bits, flags on top
 constexpr u64 CNT_ERR = 1ull << 63;      // the sending rank failed locally (nothing is exchanged)
 constexpr u64 CNT_INVALID = 1ull << 62;  // the sending rank holds a row outside the native domain
+constexpr u64 CNT_RAW = 1ull << 61;      // the sending rank cannot send packed records (its stride / alignment)
 constexpr u64 CNT_MASK = (1ull << 48) - 1;
+constexpr int CNT_STRIDE_SHIFT = 48;       // stride / 8 in bits 48..57: raw records need one stride on every rank
+constexpr u64 CNT_STRIDE_MAX = 1023;
 // d->cnt layout (u64 words, mirrored in pinned host memory)
 constexpr u32 W_SEND = 0;                      // [64] send counts
 constexpr u32 W_RECV = MAX_BUCKETS;            // [64] receive counts
@@ -462,10 +465,16 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
         m = reinterpret_cast<const uint4*>(src)[1];
         u32 w[12];
         format_ts46((u64)a.x | ((u64)a.y << 32), (u64)a.z | ((u64)a.w << 32), m.w & 0xffffu, w);
-        uint4* dst = reinterpret_cast<uint4*>(out_ts + pos * out_stride);
-        dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-        dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
-        dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
+        if (packed == 1) {
+          uint4* dst = reinterpret_cast<uint4*>(out_ts + pos * out_stride);
+          dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+          dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+          dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
+        } else {  // an output row only 8-B aligned
+          uint2* dst = reinterpret_cast<uint2*>(out_ts + pos * out_stride);
+#pragma unroll
+          for (int k = 0; k < 6; ++k) dst[k] = make_uint2(w[2 * k], w[2 * k + 1]);
+        }
       } else {
         copy_row(out_ts + pos * out_stride, src, stride);
         m = *reinterpret_cast<const uint4*>(src + stride);
@@ -498,10 +507,10 @@ __global__ void k_dist_totals(const u32* __restrict__ offs, const u32* __restric
 }
 
 // the count words this rank sends: counts (or zeros) plus the flag bits
-__global__ void k_dist_mark(u64* __restrict__ cnt, u32 G, int zero, int err, const u32* __restrict__ flags) {
+__global__ void k_dist_mark(u64* __restrict__ cnt, u32 G, int zero, int err, const u32* __restrict__ flags, u64 bits) {
   const u32 p = threadIdx.x;
   if (p >= G) return;
-  u64 v = zero ? 0ull : cnt[p];
+  u64 v = (zero ? 0ull : cnt[p]) | bits;
   if (err) v |= CNT_ERR;
   if (flags && flags[1]) v |= CNT_INVALID;
   cnt[p] = v;
@@ -1045,9 +1054,12 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   d->n_recv = 0;
   const u32 G = (u32)d->world;
   int lerr = EVM_OK;  // a local failure: the rank still joins the count exchange, flagged
-  if (stride < 46 || stride % 8 || (n && (!ts || !owner)) || n >= 0xffffffffull) lerr = EVM_EINVAL;
-  // 48-B rows, 16-B aligned: packed 32-B records (a third of the xGMI bytes of raw ones)
-  const bool packed0 = !lerr && stride == 48 && ((uintptr_t)ts & 15) == 0;
+  if (stride < 46 || stride % 8 || stride / 8 > CNT_STRIDE_MAX || (n && (!ts || !owner)) || n >= 0xffffffffull)
+    lerr = EVM_EINVAL;
+  // 48-B rows, 16-B aligned: packed 32-B records (a third of the xGMI bytes of
+  // raw ones).  Every rank must use one record format: a rank that cannot
+  // pack says so in its count words (CNT_RAW) and then every rank sends raw.
+  const bool packed0 = !lerr && stride == 48 && (n == 0 || ((uintptr_t)ts & 15) == 0);
   size_t rb = packed0 ? PACKED : stride + META;
   Scratch S(ctx);
   u32* flags = S.alloc<u32>(2);  // [0] a destination out of range, [1] a row outside the native domain
@@ -1072,8 +1084,9 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
     }
   }
   // the counts: one all-to-all of G words (flag bits on top), one read back
+  const u64 fmt = (packed0 ? 0ull : CNT_RAW) | ((u64)(lerr ? 0 : stride / 8) << CNT_STRIDE_SHIFT);
   KLAUNCH(k_dist_mark, dim3(1), dim3(MAX_BUCKETS), scnt, G, (lerr || !n) ? 1 : 0, lerr ? 1 : 0,
-          (const u32*)(lerr ? nullptr : flags));
+          (const u32*)(lerr ? nullptr : flags), fmt);
   int st = d->tx->all_to_all_u64(scnt, rcnt, ctx->stream);
   if (st) return st;
   if (!lerr) {
@@ -1085,16 +1098,23 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   HIPR(hipStreamSynchronize(ctx->stream));
   const u64* hs = d->hcnt + W_SEND;
   const u64* hr = d->hcnt + W_RECV;
-  bool any_err = lerr != EVM_OK, any_inv = false;
+  bool any_err = lerr != EVM_OK, any_inv = false, any_raw = false, mixed_stride = false;
   for (u32 p = 0; p < G; ++p) {
     any_err |= (hr[p] & CNT_ERR) != 0;
     any_inv |= (hr[p] & CNT_INVALID) != 0;
+    any_raw |= (hr[p] & CNT_RAW) != 0;
+    mixed_stride |= ((hr[p] >> CNT_STRIDE_SHIFT) & CNT_STRIDE_MAX) != stride / 8;
   }
   if (any_err) return lerr ? lerr : EVM_EDIST;  // every rank saw the flag: nobody exchanges
   const bool bad_dest = d->hcnt[W_BAD] != 0;
-  // a row outside the native domain anywhere: every rank sends raw records
-  // (the packed form cannot carry the original bytes); same slots, wider records
-  const bool packed = packed0 && !any_inv;
+  // a row outside the native domain anywhere, or a rank that cannot pack:
+  // every rank sends raw records (the packed form cannot carry the original
+  // bytes); same slots, wider records.  Every rank sees the same count words,
+  // so every rank takes the same decision.
+  const bool packed = !any_raw && !any_inv;
+  // raw records carry the row bytes at the sender's stride: one stride on
+  // every rank, or nobody exchanges (every rank sees the mismatch)
+  if (!packed && mixed_stride) return EVM_EINVAL;
   if (packed0 && !packed) {
     rb = stride + META;
     lerr = grow(&d->send, &d->send_cap, std::max<size_t>(n, 1) * rb);
@@ -1146,7 +1166,8 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
   if (!ctx || !d || (group && !group_off) || group > MAX_BUCKETS) return EVM_EINVAL;
   const size_t n = d->n_recv;
   if (n && (!out_ts || !out_owner || out_stride < d->stride || out_stride % 8)) return EVM_EINVAL;
-  if (n && d->packed && (out_stride % 16 || ((uintptr_t)out_ts & 15))) return EVM_EINVAL;  // rebuilt rows: 16-B stores
+  // rebuilt rows: 16-B stores, or 8-B stores into an output that is only 8-B aligned
+  const int packed = d->packed ? ((out_stride % 16 || ((uintptr_t)out_ts & 15)) ? 2 : 1) : 0;
   if (n > cap) return EVM_ECAPACITY;
   const u32 G = (u32)d->world;
   const u64* droff = d->cnt + W_ROFF;
@@ -1155,7 +1176,7 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
   if (!group) {
     if (n)
       KLAUNCH((k_dist_scatter<RECV>), dim3((u32)((n + DTILE - 1) / DTILE)), dim3(DT), R, (const char*)nullptr,
-              d->stride, (const u32*)nullptr, d->recv, d->rb, d->packed, n, 1u, 0, 1u, (const u32*)nullptr,
+              d->stride, (const u32*)nullptr, d->recv, d->rb, packed, n, 1u, 0, 1u, (const u32*)nullptr,
               (char*)nullptr, out_ts, out_stride, out_owner, out_aux, (u64*)out_src, droff, G + 1, (u32*)nullptr);
     return hip_ok(hipGetLastError());
   }
@@ -1171,7 +1192,7 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
     int st = partition_offsets<RECV>(ctx, S, R, d->recv, d->rb, ooff, n, group, &offs, &nblocks, tot, bad);
     if (st) return st;
     KLAUNCH((k_dist_scatter<RECV>), dim3(nblocks), dim3(DT), R, (const char*)nullptr, d->stride, (const u32*)nullptr,
-            d->recv, d->rb, d->packed, n, group, ceil_log2(group), nblocks, offs, (char*)nullptr, out_ts, out_stride,
+            d->recv, d->rb, packed, n, group, ceil_log2(group), nblocks, offs, (char*)nullptr, out_ts, out_stride,
             out_owner, out_aux, (u64*)out_src, droff, G + 1, (u32*)nullptr);
   }
   HIPR(hipMemcpyAsync(tot + MAX_BUCKETS, bad, sizeof(u32), hipMemcpyDeviceToDevice, ctx->stream));

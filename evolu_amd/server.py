@@ -28,10 +28,14 @@ Results per body: the SyncResponse bytes, an exception object standing for
 the reference's 500 answer (ParseBodyError, RangeError), or None where the
 engine does not model the request (a nodeId that is not 16 hex chars, a
 timestamp shape timestampFromString would read in a way lenient.py does not
-restate, one timestamp stored under two spellings).  A None request was not
-applied, and the user is handed to the caller for good: every later request
-of that user also answers None, so the caller runs them, in order, on the
-reference path.
+restate, one timestamp stored under two spellings).  The user is then handed
+to the caller for good: every later request of that user also answers None,
+so the caller runs them, in order, on the reference path.  A None request is
+NOT always unapplied: a spelling conflict found after `evm_server_ingest_ex`
+committed the request (pass 1, or the canonical re-ingest) leaves its rows
+in this server's store and tree.  The handover is of the user, not of one
+request: the caller must serve that user from its own reference state from
+then on and treat this server's rows and tree of that user as stale.
 """
 from __future__ import annotations
 

@@ -72,6 +72,23 @@ class ShardedServer:
             g[:n_cold] = torch.where(torch.isin(g[:n_cold], hot), torch.full_like(g[:n_cold], -1), g[:n_cold])
         return g
 
+    def client_trees(self, partial):
+        """Collective: client trees over the local ids from this rank's
+        partial ones (each owner's known messages that were routed here):
+        a cold owner's partial tree is its whole tree; a split owner's
+        slot gets the XOR merge of every rank's part (evm_dist_merge_trees),
+        the same on every rank -- what select_split expects.  Without split
+        owners that is `partial` itself."""
+        nh, base = int(self.hot.size), self.hot_base
+        if not nh:
+            return partial
+        full = self.dd.merge_trees(partial, base, nh)
+        off_c, code_c, xr_c = partial.slice_device(0, base)
+        off_h, code_h, xr_h = full.slice_device(0, nh)
+        full.free()
+        off = torch.cat([off_c, off_h[1:] + off_c[-1]])
+        return self.eng.tree_from_device_leaves(off, torch.cat([code_c, code_h]), torch.cat([xr_c, xr_h]))
+
     def new_store(self):
         if self.store is not None:
             self.store.free()
@@ -136,7 +153,9 @@ class ShardedServer:
             self.store = None
 
 
-def split_apply(eng: Engine, dd: Dist, ts: torch.Tensor, cell: torch.Tensor, n_cells: int, tree_in=None):
+def split_apply(eng: Engine, dd: Dist, ts: torch.Tensor, cell: torch.Tensor, n_cells: int, tree_in=None,
+                prior_ts: Optional[torch.Tensor] = None, prior_present: Optional[torch.Tensor] = None,
+                stored_ts: Optional[torch.Tensor] = None, stored_cell: Optional[torch.Tensor] = None):
     """applyMessages (applyMessages.ts:26-131) of ONE owner's batch split over
     the ranks by cell, through the evm_dist C ABI.
 
@@ -145,9 +164,15 @@ def split_apply(eng: Engine, dd: Dist, ts: torch.Tensor, cell: torch.Tensor, n_c
     per cell, so every row goes to its cell's rank in global batch order
     (evm_dist_cell_dest + route); the global __message PK check (one timestamp
     in two cells) runs on the rank the timestamp hash picks; statuses combine
-    over ranks.  Returns (flags u8[n] of this rank's slice, winner int64
-    [n_cells] global batch index or -1, tree = tree_in + every rank's partial
-    tree, status) -- the same winner, tree and status on every rank."""
+    over ranks.  The owner's DB state is that of a single-rank apply: every
+    cell's current max (prior_ts [n_cells, 48] + prior_present,
+    applyMessages.ts:34-40) and the __message rows holding a batch timestamp
+    (stored_ts / stored_cell, :42-45) -- the SAME tensors on every rank; each
+    rank decides its own cells against them (evm_apply_batch_ex), so a stored
+    row of another cell is the global-PK case wherever it lands.  Returns
+    (flags u8[n] of this rank's slice, winner int64 [n_cells] global batch
+    index or -1, tree = tree_in + every rank's partial tree, status) -- the
+    same winner, tree and status on every rank."""
     from . import _lib
 
     n = ts.shape[0]
@@ -163,7 +188,8 @@ def split_apply(eng: Engine, dd: Dist, ts: torch.Tensor, cell: torch.Tensor, n_c
     empty = eng.tree_new(1)
     if t_c.shape[0]:
         flags_c, win_c, part, st = eng.apply_batch(empty, t_c.contiguous(), c_c.contiguous(), n_cells,
-                                                   raise_on_error=False)
+                                                   prior_ts=prior_ts, prior_present=prior_present,
+                                                   raise_on_error=False, stored_ts=stored_ts, stored_cell=stored_cell)
     else:
         flags_c = torch.zeros(0, dtype=torch.uint8, device=ts.device)
         win_c = torch.full((n_cells,), -1, dtype=torch.int32, device=ts.device)

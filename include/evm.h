@@ -425,14 +425,17 @@ int evm_dist_directory(evm_ctx* ctx, evm_dist* d, const char* ids, size_t stride
  * source order) -- the global batch order when each rank's input is its
  * slice of the batch in rank order; *n_recv = their count (host).  48-B rows
  * travel as 32-B packed records (bytes 46-47, padding, arrive as zero)
- * unless some row anywhere in the job is outside the native domain: then
- * every rank sends raw records and every byte arrives.  A row whose
+ * unless some row anywhere in the job is outside the native domain or some
+ * rank's rows are not 48-B rows at a 16-B aligned address: then every rank
+ * sends raw records and every byte arrives (the ranks agree on the format
+ * through the count words; raw records need one stride on every rank, else
+ * every rank returns EVM_EINVAL before any data moves).  A row whose
  * destination is out of range is dropped and EVM_EINVAL returned on its
  * rank after the exchange completed. */
 int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, const uint32_t* owner,
                    const uint32_t* aux, const uint8_t* dest, uint64_t* n_recv);
 /* local: the last route's rows into caller buffers (device): out_ts rows of
- * out_stride bytes, out_owner (global ids; local ids with a directory),
+ * out_stride bytes (out_stride % 8 == 0, out_ts 8-B aligned), out_owner (global ids; local ids with a directory),
  * optional out_aux and out_src (source rank << 32 | index in that rank's
  * input).  group == 0: in receive order; 0 < group <= 64: grouped by local
  * owner (owner / world, or the directory's local id, < group), receive order

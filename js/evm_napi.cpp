@@ -1096,49 +1096,66 @@ napi_value DistSelectSplit(napi_env env, napi_callback_info info) {
   return res;
 }
 
-// distSplitApply(ctx, d, ts Uint8Array(n * 48), cell Uint32Array, nCells, treeIn)
+// distSplitApply(ctx, d, ts Uint8Array(n * 48), cell Uint32Array, nCells, treeIn
+//                [, priorTs Uint8Array(nCells * 48), priorPresent Uint8Array(nCells)
+//                 [, storedTs Uint8Array(k * 48), storedCell Uint32Array(k)]])
 //   -> { status, flags Uint8Array(n), winner Float64Array(nCells) (global batch index, -1), tree | null }
 // applyMessages of ONE owner's batch split over the ranks by cell (collective): each rank passes its
-// slice (the batch = the slices in rank order); winner and tree are the same on every rank
+// slice (the batch = the slices in rank order); winner and tree are the same on every rank.  The owner's
+// DB state is the single-rank applyMessages' (evolu_evm.js _applyArgs): every cell's current max
+// (applyMessages.ts:34-40) and the __message rows holding a batch timestamp (:42-45), the SAME arrays on
+// every rank -- each rank decides its own cells against them with evm_apply_batch_ex
 napi_value DistSplitApply(napi_env env, napi_callback_info info) {
-  napi_value a[6];
-  if (!get_args(env, info, 6, a)) return nullptr;
+  napi_value a[10];
+  size_t argc = 10;
+  if (napi_get_cb_info(env, info, &argc, a, nullptr, nullptr) != napi_ok || argc < 6) {
+    napi_throw_type_error(env, nullptr, "missing arguments");
+    return nullptr;
+  }
   Ctx* cx = ctx_of(env, a[0]);
   std::lock_guard<std::mutex> lock(cx->m);
   evm_ctx* ctx = cx->c;
   evm_dist* d = (evm_dist*)ext(env, a[1]);
-  void *ts, *cell;
-  size_t tl, cl;
+  void *ts, *cell, *pts = nullptr, *pp = nullptr, *sts = nullptr, *sc = nullptr;
+  size_t tl, cl, ptl = 0, ppl = 0, stl = 0, scl = 0;
   if (!bytes_of(env, a[2], &ts, &tl) || !bytes_of(env, a[3], &cell, &cl)) return nullptr;
   const uint32_t nc = u32(env, a[4]);
   const evm_tree* tree_in = (const evm_tree*)ext(env, a[5]);
+  if (argc >= 8 && !is_null(env, a[6]) && (!bytes_of(env, a[6], &pts, &ptl) || !bytes_of(env, a[7], &pp, &ppl)))
+    return nullptr;
+  if (argc >= 10 && !is_null(env, a[8]) && (!bytes_of(env, a[8], &sts, &stl) || !bytes_of(env, a[9], &sc, &scl)))
+    return nullptr;
   const size_t n = cl / 4;
-  if (tl != n * 48) return throw_status(env, EVM_EINVAL, "distSplitApply: sizes");
-  Dev dts(ctx, tl, ts), dcell(ctx, cl, cell), dzero(ctx, 4 * (n ? n : 1)), ddest(ctx, n ? n : 1);
+  const size_t ns = scl / 4;
+  if (tl != n * 48 || (pts && (ptl != 48ull * nc || ppl != nc)) || (sts && stl != ns * 48))
+    return throw_status(env, EVM_EINVAL, "distSplitApply: sizes");
+  Dev dts(ctx, tl, ts), dcell(ctx, cl, cell), dzero(ctx, 4 * (n ? n : 1)), ddest(ctx, n ? n : 1),
+      dpts(ctx, ptl, pts), dpp(ctx, ppl, pp), dsts(ctx, stl, sts), dsc(ctx, scl, sc);
   std::vector<uint32_t> zero(n, 0u);
   if (n) evm_copy_h2d(ctx, dzero.p, zero.data(), 4 * n);
   uint64_t nr = 0;
   int local = EVM_OK;
-  // the global PK check (applyMessages.ts:42-45): every copy of a timestamp meets on one rank
+  // the global PK check (applyMessages.ts:42-45): every copy of a timestamp meets on one rank.  A rank
+  // whose destinations failed still joins the route (with no rows) and reports in the agreement
   int st = evm_dist_ts_dest(ctx, d, (const char*)dts.p, 48, n, (uint8_t*)ddest.p);
-  if (!st) st = evm_dist_route(ctx, d, (const char*)dts.p, 48, n, (const uint32_t*)dzero.p,
-                               (const uint32_t*)dcell.p, (const uint8_t*)ddest.p, &nr);
-  if (st) return throw_status(env, st, "distSplitApply: route");
+  if (st) local = st;
+  st = evm_dist_route(ctx, d, (const char*)dts.p, 48, local ? 0 : n, (const uint32_t*)dzero.p,
+                      (const uint32_t*)dcell.p, (const uint8_t*)ddest.p, &nr);
+  if (st) return throw_status(env, st, "distSplitApply: route");  // (every rank fails a route together)
   {
     Dev rts(ctx, 48 * (nr ? nr : 1)), row(ctx, 4 * (nr ? nr : 1)), rax(ctx, 4 * (nr ? nr : 1));
     st = evm_dist_take(ctx, d, 0, (char*)rts.p, 48, (uint32_t*)row.p, (uint32_t*)rax.p, nullptr, nr, nullptr);
     int32_t found = 0;
     if (!st && nr) st = evm_cross_cell_check(ctx, (const char*)rts.p, 48, nr, (const uint32_t*)rax.p, nc, &found);
-    if (st) local = st;
-    else if (found) local = EVM_ECOLLISION;
+    if (st && !local) local = st;
+    else if (found && !local) local = EVM_ECOLLISION;
     st = EVM_OK;
   }
   // the LWW decisions (applyMessages.ts:78-124) are per cell: every row of a cell on the cell's rank
   st = evm_dist_cell_dest(ctx, d, (const uint32_t*)dcell.p, n, (uint8_t*)ddest.p);
   if (st && !local) local = st;
-  // (a failed dest: route with bad destinations -- the route reports them after the exchange)
-  st = evm_dist_route(ctx, d, (const char*)dts.p, 48, n, (const uint32_t*)dzero.p, (const uint32_t*)dcell.p,
-                      (const uint8_t*)ddest.p, &nr);
+  st = evm_dist_route(ctx, d, (const char*)dts.p, 48, local ? 0 : n, (const uint32_t*)dzero.p,
+                      (const uint32_t*)dcell.p, (const uint8_t*)ddest.p, &nr);
   if (st) return throw_status(env, st, "distSplitApply: route");  // (every rank fails a route together)
   Dev rts(ctx, 48 * (nr ? nr : 1)), row(ctx, 4 * (nr ? nr : 1)), rax(ctx, 4 * (nr ? nr : 1)),
       fl(ctx, nr ? nr : 1), win(ctx, 4ull * (nc ? nc : 1)), dflags(ctx, n ? n : 1), dwin(ctx, 8ull * (nc ? nc : 1));
@@ -1151,8 +1168,11 @@ napi_value DistSplitApply(napi_env env, napi_callback_info info) {
   st = EVM_OK;
   if (!local) {
     if (nr) {
-      const int a_st = evm_apply_batch(ctx, empty, (const char*)rts.p, 48, nr, (const uint32_t*)rax.p, nc, nullptr,
-                                       nullptr, 48, nullptr, (uint8_t*)fl.p, (int32_t*)win.p, &part);
+      const int a_st = evm_apply_batch_ex(ctx, empty, (const char*)rts.p, 48, nr, (const uint32_t*)rax.p, nc,
+                                          nullptr, pts ? (const char*)dpts.p : nullptr, 48,
+                                          pp ? (const uint8_t*)dpp.p : nullptr, ns ? (const char*)dsts.p : nullptr,
+                                          48, ns, ns ? (const uint32_t*)dsc.p : nullptr, (uint8_t*)fl.p,
+                                          (int32_t*)win.p, &part);
       if (a_st) local = a_st;
     } else {
       std::vector<int32_t> none(nc ? nc : 1, -1);

@@ -371,12 +371,25 @@ class Dist {
   }
   // collective: applyMessages (applyMessages.ts:26-131) of ONE owner's batch split over
   // the ranks by cell; each rank passes its slice (timestamps, cell ids < nCells).
+  // state (optional, the owner's DB as the single-rank applyMessages reads it, the SAME on
+  // every rank): { prior: per cell its current max timestamp or null (applyMessages.ts:34-40),
+  // stored: [{ timestamp, cell }] the __message rows holding a batch timestamp (:42-45;
+  // cell >= nCells: a cell the batch does not touch) }.
   // -> { status, flags (this slice), winner[c] (global batch index or -1), tree JSON | null }
-  applyMessagesSplit(timestamps, cells, nCells, treeJson = "{}") {
+  applyMessagesSplit(timestamps, cells, nCells, treeJson = "{}", state = null) {
     const t = addon.treeFromJson(this.engine.ctx, [treeJson]);
     try {
-      const r = addon.distSplitApply(this.engine.ctx, this.h, encodeTimestamps(timestamps), Uint32Array.from(cells),
-        nCells, t);
+      const args = [this.engine.ctx, this.h, encodeTimestamps(timestamps), Uint32Array.from(cells), nCells, t];
+      if (state) {
+        const prior = state.prior || new Array(nCells).fill(null);
+        args.push(encodeTimestamps(prior.map((p) => (p == null ? "" : p))),
+          Uint8Array.from(prior.map((p) => (p == null ? 0 : 1))));
+        const stored = state.stored || [];
+        if (stored.length) {
+          args.push(encodeTimestamps(stored.map((r) => r.timestamp)), Uint32Array.from(stored.map((r) => r.cell)));
+        }
+      }
+      const r = addon.distSplitApply(...args);
       let tree = null;
       if (r.tree) {
         tree = addon.treeToJson(this.engine.ctx, r.tree, 0);

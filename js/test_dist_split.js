@@ -44,6 +44,14 @@ if (isMainThread) {
     const r = d.applyMessagesSplit(a.timestamps.slice(lo, hi), a.cells.slice(lo, hi), a.nCells);
     out.apply = { status: r.status, flags: Array.from(r.flags), winner: r.winner, tree: r.tree };
   }
+  // the same on a non-empty DB: the cells' maxima and the stored rows of batch 2's timestamps
+  if (cases.applyPrior) {
+    const b = cases.applyPrior;
+    const [lo, hi] = cut(b.timestamps.length);
+    const r = d.applyMessagesSplit(b.timestamps.slice(lo, hi), b.cells.slice(lo, hi), b.nCells, b.treeJson,
+      { prior: b.prior, stored: b.stored });
+    out.applyPrior = { status: r.status, flags: Array.from(r.flags), winner: r.winner, tree: r.tree };
+  }
   // server: owners by murmur3(userId) % world, the hot ones split over every rank
   const s = cases.server;
   {

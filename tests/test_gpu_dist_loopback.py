@@ -159,6 +159,64 @@ def test_invalid_row_anywhere_sends_every_rank_raw():
         assert np.array_equal(res[r], ts)
 
 
+def test_one_rank_unaligned_every_rank_raw_and_8b_take():
+    """Rank 1's rows sit at an 8-B but not 16-B aligned address (the API only
+    asks stride % 8 == 0): it cannot pack, says so in its count words, and
+    every rank sends raw records -- the record sizes agree, every row arrives.
+    Then a packed route taken into an 8-B aligned output (8-B stores)."""
+    world = 2
+    slices = _slices(world, 20_000, 13, 23)
+
+    def fn(r, eng, dd):
+        ts, owner, aux = slices[r]
+        t = eng.dev(ts)
+        if r == 1:  # the same rows one 8-B word into a larger buffer
+            flat = torch.zeros(t.numel() + 8, dtype=torch.uint8, device=t.device)
+            flat[8:].copy_(t.reshape(-1))
+            t = flat[8:].view(-1, 48)
+            assert t.data_ptr() % 16 == 8
+        dd.route(t, eng.dev(owner), eng.dev(aux))
+        raw = dd.take()[0].cpu().numpy()
+        n = dd.route(eng.dev(ts), eng.dev(owner), eng.dev(aux))
+        buf = torch.zeros((n + 1) * 48 + 8, dtype=torch.uint8, device=t.device)
+        out_ts = buf[8:8 + n * 48].view(n, 48)
+        out = (out_ts, torch.empty(max(n, 1), dtype=torch.int32, device=t.device), None, None)
+        t8 = dd.take(aux=False, src=False, out=out)[0].cpu().numpy()
+        return raw, t8
+
+    res = _loop(world, fn)
+    for r in range(world):
+        ts, _, _, _ = _expected(slices, world, r, lambda o: o % world)
+        raw, t8 = res[r]
+        assert np.array_equal(raw, ts)
+        assert np.array_equal(t8[:, :46], ts[:, :46])
+
+
+def test_mixed_strides_are_refused_on_every_rank():
+    """Raw records at two strides cannot be exchanged: every rank returns
+    EVM_EINVAL before any data moves, and the next route works."""
+    from evolu_amd import _lib as L
+
+    world = 2
+    slices = _slices(world, 3000, 5, 41)
+
+    def fn(r, eng, dd):
+        ts, owner, aux = slices[r]
+        t = eng.dev(ts)
+        wide = torch.zeros((t.shape[0], 56), dtype=torch.uint8, device=t.device)
+        wide[:, :48] = t
+        st = None
+        try:
+            dd.route(wide if r == 0 else t, eng.dev(owner))
+        except L.EngineError as e:
+            st = e.status
+        return st, dd.route(t, eng.dev(owner))
+
+    res = _loop(world, fn)
+    assert res[0][0] == L.EVM_EINVAL and res[1][0] == L.EVM_EINVAL
+    assert res[0][1] + res[1][1] == 6000
+
+
 def test_local_failure_is_agreed_not_hung():
     """Rank 1 passes a bad stride: it returns EVM_EINVAL, rank 0 EVM_EDIST,
     nobody waits; the next route of both succeeds.  Same for gather_roots."""
@@ -300,3 +358,39 @@ def test_config4_bench_loopback_self_check(world):
         d = out["self_check_rank%d" % r]
         assert d["received"] == d["expected"] and d["sample_owners"] > 0
         assert d["inserted"] and d["roots"] and d["diffs"] and d["selections"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_config5_bench_loopback_self_check(world):
+    """bench.py's config-5 rank (BASELINE config 5 at N GPUs: Zipf owners,
+    the hot ones split over every rank, merged selections) on loopback ranks,
+    small: its self-check -- sampled cold owners and every split owner
+    recomputed unsharded -- must pass on every rank and must cover split
+    owners and selected rows."""
+    import argparse
+
+    import bench
+
+    a = argparse.Namespace(c5_owners=3000, c5_messages=400_000, steps=2, warmup=1, c5_sample=120, c5_share=0.1)
+    out = bench.config5_loopback(a, world)
+    assert out["parity_checked"] is True
+    assert out["config"]["n_split_owners"] >= 1
+    for r in range(world):
+        d = out["self_check_rank%d" % r]
+        assert d["split_owners_checked"] >= 1 and d["sample_owners"] > 0 and d["selected_rows"] > 0
+        assert d["inserted"] and d["roots"] and d["diffs"] and d["split_trees"] and d["selections"]
+
+
+def test_config5c_bench_loopback_self_check():
+    """bench.py's client split leg (one owner's batch split by cell over 2
+    loopback ranks) against the whole batch applied unsharded."""
+    import argparse
+
+    import bench
+
+    a = argparse.Namespace(c5c_messages=200_000, c5c_cells=300, steps=2, warmup=1)
+    out = bench.client_split_loopback(a, 2)
+    assert out["parity_checked"] is True
+    for r in range(2):
+        d = out["self_check_rank%d" % r]
+        assert d["flags"] and d["winners"] and d["tree"] and d["batch_rows"] == 400_000

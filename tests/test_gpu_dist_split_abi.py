@@ -212,3 +212,63 @@ def test_merge_select_orders_shares_and_return_restores_positions():
         n = 50 + r
         back = res[r][2]
         assert list(back) == [k * 7 + (k % world) for k in range(n)]
+
+
+@pytest.mark.parametrize("world,cross", [(2, False), (3, False), (2, True)])
+def test_cell_split_apply_on_prior_state_vs_oracle(world, cross):
+    """The split on a non-empty DB (applyMessages.ts:34-45,93-119): batch 2
+    runs on the state batch 1 left -- every cell's current max and the
+    __message rows holding a batch-2 timestamp, the same on every rank.
+    Redeliveries of batch-1 rows are no-ops or XOR toggles exactly as in one
+    process; a batch-1 timestamp re-sent under another cell is the global-PK
+    case on every rank."""
+    from evolu_amd import _lib as L
+    from evolu_amd.sharded import split_apply
+    from tests.test_gpu_apply_stored import _stored_rows, _two_batches
+
+    b1, b2 = _two_batches(21 + world, cross)
+    db = O.ClientDb()
+    tree1 = O.apply_messages(db, {}, b1)
+    cells, cid = [], {}
+    for m in b2:
+        c = (m["table"], m["row"], m["column"])
+        if c not in cid:
+            cid[c] = len(cells)
+            cells.append(c)
+    cell = np.array([cid[(m["table"], m["row"], m["column"])] for m in b2], dtype=np.uint32)
+    prior = [db.cell_max(*c) for c in cells]
+    pp = np.array([p is not None for p in prior], dtype=np.uint8)
+    rows = _stored_rows(db, b2)
+    assert rows and pp.any()
+    s_cell = np.array([cid.get((r[1], r[2], r[3]), 0xFFFFFFFF) for r in rows], dtype=np.uint32)
+    dec = []
+    want = O.apply_messages(db, tree1, b2, dec)
+    cut = _cuts(len(b2), world)
+    strs = [m["timestamp"] for m in b2]
+    tree1_js = O.merkle_tree_to_string(tree1)
+
+    def fn(r, eng, dd):
+        t = eng.timestamps(strs[cut[r]:cut[r + 1]])
+        c = eng.dev(cell[cut[r]:cut[r + 1]].view(np.int32))
+        flags, winner, tree, st = split_apply(
+            eng, dd, t, c, len(cells), tree_in=eng.tree_from_json([tree1_js]),
+            prior_ts=eng.timestamps([p or "" for p in prior]), prior_present=eng.dev(pp),
+            stored_ts=eng.timestamps([x[0] for x in rows]), stored_cell=eng.dev(s_cell))
+        return (st, flags.cpu().numpy(), None if winner is None else winner.cpu().numpy(),
+                None if tree is None else tree.to_json(0))
+
+    res = _loop(world, fn)
+    if cross:
+        assert all(x[0] == L.EVM_ECOLLISION for x in res)
+        return
+    flags = np.concatenate([x[1] for x in res])
+    for i, (ups, xr, _) in enumerate(dec):
+        assert bool(flags[i] & L.MSG_UPS) == ups and bool(flags[i] & L.MSG_XOR) == xr, i
+    last = {}
+    for i, m in enumerate(b2):
+        if dec[i][0]:
+            last[(m["table"], m["row"], m["column"])] = i
+    for x in res:
+        assert x[0] == L.EVM_OK
+        assert [int(w) for w in x[2]] == [last.get(c, -1) for c in cells]
+        assert x[3] == O.merkle_tree_to_string(want)

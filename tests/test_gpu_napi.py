@@ -188,6 +188,32 @@ def test_js_dist_split_loopback(tmp_path, world):
                         "owners": [int(o) for o in sown],
                         "clientTrees": [CO.tree_json(sts[keep & (sown == g)]) for g in range(O_)],
                         "nodeIds": node_of}}
+    # a batch on a non-empty DB (applyMessages.ts:34-45): batch 1 applied by the oracle, batch 2 split
+    from tests import workloads as W
+
+    b1, _ = W.client_batch(71, n=400, n_cells=9)
+    b2, _ = W.client_batch(72, n=300, n_cells=12, t0=W.T0 + 1800_000)
+    prng = np.random.default_rng(4)
+    for k in prng.choice(len(b1), 40, replace=False):  # redeliveries of batch-1 rows
+        b2.insert(int(prng.integers(0, len(b2) + 1)), dict(b1[int(k)]))
+    pdb = O.ClientDb()
+    ptree = O.apply_messages(pdb, {}, b1)
+    pcells, pcid = [], {}
+    for m in b2:
+        c = (m["table"], m["row"], m["column"])
+        if c not in pcid:
+            pcid[c] = len(pcells)
+            pcells.append(c)
+    from tests.test_gpu_apply_stored import _stored_rows
+
+    prows = _stored_rows(pdb, b2)
+    cases["applyPrior"] = {"timestamps": [m["timestamp"] for m in b2],
+                           "cells": [pcid[(m["table"], m["row"], m["column"])] for m in b2], "nCells": len(pcells),
+                           "treeJson": O.merkle_tree_to_string(ptree), "prior": [pdb.cell_max(*c) for c in pcells],
+                           "stored": [{"timestamp": r[0], "cell": pcid.get((r[1], r[2], r[3]), 0xFFFFFFFF)}
+                                      for r in prows]}
+    pdec = []
+    pwant = O.apply_messages(pdb, ptree, b2, pdec)
     f = tmp_path / "cases.json"
     f.write_text(json.dumps(cases))
     out = subprocess.run(["node", os.path.join(ROOT, "js", "test_dist_split.js"), str(f)], check=True,
@@ -198,6 +224,18 @@ def test_js_dist_split_loopback(tmp_path, world):
     for x in res:
         assert x["apply"]["status"] == 0 and x["apply"]["winner"] == [int(v) for v in win_o]
         assert x["apply"]["tree"] == js_o
+    assert prows
+    pflags = sum((x["applyPrior"]["flags"] for x in res), [])
+    for i, (ups, xr, _) in enumerate(pdec):
+        assert bool(pflags[i] & 1) == ups and bool(pflags[i] & 2) == xr, i
+    plast = {}
+    for i, m in enumerate(b2):
+        if pdec[i][0]:
+            plast[(m["table"], m["row"], m["column"])] = i
+    for x in res:
+        assert x["applyPrior"]["status"] == 0
+        assert x["applyPrior"]["winner"] == [plast.get(c, -1) for c in pcells]
+        assert x["applyPrior"]["tree"] == O.merkle_tree_to_string(pwant)
     counts = np.bincount(sown, minlength=O_)
     want_hot = [int(g) for g in np.flatnonzero(counts > 0.25 * len(sts) / world)]
     assert want_hot and all(x["server"]["hot"] == want_hot for x in res)
