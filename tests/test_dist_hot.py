@@ -1,7 +1,9 @@
-"""Hot-owner split (evolu_amd/dist.py OwnerMap) on CPU with gloo, world_size 2.
+"""Hot-owner split (evolu_amd/dist.py: the evm_dist_hot_owners / evm_dist_split
+plan restated over torch.distributed) on CPU with gloo, world_size 2.
 
 A skewed owner mix (BASELINE config 5: one owner holds half the messages,
-with redeliveries) is routed with the hot owner split by timestamp hash.
+with redeliveries), owners by murmur3(userId) mod world, is routed with the
+hot owner split by murmur3(timestamp) mod world (local id hot_base + h).
 Checked against one unsharded server (the oracle's verbatim-SQL
 addMessages): the per-message INSERT decisions routed back to their origin,
 the XOR-combined roots of the split owner, and its tree rebuilt from the
@@ -70,13 +72,15 @@ def _worker(rank, world, port, q):
         from evolu_amd.engine import encode_timestamps
         from oracle import evolu_oracle as O
 
+        from tests.test_dist import _user_ids
+
         msgs = _messages(rank)
         ts = torch.from_numpy(encode_timestamps([t for _, t in msgs]))
         owner = torch.tensor([o for o, _ in msgs], dtype=torch.int64)
         counts = D.owner_counts(owner, N_OWNERS)
         hot = D.hot_owners(counts, world)
-        omap = D.OwnerMap(N_OWNERS, world, rank, hot)
-        ts_r, own_r, src_rank, src_idx = D.route_by_owner(ts, owner, dest=omap.dest(owner, ts))
+        omap = D.OwnerMap(D.Directory(_user_ids(N_OWNERS), world), rank, hot)
+        ts_r, own_r, src_rank, src_idx = D.route_by_owner(ts, owner, omap.dest(owner, ts))
         loc = omap.local(own_r)
         got = [(int(o), bytes(ts_r[i, :46].numpy()).decode()) for i, o in enumerate(own_r)]
         db = O.ServerDb()
@@ -89,8 +93,10 @@ def _worker(rank, world, port, q):
         roots = torch.tensor([db.get_merkle_tree("l%d" % j).get("hash", 0) for j in range(omap.n_local)],
                              dtype=torch.int32)
         present = torch.tensor(["hash" in db.get_merkle_tree("l%d" % j) for j in range(omap.n_local)])
-        hroot, hpres = D.gather_hot_roots(roots, present, omap)
-        partial = {int(h): _leaves(db.get_merkle_tree("l%d" % (omap.per + k))) for k, h in enumerate(omap.hot.tolist())}
+        groot, gpres = D.gather_roots(roots, present, omap)
+        hroot, hpres = groot[torch.from_numpy(hot)], gpres[torch.from_numpy(hot)]
+        partial = {int(h): _leaves(db.get_merkle_tree("l%d" % (omap.hot_base + k)))
+                   for k, h in enumerate(omap.hot.tolist())}
         q.put((rank, hot.tolist(), ins_back.tolist(), hroot.tolist(), hpres.tolist(), partial))
     finally:
         dist.destroy_process_group()

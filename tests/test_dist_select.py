@@ -1,4 +1,5 @@
-"""getMessages for an owner split over ranks (evolu_amd/dist.py), gloo on CPU,
+"""getMessages for an owner split over ranks (evolu_amd/dist.py: the
+evm_dist_merge_trees / merge_select plan over torch.distributed), gloo on CPU,
 world_size 2, against one unsharded server (the oracle's verbatim SQL,
 apps/server/src/index.ts:173-202).
 
@@ -59,27 +60,29 @@ def _worker(rank, world, port, q):
         msgs = _messages(rank)
         ts = torch.from_numpy(encode_timestamps([t for _, t in msgs]))
         owner = torch.tensor([o for o, _ in msgs], dtype=torch.int64)
-        omap = D.OwnerMap(N_OWNERS, world, rank, D.hot_owners(D.owner_counts(owner, N_OWNERS), world))
-        ts_r, own_r, src_rank, src_idx = D.route_by_owner(ts, owner, dest=omap.dest(owner, ts))
+        from tests.test_dist import _user_ids
+
+        omap = D.OwnerMap(D.Directory(_user_ids(N_OWNERS), world), rank,
+                          D.hot_owners(D.owner_counts(owner, N_OWNERS), world))
+        ts_r, own_r, src_rank, src_idx = D.route_by_owner(ts, owner, omap.dest(owner, ts))
         loc = omap.local(own_r).tolist()
         gid = (src_rank * 100000 + src_idx).tolist()  # global message ids
         db = O.ServerDb()
         for i, lo in enumerate(loc):
             t = bytes(ts_r[i, :46].numpy()).decode()
             db.add_messages(db.get_merkle_tree("l%d" % lo), "l%d" % lo, [(t, str(gid[i]).encode())])
-        nh = int(omap.hot.numel())
+        nh = int(omap.hot.size)
         # cold owners: their whole tree is here
         cold = {}
-        for j in range(omap.per):
-            o = j * world + rank
-            if o >= N_OWNERS or o in omap.hot.tolist():
+        for j, o in enumerate(omap.owners_here()[:omap.hot_base].tolist()):
+            if o < 0:
                 continue
             d, rows = db.get_messages(db.get_merkle_tree("l%d" % j), _client_tree(o), "l%d" % j, _node(o))
             cold[o] = (d, [int(c) for _, c in rows])
         # hot owners: merge the partial leaf maps, diff the full trees, select shares, merge shares
         offs, codes, xrs = [0], [], []
         for k in range(nh):
-            lv = _leaves(db.get_merkle_tree("l%d" % (omap.per + k)))
+            lv = _leaves(db.get_merkle_tree("l%d" % (omap.hot_base + k)))
             for key in sorted(lv, key=key_code):
                 codes.append(key_code(key))
                 xrs.append(O.to_int32(lv[key]))
@@ -97,7 +100,8 @@ def _worker(rank, world, port, q):
             diffs.append(d)
             if d is not None:
                 since = O.timestamp_to_string(*O.create_sync_timestamp(d))
-                rows = db.conn.execute(O._SQL_SELECT_MESSAGES, ("l%d" % (omap.per + k), since, _node(o))).fetchall()
+                rows = db.conn.execute(O._SQL_SELECT_MESSAGES, ("l%d" % (omap.hot_base + k), since,
+                                                                _node(o))).fetchall()
                 for t, c in rows:
                     sel_id.append(int(c))
                     sel_key.append(_key(t))

@@ -394,3 +394,54 @@ def test_config5c_bench_loopback_self_check():
     for r in range(2):
         d = out["self_check_rank%d" % r]
         assert d["flags"] and d["winners"] and d["tree"] and d["batch_rows"] == 400_000
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_torch_plan_is_the_c_abi_partition(world):
+    """evolu_amd/dist.py (the torch.distributed restatement the gloo CPU tests
+    prove exact) assigns every row the destination rank and local id the C
+    ABI does: directory, hot owners, hot_base, the split owners' rows by
+    timestamp hash, cells by cell hash, the global-PK timestamp ranks."""
+    from evolu_amd import dist as D
+    from evolu_amd import synth
+
+    O_, N = 60, 40_000
+    ts, owner, cell = synth.config5(O_, N, seed_config=77)
+    owner = owner.astype(np.uint32)
+    ids = np.frombuffer(b"".join(b"x%020d" % g for g in range(O_)), dtype=np.uint8).reshape(O_, 21)
+    cut = [N * r // world for r in range(world + 1)]
+    dirx = D.Directory(ids, world)
+    hot_py = D.hot_owners(torch.from_numpy(np.bincount(owner, minlength=O_)), world, 0.25)
+
+    def fn(r, eng, dd):
+        pad = np.zeros((O_, 24), dtype=np.uint8)
+        pad[:, :21] = ids
+        dest, local = dd.directory((eng.dev(pad), 21))
+        t_in, o_in = eng.dev(ts[cut[r]:cut[r + 1]]), eng.dev(owner[cut[r]:cut[r + 1]])
+        hot = dd.hot_owners(o_in, O_, 0.25)
+        base = dd.split(hot, O_)
+        dd.route(t_in, o_in, aux=eng.dev(np.arange(cut[r], cut[r + 1], dtype=np.uint32)))
+        _, lo, gi, _, _ = dd.take()
+        tsd = dd.ts_dest(t_in)
+        cd = dd.cell_dest(eng.dev(cell[cut[r]:cut[r + 1]].astype(np.uint32)))
+        return (dest.cpu().numpy(), local.cpu().numpy(), hot, base, lo.cpu().numpy(), gi.cpu().numpy(),
+                tsd.cpu().numpy(), cd.cpu().numpy())
+
+    res = _loop(world, fn)
+    assert hot_py.size >= 1
+    for r in range(world):
+        dest, local, hot, base, lo, gi, tsd, cd = res[r]
+        assert np.array_equal(dest, dirx.dest) and np.array_equal(local, dirx.local)
+        assert np.array_equal(hot, hot_py)
+        omap = D.OwnerMap(dirx, r, hot_py)
+        assert base == omap.hot_base
+        t_all = torch.from_numpy(ts)
+        o_all = torch.from_numpy(owner.astype(np.int64))
+        want_dest = omap.dest(o_all, t_all).numpy()
+        # the rows this rank received: exactly those the plan sends here, in global order, same local ids
+        mine = np.flatnonzero(want_dest == r)
+        assert np.array_equal(gi.view(np.uint32).astype(np.int64), mine)
+        assert np.array_equal(lo, omap.local(o_all[mine]).numpy())
+        sl = slice(cut[r], cut[r + 1])
+        assert np.array_equal(tsd, D.ts_dest(t_all[sl], world).numpy())
+        assert np.array_equal(cd, D.cell_dest(torch.from_numpy(cell[sl].astype(np.int64)), world).numpy())

@@ -1,7 +1,7 @@
 """evm_tree_merge: the union of two insert sets' trees, XOR-combined -- the
 tree insertIntoMerkleTree gives for all inserts together in any order
 (merkleTree.test.ts:30-42).  It combines the partial trees of an owner split
-over GPUs (evolu_amd/dist.py)."""
+over GPUs (evm_dist_merge_trees, evolu_amd/sharded.py)."""
 import random
 
 import numpy as np
