@@ -518,10 +518,16 @@ def main():
     torch.cuda.synchronize()
     host_us["enqueue"].clear()
     host_us["wait"].clear()
+    st0 = eng.stats()
     t0 = time.perf_counter()
     run_pipelined(a.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    st1 = eng.stats()
+    # the path the timed batches took: every one on the tc streaming path, none redone
+    path = {k: st1[k] - st0[k] for k in ("tc_batches", "tc_redos", "small_batches", "small_fallbacks")}
+    path["batches"] = a.steps
+    path["kernels"] = sorted(prof)
     if not a.dom_events:  # the dominant kernel's duration from an identical pass
         eng.prof_enable(True)
         run_pipelined(a.steps)
@@ -583,6 +589,7 @@ def main():
                        % (a.messages, a.cells), "messages_per_gpu": a.messages, "cells": a.cells,
                        "parallelism": "owner-sharded, %d rank(s)" % world},
             "roofline": roof,
+            "path": path,
             "pipeline": {"alg_bytes_per_msg": 120, "ms_per_step_all_kernel_events": ms_all_events,
                          "batches_in_flight": DEPTH,
                          "host_enqueue_us_avg": sum(host_us["enqueue"]) / max(1, len(host_us["enqueue"])),

@@ -660,17 +660,36 @@ __device__ __forceinline__ int32_t range_hash(const TreeView& t, size_t lo, size
 
 constexpr int DIFF_LANES = 16;
 
-// At each level the three children's leaf ranges in both trees are 8 lower
-// bounds (child starts 1..3 and the end of child 3, in A and in B): lanes
-// 0-3 / 4-7 of the group search them at once and fetch the prefix XOR at their
-// bound, so a level costs one binary search + one load of latency instead of
-// up to eight searches in a row.  The greedy choice (first child whose hash
-// differs, a missing child counting as different) is then made by every lane
-// of the group on the shuffled bounds.  Once both ranges hold at most 16
-// leaves (a few levels down: ranges shrink ~3x per level), the group loads
-// them -- one leaf of A and one of B per lane -- and finishes every remaining
-// level in registers: a child's presence is a ballot of the lanes whose digit
-// at this depth selects it, its hash a 16-lane XOR reduction.
+// At each level the three children's leaf ranges in both trees are 6 lower
+// bounds (child starts 1..3 in A and in B; the end of child 3 is the node's
+// own end, known from the level above): lanes 0-2 / 4-6 of the group search
+// them at once and fetch the prefix XOR at their bound, so a level costs one
+// binary search + one load of latency instead of up to six searches in a row.
+// The greedy choice (first child whose hash differs, a missing child counting
+// as different) is then made by every lane of the group on the shuffled
+// bounds.
+//
+// The top levels are not searched at all: every leaf of both trees lies in
+// the code range of their longest common prefix (the first and the last
+// leaf of each tree bound it), and above that depth every node has ONE
+// child, present in both trees (or in the only non-empty one) and holding
+// the whole range -- its hash is its parent's, which differs -- so the
+// greedy path follows that prefix (for config-3 trees spanning 30 days: the
+// first ~6 of 16 digits, each a full-range search before).  Searches of the
+// same lines level after level were the kernel's HBM traffic: with thousands
+// of owners in flight per XCD a line is evicted from L2 between one level
+// and the next.
+//
+// Once both ranges hold at most 16 leaves (a few levels down: ranges shrink
+// ~3x per level), the group loads them -- one leaf of A and one of B per
+// lane -- and finishes every remaining level in registers: a child's
+// presence is a ballot of the lanes whose digit at this depth selects it, its
+// hash a 16-lane XOR reduction.
+__device__ __forceinline__ int code_digits_equal(u64 a, u64 b) {
+  const u64 x = (a ^ b) & ((1ull << (2 * CODE_DIGITS)) - 1);
+  return x ? (__clzll(x) - (64 - 2 * CODE_DIGITS)) >> 1 : CODE_DIGITS;
+}
+
 __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owners, int64_t* __restrict__ millis) {
   const int sub = threadIdx.x & (DIFF_LANES - 1);
   const u32 groups = gridDim.x * (blockDim.x / DIFF_LANES);
@@ -678,13 +697,35 @@ __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owne
     u64 alo = A.off[o], ahi = A.off[o + 1], blo = B.off[o], bhi = B.off[o + 1];
     // root: tree1.hash === tree2.hash (undefined for {})
     const bool ae = ahi > alo, be = bhi > blo;
-    if (ae == be && (!ae || range_hash(A, alo, ahi) == range_hash(B, blo, bhi))) {
+    int32_t pa_lo = ae ? A.pfx[alo] : 0, pa_hi = ae ? A.pfx[ahi] : 0;
+    int32_t pb_lo = be ? B.pfx[blo] : 0, pb_hi = be ? B.pfx[bhi] : 0;
+    if (ae == be && (!ae || (pa_lo ^ pa_hi) == (pb_lo ^ pb_hi))) {
       if (sub == 0) millis[o] = EVM_DIFF_NONE;
       continue;
     }
-    u64 prefix = (u64)o << 40;
-    int depth = 0;
-    u64 kval = 0;  // base-3 value of the key string k so far
+    // the common prefix of every leaf of both trees (one 8-B load per lane of 4)
+    u64 my = 0;
+    if (sub < 4) {
+      const bool inA = sub < 2;
+      const bool live = inA ? ae : be;
+      const u64* ck = inA ? A.ck : B.ck;
+      const u64 at = inA ? ((sub & 1) ? ahi - 1 : alo) : ((sub & 1) ? bhi - 1 : blo);
+      my = live ? ck[at] : ((sub & 1) ? 0ull : ~0ull);  // (an empty tree: neutral for min / max)
+    }
+    const int g0 = threadIdx.x & ~(DIFF_LANES - 1) & 63;
+    const u64 first = min(__shfl(my, g0 + 0, 64), __shfl(my, g0 + 2, 64));
+    const u64 last = max(__shfl(my, g0 + 1, 64), __shfl(my, g0 + 3, 64));
+    int depth = code_digits_equal(first, last);
+    u64 prefix = (u64)o << 40, kval = 0;
+    for (int d = 0; d < depth; ++d) {
+      const u32 dg = (u32)(first >> (2 * (CODE_DIGITS - 1 - d))) & 3u;
+      if (dg == 0) {  // the key ends here (every leaf is this one code): no deeper node
+        depth = d;
+        break;
+      }
+      prefix |= (u64)dg << (2 * (CODE_DIGITS - 1 - d));
+      kval = kval * 3 + (dg - 1);
+    }
     bool in_regs = false;
     while (depth < CODE_DIGITS) {
       if (ahi - alo <= DIFF_LANES && bhi - blo <= DIFF_LANES) {
@@ -692,10 +733,10 @@ __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owne
         break;
       }
       const int sh = 2 * (CODE_DIGITS - 1 - depth);
-      // lane s < 4: A bound of prefix + (s+1) << sh; lane 4 <= s < 8: B bound of prefix + (s-3) << sh
-      u64 my = 0;
+      // lane s < 3: A bound of prefix + (s+1) << sh; 4 <= s < 7: B bound of prefix + (s-3) << sh
+      u64 mb = 0;
       int32_t myx = 0;
-      if (sub < 8) {
+      if ((sub & 3) != 3 && sub < 8) {
         const bool inA = sub < 4;
         const u64* ck = inA ? A.ck : B.ck;
         u64 lo = inA ? alo : blo, hi = inA ? ahi : bhi;
@@ -705,19 +746,22 @@ __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owne
           if (ck[mid] < x) lo = mid + 1;
           else hi = mid;
         }
-        my = lo;
+        mb = lo;
         myx = (inA ? A.pfx : B.pfx)[lo];
       }
-      const int g0 = threadIdx.x & ~(DIFF_LANES - 1) & 63;
       u64 a[4], b[4];
       int32_t xa[4], xb[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        a[k] = __shfl(my, g0 + k, 64);
-        b[k] = __shfl(my, g0 + 4 + k, 64);
+      for (int k = 0; k < 3; ++k) {
+        a[k] = __shfl(mb, g0 + k, 64);
+        b[k] = __shfl(mb, g0 + 4 + k, 64);
         xa[k] = __shfl(myx, g0 + k, 64);
         xb[k] = __shfl(myx, g0 + 4 + k, 64);
       }
+      a[3] = ahi;  // the end of child 3 = the node's end
+      b[3] = bhi;
+      xa[3] = pa_hi;
+      xb[3] = pb_hi;
       int pick = -1;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -732,6 +776,8 @@ __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owne
       ahi = a[pick + 1];
       blo = b[pick];
       bhi = b[pick + 1];
+      pa_hi = xa[pick + 1];
+      pb_hi = xb[pick + 1];
     }
     if (in_regs) {
       const u64 ia = alo + sub, ib = blo + sub;
@@ -819,6 +865,9 @@ int evm_create(int device, evm_ctx** out) {
     return EVM_EDEVICE;
   }
   c->stream = c->own;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+    c->n_cu = ncu;
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
@@ -890,6 +939,10 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
   }
   if (option == EVM_OPT_RADIX && value >= 0 && value <= 2) {
     ctx->radix_onesweep = (int)value;
+    return EVM_OK;
+  }
+  if (option == EVM_OPT_DIFF_GRID && value >= 0 && value <= 64) {
+    ctx->diff_grid = (int)value;
     return EVM_OK;
   }
   if (option == EVM_OPT_TEST_FAIL && value >= 0 && value <= 1) {
@@ -1170,7 +1223,10 @@ int evm_merkle_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t*
 int evm::launch_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* millis) {
   if (a->n_owners == 0) return EVM_OK;
   TreeView A{a->off, a->ck, a->pfx, a->xr}, B{b->off, b->ck, b->pfx, b->xr};
-  KLAUNCH(k_diff, dim3(grid_for((size_t)a->n_owners * DIFF_LANES, 256, 1 << 16)), dim3(256), A, B, a->n_owners, millis);
+  // EVM_OPT_DIFF_GRID: workgroups per CU (fewer owners in flight: each one's lines stay in L2)
+  u32 grid = grid_for((size_t)a->n_owners * DIFF_LANES, 256, 1 << 16);
+  if (ctx->diff_grid > 0) grid = std::min<u32>(grid, (u32)ctx->diff_grid * (u32)ctx->n_cu);
+  KLAUNCH(k_diff, dim3(grid), dim3(256), A, B, a->n_owners, millis);
   return hip_ok(hipGetLastError());
 }
 

@@ -119,6 +119,7 @@ int evm_sync(evm_ctx* ctx);
 #define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 2 the same with \
                                  10-bit digits when that saves a pass; 0 histogram + scan + scatter per pass */
 #define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM) */
+#define EVM_OPT_DIFF_GRID 6   /* evm_merkle_diff / select: k_diff workgroups per CU (0: one lane group per owner) */
 int evm_set_option(evm_ctx* ctx, int option, int64_t value);
 /* kernel timing with HIP events on the context stream (for roofline reports) */
 int evm_prof_enable(evm_ctx* ctx, int on);
