@@ -11,6 +11,23 @@
 
 #include "../../include/evm.h"
 
+// min / max of one unsigned long long and one unsigned long (uint64_t, size_t):
+// HIP's overload set has no exact match for the mixed pair, and the call
+// resolves to the double overload -- 53 bits: an HLC key (millis << 16 |
+// counter, 57 bits) loses its counter.  These exact matches keep it integer.
+__device__ __forceinline__ unsigned long long min(unsigned long long a, unsigned long b) {
+  return a < (unsigned long long)b ? a : (unsigned long long)b;
+}
+__device__ __forceinline__ unsigned long long min(unsigned long a, unsigned long long b) {
+  return (unsigned long long)a < b ? (unsigned long long)a : b;
+}
+__device__ __forceinline__ unsigned long long max(unsigned long long a, unsigned long b) {
+  return a > (unsigned long long)b ? a : (unsigned long long)b;
+}
+__device__ __forceinline__ unsigned long long max(unsigned long a, unsigned long long b) {
+  return (unsigned long long)a > b ? (unsigned long long)a : b;
+}
+
 namespace evm {
 
 typedef unsigned long long u64;

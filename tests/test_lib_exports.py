@@ -58,3 +58,35 @@ def test_dist_unique_id_without_gpu():
 
     a, b = dist_unique_id(), dist_unique_id()
     assert len(a) == 128 and a != b
+
+
+def test_device_code_has_no_floating_point():
+    """Every kernel of libevm is integer work (exact integer /
+    bitwise arithmetic).  A double instruction in the device code means some
+    min / max of a 64-bit key resolved to HIP's double overload (a mixed
+    unsigned long / unsigned long long pair does) and drops the low bits of
+    millis << 16 | counter -- the bug that once made K5's max miss a
+    counter.  Disassembles the built gfx950 code objects (no GPU needed)."""
+    import glob
+    import os
+    import shutil
+    import subprocess
+    import tempfile
+
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not present")
+    from evolu_amd import _lib
+
+    with tempfile.TemporaryDirectory() as d:
+        lib = os.path.join(d, "libevm.so")
+        shutil.copy(_lib.LIB_PATH, lib)
+        subprocess.run([objdump, "--offloading", lib], check=True, capture_output=True, cwd=d)
+        objs = glob.glob(os.path.join(d, "libevm.so.*gfx950"))
+        assert objs
+        for o in objs:
+            asm = subprocess.run([objdump, "-d", "--mcpu=gfx950", o], check=True, capture_output=True,
+                                 text=True).stdout
+            # (f32 ops are the compiler's expansion of 32-bit integer division: exact)
+            bad = [ln for ln in asm.splitlines() if "_f64" in ln]
+            assert not bad, bad[:5]
