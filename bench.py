@@ -113,6 +113,8 @@ def parse():
                          "self-checked; config5shape: the config-5 stream on one GPU, unsharded (profiling)")
     ap.add_argument("--radix", type=int, default=None,
                     help="EVM_OPT_RADIX for --workload config5shape (A/B of 10-bit digits)")
+    ap.add_argument("--server-path", type=int, default=None,
+                    help="EVM_OPT_SERVER_PATH for --workload config5shape (A/B; 4 = K5 on packed records)")
     ap.add_argument("--c5", type=int, default=1, help="N>1 default run: add the config5 and config5c legs")
     ap.add_argument("--c5-owners", type=int, default=125_000, help="config5: owners per GPU")
     ap.add_argument("--c5-messages", type=int, default=125_000_000, help="config5: messages per GPU")
@@ -436,6 +438,8 @@ def main():
         eng = Engine(local)
         if a.radix is not None:
             eng.set_option(4, a.radix)
+        if a.server_path is not None:
+            eng.set_option(2, a.server_path)
         emit(dict(config5_shape_leg(eng, a), metric=METRIC + " [server config 5 shape leg]"))
         eng.close()
         return

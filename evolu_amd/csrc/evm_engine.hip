@@ -949,7 +949,7 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
     ctx->test_fail = (int)value;
     return EVM_OK;
   }
-  if (option == EVM_OPT_SERVER_PATH && value >= 0 && value <= 3) {
+  if (option == EVM_OPT_SERVER_PATH && value >= 0 && value <= 4) {
     ctx->server_path = (int)value;
     return EVM_OK;
   }

@@ -1158,7 +1158,6 @@ __global__ void k_seg_fix(SegView sv, u32 NS, const uint8_t* __restrict__ ownbig
 // segments search the global arrays as before.  Leaves the same way (an equal
 // tree leaf counts one bin higher: it is not below the new code).
 constexpr u32 SVB_LDS = 1024;
-constexpr u32 SVB_CHUNK = 8;  // consecutive output positions per thread in the merge walk
 
 __device__ __forceinline__ void svb_inclusive_prefix(u32* h, u32 m, u32* tmp) {
   // h[0..m) -> inclusive prefix sums in place (m <= SVB_LDS + 1)
@@ -1210,27 +1209,19 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     for (u32 j = threadIdx.x; j <= M; j += SVO_THREADS) hist[j] = 0;
   }
   __syncthreads();
-  // LDS case: count each stored row into the gap of the new keys it falls in
-  // (no write yet); then every output position is written exactly once, in
-  // order, by inverting the merge (below) -- stored and new rows interleave
-  // about 1:1 in a steady-state ingest, and writing the two sides in two
-  // passes left every sector half-written twice (2x the store's write bytes)
-  for (u64 k = sa + threadIdx.x; lds_rows && k < sb; k += SVO_THREADS) {
-    const u64 ktc = st.tc[k], khi = st.hi[k];
-    const u32 klo = st.lo[k];
+  for (u64 k = sa + threadIdx.x; !rows_in_place && k < sb; k += SVO_THREADS) {
+    const SKey key{o, st.tc[k], st.hi[k], st.lo[k]};  // (the segment's stored rows are all owner o's)
     u32 lo = 0, hi = M;
-    while (lo < hi) {  // (one owner: compare (tc, hi, lo))
-      const u32 mid = (lo + hi) >> 1;
-      const bool below = k_tc[mid] != ktc ? k_tc[mid] < ktc : k_hi[mid] != khi ? k_hi[mid] < khi : k_lo[mid] < klo;
-      if (below) lo = mid + 1;
-      else hi = mid;
-    }
-    atomicAdd(&hist[lo], 1u);
-  }
-  for (u64 k = sa + threadIdx.x; !lds_rows && !rows_in_place && k < sb; k += SVO_THREADS) {
-    const SKey key = skey_at(st, k);
-    u32 lo = 0, hi = M;
-    {
+    if (lds_rows) {
+      while (lo < hi) {  // (one owner: compare (tc, hi, lo))
+        const u32 mid = (lo + hi) >> 1;
+        const bool below = k_tc[mid] != key.tc ? k_tc[mid] < key.tc
+                           : k_hi[mid] != key.hi ? k_hi[mid] < key.hi : k_lo[mid] < key.lo;
+        if (below) lo = mid + 1;
+        else hi = mid;
+      }
+      atomicAdd(&hist[lo], 1u);
+    } else {
       while (lo < hi) {
         const u32 mid = (lo + hi) >> 1;
         if (skey_cmp(SKey{o, n_tc[a + mid], n_hi[a + mid], n_lo[a + mid]}, key) < 0) lo = mid + 1;
@@ -1245,43 +1236,17 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     so.id[w] = st_id[k];
   }
   __syncthreads();
-  if (lds_rows) {
-    svb_inclusive_prefix(hist, M + 1, tmp);  // hist[j] = stored rows below new row j
-    // output position w: new row j* if j* + hist[j*] == w for j* = the first
-    // new row at or after w, else stored row sa + w - j*
-    // (each thread a chunk of SVB_CHUNK consecutive positions: one search for
-    // the chunk's start, then a merge walk)
-    const u64 S = sb - sa;
-    for (u64 w0 = (u64)threadIdx.x * SVB_CHUNK; w0 < S + M; w0 += (u64)SVO_THREADS * SVB_CHUNK) {
-      u32 lo = 0, hi = M;
-      while (lo < hi) {
-        const u32 mid = (lo + hi) >> 1;
-        if ((u64)mid + hist[mid] < w0) lo = mid + 1;
-        else hi = mid;
-      }
-      const u64 we = min(w0 + SVB_CHUNK, S + M);
-      for (u64 w = w0; w < we; ++w) {
-        const u64 o_w = base + w;
-        so.owner[o_w] = o;
-        if (lo < M && (u64)lo + hist[lo] == w) {
-          so.tc[o_w] = k_tc[lo];
-          so.hi[o_w] = k_hi[lo];
-          so.lo[o_w] = k_lo[lo];
-          so.id[o_w] = n_id[a + lo];
-          ++lo;
-        } else {
-          const u64 k = sa + w - lo;
-          so.tc[o_w] = st.tc[k];
-          so.hi[o_w] = st.hi[k];
-          so.lo[o_w] = st.lo[k];
-          so.id[o_w] = st_id[k];
-        }
-      }
+  if (lds_rows) svb_inclusive_prefix(hist, M + 1, tmp);  // hist[j] = stored rows below new row j
+  for (u32 j = threadIdx.x; !rows_in_place && j < M; j += SVO_THREADS) {
+    SKey key;
+    u64 below;
+    if (lds_rows) {
+      key = SKey{o, k_tc[j], k_hi[j], k_lo[j]};
+      below = hist[j];
+    } else {
+      key = SKey{o, n_tc[a + j], n_hi[a + j], n_lo[a + j]};
+      below = store_lower(st, sa, sb, key) - sa;
     }
-  }
-  for (u32 j = threadIdx.x; !lds_rows && !rows_in_place && j < M; j += SVO_THREADS) {
-    const SKey key{o, n_tc[a + j], n_hi[a + j], n_lo[a + j]};
-    const u64 below = store_lower(st, sa, sb, key) - sa;
     const u64 w = base + j + below;
     so.owner[w] = o;
     so.tc[w] = key.tc;
@@ -1316,22 +1281,21 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     for (u32 j = threadIdx.x; j <= NL; j += SVO_THREADS) hist[j] = 0;
   }
   __syncthreads();
-  for (u64 k = la + threadIdx.x; lds_leaves && k < lb; k += SVO_THREADS) {
-    const u64 code = t_ck[k];
-    u32 lo = 0, hi = NL;
-    while (lo < hi) {
-      const u32 mid = (lo + hi) >> 1;
-      if (k_tc[mid] < code) lo = mid + 1;
-      else hi = mid;
-    }
-    const bool eq = lo < NL && k_tc[lo] == code;
-    atomicAdd(&hist[lo + (eq ? 1u : 0u)], 1u);  // (an equal tree leaf is not below new leaf j)
-  }
-  for (u64 k = la + threadIdx.x; !lds_leaves && k < lb; k += SVO_THREADS) {
+  for (u64 k = la + threadIdx.x; k < lb; k += SVO_THREADS) {
     const u64 code = t_ck[k];
     u32 j;
     bool eq;
-    {
+    if (lds_leaves) {
+      u32 lo = 0, hi = NL;
+      while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (k_tc[mid] < code) lo = mid + 1;
+        else hi = mid;
+      }
+      j = lo;
+      eq = j < NL && k_tc[j] == code;
+      atomicAdd(&hist[j + (eq ? 1u : 0u)], 1u);  // (an equal tree leaf is not below new leaf j)
+    } else {
       j = (u32)(lb_u64(l_ck, a, a + NL, code) - a);  // new leaves below this code
       eq = j < NL && l_ck[a + j] == code;
     }
@@ -1340,42 +1304,11 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     to_xr[w] = t_xr[k] ^ (eq ? l_xr[a + j] : 0);
   }
   __syncthreads();
-  if (lds_leaves) {
-    svb_inclusive_prefix(hist, NL + 1, tmp);  // hist[j] = tree leaves below new leaf j
-    // output leaf w, written once: G(j) = (j - dups before j) + hist[j] is
-    // non-decreasing; j* = the first j with G(j) >= w.  G(j*) == w: new leaf
-    // j* (a new minute) or, when j* repeats a tree leaf, that tree leaf XOR
-    // j*'s; otherwise tree leaf la + w - (new leaves placed before w)
-    const u64 T = lb - la, L = T + NL - dtot;
-    for (u64 w0 = (u64)threadIdx.x * SVB_CHUNK; w0 < L; w0 += (u64)SVO_THREADS * SVB_CHUNK) {
-      u32 lo = 0, hi = NL;
-      while (lo < hi) {
-        const u32 mid = (lo + hi) >> 1;
-        if ((u64)(mid - s_dp[mid]) + hist[mid] < w0) lo = mid + 1;
-        else hi = mid;
-      }
-      const u64 we = min(w0 + SVB_CHUNK, L);
-      for (u64 w = w0; w < we; ++w) {
-        const u64 o_w = lbase + w;
-        const u32 nd = lo - s_dp[lo];
-        if (lo < NL && (u64)nd + hist[lo] == w) {
-          const bool dup = s_dp[lo + 1] != s_dp[lo];
-          const int32_t x = l_xr[a + lo];
-          to_ck[o_w] = k_tc[lo];
-          to_xr[o_w] = dup ? t_xr[la + hist[lo]] ^ x : x;
-          ++lo;
-        } else {
-          const u64 k = la + w - nd;
-          to_ck[o_w] = t_ck[k];
-          to_xr[o_w] = t_xr[k];
-        }
-      }
-    }
-  }
-  for (u32 j = threadIdx.x; !lds_leaves && j < NL; j += SVO_THREADS) {
+  if (lds_leaves) svb_inclusive_prefix(hist, NL + 1, tmp);  // hist[j] = tree leaves below new leaf j
+  for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) {
     if (l_dup[a + j]) continue;
-    const u64 code = l_ck[a + j];
-    const u64 below = lb_u64(t_ck, la, lb, code) - la;
+    const u64 code = lds_leaves ? k_tc[j] : l_ck[a + j];
+    const u64 below = lds_leaves ? (u64)hist[j] : lb_u64(t_ck, la, lb, code) - la;
     const u64 w = lbase + (j - s_dp[j]) + below;
     to_ck[w] = code;
     to_xr[w] = l_xr[a + j];
@@ -2290,7 +2223,7 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     // the per-owner path parses 16-B aligned rows itself; the records are
     // packed only when a step needs them (cut owners, sort path, culprits)
     const bool defer = !orig && mode == 0 && s->n_owners > 0 && stride >= 48 && stride % 16 == 0 &&
-                       ((uintptr_t)ts & 15) == 0 && ctx->server_path != 3;
+                       ((uintptr_t)ts & 15) == 0 && ctx->server_path != 3 && ctx->server_path != 4;
     std::function<int()> pack_now;
     if (!orig) {
       minute = S.alloc<u32>(n);

@@ -115,7 +115,8 @@ int evm_sync(evm_ctx* ctx);
 #define EVM_OPT_OVERLAP 3     /* 1 (default): independent checks run on a second HIP stream inside a call; 0: one stream */
 #define EVM_OPT_SERVER_PATH 2 /* evm_server_ingest: 0/1 per-owner LDS path, owners above its capacity cut into
                                  key-range segments; 2 force the sort path; 3 LDS path without the segments (owners
-                                 above the capacity through the sort path) */
+                                 above the capacity through the sort path); 4 as 0 with K5 reading packed 32-B
+                                 records instead of parsing the rows itself (A/B) */
 #define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 2 the same with \
                                  10-bit digits when that saves a pass; 0 histogram + scan + scatter per pass */
 #define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM) */
