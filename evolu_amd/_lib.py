@@ -31,6 +31,7 @@ META_RANGE = 0x00040000
 MSG_UPS = 0x01
 MSG_XOR = 0x02
 MSG_INS = 0x04
+ROUTE_NO_SRC = 1  # evm_dist_route_ex: no source indexes wanted (24-B records when aux is absent)
 MSG_BAD = 0x80
 
 OPT_CLIENT_PATH = 1
@@ -111,6 +112,7 @@ SIGNATURES = {
     "evm_dist_init_loopback": (_i, [_vp, _vp, _i, C.POINTER(_vp)]),
     "evm_dist_directory": (_i, [_vp, _vp, _vp, _sz, _sz, _u32, _vp, _vp, C.POINTER(_u32)]),
     "evm_dist_route": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, C.POINTER(C.c_uint64)]),
+    "evm_dist_route_ex": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _u32, C.POINTER(C.c_uint64)]),
     "evm_dist_take": (_i, [_vp, _vp, _u32, _vp, _sz, _vp, _vp, _vp, C.c_uint64, _vp]),
     "evm_dist_gather_roots": (_i, [_vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     "evm_dist_hot_owners": (_i, [_vp, _vp, _vp, _sz, _u32, C.c_double, _vp, _u32, C.POINTER(_u32)]),

@@ -133,19 +133,18 @@ struct RcclTransport final : Transport {
     constexpr uint64_t CHUNK = 1ull << 29;
     if (r->group_start() != ncclSuccess) return EVM_EDIST;
     int st = EVM_OK;
+    // (a zero-length transfer is skipped on both sides alike: the counts agree)
     for (int p = 0; p < world; ++p) {
-      uint64_t o = 0;
-      do {
+      for (uint64_t o = 0; o < slen[p];) {
         const uint64_t k = std::min<uint64_t>(CHUNK, slen[p] - o);
         if (r->send(sbase + soff[p] + o, k, ncclUint8, p, comm, s) != ncclSuccess) st = EVM_EDIST;
         o += k;
-      } while (o < slen[p]);
-      o = 0;
-      do {
+      }
+      for (uint64_t o = 0; o < rlen[p];) {
         const uint64_t k = std::min<uint64_t>(CHUNK, rlen[p] - o);
         if (r->recv(rbase + roff[p] + o, k, ncclUint8, p, comm, s) != ncclSuccess) st = EVM_EDIST;
         o += k;
-      } while (o < rlen[p]);
+      }
     }
     if (r->group_end() != ncclSuccess) st = EVM_EDIST;  // always closed, whatever failed inside
     return st;
@@ -241,11 +240,14 @@ constexpr int DROUNDS = 16;           // rows per thread per block
 constexpr u32 DTILE = DT * DROUNDS;   // rows per block
 constexpr size_t META = 16;           // raw records: owner u32, aux u32, source index u32, pad
 constexpr size_t PACKED = 32;         // packed records (48-B timestamp rows): tc, node, owner, aux, index, case|valid
+constexpr size_t NARROW = 24;         // packed records without aux / source index (EVM_ROUTE_NO_SRC): tc, node, owner, case|valid
+enum { FMT_RAW = 0, FMT_PACKED = 1, FMT_NARROW = 2, FMT_ST8 = 4 /* RECV: rebuilt rows with 8-B stores */ };
 constexpr u32 PK_VALID = 1u << 16;
 // count words exchanged per route: the row count in the low bits, flags on top
 constexpr u64 CNT_ERR = 1ull << 63;      // the sending rank failed locally (nothing is exchanged)
 constexpr u64 CNT_INVALID = 1ull << 62;  // the sending rank holds a row outside the native domain
 constexpr u64 CNT_RAW = 1ull << 61;      // the sending rank cannot send packed records (its stride / alignment)
+constexpr u64 CNT_WIDE = 1ull << 60;     // the sending rank needs aux / source indexes: no narrow records
 constexpr u64 CNT_MASK = (1ull << 48) - 1;
 constexpr int CNT_STRIDE_SHIFT = 48;       // stride / 8 in bits 48..57: raw records need one stride on every rank
 constexpr u64 CNT_STRIDE_MAX = 1023;
@@ -278,7 +280,16 @@ struct Route {
   u32 hot_base;              // local id of hot owner 0 on every rank
   const char* ts;            // SEND: the rows (a split owner's rows go by timestamp hash)
   size_t stride;
+  // RECV: this rank's rows to itself never travel -- received rows
+  // [self_lo, self_hi) are read from the send buffer at self_rec
+  const char* self_rec;
+  u64 self_lo, self_hi;
 };
+
+// received record i: the staging buffer, or this rank's own rows in the send buffer
+__device__ __forceinline__ const char* recv_rec(const Route& R, const char* rec, size_t rb, size_t i) {
+  return (i >= R.self_lo && i < R.self_hi) ? R.self_rec + (i - R.self_lo) * rb : rec + i * rb;
+}
 
 // The timestamp-hash rank of a row (murmur3 of its 46 bytes: equal strings,
 // equal ranks -- every copy of one (owner, timestamp) meets on one rank, so
@@ -315,7 +326,7 @@ __device__ __forceinline__ u32 bucket_of(size_t i, const Route& R, const char* r
     if (R.dir_dest) return o < R.n_dir ? (u32)R.dir_dest[o] : 0xffffffffu;
     return o % R.world;
   }
-  const u32 o = *reinterpret_cast<const u32*>(rec + i * rb + ooff);
+  const u32 o = *reinterpret_cast<const u32*>(recv_rec(R, rec, rb, i) + ooff);
   return local_of(R, o);
 }
 enum { SEND = 0, RECV = 1 };
@@ -417,7 +428,7 @@ __device__ __forceinline__ void copy_row(char* __restrict__ dst, const char* __r
 template <int MODE>
 __global__ __launch_bounds__(DT) void k_dist_scatter(
     Route R, const char* __restrict__ ts, size_t stride, const u32* __restrict__ aux, const char* __restrict__ rec,
-    size_t rb, int packed, size_t n, u32 B, int bits, u32 nblocks, const u32* __restrict__ offs,
+    size_t rb, int fmt, size_t n, u32 B, int bits, u32 nblocks, const u32* __restrict__ offs,
     char* __restrict__ out_rec, char* __restrict__ out_ts, size_t out_stride, u32* __restrict__ out_owner,
     u32* __restrict__ out_aux, u64* __restrict__ out_src, const u64* __restrict__ roff, u32 n_src,
     u32* __restrict__ invalid) {
@@ -430,7 +441,7 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
     const bool ok = i < n;
     size_t pos = i;
     if (offs) {
-      const u32 b = ok ? bucket_of<MODE>(i, R, rec, rb, packed ? 16 : stride) : 0u;
+      const u32 b = ok ? bucket_of<MODE>(i, R, rec, rb, (fmt & 3) ? 16 : stride) : 0u;
       const bool act = ok && b < B;
       const u32 p = rank_slot(L, r, b, act, B, bits);
       if (!act) continue;  // (a row with an out-of-range bucket is reported by k_dist_count)
@@ -438,16 +449,23 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
     } else if (!ok) {
       continue;
     }
-    if (MODE == SEND && packed) {
+    if (MODE == SEND && fmt != FMT_RAW) {
       const uint4* row = reinterpret_cast<const uint4*>(ts + i * stride);
       const uint4 x = row[0], y = row[1], z = row[2];
       const u32 w[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w & 0xffffu};
       const Parsed p = parse_ts46(w);
       inv |= (p.meta & EVM_META_VALID) == 0;
-      uint4* dst = reinterpret_cast<uint4*>(out_rec + pos * rb);
-      dst[0] = make_uint4((u32)p.tc, (u32)(p.tc >> 32), (u32)p.node, (u32)(p.node >> 32));
-      dst[1] = make_uint4(R.owner[i], aux ? aux[i] : 0u, (u32)i,
-                          (p.meta & EVM_META_CASEMASK) | ((p.meta & EVM_META_VALID) ? PK_VALID : 0u));
+      const u32 cm = (p.meta & EVM_META_CASEMASK) | ((p.meta & EVM_META_VALID) ? PK_VALID : 0u);
+      if (fmt == FMT_NARROW) {  // 24 B at 8-B alignment
+        uint2* dst = reinterpret_cast<uint2*>(out_rec + pos * rb);
+        dst[0] = make_uint2((u32)p.tc, (u32)(p.tc >> 32));
+        dst[1] = make_uint2((u32)p.node, (u32)(p.node >> 32));
+        dst[2] = make_uint2(R.owner[i], cm);
+      } else {
+        uint4* dst = reinterpret_cast<uint4*>(out_rec + pos * rb);
+        dst[0] = make_uint4((u32)p.tc, (u32)(p.tc >> 32), (u32)p.node, (u32)(p.node >> 32));
+        dst[1] = make_uint4(R.owner[i], aux ? aux[i] : 0u, (u32)i, cm);
+      }
     } else if (MODE == SEND) {
       char* dst = out_rec + pos * rb;
       copy_row(dst, ts + i * stride, stride);
@@ -458,14 +476,22 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
       m.w = 0u;
       *reinterpret_cast<uint4*>(dst + stride) = m;
     } else {
-      const char* src = rec + i * rb;
+      const char* src = recv_rec(R, rec, rb, i);
       uint4 m;
-      if (packed) {
-        const uint4 a = reinterpret_cast<const uint4*>(src)[0];
-        m = reinterpret_cast<const uint4*>(src)[1];
+      if (fmt & 3) {
+        uint4 a;
+        if ((fmt & 3) == FMT_NARROW) {
+          const uint2* q = reinterpret_cast<const uint2*>(src);
+          const uint2 t = q[0], nd = q[1], om = q[2];
+          a = make_uint4(t.x, t.y, nd.x, nd.y);
+          m = make_uint4(om.x, 0u, 0u, om.y);
+        } else {
+          a = reinterpret_cast<const uint4*>(src)[0];
+          m = reinterpret_cast<const uint4*>(src)[1];
+        }
         u32 w[12];
         format_ts46((u64)a.x | ((u64)a.y << 32), (u64)a.z | ((u64)a.w << 32), m.w & 0xffffu, w);
-        if (packed == 1) {
+        if (!(fmt & FMT_ST8)) {
           uint4* dst = reinterpret_cast<uint4*>(out_ts + pos * out_stride);
           dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
           dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
@@ -493,7 +519,7 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
       }
     }
   }
-  if (MODE == SEND && packed && invalid && __ballot(inv) && __lane_id() == 0) atomicOr(invalid, 1u);
+  if (MODE == SEND && fmt != FMT_RAW && invalid && __ballot(inv) && __lane_id() == 0) atomicOr(invalid, 1u);
 }
 
 // bucket totals from the scanned count matrix
@@ -728,10 +754,10 @@ __global__ void k_sel_merge(const u64* __restrict__ all, u32 world, size_t per, 
 }
 
 // return path: (source index, value) of every received row, in receive order
-__global__ void k_ret_pack(const char* __restrict__ rec, size_t rb, size_t ooff, size_t n,
+__global__ void k_ret_pack(Route R, const char* __restrict__ rec, size_t rb, size_t ooff, size_t n,
                            const uint8_t* __restrict__ val, u32 elem, u64* __restrict__ out) {
   for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    const u32 idx = *reinterpret_cast<const u32*>(rec + k * rb + ooff + 8);
+    const u32 idx = *reinterpret_cast<const u32*>(recv_rec(R, rec, rb, k) + ooff + 8);
     u64 v = 0;
     for (u32 b = 0; b < elem; ++b) v |= (u64)val[k * elem + b] << (8 * b);
     out[2 * k] = idx;
@@ -752,7 +778,7 @@ __global__ void k_ret_scatter(const u64* __restrict__ in, size_t n, uint8_t* __r
 }
 
 // winners: index into the receive order -> global batch index + 1 (0: none)
-__global__ void k_win_map(const int32_t* __restrict__ win, u32 n_cells, const char* __restrict__ rec, size_t rb,
+__global__ void k_win_map(Route R, const int32_t* __restrict__ win, u32 n_cells, const char* __restrict__ rec, size_t rb,
                           size_t ooff, u64 n_recv, const u64* __restrict__ roff, u32 world,
                           const u64* __restrict__ base, u64* __restrict__ out, u32* __restrict__ bad) {
   for (u32 c = blockIdx.x * blockDim.x + threadIdx.x; c < n_cells; c += gridDim.x * blockDim.x) {
@@ -764,7 +790,7 @@ __global__ void k_win_map(const int32_t* __restrict__ win, u32 n_cells, const ch
       } else {
         u32 s = 0;
         while (s + 1 < world && roff[s + 1] <= (u64)w) ++s;
-        const u32 idx = *reinterpret_cast<const u32*>(rec + (size_t)w * rb + ooff + 8);
+        const u32 idx = *reinterpret_cast<const u32*>(recv_rec(R, rec, rb, (size_t)w) + ooff + 8);
         v = base[s] + idx + 1;
       }
     }
@@ -787,6 +813,11 @@ struct evm_dist {
   int rank = 0, world = 1;
   size_t stride = 48, rb = 64;
   int packed = 0;  // the last route's records: packed (48-B rows) or raw
+  int narrow = 0;  // ... packed without aux / source index (24 B)
+  // the last route's rows from this rank to itself stay in the send buffer:
+  // received rows [self_lo, self_hi) at send + self_off
+  uint64_t self_lo = 0, self_hi = 0;
+  size_t self_off = 0;
   char* send = nullptr;  // wire records (send side), device
   size_t send_cap = 0;   // bytes
   char* recv = nullptr;  // received records (staging for evm_dist_take)
@@ -836,6 +867,9 @@ Route route_of(const evm_dist* d, const u32* owner, const uint8_t* dest) {
   R.hot_base = d->hot_base;
   R.ts = nullptr;
   R.stride = 0;
+  R.self_rec = d->send + d->self_off;
+  R.self_lo = d->self_lo;
+  R.self_hi = d->self_hi;
   return R;
 }
 
@@ -1049,6 +1083,11 @@ int evm_dist_directory(evm_ctx* ctx, evm_dist* d, const char* ids, size_t stride
 
 int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, const uint32_t* owner,
                    const uint32_t* aux, const uint8_t* dest, uint64_t* n_recv) {
+  return evm_dist_route_ex(ctx, d, ts, stride, n, owner, aux, dest, 0u, n_recv);
+}
+
+int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                      const uint32_t* aux, const uint8_t* dest, uint32_t flags_in, uint64_t* n_recv) {
   if (!ctx || !d || !n_recv) return EVM_EINVAL;  // nothing to join the collective with
   *n_recv = 0;
   d->n_recv = 0;
@@ -1060,11 +1099,16 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   // raw ones).  Every rank must use one record format: a rank that cannot
   // pack says so in its count words (CNT_RAW) and then every rank sends raw.
   const bool packed0 = !lerr && stride == 48 && (n == 0 || ((uintptr_t)ts & 15) == 0);
-  size_t rb = packed0 ? PACKED : stride + META;
+  // no aux and no source indexes wanted: 24-B records (a quarter fewer xGMI
+  // and HBM bytes), when every rank asks for them (CNT_WIDE otherwise)
+  const bool narrow0 = packed0 && !aux && (flags_in & EVM_ROUTE_NO_SRC);
+  size_t rb = packed0 ? (narrow0 ? NARROW : PACKED) : stride + META;
   Scratch S(ctx);
   u32* flags = S.alloc<u32>(2);  // [0] a destination out of range, [1] a row outside the native domain
   u64* scnt = d->cnt + W_SEND;
   u64* rcnt = d->cnt + W_RECV;
+  d->self_lo = d->self_hi = 0;  // (a failed route leaves no rows to take)
+  d->self_off = 0;
   Route R = route_of(d, owner, dest);
   R.ts = ts;
   R.stride = stride;
@@ -1078,13 +1122,15 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
     lerr = partition_offsets<SEND>(ctx, S, R, nullptr, rb, stride, n, G, &offs, &nblocks, scnt, flags);
     if (!lerr) {
       KLAUNCH((k_dist_scatter<SEND>), dim3(nblocks), dim3(DT), R, ts, stride, aux, (const char*)nullptr, rb,
-              packed0 ? 1 : 0, n, G, ceil_log2(G), nblocks, offs, d->send, (char*)nullptr, (size_t)0, (u32*)nullptr,
-              (u32*)nullptr, (u64*)nullptr, (const u64*)nullptr, 0u, flags + 1);
+              packed0 ? (narrow0 ? (int)FMT_NARROW : (int)FMT_PACKED) : (int)FMT_RAW, n, G, ceil_log2(G), nblocks,
+              offs, d->send, (char*)nullptr, (size_t)0, (u32*)nullptr, (u32*)nullptr, (u64*)nullptr,
+              (const u64*)nullptr, 0u, flags + 1);
       lerr = hip_ok(hipGetLastError());
     }
   }
   // the counts: one all-to-all of G words (flag bits on top), one read back
-  const u64 fmt = (packed0 ? 0ull : CNT_RAW) | ((u64)(lerr ? 0 : stride / 8) << CNT_STRIDE_SHIFT);
+  const u64 fmt = (packed0 ? 0ull : CNT_RAW) | (narrow0 ? 0ull : CNT_WIDE) |
+                  ((u64)(lerr ? 0 : stride / 8) << CNT_STRIDE_SHIFT);
   KLAUNCH(k_dist_mark, dim3(1), dim3(MAX_BUCKETS), scnt, G, (lerr || !n) ? 1 : 0, lerr ? 1 : 0,
           (const u32*)(lerr ? nullptr : flags), fmt);
   int st = d->tx->all_to_all_u64(scnt, rcnt, ctx->stream);
@@ -1098,11 +1144,12 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   HIPR(hipStreamSynchronize(ctx->stream));
   const u64* hs = d->hcnt + W_SEND;
   const u64* hr = d->hcnt + W_RECV;
-  bool any_err = lerr != EVM_OK, any_inv = false, any_raw = false, mixed_stride = false;
+  bool any_err = lerr != EVM_OK, any_inv = false, any_raw = false, any_wide = false, mixed_stride = false;
   for (u32 p = 0; p < G; ++p) {
     any_err |= (hr[p] & CNT_ERR) != 0;
     any_inv |= (hr[p] & CNT_INVALID) != 0;
     any_raw |= (hr[p] & CNT_RAW) != 0;
+    any_wide |= (hr[p] & CNT_WIDE) != 0;
     mixed_stride |= ((hr[p] >> CNT_STRIDE_SHIFT) & CNT_STRIDE_MAX) != stride / 8;
   }
   if (any_err) return lerr ? lerr : EVM_EDIST;  // every rank saw the flag: nobody exchanges
@@ -1115,13 +1162,16 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   // raw records carry the row bytes at the sender's stride: one stride on
   // every rank, or nobody exchanges (every rank sees the mismatch)
   if (!packed && mixed_stride) return EVM_EINVAL;
-  if (packed0 && !packed) {
-    rb = stride + META;
+  const bool narrow = packed && !any_wide;
+  const int fmt_final = packed ? (narrow ? (int)FMT_NARROW : (int)FMT_PACKED) : (int)FMT_RAW;
+  const size_t rb_final = packed ? (narrow ? NARROW : PACKED) : stride + META;
+  if (rb_final != rb) {  // another rank's rows decide the format: scatter again in it
+    rb = rb_final;
     lerr = grow(&d->send, &d->send_cap, std::max<size_t>(n, 1) * rb);
     if (!lerr && n) {
-      KLAUNCH((k_dist_scatter<SEND>), dim3(nblocks), dim3(DT), R, ts, stride, aux, (const char*)nullptr, rb, 0, n, G,
-              ceil_log2(G), nblocks, offs, d->send, (char*)nullptr, (size_t)0, (u32*)nullptr, (u32*)nullptr,
-              (u64*)nullptr, (const u64*)nullptr, 0u, (u32*)nullptr);
+      KLAUNCH((k_dist_scatter<SEND>), dim3(nblocks), dim3(DT), R, ts, stride, aux, (const char*)nullptr, rb,
+              fmt_final, n, G, ceil_log2(G), nblocks, offs, d->send, (char*)nullptr, (size_t)0, (u32*)nullptr,
+              (u32*)nullptr, (u64*)nullptr, (const u64*)nullptr, 0u, (u32*)nullptr);
       lerr = hip_ok(hipGetLastError());
     }
   }
@@ -1143,7 +1193,16 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
     soff[p] *= rb;
     roff[p] = d->recv_off[p] * rb;
   }
+  // this rank's rows to itself stay where the scatter put them (take reads
+  // them there): at world 1 the whole batch, at world G a G-th of it, is not
+  // copied through the transport
+  const u32 me = (u32)d->rank;
+  const size_t self_off = soff[me];
+  slen[me] = rlen[me] = 0;
   if ((st = d->tx->exchange(d->send, soff, slen, d->recv, roff, rlen, ctx->stream))) return st;
+  d->self_off = self_off;
+  d->self_lo = d->recv_off[me];
+  d->self_hi = d->recv_off[me + 1];
   // receive offsets on the device (source rank of every row in evm_dist_take)
   u64* droff = d->cnt + W_ROFF;
   for (u32 p = 0; p <= G; ++p) d->hcnt[W_ROFF + p] = d->recv_off[p];
@@ -1151,6 +1210,7 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
   d->stride = stride;
   d->rb = rb;
   d->packed = packed ? 1 : 0;
+  d->narrow = narrow ? 1 : 0;
   d->n_recv = total;
   d->n_in = n;
   for (u32 p = 0; p < G; ++p) {
@@ -1166,8 +1226,11 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
   if (!ctx || !d || (group && !group_off) || group > MAX_BUCKETS) return EVM_EINVAL;
   const size_t n = d->n_recv;
   if (n && (!out_ts || !out_owner || out_stride < d->stride || out_stride % 8)) return EVM_EINVAL;
-  // rebuilt rows: 16-B stores, or 8-B stores into an output that is only 8-B aligned
-  const int packed = d->packed ? ((out_stride % 16 || ((uintptr_t)out_ts & 15)) ? 2 : 1) : 0;
+  if (n && d->narrow && out_src) return EVM_EINVAL;  // (a EVM_ROUTE_NO_SRC route carried no source indexes)
+  // record format + rebuilt rows: 16-B stores, or 8-B stores into an output that is only 8-B aligned
+  const int packed = d->packed ? ((d->narrow ? (int)FMT_NARROW : (int)FMT_PACKED) |
+                                  ((out_stride % 16 || ((uintptr_t)out_ts & 15)) ? (int)FMT_ST8 : 0))
+                               : (int)FMT_RAW;
   if (n > cap) return EVM_ECAPACITY;
   const u32 G = (u32)d->world;
   const u64* droff = d->cnt + W_ROFF;
@@ -1463,20 +1526,22 @@ int evm_dist_return(evm_ctx* ctx, evm_dist* d, const void* val, uint32_t elem, v
   const size_t n = d->n_recv;
   int lerr = EVM_OK;
   if ((elem != 1 && elem != 2 && elem != 4 && elem != 8) || (n && !val) || (n_out && !out)) lerr = EVM_EINVAL;
+  if (d->narrow) lerr = EVM_EINVAL;  // the last route carried no source indexes (EVM_ROUTE_NO_SRC)
   const size_t ooff = d->packed ? 16 : d->stride;
   Scratch S(ctx);
   u32* bad = S.alloc<u32>(1);
   u64 back = 0;
   for (u32 p = 0; p < G; ++p) back += d->sent[p];
   if (!bad) lerr = lerr ? lerr : EVM_ENOMEM;
-  if (!lerr) lerr = grow(&d->send, &d->send_cap, std::max<size_t>(n, 1) * 16);
+  // (the packed pairs go to scratch: the send buffer still holds this rank's own rows)
+  u64* sbuf = S.alloc<u64>(2 * std::max<size_t>(n, 1));
   u64* rbuf = S.alloc<u64>(2 * std::max<u64>(back, 1));
-  if (!lerr && !rbuf) lerr = EVM_ENOMEM;
+  if (!lerr && (!rbuf || !sbuf)) lerr = EVM_ENOMEM;
   if (!lerr) {
     lerr = hip_ok(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
     if (!lerr && n)
-      KLAUNCH(k_ret_pack, dim3(grid_for(n, 256)), dim3(256), (const char*)d->recv, d->rb, ooff, n,
-              (const uint8_t*)val, elem, reinterpret_cast<u64*>(d->send));
+      KLAUNCH(k_ret_pack, dim3(grid_for(n, 256)), dim3(256), route_of(d, nullptr, nullptr), (const char*)d->recv,
+              d->rb, ooff, n, (const uint8_t*)val, elem, sbuf);
   }
   if (int st = agree(ctx, d, lerr)) return st;
   // rows go back to the rank they came from: the route's counts reversed
@@ -1490,7 +1555,8 @@ int evm_dist_return(evm_ctx* ctx, evm_dist* d, const void* val, uint32_t elem, v
     so += d->recvd[p];
     ro += d->sent[p];
   }
-  int st = d->tx->exchange(d->send, soff, slen, reinterpret_cast<char*>(rbuf), roff, rlen, ctx->stream);
+  int st = d->tx->exchange(reinterpret_cast<const char*>(sbuf), soff, slen, reinterpret_cast<char*>(rbuf), roff, rlen,
+                           ctx->stream);
   if (st) return st;
   if (back)
     KLAUNCH(k_ret_scatter, dim3(grid_for(back, 256)), dim3(256), (const u64*)rbuf, (size_t)back, (uint8_t*)out, n_out,
@@ -1506,6 +1572,7 @@ int evm_dist_split_winners(evm_ctx* ctx, evm_dist* d, const int32_t* win, uint32
   const u32 G = (u32)d->world;
   int lerr = EVM_OK;
   if (n_cells && (!win || !out)) lerr = EVM_EINVAL;
+  if (d->narrow) lerr = EVM_EINVAL;  // (no source indexes)
   uint64_t nin[MAX_BUCKETS];
   int st = gather_status(ctx, d, lerr, ((u64)n_cells << 40) | d->n_in, nin);
   if (st) return st;
@@ -1525,7 +1592,8 @@ int evm_dist_split_winners(evm_ctx* ctx, evm_dist* d, const int32_t* win, uint32
     lerr = hip_ok(hipMemcpyAsync(dbase, base, sizeof(u64) * (G + 1), hipMemcpyHostToDevice, ctx->stream));
     if (!lerr) lerr = hip_ok(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
     if (!lerr && n_cells)
-      KLAUNCH(k_win_map, dim3(grid_for(n_cells, 256)), dim3(256), win, n_cells, (const char*)d->recv, d->rb,
+      KLAUNCH(k_win_map, dim3(grid_for(n_cells, 256)), dim3(256), route_of(d, nullptr, nullptr), win, n_cells,
+              (const char*)d->recv, d->rb,
               d->packed ? (size_t)16 : d->stride, (u64)d->n_recv, (const u64*)(d->cnt + W_ROFF), G,
               (const u64*)dbase, mine, bad);
     if (!lerr) {

@@ -614,12 +614,16 @@ class Dist:
         return dest[:n], local[:n]
 
     def route(self, ts: torch.Tensor, owner: torch.Tensor, aux: Optional[torch.Tensor] = None,
-              dest: Optional[torch.Tensor] = None) -> int:
-        """Collective: rows to rank dest (default owner % world) -> rows received."""
+              dest: Optional[torch.Tensor] = None, need_src: bool = True) -> int:
+        """Collective: rows to rank dest (default owner % world) -> rows received.
+        need_src=False (every rank alike): take() will not return sources and no
+        send_back / split_winners follows -- without aux the rows travel as
+        24-B records (evm_dist_route_ex, EVM_ROUTE_NO_SRC)."""
         n, stride = ts.shape
         nr = C.c_uint64()
-        check(self.eng.lib.evm_dist_route(self.eng.h, self.h, _ptr(ts), stride, n, _ptr(owner), _ptr(aux), _ptr(dest),
-                                          C.byref(nr)), "evm_dist_route")
+        flags = 0 if need_src else _lib.ROUTE_NO_SRC
+        check(self.eng.lib.evm_dist_route_ex(self.eng.h, self.h, _ptr(ts), stride, n, _ptr(owner), _ptr(aux),
+                                             _ptr(dest), flags, C.byref(nr)), "evm_dist_route")
         self.n_recv = nr.value
         self.stride = stride
         return self.n_recv

@@ -98,7 +98,7 @@ class ShardedServer:
     def route(self, ts: torch.Tensor, owner: torch.Tensor, out=None):
         """Rows (global owner ids) of this rank's slice -> the rows of this
         rank's owners from every rank: (ts, local owner int32), batch order."""
-        n = self.dd.route(ts, owner)
+        n = self.dd.route(ts, owner, need_src=False)  # (24-B records: no aux, no sources)
         t, o, _, _, _ = self.dd.take(aux=False, src=False, out=out)
         return t[:n], o[:n]
 

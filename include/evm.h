@@ -436,6 +436,14 @@ int evm_dist_directory(evm_ctx* ctx, evm_dist* d, const char* ids, size_t stride
  * rank after the exchange completed. */
 int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, const uint32_t* owner,
                    const uint32_t* aux, const uint8_t* dest, uint64_t* n_recv);
+/* evm_dist_route with flags.  EVM_ROUTE_NO_SRC: the caller will not ask
+ * evm_dist_take for source indexes nor call evm_dist_return /
+ * evm_dist_split_winners after this route -- with aux == NULL the rows then
+ * travel as 24-B records (tc, node, owner, case mask) instead of 32, when
+ * every rank routes so (the ranks agree through the count words). */
+#define EVM_ROUTE_NO_SRC 1u
+int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, const uint32_t* owner,
+                      const uint32_t* aux, const uint8_t* dest, uint32_t flags, uint64_t* n_recv);
 /* local: the last route's rows into caller buffers (device): out_ts rows of
  * out_stride bytes (out_stride % 8 == 0, out_ts 8-B aligned), out_owner (global ids; local ids with a directory),
  * optional out_aux and out_src (source rank << 32 | index in that rank's

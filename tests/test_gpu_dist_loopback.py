@@ -445,3 +445,42 @@ def test_torch_plan_is_the_c_abi_partition(world):
         sl = slice(cut[r], cut[r + 1])
         assert np.array_equal(tsd, D.ts_dest(t_all[sl], world).numpy())
         assert np.array_equal(cd, D.cell_dest(torch.from_numpy(cell[sl].astype(np.int64)), world).numpy())
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_narrow_records_route(mixed):
+    """evm_dist_route_ex with EVM_ROUTE_NO_SRC and no aux: 24-B records, every
+    row arrives byte-exact with its owner; sources cannot be taken and the
+    return path refuses (on every rank).  One rank asking for sources
+    (mixed): every rank sends 32-B records and sources work again."""
+    from evolu_amd import _lib as L
+
+    world = 2
+    slices = _slices(world, 30_000, 17, 29)
+
+    def fn(r, eng, dd):
+        ts, owner, _ = slices[r]
+        need = mixed and r == 1
+        n = dd.route(eng.dev(ts), eng.dev(owner), need_src=need)
+        t2, o2, _, _, _ = dd.take(aux=False, src=False)
+        got = (n, t2.cpu().numpy(), o2.cpu().numpy().view(np.uint32))
+        st_take = st_ret = None
+        try:
+            dd.take(aux=False, src=True)
+        except L.EngineError as e:
+            st_take = e.status
+        try:
+            dd.send_back(torch.zeros(n, dtype=torch.int32, device=t2.device), len(ts))
+        except L.EngineError as e:
+            st_ret = e.status
+        return got, st_take, st_ret
+
+    res = _loop(world, fn)
+    for r in range(world):
+        ts, owner, _, _ = _expected(slices, world, r, lambda o: o % world)
+        (n, t2, o2), st_take, st_ret = res[r]
+        assert n == len(ts) and np.array_equal(t2[:, :46], ts[:, :46]) and np.array_equal(o2, owner)
+        if mixed:
+            assert st_take is None and st_ret is None
+        else:
+            assert st_take == L.EVM_EINVAL and st_ret in (L.EVM_EINVAL, L.EVM_EDIST)
