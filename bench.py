@@ -79,6 +79,11 @@ SERVER_ALG = {
     # the same with 512-message capacity (first pass when the typical segment is small: Zipf tails)
     "(k_svo_a<512, true>)": (4 + 46 + 1 + 28, 8 + 4 + 1),
     "(k_svo_a<512, false>)": (4 + 32 + 1 + 28, 8 + 4 + 1),
+    # the same over a route's received 24-B records, read where they arrived (evm_dist_ingest)
+    "(k_svo_a<1024, SRC_WIRE>)": (4 + 24 + 1 + 28, 8 + 4 + 1),
+    "(k_svo_a<512, SRC_WIRE>)": (4 + 24 + 1 + 28, 8 + 4 + 1),
+    "k_wire_pack<false>": (24 + 4 + 4, 0),  # wire record + owner in, minute out (segment keys)
+    "k_wire_pack<true>": (24 + 4 + 32 + 4, 0),  # wire record + owner in, 32-B record + minute out
     "k_svo_b": (28 + 32, 8 + 4 + 1 + 8 + 4),  # new rows in, store rows out; new leaves in, tree leaves out
     "k_svo_b<true>": (28 + 32, 8 + 4 + 1 + 8 + 4),  # (the merge into a non-empty store: LDS-staged keys)
     "k_svo_b<false>": (28 + 32, 8 + 4 + 1 + 8 + 4),  # (an empty store)
@@ -126,6 +131,8 @@ def parse():
     ap.add_argument("--c4-owners", type=int, default=125_000, help="config4: owners per GPU")
     ap.add_argument("--c4-per-owner", type=int, default=1000, help="config4: messages per owner")
     ap.add_argument("--c4-sample", type=int, default=1000, help="config4: owners per rank in the self-check")
+    ap.add_argument("--c4-take", action="store_true",
+                    help="config4 / config5: route + take + evm_server_ingest instead of evm_dist_ingest (A/B)")
     ap.add_argument("--loopback", type=int, default=0,
                     help="config4 (or --workload config5 / config5c) rehearsal: N loopback ranks (threads) sharing "
                          "GPU 0 through evm_dist_hub (not a multi-GPU measurement)")
@@ -393,21 +400,23 @@ def main():
     if workload in ("config4", "config5", "config5c"):
         comm = TorchComm(world, dev)
 
-        def leg(fn, *args):
+        def leg(fn, *args, **kw):
             eng = Engine(local)
             dd = make_dist(eng, rank, world)
             try:
-                return fn(eng, dd, comm, *args)
+                return fn(eng, dd, comm, *args, **kw)
             finally:
                 dd.free()
                 eng.close()
                 torch.cuda.empty_cache()
 
         if workload == "config4":
-            res = leg(config4_rank, a.c4_owners, a.c4_per_owner, a.steps, a.warmup, a.c4_sample)
+            res = leg(config4_rank, a.c4_owners, a.c4_per_owner, a.steps, a.warmup, a.c4_sample,
+                      dist_ingest=not a.c4_take)
             data = "synthetic (seeded HLC streams generated on the device, SURVEY 8(d) config 4)"
         elif workload == "config5":
-            res = leg(config5_rank, a.c5_owners, a.c5_messages, a.steps, a.warmup, a.c5_sample, a.c5_share)
+            res = leg(config5_rank, a.c5_owners, a.c5_messages, a.steps, a.warmup, a.c5_sample, a.c5_share,
+                      dist_ingest=not a.c4_take)
             data = "synthetic (device generator evs_config5_shape, SURVEY 8(d) config 5)"
         else:
             res = leg(client_split_rank, a.c5c_messages, a.c5c_cells, a.steps, a.warmup)
@@ -417,7 +426,7 @@ def main():
             # BASELINE config 5 at the same N: the server on the Zipf stream with hot owners
             # split, and one owner's client batch split by cell -- both self-checked
             c5 = leg(config5_rank, a.c5_owners, a.c5_messages, min(a.steps, 5), min(a.warmup, 1), a.c5_sample,
-                     a.c5_share)
+                     a.c5_share, dist_ingest=not a.c4_take)
             c5c = leg(client_split_rank, a.c5c_messages, a.c5c_cells, min(a.steps, 5), min(a.warmup, 1))
             extra = {"config5": c5, "config5c": c5c}
         if rank == 0:
@@ -616,7 +625,7 @@ def main():
             eng4 = Engine(local)
             dd4 = make_dist(eng4, 0, 1)
             out["config4"] = config4_rank(eng4, dd4, TorchComm(1, torch.device("cuda", local)), a.c4_owners,
-                                          a.c4_per_owner, a.steps, a.warmup, a.c4_sample)
+                                          a.c4_per_owner, a.steps, a.warmup, a.c4_sample, dist_ingest=not a.c4_take)
             dd4.free()
             eng4.close()
             torch.cuda.empty_cache()
@@ -630,11 +639,12 @@ def main():
 
 
 XGMI_LINK = 153e9  # B/s per xGMI link (one link per peer in an 8-GPU node)
-ROUTE_BYTES = 32  # packed wire record per routed message (evm_dist.hip: tc, node, case mask, owner, cell, index)
-DIST_ALG = {
+ROUTE_BYTES = 24  # wire record per routed message of a server route (evm_dist.hip narrow: tc, node, owner, case mask)
+DIST_ALG = {  # (the server benches route 24-B records: no cell / source index travels)
     "(k_dist_count<MODE>)": 4,  # owner in (send side: caller's owner ids; take side: the records' owner field)
-    "(k_dist_scatter<SEND>)": 48 + 4 + 4 + 32,  # ts row + owner + cell in, packed record out
-    "(k_dist_scatter<RECV>)": 32 + 48 + 4 + 4,  # packed record in; rebuilt ts row + owner + cell out
+    "(k_dist_scatter<SEND>)": 48 + 4 + 24,  # ts row + owner in, wire record out
+    "(k_dist_scatter<RECV>)": 24 + 48 + 4,  # wire record in; rebuilt ts row + owner out (evm_dist_take)
+    "k_dist_owner": 24 + 4,  # wire record in (the owner field's sectors), local owner out (evm_dist_ingest)
 }
 
 
@@ -895,7 +905,7 @@ C4_SEED = 0xE7010004  # seed = 0xE7010000 + config number
 
 
 def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10, warmup=2, sample=1000,
-                 seed=C4_SEED, verbose=False):
+                 seed=C4_SEED, verbose=False, dist_ingest=True):
     """BASELINE config 4 on one rank: the sync server (index.ts:138-202,
     addMessages + getMessages) over owners_per_gpu x world owners of
     per_owner messages each, sharded by murmur3(userId) mod world.
@@ -959,13 +969,22 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
 
     def step():
         r0 = time.perf_counter()
-        t_r, o_r = srv.route(ts_in, owner_in, out=out)
-        route_ms.append((time.perf_counter() - r0) * 1e3)
-        srv.new_store()
-        srv.store.ingest(t_r, o_r, id_base, flags=flags)
+        if dist_ingest:
+            # route + addMessages on the received records where they lie (evm_dist_ingest)
+            n_r = srv.dd.route(ts_in, owner_in, need_src=False)
+            route_ms.append((time.perf_counter() - r0) * 1e3)
+            srv.new_store()
+            srv.dd.ingest(srv.store, id_base, flags)
+        else:
+            # route + take (48-B rows rebuilt) + evm_server_ingest
+            t_r, o_r = srv.route(ts_in, owner_in, out=out)
+            route_ms.append((time.perf_counter() - r0) * 1e3)
+            n_r = t_r.shape[0]
+            srv.new_store()
+            srv.store.ingest(t_r, o_r, id_base, flags=flags)
         diff, off, sel = srv.select(client, node)
         root, present = srv.roots()
-        last.update(n_r=t_r.shape[0], diff=diff, off=off, sel=sel, root=root, present=present)
+        last.update(n_r=n_r, diff=diff, off=off, sel=sel, root=root, present=present)
 
     for _ in range(warmup):
         step()
@@ -998,6 +1017,8 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
 
     # ---- self-check: `sample` owners re-derived unsharded on this GPU
     n_r = last["n_r"]
+    if dist_ingest:
+        srv.take_routed(out=out)  # the last round's rows (ids = receive index), for the byte compare
     k = min(sample, n_local)
     ok = n_r == n_exp
     detail = {"received": int(n_r), "expected": int(n_exp)}
@@ -1059,9 +1080,11 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
                                "msgs = %d msgs over %d GPU(s) (%d owners x %d msgs per GPU, weak scaling: 1B msgs over "
                                "1M owners at 8 GPUs), owners sharded by murmur3(userId) mod %d on the device "
                                "(evm_dist_directory), every rank's slice holds one request per owner of the job, "
-                               "routed over %s (evm_dist_route, 32-B packed records), ingest into an empty store, "
+                               "routed over %s (evm_dist_route, 24-B packed records), %s, "
                                "getMessages vs each owner's client tree (~90 %% known), roots all-gathered"
-                               % (O, P, O * P, world, owners_per_gpu, P, world, dd.transport),
+                               % (O, P, O * P, world, owners_per_gpu, P, world, dd.transport,
+                                  "ingest of the received records in place into an empty store (evm_dist_ingest)"
+                                  if dist_ingest else "take (rows rebuilt) + ingest into an empty store"),
                    "messages_per_gpu": n, "owners_total": O, "owners_per_gpu": owners_per_gpu,
                    "owners_this_rank": n_local, "parallelism": "owner-sharded (murmur3 mod %d), %s" % (world, dd.transport)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": alg / avg_s / 1e9, "peak": HBM_PEAK / 1e9,
@@ -1094,7 +1117,8 @@ def config4_loopback(a, world, device=0):
 
     def fn(r, eng, dd):
         try:
-            return config4_rank(eng, dd, comm.bind(r), a.c4_owners, a.c4_per_owner, a.steps, a.warmup, a.c4_sample)
+            return config4_rank(eng, dd, comm.bind(r), a.c4_owners, a.c4_per_owner, a.steps, a.warmup, a.c4_sample,
+                                dist_ingest=not a.c4_take)
         except BaseException:
             comm.bar.abort()  # the other ranks may wait in a bench barrier, not a collective
             raise
@@ -1139,7 +1163,7 @@ def _leaves_equal(ta, a, tb, b, count=1):
 
 
 def config5_rank(eng, dd, comm, owners_per_gpu=125_000, n_per_gpu=125_000_000, steps=5, warmup=1, sample=200,
-                 share=0.1, seed=C5_SEED, verbose=False):
+                 share=0.1, seed=C5_SEED, verbose=False, dist_ingest=True):
     """BASELINE config 5 on the server at N GPUs, through the C ABI the Node
     caller uses (evolu_amd/sharded.py ShardedServer):
     owners_per_gpu x world owners with Zipf(1.2) sizes, n_per_gpu messages
@@ -1154,8 +1178,9 @@ def config5_rank(eng, dd, comm, owners_per_gpu=125_000, n_per_gpu=125_000_000, s
     split over every rank by timestamp hash (evm_dist_split); one round routed
     and ingested to learn what each owner's client knows (keep flag, first
     copy); the client trees (a split owner's: every rank's part merged,
-    evm_dist_merge_trees).  One step = route (evm_dist_route + take, local
-    ids) + addMessages into an empty store (evm_server_ingest) + getMessages
+    evm_dist_merge_trees).  One step = route (evm_dist_route, 24-B records)
+    + addMessages of the received records in place into an empty store
+    (evm_dist_ingest; dist_ingest=False: take + evm_server_ingest) + getMessages
     (evm_server_select; split owners: full-tree diffs, each rank's share after
     the bound, shares merged in timestamp order by evm_dist_merge_select) +
     every owner's root all-gathered (evm_dist_gather_roots XORs the split
@@ -1213,17 +1238,24 @@ def config5_rank(eng, dd, comm, owners_per_gpu=125_000, n_per_gpu=125_000_000, s
 
     def step():
         r0 = time.perf_counter()
-        t, o = srv.route(ts_in, owner_in, out=out)
-        route_ms.append((time.perf_counter() - r0) * 1e3)
-        srv.new_store()
-        srv.store.ingest(t, o, id_base, flags=flags)
+        if dist_ingest:
+            n_s = srv.dd.route(ts_in, owner_in, need_src=False)
+            route_ms.append((time.perf_counter() - r0) * 1e3)
+            srv.new_store()
+            srv.dd.ingest(srv.store, id_base, flags)
+        else:
+            t, o = srv.route(ts_in, owner_in, out=out)
+            n_s = t.shape[0]
+            route_ms.append((time.perf_counter() - r0) * 1e3)
+            srv.new_store()
+            srv.store.ingest(t, o, id_base, flags=flags)
         sel = srv.select(client, node)
         if nh:
             diff, (off, sid), (hoff, hid) = sel
         else:
             (diff, off, sid), hoff, hid = sel, None, None
         root, present = srv.roots()
-        last.update(n=t.shape[0], diff=diff, off=off, sid=sid, hoff=hoff, hid=hid, root=root, present=present)
+        last.update(n=n_s, diff=diff, off=off, sid=sid, hoff=hoff, hid=hid, root=root, present=present)
 
     for _ in range(warmup):
         step()
@@ -1257,6 +1289,8 @@ def config5_rank(eng, dd, comm, owners_per_gpu=125_000, n_per_gpu=125_000_000, s
     # ---- self-check: sampled cold owners + every split owner, unsharded on this GPU
     t_chk = time.perf_counter()
     n = last["n"]
+    if dist_ingest:
+        srv.take_routed(out=out)  # the last round's rows (ids = receive index), for the byte compare
     cold = np.flatnonzero(glob[:base] >= 0)
     pick = cold[np.unique(np.linspace(0, len(cold) - 1, min(sample, len(cold))).round().astype(np.int64))] \
         if len(cold) else np.zeros(0, dtype=np.int64)
@@ -1387,7 +1421,7 @@ def config5_loopback(a, world, device=0):
     def fn(r, eng, dd):
         try:
             return config5_rank(eng, dd, comm.bind(r), a.c5_owners, a.c5_messages, a.steps, a.warmup, a.c5_sample,
-                                a.c5_share)
+                                a.c5_share, dist_ingest=not a.c4_take)
         except BaseException:
             comm.bar.abort()
             raise

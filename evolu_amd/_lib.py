@@ -114,6 +114,8 @@ SIGNATURES = {
     "evm_dist_route": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, C.POINTER(C.c_uint64)]),
     "evm_dist_route_ex": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _u32, C.POINTER(C.c_uint64)]),
     "evm_dist_take": (_i, [_vp, _vp, _u32, _vp, _sz, _vp, _vp, _vp, C.c_uint64, _vp]),
+    "evm_dist_ingest": (_i, [_vp, _vp, _vp, C.c_uint64, _vp]),
+    "evm_dist_received": (C.c_uint64, [_vp]),
     "evm_dist_gather_roots": (_i, [_vp, _vp, _vp, _u32, _u32, _vp, _vp]),
     "evm_dist_hot_owners": (_i, [_vp, _vp, _vp, _sz, _u32, C.c_double, _vp, _u32, C.POINTER(_u32)]),
     "evm_dist_split": (_i, [_vp, _vp, _vp, _u32, _u32, C.POINTER(_u32)]),

@@ -522,6 +522,13 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
   if (MODE == SEND && fmt != FMT_RAW && invalid && __ballot(inv) && __lane_id() == 0) atomicOr(invalid, 1u);
 }
 
+// the local owner of every received packed record (evm_dist_ingest): the
+// records stay where they are, only the owner column is written
+__global__ void k_dist_owner(Route R, const char* __restrict__ rec, size_t rb, size_t n, u32* __restrict__ out) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = local_of(R, *reinterpret_cast<const u32*>(recv_rec(R, rec, rb, i) + 16));
+}
+
 // bucket totals from the scanned count matrix
 __global__ void k_dist_totals(const u32* __restrict__ offs, const u32* __restrict__ total, u32 B, u32 nblocks,
                               u64* __restrict__ out) {
@@ -1266,6 +1273,32 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
   group_off[0] = 0;
   for (u32 b = 0; b < group; ++b) group_off[b + 1] = group_off[b] + h[b];
   return EVM_OK;
+}
+
+uint64_t evm_dist_received(const evm_dist* d) { return d ? d->n_recv : 0; }
+
+int evm_dist_ingest(evm_ctx* ctx, evm_dist* d, evm_store* store, uint64_t id_base, uint8_t* flags) {
+  if (!ctx || !d || !store) return EVM_EINVAL;
+  const size_t n = d->n_recv;
+  if (n == 0) return EVM_OK;
+  if (!flags || !(d->dir_local || d->hot)) return EVM_EINVAL;  // local ids come from the directory / split
+  Scratch S(ctx);
+  u32* owner = S.alloc<u32>(n);
+  if (!owner) return EVM_ENOMEM;
+  const Route R = route_of(d, nullptr, nullptr);
+  if (!d->packed) {
+    // raw records (some rank's rows are outside the native domain): the rows
+    // themselves, then the ingest that flags the culprits
+    const size_t os = (d->stride + 15) & ~(size_t)15;
+    char* rows = S.alloc<char>(n * os);
+    if (!rows) return EVM_ENOMEM;
+    int st = evm_dist_take(ctx, d, 0, rows, os, owner, nullptr, nullptr, n, nullptr);
+    if (st) return st;
+    return evm_server_ingest(ctx, store, rows, os, n, owner, id_base, flags);
+  }
+  KLAUNCH(k_dist_owner, dim3(grid_for(n, 256, 16384)), dim3(256), R, (const char*)d->recv, d->rb, n, owner);
+  const WireSrc w{d->recv, R.self_rec, R.self_lo, R.self_hi, (u32)d->rb, d->narrow ? 20u : 28u};
+  return server_ingest_wire(ctx, store, w, n, owner, id_base, flags);
 }
 
 int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* const* trees, uint32_t n_trees,

@@ -317,4 +317,33 @@ int merge_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, 
 int fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u64* ck, u32* h, size_t m,
                    const Info& host_info, evm_tree** out);
 
+// A route's received packed records, read where they lie (evm_dist_ingest):
+// record i at rec + i * rb, except this rank's own rows [self_lo, self_hi),
+// which never left the send buffer (at self).  Every record: tc u64 at 0,
+// node u64 at 8, global owner u32 at 16, case mask | EVM_META_VALID u32 at
+// moff (28 in 32-B records, 20 in 24-B ones) -- the parsed form of a 46-B
+// timestamp, rebuilt exactly by format_ts46.
+struct WireSrc {
+  const char* rec;
+  const char* self;
+  u64 self_lo, self_hi;
+  u32 rb, moff;
+};
+__device__ __forceinline__ const char* wire_at(const WireSrc& w, size_t i) {
+  return (i >= w.self_lo && i < w.self_hi) ? w.self + (i - w.self_lo) * w.rb : w.rec + i * w.rb;
+}
+__device__ __forceinline__ void wire_load(const WireSrc& w, size_t i, u64* tc, u64* node, u32* cm) {
+  const char* p = wire_at(w, i);
+  const uint2* q = reinterpret_cast<const uint2*>(p);
+  const uint2 a = q[0], b = q[1];
+  *tc = (u64)a.x | ((u64)a.y << 32);
+  *node = (u64)b.x | ((u64)b.y << 32);
+  *cm = *reinterpret_cast<const u32*>(p + w.moff);
+}
+// addMessages over received records (evm_server.hip): owner[i] = the local
+// owner of record i; ids id_base + i, flags[i] -- as evm_server_ingest over
+// the rows evm_dist_take would rebuild, without rebuilding them
+int server_ingest_wire(evm_ctx* ctx, evm_store* s, const WireSrc& w, size_t n, const u32* owner, uint64_t id_base,
+                       uint8_t* flags);
+
 }  // namespace evm

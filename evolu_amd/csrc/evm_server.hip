@@ -652,7 +652,10 @@ struct SvoLog2 {
 // owner's share in batch order): node ranks, batch index, hash; sort keys
 // (tc - tc_min) << PB | t, sorted by a bitonic network (8-B elements only);
 // runs of one tc (distinct nodes) are then put in node order.
-template <u32 CAP, bool PARSE, int THREADS = SVO_THREADS>
+// where K5 reads a message: packed records (evm_rec), the 48-B timestamp
+// rows (parsed in the workgroup), or a route's received records in place
+enum { SRC_REC = 0, SRC_ROWS = 1, SRC_WIRE = 2 };
+template <u32 CAP, int SRC, int THREADS = SVO_THREADS>
 __global__ __launch_bounds__(THREADS) void k_svo_a(
     const evm_rec* __restrict__ rec, const uint8_t* __restrict__ ts, size_t stride, Info* __restrict__ info,
     const u32* __restrict__ perm, SegView sv, StoreView st,
@@ -661,7 +664,8 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status,
     const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list, u32* __restrict__ mid1,
-    uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner, int flags_preset, u32* __restrict__ mid512) {
+    uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner, int flags_preset, u32* __restrict__ mid512,
+    WireSrc wsrc) {
   constexpr int PER = CAP / THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
   constexpr u64 PMASK = CAP - 1;
@@ -722,7 +726,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     bi[k] = t < m ? perm[a + t] : 0u;
   }
   u64 tmin = ~0ull, tmax = 0;
-  if (PARSE) {
+  if (SRC == SRC_ROWS) {
     // the timestamp rows themselves (no packed records): parse + murmur3 here
     u32 bad = 0;
     for (int k = 0; k < PER; ++k) {
@@ -749,6 +753,31 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       }
     }
     if (__ballot(bad) && lane == 0) atomicOr(&info->bad, 1u);  // nothing is applied: the host re-packs to flag them
+  } else if (SRC == SRC_WIRE) {
+    // received (tc, node, case mask): the string is rebuilt in registers for
+    // murmur3 (a canonical timestamp is a function of them)
+    u32 bad = 0;
+    for (int k = 0; k < PER; ++k) {
+      const u32 t = threadIdx.x + k * THREADS;
+      if (t < m) {
+        u64 wtc, wnode;
+        u32 cm;
+        wire_load(wsrc, bi[k], &wtc, &wnode, &cm);
+        u32 w[12];
+        format_ts46(wtc, wnode, cm & EVM_META_CASEMASK, w);
+        bad |= (cm & EVM_META_VALID) ? 0u : 1u;
+        u64 hi;
+        u32 lo;
+        node_ranks(wnode, cm & EVM_META_CASEMASK, &hi, &lo);
+        s_rh[t] = hi;
+        s_rl[t] = lo;
+        s_h[t] = murmur3_46(w);
+        tc[k] = wtc;
+        tmin = min(tmin, wtc);
+        tmax = max(tmax, wtc);
+      }
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(&info->bad, 1u);
   } else {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -1017,7 +1046,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
         if (q < sb && skey_cmp(skey_at(st, q), k) == 0) {
           const u32 pos = (u32)(s_k[p] & PMASK);
           const u32 b = perm[a + pos];
-          const u64 in_tc = PARSE ? 0ull : rec[b].tc;
+          const u64 in_tc = SRC != SRC_REC ? 0ull : rec[b].tc;
           printf("scan miss: seg %u owner %u p %u m %llu sa %llu sb %llu tc %llx tmin %llx tmax %llx CAP %u kp %llx "
                  "pos %u in_tc %llx stored_q %llu\n", s, o, p, (unsigned long long)m, (unsigned long long)sa,
                  (unsigned long long)sb, (unsigned long long)mt[r], (unsigned long long)tmin, (unsigned long long)tmax,
@@ -1758,10 +1787,69 @@ static int base3_len_host(uint32_t m) {
 // SVO_CAP or mixes key lengths: the caller takes the global sort path with
 // the same packed records.  Validity of the batch is checked here (one host
 // round trip for the whole ingest).
+// Received route records -> packed records (REC) and / or the compact
+// minutes, with the pack's checks: the local owner in range (bad_aux), the
+// native domain (bad), the minute range.  aux = the local owner.
+template <bool REC>
+__global__ __launch_bounds__(256) void k_wire_pack(WireSrc w, size_t n, const u32* __restrict__ owner, u32 limit,
+                                                   evm_rec* __restrict__ out, Info* __restrict__ info,
+                                                   u32* __restrict__ minute_out) {
+  u32 bad = 0, bad_aux = 0, mn = 0xffffffffu, mx = 0u;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    u64 tc, node;
+    u32 cm;
+    wire_load(w, i, &tc, &node, &cm);
+    const u32 o = owner[i];
+    const u32 minute = (u32)((tc >> 16) / 60000ull);
+    bad_aux |= o >= limit ? 1u : 0u;
+    if (REC) {
+      u32 ww[12];
+      format_ts46(tc, node, cm & EVM_META_CASEMASK, ww);
+      evm_rec r;
+      r.tc = tc;
+      r.node = node;
+      r.meta = cm;
+      r.hash = (cm & EVM_META_VALID) ? murmur3_46(ww) : 0u;
+      r.minute = minute;
+      r.aux = o;
+      out[i] = r;
+    }
+    if (minute_out) minute_out[i] = minute;
+    if (cm & EVM_META_VALID) {
+      mn = min(mn, minute);
+      mx = max(mx, minute);
+    } else {
+      bad = 1;
+    }
+  }
+  bad = wave_max(bad);
+  bad_aux = wave_max(bad_aux);
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) {
+    if (bad) atomic_or_if(&info->bad, 1u);
+    if (bad_aux) atomic_or_if(&info->bad_aux, 1u);
+    if (mn != 0xffffffffu) {
+      atomic_min_if(&info->minute_min, mn);
+      atomic_max_if(&info->minute_max, mx);
+    }
+  }
+}
+
+int launch_wire_pack(evm_ctx* ctx, const WireSrc& w, size_t n, const u32* owner, u32 limit, evm_rec* out, Info* info,
+                     u32* minute_out) {
+  if (n == 0) return EVM_OK;
+  if (out)
+    KLAUNCH(k_wire_pack<true>, dim3(grid_for(n, 256, 8192)), dim3(256), w, n, owner, limit, out, info, minute_out);
+  else
+    KLAUNCH(k_wire_pack<false>, dim3(grid_for(n, 256, 8192)), dim3(256), w, n, owner, limit, out, info, minute_out);
+  return hip_ok(hipGetLastError());
+}
+
 int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec* rec, const u32* minute,
                     const u32* owner, size_t n, const u32* orig, uint64_t id_base, uint8_t* flags, Info* info, u32* perm,
                     evm_store* ns, evm_tree** new_tree, bool* done, uint8_t* bigmask, bool* big_only, const char* ts,
-                    size_t stride, const std::function<int()>& pack_now) {
+                    size_t stride, const std::function<int()>& pack_now, const WireSrc* wire) {
   // fused: the records are not packed yet; K5 parses the timestamp rows itself
   // unless a step needs records or minutes (then pack_now() packs them)
   bool fused = (bool)pack_now;
@@ -1775,6 +1863,10 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   bool have_min = false;
   auto minutes = [&]() -> int {
     if (!fused || have_min) return EVM_OK;
+    if (wire) {
+      have_min = true;
+      return launch_wire_pack(ctx, *wire, n, owner, s->n_owners, nullptr, info, const_cast<u32*>(minute));
+    }
     if (stride != 48) return unfuse();
     have_min = true;
     return launch_minutes(ctx, ts, n, owner, s->n_owners, info, const_cast<u32*>(minute));
@@ -2001,6 +2093,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   // the common share size over every segment (more workgroups per CU); larger
   // shares are listed and take the SVO_CAP kernel over just those segments
   const uint8_t* tsb = reinterpret_cast<const uint8_t*>(ts);
+  const WireSrc wsrc = wire ? *wire : WireSrc{nullptr, nullptr, 0, 0, 0, 0};
   // pass A over every segment with the capacity that fits the typical share
   // (small segments -- Zipf tails, cut owners -- take the 512 kernel: half the
   // per-workgroup fixed work, twice the occupancy); larger shares are listed
@@ -2009,20 +2102,24 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   auto pass = [&](u32 cap, dim3 grid, const u32* list, u32* l1, u32* l2, u32* l512) {
 #define SVO_ARGS                                                                                                      \
   rec, tsb, stride, info, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, \
-      l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, list, l2, l1, ownbig, n_owner, preset, l512
-    // (the one-wave kernels: Zipf-tail owners of <= 128 / <= 256 messages, no cross-wave barriers)
-    if (cap == 128 && fused) KLAUNCH((k_svo_a<128, true, 64>), grid, dim3(64), SVO_ARGS);
-    else if (cap == 128) KLAUNCH((k_svo_a<128, false, 64>), grid, dim3(64), SVO_ARGS);
-    else if (cap == 256 && fused) KLAUNCH((k_svo_a<256, true, 64>), grid, dim3(64), SVO_ARGS);
-    else if (cap == 256) KLAUNCH((k_svo_a<256, false, 64>), grid, dim3(64), SVO_ARGS);
-    else if (cap == 512 && fused) KLAUNCH((k_svo_a<512, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
-    else if (cap == 512) KLAUNCH((k_svo_a<512, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
-    else if (cap == 1024 && fused) KLAUNCH((k_svo_a<1024, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
-    else if (cap == 1024) KLAUNCH((k_svo_a<1024, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
-    else if (cap == 2048 && fused) KLAUNCH((k_svo_a<2048, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
-    else if (cap == 2048) KLAUNCH((k_svo_a<2048, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
-    else if (fused) KLAUNCH((k_svo_a<SVO_CAP, true>), grid, dim3(SVO_THREADS), SVO_ARGS);
-    else KLAUNCH((k_svo_a<SVO_CAP, false>), grid, dim3(SVO_THREADS), SVO_ARGS);
+      l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, list, l2, l1, ownbig, n_owner, preset, l512, wsrc
+    // (the one-wave kernels: Zipf-tail owners of <= 128 / <= 256 messages, no cross-wave barriers;
+    // source: true = the rows, false = packed records, SRC_WIRE = received records)
+#define SVO_PASS(SRCV)                                                                         \
+  if (cap == 128) KLAUNCH((k_svo_a<128, SRCV, 64>), grid, dim3(64), SVO_ARGS);                  \
+  else if (cap == 256) KLAUNCH((k_svo_a<256, SRCV, 64>), grid, dim3(64), SVO_ARGS);             \
+  else if (cap == 512) KLAUNCH((k_svo_a<512, SRCV>), grid, dim3(SVO_THREADS), SVO_ARGS);        \
+  else if (cap == 1024) KLAUNCH((k_svo_a<1024, SRCV>), grid, dim3(SVO_THREADS), SVO_ARGS);      \
+  else if (cap == 2048) KLAUNCH((k_svo_a<2048, SRCV>), grid, dim3(SVO_THREADS), SVO_ARGS);      \
+  else KLAUNCH((k_svo_a<SVO_CAP, SRCV>), grid, dim3(SVO_THREADS), SVO_ARGS);
+    if (fused && wire) {
+      SVO_PASS(SRC_WIRE)
+    } else if (fused) {
+      SVO_PASS(true)
+    } else {
+      SVO_PASS(false)
+    }
+#undef SVO_PASS
 #undef SVO_ARGS
   };
   if (small) {
@@ -2180,7 +2277,8 @@ static int commit_store(evm_ctx* ctx, evm_store* s, evm_store& ns, evm_tree* new
 // owners are independent, so the result is the one of a single ingest;
 // mode 2: the sort path.
 static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride, size_t n, const uint32_t* owner,
-                       const u32* orig, const evm_rec* prec, uint64_t id_base, uint8_t* flags, int mode) {
+                       const u32* orig, const evm_rec* prec, uint64_t id_base, uint8_t* flags, int mode,
+                       const WireSrc* wire = nullptr) {
   if (orig && !prec) return EVM_EINVAL;
   int st;
   evm_store ns{};
@@ -2222,14 +2320,16 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
     u32* minute = nullptr;  // compact minutes (segment keys); a sub-batch reads them from the records
     // the per-owner path parses 16-B aligned rows itself; the records are
     // packed only when a step needs them (cut owners, sort path, culprits)
-    const bool defer = !orig && mode == 0 && s->n_owners > 0 && stride >= 48 && stride % 16 == 0 &&
-                       ((uintptr_t)ts & 15) == 0 && ctx->server_path != 3 && ctx->server_path != 4;
+    // (received route records: K5 reads them where they lie)
+    const bool defer = !orig && mode == 0 && s->n_owners > 0 && ctx->server_path != 3 && ctx->server_path != 4 &&
+                       (wire || (stride >= 48 && stride % 16 == 0 && ((uintptr_t)ts & 15) == 0));
     std::function<int()> pack_now;
     if (!orig) {
       minute = S.alloc<u32>(n);
       if (!minute) return EVM_ENOMEM;
       auto do_pack = [&, minute]() -> int {
-        int e = launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info, minute);
+        int e = wire ? launch_wire_pack(ctx, *wire, n, owner, s->n_owners, rec, info, minute)
+                     : launch_pack(ctx, ts, stride, n, owner, s->n_owners, rec, info, minute);
         if (!e) have_rec = true;
         return e;
       };
@@ -2245,7 +2345,7 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       uint8_t* bigmask = (mode == 0 && !orig) ? S.alloc<uint8_t>(n) : nullptr;
       if (mode == 0 && !orig && !bigmask) return EVM_ENOMEM;
       if ((st = ingest_by_owner(ctx, S, s, rec, minute, own, n, orig, id_base, flags, info, perm, &ns, &new_tree,
-                                &done, bigmask, &big_only, ts, stride, pack_now)))
+                                &done, bigmask, &big_only, ts, stride, pack_now, wire)))
         return st;
       if (done && big_only && !orig) {
         // the LDS path took every owner but the big ones: commit that, then
@@ -2473,6 +2573,15 @@ int evm_server_ingest_ex(evm_ctx* ctx, evm_store* s, const char* ts, size_t stri
 }
 
 }  // extern "C"
+
+int evm::server_ingest_wire(evm_ctx* ctx, evm_store* s, const WireSrc& w, size_t n, const u32* owner, uint64_t id_base,
+                            uint8_t* flags) {
+  if (!ctx || !s || (n && (!owner || !flags))) return EVM_EINVAL;
+  if (n == 0) return EVM_OK;
+  if (n >= 0xffffffffull) return EVM_EINVAL;
+  return ingest_impl(ctx, s, nullptr, 48, n, owner, nullptr, nullptr, id_base, flags, ctx->server_path == 2 ? 2 : 0,
+                     &w);
+}
 
 // Selection of each owner's rows after a per-owner bound (diff/since, < 0 =
 // none), optionally excluding one node (server getMessages).

@@ -646,6 +646,18 @@ class Dist:
         g = [int(x) for x in goff] if group else None
         return ts[:n], ow[:n], (ax[:n] if ax is not None else None), (sr[:n] if sr is not None else None), g
 
+    def ingest(self, store: "Store", id_base: int = 0, flags: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """addMessages of the last route's rows into `store` (evm_dist_ingest:
+        the packed records read where they arrived; row i of the receive
+        order has id id_base + i) -> flags uint8[n_recv]."""
+        n = self.n_recv
+        if flags is None:
+            flags = torch.empty(max(n, 1), dtype=torch.uint8, device=torch.device("cuda", self.eng.device))
+        if flags.numel() < n:
+            raise ValueError("flags holds %d < %d rows" % (flags.numel(), n))
+        check(self.eng.lib.evm_dist_ingest(self.eng.h, self.h, store.h, id_base, _ptr(flags)), "evm_dist_ingest")
+        return flags[:n]
+
     def gather_roots(self, trees, n_owners_global: int):
         """Collective: every global owner's (root int32, present bool) on the device.
         trees: one Trees (its owners = this rank's local owners) or a list of them."""

@@ -112,6 +112,22 @@ class ShardedServer:
         f, _ = self.store.ingest(t, o, id_base, flags=flags)
         return t, o, f
 
+    def route_ingest(self, ts: torch.Tensor, owner: torch.Tensor, id_base: int = 0,
+                     flags: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """addMessages for a round without rebuilding the received rows:
+        route (24-B records) + evm_dist_ingest into this rank's store.
+        Returns the flags in receive order (ids id_base + receive index);
+        `take_routed` gives the rows themselves when a caller needs them."""
+        self.dd.route(ts, owner, need_src=False)
+        if self.store is None:
+            self.new_store()
+        return self.dd.ingest(self.store, id_base, flags)
+
+    def take_routed(self, out=None):
+        """The last route's rows (ts, local owner int32) in receive order."""
+        t, o, _, _, _ = self.dd.take(aux=False, src=False, out=out)
+        return t, o
+
     def select(self, client, node: torch.Tensor, active: Optional[torch.Tensor] = None):
         """getMessages for this rank's owners (client: Trees over the local
         owners; node: uint8 [n_local * 16] requester nodeIds).  Without split

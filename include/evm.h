@@ -453,6 +453,16 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
  * cap < n_recv: EVM_ECAPACITY (the rows stay staged; take again). */
 int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_t out_stride, uint32_t* out_owner,
                   uint32_t* out_aux, uint64_t* out_src, uint64_t cap, uint64_t* group_off);
+/* local: addMessages of the last route's rows into `store` (its owners =
+ * this rank's local owners: the directory's local ids, a split's hot slots)
+ * -- exactly evm_server_ingest over what evm_dist_take(group 0) would return
+ * (row i of the receive order: id id_base + i, flags[i]; n_recv flags), but
+ * packed records are read where they arrived: no 48-B rows are rebuilt and
+ * parsed again.  Needs evm_dist_directory (or evm_dist_split).  The route's
+ * rows stay staged (evm_dist_take still works after it). */
+int evm_dist_ingest(evm_ctx* ctx, evm_dist* d, evm_store* store, uint64_t id_base, uint8_t* flags);
+/* rows the last route delivered to this rank (0 before any route / NULL d) */
+uint64_t evm_dist_received(const evm_dist* d);
 /* collective: every owner's root over all ranks.  This rank's local owners
  * are the owners of trees[0..n_trees) in order (one tree set for all of
  * them, or one single-owner tree per owner): local owner j = global owner

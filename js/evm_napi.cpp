@@ -865,6 +865,35 @@ napi_value DistRoute(napi_env env, napi_callback_info info) {
   return res;
 }
 
+// distIngest(ctx, d, store, idBase) -> { status, flags Uint8Array(nRecv) }   (local)
+// addMessages of the last distRoute's rows into this rank's store, read from
+// the received records (evm_dist_ingest); row i (receive order, as distRoute
+// returned it) has id idBase + i
+napi_value DistIngest(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  if (!get_args(env, info, 4, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_ctx* ctx = cx->c;
+  evm_dist* d = (evm_dist*)ext(env, a[1]);
+  evm_store* s = (evm_store*)ext(env, a[2]);
+  double base = 0;
+  napi_get_value_double(env, a[3], &base);
+  const uint64_t n = evm_dist_received(d);
+  Dev dfl(ctx, n ? n : 1);
+  const int st = evm_dist_ingest(ctx, d, s, (uint64_t)base, (uint8_t*)dfl.p);
+  if (st != EVM_OK && st != EVM_ENONCANON) return throw_status(env, st, "evm_dist_ingest");
+  void* fh;
+  napi_value fl = typed(env, napi_uint8_array, n, 1, &fh);
+  if (n) evm_copy_d2h(ctx, fh, dfl.p, n);
+  napi_value res, v;
+  napi_create_object(env, &res);
+  napi_create_int32(env, st, &v);
+  napi_set_named_property(env, res, "status", v);
+  napi_set_named_property(env, res, "flags", fl);
+  return res;
+}
+
 // distGatherRoots(ctx, d, tree, nOwnersGlobal) -> { root Int32Array, present Uint8Array }   (collective)
 napi_value DistGatherRoots(napi_env env, napi_callback_info info) {
   napi_value a[4];
@@ -1233,7 +1262,7 @@ napi_value Init(napi_env env, napi_value exports) {
              {"serverSelect", ServerSelect}, {"storeSince", StoreSince}, {"receiveFold", ReceiveFold},
              {"pbDecode", PbDecode},         {"pbEncode", PbEncode},
              {"distUniqueId", DistUniqueId}, {"distInit", DistInit},     {"distFree", DistFree},
-             {"distRoute", DistRoute},       {"distGatherRoots", DistGatherRoots},
+             {"distRoute", DistRoute},       {"distGatherRoots", DistGatherRoots}, {"distIngest", DistIngest},
              {"distHubNew", DistHubNew},     {"distHubFree", DistHubFree},   {"distHubAbort", DistHubAbort},
              {"distInitLoopback", DistInitLoopback}, {"distDirectory", DistDirectory},
              {"distHotOwners", DistHotOwners}, {"distSplit", DistSplit},   {"distSelectSplit", DistSelectSplit},

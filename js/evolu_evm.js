@@ -348,6 +348,13 @@ class Dist {
     for (let i = 0; i < r.owner.length; i++) ts.push(dec.decode(r.ts.subarray(i * STRIDE, i * STRIDE + 46)));
     return { timestamps: ts, owner: r.owner, aux: r.aux, src: r.src };
   }
+  // addMessages (index.ts:138-171) of the last route's rows into `server` (this rank's
+  // owners) from the received records themselves (evm_dist_ingest); row i of route()'s
+  // result gets id idBase + i.  -> { status, inserted: boolean[] }
+  addRouted(server, idBase = 0) {
+    const r = addon.distIngest(this.engine.ctx, this.h, server.store, idBase);
+    return { status: r.status, inserted: Array.from(r.flags, (f) => (f & 4) !== 0) };
+  }
   // collective: every owner's root (split owners: the XOR of their partial roots)
   gatherRoots(server, nOwnersGlobal) {
     return addon.distGatherRoots(this.engine.ctx, this.h, addon.storeTree(server.store), nOwnersGlobal);

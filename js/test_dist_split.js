@@ -61,7 +61,15 @@ if (isMainThread) {
     const routed = d.route(s.timestamps.slice(lo, hi), s.owners.slice(lo, hi));
     const srv = new Server(eng, d.nLocal);
     srv.nextId = rank * 2 ** 40;
-    srv.addMessages(routed.timestamps.map((t, i) => ({ owner: routed.owner[i], messages: [{ timestamp: t }] })));
+    const ins = srv.addMessages(routed.timestamps.map((t, i) => ({ owner: routed.owner[i], messages: [{ timestamp: t }] })));
+    // the same rows from the received records themselves (evm_dist_ingest)
+    const srv2 = new Server(eng, d.nLocal);
+    const r2 = d.addRouted(srv2, rank * 2 ** 40);
+    let sameTrees = true;
+    for (let j = 0; j < d.nLocal; j++) sameTrees = sameTrees && srv.merkleTree(j) === srv2.merkleTree(j);
+    out.routedIngest = { status: r2.status, sameFlags: JSON.stringify(r2.inserted) === JSON.stringify(ins), sameTrees,
+      n: r2.inserted.length };
+    srv2.close();
     // global owner of every local id (-1: unused)
     const glob = new Array(d.nLocal).fill(-1);
     for (let g = 0; g < s.userIds.length; g++) if (dir.dest[g] === rank) glob[dir.local[g]] = g;

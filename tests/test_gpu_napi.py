@@ -270,3 +270,6 @@ def test_js_dist_split_loopback(tmp_path, world):
             h = O.merkle_tree_from_string(srv.tree_json(g)).get("hash", 0)
             assert sv["root"][g] == h
     assert seen | set(want_hot) == set(range(O_))
+    for x in res:  # Dist.addRouted (evm_dist_ingest) == Server.addMessages over the routed rows
+        ri = x["routedIngest"]
+        assert ri["status"] == 0 and ri["sameFlags"] and ri["sameTrees"] and ri["n"] == len(x["server"]["rows"])

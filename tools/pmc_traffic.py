@@ -62,6 +62,8 @@ def short(name):
         # KLAUNCH names the template launch by its source text: "(k_svo_a<1024, true>)"
         args = [a.strip().rstrip("u") for a in targs[1:-1].split(",")]
         args = ["SVO_CAP" if a == "4096" else a for a in args]
+        if len(args) >= 2:  # the source is an int template argument: 0 records, 1 rows, 2 received records
+            args[1] = {"0": "false", "1": "true", "2": "SRC_WIRE"}.get(args[1], args[1])
         if len(args) == 3 and args[2] == "256":  # the default workgroup size is not in the launch text
             args = args[:2]
         return "(k_svo_a<%s>)" % ", ".join(args)
