@@ -39,6 +39,8 @@ OPT_SERVER_PATH = 2
 OPT_OVERLAP = 3
 OPT_RADIX = 4
 OPT_TEST_FAIL = 5
+OPT_DIFF_GRID = 6
+OPT_SELECT_PATH = 7
 
 PB_SYNC_REQUEST = 1
 PB_SYNC_RESPONSE = 2

@@ -338,30 +338,6 @@ enum { SEND = 0, RECV = 1 };
 // travels packed; one row outside it anywhere in the job sends every rank's
 // rows raw.
 
-// per-block bucket counts, bucket-major ([b * nblocks + block]): their
-// exclusive scan is every (bucket, block)'s first output slot, stable
-template <int MODE>
-__global__ __launch_bounds__(DT) void k_dist_count(Route R, const char* __restrict__ rec, size_t rb, size_t ooff,
-                                                   size_t n, u32 B, u32 nblocks, u32* __restrict__ counts,
-                                                   u32* __restrict__ bad) {
-  __shared__ u32 c[MAX_BUCKETS];
-  if (threadIdx.x < MAX_BUCKETS) c[threadIdx.x] = 0;
-  __syncthreads();
-  const size_t base = (size_t)blockIdx.x * DTILE;
-  bool oob = false;
-  for (int r = 0; r < DROUNDS; ++r) {
-    const size_t i = base + (size_t)r * DT + threadIdx.x;
-    if (i < n) {
-      const u32 b = bucket_of<MODE>(i, R, rec, rb, ooff);
-      if (b < B) atomicAdd(&c[b], 1u);
-      else oob = true;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < B) counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = c[threadIdx.x];
-  if (__ballot(oob) && __lane_id() == 0) atomicOr(bad, 1u);
-}
-
 // lanes holding the same bucket id (bits = ceil(log2 B) ballots)
 __device__ __forceinline__ u64 match_bucket(u32 b, bool active, int bits) {
   u64 peers = __ballot(active);
@@ -372,6 +348,34 @@ __device__ __forceinline__ u64 match_bucket(u32 b, bool active, int bits) {
   }
   return active ? peers : 0ull;
 }
+
+// per-block bucket counts, bucket-major ([b * nblocks + block]): their
+// exclusive scan is every (bucket, block)'s first output slot, stable.  The
+// lanes of one bucket add once per wave (few buckets: a per-row LDS atomic
+// would serialise on one address -- at world 1 every row is bucket 0)
+template <int MODE>
+__global__ __launch_bounds__(DT) void k_dist_count(Route R, const char* __restrict__ rec, size_t rb, size_t ooff,
+                                                   size_t n, u32 B, int bits, u32 nblocks, u32* __restrict__ counts,
+                                                   u32* __restrict__ bad) {
+  __shared__ u32 c[MAX_BUCKETS];
+  if (threadIdx.x < MAX_BUCKETS) c[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * DTILE;
+  const u64 lt = lanemask_lt();
+  bool oob = false;
+  for (int r = 0; r < DROUNDS; ++r) {
+    const size_t i = base + (size_t)r * DT + threadIdx.x;
+    const u32 b = i < n ? bucket_of<MODE>(i, R, rec, rb, ooff) : 0u;
+    const bool act = i < n && b < B;
+    oob |= i < n && b >= B;
+    const u64 peers = match_bucket(b, act, bits);
+    if (act && (peers & lt) == 0) atomicAdd(&c[b], (u32)__popcll(peers));
+  }
+  __syncthreads();
+  if (threadIdx.x < B) counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = c[threadIdx.x];
+  if (__ballot(oob) && __lane_id() == 0) atomicOr(bad, 1u);
+}
+
 
 // Stable slot of this thread's row among the rows of its bucket: rows of a
 // block in order, ranked within the block with wave ballots + a 4-wave prefix
@@ -889,7 +893,7 @@ int partition_offsets(evm_ctx* ctx, Scratch& S, const Route& R, const char* rec,
   u32* counts = S.alloc<u32>((size_t)B * nblocks);
   u32* offs = S.alloc<u32>((size_t)B * nblocks + 1);
   if (!counts || !offs) return EVM_ENOMEM;
-  KLAUNCH((k_dist_count<MODE>), dim3(nblocks), dim3(DT), R, rec, rb, ooff, n, B, nblocks, counts, bad);
+  KLAUNCH((k_dist_count<MODE>), dim3(nblocks), dim3(DT), R, rec, rb, ooff, n, B, ceil_log2(B), nblocks, counts, bad);
   int st = scan_exclusive<u32, OpAdd>(ctx, S, counts, (size_t)B * nblocks, offs, offs + (size_t)B * nblocks);
   if (st) return st;
   KLAUNCH(k_dist_totals, dim3(1), dim3(MAX_BUCKETS), offs, offs + (size_t)B * nblocks, B, nblocks, totals);

@@ -941,6 +941,10 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
     ctx->radix_onesweep = (int)value;
     return EVM_OK;
   }
+  if (option == EVM_OPT_SELECT_PATH && (value == 0 || value == 1)) {
+    ctx->select_path = (int)value;
+    return EVM_OK;
+  }
   if (option == EVM_OPT_DIFF_GRID && value >= 0 && value <= 64) {
     ctx->diff_grid = (int)value;
     return EVM_OK;

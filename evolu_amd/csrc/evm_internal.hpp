@@ -30,6 +30,7 @@ struct evm_ctx {
   int test_fail = 0;       // EVM_OPT_TEST_FAIL (tests only)
   int radix_onesweep = 1;  // EVM_OPT_RADIX: 1 one-sweep radix passes (look-back), 0 histogram + scan + scatter
   int diff_grid = 0;       // EVM_OPT_DIFF_GRID: k_diff workgroups per CU (0: one lane group per owner)
+  int select_path = 0;     // EVM_OPT_SELECT_PATH: 0 one-pass keep + rank + emit, 1 keep / scan / emit passes
   int n_cu = 256;          // compute units of the device
   hipStream_t side = nullptr;  // second stream (forked from / joined to `stream` inside a call)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;

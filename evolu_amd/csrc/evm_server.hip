@@ -1478,6 +1478,121 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_emit(u32 n_owners, u32 C
   }
 }
 
+// Passes 2 + 3 in one launch (a requester to exclude): each tile of
+// SEL_TILE candidates decides keep (the row's node is not the requester's),
+// ranks its kept rows in candidate order with wave ballots, finds the kept
+// rows of every tile before it by decoupled look-back (tiles taken in launch
+// order from a counter, so every tile waited for is already running), and
+// writes the kept ids at their selection positions (< cap; *total = all
+// kept, written by the last tile).  kst[j] = kept rows before candidate j,
+// for j an owner's first candidate (the owner offsets, k_sv_sel_off).
+constexpr int SEL_ITEMS = 8;
+constexpr u32 SEL_TILE = SEL_THREADS * SEL_ITEMS;
+constexpr u64 SEL_AGG = 1ull << 62, SEL_PRE = 2ull << 62, SEL_VAL = (1ull << 62) - 1;
+constexpr u32 SEL_SPIN_MAX = 1u << 24;
+__global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_scan(StoreView st, u32 n_owners, u32 C,
+                                                             const u32* __restrict__ cpos, const u64* __restrict__ first,
+                                                             const u64* __restrict__ req, const u64* __restrict__ id,
+                                                             u64 cap, u64* __restrict__ sel_id, u64* __restrict__ sel_key,
+                                                             u32* __restrict__ kst, u64* __restrict__ status,
+                                                             u32* __restrict__ tile_ctr, u32* __restrict__ total,
+                                                             u32* __restrict__ err) {
+  constexpr int NW = SEL_THREADS / 64;
+  __shared__ u32 range[2];
+  __shared__ u32 tile_s;
+  __shared__ u32 wc[SEL_ITEMS][NW];
+  __shared__ u64 excl_s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) tile_s = atomicAdd(tile_ctr, 1u);
+  __syncthreads();
+  const u32 tile = tile_s;
+  const u32 j0 = tile * SEL_TILE;
+  const u32 j1 = min(C, j0 + SEL_TILE) - 1;
+  if (threadIdx.x == 0) range[0] = cand_owner(cpos, 0, n_owners, j0);
+  if (threadIdx.x == 1) range[1] = cand_owner(cpos, 0, n_owners, j1) + 1;
+  __syncthreads();
+  const u64 lt = lanemask_lt();
+  u32 own[SEL_ITEMS], rk[SEL_ITEMS];
+  u64 kk[SEL_ITEMS];
+  u32 keepm = 0;
+#pragma unroll
+  for (int r = 0; r < SEL_ITEMS; ++r) {
+    const u32 j = j0 + r * SEL_THREADS + threadIdx.x;
+    bool keep = false;
+    own[r] = 0;
+    kk[r] = 0;
+    if (j <= j1) {
+      const u32 o = cand_owner(cpos, range[0], range[1], j);
+      const size_t k = first[o] + (j - cpos[o]);
+      own[r] = o;
+      kk[r] = k;
+      keep = node_hex_of(st.hi[k], st.lo[k]) != req[o];
+    }
+    const u64 b = __ballot(keep);
+    rk[r] = (u32)__popcll(b & lt);
+    if (lane == 0) wc[r][w] = (u32)__popcll(b);
+    keepm |= keep ? 1u << r : 0u;
+  }
+  __syncthreads();
+  u32 before[SEL_ITEMS], tsum = 0;  // kept rows of this tile before (round r, wave w)
+#pragma unroll
+  for (int r = 0; r < SEL_ITEMS; ++r) {
+    u32 b = tsum;
+    for (int x = 0; x < NW; ++x) {
+      if (x < w) b += wc[r][x];
+      tsum += wc[r][x];
+    }
+    before[r] = b;
+  }
+  if (threadIdx.x == 0) {
+    u64* my = status + tile;
+    u64 excl = 0;
+    if (tile == 0) {
+      __hip_atomic_store(my, SEL_PRE | (u64)tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(my, SEL_AGG | (u64)tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      u32 spins = 0;
+      for (int t = (int)tile - 1; t >= 0;) {
+        const u64 s = __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s & SEL_PRE) {
+          excl += s & SEL_VAL;
+          break;
+        }
+        if (s & SEL_AGG) {
+          excl += s & SEL_VAL;
+          --t;
+          continue;
+        }
+        if (++spins > SEL_SPIN_MAX) {
+          atomicOr(err, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __hip_atomic_store(my, SEL_PRE | (excl + tsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    excl_s = excl;
+    if (j1 == C - 1) *total = (u32)(excl + tsum);
+  }
+  __syncthreads();
+  const u64 excl = excl_s;
+#pragma unroll
+  for (int r = 0; r < SEL_ITEMS; ++r) {
+    const u32 j = j0 + r * SEL_THREADS + threadIdx.x;
+    if (j > j1) continue;
+    const u64 q = excl + before[r] + rk[r];
+    if (j == cpos[own[r]]) kst[j] = (u32)q;  // the owner's first candidate: its selection offset
+    if (!((keepm >> r) & 1u) || q >= cap) continue;
+    const size_t k = kk[r];
+    sel_id[q] = id[k];
+    if (sel_key) {
+      sel_key[3 * q] = st.tc[k];
+      sel_key[3 * q + 1] = st.hi[k];
+      sel_key[3 * q + 2] = st.lo[k];
+    }
+  }
+}
+
 // Per-owner selection offsets: sel_off[o] = kept candidates before owner o.
 __global__ void k_sv_sel_off(u32 n_owners, u32 C, const u32* __restrict__ cpos, const u32* __restrict__ kpos,
                              const u32* __restrict__ ktot, u64* __restrict__ sel_off) {
@@ -2614,6 +2729,29 @@ static int select_after(evm_ctx* ctx, Scratch& S, const evm_store* s, const int6
   u32* keep = nullptr;
   u32* kpos = nullptr;
   u32 K = C;
+  if (node && C && ctx->select_path == 0) {
+    // keep + rank + emit in one pass (decoupled look-back over the candidate tiles)
+    const u32 ntiles = (C + SEL_TILE - 1) / SEL_TILE;
+    u32* kst = S.alloc<u32>(C);
+    u64* status = S.alloc<u64>(ntiles);
+    u32* ctr = S.alloc<u32>(2);  // tile counter, look-back error
+    if (!kst || !status || !ctr) return EVM_ENOMEM;
+    HIPR(hipMemsetAsync(status, 0, sizeof(u64) * ntiles, ctx->stream));
+    HIPR(hipMemsetAsync(ctr, 0, 2 * sizeof(u32), ctx->stream));
+    KLAUNCH(k_sv_sel_scan, dim3(ntiles), dim3(SEL_THREADS), v, O, C, (const u32*)cpos, (const u64*)first,
+            (const u64*)req, (const u64*)s->id, sel_id ? (u64)cap : 0ull, (u64*)sel_id, (u64*)sel_key, kst, status,
+            ctr, tot, ctr + 1);
+    KLAUNCH(k_sv_sel_off, dim3(grid_for(O + 1, 256)), dim3(256), O, C, (const u32*)cpos, (const u32*)kst,
+            (const u32*)tot, (u64*)sel_off);
+    u32 h2[2];
+    HIPR(hipMemcpyAsync(&K, tot, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipMemcpyAsync(h2, ctr, 2 * sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+    if (h2[1]) return EVM_EDEVICE;  // a look-back wait gave up
+    *n_sel = K;
+    if (K > cap || (K && !sel_id)) return EVM_ECAPACITY;
+    return EVM_OK;
+  }
   if (node && C) {
     keep = S.alloc<u32>(C);
     kpos = S.alloc<u32>(C);

@@ -121,6 +121,8 @@ int evm_sync(evm_ctx* ctx);
                                  10-bit digits when that saves a pass; 0 histogram + scan + scatter per pass */
 #define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM) */
 #define EVM_OPT_DIFF_GRID 6   /* evm_merkle_diff / select: k_diff workgroups per CU (0: one lane group per owner) */
+#define EVM_OPT_SELECT_PATH 7 /* getMessages selection with a requester: 0 (default) keep + rank + emit in one pass \
+                                 (look-back over candidate tiles), 1 keep / scan / emit passes (A/B) */
 int evm_set_option(evm_ctx* ctx, int option, int64_t value);
 /* kernel timing with HIP events on the context stream (for roofline reports) */
 int evm_prof_enable(evm_ctx* ctx, int on);

@@ -90,8 +90,11 @@ def test_ingest_vs_oracle(eng, seed):
         assert [id_ts[int(k)] for k in ids[off[i]:off[i + 1]]] == [r[0] for r in rows]
 
 
-@pytest.mark.parametrize("seed", range(4))
-def test_select_vs_oracle(eng, seed):
+@pytest.mark.parametrize("seed,path", [(s, p) for s in range(4) for p in (0, 1)])
+def test_select_vs_oracle(eng, seed, path):
+    from evolu_amd import _lib as L
+
+    eng.set_option(L.OPT_SELECT_PATH, path)  # 0: one-pass keep/rank/emit, 1: three passes
     owners, pools, reqs = _requests(100 + seed)
     store, flags, id_ts = _run_batches(eng, owners, [reqs])
     db, _ = _oracle(owners, [reqs])
@@ -118,10 +121,61 @@ def test_select_vs_oracle(eng, seed):
     client = eng.tree_from_json(client_json)
     node_arr = eng.dev(np.frombuffer("".join(nodes).encode(), dtype=np.uint8).copy())
     diff, off, ids = store.select(client, node_arr)
+    eng.set_option(L.OPT_SELECT_PATH, 0)
     diff, off, ids = diff.cpu().numpy(), off.cpu().numpy(), ids.cpu().numpy()
     for i in range(len(owners)):
         assert int(diff[i]) == want[i][0]
         assert [id_ts[int(k)] for k in ids[off[i]:off[i + 1]]] == want[i][1]
+
+
+def test_select_paths_agree_many_tiles(eng):
+    """The one-pass selection (look-back over 2,048-candidate tiles) against
+    the keep / scan / emit passes on a store of 2M rows: offsets, ids and
+    order keys identical; a capacity below the selection returns
+    EVM_ECAPACITY with the needed count from both."""
+    import ctypes as C
+
+    import torch
+
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    dev = torch.device("cuda", 0)
+    O_, P = 20_000, 100
+    gen = synth.DeviceSynth()
+    ts, own, _ = gen.source(0xE7010007, O_, P, 1, 0, dev)
+    store = eng.store_new(O_)
+    store.ingest(ts, own, 0)
+    rng = np.random.default_rng(5)
+    tsn = ts.cpu().numpy()
+    # bounds: none / before everything / mid-stream (the owner's rows' millis); requesters: a node of the
+    # owner's rows (excluded) or a stranger
+    by = np.argsort(own.cpu().numpy(), kind="stable")
+    first_row = tsn[by.reshape(O_, P)[:, 0]]
+    bound = rng.choice([-1, 0, 1], O_).astype(np.int64)
+    mid = np.array([O.parse_canonical(bytes(r[:46]).decode())[0] for r in tsn[by.reshape(O_, P)[:, P // 2]]])
+    bound = np.where(bound == 1, mid, bound)
+    node = np.where(rng.random(O_)[:, None] < 0.5, first_row[:, 30:46],
+                    np.frombuffer(b"0123456789abcdef", dtype=np.uint8)[None, :]).astype(np.uint8)
+    b_d, n_d = eng.dev(bound), eng.dev(np.ascontiguousarray(node).reshape(-1))
+    res = []
+    for path in (0, 1):
+        eng.set_option(L.OPT_SELECT_PATH, path)
+        off, ids, key = store.select_after(b_d, n_d, keys=True)
+        res.append((off.cpu().numpy(), ids.cpu().numpy(), key.cpu().numpy()))
+        # capacity below the selection
+        k = ids.numel()
+        assert k > 4096
+        o2 = torch.empty(O_ + 1, dtype=torch.int64, device=dev)
+        i2 = torch.empty(k // 2, dtype=torch.int64, device=dev)
+        nsel = C.c_uint64()
+        st = eng.lib.evm_store_select_after(eng.h, store.h, b_d.data_ptr(), n_d.data_ptr(), None, o2.data_ptr(),
+                                            i2.data_ptr(), None, k // 2, C.byref(nsel))
+        assert st == L.EVM_ECAPACITY and nsel.value == k
+    eng.set_option(L.OPT_SELECT_PATH, 0)
+    for x, y in zip(res[0], res[1]):
+        assert np.array_equal(x, y)
+    store.free()
 
 
 def test_ingest_noncanonical_and_empty(eng):
