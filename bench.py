@@ -1002,6 +1002,7 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
     route_ms.clear()
     comm.barrier()
     torch.cuda.synchronize(dev)
+    c0 = eng.stats()
     t0 = time.perf_counter()
     for k in range(steps):
         step()
@@ -1009,6 +1010,8 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
             print("rank %d step %d" % (rank, k), file=sys.stderr, flush=True)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    c1 = eng.stats()
+    allocs = {kk: c1[kk] - c0[kk] for kk in ("workspace_regrows", "scratch_pool_allocs", "block_allocs")}
     prof_dom = eng.prof_report()
     eng.prof_enable(False)
     eng.prof_only(None)
@@ -1093,7 +1096,9 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
                      "kernel_share_of_step": tot_ms / (ms * steps)},
         "pipeline": {"alg_bytes_per_msg": SERVER_PIPELINE_BYTES,
                      "pipeline_hbm_frac": SERVER_PIPELINE_BYTES * n / (elapsed / steps) / HBM_PEAK,
-                     "kernels_ms_per_step": {kk: v[0] for kk, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:16]}},
+                     "kernels_ms_per_step": {kk: v[0] for kk, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:16]},
+                     "all_kernels_ms_per_step": sum(v[0] for v in prof.values()),
+                     "allocs_in_timed_steps": allocs},
         "route": {"ms_per_step": route_avg, "bytes_per_msg": ROUTE_BYTES, "remote_bytes_per_gpu": remote * ROUTE_BYTES,
                   "xgmi_frac": (remote * ROUTE_BYTES / (route_avg / 1e3) / ((world - 1) * XGMI_LINK))
                   if world > 1 else None},
@@ -1272,6 +1277,7 @@ def config5_rank(eng, dd, comm, owners_per_gpu=125_000, n_per_gpu=125_000_000, s
     route_ms.clear()
     comm.barrier()
     torch.cuda.synchronize(dev)
+    c0 = eng.stats()
     t0 = time.perf_counter()
     for k in range(steps):
         step()
@@ -1279,6 +1285,8 @@ def config5_rank(eng, dd, comm, owners_per_gpu=125_000, n_per_gpu=125_000_000, s
             print("rank %d config5 step %d" % (rank, k), file=sys.stderr, flush=True)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    c1 = eng.stats()
+    allocs = {kk: c1[kk] - c0[kk] for kk in ("workspace_regrows", "scratch_pool_allocs", "block_allocs")}
     prof_dom = eng.prof_report()
     eng.prof_enable(False)
     eng.prof_only(None)
@@ -1399,7 +1407,8 @@ def config5_rank(eng, dd, comm, owners_per_gpu=125_000, n_per_gpu=125_000_000, s
                      "kernel_share_of_step": tot_ms / (ms * steps)},
         "pipeline": {"alg_bytes_per_msg": SERVER_PIPELINE_BYTES,
                      "pipeline_hbm_frac": SERVER_PIPELINE_BYTES * n_per_gpu / (elapsed / steps) / HBM_PEAK,
-                     "kernels_ms_per_step": {kk: v[0] for kk, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:16]}},
+                     "kernels_ms_per_step": {kk: v[0] for kk, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:16]},
+                     "all_kernels_ms_per_step": sum(v[0] for v in prof.values()), "allocs_in_timed_steps": allocs},
         "route": {"ms_per_step": route_avg, "bytes_per_msg": ROUTE_BYTES,
                   "imbalance_max_over_mean": n_recv_max / max(1.0, n_per_gpu)},
         "parity_checked": parity, "self_check_rank%d" % rank: detail, "setup_s": setup_s,
@@ -1978,5 +1987,26 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
     return out
 
 
+def reap_children():
+    """Every process this run started has ended (subprocess.run waits for the
+    CPU-baseline legs); anything still alive here is named on stderr and
+    ended, so the run leaves no process behind."""
+    try:
+        import psutil
+    except ImportError:
+        return
+    kids = psutil.Process().children(recursive=True)
+    for c in kids:
+        try:
+            print("bench: reaping child pid %d (%s)" % (c.pid, " ".join(c.cmdline())[:120]), file=sys.stderr)
+            c.terminate()
+        except psutil.Error:
+            pass
+    psutil.wait_procs(kids, timeout=5)
+
+
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    finally:
+        reap_children()

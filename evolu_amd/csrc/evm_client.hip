@@ -1129,6 +1129,9 @@ __device__ __forceinline__ TK shfl_tk(const TK& k, int src) {
 // A row outside that (far) or a second row at a max tc (ds_max returns the key
 // it replaced: equal tc bits) marks its cell; marked cells are resolved by a
 // rescan of the range (true max tc, then the node ranks of the rows at it).
+#ifndef EVM_TP_PREFETCH  // (A/B builds: 1 = TP1 loads the next rows and cells while it parses)
+#define EVM_TP_PREFETCH 0
+#endif
 #ifndef TP_WPE
 #define TP_WPE 8  // waves per SIMD TP1 is compiled for (7: no spills, measured no faster)
 #endif
@@ -1187,9 +1190,30 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
   for (u32 k = threadIdx.x; k < (C + 31) / 32; k += TP_THREADS) cfix[k] = 0;
   if (threadIdx.x == 0) nmatch = 0;
   __syncthreads();
+#if EVM_TP_PREFETCH
+  // the next iteration's rows and cells are in flight while this one parses
+  // (the LDS restage's fences keep the compiler from hoisting them itself)
+  uint4 na, nb, nc;
+  u32 nci = 0;
+  if (beg + 64 * wv < end) {
+    clp_fetch<S48>(ts, stride, end, beg + 64 * wv, na, nb, nc);
+    if (beg + 64 * wv + lane < end) nci = __builtin_nontemporal_load(cell + beg + 64 * wv + lane);
+  }
+#endif
   for (size_t first = beg + 64 * wv; first < end; first += TP_THREADS) {  // wave-uniform
     uint4 a, b, c;
+#if EVM_TP_PREFETCH
+    a = na;
+    b = nb;
+    c = nc;
+    const u32 ci_cur = nci;
+    if (first + TP_THREADS < end) {
+      clp_fetch<S48>(ts, stride, end, first + TP_THREADS, na, nb, nc);
+      if (first + TP_THREADS + lane < end) nci = __builtin_nontemporal_load(cell + first + TP_THREADS + lane);
+    }
+#else
     clp_fetch<S48>(ts, stride, end, first, a, b, c);
+#endif
     const size_t i = first + lane;
     u32 w[12];
     if (S48) {
@@ -1223,7 +1247,11 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
 #endif
     const bool valid = (p.meta & EVM_META_VALID) != 0;
     if (i < end) {
+#if EVM_TP_PREFETCH
+      const u32 ci = ci_cur;
+#else
       const u32 ci = __builtin_nontemporal_load(cell + i);
+#endif
       const bool ok = valid && ci < C;
       const bool fast = (p.tc >> 16) < TP_MS_FAST && ((u32)p.tc & 0xffffu) < 256u;
       __builtin_nontemporal_store(!ok ? TP_INVALID : fast ? tpc_pack(p.tc, ci) : TP_FAR, tcs + i);
