@@ -480,6 +480,8 @@ __global__ __launch_bounds__(RUN_THREADS) void k_run_emit(const u32* __restrict_
   }
 }
 
+constexpr u32 SEG_NOBASE = 0xffffffffu;  // SegView::cbase: the segment is not one run
+
 // lengths of the runs in (owner, batch) order
 __global__ void k_run_len(const u32* __restrict__ run_start, const u32* __restrict__ order, u32 R, size_t n,
                           u32* __restrict__ len) {
@@ -490,8 +492,11 @@ __global__ void k_run_len(const u32* __restrict__ run_start, const u32* __restri
 }
 
 // first message position of every owner: the position of its first run
+// (and cbase[o]: the batch start of an owner whose share is one run -- a
+// whole SyncRequest, the common case -- so K5 reads no perm for it)
 __global__ void k_run_seg(const u32* __restrict__ run_owner_sorted, u32 R, const u32* __restrict__ run_pos, u32 O,
-                          u64* __restrict__ seg, Info* __restrict__ info) {
+                          u64* __restrict__ seg, Info* __restrict__ info, const u32* __restrict__ run_start,
+                          const u32* __restrict__ order, u32* __restrict__ cbase) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && R && run_owner_sorted[R - 1] >= O) atomicOr(&info->bad_aux, 1u);
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o <= O; o += gridDim.x * blockDim.x) {
     u32 a = 0, b = R;
@@ -501,6 +506,10 @@ __global__ void k_run_seg(const u32* __restrict__ run_owner_sorted, u32 R, const
       else b = m;
     }
     seg[o] = run_pos[a];  // run_pos[R] = n
+    if (o < O && cbase) {
+      const bool one = a < R && run_owner_sorted[a] == o && (a + 1 == R || run_owner_sorted[a + 1] != o);
+      cbase[o] = one ? run_start[order[a]] : SEG_NOBASE;
+    }
   }
 }
 
@@ -608,6 +617,9 @@ constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while 
 #ifndef EVM_SVB_LDS  // (A/B builds only: 0 = the merge without LDS-staged keys)
 #define EVM_SVB_LDS 1
 #endif
+#ifndef EVM_SVO_CBASE  // (A/B builds only: 0 = K5 reads every batch index from perm)
+#define EVM_SVO_CBASE 1
+#endif
 #ifndef EVM_SVB_PFX  // (A/B builds only: 0 = the tree's prefix XOR by a scan after the merge)
 #define EVM_SVB_PFX 1
 #endif
@@ -643,6 +655,9 @@ struct SegView {
   const u64* sb;
   const u64* la;     // tree leaves [la[s], lb[s])
   const u64* lb;
+  // [NS] (or null): a segment whose messages are ONE request run -- batch
+  // positions cbase[s] + t, no perm read (SEG_NOBASE: read perm)
+  const u32* cbase = nullptr;
 };
 __device__ __forceinline__ u32 seg_owner(const SegView& v, u32 s) { return v.owner ? v.owner[s] : s; }
 
@@ -699,6 +714,9 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   const u64 a = sv.start[s];
   const u64 m = sv.start[s + 1] - a;  // an unsorted owner column (bad ids) may underflow: "big"
   const u64 la = sv.la[s], lb = sv.lb[s];
+  // the batch index of share position t (the set is what matters, not its order)
+  const u32 cb = sv.cbase ? sv.cbase[s] : SEG_NOBASE;
+  auto pidx = [&](u32 t) -> u32 { return cb != SEG_NOBASE ? cb + t : perm[a + t]; };
   if (m > CAP || m == 0) {
     if (threadIdx.x == 0) {
       if (m <= 512 && mid512) {
@@ -726,7 +744,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const u32 t = threadIdx.x + k * THREADS;
-    bi[k] = t < m ? perm[a + t] : 0u;
+    bi[k] = t < m ? pidx(t) : 0u;
   }
   u64 tmin = ~0ull, tmax = 0;
   if (SRC == SRC_ROWS) {
@@ -971,9 +989,9 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     if (p > 0 && same(p - 1, p)) continue;  // not a run start: the start decides
     u32 e = p + 1;
     if (e < m && same(p, e)) {
-      u32 best = p, bb = perm[a + pp];
+      u32 best = p, bb = pidx(pp);
       for (; e < m && same(e - 1, e); ++e) {
-        const u32 be = perm[a + (u32)(s_k[e] & PMASK)];
+        const u32 be = pidx((u32)(s_k[e] & PMASK));
         if (be < bb) {
           bb = be;
           best = e;
@@ -1034,7 +1052,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       mt[r] = tmin + (kp >> PB);
       mh[r] = s_rh[pos];
       ml[r] = rl_get(pos);
-      mb[r] = perm[a + pos];
+      mb[r] = pidx(pos);
       mhash[r] = s_h[pos];
       bool ins = cnt_get(p) != 0;
       if (ins && sb > sa && !scan_stored) {
@@ -1048,7 +1066,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
         const size_t q = store_lower(st, sa, sb, k);
         if (q < sb && skey_cmp(skey_at(st, q), k) == 0) {
           const u32 pos = (u32)(s_k[p] & PMASK);
-          const u32 b = perm[a + pos];
+          const u32 b = pidx(pos);
           const u64 in_tc = SRC != SRC_REC ? 0ull : rec[b].tc;
           printf("scan miss: seg %u owner %u p %u m %llu sa %llu sb %llu tc %llx tmin %llx tmax %llx CAP %u kp %llx "
                  "pos %u in_tc %llx stored_q %llu\n", s, o, p, (unsigned long long)m, (unsigned long long)sa,
@@ -2154,7 +2172,10 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if ((st = radix_sort_pairs<u32>(ctx, S, rk, rv, R, 0, obits))) return st;
     KLAUNCH(k_run_len, dim3(grid_for(R, 256)), dim3(256), run_start, rv, R, n, len);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, len, R, run_pos, run_pos + R))) return st;
-    KLAUNCH(k_run_seg, dim3(grid_for((size_t)O + 1, 256)), dim3(256), rk, R, run_pos, O, seg, info);
+    u32* cbase = EVM_SVO_CBASE ? S.alloc<u32>(std::max<u32>(O, 1)) : nullptr;
+    KLAUNCH(k_run_seg, dim3(grid_for((size_t)O + 1, 256)), dim3(256), rk, R, run_pos, O, seg, info,
+            (const u32*)run_start, (const u32*)rv, cbase);
+    sv.cbase = cbase;
     KLAUNCH(k_run_fill, dim3(grid_for(R, 4 * RF_RUNS, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
     // owners above SEG_SPLIT_MIN: key-range segments, splitters from every
     // 16th message of their share
