@@ -1762,14 +1762,19 @@ __device__ __forceinline__ u32 xf_minute_off(u64 tc, u64 base_ms, u32 mlo, bool 
 
 // A tile of THREADS x ITEMS pairs is staged in LDS with its bucket ids and
 // written back bucket by bucket (EVM_XF_SCATTER picks the shape).
+#ifndef EVM_XF_NOSTAGE  // (A/B builds: 1 = pairs written straight from registers, L2 merges a bucket's run)
+#define EVM_XF_NOSTAGE 0
+#endif
 template <int THREADS, int ITEMS>
 __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ hash, const u64* __restrict__ tcs,
                                                           const u64* __restrict__ tcs_far,
                                                           const u32* __restrict__ cell, size_t n, int kb, int cbits,
                                                           u32 cap, u32* __restrict__ cursor, u64* __restrict__ out,
                                                           Info* __restrict__ info, u32 tl) {
-  __shared__ u64 stage[(THREADS * ITEMS)];
-  __shared__ uint16_t sbk[(THREADS * ITEMS)];      // the bucket of each staged pair
+  // staged: 1 workgroup of 1,024 per CU (its LDS); unstaged: 8 KiB, two per CU
+  constexpr int SN = EVM_XF_NOSTAGE ? 1 : THREADS * ITEMS;
+  __shared__ u64 stage[SN];
+  __shared__ uint16_t sbk[SN];      // the bucket of each staged pair
   __shared__ u32 cnt[1u << XP_MAX_KB];  // per bucket: count, then local offset
   __shared__ u32 gb[1u << XP_MAX_KB];   // per bucket: this tile's base inside the bucket
   __shared__ u32 scan_tmp[THREADS / 64 + 1];
@@ -1832,6 +1837,15 @@ __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ 
   }
   if (__ballot(full) && (threadIdx.x & 63) == 0) atomic_or_if(&info->xf_redo, 1u);
   __syncthreads();
+  if (EVM_XF_NOSTAGE) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k)
+      if (bk[k] < B) {
+        const u32 slot = gb[bk[k]] + r[k];
+        if (slot < cap) out[(size_t)bk[k] * cap + slot] = v[k];
+      }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k)
     if (bk[k] < B) {

@@ -9,6 +9,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 rc=$?; ok $rc || exit $rc
 timeout -k 10 200 python -u bench.py --workload client --steps 20 --warmup 5 --cpu-seconds 0 --extra 0 > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err &&
 EVM_LIB_PATH=_var/tp_pf/libevm.so timeout -k 10 200 python -u bench.py --workload client --steps 20 --warmup 5 --cpu-seconds 0 --extra 0 > gpurun_out/b_c2_pf.json 2>> gpurun_out/b_c2.err &&
+EVM_LIB_PATH=_var/xf_nostage/libevm.so timeout -k 10 200 python -u bench.py --workload client --steps 20 --warmup 5 --cpu-seconds 0 --extra 0 > gpurun_out/b_c2_xfns.json 2>> gpurun_out/b_c2.err &&
 timeout -k 10 300 python -u bench.py --workload config4 --steps 5 --warmup 1 --cpu-seconds 0 > gpurun_out/b_c4.json 2> gpurun_out/b_c4.err &&
 timeout -k 10 300 python -u bench.py --workload config4 --steps 5 --warmup 1 --cpu-seconds 0 --c4-take > gpurun_out/b_c4_take.json 2>> gpurun_out/b_c4.err &&
 timeout -k 10 400 python -u bench.py --workload server --steps 5 --warmup 2 --cpu-seconds 0 > gpurun_out/b_server.json 2> gpurun_out/b_server.err &&
