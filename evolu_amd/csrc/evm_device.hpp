@@ -307,6 +307,25 @@ __host__ __device__ __forceinline__ Parsed parse_ts46(const u32 (&w)[12]) {
   return p;
 }
 
+// The minute (floor(millis / 60000)) of a timestamp row from its first 16
+// bytes, "YYYY-MM-DDTHH:MM" -- parse_ts46's minute on the native domain,
+// without its checks (garbage for a row outside it, which the full parse
+// flags later).
+__host__ __device__ __forceinline__ u32 minute16(u32 w0, u32 w1, u32 w2, u32 w3) {
+  const u32 d0 = w0 - 0x30303030u;
+  const u32 year = mul24(mul24(d0 & 0xffu, 10u) + ((d0 >> 8) & 0xffu), 100u) + mul24((d0 >> 16) & 0xffu, 10u) +
+                   (d0 >> 24);
+  auto two = [](u32 x, int sh) { return mul24((x >> sh) & 0xffu, 10u) + ((x >> (sh + 8)) & 0xffu) - 528u; };
+  const u32 mon = two(w1, 8), day = two(w2, 0), mi = two(w3, 16);
+  const u32 hh = mul24((w2 >> 24) - 0x30u, 10u) + (w3 & 0xffu) - 0x30u;
+  const u32 y = year - (mon <= 2u ? 1u : 0u);
+  const u32 yc = mul24(y, 5243u) >> 19;
+  const u32 mp = mon > 2u ? mon - 3u : mon + 9u;
+  const u32 doy = (mul24(mul24(mp & 15u, 153u) + 2u, 52429u) >> 18) + day - 1u;
+  const u32 days = mul24(y, 365u) + (y >> 2) - yc + (yc >> 2) + doy - 719468u;
+  return mul24(days & 0xffffffu, 1440u) + mul24(hh & 0xffu, 60u) + mi;
+}
+
 // The inverse of parse_ts46 on the native domain: timestamp.ts:43-48
 // timestampToString of (tc, node, case mask) as 12 little-endian words
 // (bytes 46-47 zero).  Proleptic Gregorian civil date of the day count.

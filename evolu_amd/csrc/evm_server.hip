@@ -620,6 +620,9 @@ constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while 
 #ifndef EVM_SVO_CBASE  // (A/B builds only: 0 = K5 reads every batch index from perm)
 #define EVM_SVO_CBASE 1
 #endif
+#ifndef EVM_SEG_FUSED  // (A/B builds only: 0 = a minutes pass before the plan of interleaved owners)
+#define EVM_SEG_FUSED 1
+#endif
 #ifndef EVM_SVB_PFX  // (A/B builds only: 0 = the tree's prefix XOR by a scan after the merge)
 #define EVM_SVB_PFX 1
 #endif
@@ -627,6 +630,7 @@ constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while 
 struct SvoStatus {
   u32 big;       // an owner's share exceeds the launch's capacity
   u32 fallback;  // a share spans > 2^37 ms, a tie run is longer than SVO_TIE_MAX, or new leaves mix key lengths
+  u32 lens;      // bit L: some segment's first or last new leaf has a base-3 key of length L
 };
 
 // first k in [lo, hi) with a[k] >= x
@@ -1138,7 +1142,11 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0 && NL && base3_len(s_lm[0]) != base3_len(s_lm[NL - 1])) atomicOr(&status->fallback, 1u);
+  if (threadIdx.x == 0 && NL) {
+    const int l0 = base3_len(s_lm[0]), l1 = base3_len(s_lm[NL - 1]);
+    if (l0 != l1) atomicOr(&status->fallback, 1u);
+    atomicOr(&status->lens, (1u << l0) | (1u << l1));  // (one key length over the batch: code order = minute order)
+  }
   u32 dups = 0;
   for (u32 l = threadIdx.x; l < NL; l += THREADS) {
     const u64 code = ((u64)o << 40) | minute_code_from(s_lm[l], [&](u32 x) { return (u32)s_b3[x]; });
@@ -1860,11 +1868,36 @@ __global__ void k_seg_own(const u32* __restrict__ bbase, const u32* __restrict__
 // so the L2 round trips overlap; the batch index is not written (the segment
 // sort's first pass makes the identity values).
 constexpr int SK_ITEMS = 4;
-__global__ __launch_bounds__(256) void k_seg_key(const evm_rec* __restrict__ rec, const u32* __restrict__ minute,
-                                                 const u32* __restrict__ owner, size_t n,
-                                                 const SegOwn* __restrict__ own, const u32* __restrict__ sp,
-                                                 const u32* __restrict__ tab, u32* __restrict__ key) {
+// Where a message's minute comes from: the compact minutes / packed records,
+// the timestamp row's first 16 bytes (minute16), or a received record's tc.
+struct MinuteSrc {
+  const evm_rec* rec;
+  const u32* minute;
+  const uint8_t* ts;  // rows (16-B aligned, stride % 16 == 0), or null
+  size_t stride;
+  WireSrc wire;               // wire.rec != null: received records
+};
+__device__ __forceinline__ u32 minute_at(const MinuteSrc& m, size_t i) {
+  if (m.ts) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(m.ts + i * m.stride));
+    return minute16(v.x, v.y, v.z, v.w);
+  }
+  if (m.wire.rec) {
+    u64 tc, node;
+    u32 cm;
+    wire_load(m.wire, i, &tc, &node, &cm);
+    return (u32)((tc >> 16) / 60000ull);
+  }
+  return minute_of(m.rec, m.minute, i);
+}
+// (an owner >= O -- the batch is refused -- gets key NS, after every segment)
+__global__ __launch_bounds__(256) void k_seg_key(MinuteSrc msrc, const u32* __restrict__ owner, size_t n, u32 O,
+                                                 u32 NS, const SegOwn* __restrict__ own, const u32* __restrict__ sp,
+                                                 const u32* __restrict__ tab, u32* __restrict__ key,
+                                                 Info* __restrict__ info) {
   const size_t stride = (size_t)gridDim.x * blockDim.x * SK_ITEMS;
+  bool bad = false;
   for (size_t i0 = (size_t)blockIdx.x * blockDim.x * SK_ITEMS + threadIdx.x; i0 < n; i0 += stride) {
     u32 o[SK_ITEMS], mnt[SK_ITEMS], k[SK_ITEMS];
     SegOwn r[SK_ITEMS];
@@ -1872,10 +1905,15 @@ __global__ __launch_bounds__(256) void k_seg_key(const evm_rec* __restrict__ rec
     for (int j = 0; j < SK_ITEMS; ++j) {
       const size_t i = i0 + (size_t)j * blockDim.x;
       o[j] = i < n ? owner[i] : 0u;
-      mnt[j] = i < n ? minute_of(rec, minute, i) : 0u;
+      mnt[j] = i < n ? minute_at(msrc, i) : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < SK_ITEMS; ++j) r[j] = own[o[j]];
+    for (int j = 0; j < SK_ITEMS; ++j) {
+      const bool ok = o[j] < O;
+      bad |= !ok;
+      r[j] = own[ok ? o[j] : 0u];
+      if (!ok) r[j].b0 = NS, r[j].nbo = 1;
+    }
 #pragma unroll
     for (int j = 0; j < SK_ITEMS; ++j) {
       k[j] = r[j].b0;
@@ -1894,6 +1932,34 @@ __global__ __launch_bounds__(256) void k_seg_key(const evm_rec* __restrict__ rec
       if (i < n) key[i] = k[j];
     }
   }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomic_or_if(&info->bad_aux, 1u);
+}
+
+// The fused plan's samples (no minutes pass): every 16th message's minute
+// straight from its row / record, the sampled minute range, and the owner
+// check of the sampled rows.  mm = {min, max} (k_seg_key checks every owner).
+__global__ void k_seg_smin(MinuteSrc msrc, const u32* __restrict__ owner, size_t n, u32 O, u32* __restrict__ smin,
+                           u32* __restrict__ mm, Info* __restrict__ info) {
+  const size_t nq = (n + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE;
+  u32 mn = 0xffffffffu, mx = 0u, bad = 0u;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = q * SAMPLE_STRIDE;
+    const u32 m = minute_at(msrc, i);
+    smin[q] = m;
+    mn = min(mn, m);
+    mx = max(mx, m);
+    bad |= owner[i] >= O ? 1u : 0u;
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  bad = wave_max(bad);
+  if ((threadIdx.x & 63) == 0) {
+    if (mn != 0xffffffffu) {
+      atomicMin(&mm[0], mn);
+      atomicMax(&mm[1], mx);
+    }
+    if (bad) atomic_or_if(&info->bad_aux, 1u);
+  }
 }
 
 __global__ void k_seg_start(const u32* __restrict__ skey, size_t n, u32 NS, u64* __restrict__ start) {
@@ -1909,14 +1975,15 @@ __global__ void k_seg_start(const u32* __restrict__ skey, size_t n, u32 NS, u64*
 }
 
 // every 16th batch position: (owner, minute - gmin) (mb = 0: owner only)
+// (smin: the samples' minutes by sample index, from k_seg_smin)
 __global__ void k_seg_sample_all(const evm_rec* __restrict__ rec, const u32* __restrict__ minute,
                                  const u32* __restrict__ owner, size_t n, u32 gmin, int mb, u64* __restrict__ key,
-                                 u32* __restrict__ val) {
+                                 u32* __restrict__ val, const u32* __restrict__ smin) {
   const size_t nq = (n + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE;
   for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (size_t)gridDim.x * blockDim.x) {
     const size_t i = q * SAMPLE_STRIDE;
     u64 k = (u64)owner[i] << mb;
-    if (mb) k |= (u64)(minute_of(rec, minute, i) - gmin);
+    if (mb) k |= (u64)((smin ? smin[q] : minute_of(rec, minute, i)) - gmin);
     key[q] = k;
     val[q] = (u32)q;
   }
@@ -2154,6 +2221,18 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   const u32* kperm = ov;  // batch indices, segment by segment
   bool split = false;
   u64* skey = nullptr;   // sorted samples: owner << mb | minute - gmin
+  // interleaved owners with K5 parsing the rows / records itself: the plan
+  // reads the minutes from them directly (no minutes pass; EVM_SEG_FUSED)
+  const bool seg_fused = EVM_SEG_FUSED && fused && (wire || (stride % 16 == 0 && ((uintptr_t)ts & 15) == 0));
+  u32* smin = nullptr;   // the samples' minutes (seg_fused)
+  MinuteSrc msrc{rec, minute, nullptr, 0, WireSrc{nullptr, nullptr, 0, 0, 0, 0}};
+  if (seg_fused) {
+    if (wire) msrc.wire = *wire;
+    else {
+      msrc.ts = reinterpret_cast<const uint8_t*>(ts);
+      msrc.stride = stride;
+    }
+  }
   u32 gmin = 0;
   int mb = 1;
   u32 nspl = 0;
@@ -2210,8 +2289,27 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     // wrong estimate costs speed only -- an overfull segment sends its owner
     // to the sort path); then ONE sort of the batch by segment, which also
     // groups the owners (no separate owner sort)
-    if ((st = minutes())) return st;
-    if ((st = check_info())) return st;
+    const u32 nq = (u32)((n + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE);
+    if (seg_fused) {
+      // no minutes pass: the sampled rows' minutes give the range (the
+      // segments' first / last splitters are open-ended, so a minute outside
+      // it still lands in a segment; K5 reports the key lengths it saw)
+      smin = S.alloc<u32>(nq);
+      u32* mm = S.alloc<u32>(2);
+      if (!smin || !mm) return EVM_ENOMEM;
+      HIPR(hipMemsetAsync(mm, 0xff, sizeof(u32), ctx->stream));
+      HIPR(hipMemsetAsync(mm + 1, 0, sizeof(u32), ctx->stream));
+      KLAUNCH(k_seg_smin, dim3(grid_for(nq, 256)), dim3(256), msrc, owner, n, O, smin, mm, info);
+      u32 hmm[2];
+      HIPR(hipMemcpyAsync(hmm, mm, sizeof(hmm), hipMemcpyDeviceToHost, ctx->stream));
+      if ((st = read_info(ctx, info, &hi))) return st;
+      if (hi.bad_aux) return EVM_EINVAL;
+      hi.minute_min = hmm[0];
+      hi.minute_max = hmm[1];
+    } else {
+      if ((st = minutes())) return st;
+      if ((st = check_info())) return st;
+    }
     if (cuttable()) {
       gmin = hi.minute_min;
       mb = std::max(1, ceil_log2((size_t)(hi.minute_max - gmin) + 1));
@@ -2219,11 +2317,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
       gmin = 0;
       mb = 0;  // no minutes in the key: one segment per owner
     }
-    const u32 nq = (u32)((n + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE);
     skey = S.alloc<u64>(nq);
     u32* sval = S.alloc<u32>(nq);
     if (!skey || !sval) return EVM_ENOMEM;
-    KLAUNCH(k_seg_sample_all, dim3(grid_for(nq, 256)), dim3(256), rec, minute, owner, n, gmin, mb, skey, sval);
+    KLAUNCH(k_seg_sample_all, dim3(grid_for(nq, 256)), dim3(256), rec, minute, owner, n, gmin, mb, skey, sval,
+            (const u32*)smin);
     if ((st = radix_sort_pairs<u64>(ctx, S, skey, sval, nq, 0, mb + obits))) return st;
     KLAUNCH(k_seg_soff, dim3(grid_for((size_t)O + 1, 256)), dim3(256), skey, nq, O, mb, soff);
     KLAUNCH(k_seg_plan_est, dim3(grid_for(O, 256)), dim3(256), soff, O, mb > 0 ? 1 : 0, seg_target(), nb, nsp);
@@ -2264,11 +2362,14 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     SegOwn* sown_rec = S.alloc<SegOwn>(std::max<u32>(O, 1));
     if (!sown_rec) return EVM_ENOMEM;
     KLAUNCH(k_seg_own, dim3(grid_for(O, 256)), dim3(256), bbase, spoff, sp, tboff, O, sown_rec);
-    KLAUNCH(k_seg_key, dim3(grid_for((n + SK_ITEMS - 1) / SK_ITEMS, 256)), dim3(256), rec, minute, owner, n,
-            (const SegOwn*)sown_rec, sp, tab, bkey);
+    // (the minutes from the rows / records when the plan read them so, else the minutes array)
+    MinuteSrc kms = msrc;
+    if (!(seg_fused && !runs)) kms = MinuteSrc{rec, minute, nullptr, 0, WireSrc{nullptr, nullptr, 0, 0, 0, 0}};
+    KLAUNCH(k_seg_key, dim3(grid_for((n + SK_ITEMS - 1) / SK_ITEMS, 256)), dim3(256), kms, owner, n, O, NS,
+            (const SegOwn*)sown_rec, sp, tab, bkey, info);
     u32* bk = bkey;
     u32* bv = nullptr;  // the batch index: the identity, made by the sort's first pass
-    if ((st = radix_sort_pairs<u32>(ctx, S, bk, bv, n, 0, std::max(1, ceil_log2(NS))))) return st;
+    if ((st = radix_sort_pairs<u32>(ctx, S, bk, bv, n, 0, std::max(1, ceil_log2((size_t)NS + 1))))) return st;
     KLAUNCH(k_seg_start, dim3(grid_for((size_t)NS + 1, 256)), dim3(256), bk, n, NS, sstart);
     KLAUNCH(k_seg_ranges, dim3(grid_for(NS, 256)), dim3(256), bbase, spoff, sp, O, NS, view_of(s), (const u64*)t->off,
             (const u64*)t->ck, sown, ssa, sla);
@@ -2375,6 +2476,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   if (fused) {
     // the parse's verdict: a row outside the native domain -> pack to flag the culprits
     if ((st = read_info(ctx, info, &hi))) return st;
+    if (hi.bad_aux) return EVM_EINVAL;  // (the fused plan checks every owner in k_seg_key)
     if (hi.bad) {
       if ((st = unfuse())) return st;
       KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
@@ -2383,6 +2485,10 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     }
   }
   if (hs.fallback) return unfuse();  // the sort path redoes every flag (from packed records)
+  // a plan from sampled minutes may have cut owners although the batch's
+  // minutes have two key lengths (then code order != minute order across an
+  // owner's segments): the sort path
+  if (seg_fused && !runs && nspl && __builtin_popcount(hs.lens) > 1) return unfuse();
   if (hs.big && bigmask && (st = unfuse())) return st;  // the big owners' sub-batch reads packed records
   if (hs.big) {
     if (!bigmask) return EVM_OK;

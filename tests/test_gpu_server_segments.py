@@ -103,6 +103,23 @@ def test_mixed_key_lengths_disable_segments(eng):
     _same(seg, _run(eng, 2, 2, ts_np, owner_np, cut))
 
 
+def test_unsampled_key_length_falls_back(eng):
+    """One 1990 timestamp at a batch position the plan does not sample (the
+    interleaved-owner plan reads every 16th row's minute, no minutes pass):
+    the big owners are cut from the sampled range, K5 reports the second key
+    length, and the batch takes the sort path -- results unchanged."""
+    rng = random.Random(8)
+    nodes = [W.node_id(rng) for _ in range(4)]
+    strings = W.hlc_timestamps(rng, 12000, nodes, span=86_400_000)
+    rng.shuffle(strings)
+    strings.insert(17, O.timestamp_to_string(631_152_000_000, 0, nodes[1]))  # 17 % 16 != 0: never sampled
+    owner_np = (np.arange(len(strings)) % 3 == 0).astype(np.uint32)
+    owner_np[17] = 0
+    ts_np = eng.timestamps(strings).cpu().numpy()
+    cut = len(strings) // 2
+    _same(_run(eng, 0, 2, ts_np, owner_np, cut), _run(eng, 2, 2, ts_np, owner_np, cut))
+
+
 @pytest.mark.parametrize("burst", [2600, 5000])
 def test_size_classes_with_burst_segment(eng, burst):
     """Many small owners (the batch takes the size-class passes: the one-wave
