@@ -412,11 +412,11 @@ def main():
 
         if workload == "config4":
             res = leg(config4_rank, a.c4_owners, a.c4_per_owner, a.steps, a.warmup, a.c4_sample,
-                      dist_ingest=not a.c4_take)
+                      dist_ingest=not getattr(a, "c4_take", False))
             data = "synthetic (seeded HLC streams generated on the device, SURVEY 8(d) config 4)"
         elif workload == "config5":
             res = leg(config5_rank, a.c5_owners, a.c5_messages, a.steps, a.warmup, a.c5_sample, a.c5_share,
-                      dist_ingest=not a.c4_take)
+                      dist_ingest=not getattr(a, "c4_take", False))
             data = "synthetic (device generator evs_config5_shape, SURVEY 8(d) config 5)"
         else:
             res = leg(client_split_rank, a.c5c_messages, a.c5c_cells, a.steps, a.warmup)
@@ -426,7 +426,7 @@ def main():
             # BASELINE config 5 at the same N: the server on the Zipf stream with hot owners
             # split, and one owner's client batch split by cell -- both self-checked
             c5 = leg(config5_rank, a.c5_owners, a.c5_messages, min(a.steps, 5), min(a.warmup, 1), a.c5_sample,
-                     a.c5_share, dist_ingest=not a.c4_take)
+                     a.c5_share, dist_ingest=not getattr(a, "c4_take", False))
             c5c = leg(client_split_rank, a.c5c_messages, a.c5c_cells, min(a.steps, 5), min(a.warmup, 1))
             extra = {"config5": c5, "config5c": c5c}
         if rank == 0:
@@ -625,7 +625,8 @@ def main():
             eng4 = Engine(local)
             dd4 = make_dist(eng4, 0, 1)
             out["config4"] = config4_rank(eng4, dd4, TorchComm(1, torch.device("cuda", local)), a.c4_owners,
-                                          a.c4_per_owner, a.steps, a.warmup, a.c4_sample, dist_ingest=not a.c4_take)
+                                          a.c4_per_owner, a.steps, a.warmup, a.c4_sample,
+                                          dist_ingest=not getattr(a, "c4_take", False))
             dd4.free()
             eng4.close()
             torch.cuda.empty_cache()
@@ -1123,7 +1124,7 @@ def config4_loopback(a, world, device=0):
     def fn(r, eng, dd):
         try:
             return config4_rank(eng, dd, comm.bind(r), a.c4_owners, a.c4_per_owner, a.steps, a.warmup, a.c4_sample,
-                                dist_ingest=not a.c4_take)
+                                dist_ingest=not getattr(a, "c4_take", False))
         except BaseException:
             comm.bar.abort()  # the other ranks may wait in a bench barrier, not a collective
             raise
@@ -1430,7 +1431,7 @@ def config5_loopback(a, world, device=0):
     def fn(r, eng, dd):
         try:
             return config5_rank(eng, dd, comm.bind(r), a.c5_owners, a.c5_messages, a.steps, a.warmup, a.c5_sample,
-                                a.c5_share, dist_ingest=not a.c4_take)
+                                a.c5_share, dist_ingest=not getattr(a, "c4_take", False))
         except BaseException:
             comm.bar.abort()
             raise
