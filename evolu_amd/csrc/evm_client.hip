@@ -1129,9 +1129,6 @@ __device__ __forceinline__ TK shfl_tk(const TK& k, int src) {
 // A row outside that (far) or a second row at a max tc (ds_max returns the key
 // it replaced: equal tc bits) marks its cell; marked cells are resolved by a
 // rescan of the range (true max tc, then the node ranks of the rows at it).
-#ifndef EVM_TP_PREFETCH  // (A/B builds: 1 = TP1 loads the next rows and cells while it parses)
-#define EVM_TP_PREFETCH 0
-#endif
 #ifndef TP_WPE
 #define TP_WPE 8  // waves per SIMD TP1 is compiled for (7: no spills, measured no faster)
 #endif
@@ -1190,30 +1187,9 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
   for (u32 k = threadIdx.x; k < (C + 31) / 32; k += TP_THREADS) cfix[k] = 0;
   if (threadIdx.x == 0) nmatch = 0;
   __syncthreads();
-#if EVM_TP_PREFETCH
-  // the next iteration's rows and cells are in flight while this one parses
-  // (the LDS restage's fences keep the compiler from hoisting them itself)
-  uint4 na, nb, nc;
-  u32 nci = 0;
-  if (beg + 64 * wv < end) {
-    clp_fetch<S48>(ts, stride, end, beg + 64 * wv, na, nb, nc);
-    if (beg + 64 * wv + lane < end) nci = __builtin_nontemporal_load(cell + beg + 64 * wv + lane);
-  }
-#endif
   for (size_t first = beg + 64 * wv; first < end; first += TP_THREADS) {  // wave-uniform
     uint4 a, b, c;
-#if EVM_TP_PREFETCH
-    a = na;
-    b = nb;
-    c = nc;
-    const u32 ci_cur = nci;
-    if (first + TP_THREADS < end) {
-      clp_fetch<S48>(ts, stride, end, first + TP_THREADS, na, nb, nc);
-      if (first + TP_THREADS + lane < end) nci = __builtin_nontemporal_load(cell + first + TP_THREADS + lane);
-    }
-#else
     clp_fetch<S48>(ts, stride, end, first, a, b, c);
-#endif
     const size_t i = first + lane;
     u32 w[12];
     if (S48) {
@@ -1247,11 +1223,7 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
 #endif
     const bool valid = (p.meta & EVM_META_VALID) != 0;
     if (i < end) {
-#if EVM_TP_PREFETCH
-      const u32 ci = ci_cur;
-#else
       const u32 ci = __builtin_nontemporal_load(cell + i);
-#endif
       const bool ok = valid && ci < C;
       const bool fast = (p.tc >> 16) < TP_MS_FAST && ((u32)p.tc & 0xffffu) < 256u;
       __builtin_nontemporal_store(!ok ? TP_INVALID : fast ? tpc_pack(p.tc, ci) : TP_FAR, tcs + i);
@@ -1762,19 +1734,14 @@ __device__ __forceinline__ u32 xf_minute_off(u64 tc, u64 base_ms, u32 mlo, bool 
 
 // A tile of THREADS x ITEMS pairs is staged in LDS with its bucket ids and
 // written back bucket by bucket (EVM_XF_SCATTER picks the shape).
-#ifndef EVM_XF_NOSTAGE  // (A/B builds: 1 = pairs written straight from registers, L2 merges a bucket's run)
-#define EVM_XF_NOSTAGE 0
-#endif
 template <int THREADS, int ITEMS>
 __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ hash, const u64* __restrict__ tcs,
                                                           const u64* __restrict__ tcs_far,
                                                           const u32* __restrict__ cell, size_t n, int kb, int cbits,
                                                           u32 cap, u32* __restrict__ cursor, u64* __restrict__ out,
                                                           Info* __restrict__ info, u32 tl) {
-  // staged: 1 workgroup of 1,024 per CU (its LDS); unstaged: 8 KiB, two per CU
-  constexpr int SN = EVM_XF_NOSTAGE ? 1 : THREADS * ITEMS;
-  __shared__ u64 stage[SN];
-  __shared__ uint16_t sbk[SN];      // the bucket of each staged pair
+  __shared__ u64 stage[(THREADS * ITEMS)];
+  __shared__ uint16_t sbk[(THREADS * ITEMS)];      // the bucket of each staged pair
   __shared__ u32 cnt[1u << XP_MAX_KB];  // per bucket: count, then local offset
   __shared__ u32 gb[1u << XP_MAX_KB];   // per bucket: this tile's base inside the bucket
   __shared__ u32 scan_tmp[THREADS / 64 + 1];
@@ -1837,15 +1804,6 @@ __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ 
   }
   if (__ballot(full) && (threadIdx.x & 63) == 0) atomic_or_if(&info->xf_redo, 1u);
   __syncthreads();
-  if (EVM_XF_NOSTAGE) {
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k)
-      if (bk[k] < B) {
-        const u32 slot = gb[bk[k]] + r[k];
-        if (slot < cap) out[(size_t)bk[k] * cap + slot] = v[k];
-      }
-    return;
-  }
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k)
     if (bk[k] < B) {

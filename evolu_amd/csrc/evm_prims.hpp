@@ -19,6 +19,58 @@ __device__ __forceinline__ u64 lanemask_lt() {
 }
 
 // ----------------------------------------------------------------------------
+// Decoupled look-back by one whole wave (every lane of the calling wave must
+// call it): tile `tile` has published its own aggregate; each step reads the
+// status words of the 64 tiles before the window in parallel, and folds the
+// aggregates of the tiles nearer than the nearest inclusive prefix -- so a
+// tile walks back 64 predecessors per L2 round trip, not one.  Status word:
+// LB_AGG | value, or LB_PRE | value (value: the low 62 bits); 0 = not ready.
+// Returns the fold of every tile before `tile` (exclusive prefix); a wait
+// past `spin_max` polls sets *err and returns what it has.
+// ----------------------------------------------------------------------------
+constexpr u64 LB_AGG = 1ull << 62, LB_PRE = 2ull << 62, LB_VAL = (1ull << 62) - 1;
+template <typename Op>
+__device__ __forceinline__ u64 lookback_wave(const u64* status, u32 tile, Op op, u32 spin_max, u32* err) {
+  const int lane = __lane_id();
+  u64 acc = Op::id();
+  long t = (long)tile - 1;
+  u32 spins = 0;
+  while (t >= 0) {
+    const long idx = t - lane;
+    const u64 w = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : LB_PRE;
+    const u64 pre = __ballot((w & LB_PRE) != 0);
+    const u64 ready = __ballot((w & (LB_PRE | LB_AGG)) != 0);
+    const int k = pre ? __builtin_ctzll(pre) : 63;  // the nearest inclusive prefix in the window
+    const u64 need = k == 63 ? ~0ull : ((2ull << k) - 1ull);
+    if ((ready & need) != need) {  // a tile in the way has not published yet
+      if (++spins > spin_max) {
+        if (lane == 0) atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    u64 v = lane <= k ? (w & LB_VAL) : Op::id();
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = op(v, __shfl_xor(v, d, 64));
+    acc = op(acc, v);
+    if (pre) break;
+    t -= 64;
+  }
+  return acc;
+}
+template <typename T>
+struct LbAdd {
+  __device__ static T id() { return T(0); }
+  __device__ T operator()(T a, T b) const { return a + b; }
+};
+template <typename T>
+struct LbXor {
+  __device__ static T id() { return T(0); }
+  __device__ T operator()(T a, T b) const { return a ^ b; }
+};
+
+// ----------------------------------------------------------------------------
 // Status bounds (Info.minute_min & co.).  Same-address atomics from every wave
 // serialise at the memory side (a min+max per wave made the pack kernel 2-5x
 // slower at 2-8k blocks): reduce over the block first, then touch the global

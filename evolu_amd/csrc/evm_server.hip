@@ -1244,7 +1244,6 @@ struct SvbPfx {
   u64* status;   // [NS] flag:2 | xor:32, zeroed
   u32* ctr;      // segment counter, look-back error
 };
-constexpr u64 SVB_AGG = 1ull << 62, SVB_PRE = 2ull << 62;
 constexpr u32 SVB_SPIN_MAX = 1u << 24;
 
 template <bool MERGE>
@@ -1409,35 +1408,16 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   u32 segx;
   block_inclusive_scan<u32>(xacc, tmp, OpXor<u32>(), &segx);
   const u64 nout = (lb - la) + NL - dtot;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {  // wave 0: publish, look back 64 segments per step, publish the prefix
     u64* my = px.status + s;
-    u32 excl = 0;
-    if (s == 0) {
-      __hip_atomic_store(my, SVB_PRE | (u64)segx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(my, SVB_AGG | (u64)segx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      u32 spins = 0;
-      for (int t = (int)s - 1; t >= 0;) {
-        const u64 w = __hip_atomic_load(px.status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (w & SVB_PRE) {
-          excl ^= (u32)w;
-          break;
-        }
-        if (w & SVB_AGG) {
-          excl ^= (u32)w;
-          --t;
-          continue;
-        }
-        if (++spins > SVB_SPIN_MAX) {
-          atomicOr(px.ctr + 1, 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      __hip_atomic_store(my, SVB_PRE | (u64)(excl ^ segx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0)
+      __hip_atomic_store(my, (s == 0 ? LB_PRE : LB_AGG) | (u64)segx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32 excl = s ? (u32)lookback_wave(px.status, s, LbXor<u64>(), SVB_SPIN_MAX, px.ctr + 1) : 0u;
+    if (threadIdx.x == 0) {
+      if (s) __hip_atomic_store(my, LB_PRE | (u64)(excl ^ segx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_excl = excl;
+      if (s == NS - 1) px.pfx[lbase + nout] = (int32_t)(excl ^ segx);  // the whole tree's XOR
     }
-    s_excl = excl;
-    if (s == NS - 1) px.pfx[lbase + nout] = (int32_t)(excl ^ segx);  // the whole tree's XOR
   }
   __syncthreads();  // (the segment's leaves written above are visible to the whole workgroup)
   // exclusive prefix XOR over the segment's output leaves, in chunks of 4 per thread
@@ -1598,7 +1578,6 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_emit(u32 n_owners, u32 C
 // for j an owner's first candidate (the owner offsets, k_sv_sel_off).
 constexpr int SEL_ITEMS = 8;
 constexpr u32 SEL_TILE = SEL_THREADS * SEL_ITEMS;
-constexpr u64 SEL_AGG = 1ull << 62, SEL_PRE = 2ull << 62, SEL_VAL = (1ull << 62) - 1;
 constexpr u32 SEL_SPIN_MAX = 1u << 24;
 __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_scan(StoreView st, u32 n_owners, u32 C,
                                                              const u32* __restrict__ cpos, const u64* __restrict__ first,
@@ -1654,35 +1633,16 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_scan(StoreView st, u32 n
     }
     before[r] = b;
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {  // wave 0: publish, look back 64 tiles per step, publish the prefix
     u64* my = status + tile;
-    u64 excl = 0;
-    if (tile == 0) {
-      __hip_atomic_store(my, SEL_PRE | (u64)tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(my, SEL_AGG | (u64)tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      u32 spins = 0;
-      for (int t = (int)tile - 1; t >= 0;) {
-        const u64 s = __hip_atomic_load(status + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (s & SEL_PRE) {
-          excl += s & SEL_VAL;
-          break;
-        }
-        if (s & SEL_AGG) {
-          excl += s & SEL_VAL;
-          --t;
-          continue;
-        }
-        if (++spins > SEL_SPIN_MAX) {
-          atomicOr(err, 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      __hip_atomic_store(my, SEL_PRE | (excl + tsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0)
+      __hip_atomic_store(my, (tile == 0 ? LB_PRE : LB_AGG) | (u64)tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u64 excl = tile ? lookback_wave(status, tile, LbAdd<u64>(), SEL_SPIN_MAX, err) : 0ull;
+    if (threadIdx.x == 0) {
+      if (tile) __hip_atomic_store(my, LB_PRE | (excl + tsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      excl_s = excl;
+      if (j1 == C - 1) *total = (u32)(excl + tsum);
     }
-    excl_s = excl;
-    if (j1 == C - 1) *total = (u32)(excl + tsum);
   }
   __syncthreads();
   const u64 excl = excl_s;

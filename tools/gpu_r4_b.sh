@@ -2,6 +2,7 @@ set -o pipefail
 export PYTHONUNBUFFERED=1
 cd "$GRAFT_REPO_ROOT"
 # server (config 3 + reingest) and config-5 shape A/Bs of this round's options
+timeout -k 10 300 python -u bench.py --workload config4 --steps 5 --warmup 1 --cpu-seconds 0 > gpurun_out/b_c4.json 2> gpurun_out/b_c4.err &&
 timeout -k 10 400 python -u bench.py --workload server --steps 5 --warmup 2 --cpu-seconds 0 > gpurun_out/b_server.json 2> gpurun_out/b_server.err &&
 EVM_LIB_PATH=_var/svb_nopfx/libevm.so timeout -k 10 400 python -u bench.py --workload server --steps 5 --warmup 2 --cpu-seconds 0 > gpurun_out/b_server_nopfx.json 2>> gpurun_out/b_server.err &&
 EVM_LIB_PATH=_var/nocbase/libevm.so timeout -k 10 400 python -u bench.py --workload server --steps 5 --warmup 2 --cpu-seconds 0 > gpurun_out/b_server_nocbase.json 2>> gpurun_out/b_server.err &&
