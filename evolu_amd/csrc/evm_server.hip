@@ -1898,7 +1898,7 @@ __global__ __launch_bounds__(256) void k_seg_key(MinuteSrc msrc, const u32* __re
 // The fused plan's samples (no minutes pass): every 16th message's minute
 // straight from its row / record, the sampled minute range, and the owner
 // check of the sampled rows.  mm = {min, max} (k_seg_key checks every owner).
-__global__ void k_seg_smin(MinuteSrc msrc, const u32* __restrict__ owner, size_t n, u32 O, u32* __restrict__ smin,
+__global__ __launch_bounds__(256) void k_seg_smin(MinuteSrc msrc, const u32* __restrict__ owner, size_t n, u32 O, u32* __restrict__ smin,
                            u32* __restrict__ mm, Info* __restrict__ info) {
   const size_t nq = (n + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE;
   u32 mn = 0xffffffffu, mx = 0u, bad = 0u;
@@ -1910,16 +1910,9 @@ __global__ void k_seg_smin(MinuteSrc msrc, const u32* __restrict__ owner, size_t
     mx = max(mx, m);
     bad |= owner[i] >= O ? 1u : 0u;
   }
-  mn = wave_min(mn);
-  mx = wave_max(mx);
-  bad = wave_max(bad);
-  if ((threadIdx.x & 63) == 0) {
-    if (mn != 0xffffffffu) {
-      atomicMin(&mm[0], mn);
-      atomicMax(&mm[1], mx);
-    }
-    if (bad) atomic_or_if(&info->bad_aux, 1u);
-  }
+  // (one conditional global update per workgroup: same-address atomics from
+  // every wave serialise at the memory side)
+  block_fold_bounds<u32, 256>(mn, mx, bad, &mm[0], &mm[1], &info->bad_aux);
 }
 
 __global__ void k_seg_start(const u32* __restrict__ skey, size_t n, u32 NS, u64* __restrict__ start) {
