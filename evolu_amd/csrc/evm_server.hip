@@ -623,9 +623,6 @@ constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while 
 #ifndef EVM_SEG_FUSED  // (A/B builds only: 0 = a minutes pass before the plan of interleaved owners)
 #define EVM_SEG_FUSED 1
 #endif
-#ifndef EVM_SVB_PFX  // (A/B builds only: 0 = the tree's prefix XOR by a scan after the merge)
-#define EVM_SVB_PFX 1
-#endif
 
 struct SvoStatus {
   u32 big;       // an owner's share exceeds the launch's capacity
@@ -1233,19 +1230,6 @@ __device__ __forceinline__ void svb_inclusive_prefix(u32* h, u32 m, u32* tmp) {
 
 // MERGE = false: the store is empty (no stored rows, no tree leaves): no LDS
 // staging (its 24 KiB would cost occupancy for nothing).
-// The tree's prefix XOR (node hash = range XOR of the leaves) comes out of
-// the merge itself: segments are taken in launch order from a counter, each
-// publishes the XOR of its output leaves and finds the XOR of every earlier
-// segment's by decoupled look-back (as the selection's tiles do), then writes
-// its leaves' exclusive prefix -- re-reading its own just-written leaves from
-// L2 -- instead of three scan passes over the whole tree afterwards.
-struct SvbPfx {
-  int32_t* pfx;  // [leaves + 1] (null: the caller scans)
-  u64* status;   // [NS] flag:2 | xor:32, zeroed
-  u32* ctr;      // segment counter, look-back error
-};
-constexpr u32 SVB_SPIN_MAX = 1u << 24;
-
 template <bool MERGE>
 __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     SegView sv, u32 NS, u32 n_owners, StoreView st, const u64* __restrict__ st_id, const u64* __restrict__ n_tc,
@@ -1254,19 +1238,14 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     const u64* __restrict__ t_ck, const int32_t* __restrict__ t_xr, const u64* __restrict__ l_ck,
     const int32_t* __restrict__ l_xr, const uint8_t* __restrict__ l_dup, const u32* __restrict__ cnt_new,
     const u32* __restrict__ leaf_pos, StoreOut so, u64* __restrict__ so_off, u64* __restrict__ to_ck,
-    int32_t* __restrict__ to_xr, u64* __restrict__ to_off, int rows_in_place, SvbPfx px) {
+    int32_t* __restrict__ to_xr, u64* __restrict__ to_off, int rows_in_place) {
   __shared__ u32 s_dp[SVO_CAP + 1];  // exclusive prefix count of the new leaves already in the tree
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
   constexpr u32 LN = MERGE ? SVB_LDS : 1;
   __shared__ u64 k_tc[LN], k_hi[LN];  // new row keys (then new leaf codes in k_tc)
   __shared__ u32 k_lo[LN];
   __shared__ u32 hist[LN + 1];
-  __shared__ u32 s_seg, s_excl;
-  if (px.pfx) {
-    if (threadIdx.x == 0) s_seg = atomicAdd(px.ctr, 1u);
-    __syncthreads();
-  }
-  const u32 s = px.pfx ? s_seg : blockIdx.x;
+  const u32 s = blockIdx.x;
   const u32 o = seg_owner(sv, s);
   const u64 a = sv.start[s];
   const u32 M = cnt_rows[s], NL = cnt_new[s];
@@ -1331,8 +1310,6 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     so.id[w] = n_id[a + j];
   }
   // leaves: union of the tree's and the new ones by code, equal codes XOR-combined
-  // (xacc: this thread's share of the XOR of every output leaf = tree leaves ^ new leaves)
-  u32 xacc = 0;
   const u64 la = sv.la[s], lb = sv.lb[s];
   const u64 lbase = leaf_pos[s];
   constexpr int PERB = SVO_CAP / SVO_THREADS;
@@ -1380,12 +1357,10 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     const u64 w = lbase + (k - la) + j - s_dp[j];
     to_ck[w] = code;
     to_xr[w] = t_xr[k] ^ (eq ? l_xr[a + j] : 0);
-    xacc ^= (u32)t_xr[k];
   }
   __syncthreads();
   if (lds_leaves) svb_inclusive_prefix(hist, NL + 1, tmp);  // hist[j] = tree leaves below new leaf j
   for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) {
-    xacc ^= (u32)l_xr[a + j];
     if (l_dup[a + j]) continue;
     const u64 code = lds_leaves ? k_tc[j] : l_ck[a + j];
     const u64 below = lds_leaves ? (u64)hist[j] : lb_u64(t_ck, la, lb, code) - la;
@@ -1402,45 +1377,6 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
       so_off[n_owners] = base + (sb - sa) + M;
       to_off[n_owners] = lbase + (lb - la) + NL - dtot;
     }
-  }
-  if (!px.pfx) return;
-  // the segment's XOR, published; the earlier segments' by look-back
-  u32 segx;
-  block_inclusive_scan<u32>(xacc, tmp, OpXor<u32>(), &segx);
-  const u64 nout = (lb - la) + NL - dtot;
-  if (threadIdx.x < 64) {  // wave 0: publish, look back 64 segments per step, publish the prefix
-    u64* my = px.status + s;
-    if (threadIdx.x == 0)
-      __hip_atomic_store(my, (s == 0 ? LB_PRE : LB_AGG) | (u64)segx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const u32 excl = s ? (u32)lookback_wave(px.status, s, LbXor<u64>(), SVB_SPIN_MAX, px.ctr + 1) : 0u;
-    if (threadIdx.x == 0) {
-      if (s) __hip_atomic_store(my, LB_PRE | (u64)(excl ^ segx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_excl = excl;
-      if (s == NS - 1) px.pfx[lbase + nout] = (int32_t)(excl ^ segx);  // the whole tree's XOR
-    }
-  }
-  __syncthreads();  // (the segment's leaves written above are visible to the whole workgroup)
-  // exclusive prefix XOR over the segment's output leaves, in chunks of 4 per thread
-  u32 carry = s_excl;
-  for (u64 c0 = 0; c0 < nout; c0 += 4 * SVO_THREADS) {
-    u32 v[4], x = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const u64 q = c0 + threadIdx.x * 4 + r;
-      // (agent-scope loads: past the CU's L1, which another workgroup may have
-      // filled with a neighbouring segment's line before this one wrote it)
-      v[r] = q < nout ? (u32)__hip_atomic_load(to_xr + lbase + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      x ^= v[r];
-    }
-    u32 ctot;
-    u32 run = block_inclusive_scan<u32>(x, tmp, OpXor<u32>(), &ctot) ^ x ^ carry;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const u64 q = c0 + threadIdx.x * 4 + r;
-      if (q < nout) px.pfx[lbase + q] = (int32_t)run;
-      run ^= v[r];
-    }
-    carry ^= ctot;
   }
 }
 
@@ -2467,37 +2403,18 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     return st;
   }
   const StoreOut so{ns->owner, ns->tc, ns->hi, ns->lo, ns->id};
-  // the tree's prefix XOR from the merge's look-back (EVM_SVB_PFX), or a scan afterwards
-  SvbPfx px{nullptr, nullptr, nullptr};
-  if (EVM_SVB_PFX && NS) {
-    px.status = S.alloc<u64>(NS);
-    px.ctr = S.alloc<u32>(2);
-    if (!px.status || !px.ctr) {
-      store_release_arrays(ctx, ns);
-      tree_destroy(ctx, nt);
-      return EVM_ENOMEM;
-    }
-    HIPR(hipMemsetAsync(px.status, 0, sizeof(u64) * NS, ctx->stream));
-    HIPR(hipMemsetAsync(px.ctr, 0, 2 * sizeof(u32), ctx->stream));
-    px.pfx = nt->pfx;
-  }
   if (s->n)
     KLAUNCH(k_svo_b<true>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
           c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + NS, so, ns->off, nt->ck, nt->xr,
-          nt->off, in_place, px);
+          nt->off, in_place);
   else
     KLAUNCH(k_svo_b<false>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
           c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + NS, so, ns->off, nt->ck, nt->xr,
-          nt->off, in_place, px);
-  if (px.pfx) {
-    u32 herr = 0;
-    HIPR(hipMemcpyAsync(&herr, px.ctr + 1, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipStreamSynchronize(ctx->stream));
-    if (herr) st = EVM_EDEVICE;  // a look-back wait gave up
-  } else {
-    st = scan_exclusive<int32_t, OpXor>(ctx, S, nt->xr, ht[1], nt->pfx, nt->pfx + ht[1]);
-  }
-  if (st) {
+          nt->off, in_place);
+  // (the prefix XOR inside the merge -- segments by decoupled look-back, each
+  // re-reading its own leaves -- measured 1.88 vs 0.79 + 0.39 ms of scans on
+  // config 3: the merge's workgroups then wait on each other)
+  if ((st = scan_exclusive<int32_t, OpXor>(ctx, S, nt->xr, ht[1], nt->pfx, nt->pfx + ht[1]))) {
     store_release_arrays(ctx, ns);
     tree_destroy(ctx, nt);
     return st;
