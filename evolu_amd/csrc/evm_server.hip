@@ -1151,7 +1151,9 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SvoWpe<
   if (threadIdx.x == 0 && NL) {
     const int l0 = base3_len(s_lm[0]), l1 = base3_len(s_lm[NL - 1]);
     if (l0 != l1) atomicOr(&status->fallback, 1u);
-    atomicOr(&status->lens, (1u << l0) | (1u << l1));  // (one key length over the batch: code order = minute order)
+    // (one key length over the batch: code order = minute order; a same-address
+    // atomic from every workgroup would serialise -- only new bits are written)
+    atomic_or_if(&status->lens, (1u << l0) | (1u << l1));
   }
   u32 dups = 0;
   for (u32 l = threadIdx.x; l < NL; l += THREADS) {
