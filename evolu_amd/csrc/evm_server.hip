@@ -674,17 +674,11 @@ struct SvoLog2 {
 // where K5 reads a message: packed records (evm_rec), the 48-B timestamp
 // rows (parsed in the workgroup), or a route's received records in place
 enum { SRC_REC = 0, SRC_ROWS = 1, SRC_WIRE = 2 };
-// waves per SIMD K5 is compiled for: its LDS fits six 1,024-capacity
-// workgroups per CU; the registers alone would allow five (EVM_K5_WPE: A/B)
-#ifndef EVM_K5_WPE
-#define EVM_K5_WPE 0
-#endif
-template <u32 CAP, int THREADS>
-struct SvoWpe {
-  static constexpr int v = (EVM_K5_WPE && CAP == 1024 && THREADS == 256) ? EVM_K5_WPE : 1;
-};
+// (compiled for six waves per SIMD instead of the five its registers allow
+// -- the LDS fits six 1,024-capacity workgroups per CU -- it ran no faster:
+// config 3 2.60 vs 2.58 ms, config 4 3.31 vs 3.24)
 template <u32 CAP, int SRC, int THREADS = SVO_THREADS>
-__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(SvoWpe<CAP, THREADS>::v))) void k_svo_a(
+__global__ __launch_bounds__(THREADS) void k_svo_a(
     const evm_rec* __restrict__ rec, const uint8_t* __restrict__ ts, size_t stride, Info* __restrict__ info,
     const u32* __restrict__ perm, SegView sv, StoreView st,
     const u64* __restrict__ t_ck, u64 id_base, uint8_t* __restrict__ flags,
