@@ -25,7 +25,8 @@ pmc client --extra 0 --steps 3 --warmup 1 --cpu-seconds 0
 pmc client_adversarial --workload adversarial --steps 3 --warmup 1
 pmc config3 --workload server --steps 2 --warmup 1 --cpu-seconds 0
 pmc config4 --workload config4 --steps 2 --warmup 1
-pmc config5 --workload config5 --steps 2 --warmup 1
+pmc config5 --workload config5shape --steps 2 --warmup 1
+pmc config5n --workload config5 --steps 2 --warmup 1
 if [ "$1" = "sq" ]; then
   B=(python3 "$R/bench.py" --extra 0 --steps 3 --warmup 1 --cpu-seconds 0)
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU \
