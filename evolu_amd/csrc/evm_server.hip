@@ -1218,6 +1218,10 @@ __global__ void k_seg_fix(SegView sv, u32 NS, const uint8_t* __restrict__ ownbig
 // segments search the global arrays as before.  Leaves the same way (an equal
 // tree leaf counts one bin higher: it is not below the new code).
 constexpr u32 SVB_LDS = 1024;
+#ifndef EVM_SVB_BATCH  // (A/B builds only: stored rows / leaves per thread whose loads are issued together)
+#define EVM_SVB_BATCH 4
+#endif
+constexpr int SVB_B = EVM_SVB_BATCH;
 
 __device__ __forceinline__ void svb_inclusive_prefix(u32* h, u32 m, u32* tmp) {
   // h[0..m) -> inclusive prefix sums in place (m <= SVB_LDS + 1)
@@ -1269,50 +1273,82 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     for (u32 j = threadIdx.x; j <= M; j += SVO_THREADS) hist[j] = 0;
   }
   __syncthreads();
-  for (u64 k = sa + threadIdx.x; !rows_in_place && k < sb; k += SVO_THREADS) {
-    const SKey key{o, st.tc[k], st.hi[k], st.lo[k]};  // (the segment's stored rows are all owner o's)
-    u32 lo = 0, hi = M;
-    if (lds_rows) {
-      while (lo < hi) {  // (one owner: compare (tc, hi, lo))
-        const u32 mid = (lo + hi) >> 1;
-        const bool below = k_tc[mid] != key.tc ? k_tc[mid] < key.tc
-                           : k_hi[mid] != key.hi ? k_hi[mid] < key.hi : k_lo[mid] < key.lo;
-        if (below) lo = mid + 1;
-        else hi = mid;
-      }
-      atomicAdd(&hist[lo], 1u);
-    } else {
-      while (lo < hi) {
-        const u32 mid = (lo + hi) >> 1;
-        if (skey_cmp(SKey{o, n_tc[a + mid], n_hi[a + mid], n_lo[a + mid]}, key) < 0) lo = mid + 1;
-        else hi = mid;
+  // (SVB_B rows per thread per round, all their loads issued before any is
+  // used: one memory latency per round instead of one per row)
+  for (u64 k0 = sa + threadIdx.x; !rows_in_place && k0 < sb; k0 += (u64)SVB_B * SVO_THREADS) {
+    u64 rtc[SVB_B], rhi[SVB_B], rid[SVB_B];
+    u32 rlo[SVB_B];
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u64 k = k0 + (u64)r * SVO_THREADS;
+      rtc[r] = rhi[r] = rid[r] = 0;
+      rlo[r] = 0;
+      if (k < sb) {
+        rtc[r] = st.tc[k];
+        rhi[r] = st.hi[k];
+        rlo[r] = st.lo[k];
+        rid[r] = st_id[k];
       }
     }
-    const u64 w = base + (k - sa) + lo;
-    so.owner[w] = o;
-    so.tc[w] = key.tc;
-    so.hi[w] = key.hi;
-    so.lo[w] = key.lo;
-    so.id[w] = st_id[k];
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u64 k = k0 + (u64)r * SVO_THREADS;
+      if (k >= sb) break;
+      const SKey key{o, rtc[r], rhi[r], rlo[r]};  // (the segment's stored rows are all owner o's)
+      u32 lo = 0, hi = M;
+      if (lds_rows) {
+        while (lo < hi) {  // (one owner: compare (tc, hi, lo))
+          const u32 mid = (lo + hi) >> 1;
+          const bool below = k_tc[mid] != key.tc ? k_tc[mid] < key.tc
+                             : k_hi[mid] != key.hi ? k_hi[mid] < key.hi : k_lo[mid] < key.lo;
+          if (below) lo = mid + 1;
+          else hi = mid;
+        }
+        atomicAdd(&hist[lo], 1u);
+      } else {
+        while (lo < hi) {
+          const u32 mid = (lo + hi) >> 1;
+          if (skey_cmp(SKey{o, n_tc[a + mid], n_hi[a + mid], n_lo[a + mid]}, key) < 0) lo = mid + 1;
+          else hi = mid;
+        }
+      }
+      const u64 w = base + (k - sa) + lo;
+      so.owner[w] = o;
+      so.tc[w] = key.tc;
+      so.hi[w] = key.hi;
+      so.lo[w] = key.lo;
+      so.id[w] = rid[r];
+    }
   }
   __syncthreads();
   if (lds_rows) svb_inclusive_prefix(hist, M + 1, tmp);  // hist[j] = stored rows below new row j
-  for (u32 j = threadIdx.x; !rows_in_place && j < M; j += SVO_THREADS) {
-    SKey key;
-    u64 below;
-    if (lds_rows) {
-      key = SKey{o, k_tc[j], k_hi[j], k_lo[j]};
-      below = hist[j];
-    } else {
-      key = SKey{o, n_tc[a + j], n_hi[a + j], n_lo[a + j]};
-      below = store_lower(st, sa, sb, key) - sa;
+  for (u32 j0 = threadIdx.x; !rows_in_place && j0 < M; j0 += SVB_B * SVO_THREADS) {
+    u64 nid[SVB_B];
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u32 j = j0 + r * SVO_THREADS;
+      nid[r] = j < M ? n_id[a + j] : 0ull;
     }
-    const u64 w = base + j + below;
-    so.owner[w] = o;
-    so.tc[w] = key.tc;
-    so.hi[w] = key.hi;
-    so.lo[w] = key.lo;
-    so.id[w] = n_id[a + j];
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u32 j = j0 + r * SVO_THREADS;
+      if (j >= M) break;
+      SKey key;
+      u64 below;
+      if (lds_rows) {
+        key = SKey{o, k_tc[j], k_hi[j], k_lo[j]};
+        below = hist[j];
+      } else {
+        key = SKey{o, n_tc[a + j], n_hi[a + j], n_lo[a + j]};
+        below = store_lower(st, sa, sb, key) - sa;
+      }
+      const u64 w = base + j + below;
+      so.owner[w] = o;
+      so.tc[w] = key.tc;
+      so.hi[w] = key.hi;
+      so.lo[w] = key.lo;
+      so.id[w] = nid[r];
+    }
   }
   // leaves: union of the tree's and the new ones by code, equal codes XOR-combined
   const u64 la = sv.la[s], lb = sv.lb[s];
@@ -1341,27 +1377,40 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     for (u32 j = threadIdx.x; j <= NL; j += SVO_THREADS) hist[j] = 0;
   }
   __syncthreads();
-  for (u64 k = la + threadIdx.x; k < lb; k += SVO_THREADS) {
-    const u64 code = t_ck[k];
-    u32 j;
-    bool eq;
-    if (lds_leaves) {
-      u32 lo = 0, hi = NL;
-      while (lo < hi) {
-        const u32 mid = (lo + hi) >> 1;
-        if (k_tc[mid] < code) lo = mid + 1;
-        else hi = mid;
-      }
-      j = lo;
-      eq = j < NL && k_tc[j] == code;
-      atomicAdd(&hist[j + (eq ? 1u : 0u)], 1u);  // (an equal tree leaf is not below new leaf j)
-    } else {
-      j = (u32)(lb_u64(l_ck, a, a + NL, code) - a);  // new leaves below this code
-      eq = j < NL && l_ck[a + j] == code;
+  for (u64 k0 = la + threadIdx.x; k0 < lb; k0 += (u64)SVB_B * SVO_THREADS) {
+    u64 tcode[SVB_B];
+    int32_t txr[SVB_B];
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u64 k = k0 + (u64)r * SVO_THREADS;
+      tcode[r] = k < lb ? t_ck[k] : 0ull;
+      txr[r] = k < lb ? t_xr[k] : 0;
     }
-    const u64 w = lbase + (k - la) + j - s_dp[j];
-    to_ck[w] = code;
-    to_xr[w] = t_xr[k] ^ (eq ? l_xr[a + j] : 0);
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u64 k = k0 + (u64)r * SVO_THREADS;
+      if (k >= lb) break;
+      const u64 code = tcode[r];
+      u32 j;
+      bool eq;
+      if (lds_leaves) {
+        u32 lo = 0, hi = NL;
+        while (lo < hi) {
+          const u32 mid = (lo + hi) >> 1;
+          if (k_tc[mid] < code) lo = mid + 1;
+          else hi = mid;
+        }
+        j = lo;
+        eq = j < NL && k_tc[j] == code;
+        atomicAdd(&hist[j + (eq ? 1u : 0u)], 1u);  // (an equal tree leaf is not below new leaf j)
+      } else {
+        j = (u32)(lb_u64(l_ck, a, a + NL, code) - a);  // new leaves below this code
+        eq = j < NL && l_ck[a + j] == code;
+      }
+      const u64 w = lbase + (k - la) + j - s_dp[j];
+      to_ck[w] = code;
+      to_xr[w] = txr[r] ^ (eq ? l_xr[a + j] : 0);
+    }
   }
   __syncthreads();
   if (lds_leaves) svb_inclusive_prefix(hist, NL + 1, tmp);  // hist[j] = tree leaves below new leaf j
