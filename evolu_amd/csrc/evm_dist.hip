@@ -240,7 +240,8 @@ constexpr int DROUNDS = 16;           // rows per thread per block
 constexpr u32 DTILE = DT * DROUNDS;   // rows per block
 constexpr size_t META = 16;           // raw records: owner u32, aux u32, source index u32, pad
 constexpr size_t PACKED = 32;         // packed records (48-B timestamp rows): tc, node, owner, aux, index, case|valid
-constexpr size_t NARROW = 24;         // packed records without aux / source index (EVM_ROUTE_NO_SRC): tc, node, owner, case|valid
+constexpr size_t NARROW = 24;         // bytes per row without aux / source index (EVM_ROUTE_NO_SRC), as three
+                                      // arrays: (tc, node) 16 B, case|valid 4 B, the receiver's owner id 4 B
 enum { FMT_RAW = 0, FMT_PACKED = 1, FMT_NARROW = 2, FMT_ST8 = 4 /* RECV: rebuilt rows with 8-B stores */ };
 constexpr u32 PK_VALID = 1u << 16;
 // count words exchanged per route: the row count in the low bits, flags on top
@@ -284,11 +285,30 @@ struct Route {
   // [self_lo, self_hi) are read from the send buffer at self_rec
   const char* self_rec;
   u64 self_lo, self_hi;
+  // narrow routes travel as three arrays (SoA): (tc, node) 16 B, case mask |
+  // valid 4 B, and the owner 4 B -- the receiver's local id when a directory
+  // or split is set (so the received owner column is the store's owner array
+  // as it arrives), else the global id.  RECV: the received arrays (the owner
+  // one contiguous, this rank's own part copied in) and this rank's own rows'
+  // (tc, node) and masks in the send buffer.
+  const char* soa_a;
+  const u32* soa_b;
+  const u32* soa_c;
+  const char* self_a;
+  const u32* self_b;
 };
 
 // received record i: the staging buffer, or this rank's own rows in the send buffer
 __device__ __forceinline__ const char* recv_rec(const Route& R, const char* rec, size_t rb, size_t i) {
   return (i >= R.self_lo && i < R.self_hi) ? R.self_rec + (i - R.self_lo) * rb : rec + i * rb;
+}
+__device__ __forceinline__ bool is_self(const Route& R, size_t i) { return i >= R.self_lo && i < R.self_hi; }
+// a narrow route's received row i: (tc, node) and the case mask | valid word
+__device__ __forceinline__ uint4 narrow_tn(const Route& R, size_t i) {
+  return *reinterpret_cast<const uint4*>(is_self(R, i) ? R.self_a + (i - R.self_lo) * 16 : R.soa_a + i * 16);
+}
+__device__ __forceinline__ u32 narrow_cm(const Route& R, size_t i) {
+  return is_self(R, i) ? R.self_b[i - R.self_lo] : R.soa_b[i];
 }
 
 // The timestamp-hash rank of a row (murmur3 of its 46 bytes: equal strings,
@@ -325,6 +345,10 @@ __device__ __forceinline__ u32 bucket_of(size_t i, const Route& R, const char* r
     if (is_hot(R, o)) return ts_rank(R.ts + i * R.stride, R.world);
     if (R.dir_dest) return o < R.n_dir ? (u32)R.dir_dest[o] : 0xffffffffu;
     return o % R.world;
+  }
+  if (R.soa_c) {  // narrow: the owner column arrived as the sender wrote it
+    const u32 c = R.soa_c[i];
+    return (R.dir_local || R.hot) ? c : c / R.world;
   }
   const u32 o = *reinterpret_cast<const u32*>(recv_rec(R, rec, rb, i) + ooff);
   return local_of(R, o);
@@ -429,13 +453,14 @@ __device__ __forceinline__ void copy_row(char* __restrict__ dst, const char* __r
 //   SEND: caller rows -> wire records (packed, or ts | owner, aux, index);
 //         a row outside the native domain sets *invalid (packed only)
 //   RECV: wire records -> caller arrays (+ source rank from the receive offsets)
+// (SEND, narrow: out_rec holds the three arrays of soa_n rows each)
 template <int MODE>
 __global__ __launch_bounds__(DT) void k_dist_scatter(
     Route R, const char* __restrict__ ts, size_t stride, const u32* __restrict__ aux, const char* __restrict__ rec,
     size_t rb, int fmt, size_t n, u32 B, int bits, u32 nblocks, const u32* __restrict__ offs,
     char* __restrict__ out_rec, char* __restrict__ out_ts, size_t out_stride, u32* __restrict__ out_owner,
     u32* __restrict__ out_aux, u64* __restrict__ out_src, const u64* __restrict__ roff, u32 n_src,
-    u32* __restrict__ invalid) {
+    u32* __restrict__ invalid, size_t soa_n) {
   __shared__ Ranker L;
   if (offs && threadIdx.x < B) L.run[threadIdx.x] = offs[(size_t)threadIdx.x * nblocks + blockIdx.x];
   const size_t base = (size_t)blockIdx.x * DTILE;
@@ -460,11 +485,12 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
       const Parsed p = parse_ts46(w);
       inv |= (p.meta & EVM_META_VALID) == 0;
       const u32 cm = (p.meta & EVM_META_CASEMASK) | ((p.meta & EVM_META_VALID) ? PK_VALID : 0u);
-      if (fmt == FMT_NARROW) {  // 24 B at 8-B alignment
-        uint2* dst = reinterpret_cast<uint2*>(out_rec + pos * rb);
-        dst[0] = make_uint2((u32)p.tc, (u32)(p.tc >> 32));
-        dst[1] = make_uint2((u32)p.node, (u32)(p.node >> 32));
-        dst[2] = make_uint2(R.owner[i], cm);
+      if (fmt == FMT_NARROW) {  // three arrays: (tc, node), mask, the receiver's owner id
+        const u32 o = R.owner[i];
+        reinterpret_cast<uint4*>(out_rec)[pos] = make_uint4((u32)p.tc, (u32)(p.tc >> 32), (u32)p.node,
+                                                            (u32)(p.node >> 32));
+        reinterpret_cast<u32*>(out_rec + soa_n * 16)[pos] = cm;
+        reinterpret_cast<u32*>(out_rec + soa_n * 20)[pos] = (R.dir_local || R.hot) ? local_of(R, o) : o;
       } else {
         uint4* dst = reinterpret_cast<uint4*>(out_rec + pos * rb);
         dst[0] = make_uint4((u32)p.tc, (u32)(p.tc >> 32), (u32)p.node, (u32)(p.node >> 32));
@@ -480,15 +506,14 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
       m.w = 0u;
       *reinterpret_cast<uint4*>(dst + stride) = m;
     } else {
-      const char* src = recv_rec(R, rec, rb, i);
+      const bool nar = (fmt & 3) == FMT_NARROW;
+      const char* src = nar ? nullptr : recv_rec(R, rec, rb, i);
       uint4 m;
       if (fmt & 3) {
         uint4 a;
-        if ((fmt & 3) == FMT_NARROW) {
-          const uint2* q = reinterpret_cast<const uint2*>(src);
-          const uint2 t = q[0], nd = q[1], om = q[2];
-          a = make_uint4(t.x, t.y, nd.x, nd.y);
-          m = make_uint4(om.x, 0u, 0u, om.y);
+        if (nar) {
+          a = narrow_tn(R, i);
+          m = make_uint4(R.soa_c[i], 0u, 0u, narrow_cm(R, i));
         } else {
           a = reinterpret_cast<const uint4*>(src)[0];
           m = reinterpret_cast<const uint4*>(src)[1];
@@ -509,7 +534,8 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
         copy_row(out_ts + pos * out_stride, src, stride);
         m = *reinterpret_cast<const uint4*>(src + stride);
       }
-      out_owner[pos] = (R.dir_local || R.hot) ? local_of(R, m.x) : m.x;
+      // (a narrow route's owner column is already the receiver's id)
+      out_owner[pos] = (!nar && (R.dir_local || R.hot)) ? local_of(R, m.x) : m.x;
       if (out_aux) out_aux[pos] = m.y;
       if (out_src) {
         // source rank: the last r with roff[r] <= i
@@ -829,6 +855,7 @@ struct evm_dist {
   // received rows [self_lo, self_hi) at send + self_off
   uint64_t self_lo = 0, self_hi = 0;
   size_t self_off = 0;
+  uint64_t self_row = 0;  // (narrow: the first of them among the send buffer's rows)
   char* send = nullptr;  // wire records (send side), device
   size_t send_cap = 0;   // bytes
   char* recv = nullptr;  // received records (staging for evm_dist_take)
@@ -881,6 +908,18 @@ Route route_of(const evm_dist* d, const u32* owner, const uint8_t* dest) {
   R.self_rec = d->send + d->self_off;
   R.self_lo = d->self_lo;
   R.self_hi = d->self_hi;
+  R.soa_a = nullptr;
+  R.soa_b = nullptr;
+  R.soa_c = nullptr;
+  R.self_a = nullptr;
+  R.self_b = nullptr;
+  if (d->narrow && d->packed) {  // the last route's three arrays (receive side) and this rank's own rows
+    R.soa_a = d->recv;
+    R.soa_b = reinterpret_cast<const u32*>(d->recv + d->n_recv * 16);
+    R.soa_c = reinterpret_cast<const u32*>(d->recv + d->n_recv * 20);
+    R.self_a = d->send + d->self_row * 16;
+    R.self_b = reinterpret_cast<const u32*>(d->send + d->n_in * 16) + d->self_row;
+  }
   return R;
 }
 
@@ -1120,6 +1159,8 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   u64* rcnt = d->cnt + W_RECV;
   d->self_lo = d->self_hi = 0;  // (a failed route leaves no rows to take)
   d->self_off = 0;
+  d->self_row = 0;
+  d->packed = d->narrow = 0;
   Route R = route_of(d, owner, dest);
   R.ts = ts;
   R.stride = stride;
@@ -1135,7 +1176,7 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
       KLAUNCH((k_dist_scatter<SEND>), dim3(nblocks), dim3(DT), R, ts, stride, aux, (const char*)nullptr, rb,
               packed0 ? (narrow0 ? (int)FMT_NARROW : (int)FMT_PACKED) : (int)FMT_RAW, n, G, ceil_log2(G), nblocks,
               offs, d->send, (char*)nullptr, (size_t)0, (u32*)nullptr, (u32*)nullptr, (u64*)nullptr,
-              (const u64*)nullptr, 0u, flags + 1);
+              (const u64*)nullptr, 0u, flags + 1, n);
       lerr = hip_ok(hipGetLastError());
     }
   }
@@ -1182,7 +1223,7 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
     if (!lerr && n) {
       KLAUNCH((k_dist_scatter<SEND>), dim3(nblocks), dim3(DT), R, ts, stride, aux, (const char*)nullptr, rb,
               fmt_final, n, G, ceil_log2(G), nblocks, offs, d->send, (char*)nullptr, (size_t)0, (u32*)nullptr,
-              (u32*)nullptr, (u64*)nullptr, (const u64*)nullptr, 0u, (u32*)nullptr);
+              (u32*)nullptr, (u64*)nullptr, (const u64*)nullptr, 0u, (u32*)nullptr, n);
       lerr = hip_ok(hipGetLastError());
     }
   }
@@ -1209,9 +1250,32 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   // copied through the transport
   const u32 me = (u32)d->rank;
   const size_t self_off = soff[me];
+  const uint64_t self_row = self_off / rb;
   slen[me] = rlen[me] = 0;
-  if ((st = d->tx->exchange(d->send, soff, slen, d->recv, roff, rlen, ctx->stream))) return st;
+  if (narrow) {
+    // three arrays, each exchanged per peer at its own element size; the
+    // owner column of this rank's own rows is copied into place, so the
+    // received owner column is contiguous
+    const size_t esz[3] = {16, 4, 4}, sb0[3] = {0, n * 16, n * 20}, rb0[3] = {0, total * 16, total * 20};
+    for (int k = 0; k < 3; ++k) {
+      uint64_t so[MAX_BUCKETS], sl[MAX_BUCKETS], ro[MAX_BUCKETS], rl[MAX_BUCKETS];
+      for (u32 p = 0; p < G; ++p) {
+        so[p] = soff[p] / rb * esz[k];
+        sl[p] = slen[p] / rb * esz[k];
+        ro[p] = roff[p] / rb * esz[k];
+        rl[p] = rlen[p] / rb * esz[k];
+      }
+      if ((st = d->tx->exchange(d->send + sb0[k], so, sl, d->recv + rb0[k], ro, rl, ctx->stream))) return st;
+    }
+    const uint64_t mine = d->recv_off[me + 1] - d->recv_off[me];
+    if (mine)
+      HIPR(hipMemcpyAsync(d->recv + total * 20 + d->recv_off[me] * 4, d->send + n * 20 + self_row * 4, mine * 4,
+                          hipMemcpyDeviceToDevice, ctx->stream));
+  } else if ((st = d->tx->exchange(d->send, soff, slen, d->recv, roff, rlen, ctx->stream))) {
+    return st;
+  }
   d->self_off = self_off;
+  d->self_row = self_row;
   d->self_lo = d->recv_off[me];
   d->self_hi = d->recv_off[me + 1];
   // receive offsets on the device (source rank of every row in evm_dist_take)
@@ -1251,7 +1315,8 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
     if (n)
       KLAUNCH((k_dist_scatter<RECV>), dim3((u32)((n + DTILE - 1) / DTILE)), dim3(DT), R, (const char*)nullptr,
               d->stride, (const u32*)nullptr, d->recv, d->rb, packed, n, 1u, 0, 1u, (const u32*)nullptr,
-              (char*)nullptr, out_ts, out_stride, out_owner, out_aux, (u64*)out_src, droff, G + 1, (u32*)nullptr);
+              (char*)nullptr, out_ts, out_stride, out_owner, out_aux, (u64*)out_src, droff, G + 1, (u32*)nullptr,
+              (size_t)0);
     return hip_ok(hipGetLastError());
   }
   Scratch S(ctx);
@@ -1267,7 +1332,7 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
     if (st) return st;
     KLAUNCH((k_dist_scatter<RECV>), dim3(nblocks), dim3(DT), R, (const char*)nullptr, d->stride, (const u32*)nullptr,
             d->recv, d->rb, packed, n, group, ceil_log2(group), nblocks, offs, (char*)nullptr, out_ts, out_stride,
-            out_owner, out_aux, (u64*)out_src, droff, G + 1, (u32*)nullptr);
+            out_owner, out_aux, (u64*)out_src, droff, G + 1, (u32*)nullptr, (size_t)0);
   }
   HIPR(hipMemcpyAsync(tot + MAX_BUCKETS, bad, sizeof(u32), hipMemcpyDeviceToDevice, ctx->stream));
   uint64_t h[MAX_BUCKETS + 1];
@@ -1286,10 +1351,14 @@ int evm_dist_ingest(evm_ctx* ctx, evm_dist* d, evm_store* store, uint64_t id_bas
   const size_t n = d->n_recv;
   if (n == 0) return EVM_OK;
   if (!flags || !(d->dir_local || d->hot)) return EVM_EINVAL;  // local ids come from the directory / split
+  const Route R = route_of(d, nullptr, nullptr);
+  if (d->packed && d->narrow) {  // the owner column arrived as the store's owner ids
+    const WireSrc w{nullptr, nullptr, R.self_lo, R.self_hi, 0u, 0u, R.soa_a, R.self_a, R.soa_b, R.self_b};
+    return server_ingest_wire(ctx, store, w, n, R.soa_c, id_base, flags);
+  }
   Scratch S(ctx);
   u32* owner = S.alloc<u32>(n);
   if (!owner) return EVM_ENOMEM;
-  const Route R = route_of(d, nullptr, nullptr);
   if (!d->packed) {
     // raw records (some rank's rows are outside the native domain): the rows
     // themselves, then the ingest that flags the culprits
@@ -1301,7 +1370,7 @@ int evm_dist_ingest(evm_ctx* ctx, evm_dist* d, evm_store* store, uint64_t id_bas
     return evm_server_ingest(ctx, store, rows, os, n, owner, id_base, flags);
   }
   KLAUNCH(k_dist_owner, dim3(grid_for(n, 256, 16384)), dim3(256), R, (const char*)d->recv, d->rb, n, owner);
-  const WireSrc w{d->recv, R.self_rec, R.self_lo, R.self_hi, (u32)d->rb, d->narrow ? 20u : 28u};
+  const WireSrc w{d->recv, R.self_rec, R.self_lo, R.self_hi, (u32)d->rb, 28u, nullptr, nullptr, nullptr, nullptr};
   return server_ingest_wire(ctx, store, w, n, owner, id_base, flags);
 }
 

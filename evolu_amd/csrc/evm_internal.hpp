@@ -319,22 +319,33 @@ int fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u
                    const Info& host_info, evm_tree** out);
 
 // A route's received packed records, read where they lie (evm_dist_ingest):
-// record i at rec + i * rb, except this rank's own rows [self_lo, self_hi),
-// which never left the send buffer (at self).  Every record: tc u64 at 0,
-// node u64 at 8, global owner u32 at 16, case mask | EVM_META_VALID u32 at
-// moff (28 in 32-B records, 20 in 24-B ones) -- the parsed form of a 46-B
-// timestamp, rebuilt exactly by format_ts46.
+// the parsed form of each 46-B timestamp -- tc, node, case mask |
+// EVM_META_VALID -- from which format_ts46 rebuilds the string exactly.
+// Record i is in the receive buffer, except this rank's own rows
+// [self_lo, self_hi), which never left the send buffer.  32-B records (rec,
+// self non-null): tc u64 at 0, node u64 at 8, the mask word at moff.  Narrow
+// routes (tn non-null): (tc, node) 16 B per row in one array, the mask words
+// in another.
 struct WireSrc {
   const char* rec;
   const char* self;
   u64 self_lo, self_hi;
   u32 rb, moff;
+  const char* tn;
+  const char* self_tn;
+  const u32* cm;
+  const u32* self_cm;
 };
-__device__ __forceinline__ const char* wire_at(const WireSrc& w, size_t i) {
-  return (i >= w.self_lo && i < w.self_hi) ? w.self + (i - w.self_lo) * w.rb : w.rec + i * w.rb;
-}
 __device__ __forceinline__ void wire_load(const WireSrc& w, size_t i, u64* tc, u64* node, u32* cm) {
-  const char* p = wire_at(w, i);
+  const bool mine = i >= w.self_lo && i < w.self_hi;
+  if (w.tn) {
+    const uint4 v = *reinterpret_cast<const uint4*>(mine ? w.self_tn + (i - w.self_lo) * 16 : w.tn + i * 16);
+    *tc = (u64)v.x | ((u64)v.y << 32);
+    *node = (u64)v.z | ((u64)v.w << 32);
+    *cm = mine ? w.self_cm[i - w.self_lo] : w.cm[i];
+    return;
+  }
+  const char* p = mine ? w.self + (i - w.self_lo) * w.rb : w.rec + i * w.rb;
   const uint2* q = reinterpret_cast<const uint2*>(p);
   const uint2 a = q[0], b = q[1];
   *tc = (u64)a.x | ((u64)a.y << 32);

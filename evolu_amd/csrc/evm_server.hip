@@ -1833,7 +1833,7 @@ __device__ __forceinline__ u32 minute_at(const MinuteSrc& m, size_t i) {
     const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(m.ts + i * m.stride));
     return minute16(v.x, v.y, v.z, v.w);
   }
-  if (m.wire.rec) {
+  if (m.wire.rec || m.wire.tn) {
     u64 tc, node;
     u32 cm;
     wire_load(m.wire, i, &tc, &node, &cm);
@@ -2168,7 +2168,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   // reads the minutes from them directly (no minutes pass; EVM_SEG_FUSED)
   const bool seg_fused = EVM_SEG_FUSED && fused && (wire || (stride % 16 == 0 && ((uintptr_t)ts & 15) == 0));
   u32* smin = nullptr;   // the samples' minutes (seg_fused)
-  MinuteSrc msrc{rec, minute, nullptr, 0, WireSrc{nullptr, nullptr, 0, 0, 0, 0}};
+  MinuteSrc msrc{rec, minute, nullptr, 0, WireSrc{nullptr, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr}};
   if (seg_fused) {
     if (wire) msrc.wire = *wire;
     else {
@@ -2307,7 +2307,8 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     KLAUNCH(k_seg_own, dim3(grid_for(O, 256)), dim3(256), bbase, spoff, sp, tboff, O, sown_rec);
     // (the minutes from the rows / records when the plan read them so, else the minutes array)
     MinuteSrc kms = msrc;
-    if (!(seg_fused && !runs)) kms = MinuteSrc{rec, minute, nullptr, 0, WireSrc{nullptr, nullptr, 0, 0, 0, 0}};
+    if (!(seg_fused && !runs))
+      kms = MinuteSrc{rec, minute, nullptr, 0, WireSrc{nullptr, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr}};
     KLAUNCH(k_seg_key, dim3(grid_for((n + SK_ITEMS - 1) / SK_ITEMS, 256)), dim3(256), kms, owner, n, O, NS,
             (const SegOwn*)sown_rec, sp, tab, bkey, info);
     u32* bk = bkey;
@@ -2357,7 +2358,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   // the common share size over every segment (more workgroups per CU); larger
   // shares are listed and take the SVO_CAP kernel over just those segments
   const uint8_t* tsb = reinterpret_cast<const uint8_t*>(ts);
-  const WireSrc wsrc = wire ? *wire : WireSrc{nullptr, nullptr, 0, 0, 0, 0};
+  const WireSrc wsrc = wire ? *wire : WireSrc{nullptr, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr};
   // pass A over every segment with the capacity that fits the typical share
   // (small segments -- Zipf tails, cut owners -- take the 512 kernel: half the
   // per-workgroup fixed work, twice the occupancy); larger shares are listed

@@ -441,8 +441,11 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
 /* evm_dist_route with flags.  EVM_ROUTE_NO_SRC: the caller will not ask
  * evm_dist_take for source indexes nor call evm_dist_return /
  * evm_dist_split_winners after this route -- with aux == NULL the rows then
- * travel as 24-B records (tc, node, owner, case mask) instead of 32, when
- * every rank routes so (the ranks agree through the count words). */
+ * travel as 24 B instead of 32, when every rank routes so (the ranks agree
+ * through the count words): three arrays -- (tc, node), case mask, and the
+ * owner as the receiver will use it (its local id when a directory or split
+ * is set, else the global id), so evm_dist_ingest reads the owner column as
+ * it arrives. */
 #define EVM_ROUTE_NO_SRC 1u
 int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, const uint32_t* owner,
                       const uint32_t* aux, const uint8_t* dest, uint32_t flags, uint64_t* n_recv);
