@@ -1935,6 +1935,17 @@ __global__ __launch_bounds__(FR_THREADS) void k_xf_blocks(u32* __restrict__ dx, 
 // An enqueued streaming batch (evm_apply_batch_async): the call's arguments
 // (the caller keeps them valid until evm_apply_wait), the pinned landing slot
 // of its status record, the event after its last kernel, and its outputs.
+#ifndef EVM_INFO_KERNEL  // (A/B builds: 1 = a kernel lands the async status record in pinned memory)
+#define EVM_INFO_KERNEL 0
+#endif
+__global__ void k_info_land(const Info* __restrict__ info, Info* host) {
+  static_assert(sizeof(Info) % 4 == 0, "word copy");
+  const u32* src = reinterpret_cast<const u32*>(info);
+  volatile u32* dst = reinterpret_cast<volatile u32*>(host);
+  for (u32 k = threadIdx.x; k < sizeof(Info) / 4; k += blockDim.x) dst[k] = src[k];
+  __threadfence_system();
+}
+
 struct evm_pending {
   const evm_tree* tree_in;
   const char* ts;
@@ -2255,7 +2266,14 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       HIPR(hipEventRecord(ctx->ev_join, ctx->stream));
       HIPR(hipStreamWaitEvent(xs, ctx->ev_join, 0));
     }
+#if EVM_INFO_KERNEL
+    // (one workgroup writes the record into the pinned slot itself: the
+    // runtime's copy of 64 bytes to the host was an 18-us blit per batch)
+    hipLaunchKernelGGL(k_info_land, dim3(1), dim3(64), 0, xs, (const Info*)info, pend->hinfo);
+    HIPR(hipGetLastError());
+#else
     HIPR(hipMemcpyAsync(pend->hinfo, info, sizeof(Info), hipMemcpyDeviceToHost, xs));
+#endif
     HIPR(hipEventRecord(pend->ev, xs));
     side.detach();
     pend->spec = spec;
