@@ -620,9 +620,6 @@ constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while 
 #ifndef EVM_SVO_CBASE  // (A/B builds only: 0 = K5 reads every batch index from perm)
 #define EVM_SVO_CBASE 1
 #endif
-#ifndef EVM_K5_T1024
-#define EVM_K5_T1024 256
-#endif
 #ifndef EVM_SEG_FUSED  // (A/B builds only: 0 = a minutes pass before the plan of interleaved owners)
 #define EVM_SEG_FUSED 1
 #endif
@@ -2373,11 +2370,9 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
       l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, list, l2, l1, ownbig, n_owner, preset, l512, wsrc
     // (the one-wave kernels: Zipf-tail owners of <= 128 / <= 256 messages, no cross-wave barriers;
     // source: true = the rows, false = packed records, SRC_WIRE = received records)
-#if EVM_K5_T1024 == 512  // (A/B builds only: the 1,024 kernel with 512 threads, two messages each)
-#define K5_1024(SRCV) KLAUNCH((k_svo_a<1024, SRCV, 512>), grid, dim3(512), SVO_ARGS)
-#else
+// (the 1,024 kernel with 512 threads, two messages each, measured slower:
+// config 3 2.80 vs 2.59 ms, config-5 shape 4.87 vs 4.04)
 #define K5_1024(SRCV) KLAUNCH((k_svo_a<1024, SRCV>), grid, dim3(SVO_THREADS), SVO_ARGS)
-#endif
 #define SVO_PASS(SRCV)                                                                         \
   if (cap == 128) KLAUNCH((k_svo_a<128, SRCV, 64>), grid, dim3(64), SVO_ARGS);                  \
   else if (cap == 256) KLAUNCH((k_svo_a<256, SRCV, 64>), grid, dim3(64), SVO_ARGS);             \
