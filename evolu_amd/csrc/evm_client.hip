@@ -1935,8 +1935,8 @@ __global__ __launch_bounds__(FR_THREADS) void k_xf_blocks(u32* __restrict__ dx, 
 // An enqueued streaming batch (evm_apply_batch_async): the call's arguments
 // (the caller keeps them valid until evm_apply_wait), the pinned landing slot
 // of its status record, the event after its last kernel, and its outputs.
-#ifndef EVM_INFO_KERNEL  // (A/B builds: 1 = a kernel lands the async status record in pinned memory)
-#define EVM_INFO_KERNEL 0
+#ifndef EVM_INFO_KERNEL  // (A/B builds: 0 = the runtime's copy lands the async status record)
+#define EVM_INFO_KERNEL 1  // (config 2: 0.2938 / 0.2989 vs 0.2971 / 0.3027 ms per step, two pairs)
 #endif
 __global__ void k_info_land(const Info* __restrict__ info, Info* host) {
   static_assert(sizeof(Info) % 4 == 0, "word copy");
