@@ -611,6 +611,10 @@ constexpr u32 SVO_CAP = 4096;  // largest share of one owner handled in LDS
 constexpr int SVO_TIE_MAX = 32;  // longest run of one (millis, counter) with distinct nodes
 constexpr u32 SVO_BUCKET_MAX = 16;  // counting-sort bucket size finished by insertion sort
 constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while <= 16 x its new rows
+#ifndef EVM_SVO_SB  // (A/B builds only: stored rows per thread whose loads are issued together)
+#define EVM_SVO_SB 4
+#endif
+constexpr int SVO_SB = EVM_SVO_SB;
 #ifndef EVM_SVO_SCAN  // (A/B builds only: 0 = a binary search of the stored rows per candidate)
 #define EVM_SVO_SCAN 1
 #endif
@@ -1017,26 +1021,46 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   const u64 sa = sv.sa[s], sb = sv.sb[s];
   const bool scan_stored = EVM_SVO_SCAN && sb > sa && sb - sa <= SVO_SCAN_STORED * m;
   if (scan_stored) {
-    for (u64 k = sa + threadIdx.x; k < sb; k += THREADS) {
-      const u64 ktc = st.tc[k];
-      if (ktc < tmin || ktc > tmax) continue;
-      const u64 kd = ktc - tmin, khi = st.hi[k];
-      const u32 klo = st.lo[k];
-      u32 lo = 0, hi = (u32)m;
-      while (lo < hi) {  // first sorted position >= (tc, ranks)
-        const u32 mid = (lo + hi) >> 1;
-        const u64 kp = s_k[mid];
-        const u64 td = kp >> PB;
-        const u32 px = (u32)(kp & PMASK);
-        const bool below = td != kd ? td < kd : s_rh[px] != khi ? s_rh[px] < khi : rl_get(px) < klo;
-        if (below) lo = mid + 1;
-        else hi = mid;
+    // (SVO_SB stored rows per thread per round: their tc loads, then the
+    // ranks of those in the new keys' span, each batch issued together)
+    constexpr int SB = SVO_SB;
+    for (u64 k0 = sa + threadIdx.x; k0 < sb; k0 += (u64)SB * THREADS) {
+      u64 btc[SB], bhi[SB];
+      u32 blo[SB];
+#pragma unroll
+      for (int r = 0; r < SB; ++r) {
+        const u64 k = k0 + (u64)r * THREADS;
+        btc[r] = k < sb ? st.tc[k] : ~0ull;
       }
-      for (u32 p = lo; p < m; ++p) {  // the timestamp's run: its candidate is already stored
-        const u64 kp = s_k[p];
-        const u32 px = (u32)(kp & PMASK);
-        if ((kp >> PB) != kd || s_rh[px] != khi || rl_get(px) != klo) break;
-        cnt_set(p, 0u);
+#pragma unroll
+      for (int r = 0; r < SB; ++r) {
+        const u64 k = k0 + (u64)r * THREADS;
+        const bool in = k < sb && btc[r] >= tmin && btc[r] <= tmax;
+        bhi[r] = in ? st.hi[k] : 0ull;
+        blo[r] = in ? st.lo[k] : 0u;
+      }
+#pragma unroll
+      for (int r = 0; r < SB; ++r) {
+        const u64 ktc = btc[r];
+        if (k0 + (u64)r * THREADS >= sb || ktc < tmin || ktc > tmax) continue;
+        const u64 kd = ktc - tmin, khi = bhi[r];
+        const u32 klo = blo[r];
+        u32 lo = 0, hi = (u32)m;
+        while (lo < hi) {  // first sorted position >= (tc, ranks)
+          const u32 mid = (lo + hi) >> 1;
+          const u64 kp = s_k[mid];
+          const u64 td = kp >> PB;
+          const u32 px = (u32)(kp & PMASK);
+          const bool below = td != kd ? td < kd : s_rh[px] != khi ? s_rh[px] < khi : rl_get(px) < klo;
+          if (below) lo = mid + 1;
+          else hi = mid;
+        }
+        for (u32 p = lo; p < m; ++p) {  // the timestamp's run: its candidate is already stored
+          const u64 kp = s_k[p];
+          const u32 px = (u32)(kp & PMASK);
+          if ((kp >> PB) != kd || s_rh[px] != khi || rl_get(px) != klo) break;
+          cnt_set(p, 0u);
+        }
       }
     }
     __syncthreads();
