@@ -1246,10 +1246,7 @@ constexpr u32 SVB_LDS = 1024;
 #define EVM_SVB_BATCH 4
 #endif
 constexpr int SVB_B = EVM_SVB_BATCH;
-#ifndef EVM_SVB_STAGE  // (A/B builds only: 0 = no LDS-assembled output columns)
-#define EVM_SVB_STAGE 1
-#endif
-constexpr u32 SVB_STAGE = 2048;  // stored + new rows of a segment assembled in LDS (s_dp: 2,048 x 8 B)
+
 
 __device__ __forceinline__ void svb_inclusive_prefix(u32* h, u32 m, u32* tmp) {
   // h[0..m) -> inclusive prefix sums in place (m <= SVB_LDS + 1)
@@ -1301,66 +1298,11 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     for (u32 j = threadIdx.x; j <= M; j += SVO_THREADS) hist[j] = 0;
   }
   __syncthreads();
-  // A segment of <= SVB_STAGE rows in all: each output column is assembled in
-  // LDS (the stored rows at their ranks among the new keys, the new rows after
-  // the stored rows below them) and written once, coalesced -- the two
-  // scattered passes below write every output line twice (stored rows, then
-  // the gaps), which doubled the merge's write bytes.
-  const u32 S = (u32)(sb - sa);
-  const bool stage_rows = lds_rows && EVM_SVB_STAGE && (u64)S + M <= SVB_STAGE;
-  if (stage_rows) {
-    constexpr int SR = SVB_STAGE / SVO_THREADS;
-    u32 spos[SR];
-#pragma unroll
-    for (int r = 0; r < SR; ++r) {
-      const u32 k = threadIdx.x + r * SVO_THREADS;
-      spos[r] = 0;
-      if (k < S) {
-        const u64 ktc = st.tc[sa + k], khi = st.hi[sa + k];
-        const u32 klo = st.lo[sa + k];
-        u32 lo = 0, hi = M;
-        while (lo < hi) {
-          const u32 mid = (lo + hi) >> 1;
-          const bool below = k_tc[mid] != ktc ? k_tc[mid] < ktc : k_hi[mid] != khi ? k_hi[mid] < khi : k_lo[mid] < klo;
-          if (below) lo = mid + 1;
-          else hi = mid;
-        }
-        atomicAdd(&hist[lo], 1u);
-        spos[r] = k + lo;
-      }
-    }
-    __syncthreads();
-    svb_inclusive_prefix(hist, M + 1, tmp);  // hist[j] = stored rows below new row j
-    const u32 T = S + M;
-    for (u32 q = threadIdx.x; q < T; q += SVO_THREADS) so.owner[base + q] = o;
-    u64* s8 = reinterpret_cast<u64*>(s_dp);
-    for (int c = 0; c < 3; ++c) {  // the 8-B columns: tc, ranks hi, id
-      const u64* stored = c == 0 ? st.tc : c == 1 ? st.hi : st_id;
-      u64* out = c == 0 ? so.tc : c == 1 ? so.hi : so.id;
-#pragma unroll
-      for (int r = 0; r < SR; ++r) {
-        const u32 k = threadIdx.x + r * SVO_THREADS;
-        if (k < S) s8[spos[r]] = stored[sa + k];
-      }
-      for (u32 j = threadIdx.x; j < M; j += SVO_THREADS)
-        s8[j + hist[j]] = c == 0 ? k_tc[j] : c == 1 ? k_hi[j] : n_id[a + j];
-      __syncthreads();
-      for (u32 q = threadIdx.x; q < T; q += SVO_THREADS) out[base + q] = s8[q];
-      __syncthreads();
-    }
-#pragma unroll
-    for (int r = 0; r < SR; ++r) {
-      const u32 k = threadIdx.x + r * SVO_THREADS;
-      if (k < S) s_dp[spos[r]] = st.lo[sa + k];
-    }
-    for (u32 j = threadIdx.x; j < M; j += SVO_THREADS) s_dp[j + hist[j]] = k_lo[j];
-    __syncthreads();
-    for (u32 q = threadIdx.x; q < T; q += SVO_THREADS) so.lo[base + q] = s_dp[q];
-    __syncthreads();
-  }
+  // (assembling each output column of a segment in LDS and writing it once,
+  // coalesced, measured slower: reingest merge 5.77 vs 4.91 ms in one run)
   // (SVB_B rows per thread per round, all their loads issued before any is
   // used: one memory latency per round instead of one per row)
-  for (u64 k0 = sa + threadIdx.x; !rows_in_place && !stage_rows && k0 < sb; k0 += (u64)SVB_B * SVO_THREADS) {
+  for (u64 k0 = sa + threadIdx.x; !rows_in_place && k0 < sb; k0 += (u64)SVB_B * SVO_THREADS) {
     u64 rtc[SVB_B], rhi[SVB_B], rid[SVB_B];
     u32 rlo[SVB_B];
 #pragma unroll
@@ -1406,8 +1348,8 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     }
   }
   __syncthreads();
-  if (lds_rows && !stage_rows) svb_inclusive_prefix(hist, M + 1, tmp);  // hist[j] = stored rows below new row j
-  for (u32 j0 = threadIdx.x; !rows_in_place && !stage_rows && j0 < M; j0 += SVB_B * SVO_THREADS) {
+  if (lds_rows) svb_inclusive_prefix(hist, M + 1, tmp);  // hist[j] = stored rows below new row j
+  for (u32 j0 = threadIdx.x; !rows_in_place && j0 < M; j0 += SVB_B * SVO_THREADS) {
     u64 nid[SVB_B];
 #pragma unroll
     for (int r = 0; r < SVB_B; ++r) {
