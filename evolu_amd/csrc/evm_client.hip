@@ -2427,6 +2427,9 @@ __global__ __launch_bounds__(256) void k_sm_pack(const uint8_t* __restrict__ ts,
 // (K3's cursors).  One workgroup, tiles of 16,384 counts: 16 consecutive per
 // thread (four 16-B loads), a block scan, the running total carried.
 constexpr u32 SM_SCAN_ITEMS = 16;
+#ifndef EVM_SM_SCAN_LB  // (A/B builds: 0 = the one-workgroup cell-offset scan)
+#define EVM_SM_SCAN_LB 1
+#endif
 // One workgroup, tiles of SM_FOLD_THREADS x 16 counts; the next tile's loads
 // are issued before this tile is scanned (a 100k-message batch has ~55k cells:
 // four tiles, one load latency instead of four).
@@ -2489,6 +2492,66 @@ __global__ __launch_bounds__(SM_FOLD_THREADS) void k_sm_scan(u32* __restrict__ c
     carry += tot;
   }
   if (threadIdx.x == 0) off[C] = carry;
+}
+
+// The same over several workgroups (one tile of SM_FOLD_THREADS x 16 counts
+// each, tiles in launch order from a counter): each tile's offsets after the
+// counts of every tile before it, by decoupled look-back (status words and
+// the counter zeroed with the batch's other scratch).  A 100k-message batch
+// of ~55k cells: four tiles side by side instead of one after another.
+constexpr u32 SM_SCAN_TILE = SM_FOLD_THREADS * SM_SCAN_ITEMS;
+__global__ __launch_bounds__(SM_FOLD_THREADS) void k_sm_scan_lb(u32* __restrict__ cnt, u32 C, u32* __restrict__ off,
+                                                                u64* __restrict__ status, u32* __restrict__ ctr,
+                                                                u32* __restrict__ err) {
+  __shared__ u32 lds[SM_FOLD_THREADS / 64 + 1];
+  __shared__ u32 tile_s, excl_s;
+  if (threadIdx.x == 0) tile_s = atomicAdd(ctr, 1u);
+  __syncthreads();
+  const u32 tile = tile_s;
+  const u32 a = tile * SM_SCAN_TILE + threadIdx.x * SM_SCAN_ITEMS;
+  u32 v[SM_SCAN_ITEMS];
+  sm_scan_load(cnt, C, a, v);
+  u32 sum = 0;
+#pragma unroll
+  for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) sum += v[q];
+  u32 tot;
+  const u32 incl = block_inclusive_scan<u32, OpAdd<u32>>(sum, lds, OpAdd<u32>(), &tot);
+  if (threadIdx.x < 64) {
+    if (threadIdx.x == 0)
+      __hip_atomic_store(status + tile, (tile == 0 ? LB_PRE : LB_AGG) | (u64)tot, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    const u32 excl = tile ? (u32)lookback_wave(status, tile, LbAdd<u64>(), 1u << 24, err) : 0u;
+    if (threadIdx.x == 0) {
+      if (tile) __hip_atomic_store(status + tile, LB_PRE | (u64)(excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      excl_s = excl;
+      if ((u64)(tile + 1) * SM_SCAN_TILE >= C) off[C] = excl + tot;
+    }
+  }
+  __syncthreads();
+  u32 run = excl_s + incl - sum;
+  u32 x[SM_SCAN_ITEMS];
+#pragma unroll
+  for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) {
+    x[q] = run;
+    run += v[q];
+  }
+  if (a + SM_SCAN_ITEMS <= C) {
+    uint4* po = reinterpret_cast<uint4*>(off + a);
+    uint4* pc = reinterpret_cast<uint4*>(cnt + a);
+#pragma unroll
+    for (u32 q = 0; q < SM_SCAN_ITEMS / 4; ++q) {
+      const uint4 y = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+      po[q] = y;
+      pc[q] = y;
+    }
+  } else {
+#pragma unroll
+    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q)
+      if (a + q < C) {
+        off[a + q] = x[q];
+        cnt[a + q] = x[q];
+      }
+  }
 }
 
 __global__ void k_sm_scatter(const evm_rec* __restrict__ rec, size_t n, u32 C, u32* __restrict__ cur,
@@ -2881,7 +2944,9 @@ static int apply_small(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tre
   const int lg = ceil_log2(2 * n);
   const size_t a_cnt = ((size_t)(C + 1) * 4 + 255) & ~(size_t)255;
   const size_t a_bins = (size_t)SM_BINS * 4, a_pres = (size_t)SM_BINS / 8;
-  const size_t zero_bytes = a_cnt + a_bins + a_pres + (sizeof(u64) << lg);
+  const u32 n_scan_tiles = (u32)std::max<size_t>(1, (C + SM_SCAN_TILE - 1) / SM_SCAN_TILE);
+  const size_t a_scan = ((size_t)n_scan_tiles * 8 + 16 + 255) & ~(size_t)255;  // look-back words, counter, error
+  const size_t zero_bytes = a_cnt + a_bins + a_pres + (sizeof(u64) << lg) + (EVM_SM_SCAN_LB ? a_scan : 0);
   char* z = S.alloc<char>(zero_bytes);
   evm_rec* rec = S.alloc<evm_rec>(n);
   u32* off = S.alloc<u32>(C + 1);
@@ -2903,7 +2968,16 @@ static int apply_small(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tre
   HIPR(hipMemsetAsync(z, 0, zero_bytes, ctx->stream));
   KLAUNCH(k_sm_pack, dim3(grid_for(n, 256, 1024)), dim3(256), (const uint8_t*)ts, stride, n, cell, C, rec, cnt, table,
           (u32)lg, info);
-  KLAUNCH(k_sm_scan, dim3(1), dim3(SM_FOLD_THREADS), cnt, C, off);
+  if (EVM_SM_SCAN_LB) {
+    u64* lb_status = reinterpret_cast<u64*>(z + a_cnt + a_bins + a_pres + (sizeof(u64) << lg));
+    u32* lb_ctr = reinterpret_cast<u32*>(lb_status + n_scan_tiles);
+    // (a look-back that gives up sends the batch to the sort path; a partial
+    // prefix keeps every slot in range meanwhile)
+    KLAUNCH(k_sm_scan_lb, dim3(n_scan_tiles), dim3(SM_FOLD_THREADS), cnt, C, off, lb_status, lb_ctr,
+            &info->fold_overflow);
+  } else {
+    KLAUNCH(k_sm_scan, dim3(1), dim3(SM_FOLD_THREADS), cnt, C, off);
+  }
   KLAUNCH(k_sm_scatter, dim3(grid_for(n, 256, 1024)), dim3(256), (const evm_rec*)rec, n, C, cnt, grp);
   KLAUNCH(k_sm_lww, dim3(grid_for(C, 256, 4096)), dim3(256), (const evm_rec*)rec, (const u32*)off, (const u32*)grp, C,
           prior, prior_present, flags, winner, bins, pres, long_list, long_n, info);
