@@ -484,3 +484,44 @@ def test_narrow_records_route(mixed):
             assert st_take is None and st_ret is None
         else:
             assert st_take == L.EVM_EINVAL and st_ret in (L.EVM_EINVAL, L.EVM_EDIST)
+
+
+@pytest.mark.parametrize("directory", [False, True])
+def test_narrow_grouped_take(directory):
+    """A 24-B route (three arrays, the owner column written as the receiver
+    uses it) taken grouped by local owner, with and without a directory:
+    rows, owners and group bounds as the 32-B route would give them."""
+    from evolu_amd import synth
+
+    world, n_owners = 3, 61
+    ids = synth.config4_owner_ids(SEED, n_owners)
+    dest_want = np.array([O.murmur3_32(bytes(r)) % world for r in ids]) if directory else np.arange(n_owners) % world
+    local_want = np.zeros(n_owners, dtype=np.int64)
+    for r in range(world):
+        local_want[dest_want == r] = np.arange((dest_want == r).sum())
+    if not directory:
+        local_want = np.arange(n_owners) // world
+    slices = _slices(world, [20_000, 33_333, 7], n_owners, 13)
+    groups = int(local_want.max()) + 1
+
+    def fn(r, eng, dd):
+        if directory:
+            pad = np.zeros((n_owners, 24), dtype=np.uint8)
+            pad[:, :21] = ids
+            dd.directory((eng.dev(pad), 21))
+        ts, owner, _ = slices[r]
+        n = dd.route(eng.dev(ts), eng.dev(owner), need_src=False)
+        t2, o2, _, _, goff = dd.take(group=groups, aux=False, src=False)
+        return n, t2.cpu().numpy(), o2.cpu().numpy().view(np.uint32), goff
+
+    res = _loop(world, fn)
+    for r in range(world):
+        ts, owner, _, _ = _expected(slices, world, r, lambda o: dest_want[o])
+        lo = local_want[owner]
+        order = np.argsort(lo, kind="stable")
+        n, t2, o2, goff = res[r]
+        assert n == len(ts)
+        assert np.array_equal(t2[:, :46], ts[order][:, :46])
+        # the owner column: local ids with a directory, global ids without (as evm_dist_take documents)
+        assert np.array_equal(o2, (lo if directory else owner)[order].astype(np.uint32))
+        assert goff == list(np.concatenate([[0], np.cumsum(np.bincount(lo, minlength=groups))]))
