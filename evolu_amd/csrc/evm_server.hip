@@ -611,9 +611,6 @@ constexpr u32 SVO_CAP = 4096;  // largest share of one owner handled in LDS
 constexpr int SVO_TIE_MAX = 32;  // longest run of one (millis, counter) with distinct nodes
 constexpr u32 SVO_BUCKET_MAX = 16;  // counting-sort bucket size finished by insertion sort
 constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while <= 16 x its new rows
-#ifndef EVM_SVB_PAD
-#define EVM_SVB_PAD 0
-#endif
 #ifndef EVM_SVO_SB  // (A/B builds only: stored rows per thread whose loads are issued together)
 #define EVM_SVO_SB 4
 #endif
@@ -2493,9 +2490,9 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   }
   const StoreOut so{ns->owner, ns->tc, ns->hi, ns->lo, ns->id};
   if (s->n)
-    // (EVM_SVB_PAD: A/B builds only -- extra LDS per workgroup, so fewer
-    // segments' output windows are in flight per XCD at once)
-    KLAUNCH_LDS(k_svo_b<true>, dim3(NS), dim3(SVO_THREADS), (size_t)EVM_SVB_PAD, sv, NS, O, view_of(s),
+    // (fewer merge workgroups per CU -- an LDS pad of 40/80 KB -- made the
+    // merge 19 %/100 % slower: its write traffic is not an L2 capacity effect)
+    KLAUNCH(k_svo_b<true>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s),
                 (const u64*)s->id, n_tc, n_hi, n_lo, n_id, c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup,
                 c_new, pos + NS, so, ns->off, nt->ck, nt->xr, nt->off, in_place);
   else
