@@ -1843,6 +1843,10 @@ __device__ __forceinline__ bool xf_insert(u32* tab, const u64* bp, u64 p, u32 k,
   return false;
 }
 
+// (a 16K-slot set with the minute histograms in dynamic LDS -- 74 KB, 20
+// VGPRs, two workgroups per CU beside the next batch's TP1 -- made the
+// headline step slower, 0.307/0.302 vs 0.2985/0.2977 ms in one run: the
+// longer probe chains at 60 % load cost more than the occupancy gave)
 __global__ __launch_bounds__(XP_THREADS) void k_xf_dedup(const u64* __restrict__ pairs, const u32* __restrict__ cursor,
                                                         u32 cap, int kb, int cbits, u32* __restrict__ dx,
                                                         u32* __restrict__ dc, Info* __restrict__ info) {
