@@ -1045,7 +1045,10 @@ __device__ __forceinline__ void tpc_unpack(u64 v, const u64* __restrict__ far, c
 }
 __device__ __forceinline__ u32 minute_of_tc(u64 tc) { return (u32)((tc >> 16) / 60000ull); }
 constexpr int TP_THREADS = 256;
-constexpr int TP_RANGES = 2048;  // ~8 ranges per CU: TP1's occupancy
+#ifndef EVM_TP_RANGES  // (A/B builds only: tools/build_variant.sh NAME -DEVM_TP_RANGES=...)
+#define EVM_TP_RANGES 2048
+#endif
+constexpr int TP_RANGES = EVM_TP_RANGES;  // ~8 ranges per CU: TP1's occupancy
 constexpr u32 ROW_NONE = 0xffffffffu;   // no max (SQL NULL: below every timestamp)
 constexpr u32 ROW_PRIOR = 0xfffffffeu;  // the max is the caller's prior row of the cell
 constexpr u32 TP_MATCH_MAX = 512;       // TP1 rescan: rows tied at a cell's range max
@@ -2069,8 +2072,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   size_t range, G;
   TpRanges TR{};
   if (TC) {
-    static const size_t tp_ranges = getenv("EVM_TP_RANGES") ? (size_t)atol(getenv("EVM_TP_RANGES")) : TP_RANGES;
-    range = std::max<size_t>(1024, ((n + tp_ranges - 1) / tp_ranges + 255) / 256 * 256);
+    range = std::max<size_t>(1024, ((n + TP_RANGES - 1) / TP_RANGES + 255) / 256 * 256);
     range = std::min<size_t>(range, TP_ROWS_MAX);  // (TP1's key holds a 13-bit row offset)
     TR = TpRanges{range, (range / 16) & ~(size_t)63};
     G = (n + range - 1) / range + 4;  // (the first range in five geometric pieces)

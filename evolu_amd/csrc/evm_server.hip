@@ -1721,18 +1721,14 @@ void store_release_arrays(evm_ctx* ctx, evm_store* s) {
 }
 
 // ------------------------------------------- key-range segments (big owners)
-constexpr u32 SEG_TARGET = 560;     // messages per segment of a cut owner: minute-granular splitters and
-                                    // sampling noise keep nearly all below 1,024 (the fast kernel)
+#ifndef EVM_SEG_TARGET  // (A/B builds only: tools/build_variant.sh NAME -DEVM_SEG_TARGET=...)
+#define EVM_SEG_TARGET 560
+#endif
+constexpr u32 SEG_TARGET = EVM_SEG_TARGET;  // messages per segment of a cut owner: minute-granular splitters and
+                                            // sampling noise keep nearly all below 1,024 (the fast kernel)
+static_assert(SEG_TARGET >= 64 && SEG_TARGET <= 4096, "segment target");
 constexpr u32 SEG_SPLIT_MIN = 1024; // shares above this are cut (the 1,024 kernel is the fast one)
-// (EVM_SEG_TARGET overrides SEG_TARGET: tuning experiments only)
-static u32 seg_target() {
-  static const u32 t = [] {
-    const char* e = getenv("EVM_SEG_TARGET");
-    const long v = e ? atol(e) : 0;
-    return v >= 64 && v <= 4096 ? (u32)v : SEG_TARGET;
-  }();
-  return t;
-}
+static u32 seg_target() { return SEG_TARGET; }
 constexpr u32 SAMPLE_STRIDE = 16;   // one sampled minute per 16 messages of a cut owner
 constexpr u32 SEG_TABLE_RATIO = 64; // minute -> segment table when the splitters span <= 64 minutes per segment
 
