@@ -1246,6 +1246,17 @@ constexpr u32 SVB_LDS = 1024;
 #define EVM_SVB_BATCH 4
 #endif
 constexpr int SVB_B = EVM_SVB_BATCH;
+// Rows of a segment with <= SVB_SRC output rows (stored + new) are written
+// once, in output order: the searches fill a source map in LDS (output
+// position -> stored row or new row) and a third pass copies each output row
+// from its source, consecutive lanes on consecutive rows.  (Writing stored
+// rows at their places and the new ones into the gaps afterwards touched
+// every output line twice: 16.4 GB written per reingest merge vs ~8.7 GB.)
+#ifndef EVM_SVB_SRC  // (A/B builds: 0 = the two-pass row writes)
+#define EVM_SVB_SRC 1
+#endif
+constexpr u32 SVB_SRC = 4096;
+constexpr uint16_t SVB_NEW = 0x8000;
 
 
 __device__ __forceinline__ void svb_inclusive_prefix(u32* h, u32 m, u32* tmp) {
@@ -1279,6 +1290,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   __shared__ u64 k_tc[LN], k_hi[LN];  // new row keys (then new leaf codes in k_tc)
   __shared__ u32 k_lo[LN];
   __shared__ u32 hist[LN + 1];
+  __shared__ uint16_t src[MERGE && EVM_SVB_SRC ? SVB_SRC : 1];  // output row -> source (SVB_NEW | new j, or stored k - sa)
   const u32 s = blockIdx.x;
   const u32 o = seg_owner(sv, s);
   const u64 a = sv.start[s];
@@ -1289,6 +1301,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   // rows_in_place: an empty store whose every message was inserted -- the
   // K5 rows already sit at their final places (position = batch position)
   const bool lds_rows = MERGE && EVM_SVB_LDS && !rows_in_place && M <= SVB_LDS;
+  const bool by_src = lds_rows && EVM_SVB_SRC && (sb - sa) + M <= SVB_SRC;
   if (lds_rows) {
     for (u32 j = threadIdx.x; j < M; j += SVO_THREADS) {
       k_tc[j] = n_tc[a + j];
@@ -1314,7 +1327,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
         rtc[r] = st.tc[k];
         rhi[r] = st.hi[k];
         rlo[r] = st.lo[k];
-        rid[r] = st_id[k];
+        if (!by_src) rid[r] = st_id[k];
       }
     }
 #pragma unroll
@@ -1339,6 +1352,10 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
           else hi = mid;
         }
       }
+      if (by_src) {
+        src[(k - sa) + lo] = (uint16_t)(k - sa);
+        continue;
+      }
       const u64 w = base + (k - sa) + lo;
       so.owner[w] = o;
       so.tc[w] = key.tc;
@@ -1349,7 +1366,49 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   }
   __syncthreads();
   if (lds_rows) svb_inclusive_prefix(hist, M + 1, tmp);  // hist[j] = stored rows below new row j
-  for (u32 j0 = threadIdx.x; !rows_in_place && j0 < M; j0 += SVB_B * SVO_THREADS) {
+  if (by_src) {
+    for (u32 j = threadIdx.x; j < M; j += SVO_THREADS) src[j + hist[j]] = (uint16_t)(SVB_NEW | j);
+    __syncthreads();
+    const u32 T = (u32)(sb - sa) + M;
+    for (u32 p0 = threadIdx.x; p0 < T; p0 += SVB_B * SVO_THREADS) {
+      u64 vtc[SVB_B], vhi[SVB_B], vid[SVB_B];
+      u32 vlo[SVB_B];
+#pragma unroll
+      for (int r = 0; r < SVB_B; ++r) {
+        const u32 p = p0 + r * SVO_THREADS;
+        vtc[r] = vhi[r] = vid[r] = 0;
+        vlo[r] = 0;
+        if (p < T) {
+          const u32 e = src[p];
+          if (e & SVB_NEW) {
+            const u32 j = e & (SVB_NEW - 1u);
+            vtc[r] = k_tc[j];
+            vhi[r] = k_hi[j];
+            vlo[r] = k_lo[j];
+            vid[r] = n_id[a + j];
+          } else {
+            const u64 k = sa + e;
+            vtc[r] = st.tc[k];
+            vhi[r] = st.hi[k];
+            vlo[r] = st.lo[k];
+            vid[r] = st_id[k];
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < SVB_B; ++r) {
+        const u32 p = p0 + r * SVO_THREADS;
+        if (p >= T) break;
+        const u64 w = base + p;
+        so.owner[w] = o;
+        so.tc[w] = vtc[r];
+        so.hi[w] = vhi[r];
+        so.lo[w] = vlo[r];
+        so.id[w] = vid[r];
+      }
+    }
+  }
+  for (u32 j0 = threadIdx.x; !rows_in_place && !by_src && j0 < M; j0 += SVB_B * SVO_THREADS) {
     u64 nid[SVB_B];
 #pragma unroll
     for (int r = 0; r < SVB_B; ++r) {
