@@ -1255,8 +1255,12 @@ constexpr int SVB_B = EVM_SVB_BATCH;
 #ifndef EVM_SVB_SRC  // (A/B builds: 0 = the two-pass row writes)
 #define EVM_SVB_SRC 1
 #endif
+#ifndef EVM_SVB_SRC_LEAVES  // (A/B builds: 0 = rows through the map, leaves in two passes)
+#define EVM_SVB_SRC_LEAVES 1
+#endif
 constexpr u32 SVB_SRC = 4096;
-constexpr uint16_t SVB_NEW = 0x8000;
+constexpr uint16_t SVB_NEW = 0x8000, SVB_EQ = 0x4000;
+static_assert(SVB_LDS <= SVB_EQ && SVB_SRC <= SVB_NEW, "source map fields");
 
 
 __device__ __forceinline__ void svb_inclusive_prefix(u32* h, u32 m, u32* tmp) {
@@ -1457,6 +1461,12 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   }
   if (threadIdx.x == 0) s_dp[NL] = dtot;
   const bool lds_leaves = MERGE && EVM_SVB_LDS && NL <= SVB_LDS;
+  // leaves written once through the source map too: a tree leaf's entry is
+  // its index, a new leaf's SVB_NEW | j, a tree leaf equal to new leaf j
+  // SVB_NEW | SVB_EQ | j with the combined XOR parked in eqx[j] (k_hi is free)
+  const u64 TL = (lb - la) + NL - dtot;
+  const bool leaves_src = lds_leaves && EVM_SVB_SRC && EVM_SVB_SRC_LEAVES && TL <= SVB_SRC;
+  u32* eqx = reinterpret_cast<u32*>(k_hi);
   __syncthreads();  // (the rows' LDS keys are dead: the leaf codes take k_tc)
   if (lds_leaves) {
     for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) k_tc[j] = l_ck[a + j];
@@ -1489,6 +1499,16 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
         j = lo;
         eq = j < NL && k_tc[j] == code;
         atomicAdd(&hist[j + (eq ? 1u : 0u)], 1u);  // (an equal tree leaf is not below new leaf j)
+        if (leaves_src) {
+          const u32 q = (u32)(k - la) + j - s_dp[j];
+          if (eq) {
+            eqx[j] = (u32)(txr[r] ^ l_xr[a + j]);
+            src[q] = (uint16_t)(SVB_NEW | SVB_EQ | j);
+          } else {
+            src[q] = (uint16_t)(k - la);
+          }
+          continue;
+        }
       } else {
         j = (u32)(lb_u64(l_ck, a, a + NL, code) - a);  // new leaves below this code
         eq = j < NL && l_ck[a + j] == code;
@@ -1500,7 +1520,40 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   }
   __syncthreads();
   if (lds_leaves) svb_inclusive_prefix(hist, NL + 1, tmp);  // hist[j] = tree leaves below new leaf j
-  for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) {
+  if (leaves_src) {
+    for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS)
+      if (!l_dup[a + j]) src[(j - s_dp[j]) + hist[j]] = (uint16_t)(SVB_NEW | j);
+    __syncthreads();
+    for (u32 q0 = threadIdx.x; q0 < (u32)TL; q0 += SVB_B * SVO_THREADS) {
+      u64 vck[SVB_B];
+      int32_t vxr[SVB_B];
+#pragma unroll
+      for (int r = 0; r < SVB_B; ++r) {
+        const u32 q = q0 + r * SVO_THREADS;
+        vck[r] = 0;
+        vxr[r] = 0;
+        if (q < (u32)TL) {
+          const u32 e = src[q];
+          if (e & SVB_NEW) {
+            const u32 j = e & (SVB_EQ - 1u);
+            vck[r] = k_tc[j];
+            vxr[r] = (e & SVB_EQ) ? (int32_t)eqx[j] : l_xr[a + j];
+          } else {
+            vck[r] = t_ck[la + e];
+            vxr[r] = t_xr[la + e];
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < SVB_B; ++r) {
+        const u32 q = q0 + r * SVO_THREADS;
+        if (q >= (u32)TL) break;
+        to_ck[lbase + q] = vck[r];
+        to_xr[lbase + q] = vxr[r];
+      }
+    }
+  }
+  for (u32 j = threadIdx.x; !leaves_src && j < NL; j += SVO_THREADS) {
     if (l_dup[a + j]) continue;
     const u64 code = lds_leaves ? k_tc[j] : l_ck[a + j];
     const u64 below = lds_leaves ? (u64)hist[j] : lb_u64(t_ck, la, lb, code) - la;
@@ -1516,6 +1569,83 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     if (s == NS - 1) {
       so_off[n_owners] = base + (sb - sa) + M;
       to_off[n_owners] = lbase + (lb - la) + NL - dtot;
+    }
+  }
+}
+
+// The empty store's commit (no stored rows, no tree leaves: k_svo_b<false>'s
+// case): each segment's rows -- unless K5 already placed them -- and its new
+// leaves copied to their places, one wave per segment and SVB_B items per lane
+// in flight.  Nothing merges, so none of the merge's block scans and barriers
+// (~100k segments of ~1,000 rows: the merge's per-workgroup fixed work was
+// most of its time).
+#ifndef EVM_SVO_COPY  // (A/B builds: 0 = k_svo_b<false> for the empty store)
+#define EVM_SVO_COPY 1
+#endif
+constexpr int SVC_WAVES = 4;
+__global__ __launch_bounds__(64 * SVC_WAVES) void k_svo_copy(
+    SegView sv, u32 NS, u32 n_owners, const u64* __restrict__ n_tc, const u64* __restrict__ n_hi,
+    const u32* __restrict__ n_lo, const u64* __restrict__ n_id, const u32* __restrict__ cnt_rows,
+    const u32* __restrict__ row_pos, const u64* __restrict__ l_ck, const int32_t* __restrict__ l_xr,
+    const u32* __restrict__ cnt_new, const u32* __restrict__ leaf_pos, StoreOut so, u64* __restrict__ so_off,
+    u64* __restrict__ to_ck, int32_t* __restrict__ to_xr, u64* __restrict__ to_off, int rows_in_place) {
+  const u32 s = blockIdx.x * SVC_WAVES + (threadIdx.x >> 6);
+  if (s >= NS) return;  // (a whole wave: the kernel has no block barrier)
+  const u32 lane = threadIdx.x & 63;
+  const u32 o = seg_owner(sv, s);
+  const u64 a = sv.start[s];
+  const u32 M = cnt_rows[s], NL = cnt_new[s];
+  const u64 base = sv.sa[s] + row_pos[s];
+  const u64 lbase = leaf_pos[s];
+  for (u32 j0 = lane; !rows_in_place && j0 < M; j0 += SVB_B * 64) {
+    u64 vtc[SVB_B], vhi[SVB_B], vid[SVB_B];
+    u32 vlo[SVB_B];
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u32 j = j0 + r * 64;
+      const bool in = j < M;
+      vtc[r] = in ? n_tc[a + j] : 0ull;
+      vhi[r] = in ? n_hi[a + j] : 0ull;
+      vlo[r] = in ? n_lo[a + j] : 0u;
+      vid[r] = in ? n_id[a + j] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u32 j = j0 + r * 64;
+      if (j >= M) break;
+      const u64 w = base + j;
+      so.owner[w] = o;
+      so.tc[w] = vtc[r];
+      so.hi[w] = vhi[r];
+      so.lo[w] = vlo[r];
+      so.id[w] = vid[r];
+    }
+  }
+  for (u32 j0 = lane; j0 < NL; j0 += SVB_B * 64) {
+    u64 vck[SVB_B];
+    int32_t vxr[SVB_B];
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u32 j = j0 + r * 64;
+      vck[r] = j < NL ? l_ck[a + j] : 0ull;
+      vxr[r] = j < NL ? l_xr[a + j] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < SVB_B; ++r) {
+      const u32 j = j0 + r * 64;
+      if (j >= NL) break;
+      to_ck[lbase + j] = vck[r];
+      to_xr[lbase + j] = vxr[r];
+    }
+  }
+  if (lane == 0) {
+    if (s == 0 || seg_owner(sv, s - 1) != o) {  // the owner's first segment starts its rows and leaves
+      so_off[o] = base;
+      to_off[o] = lbase;
+    }
+    if (s == NS - 1) {
+      so_off[n_owners] = base + M;
+      to_off[n_owners] = lbase + NL;
     }
   }
 }
@@ -2550,6 +2680,9 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     KLAUNCH(k_svo_b<true>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s),
                 (const u64*)s->id, n_tc, n_hi, n_lo, n_id, c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup,
                 c_new, pos + NS, so, ns->off, nt->ck, nt->xr, nt->off, in_place);
+  else if (EVM_SVO_COPY && t->n_leaves == 0)
+    KLAUNCH(k_svo_copy, dim3((NS + SVC_WAVES - 1) / SVC_WAVES), dim3(64 * SVC_WAVES), sv, NS, O, n_tc, n_hi, n_lo, n_id,
+            c_rows, pos, l_ck, l_xr, c_new, pos + NS, so, ns->off, nt->ck, nt->xr, nt->off, in_place);
   else
     KLAUNCH(k_svo_b<false>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
           c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + NS, so, ns->off, nt->ck, nt->xr,
