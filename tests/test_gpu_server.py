@@ -401,3 +401,56 @@ def test_big_owner_tie_runs(eng, run):
         assert store.tree().to_json(o) == srv.tree_json(o)
     assert ((got.cpu().numpy() & L.MSG_INS) != 0).sum() == sum(len({s for s, w in zip(strings, owner) if w == o})
                                                          for o in range(3))
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_merge_paths_by_segment_size(eng, seed):
+    """Round 2 into a non-empty store through every merge shape (k_svo_b<true>):
+    a segment whose stored + new rows and leaves fit the LDS source map
+    (<= 4,096: written once in output order), one that exceeds it (stored
+    rows first, new rows into the gaps), small ones, a new owner and an owner
+    with no new rows -- with redeliveries of stored rows (equal tree leaves
+    XOR-combined) -- against the C oracle of addMessages
+    (apps/server/src/index.ts:138-171): flags, stored rows, trees."""
+    from evolu_amd import _lib as L
+    from oracle import c_oracle as CO
+
+    rng = random.Random(7100 + seed)
+    day = 86_400_000
+    # owner: (stored rows, new rows); minutes spread so the leaf lists are long too
+    shape = {0: (3000, 1000), 1: (3600, 600), 2: (200, 100), 3: (0, 50), 4: (100, 0)}
+    r1, r2 = [], []
+    for o, (ns, nn) in shape.items():
+        nodes = [W.node_id(rng, upper=rng.random() < 0.3) for _ in range(4)]
+        old = W.hlc_timestamps(rng, ns, nodes, span=5 * day) if ns else []
+        new = W.hlc_timestamps(rng, nn, [W.node_id(rng) for _ in range(3)], span=5 * day) if nn else []
+        redo = [rng.choice(old) for _ in range(nn // 10)] if old and nn else []
+        r1 += [(s, o) for s in old]
+        r2 += [(s, o) for s in new + redo]
+    rng.shuffle(r1)
+    rng.shuffle(r2)
+    srv = CO.Server(len(shape), len(r1) + len(r2))
+    store = eng.store_new(len(shape))
+    got_all = []
+    for batch, base in ((r1, 0), (r2, 1 << 40)):
+        ts_np = eng.timestamps([s for s, _ in batch]).cpu().numpy()
+        own = np.array([o for _, o in batch], dtype=np.uint32)
+        st, want = srv.ingest(ts_np, own)
+        assert st == 0
+        got, st = store.ingest(eng.dev(ts_np), eng.dev(own), base)
+        assert st == 0
+        got_all.append(got.cpu().numpy())
+        assert np.array_equal(got_all[-1], want)
+    assert (got_all[1] & L.MSG_INS).astype(bool).sum() == sum(nn for _, nn in shape.values())
+    off, ids = store.messages()
+    both = r1 + r2
+    id_of = {}
+    for k, (s, o) in enumerate(r1):
+        id_of.setdefault((s, o), k)
+    for k, (s, o) in enumerate(r2):
+        id_of.setdefault((s, o), (1 << 40) + k)
+    for o in shape:
+        rows = sorted({s for s, w in both if w == o})
+        assert [int(k) for k in ids[off[o]:off[o + 1]]] == [id_of[(s, o)] for s in rows]
+        assert store.tree().to_json(o) == srv.tree_json(o)
+    assert store.n_messages == len(set(both))
