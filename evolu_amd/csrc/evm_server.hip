@@ -688,7 +688,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     const u64* __restrict__ t_ck, u64 id_base, uint8_t* __restrict__ flags,
     u64* __restrict__ n_tc, u64* __restrict__ n_hi, u32* __restrict__ n_lo, u64* __restrict__ n_id,
     u64* __restrict__ l_ck, int32_t* __restrict__ l_xr, uint8_t* __restrict__ l_dup, u32* __restrict__ cnt_rows,
-    u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, SvoStatus* __restrict__ status,
+    u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, u32* __restrict__ cnt_xor, SvoStatus* __restrict__ status,
     const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list, u32* __restrict__ mid1,
     uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner, int flags_preset, u32* __restrict__ mid512,
     WireSrc wsrc) {
@@ -740,6 +740,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       cnt_rows[s] = 0;
       cnt_new[s] = 0;
       cnt_leaves[s] = (u32)(lb - la);
+      cnt_xor[s] = 0;
     }
     return;
   }
@@ -1173,7 +1174,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     // atomic from every workgroup would serialise -- only new bits are written)
     atomic_or_if(&status->lens, (1u << l0) | (1u << l1));
   }
-  u32 dups = 0;
+  u32 dups = 0, lx = 0;
   for (u32 l = threadIdx.x; l < NL; l += THREADS) {
     const u64 code = ((u64)o << 40) | minute_code_from(s_lm[l], [&](u32 x) { return (u32)s_b3[x]; });
     const u64 k = lb_u64(t_ck, la, lb, code);
@@ -1182,13 +1183,23 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     l_xr[a + l] = (int32_t)s_lx[l];
     l_dup[a + l] = dup ? 1 : 0;
     dups += dup ? 1u : 0u;
+    lx ^= s_lx[l];
   }
   u32 dtot;
   block_inclusive_scan<u32>(dups, tmp, OpAdd<u32>(), &dtot);
+  // the XOR of the segment's new leaves (the empty store's copy writes the
+  // tree's prefix XOR from these: no scan over the leaves)
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) lx ^= __shfl_xor(lx, d, 64);
+  if ((threadIdx.x & 63) == 0) tmp[threadIdx.x >> 6] = lx;
+  __syncthreads();
   if (threadIdx.x == 0) {
+    u32 x = 0;
+    for (int w = 0; w < THREADS / 64; ++w) x ^= tmp[w];
     cnt_rows[s] = M;
     cnt_new[s] = NL;
     cnt_leaves[s] = (u32)(lb - la) + NL - dtot;
+    cnt_xor[s] = x;
   }
 }
 
@@ -1224,12 +1235,13 @@ __global__ void k_seg_classes(SegView sv, u32 NS, u32* __restrict__ lists) {
 // segments of an owner sent to the sort path contribute nothing here (its
 // stored rows and leaves are still copied)
 __global__ void k_seg_fix(SegView sv, u32 NS, const uint8_t* __restrict__ ownbig, u32* __restrict__ cnt_rows,
-                          u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves) {
+                          u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, u32* __restrict__ cnt_xor) {
   for (u32 s = blockIdx.x * blockDim.x + threadIdx.x; s < NS; s += gridDim.x * blockDim.x) {
     if (!ownbig[seg_owner(sv, s)]) continue;
     cnt_rows[s] = 0;
     cnt_new[s] = 0;
     cnt_leaves[s] = (u32)(sv.lb[s] - sv.la[s]);
+    cnt_xor[s] = 0;
   }
 }
 
@@ -1588,7 +1600,8 @@ __global__ __launch_bounds__(64 * SVC_WAVES) void k_svo_copy(
     const u32* __restrict__ n_lo, const u64* __restrict__ n_id, const u32* __restrict__ cnt_rows,
     const u32* __restrict__ row_pos, const u64* __restrict__ l_ck, const int32_t* __restrict__ l_xr,
     const u32* __restrict__ cnt_new, const u32* __restrict__ leaf_pos, StoreOut so, u64* __restrict__ so_off,
-    u64* __restrict__ to_ck, int32_t* __restrict__ to_xr, u64* __restrict__ to_off, int rows_in_place) {
+    u64* __restrict__ to_ck, int32_t* __restrict__ to_xr, u64* __restrict__ to_off, int rows_in_place,
+    const int32_t* __restrict__ xpos, int32_t* __restrict__ to_pfx) {
   const u32 s = blockIdx.x * SVC_WAVES + (threadIdx.x >> 6);
   if (s >= NS) return;  // (a whole wave: the kernel has no block barrier)
   const u32 lane = threadIdx.x & 63;
@@ -1621,7 +1634,11 @@ __global__ __launch_bounds__(64 * SVC_WAVES) void k_svo_copy(
       so.id[w] = vid[r];
     }
   }
-  for (u32 j0 = lane; j0 < NL; j0 += SVB_B * 64) {
+  // the tree's exclusive prefix XOR over the copied leaves, carried from the
+  // segments before (xpos: a scan of K5's per-segment XORs)
+  u32 carry = (u32)xpos[s];
+  for (u32 k0 = 0; k0 < NL; k0 += SVB_B * 64) {  // (wave-uniform bounds: every lane takes part in the shuffles)
+    const u32 j0 = k0 + lane;
     u64 vck[SVB_B];
     int32_t vxr[SVB_B];
 #pragma unroll
@@ -1633,11 +1650,21 @@ __global__ __launch_bounds__(64 * SVC_WAVES) void k_svo_copy(
 #pragma unroll
     for (int r = 0; r < SVB_B; ++r) {
       const u32 j = j0 + r * 64;
-      if (j >= NL) break;
-      to_ck[lbase + j] = vck[r];
-      to_xr[lbase + j] = vxr[r];
+      u32 inc = (u32)vxr[r];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(inc, d, 64);
+        if (lane >= (u32)d) inc ^= y;
+      }
+      if (j < NL) {
+        to_ck[lbase + j] = vck[r];
+        to_xr[lbase + j] = vxr[r];
+        to_pfx[lbase + j] = (int32_t)(carry ^ inc ^ (u32)vxr[r]);
+      }
+      carry ^= __shfl(inc, 63, 64);
     }
   }
+  if (lane == 0 && s == NS - 1) to_pfx[lbase + NL] = (int32_t)carry;  // the tree's total
   if (lane == 0) {
     if (s == 0 || seg_owner(sv, s - 1) != o) {  // the owner's first segment starts its rows and leaves
       so_off[o] = base;
@@ -2534,11 +2561,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     sv = SegView{sown, sstart, ssa, ssb, sla, slb};
     kperm = bv;
   }
-  u32* cnt = S.alloc<u32>(3 * (size_t)NS);  // rows, new leaves, merged leaves (per segment)
+  u32* cnt = S.alloc<u32>(4 * (size_t)NS + 1);  // rows, new leaves, merged leaves, new leaves' XOR (per segment)
   u32* pos = S.alloc<u32>(2 * (size_t)NS);  // row / leaf offsets
   u32* mid = S.alloc<u32>((size_t)NS + 1);  // [count, segments whose share is in (1024, SVO_CAP]]
   if (!cnt || !pos || !mid) return EVM_ENOMEM;
-  u32 *c_rows = cnt, *c_new = cnt + NS, *c_leaves = cnt + 2 * (size_t)NS;
+  u32 *c_rows = cnt, *c_new = cnt + NS, *c_leaves = cnt + 2 * (size_t)NS, *c_xor = cnt + 3 * (size_t)NS;
   // an empty store (a new server, config 3): K5 writes its rows straight into
   // the new store's arrays at their batch positions -- if every message is
   // inserted that is the final layout and k_svo_b copies no row
@@ -2579,7 +2606,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   auto pass = [&](u32 cap, dim3 grid, const u32* list, u32* l1, u32* l2, u32* l512) {
 #define SVO_ARGS                                                                                                      \
   rec, tsb, stride, info, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, \
-      l_xr, l_dup, c_rows, c_new, c_leaves, status, orig, list, l2, l1, ownbig, n_owner, preset, l512, wsrc
+      l_xr, l_dup, c_rows, c_new, c_leaves, c_xor, status, orig, list, l2, l1, ownbig, n_owner, preset, l512, wsrc
     // (the one-wave kernels: Zipf-tail owners of <= 128 / <= 256 messages, no cross-wave barriers;
     // source: true = the rows, false = packed records, SRC_WIRE = received records)
 // (the 1,024 kernel with 512 threads, two messages each, measured slower:
@@ -2627,9 +2654,17 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     HIPR(hipStreamSynchronize(ctx->stream));
     if (hmid) pass(SVO_CAP, dim3(hmid), (const u32*)(mid + 1), (u32*)nullptr, (u32*)nullptr, (u32*)nullptr);
   }
-  KLAUNCH(k_seg_fix, dim3(grid_for(NS, 256)), dim3(256), sv, NS, ownbig, c_rows, c_new, c_leaves);
+  KLAUNCH(k_seg_fix, dim3(grid_for(NS, 256)), dim3(256), sv, NS, ownbig, c_rows, c_new, c_leaves, c_xor);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, NS, pos, tot))) return st;
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, NS, pos + NS, tot + 1))) return st;
+  // the empty store's commit copies (k_svo_copy) and writes the prefix XOR itself
+  const bool by_copy = EVM_SVO_COPY && s->n == 0 && t->n_leaves == 0;
+  int32_t* xpos = nullptr;
+  if (by_copy) {
+    xpos = S.alloc<int32_t>((size_t)NS + 1);
+    if (!xpos) return EVM_ENOMEM;
+    if ((st = scan_exclusive<int32_t, OpXor>(ctx, S, (const int32_t*)c_xor, NS, xpos, xpos + NS))) return st;
+  }
   HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipMemcpyAsync(ht, tot, sizeof(ht), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
@@ -2680,9 +2715,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     KLAUNCH(k_svo_b<true>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s),
                 (const u64*)s->id, n_tc, n_hi, n_lo, n_id, c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup,
                 c_new, pos + NS, so, ns->off, nt->ck, nt->xr, nt->off, in_place);
-  else if (EVM_SVO_COPY && t->n_leaves == 0)
+  else if (by_copy && NS == 0)
+    HIPR(hipMemsetAsync(nt->pfx, 0, sizeof(int32_t), ctx->stream));
+  else if (by_copy)
     KLAUNCH(k_svo_copy, dim3((NS + SVC_WAVES - 1) / SVC_WAVES), dim3(64 * SVC_WAVES), sv, NS, O, n_tc, n_hi, n_lo, n_id,
-            c_rows, pos, l_ck, l_xr, c_new, pos + NS, so, ns->off, nt->ck, nt->xr, nt->off, in_place);
+            c_rows, pos, l_ck, l_xr, c_new, pos + NS, so, ns->off, nt->ck, nt->xr, nt->off, in_place, xpos, nt->pfx);
   else
     KLAUNCH(k_svo_b<false>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
           c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + NS, so, ns->off, nt->ck, nt->xr,
@@ -2690,7 +2727,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   // (the prefix XOR inside the merge -- segments by decoupled look-back, each
   // re-reading its own leaves -- measured 1.88 vs 0.79 + 0.39 ms of scans on
   // config 3: the merge's workgroups then wait on each other)
-  if ((st = scan_exclusive<int32_t, OpXor>(ctx, S, nt->xr, ht[1], nt->pfx, nt->pfx + ht[1]))) {
+  if (!by_copy && (st = scan_exclusive<int32_t, OpXor>(ctx, S, nt->xr, ht[1], nt->pfx, nt->pfx + ht[1]))) {
     store_release_arrays(ctx, ns);
     tree_destroy(ctx, nt);
     return st;

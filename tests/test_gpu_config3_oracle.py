@@ -71,7 +71,10 @@ def test_config3_shape_and_reingest_vs_c_oracle(eng):
     store = eng.store_new(O_)
     (f1, st1), rep1 = _ran(eng, lambda: store.ingest(t1, o1, 0))
     assert st1 == 0 and "(k_svo_a<1024, true>)" in rep1, sorted(rep1)
-    assert "k_svo_copy" in rep1, sorted(rep1)  # the empty store's commit
+    assert "k_svo_copy" in rep1, sorted(rep1)  # the empty store's commit (prefix XOR included)
+    from tests.test_gpu_server import _check_prefix_xor
+
+    _check_prefix_xor(eng, store.tree())
     assert np.array_equal(f1.cpu().numpy(), f1_want)
     (f2, st2), rep2 = _ran(eng, lambda: store.ingest(eng.dev(ts2), eng.dev(own2), 1 << 40))
     assert st2 == 0 and "k_svo_b<true>" in rep2, sorted(rep2)

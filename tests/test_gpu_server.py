@@ -403,6 +403,22 @@ def test_big_owner_tie_runs(eng, run):
                                                          for o in range(3))
 
 
+def _check_prefix_xor(eng, tree):
+    """The tree's prefix XOR (written by the empty store's copy kernel, or by
+    the scan after a merge) against its own leaves: every owner's root is
+    the XOR of its leaves, and a diff with the same leaves rebuilt through
+    evm_tree_from_leaves (whose prefix is a scan) finds nothing at any level."""
+    from evolu_amd import _lib as L
+
+    off, code, xr = tree.leaves()
+    px = np.concatenate([[0], np.bitwise_xor.accumulate(xr.astype(np.int32))]).astype(np.int32)
+    o = off.astype(np.int64)
+    r, _ = tree.roots()
+    assert np.array_equal(r, px[o[1:]] ^ px[o[:-1]])
+    same = eng.tree_from_leaves(off, code, xr)
+    assert (eng.merkle_diff(tree, same).cpu().numpy() == L.DIFF_NONE).all()
+
+
 @pytest.mark.parametrize("seed", [0, 1])
 def test_merge_paths_by_segment_size(eng, seed):
     """Round 2 into a non-empty store through every merge shape (k_svo_b<true>):
@@ -441,6 +457,7 @@ def test_merge_paths_by_segment_size(eng, seed):
         assert st == 0
         got_all.append(got.cpu().numpy())
         assert np.array_equal(got_all[-1], want)
+        _check_prefix_xor(eng, store.tree())
     assert (got_all[1] & L.MSG_INS).astype(bool).sum() == sum(nn for _, nn in shape.values())
     off, ids = store.messages()
     both = r1 + r2
