@@ -87,7 +87,7 @@ SERVER_ALG = {
     "k_svo_b": (28 + 32, 8 + 4 + 1 + 8 + 4),  # new rows in, store rows out; new leaves in, tree leaves out
     "k_svo_b<true>": (28 + 32, 8 + 4 + 1 + 8 + 4),  # (the merge into a non-empty store: LDS-staged keys)
     "k_svo_b<false>": (28 + 32, 8 + 4 + 1 + 8 + 4),  # (an empty store, a tree with leaves)
-    "k_svo_copy": (28 + 32, 8 + 4 + 8 + 4),  # (an empty store and tree: rows unless K5 placed them, leaves)
+    "k_svo_copy": (28 + 32, 8 + 4 + 8 + 4 + 4),  # (an empty store and tree: rows unless K5 placed them, leaves + prefix XOR)
     "k_seg_key": (4 + 4 + 8, 0),  # owner + minute in, (segment, index) out
 }
 SERVER_PIPELINE_BYTES = 127  # the ideal server pipeline, one sort pass

@@ -168,6 +168,9 @@ int evm::launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, cons
 // ============================================================================
 // Scans and sorts (host drivers for evm_prims.hpp)
 // ============================================================================
+#ifndef EVM_SCAN_SMALL  // (A/B builds: 0 = small scans in three launches too)
+#define EVM_SCAN_SMALL 1
+#endif
 template <typename T, template <typename> class Op>
 int evm::scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out, T* total_dev) {
   if (n == 0) {
@@ -175,6 +178,16 @@ int evm::scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out,
     return EVM_OK;
   }
   const size_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if constexpr (sizeof(T) == 4) {
+    if (EVM_SCAN_SMALL && nt <= SCAN_LB_TILES && (const void*)in != (const void*)out) {
+      u64* status = S.alloc<u64>(nt + 1);  // look-back words, then the tile counter
+      if (!status) return EVM_ENOMEM;
+      HIPR(hipMemsetAsync(status, 0, (nt + 1) * sizeof(u64), ctx->stream));
+      KLAUNCH((k_scan_small<T, Op<T>>), dim3(nt), dim3(SCAN_THREADS), in, n, out, status, (u32*)(status + nt),
+              total_dev);
+      return hip_ok(hipGetLastError());
+    }
+  }
   T* part = S.alloc<T>(nt);
   if (!part) return EVM_ENOMEM;
   KLAUNCH((k_scan_reduce<T, Op<T>>), dim3(nt), dim3(SCAN_THREADS), in, n, part);
