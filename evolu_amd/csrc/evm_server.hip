@@ -496,7 +496,7 @@ __global__ void k_run_len(const u32* __restrict__ run_start, const u32* __restri
 // whole SyncRequest, the common case -- so K5 reads no perm for it)
 __global__ void k_run_seg(const u32* __restrict__ run_owner_sorted, u32 R, const u32* __restrict__ run_pos, u32 O,
                           u64* __restrict__ seg, Info* __restrict__ info, const u32* __restrict__ run_start,
-                          const u32* __restrict__ order, u32* __restrict__ cbase) {
+                          const u32* __restrict__ order, u32* __restrict__ cbase, u32* __restrict__ multi) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && R && run_owner_sorted[R - 1] >= O) atomicOr(&info->bad_aux, 1u);
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o <= O; o += gridDim.x * blockDim.x) {
     u32 a = 0, b = R;
@@ -507,8 +507,10 @@ __global__ void k_run_seg(const u32* __restrict__ run_owner_sorted, u32 R, const
     }
     seg[o] = run_pos[a];  // run_pos[R] = n
     if (o < O && cbase) {
-      const bool one = a < R && run_owner_sorted[a] == o && (a + 1 == R || run_owner_sorted[a + 1] != o);
+      const bool has = a < R && run_owner_sorted[a] == o;
+      const bool one = has && (a + 1 == R || run_owner_sorted[a + 1] != o);
       cbase[o] = one ? run_start[order[a]] : SEG_NOBASE;
+      if (has && !one) atomic_or_if(multi, 1u);  // an owner of several runs: K5 reads its share through perm
     }
   }
 }
@@ -518,6 +520,9 @@ __global__ void k_run_seg(const u32* __restrict__ run_owner_sorted, u32 R, const
 // fetch one run's (position, start) each, then the wave writes the whole
 // range coalesced, each element finding its run among the RF_RUNS bounds.
 constexpr int RF_RUNS = 8;
+#ifndef EVM_RUN_FILL_ALWAYS  // (A/B builds: 1 = the permutation written for every run-structured batch)
+#define EVM_RUN_FILL_ALWAYS 0
+#endif
 __global__ __launch_bounds__(256) void k_run_fill(const u32* __restrict__ run_pos, const u32* __restrict__ run_start,
                                                   const u32* __restrict__ order, u32 R, u32* __restrict__ perm) {
   const u32 lane = threadIdx.x & 63;
@@ -2434,24 +2439,33 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     KLAUNCH(k_run_len, dim3(grid_for(R, 256)), dim3(256), run_start, rv, R, n, len);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, len, R, run_pos, run_pos + R))) return st;
     u32* cbase = EVM_SVO_CBASE ? S.alloc<u32>(std::max<u32>(O, 1)) : nullptr;
+    u32* multi = S.alloc<u32>(1);
+    if (!multi) return EVM_ENOMEM;
+    HIPR(hipMemsetAsync(multi, 0, sizeof(u32), ctx->stream));
     KLAUNCH(k_run_seg, dim3(grid_for((size_t)O + 1, 256)), dim3(256), rk, R, run_pos, O, seg, info,
-            (const u32*)run_start, (const u32*)rv, cbase);
+            (const u32*)run_start, (const u32*)rv, cbase, multi);
     sv.cbase = cbase;
-    KLAUNCH(k_run_fill, dim3(grid_for(R, 4 * RF_RUNS, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
     // owners above SEG_SPLIT_MIN: key-range segments, splitters from every
     // 16th message of their share
     KLAUNCH(k_seg_plan, dim3(grid_for(O, 256)), dim3(256), seg, O, seg_target(), nb, nsm, nsp);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nb, O, bbase, bbase + O))) return st;
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsm, O, soff, soff + O))) return st;
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsp, O, spoff, spoff + O))) return st;
-    u32 plan[3] = {0, 0, 0};  // segments, samples, splitters
+    u32 plan[4] = {0, 0, 0, 0};  // segments, samples, splitters, an owner of several runs
     HIPR(hipMemcpyAsync(&plan[0], bbase + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipMemcpyAsync(&plan[1], soff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipMemcpyAsync(&plan[2], spoff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipMemcpyAsync(&plan[3], multi, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipStreamSynchronize(ctx->stream));
     if (plan[1] > 0 && (st = minutes())) return st;  // cut owners: the splitters need the minutes
     if ((st = check_info())) return st;
     split = plan[1] > 0 && cuttable();
+    // the batch indices in owner order: read by the cut owners' sampling and
+    // by K5 for owners of several runs; when every owner is one run (one
+    // SyncRequest per owner, config 3) K5 indexes from the run starts and the
+    // 4-B-per-message permutation is not written at all
+    if (!cbase || plan[3] || split || EVM_RUN_FILL_ALWAYS)
+      KLAUNCH(k_run_fill, dim3(grid_for(R, 4 * RF_RUNS, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
     if (split) {
       gmin = hi.minute_min;
       mb = std::max(1, ceil_log2((size_t)(hi.minute_max - gmin) + 1));
