@@ -171,6 +171,39 @@ int evm::launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, cons
 #ifndef EVM_SCAN_SMALL  // (A/B builds: 0 = small scans in three launches too)
 #define EVM_SCAN_SMALL 1
 #endif
+// k columns (k <= SCAN_COLS) of n <= SCAN_LB_TILES tiles in one launch
+template <typename T, template <typename> class Op>
+static int scan_small_cols(evm_ctx* ctx, Scratch& S, int k, const T* const* ins, size_t n, T* const* outs,
+                           T* const* tots) {
+  const size_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+  u64* status = S.alloc<u64>((size_t)k * (nt + 1));  // per column: look-back words, then the tile counter
+  if (!status) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(status, 0, (size_t)k * (nt + 1) * sizeof(u64), ctx->stream));
+  ScanCols<T> cols{};
+  for (int c = 0; c < k; ++c) {
+    cols.in[c] = ins[c];
+    cols.out[c] = outs[c];
+    cols.total[c] = tots[c];
+  }
+  KLAUNCH((k_scan_small<T, Op<T>>), dim3((unsigned)nt, (unsigned)k), dim3(SCAN_THREADS), cols, n, status);
+  return hip_ok(hipGetLastError());
+}
+
+// Several exclusive add-scans of one length (per-owner / per-segment counts):
+// one launch when they are small, else one scan after the other.
+int evm::scan_exclusive_cols(evm_ctx* ctx, Scratch& S, int k, const u32* const* ins, size_t n, u32* const* outs,
+                             u32* const* tots) {
+  const size_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+  bool ok = EVM_SCAN_SMALL && n > 0 && nt <= SCAN_LB_TILES && k <= SCAN_COLS;
+  for (int c = 0; c < k && ok; ++c) ok = (const void*)ins[c] != (const void*)outs[c];
+  if (ok) return scan_small_cols<u32, OpAdd>(ctx, S, k, ins, n, outs, tots);
+  for (int c = 0; c < k; ++c) {
+    const int st = scan_exclusive<u32, OpAdd>(ctx, S, ins[c], n, outs[c], tots[c]);
+    if (st) return st;
+  }
+  return EVM_OK;
+}
+
 template <typename T, template <typename> class Op>
 int evm::scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out, T* total_dev) {
   if (n == 0) {
@@ -180,12 +213,10 @@ int evm::scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out,
   const size_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
   if constexpr (sizeof(T) == 4) {
     if (EVM_SCAN_SMALL && nt <= SCAN_LB_TILES && (const void*)in != (const void*)out) {
-      u64* status = S.alloc<u64>(nt + 1);  // look-back words, then the tile counter
-      if (!status) return EVM_ENOMEM;
-      HIPR(hipMemsetAsync(status, 0, (nt + 1) * sizeof(u64), ctx->stream));
-      KLAUNCH((k_scan_small<T, Op<T>>), dim3(nt), dim3(SCAN_THREADS), in, n, out, status, (u32*)(status + nt),
-              total_dev);
-      return hip_ok(hipGetLastError());
+      const T* ins[1] = {in};
+      T* outs[1] = {out};
+      T* tots[1] = {total_dev};
+      return scan_small_cols<T, Op>(ctx, S, 1, ins, n, outs, tots);
     }
   }
   T* part = S.alloc<T>(nt);

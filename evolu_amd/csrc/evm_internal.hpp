@@ -300,6 +300,9 @@ int launch_minutes(evm_ctx* ctx, const char* ts, size_t n, const u32* aux, u32 a
                    u32* minute_out);
 template <typename T, template <typename> class Op>
 int scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out, T* total_dev);
+// k <= 3 exclusive add-scans of one length n (one launch when n is small)
+int scan_exclusive_cols(evm_ctx* ctx, Scratch& S, int k, const uint32_t* const* ins, size_t n, uint32_t* const* outs,
+                        uint32_t* const* tots);
 template <typename K>
 int radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t n, int lo_bit, int hi_bit);
 int reduce_runs(evm_ctx* ctx, Scratch& S, const u64* ck, const int32_t* h, size_t m, u64* out_ck, int32_t* out_xr,

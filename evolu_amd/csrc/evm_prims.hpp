@@ -311,11 +311,24 @@ struct Lb32 {  // the look-back's fold of 32-bit values held in the status words
   __device__ static u64 id() { return (u64)(u32)Op::id(); }
   __device__ u64 operator()(u64 a, u64 b) const { return (u64)(u32)Op()((T)(u32)a, (T)(u32)b); }
 };
+// Up to SCAN_COLS scans of one length in one launch (blockIdx.y = the
+// column; column c's look-back words and counter at status + c * (nt + 1)).
+constexpr int SCAN_COLS = 3;
+template <typename T>
+struct ScanCols {
+  const T* in[SCAN_COLS];
+  T* out[SCAN_COLS];
+  T* total[SCAN_COLS];
+};
 template <typename T, typename Op>
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan_small(const T* __restrict__ in, size_t n, T* __restrict__ out,
-                                                             u64* __restrict__ status, u32* __restrict__ ticket,
-                                                             T* __restrict__ total_out) {
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_small(ScanCols<T> cols, size_t n, u64* __restrict__ status_all) {
   static_assert(sizeof(T) == 4, "32-bit scan values");
+  const u32 col = blockIdx.y;
+  const T* __restrict__ in = cols.in[col];
+  T* __restrict__ out = cols.out[col];
+  T* __restrict__ total_out = cols.total[col];
+  u64* __restrict__ status = status_all + (size_t)col * (gridDim.x + 1);
+  u32* __restrict__ ticket = reinterpret_cast<u32*>(status + gridDim.x);
   __shared__ T tile_lds[SCAN_TILE + SCAN_TILE / 32];
   __shared__ T lds[SCAN_THREADS / 64 + 1];
   __shared__ T ex[SCAN_THREADS];

@@ -2448,9 +2448,12 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     // owners above SEG_SPLIT_MIN: key-range segments, splitters from every
     // 16th message of their share
     KLAUNCH(k_seg_plan, dim3(grid_for(O, 256)), dim3(256), seg, O, seg_target(), nb, nsm, nsp);
-    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nb, O, bbase, bbase + O))) return st;
-    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsm, O, soff, soff + O))) return st;
-    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsp, O, spoff, spoff + O))) return st;
+    {
+      const u32* ins[3] = {nb, nsm, nsp};
+      u32* outs[3] = {bbase, soff, spoff};
+      u32* tots[3] = {bbase + O, soff + O, spoff + O};
+      if ((st = scan_exclusive_cols(ctx, S, 3, ins, O, outs, tots))) return st;
+    }
     u32 plan[4] = {0, 0, 0, 0};  // segments, samples, splitters, an owner of several runs
     HIPR(hipMemcpyAsync(&plan[0], bbase + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipMemcpyAsync(&plan[1], soff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
@@ -2521,8 +2524,12 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if ((st = radix_sort_pairs<u64>(ctx, S, skey, sval, nq, 0, mb + obits))) return st;
     KLAUNCH(k_seg_soff, dim3(grid_for((size_t)O + 1, 256)), dim3(256), skey, nq, O, mb, soff);
     KLAUNCH(k_seg_plan_est, dim3(grid_for(O, 256)), dim3(256), soff, O, mb > 0 ? 1 : 0, seg_target(), nb, nsp);
-    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nb, O, bbase, bbase + O))) return st;
-    if ((st = scan_exclusive<u32, OpAdd>(ctx, S, nsp, O, spoff, spoff + O))) return st;
+    {
+      const u32* ins[2] = {nb, nsp};
+      u32* outs[2] = {bbase, spoff};
+      u32* tots[2] = {bbase + O, spoff + O};
+      if ((st = scan_exclusive_cols(ctx, S, 2, ins, O, outs, tots))) return st;
+    }
     u32 plan[2] = {0, 0};
     HIPR(hipMemcpyAsync(&plan[0], bbase + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
     HIPR(hipMemcpyAsync(&plan[1], spoff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
@@ -2669,8 +2676,12 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if (hmid) pass(SVO_CAP, dim3(hmid), (const u32*)(mid + 1), (u32*)nullptr, (u32*)nullptr, (u32*)nullptr);
   }
   KLAUNCH(k_seg_fix, dim3(grid_for(NS, 256)), dim3(256), sv, NS, ownbig, c_rows, c_new, c_leaves, c_xor);
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_rows, NS, pos, tot))) return st;
-  if ((st = scan_exclusive<u32, OpAdd>(ctx, S, c_leaves, NS, pos + NS, tot + 1))) return st;
+  {
+    const u32* ins[2] = {c_rows, c_leaves};
+    u32* outs[2] = {pos, pos + NS};
+    u32* tots[2] = {tot, tot + 1};
+    if ((st = scan_exclusive_cols(ctx, S, 2, ins, NS, outs, tots))) return st;
+  }
   // the empty store's commit copies (k_svo_copy) and writes the prefix XOR itself
   const bool by_copy = EVM_SVO_COPY && s->n == 0 && t->n_leaves == 0;
   int32_t* xpos = nullptr;
