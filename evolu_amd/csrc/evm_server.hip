@@ -616,6 +616,9 @@ constexpr u32 SVO_CAP = 4096;  // largest share of one owner handled in LDS
 constexpr int SVO_TIE_MAX = 32;  // longest run of one (millis, counter) with distinct nodes
 constexpr u32 SVO_BUCKET_MAX = 16;  // counting-sort bucket size finished by insertion sort
 constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while <= 16 x its new rows
+#ifndef EVM_K5_LEAF_LDS  // (A/B builds: 1 = the new leaves' tree searches in LDS)
+#define EVM_K5_LEAF_LDS 0
+#endif
 #ifndef EVM_SVO_SB  // (A/B builds only: stored rows per thread whose loads are issued together)
 #define EVM_SVO_SB 4
 #endif
@@ -1180,10 +1183,39 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     atomic_or_if(&status->lens, (1u << l0) | (1u << l1));
   }
   u32 dups = 0, lx = 0;
+#if EVM_K5_LEAF_LDS
+  // (A/B builds: the segment's tree codes staged in the dead rank / hash
+  // arrays, so the new leaves' searches stay in LDS)
+  const u64 tl = lb - la;
+  const bool leaf_lds = tl <= CAP;
+  if (leaf_lds)
+    for (u32 i = threadIdx.x; i < (u32)tl; i += THREADS) {
+      const u64 c = t_ck[la + i];
+      s_rl[i] = (u32)(c >> 32);
+      s_h[i] = (u32)c;
+    }
+  __syncthreads();
+#endif
   for (u32 l = threadIdx.x; l < NL; l += THREADS) {
     const u64 code = ((u64)o << 40) | minute_code_from(s_lm[l], [&](u32 x) { return (u32)s_b3[x]; });
-    const u64 k = lb_u64(t_ck, la, lb, code);
-    const bool dup = k < lb && t_ck[k] == code;
+    u64 k;
+    bool dup;
+#if EVM_K5_LEAF_LDS
+    if (leaf_lds) {
+      u32 lo = 0, hi = (u32)tl;
+      while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if ((((u64)s_rl[mid] << 32) | s_h[mid]) < code) lo = mid + 1;
+        else hi = mid;
+      }
+      k = la + lo;
+      dup = lo < (u32)tl && (((u64)s_rl[lo] << 32) | s_h[lo]) == code;
+    } else
+#endif
+    {
+      k = lb_u64(t_ck, la, lb, code);
+      dup = k < lb && t_ck[k] == code;
+    }
     l_ck[a + l] = code;
     l_xr[a + l] = (int32_t)s_lx[l];
     l_dup[a + l] = dup ? 1 : 0;
