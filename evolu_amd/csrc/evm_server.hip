@@ -619,6 +619,10 @@ constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while 
 #ifndef EVM_K5_LEAF_LDS  // (A/B builds: 1 = the new leaves' tree searches in LDS)
 #define EVM_K5_LEAF_LDS 0
 #endif
+// (measured: reingest K5 4.00 -> 3.26-3.30 ms, but the empty store's K5
+// 2.60 -> 2.72 ms: the LDS search takes 81 VGPRs, five waves per SIMD
+// instead of six; forcing six spills 28 B per lane -- off until a register
+// is shaved elsewhere in K5)
 #ifndef EVM_SVO_SB  // (A/B builds only: stored rows per thread whose loads are issued together)
 #define EVM_SVO_SB 4
 #endif
