@@ -80,6 +80,9 @@ SERVER_ALG = {
     "(k_svo_a<512, true>)": (4 + 46 + 1 + 28, 8 + 4 + 1),
     "(k_svo_a<512, false>)": (4 + 32 + 1 + 28, 8 + 4 + 1),
     # the same over a route's received 24-B records, read where they arrived (evm_dist_ingest)
+    # (into a store that has a tree: the new leaves' searches over the tree codes in LDS)
+    "(k_svo_a<1024, true, SVO_THREADS, true>)": (4 + 46 + 1 + 28, 8 + 4 + 1),
+    "(k_svo_a<1024, false, SVO_THREADS, true>)": (4 + 32 + 1 + 28, 8 + 4 + 1),
     "(k_svo_a<1024, SRC_WIRE>)": (4 + 24 + 1 + 28, 8 + 4 + 1),
     "(k_svo_a<512, SRC_WIRE>)": (4 + 24 + 1 + 28, 8 + 4 + 1),
     "k_wire_pack<false>": (24 + 4 + 4, 0),  # wire record + owner in, minute out (segment keys)

@@ -616,13 +616,13 @@ constexpr u32 SVO_CAP = 4096;  // largest share of one owner handled in LDS
 constexpr int SVO_TIE_MAX = 32;  // longest run of one (millis, counter) with distinct nodes
 constexpr u32 SVO_BUCKET_MAX = 16;  // counting-sort bucket size finished by insertion sort
 constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while <= 16 x its new rows
-#ifndef EVM_K5_LEAF_LDS  // (A/B builds: 1 = the new leaves' tree searches in LDS)
-#define EVM_K5_LEAF_LDS 0
+#ifndef EVM_K5_LEAF_LDS  // (A/B builds: 0 = the new leaves' tree searches in global memory always)
+#define EVM_K5_LEAF_LDS 1
 #endif
-// (measured: reingest K5 4.00 -> 3.26-3.30 ms, but the empty store's K5
-// 2.60 -> 2.72 ms: the LDS search takes 81 VGPRs, five waves per SIMD
-// instead of six; forcing six spills 28 B per lane -- off until a register
-// is shaved elsewhere in K5)
+// (measured: reingest K5 4.00 -> 3.26-3.30 ms, but the LDS search takes 81
+// VGPRs -- five waves per SIMD instead of six, the empty store's K5 2.60 ->
+// 2.72 ms; forcing six spills 28 B per lane.  So the 1,024 class takes the
+// LDS search only into a store that has a tree: K5 is instantiated both ways)
 #ifndef EVM_SVO_SB  // (A/B builds only: stored rows per thread whose loads are issued together)
 #define EVM_SVO_SB 4
 #endif
@@ -693,7 +693,7 @@ enum { SRC_REC = 0, SRC_ROWS = 1, SRC_WIRE = 2 };
 // (compiled for six waves per SIMD instead of the five its registers allow
 // -- the LDS fits six 1,024-capacity workgroups per CU -- it ran no faster:
 // config 3 2.60 vs 2.58 ms, config 4 3.31 vs 3.24)
-template <u32 CAP, int SRC, int THREADS = SVO_THREADS>
+template <u32 CAP, int SRC, int THREADS = SVO_THREADS, bool LEAF = false>
 __global__ __launch_bounds__(THREADS) void k_svo_a(
     const evm_rec* __restrict__ rec, const uint8_t* __restrict__ ts, size_t stride, Info* __restrict__ info,
     const u32* __restrict__ perm, SegView sv, StoreView st,
@@ -1187,24 +1187,23 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     atomic_or_if(&status->lens, (1u << l0) | (1u << l1));
   }
   u32 dups = 0, lx = 0;
-#if EVM_K5_LEAF_LDS
-  // (A/B builds: the segment's tree codes staged in the dead rank / hash
-  // arrays, so the new leaves' searches stay in LDS)
+  // LEAF (a store with a tree): the segment's tree codes staged in the dead
+  // rank / hash arrays, so the new leaves' searches stay in LDS
   const u64 tl = lb - la;
-  const bool leaf_lds = tl <= CAP;
-  if (leaf_lds)
-    for (u32 i = threadIdx.x; i < (u32)tl; i += THREADS) {
-      const u64 c = t_ck[la + i];
-      s_rl[i] = (u32)(c >> 32);
-      s_h[i] = (u32)c;
-    }
-  __syncthreads();
-#endif
+  const bool leaf_lds = LEAF && tl <= CAP;
+  if constexpr (LEAF) {
+    if (leaf_lds)
+      for (u32 i = threadIdx.x; i < (u32)tl; i += THREADS) {
+        const u64 c = t_ck[la + i];
+        s_rl[i] = (u32)(c >> 32);
+        s_h[i] = (u32)c;
+      }
+    __syncthreads();
+  }
   for (u32 l = threadIdx.x; l < NL; l += THREADS) {
     const u64 code = ((u64)o << 40) | minute_code_from(s_lm[l], [&](u32 x) { return (u32)s_b3[x]; });
     u64 k;
     bool dup;
-#if EVM_K5_LEAF_LDS
     if (leaf_lds) {
       u32 lo = 0, hi = (u32)tl;
       while (lo < hi) {
@@ -1214,9 +1213,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       }
       k = la + lo;
       dup = lo < (u32)tl && (((u64)s_rl[lo] << 32) | s_h[lo]) == code;
-    } else
-#endif
-    {
+    } else {
       k = lb_u64(t_ck, la, lb, code);
       dup = k < lb && t_ck[k] == code;
     }
@@ -2660,6 +2657,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   // per-workgroup fixed work, twice the occupancy); larger shares are listed
   // for the 1,024 and SVO_CAP passes
   const bool small = NS && n / NS < 400;
+  const bool leaf = EVM_K5_LEAF_LDS && t->n_leaves > 0;
   auto pass = [&](u32 cap, dim3 grid, const u32* list, u32* l1, u32* l2, u32* l512) {
 #define SVO_ARGS                                                                                                      \
   rec, tsb, stride, info, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, \
@@ -2668,7 +2666,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     // source: true = the rows, false = packed records, SRC_WIRE = received records)
 // (the 1,024 kernel with 512 threads, two messages each, measured slower:
 // config 3 2.80 vs 2.59 ms, config-5 shape 4.87 vs 4.04)
-#define K5_1024(SRCV) KLAUNCH((k_svo_a<1024, SRCV>), grid, dim3(SVO_THREADS), SVO_ARGS)
+#define K5_1024(SRCV)                                                                             \
+  do {                                                                                              \
+    if (leaf) KLAUNCH((k_svo_a<1024, SRCV, SVO_THREADS, true>), grid, dim3(SVO_THREADS), SVO_ARGS); \
+    else KLAUNCH((k_svo_a<1024, SRCV>), grid, dim3(SVO_THREADS), SVO_ARGS);                          \
+  } while (0)
 #define SVO_PASS(SRCV)                                                                         \
   if (cap == 128) KLAUNCH((k_svo_a<128, SRCV, 64>), grid, dim3(64), SVO_ARGS);                  \
   else if (cap == 256) KLAUNCH((k_svo_a<256, SRCV, 64>), grid, dim3(64), SVO_ARGS);             \

@@ -78,6 +78,7 @@ def test_config3_shape_and_reingest_vs_c_oracle(eng):
     assert np.array_equal(f1.cpu().numpy(), f1_want)
     (f2, st2), rep2 = _ran(eng, lambda: store.ingest(eng.dev(ts2), eng.dev(own2), 1 << 40))
     assert st2 == 0 and "k_svo_b<true>" in rep2, sorted(rep2)
+    assert "(k_svo_a<1024, true, SVO_THREADS, true>)" in rep2, sorted(rep2)  # tree searches in LDS
     f2 = f2.cpu().numpy()
     assert np.array_equal(f2, f2_want)
     assert (f2 & L.MSG_INS).astype(bool).sum() == O_ * 900  # every redelivery ignored
