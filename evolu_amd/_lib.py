@@ -21,6 +21,7 @@ EVM_EDEVICE = 6
 EVM_ENOMEM = 7
 EVM_ECAPACITY = 8
 EVM_EDIST = 9
+EVM_ESTATE = 10
 DIST_ID_BYTES = 128
 
 META_CASEMASK = 0x0000FFFF

@@ -26,12 +26,33 @@ SYNTH_SOURCES = ["evm_synth.hip"]
 
 
 def _build(lib, sources, headers, extra, force, verbose):
+    """Each source compiled to its own object in parallel (the two large
+    kernel files dominate), then one link."""
+    from concurrent.futures import ThreadPoolExecutor
+
     srcs = [os.path.join(CSRC, s) for s in sources]
     deps = srcs + [os.path.join(CSRC, h) for h in headers] + [os.path.join(INCLUDE, "evm.h")]
     if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _newest(deps):
         return lib
-    cmd = [HIPCC, "-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function", "-I" + INCLUDE] + srcs + extra + ["-o", lib + ".tmp"]
+    odir = os.path.join(HERE, "build", os.path.basename(lib))
+    os.makedirs(odir, exist_ok=True)
+    base = [HIPCC, "-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+            "-I" + INCLUDE]
+    hdr_time = _newest([os.path.join(CSRC, h) for h in headers] + [os.path.join(INCLUDE, "evm.h")])
+
+    def obj(src):
+        o = os.path.join(odir, os.path.basename(src) + ".o")
+        if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr_time):
+            cmd = base + ["-c", src, "-o", o + ".tmp"]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+            os.replace(o + ".tmp", o)
+        return o
+
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(obj, srcs))
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-fPIC", "-shared"] + objs + extra + ["-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

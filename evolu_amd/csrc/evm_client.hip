@@ -1045,10 +1045,7 @@ __device__ __forceinline__ void tpc_unpack(u64 v, const u64* __restrict__ far, c
 }
 __device__ __forceinline__ u32 minute_of_tc(u64 tc) { return (u32)((tc >> 16) / 60000ull); }
 constexpr int TP_THREADS = 256;
-#ifndef EVM_TP_RANGES  // (A/B builds only: tools/build_variant.sh NAME -DEVM_TP_RANGES=...)
-#define EVM_TP_RANGES 2048
-#endif
-constexpr int TP_RANGES = EVM_TP_RANGES;  // ~8 ranges per CU: TP1's occupancy
+constexpr int TP_RANGES = 2048;  // ~8 ranges per CU: TP1's occupancy
 constexpr u32 ROW_NONE = 0xffffffffu;   // no max (SQL NULL: below every timestamp)
 constexpr u32 ROW_PRIOR = 0xfffffffeu;  // the max is the caller's prior row of the cell
 constexpr u32 TP_MATCH_MAX = 512;       // TP1 rescan: rows tied at a cell's range max
@@ -1132,9 +1129,7 @@ __device__ __forceinline__ TK shfl_tk(const TK& k, int src) {
 // A row outside that (far) or a second row at a max tc (ds_max returns the key
 // it replaced: equal tc bits) marks its cell; marked cells are resolved by a
 // rescan of the range (true max tc, then the node ranks of the rows at it).
-#ifndef TP_WPE
-#define TP_WPE 8  // waves per SIMD TP1 is compiled for (7: no spills, measured no faster)
-#endif
+constexpr int TP_WPE = 8;  // waves per SIMD TP1 is compiled for (7: no spills, measured no faster)
 
 constexpr u32 TP_ROWS_MAX = 8192;  // rows per range (the key's 13-bit row offset)
 
@@ -1212,18 +1207,7 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
       w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
       w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w & 0xffffu;
     }
-#if EVM_ABL_TP == 1  // (ablation builds only: no parse at all)
-    Parsed p{};
-    p.tc = (((u64)w[1] << 32) | w[0]) & 0x00007fffffffffffull;
-    p.hash = w[2];
-    p.minute = w[3] & 0xffffu;
-    p.meta = EVM_META_VALID;
-#else
     Parsed p = parse_ts46(w);  // (the node ranks it can compute are dead here)
-#endif
-#if EVM_ABL_TP == 2  // (ablation: no murmur3)
-    p.hash = w[5];
-#endif
     const bool valid = (p.meta & EVM_META_VALID) != 0;
     if (i < end) {
       const u32 ci = __builtin_nontemporal_load(cell + i);
@@ -1236,12 +1220,7 @@ __global__ __launch_bounds__(TP_THREADS) __attribute__((amdgpu_waves_per_eu(TP_W
         const u64 ms = p.tc >> 16;
         const u32 ctr = (u32)p.tc & 0xffffu;
         bool mark = true;  // far
-#if EVM_ABL_TP == 3  // (ablation: no per-range LDS max)
-        mark = false;
-        if (false) {
-#else
         if (ms < TP_MS_FAST && ctr < 256u) {
-#endif
           const u64 key = (ms << 21) | ((u64)ctr << 13) | (u64)(TP_ROWS_MAX - 1u - (u32)(i - beg));
           mark = (atomicMax(&cmax[ci], key) >> 13) == (key >> 13);  // a second row at this tc (or tc 0)
         }
@@ -1942,9 +1921,8 @@ __global__ __launch_bounds__(FR_THREADS) void k_xf_blocks(u32* __restrict__ dx, 
 // An enqueued streaming batch (evm_apply_batch_async): the call's arguments
 // (the caller keeps them valid until evm_apply_wait), the pinned landing slot
 // of its status record, the event after its last kernel, and its outputs.
-#ifndef EVM_INFO_KERNEL  // (A/B builds: 0 = the runtime's copy lands the async status record)
-#define EVM_INFO_KERNEL 1  // (config 2: 0.2938 / 0.2989 vs 0.2971 / 0.3027 ms per step, two pairs)
-#endif
+// (the status record lands by a kernel, k_info_land, not the runtime's copy:
+// config 2 0.2938 / 0.2989 vs 0.2971 / 0.3027 ms per step, two pairs)
 __global__ void k_info_land(const Info* __restrict__ info, Info* host) {
   static_assert(sizeof(Info) % 4 == 0, "word copy");
   const u32* src = reinterpret_cast<const u32*>(info);
@@ -2272,14 +2250,10 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       HIPR(hipEventRecord(ctx->ev_join, ctx->stream));
       HIPR(hipStreamWaitEvent(xs, ctx->ev_join, 0));
     }
-#if EVM_INFO_KERNEL
     // (one workgroup writes the record into the pinned slot itself: the
     // runtime's copy of 64 bytes to the host was an 18-us blit per batch)
     hipLaunchKernelGGL(k_info_land, dim3(1), dim3(64), 0, xs, (const Info*)info, pend->hinfo);
     HIPR(hipGetLastError());
-#else
-    HIPR(hipMemcpyAsync(pend->hinfo, info, sizeof(Info), hipMemcpyDeviceToHost, xs));
-#endif
     HIPR(hipEventRecord(pend->ev, xs));
     side.detach();
     pend->spec = spec;
@@ -2349,7 +2323,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
 // five kernels and ONE status read:
 //   K1 k_sm_pack    parse + canonical check + murmur3 (rec), rows per cell,
 //                   the cross-cell PK set (raw-byte compare), minute bounds
-//   K2 k_sm_scan    one workgroup: cell offsets (exclusive scan of the counts)
+//   K2 k_sm_scan_lb cell offsets (exclusive scan of the counts, look-back)
 //   K3 k_sm_scatter rows -> their cell's slots (unordered within the cell)
 //   K4 k_sm_lww     a thread per cell: its rows in batch order (repeated
 //                   selection, <= SM_SEG of them; longer cells: a workgroup
@@ -2430,15 +2404,9 @@ __global__ __launch_bounds__(256) void k_sm_pack(const uint8_t* __restrict__ ts,
 }
 
 // cell offsets: off[c] = rows of cells < c (off[C] = all), and cnt[c] = off[c]
-// (K3's cursors).  One workgroup, tiles of 16,384 counts: 16 consecutive per
-// thread (four 16-B loads), a block scan, the running total carried.
+// (K3's cursors): 16 consecutive counts per thread (four 16-B loads).
 constexpr u32 SM_SCAN_ITEMS = 16;
-#ifndef EVM_SM_SCAN_LB  // (A/B builds: 0 = the one-workgroup cell-offset scan)
-#define EVM_SM_SCAN_LB 1
-#endif
-// One workgroup, tiles of SM_FOLD_THREADS x 16 counts; the next tile's loads
-// are issued before this tile is scanned (a 100k-message batch has ~55k cells:
-// four tiles, one load latency instead of four).
+// (loads of 16 counts from a tile: 16-B loads where the tile is whole)
 __device__ __forceinline__ void sm_scan_load(const u32* cnt, u32 C, u32 a, u32 (&v)[SM_SCAN_ITEMS]) {
   if (a + SM_SCAN_ITEMS <= C) {  // (cnt is 256-B aligned scratch: a is a multiple of 16)
     const uint4* p = reinterpret_cast<const uint4*>(cnt + a);
@@ -2455,56 +2423,11 @@ __device__ __forceinline__ void sm_scan_load(const u32* cnt, u32 C, u32 a, u32 (
     for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) v[q] = a + q < C ? cnt[a + q] : 0u;
   }
 }
-__global__ __launch_bounds__(SM_FOLD_THREADS) void k_sm_scan(u32* __restrict__ cnt, u32 C, u32* __restrict__ off) {
-  __shared__ u32 lds[SM_FOLD_THREADS / 64 + 1];
-  constexpr u32 TILE = SM_FOLD_THREADS * SM_SCAN_ITEMS;
-  u32 carry = 0;
-  u32 nv[SM_SCAN_ITEMS];
-  sm_scan_load(cnt, C, threadIdx.x * SM_SCAN_ITEMS, nv);
-  for (u32 base = 0; base < C; base += TILE) {
-    const u32 a = base + threadIdx.x * SM_SCAN_ITEMS;
-    u32 v[SM_SCAN_ITEMS];
-#pragma unroll
-    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) v[q] = nv[q];
-    if (base + TILE < C) sm_scan_load(cnt, C, a + TILE, nv);  // (in flight during this tile's scan)
-    u32 sum = 0;
-#pragma unroll
-    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) sum += v[q];
-    u32 tot;
-    u32 run = carry + block_inclusive_scan<u32, OpAdd<u32>>(sum, lds, OpAdd<u32>(), &tot) - sum;
-    u32 x[SM_SCAN_ITEMS];
-#pragma unroll
-    for (u32 q = 0; q < SM_SCAN_ITEMS; ++q) {
-      x[q] = run;
-      run += v[q];
-    }
-    if (a + SM_SCAN_ITEMS <= C) {  // 16-B stores (off is 256-B aligned scratch too)
-      uint4* po = reinterpret_cast<uint4*>(off + a);
-      uint4* pc = reinterpret_cast<uint4*>(cnt + a);
-#pragma unroll
-      for (u32 q = 0; q < SM_SCAN_ITEMS / 4; ++q) {
-        const uint4 y = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-        po[q] = y;
-        pc[q] = y;
-      }
-    } else {
-#pragma unroll
-      for (u32 q = 0; q < SM_SCAN_ITEMS; ++q)
-        if (a + q < C) {
-          off[a + q] = x[q];
-          cnt[a + q] = x[q];
-        }
-    }
-    carry += tot;
-  }
-  if (threadIdx.x == 0) off[C] = carry;
-}
-
-// The same over several workgroups (one tile of SM_FOLD_THREADS x 16 counts
-// each, tiles in launch order from a counter): each tile's offsets after the
-// counts of every tile before it, by decoupled look-back (status words and
-// the counter zeroed with the batch's other scratch).  A 100k-message batch
-// of ~55k cells: four tiles side by side instead of one after another.
+// Several workgroups (one tile of SM_FOLD_THREADS x 16 counts each, tiles in
+// launch order from a counter): each tile's offsets after the counts of every
+// tile before it, by decoupled look-back (status words and the counter zeroed
+// with the batch's other scratch).  A 100k-message batch of ~55k cells: four
+// tiles side by side (the one-workgroup scan it replaced: 23.4 vs 10.2 us).
 constexpr u32 SM_SCAN_TILE = SM_FOLD_THREADS * SM_SCAN_ITEMS;
 __global__ __launch_bounds__(SM_FOLD_THREADS) void k_sm_scan_lb(u32* __restrict__ cnt, u32 C, u32* __restrict__ off,
                                                                 u64* __restrict__ status, u32* __restrict__ ctr,
@@ -2952,7 +2875,7 @@ static int apply_small(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tre
   const size_t a_bins = (size_t)SM_BINS * 4, a_pres = (size_t)SM_BINS / 8;
   const u32 n_scan_tiles = (u32)std::max<size_t>(1, (C + SM_SCAN_TILE - 1) / SM_SCAN_TILE);
   const size_t a_scan = ((size_t)n_scan_tiles * 8 + 16 + 255) & ~(size_t)255;  // look-back words, counter, error
-  const size_t zero_bytes = a_cnt + a_bins + a_pres + (sizeof(u64) << lg) + (EVM_SM_SCAN_LB ? a_scan : 0);
+  const size_t zero_bytes = a_cnt + a_bins + a_pres + (sizeof(u64) << lg) + a_scan;
   char* z = S.alloc<char>(zero_bytes);
   evm_rec* rec = S.alloc<evm_rec>(n);
   u32* off = S.alloc<u32>(C + 1);
@@ -2974,15 +2897,13 @@ static int apply_small(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tre
   HIPR(hipMemsetAsync(z, 0, zero_bytes, ctx->stream));
   KLAUNCH(k_sm_pack, dim3(grid_for(n, 256, 1024)), dim3(256), (const uint8_t*)ts, stride, n, cell, C, rec, cnt, table,
           (u32)lg, info);
-  if (EVM_SM_SCAN_LB) {
+  {
     u64* lb_status = reinterpret_cast<u64*>(z + a_cnt + a_bins + a_pres + (sizeof(u64) << lg));
     u32* lb_ctr = reinterpret_cast<u32*>(lb_status + n_scan_tiles);
     // (a look-back that gives up sends the batch to the sort path; a partial
     // prefix keeps every slot in range meanwhile)
     KLAUNCH(k_sm_scan_lb, dim3(n_scan_tiles), dim3(SM_FOLD_THREADS), cnt, C, off, lb_status, lb_ctr,
             &info->fold_overflow);
-  } else {
-    KLAUNCH(k_sm_scan, dim3(1), dim3(SM_FOLD_THREADS), cnt, C, off);
   }
   KLAUNCH(k_sm_scatter, dim3(grid_for(n, 256, 1024)), dim3(256), (const evm_rec*)rec, n, C, cnt, grp);
   KLAUNCH(k_sm_lww, dim3(grid_for(C, 256, 4096)), dim3(256), (const evm_rec*)rec, (const u32*)off, (const u32*)grp, C,

@@ -856,6 +856,12 @@ struct evm_dist {
   uint64_t self_lo = 0, self_hi = 0;
   size_t self_off = 0;
   uint64_t self_row = 0;  // (narrow: the first of them among the send buffer's rows)
+  // INVARIANT: `send` belongs to the last route until the next one -- take,
+  // ingest, return and split_winners read this rank's own rows from it.  Any
+  // other writer of `send` must set send_gen = 0 first; the readers check
+  // send_gen == route_gen (self_rows_intact) and refuse the call otherwise.
+  uint64_t route_gen = 0;  // routes finished by this rank
+  uint64_t send_gen = 0;   // the route whose records `send` holds (0: none)
   char* send = nullptr;  // wire records (send side), device
   size_t send_cap = 0;   // bytes
   char* recv = nullptr;  // received records (staging for evm_dist_take)
@@ -880,6 +886,9 @@ struct evm_dist {
 };
 
 namespace {
+
+// the last route's own rows are still where it left them (see evm_dist)
+bool self_rows_intact(const evm_dist* d) { return d->self_hi == d->self_lo || d->send_gen == d->route_gen; }
 
 int grow(char** p, size_t* cap, size_t want) {
   if (want <= *cap) return EVM_OK;
@@ -1148,7 +1157,8 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   // 48-B rows, 16-B aligned: packed 32-B records (a third of the xGMI bytes of
   // raw ones).  Every rank must use one record format: a rank that cannot
   // pack says so in its count words (CNT_RAW) and then every rank sends raw.
-  const bool packed0 = !lerr && stride == 48 && (n == 0 || ((uintptr_t)ts & 15) == 0);
+  // (a rank with no rows sends nothing: it votes for no format and no stride)
+  const bool packed0 = !lerr && (n == 0 || (stride == 48 && ((uintptr_t)ts & 15) == 0));
   // no aux and no source indexes wanted: 24-B records (a quarter fewer xGMI
   // and HBM bytes), when every rank asks for them (CNT_WIDE otherwise)
   const bool narrow0 = packed0 && !aux && (flags_in & EVM_ROUTE_NO_SRC);
@@ -1161,6 +1171,7 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   d->self_off = 0;
   d->self_row = 0;
   d->packed = d->narrow = 0;
+  d->send_gen = 0;  // (rewritten below)
   Route R = route_of(d, owner, dest);
   R.ts = ts;
   R.stride = stride;
@@ -1182,7 +1193,7 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   }
   // the counts: one all-to-all of G words (flag bits on top), one read back
   const u64 fmt = (packed0 ? 0ull : CNT_RAW) | (narrow0 ? 0ull : CNT_WIDE) |
-                  ((u64)(lerr ? 0 : stride / 8) << CNT_STRIDE_SHIFT);
+                  ((u64)(lerr || !n ? 0 : stride / 8) << CNT_STRIDE_SHIFT);
   KLAUNCH(k_dist_mark, dim3(1), dim3(MAX_BUCKETS), scnt, G, (lerr || !n) ? 1 : 0, lerr ? 1 : 0,
           (const u32*)(lerr ? nullptr : flags), fmt);
   int st = d->tx->all_to_all_u64(scnt, rcnt, ctx->stream);
@@ -1197,12 +1208,15 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   const u64* hs = d->hcnt + W_SEND;
   const u64* hr = d->hcnt + W_RECV;
   bool any_err = lerr != EVM_OK, any_inv = false, any_raw = false, any_wide = false, mixed_stride = false;
+  u64 agreed = 0;  // the stride of the ranks that hold rows (0: a rank without rows -- a wildcard)
   for (u32 p = 0; p < G; ++p) {
     any_err |= (hr[p] & CNT_ERR) != 0;
     any_inv |= (hr[p] & CNT_INVALID) != 0;
     any_raw |= (hr[p] & CNT_RAW) != 0;
     any_wide |= (hr[p] & CNT_WIDE) != 0;
-    mixed_stride |= ((hr[p] >> CNT_STRIDE_SHIFT) & CNT_STRIDE_MAX) != stride / 8;
+    const u64 sw = (hr[p] >> CNT_STRIDE_SHIFT) & CNT_STRIDE_MAX;
+    if (sw && agreed && sw != agreed) mixed_stride = true;
+    if (sw) agreed = sw;
   }
   if (any_err) return lerr ? lerr : EVM_EDIST;  // every rank saw the flag: nobody exchanges
   const bool bad_dest = d->hcnt[W_BAD] != 0;
@@ -1214,6 +1228,8 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   // raw records carry the row bytes at the sender's stride: one stride on
   // every rank, or nobody exchanges (every rank sees the mismatch)
   if (!packed && mixed_stride) return EVM_EINVAL;
+  // a rank without rows receives raw records at the senders' stride
+  if (!packed && !n && agreed) stride = (size_t)agreed * 8;
   const bool narrow = packed && !any_wide;
   const int fmt_final = packed ? (narrow ? (int)FMT_NARROW : (int)FMT_PACKED) : (int)FMT_RAW;
   const size_t rb_final = packed ? (narrow ? NARROW : PACKED) : stride + META;
@@ -1288,6 +1304,7 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   d->narrow = narrow ? 1 : 0;
   d->n_recv = total;
   d->n_in = n;
+  d->send_gen = ++d->route_gen;
   for (u32 p = 0; p < G; ++p) {
     d->sent[p] = hs[p] & CNT_MASK;
     d->recvd[p] = hr[p] & CNT_MASK;
@@ -1307,6 +1324,7 @@ int evm_dist_take(evm_ctx* ctx, evm_dist* d, uint32_t group, char* out_ts, size_
                                   ((out_stride % 16 || ((uintptr_t)out_ts & 15)) ? (int)FMT_ST8 : 0))
                                : (int)FMT_RAW;
   if (n > cap) return EVM_ECAPACITY;
+  if (!self_rows_intact(d)) return EVM_EINVAL;
   const u32 G = (u32)d->world;
   const u64* droff = d->cnt + W_ROFF;
   const Route R = route_of(d, nullptr, nullptr);
@@ -1351,6 +1369,7 @@ int evm_dist_ingest(evm_ctx* ctx, evm_dist* d, evm_store* store, uint64_t id_bas
   const size_t n = d->n_recv;
   if (n == 0) return EVM_OK;
   if (!flags || !(d->dir_local || d->hot)) return EVM_EINVAL;  // local ids come from the directory / split
+  if (!self_rows_intact(d)) return EVM_EINVAL;
   const Route R = route_of(d, nullptr, nullptr);
   if (d->packed && d->narrow) {  // the owner column arrived as the store's owner ids
     const WireSrc w{nullptr, nullptr, R.self_lo, R.self_hi, 0u, 0u, R.soa_a, R.self_a, R.soa_b, R.self_b};
@@ -1633,6 +1652,7 @@ int evm_dist_return(evm_ctx* ctx, evm_dist* d, const void* val, uint32_t elem, v
   int lerr = EVM_OK;
   if ((elem != 1 && elem != 2 && elem != 4 && elem != 8) || (n && !val) || (n_out && !out)) lerr = EVM_EINVAL;
   if (d->narrow) lerr = EVM_EINVAL;  // the last route carried no source indexes (EVM_ROUTE_NO_SRC)
+  if (!self_rows_intact(d)) lerr = EVM_EINVAL;
   const size_t ooff = d->packed ? 16 : d->stride;
   Scratch S(ctx);
   u32* bad = S.alloc<u32>(1);
@@ -1679,6 +1699,7 @@ int evm_dist_split_winners(evm_ctx* ctx, evm_dist* d, const int32_t* win, uint32
   int lerr = EVM_OK;
   if (n_cells && (!win || !out)) lerr = EVM_EINVAL;
   if (d->narrow) lerr = EVM_EINVAL;  // (no source indexes)
+  if (!self_rows_intact(d)) lerr = EVM_EINVAL;
   uint64_t nin[MAX_BUCKETS];
   int st = gather_status(ctx, d, lerr, ((u64)n_cells << 40) | d->n_in, nin);
   if (st) return st;

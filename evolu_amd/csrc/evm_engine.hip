@@ -168,9 +168,6 @@ int evm::launch_pack(evm_ctx* ctx, const char* ts, size_t stride, size_t n, cons
 // ============================================================================
 // Scans and sorts (host drivers for evm_prims.hpp)
 // ============================================================================
-#ifndef EVM_SCAN_SMALL  // (A/B builds: 0 = small scans in three launches too)
-#define EVM_SCAN_SMALL 1
-#endif
 // k columns (k <= SCAN_COLS) of n <= SCAN_LB_TILES tiles in one launch
 template <typename T, template <typename> class Op>
 static int scan_small_cols(evm_ctx* ctx, Scratch& S, int k, const T* const* ins, size_t n, T* const* outs,
@@ -194,7 +191,7 @@ static int scan_small_cols(evm_ctx* ctx, Scratch& S, int k, const T* const* ins,
 int evm::scan_exclusive_cols(evm_ctx* ctx, Scratch& S, int k, const u32* const* ins, size_t n, u32* const* outs,
                              u32* const* tots) {
   const size_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
-  bool ok = EVM_SCAN_SMALL && n > 0 && nt <= SCAN_LB_TILES && k <= SCAN_COLS;
+  bool ok = n > 0 && nt <= SCAN_LB_TILES && k <= SCAN_COLS;
   for (int c = 0; c < k && ok; ++c) ok = (const void*)ins[c] != (const void*)outs[c];
   if (ok) return scan_small_cols<u32, OpAdd>(ctx, S, k, ins, n, outs, tots);
   for (int c = 0; c < k; ++c) {
@@ -212,7 +209,7 @@ int evm::scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out,
   }
   const size_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
   if constexpr (sizeof(T) == 4) {
-    if (EVM_SCAN_SMALL && nt <= SCAN_LB_TILES && (const void*)in != (const void*)out) {
+    if (nt <= SCAN_LB_TILES && (const void*)in != (const void*)out) {
       const T* ins[1] = {in};
       T* outs[1] = {out};
       T* tots[1] = {total_dev};
@@ -993,7 +990,7 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
     ctx->diff_grid = (int)value;
     return EVM_OK;
   }
-  if (option == EVM_OPT_TEST_FAIL && value >= 0 && value <= 1) {
+  if (option == EVM_OPT_TEST_FAIL && value >= 0 && value <= 2) {
     ctx->test_fail = (int)value;
     return EVM_OK;
   }

@@ -406,10 +406,7 @@ constexpr int SORT_THREADS = 256;
 // 24 keys per thread (6,144 per tile): measured over 8..32 on the config-5
 // sort path (80M u64 keys, 6 passes): 8: 9.0 ms, 16: 7.6, 20: 6.9, 24: 6.6,
 // 28: 8.6, 32: 8.4
-#ifndef EVM_SORT_ITEMS
-#define EVM_SORT_ITEMS 24
-#endif
-constexpr int SORT_ITEMS = EVM_SORT_ITEMS;
+constexpr int SORT_ITEMS = 24;
 constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;
 
 template <typename K>

@@ -311,6 +311,12 @@ __global__ void k_sv_bad(const evm_rec* __restrict__ rec, size_t n, uint8_t* __r
     flags[orig ? orig[i] : i] = (rec[i].meta & EVM_META_VALID) ? 0u : EVM_MSG_BAD;
 }
 
+// nothing inserted (a call that commits nothing after K5 wrote its flags)
+__global__ void k_flags_clear(size_t n, uint8_t* __restrict__ flags, const u32* __restrict__ orig) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    flags[orig ? orig[i] : i] = 0;
+}
+
 __global__ void k_sv_sorted_check(const u64* __restrict__ ck, size_t m, u32* __restrict__ unsorted) {
   for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x + 1; q < m; q += (size_t)gridDim.x * blockDim.x)
     if (ck[q] < ck[q - 1]) *unsorted = 1u;
@@ -387,9 +393,6 @@ __device__ __forceinline__ bool run_head(const u32* __restrict__ owner, size_t n
   return i < n && (i == 0 || owner[i] != owner[i - 1]);
 }
 
-#ifndef EVM_RUN_VEC
-#define EVM_RUN_VEC 1
-#endif
 // Full tiles of a 16-B aligned column: a lane reads 4 consecutive owners per
 // step (a wave step = 1 KiB), the owner before its first one comes from the
 // lane below (lane 0: the previous step's last, or the owner before the tile).
@@ -401,7 +404,7 @@ __device__ __forceinline__ u32 run_heads4(const uint4 v, u32& carry, int lane) {
   return (v.x != prev ? 1u : 0u) | (v.y != v.x ? 2u : 0u) | (v.z != v.y ? 4u : 0u) | (v.w != v.z ? 8u : 0u);
 }
 __device__ __forceinline__ bool run_vec_tile(const u32* __restrict__ owner, size_t n, size_t base) {
-  return EVM_RUN_VEC && base + RUN_TILE <= n && ((uintptr_t)owner & 15) == 0;
+  return base + RUN_TILE <= n && ((uintptr_t)owner & 15) == 0;
 }
 __device__ __forceinline__ u32 run_carry0(const u32* __restrict__ owner, size_t base) {
   return base ? owner[base - 1] : ~owner[0];  // message 0 always starts a run
@@ -520,9 +523,6 @@ __global__ void k_run_seg(const u32* __restrict__ run_owner_sorted, u32 R, const
 // fetch one run's (position, start) each, then the wave writes the whole
 // range coalesced, each element finding its run among the RF_RUNS bounds.
 constexpr int RF_RUNS = 8;
-#ifndef EVM_RUN_FILL_ALWAYS  // (A/B builds: 1 = the permutation written for every run-structured batch)
-#define EVM_RUN_FILL_ALWAYS 0
-#endif
 __global__ __launch_bounds__(256) void k_run_fill(const u32* __restrict__ run_pos, const u32* __restrict__ run_start,
                                                   const u32* __restrict__ order, u32 R, u32* __restrict__ perm) {
   const u32 lane = threadIdx.x & 63;
@@ -616,29 +616,12 @@ constexpr u32 SVO_CAP = 4096;  // largest share of one owner handled in LDS
 constexpr int SVO_TIE_MAX = 32;  // longest run of one (millis, counter) with distinct nodes
 constexpr u32 SVO_BUCKET_MAX = 16;  // counting-sort bucket size finished by insertion sort
 constexpr u64 SVO_SCAN_STORED = 16;  // stored rows read once per segment while <= 16 x its new rows
-#ifndef EVM_K5_LEAF_LDS  // (A/B builds: 0 = the new leaves' tree searches in global memory always)
-#define EVM_K5_LEAF_LDS 1
-#endif
+// The new leaves' tree searches run over the segment's tree codes staged in LDS
 // (measured: reingest K5 4.00 -> 3.26-3.30 ms, but the LDS search takes 81
 // VGPRs -- five waves per SIMD instead of six, the empty store's K5 2.60 ->
 // 2.72 ms; forcing six spills 28 B per lane.  So the 1,024 class takes the
 // LDS search only into a store that has a tree: K5 is instantiated both ways)
-#ifndef EVM_SVO_SB  // (A/B builds only: stored rows per thread whose loads are issued together)
-#define EVM_SVO_SB 4
-#endif
-constexpr int SVO_SB = EVM_SVO_SB;
-#ifndef EVM_SVO_SCAN  // (A/B builds only: 0 = a binary search of the stored rows per candidate)
-#define EVM_SVO_SCAN 1
-#endif
-#ifndef EVM_SVB_LDS  // (A/B builds only: 0 = the merge without LDS-staged keys)
-#define EVM_SVB_LDS 1
-#endif
-#ifndef EVM_SVO_CBASE  // (A/B builds only: 0 = K5 reads every batch index from perm)
-#define EVM_SVO_CBASE 1
-#endif
-#ifndef EVM_SEG_FUSED  // (A/B builds only: 0 = a minutes pass before the plan of interleaved owners)
-#define EVM_SEG_FUSED 1
-#endif
+constexpr int SVO_SB = 4;  // stored rows per thread whose loads are issued together
 
 struct SvoStatus {
   u32 big;       // an owner's share exceeds the launch's capacity
@@ -703,7 +686,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, u32* __restrict__ cnt_xor, SvoStatus* __restrict__ status,
     const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list, u32* __restrict__ mid1,
     uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner, int flags_preset, u32* __restrict__ mid512,
-    WireSrc wsrc) {
+    WireSrc wsrc, int skip_stored) {
   constexpr int PER = CAP / THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
   constexpr u64 PMASK = CAP - 1;
@@ -779,12 +762,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
         const v4u x = __builtin_nontemporal_load(row), y = __builtin_nontemporal_load(row + 1),
                   z = __builtin_nontemporal_load(row + 2);
         const u32 w[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w & 0xffffu};
-#if EVM_ABL_SV == 1  // (ablation builds only: no murmur3)
-        Parsed p = parse_ts46(w);
-        p.hash = w[5];
-#else
         const Parsed p = parse_ts46(w);
-#endif
         bad |= (p.meta & EVM_META_VALID) ? 0u : 1u;
         s_rh[t] = p.rh;  // (== node_ranks(p.node, case mask): the parse's SWAR ranks)
         s_rl[t] = p.rl;
@@ -944,7 +922,6 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     }
   }
   __syncthreads();
-#if EVM_ABL_SV != 2  // (ablation 2: no tie-run ordering)
   // runs of one tc: order by the node ranks (then position).  Each member
   // finds its run's bounds and counts the members below it, all in parallel
   // (runs are short: distinct nodes at one (millis, counter))
@@ -990,16 +967,11 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     }
   }
   __syncthreads();
-#endif
   // among equal timestamps the one first in the batch (smallest batch index)
   // is the candidate insert -- independent of the order the segment's
   // messages were listed in (key-range segments are gathered unordered).
   // s_cnt[p] = 1: p is its timestamp's candidate.  A run's first position
   // decides the whole run (O(run) per run).
-#if EVM_ABL_SV == 3  // (ablation: every position a candidate)
-  for (u32 p = threadIdx.x; p < m; p += THREADS) cnt_set(p, 1u);
-  if (false)
-#endif
   for (u32 p = threadIdx.x; p < m; p += THREADS) {
     const u64 kp = s_k[p];
     const u32 pp = (u32)(kp & PMASK);
@@ -1032,7 +1004,9 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   // step, ~10 steps: the steady-state ingest's cost before).  A segment with
   // far more stored rows than new ones keeps the per-candidate searches.
   const u64 sa = sv.sa[s], sb = sv.sb[s];
-  const bool scan_stored = EVM_SVO_SCAN && sb > sa && sb - sa <= SVO_SCAN_STORED * m;
+  // (skip_stored: EVM_OPT_TEST_FAIL 2 -- the check left out, so that a
+  // stored timestamp reaches the merge as a new row: its guard's test)
+  const bool scan_stored = !skip_stored && sb > sa && sb - sa <= SVO_SCAN_STORED * m;
   if (scan_stored) {
     // (SVO_SB stored rows per thread per round: their tc loads, then the
     // ranks of those in the new keys' span, each batch issued together)
@@ -1096,27 +1070,11 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       mb[r] = pidx(pos);
       mhash[r] = s_h[pos];
       bool ins = cnt_get(p) != 0;
-      if (ins && sb > sa && !scan_stored) {
+      if (ins && sb > sa && !scan_stored && !skip_stored) {
         const SKey k{o, mt[r], mh[r], ml[r]};
         const size_t q = store_lower(st, sa, sb, k);
         ins = !(q < sb && skey_cmp(skey_at(st, q), k) == 0);
       }
-#ifdef EVM_DBG_SCAN  // (debug builds: the scan's verdict against the per-candidate search)
-      if (ins && sb > sa && scan_stored) {
-        const SKey k{o, mt[r], mh[r], ml[r]};
-        const size_t q = store_lower(st, sa, sb, k);
-        if (q < sb && skey_cmp(skey_at(st, q), k) == 0) {
-          const u32 pos = (u32)(s_k[p] & PMASK);
-          const u32 b = pidx(pos);
-          const u64 in_tc = SRC != SRC_REC ? 0ull : rec[b].tc;
-          printf("scan miss: seg %u owner %u p %u m %llu sa %llu sb %llu tc %llx tmin %llx tmax %llx CAP %u kp %llx "
-                 "pos %u in_tc %llx stored_q %llu\n", s, o, p, (unsigned long long)m, (unsigned long long)sa,
-                 (unsigned long long)sb, (unsigned long long)mt[r], (unsigned long long)tmin, (unsigned long long)tmax,
-                 CAP, (unsigned long long)s_k[p], pos, (unsigned long long)in_tc, (unsigned long long)q);
-          atomicOr(&status->fallback, 1u);
-        }
-      }
-#endif
       if (ins) {
         insm |= 1u << r;
         ++c;
@@ -1292,22 +1250,13 @@ __global__ void k_seg_fix(SegView sv, u32 NS, const uint8_t* __restrict__ ownbig
 // segments search the global arrays as before.  Leaves the same way (an equal
 // tree leaf counts one bin higher: it is not below the new code).
 constexpr u32 SVB_LDS = 1024;
-#ifndef EVM_SVB_BATCH  // (A/B builds only: stored rows / leaves per thread whose loads are issued together)
-#define EVM_SVB_BATCH 4
-#endif
-constexpr int SVB_B = EVM_SVB_BATCH;
+constexpr int SVB_B = 4;  // stored rows / leaves per thread whose loads are issued together
 // Rows of a segment with <= SVB_SRC output rows (stored + new) are written
 // once, in output order: the searches fill a source map in LDS (output
 // position -> stored row or new row) and a third pass copies each output row
 // from its source, consecutive lanes on consecutive rows.  (Writing stored
 // rows at their places and the new ones into the gaps afterwards touched
 // every output line twice: 16.4 GB written per reingest merge vs ~8.7 GB.)
-#ifndef EVM_SVB_SRC  // (A/B builds: 0 = the two-pass row writes)
-#define EVM_SVB_SRC 1
-#endif
-#ifndef EVM_SVB_SRC_LEAVES  // (A/B builds: 0 = rows through the map, leaves in two passes)
-#define EVM_SVB_SRC_LEAVES 1
-#endif
 constexpr u32 SVB_SRC = 4096;
 constexpr uint16_t SVB_NEW = 0x8000, SVB_EQ = 0x4000;
 static_assert(SVB_LDS <= SVB_EQ && SVB_SRC <= SVB_NEW, "source map fields");
@@ -1337,14 +1286,22 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     const u64* __restrict__ t_ck, const int32_t* __restrict__ t_xr, const u64* __restrict__ l_ck,
     const int32_t* __restrict__ l_xr, const uint8_t* __restrict__ l_dup, const u32* __restrict__ cnt_new,
     const u32* __restrict__ leaf_pos, StoreOut so, u64* __restrict__ so_off, u64* __restrict__ to_ck,
-    int32_t* __restrict__ to_xr, u64* __restrict__ to_off, int rows_in_place) {
+    int32_t* __restrict__ to_xr, u64* __restrict__ to_off, int rows_in_place, u32* __restrict__ merr) {
   __shared__ u32 s_dp[SVO_CAP + 1];  // exclusive prefix count of the new leaves already in the tree
+  // The merge places rows by assuming the segment's stored and new keys are
+  // disjoint (K5 dropped every stored timestamp) and that K5's l_dup marks
+  // exactly the new leaves equal to a tree leaf.  Both are checked here: a
+  // stored row equal to a new one, a hole left in a source map, or a count of
+  // equal leaves other than K5's sets *merr (the host then discards the new
+  // store and returns EVM_ESTATE) and the segment writes nothing past that
+  // point; the writes before it stay inside the segment's output range.
+  __shared__ u32 s_bad, s_eq;
   __shared__ u32 tmp[SVO_THREADS / 64 + 1];
   constexpr u32 LN = MERGE ? SVB_LDS : 1;
   __shared__ u64 k_tc[LN], k_hi[LN];  // new row keys (then new leaf codes in k_tc)
   __shared__ u32 k_lo[LN];
   __shared__ u32 hist[LN + 1];
-  __shared__ uint16_t src[MERGE && EVM_SVB_SRC ? SVB_SRC : 1];  // output row -> source (SVB_NEW | new j, or stored k - sa)
+  __shared__ uint16_t src[MERGE ? SVB_SRC : 1];  // output row -> source (SVB_NEW | new j, or stored k - sa)
   const u32 s = blockIdx.x;
   const u32 o = seg_owner(sv, s);
   const u64 a = sv.start[s];
@@ -1354,8 +1311,10 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   // rows: the owner's stored and new keys are disjoint sorted lists
   // rows_in_place: an empty store whose every message was inserted -- the
   // K5 rows already sit at their final places (position = batch position)
-  const bool lds_rows = MERGE && EVM_SVB_LDS && !rows_in_place && M <= SVB_LDS;
-  const bool by_src = lds_rows && EVM_SVB_SRC && (sb - sa) + M <= SVB_SRC;
+  const bool lds_rows = MERGE && !rows_in_place && M <= SVB_LDS;
+  const bool by_src = lds_rows && (sb - sa) + M <= SVB_SRC;
+  constexpr uint16_t SRC_HOLE = 0xffff;  // (no valid entry: row / leaf indexes stay below SVB_EQ)
+  if (threadIdx.x == 0) s_bad = s_eq = 0;
   if (lds_rows) {
     for (u32 j = threadIdx.x; j < M; j += SVO_THREADS) {
       k_tc[j] = n_tc[a + j];
@@ -1363,6 +1322,8 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
       k_lo[j] = n_lo[a + j];
     }
     for (u32 j = threadIdx.x; j <= M; j += SVO_THREADS) hist[j] = 0;
+    if (by_src)
+      for (u32 p = threadIdx.x; p < (u32)(sb - sa) + M; p += SVO_THREADS) src[p] = SRC_HOLE;
   }
   __syncthreads();
   // (assembling each output column of a segment in LDS and writing it once,
@@ -1398,6 +1359,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
           if (below) lo = mid + 1;
           else hi = mid;
         }
+        if (lo < M && k_tc[lo] == key.tc && k_hi[lo] == key.hi && k_lo[lo] == key.lo) s_bad = 1;  // not disjoint
         atomicAdd(&hist[lo], 1u);
       } else {
         while (lo < hi) {
@@ -1405,6 +1367,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
           if (skey_cmp(SKey{o, n_tc[a + mid], n_hi[a + mid], n_lo[a + mid]}, key) < 0) lo = mid + 1;
           else hi = mid;
         }
+        if (lo < M && skey_cmp(SKey{o, n_tc[a + lo], n_hi[a + lo], n_lo[a + lo]}, key) == 0) s_bad = 1;
       }
       if (by_src) {
         src[(k - sa) + lo] = (uint16_t)(k - sa);
@@ -1423,6 +1386,15 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   if (by_src) {
     for (u32 j = threadIdx.x; j < M; j += SVO_THREADS) src[j + hist[j]] = (uint16_t)(SVB_NEW | j);
     __syncthreads();
+    for (u32 p = threadIdx.x; p < (u32)(sb - sa) + M; p += SVO_THREADS)
+      if (src[p] == SRC_HOLE) s_bad = 1;  // (two rows placed at one output position)
+    __syncthreads();
+  }
+  if (s_bad) {  // (uniform: read after a barrier)
+    if (threadIdx.x == 0) atomicOr(merr, 1u);
+    return;
+  }
+  if (by_src) {
     const u32 T = (u32)(sb - sa) + M;
     for (u32 p0 = threadIdx.x; p0 < T; p0 += SVB_B * SVO_THREADS) {
       u64 vtc[SVB_B], vhi[SVB_B], vid[SVB_B];
@@ -1510,17 +1482,19 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     run += d[r];
   }
   if (threadIdx.x == 0) s_dp[NL] = dtot;
-  const bool lds_leaves = MERGE && EVM_SVB_LDS && NL <= SVB_LDS;
+  const bool lds_leaves = MERGE && NL <= SVB_LDS;
   // leaves written once through the source map too: a tree leaf's entry is
   // its index, a new leaf's SVB_NEW | j, a tree leaf equal to new leaf j
   // SVB_NEW | SVB_EQ | j with the combined XOR parked in eqx[j] (k_hi is free)
   const u64 TL = (lb - la) + NL - dtot;
-  const bool leaves_src = lds_leaves && EVM_SVB_SRC && EVM_SVB_SRC_LEAVES && TL <= SVB_SRC;
+  const bool leaves_src = lds_leaves && TL <= SVB_SRC;
   u32* eqx = reinterpret_cast<u32*>(k_hi);
   __syncthreads();  // (the rows' LDS keys are dead: the leaf codes take k_tc)
   if (lds_leaves) {
     for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) k_tc[j] = l_ck[a + j];
     for (u32 j = threadIdx.x; j <= NL; j += SVO_THREADS) hist[j] = 0;
+    if (leaves_src)
+      for (u32 q = threadIdx.x; q < (u32)TL; q += SVO_THREADS) src[q] = SRC_HOLE;
   }
   __syncthreads();
   for (u64 k0 = la + threadIdx.x; k0 < lb; k0 += (u64)SVB_B * SVO_THREADS) {
@@ -1548,6 +1522,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
         }
         j = lo;
         eq = j < NL && k_tc[j] == code;
+        if (eq) atomicAdd(&s_eq, 1u);
         atomicAdd(&hist[j + (eq ? 1u : 0u)], 1u);  // (an equal tree leaf is not below new leaf j)
         if (leaves_src) {
           const u32 q = (u32)(k - la) + j - s_dp[j];
@@ -1562,18 +1537,31 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
       } else {
         j = (u32)(lb_u64(l_ck, a, a + NL, code) - a);  // new leaves below this code
         eq = j < NL && l_ck[a + j] == code;
+        if (eq) atomicAdd(&s_eq, 1u);
       }
       const u64 w = lbase + (k - la) + j - s_dp[j];
+      if (w >= lbase + TL) continue;  // (only when l_dup and the tree disagree: flagged below)
       to_ck[w] = code;
       to_xr[w] = txr[r] ^ (eq ? l_xr[a + j] : 0);
     }
   }
   __syncthreads();
   if (lds_leaves) svb_inclusive_prefix(hist, NL + 1, tmp);  // hist[j] = tree leaves below new leaf j
+  if (s_eq != dtot) {  // (uniform: read after a barrier) K5's equal leaves are not the tree's
+    if (threadIdx.x == 0) atomicOr(merr, 2u);
+    return;
+  }
   if (leaves_src) {
     for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS)
       if (!l_dup[a + j]) src[(j - s_dp[j]) + hist[j]] = (uint16_t)(SVB_NEW | j);
     __syncthreads();
+    for (u32 q = threadIdx.x; q < (u32)TL; q += SVO_THREADS)
+      if (src[q] == SRC_HOLE) s_bad = 1;
+    __syncthreads();
+    if (s_bad) {
+      if (threadIdx.x == 0) atomicOr(merr, 4u);
+      return;
+    }
     for (u32 q0 = threadIdx.x; q0 < (u32)TL; q0 += SVB_B * SVO_THREADS) {
       u64 vck[SVB_B];
       int32_t vxr[SVB_B];
@@ -1608,6 +1596,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     const u64 code = lds_leaves ? k_tc[j] : l_ck[a + j];
     const u64 below = lds_leaves ? (u64)hist[j] : lb_u64(t_ck, la, lb, code) - la;
     const u64 w = lbase + (j - s_dp[j]) + below;
+    if (w >= lbase + TL) continue;
     to_ck[w] = code;
     to_xr[w] = l_xr[a + j];
   }
@@ -1629,9 +1618,6 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
 // in flight.  Nothing merges, so none of the merge's block scans and barriers
 // (~100k segments of ~1,000 rows: the merge's per-workgroup fixed work was
 // most of its time).
-#ifndef EVM_SVO_COPY  // (A/B builds: 0 = k_svo_b<false> for the empty store)
-#define EVM_SVO_COPY 1
-#endif
 constexpr int SVC_WAVES = 4;
 __global__ __launch_bounds__(64 * SVC_WAVES) void k_svo_copy(
     SegView sv, u32 NS, u32 n_owners, const u64* __restrict__ n_tc, const u64* __restrict__ n_hi,
@@ -1975,10 +1961,7 @@ void store_release_arrays(evm_ctx* ctx, evm_store* s) {
 }
 
 // ------------------------------------------- key-range segments (big owners)
-#ifndef EVM_SEG_TARGET  // (A/B builds only: tools/build_variant.sh NAME -DEVM_SEG_TARGET=...)
-#define EVM_SEG_TARGET 560
-#endif
-constexpr u32 SEG_TARGET = EVM_SEG_TARGET;  // messages per segment of a cut owner: minute-granular splitters and
+constexpr u32 SEG_TARGET = 560;  // messages per segment of a cut owner: minute-granular splitters and
                                             // sampling noise keep nearly all below 1,024 (the fast kernel)
 static_assert(SEG_TARGET >= 64 && SEG_TARGET <= 4096, "segment target");
 constexpr u32 SEG_SPLIT_MIN = 1024; // shares above this are cut (the 1,024 kernel is the fast one)
@@ -2442,8 +2425,8 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   bool split = false;
   u64* skey = nullptr;   // sorted samples: owner << mb | minute - gmin
   // interleaved owners with K5 parsing the rows / records itself: the plan
-  // reads the minutes from them directly (no minutes pass; EVM_SEG_FUSED)
-  const bool seg_fused = EVM_SEG_FUSED && fused && (wire || (stride % 16 == 0 && ((uintptr_t)ts & 15) == 0));
+  // reads the minutes from them directly (no minutes pass)
+  const bool seg_fused = fused && (wire || (stride % 16 == 0 && ((uintptr_t)ts & 15) == 0));
   u32* smin = nullptr;   // the samples' minutes (seg_fused)
   MinuteSrc msrc{rec, minute, nullptr, 0, WireSrc{nullptr, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr}};
   if (seg_fused) {
@@ -2471,9 +2454,9 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if ((st = radix_sort_pairs<u32>(ctx, S, rk, rv, R, 0, obits))) return st;
     KLAUNCH(k_run_len, dim3(grid_for(R, 256)), dim3(256), run_start, rv, R, n, len);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, len, R, run_pos, run_pos + R))) return st;
-    u32* cbase = EVM_SVO_CBASE ? S.alloc<u32>(std::max<u32>(O, 1)) : nullptr;
+    u32* cbase = S.alloc<u32>(std::max<u32>(O, 1));
     u32* multi = S.alloc<u32>(1);
-    if (!multi) return EVM_ENOMEM;
+    if (!cbase || !multi) return EVM_ENOMEM;
     HIPR(hipMemsetAsync(multi, 0, sizeof(u32), ctx->stream));
     KLAUNCH(k_run_seg, dim3(grid_for((size_t)O + 1, 256)), dim3(256), rk, R, run_pos, O, seg, info,
             (const u32*)run_start, (const u32*)rv, cbase, multi);
@@ -2500,7 +2483,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     // by K5 for owners of several runs; when every owner is one run (one
     // SyncRequest per owner, config 3) K5 indexes from the run starts and the
     // 4-B-per-message permutation is not written at all
-    if (!cbase || plan[3] || split || EVM_RUN_FILL_ALWAYS)
+    if (plan[3] || split)
       KLAUNCH(k_run_fill, dim3(grid_for(R, 4 * RF_RUNS, 1 << 16)), dim3(256), run_pos, run_start, rv, R, perm);
     if (split) {
       gmin = hi.minute_min;
@@ -2657,11 +2640,13 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   // per-workgroup fixed work, twice the occupancy); larger shares are listed
   // for the 1,024 and SVO_CAP passes
   const bool small = NS && n / NS < 400;
-  const bool leaf = EVM_K5_LEAF_LDS && t->n_leaves > 0;
+  const bool leaf = t->n_leaves > 0;
+  const int skip_stored = ctx->test_fail == 2 ? 1 : 0;
   auto pass = [&](u32 cap, dim3 grid, const u32* list, u32* l1, u32* l2, u32* l512) {
 #define SVO_ARGS                                                                                                      \
   rec, tsb, stride, info, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, \
-      l_xr, l_dup, c_rows, c_new, c_leaves, c_xor, status, orig, list, l2, l1, ownbig, n_owner, preset, l512, wsrc
+      l_xr, l_dup, c_rows, c_new, c_leaves, c_xor, status, orig, list, l2, l1, ownbig, n_owner, preset, l512, wsrc,  \
+      skip_stored
     // (the one-wave kernels: Zipf-tail owners of <= 128 / <= 256 messages, no cross-wave barriers;
     // source: true = the rows, false = packed records, SRC_WIRE = received records)
 // (the 1,024 kernel with 512 threads, two messages each, measured slower:
@@ -2721,7 +2706,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if ((st = scan_exclusive_cols(ctx, S, 2, ins, NS, outs, tots))) return st;
   }
   // the empty store's commit copies (k_svo_copy) and writes the prefix XOR itself
-  const bool by_copy = EVM_SVO_COPY && s->n == 0 && t->n_leaves == 0;
+  const bool by_copy = s->n == 0 && t->n_leaves == 0;
   int32_t* xpos = nullptr;
   if (by_copy) {
     xpos = S.alloc<int32_t>((size_t)NS + 1);
@@ -2772,12 +2757,22 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     return st;
   }
   const StoreOut so{ns->owner, ns->tc, ns->hi, ns->lo, ns->id};
+  u32* merr = nullptr;  // the merge's invariant checks (k_svo_b)
+  if (!by_copy) {
+    merr = S.alloc<u32>(1);
+    if (!merr) {
+      store_release_arrays(ctx, ns);
+      tree_destroy(ctx, nt);
+      return EVM_ENOMEM;
+    }
+    HIPR(hipMemsetAsync(merr, 0, sizeof(u32), ctx->stream));
+  }
   if (s->n)
     // (fewer merge workgroups per CU -- an LDS pad of 40/80 KB -- made the
     // merge 19 %/100 % slower: its write traffic is not an L2 capacity effect)
     KLAUNCH(k_svo_b<true>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s),
                 (const u64*)s->id, n_tc, n_hi, n_lo, n_id, c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup,
-                c_new, pos + NS, so, ns->off, nt->ck, nt->xr, nt->off, in_place);
+                c_new, pos + NS, so, ns->off, nt->ck, nt->xr, nt->off, in_place, merr);
   else if (by_copy && NS == 0)
     HIPR(hipMemsetAsync(nt->pfx, 0, sizeof(int32_t), ctx->stream));
   else if (by_copy)
@@ -2786,7 +2781,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   else
     KLAUNCH(k_svo_b<false>, dim3(NS), dim3(SVO_THREADS), sv, NS, O, view_of(s), (const u64*)s->id, n_tc, n_hi, n_lo, n_id,
           c_rows, pos, (const u64*)t->ck, t->xr, l_ck, l_xr, l_dup, c_new, pos + NS, so, ns->off, nt->ck, nt->xr,
-          nt->off, in_place);
+          nt->off, in_place, merr);
   // (the prefix XOR inside the merge -- segments by decoupled look-back, each
   // re-reading its own leaves -- measured 1.88 vs 0.79 + 0.39 ms of scans on
   // config 3: the merge's workgroups then wait on each other)
@@ -2794,6 +2789,17 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     store_release_arrays(ctx, ns);
     tree_destroy(ctx, nt);
     return st;
+  }
+  if (merr) {
+    u32 herr = 0;
+    st = hip_ok(hipMemcpyAsync(&herr, merr, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+    if (!st) st = hip_ok(hipStreamSynchronize(ctx->stream));
+    if (!st && herr) st = EVM_ESTATE;  // the store's invariants broke: nothing is committed
+    if (st) {
+      store_release_arrays(ctx, ns);
+      tree_destroy(ctx, nt);
+      return st;
+    }
   }
   *new_tree = nt;
   *done = true;
@@ -2939,8 +2945,13 @@ static int ingest_impl(evm_ctx* ctx, evm_store* s, const char* ts, size_t stride
       uint8_t* bigmask = (mode == 0 && !orig) ? S.alloc<uint8_t>(n) : nullptr;
       if (mode == 0 && !orig && !bigmask) return EVM_ENOMEM;
       if ((st = ingest_by_owner(ctx, S, s, rec, minute, own, n, orig, id_base, flags, info, perm, &ns, &new_tree,
-                                &done, bigmask, &big_only, ts, stride, pack_now, wire)))
+                                &done, bigmask, &big_only, ts, stride, pack_now, wire))) {
+        if (st == EVM_ESTATE) {  // the merge refused: no message is reported inserted
+          KLAUNCH(k_flags_clear, dim3(grid_for(n, 256)), dim3(256), n, flags, orig);
+          (void)evm_sync(ctx);
+        }
         return st;
+      }
       if (done && big_only && !orig) {
         // the LDS path took every owner but the big ones: commit that, then
         // the big owners' messages (in batch order) through the sort path

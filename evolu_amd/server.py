@@ -30,12 +30,13 @@ engine does not model the request (a nodeId that is not 16 hex chars, a
 timestamp shape timestampFromString would read in a way lenient.py does not
 restate, one timestamp stored under two spellings).  The user is then handed
 to the caller for good: every later request of that user also answers None,
-so the caller runs them, in order, on the reference path.  A None request is
-NOT always unapplied: a spelling conflict found after `evm_server_ingest_ex`
-committed the request (pass 1, or the canonical re-ingest) leaves its rows
-in this server's store and tree.  The handover is of the user, not of one
-request: the caller must serve that user from its own reference state from
-then on and treat this server's rows and tree of that user as stale.
+so the caller runs them, in order, on the reference path.  None always means
+unapplied.  A spelling conflict found only after `evm_server_ingest_ex`
+committed the request (pass 1, or the canonical re-ingest) answers
+`HandedOver(applied=True)` instead: its rows are in this server's store and
+tree, the user is handed over all the same, and the caller must serve that
+user from its own reference state from then on and treat this server's rows
+and tree of that user as stale.
 """
 from __future__ import annotations
 
@@ -48,7 +49,18 @@ from . import lenient as LN
 from . import wire
 from .engine import TS_LEN, Engine
 
-Result = Union[bytes, Exception, None]
+class HandedOver:
+    """A request whose user was handed to the caller after this server had
+    already committed it (applied=True): unlike None, its rows are in the store."""
+
+    def __init__(self, applied: bool):
+        self.applied = applied
+
+    def __repr__(self):
+        return "HandedOver(applied=%r)" % self.applied
+
+
+Result = Union[bytes, Exception, HandedOver, None]
 _HEX = set(b"0123456789abcdefABCDEF")
 
 
@@ -199,6 +211,7 @@ class SyncServer:
                 sp = [(t, t) for t in d.timestamps()]
                 if self._check(d.user, sp, flags[k], range(mids[k], mids[k] + len(sp))) is None:
                     self.detached.add(d.user)
+                    out[i] = HandedOver(applied=True)  # (committed by the ingest above)
                     continue
             answered.append((i, d, s))
         # the rejected owners' requests: invalid date -> 500; lenient -> their canonical form
@@ -227,6 +240,8 @@ class SyncServer:
                 added = None if k in rej2 else self._check(d.user, sp, f2[k], range(mids2[k], mids2[k] + len(sp)))
                 if added is None:
                     self.detached.add(d.user)
+                    if k not in rej2:
+                        out[i] = HandedOver(applied=True)  # (committed by the re-ingest)
                     continue
                 self.lenient.setdefault(d.user, {}).update(added)
                 for raw, mid in added.values():
@@ -298,4 +313,4 @@ class SyncServer:
         return [(t, c) for t, c, _ in keep]
 
 
-__all__ = ["SyncServer", "ParseBodyError", "RangeError"]
+__all__ = ["SyncServer", "ParseBodyError", "RangeError", "HandedOver"]

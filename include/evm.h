@@ -49,7 +49,8 @@ enum evm_status {
   EVM_EDEVICE = 6,    /* HIP error */
   EVM_ENOMEM = 7,     /* device allocation failed */
   EVM_ECAPACITY = 8,  /* output buffer too small */
-  EVM_EDIST = 9       /* RCCL missing or a collective failed (evm_dist_*) */
+  EVM_EDIST = 9,      /* RCCL missing or a collective failed (evm_dist_*) */
+  EVM_ESTATE = 10     /* a store invariant broke in a merge (stored and new keys not disjoint); nothing committed */
 };
 
 /* ---- packed timestamp record (32 bytes, device) -------------------------
@@ -119,7 +120,9 @@ int evm_sync(evm_ctx* ctx);
                                  records instead of parsing the rows itself (A/B) */
 #define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 2 the same with \
                                  10-bit digits when that saves a pass; 0 histogram + scan + scatter per pass */
-#define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM) */
+#define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM); \
+                                 2 = K5 skips its check against the stored rows (the merge's guard then \
+                                 returns EVM_ESTATE) */
 #define EVM_OPT_DIFF_GRID 6   /* evm_merkle_diff / select: k_diff workgroups per CU (0: one lane group per owner) */
 #define EVM_OPT_SELECT_PATH 7 /* getMessages selection with a requester: 0 (default) keep + rank + emit in one pass \
                                  (look-back over candidate tiles), 1 keep / scan / emit passes (A/B) */

@@ -79,12 +79,15 @@ class Engine {
   }
 
   // applyMessages.ts:26-131.  db: { cellMax(table, row, column) -> string|null,
-  // storedRows(timestamps) -> [{timestamp, table, row, column}] (optional: the
+  // storedRows(timestamps) -> [{timestamp, table, row, column}] (required: the
   // "__message" rows holding one of the batch's timestamps, PK "timestamp",
   // initDbModel.ts:44), upsert(table, row, column, value), insertMessage(message) }.
   // Returns the new MerkleTree JSON, or null when the batch needs the reference path
   // (a non-canonical timestamp, or one timestamp under two cells in the batch or
   // against a stored row: the reference then ignores that INSERT, :104-119).
+  // An adapter without storedRows is refused (TypeError; Left in the async form):
+  // the engine could not see a stored timestamp under another cell and would
+  // return other upserts and XORs than the reference, with no error.
   applyMessages(db, treeJson, messages) {
     const args = this._applyArgs(db, treeJson, messages);
     const r = addon.applyBatch(this.ctx, ...args);
@@ -95,7 +98,12 @@ class Engine {
   // the same, the GPU work on a libuv worker thread: Promise<Either<UnknownError, json|null>>
   // (the reference's Effect-returning shape, types.ts:317-399)
   async applyMessagesAsync(db, treeJson, messages) {
-    const args = this._applyArgs(db, treeJson, messages);
+    let args;
+    try {
+      args = this._applyArgs(db, treeJson, messages);
+    } catch (error) {
+      return { _tag: "Left", left: { type: "UnknownError", error } };
+    }
     const e = await addon.applyBatchAsync(this.ctx, ...args);
     addon.treeFree(this.ctx, args[0]);
     if (e._tag === "Left") return e;
@@ -103,6 +111,9 @@ class Engine {
   }
 
   _applyArgs(db, treeJson, messages) {
+    if (typeof db.storedRows !== "function")
+      throw new TypeError("applyMessages: the db adapter must provide storedRows(timestamps) " +
+        "(the __message rows of the batch's timestamps, applyMessages.ts:42-45)");
     const ids = new Map();
     const cells = [];
     const cell = new Uint32Array(messages.length);
@@ -122,13 +133,11 @@ class Engine {
     const priorPresent = Uint8Array.from(prior.map((p) => (p == null ? 0 : 1)));
     let storedTs = null;
     let storedCell = null;
-    if (typeof db.storedRows === "function") {
-      const rows = db.storedRows(Array.from(new Set(messages.map((m) => m.timestamp))));
-      if (rows.length) {
-        storedTs = encodeTimestamps(rows.map((r) => r.timestamp));
-        // a row of a cell the batch does not touch: any id >= the cell count
-        storedCell = Uint32Array.from(rows, (r) => { const c = ids.get(key(r)); return c === undefined ? 0xffffffff : c; });
-      }
+    const rows = db.storedRows(Array.from(new Set(messages.map((m) => m.timestamp))));
+    if (rows.length) {
+      storedTs = encodeTimestamps(rows.map((r) => r.timestamp));
+      // a row of a cell the batch does not touch: any id >= the cell count
+      storedCell = Uint32Array.from(rows, (r) => { const c = ids.get(key(r)); return c === undefined ? 0xffffffff : c; });
     }
     return [this._tree(treeJson), encodeTimestamps(messages.map((m) => m.timestamp)), STRIDE, cell, cells.length,
       encodeTimestamps(prior.map((p) => (p == null ? "" : p))), priorPresent, storedTs, storedCell];
@@ -391,7 +400,10 @@ class Dist {
         const prior = state.prior || new Array(nCells).fill(null);
         args.push(encodeTimestamps(prior.map((p) => (p == null ? "" : p))),
           Uint8Array.from(prior.map((p) => (p == null ? 0 : 1))));
-        const stored = state.stored || [];
+        // (a non-empty DB must say which of the batch's timestamps "__message" holds)
+        if (!Array.isArray(state.stored))
+          throw new TypeError("applyMessagesSplit: state.stored (the __message rows of the batch's timestamps) is required");
+        const stored = state.stored;
         if (stored.length) {
           args.push(encodeTimestamps(stored.map((r) => r.timestamp)), Uint32Array.from(stored.map((r) => r.cell)));
         }

@@ -82,6 +82,18 @@ async function asyncPart() {
   const addon = require("./evm_napi.node");
   out.leftOnError = await addon.serverIngestAsync(eng.ctx, s2.store, new Uint8Array(48), 48, new Uint32Array([99]), 0);
   s2.close();
+  // an adapter without storedRows is refused, not run blind (applyMessages.ts:42-45)
+  const c0 = cases.apply[0];
+  const noStored = Object.assign({}, fakeDb(c0).db);
+  delete noStored.storedRows;
+  try {
+    eng.applyMessages(noStored, c0.tree, c0.messages);
+    out.noStoredRows = "accepted";
+  } catch (e) {
+    out.noStoredRows = e instanceof TypeError ? "TypeError" : String(e);
+  }
+  const e2 = await eng.applyMessagesAsync(noStored, c0.tree, c0.messages);
+  out.noStoredRowsAsync = e2._tag === "Left" ? e2.left.type + ":" + e2.left.error.constructor.name : "Right";
 }
 asyncPart().then(() => {
   eng.close();

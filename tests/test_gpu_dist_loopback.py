@@ -217,6 +217,37 @@ def test_mixed_strides_are_refused_on_every_rank():
     assert res[0][1] + res[1][1] == 6000
 
 
+@pytest.mark.parametrize("raw", [False, True])
+def test_empty_rank_stride_is_a_wildcard(raw):
+    """A rank with no rows votes for no record format and no stride: its
+    stride (56) neither sends the others raw nor fails the route as mixed
+    strides.  raw=True: another rank holds a row outside the native domain, so
+    every rank sends raw records at 48 B -- the empty rank receives them at
+    the senders' stride."""
+    world = 3
+    slices = _slices(world, [20_000, 15_000, 0], 11, 61)
+    if raw:
+        slices[1][0][77, 3] = ord("x")  # not a date: raw records everywhere
+
+    def fn(r, eng, dd):
+        ts, owner, aux = slices[r]
+        if r == 2:
+            t = torch.zeros((0, 56), dtype=torch.uint8, device=torch.device("cuda", eng.device))
+            o = torch.zeros(0, dtype=torch.int32, device=t.device)
+            n = dd.route(t, o)
+        else:
+            n = dd.route(eng.dev(ts), eng.dev(owner))
+        t2 = dd.take(aux=False, src=False)[0].cpu().numpy()
+        return n, t2
+
+    res = _loop(world, fn)
+    for r in range(world):
+        ts, _, _, _ = _expected(slices, world, r, lambda o: o % world)
+        n, t2 = res[r]
+        assert n == len(ts)
+        assert np.array_equal(t2[:, :46], ts[:, :46])
+
+
 def test_local_failure_is_agreed_not_hung():
     """Rank 1 passes a bad stride: it returns EVM_EINVAL, rank 0 EVM_EDIST,
     nobody waits; the next route of both succeeds.  Same for gather_roots."""

@@ -143,6 +143,9 @@ def test_js_entry_points(tmp_path):
     assert res["dist"]["roots"] == res["dist"]["treeHashes"]
     # a device error reaches the caller as Left(UnknownError), not as a throw
     assert res["leftOnError"]["_tag"] == "Left" and res["leftOnError"]["left"]["type"] == "UnknownError"
+    # storedRows is required: without it a stored timestamp under another cell is invisible
+    assert res["noStoredRows"] == "TypeError"
+    assert res["noStoredRowsAsync"] == "UnknownError:TypeError"
     id_ts = [m["timestamp"] for b in batches for r in b for m in r["messages"]]
     for o in range(n_owners):
         rows = [] if since[o] is None else sdb.conn.execute(

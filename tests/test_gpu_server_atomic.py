@@ -89,3 +89,53 @@ def test_steady_state_makes_no_allocations(eng):
     assert b["workspace_regrows"] == a["workspace_regrows"]
     assert b["block_allocs"] == a["block_allocs"]
     assert b["scratch_pool_allocs"] == a["scratch_pool_allocs"]
+
+
+def test_merge_guard_refuses_overlapping_keys(eng):
+    """The merge (k_svo_b) places rows assuming the segment's stored and new
+    keys are disjoint.  With K5's check against the stored rows switched off
+    (EVM_OPT_TEST_FAIL 2) a redelivered stored timestamp reaches the merge as
+    a new row: the guard must return EVM_ESTATE -- not fault, not commit --
+    leave the store as it was and report nothing inserted; the same batch
+    then ingests normally."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    n_owners = 200
+    ts, own, _ = synth.config3(n_owners, 300, request=300, seed_config=71)
+    half = len(ts) // 2
+    store = eng.store_new(n_owners)
+    store.ingest(eng.dev(ts[:half]), eng.dev(own[:half]), 0)
+    before = _snapshot(store)
+    # the second half plus a redelivery of every 7th stored row, in their owners' requests
+    rng = np.random.default_rng(5)
+    redo = np.arange(0, half, 7)
+    ts_b = np.concatenate([ts[half:], ts[redo]])
+    own_b = np.concatenate([own[half:], own[redo]])
+    order = np.argsort(own_b, kind="stable")  # requests stay runs of one owner
+    ts_b, own_b = ts_b[order], own_b[order]
+    del rng
+    for path in (0, 3):  # segments of one owner; the LDS path without segments
+        eng.set_option(L.OPT_SERVER_PATH, path)
+        flags = eng.dev(np.full(len(ts_b), 0x55, dtype=np.uint8))
+        eng.set_option(L.OPT_TEST_FAIL, 2)
+        _, st = store.ingest(eng.dev(ts_b), eng.dev(own_b), 10_000_000, flags=flags, raise_on_error=False)
+        eng.set_option(L.OPT_TEST_FAIL, 0)
+        assert st == L.EVM_ESTATE
+        assert int(flags.cpu().numpy().astype(np.int64).sum()) == 0, "no message reported as inserted"
+        for x, y in zip(before, _snapshot(store)):
+            assert np.array_equal(x, y)
+    eng.set_option(L.OPT_SERVER_PATH, 0)
+    f_ok, st = store.ingest(eng.dev(ts_b), eng.dev(own_b), 10_000_000, raise_on_error=False)
+    assert st == L.EVM_OK
+    ref = eng.store_new(n_owners)
+    eng.set_option(L.OPT_SERVER_PATH, 2)
+    ref.ingest(eng.dev(ts[:half]), eng.dev(own[:half]), 0)
+    f_ref, _ = ref.ingest(eng.dev(ts_b), eng.dev(own_b), 10_000_000)
+    eng.set_option(L.OPT_SERVER_PATH, 0)
+    assert np.array_equal(f_ok.cpu().numpy(), f_ref.cpu().numpy())
+    assert int((f_ok.cpu().numpy() & L.MSG_INS).astype(bool).sum()) == len(ts) - half
+    for x, y in zip(_snapshot(store), _snapshot(ref)):
+        assert np.array_equal(x, y)
+    store.free()
+    ref.free()

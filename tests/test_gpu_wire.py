@@ -116,7 +116,7 @@ def test_per_request_failure_and_lenient_timestamps(eng):
     counter parses) is stored under its raw spelling and XORed in its
     canonical form -- the responses, including later requests of the same
     owners, are byte-identical to the reference's."""
-    from evolu_amd.server import RangeError, SyncServer
+    from evolu_amd.server import HandedOver, RangeError, SyncServer
 
     rng = random.Random(21)
     users = ["%021x" % rng.getrandbits(84) for _ in range(5)]
@@ -159,7 +159,9 @@ def test_per_request_failure_and_lenient_timestamps(eng):
     more = [req(users[2], [canon]), req(users[2], pools[users[2]][9:11]), req(users[4], pools[users[4]][:3])]
     got2 = srv.sync(more)
     want2 = _expected(bodies + more)[len(bodies):]
-    assert got2[0] is None and got2[1] is None and users[2] in srv.detached
+    # (the conflicting request was committed before the conflict showed: not None)
+    assert isinstance(got2[0], HandedOver) and got2[0].applied
+    assert got2[1] is None and users[2] in srv.detached
     assert got2[2] == want2[2]
     srv.close()
 
