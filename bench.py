@@ -976,7 +976,7 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
         r0 = time.perf_counter()
         if dist_ingest:
             # route + addMessages on the received records where they lie (evm_dist_ingest)
-            n_r = srv.dd.route(ts_in, owner_in, need_src=False)
+            n_r = srv.dd.route(ts_in, owner_in, need_src=False, keep_input=True)
             route_ms.append((time.perf_counter() - r0) * 1e3)
             srv.new_store()
             srv.dd.ingest(srv.store, id_base, flags)
@@ -1249,7 +1249,7 @@ def config5_rank(eng, dd, comm, owners_per_gpu=125_000, n_per_gpu=125_000_000, s
     def step():
         r0 = time.perf_counter()
         if dist_ingest:
-            n_s = srv.dd.route(ts_in, owner_in, need_src=False)
+            n_s = srv.dd.route(ts_in, owner_in, need_src=False, keep_input=True)
             route_ms.append((time.perf_counter() - r0) * 1e3)
             srv.new_store()
             srv.dd.ingest(srv.store, id_base, flags)

@@ -33,6 +33,7 @@ MSG_UPS = 0x01
 MSG_XOR = 0x02
 MSG_INS = 0x04
 ROUTE_NO_SRC = 1  # evm_dist_route_ex: no source indexes wanted (24-B records when aux is absent)
+ROUTE_KEEP_INPUT = 2  # ... and the caller keeps ts until the last take / ingest (own rows never copied)
 MSG_BAD = 0x80
 
 OPT_CLIENT_PATH = 1

@@ -3025,6 +3025,7 @@ static int apply_entry(evm_ctx* ctx, const evm_tree* tree_in, const char* ts, si
                        size_t n_stored, const uint32_t* stored_cell, uint8_t* flags, int32_t* winner,
                        evm_tree** tree_out, int path, evm_pending* pend) {
   if (!ctx || !tree_in || !tree_out || stride < 46 || (n && (!ts || !cell || !flags))) return EVM_EINVAL;
+  if (int e = tree_compact(ctx, tree_in)) return e;
   if (n_cells && !winner) return EVM_EINVAL;
   if (prior_present && (!prior_ts || prior_stride < 46)) return EVM_EINVAL;
   if (n_stored && (!stored_ts || !stored_cell || stored_stride < 46)) return EVM_EINVAL;

@@ -296,7 +296,15 @@ struct Route {
   const u32* soa_c;
   const char* self_a;
   const u32* self_b;
+  // EVM_ROUTE_KEEP_INPUT on a narrow route.  SEND: rows of bucket keep_me
+  // are not parsed or copied; their input index goes to self_idx (from the
+  // bucket's first slot).  RECV: own row i is ts row self_idx[i - self_lo].
+  u32 keep_me;
+  u32* self_idx;
+  const char* self_ts;
+  size_t self_stride;
 };
+constexpr u32 NO_KEEP = 0xffffffffu;
 
 // received record i: the staging buffer, or this rank's own rows in the send buffer
 __device__ __forceinline__ const char* recv_rec(const Route& R, const char* rec, size_t rb, size_t i) {
@@ -464,18 +472,31 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
   __shared__ Ranker L;
   if (offs && threadIdx.x < B) L.run[threadIdx.x] = offs[(size_t)threadIdx.x * nblocks + blockIdx.x];
   const size_t base = (size_t)blockIdx.x * DTILE;
+  // (keep-input: the first slot of this rank's own bucket)
+  const u32 keep_first = (MODE == SEND && fmt == FMT_NARROW && R.keep_me != NO_KEEP) ? offs[(size_t)R.keep_me * nblocks]
+                                                                                     : 0u;
   bool inv = false;
   for (int r = 0; r < DROUNDS; ++r) {
     const size_t i = base + (size_t)r * DT + threadIdx.x;
     const bool ok = i < n;
     size_t pos = i;
+    u32 bk = 0;
     if (offs) {
       const u32 b = ok ? bucket_of<MODE>(i, R, rec, rb, (fmt & 3) ? 16 : stride) : 0u;
       const bool act = ok && b < B;
       const u32 p = rank_slot(L, r, b, act, B, bits);
       if (!act) continue;  // (a row with an out-of-range bucket is reported by k_dist_count)
       pos = p;
+      bk = b;
     } else if (!ok) {
+      continue;
+    }
+    if (MODE == SEND && fmt == FMT_NARROW && offs && bk == R.keep_me) {
+      // this rank's own row stays in the caller's rows: its index, and the
+      // owner column (the receiver's id) -- not parsed, not copied
+      const u32 o = R.owner[i];
+      R.self_idx[pos - keep_first] = (u32)i;
+      reinterpret_cast<u32*>(out_rec + soa_n * 20)[pos] = (R.dir_local || R.hot) ? local_of(R, o) : o;
       continue;
     }
     if (MODE == SEND && fmt != FMT_RAW) {
@@ -511,15 +532,25 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
       uint4 m;
       if (fmt & 3) {
         uint4 a;
-        if (nar) {
-          a = narrow_tn(R, i);
-          m = make_uint4(R.soa_c[i], 0u, 0u, narrow_cm(R, i));
-        } else {
-          a = reinterpret_cast<const uint4*>(src)[0];
-          m = reinterpret_cast<const uint4*>(src)[1];
-        }
         u32 w[12];
-        format_ts46((u64)a.x | ((u64)a.y << 32), (u64)a.z | ((u64)a.w << 32), m.w & 0xffffu, w);
+        if (nar && R.self_ts && is_self(R, i)) {  // (keep-input: the caller's own row, byte for byte)
+          const size_t k = R.self_idx ? (size_t)R.self_idx[i - R.self_lo] : i - R.self_lo;
+          const uint4* row = reinterpret_cast<const uint4*>(R.self_ts + k * R.self_stride);
+          const uint4 x = row[0], y = row[1], z = row[2];
+          w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+          w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+          w[8] = z.x; w[9] = z.y; w[10] = z.z; w[11] = z.w & 0xffffu;
+          m = make_uint4(R.soa_c[i], 0u, 0u, 0u);
+        } else {
+          if (nar) {
+            a = narrow_tn(R, i);
+            m = make_uint4(R.soa_c[i], 0u, 0u, narrow_cm(R, i));
+          } else {
+            a = reinterpret_cast<const uint4*>(src)[0];
+            m = reinterpret_cast<const uint4*>(src)[1];
+          }
+          format_ts46((u64)a.x | ((u64)a.y << 32), (u64)a.z | ((u64)a.w << 32), m.w & 0xffffu, w);
+        }
         if (!(fmt & FMT_ST8)) {
           uint4* dst = reinterpret_cast<uint4*>(out_ts + pos * out_stride);
           dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -552,6 +583,22 @@ __global__ __launch_bounds__(DT) void k_dist_scatter(
   if (MODE == SEND && fmt != FMT_RAW && invalid && __ballot(inv) && __lane_id() == 0) atomicOr(invalid, 1u);
 }
 
+__global__ void k_owner_over(const u32* __restrict__ owner, size_t n, u32 limit, u32* __restrict__ bad) {
+  // (16-B loads where the column is 16-B aligned; the head and tail one by one)
+  const size_t head = std::min<size_t>(n, ((16 - ((uintptr_t)owner & 15)) & 15) / 4);
+  const size_t nq = (n - head) / 4;
+  const uint4* q = reinterpret_cast<const uint4*>(owner + head);
+  bool b = false;
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = tid; i < nq; i += nt) {
+    const uint4 v = __builtin_nontemporal_load(q + i);
+    b |= (v.x >= limit) | (v.y >= limit) | (v.z >= limit) | (v.w >= limit);
+  }
+  for (size_t i = tid; i < head; i += nt) b |= owner[i] >= limit;
+  for (size_t i = head + nq * 4 + tid; i < n; i += nt) b |= owner[i] >= limit;
+  if (__ballot(b) && __lane_id() == 0) atomicOr(bad, 1u);
+}
+
 // the local owner of every received packed record (evm_dist_ingest): the
 // records stay where they are, only the owner column is written
 __global__ void k_dist_owner(Route R, const char* __restrict__ rec, size_t rb, size_t n, u32* __restrict__ out) {
@@ -579,12 +626,12 @@ __global__ void k_dist_mark(u64* __restrict__ cnt, u32 G, int zero, int err, con
   cnt[p] = v;
 }
 
-__global__ void k_dist_root_pack(const u64* __restrict__ off, const int32_t* __restrict__ pfx, u32 n_owners, u32 per,
-                                 u64* __restrict__ out) {
+__global__ void k_dist_root_pack(const u64* __restrict__ off, const u64* __restrict__ end, const int32_t* __restrict__ pfx,
+                                 u32 n_owners, u32 per, u64* __restrict__ out) {
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < per; o += gridDim.x * blockDim.x) {
     u64 v = 0;
     if (o < n_owners) {
-      const u64 a = off[o], b = off[o + 1];
+      const u64 a = off[o], b = end[o];
       v = (u64)(uint32_t)(pfx[b] ^ pfx[a]) | ((u64)(b > a) << 32);
     }
     out[o] = v;
@@ -860,6 +907,16 @@ struct evm_dist {
   // ingest, return and split_winners read this rank's own rows from it.  Any
   // other writer of `send` must set send_gen = 0 first; the readers check
   // send_gen == route_gen (self_rows_intact) and refuse the call otherwise.
+  // EVM_ROUTE_KEEP_INPUT: the last route left this rank's own rows in the
+  // caller's rows (self_ts; received row self_lo + k is row self_idx[k])
+  const char* self_ts = nullptr;
+  size_t self_stride = 0;
+  u32* self_idx = nullptr;  // (null with self_identity: row k is ts row k)
+  size_t self_idx_cap = 0;  // bytes
+  // world 1, keep-input, no split: the route IS the caller's rows (owner
+  // column included: at world 1 every owner's local id is itself)
+  bool self_identity = false;
+  const u32* self_owner = nullptr;
   uint64_t route_gen = 0;  // routes finished by this rank
   uint64_t send_gen = 0;   // the route whose records `send` holds (0: none)
   char* send = nullptr;  // wire records (send side), device
@@ -922,7 +979,14 @@ Route route_of(const evm_dist* d, const u32* owner, const uint8_t* dest) {
   R.soa_c = nullptr;
   R.self_a = nullptr;
   R.self_b = nullptr;
-  if (d->narrow && d->packed) {  // the last route's three arrays (receive side) and this rank's own rows
+  R.keep_me = NO_KEEP;
+  R.self_idx = d->self_idx;
+  R.self_ts = d->self_ts;
+  R.self_stride = d->self_stride;
+  if (d->self_identity) {  // (the caller's rows as they lie: owner column included)
+    R.soa_c = d->self_owner;
+    R.self_idx = nullptr;
+  } else if (d->narrow && d->packed) {  // the last route's three arrays (receive side) and this rank's own rows
     R.soa_a = d->recv;
     R.soa_b = reinterpret_cast<const u32*>(d->recv + d->n_recv * 16);
     R.soa_c = reinterpret_cast<const u32*>(d->recv + d->n_recv * 20);
@@ -1078,6 +1142,7 @@ void evm_dist_free(evm_ctx* ctx, evm_dist* d) {
   if (ctx) (void)hipStreamSynchronize(ctx->stream);
   delete d->tx;
   if (d->send) (void)hipFree(d->send);
+  if (d->self_idx) (void)hipFree(d->self_idx);
   if (d->recv) (void)hipFree(d->recv);
   if (d->cnt) (void)hipFree(d->cnt);
   if (d->hcnt) (void)hipHostFree(d->hcnt);
@@ -1162,7 +1227,48 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   // no aux and no source indexes wanted: 24-B records (a quarter fewer xGMI
   // and HBM bytes), when every rank asks for them (CNT_WIDE otherwise)
   const bool narrow0 = packed0 && !aux && (flags_in & EVM_ROUTE_NO_SRC);
+  // own rows left in the caller's rows (read there by take / ingest)
+  const bool keep0 = narrow0 && (flags_in & EVM_ROUTE_KEEP_INPUT) && n > 0;
   size_t rb = packed0 ? (narrow0 ? NARROW : PACKED) : stride + META;
+  d->self_identity = false;
+  if (G == 1 && keep0 && !lerr && !dest && !d->hot) {
+    // one rank and the caller keeps its rows: there is nothing to move --
+    // the received rows are the caller's rows as they lie (at world 1 the
+    // directory's local id of every owner is itself); only the owners' range
+    // is checked, as the partition would
+    bool ok = true;
+    if (d->dir_dest) {
+      Scratch S1(ctx);
+      u32* bad = S1.alloc<u32>(1);
+      if (!bad) return EVM_ENOMEM;
+      HIPR(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
+      KLAUNCH(k_owner_over, dim3(grid_for(n / 4, 256, 8192)), dim3(256), owner, n, d->n_dir, bad);
+      u32 hb = 0;
+      HIPR(hipMemcpyAsync(&hb, bad, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+      HIPR(hipStreamSynchronize(ctx->stream));
+      ok = hb == 0;
+    }
+    if (ok) {
+      d->self_off = d->self_row = 0;
+      d->self_lo = 0;
+      d->self_hi = n;
+      d->recv_off[0] = 0;
+      d->recv_off[1] = n;
+      d->stride = stride;
+      d->rb = NARROW;
+      d->packed = d->narrow = 1;
+      d->n_recv = n;
+      d->n_in = n;
+      d->sent[0] = d->recvd[0] = n;
+      d->send_gen = ++d->route_gen;
+      d->self_ts = ts;
+      d->self_stride = stride;
+      d->self_owner = owner;
+      d->self_identity = true;
+      *n_recv = n;
+      return EVM_OK;
+    }
+  }
   Scratch S(ctx);
   u32* flags = S.alloc<u32>(2);  // [0] a destination out of range, [1] a row outside the native domain
   u64* scnt = d->cnt + W_SEND;
@@ -1172,9 +1278,15 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   d->self_row = 0;
   d->packed = d->narrow = 0;
   d->send_gen = 0;  // (rewritten below)
+  d->self_ts = nullptr;
   Route R = route_of(d, owner, dest);
   R.ts = ts;
   R.stride = stride;
+  if (keep0 && !lerr) {
+    lerr = grow(reinterpret_cast<char**>(&d->self_idx), &d->self_idx_cap, n * sizeof(u32));
+    R.keep_me = (u32)d->rank;
+    R.self_idx = d->self_idx;
+  }
   u32* offs = nullptr;
   u32 nblocks = 0;
   d->n_in = 0;
@@ -1305,6 +1417,10 @@ int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, 
   d->n_recv = total;
   d->n_in = n;
   d->send_gen = ++d->route_gen;
+  if (keep0 && narrow) {
+    d->self_ts = ts;
+    d->self_stride = stride;
+  }
   for (u32 p = 0; p < G; ++p) {
     d->sent[p] = hs[p] & CNT_MASK;
     d->recvd[p] = hr[p] & CNT_MASK;
@@ -1370,9 +1486,13 @@ int evm_dist_ingest(evm_ctx* ctx, evm_dist* d, evm_store* store, uint64_t id_bas
   if (n == 0) return EVM_OK;
   if (!flags || !(d->dir_local || d->hot)) return EVM_EINVAL;  // local ids come from the directory / split
   if (!self_rows_intact(d)) return EVM_EINVAL;
+  if (d->self_identity)  // (world 1: the caller's rows and owners, as they lie)
+    return evm_server_ingest(ctx, store, d->self_ts, d->self_stride, n, d->self_owner, id_base, flags);
   const Route R = route_of(d, nullptr, nullptr);
   if (d->packed && d->narrow) {  // the owner column arrived as the store's owner ids
-    const WireSrc w{nullptr, nullptr, R.self_lo, R.self_hi, 0u, 0u, R.soa_a, R.self_a, R.soa_b, R.self_b};
+    const WireSrc w{nullptr,  nullptr,  R.self_lo,  R.self_hi,          0u,         0u,
+                    R.soa_a,  R.self_a, R.soa_b,    R.self_b,           (const uint8_t*)d->self_ts,
+                    (u32)d->self_stride, d->self_idx};
     return server_ingest_wire(ctx, store, w, n, R.soa_c, id_base, flags);
   }
   Scratch S(ctx);
@@ -1422,7 +1542,7 @@ int evm_dist_gather_roots(evm_ctx* ctx, evm_dist* d, const evm_tree* const* tree
     for (u32 k = 0; k < n_trees; ++k) {
       const evm_tree* t = trees[k];
       if (t->n_owners)
-        KLAUNCH(k_dist_root_pack, dim3(grid_for(t->n_owners, 256)), dim3(256), t->off, t->pfx, t->n_owners,
+        KLAUNCH(k_dist_root_pack, dim3(grid_for(t->n_owners, 256)), dim3(256), t->off, t->end, t->pfx, t->n_owners,
                 t->n_owners, mine + at);
       at += t->n_owners;
     }
@@ -1542,6 +1662,7 @@ int evm_dist_merge_trees(evm_ctx* ctx, evm_dist* d, const evm_tree* t, uint32_t 
   const u32 G = (u32)d->world;
   int lerr = EVM_OK;
   if (!t || owner_lo + (uint64_t)count > t->n_owners) lerr = EVM_EINVAL;
+  if (!lerr) lerr = tree_compact(ctx, t);  // (a rank that fails still joins the gathers, flagged)
   u64 ab[2] = {0, 0};
   if (!lerr && count) {
     HIPR(hipMemcpyAsync(&ab[0], t->off + owner_lo, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));

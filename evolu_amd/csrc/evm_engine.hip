@@ -226,6 +226,7 @@ int evm::scan_exclusive(evm_ctx* ctx, Scratch& S, const T* in, size_t n, T* out,
 template int evm::scan_exclusive<u32, OpAdd>(evm_ctx*, Scratch&, const u32*, size_t, u32*, u32*);
 template int evm::scan_exclusive<int32_t, OpXor>(evm_ctx*, Scratch&, const int32_t*, size_t, int32_t*, int32_t*);
 template int evm::scan_exclusive<u64, OpMax>(evm_ctx*, Scratch&, const u64*, size_t, u64*, u64*);
+template int evm::scan_exclusive<u64, OpAdd>(evm_ctx*, Scratch&, const u64*, size_t, u64*, u64*);
 
 template <typename K>
 int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t n, int lo_bit, int hi_bit) {
@@ -506,6 +507,7 @@ static int tree_alloc(evm_ctx* ctx, evm_tree* t, u32 n_owners, uint64_t L) {
   t->n_owners = n_owners;
   t->n_leaves = L;
   t->off = nullptr;
+  t->end = nullptr;
   t->ck = nullptr;
   t->xr = nullptr;
   t->pfx = nullptr;
@@ -518,9 +520,12 @@ static int tree_alloc(evm_ctx* ctx, evm_tree* t, u32 n_owners, uint64_t L) {
   if (!base) return EVM_ENOMEM;
   t->bytes = bytes;
   t->off = reinterpret_cast<unsigned long long*>(base);
+  t->end = t->off + 1;
   t->ck = reinterpret_cast<unsigned long long*>(base + b_off);
   t->xr = reinterpret_cast<int32_t*>(base + b_off + b_ck);
   t->pfx = reinterpret_cast<int32_t*>(base + b_off + b_ck + b_xr);
+  t->cap = L;
+  t->gapped = false;
   return EVM_OK;
 }
 
@@ -580,6 +585,100 @@ int evm::tree_alloc_cap(evm_ctx* ctx, u32 n_owners, uint64_t cap, evm_tree** out
   }
   *out = t;
   return EVM_OK;
+}
+
+int evm::tree_alloc_gapped(evm_ctx* ctx, u32 n_owners, uint64_t cap, evm_tree** out) {
+  evm_tree* t = new evm_tree;
+  t->n_owners = n_owners;
+  t->n_leaves = 0;
+  t->off = t->end = t->ck = nullptr;
+  t->xr = t->pfx = nullptr;
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_off = up(sizeof(u64) * (n_owners + 1)), b_end = up(sizeof(u64) * std::max<u32>(n_owners, 1)),
+               b_ck = up(sizeof(u64) * std::max<uint64_t>(cap, 1)), b_xr = up(sizeof(int32_t) * std::max<uint64_t>(cap, 1)),
+               b_pfx = up(sizeof(int32_t) * (cap + 1));
+  size_t bytes = b_off + b_end + b_ck + b_xr + b_pfx;
+  char* base = static_cast<char*>(block_alloc(ctx, &bytes));
+  if (!base) {
+    delete t;
+    return EVM_ENOMEM;
+  }
+  t->bytes = bytes;
+  t->off = reinterpret_cast<unsigned long long*>(base);
+  t->end = reinterpret_cast<unsigned long long*>(base + b_off);
+  t->ck = reinterpret_cast<unsigned long long*>(base + b_off + b_end);
+  t->xr = reinterpret_cast<int32_t*>(base + b_off + b_end + b_ck);
+  t->pfx = reinterpret_cast<int32_t*>(base + b_off + b_end + b_ck + b_xr);
+  t->cap = cap;
+  t->gapped = true;
+  *out = t;
+  return EVM_OK;
+}
+
+// per owner: its leaf count and its root (the last entry of its own prefix)
+__global__ void k_gap_counts(const u64* __restrict__ off, const u64* __restrict__ end, const int32_t* __restrict__ pfx,
+                             u32 n_owners, u64* __restrict__ cnt, int32_t* __restrict__ root) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
+    const u64 a = off[o], b = end[o];
+    cnt[o] = b - a;
+    root[o] = b > a ? pfx[b] : 0;
+  }
+}
+
+// one wave per owner: its leaves to their compact places; the global
+// exclusive prefix = the XOR of the owners before (carry) ^ its own prefix
+__global__ void k_gap_compact(const u64* __restrict__ off, const u64* __restrict__ end, const u64* __restrict__ ck,
+                              const int32_t* __restrict__ xr, const int32_t* __restrict__ pfx, u32 n_owners,
+                              const u64* __restrict__ pos, const int32_t* __restrict__ carry, u64* __restrict__ o_off,
+                              u64* __restrict__ o_ck, int32_t* __restrict__ o_xr, int32_t* __restrict__ o_pfx) {
+  const u32 lane = threadIdx.x & 63;
+  for (u32 o = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; o < n_owners; o += (gridDim.x * blockDim.x) >> 6) {
+    const u64 a = off[o], L = end[o] - a, w = pos[o];
+    const int32_t c = carry[o];
+    for (u64 k = lane; k < L; k += 64) {
+      o_ck[w + k] = ck[a + k];
+      o_xr[w + k] = xr[a + k];
+      o_pfx[w + k] = c ^ pfx[a + k];
+    }
+    if (lane == 0) o_off[o] = w;
+  }
+}
+
+int evm::tree_compact(evm_ctx* ctx, const evm_tree* tc) {
+  if (!tc || !tc->gapped) return EVM_OK;
+  evm_tree* t = const_cast<evm_tree*>(tc);  // (the same tree, another layout)
+  const u32 O = t->n_owners;
+  Scratch S(ctx);
+  u64* cnt = S.alloc<u64>((size_t)O + 1);
+  int32_t* root = S.alloc<int32_t>((size_t)O + 1);
+  evm_tree nt{};
+  if (!cnt || !root) return EVM_ENOMEM;
+  int st = tree_alloc(ctx, &nt, O, t->n_leaves);
+  if (st) return st;
+  if (O) {
+    KLAUNCH(k_gap_counts, dim3(grid_for(O, 256)), dim3(256), (const u64*)t->off, (const u64*)t->end,
+            (const int32_t*)t->pfx, O, cnt, root);
+    if (!st) st = scan_exclusive<u64, OpAdd>(ctx, S, cnt, O, nt.off, nt.off + O);
+    int32_t* carry = S.alloc<int32_t>((size_t)O + 1);
+    if (!st && !carry) st = EVM_ENOMEM;
+    if (!st) st = scan_exclusive<int32_t, OpXor>(ctx, S, root, O, carry, nt.pfx + t->n_leaves);
+    if (!st)
+      KLAUNCH(k_gap_compact, dim3(grid_for((size_t)O * 64, 256, 1 << 14)), dim3(256), (const u64*)t->off,
+              (const u64*)t->end, (const u64*)t->ck, (const int32_t*)t->xr, (const int32_t*)t->pfx, O,
+              (const u64*)nt.off, (const int32_t*)carry, nt.off, nt.ck, nt.xr, nt.pfx);
+  } else {
+    st = hip_ok(hipMemsetAsync(nt.off, 0, sizeof(u64), ctx->stream));
+    if (!st) st = hip_ok(hipMemsetAsync(nt.pfx, 0, sizeof(int32_t), ctx->stream));
+  }
+  if (st) {
+    block_free(ctx, nt.off, nt.bytes);
+    return st;
+  }
+  block_free(ctx, t->off, t->bytes);  // (stream-ordered: behind the copy)
+  const uint64_t L = t->n_leaves;
+  *t = nt;
+  t->n_leaves = L;
+  return hip_ok(hipGetLastError());
 }
 
 // Builds a tree object from device leaves (ck sorted unique, xr); copies them.
@@ -667,7 +766,8 @@ int evm::fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owne
 // Merges sorted unique leaves (nck, nxr) into `in`; equal keys XOR-combine.
 int evm::merge_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, const u64* nck,
                          const int32_t* nxr, uint64_t L1, evm_tree** out) {
-  int st = EVM_OK;
+  int st = in ? tree_compact(ctx, in) : EVM_OK;
+  if (st) return st;
   const uint64_t L0 = in ? in->n_leaves : 0;
   if (L0 == 0) return tree_finalize(ctx, S, n_owners, nck, nxr, L1, out);
   if (L1 == 0) return tree_finalize(ctx, S, n_owners, in->ck, in->xr, L0, out);
@@ -692,6 +792,7 @@ int evm::merge_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_own
 // ============================================================================
 struct TreeView {
   const u64* off;
+  const u64* end;  // owner o's leaves: [off[o], end[o])
   const u64* ck;
   const int32_t* pfx;
   const int32_t* xr;
@@ -735,7 +836,7 @@ __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owne
   const int sub = threadIdx.x & (DIFF_LANES - 1);
   const u32 groups = gridDim.x * (blockDim.x / DIFF_LANES);
   for (u32 o = (blockIdx.x * blockDim.x + threadIdx.x) / DIFF_LANES; o < n_owners; o += groups) {
-    u64 alo = A.off[o], ahi = A.off[o + 1], blo = B.off[o], bhi = B.off[o + 1];
+    u64 alo = A.off[o], ahi = A.end[o], blo = B.off[o], bhi = B.end[o];
     // root: tree1.hash === tree2.hash (undefined for {})
     const bool ae = ahi > alo, be = bhi > blo;
     int32_t pa_lo = ae ? A.pfx[alo] : 0, pa_hi = ae ? A.pfx[ahi] : 0;
@@ -861,10 +962,10 @@ __global__ __launch_bounds__(256) void k_diff(TreeView A, TreeView B, u32 n_owne
   }
 }
 
-__global__ void k_roots(const u64* __restrict__ off, const int32_t* __restrict__ pfx, u32 n_owners,
-                        int32_t* __restrict__ root, uint8_t* __restrict__ present) {
+__global__ void k_roots(const u64* __restrict__ off, const u64* __restrict__ end, const int32_t* __restrict__ pfx,
+                        u32 n_owners, int32_t* __restrict__ root, uint8_t* __restrict__ present) {
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n_owners; o += gridDim.x * blockDim.x) {
-    const u64 a = off[o], b = off[o + 1];
+    const u64 a = off[o], b = end[o];
     root[o] = pfx[b] ^ pfx[a];
     present[o] = b > a;
   }
@@ -1154,6 +1255,7 @@ int evm_tree_from_device_leaves(evm_ctx* ctx, uint32_t n_owners, const uint64_t*
 int evm_tree_slice(evm_ctx* ctx, const evm_tree* t, uint32_t owner_lo, uint32_t count, uint64_t* off, uint64_t* code,
                    int32_t* xr, uint64_t cap, uint64_t* n_leaves) {
   if (!ctx || !t || !n_leaves || owner_lo + (uint64_t)count > t->n_owners || (count && !off)) return EVM_EINVAL;
+  if (int e = tree_compact(ctx, t)) return e;
   u64 ab[2] = {0, 0};
   HIPR(hipMemcpyAsync(&ab[0], t->off + owner_lo, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipMemcpyAsync(&ab[1], t->off + owner_lo + count, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
@@ -1187,7 +1289,7 @@ int evm_tree_info(const evm_tree* t, uint32_t* n_owners, uint64_t* n_leaves) {
 }
 
 int evm_tree_device(const evm_tree* t, const uint64_t** off, const uint64_t** code, const int32_t** xr) {
-  if (!t) return EVM_EINVAL;
+  if (!t || t->gapped) return EVM_EINVAL;  // (a gapped tree: evm_tree_leaves / slice compact it)
   if (off) *off = (const uint64_t*)t->off;
   if (code) *code = (const uint64_t*)t->ck;
   if (xr) *xr = t->xr;
@@ -1196,6 +1298,7 @@ int evm_tree_device(const evm_tree* t, const uint64_t** off, const uint64_t** co
 
 int evm_tree_leaves(evm_ctx* ctx, const evm_tree* t, uint64_t* off, uint64_t* code, int32_t* xr) {
   if (!ctx || !t) return EVM_EINVAL;
+  if (int e = tree_compact(ctx, t)) return e;
   if (off) HIPR(hipMemcpyAsync(off, t->off, sizeof(u64) * (t->n_owners + 1), hipMemcpyDeviceToHost, ctx->stream));
   if (code && t->n_leaves)
     HIPR(hipMemcpyAsync(code, t->ck, sizeof(u64) * t->n_leaves, hipMemcpyDeviceToHost, ctx->stream));
@@ -1214,8 +1317,7 @@ int evm_tree_roots(evm_ctx* ctx, const evm_tree* t, int32_t* root, uint8_t* pres
   uint8_t* dp = S.alloc<uint8_t>(std::max<u32>(t->n_owners, 1));
   if (!dr || !dp) return EVM_ENOMEM;
   if (t->n_owners == 0) return EVM_OK;
-  KLAUNCH(k_roots, dim3(grid_for(t->n_owners, 256)), dim3(256), t->off, t->pfx, t->n_owners,
-                     dr, dp);
+  KLAUNCH(k_roots, dim3(grid_for(t->n_owners, 256)), dim3(256), t->off, t->end, t->pfx, t->n_owners, dr, dp);
   HIPR(hipMemcpyAsync(root, dr, sizeof(int32_t) * t->n_owners, hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipMemcpyAsync(present, dp, t->n_owners, hipMemcpyDeviceToHost, ctx->stream));
   return hip_ok(hipStreamSynchronize(ctx->stream));
@@ -1224,6 +1326,7 @@ int evm_tree_roots(evm_ctx* ctx, const evm_tree* t, int32_t* root, uint8_t* pres
 int evm_merkle_insert(evm_ctx* ctx, const evm_tree* in, const char* ts, size_t stride, size_t n, const uint32_t* owner,
                       evm_tree** out) {
   if (!ctx || !in || !out || stride < 46 || (n && !ts)) return EVM_EINVAL;
+  if (int e = tree_compact(ctx, in)) return e;
   Scratch S(ctx);
   Info* info = nullptr;
   int st = new_info(ctx, S, &info);
@@ -1250,6 +1353,8 @@ int evm_merkle_insert(evm_ctx* ctx, const evm_tree* in, const char* ts, size_t s
 
 int evm_tree_merge(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, evm_tree** out) {
   if (!ctx || !a || !b || !out || a->n_owners != b->n_owners) return EVM_EINVAL;
+  if (int e = tree_compact(ctx, a)) return e;
+  if (int e = tree_compact(ctx, b)) return e;
   Scratch S(ctx);
   // b's leaves are sorted and unique per owner; equal keys XOR-combine
   const int st = merge_into_tree(ctx, S, a, a->n_owners, (const u64*)b->ck, b->xr, b->n_leaves, out);
@@ -1267,7 +1372,7 @@ int evm_merkle_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t*
 
 int evm::launch_diff(evm_ctx* ctx, const evm_tree* a, const evm_tree* b, int64_t* millis) {
   if (a->n_owners == 0) return EVM_OK;
-  TreeView A{a->off, a->ck, a->pfx, a->xr}, B{b->off, b->ck, b->pfx, b->xr};
+  TreeView A{a->off, a->end, a->ck, a->pfx, a->xr}, B{b->off, b->end, b->ck, b->pfx, b->xr};
   // EVM_OPT_DIFF_GRID: workgroups per CU (fewer owners in flight: each one's lines stay in L2)
   u32 grid = grid_for((size_t)a->n_owners * DIFF_LANES, 256, 1 << 16);
   if (ctx->diff_grid > 0) grid = std::min<u32>(grid, (u32)ctx->diff_grid * (u32)ctx->n_cu);

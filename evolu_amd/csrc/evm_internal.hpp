@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/evm.h"
+#include "evm_device.hpp"
 
 namespace evm {
 struct Info;
@@ -56,14 +57,26 @@ struct evm_ctx {
 
 // One MerkleTree per owner, as sorted unique leaves keyed by
 // ck = owner << 40 | code (code: 20 base-4 digits, see evm_device.hpp).
+//
+// Owner o's leaves are [off[o], end[o]).  A compact tree has end = off + 1
+// (the owners' ranges back to back, pfx one exclusive prefix XOR over all of
+// them).  A GAPPED tree -- what an ingest into an empty store leaves, K5
+// having written each owner's leaves where its messages sat in the batch --
+// has owner ranges with room between them and pfx exclusive per owner
+// (pfx[off[o]] = 0, pfx[end[o]] = the owner's root).  Either way the hash of
+// a node is pfx[hi] ^ pfx[lo] over its owner-local range, which is all the
+// diff and the roots read; every other reader first calls tree_compact.
 struct evm_tree {
   size_t bytes;  // size of the one device block holding the arrays (base = off)
   uint32_t n_owners;
-  uint64_t n_leaves;
-  unsigned long long* off;  // [n_owners + 1] leaf range of each owner
-  unsigned long long* ck;   // [n_leaves]
+  uint64_t n_leaves;  // leaves (a gapped tree: the sum of its owners' ranges)
+  unsigned long long* off;  // [n_owners + 1] leaf range of each owner: [off[o], end[o])
+  unsigned long long* end;  // off + 1, or (gapped) its own [n_owners] array
+  unsigned long long* ck;   // [n_leaves] (gapped: [cap])
   int32_t* xr;    // [n_leaves] XOR of the hashes whose key ends at the leaf
   int32_t* pfx;   // [n_leaves + 1] exclusive prefix XOR of xr (node hash = range XOR)
+  uint64_t cap = 0;     // gapped: leaf slots allocated
+  bool gapped = false;
 };
 
 namespace evm {
@@ -318,6 +331,12 @@ int tree_finalize_dev(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* ck, con
                       uint64_t cap, evm_tree** out);
 int merge_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, const u64* nck, const int32_t* nxr,
                     uint64_t L1, evm_tree** out);
+// A gapped tree with room for `cap` leaves (off, end, ck, xr, pfx all filled by
+// the caller's kernels; n_leaves set by the caller).
+int tree_alloc_gapped(evm_ctx* ctx, u32 n_owners, uint64_t cap, evm_tree** out);
+// A gapped tree made compact in place (same object; nothing to do for a
+// compact one).  Every reader but the diff and the roots calls it first.
+int tree_compact(evm_ctx* ctx, const evm_tree* t);
 int fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u64* ck, u32* h, size_t m,
                    const Info& host_info, evm_tree** out);
 
@@ -338,9 +357,35 @@ struct WireSrc {
   const char* self_tn;
   const u32* cm;
   const u32* self_cm;
+  // EVM_ROUTE_KEEP_INPUT: this rank's own rows never left the caller's rows
+  // -- received row i in [self_lo, self_hi) is ts row self_idx[i - self_lo]
+  const uint8_t* self_ts = nullptr;
+  u32 self_stride = 0;
+  const u32* self_idx = nullptr;
 };
+__device__ __forceinline__ bool wire_self_row(const WireSrc& w, size_t i) {
+  return w.self_ts && i >= w.self_lo && i < w.self_hi;
+}
+// an own row of a keep-input route, as its 12 little-endian words (bytes 46-47 zero)
+__device__ __forceinline__ void wire_self_words(const WireSrc& w, size_t i, u32 (&x)[12]) {
+  const size_t k = w.self_idx ? (size_t)w.self_idx[i - w.self_lo] : i - w.self_lo;  // (null: the rows as they lie)
+  const uint4* row = reinterpret_cast<const uint4*>(w.self_ts + k * w.self_stride);
+  const uint4 a = row[0], b = row[1], c = row[2];
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+  x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  x[8] = c.x; x[9] = c.y; x[10] = c.z; x[11] = c.w & 0xffffu;
+}
 __device__ __forceinline__ void wire_load(const WireSrc& w, size_t i, u64* tc, u64* node, u32* cm) {
   const bool mine = i >= w.self_lo && i < w.self_hi;
+  if (w.self_ts && mine) {  // (parsed here: the same words the route would have sent)
+    u32 x[12];
+    wire_self_words(w, i, x);
+    const Parsed p = parse_ts46(x);
+    *tc = p.tc;
+    *node = p.node;
+    *cm = p.meta & (EVM_META_CASEMASK | EVM_META_VALID);
+    return;
+  }
   if (w.tn) {
     const uint4 v = *reinterpret_cast<const uint4*>(mine ? w.self_tn + (i - w.self_lo) * 16 : w.tn + i * 16);
     *tc = (u64)v.x | ((u64)v.y << 32);

@@ -164,6 +164,7 @@ struct Parser {
 
 extern "C" int evm_tree_to_json(evm_ctx* ctx, const evm_tree* t, uint32_t owner, char* buf, size_t cap, size_t* len) {
   if (!ctx || !t || !len || owner >= t->n_owners) return EVM_EINVAL;
+  if (int e = evm::tree_compact(ctx, t)) return e;
   uint64_t ab[2];
   HIPR(hipMemcpyAsync(ab, t->off + owner, sizeof(ab), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));

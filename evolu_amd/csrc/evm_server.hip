@@ -686,7 +686,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     u32* __restrict__ cnt_new, u32* __restrict__ cnt_leaves, u32* __restrict__ cnt_xor, SvoStatus* __restrict__ status,
     const u32* __restrict__ orig, const u32* __restrict__ list, u32* __restrict__ mid_list, u32* __restrict__ mid1,
     uint8_t* __restrict__ ownbig, u32* __restrict__ n_owner, int flags_preset, u32* __restrict__ mid512,
-    WireSrc wsrc, int skip_stored) {
+    WireSrc wsrc, int skip_stored, int32_t* __restrict__ l_pfx, u64* __restrict__ g_off, u64* __restrict__ g_end) {
   constexpr int PER = CAP / THREADS;
   constexpr int PB = SvoLog2<CAP>::v;
   constexpr u64 PMASK = CAP - 1;
@@ -717,6 +717,9 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   const u64 a = sv.start[s];
   const u64 m = sv.start[s + 1] - a;  // an unsorted owner column (bad ids) may underflow: "big"
   const u64 la = sv.la[s], lb = sv.lb[s];
+  // the segment's new leaves: slots [a + s, a + s + m] (one more than its
+  // messages: room for a gapped tree's owner-local prefix end, l_pfx)
+  const u64 lb0 = a + s;
   // the batch index of share position t (the set is what matters, not its order)
   const u32 cb = sv.cbase ? sv.cbase[s] : SEG_NOBASE;
   auto pidx = [&](u32 t) -> u32 { return cb != SEG_NOBASE ? cb + t : perm[a + t]; };
@@ -736,6 +739,10 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       cnt_new[s] = 0;
       cnt_leaves[s] = (u32)(lb - la);
       cnt_xor[s] = 0;
+      if (g_off) {  // (a deferred segment's pass writes these again)
+        g_off[o] = g_end[o] = lb0;
+        l_pfx[lb0] = 0;
+      }
     }
     return;
   }
@@ -754,13 +761,26 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   if (SRC == SRC_ROWS) {
     // the timestamp rows themselves (no packed records): parse + murmur3 here
     u32 bad = 0;
-    for (int k = 0; k < PER; ++k) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    // double-buffered: row k + 1's loads in flight while row k is parsed
+    // (config 3 K5 2.55 -> 2.50 ms, into a 100M-row store 3.21 -> 2.87 ms)
+    v4u nx{}, ny{}, nz{};
+    auto load_row = [&](int k) {
       const u32 t = threadIdx.x + k * THREADS;
       if (t < m) {
-        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
         const v4u* row = reinterpret_cast<const v4u*>(ts + (size_t)bi[k] * stride);
-        const v4u x = __builtin_nontemporal_load(row), y = __builtin_nontemporal_load(row + 1),
-                  z = __builtin_nontemporal_load(row + 2);
+        nx = __builtin_nontemporal_load(row);
+        ny = __builtin_nontemporal_load(row + 1);
+        nz = __builtin_nontemporal_load(row + 2);
+      }
+    };
+    load_row(0);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const v4u x = nx, y = ny, z = nz;
+      if (k + 1 < PER) load_row(k + 1);
+      const u32 t = threadIdx.x + k * THREADS;
+      if (t < m) {
         const u32 w[12] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y, z.z, z.w & 0xffffu};
         const Parsed p = parse_ts46(w);
         bad |= (p.meta & EVM_META_VALID) ? 0u : 1u;
@@ -779,10 +799,22 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     u32 bad = 0;
     for (int k = 0; k < PER; ++k) {
       const u32 t = threadIdx.x + k * THREADS;
-      if (t < m) {
+      if (t < m && wire_self_row(wsrc, bi[k])) {
+        // a keep-input route's own row: the caller's string, parsed here
+        u32 x[12];
+        wire_self_words(wsrc, bi[k], x);
+        const Parsed p = parse_ts46(x);
+        bad |= (p.meta & EVM_META_VALID) ? 0u : 1u;
+        s_rh[t] = p.rh;
+        s_rl[t] = p.rl;
+        s_h[t] = p.hash;
+        tc[k] = p.tc;
+        tmin = min(tmin, p.tc);
+        tmax = max(tmax, p.tc);
+      } else if (t < m) {
         u64 wtc, wnode;
         u32 cm;
-        wire_load(wsrc, bi[k], &wtc, &wnode, &cm);
+        wire_load(wsrc, bi[k], &wtc, &wnode, &cm);  // (all PER loads up front: 86 -> more VGPRs, 15 % slower)
         u32 w[12];
         format_ts46(wtc, wnode, cm & EVM_META_CASEMASK, w);
         bad |= (cm & EVM_META_VALID) ? 0u : 1u;
@@ -1175,11 +1207,47 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       k = lb_u64(t_ck, la, lb, code);
       dup = k < lb && t_ck[k] == code;
     }
-    l_ck[a + l] = code;
-    l_xr[a + l] = (int32_t)s_lx[l];
-    l_dup[a + l] = dup ? 1 : 0;
+    l_ck[lb0 + l] = code;
+    l_xr[lb0 + l] = (int32_t)s_lx[l];
+    l_dup[lb0 + l] = dup ? 1 : 0;
     dups += dup ? 1u : 0u;
     lx ^= s_lx[l];
+  }
+  if (g_off) {
+    // a gapped tree (the empty store, one segment per owner): the owner's
+    // leaves stay where they are, with their owner-local exclusive prefix XOR
+    // -- each wave scans one contiguous quarter of the leaves 64 at a time
+    // (coalesced stores), carried in from the quarters before it
+    constexpr u32 NW = THREADS / 64;
+    const u32 ch = ((NL + NW - 1) / NW + 63) & ~63u;
+    const u32 l0 = min(NL, wv * ch), l1 = min(NL, l0 + ch);
+    u32 x = 0;
+    for (u32 l = l0 + lane; l < l1; l += 64) x ^= s_lx[l];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d, 64);
+    __syncthreads();  // (tmp: free after the scans above)
+    if (lane == 0) tmp[wv] = x;
+    __syncthreads();
+    u32 carry = 0;
+    for (u32 w = 0; w < wv; ++w) carry ^= tmp[w];
+    for (u32 b = l0; b < l1; b += 64) {  // (wave-uniform bounds: every lane takes part in the shuffles)
+      const u32 l = b + lane;
+      const u32 v = l < l1 ? s_lx[l] : 0u;
+      u32 inc = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(inc, d, 64);
+        if (lane >= (u32)d) inc ^= y;
+      }
+      if (l < l1) l_pfx[lb0 + l] = (int32_t)(carry ^ inc ^ v);
+      carry ^= __shfl(inc, 63, 64);
+    }
+    if (wv == NW - 1 && lane == 0) {  // (the last wave's carry: every leaf)
+      l_pfx[lb0 + NL] = (int32_t)carry;
+      g_off[o] = lb0;
+      g_end[o] = lb0 + NL;
+    }
+    __syncthreads();  // (tmp is read again below)
   }
   u32 dtot;
   block_inclusive_scan<u32>(dups, tmp, OpAdd<u32>(), &dtot);
@@ -1463,14 +1531,16 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     }
   }
   // leaves: union of the tree's and the new ones by code, equal codes XOR-combined
+  // (K5 wrote the segment's new leaves at slots a + s ..)
   const u64 la = sv.la[s], lb = sv.lb[s];
+  const u64 an = a + s;
   const u64 lbase = leaf_pos[s];
   constexpr int PERB = SVO_CAP / SVO_THREADS;
   u32 d[PERB], c = 0;
 #pragma unroll
   for (int r = 0; r < PERB; ++r) {
     const u32 j = threadIdx.x * PERB + r;
-    d[r] = j < NL ? (u32)l_dup[a + j] : 0u;
+    d[r] = j < NL ? (u32)l_dup[an + j] : 0u;
     c += d[r];
   }
   u32 dtot;
@@ -1491,7 +1561,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   u32* eqx = reinterpret_cast<u32*>(k_hi);
   __syncthreads();  // (the rows' LDS keys are dead: the leaf codes take k_tc)
   if (lds_leaves) {
-    for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) k_tc[j] = l_ck[a + j];
+    for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS) k_tc[j] = l_ck[an + j];
     for (u32 j = threadIdx.x; j <= NL; j += SVO_THREADS) hist[j] = 0;
     if (leaves_src)
       for (u32 q = threadIdx.x; q < (u32)TL; q += SVO_THREADS) src[q] = SRC_HOLE;
@@ -1527,7 +1597,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
         if (leaves_src) {
           const u32 q = (u32)(k - la) + j - s_dp[j];
           if (eq) {
-            eqx[j] = (u32)(txr[r] ^ l_xr[a + j]);
+            eqx[j] = (u32)(txr[r] ^ l_xr[an + j]);
             src[q] = (uint16_t)(SVB_NEW | SVB_EQ | j);
           } else {
             src[q] = (uint16_t)(k - la);
@@ -1535,14 +1605,14 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
           continue;
         }
       } else {
-        j = (u32)(lb_u64(l_ck, a, a + NL, code) - a);  // new leaves below this code
-        eq = j < NL && l_ck[a + j] == code;
+        j = (u32)(lb_u64(l_ck, an, an + NL, code) - an);  // new leaves below this code
+        eq = j < NL && l_ck[an + j] == code;
         if (eq) atomicAdd(&s_eq, 1u);
       }
       const u64 w = lbase + (k - la) + j - s_dp[j];
       if (w >= lbase + TL) continue;  // (only when l_dup and the tree disagree: flagged below)
       to_ck[w] = code;
-      to_xr[w] = txr[r] ^ (eq ? l_xr[a + j] : 0);
+      to_xr[w] = txr[r] ^ (eq ? l_xr[an + j] : 0);
     }
   }
   __syncthreads();
@@ -1553,7 +1623,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
   }
   if (leaves_src) {
     for (u32 j = threadIdx.x; j < NL; j += SVO_THREADS)
-      if (!l_dup[a + j]) src[(j - s_dp[j]) + hist[j]] = (uint16_t)(SVB_NEW | j);
+      if (!l_dup[an + j]) src[(j - s_dp[j]) + hist[j]] = (uint16_t)(SVB_NEW | j);
     __syncthreads();
     for (u32 q = threadIdx.x; q < (u32)TL; q += SVO_THREADS)
       if (src[q] == SRC_HOLE) s_bad = 1;
@@ -1575,7 +1645,7 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
           if (e & SVB_NEW) {
             const u32 j = e & (SVB_EQ - 1u);
             vck[r] = k_tc[j];
-            vxr[r] = (e & SVB_EQ) ? (int32_t)eqx[j] : l_xr[a + j];
+            vxr[r] = (e & SVB_EQ) ? (int32_t)eqx[j] : l_xr[an + j];
           } else {
             vck[r] = t_ck[la + e];
             vxr[r] = t_xr[la + e];
@@ -1592,13 +1662,13 @@ __global__ __launch_bounds__(SVO_THREADS) void k_svo_b(
     }
   }
   for (u32 j = threadIdx.x; !leaves_src && j < NL; j += SVO_THREADS) {
-    if (l_dup[a + j]) continue;
-    const u64 code = lds_leaves ? k_tc[j] : l_ck[a + j];
+    if (l_dup[an + j]) continue;
+    const u64 code = lds_leaves ? k_tc[j] : l_ck[an + j];
     const u64 below = lds_leaves ? (u64)hist[j] : lb_u64(t_ck, la, lb, code) - la;
     const u64 w = lbase + (j - s_dp[j]) + below;
     if (w >= lbase + TL) continue;
     to_ck[w] = code;
-    to_xr[w] = l_xr[a + j];
+    to_xr[w] = l_xr[an + j];
   }
   if (threadIdx.x == 0) {
     if (s == 0 || seg_owner(sv, s - 1) != o) {  // the owner's first segment starts its rows and leaves
@@ -1668,8 +1738,8 @@ __global__ __launch_bounds__(64 * SVC_WAVES) void k_svo_copy(
 #pragma unroll
     for (int r = 0; r < SVB_B; ++r) {
       const u32 j = j0 + r * 64;
-      vck[r] = j < NL ? l_ck[a + j] : 0ull;
-      vxr[r] = j < NL ? l_xr[a + j] : 0;
+      vck[r] = j < NL ? l_ck[a + s + j] : 0ull;  // (K5's slots for the segment's new leaves)
+      vxr[r] = j < NL ? l_xr[a + s + j] : 0;
     }
 #pragma unroll
     for (int r = 0; r < SVB_B; ++r) {
@@ -2225,8 +2295,9 @@ __global__ void k_widen(const u32* __restrict__ a, size_t n, u64* __restrict__ b
 
 // segment b's owner and the first stored row / tree leaf of its minute range
 __global__ void k_seg_ranges(const u32* __restrict__ bbase, const u32* __restrict__ spoff, const u32* __restrict__ sp,
-                             u32 O, u32 NS, StoreView st, const u64* __restrict__ t_off, const u64* __restrict__ t_ck,
-                             u32* __restrict__ sowner, u64* __restrict__ sa, u64* __restrict__ la) {
+                             u32 O, u32 NS, StoreView st, const u64* __restrict__ t_off, const u64* __restrict__ t_end,
+                             const u64* __restrict__ t_ck, u32* __restrict__ sowner, u64* __restrict__ sa,
+                             u64* __restrict__ la) {
   for (u32 b = blockIdx.x * blockDim.x + threadIdx.x; b < NS; b += gridDim.x * blockDim.x) {
     const u32 o = upper_u32(bbase, O + 1, b) - 1;
     const u32 k = b - bbase[o];
@@ -2241,21 +2312,21 @@ __global__ void k_seg_ranges(const u32* __restrict__ bbase, const u32* __restric
         if (st.tc[mid] < tc0) r0 = mid + 1;
         else hi = mid;
       }
-      l0 = lb_u64(t_ck, l0, t_off[o + 1], ((u64)o << 40) | minute_code(mlo));
+      l0 = lb_u64(t_ck, l0, t_end[o], ((u64)o << 40) | minute_code(mlo));
     }
     sa[b] = r0;
     la[b] = l0;
   }
 }
 
-__global__ void k_seg_ends(const u32* __restrict__ sowner, u32 NS, StoreView st, const u64* __restrict__ t_off,
+__global__ void k_seg_ends(const u32* __restrict__ sowner, u32 NS, StoreView st, const u64* __restrict__ t_end,
                            const u64* __restrict__ sa, const u64* __restrict__ la, u64* __restrict__ sb,
                            u64* __restrict__ lb) {
   for (u32 b = blockIdx.x * blockDim.x + threadIdx.x; b < NS; b += gridDim.x * blockDim.x) {
     const u32 o = sowner[b];
     const bool next = b + 1 < NS && sowner[b + 1] == o;
     sb[b] = next ? sa[b + 1] : st.off[o + 1];
-    lb[b] = next ? la[b + 1] : t_off[o + 1];
+    lb[b] = next ? la[b + 1] : t_end[o];
   }
 }
 
@@ -2369,13 +2440,9 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   u64* n_hi = S.alloc<u64>(n);
   u32* n_lo = S.alloc<u32>(n);
   u64* n_id = S.alloc<u64>(n);
-  u64* l_ck = S.alloc<u64>(n);
-  int32_t* l_xr = S.alloc<int32_t>(n);
-  uint8_t* l_dup = S.alloc<uint8_t>(n);
   u32* tot = S.alloc<u32>(2);
   uint8_t* ownbig = S.alloc<uint8_t>(O);
-  if (!seg || !status || !n_tc || !n_hi || !n_lo || !n_id || !l_ck || !l_xr || !l_dup || !tot || !ownbig)
-    return EVM_ENOMEM;
+  if (!seg || !status || !n_tc || !n_hi || !n_lo || !n_id || !tot || !ownbig) return EVM_ENOMEM;
   const int obits = O > 1 ? 32 - __builtin_clz(O - 1) : 0;
   // requests arrive as runs of one owner (index.ts:224-248): sort the runs,
   // not the messages, when they are long enough
@@ -2419,7 +2486,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   u32* soff = S.alloc<u32>((size_t)O + 1);
   u32* spoff = S.alloc<u32>((size_t)O + 1);
   if (!nb || !nsm || !nsp || !bbase || !soff || !spoff) return EVM_ENOMEM;
-  SegView sv{nullptr, seg, s->off, s->off + 1, t->off, t->off + 1};
+  SegView sv{nullptr, seg, s->off, s->off + 1, t->off, t->end};  // (a gapped tree: its owners' ranges as they lie)
   u32 NS = O;
   const u32* kperm = ov;  // batch indices, segment by segment
   bool split = false;
@@ -2592,12 +2659,34 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if ((st = radix_sort_pairs<u32>(ctx, S, bk, bv, n, 0, std::max(1, ceil_log2((size_t)NS + 1))))) return st;
     KLAUNCH(k_seg_start, dim3(grid_for((size_t)NS + 1, 256)), dim3(256), bk, n, NS, sstart);
     KLAUNCH(k_seg_ranges, dim3(grid_for(NS, 256)), dim3(256), bbase, spoff, sp, O, NS, view_of(s), (const u64*)t->off,
-            (const u64*)t->ck, sown, ssa, sla);
-    KLAUNCH(k_seg_ends, dim3(grid_for(NS, 256)), dim3(256), sown, NS, view_of(s), (const u64*)t->off, ssa, sla, ssb,
+            (const u64*)t->end, (const u64*)t->ck, sown, ssa, sla);
+    KLAUNCH(k_seg_ends, dim3(grid_for(NS, 256)), dim3(256), sown, NS, view_of(s), (const u64*)t->end, ssa, sla, ssb,
             slb);
     sv = SegView{sown, sstart, ssa, ssb, sla, slb};
     kperm = bv;
   }
+  // K5's new leaves: segment s's at slots [start + s, start + s + m] (n + NS + 1 in all).
+  // Into an empty store with one segment per owner they are the new tree
+  // itself, gapped (evm_tree): each owner's leaves where K5 wrote them, with
+  // its owner-local prefix XOR -- no copy pass (adopted below when every
+  // message was inserted; otherwise k_svo_copy compacts them as before).
+  const size_t n_slots = n + (size_t)NS + 1;
+  evm_tree* gt = nullptr;
+  struct GapGuard {
+    evm_ctx* ctx;
+    evm_tree*& t;
+    ~GapGuard() {
+      if (t) tree_destroy(ctx, t);
+    }
+  } gap_guard{ctx, gt};
+  if (s->n == 0 && t->n_leaves == 0 && !split && (st = tree_alloc_gapped(ctx, O, n_slots, &gt))) return st;
+  u64* l_ck = gt ? (u64*)gt->ck : S.alloc<u64>(n_slots);
+  int32_t* l_xr = gt ? gt->xr : S.alloc<int32_t>(n_slots);
+  uint8_t* l_dup = S.alloc<uint8_t>(n_slots);
+  if (!l_ck || !l_xr || !l_dup) return EVM_ENOMEM;
+  int32_t* l_pfx = gt ? gt->pfx : nullptr;
+  u64* g_off = gt ? (u64*)gt->off : nullptr;
+  u64* g_end = gt ? (u64*)gt->end : nullptr;
   u32* cnt = S.alloc<u32>(4 * (size_t)NS + 1);  // rows, new leaves, merged leaves, new leaves' XOR (per segment)
   u32* pos = S.alloc<u32>(2 * (size_t)NS);  // row / leaf offsets
   u32* mid = S.alloc<u32>((size_t)NS + 1);  // [count, segments whose share is in (1024, SVO_CAP]]
@@ -2646,7 +2735,7 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
 #define SVO_ARGS                                                                                                      \
   rec, tsb, stride, info, kperm, sv, view_of(s), (const u64*)t->ck, (u64)id_base, flags, n_tc, n_hi, n_lo, n_id, l_ck, \
       l_xr, l_dup, c_rows, c_new, c_leaves, c_xor, status, orig, list, l2, l1, ownbig, n_owner, preset, l512, wsrc,  \
-      skip_stored
+      skip_stored, l_pfx, g_off, g_end
     // (the one-wave kernels: Zipf-tail owners of <= 128 / <= 256 messages, no cross-wave barriers;
     // source: true = the rows, false = packed records, SRC_WIRE = received records)
 // (the 1,024 kernel with 512 threads, two messages each, measured slower:
@@ -2743,6 +2832,20 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   }
   // new store and tree, exactly sized
   const int in_place = (n_owner && ht[0] == n) ? 1 : 0;
+  if (in_place && gt && !hs.big) {
+    // every message inserted, one segment per owner: K5 left the final rows
+    // (at their batch positions: the owner offsets are the segment starts)
+    // and the final gapped tree -- nothing is copied
+    *ns = pre;
+    ns->n = n;
+    pre = evm_store{};
+    HIPR(hipMemcpyAsync(ns->off, seg, sizeof(u64) * ((size_t)O + 1), hipMemcpyDeviceToDevice, ctx->stream));
+    gt->n_leaves = ht[1];
+    *new_tree = gt;
+    gt = nullptr;
+    *done = true;
+    return hip_ok(hipGetLastError());
+  }
   if (in_place) {
     *ns = pre;  // adopt the pre-allocated store (its rows are final)
     ns->n = n;

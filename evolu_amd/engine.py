@@ -614,14 +614,20 @@ class Dist:
         return dest[:n], local[:n]
 
     def route(self, ts: torch.Tensor, owner: torch.Tensor, aux: Optional[torch.Tensor] = None,
-              dest: Optional[torch.Tensor] = None, need_src: bool = True) -> int:
+              dest: Optional[torch.Tensor] = None, need_src: bool = True, keep_input: bool = False) -> int:
         """Collective: rows to rank dest (default owner % world) -> rows received.
         need_src=False (every rank alike): take() will not return sources and no
         send_back / split_winners follows -- without aux the rows travel as
-        24-B records (evm_dist_route_ex, EVM_ROUTE_NO_SRC)."""
+        24-B records (evm_dist_route_ex, EVM_ROUTE_NO_SRC).  keep_input=True
+        (with need_src=False): `ts` stays valid and unchanged until the last
+        take() / ingest() of this route, which read this rank's own rows there
+        (EVM_ROUTE_KEEP_INPUT: the route neither parses nor copies them)."""
         n, stride = ts.shape
         nr = C.c_uint64()
         flags = 0 if need_src else _lib.ROUTE_NO_SRC
+        if keep_input and not need_src:
+            flags |= _lib.ROUTE_KEEP_INPUT
+            self._kept = (ts, owner)  # (alive until the next route: take / ingest read them)
         check(self.eng.lib.evm_dist_route_ex(self.eng.h, self.h, _ptr(ts), stride, n, _ptr(owner), _ptr(aux),
                                              _ptr(dest), flags, C.byref(nr)), "evm_dist_route")
         self.n_recv = nr.value

@@ -98,7 +98,8 @@ class ShardedServer:
     def route(self, ts: torch.Tensor, owner: torch.Tensor, out=None):
         """Rows (global owner ids) of this rank's slice -> the rows of this
         rank's owners from every rank: (ts, local owner int32), batch order."""
-        n = self.dd.route(ts, owner, need_src=False)  # (24-B records: no aux, no sources)
+        # (24-B records: no aux, no sources; this rank's own rows read from ts by the take)
+        n = self.dd.route(ts, owner, need_src=False, keep_input=True)
         t, o, _, _, _ = self.dd.take(aux=False, src=False, out=out)
         return t[:n], o[:n]
 
@@ -117,8 +118,10 @@ class ShardedServer:
         """addMessages for a round without rebuilding the received rows:
         route (24-B records) + evm_dist_ingest into this rank's store.
         Returns the flags in receive order (ids id_base + receive index);
-        `take_routed` gives the rows themselves when a caller needs them."""
-        self.dd.route(ts, owner, need_src=False)
+        `take_routed` gives the rows themselves when a caller needs them
+        (this rank's own rows are read from `ts` by the ingest and by
+        take_routed: the caller keeps it until then)."""
+        self.dd.route(ts, owner, need_src=False, keep_input=True)
         if self.store is None:
             self.new_store()
         return self.dd.ingest(self.store, id_base, flags)

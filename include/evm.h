@@ -450,6 +450,14 @@ int evm_dist_route(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, siz
  * is set, else the global id), so evm_dist_ingest reads the owner column as
  * it arrives. */
 #define EVM_ROUTE_NO_SRC 1u
+/* EVM_ROUTE_KEEP_INPUT (with EVM_ROUTE_NO_SRC): the caller keeps `ts` and
+ * `owner` valid and unchanged until the route's last evm_dist_take /
+ * evm_dist_ingest.  On a 24-B route this rank's own rows are then neither
+ * parsed nor copied by the route (at world 1 without a split: nothing moves at
+ * all -- the received rows and owner ids are the caller's as they lie): take
+ * copies them from `ts`, ingest parses them there.  A row of them outside the native domain is then found by the
+ * ingest (EVM_ENONCANON, flagged), not by the route's format vote. */
+#define EVM_ROUTE_KEEP_INPUT 2u
 int evm_dist_route_ex(evm_ctx* ctx, evm_dist* d, const char* ts, size_t stride, size_t n, const uint32_t* owner,
                       const uint32_t* aux, const uint8_t* dest, uint32_t flags, uint64_t* n_recv);
 /* local: the last route's rows into caller buffers (device): out_ts rows of

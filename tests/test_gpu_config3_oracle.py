@@ -71,8 +71,11 @@ def test_config3_shape_and_reingest_vs_c_oracle(eng):
     store = eng.store_new(O_)
     (f1, st1), rep1 = _ran(eng, lambda: store.ingest(t1, o1, 0))
     assert st1 == 0 and "(k_svo_a<1024, true>)" in rep1, sorted(rep1)
-    assert "k_svo_copy" in rep1, sorted(rep1)  # the empty store's commit (prefix XOR included)
-    from tests.test_gpu_server import _check_prefix_xor
+    # the empty store's commit: nothing -- K5 left the rows and a gapped tree in place
+    assert "k_svo_copy" not in rep1 and "k_svo_b<false>" not in rep1, sorted(rep1)
+    from tests.test_gpu_server import _check_prefix_xor, _is_gapped
+
+    assert _is_gapped(eng, store.tree())
 
     _check_prefix_xor(eng, store.tree())
     assert np.array_equal(f1.cpu().numpy(), f1_want)

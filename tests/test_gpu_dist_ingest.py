@@ -39,7 +39,7 @@ def _slices(world, n_owners, grouped, seed):
     return out
 
 
-def _run(world, grouped, need_src, invalid=False, hot=False, path=0):
+def _run(world, grouped, need_src, invalid=False, hot=False, path=0, keep=False):
     from evolu_amd import _lib as L
     from evolu_amd import synth
     from evolu_amd.engine import run_loopback
@@ -60,7 +60,8 @@ def _run(world, grouped, need_src, invalid=False, hot=False, path=0):
         ts, owner = slices[r]
         if hot:
             sv.set_hot([0, 7])
-        n = dd.route(eng.dev(ts), eng.dev(owner), need_src=need_src)
+        t_in = eng.dev(ts)
+        n = dd.route(t_in, eng.dev(owner), need_src=need_src, keep_input=keep)
         a = eng.store_new(sv.n_local)
         st_a = L.EVM_OK
         fa = torch.empty(max(n, 1), dtype=torch.uint8, device=torch.device("cuda", eng.device))
@@ -122,3 +123,35 @@ def test_dist_ingest_raw_records_flag_the_culprit():
     res = _run(2, False, False, invalid=True)
     _check(res, ok=False)
     assert any(out["st"][0] == L.EVM_ENONCANON for out in res)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("grouped", [False, True])
+def test_keep_input_route_equals_copied_route(world, grouped):
+    """EVM_ROUTE_KEEP_INPUT: this rank's own rows are neither parsed nor
+    copied by the route; take and ingest read them from the caller's rows.
+    Flags, stored rows and trees equal the route that copies them, and take
+    + ingest equals the dist ingest."""
+    a = _run(world, grouped, False, keep=True)
+    _check(a)
+    b = _run(world, grouped, False, keep=False)
+    for x, y in zip(a, b):
+        assert x["n"] == y["n"] and x["st"] == y["st"]
+        assert np.array_equal(x["flags"][0], y["flags"][0])
+        for u, v in zip(x["msgs"][0], y["msgs"][0]):
+            assert np.array_equal(u, v)
+        for u, v in zip(x["tree"][0], y["tree"][0]):
+            assert np.array_equal(u, v)
+
+
+def test_keep_input_invalid_own_row_is_flagged_by_the_ingest():
+    """With the own rows left unparsed, a row of them outside the native
+    domain does not send the route raw: the ingest finds it (EVM_ENONCANON,
+    the row flagged EVM_MSG_BAD), exactly as take + evm_server_ingest."""
+    from evolu_amd import _lib as L
+
+    res = _run(1, False, False, invalid=True, keep=True)
+    _check(res, ok=False)
+    st_a, _ = res[0]["st"]
+    assert st_a == L.EVM_ENONCANON
+    assert res[0]["flags"][0][5] == L.MSG_BAD

@@ -404,16 +404,16 @@ def test_big_owner_tie_runs(eng, run):
 
 
 def _check_prefix_xor(eng, tree):
-    """The tree's prefix XOR (written by the empty store's copy kernel, or by
-    the scan after a merge) against its own leaves: every owner's root is
+    """The tree's prefix XOR (written by K5 for a gapped tree, by the empty
+    store's copy kernel, or by the scan after a merge) against its own leaves: every owner's root is
     the XOR of its leaves, and a diff with the same leaves rebuilt through
     evm_tree_from_leaves (whose prefix is a scan) finds nothing at any level."""
     from evolu_amd import _lib as L
 
+    r, _ = tree.roots()  # (read as the tree is: gapped -- owner-local prefix -- or compact)
     off, code, xr = tree.leaves()
     px = np.concatenate([[0], np.bitwise_xor.accumulate(xr.astype(np.int32))]).astype(np.int32)
     o = off.astype(np.int64)
-    r, _ = tree.roots()
     assert np.array_equal(r, px[o[1:]] ^ px[o[:-1]])
     same = eng.tree_from_leaves(off, code, xr)
     assert (eng.merkle_diff(tree, same).cpu().numpy() == L.DIFF_NONE).all()
@@ -471,3 +471,85 @@ def test_merge_paths_by_segment_size(eng, seed):
         assert [int(k) for k in ids[off[o]:off[o + 1]]] == [id_of[(s, o)] for s in rows]
         assert store.tree().to_json(o) == srv.tree_json(o)
     assert store.n_messages == len(set(both))
+
+
+def _is_gapped(eng, tree):
+    import ctypes as C
+
+    from evolu_amd import _lib as L
+
+    p = C.c_void_p()
+    return eng.lib.evm_tree_device(tree.h, C.byref(p), C.byref(p), C.byref(p)) == L.EVM_EINVAL
+
+
+def test_gapped_tree_reads_equal_compact(eng):
+    """An ingest into an empty store of one request per owner, every message
+    inserted, leaves a GAPPED tree (each owner's leaves where K5 wrote them,
+    owner-local prefix XOR; no copy pass).  Its roots and diffs, read gapped,
+    equal the same reads after it is compacted, and the compacted leaves
+    equal the sort path's tree; a second ingest into that store (which
+    compacts first) equals the sort path's two ingests."""
+    from evolu_amd import _lib as L
+    from evolu_amd import synth
+
+    n_owners, per = 400, 250
+    ts, own, millis = synth.config3(n_owners, per, request=per, seed_config=91)
+    ts2, own2, _ = synth.config3(n_owners, per, request=per, seed_config=92)
+    store = eng.store_new(n_owners)
+    f, _ = store.ingest(eng.dev(ts), eng.dev(own), 0)
+    assert int((f.cpu().numpy() & L.MSG_INS).astype(bool).sum()) == len(ts)
+    tree = store.tree()
+    assert _is_gapped(eng, tree)
+    # client trees: each owner's first 90 % by time (config 3)
+    o64 = own.astype(np.int64)
+    order = np.lexsort((millis, o64))
+    rank = np.empty(len(order), dtype=np.int64)
+    cnt = np.bincount(o64, minlength=n_owners)
+    rank[order] = np.arange(len(order)) - (np.cumsum(cnt) - cnt)[o64[order]]
+    keep = rank < (0.9 * cnt[o64]).astype(np.int64)
+    client = eng.merkle_insert(eng.tree_new(n_owners), eng.dev(np.ascontiguousarray(ts[keep])),
+                               eng.dev(np.ascontiguousarray(own[keep])))
+    r_gap, p_gap = tree.roots()
+    d_gap = eng.merkle_diff(tree, client).cpu().numpy()
+    d_gap_rev = eng.merkle_diff(client, tree).cpu().numpy()
+    node = eng.dev(np.frombuffer(b"0123456789abcdef" * n_owners, dtype=np.uint8).copy())
+    s_diff, s_off, s_ids = store.select(client, node)
+    s_diff, s_off, s_ids = s_diff.cpu().numpy(), s_off.cpu().numpy(), s_ids.cpu().numpy()
+    assert _is_gapped(eng, tree)  # (diff, roots and select read it as it is)
+    off, code, xr = tree.leaves()  # compacts
+    assert not _is_gapped(eng, tree)
+    r_c, p_c = tree.roots()
+    assert np.array_equal(r_gap, r_c) and np.array_equal(p_gap, p_c)
+    assert np.array_equal(d_gap, eng.merkle_diff(tree, client).cpu().numpy())
+    assert np.array_equal(d_gap_rev, eng.merkle_diff(client, tree).cpu().numpy())
+    assert (d_gap >= 0).all()
+    # against the sort path
+    eng.set_option(L.OPT_SERVER_PATH, 2)
+    ref = eng.store_new(n_owners)
+    ref.ingest(eng.dev(ts), eng.dev(own), 0)
+    eng.set_option(L.OPT_SERVER_PATH, 0)
+    ro, rc, rx = ref.tree().leaves()
+    assert np.array_equal(off, ro) and np.array_equal(code, rc) and np.array_equal(xr, rx)
+    r_ref, _ = ref.tree().roots()
+    assert np.array_equal(r_ref, r_gap)
+    d2, o2, i2 = ref.select(client, node)
+    assert np.array_equal(d2.cpu().numpy(), s_diff) and np.array_equal(o2.cpu().numpy(), s_off)
+    assert np.array_equal(i2.cpu().numpy(), s_ids)
+    for o in (0, 7, n_owners - 1):
+        assert tree.to_json(o) == ref.tree().to_json(o)
+    # a second round: the gapped store compacts, then merges
+    fresh = eng.store_new(n_owners)
+    fresh.ingest(eng.dev(ts), eng.dev(own), 0)
+    assert _is_gapped(eng, fresh.tree())
+    fa, _ = fresh.ingest(eng.dev(ts2), eng.dev(own2), 1 << 40)
+    eng.set_option(L.OPT_SERVER_PATH, 2)
+    fb, _ = ref.ingest(eng.dev(ts2), eng.dev(own2), 1 << 40)
+    eng.set_option(L.OPT_SERVER_PATH, 0)
+    assert np.array_equal(fa.cpu().numpy(), fb.cpu().numpy())
+    for x, y in zip(fresh.tree().leaves(), ref.tree().leaves()):
+        assert np.array_equal(x, y)
+    for x, y in zip(fresh.messages(), ref.messages()):
+        assert np.array_equal(x, y)
+    for t in (store, ref, fresh):
+        t.free()
+    client.free()
