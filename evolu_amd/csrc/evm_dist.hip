@@ -587,11 +587,12 @@ __global__ void k_owner_over(const u32* __restrict__ owner, size_t n, u32 limit,
   // (16-B loads where the column is 16-B aligned; the head and tail one by one)
   const size_t head = std::min<size_t>(n, ((16 - ((uintptr_t)owner & 15)) & 15) / 4);
   const size_t nq = (n - head) / 4;
-  const uint4* q = reinterpret_cast<const uint4*>(owner + head);
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u* q = reinterpret_cast<const v4u*>(owner + head);
   bool b = false;
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (size_t)gridDim.x * blockDim.x;
   for (size_t i = tid; i < nq; i += nt) {
-    const uint4 v = __builtin_nontemporal_load(q + i);
+    const v4u v = __builtin_nontemporal_load(q + i);
     b |= (v.x >= limit) | (v.y >= limit) | (v.z >= limit) | (v.w >= limit);
   }
   for (size_t i = tid; i < head; i += nt) b |= owner[i] >= limit;
