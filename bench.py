@@ -141,6 +141,7 @@ def parse():
                     help="config4 (or --workload config5 / config5c) rehearsal: N loopback ranks (threads) sharing "
                          "GPU 0 through evm_dist_hub (not a multi-GPU measurement)")
     ap.add_argument("--extra", type=int, default=1, help="N=1 client run: add the config-1 and config-3 legs")
+    ap.add_argument("--e2e", type=int, default=1, help="config 3 leg: add the end-to-end SyncServer round")
     ap.add_argument("--shape", choices=["auto", "config2", "config4c"], default="auto",
                     help="client workload: config2 = one owner per GPU, no exchange; config4c = owners_per_rank "
                          "owners per GPU, every rank's batch holds messages of all the job's owners and routes them "
@@ -1866,6 +1867,91 @@ def reingest(eng, a, ts1, own1, owners, per_owner, request, flags):
             "kernels_ms": {k: v[0] for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:10]}}
 
 
+def e2e_bodies(eng, ts_np, owner_np, client, node16=b"0123456789abcdef", content_bytes=16):
+    """The config-3 round as the server receives it: one SyncRequest body per
+    request run of ts_np (one owner each), userId = the owner as 21 hex
+    chars, nodeId = node16, merkleTree = the owner's client tree (JSON by the
+    device emitter), contents = content_bytes per message -- encoded on host
+    threads (evm_pb_encode_requests).  -> (arena uint8, offsets uint64[R + 1])."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from evolu_amd import _lib as L
+
+    lib = L.load()
+    n = len(ts_np)
+    starts = np.flatnonzero(np.r_[True, owner_np[1:] != owner_np[:-1]])
+    R = len(starts)
+    msg_off = np.r_[starts, n].astype(np.uint64)
+    req_owner = owner_np[starts].astype(np.int64)
+    users = np.frombuffer("".join("%021x" % o for o in req_owner).encode(), dtype=np.uint8)
+    user_off = (np.arange(R + 1, dtype=np.uint64) * 21)
+    nodes = np.frombuffer(node16 * R, dtype=np.uint8)
+    node_off = np.arange(R + 1, dtype=np.uint64) * len(node16)
+    jb, jo = client.to_json_batch(torch.from_numpy(req_owner.astype(np.int32)).to("cuda:%d" % eng.device))
+    jb, jo = jb.cpu().numpy(), np.ascontiguousarray(jo.cpu().numpy(), dtype=np.uint64)
+    content = np.arange(n * content_bytes // 8 + 1, dtype=np.uint64).view(np.uint8)
+    content_off = np.arange(n + 1, dtype=np.uint64) * content_bytes
+    p = lambda x: C.c_void_p(x.ctypes.data)  # noqa: E731
+    ts_c = np.ascontiguousarray(ts_np)
+    args = [R, p(msg_off), p(ts_c), ts_c.shape[1], p(content_off), p(content), p(users), p(user_off), p(nodes),
+            p(node_off), p(jb), p(jo)]
+    off = np.zeros(R + 1, dtype=np.uint64)
+    L.check(lib.evm_pb_encode_requests(*args, None, p(off)), "evm_pb_encode_requests")
+    arena = np.empty(int(off[-1]), dtype=np.uint8)
+    L.check(lib.evm_pb_encode_requests(*args, p(arena), p(off)), "evm_pb_encode_requests")
+    return arena, off
+
+
+def e2e_leg(eng, ts_np, owner_np, client, device_ms, sample=8):
+    """BASELINE config 3 end to end: every owner's SyncRequest body through
+    evolu_amd.server.SyncServer (index.ts:204-251: parseBody, addMessages,
+    getMessages, SyncResponse.toBinary) into an empty store, bodies in host
+    memory to response bodies in host memory, timed by part (SyncServer.timing:
+    protobuf decode, ingest incl. H2D, client-tree JSON parse, selection,
+    the trees' JSON on the device + D2H, response encode).  Self-check: a
+    sample of the requests through the per-request path on a fresh server
+    gives the same bytes (the byte compare against the oracle's ServerDb.sync
+    is tests/test_gpu_wire.py::test_e2e_bodies_vs_oracle, same generator)."""
+    import numpy as np
+
+    from evolu_amd.server import SyncServer
+
+    t0 = time.perf_counter()
+    arena, off = e2e_bodies(eng, ts_np, owner_np, client)
+    gen_s = time.perf_counter() - t0
+    R = len(off) - 1
+    O = int(owner_np.max()) + 1
+    srv = SyncServer(eng, O)
+    t0 = time.perf_counter()
+    out = srv.sync_arena(arena, off)
+    wall = time.perf_counter() - t0
+    timing = dict(srv.timing)
+    ok = sum(1 for x in out if isinstance(x, memoryview))
+    resp_bytes = sum(len(x) for x in out if isinstance(x, memoryview))
+    pick = np.linspace(0, R - 1, min(sample, R)).round().astype(np.int64)
+    ref = SyncServer(eng, O)
+    same = True
+    for k in pick:
+        body = arena[int(off[k]):int(off[k + 1])].tobytes()
+        (r,) = ref.sync_per_request([body])
+        same = same and isinstance(r, bytes) and bytes(out[k]) == r
+    ref.close()
+    srv.close()
+    n = len(ts_np)
+    return {"workload": "config 3 end to end: %d SyncRequest bodies (%d owners x %d msgs, %d-B contents, the "
+                        "client's tree JSON) -> SyncServer.sync -> %d SyncResponse bodies, into an empty store"
+                        % (R, R, n // max(R, 1), 16, R),
+            "ms": wall * 1e3, "msgs_per_s": n / wall, "device_step_ms": device_ms,
+            "ratio_to_device_step": wall * 1e3 / device_ms if device_ms else None,
+            "ms_by_part": {k: v * 1e3 for k, v in timing.items()},
+            "request_bytes": int(off[-1]), "response_bytes": int(resp_bytes), "responses": ok,
+            "host_threads": os.environ.get("EVM_HOST_THREADS", "default (<= 16)"),
+            "bodies_generation_s": gen_s, "self_check": {"sample": int(len(pick)), "same_bytes": bool(same)}}
+
+
 def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=False, leg=False):
     """Config 3 (or the Zipf stream with --zipf) on ONE GPU: server ingest of
     `owners x per_owner` messages into an empty store, then getMessages for
@@ -1984,6 +2070,8 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
             out.pop(k)
     if zipf <= 0:
         out["reingest"] = reingest(eng, a, ts_r, lown, owners, per_owner, request, flags)
+        if getattr(a, "e2e", 1) and request >= per_owner:
+            out["e2e"] = e2e_leg(eng, ts_np, owner_np, client, ms)
     eng.close()
     del ts_r, lown, keep, client, flags
     torch.cuda.empty_cache()

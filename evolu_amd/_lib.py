@@ -88,6 +88,7 @@ SIGNATURES = {
     "evm_tree_leaves": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "evm_tree_roots": (_i, [_vp, _vp, _vp, _vp]),
     "evm_tree_to_json": (_i, [_vp, _vp, _u32, _vp, _sz, C.POINTER(_sz)]),
+    "evm_tree_to_json_batch": (_i, [_vp, _vp, _vp, _u32, _vp, _sz, _vp, C.POINTER(C.c_uint64)]),
     "evm_tree_from_json": (_i, [_vp, _u32, C.POINTER(C.c_char_p), C.POINTER(_sz), C.POINTER(_vp)]),
     "evm_merkle_insert": (_i, [_vp, _vp, _vp, _sz, _sz, _vp, C.POINTER(_vp)]),
     "evm_merkle_diff": (_i, [_vp, _vp, _vp, _vp]),
@@ -103,6 +104,10 @@ SIGNATURES = {
     "evm_pb_scan": (_i, [_i, _vp, _sz, _vp]),
     "evm_pb_split": (_i, [_i, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp]),
     "evm_pb_encode": (_i, [_i, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _sz, C.POINTER(_sz)]),
+    "evm_pb_scan_batch": (_i, [_i, _vp, _vp, _u32, _vp, _vp]),
+    "evm_pb_split_batch": (_i, [_i, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    "evm_pb_encode_requests": (_i, [_u32, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "evm_pb_encode_responses": (_i, [_u32, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
     "evm_store_since": (_i, [_vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_server_select": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_store_select_after": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),

@@ -12,8 +12,12 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "evm_internal.hpp"
@@ -160,6 +164,21 @@ struct Parser {
   }
 };
 
+// f(begin, end) over disjoint runs of [0, n) on host threads (EVM_HOST_THREADS, at most 16)
+template <typename F>
+void run_parallel(size_t n, F f) {
+  int T = (int)std::thread::hardware_concurrency();
+  if (const char* e = getenv("EVM_HOST_THREADS")) T = atoi(e);
+  T = (int)std::min<size_t>((size_t)std::max(1, std::min(T, 16)), std::max<size_t>(1, n / 16));
+  if (T <= 1) {
+    f((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int k = 0; k < T; ++k) th.emplace_back([=]() { f(n * k / T, n * (k + 1) / T); });
+  for (auto& x : th) x.join();
+}
+
 }  // namespace
 
 extern "C" int evm_tree_to_json(evm_ctx* ctx, const evm_tree* t, uint32_t owner, char* buf, size_t cap, size_t* len) {
@@ -195,23 +214,42 @@ extern "C" int evm_tree_to_json(evm_ctx* ctx, const evm_tree* t, uint32_t owner,
 extern "C" int evm_tree_from_json(evm_ctx* ctx, uint32_t n_owners, const char* const* json, const size_t* lens,
                                   evm_tree** out) {
   if (!ctx || !out || (n_owners && (!json || !lens))) return EVM_EINVAL;
-  std::vector<uint64_t> off(n_owners + 1, 0), codes;
-  std::vector<int32_t> xors;
-  for (uint32_t o = 0; o < n_owners; ++o) {
-    Parser ps{json[o], json[o] + lens[o], {}, {}};
-    int32_t h = 0;
-    bool hh = false;
-    if (!ps.node(0, 0, true, &h, &hh)) return EVM_ETREE;
-    ps.ws();
-    if (ps.p != ps.e) return EVM_ETREE;
-    std::vector<std::pair<uint64_t, int32_t>> v(ps.codes.size());
-    for (size_t i = 0; i < v.size(); ++i) v[i] = {ps.codes[i], ps.xors[i]};
-    std::sort(v.begin(), v.end());
-    for (const auto& kv : v) {
-      codes.push_back(kv.first);
-      xors.push_back(kv.second);
+  // owners parse independently: runs of them on host threads (a round's
+  // client trees, index.ts:187), then one copy into the leaf arrays
+  std::vector<std::vector<std::pair<uint64_t, int32_t>>> per(n_owners);
+  std::atomic<int> bad{0};
+  auto work = [&](size_t a, size_t b) {
+    for (size_t o = a; o < b && !bad.load(std::memory_order_relaxed); ++o) {
+      Parser ps{json[o], json[o] + lens[o], {}, {}};
+      int32_t h = 0;
+      bool hh = false;
+      if (!ps.node(0, 0, true, &h, &hh)) {
+        bad = 1;
+        return;
+      }
+      ps.ws();
+      if (ps.p != ps.e) {
+        bad = 1;
+        return;
+      }
+      auto& v = per[o];
+      v.resize(ps.codes.size());
+      for (size_t i = 0; i < v.size(); ++i) v[i] = {ps.codes[i], ps.xors[i]};
+      std::sort(v.begin(), v.end());
     }
-    off[o + 1] = codes.size();
-  }
+  };
+  run_parallel(n_owners, work);
+  if (bad) return EVM_ETREE;
+  std::vector<uint64_t> off(n_owners + 1, 0);
+  for (uint32_t o = 0; o < n_owners; ++o) off[o + 1] = off[o] + per[o].size();
+  std::vector<uint64_t> codes(off[n_owners]);
+  std::vector<int32_t> xors(off[n_owners]);
+  run_parallel(n_owners, [&](size_t a, size_t b) {
+    for (size_t o = a; o < b; ++o)
+      for (size_t i = 0; i < per[o].size(); ++i) {
+        codes[off[o] + i] = per[o][i].first;
+        xors[off[o] + i] = per[o][i].second;
+      }
+  });
   return evm_tree_from_leaves(ctx, n_owners, off.data(), codes.data(), xors.data(), out);
 }

@@ -250,3 +250,202 @@ int evm_pb_encode(int kind, const char* ts, size_t stride, const uint32_t* ts_le
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Batches of bodies (a server round: index.ts:224-248 per request), on host
+// threads.  Bodies are independent, so each thread takes a contiguous run of
+// them; EVM_HOST_THREADS caps the threads (default: the machine's, at most 16).
+#include <stdlib.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+namespace {
+
+int host_threads(size_t items) {
+  int t = (int)std::thread::hardware_concurrency();
+  if (const char* e = getenv("EVM_HOST_THREADS")) t = atoi(e);
+  t = std::max(1, std::min(t, 16));
+  return (int)std::min<size_t>((size_t)t, std::max<size_t>(1, items / 32));
+}
+
+template <typename F>
+void parallel_for(size_t n, F f) {  // f(begin, end) over disjoint runs of [0, n)
+  const int T = host_threads(n);
+  if (T <= 1) {
+    f((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int k = 0; k < T; ++k) {
+    const size_t a = n * k / T, b = n * (k + 1) / T;
+    th.emplace_back([=]() { f(a, b); });
+  }
+  for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+int evm_pb_scan_batch(int kind, const uint8_t* arena, const uint64_t* off, uint32_t n, evm_pb_sync* info,
+                      int32_t* status) {
+  if ((n && (!arena || !off || !info || !status)) || (kind != EVM_PB_SYNC_REQUEST && kind != EVM_PB_SYNC_RESPONSE))
+    return EVM_EINVAL;
+  parallel_for(n, [&](size_t a, size_t b) {
+    for (size_t k = a; k < b; ++k) {
+      status[k] = off[k + 1] < off[k] ? EVM_EINVAL : evm_pb_scan(kind, arena + off[k], off[k + 1] - off[k], &info[k]);
+      if (status[k]) memset(&info[k], 0, sizeof(evm_pb_sync));
+    }
+  });
+  return EVM_OK;
+}
+
+int evm_pb_split_batch(int kind, const uint8_t* arena, const uint64_t* off, uint32_t n, const int32_t* status,
+                       const uint64_t* msg_base, const uint64_t* content_base, char* ts, size_t stride,
+                       uint32_t* ts_len, uint64_t* ts_off, uint64_t* content_off, uint8_t* content) {
+  if (n && (!arena || !off || !status || !msg_base || !content_base || !ts || !content_off)) return EVM_EINVAL;
+  if (stride < 46) return EVM_EINVAL;
+  int bad = EVM_OK;
+  std::vector<int> errs((size_t)std::max(1, host_threads(n)), EVM_OK);
+  parallel_for(n, [&](size_t a, size_t b) {
+    std::vector<uint64_t> co;
+    for (size_t k = a; k < b; ++k) {
+      if (status[k]) continue;
+      const uint64_t m0 = msg_base[k], c0 = content_base[k];
+      const uint8_t* body = arena + off[k];
+      const size_t len = off[k + 1] - off[k];
+      evm_pb_sync s;
+      if (evm_pb_scan(kind, body, len, &s)) continue;  // (scanned fine before: unchanged bytes)
+      co.assign(s.n_messages + 1, 0);
+      const int st = evm_pb_split(kind, body, len, ts + m0 * stride, stride, ts_len ? ts_len + m0 : nullptr,
+                                  ts_off ? ts_off + m0 : nullptr, co.data(), content ? content + c0 : nullptr);
+      if (st) {
+        errs[0] = st;  // (a body that changed between the passes)
+        continue;
+      }
+      for (uint64_t i = 0; i < s.n_messages; ++i) {
+        content_off[m0 + i] = c0 + co[i];
+        if (ts_off) ts_off[m0 + i] += off[k];
+      }
+      // the entry after a body's last message is the next body's first (or
+      // the end): written once, by whoever holds the total
+      content_off[m0 + s.n_messages] = c0 + co[s.n_messages];
+    }
+  });
+  for (int e : errs) bad = bad ? bad : e;
+  return bad;
+}
+
+// SyncResponse bodies (index.ts:235-245) for n requests: request r's
+// messages are the ids sel_id[sel_off[r] .. sel_off[r + 1]); a message id
+// lies in log segment s = the last with seg_base[s] <= id (row k = id -
+// seg_base[s], or seg_row[s][k] when a segment indexes shared arrays): its
+// 46-B timestamp at seg_ts[s] + row * stride, its content
+// seg_content[s][seg_coff[s][row] ..  seg_coff[s][row + 1]); the merkleTree
+// text json[json_off[r] .. json_off[r + 1]).  out == NULL: out_off[0..n]
+// only (the sizes' exclusive prefix, out_off[n] = the total).
+int evm_pb_encode_responses(uint32_t n, const uint64_t* sel_off, const uint64_t* sel_id, uint32_t n_seg,
+                            const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
+                            size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
+                            const char* json, const uint64_t* json_off, uint8_t* out, uint64_t* out_off) {
+  if (n && (!sel_off || !json_off || !out_off || (n_seg && (!seg_base || !seg_ts || !seg_coff || !seg_content))))
+    return EVM_EINVAL;
+  if (stride < 46) return EVM_EINVAL;
+  std::vector<int> bad((size_t)host_threads(n) + 1, 0);
+  auto locate = [&](uint64_t id, const char** t, const uint8_t** c, uint64_t* cl) -> bool {
+    const uint32_t s = (uint32_t)(std::upper_bound(seg_base, seg_base + n_seg, id) - seg_base);
+    if (s == 0) return false;
+    const uint64_t k = id - seg_base[s - 1];
+    const uint64_t row = seg_row && seg_row[s - 1] ? seg_row[s - 1][k] : k;
+    *t = seg_ts[s - 1] + row * stride;
+    const uint64_t a = seg_coff[s - 1][row], b = seg_coff[s - 1][row + 1];
+    *c = seg_content[s - 1] + a;
+    *cl = b - a;
+    return true;
+  };
+  auto encode = [&](size_t r, uint8_t* dst, size_t cap) -> size_t {
+    Writer w{dst, cap};
+    for (uint64_t j = sel_off[r]; j < sel_off[r + 1]; ++j) {
+      const char* t;
+      const uint8_t* c;
+      uint64_t cl;
+      if (!locate(sel_id[j], &t, &c, &cl)) {
+        bad[0] = 1;
+        continue;
+      }
+      w.varint(1u << 3 | 2);
+      w.varint(1 + varint_len(46) + 46 + (cl ? 1 + varint_len(cl) + cl : 0));
+      w.str(1, t, 46);
+      w.str(2, c, cl);
+    }
+    w.str(2, json + json_off[r], json_off[r + 1] - json_off[r]);
+    return w.n;
+  };
+  std::vector<uint64_t> size(n);
+  parallel_for(n, [&](size_t a, size_t b) {
+    for (size_t r = a; r < b; ++r) size[r] = encode(r, nullptr, 0);
+  });
+  if (bad[0]) return EVM_EINVAL;  // (an id in no segment)
+  uint64_t acc = 0;
+  for (uint32_t r = 0; r < n; ++r) {
+    out_off[r] = acc;
+    acc += size[r];
+  }
+  out_off[n] = acc;
+  if (!out) return EVM_OK;
+  parallel_for(n, [&](size_t a, size_t b) {
+    for (size_t r = a; r < b; ++r) encode(r, out + out_off[r], size[r]);
+  });
+  return EVM_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// SyncRequest bodies for n requests (a client fleet's round: sync.worker.ts
+// SyncRequest.toBinary), on host threads: request r's messages are rows
+// [msg_off[r], msg_off[r + 1]) of ts (46-B timestamps at `stride`) with
+// contents content[content_off[row] .. content_off[row + 1]); its userId,
+// nodeId and merkleTree are the strings [x_off[r], x_off[r + 1]) of the
+// user / node / tree arenas.  out == NULL: out_off only (sizes' prefix).
+int evm_pb_encode_requests(uint32_t n, const uint64_t* msg_off, const char* ts, size_t stride,
+                           const uint64_t* content_off, const uint8_t* content, const char* user,
+                           const uint64_t* user_off, const char* node, const uint64_t* node_off, const char* tree,
+                           const uint64_t* tree_off, uint8_t* out, uint64_t* out_off) {
+  if (n && (!msg_off || !out_off || !user_off || !node_off || !tree_off)) return EVM_EINVAL;
+  if (stride < 46) return EVM_EINVAL;
+  auto encode = [&](size_t r, uint8_t* dst, size_t cap) -> size_t {
+    Writer w{dst, cap};
+    for (uint64_t i = msg_off[r]; i < msg_off[r + 1]; ++i) {
+      const uint64_t cl = content_off[i + 1] - content_off[i];
+      w.varint(1u << 3 | 2);
+      w.varint(1 + varint_len(46) + 46 + (cl ? 1 + varint_len(cl) + cl : 0));
+      w.str(1, ts + i * stride, 46);
+      w.str(2, content + content_off[i], cl);
+    }
+    w.str(2, user + user_off[r], user_off[r + 1] - user_off[r]);
+    w.str(3, node + node_off[r], node_off[r + 1] - node_off[r]);
+    w.str(4, tree + tree_off[r], tree_off[r + 1] - tree_off[r]);
+    return w.n;
+  };
+  std::vector<uint64_t> size(n);
+  parallel_for(n, [&](size_t a, size_t b) {
+    for (size_t r = a; r < b; ++r) size[r] = encode(r, nullptr, 0);
+  });
+  uint64_t acc = 0;
+  for (uint32_t r = 0; r < n; ++r) {
+    out_off[r] = acc;
+    acc += size[r];
+  }
+  out_off[n] = acc;
+  if (!out) return EVM_OK;
+  parallel_for(n, [&](size_t a, size_t b) {
+    for (size_t r = a; r < b; ++r) encode(r, out + out_off[r], size[r]);
+  });
+  return EVM_OK;
+}
+
+}  // extern "C"

@@ -459,6 +459,21 @@ class Trees:
                                           p.ctypes.data_as(C.c_void_p)), "evm_tree_roots")
         return r[: self.n_owners], p[: self.n_owners].astype(bool)
 
+    def to_json_batch(self, owners: Optional[torch.Tensor] = None, count: Optional[int] = None):
+        """Many owners' JSON in one device call (evm_tree_to_json_batch):
+        owners (device int32/uint32, or None = 0..count-1) -> (bytes uint8
+        device tensor, offsets int64 device tensor [n + 1])."""
+        dev = torch.device("cuda", self.eng.device)
+        n = int(owners.numel()) if owners is not None else (self.n_owners if count is None else count)
+        off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        tot = C.c_uint64()
+        check(self.eng.lib.evm_tree_to_json_batch(self.eng.h, self.h, _ptr(owners), n, None, 0, _ptr(off),
+                                                  C.byref(tot)), "evm_tree_to_json_batch")
+        out = torch.empty(max(tot.value, 1), dtype=torch.uint8, device=dev)
+        check(self.eng.lib.evm_tree_to_json_batch(self.eng.h, self.h, _ptr(owners), n, _ptr(out), out.numel(),
+                                                  _ptr(off), C.byref(tot)), "evm_tree_to_json_batch")
+        return out[: tot.value], off
+
     def to_json(self, owner: int = 0) -> str:
         ln = C.c_size_t()
         check(self.eng.lib.evm_tree_to_json(self.eng.h, self.h, owner, None, 0, C.byref(ln)), "evm_tree_to_json")

@@ -24,6 +24,16 @@ string, which is what the reference stores.  Rows stored under a lenient
 spelling are tracked per user, so getMessages still orders and bounds them
 by their raw strings.
 
+The common case runs as whole-call arrays (`_sync_fast`): every body
+decoded on host threads in one call (evm_pb_scan_batch / split_batch), each
+round's requests ingested together, their client trees parsed on host
+threads in one call (evm_tree_from_json), one selection, every touched
+owner's tree JSON emitted on the device in one launch
+(evm_tree_to_json_batch) and every response encoded on host threads in one
+call (evm_pb_encode_responses).  Requests of users with rows stored under a
+lenient spelling, and requests whose owner the ingest rejected, take the
+per-request path below (`_round`) -- the same results either way.
+
 Results per body: the SyncResponse bytes, an exception object standing for
 the reference's 500 answer (ParseBodyError, RangeError), or None where the
 engine does not model the request (a nodeId that is not 16 hex chars, a
@@ -40,11 +50,13 @@ and tree of that user as stale.
 """
 from __future__ import annotations
 
+import ctypes as C
 from typing import Dict, List, Sequence, Set, Union
 
 import numpy as np
 
 from . import _lib
+from ._lib import check
 from . import lenient as LN
 from . import wire
 from .engine import TS_LEN, Engine
@@ -61,6 +73,13 @@ class HandedOver:
 
 
 Result = Union[bytes, Exception, HandedOver, None]
+REQUEST_KIND = _lib.PB_SYNC_REQUEST
+_EMPTY = C.create_string_buffer(b"{}")  # the client tree of an owner not in the round
+_EMPTY_PTR = C.addressof(_EMPTY)
+
+
+def _np_ptr(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data)
 _HEX = set(b"0123456789abcdefABCDEF")
 
 
@@ -82,10 +101,13 @@ class SyncServer:
         self.capacity = capacity
         self.slot: Dict[str, int] = {}
         self.next_id = 0
-        self._base: List[int] = []          # first message id of each ingested batch
-        self._ts: List[np.ndarray] = []     # that batch's (n, stride) timestamp rows
-        self._off: List[np.ndarray] = []    # its content offsets (n + 1)
-        self._content: List[bytes] = []     # its concatenated contents
+        # the message log, by id: segments of ids [base, base + n) -- the
+        # timestamp rows (N, 48), content offsets (N + 1) and contents of a
+        # decode, and a row map (id - base -> row) when a segment covers part
+        # of them (None: row = id - base)
+        self._base: List[int] = []
+        self._segs: List[tuple] = []
+        self.timing: Dict[str, float] = {}  # seconds of the last sync() by part (host / device)
         self._raw: Dict[int, str] = {}      # message id -> the raw timestamp, for rows stored under a lenient spelling
         # user -> canonical timestamp -> (raw spelling, message id) of rows stored under a lenient spelling
         self.lenient: Dict[str, Dict[str, tuple]] = {}
@@ -102,16 +124,37 @@ class SyncServer:
             s = self.slot[user] = len(self.slot)
         return s
 
+    def _log(self, base: int, ts: np.ndarray, coff: np.ndarray, content: np.ndarray, rowmap=None):
+        self._base.append(base)
+        self._segs.append((ts, np.ascontiguousarray(coff, dtype=np.uint64), content,
+                           None if rowmap is None else np.ascontiguousarray(rowmap, dtype=np.uint64)))
+
     def _message(self, mid: int):
         r = int(np.searchsorted(np.asarray(self._base), mid, side="right")) - 1
+        ts_a, o, content, rowmap = self._segs[r]
         k = mid - self._base[r]
-        o = self._off[r]
+        if rowmap is not None:
+            k = int(rowmap[k])
         ts = self._raw.get(mid)
         if ts is None:
-            ts = bytes(self._ts[r][k, :TS_LEN]).decode("latin-1")
-        return ts, self._content[r][int(o[k]):int(o[k + 1])]
+            ts = bytes(ts_a[k, :TS_LEN]).decode("latin-1")
+        return ts, content[int(o[k]):int(o[k + 1])].tobytes()
 
     def sync(self, bodies: Sequence[bytes]) -> List[Result]:
+        n = len(bodies)
+        boff = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(np.fromiter((len(b) for b in bodies), dtype=np.uint64, count=n), out=boff[1:])
+        return self._sync_fast(np.frombuffer(b"".join(bodies) or b"\0", dtype=np.uint8), boff)
+
+    def sync_arena(self, arena: np.ndarray, off: np.ndarray, views: bool = True) -> List[Result]:
+        """sync() of the bodies arena[off[k] .. off[k + 1]) (uint8 / uint64 arrays);
+        views=True: the responses are memoryviews into one response arena
+        (no per-response copy), equal to the bytes sync() would return."""
+        return self._sync_fast(np.ascontiguousarray(arena, dtype=np.uint8),
+                               np.ascontiguousarray(off, dtype=np.uint64), views)
+
+    def sync_per_request(self, bodies: Sequence[bytes]) -> List[Result]:
+        """The same, every request through the per-request path (A/B, tests)."""
         out: List[Result] = [None] * len(bodies)
         reqs = []
         for i, b in enumerate(bodies):
@@ -133,6 +176,198 @@ class SyncServer:
         for rnd in rounds:
             self._round(rnd, out)
         return out
+
+    # ------------------------------------------------------------ fast path
+    def _sync_fast(self, arena: np.ndarray, boff: np.ndarray, views: bool = False) -> List[Result]:
+        """sync() over whole-call arrays (module docstring); timings by part in self.timing."""
+        import time
+
+        import torch
+
+        lib, eng = _lib.load(), self.eng
+        T = self.timing = dict.fromkeys(("decode", "ingest", "trees", "select", "json", "encode", "per_request"), 0.0)
+        n = len(boff) - 1
+        out: List[Result] = [None] * n
+        if n == 0:
+            return out
+        t0 = time.perf_counter()
+        info = (wire._Sync * n)()
+        st = np.zeros(n, dtype=np.int32)
+        check(lib.evm_pb_scan_batch(REQUEST_KIND, _np_ptr(arena), _np_ptr(boff), n, info, _np_ptr(st)),
+              "evm_pb_scan_batch")
+        inf = np.ctypeslib.as_array(info).view(np.uint64).reshape(n, 9).copy()
+        ok = st == 0
+        inf[~ok] = 0
+        nmsg, cbytes = inf[:, 0], inf[:, 1]
+        msg_base = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(nmsg, out=msg_base[1:])
+        con_base = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(cbytes, out=con_base[1:])
+        N, CB = int(msg_base[n]), int(con_base[n])
+        ts = np.zeros((max(N, 1), 48), dtype=np.uint8)
+        ts_len = np.zeros(max(N, 1), dtype=np.uint32)
+        ts_off = np.zeros(max(N, 1), dtype=np.uint64)
+        coff = np.zeros(N + 1, dtype=np.uint64)
+        content = np.zeros(max(CB, 1), dtype=np.uint8)
+        check(lib.evm_pb_split_batch(REQUEST_KIND, _np_ptr(arena), _np_ptr(boff), n, _np_ptr(st), _np_ptr(msg_base),
+                                     _np_ptr(con_base), _np_ptr(ts), 48, _np_ptr(ts_len), _np_ptr(ts_off),
+                                     _np_ptr(coff), _np_ptr(content)), "evm_pb_split_batch")
+        for i in np.flatnonzero(~ok):
+            out[i] = ParseBodyError(_lib.load().evm_strerror(int(st[i])).decode())
+        span = lambda i, f: arena[int(boff[i] + inf[i, f]):int(boff[i] + inf[i, f] + inf[i, f + 1])]  # noqa: E731
+        users = [span(i, 2).tobytes().decode("utf-8", "replace") if ok[i] else None for i in range(n)]
+        # nodeId usable by NOT LIKE '%' || nodeId: 16 hex chars (else the user is handed over)
+        node_ok = np.zeros(n, dtype=bool)
+        nodes16 = np.full((n, 16), ord("0"), dtype=np.uint8)
+        has16 = ok & (inf[:, 5] == 16)
+        if has16.any():
+            k16 = np.flatnonzero(has16)
+            nodes16[k16] = arena[(boff[k16] + inf[k16, 4])[:, None].astype(np.int64) + np.arange(16)]
+            hexok = np.isin(nodes16[k16], np.frombuffer(b"0123456789abcdefABCDEF", dtype=np.uint8)).all(1)
+            node_ok[k16[hexok]] = True
+        rnd_of = np.full(n, -1, dtype=np.int64)
+        seen: Dict[str, int] = {}
+        for i in np.flatnonzero(ok):
+            k = seen.get(users[i], 0)
+            seen[users[i]] = k + 1
+            rnd_of[i] = k
+        T["decode"] += time.perf_counter() - t0
+        log = (ts, coff, content)
+        ts_dev = None
+        for k in range(int(rnd_of.max()) + 1 if n else 0):
+            idx = np.flatnonzero(rnd_of == k)
+            fast, slow = [], []
+            for i in idx:
+                u = users[i]
+                if u in self.detached:
+                    continue  # out[i] stays None
+                if not node_ok[i]:
+                    self.detached.add(u)  # NOT LIKE '%' || nodeId with any nodeId is not modelled
+                    continue
+                (slow if u in self.lenient else fast).append(int(i))
+            rejected = []
+            if fast:
+                t0 = time.perf_counter()
+                if ts_dev is None:
+                    ts_dev = eng.dev(ts)
+                F = np.asarray(fast, dtype=np.int64)
+                slots = np.fromiter((self._slot(users[i]) for i in F), dtype=np.int64, count=len(F))
+                cnt = nmsg[F].astype(np.int64)
+                tot = int(cnt.sum())
+                first = np.cumsum(cnt) - cnt
+                rows = (np.repeat(msg_base[F].astype(np.int64) - first, cnt) + np.arange(tot)).astype(np.int64)
+                owner = np.repeat(slots, cnt).astype(np.int32)
+                if tot:
+                    rows_dev = torch.from_numpy(rows).to(ts_dev.device)
+                    flags, ost, _ = self.store.ingest_ex(ts_dev.index_select(0, rows_dev),
+                                                         torch.from_numpy(owner).to(ts_dev.device), self.next_id)
+                    ost = ost.cpu().numpy()
+                    self._log(self.next_id, ts, coff, content, rowmap=rows)
+                    self.next_id += tot
+                    bad = ost[slots] != 0
+                else:
+                    bad = np.zeros(len(F), dtype=bool)
+                rejected = [int(i) for i in F[bad]]
+                answered = [(int(i), int(sl)) for i, sl in zip(F[~bad], slots[~bad])]
+                T["ingest"] += time.perf_counter() - t0
+            else:
+                answered = []
+            if slow or rejected:
+                # rows stored under lenient spellings, or an owner the ingest rejected
+                # (its requests committed nothing there): the per-request path
+                t0 = time.perf_counter()
+                self._round([(i, self._request_at(i, arena, boff, inf, users, log, ts_len, ts_off, msg_base))
+                             for i in sorted(slow + rejected)], out)
+                T["per_request"] += time.perf_counter() - t0
+            if answered:
+                self._respond_fast(answered, arena, boff, inf, nodes16, out, T,
+                                   lambda i: self._request_at(i, arena, boff, inf, users, log, ts_len, ts_off,
+                                                              msg_base), views)
+        return out
+
+    def _request_at(self, i, arena, boff, inf, users, log, ts_len, ts_off, msg_base):
+        """Request i of a fast-path call as the per-request path's Sync."""
+        ts, coff, content = log
+        m0, k = int(msg_base[i]), int(inf[i, 0])
+        c0, c1 = int(coff[m0]), int(coff[m0 + k])
+        raw = [arena[int(o):int(o) + int(ln)].tobytes().decode("utf-8", "replace")
+               for o, ln in zip(ts_off[m0:m0 + k], ts_len[m0:m0 + k])]
+        span = lambda f: arena[int(boff[i] + inf[i, f]):int(boff[i] + inf[i, f] + inf[i, f + 1])]  # noqa: E731
+        return wire.Sync(ts[m0:m0 + k].copy(), ts_len[m0:m0 + k].copy(), (coff[m0:m0 + k + 1] - c0).copy(),
+                         content[c0:c1].tobytes(), span(6).tobytes().decode("utf-8", "replace"), raw=raw,
+                         user=users[i], node=span(4).tobytes().decode("utf-8", "replace"))
+
+    def _respond_fast(self, answered, arena, boff, inf, nodes16, out: List[Result], T, request_at, views=False):
+        """getMessages + SyncResponse.toBinary for requests i at owner slots
+        sl (no lenient rows): client trees parsed on host threads in one call,
+        one selection, the trees' JSON in one device launch, the responses
+        encoded on host threads in one call."""
+        import time
+
+        import torch
+
+        lib, eng, O = _lib.load(), self.eng, self.capacity
+        t0 = time.perf_counter()
+        req = np.asarray([i for i, _ in answered], dtype=np.int64)
+        sl = np.asarray([s_ for _, s_ in answered], dtype=np.int64)
+        ptrs = np.full(O, _EMPTY_PTR, dtype=np.uint64)
+        lens = np.full(O, 2, dtype=np.uint64)
+        base = arena.ctypes.data
+        ptrs[sl] = base + boff[req] + inf[req, 6]
+        lens[sl] = inf[req, 7]
+        h = C.c_void_p()
+        stt = lib.evm_tree_from_json(eng.h, O, ptrs.ctypes.data_as(C.POINTER(C.c_char_p)),
+                                     lens.ctypes.data_as(C.POINTER(C.c_size_t)), C.byref(h))
+        T["trees"] += time.perf_counter() - t0
+        if stt != _lib.EVM_OK:
+            # some request's merkleTree does not parse (merkleTreeFromString throws -> 500 for that
+            # request only): the per-request selection finds which
+            t0 = time.perf_counter()
+            self._select([(int(i), request_at(int(i)), int(s_)) for i, s_ in answered], out)
+            T["per_request"] += time.perf_counter() - t0
+            return
+        from .engine import Trees
+
+        client = Trees(eng, h)
+        t0 = time.perf_counter()
+        node = np.full((O, 16), ord("0"), dtype=np.uint8)
+        node[sl] = nodes16[req]
+        active = np.zeros(O, dtype=np.uint8)
+        active[sl] = 1
+        diff, soff, sid = self.store.select(client, eng.dev(node), eng.dev(active))
+        client.free()
+        diff, soff, sid = diff.cpu().numpy(), soff.cpu().numpy().astype(np.int64), sid.cpu().numpy()
+        T["select"] += time.perf_counter() - t0
+        t0 = time.perf_counter()
+        jbuf, joff = self.store.tree().to_json_batch(torch.from_numpy(sl.astype(np.int32)).to(f"cuda:{eng.device}"))
+        jbuf, joff = jbuf.cpu().numpy(), joff.cpu().numpy()
+        T["json"] += time.perf_counter() - t0
+        t0 = time.perf_counter()
+        rng_err = diff[sl] == _lib.DIFF_RANGE_ERROR
+        cnt = np.where(rng_err, 0, soff[sl + 1] - soff[sl])
+        first = np.cumsum(cnt) - cnt
+        tot = int(cnt.sum())
+        pick = np.repeat(soff[sl] - first, cnt) + np.arange(tot)
+        sel = np.ascontiguousarray(sid[pick], dtype=np.uint64)
+        sel_off = np.zeros(len(sl) + 1, dtype=np.uint64)
+        np.cumsum(cnt, out=sel_off[1:])
+        segs = self._segs
+        seg_base = np.asarray(self._base, dtype=np.uint64)
+        P = C.c_void_p
+        seg_row = (P * len(segs))(*[None if r is None else r.ctypes.data for _, _, _, r in segs])
+        seg_ts = (P * len(segs))(*[t.ctypes.data for t, _, _, _ in segs])
+        seg_coff = (P * len(segs))(*[o.ctypes.data for _, o, _, _ in segs])
+        seg_con = (P * len(segs))(*[c.ctypes.data for _, _, c, _ in segs])
+        ooff = np.zeros(len(sl) + 1, dtype=np.uint64)
+        args = [len(sl), _np_ptr(sel_off), _np_ptr(sel), len(segs), _np_ptr(seg_base), seg_row, seg_ts, 48, seg_coff,
+                seg_con, _np_ptr(jbuf), _np_ptr(joff)]
+        check(lib.evm_pb_encode_responses(*args, None, _np_ptr(ooff)), "evm_pb_encode_responses")
+        resp = np.zeros(max(int(ooff[-1]), 1), dtype=np.uint8)
+        check(lib.evm_pb_encode_responses(*args, _np_ptr(resp), _np_ptr(ooff)), "evm_pb_encode_responses")
+        rb = memoryview(resp) if views else resp.tobytes()
+        for k, i in enumerate(req):
+            out[int(i)] = RangeError("Invalid count value") if rng_err[k] else rb[int(ooff[k]):int(ooff[k + 1])]
+        T["encode"] += time.perf_counter() - t0
 
     # ------------------------------------------------------------------ ingest
     def _ingest(self, reqs, rows_of):
@@ -160,10 +395,7 @@ class SyncServer:
         flags, ost, _ = self.store.ingest_ex(eng.dev(ts), eng.dev(owner), self.next_id)
         flags, ost = flags.cpu().numpy(), ost.cpu().numpy()
         base = self.next_id
-        self._base.append(base)
-        self._ts.append(ts)
-        self._off.append(off)
-        self._content.append(b"".join(content))
+        self._log(base, ts, off, np.frombuffer(b"".join(content) or b"\0", dtype=np.uint8))
         self.next_id += n
         rejected = {k for k, (_, _, s) in enumerate(reqs) if ost[s]}
         return [flags[a:b] for a, b in spans], rejected, [base + a for a, _ in spans]

@@ -173,6 +173,14 @@ int evm_tree_leaves(evm_ctx* ctx, const evm_tree* t, uint64_t* owner_off, uint64
 int evm_tree_roots(evm_ctx* ctx, const evm_tree* t, int32_t* root_hash, uint8_t* present);
 /* types.ts:80-81 JSON.stringify(tree of `owner`); *len = bytes needed (no NUL) */
 int evm_tree_to_json(evm_ctx* ctx, const evm_tree* t, uint32_t owner, char* buf, size_t cap, size_t* len);
+/* The same for many owners in one call, on the device (index.ts:160-163,:240
+ * for every request of a round): owners[0..n) (device u32; NULL = owners
+ * 0..n-1) -> their texts back to back in `out` (device, cap bytes), owner j's
+ * at [off[j], off[j+1]) (off: device, n + 1 entries); *total = the bytes
+ * needed.  out == NULL: only off and *total.  EVM_ECAPACITY when total > cap;
+ * EVM_EINVAL for an owner id out of range. */
+int evm_tree_to_json_batch(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, char* out, size_t cap,
+                           uint64_t* off, uint64_t* total);
 /* types.ts:83-84, one JSON text per owner (host strings) */
 int evm_tree_from_json(evm_ctx* ctx, uint32_t n_owners, const char* const* json, const size_t* lens, evm_tree** out);
 
@@ -374,6 +382,39 @@ int evm_pb_encode(int kind, const char* ts, size_t stride, const uint32_t* ts_le
                   const uint64_t* content_off, const uint8_t* content, const char* user, size_t user_len,
                   const char* node, size_t node_len, const char* tree, size_t tree_len, uint8_t* out, size_t cap,
                   size_t* out_len);
+/* Batches of bodies on host threads (a server round, index.ts:224-248 per
+ * request; EVM_HOST_THREADS caps the threads).  Bodies are arena[off[k] ..
+ * off[k + 1]).  scan: per body its evm_pb_sync and status (EVM_EINVAL = the
+ * reference's parseBody throw).  split: the bodies with status 0 into one
+ * timestamp arena / content arena, body k's messages from global index
+ * msg_base[k] and content byte content_base[k] (content_off: N + 1 global
+ * entries; ts_off: offsets into the arena). */
+int evm_pb_scan_batch(int kind, const uint8_t* arena, const uint64_t* off, uint32_t n, evm_pb_sync* info,
+                      int32_t* status);
+int evm_pb_split_batch(int kind, const uint8_t* arena, const uint64_t* off, uint32_t n, const int32_t* status,
+                       const uint64_t* msg_base, const uint64_t* content_base, char* ts, size_t stride,
+                       uint32_t* ts_len, uint64_t* ts_off, uint64_t* content_off, uint8_t* content);
+/* SyncResponse bodies (index.ts:235-245) for n requests: request r's
+ * messages are the ids sel_id[sel_off[r] .. sel_off[r + 1]) (a getMessages
+ * selection); id -> log segment s = the last with seg_base[s] <= id, row =
+ * id - seg_base[s] (or seg_row[s][that], when seg_row[s] is not NULL): its
+ * 46-B timestamp at seg_ts[s] + row * stride, its content
+ * seg_content[s][seg_coff[s][row] .. seg_coff[s][row + 1]); the merkleTree
+ * text json[json_off[r] .. json_off[r + 1]).  Responses back to back in out
+ * (out_off: n + 1 entries; out NULL: sizes only). */
+/* SyncRequest bodies for n requests (the client side's toBinary,
+ * sync.worker.ts:102; the bench's synthetic rounds): request r's messages
+ * are ts rows [msg_off[r], msg_off[r + 1]) with contents by content_off; its
+ * userId / nodeId / merkleTree the strings [x_off[r], x_off[r + 1]) of the
+ * user / node / tree arenas.  out NULL: out_off (n + 1) only. */
+int evm_pb_encode_requests(uint32_t n, const uint64_t* msg_off, const char* ts, size_t stride,
+                           const uint64_t* content_off, const uint8_t* content, const char* user,
+                           const uint64_t* user_off, const char* node, const uint64_t* node_off, const char* tree,
+                           const uint64_t* tree_off, uint8_t* out, uint64_t* out_off);
+int evm_pb_encode_responses(uint32_t n, const uint64_t* sel_off, const uint64_t* sel_id, uint32_t n_seg,
+                            const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
+                            size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
+                            const char* json, const uint64_t* json_off, uint8_t* out, uint64_t* out_off);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU owner sharding (evm_dist.hip).  One process per

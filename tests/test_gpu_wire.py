@@ -62,7 +62,7 @@ def _expected(bodies):
             continue
         try:
             tree, _, rows = sdb.sync(r.userId, r.nodeId, r.merkleTree, [(m.timestamp, m.content) for m in r.messages])
-        except O.RangeErrorJS:
+        except (O.RangeErrorJS, ValueError):  # (ValueError: JSON.parse of the client's tree threw)
             out.append("500")  # index.ts:224-233: the request rolled back
             continue
         out.append(RESP(messages=[dict(timestamp=t, content=c) for t, c in rows],
@@ -186,3 +186,79 @@ def test_node_id_not_hex_is_handed_over_unapplied(eng):
     assert got[2] == _expected(b[2:])[0]
     assert srv.store.n_messages == 3  # nothing of "u" was stored
     srv.close()
+
+
+def test_fast_path_equals_per_request_path(eng):
+    """sync() runs a call's common requests as whole-call arrays (batch
+    decode, one ingest per round, one tree parse, one selection, the trees'
+    JSON in one device launch, batch encode); sync_per_request() runs every
+    request through the per-request path.  Same bytes, same errors, over
+    several rounds per user, a truncated body, a client tree that does not
+    parse, a nodeId that is not 16 hex chars, an invalid date (500) and a
+    lenient timestamp."""
+    from evolu_amd.server import SyncServer
+
+    rng = random.Random(77)
+    bodies = _requests(5, n_users=20, n_req=160)
+    nodes = [W.node_id(rng) for _ in range(2)]
+    u0 = REQ.FromString(bodies[0]).userId
+    bodies.insert(11, b"\x0a\x05ab")
+    bodies.insert(20, REQ(messages=REQ.FromString(bodies[3]).messages, userId="tree-bad", nodeId=nodes[0],
+                          merkleTree='{"hash":').SerializeToString())
+    bodies.insert(30, REQ(messages=REQ.FromString(bodies[4]).messages, userId="node-bad", nodeId="xyz",
+                          merkleTree="{}").SerializeToString())
+    bodies.insert(40, REQ(messages=[dict(timestamp="2024-02-32T10:00:00.000Z-0000-" + nodes[1], content=b"z")],
+                          userId=u0, nodeId=nodes[1], merkleTree="{}").SerializeToString())
+    bodies.insert(50, REQ(messages=[dict(timestamp="2024-02-30T23:59:59.999Z-000a-" + nodes[1], content=b"l")],
+                          userId="lenient", nodeId=nodes[1], merkleTree="{}").SerializeToString())
+    bodies.append(REQ(messages=REQ.FromString(bodies[60]).messages, userId="lenient", nodeId=nodes[0],
+                      merkleTree="{}").SerializeToString())
+    a = SyncServer(eng, 32)
+    b = SyncServer(eng, 32)
+    ga, gb = a.sync(bodies), b.sync_per_request(bodies)
+    assert set(a.timing) >= {"decode", "ingest", "trees", "select", "json", "encode", "per_request"}
+    for i, (x, y) in enumerate(zip(ga, gb)):
+        if isinstance(x, (bytes, type(None))):
+            assert x == y, i
+        else:
+            assert type(x) is type(y), (i, x, y)
+    want = _expected(bodies)
+    for i, (x, w) in enumerate(zip(ga, want)):
+        if isinstance(x, bytes):
+            assert x == w, i
+    assert sum(isinstance(x, bytes) for x in ga) > 150
+    a.close()
+    b.close()
+
+
+def test_e2e_bodies_vs_oracle(eng):
+    """The bench's config3_e2e round in miniature (bench.e2e_bodies: one
+    SyncRequest per owner with its client tree's JSON from the device
+    emitter): SyncServer.sync_arena's responses byte for byte against the
+    oracle's ServerDb.sync (index.ts:204-216) of the same bodies."""
+    import numpy as np
+
+    import bench
+    from evolu_amd import synth
+    from evolu_amd.server import SyncServer
+
+    owners, per = 24, 60
+    ts_np, owner_np, millis = synth.config3(owners, per, seed_config=31, request=per)
+    o64 = owner_np.astype(np.int64)
+    order = np.lexsort((millis, o64))
+    rank = np.empty(len(order), dtype=np.int64)
+    cnt = np.bincount(o64, minlength=owners)
+    rank[order] = np.arange(len(order)) - (np.cumsum(cnt) - cnt)[o64[order]]
+    keep = rank < (0.9 * cnt[o64]).astype(np.int64)
+    client = eng.merkle_insert(eng.tree_new(owners), eng.dev(np.ascontiguousarray(ts_np[keep])),
+                               eng.dev(np.ascontiguousarray(owner_np[keep])))
+    arena, off = bench.e2e_bodies(eng, ts_np, owner_np, client)
+    bodies = [arena[int(off[k]):int(off[k + 1])].tobytes() for k in range(len(off) - 1)]
+    want = _expected(bodies)
+    srv = SyncServer(eng, owners)
+    got = srv.sync_arena(arena, off)
+    assert len(got) == len(want) == owners
+    for g, w in zip(got, want):
+        assert isinstance(g, memoryview) and bytes(g) == w
+    srv.close()
+    client.free()
