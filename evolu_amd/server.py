@@ -186,6 +186,7 @@ class SyncServer:
 
         lib, eng = _lib.load(), self.eng
         T = self.timing = dict.fromkeys(("decode", "ingest", "trees", "select", "json", "encode", "per_request"), 0.0)
+        t_call = time.perf_counter()
         n = len(boff) - 1
         out: List[Result] = [None] * n
         if n == 0:
@@ -237,14 +238,19 @@ class SyncServer:
         for k in range(int(rnd_of.max()) + 1 if n else 0):
             idx = np.flatnonzero(rnd_of == k)
             fast, slow = [], []
-            for i in idx:
-                u = users[i]
-                if u in self.detached:
-                    continue  # out[i] stays None
-                if not node_ok[i]:
-                    self.detached.add(u)  # NOT LIKE '%' || nodeId with any nodeId is not modelled
-                    continue
-                (slow if u in self.lenient else fast).append(int(i))
+            if not self.detached and not self.lenient:  # (the common case, without a loop)
+                for i in idx[~node_ok[idx]]:
+                    self.detached.add(users[i])  # NOT LIKE '%' || nodeId with any nodeId is not modelled
+                fast = idx[node_ok[idx]].tolist()
+            else:
+                for i in idx.tolist():
+                    u = users[i]
+                    if u in self.detached:
+                        continue  # out[i] stays None
+                    if not node_ok[i]:
+                        self.detached.add(u)
+                        continue
+                    (slow if u in self.lenient else fast).append(i)
             rejected = []
             if fast:
                 t0 = time.perf_counter()
@@ -283,6 +289,7 @@ class SyncServer:
                 self._respond_fast(answered, arena, boff, inf, nodes16, out, T,
                                    lambda i: self._request_at(i, arena, boff, inf, users, log, ts_len, ts_off,
                                                               msg_base), views)
+        T["other"] = time.perf_counter() - t_call - sum(T.values())  # (the host's round bookkeeping)
         return out
 
     def _request_at(self, i, arena, boff, inf, users, log, ts_len, ts_off, msg_base):
