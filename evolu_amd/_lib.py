@@ -46,6 +46,7 @@ OPT_SELECT_PATH = 7
 
 PB_SYNC_REQUEST = 1
 PB_SYNC_RESPONSE = 2
+TREE_UNSORTED = 1000  # evm_tree_from_json_dev: children keys out of order (the host parser reads it)
 
 DIFF_NONE = -1
 DIFF_RANGE_ERROR = -2
@@ -108,6 +109,12 @@ SIGNATURES = {
     "evm_pb_split_batch": (_i, [_i, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     "evm_pb_encode_requests": (_i, [_u32, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "evm_pb_encode_responses": (_i, [_u32, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "evm_pb_scan_dev": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp]),
+    "evm_pb_split_dev": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "evm_gather_spans_dev": (_i, [_vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    "evm_tree_from_json_dev": (_i, [_vp, _u32, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),
+    "evm_pb_encode_responses_dev": (_i, [_vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _sz,
+                                         _vp, C.POINTER(C.c_uint64)]),
     "evm_store_since": (_i, [_vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_server_select": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_store_select_after": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),

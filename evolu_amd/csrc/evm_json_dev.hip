@@ -241,6 +241,21 @@ __global__ __launch_bounds__(JT) void k_json_emit(TreeJ t, const u32* __restrict
 
 }  // namespace
 
+// the two passes for a caller that places the texts itself (the device
+// SyncResponse encoder: each text straight into its response)
+int evm::json_lengths(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, uint64_t* len, uint32_t* bad) {
+  const TreeJ tv{t->off, t->end, t->ck, t->pfx, t->n_owners};
+  const u32 grid = (u32)std::min<size_t>(std::max<u32>(n, 1), (size_t)ctx->n_cu * 8);
+  if (n) KLAUNCH(k_json_len, dim3(grid), dim3(JT), tv, owners, n, (u64*)len, bad);
+  return hip_ok(hipGetLastError());
+}
+int evm::json_emit(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, const uint64_t* off, char* out) {
+  const TreeJ tv{t->off, t->end, t->ck, t->pfx, t->n_owners};
+  const u32 grid = (u32)std::min<size_t>(std::max<u32>(n, 1), (size_t)ctx->n_cu * 8);
+  if (n) KLAUNCH(k_json_emit, dim3(grid), dim3(JT), tv, owners, n, (const u64*)off, out);
+  return hip_ok(hipGetLastError());
+}
+
 extern "C" int evm_tree_to_json_batch(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, char* out,
                                       size_t cap, uint64_t* off, uint64_t* total) {
   if (!ctx || !t || !off || !total || (n && !owners && n > t->n_owners)) return EVM_EINVAL;

@@ -2185,7 +2185,6 @@ __global__ __launch_bounds__(256) void k_seg_key(MinuteSrc msrc, const u32* __re
     for (int j = 0; j < SK_ITEMS; ++j) {
       const size_t i = i0 + (size_t)j * blockDim.x;
       o[j] = i < n ? owner[i] : 0u;
-      mnt[j] = i < n ? minute_at(msrc, i) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < SK_ITEMS; ++j) {
@@ -2193,6 +2192,13 @@ __global__ __launch_bounds__(256) void k_seg_key(MinuteSrc msrc, const u32* __re
       bad |= !ok;
       r[j] = own[ok ? o[j] : 0u];
       if (!ok) r[j].b0 = NS, r[j].nbo = 1;
+    }
+    // only a message of a cut owner needs its minute: the rows of the rest
+    // (an owner of one segment -- most owners of a Zipf stream) are not read
+#pragma unroll
+    for (int j = 0; j < SK_ITEMS; ++j) {
+      const size_t i = i0 + (size_t)j * blockDim.x;
+      mnt[j] = i < n && r[j].nbo > 1 ? minute_at(msrc, i) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < SK_ITEMS; ++j) {

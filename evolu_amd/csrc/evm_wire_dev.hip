@@ -1,0 +1,676 @@
+// The sync server's wire work on the device: a round's SyncRequest bodies
+// decoded where they lie in HBM, their client trees parsed, and the
+// SyncResponse bodies built in HBM (apps/server/src/index.ts:112-116
+// parseBody = SyncRequest.fromBinary, :121-136 merkleTreeFromString of the
+// request's tree, :233-241 SyncResponse.toBinary with merkleTreeToString).
+//
+// Same grammar, same results as the host codecs (evm_proto.cpp's Reader /
+// walk / read_msg, evm_json.cpp's Parser, evm_pb_encode_responses): one
+// thread per body or tree runs the same sequential walk, so the accept /
+// reject decisions are the host's by construction -- the tests compare the
+// two byte for byte.  A tree the device reads in an order the leaf list
+// cannot hold without a sort (children keys not ascending: JSON.stringify
+// never writes that, a hand-made client might) is reported per owner
+// (EVM_TREE_UNSORTED) and left to the host parser.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "evm_device.hpp"
+#include "evm_internal.hpp"
+#include "evm_prims.hpp"
+
+using namespace evm;
+
+namespace {
+
+// ------------------------------------------------------------------ protobuf
+// evm_proto.cpp's Reader on device bytes (the same checks, in the same order)
+struct DReader {
+  const uint8_t* p;
+  const uint8_t* e;
+  bool ok;
+  __device__ bool more() const { return ok && p < e; }
+  __device__ u64 varint() {
+    u64 v = 0;
+    for (int sh = 0; sh < 70; sh += 7) {
+      if (p >= e) {
+        ok = false;
+        return 0;
+      }
+      const uint8_t b = *p++;
+      if (sh == 63 && b > 1) {
+        ok = false;
+        return 0;
+      }
+      v |= (u64)(b & 0x7f) << sh;
+      if (!(b & 0x80)) return v;
+    }
+    ok = false;
+    return 0;
+  }
+  __device__ bool bytes(const uint8_t** q, u64* n) {
+    const u64 len = varint();
+    if (!ok || len > (u64)(e - p)) return ok = false;
+    *q = p;
+    *n = len;
+    p += len;
+    return true;
+  }
+  __device__ bool skip(u32 wt) {
+    switch (wt) {
+      case 0:
+        varint();
+        return ok;
+      case 1:
+        if (e - p < 8) return ok = false;
+        p += 8;
+        return true;
+      case 2: {
+        const uint8_t* q;
+        u64 n;
+        return bytes(&q, &n);
+      }
+      case 5:
+        if (e - p < 4) return ok = false;
+        p += 4;
+        return true;
+      default:
+        return ok = false;
+    }
+  }
+};
+
+struct DMsg {
+  const uint8_t* ts;
+  u64 ts_len;
+  const uint8_t* content;
+  u64 content_len;
+};
+
+__device__ bool d_read_msg(const uint8_t* q, u64 n, DMsg* m) {
+  DReader r{q, q + n, true};
+  *m = DMsg{nullptr, 0, nullptr, 0};
+  while (r.more()) {
+    const u64 tag = r.varint();
+    if (!r.ok) return false;
+    const u32 field = (u32)(tag >> 3), wt = (u32)(tag & 7);
+    if (field == 1 || field == 2) {
+      if (wt != 2) return false;
+      if (field == 1) r.bytes(&m->ts, &m->ts_len);
+      else r.bytes(&m->content, &m->content_len);
+    } else if (field == 0 || !r.skip(wt)) {
+      return false;
+    }
+  }
+  return r.ok;
+}
+
+// evm_proto.cpp's walk(): on_msg(index, msg) per message
+template <typename F>
+__device__ int d_walk(int kind, const uint8_t* buf, u64 len, evm_pb_sync* info, F on_msg) {
+  DReader r{buf, buf + len, true};
+  evm_pb_sync s{0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const u32 tree_field = kind == EVM_PB_SYNC_REQUEST ? 4u : 2u;
+  while (r.more()) {
+    const u64 tag = r.varint();
+    if (!r.ok) return EVM_EINVAL;
+    const u32 field = (u32)(tag >> 3), wt = (u32)(tag & 7);
+    if (field == 0) return EVM_EINVAL;
+    const bool is_str = field == 1 || field == tree_field || (kind == EVM_PB_SYNC_REQUEST && (field == 2 || field == 3));
+    if (!is_str) {
+      if (!r.skip(wt)) return EVM_EINVAL;
+      continue;
+    }
+    if (wt != 2) return EVM_EINVAL;
+    const uint8_t* q;
+    u64 n;
+    if (!r.bytes(&q, &n)) return EVM_EINVAL;
+    const u64 off = (u64)(q - buf);
+    if (field == 1) {
+      DMsg m;
+      if (!d_read_msg(q, n, &m)) return EVM_EINVAL;
+      if (m.ts_len != 46) ++s.nonstd_ts;
+      s.content_bytes += m.content_len;
+      on_msg(s.n_messages, m);
+      ++s.n_messages;
+    } else if (field == tree_field) {
+      s.tree_off = off;
+      s.tree_len = n;
+    } else if (field == 2) {
+      s.user_off = off;
+      s.user_len = n;
+    } else {
+      s.node_off = off;
+      s.node_len = n;
+    }
+  }
+  if (!r.ok) return EVM_EINVAL;
+  if (info) *info = s;
+  return EVM_OK;
+}
+
+__global__ void k_pb_scan(int kind, const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
+                          evm_pb_sync* __restrict__ info, int32_t* __restrict__ status) {
+  for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const u64 a = off[k], b = off[k + 1];
+    evm_pb_sync s{0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int st = b < a ? EVM_EINVAL : d_walk(kind, arena + a, b - a, &s, [](u64, const DMsg&) {});
+    if (st) s = evm_pb_sync{0, 0, 0, 0, 0, 0, 0, 0, 0};
+    info[k] = s;
+    status[k] = st;
+  }
+}
+
+// body k's messages into the engine's rows (evm_pb_split_batch's layout):
+// ts rows from msg_base[k] (46 bytes + zero padding, 0xFF for a timestamp
+// that is not 46 bytes), contents concatenated from content_base[k],
+// content_off (N + 1 global entries), the owner of each row (owner_of[k])
+__global__ void k_pb_split(int kind, const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
+                           const int32_t* __restrict__ status, const u64* __restrict__ msg_base,
+                           const u64* __restrict__ content_base, const u32* __restrict__ owner_of, char* __restrict__ ts,
+                           u64 stride, u64* __restrict__ content_off, uint8_t* __restrict__ content,
+                           u32* __restrict__ owner, u32* __restrict__ bad) {
+  for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    if (status[k]) continue;
+    const u64 a = off[k];
+    const u64 m0 = msg_base[k], c0 = content_base[k];
+    const u32 ow = owner_of ? owner_of[k] : 0u;
+    u64 co = 0;
+    const int st = d_walk(kind, arena + a, off[k + 1] - a, nullptr, [&](u64 i, const DMsg& m) {
+      char* row = ts + (m0 + i) * stride;
+      if (m.ts_len == 46)
+        for (int j = 0; j < 46; ++j) row[j] = (char)m.ts[j];
+      else
+        for (int j = 0; j < 46; ++j) row[j] = (char)0xff;
+      for (u64 j = 46; j < stride; ++j) row[j] = 0;
+      content_off[m0 + i] = c0 + co;
+      for (u64 j = 0; j < m.content_len; ++j) content[c0 + co + j] = m.content[j];
+      co += m.content_len;
+      if (owner) owner[m0 + i] = ow;
+    });
+    if (st) atomicOr(bad, 1u);  // (a body that scanned fine: cannot happen)
+    // the entry after a body's last message is the next body's first (or the end)
+    if (!st) content_off[msg_base[k + 1]] = c0 + co;
+  }
+}
+
+// packed copies of n byte spans: dst[dst_off[k] ..] = src[src_off[k] .. + len[k])
+__global__ void k_gather_spans(const uint8_t* __restrict__ src, const u64* __restrict__ src_off,
+                               const u64* __restrict__ len, const u64* __restrict__ dst_off, u32 n,
+                               uint8_t* __restrict__ dst) {
+  for (u32 k = blockIdx.x; k < n; k += gridDim.x)
+    for (u64 j = threadIdx.x; j < len[k]; j += blockDim.x) dst[dst_off[k] + j] = src[src_off[k] + j];
+}
+
+// ---------------------------------------------------------------- tree JSON
+// evm_json.cpp's Parser as an explicit stack (depth <= CODE_DIGITS), one
+// thread per owner; the frames of a block's threads live in LDS.
+constexpr int JP_THREADS = 64;
+constexpr int JP_LEVELS = CODE_DIGITS + 1;
+constexpr u32 JP_MIN_NODE = 14;
+constexpr u64 CODE_MASK40 = (1ull << 40) - 1;  // `"0":{"hash":0}`: the fewest bytes of a non-root node
+
+__device__ __forceinline__ bool jws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+struct JText {
+  const uint8_t* p;
+  const uint8_t* e;
+  __device__ void ws() {
+    while (p < e && jws(*p)) ++p;
+  }
+  __device__ bool lit(uint8_t c) {
+    ws();
+    if (p < e && *p == c) {
+      ++p;
+      return true;
+    }
+    return false;
+  }
+  __device__ int key() {  // 0, 1, 2 for the digits, 3 for "hash", -1 otherwise
+    ws();
+    if (p >= e || *p != '"') return -1;
+    const uint8_t* q = ++p;
+    while (p < e && *p != '"') {
+      if (*p == '\\') return -1;
+      ++p;
+    }
+    if (p >= e) return -1;
+    const u64 len = (u64)(p - q);
+    ++p;
+    if (len == 1 && q[0] >= '0' && q[0] <= '2') return q[0] - '0';
+    if (len == 4 && q[0] == 'h' && q[1] == 'a' && q[2] == 's' && q[3] == 'h') return 3;
+    return -1;
+  }
+  __device__ bool integer(int32_t* v) {
+    ws();
+    bool neg = false;
+    if (p < e && *p == '-') {
+      neg = true;
+      ++p;
+    }
+    if (p >= e || *p < '0' || *p > '9') return false;
+    if (*p == '0' && p + 1 < e && p[1] >= '0' && p[1] <= '9') return false;
+    int64_t x = 0;
+    while (p < e && *p >= '0' && *p <= '9') {
+      x = x * 10 + (*p - '0');
+      if (x > 2147483648LL) return false;
+      ++p;
+    }
+    if (p < e && (*p == '.' || *p == 'e' || *p == 'E')) return false;
+    if (neg) x = -x;
+    if (x < (int64_t)INT32_MIN || x > (int64_t)INT32_MAX || (neg && x == 0)) return false;
+    *v = (int32_t)x;
+    return true;
+  }
+};
+
+// owner o's text at json + jat[o], jlen[o] bytes (jlen 0: no request, the
+// empty tree); its leaves from slot base[o] (room for the bound), the
+// owner-local exclusive prefix XOR beside them; status[o]: 0, EVM_ETREE, or
+// EVM_TREE_UNSORTED
+__global__ __launch_bounds__(JP_THREADS) void k_json_parse(const uint8_t* __restrict__ json, const u64* __restrict__ jat,
+                                                           const u64* __restrict__ jlen, u32 n_owners,
+                                                           const u64* __restrict__ base, u64* __restrict__ t_off,
+                                                           u64* __restrict__ t_end, u64* __restrict__ ck,
+                                                           int32_t* __restrict__ xr, int32_t* __restrict__ pfx,
+                                                           int32_t* __restrict__ status, u64* __restrict__ n_leaves) {
+  __shared__ int32_t s_h[JP_LEVELS][JP_THREADS];
+  __shared__ int32_t s_cx[JP_LEVELS][JP_THREADS];
+  __shared__ uint8_t s_fl[JP_LEVELS][JP_THREADS];  // seen keys (bits 0-3) | any child (bit 4)
+  __shared__ u32 s_first[JP_LEVELS][JP_THREADS];    // leaves emitted when the node opened
+  const u32 o = blockIdx.x * JP_THREADS + threadIdx.x;
+  if (o >= n_owners) return;
+  const u32 me = threadIdx.x;
+  const u64 b0 = base[o];
+  const u64 bound = base[o + 1] - b0 - 1;  // leaf slots (one more holds the root's prefix)
+  t_off[o] = b0;
+  u64 cnt = 0;
+  int32_t run = 0;
+  int st = 0;
+  const u64 L = jlen[o];
+  if (L) {
+    JText tx{json + jat[o], json + jat[o] + L};
+    // the frame of the node being read at depth d: prefix = the code so far
+    u64 prefix = 0;
+    int d = 0;
+    if (!tx.lit('{')) st = EVM_ETREE;
+    s_fl[0][me] = 0;
+    s_h[0][me] = 0;
+    s_cx[0][me] = 0;
+    s_first[0][me] = 0;
+    bool fresh = true;  // just after a node's '{'
+    while (!st) {
+      // next member of the node at depth d, or its end
+      bool close = false;
+      if (fresh) {
+        close = tx.lit('}');
+      } else if (tx.lit(',')) {
+        close = false;
+      } else if (tx.lit('}')) {
+        close = true;
+      } else {
+        st = EVM_ETREE;
+        break;
+      }
+      fresh = false;
+      if (!close) {
+        const int k = tx.key();
+        const uint8_t fl = s_fl[d][me];
+        if (k < 0 || (fl >> k) & 1u || !tx.lit(':')) {
+          st = EVM_ETREE;
+          break;
+        }
+        s_fl[d][me] = fl | (uint8_t)(1u << k);
+        if (k == 3) {
+          int32_t h;
+          if (!tx.integer(&h)) {
+            st = EVM_ETREE;
+            break;
+          }
+          s_h[d][me] = h;
+          continue;
+        }
+        if (d >= CODE_DIGITS) {
+          st = EVM_ETREE;
+          break;
+        }
+        const int sh = 2 * (CODE_DIGITS - 1 - d);
+        prefix |= (u64)(k + 1) << sh;
+        ++d;
+        s_fl[d][me] = 0;
+        s_h[d][me] = 0;
+        s_cx[d][me] = 0;
+        s_first[d][me] = (u32)cnt;
+        if (!tx.lit('{')) {
+          st = EVM_ETREE;
+          break;
+        }
+        fresh = true;
+        continue;
+      }
+      // the node at depth d ends
+      const uint8_t fl = s_fl[d][me];
+      const bool seen_h = (fl >> 3) & 1u, any = (fl >> 4) & 1u;
+      const int32_t h = s_h[d][me], cx = s_cx[d][me];
+      if (d == 0) {  // the root: {} only, or children + a hash equal to their XOR
+        if (seen_h ? !(any && (h ^ cx) == 0) : any) st = EVM_ETREE;
+        break;
+      }
+      if (!seen_h) {
+        st = EVM_ETREE;
+        break;
+      }
+      const int32_t t = h ^ cx;
+      if (!any || t != 0) {
+        // a node closes after its subtree's leaves, whose codes extend its
+        // own: it goes in front of them (a node with children and its own
+        // leaf -- a shorter key -- is rare), after every leaf read before
+        const u64 at = s_first[d][me];
+        if (at && (ck[b0 + at - 1] & CODE_MASK40) >= prefix) {
+          st = EVM_TREE_UNSORTED;  // (children keys not ascending: the host parser sorts)
+          break;
+        }
+        if (cnt >= bound) {
+          st = EVM_ETREE;
+          break;
+        }
+        for (u64 i = cnt; i > at; --i) {
+          ck[b0 + i] = ck[b0 + i - 1];
+          xr[b0 + i] = xr[b0 + i - 1];
+          pfx[b0 + i] = pfx[b0 + i - 1] ^ t;
+        }
+        ck[b0 + at] = ((u64)o << 40) | prefix;
+        xr[b0 + at] = t;
+        if (at == cnt) pfx[b0 + at] = run;
+        run ^= t;
+        ++cnt;
+      }
+      // back to the parent: its children's XOR and presence
+      --d;
+      s_cx[d][me] ^= h;
+      s_fl[d][me] |= 0x10;
+      prefix &= ~((4ull << (2 * (CODE_DIGITS - 1 - d))) - 1ull);  // (the digit at depth d and below)
+    }
+    if (!st) {
+      tx.ws();
+      if (tx.p != tx.e) st = EVM_ETREE;
+    }
+  }
+  if (st) cnt = 0;
+  pfx[b0 + cnt] = st ? 0 : run;
+  t_end[o] = b0 + cnt;
+  status[o] = st;
+  if (cnt) atomicAdd(n_leaves, cnt);
+}
+
+// leaf slots per owner: the bound on its nodes + 1 (the root's prefix slot)
+__global__ void k_json_bound(const u64* __restrict__ jlen, u32 n, u64* __restrict__ slots) {
+  for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x)
+    slots[o] = jlen[o] / JP_MIN_NODE + 2;
+}
+
+// -------------------------------------------------------------- responses
+// A message log segment as the device reads it (evm_pb_encode_responses'
+// seg_* arrays): ids [base, next base), row = id - base or row[id - base],
+// 46-B timestamp at ts + row * stride, content [coff[row], coff[row + 1]).
+struct DSeg {
+  u64 base;
+  const u64* row;
+  const char* ts;
+  const u64* coff;
+  const uint8_t* content;
+};
+
+__device__ __forceinline__ u32 vlen(u64 v) {
+  u32 k = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    ++k;
+  }
+  return k;
+}
+__device__ __forceinline__ u32 put_varint(uint8_t* d, u64 v) {
+  u32 k = 0;
+  while (v >= 0x80) {
+    d[k++] = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  d[k++] = (uint8_t)v;
+  return k;
+}
+
+__device__ __forceinline__ bool locate(const DSeg* segs, u32 n_seg, u64 id, u64 stride, const char** t,
+                                       const uint8_t** c, u64* cl) {
+  u32 lo = 0, hi = n_seg;  // first segment with base > id
+  while (lo < hi) {
+    const u32 m = (lo + hi) >> 1;
+    if (segs[m].base <= id) lo = m + 1;
+    else hi = m;
+  }
+  if (lo == 0) return false;
+  const DSeg& s = segs[lo - 1];
+  const u64 k = id - s.base;
+  const u64 row = s.row ? s.row[k] : k;
+  *t = s.ts + row * stride;
+  const u64 a = s.coff[row], b = s.coff[row + 1];
+  *c = s.content + a;
+  *cl = b - a;
+  return true;
+}
+
+// bytes of selected message m: `messages` field (1) around {timestamp (1), content (2)}
+__global__ void k_resp_msg_size(const u64* __restrict__ sel_id, u64 S, const DSeg* __restrict__ segs, u32 n_seg,
+                                u64 stride, u64* __restrict__ msz, u32* __restrict__ bad) {
+  for (u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x; m < S; m += (u64)gridDim.x * blockDim.x) {
+    const char* t;
+    const uint8_t* c;
+    u64 cl = 0;
+    u64 body = 48;
+    if (!locate(segs, n_seg, sel_id[m], stride, &t, &c, &cl)) atomicOr(bad, 1u);
+    else if (cl) body += 1 + vlen(cl) + cl;
+    msz[m] = 1 + vlen(body) + body;
+  }
+}
+
+// per response: its messages' bytes + the merkleTree field (2)
+__global__ void k_resp_len(u32 n, const u64* __restrict__ sel_off, const u64* __restrict__ mpos,
+                           const u64* __restrict__ jlen, u64* __restrict__ rlen) {
+  for (u32 r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+    const u64 jl = jlen[r];
+    rlen[r] = (mpos[sel_off[r + 1]] - mpos[sel_off[r]]) + (jl ? 1 + vlen(jl) + jl : 0);
+  }
+}
+
+// the merkleTree field's header; jdst[r] = where its text goes
+__global__ void k_resp_tree_hdr(u32 n, const u64* __restrict__ sel_off, const u64* __restrict__ mpos,
+                                const u64* __restrict__ jlen, const u64* __restrict__ out_off, uint8_t* __restrict__ out,
+                                u64* __restrict__ jdst) {
+  for (u32 r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+    const u64 jl = jlen[r];
+    u64 at = out_off[r] + (mpos[sel_off[r + 1]] - mpos[sel_off[r]]);
+    if (jl) {
+      out[at++] = (uint8_t)(2u << 3 | 2u);
+      at += put_varint(out + at, jl);
+    }
+    jdst[r] = at;
+  }
+}
+
+// every selected message's bytes, one thread each
+__global__ void k_resp_msgs(u32 n, const u64* __restrict__ sel_off, const u64* __restrict__ sel_id, u64 S,
+                            const DSeg* __restrict__ segs, u32 n_seg, u64 stride, const u64* __restrict__ mpos,
+                            const u64* __restrict__ out_off, uint8_t* __restrict__ out) {
+  for (u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x; m < S; m += (u64)gridDim.x * blockDim.x) {
+    u32 lo = 0, hi = n;  // the response: last r with sel_off[r] <= m
+    while (lo < hi) {
+      const u32 mid = (lo + hi) >> 1;
+      if (sel_off[mid + 1] <= m) lo = mid + 1;
+      else hi = mid;
+    }
+    const u32 r = lo;
+    const char* t;
+    const uint8_t* c;
+    u64 cl = 0;
+    if (!locate(segs, n_seg, sel_id[m], stride, &t, &c, &cl)) continue;  // (reported by k_resp_msg_size)
+    uint8_t* d = out + out_off[r] + (mpos[m] - mpos[sel_off[r]]);
+    const u64 body = 48 + (cl ? 1 + vlen(cl) + cl : 0);
+    u32 k = 0;
+    d[k++] = (uint8_t)(1u << 3 | 2u);
+    k += put_varint(d + k, body);
+    d[k++] = (uint8_t)(1u << 3 | 2u);
+    d[k++] = 46;
+    for (int j = 0; j < 46; ++j) d[k + j] = (uint8_t)t[j];
+    k += 46;
+    if (cl) {
+      d[k++] = (uint8_t)(2u << 3 | 2u);
+      k += put_varint(d + k, cl);
+      for (u64 j = 0; j < cl; ++j) d[k + j] = c[j];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int evm_pb_scan_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n, evm_pb_sync* info,
+                    int32_t* status) {
+  if (!ctx || (n && (!arena || !off || !info || !status)) ||
+      (kind != EVM_PB_SYNC_REQUEST && kind != EVM_PB_SYNC_RESPONSE))
+    return EVM_EINVAL;
+  if (n) KLAUNCH(k_pb_scan, dim3(grid_for(n, 64, 1 << 16)), dim3(64), kind, arena, (const u64*)off, n, info, status);
+  return hip_ok(hipGetLastError());
+}
+
+int evm_pb_split_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n,
+                     const int32_t* status, const uint64_t* msg_base, const uint64_t* content_base,
+                     const uint32_t* owner_of, char* ts, size_t stride, uint64_t* content_off, uint8_t* content,
+                     uint32_t* owner) {
+  if (!ctx || (n && (!arena || !off || !status || !msg_base || !content_base || !ts || !content_off || !content)) ||
+      stride < 46 || (kind != EVM_PB_SYNC_REQUEST && kind != EVM_PB_SYNC_RESPONSE))
+    return EVM_EINVAL;
+  if (!n) return EVM_OK;
+  Scratch S(ctx);
+  u32* bad = S.alloc<u32>(1);
+  if (!bad) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
+  KLAUNCH(k_pb_split, dim3(grid_for(n, 64, 1 << 16)), dim3(64), kind, arena, (const u64*)off, n, status,
+          (const u64*)msg_base, (const u64*)content_base, owner_of, ts, (u64)stride, (u64*)content_off, content, owner,
+          bad);
+  u32 hb = 0;
+  HIPR(hipMemcpyAsync(&hb, bad, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  return hb ? EVM_EINVAL : EVM_OK;
+}
+
+int evm_gather_spans_dev(evm_ctx* ctx, const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
+                         const uint64_t* dst_off, uint32_t n, uint8_t* dst) {
+  if (!ctx || (n && (!src || !src_off || !len || !dst_off || !dst))) return EVM_EINVAL;
+  if (n) KLAUNCH(k_gather_spans, dim3(grid_for(n, 1, 1 << 16)), dim3(64), src, (const u64*)src_off, (const u64*)len,
+                 (const u64*)dst_off, n, dst);
+  return hip_ok(hipGetLastError());
+}
+
+int evm_tree_from_json_dev(evm_ctx* ctx, uint32_t n_owners, const uint8_t* json, const uint64_t* at,
+                           const uint64_t* len, int32_t* status, evm_tree** out) {
+  if (!ctx || !out || !status || (n_owners && (!json || !at || !len))) return EVM_EINVAL;
+  *out = nullptr;
+  Scratch S(ctx);
+  u64* bnd = S.alloc<u64>((size_t)n_owners + 1);
+  u64* slots = S.alloc<u64>((size_t)n_owners + 1);
+  u64* nl = S.alloc<u64>(1);
+  if (!bnd || !slots || !nl) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(nl, 0, sizeof(u64), ctx->stream));
+  if (n_owners) KLAUNCH(k_json_bound, dim3(grid_for(n_owners, 256)), dim3(256), (const u64*)len, n_owners, bnd);
+  int st = scan_exclusive<u64, OpAdd>(ctx, S, bnd, n_owners, slots, slots + n_owners);
+  if (st) return st;
+  u64 cap = 0;
+  HIPR(hipMemcpyAsync(&cap, slots + n_owners, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  evm_tree* t = nullptr;
+  if ((st = tree_alloc_gapped(ctx, n_owners, std::max<u64>(cap, 1), &t))) return st;
+  HIPR(hipMemsetAsync(t->off + n_owners, 0, sizeof(u64), ctx->stream));
+  if (n_owners)
+    KLAUNCH(k_json_parse, dim3((n_owners + JP_THREADS - 1) / JP_THREADS), dim3(JP_THREADS), json, (const u64*)at,
+            (const u64*)len, n_owners, (const u64*)slots, (u64*)t->off, (u64*)t->end, (u64*)t->ck, t->xr, t->pfx,
+            status, nl);
+  u64 hl = 0;
+  st = hip_ok(hipMemcpyAsync(&hl, nl, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+  if (!st) st = hip_ok(hipStreamSynchronize(ctx->stream));
+  if (st) {
+    tree_destroy(ctx, t);
+    return st;
+  }
+  t->n_leaves = hl;
+  *out = t;
+  return EVM_OK;
+}
+
+int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, const uint32_t* owners,
+                                const uint64_t* sel_off, const uint64_t* sel_id, uint32_t n_seg,
+                                const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
+                                size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
+                                uint8_t* out, size_t cap, uint64_t* out_off, uint64_t* total) {
+  if (!ctx || !tree || !total || (n && (!owners || !sel_off || !out_off)) || stride < 46 ||
+      (n_seg && (!seg_base || !seg_ts || !seg_coff || !seg_content)))
+    return EVM_EINVAL;
+  *total = 0;
+  Scratch S(ctx);
+  u64 hs[2] = {0, 0};  // selected ids: sel_off[n] (device)
+  if (n) {
+    HIPR(hipMemcpyAsync(&hs[0], sel_off + n, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+    HIPR(hipStreamSynchronize(ctx->stream));
+  }
+  const u64 NS = hs[0];
+  if (NS && !sel_id) return EVM_EINVAL;
+  std::vector<DSeg> hseg(n_seg);
+  for (u32 s = 0; s < n_seg; ++s) {
+    hseg[s] = DSeg{seg_base[s], seg_row ? (const u64*)seg_row[s] : nullptr, seg_ts[s], (const u64*)seg_coff[s],
+                   seg_content[s]};
+    if (s && seg_base[s] < seg_base[s - 1]) return EVM_EINVAL;
+  }
+  DSeg* dseg = S.alloc<DSeg>(std::max<u32>(n_seg, 1));
+  u64* jlen = S.alloc<u64>((size_t)n + 1);
+  u64* msz = S.alloc<u64>(NS + 1);
+  u64* mpos = S.alloc<u64>(NS + 1);
+  u64* rlen = S.alloc<u64>((size_t)n + 1);
+  u64* jdst = S.alloc<u64>((size_t)n + 1);
+  u32* bad = S.alloc<u32>(1);
+  if (!dseg || !jlen || !msz || !mpos || !rlen || !jdst || !bad) return EVM_ENOMEM;
+  if (n_seg) HIPR(hipMemcpyAsync(dseg, hseg.data(), sizeof(DSeg) * n_seg, hipMemcpyHostToDevice, ctx->stream));
+  HIPR(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
+  int st = tree_compact(ctx, tree);
+  if (!st) st = json_lengths(ctx, tree, owners, n, reinterpret_cast<uint64_t*>(jlen), bad);
+  if (st) return st;
+  if (NS)
+    KLAUNCH(k_resp_msg_size, dim3(grid_for(NS, 256)), dim3(256), (const u64*)sel_id, NS, (const DSeg*)dseg, n_seg,
+            (u64)stride, msz, bad);
+  if ((st = scan_exclusive<u64, OpAdd>(ctx, S, msz, NS, mpos, mpos + NS))) return st;
+  if (n)
+    KLAUNCH(k_resp_len, dim3(grid_for(n, 256)), dim3(256), n, (const u64*)sel_off, (const u64*)mpos, (const u64*)jlen,
+            rlen);
+  u64* doff = reinterpret_cast<u64*>(out_off);
+  if ((st = scan_exclusive<u64, OpAdd>(ctx, S, rlen, n, doff, doff + n))) return st;
+  u32 hb = 0;
+  HIPR(hipMemcpyAsync(&hs[1], doff + n, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipMemcpyAsync(&hb, bad, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
+  HIPR(hipStreamSynchronize(ctx->stream));
+  if (hb) return EVM_EINVAL;  // (an owner out of range, or an id in no segment)
+  *total = hs[1];
+  if (!out) return EVM_OK;
+  if (hs[1] > cap) return EVM_ECAPACITY;
+  if (n)
+    KLAUNCH(k_resp_tree_hdr, dim3(grid_for(n, 256)), dim3(256), n, (const u64*)sel_off, (const u64*)mpos,
+            (const u64*)jlen, (const u64*)doff, out, jdst);
+  if ((st = json_emit(ctx, tree, owners, n, reinterpret_cast<const uint64_t*>(jdst), reinterpret_cast<char*>(out))))
+    return st;
+  if (NS)
+    KLAUNCH(k_resp_msgs, dim3(grid_for(NS, 256)), dim3(256), n, (const u64*)sel_off, (const u64*)sel_id, NS,
+            (const DSeg*)dseg, n_seg, (u64)stride, (const u64*)mpos, (const u64*)doff, out);
+  return hip_ok(hipGetLastError());
+}
+
+}  // extern "C"

@@ -83,6 +83,56 @@ def _np_ptr(a: np.ndarray):
 _HEX = set(b"0123456789abcdefABCDEF")
 
 
+class _Seg:
+    """A message-log segment (SyncServer._log): the timestamp rows (N, 48),
+    content offsets (N + 1), contents and an optional row map, held where the
+    call that logged them had them (numpy arrays: the host path; device
+    tensors: sync_device) and copied to the other side on first use there."""
+
+    def __init__(self, ts, coff, content, rowmap=None):
+        self.h = self.d = None
+        if isinstance(ts, np.ndarray):
+            self.h = (ts, np.ascontiguousarray(coff, dtype=np.uint64), content,
+                      None if rowmap is None else np.ascontiguousarray(rowmap, dtype=np.uint64))
+        else:
+            self.d = (ts, coff, content, rowmap)
+
+    def host(self):
+        if self.h is None:
+            ts, coff, content, rowmap = self.d
+            self.h = (ts.cpu().numpy(), coff.cpu().numpy().view(np.uint64), content.cpu().numpy(),
+                      None if rowmap is None else rowmap.cpu().numpy().view(np.uint64))
+        return self.h
+
+    def dev(self, device):
+        if self.d is None:
+            import torch
+
+            ts, coff, content, rowmap = self.h
+            up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+            self.d = (up(ts), up(coff.view(np.int64)), up(content), None if rowmap is None else up(rowmap.view(np.int64)))
+        return self.d
+
+
+class DeviceResponses:
+    """sync_device's answer: result[i] is True where response i is the bytes
+    buf[off[i] .. off[i + 1]) of the device buffer `buf`, else what sync()
+    would return for it (bytes from the host path, an exception object, a
+    HandedOver, or None)."""
+
+    def __init__(self, buf, off: np.ndarray, result: List):
+        self.buf, self.off, self.result = buf, off, result
+
+    def __len__(self):
+        return len(self.result)
+
+    def to_host(self) -> List[Result]:
+        """Every result as sync() returns it (the device bytes copied back)."""
+        hb = self.buf.cpu().numpy() if self.buf is not None else None
+        return [hb[int(self.off[i]):int(self.off[i + 1])].tobytes() if r is True else r
+                for i, r in enumerate(self.result)]
+
+
 class ParseBodyError(Exception):
     """index.ts:108-116: SyncRequest.fromBinary threw."""
 
@@ -124,14 +174,13 @@ class SyncServer:
             s = self.slot[user] = len(self.slot)
         return s
 
-    def _log(self, base: int, ts: np.ndarray, coff: np.ndarray, content: np.ndarray, rowmap=None):
+    def _log(self, base: int, ts, coff, content, rowmap=None):
         self._base.append(base)
-        self._segs.append((ts, np.ascontiguousarray(coff, dtype=np.uint64), content,
-                           None if rowmap is None else np.ascontiguousarray(rowmap, dtype=np.uint64)))
+        self._segs.append(_Seg(ts, coff, content, rowmap))
 
     def _message(self, mid: int):
         r = int(np.searchsorted(np.asarray(self._base), mid, side="right")) - 1
-        ts_a, o, content, rowmap = self._segs[r]
+        ts_a, o, content, rowmap = self._segs[r].host()
         k = mid - self._base[r]
         if rowmap is not None:
             k = int(rowmap[k])
@@ -176,6 +225,186 @@ class SyncServer:
         for rnd in rounds:
             self._round(rnd, out)
         return out
+
+    # ---------------------------------------------------------- device path
+    def sync_device(self, arena, off) -> "DeviceResponses":
+        """sync() of bodies resident in device memory: arena (uint8 tensor on
+        the engine's GPU), off (host uint64 [n + 1]).  The round runs on the
+        device end to end -- bodies decoded where they lie (evm_pb_scan_dev /
+        split_dev), one evm_server_ingest_ex, the client trees parsed there
+        (evm_tree_from_json_dev), one selection, the responses built in device
+        memory (evm_pb_encode_responses_dev, each tree's JSON emitted straight
+        into its response) -- and answers a DeviceResponses.  Only the round's
+        bookkeeping comes to the host: per body its sizes, userId and nodeId.
+
+        The same results as sync() on the same bodies: a call the device path
+        does not model as a whole -- an unparsable body, a timestamp that is
+        not 46 bytes, a nodeId that is not 16 hex chars, a userId twice, users
+        with rows under lenient spellings or handed over -- runs sync() on a
+        host copy of the bodies; requests whose owner the ingest rejects, or
+        whose merkleTree the device does not read (EVM_ETREE, or keys out of
+        order), take the per-request path as in sync()."""
+        import time
+
+        import torch
+
+        lib, eng = _lib.load(), self.eng
+        T = self.timing = dict.fromkeys(("decode", "ingest", "trees", "select", "encode", "per_request"), 0.0)
+        t_call = time.perf_counter()
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        n = len(off) - 1
+        dev = arena.device
+        P = lambda x: C.c_void_p(x.data_ptr())  # noqa: E731
+        if n == 0:
+            return DeviceResponses(None, np.zeros(1, dtype=np.uint64), [])
+        t0 = time.perf_counter()
+        off_d = torch.from_numpy(off.view(np.int64)).to(dev)
+        info_d = torch.empty((n, 9), dtype=torch.int64, device=dev)
+        st_d = torch.empty(n, dtype=torch.int32, device=dev)
+        check(lib.evm_pb_scan_dev(eng.h, REQUEST_KIND, P(arena), P(off_d), n, P(info_d), P(st_d)), "evm_pb_scan_dev")
+        inf = info_d.cpu().numpy().view(np.uint64)
+        st = st_d.cpu().numpy()
+        if st.any() or inf[:, 8].any() or (inf[:, 5] != 16).any() or self.detached or self.lenient:
+            return self._device_fallback(arena, off, T, t_call)
+        # the userIds and nodeIds, packed, to the host
+        ulen = inf[:, 3]
+        lens = np.concatenate([ulen, np.full(n, 16, dtype=np.uint64)])
+        src = np.concatenate([off[:-1] + inf[:, 2], off[:-1] + inf[:, 4]])
+        dst = np.zeros(2 * n + 1, dtype=np.uint64)
+        np.cumsum(lens, out=dst[1:])
+        packed = torch.empty(max(int(dst[-1]), 1), dtype=torch.uint8, device=dev)
+        up = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+        src_d, len_d, dst_d = up(src), up(lens), up(dst[:-1])
+        check(lib.evm_gather_spans_dev(eng.h, P(arena), P(src_d), P(len_d), P(dst_d), 2 * n, P(packed)),
+              "evm_gather_spans_dev")
+        pk = packed.cpu().numpy()
+        ub = int(dst[n])
+        nodes16 = pk[ub:ub + 16 * n].reshape(n, 16)
+        if not np.isin(nodes16, np.frombuffer(b"0123456789abcdefABCDEF", dtype=np.uint8)).all():
+            return self._device_fallback(arena, off, T, t_call)
+        uo = dst[:n + 1].astype(np.int64)
+        pkb = pk[:ub].tobytes()
+        users = [pkb[uo[k]:uo[k + 1]].decode("utf-8", "replace") for k in range(n)]
+        if len(set(users)) != n:
+            return self._device_fallback(arena, off, T, t_call)  # (an owner twice: rounds)
+        slots = np.fromiter((self._slot(u) for u in users), dtype=np.int64, count=n)
+        nmsg, cbytes = inf[:, 0], inf[:, 1]
+        msg_base = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(nmsg, out=msg_base[1:])
+        con_base = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(cbytes, out=con_base[1:])
+        N, CB = int(msg_base[n]), int(con_base[n])
+        ts = torch.zeros((max(N, 1), 48), dtype=torch.uint8, device=dev)
+        coff = torch.empty(N + 1, dtype=torch.int64, device=dev)
+        coff[N] = CB
+        content = torch.empty(max(CB, 1), dtype=torch.uint8, device=dev)
+        owner = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
+        slot_d = torch.from_numpy(slots.astype(np.int32)).to(dev)
+        mb_d, cb_d = up(msg_base), up(con_base)  # (held: the kernels read them after P() returns)
+        check(lib.evm_pb_split_dev(eng.h, REQUEST_KIND, P(arena), P(off_d), n, P(st_d), P(mb_d), P(cb_d), P(slot_d),
+                                   P(ts), 48, P(coff), P(content), P(owner)), "evm_pb_split_dev")
+        T["decode"] += time.perf_counter() - t0
+        t0 = time.perf_counter()
+        bad = np.zeros(n, dtype=bool)
+        if N:
+            _, ost, _ = self.store.ingest_ex(ts[:N], owner[:N], self.next_id)
+            bad = ost.cpu().numpy()[slots] != 0
+            self._log(self.next_id, ts[:N], coff, content)
+            self.next_id += N
+        T["ingest"] += time.perf_counter() - t0
+        # the client trees (owners without a request this round: the empty tree)
+        t0 = time.perf_counter()
+        O = self.capacity
+        at = np.zeros(O, dtype=np.uint64)
+        ln = np.zeros(O, dtype=np.uint64)
+        ok = ~bad
+        at[slots[ok]] = off[:-1][ok] + inf[ok, 6]
+        ln[slots[ok]] = inf[ok, 7]
+        tst_d = torch.empty(max(O, 1), dtype=torch.int32, device=dev)
+        h = C.c_void_p()
+        at_d, ln_d = up(at), up(ln)
+        check(lib.evm_tree_from_json_dev(eng.h, O, P(arena), P(at_d), P(ln_d), P(tst_d), C.byref(h)),
+              "evm_tree_from_json_dev")
+        from .engine import Trees
+
+        client = Trees(eng, h)
+        tbad = tst_d.cpu().numpy()[slots] != 0
+        T["trees"] += time.perf_counter() - t0
+        result: List = [None] * n
+        late = np.flatnonzero(bad | (tbad & ok))  # the per-request path's requests
+        ans = np.flatnonzero(ok & ~tbad)
+        buf, roff = None, np.zeros(n + 1, dtype=np.uint64)
+        if len(ans):
+            t0 = time.perf_counter()
+            sl = slots[ans]
+            node = np.full((O, 16), ord("0"), dtype=np.uint8)
+            node[sl] = nodes16[ans]
+            active = np.zeros(O, dtype=np.uint8)
+            active[sl] = 1
+            diff, soff, sid = self.store.select(client, eng.dev(node), eng.dev(active))
+            client.free()
+            sl_d = torch.from_numpy(sl).to(dev)
+            rng_err_d = diff[sl_d] == _lib.DIFF_RANGE_ERROR
+            cnt = torch.where(rng_err_d, torch.zeros_like(sl_d), soff[sl_d + 1] - soff[sl_d])
+            sel_off = torch.zeros(len(sl) + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(cnt, 0, out=sel_off[1:])
+            first = sel_off[:-1]
+            pick = torch.repeat_interleave(soff[sl_d] - first, cnt) + torch.arange(int(sel_off[-1]), device=dev)
+            sel = sid[pick].contiguous()
+            rng_err = rng_err_d.cpu().numpy()
+            T["select"] += time.perf_counter() - t0
+            t0 = time.perf_counter()
+            segs = [g.dev(dev) for g in self._segs]
+            VP = C.c_void_p * max(len(segs), 1)
+            seg_base = np.asarray(self._base, dtype=np.uint64)
+            seg_row = VP(*[None if r is None else r.data_ptr() for _, _, _, r in segs])
+            seg_ts = VP(*[t.data_ptr() for t, _, _, _ in segs])
+            seg_coff = VP(*[o.data_ptr() for _, o, _, _ in segs])
+            seg_con = VP(*[c.data_ptr() for _, _, c, _ in segs])
+            owners_d = sl_d.to(torch.int32)
+            rout = torch.empty(len(sl) + 1, dtype=torch.int64, device=dev)
+            tot = C.c_uint64()
+            tree = self.store.tree()
+            args = [eng.h, len(sl), tree.h, P(owners_d), P(sel_off), P(sel), len(segs), _np_ptr(seg_base), seg_row,
+                    seg_ts, 48, seg_coff, seg_con]
+            check(lib.evm_pb_encode_responses_dev(*args, None, 0, P(rout), C.byref(tot)), "evm_pb_encode_responses_dev")
+            buf = torch.empty(max(tot.value, 1), dtype=torch.uint8, device=dev)
+            check(lib.evm_pb_encode_responses_dev(*args, P(buf), tot.value, P(rout), C.byref(tot)),
+                  "evm_pb_encode_responses_dev")
+            ro = rout.cpu().numpy().view(np.uint64)
+            for k, i in enumerate(ans.tolist()):
+                roff[i], roff[i + 1] = ro[k], ro[k + 1]
+                result[i] = RangeError("Invalid count value") if rng_err[k] else True
+            T["encode"] += time.perf_counter() - t0
+        else:
+            client.free()
+        if len(late):
+            # an owner the ingest rejected: the per-request path's round (nothing of
+            # it was stored); a tree the device did not read: that request's select
+            t0 = time.perf_counter()
+            out: List[Result] = [None] * n
+            hb = {int(i): arena[int(off[i]):int(off[i + 1])].cpu().numpy().tobytes() for i in late}
+            rnd = [(int(i), wire.decode(wire.REQUEST, hb[int(i)])) for i in late if bad[i]]
+            if rnd:
+                self._round(rnd, out)
+            sel_only = [(int(i), wire.decode(wire.REQUEST, hb[int(i)]), int(slots[i])) for i in late if not bad[i]]
+            if sel_only:
+                self._select(sel_only, out)
+            for i in late:
+                result[int(i)] = out[int(i)]
+            T["per_request"] += time.perf_counter() - t0
+        T["other"] = time.perf_counter() - t_call - sum(T.values())
+        return DeviceResponses(buf, roff, result)
+
+    def _device_fallback(self, arena, off, T, t_call):
+        """sync_device's whole-call fallback: sync() on a host copy of the bodies."""
+        import time
+
+        t0 = time.perf_counter()
+        host = arena.cpu().numpy()
+        res = self._sync_fast(host, off)
+        self.timing = dict(self.timing, device_fallback=time.perf_counter() - t0)
+        return DeviceResponses(None, np.zeros(len(off), dtype=np.uint64), res)
 
     # ------------------------------------------------------------ fast path
     def _sync_fast(self, arena: np.ndarray, boff: np.ndarray, views: bool = False) -> List[Result]:
@@ -358,7 +587,7 @@ class SyncServer:
         sel = np.ascontiguousarray(sid[pick], dtype=np.uint64)
         sel_off = np.zeros(len(sl) + 1, dtype=np.uint64)
         np.cumsum(cnt, out=sel_off[1:])
-        segs = self._segs
+        segs = [g.host() for g in self._segs]
         seg_base = np.asarray(self._base, dtype=np.uint64)
         P = C.c_void_p
         seg_row = (P * len(segs))(*[None if r is None else r.ctypes.data for _, _, _, r in segs])

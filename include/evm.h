@@ -416,6 +416,51 @@ int evm_pb_encode_responses(uint32_t n, const uint64_t* sel_off, const uint64_t*
                             size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
                             const char* json, const uint64_t* json_off, uint8_t* out, uint64_t* out_off);
 
+/* ------------------------------------------------------- wire codec, device
+ * The same codecs over bodies resident in DEVICE memory (evm_wire_dev.hip):
+ * a server round's SyncRequests decoded where they lie in HBM, their client
+ * trees parsed and the SyncResponses built there (index.ts:112-116, :121-136,
+ * :233-241).  Same grammar and results as the host calls above (one device
+ * thread runs the host's walk per body / tree).  All array arguments are
+ * device pointers unless marked host.
+ *
+ * scan: per body (arena[off[k] .. off[k + 1])) its evm_pb_sync and status, as
+ * evm_pb_scan_batch.  split: as evm_pb_split_batch (ts rows, content_off of
+ * N + 1 entries, contents concatenated) plus owner[i] = owner_of[k] for body
+ * k's rows (owner_of / owner may be NULL); ts_len / ts_off are not produced
+ * (the device path takes only bodies whose timestamps are all 46 bytes).
+ * gather: n byte spans of src packed into dst (dst_off from the caller). */
+int evm_pb_scan_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n, evm_pb_sync* info,
+                    int32_t* status);
+int evm_pb_split_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n,
+                     const int32_t* status, const uint64_t* msg_base, const uint64_t* content_base,
+                     const uint32_t* owner_of, char* ts, size_t stride, uint64_t* content_off, uint8_t* content,
+                     uint32_t* owner);
+int evm_gather_spans_dev(evm_ctx* ctx, const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
+                         const uint64_t* dst_off, uint32_t n, uint8_t* dst);
+/* evm_tree_from_json for n_owners texts json[at[o] .. at[o] + len[o]) (len 0:
+ * the owner sent no tree -> the empty tree).  status[o] (device int32): 0,
+ * EVM_ETREE (the host parser rejects the text: merkleTreeFromString throws),
+ * or EVM_TREE_UNSORTED (children keys out of ascending order -- valid JSON
+ * that JSON.stringify never writes: parse it on the host).  The tree is
+ * returned whatever the statuses (an owner with a nonzero status is empty in
+ * it); the call fails only on a bad argument or an allocation. */
+#define EVM_TREE_UNSORTED 1000
+int evm_tree_from_json_dev(evm_ctx* ctx, uint32_t n_owners, const uint8_t* json, const uint64_t* at,
+                           const uint64_t* len, int32_t* status, evm_tree** out);
+/* evm_pb_encode_responses with the selection, the log and the output on the
+ * device: response r's messages are ids sel_id[sel_off[r] .. sel_off[r + 1])
+ * (sel_off: n + 1 entries), its merkleTree the JSON of owner owners[r] of
+ * `tree`, emitted straight into the response.  seg_base (host, ascending)
+ * and the host arrays of device pointers seg_row / seg_ts / seg_coff /
+ * seg_content describe the log as in evm_pb_encode_responses.  out NULL:
+ * out_off (n + 1) and *total (host) only; else cap >= *total bytes. */
+int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, const uint32_t* owners,
+                                const uint64_t* sel_off, const uint64_t* sel_id, uint32_t n_seg,
+                                const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
+                                size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
+                                uint8_t* out, size_t cap, uint64_t* out_off, uint64_t* total);
+
 /* ------------------------------------------------------------------------
  * Multi-GPU owner sharding (evm_dist.hip).  One process per
  * GPU and one evm_dist per context; every call below is collective (all
