@@ -1758,31 +1758,6 @@ __global__ __launch_bounds__(THREADS) void k_xf_scatter(const u32* __restrict__ 
     r[k] = bk[k] < B ? atomicAdd(&cnt[bk[k]], 1u) : 0u;
   }
   __syncthreads();
-#ifdef XF_DIRECT
-  {
-    // every pair straight to its bucket slot: the tile reserves a run per
-    // bucket, each pair's place in it is its LDS rank (the lines merge in L2)
-    bool full = false;
-    for (u32 b = threadIdx.x; b < B; b += THREADS) {
-      const u32 c = cnt[b];
-      u32 gg = 0;
-      if (c) {
-        gg = atomicAdd(&cursor[b], c);
-        full |= gg + c > cap;
-      }
-      gb[b] = gg;
-    }
-    if (__ballot(full) && (threadIdx.x & 63) == 0) atomic_or_if(&info->xf_redo, 1u);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k)
-      if (bk[k] < B) {
-        const u32 slot = gb[bk[k]] + r[k];
-        if (slot < cap) out[(size_t)bk[k] * cap + slot] = v[k];
-      }
-    return;
-  }
-#endif
   const u32 per = (B + THREADS - 1) / THREADS;
   u32 loc[(1u << XP_MAX_KB) / THREADS];
   u32 sum = 0;
@@ -1836,16 +1811,8 @@ __device__ __forceinline__ bool xf_insert(u32* tab, const u64* bp, u64 p, u32 k,
   const u32 h = (u32)(p >> 32);
   const u32 mine = ((h >> 15) << 15) | (k + 1);
   for (u32 probe = 0; probe < budget; ++probe) {
-#ifdef XF_RBC
-    u32 prev = __hip_atomic_load(&tab[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (prev == 0) {
-      prev = atomicCAS(&tab[pos], 0u, mine);
-      if (prev == 0) return true;  // inserted
-    }
-#else
     const u32 prev = atomicCAS(&tab[pos], 0u, mine);
     if (prev == 0) return true;  // inserted
-#endif
     if ((prev >> 15) == (h >> 15)) {
       const u64 q = bp[(prev & 0x7fffu) - 1];
       if ((q | cmask) == (p | cmask)) {  // equal fingerprints: a copy of one timestamp (or a near-impossible twin)
@@ -2144,11 +2111,8 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
   // scatter tiles of 12,288 rows (rounding the tile count up to whole rounds
   // of the chip -- 1,024 tiles of 9,766 rows for 10M -- measured slower, 85
   // vs 78-81 us: shorter bucket runs cost more than the last round's sliver)
-#ifndef XF_TL
-#define XF_TL 12288
-#endif
-  const u32 xft = (u32)((n + XF_TL - 1) / XF_TL);
-  const u32 xf_tl = XF_TL;
+  const u32 xft = (u32)((n + 12287) / 12288);
+  const u32 xf_tl = 12288;
 
   // it reads only the timestamps, cells and K1's hashes: a second stream runs
   // it beside the walks, forked right after K1 (joined before the status
@@ -2210,10 +2174,7 @@ static int apply_stream(evm_ctx* ctx, Scratch& S, Info* info, const evm_tree* tr
       // after the walk XORs its exact redeliveries out again)
       {
         evm::ProfScope ps_(ctx, "k_xf_scatter", xs);
-#ifndef XF_ST
-#define XF_ST 1024
-#endif
-        hipLaunchKernelGGL((k_xf_scatter<XF_ST, 12>), dim3(xft), dim3(XF_ST), 0, xs, hash, (const u64*)tcs,
+        hipLaunchKernelGGL((k_xf_scatter<1024, 12>), dim3(xft), dim3(1024), 0, xs, hash, (const u64*)tcs,
                            (const u64*)sb.tcs_far, cell, n, kb, cbits, cap, xcur, xpairs, info, xf_tl);
       }
       evm::ProfScope ps_(ctx, "k_xf_dedup", xs);
