@@ -1941,6 +1941,7 @@ def e2e_leg(eng, ts_np, owner_np, client, device_ms, sample=8):
     ref.close()
     srv.close()
     n = len(ts_np)
+    dev = e2e_device(eng, arena, off, out, O, pick, device_ms)
     return {"workload": "config 3 end to end: %d SyncRequest bodies (%d owners x %d msgs, %d-B contents, the "
                         "client's tree JSON) -> SyncServer.sync -> %d SyncResponse bodies, into an empty store"
                         % (R, R, n // max(R, 1), 16, R),
@@ -1949,7 +1950,59 @@ def e2e_leg(eng, ts_np, owner_np, client, device_ms, sample=8):
             "ms_by_part": {k: v * 1e3 for k, v in timing.items()},
             "request_bytes": int(off[-1]), "response_bytes": int(resp_bytes), "responses": ok,
             "host_threads": os.environ.get("EVM_HOST_THREADS", "default (<= 16)"),
-            "bodies_generation_s": gen_s, "self_check": {"sample": int(len(pick)), "same_bytes": bool(same)}}
+            "bodies_generation_s": gen_s, "self_check": {"sample": int(len(pick)), "same_bytes": bool(same)},
+            "device_resident": dev}
+
+
+def e2e_device(eng, arena, off, host_out, O, pick, device_ms):
+    """The same round with the bodies resident in HBM (SyncServer.sync_device:
+    decode, ingest, client-tree parse, selection and response encode all on
+    the device; only per-body sizes, userIds and nodeIds come to the host),
+    the responses left in HBM.  One untimed round on a fresh server first,
+    then the timed round on another; self-check: the sampled responses equal
+    the host path's bytes."""
+    import numpy as np
+    import torch
+
+    from evolu_amd.server import SyncServer
+
+    a_d = torch.from_numpy(arena).to("cuda:%d" % eng.device)
+    n = len(off) - 1
+    prof = None
+    for rep in range(3):
+        srv = SyncServer(eng, O)
+        if rep == 2:  # (an untimed profiled round: the kernels' share)
+            eng.prof_enable(True)
+            eng.prof_reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = srv.sync_device(a_d, off)
+        torch.cuda.synchronize()
+        if rep == 2:
+            prof = eng.prof_report()
+            eng.prof_enable(False)
+        else:
+            wall = time.perf_counter() - t0
+            timing = dict(srv.timing)
+        if rep < 2:
+            del res
+            srv.close()
+    ok = sum(1 for r in res.result if r is True)
+    same = True
+    for k in pick:
+        k = int(k)
+        if res.result[k] is not True:
+            same = False
+            continue
+        got = res.buf[int(res.off[k]):int(res.off[k + 1])].cpu().numpy().tobytes()
+        same = same and got == bytes(host_out[k])
+    resp_bytes = int(res.buf.numel()) if res.buf is not None else 0
+    srv.close()
+    return {"ms": wall * 1e3, "ratio_to_device_step": wall * 1e3 / device_ms if device_ms else None,
+            "ms_by_part": {k: v * 1e3 for k, v in timing.items()}, "responses": ok, "response_bytes": resp_bytes,
+            "fallback": "device_fallback" in timing,
+            "kernels_ms": {k: v[0] for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:16]},
+            "self_check": {"sample": int(len(pick)), "same_bytes_as_host_path": bool(same)}}
 
 
 def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=False, leg=False):

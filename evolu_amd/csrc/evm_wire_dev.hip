@@ -27,20 +27,73 @@ using namespace evm;
 namespace {
 
 // ------------------------------------------------------------------ protobuf
+// Sequential reads of device bytes through a 64-B register window: one
+// refill (four independent 16-B loads) per 64 bytes walked instead of one
+// dependent load per byte.  A refill loads only the 16-B chunks below
+// `lim` (the chunk boundary after the last byte of the buffer): the callers'
+// buffers are readable in whole 16-B chunks (evm.h).
+struct Win {
+  const uint8_t* w;    // window start (16-B aligned)
+  const uint8_t* lim;  // loads stay below this (16-B aligned)
+  uint4 v0, v1, v2, v3;
+  __device__ __forceinline__ void init(const uint8_t* end) {
+    lim = reinterpret_cast<const uint8_t*>(((uintptr_t)end + 15) & ~(uintptr_t)15);
+    w = nullptr;
+  }
+  __device__ __forceinline__ uint4 chunk(const uint8_t* c) const {
+    return c < lim ? *reinterpret_cast<const uint4*>(c) : make_uint4(0, 0, 0, 0);
+  }
+  __device__ __forceinline__ void refill(const uint8_t* p) {
+    w = reinterpret_cast<const uint8_t*>((uintptr_t)p & ~(uintptr_t)15);
+    v0 = chunk(w);
+    v1 = chunk(w + 16);
+    v2 = chunk(w + 32);
+    v3 = chunk(w + 48);
+  }
+  // (selects of values: a select of the members' addresses would keep the
+  // window in scratch memory)
+  static __device__ __forceinline__ u32 pick(u32 j, u32 a, u32 b, u32 c, u32 d) {
+    const u32 lo = (j & 1u) ? b : a, hi = (j & 1u) ? d : c;
+    return (j & 2u) ? hi : lo;
+  }
+  __device__ __forceinline__ u32 word(u32 i) const {  // i < 16
+    return pick(i >> 2, pick(i & 3u, v0.x, v0.y, v0.z, v0.w), pick(i & 3u, v1.x, v1.y, v1.z, v1.w),
+                pick(i & 3u, v2.x, v2.y, v2.z, v2.w), pick(i & 3u, v3.x, v3.y, v3.z, v3.w));
+  }
+  // bytes p .. p + 7, little-endian (past the buffer: whatever the chunk holds, or 0)
+  __device__ __forceinline__ u64 get8(const uint8_t* p) {
+    if (p < w || p + 8 > w + 64) refill(p);
+    const u32 k = (u32)(p - w), j = k >> 2, sh = (k & 3u) * 8u;
+    const u32 a = word(j), b = word(j + 1), c = word(min(j + 2, 15u));
+    const u32 lo = sh ? (a >> sh) | (b << (32u - sh)) : a;
+    const u32 hi = sh ? (b >> sh) | (c << (32u - sh)) : b;
+    return ((u64)hi << 32) | lo;
+  }
+  __device__ __forceinline__ uint8_t get(const uint8_t* p) {
+    if (p < w || p >= w + 64) refill(p);
+    const u32 k = (u32)(p - w);
+    const u32 j = (k >> 2) & 3u, c = k >> 4;
+    const u32 word = pick(c, pick(j, v0.x, v0.y, v0.z, v0.w), pick(j, v1.x, v1.y, v1.z, v1.w),
+                          pick(j, v2.x, v2.y, v2.z, v2.w), pick(j, v3.x, v3.y, v3.z, v3.w));
+    return (uint8_t)(word >> ((k & 3u) * 8u));
+  }
+};
+
 // evm_proto.cpp's Reader on device bytes (the same checks, in the same order)
 struct DReader {
   const uint8_t* p;
   const uint8_t* e;
   bool ok;
-  __device__ bool more() const { return ok && p < e; }
-  __device__ u64 varint() {
+  Win* win;
+  __device__ __forceinline__ bool more() const { return ok && p < e; }
+  __device__ __forceinline__ u64 varint() {
     u64 v = 0;
     for (int sh = 0; sh < 70; sh += 7) {
       if (p >= e) {
         ok = false;
         return 0;
       }
-      const uint8_t b = *p++;
+      const uint8_t b = win->get(p++);
       if (sh == 63 && b > 1) {
         ok = false;
         return 0;
@@ -51,7 +104,7 @@ struct DReader {
     ok = false;
     return 0;
   }
-  __device__ bool bytes(const uint8_t** q, u64* n) {
+  __device__ __forceinline__ bool bytes(const uint8_t** q, u64* n) {
     const u64 len = varint();
     if (!ok || len > (u64)(e - p)) return ok = false;
     *q = p;
@@ -59,7 +112,7 @@ struct DReader {
     p += len;
     return true;
   }
-  __device__ bool skip(u32 wt) {
+  __device__ __forceinline__ bool skip(u32 wt) {
     switch (wt) {
       case 0:
         varint();
@@ -90,8 +143,8 @@ struct DMsg {
   u64 content_len;
 };
 
-__device__ bool d_read_msg(const uint8_t* q, u64 n, DMsg* m) {
-  DReader r{q, q + n, true};
+__device__ __forceinline__ bool d_read_msg(const uint8_t* q, u64 n, DMsg* m, Win* win) {
+  DReader r{q, q + n, true, win};
   *m = DMsg{nullptr, 0, nullptr, 0};
   while (r.more()) {
     const u64 tag = r.varint();
@@ -110,8 +163,8 @@ __device__ bool d_read_msg(const uint8_t* q, u64 n, DMsg* m) {
 
 // evm_proto.cpp's walk(): on_msg(index, msg) per message
 template <typename F>
-__device__ int d_walk(int kind, const uint8_t* buf, u64 len, evm_pb_sync* info, F on_msg) {
-  DReader r{buf, buf + len, true};
+__device__ __forceinline__ int d_walk(int kind, const uint8_t* buf, u64 len, evm_pb_sync* info, Win* win, F on_msg) {
+  DReader r{buf, buf + len, true, win};
   evm_pb_sync s{0, 0, 0, 0, 0, 0, 0, 0, 0};
   const u32 tree_field = kind == EVM_PB_SYNC_REQUEST ? 4u : 2u;
   while (r.more()) {
@@ -131,7 +184,7 @@ __device__ int d_walk(int kind, const uint8_t* buf, u64 len, evm_pb_sync* info, 
     const u64 off = (u64)(q - buf);
     if (field == 1) {
       DMsg m;
-      if (!d_read_msg(q, n, &m)) return EVM_EINVAL;
+      if (!d_read_msg(q, n, &m, win)) return EVM_EINVAL;
       if (m.ts_len != 46) ++s.nonstd_ts;
       s.content_bytes += m.content_len;
       on_msg(s.n_messages, m);
@@ -157,7 +210,9 @@ __global__ void k_pb_scan(int kind, const uint8_t* __restrict__ arena, const u64
   for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
     const u64 a = off[k], b = off[k + 1];
     evm_pb_sync s{0, 0, 0, 0, 0, 0, 0, 0, 0};
-    int st = b < a ? EVM_EINVAL : d_walk(kind, arena + a, b - a, &s, [](u64, const DMsg&) {});
+    Win win;
+    win.init(arena + b);
+    int st = b < a ? EVM_EINVAL : d_walk(kind, arena + a, b - a, &s, &win, [](u64, const DMsg&) {});
     if (st) s = evm_pb_sync{0, 0, 0, 0, 0, 0, 0, 0, 0};
     info[k] = s;
     status[k] = st;
@@ -179,15 +234,23 @@ __global__ void k_pb_split(int kind, const uint8_t* __restrict__ arena, const u6
     const u64 m0 = msg_base[k], c0 = content_base[k];
     const u32 ow = owner_of ? owner_of[k] : 0u;
     u64 co = 0;
-    const int st = d_walk(kind, arena + a, off[k + 1] - a, nullptr, [&](u64 i, const DMsg& m) {
-      char* row = ts + (m0 + i) * stride;
-      if (m.ts_len == 46)
-        for (int j = 0; j < 46; ++j) row[j] = (char)m.ts[j];
-      else
-        for (int j = 0; j < 46; ++j) row[j] = (char)0xff;
-      for (u64 j = 46; j < stride; ++j) row[j] = 0;
+    Win win;
+    win.init(arena + off[k + 1]);
+    const int st = d_walk(kind, arena + a, off[k + 1] - a, nullptr, &win, [&](u64 i, const DMsg& m) {
+      // the row in 4-B stores (rows are 16-B aligned, stride % 4 == 0)
+      u32* row = reinterpret_cast<u32*>(ts + (m0 + i) * stride);
+      for (int j = 0; j < 12; ++j) {
+        u32 x = 0;
+        for (int b = 0; b < 4; ++b) {
+          const int at = 4 * j + b;
+          const u32 c = at >= 46 ? 0u : m.ts_len == 46 ? (u32)win.get(m.ts + at) : 0xffu;
+          x |= c << (8 * b);
+        }
+        row[j] = x;
+      }
+      for (u64 j = 48; j < stride; j += 4) row[j >> 2] = 0u;
       content_off[m0 + i] = c0 + co;
-      for (u64 j = 0; j < m.content_len; ++j) content[c0 + co + j] = m.content[j];
+      for (u64 j = 0; j < m.content_len; ++j) content[c0 + co + j] = win.get(m.content + j);
       co += m.content_len;
       if (owner) owner[m0 + i] = ow;
     });
@@ -218,54 +281,178 @@ __device__ __forceinline__ bool jws(uint8_t c) { return c == ' ' || c == '\t' ||
 struct JText {
   const uint8_t* p;
   const uint8_t* e;
-  __device__ void ws() {
-    while (p < e && jws(*p)) ++p;
+  Win win;
+  __device__ __forceinline__ uint8_t at(const uint8_t* q) { return win.get(q); }
+  __device__ __forceinline__ void ws() {
+    while (p < e && jws(at(p))) ++p;
   }
-  __device__ bool lit(uint8_t c) {
+  __device__ __forceinline__ bool lit(uint8_t c) {
     ws();
-    if (p < e && *p == c) {
+    if (p < e && at(p) == c) {
       ++p;
       return true;
     }
     return false;
   }
-  __device__ int key() {  // 0, 1, 2 for the digits, 3 for "hash", -1 otherwise
+  __device__ __forceinline__ int key() {  // 0, 1, 2 for the digits, 3 for "hash", -1 otherwise
     ws();
-    if (p >= e || *p != '"') return -1;
+    if (p >= e || at(p) != '"') return -1;
     const uint8_t* q = ++p;
-    while (p < e && *p != '"') {
-      if (*p == '\\') return -1;
+    uint8_t c;
+    while (p < e && (c = at(p)) != '"') {
+      if (c == '\\') return -1;
       ++p;
     }
     if (p >= e) return -1;
     const u64 len = (u64)(p - q);
     ++p;
-    if (len == 1 && q[0] >= '0' && q[0] <= '2') return q[0] - '0';
-    if (len == 4 && q[0] == 'h' && q[1] == 'a' && q[2] == 's' && q[3] == 'h') return 3;
+    if (len == 1) {
+      c = at(q);
+      return c >= '0' && c <= '2' ? c - '0' : -1;
+    }
+    if (len == 4 && at(q) == 'h' && at(q + 1) == 'a' && at(q + 2) == 's' && at(q + 3) == 'h') return 3;
     return -1;
   }
-  __device__ bool integer(int32_t* v) {
+  __device__ __forceinline__ bool integer(int32_t* v) {
     ws();
     bool neg = false;
-    if (p < e && *p == '-') {
+    if (p < e && at(p) == '-') {
       neg = true;
       ++p;
     }
-    if (p >= e || *p < '0' || *p > '9') return false;
-    if (*p == '0' && p + 1 < e && p[1] >= '0' && p[1] <= '9') return false;
+    if (p >= e || at(p) < '0' || at(p) > '9') return false;
+    if (at(p) == '0' && p + 1 < e && at(p + 1) >= '0' && at(p + 1) <= '9') return false;
     int64_t x = 0;
-    while (p < e && *p >= '0' && *p <= '9') {
-      x = x * 10 + (*p - '0');
+    uint8_t c;
+    while (p < e && (c = at(p)) >= '0' && c <= '9') {
+      x = x * 10 + (c - '0');
       if (x > 2147483648LL) return false;
       ++p;
     }
-    if (p < e && (*p == '.' || *p == 'e' || *p == 'E')) return false;
+    if (p < e && ((c = at(p)) == '.' || c == 'e' || c == 'E')) return false;
     if (neg) x = -x;
     if (x < (int64_t)INT32_MIN || x > (int64_t)INT32_MAX || (neg && x == 0)) return false;
     *v = (int32_t)x;
     return true;
   }
 };
+
+// The common text first: JSON.stringify's own form, read token by token --
+// `"d":{` opens a child (digits ascending), `"hash":N}` closes the node, a
+// comma follows every child -- 8 bytes of lookahead per token from the
+// register window.  Anything else (whitespace, another key order, a
+// malformed text) leaves the owner JP_SLOW for k_json_parse, which decides
+// exactly as the host parser.  Same outputs as k_json_parse.
+constexpr int32_t JP_SLOW = -1;
+constexpr u64 JP_KEY_MASK = 0xFFFFFF00FFull, JP_KEY = 0x7B3A220022ull;          // `"?":{`
+constexpr u64 JP_HASH_MASK = 0x00FFFFFFFFFFFFFFull, JP_HASH = 0x003A226873616822ull;  // `"hash":`
+__global__ __launch_bounds__(JP_THREADS) void k_json_canon(const uint8_t* __restrict__ json, const u64* __restrict__ jat,
+                                                           const u64* __restrict__ jlen, u32 n_owners,
+                                                           const u64* __restrict__ base, u64* __restrict__ t_off,
+                                                           u64* __restrict__ t_end, u64* __restrict__ ck,
+                                                           int32_t* __restrict__ xr, int32_t* __restrict__ pfx,
+                                                           int32_t* __restrict__ status, u64* __restrict__ n_leaves) {
+  __shared__ int32_t s_cx[JP_LEVELS][JP_THREADS];
+  __shared__ u32 s_first[JP_LEVELS][JP_THREADS];
+  __shared__ uint8_t s_fl[JP_LEVELS][JP_THREADS];  // any child (bit 0) | last child's digit + 1 (bits 1-2)
+  const u32 o = blockIdx.x * JP_THREADS + threadIdx.x;
+  if (o >= n_owners) return;
+  const u32 me = threadIdx.x;
+  const u64 b0 = base[o];
+  const u64 bound = base[o + 1] - b0 - 1;
+  t_off[o] = b0;
+  u64 cnt = 0;
+  int32_t run = 0;
+  int st = 0;
+  const u64 L = jlen[o];
+  if (L) {
+    const uint8_t* p = json + jat[o];
+    const uint8_t* e = p + L;
+    Win win;
+    win.init(e);
+    if (!(L == 2 && win.get(p) == '{' && win.get(p + 1) == '}')) {  // ({} : the empty tree)
+      st = JP_SLOW;
+      if (win.get(p) == '{') {
+        ++p;
+        int d = 0;
+        u64 prefix = 0;
+        s_cx[0][me] = 0;
+        s_fl[0][me] = 0;
+        s_first[0][me] = 0;
+        for (;;) {
+          if (e - p < 8) break;
+          const u64 x = win.get8(p);
+          if ((x & JP_KEY_MASK) == JP_KEY) {
+            const u32 k = (u32)((x >> 8) & 0xffu) - '0';
+            const uint8_t fl = s_fl[d][me];
+            if (k > 2 || d >= CODE_DIGITS || k + 1 <= (u32)(fl >> 1)) break;
+            s_fl[d][me] = (uint8_t)(((k + 1) << 1) | (fl & 1u));
+            prefix |= (u64)(k + 1) << (2 * (CODE_DIGITS - 1 - d));
+            ++d;
+            s_cx[d][me] = 0;
+            s_fl[d][me] = 0;
+            s_first[d][me] = (u32)cnt;
+            p += 5;
+            continue;
+          }
+          if ((x & JP_HASH_MASK) != JP_HASH) break;
+          p += 7;
+          // -?(0|[1-9][0-9]*) within int32, then `}`
+          bool neg = false;
+          if (p < e && win.get(p) == '-') {
+            neg = true;
+            ++p;
+          }
+          int64_t v = 0;
+          int nd = 0;
+          uint8_t c = 0;
+          while (p < e && (c = win.get(p)) >= '0' && c <= '9' && nd < 11) {
+            v = v * 10 + (c - '0');
+            ++nd;
+            ++p;
+          }
+          if (nd == 0 || nd > 10 || (nd > 1 && win.get(p - nd) == '0') || (neg && v == 0) || p >= e || c != '}') break;
+          if (neg) v = -v;
+          if (v < (int64_t)INT32_MIN || v > (int64_t)INT32_MAX) break;
+          ++p;
+          const int32_t h = (int32_t)v;
+          const int32_t cx = s_cx[d][me];
+          const bool any = s_fl[d][me] & 1u;
+          if (d == 0) {  // the root: children, their XOR as its hash, the end of the text
+            if (any && (h ^ cx) == 0 && p == e) st = 0;
+            break;
+          }
+          const int32_t t = h ^ cx;
+          if (!any || t != 0) {
+            if (cnt >= bound) break;
+            const u64 at = s_first[d][me];  // (in front of its subtree's leaves: see k_json_parse)
+            for (u64 i = cnt; i > at; --i) {
+              ck[b0 + i] = ck[b0 + i - 1];
+              xr[b0 + i] = xr[b0 + i - 1];
+              pfx[b0 + i] = pfx[b0 + i - 1] ^ t;
+            }
+            ck[b0 + at] = ((u64)o << 40) | prefix;
+            xr[b0 + at] = t;
+            if (at == cnt) pfx[b0 + at] = run;
+            run ^= t;
+            ++cnt;
+          }
+          --d;
+          s_cx[d][me] ^= h;
+          s_fl[d][me] |= 1u;
+          prefix &= ~((4ull << (2 * (CODE_DIGITS - 1 - d))) - 1ull);
+          if (p >= e || win.get(p) != ',') break;  // (a child is followed by its parent's next member)
+          ++p;
+        }
+      }
+    }
+  }
+  if (st) cnt = 0;
+  pfx[b0 + cnt] = st ? 0 : run;
+  t_end[o] = b0 + cnt;
+  status[o] = st;
+  if (cnt) atomicAdd(n_leaves, cnt);
+}
 
 // owner o's text at json + jat[o], jlen[o] bytes (jlen 0: no request, the
 // empty tree); its leaves from slot base[o] (room for the bound), the
@@ -282,7 +469,7 @@ __global__ __launch_bounds__(JP_THREADS) void k_json_parse(const uint8_t* __rest
   __shared__ uint8_t s_fl[JP_LEVELS][JP_THREADS];  // seen keys (bits 0-3) | any child (bit 4)
   __shared__ u32 s_first[JP_LEVELS][JP_THREADS];    // leaves emitted when the node opened
   const u32 o = blockIdx.x * JP_THREADS + threadIdx.x;
-  if (o >= n_owners) return;
+  if (o >= n_owners || status[o] != JP_SLOW) return;  // (k_json_canon read it)
   const u32 me = threadIdx.x;
   const u64 b0 = base[o];
   const u64 bound = base[o + 1] - b0 - 1;  // leaf slots (one more holds the root's prefix)
@@ -292,7 +479,10 @@ __global__ __launch_bounds__(JP_THREADS) void k_json_parse(const uint8_t* __rest
   int st = 0;
   const u64 L = jlen[o];
   if (L) {
-    JText tx{json + jat[o], json + jat[o] + L};
+    JText tx;
+    tx.p = json + jat[o];
+    tx.e = tx.p + L;
+    tx.win.init(tx.e);
     // the frame of the node being read at depth d: prefix = the code so far
     u64 prefix = 0;
     int d = 0;
@@ -550,7 +740,7 @@ int evm_pb_split_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_
                      const uint32_t* owner_of, char* ts, size_t stride, uint64_t* content_off, uint8_t* content,
                      uint32_t* owner) {
   if (!ctx || (n && (!arena || !off || !status || !msg_base || !content_base || !ts || !content_off || !content)) ||
-      stride < 46 || (kind != EVM_PB_SYNC_REQUEST && kind != EVM_PB_SYNC_RESPONSE))
+      stride < 48 || stride % 16 || (kind != EVM_PB_SYNC_REQUEST && kind != EVM_PB_SYNC_RESPONSE))
     return EVM_EINVAL;
   if (!n) return EVM_OK;
   Scratch S(ctx);
@@ -593,6 +783,10 @@ int evm_tree_from_json_dev(evm_ctx* ctx, uint32_t n_owners, const uint8_t* json,
   evm_tree* t = nullptr;
   if ((st = tree_alloc_gapped(ctx, n_owners, std::max<u64>(cap, 1), &t))) return st;
   HIPR(hipMemsetAsync(t->off + n_owners, 0, sizeof(u64), ctx->stream));
+  if (n_owners)
+    KLAUNCH(k_json_canon, dim3((n_owners + JP_THREADS - 1) / JP_THREADS), dim3(JP_THREADS), json, (const u64*)at,
+            (const u64*)len, n_owners, (const u64*)slots, (u64*)t->off, (u64*)t->end, (u64*)t->ck, t->xr, t->pfx,
+            status, nl);
   if (n_owners)
     KLAUNCH(k_json_parse, dim3((n_owners + JP_THREADS - 1) / JP_THREADS), dim3(JP_THREADS), json, (const u64*)at,
             (const u64*)len, n_owners, (const u64*)slots, (u64*)t->off, (u64*)t->end, (u64*)t->ck, t->xr, t->pfx,

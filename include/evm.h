@@ -422,12 +422,15 @@ int evm_pb_encode_responses(uint32_t n, const uint64_t* sel_off, const uint64_t*
  * trees parsed and the SyncResponses built there (index.ts:112-116, :121-136,
  * :233-241).  Same grammar and results as the host calls above (one device
  * thread runs the host's walk per body / tree).  All array arguments are
- * device pointers unless marked host.
+ * device pointers unless marked host.  The kernels read the bodies / texts
+ * in whole 16-B chunks: the chunks holding the arena's bytes must be
+ * readable (any device allocation is; torch's are 512-B granular).
  *
  * scan: per body (arena[off[k] .. off[k + 1])) its evm_pb_sync and status, as
  * evm_pb_scan_batch.  split: as evm_pb_split_batch (ts rows, content_off of
  * N + 1 entries, contents concatenated) plus owner[i] = owner_of[k] for body
- * k's rows (owner_of / owner may be NULL); ts_len / ts_off are not produced
+ * k's rows (owner_of / owner may be NULL); rows of stride % 16 == 0, >= 48
+ * (16-B aligned ts); ts_len / ts_off are not produced
  * (the device path takes only bodies whose timestamps are all 46 bytes).
  * gather: n byte spans of src packed into dst (dst_off from the caller). */
 int evm_pb_scan_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n, evm_pb_sync* info,
