@@ -237,20 +237,18 @@ __global__ void k_pb_split(int kind, const uint8_t* __restrict__ arena, const u6
     Win win;
     win.init(arena + off[k + 1]);
     const int st = d_walk(kind, arena + a, off[k + 1] - a, nullptr, &win, [&](u64 i, const DMsg& m) {
-      // the row in 4-B stores (rows are 16-B aligned, stride % 4 == 0)
-      u32* row = reinterpret_cast<u32*>(ts + (m0 + i) * stride);
-      for (int j = 0; j < 12; ++j) {
-        u32 x = 0;
-        for (int b = 0; b < 4; ++b) {
-          const int at = 4 * j + b;
-          const u32 c = at >= 46 ? 0u : m.ts_len == 46 ? (u32)win.get(m.ts + at) : 0xffu;
-          x |= c << (8 * b);
-        }
-        row[j] = x;
-      }
-      for (u64 j = 48; j < stride; j += 4) row[j >> 2] = 0u;
+      // the row in 8-B stores (rows are 16-B aligned: stride % 16 == 0)
+      u64* row = reinterpret_cast<u64*>(ts + (m0 + i) * stride);
+      const bool std46 = m.ts_len == 46;
+      for (int j = 0; j < 5; ++j) row[j] = std46 ? win.get8(m.ts + 8 * j) : ~0ull;
+      row[5] = (std46 ? win.get8(m.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
+      for (u64 j = 48; j < stride; j += 8) row[j >> 3] = 0ull;
       content_off[m0 + i] = c0 + co;
-      for (u64 j = 0; j < m.content_len; ++j) content[c0 + co + j] = win.get(m.content + j);
+      for (u64 j = 0; j < m.content_len; j += 8) {
+        const u64 x = win.get8(m.content + j);
+        const u64 nb = min((u64)8, m.content_len - j);
+        for (u64 b = 0; b < nb; ++b) content[c0 + co + j + b] = (uint8_t)(x >> (8 * b));
+      }
       co += m.content_len;
       if (owner) owner[m0 + i] = ow;
     });
@@ -397,24 +395,27 @@ __global__ __launch_bounds__(JP_THREADS) void k_json_canon(const uint8_t* __rest
           }
           if ((x & JP_HASH_MASK) != JP_HASH) break;
           p += 7;
-          // -?(0|[1-9][0-9]*) within int32, then `}`
-          bool neg = false;
-          if (p < e && win.get(p) == '-') {
-            neg = true;
-            ++p;
-          }
+          // -?(0|[1-9][0-9]*) within int32, then `}` (and `,` after a child): at most
+          // 13 bytes, all in the next 16
+          const u64 y1 = win.get8(p), y2 = win.get8(p + 8);
+          auto byte_at = [&](u32 k) -> u32 { return (u32)((k < 8 ? y1 >> (8 * k) : y2 >> (8 * (k - 8))) & 0xffu); };
+          u32 k = 0;
+          const bool neg = byte_at(0) == '-';
+          if (neg) k = 1;
           int64_t v = 0;
-          int nd = 0;
-          uint8_t c = 0;
-          while (p < e && (c = win.get(p)) >= '0' && c <= '9' && nd < 11) {
+          u32 nd = 0, c = 0;
+          while (k < 12 && (c = byte_at(k)) >= '0' && c <= '9') {
             v = v * 10 + (c - '0');
             ++nd;
-            ++p;
+            ++k;
           }
-          if (nd == 0 || nd > 10 || (nd > 1 && win.get(p - nd) == '0') || (neg && v == 0) || p >= e || c != '}') break;
+          if (nd == 0 || nd > 10 || (nd > 1 && byte_at(k - nd) == '0') || (neg && v == 0) || c != '}' ||
+              p + k >= e)
+            break;
           if (neg) v = -v;
           if (v < (int64_t)INT32_MIN || v > (int64_t)INT32_MAX) break;
-          ++p;
+          const bool comma = p + k + 1 < e && byte_at(k + 1) == ',';
+          p += k + 1;
           const int32_t h = (int32_t)v;
           const int32_t cx = s_cx[d][me];
           const bool any = s_fl[d][me] & 1u;
@@ -441,7 +442,7 @@ __global__ __launch_bounds__(JP_THREADS) void k_json_canon(const uint8_t* __rest
           s_cx[d][me] ^= h;
           s_fl[d][me] |= 1u;
           prefix &= ~((4ull << (2 * (CODE_DIGITS - 1 - d))) - 1ull);
-          if (p >= e || win.get(p) != ',') break;  // (a child is followed by its parent's next member)
+          if (!comma) break;  // (a child is followed by its parent's next member)
           ++p;
         }
       }

@@ -114,6 +114,20 @@ class _Seg:
         return self.d
 
 
+def _decode_spans(pk: np.ndarray, off: np.ndarray, ln: np.ndarray) -> List[str]:
+    """The byte spans pk[off[k] .. off[k + 1]) as str (UTF-8, errors replaced),
+    as the host path decodes userIds; equal-length spans without NUL bytes in
+    one numpy call."""
+    n = len(off) - 1
+    if n and (ln == ln[0]).all() and int(ln[0]) > 0 and (pk < 0x80).all():  # (ASCII: bytes = chars)
+        L = int(ln[0])
+        big = pk.tobytes().decode("ascii")
+        return [big[i:i + L] for i in range(0, n * L, L)]
+    b = pk.tobytes()
+    o = off.astype(np.int64)
+    return [b[o[k]:o[k + 1]].decode("utf-8", "replace") for k in range(n)]
+
+
 class DeviceResponses:
     """sync_device's answer: result[i] is True where response i is the bytes
     buf[off[i] .. off[i + 1]) of the device buffer `buf`, else what sync()
@@ -282,12 +296,19 @@ class SyncServer:
         nodes16 = pk[ub:ub + 16 * n].reshape(n, 16)
         if not np.isin(nodes16, np.frombuffer(b"0123456789abcdefABCDEF", dtype=np.uint8)).all():
             return self._device_fallback(arena, off, T, t_call)
-        uo = dst[:n + 1].astype(np.int64)
-        pkb = pk[:ub].tobytes()
-        users = [pkb[uo[k]:uo[k + 1]].decode("utf-8", "replace") for k in range(n)]
-        if len(set(users)) != n:
+        t1 = time.perf_counter()
+        users = _decode_spans(pk[:ub], dst[:n + 1], ulen)
+        get = self.slot.get
+        new = [u for u in users if get(u) is None]  # (new users take slots in request order)
+        if new:
+            new = list(dict.fromkeys(new))
+            if len(self.slot) + len(new) > self.capacity:
+                raise _lib.EngineError(_lib.EVM_ECAPACITY, "SyncServer: more users than owner slots")
+            self.slot.update(zip(new, range(len(self.slot), len(self.slot) + len(new))))
+        slots = np.fromiter(map(get, users), dtype=np.int64, count=n)
+        if np.unique(slots).size != n:
             return self._device_fallback(arena, off, T, t_call)  # (an owner twice: rounds)
-        slots = np.fromiter((self._slot(u) for u in users), dtype=np.int64, count=n)
+        T["users"] = time.perf_counter() - t1
         nmsg, cbytes = inf[:, 0], inf[:, 1]
         msg_base = np.zeros(n + 1, dtype=np.uint64)
         np.cumsum(nmsg, out=msg_base[1:])
@@ -393,7 +414,7 @@ class SyncServer:
             for i in late:
                 result[int(i)] = out[int(i)]
             T["per_request"] += time.perf_counter() - t0
-        T["other"] = time.perf_counter() - t_call - sum(T.values())
+        T["other"] = time.perf_counter() - t_call - sum(v for k, v in T.items() if k != "users")  # (users: part of decode)
         return DeviceResponses(buf, roff, result)
 
     def _device_fallback(self, arena, off, T, t_call):
