@@ -1860,10 +1860,31 @@ def reingest(eng, a, ts1, own1, owners, per_owner, request, flags):
     m = sorted(ms)[len(ms) // 2]
     dom = dominant(prof, SERVER_ALG)
     tot_ms, launches = prof[dom]
+    # the store growing round after round: rounds 2, 3, 4 of
+    # new timestamps into one store holding 1, 2, 3 rounds
+    rounds = [(ts2, own2)]
+    for k in (2, 3):
+        t_np, o_np, _ = synth.config3(owners, per_owner, seed_config=3 + 7919 * k, request=request)
+        rounds.append((eng.dev(t_np), eng.dev(o_np)))
+        del t_np, o_np
+    st = eng.store_new(owners)
+    st.ingest(ts1, own1, 0, flags=flags)
+    round_ms = []
+    for k, (tsk, owk) in enumerate(rounds):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st.ingest(tsk, owk, (k + 1) << 40, flags=f2)
+        torch.cuda.synchronize()
+        round_ms.append((time.perf_counter() - t0) * 1e3)
+    stored_rounds = int(st.n_messages)
+    st.free()
+    del rounds
     return {"workload": "a second round of %d msgs (%d owners, new timestamps) into a store holding %d rows: "
                         "addMessages with the stored rows and trees merged" % (n, owners, ts1.shape[0]),
             "value": n / m * 1e3, "unit": "msgs/s", "ms_per_ingest_median": m, "ms_per_ingest": [round(x, 3) for x in ms],
             "stored_after": int(n_stored), "dominant_kernel": dom, "dominant_kernel_ms": tot_ms / launches,
+            "rounds_2_3_4_ms": [round(x, 3) for x in round_ms],
+            "rounds_vs_round_2": [round(x / round_ms[0], 3) for x in round_ms], "stored_after_round_4": stored_rounds,
             "kernels_ms": {k: v[0] for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:10]}}
 
 

@@ -587,6 +587,54 @@ int evm::tree_alloc_cap(evm_ctx* ctx, u32 n_owners, uint64_t cap, evm_tree** out
   return EVM_OK;
 }
 
+struct LandArgs {
+  const u32* src[LAND_MAX];
+  int n;
+};
+__global__ void k_land_words(LandArgs a, volatile u32* host) {
+  const int k = threadIdx.x;
+  if (k < a.n) host[k] = *a.src[k];
+  __threadfence_system();
+}
+int evm::land_words(evm_ctx* ctx, const LandList& l) {
+  if (l.n == 0) return EVM_OK;
+  if (!ctx->hland) {  // (no pinned buffer: the runtime's copies)
+    for (int k = 0; k < l.n; ++k) HIPR(hipMemcpyAsync(l.dst[k], l.src[k], 4, hipMemcpyDeviceToHost, ctx->stream));
+    return hip_ok(hipStreamSynchronize(ctx->stream));
+  }
+  LandArgs a;
+  for (int k = 0; k < l.n; ++k) a.src[k] = l.src[k];
+  a.n = l.n;
+  KLAUNCH(k_land_words, dim3(1), dim3(64), a, (volatile u32*)ctx->hland);
+  HIPR(hipStreamSynchronize(ctx->stream));
+  for (int k = 0; k < l.n; ++k) *static_cast<u32*>(l.dst[k]) = ctx->hland[k];
+  return EVM_OK;
+}
+
+struct ZeroArgs {
+  u32* p[ZERO_MAX];
+  u32 words[ZERO_MAX];
+  u32 fill[ZERO_MAX];
+  int n;
+};
+__global__ void k_zero_small(ZeroArgs a) {
+  const int b = blockIdx.x;
+  if (b >= a.n) return;
+  for (u32 k = threadIdx.x; k < a.words[b]; k += blockDim.x) a.p[b][k] = a.fill[b];
+}
+int evm::zero_small(evm_ctx* ctx, const ZeroList& z) {
+  if (z.n == 0) return EVM_OK;
+  ZeroArgs a;
+  for (int k = 0; k < z.n; ++k) {
+    a.p[k] = z.p[k];
+    a.words[k] = z.words[k];
+    a.fill[k] = z.fill[k];
+  }
+  a.n = z.n;
+  KLAUNCH(k_zero_small, dim3(z.n), dim3(256), a);
+  return hip_ok(hipGetLastError());
+}
+
 int evm::tree_alloc_gapped(evm_ctx* ctx, u32 n_owners, uint64_t cap, evm_tree** out) {
   evm_tree* t = new evm_tree;
   t->n_owners = n_owners;
@@ -1017,6 +1065,8 @@ int evm_create(int device, evm_ctx** out) {
   // pinned landing buffer for the per-call status record (a pageable D2H
   // copy would stage through a bounce buffer on every call)
   if (hipHostMalloc((void**)&c->hinfo, sizeof(Info), hipHostMallocDefault) != hipSuccess) c->hinfo = nullptr;
+  if (hipHostMalloc((void**)&c->hland, sizeof(uint32_t) * LAND_MAX, hipHostMallocDefault) != hipSuccess)
+    c->hland = nullptr;
   // keep freed scratch in the stream-ordered pool between calls
   hipMemPool_t pool;
   if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
@@ -1041,6 +1091,7 @@ void evm_destroy(evm_ctx* ctx) {
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->own);
   if (ctx->hinfo) (void)hipHostFree(ctx->hinfo);
+  if (ctx->hland) (void)hipHostFree(ctx->hland);
   delete ctx;
 }
 

@@ -24,6 +24,7 @@ struct evm_ctx {
   // kernel timing (evm_prof_*): HIP event pairs per kernel name, on `stream`
   bool prof = false;
   evm::Info* hinfo = nullptr;  // pinned host copy of a call's status record (read_info)
+  uint32_t* hland = nullptr;   // pinned landing words (evm::land_words)
   std::string prof_only;  // evm_prof_only: time just this kernel ("" = all)
   int client_path = 0;  // EVM_OPT_CLIENT_PATH
   int server_path = 0;  // EVM_OPT_SERVER_PATH
@@ -268,12 +269,44 @@ inline int ceil_log2(size_t x) {
   return k;
 }
 
+// Small device values to the host in ONE launch and one synchronisation: a
+// kernel stores the 4-B words into pinned host memory (no copy-engine blit
+// per value, no pageable staging); up to LAND_MAX words per call.
+constexpr int LAND_MAX = 32;
+struct LandList {
+  const uint32_t* src[LAND_MAX];
+  void* dst[LAND_MAX];
+  int n = 0;
+  // `bytes` (a multiple of 4) at dev -> host
+  void add(const void* dev, void* host, size_t bytes) {
+    for (size_t k = 0; k < bytes / 4 && n < LAND_MAX; ++k, ++n) {
+      src[n] = static_cast<const uint32_t*>(dev) + k;
+      dst[n] = static_cast<uint32_t*>(host) + k;
+    }
+  }
+};
+int land_words(evm_ctx* ctx, const LandList& l);
+// Zero up to ZERO_MAX small device buffers (a multiple of 4 bytes each) in one launch.
+constexpr int ZERO_MAX = 8;
+struct ZeroList {
+  uint32_t* p[ZERO_MAX];
+  uint32_t words[ZERO_MAX];
+  uint32_t fill[ZERO_MAX];
+  int n = 0;
+  void add(void* dev, size_t bytes, uint32_t value = 0) {
+    p[n] = static_cast<uint32_t*>(dev);
+    words[n] = (uint32_t)(bytes / 4);
+    fill[n] = value;
+    ++n;
+  }
+};
+int zero_small(evm_ctx* ctx, const ZeroList& z);
+
 inline int read_info(evm_ctx* ctx, const Info* dev, Info* host) {
-  Info* land = ctx->hinfo ? ctx->hinfo : host;  // pinned when the context has it
-  HIPR(hipMemcpyAsync(land, dev, sizeof(Info), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
-  if (land != host) *host = *land;
-  return EVM_OK;
+  static_assert(sizeof(Info) % 4 == 0 && sizeof(Info) / 4 <= LAND_MAX, "Info lands as words");
+  LandList l;
+  l.add(dev, host, sizeof(Info));
+  return land_words(ctx, l);
 }
 
 // the initial record is written by a one-thread kernel (launch argument), not

@@ -2461,8 +2461,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   KLAUNCH(k_run_count, rgrid, dim3(RUN_THREADS), owner, n, tcnt);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, tcnt, n_rt, toff, nrun))) return st;
   u32 R = 0;
-  HIPR(hipMemcpyAsync(&R, nrun, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
+  {
+    LandList l;
+    l.add(nrun, &R, sizeof(u32));
+    if ((st = land_words(ctx, l))) return st;
+  }
   u32* ov = perm;
   const bool runs = (size_t)R * 8 <= n;
   const evm_tree* t = s->tree;
@@ -2544,11 +2547,14 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
       if ((st = scan_exclusive_cols(ctx, S, 3, ins, O, outs, tots))) return st;
     }
     u32 plan[4] = {0, 0, 0, 0};  // segments, samples, splitters, an owner of several runs
-    HIPR(hipMemcpyAsync(&plan[0], bbase + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipMemcpyAsync(&plan[1], soff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipMemcpyAsync(&plan[2], spoff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipMemcpyAsync(&plan[3], multi, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipStreamSynchronize(ctx->stream));
+    {
+      LandList l;
+      l.add(bbase + O, &plan[0], sizeof(u32));
+      l.add(soff + O, &plan[1], sizeof(u32));
+      l.add(spoff + O, &plan[2], sizeof(u32));
+      l.add(multi, &plan[3], sizeof(u32));
+      if ((st = land_words(ctx, l))) return st;
+    }
     if (plan[1] > 0 && (st = minutes())) return st;  // cut owners: the splitters need the minutes
     if ((st = check_info())) return st;
     split = plan[1] > 0 && cuttable();
@@ -2585,8 +2591,12 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
       smin = S.alloc<u32>(nq);
       u32* mm = S.alloc<u32>(2);
       if (!smin || !mm) return EVM_ENOMEM;
-      HIPR(hipMemsetAsync(mm, 0xff, sizeof(u32), ctx->stream));
-      HIPR(hipMemsetAsync(mm + 1, 0, sizeof(u32), ctx->stream));
+      {
+        ZeroList z;
+        z.add(mm, sizeof(u32), 0xffffffffu);
+        z.add(mm + 1, sizeof(u32));
+        if ((st = zero_small(ctx, z))) return st;
+      }
       KLAUNCH(k_seg_smin, dim3(grid_for(nq, 256)), dim3(256), msrc, owner, n, O, smin, mm, info);
       u32 hmm[2];
       HIPR(hipMemcpyAsync(hmm, mm, sizeof(hmm), hipMemcpyDeviceToHost, ctx->stream));
@@ -2620,9 +2630,12 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
       if ((st = scan_exclusive_cols(ctx, S, 2, ins, O, outs, tots))) return st;
     }
     u32 plan[2] = {0, 0};
-    HIPR(hipMemcpyAsync(&plan[0], bbase + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipMemcpyAsync(&plan[1], spoff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipStreamSynchronize(ctx->stream));
+    {
+      LandList l;
+      l.add(bbase + O, &plan[0], sizeof(u32));
+      l.add(spoff + O, &plan[1], sizeof(u32));
+      if ((st = land_words(ctx, l))) return st;
+    }
     split = true;  // (possibly one segment per owner)
     NS = plan[0];
     nspl = plan[1];
@@ -2646,8 +2659,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     KLAUNCH(k_seg_tlen, dim3(grid_for(O, 256)), dim3(256), spoff, sp, O, tlen);
     if ((st = scan_exclusive<u32, OpAdd>(ctx, S, tlen, O, tboff, tboff + O))) return st;
     u32 ntab = 0;
-    HIPR(hipMemcpyAsync(&ntab, tboff + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipStreamSynchronize(ctx->stream));
+    {
+      LandList l;
+      l.add(tboff + O, &ntab, sizeof(u32));
+      if ((st = land_words(ctx, l))) return st;
+    }
     u32* tab = S.alloc<u32>(std::max<u32>(ntab, 1));
     if (!tab) return EVM_ENOMEM;
     if (ntab) KLAUNCH(k_seg_table, dim3(grid_for(ntab, 256)), dim3(256), spoff, sp, tboff, O, ntab, tab);
@@ -2723,8 +2739,12 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   u32 ht[2], hmid = 0;
   const int preset = orig ? 0 : 1;
   if (preset) HIPR(hipMemsetAsync(flags, EVM_MSG_INS, n, ctx->stream));
-  HIPR(hipMemsetAsync(status, 0, sizeof(SvoStatus), ctx->stream));
-  HIPR(hipMemsetAsync(mid, 0, sizeof(u32), ctx->stream));
+  {
+    ZeroList z;
+    z.add(status, sizeof(SvoStatus));
+    z.add(mid, sizeof(u32));
+    if ((st = zero_small(ctx, z))) return st;
+  }
   HIPR(hipMemsetAsync(ownbig, 0, O, ctx->stream));
   // the common share size over every segment (more workgroups per CU); larger
   // shares are listed and take the SVO_CAP kernel over just those segments
@@ -2775,13 +2795,19 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     // segments (the one-wave kernel for <= 128 messages)
     u32* lists = S.alloc<u32>(SEG_CLASSES * ((size_t)NS + 1));
     if (!lists) return EVM_ENOMEM;
-    for (int c = 0; c < SEG_CLASSES; ++c)
-      HIPR(hipMemsetAsync(lists + (size_t)c * (NS + 1), 0, sizeof(u32), ctx->stream));
+    {
+      static_assert(SEG_CLASSES <= ZERO_MAX, "one launch");
+      ZeroList z;
+      for (int c = 0; c < SEG_CLASSES; ++c) z.add(lists + (size_t)c * (NS + 1), sizeof(u32));
+      if ((st = zero_small(ctx, z))) return st;
+    }
     KLAUNCH(k_seg_classes, dim3(grid_for(NS, 256)), dim3(256), sv, NS, lists);
     u32 hc[SEG_CLASSES];
-    for (int c = 0; c < SEG_CLASSES; ++c)
-      HIPR(hipMemcpyAsync(&hc[c], lists + (size_t)c * (NS + 1), sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipStreamSynchronize(ctx->stream));
+    {
+      LandList l;
+      for (int c = 0; c < SEG_CLASSES; ++c) l.add(lists + (size_t)c * (NS + 1), &hc[c], sizeof(u32));
+      if ((st = land_words(ctx, l))) return st;
+    }
     const u32 caps[SEG_CLASSES] = {128, 256, 512, 1024, 2048, SVO_CAP};
     for (int c = 0; c < SEG_CLASSES; ++c)
       if (hc[c])
@@ -2808,12 +2834,17 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
     if (!xpos) return EVM_ENOMEM;
     if ((st = scan_exclusive<int32_t, OpXor>(ctx, S, (const int32_t*)c_xor, NS, xpos, xpos + NS))) return st;
   }
-  HIPR(hipMemcpyAsync(&hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipMemcpyAsync(ht, tot, sizeof(ht), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
+  {
+    // K5's status, the totals and (fused) the parse's verdict in one landing
+    static_assert(sizeof(SvoStatus) % 4 == 0, "words");
+    LandList l;
+    l.add(status, &hs, sizeof(hs));
+    l.add(tot, ht, sizeof(ht));
+    if (fused) l.add(info, &hi, sizeof(Info));
+    if ((st = land_words(ctx, l))) return st;
+  }
   if (fused) {
     // the parse's verdict: a row outside the native domain -> pack to flag the culprits
-    if ((st = read_info(ctx, info, &hi))) return st;
     if (hi.bad_aux) return EVM_EINVAL;  // (the fused plan checks every owner in k_seg_key)
     if (hi.bad) {
       if ((st = unfuse())) return st;
@@ -3319,9 +3350,12 @@ static int select_after(evm_ctx* ctx, Scratch& S, const evm_store* s, const int6
           cand, req, tot + 1);
   if ((st = scan_exclusive<u32, OpAdd>(ctx, S, cand, O, cpos, cpos + O))) return st;
   u32 h[2];
-  HIPR(hipMemcpyAsync(&h[0], cpos + O, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipMemcpyAsync(&h[1], tot + 1, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
+  {
+    LandList l;
+    l.add(cpos + O, &h[0], sizeof(u32));
+    l.add(tot + 1, &h[1], sizeof(u32));
+    if ((st = land_words(ctx, l))) return st;
+  }
   if (h[1]) return EVM_EINVAL;  // a requester nodeId is not 16 hex chars
   const u32 C = h[0];
   const int grid = grid_for(C, SEL_THREADS, 16384);
@@ -3335,17 +3369,24 @@ static int select_after(evm_ctx* ctx, Scratch& S, const evm_store* s, const int6
     u64* status = S.alloc<u64>(ntiles);
     u32* ctr = S.alloc<u32>(2);  // tile counter, look-back error
     if (!kst || !status || !ctr) return EVM_ENOMEM;
-    HIPR(hipMemsetAsync(status, 0, sizeof(u64) * ntiles, ctx->stream));
-    HIPR(hipMemsetAsync(ctr, 0, 2 * sizeof(u32), ctx->stream));
+    {
+      ZeroList z;
+      z.add(status, sizeof(u64) * ntiles);
+      z.add(ctr, 2 * sizeof(u32));
+      if ((st = zero_small(ctx, z))) return st;
+    }
     KLAUNCH(k_sv_sel_scan, dim3(ntiles), dim3(SEL_THREADS), v, O, C, (const u32*)cpos, (const u64*)first,
             (const u64*)req, (const u64*)s->id, sel_id ? (u64)cap : 0ull, (u64*)sel_id, (u64*)sel_key, kst, status,
             ctr, tot, ctr + 1);
     KLAUNCH(k_sv_sel_off, dim3(grid_for(O + 1, 256)), dim3(256), O, C, (const u32*)cpos, (const u32*)kst,
             (const u32*)tot, (u64*)sel_off);
     u32 h2[2];
-    HIPR(hipMemcpyAsync(&K, tot, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipMemcpyAsync(h2, ctr, 2 * sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipStreamSynchronize(ctx->stream));
+    {
+      LandList l;
+      l.add(tot, &K, sizeof(u32));
+      l.add(ctr, h2, 2 * sizeof(u32));
+      if ((st = land_words(ctx, l))) return st;
+    }
     if (h2[1]) return EVM_EDEVICE;  // a look-back wait gave up
     *n_sel = K;
     if (K > cap || (K && !sel_id)) return EVM_ECAPACITY;

@@ -109,7 +109,7 @@ class _Seg:
             import torch
 
             ts, coff, content, rowmap = self.h
-            up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+            up = lambda a: torch.from_numpy(a if a.flags.c_contiguous and a.flags.writeable else a.copy()).to(device)  # noqa: E731
             self.d = (up(ts), up(coff.view(np.int64)), up(content), None if rowmap is None else up(rowmap.view(np.int64)))
         return self.d
 
