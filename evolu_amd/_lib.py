@@ -113,8 +113,8 @@ SIGNATURES = {
     "evm_pb_split_dev": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "evm_gather_spans_dev": (_i, [_vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     "evm_tree_from_json_dev": (_i, [_vp, _u32, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),
-    "evm_pb_encode_responses_dev": (_i, [_vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _sz,
-                                         _vp, C.POINTER(C.c_uint64)]),
+    "evm_pb_encode_responses_dev": (_i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp, _vp,
+                                         _sz, _vp, C.POINTER(C.c_uint64)]),
     "evm_store_since": (_i, [_vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_server_select": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_store_select_after": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),

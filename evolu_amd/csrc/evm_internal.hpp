@@ -371,9 +371,17 @@ int tree_alloc_gapped(evm_ctx* ctx, u32 n_owners, uint64_t cap, evm_tree** out);
 // compact one).  Every reader but the diff and the roots calls it first.
 int tree_compact(evm_ctx* ctx, const evm_tree* t);
 // evm_json_dev.hip: per requested owner its tree JSON's length (device len[n];
-// *bad |= 1 for an owner out of range), and the texts written at out + off[j]
-int json_lengths(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, uint64_t* len, uint32_t* bad);
-int json_emit(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, const uint64_t* off, char* out);
+// *bad |= 1 for an owner out of range) and the plan the emit follows (arrays
+// in S); the texts written at out + off[j]
+struct JsonPlan {
+  uint64_t* cbase = nullptr;
+  uint64_t* cpos = nullptr;
+  uint64_t nchunks = 0;
+};
+int json_plan(evm_ctx* ctx, Scratch& S, const evm_tree* t, const uint32_t* owners, uint32_t n, uint64_t* len,
+              uint32_t* bad, JsonPlan* plan);
+int json_emit(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, const JsonPlan& plan,
+              const uint64_t* off, char* out);
 int fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u64* ck, u32* h, size_t m,
                    const Info& host_info, evm_tree** out);
 

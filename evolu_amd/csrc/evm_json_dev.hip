@@ -6,22 +6,26 @@
 // like keys ascending, then "hash" (evm_json.cpp's host emitter, pinned by
 // node).  Over an owner's leaves in code order (= depth-first order) the
 // text is a concatenation of one piece per leaf i:
-//   opens   the nodes on leaf i's path below its common prefix c_i with leaf
+//   opens   the nodes on leaf i's path below its common prefix cp_i with leaf
 //           i-1: `"d":{` each, a comma before the first one when leaf i-1
-//           went deeper than c_i (the new node has an elder sibling);
-//   closes  the nodes on leaf i's path below its common prefix with leaf i+1
-//           (all of them after the last leaf), deepest first: `"hash":H}`,
-//           with a comma in front unless the node is leaf i's own node (a
-//           node closed later than its own leaf has children);
+//           went deeper than cp_i (the new node has an elder sibling);
+//   closes  the nodes on leaf i's path below its common prefix cn_i with leaf
+//           i+1 (all of them after the last leaf), deepest first:
+//           `"hash":H}`, with a comma in front unless the node is leaf i's
+//           own node (a node closed later than its own leaf has children);
 // wrapped in the root's `{` ... `,"hash":R}` (an empty tree: `{}`).  A node's
-// hash H is the XOR of its leaves: the owner's prefix XOR at leaf i + 1 (the
-// node's last leaf is i) ^ at its first leaf (a lower bound of its code
-// prefix among leaves 0..i).
+// hash H is the XOR of its leaves: the owner's prefix XOR after leaf i (the
+// node's last leaf) ^ before the node's first leaf, which is the last leaf j
+// <= i that opened a node at that depth (cp_j < d).
 //
-// Two passes, each a workgroup per owner over chunks of 256 leaves (one per
-// thread): k_json_len sums the pieces' lengths; after a scan of the owners'
-// lengths k_json_emit writes each chunk's pieces into LDS and copies them
-// out coalesced (a chunk too long for the stage writes its bytes directly).
+// Work unit: a chunk of 64 leaves, one wave, one leaf per lane.  The node
+// starts come from 20 ballots (lane j: cp_j < d) -- the last opener at or
+// below a lane -- and, for nodes opened before the chunk, from one search per
+// depth for the chunk's first leaf (20 lanes, once per chunk) instead of a
+// search per closed node.  k_jp_len sums each chunk's text; after a scan of
+// the chunk lengths (every chunk's place) k_jp_emit writes each chunk's
+// pieces into LDS and copies them out (a chunk too long for the stage writes
+// its bytes directly).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,9 +39,9 @@ using namespace evm;
 
 namespace {
 
-constexpr int JT = 256;            // threads per owner (one leaf each per chunk)
-constexpr u32 JCAP = 2048;         // an owner's leaves staged in LDS (more: read from global memory)
-constexpr u32 JSTAGE = 24 * 1024;  // bytes of a chunk's text staged in LDS
+constexpr int JW = 64;                 // leaves per chunk: one wave
+constexpr int JW_WAVES = 4;            // waves (chunks) per workgroup
+constexpr u32 JW_STAGE = 8 * 1024;     // bytes of a chunk's text staged in LDS
 constexpr u64 CODE_MASK = (1ull << 40) - 1;
 
 struct TreeJ {  // the tree as the kernels read it (gapped or compact: owner o's leaves [off[o], end[o]))
@@ -67,38 +71,111 @@ __device__ __forceinline__ u32 dec_len(int32_t v) {
   }
   return n + (v < 0 ? 1u : 0u);
 }
+// the root's tail after the last leaf: `,"hash":R}`
+__device__ __forceinline__ u32 root_tail_len(int32_t r) { return 9u + dec_len(r); }
 
-// An owner's leaves: codes (without the owner bits) and the owner-local
-// exclusive prefix XOR, from LDS when staged there, else from the tree.
-struct Leaves {
-  const u64* g_ck;
-  const int32_t* g_pfx;
-  u64 base;
-  int32_t p0;  // pfx at the owner's first leaf (a compact tree's prefix is global)
-  const u64* s_ck;
-  const int32_t* s_pfx;
-  __device__ __forceinline__ u64 code(u32 i) const { return s_ck ? s_ck[i] : (g_ck[base + i] & CODE_MASK); }
-  __device__ __forceinline__ int32_t pfx(u32 i) const { return s_pfx ? s_pfx[i] : (g_pfx[base + i] ^ p0); }
-  __device__ __forceinline__ u32 lower(u32 hi, u64 x) const {  // first k < hi with code(k) >= x
-    u32 lo = 0;
-    while (lo < hi) {
-      const u32 mid = (lo + hi) >> 1;
-      if (code(mid) < x) lo = mid + 1;
-      else hi = mid;
-    }
-    return lo;
+// A wave's chunk: its owner and its leaves' places
+struct Chunk {
+  u32 j;      // the request (owners[j])
+  u32 L;      // the owner's leaves
+  u64 a;      // its first leaf's slot
+  u32 k;      // chunk number inside the owner
+  int32_t p0; // pfx at the owner's first leaf (a compact tree's prefix is global)
+  bool in;    // owner in range
+};
+__device__ __forceinline__ Chunk chunk_of(const TreeJ& t, const u32* owners, const u64* cbase, u32 n, u64 c) {
+  u32 lo = 0, hi = n;  // the last j with cbase[j] <= c
+  while (lo < hi) {
+    const u32 mid = (lo + hi) >> 1;
+    if (cbase[mid + 1] <= c) lo = mid + 1;
+    else hi = mid;
   }
+  Chunk ch;
+  ch.j = lo;
+  const u32 o = owners ? owners[lo] : lo;
+  ch.in = o < t.n_owners;
+  const u64 a = ch.in ? t.off[o] : 0, b = ch.in ? t.end[o] : 0;
+  ch.L = (u32)(b - a);
+  ch.a = a;
+  ch.k = (u32)(c - cbase[lo]);
+  ch.p0 = ch.L ? t.pfx[a] : 0;
+  return ch;
+}
+
+// Per wave, in LDS: the ballot of openers per depth, the prefix at the start
+// of every node open before the chunk, and each lane's prefix before its leaf.
+struct WaveLds {
+  u64 opener[CODE_DIGITS + 1];
+  int32_t carry[CODE_DIGITS + 1];
+  int32_t p[JW];
 };
 
-// Leaf i's piece: its length, and (out != null) its bytes.
+// One lane's leaf: its code and neighbours, and (after chunk_setup) what
+// its piece needs.
+struct Lane {
+  bool valid;
+  u32 l, i;
+  u64 c;
+  int D, cp, cn, prevD;
+  int32_t pn;  // prefix XOR after the leaf
+};
+
+__device__ __forceinline__ Lane chunk_setup(const TreeJ& t, const Chunk& ch, WaveLds* w) {
+  Lane ln;
+  ln.l = threadIdx.x & (JW - 1);
+  ln.i = ch.k * JW + ln.l;
+  ln.valid = ln.i < ch.L;
+  const u64 base = ch.a;
+  ln.c = ln.valid ? (t.ck[base + ln.i] & CODE_MASK) : 0ull;
+  const int32_t p = ln.valid ? (t.pfx[base + ln.i] ^ ch.p0) : 0;
+  ln.pn = ln.valid ? (t.pfx[base + ln.i + 1] ^ ch.p0) : 0;
+  u64 prevc = __shfl_up(ln.c, 1, 64);
+  u64 nextc = __shfl_down(ln.c, 1, 64);
+  if (ln.l == 0 && ln.i > 0 && ln.valid) prevc = t.ck[base + ln.i - 1] & CODE_MASK;
+  if (ln.l == JW - 1 && ln.i + 1 < ch.L) nextc = t.ck[base + ln.i + 1] & CODE_MASK;
+  ln.cp = ln.valid && ln.i > 0 ? code_lcp(prevc, ln.c) : 0;
+  ln.cn = ln.valid && ln.i + 1 < ch.L ? code_lcp(ln.c, nextc) : 0;
+  ln.D = ln.valid ? code_depth(ln.c) : 0;
+  ln.prevD = ln.valid && ln.i > 0 ? code_depth(prevc) : 0;
+  w->p[ln.l] = p;
+#pragma unroll
+  for (int d = 1; d <= CODE_DIGITS; ++d) {
+    const u64 m = __ballot(ln.valid && ln.cp < d);
+    if (ln.l == 0) w->opener[d] = m;
+  }
+  // nodes open before the chunk: their first leaf, one search per depth
+  const u64 cf = __shfl(ln.c, 0, 64);
+  if (ln.l < CODE_DIGITS && ch.k > 0) {
+    const int d = (int)ln.l + 1;
+    const u64 x = code_prefix(cf, d);
+    u32 lo = 0, hi = ch.k * JW;
+    while (lo < hi) {
+      const u32 mid = (lo + hi) >> 1;
+      if ((t.ck[base + mid] & CODE_MASK) < x) lo = mid + 1;
+      else hi = mid;
+    }
+    w->carry[d] = t.pfx[base + lo] ^ ch.p0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return ln;
+}
+
+// the prefix before the first leaf of leaf ln's node at depth d
+__device__ __forceinline__ int32_t node_start(const WaveLds* w, const Lane& ln, int d) {
+  const u64 m = w->opener[d] & (ln.l == 63 ? ~0ull : ((2ull << ln.l) - 1ull));
+  return m ? w->p[63 - __clzll(m)] : w->carry[d];
+}
+
+// Leaf ln's piece: its length, and (put) its bytes.
 template <typename Put>
-__device__ __forceinline__ u32 leaf_piece(const Leaves& lv, u32 i, u32 L, Put put) {
-  const u64 c = lv.code(i);
-  const int D = code_depth(c);
-  const int cp = i ? code_lcp(lv.code(i - 1), c) : 0;
-  const int cn = i + 1 < L ? code_lcp(c, lv.code(i + 1)) : 0;
+__device__ __forceinline__ u32 leaf_piece(const WaveLds* w, const Lane& ln, Put put) {
+  if (!ln.valid) return 0;
+  const u64 c = ln.c;
+  const int D = ln.D, cp = ln.cp, cn = ln.cn;
   u32 n = 0;
-  if (i && code_depth(lv.code(i - 1)) > cp) put(n++, ',');
+  if (ln.i && ln.prevD > cp) put(n++, ',');
   for (int k = cp + 1; k <= D; ++k) {
     const u32 dg = (u32)(c >> (2 * (CODE_DIGITS - k))) & 3u;  // digit + 1
     put(n++, '"');
@@ -107,11 +184,8 @@ __device__ __forceinline__ u32 leaf_piece(const Leaves& lv, u32 i, u32 L, Put pu
     put(n++, ':');
     put(n++, '{');
   }
-  const int32_t after = lv.pfx(i + 1);
-  u32 lo = i + 1;
   for (int d = D; d > cn; --d) {
-    lo = lv.lower(lo, code_prefix(c, d));  // (shallower nodes start no later)
-    const int32_t h = after ^ lv.pfx(lo);
+    const int32_t h = ln.pn ^ node_start(w, ln, d);
     if (d < D) put(n++, ',');
     put(n++, '"');
     put(n++, 'h');
@@ -133,126 +207,171 @@ __device__ __forceinline__ u32 leaf_piece(const Leaves& lv, u32 i, u32 L, Put pu
   return n;
 }
 
-// the root's tail after the last leaf: `,"hash":R}`
-__device__ __forceinline__ u32 root_tail_len(int32_t r) { return 9u + dec_len(r); }
+__device__ __forceinline__ u32 wave_excl_sum(u32 v, u32* total) {
+  u32 x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u32 y = __shfl_up(x, d, 64);
+    if ((int)(threadIdx.x & 63) >= d) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
 
-__device__ __forceinline__ Leaves stage_leaves(const TreeJ& t, u32 o, u32* L_out, u64* s_ck, int32_t* s_pfx) {
-  const bool in = o < t.n_owners;  // (an owner out of range: reported by k_json_len, emitted as {})
-  const u64 a = in ? t.off[o] : 0, b = in ? t.end[o] : 0;
-  const u32 L = (u32)(b - a);
-  *L_out = L;
-  Leaves lv{t.ck, t.pfx, a, L ? t.pfx[a] : 0, nullptr, nullptr};
-  if (L <= JCAP) {
-    for (u32 i = threadIdx.x; i <= L; i += JT) {
-      if (i < L) s_ck[i] = t.ck[a + i] & CODE_MASK;
-      s_pfx[i] = t.pfx[a + i] ^ lv.p0;
+// chunks per requested owner (an empty or out-of-range owner: one, its `{}`)
+__global__ void k_jp_chunks(TreeJ t, const u32* __restrict__ owners, u32 n, u64* __restrict__ nch,
+                            u32* __restrict__ bad) {
+  for (u32 j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const u32 o = owners ? owners[j] : j;
+    if (o >= t.n_owners) atomicOr(bad, 1u);
+    const u64 L = o < t.n_owners ? t.end[o] - t.off[o] : 0;
+    nch[j] = L ? (L + JW - 1) / JW : 1;
+  }
+}
+
+// the text of a chunk: `{` before the owner's first piece, its pieces, the
+// root's tail after the last (an empty tree: `{}`)
+__global__ __launch_bounds__(JW * JW_WAVES) void k_jp_len(TreeJ t, const u32* __restrict__ owners, u32 n,
+                                                          const u64* __restrict__ cbase, u64 nchunks,
+                                                          u64* __restrict__ clen) {
+  __shared__ WaveLds lds[JW_WAVES];
+  WaveLds* w = &lds[threadIdx.x / JW];
+  for (u64 c = (u64)blockIdx.x * JW_WAVES + threadIdx.x / JW; c < nchunks; c += (u64)gridDim.x * JW_WAVES) {
+    const Chunk ch = chunk_of(t, owners, cbase, n, c);
+    if (ch.L == 0) {
+      if ((threadIdx.x & 63) == 0) clen[c] = 2;
+      continue;
     }
-    __syncthreads();
-    lv.s_ck = s_ck;
-    lv.s_pfx = s_pfx;
-  }
-  return lv;
-}
-
-__global__ __launch_bounds__(JT) void k_json_len(TreeJ t, const u32* __restrict__ owners, u32 n,
-                                                 u64* __restrict__ len, u32* __restrict__ bad) {
-  __shared__ u64 s_ck[JCAP];
-  __shared__ int32_t s_pfx[JCAP + 1];
-  __shared__ u32 tmp[JT / 64 + 1];
-  for (u32 j = blockIdx.x; j < n; j += gridDim.x) {
-    const u32 o = owners ? owners[j] : j;
-    if (o >= t.n_owners && threadIdx.x == 0) atomicOr(bad, 1u);
-    u32 L;
-    const Leaves lv = stage_leaves(t, o, &L, s_ck, s_pfx);
-    u32 sum = 0;
-    for (u32 i = threadIdx.x; i < L; i += JT) sum += leaf_piece(lv, i, L, [](u32, char) {});
+    const Lane ln = chunk_setup(t, ch, w);
     u32 tot;
-    block_inclusive_scan<u32>(sum, tmp, OpAdd<u32>(), &tot);
-    if (threadIdx.x == 0) len[j] = L ? 1u + tot + root_tail_len(lv.pfx(L)) : 2u;
-    __syncthreads();  // (the staged leaves of the next owner)
+    wave_excl_sum(leaf_piece(w, ln, [](u32, char) {}), &tot);
+    if (ln.l == 0) {
+      const bool last = (u64)(ch.k + 1) * JW >= ch.L;
+      clen[c] = tot + (ch.k == 0 ? 1u : 0u) + (last ? root_tail_len(t.pfx[ch.a + ch.L] ^ ch.p0) : 0u);
+    }
+    __builtin_amdgcn_wave_barrier();  // (the wave's LDS is rewritten by its next chunk)
   }
 }
 
-__global__ __launch_bounds__(JT) void k_json_emit(TreeJ t, const u32* __restrict__ owners, u32 n,
-                                                  const u64* __restrict__ off, char* __restrict__ out) {
-  __shared__ u64 s_ck[JCAP];
-  __shared__ int32_t s_pfx[JCAP + 1];
-  __shared__ u32 tmp[JT / 64 + 1];
-  __shared__ unsigned char stage[JSTAGE];
-  for (u32 j = blockIdx.x; j < n; j += gridDim.x) {
-    const u32 o = owners ? owners[j] : j;
-    u32 L;
-    const Leaves lv = stage_leaves(t, o, &L, s_ck, s_pfx);
-    char* dst = out + off[j];
-    if (L == 0) {
-      if (threadIdx.x == 0) {
+__global__ void k_jp_owner_len(u32 n, const u64* __restrict__ cbase, const u64* __restrict__ cpos,
+                               u64* __restrict__ len) {
+  for (u32 j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+    len[j] = cpos[cbase[j + 1]] - cpos[cbase[j]];
+}
+
+__global__ __launch_bounds__(JW * JW_WAVES) void k_jp_emit(TreeJ t, const u32* __restrict__ owners, u32 n,
+                                                           const u64* __restrict__ cbase, u64 nchunks,
+                                                           const u64* __restrict__ cpos, const u64* __restrict__ off,
+                                                           char* __restrict__ out) {
+  __shared__ WaveLds lds[JW_WAVES];
+  __shared__ unsigned char stage[JW_WAVES][JW_STAGE];
+  const u32 wv = threadIdx.x / JW, lane = threadIdx.x & 63;
+  WaveLds* w = &lds[wv];
+  unsigned char* sg = stage[wv];
+  for (u64 c = (u64)blockIdx.x * JW_WAVES + wv; c < nchunks; c += (u64)gridDim.x * JW_WAVES) {
+    const Chunk ch = chunk_of(t, owners, cbase, n, c);
+    char* dst = out + off[ch.j] + (cpos[c] - cpos[cbase[ch.j]]);
+    if (ch.L == 0) {
+      if (lane == 0) {
         dst[0] = '{';
         dst[1] = '}';
       }
-      __syncthreads();
       continue;
     }
-    if (threadIdx.x == 0) dst[0] = '{';
-    u64 at = 1;  // bytes of the owner's text written so far
-    for (u32 i0 = 0; i0 < L; i0 += JT) {
-      const u32 i = i0 + threadIdx.x;
-      const u32 my = i < L ? leaf_piece(lv, i, L, [](u32, char) {}) : 0u;
-      u32 tot;
-      const u32 pos = block_inclusive_scan<u32>(my, tmp, OpAdd<u32>(), &tot) - my;
-      if (tot <= JSTAGE) {
-        if (i < L) leaf_piece(lv, i, L, [&](u32 k, char ch) { stage[pos + k] = (unsigned char)ch; });
-        __syncthreads();
-        // copy out: 4-B stores from the first 4-B aligned byte, single bytes at the ends
-        char* d = dst + at;
-        const u32 head = std::min<u32>(tot, (u32)((4u - ((uintptr_t)d & 3u)) & 3u));
-        if (threadIdx.x < head) d[threadIdx.x] = (char)stage[threadIdx.x];
-        const u32 words = (tot - head) >> 2;
-        u32* dw = reinterpret_cast<u32*>(d + head);
-        for (u32 w = threadIdx.x; w < words; w += JT) {
-          const u32 b = head + 4u * w;
-          dw[w] = (u32)stage[b] | ((u32)stage[b + 1] << 8) | ((u32)stage[b + 2] << 16) | ((u32)stage[b + 3] << 24);
-        }
-        const u32 tail = head + 4u * words;
-        if (threadIdx.x < tot - tail) d[tail + threadIdx.x] = (char)stage[tail + threadIdx.x];
-        __syncthreads();  // (the stage is reused by the next chunk)
-      } else if (i < L) {  // (a chunk of very deep, sparse leaves: its bytes straight out)
-        char* d = dst + at + pos;
-        leaf_piece(lv, i, L, [&](u32 k, char ch) { d[k] = ch; });
-      }
-      at += tot;
-    }
-    if (threadIdx.x == 0) {  // the root: `,"hash":R}`
-      const int32_t r = lv.pfx(L);
-      char* d = dst + at;
+    const Lane ln = chunk_setup(t, ch, w);
+    const u32 my = leaf_piece(w, ln, [](u32, char) {});
+    u32 tot;
+    const u32 head = ch.k == 0 ? 1u : 0u;
+    const u32 pos = head + wave_excl_sum(my, &tot);
+    const bool last = (u64)(ch.k + 1) * JW >= ch.L;
+    const int32_t R = last ? (t.pfx[ch.a + ch.L] ^ ch.p0) : 0;
+    const u32 total = head + tot + (last ? root_tail_len(R) : 0u);
+    auto tail = [&](auto put) {  // `,"hash":R}` at head + tot
       const char* h = ",\"hash\":";
-      for (int k = 0; k < 8; ++k) d[k] = h[k];
-      const u32 len = dec_len(r);
-      u32 x = r < 0 ? 0u - (u32)r : (u32)r;
-      for (u32 k = len; k-- > (r < 0 ? 1u : 0u);) {
-        d[8 + k] = (char)('0' + x % 10u);
+      u32 q = head + tot;
+      for (int k = 0; k < 8; ++k) put(q + k, h[k]);
+      const u32 len = dec_len(R);
+      u32 x = R < 0 ? 0u - (u32)R : (u32)R;
+      for (u32 k = len; k-- > (R < 0 ? 1u : 0u);) {
+        put(q + 8 + k, (char)('0' + x % 10u));
         x /= 10u;
       }
-      if (r < 0) d[8] = '-';
-      d[8 + len] = '}';
+      if (R < 0) put(q + 8, '-');
+      put(q + 8 + len, '}');
+    };
+    if (total <= JW_STAGE) {
+      leaf_piece(w, ln, [&](u32 k, char b) { sg[pos + k] = (unsigned char)b; });
+      if (lane == 0) {
+        if (head) sg[0] = '{';
+        if (last) tail([&](u32 k, char b) { sg[k] = (unsigned char)b; });
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // copy out: 4-B stores from the first 4-B aligned byte, single bytes at the ends
+      const u32 h0 = std::min<u32>(total, (u32)((4u - ((uintptr_t)dst & 3u)) & 3u));
+      if (lane < h0) dst[lane] = (char)sg[lane];
+      const u32 words = (total - h0) >> 2;
+      u32* dw = reinterpret_cast<u32*>(dst + h0);
+      for (u32 q = lane; q < words; q += JW) {
+        const u32 b = h0 + 4u * q;
+        dw[q] = (u32)sg[b] | ((u32)sg[b + 1] << 8) | ((u32)sg[b + 2] << 16) | ((u32)sg[b + 3] << 24);
+      }
+      const u32 t0 = h0 + 4u * words;
+      if (lane < total - t0) dst[t0 + lane] = (char)sg[t0 + lane];
+    } else {  // (a chunk of very deep, sparse leaves: its bytes straight out)
+      leaf_piece(w, ln, [&](u32 k, char b) { dst[pos + k] = b; });
+      if (lane == 0) {
+        if (head) dst[0] = '{';
+        if (last) tail([&](u32 k, char b) { dst[k] = b; });
+      }
     }
-    __syncthreads();  // (the staged leaves of the next owner)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // (the stage and the wave's LDS are rewritten by its next chunk)
   }
 }
 
 }  // namespace
 
-// the two passes for a caller that places the texts itself (the device
-// SyncResponse encoder: each text straight into its response)
-int evm::json_lengths(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, uint64_t* len, uint32_t* bad) {
+// The plan (chunks, their places, each owner's text length) and the emit, for
+// a caller that places the texts itself (the device SyncResponse encoder:
+// each text straight into its response).  The plan's arrays live in S.
+int evm::json_plan(evm_ctx* ctx, Scratch& S, const evm_tree* t, const uint32_t* owners, uint32_t n, uint64_t* len,
+                   uint32_t* bad, JsonPlan* plan) {
   const TreeJ tv{t->off, t->end, t->ck, t->pfx, t->n_owners};
-  const u32 grid = (u32)std::min<size_t>(std::max<u32>(n, 1), (size_t)ctx->n_cu * 8);
-  if (n) KLAUNCH(k_json_len, dim3(grid), dim3(JT), tv, owners, n, (u64*)len, bad);
+  u64* nch = S.alloc<u64>((size_t)n + 1);
+  u64* cbase = S.alloc<u64>((size_t)n + 1);
+  if (!nch || !cbase) return EVM_ENOMEM;
+  if (n) KLAUNCH(k_jp_chunks, dim3(grid_for(n, 256)), dim3(256), tv, owners, n, nch, bad);
+  int st = scan_exclusive<u64, OpAdd>(ctx, S, nch, n, cbase, cbase + n);
+  if (st) return st;
+  u64 nchunks = 0;
+  {
+    LandList l;
+    l.add(cbase + n, &nchunks, sizeof(u64));
+    if ((st = land_words(ctx, l))) return st;
+  }
+  u64* clen = S.alloc<u64>(nchunks + 1);
+  u64* cpos = S.alloc<u64>(nchunks + 1);
+  if (!clen || !cpos) return EVM_ENOMEM;
+  const u32 grid = (u32)std::min<u64>((nchunks + JW_WAVES - 1) / JW_WAVES, (u64)ctx->n_cu * 16);
+  if (nchunks)
+    KLAUNCH(k_jp_len, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (const u64*)cbase, nchunks,
+            clen);
+  if ((st = scan_exclusive<u64, OpAdd>(ctx, S, clen, nchunks, cpos, cpos + nchunks))) return st;
+  if (n) KLAUNCH(k_jp_owner_len, dim3(grid_for(n, 256)), dim3(256), n, (const u64*)cbase, (const u64*)cpos, (u64*)len);
+  plan->cbase = reinterpret_cast<uint64_t*>(cbase);
+  plan->cpos = reinterpret_cast<uint64_t*>(cpos);
+  plan->nchunks = nchunks;
   return hip_ok(hipGetLastError());
 }
-int evm::json_emit(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, const uint64_t* off, char* out) {
+int evm::json_emit(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, const JsonPlan& plan,
+                   const uint64_t* off, char* out) {
   const TreeJ tv{t->off, t->end, t->ck, t->pfx, t->n_owners};
-  const u32 grid = (u32)std::min<size_t>(std::max<u32>(n, 1), (size_t)ctx->n_cu * 8);
-  if (n) KLAUNCH(k_json_emit, dim3(grid), dim3(JT), tv, owners, n, (const u64*)off, out);
+  const u32 grid = (u32)std::min<u64>((plan.nchunks + JW_WAVES - 1) / JW_WAVES, (u64)ctx->n_cu * 16);
+  if (plan.nchunks)
+    KLAUNCH(k_jp_emit, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (const u64*)plan.cbase,
+            (u64)plan.nchunks, (const u64*)plan.cpos, (const u64*)off, out);
   return hip_ok(hipGetLastError());
 }
 
@@ -265,21 +384,22 @@ extern "C" int evm_tree_to_json_batch(evm_ctx* ctx, const evm_tree* t, const uin
   u32* bad = S.alloc<u32>(1);
   if (!len || !bad) return EVM_ENOMEM;
   HIPR(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
-  const TreeJ tv{t->off, t->end, t->ck, t->pfx, t->n_owners};
-  const u32 grid = (u32)std::min<size_t>(std::max<u32>(n, 1), (size_t)ctx->n_cu * 8);
-  if (n) KLAUNCH(k_json_len, dim3(grid), dim3(JT), tv, owners, n, len, bad);
-  u64* doff = reinterpret_cast<u64*>(off);
-  int st = scan_exclusive<u64, OpAdd>(ctx, S, len, n, doff, doff + n);
+  JsonPlan plan;
+  int st = json_plan(ctx, S, t, owners, n, reinterpret_cast<uint64_t*>(len), bad, &plan);
   if (st) return st;
+  u64* doff = reinterpret_cast<u64*>(off);
+  if ((st = scan_exclusive<u64, OpAdd>(ctx, S, len, n, doff, doff + n))) return st;
   u64 h = 0;
   u32 hb = 0;
-  HIPR(hipMemcpyAsync(&h, doff + n, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipMemcpyAsync(&hb, bad, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
+  {
+    LandList l;
+    l.add(doff + n, &h, sizeof(u64));
+    l.add(bad, &hb, sizeof(u32));
+    if ((st = land_words(ctx, l))) return st;
+  }
   if (hb) return EVM_EINVAL;
   *total = h;
   if (!out) return EVM_OK;
   if (h > cap) return EVM_ECAPACITY;
-  if (n) KLAUNCH(k_json_emit, dim3(grid), dim3(JT), tv, owners, n, (const u64*)doff, out);
-  return hip_ok(hipGetLastError());
+  return json_emit(ctx, t, owners, n, plan, off, out);
 }

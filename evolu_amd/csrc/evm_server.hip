@@ -2470,6 +2470,17 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
   const bool runs = (size_t)R * 8 <= n;
   const evm_tree* t = s->tree;
   Info hi;
+  auto check_landed = [&]() -> int {  // (hi already read)
+    int e;
+    if (hi.bad_aux) return EVM_EINVAL;
+    if (hi.bad) {
+      if ((e = unfuse())) return e;  // the culprits are flagged from packed records
+      KLAUNCH(k_sv_bad, dim3(grid_for(n, 256)), dim3(256), rec, n, flags, orig);
+      (void)evm_sync(ctx);
+      return EVM_ENONCANON;
+    }
+    return EVM_OK;
+  };
   auto check_info = [&]() -> int {
     int e = read_info(ctx, info, &hi);
     if (e) return e;
@@ -2553,10 +2564,11 @@ int ingest_by_owner(evm_ctx* ctx, Scratch& S, const evm_store* s, const evm_rec*
       l.add(soff + O, &plan[1], sizeof(u32));
       l.add(spoff + O, &plan[2], sizeof(u32));
       l.add(multi, &plan[3], sizeof(u32));
+      l.add(info, &hi, sizeof(Info));  // (the status record too: no cut owner, no minutes pass)
       if ((st = land_words(ctx, l))) return st;
     }
     if (plan[1] > 0 && (st = minutes())) return st;  // cut owners: the splitters need the minutes
-    if ((st = check_info())) return st;
+    if ((st = plan[1] > 0 ? check_info() : check_landed())) return st;
     split = plan[1] > 0 && cuttable();
     // the batch indices in owner order: read by the cut owners' sampling and
     // by K5 for owners of several runs; when every owner is one run (one

@@ -652,6 +652,32 @@ __device__ __forceinline__ bool locate(const DSeg* segs, u32 n_seg, u64 id, u64 
   return true;
 }
 
+// response r's selection: owner owners[r]'s ids (a getMessages selection by
+// owner), none when skip[r] -- counts, then the ids back to back
+__global__ void k_resp_count(u32 n, const u32* __restrict__ owners, const u64* __restrict__ osel_off,
+                             const uint8_t* __restrict__ skip, u32 n_owners, u64* __restrict__ cnt,
+                             u32* __restrict__ bad) {
+  for (u32 r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+    const u32 o = owners[r];
+    if (o >= n_owners) {
+      atomicOr(bad, 1u);
+      cnt[r] = 0;
+      continue;
+    }
+    cnt[r] = skip && skip[r] ? 0ull : osel_off[o + 1] - osel_off[o];
+  }
+}
+__global__ void k_resp_expand(u32 n, const u32* __restrict__ owners, const u64* __restrict__ osel_off,
+                              const u64* __restrict__ osel_id, const u64* __restrict__ roff, u64* __restrict__ sel) {
+  const u32 lane = threadIdx.x & 63;
+  for (u32 r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n; r += (gridDim.x * blockDim.x) >> 6) {
+    const u64 a = roff[r], m = roff[r + 1] - a;
+    if (!m) continue;
+    const u64 b = osel_off[owners[r]];
+    for (u64 j = lane; j < m; j += 64) sel[a + j] = osel_id[b + j];
+  }
+}
+
 // bytes of selected message m: `messages` field (1) around {timestamp (1), content (2)}
 __global__ void k_resp_msg_size(const u64* __restrict__ sel_id, u64 S, const DSeg* __restrict__ segs, u32 n_seg,
                                 u64 stride, u64* __restrict__ msz, u32* __restrict__ bad) {
@@ -805,22 +831,42 @@ int evm_tree_from_json_dev(evm_ctx* ctx, uint32_t n_owners, const uint8_t* json,
 }
 
 int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, const uint32_t* owners,
-                                const uint64_t* sel_off, const uint64_t* sel_id, uint32_t n_seg,
+                                const uint64_t* osel_off, const uint64_t* osel_id, const uint8_t* skip, uint32_t n_seg,
                                 const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
                                 size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
                                 uint8_t* out, size_t cap, uint64_t* out_off, uint64_t* total) {
-  if (!ctx || !tree || !total || (n && (!owners || !sel_off || !out_off)) || stride < 46 ||
+  if (!ctx || !tree || !total || (n && (!owners || !osel_off || !out_off)) || stride < 46 ||
       (n_seg && (!seg_base || !seg_ts || !seg_coff || !seg_content)))
     return EVM_EINVAL;
   *total = 0;
   Scratch S(ctx);
-  u64 hs[2] = {0, 0};  // selected ids: sel_off[n] (device)
-  if (n) {
-    HIPR(hipMemcpyAsync(&hs[0], sel_off + n, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
-    HIPR(hipStreamSynchronize(ctx->stream));
+  int st;
+  // the responses' selections back to back: sel_off (n + 1), sel_id
+  u64* rcnt = S.alloc<u64>((size_t)n + 1);
+  u64* sel_off = S.alloc<u64>((size_t)n + 1);
+  u32* bad0 = S.alloc<u32>(1);
+  if (!rcnt || !sel_off || !bad0) return EVM_ENOMEM;
+  HIPR(hipMemsetAsync(bad0, 0, sizeof(u32), ctx->stream));
+  if (n)
+    KLAUNCH(k_resp_count, dim3(grid_for(n, 256)), dim3(256), n, owners, (const u64*)osel_off, skip, tree->n_owners,
+            rcnt, bad0);
+  if ((st = scan_exclusive<u64, OpAdd>(ctx, S, rcnt, n, sel_off, sel_off + n))) return st;
+  u64 hs[2] = {0, 0};
+  u32 hb0 = 0;
+  {
+    LandList l;
+    l.add(sel_off + n, &hs[0], sizeof(u64));
+    l.add(bad0, &hb0, sizeof(u32));
+    if ((st = land_words(ctx, l))) return st;
   }
+  if (hb0) return EVM_EINVAL;
   const u64 NS = hs[0];
-  if (NS && !sel_id) return EVM_EINVAL;
+  if (NS && !osel_id) return EVM_EINVAL;
+  u64* sel_id = S.alloc<u64>(NS + 1);
+  if (!sel_id) return EVM_ENOMEM;
+  if (NS)
+    KLAUNCH(k_resp_expand, dim3(grid_for((size_t)n * 64, 256)), dim3(256), n, owners, (const u64*)osel_off,
+            (const u64*)osel_id, (const u64*)sel_off, sel_id);
   std::vector<DSeg> hseg(n_seg);
   for (u32 s = 0; s < n_seg; ++s) {
     hseg[s] = DSeg{seg_base[s], seg_row ? (const u64*)seg_row[s] : nullptr, seg_ts[s], (const u64*)seg_coff[s],
@@ -837,8 +883,9 @@ int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, 
   if (!dseg || !jlen || !msz || !mpos || !rlen || !jdst || !bad) return EVM_ENOMEM;
   if (n_seg) HIPR(hipMemcpyAsync(dseg, hseg.data(), sizeof(DSeg) * n_seg, hipMemcpyHostToDevice, ctx->stream));
   HIPR(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
-  int st = tree_compact(ctx, tree);
-  if (!st) st = json_lengths(ctx, tree, owners, n, reinterpret_cast<uint64_t*>(jlen), bad);
+  st = tree_compact(ctx, tree);
+  JsonPlan jplan;
+  if (!st) st = json_plan(ctx, S, tree, owners, n, reinterpret_cast<uint64_t*>(jlen), bad, &jplan);
   if (st) return st;
   if (NS)
     KLAUNCH(k_resp_msg_size, dim3(grid_for(NS, 256)), dim3(256), (const u64*)sel_id, NS, (const DSeg*)dseg, n_seg,
@@ -850,9 +897,12 @@ int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, 
   u64* doff = reinterpret_cast<u64*>(out_off);
   if ((st = scan_exclusive<u64, OpAdd>(ctx, S, rlen, n, doff, doff + n))) return st;
   u32 hb = 0;
-  HIPR(hipMemcpyAsync(&hs[1], doff + n, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipMemcpyAsync(&hb, bad, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
+  {
+    LandList l;
+    l.add(doff + n, &hs[1], sizeof(u64));
+    l.add(bad, &hb, sizeof(u32));
+    if ((st = land_words(ctx, l))) return st;
+  }
   if (hb) return EVM_EINVAL;  // (an owner out of range, or an id in no segment)
   *total = hs[1];
   if (!out) return EVM_OK;
@@ -860,7 +910,7 @@ int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, 
   if (n)
     KLAUNCH(k_resp_tree_hdr, dim3(grid_for(n, 256)), dim3(256), n, (const u64*)sel_off, (const u64*)mpos,
             (const u64*)jlen, (const u64*)doff, out, jdst);
-  if ((st = json_emit(ctx, tree, owners, n, reinterpret_cast<const uint64_t*>(jdst), reinterpret_cast<char*>(out))))
+  if ((st = json_emit(ctx, tree, owners, n, jplan, reinterpret_cast<const uint64_t*>(jdst), reinterpret_cast<char*>(out))))
     return st;
   if (NS)
     KLAUNCH(k_resp_msgs, dim3(grid_for(NS, 256)), dim3(256), n, (const u64*)sel_off, (const u64*)sel_id, NS,

@@ -365,14 +365,7 @@ class SyncServer:
             diff, soff, sid = self.store.select(client, eng.dev(node), eng.dev(active))
             client.free()
             sl_d = torch.from_numpy(sl).to(dev)
-            rng_err_d = diff[sl_d] == _lib.DIFF_RANGE_ERROR
-            cnt = torch.where(rng_err_d, torch.zeros_like(sl_d), soff[sl_d + 1] - soff[sl_d])
-            sel_off = torch.zeros(len(sl) + 1, dtype=torch.int64, device=dev)
-            torch.cumsum(cnt, 0, out=sel_off[1:])
-            first = sel_off[:-1]
-            pick = torch.repeat_interleave(soff[sl_d] - first, cnt) + torch.arange(int(sel_off[-1]), device=dev)
-            sel = sid[pick].contiguous()
-            rng_err = rng_err_d.cpu().numpy()
+            rng_err_d = (diff[sl_d] == _lib.DIFF_RANGE_ERROR).to(torch.uint8)
             T["select"] += time.perf_counter() - t0
             t0 = time.perf_counter()
             segs = [g.dev(dev) for g in self._segs]
@@ -386,16 +379,23 @@ class SyncServer:
             rout = torch.empty(len(sl) + 1, dtype=torch.int64, device=dev)
             tot = C.c_uint64()
             tree = self.store.tree()
-            args = [eng.h, len(sl), tree.h, P(owners_d), P(sel_off), P(sel), len(segs), _np_ptr(seg_base), seg_row,
-                    seg_ts, 48, seg_coff, seg_con]
+            args = [eng.h, len(sl), tree.h, P(owners_d), P(soff), P(sid), P(rng_err_d), len(segs), _np_ptr(seg_base),
+                    seg_row, seg_ts, 48, seg_coff, seg_con]
             check(lib.evm_pb_encode_responses_dev(*args, None, 0, P(rout), C.byref(tot)), "evm_pb_encode_responses_dev")
             buf = torch.empty(max(tot.value, 1), dtype=torch.uint8, device=dev)
             check(lib.evm_pb_encode_responses_dev(*args, P(buf), tot.value, P(rout), C.byref(tot)),
                   "evm_pb_encode_responses_dev")
             ro = rout.cpu().numpy().view(np.uint64)
-            for k, i in enumerate(ans.tolist()):
-                roff[i], roff[i + 1] = ro[k], ro[k + 1]
-                result[i] = RangeError("Invalid count value") if rng_err[k] else True
+            rng_err = rng_err_d.cpu().numpy().astype(bool)
+            # (the responses lie in buf in request order: per-request lengths -> offsets)
+            rlen = np.zeros(n, dtype=np.uint64)
+            rlen[ans] = np.diff(ro)
+            np.cumsum(rlen, out=roff[1:])
+            res = np.empty(n, dtype=object)
+            res[ans] = True
+            for i in ans[rng_err].tolist():
+                res[i] = RangeError("Invalid count value")
+            result = res.tolist()
             T["encode"] += time.perf_counter() - t0
         else:
             client.free()

@@ -452,14 +452,16 @@ int evm_gather_spans_dev(evm_ctx* ctx, const uint8_t* src, const uint64_t* src_o
 int evm_tree_from_json_dev(evm_ctx* ctx, uint32_t n_owners, const uint8_t* json, const uint64_t* at,
                            const uint64_t* len, int32_t* status, evm_tree** out);
 /* evm_pb_encode_responses with the selection, the log and the output on the
- * device: response r's messages are ids sel_id[sel_off[r] .. sel_off[r + 1])
- * (sel_off: n + 1 entries), its merkleTree the JSON of owner owners[r] of
- * `tree`, emitted straight into the response.  seg_base (host, ascending)
+ * device: response r answers owner owners[r] -- its messages are the ids
+ * sel_id[sel_off[o] .. sel_off[o + 1]) of that owner in an
+ * evm_server_select result (sel_off: tree's n_owners + 1 entries), none when
+ * skip[r] (uint8, may be NULL; a RangeError request), its merkleTree the
+ * JSON of that owner of `tree`, emitted straight into the response.  seg_base (host, ascending)
  * and the host arrays of device pointers seg_row / seg_ts / seg_coff /
  * seg_content describe the log as in evm_pb_encode_responses.  out NULL:
  * out_off (n + 1) and *total (host) only; else cap >= *total bytes. */
 int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, const uint32_t* owners,
-                                const uint64_t* sel_off, const uint64_t* sel_id, uint32_t n_seg,
+                                const uint64_t* sel_off, const uint64_t* sel_id, const uint8_t* skip, uint32_t n_seg,
                                 const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
                                 size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
                                 uint8_t* out, size_t cap, uint64_t* out_off, uint64_t* total);
