@@ -219,42 +219,72 @@ __global__ void k_pb_scan(int kind, const uint8_t* __restrict__ arena, const u64
   }
 }
 
-// body k's messages into the engine's rows (evm_pb_split_batch's layout):
-// ts rows from msg_base[k] (46 bytes + zero padding, 0xFF for a timestamp
-// that is not 46 bytes), contents concatenated from content_base[k],
-// content_off (N + 1 global entries), the owner of each row (owner_of[k])
-__global__ void k_pb_split(int kind, const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
-                           const int32_t* __restrict__ status, const u64* __restrict__ msg_base,
-                           const u64* __restrict__ content_base, const u32* __restrict__ owner_of, char* __restrict__ ts,
-                           u64 stride, u64* __restrict__ content_off, uint8_t* __restrict__ content,
-                           u32* __restrict__ owner, u32* __restrict__ bad) {
+// The split in three parallel steps: the bodies' top-level walk only finds
+// their messages (a thread per body, the walk's loads one window refill per
+// message or so), then a thread per message parses it into its row, and
+// after a scan of the content lengths copies its content.
+__global__ void k_pb_offsets(int kind, const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
+                             const int32_t* __restrict__ status, const u64* __restrict__ msg_base,
+                             const u32* __restrict__ owner_of, u64* __restrict__ mat, u32* __restrict__ mlen,
+                             u32* __restrict__ owner, u32* __restrict__ bad) {
   for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
     if (status[k]) continue;
-    const u64 a = off[k];
-    const u64 m0 = msg_base[k], c0 = content_base[k];
+    const u64 a = off[k], m0 = msg_base[k], mn = msg_base[k + 1] - m0;
     const u32 ow = owner_of ? owner_of[k] : 0u;
-    u64 co = 0;
     Win win;
     win.init(arena + off[k + 1]);
-    const int st = d_walk(kind, arena + a, off[k + 1] - a, nullptr, &win, [&](u64 i, const DMsg& m) {
-      // the row in 8-B stores (rows are 16-B aligned: stride % 16 == 0)
-      u64* row = reinterpret_cast<u64*>(ts + (m0 + i) * stride);
-      const bool std46 = m.ts_len == 46;
-      for (int j = 0; j < 5; ++j) row[j] = std46 ? win.get8(m.ts + 8 * j) : ~0ull;
-      row[5] = (std46 ? win.get8(m.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
-      for (u64 j = 48; j < stride; j += 8) row[j >> 3] = 0ull;
-      content_off[m0 + i] = c0 + co;
-      for (u64 j = 0; j < m.content_len; j += 8) {
-        const u64 x = win.get8(m.content + j);
-        const u64 nb = min((u64)8, m.content_len - j);
-        for (u64 b = 0; b < nb; ++b) content[c0 + co + j + b] = (uint8_t)(x >> (8 * b));
+    DReader r{arena + a, arena + off[k + 1], true, &win};
+    const u32 tree_field = kind == EVM_PB_SYNC_REQUEST ? 4u : 2u;
+    u64 i = 0;
+    // (the body scanned fine: the same grammar as d_walk, inner messages not re-read)
+    while (r.more()) {
+      const u64 tag = r.varint();
+      const u32 field = (u32)(tag >> 3), wt = (u32)(tag & 7);
+      const bool is_str = field == 1 || field == tree_field || (kind == EVM_PB_SYNC_REQUEST && (field == 2 || field == 3));
+      if (!is_str) {
+        r.skip(wt);
+        continue;
       }
-      co += m.content_len;
-      if (owner) owner[m0 + i] = ow;
-    });
-    if (st) atomicOr(bad, 1u);  // (a body that scanned fine: cannot happen)
-    // the entry after a body's last message is the next body's first (or the end)
-    if (!st) content_off[msg_base[k + 1]] = c0 + co;
+      const uint8_t* q;
+      u64 len;
+      if (!r.bytes(&q, &len)) break;
+      if (field == 1) {
+        if (i < mn) {
+          mat[m0 + i] = (u64)(q - arena);
+          mlen[m0 + i] = (u32)len;
+          if (owner) owner[m0 + i] = ow;
+        }
+        ++i;
+      }
+    }
+    if (!r.ok || i != mn) atomicOr(bad, 1u);  // (cannot happen for a body that scanned fine)
+  }
+}
+
+__global__ void k_pb_rows(const uint8_t* __restrict__ arena, const u64* __restrict__ mat, const u32* __restrict__ mlen,
+                          u64 N, char* __restrict__ ts, u64 stride, u64* __restrict__ cat, u64* __restrict__ clen) {
+  for (u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x; m < N; m += (u64)gridDim.x * blockDim.x) {
+    const uint8_t* q = arena + mat[m];
+    Win win;
+    win.init(q + mlen[m]);
+    DMsg msg;
+    d_read_msg(q, mlen[m], &msg, &win);
+    u64* row = reinterpret_cast<u64*>(ts + m * stride);
+    const bool std46 = msg.ts_len == 46;
+    for (int j = 0; j < 5; ++j) row[j] = std46 ? win.get8(msg.ts + 8 * j) : ~0ull;
+    row[5] = (std46 ? win.get8(msg.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
+    for (u64 j = 48; j < stride; j += 8) row[j >> 3] = 0ull;
+    cat[m] = msg.content ? (u64)(msg.content - arena) : 0ull;
+    clen[m] = msg.content_len;
+  }
+}
+
+__global__ void k_pb_content(const uint8_t* __restrict__ arena, const u64* __restrict__ cat,
+                             const u64* __restrict__ content_off, u64 N, uint8_t* __restrict__ content) {
+  for (u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x; m < N; m += (u64)gridDim.x * blockDim.x) {
+    const u64 d = content_off[m], len = content_off[m + 1] - d;
+    const uint8_t* src = arena + cat[m];
+    for (u64 j = 0; j < len; ++j) content[d + j] = src[j];
   }
 }
 
@@ -770,16 +800,36 @@ int evm_pb_split_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_
       stride < 48 || stride % 16 || (kind != EVM_PB_SYNC_REQUEST && kind != EVM_PB_SYNC_RESPONSE))
     return EVM_EINVAL;
   if (!n) return EVM_OK;
+  (void)content_base;  // (the content offsets come from one scan over every message's length)
   Scratch S(ctx);
+  int st;
+  u64 N = 0;
+  {
+    LandList l;
+    l.add(msg_base + n, &N, sizeof(u64));
+    if ((st = land_words(ctx, l))) return st;
+  }
   u32* bad = S.alloc<u32>(1);
-  if (!bad) return EVM_ENOMEM;
+  u64* mat = S.alloc<u64>(N + 1);
+  u32* mlen = S.alloc<u32>(N + 1);
+  u64* cat = S.alloc<u64>(N + 1);
+  u64* clen = S.alloc<u64>(N + 1);
+  if (!bad || !mat || !mlen || !cat || !clen) return EVM_ENOMEM;
   HIPR(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
-  KLAUNCH(k_pb_split, dim3(grid_for(n, 64, 1 << 16)), dim3(64), kind, arena, (const u64*)off, n, status,
-          (const u64*)msg_base, (const u64*)content_base, owner_of, ts, (u64)stride, (u64*)content_off, content, owner,
-          bad);
+  KLAUNCH(k_pb_offsets, dim3(grid_for(n, 64, 1 << 16)), dim3(64), kind, arena, (const u64*)off, n, status,
+          (const u64*)msg_base, owner_of, mat, mlen, owner, bad);
+  if (N) KLAUNCH(k_pb_rows, dim3(grid_for(N, 256, 1 << 16)), dim3(256), arena, (const u64*)mat, (const u32*)mlen, N, ts,
+                 (u64)stride, cat, clen);
+  u64* co = reinterpret_cast<u64*>(content_off);
+  if ((st = scan_exclusive<u64, OpAdd>(ctx, S, clen, N, co, co + N))) return st;
+  if (N) KLAUNCH(k_pb_content, dim3(grid_for(N, 256, 1 << 16)), dim3(256), arena, (const u64*)cat, (const u64*)co, N,
+                 content);
   u32 hb = 0;
-  HIPR(hipMemcpyAsync(&hb, bad, sizeof(u32), hipMemcpyDeviceToHost, ctx->stream));
-  HIPR(hipStreamSynchronize(ctx->stream));
+  {
+    LandList l;
+    l.add(bad, &hb, sizeof(u32));
+    if ((st = land_words(ctx, l))) return st;
+  }
   return hb ? EVM_EINVAL : EVM_OK;
 }
 
