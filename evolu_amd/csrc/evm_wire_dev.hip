@@ -746,36 +746,79 @@ __global__ void k_resp_tree_hdr(u32 n, const u64* __restrict__ sel_off, const u6
   }
 }
 
-// every selected message's bytes, one thread each
-__global__ void k_resp_msgs(u32 n, const u64* __restrict__ sel_off, const u64* __restrict__ sel_id, u64 S,
-                            const DSeg* __restrict__ segs, u32 n_seg, u64 stride, const u64* __restrict__ mpos,
-                            const u64* __restrict__ out_off, uint8_t* __restrict__ out) {
-  for (u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x; m < S; m += (u64)gridDim.x * blockDim.x) {
-    u32 lo = 0, hi = n;  // the response: last r with sel_off[r] <= m
-    while (lo < hi) {
-      const u32 mid = (lo + hi) >> 1;
-      if (sel_off[mid + 1] <= m) lo = mid + 1;
-      else hi = mid;
+// every selected message's bytes: a wave per 64 messages -- each lane works
+// out one message's place, header and sources, then the wave writes the
+// messages one after another, a byte per lane (64-B coalesced stores instead
+// of ~70 scattered byte stores per lane)
+struct RespMsg {
+  uint8_t* d;
+  const char* t;
+  const uint8_t* c;
+  u32 cl, hdr, len;
+  uint8_t h[12];  // `messages` tag + body length, timestamp tag + 46
+};
+__global__ __launch_bounds__(256) void k_resp_msgs(u32 n, const u64* __restrict__ sel_off,
+                                                   const u64* __restrict__ sel_id, u64 S, const DSeg* __restrict__ segs,
+                                                   u32 n_seg, u64 stride, const u64* __restrict__ mpos,
+                                                   const u64* __restrict__ out_off, uint8_t* __restrict__ out) {
+  __shared__ RespMsg meta[4][64];
+  const u32 wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (u64 m0 = ((u64)blockIdx.x * 4 + wv) * 64; m0 < S; m0 += (u64)gridDim.x * 4 * 64) {
+    const u64 m = m0 + lane;
+    RespMsg& r = meta[wv][lane];  // (built in LDS: a local copy with its byte array would live in scratch)
+    r.len = 0;
+    if (m < S) {
+      u32 lo = 0, hi = n;  // the response: last q with sel_off[q] <= m
+      while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (sel_off[mid + 1] <= m) lo = mid + 1;
+        else hi = mid;
+      }
+      const char* t;
+      const uint8_t* c;
+      u64 cl = 0;
+      if (locate(segs, n_seg, sel_id[m], stride, &t, &c, &cl)) {  // (a miss: reported by k_resp_msg_size)
+        r.d = out + out_off[lo] + (mpos[m] - mpos[sel_off[lo]]);
+        r.t = t;
+        r.c = c;
+        r.cl = (u32)cl;
+        const u64 body = 48 + (cl ? 1 + vlen(cl) + cl : 0);
+        u32 k = 0;
+        r.h[k++] = (uint8_t)(1u << 3 | 2u);
+        k += put_varint(r.h + k, body);
+        r.h[k++] = (uint8_t)(1u << 3 | 2u);
+        r.h[k++] = 46;
+        r.hdr = k;
+        r.len = k + 46 + (cl ? 1 + vlen(cl) + (u32)cl : 0);
+      }
     }
-    const u32 r = lo;
-    const char* t;
-    const uint8_t* c;
-    u64 cl = 0;
-    if (!locate(segs, n_seg, sel_id[m], stride, &t, &c, &cl)) continue;  // (reported by k_resp_msg_size)
-    uint8_t* d = out + out_off[r] + (mpos[m] - mpos[sel_off[r]]);
-    const u64 body = 48 + (cl ? 1 + vlen(cl) + cl : 0);
-    u32 k = 0;
-    d[k++] = (uint8_t)(1u << 3 | 2u);
-    k += put_varint(d + k, body);
-    d[k++] = (uint8_t)(1u << 3 | 2u);
-    d[k++] = 46;
-    for (int j = 0; j < 46; ++j) d[k + j] = (uint8_t)t[j];
-    k += 46;
-    if (cl) {
-      d[k++] = (uint8_t)(2u << 3 | 2u);
-      k += put_varint(d + k, cl);
-      for (u64 j = 0; j < cl; ++j) d[k + j] = c[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int j = 0; j < 64; ++j) {
+      const RespMsg& q = meta[wv][j];
+      const u32 len = q.len;
+      if (!len) continue;  // (wave-uniform)
+      const u32 ts_end = q.hdr + 46;
+      for (u32 k = lane; k < len; k += 64) {
+        uint8_t b;
+        if (k < q.hdr) b = q.h[k];
+        else if (k < ts_end) b = (uint8_t)q.t[k - q.hdr];
+        else {
+          // content field: tag, varint length, bytes
+          const u32 e = k - ts_end;
+          const u32 vl = vlen(q.cl);
+          if (e == 0) b = (uint8_t)(2u << 3 | 2u);
+          else if (e <= vl) {
+            u64 v = q.cl;
+            for (u32 z = 1; z < e; ++z) v >>= 7;
+            b = (uint8_t)((v & 0x7f) | (e < vl ? 0x80 : 0));
+          } else b = q.c[e - 1 - vl];
+        }
+        q.d[k] = b;
+      }
     }
+    __builtin_amdgcn_wave_barrier();  // (meta is rewritten by the next round)
   }
 }
 
@@ -963,7 +1006,7 @@ int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, 
   if ((st = json_emit(ctx, tree, owners, n, jplan, reinterpret_cast<const uint64_t*>(jdst), reinterpret_cast<char*>(out))))
     return st;
   if (NS)
-    KLAUNCH(k_resp_msgs, dim3(grid_for(NS, 256)), dim3(256), n, (const u64*)sel_off, (const u64*)sel_id, NS,
+    KLAUNCH(k_resp_msgs, dim3(grid_for((NS + 63) / 64, 4)), dim3(256), n, (const u64*)sel_off, (const u64*)sel_id, NS,
             (const DSeg*)dseg, n_seg, (u64)stride, (const u64*)mpos, (const u64*)doff, out);
   return hip_ok(hipGetLastError());
 }
