@@ -298,16 +298,24 @@ class SyncServer:
             return self._device_fallback(arena, off, T, t_call)
         t1 = time.perf_counter()
         users = _decode_spans(pk[:ub], dst[:n + 1], ulen)
-        get = self.slot.get
-        new = [u for u in users if get(u) is None]  # (new users take slots in request order)
-        if new:
-            new = list(dict.fromkeys(new))
-            if len(self.slot) + len(new) > self.capacity:
-                raise _lib.EngineError(_lib.EVM_ECAPACITY, "SyncServer: more users than owner slots")
-            self.slot.update(zip(new, range(len(self.slot), len(self.slot) + len(new))))
-        slots = np.fromiter(map(get, users), dtype=np.int64, count=n)
-        if np.unique(slots).size != n:
-            return self._device_fallback(arena, off, T, t_call)  # (an owner twice: rounds)
+        if not self.slot and n <= self.capacity:
+            # a new server's first round: every user new, slots in request order
+            self.slot = dict(zip(users, range(n)))
+            if len(self.slot) != n:
+                self.slot = {}
+                return self._device_fallback(arena, off, T, t_call)  # (an owner twice: rounds)
+            slots = np.arange(n, dtype=np.int64)
+        else:
+            get = self.slot.get
+            new = [u for u in users if get(u) is None]  # (new users take slots in request order)
+            if new:
+                new = list(dict.fromkeys(new))
+                if len(self.slot) + len(new) > self.capacity:
+                    raise _lib.EngineError(_lib.EVM_ECAPACITY, "SyncServer: more users than owner slots")
+                self.slot.update(zip(new, range(len(self.slot), len(self.slot) + len(new))))
+            slots = np.fromiter(map(get, users), dtype=np.int64, count=n)
+            if np.unique(slots).size != n:
+                return self._device_fallback(arena, off, T, t_call)  # (an owner twice: rounds)
         T["users"] = time.perf_counter() - t1
         nmsg, cbytes = inf[:, 0], inf[:, 1]
         msg_base = np.zeros(n + 1, dtype=np.uint64)
