@@ -243,9 +243,7 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
   // 10-bit digits when they save a pass (EVM_OPT_RADIX 2): 1,024 digits per
   // pass, 4 per thread in the look-back
   const bool wide = ctx->radix_onesweep == 2 && (B + 9) / 10 < (B + RADIX_BITS - 1) / RADIX_BITS;
-  // 9-bit digits when they save a pass (EVM_OPT_RADIX 3): 512 digits, 2 per thread
-  const bool nine = ctx->radix_onesweep == 3 && (B + 8) / 9 < (B + RADIX_BITS - 1) / RADIX_BITS;
-  const int rb = wide ? 10 : nine ? 9 : RADIX_BITS;
+  const int rb = wide ? 10 : RADIX_BITS;
   const int bins = 1 << rb;
   const int passes = (B + rb - 1) / rb;
   const int width = (B + passes - 1) / passes;
@@ -269,10 +267,6 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
       KLAUNCH((k_radix_ghist<K, 10>), dim3(std::min<u32>(ntiles, 2048)), dim3(SORT_THREADS), keys, n, lo_bit, width,
               hi_bit, passes, gh);
       KLAUNCH((k_radix_gscan<10>), dim3(1), dim3(SORT_THREADS), gh, passes);
-    } else if (nine) {
-      KLAUNCH((k_radix_ghist<K, 9>), dim3(std::min<u32>(ntiles, 2048)), dim3(SORT_THREADS), keys, n, lo_bit, width,
-              hi_bit, passes, gh);
-      KLAUNCH((k_radix_gscan<9>), dim3(1), dim3(SORT_THREADS), gh, passes);
     } else {
       KLAUNCH((k_radix_ghist<K>), dim3(std::min<u32>(ntiles, 2048)), dim3(SORT_THREADS), keys, n, lo_bit, width,
               hi_bit, passes, gh);
@@ -283,9 +277,6 @@ int evm::radix_sort_pairs(evm_ctx* ctx, Scratch& S, K*& keys, u32*& vals, size_t
       const int bits = std::min(width, hi_bit - shift);
       if (wide)
         KLAUNCH((k_radix_onesweep<K, 10>), dim3(ntiles), dim3(SORT_THREADS), keys, vals, k2, v2, n, shift, bits,
-                gh + (size_t)p * bins, status, ctr + p, p, err);
-      else if (nine)
-        KLAUNCH((k_radix_onesweep<K, 9>), dim3(ntiles), dim3(SORT_THREADS), keys, vals, k2, v2, n, shift, bits,
                 gh + (size_t)p * bins, status, ctr + p, p, err);
       else
         KLAUNCH((k_radix_onesweep<K>), dim3(ntiles), dim3(SORT_THREADS), keys, vals, k2, v2, n, shift, bits,
@@ -1139,7 +1130,7 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
     ctx->overlap = (int)value;
     return EVM_OK;
   }
-  if (option == EVM_OPT_RADIX && value >= 0 && value <= 3) {
+  if (option == EVM_OPT_RADIX && value >= 0 && value <= 2) {
     ctx->radix_onesweep = (int)value;
     return EVM_OK;
   }

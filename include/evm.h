@@ -119,8 +119,7 @@ int evm_sync(evm_ctx* ctx);
                                  above the capacity through the sort path); 4 as 0 with K5 reading packed 32-B
                                  records instead of parsing the rows itself (A/B) */
 #define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 2 the same with \
-                                 10-bit digits when that saves a pass; 3 with 9-bit digits when that saves a pass; \
-                                 0 histogram + scan + scatter per pass */
+                                 10-bit digits when that saves a pass; 0 histogram + scan + scatter per pass */
 #define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM); \
                                  2 = K5 skips its check against the stored rows (the merge's guard then \
                                  returns EVM_ESTATE) */
