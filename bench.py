@@ -373,6 +373,14 @@ def emit(obj):
         os.write(_STDOUT, line)
 
 
+def progress(what):
+    """A line on stderr as each part of a long run starts (the JSON line comes at the end)."""
+    print("bench: %s (%.0f s)" % (what, time.perf_counter() - T_START), file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+
+
 def main():
     global TRAFFIC_DIR
     quiet_stdout()
@@ -618,15 +626,20 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and a.cpu_seconds > 0:
+            progress("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(ts_np, cell_np, a.cpu_seconds)
         del ts, cell, flags, ts_h, cell_h
         if world == 1 and a.extra:
+            progress("leg client_adversarial")
             out["client_adversarial"] = adversarial_leg(eng, a)
+            progress("leg config1")
             out["config1"] = config1_leg(eng, a)
             eng.close()
             torch.cuda.empty_cache()
+            progress("leg config3")
             out["config3"] = server_run(a, 0, 1, local, 100_000, 1000, 0.0, 1000, cpu=a.cpu_seconds > 0, leg=True)
             # config 4 at world 1: the per-GPU work of the N-GPU line (its weak-scaling base)
+            progress("leg config4")
             eng4 = Engine(local)
             dd4 = make_dist(eng4, 0, 1)
             out["config4"] = config4_rank(eng4, dd4, TorchComm(1, torch.device("cuda", local)), a.c4_owners,
@@ -635,6 +648,7 @@ def main():
             dd4.free()
             eng4.close()
             torch.cuda.empty_cache()
+            progress("leg config5_shape")
             eng5 = Engine(local)
             out["config5_shape"] = config5_shape_leg(eng5, a)
             eng5.close()
@@ -1832,6 +1846,7 @@ def reingest(eng, a, ts1, own1, owners, per_owner, request, flags):
 
     from evolu_amd import synth
 
+    progress("reingest")
     ts2_np, own2_np, _ = synth.config3(owners, per_owner, seed_config=3 + 7919, request=request)
     ts2, own2 = eng.dev(ts2_np), eng.dev(own2_np)
     del ts2_np, own2_np
@@ -1861,12 +1876,16 @@ def reingest(eng, a, ts1, own1, owners, per_owner, request, flags):
     dom = dominant(prof, SERVER_ALG)
     tot_ms, launches = prof[dom]
     # the store growing round after round: rounds 2, 3, 4 of
-    # new timestamps into one store holding 1, 2, 3 rounds
-    rounds = [(ts2, own2)]
-    for k in (2, 3):
-        t_np, o_np, _ = synth.config3(owners, per_owner, seed_config=3 + 7919 * k, request=request)
-        rounds.append((eng.dev(t_np), eng.dev(o_np)))
-        del t_np, o_np
+    # new messages of the same owners into one store holding 1, 2, 3 rounds
+    # (rounds 2-4 from the config-4 device generator at world 1: every owner's
+    # messages as one request, another seed per round -- seconds of host time
+    # saved per round against synth.config3)
+    progress("reingest rounds 2-4")
+    gen = synth.DeviceSynth()
+    rounds = []
+    for k in range(3):
+        t_d, o_d, _ = gen.source(0xE7040000 + k, owners, per_owner, 1, 0, ts2.device)
+        rounds.append((t_d, o_d))
     st = eng.store_new(owners)
     st.ingest(ts1, own1, 0, flags=flags)
     round_ms = []
@@ -1940,6 +1959,7 @@ def e2e_leg(eng, ts_np, owner_np, client, device_ms, sample=8):
 
     from evolu_amd.server import SyncServer
 
+    progress("e2e: bodies")
     t0 = time.perf_counter()
     arena, off = e2e_bodies(eng, ts_np, owner_np, client)
     gen_s = time.perf_counter() - t0
@@ -1987,6 +2007,7 @@ def e2e_device(eng, arena, off, host_out, O, pick, device_ms):
 
     from evolu_amd.server import SyncServer
 
+    progress("e2e: device round")
     a_d = torch.from_numpy(arena).to("cuda:%d" % eng.device)
     n = len(off) - 1
     prof = None
