@@ -365,124 +365,359 @@ struct JText {
   }
 };
 
-// The common text first: JSON.stringify's own form, read token by token --
-// `"d":{` opens a child (digits ascending), `"hash":N}` closes the node, a
-// comma follows every child -- 8 bytes of lookahead per token from the
-// register window.  Anything else (whitespace, another key order, a
-// malformed text) leaves the owner JP_SLOW for k_json_parse, which decides
-// exactly as the host parser.  Same outputs as k_json_parse.
+// The common text first: JSON.stringify's own form, `{` then tokens --
+// OPEN `"d":{` (a child, digits ascending), HASH `"hash":N}` (closes the
+// node; a `,` follows unless it is the root's) -- read a wave per tree, 1 KB
+// per step.  A token starts at every `"` after `{` or `,` and nowhere else in
+// that form, so the lanes find them in their 16 bytes independently; each
+// token checks that its successor starts right after it (through a `,` after
+// a HASH), hence the chain from the first token covers the text exactly.  The
+// structure then comes from wave scans over the tokens: the depth (+1 / -1),
+// the code (each token an operation "keep the digits above depth a, then set
+// B": composable), and the XOR of the leaves (childless nodes) before each
+// token; an internal node's hash must equal its leaves' XOR (the leaves XOR
+// at its close ^ at its open: the open is the last OPEN one depth up, found
+// by a ballot per depth or, from an earlier step, kept per depth in LDS).
+// Such a tree's leaves are its childless nodes in text order, exactly what
+// k_json_parse emits for it.  Anything else -- whitespace, another key
+// order, an internal node whose hash is not its leaves' XOR (a shorter key
+// of its own), a malformed text -- leaves the owner JP_SLOW for
+// k_json_parse, which decides exactly as the host parser.
 constexpr int32_t JP_SLOW = -1;
 constexpr u64 JP_KEY_MASK = 0xFFFFFF00FFull, JP_KEY = 0x7B3A220022ull;          // `"?":{`
 constexpr u64 JP_HASH_MASK = 0x00FFFFFFFFFFFFFFull, JP_HASH = 0x003A226873616822ull;  // `"hash":`
-__global__ __launch_bounds__(JP_THREADS) void k_json_canon(const uint8_t* __restrict__ json, const u64* __restrict__ jat,
-                                                           const u64* __restrict__ jlen, u32 n_owners,
-                                                           const u64* __restrict__ base, u64* __restrict__ t_off,
-                                                           u64* __restrict__ t_end, u64* __restrict__ ck,
-                                                           int32_t* __restrict__ xr, int32_t* __restrict__ pfx,
-                                                           int32_t* __restrict__ status, u64* __restrict__ n_leaves) {
-  __shared__ int32_t s_cx[JP_LEVELS][JP_THREADS];
-  __shared__ u32 s_first[JP_LEVELS][JP_THREADS];
-  __shared__ uint8_t s_fl[JP_LEVELS][JP_THREADS];  // any child (bit 0) | last child's digit + 1 (bits 1-2)
-  const u32 o = blockIdx.x * JP_THREADS + threadIdx.x;
-  if (o >= n_owners) return;
-  const u32 me = threadIdx.x;
+constexpr int JV_WAVES = 4;
+constexpr u32 JV_STEP = 2048;                // text bytes per step: 32 per lane
+constexpr u32 JV_BUF = 16 + JV_STEP + 48;    // the chunk before (a token's `{` / `,`), the step, lookahead
+constexpr u32 JV_TOK = JV_STEP / 2;          // token starts in a step (>= 2 bytes apart: `,"` in a malformed text)
+constexpr u32 JV_HASH = 3, JV_END = 4, JV_BAD = 5, JV_ROOT = 6, JV_NONE = 7;  // token kinds (0-2: OPEN digit)
+constexpr u64 CODE_ALL = (1ull << (2 * CODE_DIGITS)) - 1ull;
+
+struct alignas(16) JvLds {
+  u32 buf[JV_BUF / 4];
+  uint16_t pos[JV_TOK];      // the step's token starts (buffer bytes), in text order
+  int32_t stk[CODE_DIGITS];  // the leaves' XOR before the last OPEN at each depth (earlier chunks)
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// bit k: byte k of w equals c (c4 = c in every byte)
+__device__ __forceinline__ u32 bytes_eq(u32 w, u32 c4) {
+  const u32 x = w ^ c4;
+  const u32 t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 in the zero bytes
+  return ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+}
+
+// the code's bits of the digits above depth a (digit d at bits 2 * (CODE_DIGITS - 1 - d))
+__device__ __forceinline__ u64 digits_above(int a) {
+  const int sh = min(max(2 * (CODE_DIGITS - a), 0), 2 * CODE_DIGITS);
+  return CODE_ALL & ~((1ull << sh) - 1ull);
+}
+
+__device__ __forceinline__ u64 shfl_up_u64(u64 v, int d) {
+  return ((u64)(u32)__shfl_up((int)(u32)(v >> 32), d, 64) << 32) | (u32)__shfl_up((int)(u32)v, d, 64);
+}
+
+// Wave scans on the DPP network (row shifts 1, 2, 4, 8, then the row
+// broadcasts of lanes 15 and 31): combine(earlier, later) at each step.
+template <int CTRL>
+__device__ __forceinline__ u32 dpp(u32 x) {
+  return (u32)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ u32 rl(u32 x, int l) { return (u32)__builtin_amdgcn_readlane((int)x, l); }
+template <int CTRL>
+__device__ __forceinline__ u64 dpp64(u64 x) {
+  return ((u64)dpp<CTRL>((u32)(x >> 32)) << 32) | dpp<CTRL>((u32)x);
+}
+template <class T, class Comb>
+__device__ __forceinline__ T wave_scan(T x, int lane, Comb comb) {
+  const int r = lane & 15;
+  T y = x.template shift<0x111>();
+  x = r >= 1 ? comb(y, x) : x;
+  y = x.template shift<0x112>();
+  x = r >= 2 ? comb(y, x) : x;
+  y = x.template shift<0x114>();
+  x = r >= 4 ? comb(y, x) : x;
+  y = x.template shift<0x118>();
+  x = r >= 8 ? comb(y, x) : x;
+  // across the rows: lane 15 of each row into the next, then lane 31 into rows 2 and 3
+  y = x.template shift<0x142>();
+  x = (lane & 31) >= 16 ? comb(y, x) : x;
+  y = x.template shift<0x143>();
+  x = lane >= 32 ? comb(y, x) : x;
+  return x;
+}
+// (the scanned values: a count; depth change and leaf XOR; the code operation
+// "keep the digits above depth a, then set B"; a min and a max)
+struct JvCount {
+  u32 n;
+  template <int CTRL>
+  __device__ __forceinline__ JvCount shift() const { return JvCount{dpp<CTRL>(n)}; }
+  __device__ __forceinline__ JvCount at(int l) const { return JvCount{rl(n, l)}; }
+};
+struct JvDepth {
+  int dx;
+  u32 px;
+  template <int CTRL>
+  __device__ __forceinline__ JvDepth shift() const { return JvDepth{(int)dpp<CTRL>((u32)dx), dpp<CTRL>(px)}; }
+  __device__ __forceinline__ JvDepth at(int l) const { return JvDepth{(int)rl((u32)dx, l), rl(px, l)}; }
+};
+struct JvOp {
+  int a;
+  u64 B;
+  template <int CTRL>
+  __device__ __forceinline__ JvOp shift() const { return JvOp{(int)dpp<CTRL>((u32)a), dpp64<CTRL>(B)}; }
+  __device__ __forceinline__ JvOp at(int l) const { return JvOp{(int)rl((u32)a, l), ((u64)rl((u32)(B >> 32), l) << 32) | rl((u32)B, l)}; }
+};
+struct JvRange {
+  int mn, mx;
+  template <int CTRL>
+  __device__ __forceinline__ JvRange shift() const { return JvRange{(int)dpp<CTRL>((u32)mn), (int)dpp<CTRL>((u32)mx)}; }
+  __device__ __forceinline__ JvRange at(int l) const { return JvRange{(int)rl((u32)mn, l), (int)rl((u32)mx, l)}; }
+};
+
+// The token at buffer byte pb (text position p, the text ends at E): its kind
+// (0-2, JV_HASH, JV_END, or JV_BAD) and hash.
+__device__ __forceinline__ u32 jv_token(const JvLds* w, u32 pb, u64 p, u64 E, int32_t* hv) {
+  const u32 a = pb >> 2, s = pb & 3u;
+  const u32 w0 = w->buf[a], w1 = w->buf[a + 1], w2 = w->buf[a + 2], w3 = w->buf[a + 3], w4 = w->buf[a + 4],
+            w5 = w->buf[a + 5], w6 = w->buf[a + 6];
+  const u64 X = ((u64)__builtin_amdgcn_alignbyte(w2, w1, s) << 32) | __builtin_amdgcn_alignbyte(w1, w0, s);
+  const u64 X1 = ((u64)__builtin_amdgcn_alignbyte(w4, w3, s) << 32) | __builtin_amdgcn_alignbyte(w3, w2, s);
+  const u64 X2 = ((u64)__builtin_amdgcn_alignbyte(w6, w5, s) << 32) | __builtin_amdgcn_alignbyte(w5, w4, s);
+  auto byte = [&](int k) -> u32 {
+    return (u32)((k < 8 ? X >> (8 * k) : k < 16 ? X1 >> (8 * (k - 8)) : X2 >> (8 * (k - 16))) & 0xffu);
+  };
+  *hv = 0;
+  if ((X & JP_KEY_MASK) == JP_KEY) {
+    const u32 d = byte(1) - '0';
+    return d < 3u && byte(5) == '"' && p + 5 < E ? d : JV_BAD;
+  }
+  if ((X & JP_HASH_MASK) != JP_HASH) return JV_BAD;
+  // -?(0|[1-9][0-9]*) within int32, `}`, then `,"` or the end of the text
+  const bool neg = byte(7) == '-';
+  u32 run = 1, nd = 0, after = 0, t0 = 0, t1 = 0, t2 = 0, d0 = 0;
+  u64 v = 0;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const u32 c = neg ? byte(8 + k) : byte(7 + k);
+    const u32 dg = c - '0';
+    if (k == 0) d0 = c;
+    const bool more = run && dg < 10u && k < 11;
+    v = more ? v * 10u + dg : v;
+    nd += more ? 1u : 0u;
+    t0 = run && !more ? c : t0;
+    t1 = after == 1 ? c : t1;
+    t2 = after == 2 ? c : t2;
+    after = run && !more ? 1u : after ? after + 1u : 0u;
+    run = more ? 1u : 0u;
+  }
+  if (nd == 0 || nd > 10 || (nd > 1 && d0 == '0') || (neg && v == 0) || t0 != '}' ||
+      v > (neg ? 2147483648ull : 2147483647ull))
+    return JV_BAD;
+  *hv = (int32_t)(neg ? 0ull - v : v);
+  const u64 end = p + 8 + (neg ? 1 : 0) + nd;
+  if (end == E) return JV_END;
+  return t1 == ',' && t2 == '"' && end + 1 < E ? JV_HASH : JV_BAD;
+}
+
+__global__ __launch_bounds__(64 * JV_WAVES) void k_json_wave(const uint8_t* __restrict__ json, const u64* __restrict__ jat,
+                                                              const u64* __restrict__ jlen, u32 n_owners,
+                                                              const u64* __restrict__ base, u64* __restrict__ t_off,
+                                                              u64* __restrict__ t_end, u64* __restrict__ ck,
+                                                              int32_t* __restrict__ xr, int32_t* __restrict__ pfx,
+                                                              int32_t* __restrict__ status, u64* __restrict__ n_leaves) {
+  __shared__ JvLds lds[JV_WAVES];
+  JvLds* w = &lds[threadIdx.x >> 6];
+  const int lane = (int)(threadIdx.x & 63);
+  const u32 o = blockIdx.x * JV_WAVES + (threadIdx.x >> 6);
+  if (o >= n_owners) return;  // (the whole wave)
+  const u64 lt = (1ull << lane) - 1ull;
   const u64 b0 = base[o];
   const u64 bound = base[o + 1] - b0 - 1;
-  t_off[o] = b0;
-  u64 cnt = 0;
-  int32_t run = 0;
-  int st = 0;
   const u64 L = jlen[o];
-  if (L) {
-    const uint8_t* p = json + jat[o];
-    const uint8_t* e = p + L;
-    Win win;
-    win.init(e);
-    if (!(L == 2 && win.get(p) == '{' && win.get(p + 1) == '}')) {  // ({} : the empty tree)
-      st = JP_SLOW;
-      if (win.get(p) == '{') {
-        ++p;
-        int d = 0;
-        u64 prefix = 0;
-        s_cx[0][me] = 0;
-        s_fl[0][me] = 0;
-        s_first[0][me] = 0;
-        for (;;) {
-          if (e - p < 8) break;
-          const u64 x = win.get8(p);
-          if ((x & JP_KEY_MASK) == JP_KEY) {
-            const u32 k = (u32)((x >> 8) & 0xffu) - '0';
-            const uint8_t fl = s_fl[d][me];
-            if (k > 2 || d >= CODE_DIGITS || k + 1 <= (u32)(fl >> 1)) break;
-            s_fl[d][me] = (uint8_t)(((k + 1) << 1) | (fl & 1u));
-            prefix |= (u64)(k + 1) << (2 * (CODE_DIGITS - 1 - d));
-            ++d;
-            s_cx[d][me] = 0;
-            s_fl[d][me] = 0;
-            s_first[d][me] = (u32)cnt;
-            p += 5;
-            continue;
+  int st = JP_SLOW;
+  u64 cnt = 0;
+  int32_t P = 0;  // the leaves' XOR so far
+  if (L == 0) {
+    st = 0;
+  } else if (L >= 2) {
+    const uint8_t* tx = json + jat[o];
+    const uint8_t c0 = tx[0], c1 = tx[1];
+    if (L == 2 && c0 == '{' && c1 == '}') {
+      st = 0;
+    } else if (c0 == '{' && c1 == '"') {
+      const uint8_t* A = reinterpret_cast<const uint8_t*>((uintptr_t)tx & ~(uintptr_t)15);
+      const uint8_t* lim = reinterpret_cast<const uint8_t*>(((uintptr_t)(tx + L) + 15) & ~(uintptr_t)15);
+      const u64 s0 = (u64)(tx - A), E = s0 + L;  // text positions from A
+      auto chunk = [lim](const uint8_t* c) -> uint4 {
+        if (c < lim) return *reinterpret_cast<const uint4*>(c);
+        return make_uint4(0, 0, 0, 0);
+      };
+      int depth = 0;
+      u64 code = 0, lastcode = 0;
+      u32 lastk = JV_ROOT;
+      bool bad = false;
+      // the step's 32 bytes per lane and the 48 after the step (lanes 0-2), loaded
+      // one step ahead
+      uint4 v0 = chunk(A + 32 * lane), v1 = chunk(A + 32 * lane + 16), la = make_uint4(0, 0, 0, 0);
+      if (lane < 3) la = chunk(A + JV_STEP + 16 * lane);
+      uint4 last1 = make_uint4(0, 0, 0, 0);  // (lane 63: the step before's last 16 bytes)
+      for (u64 P0 = 0; P0 < E && !bad; P0 += JV_STEP) {
+        const uint8_t* S1 = A + P0 + JV_STEP;
+        const uint4 n0 = chunk(S1 + 32 * lane), n1 = chunk(S1 + 32 * lane + 16);
+        uint4 nla = make_uint4(0, 0, 0, 0);
+        if (lane < 3) nla = chunk(S1 + JV_STEP + 16 * lane);
+        // stage the step's bytes, the chunk before them and the lookahead in LDS
+        uint4* b4 = reinterpret_cast<uint4*>(w->buf);
+        b4[1 + 2 * lane] = v0;
+        b4[2 + 2 * lane] = v1;
+        if (lane < 3) b4[1 + 2 * 64 + lane] = la;
+        if (lane == 63) b4[0] = last1;
+        wave_sync();
+        // token starts in this lane's 32 bytes: `"` after `{` or `,`, within [s0 + 1, E)
+        const u32 prev = w->buf[3 + 8 * lane] >> 24;
+        auto oc4 = [](u32 x) { return bytes_eq(x, 0x7B7B7B7Bu) | bytes_eq(x, 0x2C2C2C2Cu); };
+        auto q4 = [](u32 x) { return bytes_eq(x, 0x22222222u); };
+        const u32 q = q4(v0.x) | q4(v0.y) << 4 | q4(v0.z) << 8 | q4(v0.w) << 12 | q4(v1.x) << 16 | q4(v1.y) << 20 |
+                      q4(v1.z) << 24 | q4(v1.w) << 28;
+        const u32 oc = oc4(v0.x) | oc4(v0.y) << 4 | oc4(v0.z) << 8 | oc4(v0.w) << 12 | oc4(v1.x) << 16 |
+                       oc4(v1.y) << 20 | oc4(v1.z) << 24 | oc4(v1.w) << 28;
+        u32 starts = q & ((oc << 1) | (prev == '{' || prev == ',' ? 1u : 0u));
+        const u64 pos0 = P0 + 32 * (u64)lane;
+        const int64_t lo = (int64_t)(s0 + 1) - (int64_t)pos0, hi = (int64_t)E - (int64_t)pos0;
+        if (lo > 0) starts &= lo >= 32 ? 0u : ~((1u << lo) - 1u);
+        if (hi < 32) starts &= hi <= 0 ? 0u : (1u << hi) - 1u;
+        last1 = v1;
+        v0 = n0;
+        v1 = n1;
+        la = nla;
+        const u32 nt = __popc(starts);
+        u32 tb = wave_scan(JvCount{nt}, lane, [](JvCount y, JvCount x) { return JvCount{x.n + y.n}; }).n;
+        const u32 T = __builtin_amdgcn_readlane(tb, 63);
+        tb -= nt;
+        while (starts) {
+          const u32 j = __ffs(starts) - 1;
+          starts &= starts - 1;
+          w->pos[tb++] = (uint16_t)(16 + 32 * lane + j);
+        }
+        wave_sync();
+        // the tokens, 64 at a time, one per lane
+        for (u32 c = 0; c < T; c += 64) {
+          const u32 i = c + lane;
+          int32_t h = 0;
+          u32 k = JV_NONE;
+          if (i < T) {
+            const u32 pb = w->pos[i];
+            k = jv_token(w, pb, P0 + pb - 16, E, &h);
           }
-          if ((x & JP_HASH_MASK) != JP_HASH) break;
-          p += 7;
-          // -?(0|[1-9][0-9]*) within int32, then `}` (and `,` after a child): at most
-          // 13 bytes, all in the next 16
-          const u64 y1 = win.get8(p), y2 = win.get8(p + 8);
-          auto byte_at = [&](u32 k) -> u32 { return (u32)((k < 8 ? y1 >> (8 * k) : y2 >> (8 * (k - 8))) & 0xffu); };
-          u32 k = 0;
-          const bool neg = byte_at(0) == '-';
-          if (neg) k = 1;
-          int64_t v = 0;
-          u32 nd = 0, c = 0;
-          while (k < 12 && (c = byte_at(k)) >= '0' && c <= '9') {
-            v = v * 10 + (c - '0');
-            ++nd;
-            ++k;
+          const bool open = k < 3, hash = k == JV_HASH || k == JV_END;
+          const int dlt = open ? 1 : hash ? -1 : 0;
+          // the token before: its kind, and (below) the code before it
+          u32 pk = (u32)__shfl_up((int)k, 1, 64);
+          if (lane == 0) pk = lastk;
+          const bool leaf = hash && pk < 3;
+          const int32_t lv = leaf ? h : 0;
+          // depth and leaf XOR: inclusive scans
+          const JvDepth sc = wave_scan(JvDepth{dlt, (u32)lv}, lane,
+                                       [](JvDepth y, JvDepth x) { return JvDepth{x.dx + y.dx, x.px ^ y.px}; });
+          const int db = depth + sc.dx - dlt;  // the depth before each token
+          const int32_t pb = P ^ (int32_t)sc.px ^ lv;
+          bool bl = k == JV_BAD || (open && db >= CODE_DIGITS) || (k == JV_HASH && db <= 0) || (k == JV_END && db != 0);
+          // the code before each token: the composition of the operations before it
+          JvOp op{63, 0};
+          if (open && db < CODE_DIGITS) {
+            op.a = db;
+            op.B = (u64)(k + 1) << (2 * (CODE_DIGITS - 1 - db));
+          } else if (hash) {
+            op.a = db > 0 ? db - 1 : 0;
           }
-          if (nd == 0 || nd > 10 || (nd > 1 && byte_at(k - nd) == '0') || (neg && v == 0) || c != '}' ||
-              p + k >= e)
-            break;
-          if (neg) v = -v;
-          if (v < (int64_t)INT32_MIN || v > (int64_t)INT32_MAX) break;
-          const bool comma = p + k + 1 < e && byte_at(k + 1) == ',';
-          p += k + 1;
-          const int32_t h = (int32_t)v;
-          const int32_t cx = s_cx[d][me];
-          const bool any = s_fl[d][me] & 1u;
-          if (d == 0) {  // the root: children, their XOR as its hash, the end of the text
-            if (any && (h ^ cx) == 0 && p == e) st = 0;
-            break;
+          const JvOp oc2 = wave_scan(op, lane, [](JvOp y, JvOp x) {  // (y before x)
+            return JvOp{min(x.a, y.a), (y.B & digits_above(x.a)) | x.B};
+          });
+          int ea = __shfl_up(oc2.a, 1, 64);
+          u64 eB = shfl_up_u64(oc2.B, 1);
+          if (lane == 0) {
+            ea = 63;
+            eB = 0;
           }
-          const int32_t t = h ^ cx;
-          if (!any || t != 0) {
-            if (cnt >= bound) break;
-            const u64 at = s_first[d][me];  // (in front of its subtree's leaves: see k_json_parse)
-            for (u64 i = cnt; i > at; --i) {
-              ck[b0 + i] = ck[b0 + i - 1];
-              xr[b0 + i] = xr[b0 + i - 1];
-              pfx[b0 + i] = pfx[b0 + i - 1] ^ t;
+          const u64 cb = (code & digits_above(ea)) | eB;
+          u64 pc = shfl_up_u64(cb, 1);
+          if (lane == 0) pc = lastcode;
+          // an internal node's open: the last OPEN one depth up (in this chunk: a
+          // ballot per depth present; before it: the depth's entry in stk)
+          const int need = hash && !leaf && db >= 1 ? db - 1 : -1;
+          u64 mneed = 0, mown = 0;
+          const u64 opens = __ballot(open && db < CODE_DIGITS);
+          if (opens) {
+            const bool o2 = open && db < CODE_DIGITS;
+            const JvRange r = wave_scan(JvRange{o2 ? db : 64, o2 ? db : -1}, lane,
+                                        [](JvRange y, JvRange x) { return JvRange{min(x.mn, y.mn), max(x.mx, y.mx)}; });
+            const int dmin = __builtin_amdgcn_readlane(r.mn, 63), dmax = __builtin_amdgcn_readlane(r.mx, 63);
+            for (int d = dmin; d <= dmax; ++d) {
+              const u64 b = __ballot(open && db == d);
+              mneed = need == d ? b : mneed;
+              mown = open && db == d ? b : mown;
             }
-            ck[b0 + at] = ((u64)o << 40) | prefix;
-            xr[b0 + at] = t;
-            if (at == cnt) pfx[b0 + at] = run;
-            run ^= t;
-            ++cnt;
           }
-          --d;
-          s_cx[d][me] ^= h;
-          s_fl[d][me] |= 1u;
-          prefix &= ~((4ull << (2 * (CODE_DIGITS - 1 - d))) - 1ull);
-          if (!comma) break;  // (a child is followed by its parent's next member)
-          ++p;
+          const u64 mm = mneed & lt;
+          const int32_t po_lane = __shfl(pb, mm ? 63 - __clzll(mm) : lane, 64);
+          if (hash && !leaf) {
+            if (db == 0) bl |= pk != JV_HASH || h != pb;  // the root: children, their leaves' XOR
+            else if (db > 0) bl |= h != (pb ^ (mm ? po_lane : w->stk[need]));
+          }
+          if (open && pk == JV_HASH && db < CODE_DIGITS)  // the previous sibling's digit below this one
+            bl |= ((pc >> (2 * (CODE_DIGITS - 1 - db))) & 3u) > k;
+          // the leaves out, in text order
+          const u64 lb = __ballot(leaf);
+          const u64 at = cnt + __popcll(lb & lt);
+          if (leaf) {
+            if (at >= bound) {
+              bl = true;
+            } else {
+              ck[b0 + at] = ((u64)o << 40) | cb;
+              xr[b0 + at] = h;
+              pfx[b0 + at] = pb;
+            }
+          }
+          wave_sync();
+          if (open && db < CODE_DIGITS && (mown >> lane) == 1ull) w->stk[db] = pb;
+          wave_sync();
+          cnt += __popcll(lb);
+          depth = __builtin_amdgcn_readlane(depth + sc.dx, 63);
+          P = __builtin_amdgcn_readlane(pb ^ lv, 63);
+          const u64 ca = (cb & digits_above(op.a)) | op.B;
+          code = ((u64)rl((u32)(ca >> 32), 63) << 32) | rl((u32)ca, 63);
+          const int last = (int)min<u32>(T - c, 64u) - 1;
+          lastk = __builtin_amdgcn_readlane(k, last);
+          lastcode = ((u64)rl((u32)(cb >> 32), last) << 32) | rl((u32)cb, last);
+#ifdef JV_DEBUG
+          if (lane == 0)
+            printf("P0 %llu c %u T %u depth %d code %llx P %d lastk %u lastcode %llx cnt %llu bl %d\n",
+                   (unsigned long long)P0, c, T, depth, (unsigned long long)code, P, lastk,
+                   (unsigned long long)lastcode, (unsigned long long)cnt, (int)(__ballot(bl) != 0));
+#endif
+          if (__ballot(bl)) {
+            bad = true;
+            break;
+          }
         }
       }
+      if (!bad && lastk == JV_END) st = 0;
     }
   }
   if (st) cnt = 0;
-  pfx[b0 + cnt] = st ? 0 : run;
-  t_end[o] = b0 + cnt;
-  status[o] = st;
-  if (cnt) atomicAdd(n_leaves, cnt);
+  if (lane == 0) {
+    t_off[o] = b0;
+    pfx[b0 + cnt] = st ? 0 : P;
+    t_end[o] = b0 + cnt;
+    status[o] = st;
+    if (cnt) atomicAdd(n_leaves, cnt);
+  }
 }
 
 // owner o's text at json + jat[o], jlen[o] bytes (jlen 0: no request, the
@@ -500,7 +735,7 @@ __global__ __launch_bounds__(JP_THREADS) void k_json_parse(const uint8_t* __rest
   __shared__ uint8_t s_fl[JP_LEVELS][JP_THREADS];  // seen keys (bits 0-3) | any child (bit 4)
   __shared__ u32 s_first[JP_LEVELS][JP_THREADS];    // leaves emitted when the node opened
   const u32 o = blockIdx.x * JP_THREADS + threadIdx.x;
-  if (o >= n_owners || status[o] != JP_SLOW) return;  // (k_json_canon read it)
+  if (o >= n_owners || status[o] != JP_SLOW) return;  // (k_json_wave read it)
   const u32 me = threadIdx.x;
   const u64 b0 = base[o];
   const u64 bound = base[o + 1] - b0 - 1;  // leaf slots (one more holds the root's prefix)
@@ -904,7 +1139,7 @@ int evm_tree_from_json_dev(evm_ctx* ctx, uint32_t n_owners, const uint8_t* json,
   if ((st = tree_alloc_gapped(ctx, n_owners, std::max<u64>(cap, 1), &t))) return st;
   HIPR(hipMemsetAsync(t->off + n_owners, 0, sizeof(u64), ctx->stream));
   if (n_owners)
-    KLAUNCH(k_json_canon, dim3((n_owners + JP_THREADS - 1) / JP_THREADS), dim3(JP_THREADS), json, (const u64*)at,
+    KLAUNCH(k_json_wave, dim3((n_owners + JV_WAVES - 1) / JV_WAVES), dim3(64 * JV_WAVES), json, (const u64*)at,
             (const u64*)len, n_owners, (const u64*)slots, (u64*)t->off, (u64*)t->end, (u64*)t->ck, t->xr, t->pfx,
             status, nl);
   if (n_owners)
