@@ -111,6 +111,8 @@ SIGNATURES = {
     "evm_pb_encode_responses": (_i, [_u32, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
     "evm_pb_scan_dev": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp]),
     "evm_pb_split_dev": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "evm_pb_scan_index_dev": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp, _vp]),
+    "evm_pb_split_index_dev": (_i, [_vp, _i, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     "evm_gather_spans_dev": (_i, [_vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     "evm_tree_from_json_dev": (_i, [_vp, _u32, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),
     "evm_pb_encode_responses_dev": (_i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp, _vp,

@@ -161,13 +161,14 @@ __device__ __forceinline__ bool d_read_msg(const uint8_t* q, u64 n, DMsg* m, Win
   return r.ok;
 }
 
-// evm_proto.cpp's walk(): on_msg(index, msg) per message
+// evm_proto.cpp's walk(): on_msg(index, msg, its field's tag) per message
 template <typename F>
 __device__ __forceinline__ int d_walk(int kind, const uint8_t* buf, u64 len, evm_pb_sync* info, Win* win, F on_msg) {
   DReader r{buf, buf + len, true, win};
   evm_pb_sync s{0, 0, 0, 0, 0, 0, 0, 0, 0};
   const u32 tree_field = kind == EVM_PB_SYNC_REQUEST ? 4u : 2u;
   while (r.more()) {
+    const uint8_t* at = r.p;
     const u64 tag = r.varint();
     if (!r.ok) return EVM_EINVAL;
     const u32 field = (u32)(tag >> 3), wt = (u32)(tag & 7);
@@ -187,7 +188,7 @@ __device__ __forceinline__ int d_walk(int kind, const uint8_t* buf, u64 len, evm
       if (!d_read_msg(q, n, &m, win)) return EVM_EINVAL;
       if (m.ts_len != 46) ++s.nonstd_ts;
       s.content_bytes += m.content_len;
-      on_msg(s.n_messages, m);
+      on_msg(s.n_messages, m, at);
       ++s.n_messages;
     } else if (field == tree_field) {
       s.tree_off = off;
@@ -205,14 +206,22 @@ __device__ __forceinline__ int d_walk(int kind, const uint8_t* buf, u64 len, evm
   return EVM_OK;
 }
 
+// (slots: where each message's field starts, body k's i-th at slots[a / 50 + i]
+// -- a message with a 46-byte timestamp takes >= 50 bytes, so the bodies'
+// ranges [a / 50, b / 50) do not overlap; a body with a shorter message may
+// not have room for every one: its nonstd_ts count is nonzero)
+constexpr u64 PB_MIN_MSG = 50;
 __global__ void k_pb_scan(int kind, const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
-                          evm_pb_sync* __restrict__ info, int32_t* __restrict__ status) {
+                          evm_pb_sync* __restrict__ info, int32_t* __restrict__ status, u64* __restrict__ slots) {
   for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
     const u64 a = off[k], b = off[k + 1];
     evm_pb_sync s{0, 0, 0, 0, 0, 0, 0, 0, 0};
     Win win;
     win.init(arena + b);
-    int st = b < a ? EVM_EINVAL : d_walk(kind, arena + a, b - a, &s, &win, [](u64, const DMsg&) {});
+    const u64 s0 = a / PB_MIN_MSG, room = b / PB_MIN_MSG - s0;
+    int st = b < a ? EVM_EINVAL : d_walk(kind, arena + a, b - a, &s, &win, [&](u64 i, const DMsg&, const uint8_t* at) {
+      if (slots && i < room) slots[s0 + i] = (u64)(at - arena);
+    });
     if (st) s = evm_pb_sync{0, 0, 0, 0, 0, 0, 0, 0, 0};
     info[k] = s;
     status[k] = st;
@@ -276,6 +285,53 @@ __global__ void k_pb_rows(const uint8_t* __restrict__ arena, const u64* __restri
     for (u64 j = 48; j < stride; j += 8) row[j >> 3] = 0ull;
     cat[m] = msg.content ? (u64)(msg.content - arena) : 0ull;
     clen[m] = msg.content_len;
+  }
+}
+
+// k_pb_rows from the scan's slots: a wave per body, a lane per message
+__global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
+                                                     const int32_t* __restrict__ status, const u64* __restrict__ msg_base,
+                                                     const u64* __restrict__ slots, const u32* __restrict__ owner_of,
+                                                     char* __restrict__ ts, u64 stride, u64* __restrict__ cat,
+                                                     u64* __restrict__ clen, u32* __restrict__ owner, u32* __restrict__ bad) {
+  const u32 lane = threadIdx.x & 63;
+  for (u32 k = blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += gridDim.x * 4) {
+    if (status[k]) continue;
+    const u64 a = off[k], b = off[k + 1], m0 = msg_base[k], mn = msg_base[k + 1] - m0;
+    const u64 s0 = a / PB_MIN_MSG;
+    const u32 ow = owner_of ? owner_of[k] : 0u;
+    if (mn > b / PB_MIN_MSG - s0) {  // (a message shorter than 50 bytes: its timestamp is not 46)
+      if (lane == 0) atomicOr(bad, 1u);
+      for (u64 i = lane; i < mn; i += 64) {  // (its rows empty, no content: the call fails)
+        u64* row = reinterpret_cast<u64*>(ts + (m0 + i) * stride);
+        for (u64 j = 0; j < stride; j += 8) row[j >> 3] = ~0ull;
+        cat[m0 + i] = 0;
+        clen[m0 + i] = 0;
+        if (owner) owner[m0 + i] = ow;
+      }
+      continue;
+    }
+    for (u64 i = lane; i < mn; i += 64) {
+      const uint8_t* f = arena + slots[s0 + i];
+      Win win;
+      win.init(arena + b);
+      DReader r{f, arena + b, true, &win};
+      r.varint();  // (the field's tag: 1, length-delimited -- the scan read it)
+      const uint8_t* q;
+      u64 len;
+      r.bytes(&q, &len);
+      DMsg msg;
+      d_read_msg(q, len, &msg, &win);
+      const u64 m = m0 + i;
+      u64* row = reinterpret_cast<u64*>(ts + m * stride);
+      const bool std46 = msg.ts_len == 46;
+      for (int j = 0; j < 5; ++j) row[j] = std46 ? win.get8(msg.ts + 8 * j) : ~0ull;
+      row[5] = (std46 ? win.get8(msg.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
+      for (u64 j = 48; j < stride; j += 8) row[j >> 3] = 0ull;
+      cat[m] = msg.content ? (u64)(msg.content - arena) : 0ull;
+      clen[m] = msg.content_len;
+      if (owner) owner[m] = ow;
+    }
   }
 }
 
@@ -498,24 +554,30 @@ __device__ __forceinline__ u32 jv_token(const JvLds* w, u32 pb, u64 p, u64 E, in
     return d < 3u && byte(5) == '"' && p + 5 < E ? d : JV_BAD;
   }
   if ((X & JP_HASH_MASK) != JP_HASH) return JV_BAD;
-  // -?(0|[1-9][0-9]*) within int32, `}`, then `,"` or the end of the text
+  // -?(0|[1-9][0-9]*) within int32, `}`, then `,"` or the end of the text: the
+  // 16 bytes after the sign as two words, the digits found and read 8 at a time
   const bool neg = byte(7) == '-';
-  u32 run = 1, nd = 0, after = 0, t0 = 0, t1 = 0, t2 = 0, d0 = 0;
-  u64 v = 0;
-#pragma unroll
-  for (int k = 0; k < 14; ++k) {
-    const u32 c = neg ? byte(8 + k) : byte(7 + k);
-    const u32 dg = c - '0';
-    if (k == 0) d0 = c;
-    const bool more = run && dg < 10u && k < 11;
-    v = more ? v * 10u + dg : v;
-    nd += more ? 1u : 0u;
-    t0 = run && !more ? c : t0;
-    t1 = after == 1 ? c : t1;
-    t2 = after == 2 ? c : t2;
-    after = run && !more ? 1u : after ? after + 1u : 0u;
-    run = more ? 1u : 0u;
-  }
+  const u64 lo = neg ? X1 : (X >> 56) | (X1 << 8), hi = neg ? X2 : (X1 >> 56) | (X2 << 8);
+  auto nondigit = [](u64 x) -> u64 {  // 0x80 in the bytes that are not '0'-'9'
+    const u64 y = ((x & 0xF0F0F0F0F0F0F0F0ull) ^ 0x3030303030303030ull) |
+                  (((x & 0x0F0F0F0F0F0F0F0Full) + 0x0606060606060606ull) & 0x1010101010101010ull);
+    return (((y & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | y) & 0x8080808080808080ull;
+  };
+  auto eight = [](u64 x) -> u64 {  // 8 digits, the first in the low byte
+    x = (x & 0x0F0F0F0F0F0F0F0Full) * 2561 >> 8;
+    x = (x & 0x00FF00FF00FF00FFull) * 6553601 >> 16;
+    return (x & 0x0000FFFF0000FFFFull) * 42949672960001ull >> 32;
+  };
+  const u64 ml = nondigit(lo), mh = nondigit(hi);
+  const u32 nd = ml ? (u32)__builtin_ctzll(ml) >> 3 : 8u + (mh ? (u32)__builtin_ctzll(mh) >> 3 : 8u);
+  if (nd == 0 || nd > 10) return JV_BAD;
+  const u32 sh = 8 * nd;
+  const u64 tail = sh < 64 ? (lo >> sh) | (hi << (64 - sh)) : hi >> (sh - 64);
+  const u32 t0 = (u32)tail & 0xffu, t1 = (u32)(tail >> 8) & 0xffu, t2 = (u32)(tail >> 16) & 0xffu;
+  const u32 d0 = (u32)lo & 0xffu;
+  const u64 e8 = eight(nd >= 8 ? lo : lo << (64 - sh));
+  const u64 d8 = (hi & 0xffu) - '0', d9 = ((hi >> 8) & 0xffu) - '0';
+  const u64 v = nd <= 8 ? e8 : nd == 9 ? e8 * 10u + d8 : e8 * 100u + d8 * 10u + d9;
   if (nd == 0 || nd > 10 || (nd > 1 && d0 == '0') || (neg && v == 0) || t0 != '}' ||
       v > (neg ? 2147483648ull : 2147483647ull))
     return JV_BAD;
@@ -1061,19 +1123,26 @@ __global__ __launch_bounds__(256) void k_resp_msgs(u32 n, const u64* __restrict_
 
 extern "C" {
 
-int evm_pb_scan_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n, evm_pb_sync* info,
-                    int32_t* status) {
+int evm_pb_scan_index_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n,
+                          evm_pb_sync* info, int32_t* status, uint64_t* slots) {
   if (!ctx || (n && (!arena || !off || !info || !status)) ||
       (kind != EVM_PB_SYNC_REQUEST && kind != EVM_PB_SYNC_RESPONSE))
     return EVM_EINVAL;
-  if (n) KLAUNCH(k_pb_scan, dim3(grid_for(n, 64, 1 << 16)), dim3(64), kind, arena, (const u64*)off, n, info, status);
+  if (n)
+    KLAUNCH(k_pb_scan, dim3(grid_for(n, 64, 1 << 16)), dim3(64), kind, arena, (const u64*)off, n, info, status,
+            (u64*)slots);
   return hip_ok(hipGetLastError());
 }
 
-int evm_pb_split_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n,
-                     const int32_t* status, const uint64_t* msg_base, const uint64_t* content_base,
-                     const uint32_t* owner_of, char* ts, size_t stride, uint64_t* content_off, uint8_t* content,
-                     uint32_t* owner) {
+int evm_pb_scan_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n, evm_pb_sync* info,
+                    int32_t* status) {
+  return evm_pb_scan_index_dev(ctx, kind, arena, off, n, info, status, nullptr);
+}
+
+int evm_pb_split_index_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n,
+                           const int32_t* status, const uint64_t* msg_base, const uint64_t* content_base,
+                           const uint32_t* owner_of, char* ts, size_t stride, uint64_t* content_off, uint8_t* content,
+                           uint32_t* owner, const uint64_t* slots) {
   if (!ctx || (n && (!arena || !off || !status || !msg_base || !content_base || !ts || !content_off || !content)) ||
       stride < 48 || stride % 16 || (kind != EVM_PB_SYNC_REQUEST && kind != EVM_PB_SYNC_RESPONSE))
     return EVM_EINVAL;
@@ -1088,16 +1157,23 @@ int evm_pb_split_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_
     if ((st = land_words(ctx, l))) return st;
   }
   u32* bad = S.alloc<u32>(1);
-  u64* mat = S.alloc<u64>(N + 1);
-  u32* mlen = S.alloc<u32>(N + 1);
   u64* cat = S.alloc<u64>(N + 1);
   u64* clen = S.alloc<u64>(N + 1);
-  if (!bad || !mat || !mlen || !cat || !clen) return EVM_ENOMEM;
+  if (!bad || !cat || !clen) return EVM_ENOMEM;
   HIPR(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
-  KLAUNCH(k_pb_offsets, dim3(grid_for(n, 64, 1 << 16)), dim3(64), kind, arena, (const u64*)off, n, status,
-          (const u64*)msg_base, owner_of, mat, mlen, owner, bad);
-  if (N) KLAUNCH(k_pb_rows, dim3(grid_for(N, 256, 1 << 16)), dim3(256), arena, (const u64*)mat, (const u32*)mlen, N, ts,
-                 (u64)stride, cat, clen);
+  if (slots) {
+    KLAUNCH(k_pb_rows_idx, dim3(grid_for(n, 4, 1 << 16)), dim3(256), arena, (const u64*)off, n, status,
+            (const u64*)msg_base, (const u64*)slots, owner_of, ts, (u64)stride, cat, clen, owner, bad);
+  } else {
+    u64* mat = S.alloc<u64>(N + 1);
+    u32* mlen = S.alloc<u32>(N + 1);
+    if (!mat || !mlen) return EVM_ENOMEM;
+    KLAUNCH(k_pb_offsets, dim3(grid_for(n, 64, 1 << 16)), dim3(64), kind, arena, (const u64*)off, n, status,
+            (const u64*)msg_base, owner_of, mat, mlen, owner, bad);
+    if (N)
+      KLAUNCH(k_pb_rows, dim3(grid_for(N, 256, 1 << 16)), dim3(256), arena, (const u64*)mat, (const u32*)mlen, N, ts,
+              (u64)stride, cat, clen);
+  }
   u64* co = reinterpret_cast<u64*>(content_off);
   if ((st = scan_exclusive<u64, OpAdd>(ctx, S, clen, N, co, co + N))) return st;
   if (N) KLAUNCH(k_pb_content, dim3(grid_for(N, 256, 1 << 16)), dim3(256), arena, (const u64*)cat, (const u64*)co, N,
@@ -1109,6 +1185,14 @@ int evm_pb_split_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_
     if ((st = land_words(ctx, l))) return st;
   }
   return hb ? EVM_EINVAL : EVM_OK;
+}
+
+int evm_pb_split_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n,
+                     const int32_t* status, const uint64_t* msg_base, const uint64_t* content_base,
+                     const uint32_t* owner_of, char* ts, size_t stride, uint64_t* content_off, uint8_t* content,
+                     uint32_t* owner) {
+  return evm_pb_split_index_dev(ctx, kind, arena, off, n, status, msg_base, content_base, owner_of, ts, stride,
+                                content_off, content, owner, nullptr);
 }
 
 int evm_gather_spans_dev(evm_ctx* ctx, const uint8_t* src, const uint64_t* src_off, const uint64_t* len,

@@ -244,8 +244,8 @@ class SyncServer:
     def sync_device(self, arena, off) -> "DeviceResponses":
         """sync() of bodies resident in device memory: arena (uint8 tensor on
         the engine's GPU), off (host uint64 [n + 1]).  The round runs on the
-        device end to end -- bodies decoded where they lie (evm_pb_scan_dev /
-        split_dev), one evm_server_ingest_ex, the client trees parsed there
+        device end to end -- bodies decoded where they lie (evm_pb_scan_index_dev /
+        split_index_dev), one evm_server_ingest_ex, the client trees parsed there
         (evm_tree_from_json_dev), one selection, the responses built in device
         memory (evm_pb_encode_responses_dev, each tree's JSON emitted straight
         into its response) -- and answers a DeviceResponses.  Only the round's
@@ -275,7 +275,9 @@ class SyncServer:
         off_d = torch.from_numpy(off.view(np.int64)).to(dev)
         info_d = torch.empty((n, 9), dtype=torch.int64, device=dev)
         st_d = torch.empty(n, dtype=torch.int32, device=dev)
-        check(lib.evm_pb_scan_dev(eng.h, REQUEST_KIND, P(arena), P(off_d), n, P(info_d), P(st_d)), "evm_pb_scan_dev")
+        slots_d = torch.empty(int(off[-1]) // 50 + 1, dtype=torch.int64, device=dev)  # (each message's place: the split reads it)
+        check(lib.evm_pb_scan_index_dev(eng.h, REQUEST_KIND, P(arena), P(off_d), n, P(info_d), P(st_d), P(slots_d)),
+              "evm_pb_scan_index_dev")
         inf = info_d.cpu().numpy().view(np.uint64)
         st = st_d.cpu().numpy()
         if st.any() or inf[:, 8].any() or (inf[:, 5] != 16).any() or self.detached or self.lenient:
@@ -330,8 +332,10 @@ class SyncServer:
         owner = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
         slot_d = torch.from_numpy(slots.astype(np.int32)).to(dev)
         mb_d, cb_d = up(msg_base), up(con_base)  # (held: the kernels read them after P() returns)
-        check(lib.evm_pb_split_dev(eng.h, REQUEST_KIND, P(arena), P(off_d), n, P(st_d), P(mb_d), P(cb_d), P(slot_d),
-                                   P(ts), 48, P(coff), P(content), P(owner)), "evm_pb_split_dev")
+        check(lib.evm_pb_split_index_dev(eng.h, REQUEST_KIND, P(arena), P(off_d), n, P(st_d), P(mb_d), P(cb_d),
+                                         P(slot_d), P(ts), 48, P(coff), P(content), P(owner), P(slots_d)),
+              "evm_pb_split_index_dev")
+        del slots_d
         T["decode"] += time.perf_counter() - t0
         t0 = time.perf_counter()
         bad = np.zeros(n, dtype=bool)

@@ -439,6 +439,19 @@ int evm_pb_split_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_
                      const int32_t* status, const uint64_t* msg_base, const uint64_t* content_base,
                      const uint32_t* owner_of, char* ts, size_t stride, uint64_t* content_off, uint8_t* content,
                      uint32_t* owner);
+/* The same two steps sharing the scan's walk: scan_index also records where
+ * each message's field starts, body k's i-th message at slots[off[k] / 50 + i]
+ * (slots: off[n] / 50 + 1 entries; a message whose timestamp is 46 bytes takes
+ * >= 50, so the bodies' ranges do not overlap), and split_index reads them
+ * instead of walking the bodies again (a body whose messages do not fit its
+ * range -- a shorter timestamp -- fails the split with EVM_EINVAL: the caller
+ * takes only bodies whose evm_pb_sync.nonstd_ts is 0). */
+int evm_pb_scan_index_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n,
+                          evm_pb_sync* info, int32_t* status, uint64_t* slots);
+int evm_pb_split_index_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const uint64_t* off, uint32_t n,
+                           const int32_t* status, const uint64_t* msg_base, const uint64_t* content_base,
+                           const uint32_t* owner_of, char* ts, size_t stride, uint64_t* content_off, uint8_t* content,
+                           uint32_t* owner, const uint64_t* slots);
 int evm_gather_spans_dev(evm_ctx* ctx, const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
                          const uint64_t* dst_off, uint32_t n, uint8_t* dst);
 /* evm_tree_from_json for n_owners texts json[at[o] .. at[o] + len[o]) (len 0:

@@ -93,6 +93,56 @@ def test_scan_and_split_equal_the_host_codec(eng):
     assert (dco.cpu().numpy().view(np.uint64) == hco).all()
     assert (dc.cpu().numpy()[:CB] == hc[:CB]).all()
     assert (down.cpu().numpy()[:N] == np.repeat(np.arange(n) + 7, hi[:, 0].astype(np.int64))).all()
+    # the indexed pair: the scan records each message's place, the split reads it
+    # (bodies whose timestamps are all 46 bytes; body 18's is not: left out here)
+    slots = torch.full((int(off[-1]) // 50 + 1,), -1, dtype=torch.int64, device=a_d.device)
+    info2 = torch.empty_like(info_d)
+    st2 = torch.empty_like(st_d)
+    L.check(lib.evm_pb_scan_index_dev(eng.h, L.PB_SYNC_REQUEST, _P(a_d), _P(off_d), n, _P(info2), _P(st2), _P(slots)),
+            "scan_index_dev")
+    assert (st2.cpu().numpy() == hst).all() and (info2.cpu().numpy().view(np.uint64) == hi).all()
+    sl = slots.cpu().numpy()
+    for k in np.flatnonzero((hst == 0) & (hi[:, 8] == 0)):
+        at = sl[int(off[k]) // 50: int(off[k]) // 50 + int(hi[k, 0])]
+        assert (at >= int(off[k])).all() and (at < int(off[k + 1])).all() and (np.diff(at) > 0).all()
+        assert (arena[at] == 0x0A).all()  # (field 1, length-delimited)
+    hx = hst.copy()
+    hx[18] = 1
+    ix = hi.copy()
+    ix[18] = 0
+    mb = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(ix[:, 0], out=mb[1:])
+    cb = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(ix[:, 1], out=cb[1:])
+    N, CB = int(mb[-1]), int(cb[-1])
+    hts = np.zeros((max(N, 1), 48), dtype=np.uint8)
+    hco = np.zeros(N + 1, dtype=np.uint64)
+    hc = np.zeros(max(CB, 1), dtype=np.uint8)
+    L.check(lib.evm_pb_split_batch(L.PB_SYNC_REQUEST, p(arena), p(off), n, p(hx), p(mb), p(cb), p(hts), 48, None, None,
+                                   p(hco), p(hc)), "split")
+    dts = torch.zeros((max(N, 1), 64), dtype=torch.uint8, device=a_d.device)
+    dco = torch.zeros(N + 1, dtype=torch.int64, device=a_d.device)
+    dc = torch.zeros(max(CB, 1), dtype=torch.uint8, device=a_d.device)
+    down = torch.zeros(max(N, 1), dtype=torch.int32, device=a_d.device)
+    hx_d = eng.dev(hx)
+    mb_d, cb_d = eng.dev(mb.view(np.int64)), eng.dev(cb.view(np.int64))
+    L.check(lib.evm_pb_split_index_dev(eng.h, L.PB_SYNC_REQUEST, _P(a_d), _P(off_d), n, _P(hx_d), _P(mb_d), _P(cb_d),
+                                       _P(own_of), _P(dts), 64, _P(dco), _P(dc), _P(down), _P(slots)), "split_index_dev")
+    assert (dts.cpu().numpy()[:N, :48] == hts[:N]).all() and not dts.cpu().numpy()[:N, 48:].any()
+    assert (dco.cpu().numpy().view(np.uint64) == hco).all()
+    assert (dc.cpu().numpy()[:CB] == hc[:CB]).all()
+    assert (down.cpu().numpy()[:N] == np.repeat(np.arange(n) + 7, ix[:, 0].astype(np.int64))).all()
+    # a body whose messages do not fit its slots (the shorter timestamp, body 18 kept): refused
+    if hi[18, 0] > (int(off[19]) // 50 - int(off[18]) // 50):
+        mbf = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(hi[:, 0], out=mbf[1:])
+        mbf_d = eng.dev(mbf.view(np.int64))
+        dts = torch.zeros((int(mbf[-1]), 64), dtype=torch.uint8, device=a_d.device)
+        dco = torch.zeros(int(mbf[-1]) + 1, dtype=torch.int64, device=a_d.device)
+        dc = torch.zeros(int(hi[:, 1].sum()) + 1, dtype=torch.uint8, device=a_d.device)
+        with pytest.raises(L.EngineError):
+            L.check(lib.evm_pb_split_index_dev(eng.h, L.PB_SYNC_REQUEST, _P(a_d), _P(off_d), n, _P(st_d), _P(mbf_d),
+                                               _P(cb_d), None, _P(dts), 64, _P(dco), _P(dc), None, _P(slots)), "split")
 
 
 def _tree_texts():
