@@ -41,7 +41,7 @@ namespace {
 
 constexpr int JW = 64;                 // leaves per chunk: one wave
 constexpr int JW_WAVES = 4;            // waves (chunks) per workgroup
-constexpr u32 JW_STAGE = 8 * 1024;     // bytes of a chunk's text staged in LDS
+constexpr u32 JW_STAGE = 8 * 1024;     // bytes of a chunk's text staged in LDS (after the destination's offset mod 16)
 constexpr u64 CODE_MASK = (1ull << 40) - 1;
 
 struct TreeJ {  // the tree as the kernels read it (gapped or compact: owner o's leaves [off[o], end[o]))
@@ -62,14 +62,10 @@ __device__ __forceinline__ int code_lcp(u64 a, u64 b) {  // common leading digit
 __device__ __forceinline__ u64 code_prefix(u64 c, int d) {  // the first d digits of c
   return d >= CODE_DIGITS ? c : c & ~((1ull << (2 * (CODE_DIGITS - d))) - 1ull);
 }
-__device__ __forceinline__ u32 dec_len(int32_t v) {
-  u32 x = v < 0 ? 0u - (u32)v : (u32)v;
-  u32 n = 1;
-  while (x >= 10u) {
-    x /= 10u;
-    ++n;
-  }
-  return n + (v < 0 ? 1u : 0u);
+__device__ __forceinline__ u32 dec_len(int32_t v) {  // (compares, not a division loop)
+  const u32 x = v < 0 ? 0u - (u32)v : (u32)v;
+  return 1u + (x >= 10u) + (x >= 100u) + (x >= 1000u) + (x >= 10000u) + (x >= 100000u) + (x >= 1000000u) +
+         (x >= 10000000u) + (x >= 100000000u) + (x >= 1000000000u) + (v < 0 ? 1u : 0u);
 }
 // the root's tail after the last leaf: `,"hash":R}`
 __device__ __forceinline__ u32 root_tail_len(int32_t r) { return 9u + dec_len(r); }
@@ -264,7 +260,7 @@ __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_emit(TreeJ t, const u32* _
                                                            const u64* __restrict__ cpos, const u64* __restrict__ off,
                                                            char* __restrict__ out) {
   __shared__ WaveLds lds[JW_WAVES];
-  __shared__ unsigned char stage[JW_WAVES][JW_STAGE];
+  __shared__ __attribute__((aligned(16))) unsigned char stage[JW_WAVES][JW_STAGE + 16];
   const u32 wv = threadIdx.x / JW, lane = threadIdx.x & 63;
   WaveLds* w = &lds[wv];
   unsigned char* sg = stage[wv];
@@ -300,25 +296,27 @@ __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_emit(TreeJ t, const u32* _
       put(q + 8 + len, '}');
     };
     if (total <= JW_STAGE) {
-      leaf_piece(w, ln, [&](u32 k, char b) { sg[pos + k] = (unsigned char)b; });
+      // staged at the destination's offset mod 16: the copy out is whole 16-B
+      // LDS reads and stores between the ends
+      const u32 s0 = (u32)((uintptr_t)dst & 15u);
+      unsigned char* sgo = sg + s0;
+      leaf_piece(w, ln, [&](u32 k, char b) { sgo[pos + k] = (unsigned char)b; });
       if (lane == 0) {
-        if (head) sg[0] = '{';
-        if (last) tail([&](u32 k, char b) { sg[k] = (unsigned char)b; });
+        if (head) sgo[0] = '{';
+        if (last) tail([&](u32 k, char b) { sgo[k] = (unsigned char)b; });
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // copy out: 4-B stores from the first 4-B aligned byte, single bytes at the ends
-      const u32 h0 = std::min<u32>(total, (u32)((4u - ((uintptr_t)dst & 3u)) & 3u));
-      if (lane < h0) dst[lane] = (char)sg[lane];
-      const u32 words = (total - h0) >> 2;
-      u32* dw = reinterpret_cast<u32*>(dst + h0);
-      for (u32 q = lane; q < words; q += JW) {
-        const u32 b = h0 + 4u * q;
-        dw[q] = (u32)sg[b] | ((u32)sg[b + 1] << 8) | ((u32)sg[b + 2] << 16) | ((u32)sg[b + 3] << 24);
-      }
-      const u32 t0 = h0 + 4u * words;
-      if (lane < total - t0) dst[t0 + lane] = (char)sg[t0 + lane];
+      char* d16 = dst - s0;  // 16-B aligned
+      const u32 end = s0 + total;
+      const u32 first = std::min<u32>(end, 16u);  // bytes [s0, first) of the first 16
+      if (lane >= s0 && lane < first) d16[lane] = (char)sg[lane];
+      const u32 full = end >> 4;  // 16-B blocks [1, full) whole; the last block's bytes below `end`
+      for (u32 q = 1 + lane; q < full; q += JW)
+        reinterpret_cast<uint4*>(d16)[q] = reinterpret_cast<const uint4*>(sg)[q];
+      const u32 t0 = std::max<u32>(16u, full << 4);
+      if (t0 + lane < end) d16[t0 + lane] = (char)sg[t0 + lane];
     } else {  // (a chunk of very deep, sparse leaves: its bytes straight out)
       leaf_piece(w, ln, [&](u32 k, char b) { dst[pos + k] = b; });
       if (lane == 0) {
