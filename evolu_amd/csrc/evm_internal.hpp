@@ -374,9 +374,7 @@ int tree_compact(evm_ctx* ctx, const evm_tree* t);
 // *bad |= 1 for an owner out of range) and the plan the emit follows (arrays
 // in S); the texts written at out + off[j]
 struct JsonPlan {
-  uint64_t* cbase = nullptr;
-  uint64_t* cpos = nullptr;
-  uint64_t nchunks = 0;
+  uint32_t n = 0;  // (the texts are placed by the caller from the lengths)
 };
 int json_plan(evm_ctx* ctx, Scratch& S, const evm_tree* t, const uint32_t* owners, uint32_t n, uint64_t* len,
               uint32_t* bad, JsonPlan* plan);

@@ -18,14 +18,13 @@
 // node's last leaf) ^ before the node's first leaf, which is the last leaf j
 // <= i that opened a node at that depth (cp_j < d).
 //
-// Work unit: a chunk of 64 leaves, one wave, one leaf per lane.  The node
-// starts come from 20 ballots (lane j: cp_j < d) -- the last opener at or
-// below a lane -- and, for nodes opened before the chunk, from one search per
-// depth for the chunk's first leaf (20 lanes, once per chunk) instead of a
-// search per closed node.  k_jp_len sums each chunk's text; after a scan of
-// the chunk lengths (every chunk's place) k_jp_emit writes each chunk's
-// pieces into LDS and copies them out (a chunk too long for the stage writes
-// its bytes directly).
+// Work unit: a wave per requested owner, its leaves 64 at a time (a chunk,
+// one leaf per lane).  The node starts come from 20 ballots (lane j: cp_j <
+// d) -- the last opener at or below a lane -- and, for nodes opened before
+// the chunk, from the owner's previous chunks: their last opener per depth,
+// carried in LDS.  k_jp_len sums each owner's text; after the caller's scan
+// of the lengths k_jp_emit writes each chunk's pieces into LDS and copies
+// them out (a chunk too long for the stage writes its bytes directly).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -79,13 +78,8 @@ struct Chunk {
   int32_t p0; // pfx at the owner's first leaf (a compact tree's prefix is global)
   bool in;    // owner in range
 };
-__device__ __forceinline__ Chunk chunk_of(const TreeJ& t, const u32* owners, const u64* cbase, u32 n, u64 c) {
-  u32 lo = 0, hi = n;  // the last j with cbase[j] <= c
-  while (lo < hi) {
-    const u32 mid = (lo + hi) >> 1;
-    if (cbase[mid + 1] <= c) lo = mid + 1;
-    else hi = mid;
-  }
+__device__ __forceinline__ Chunk chunk_of(const TreeJ& t, const u32* owners, const u64* cbase, const u32* cj, u64 c) {
+  const u32 lo = cj[c];  // (the request whose chunks hold c: k_jp_chunk_req)
   Chunk ch;
   ch.j = lo;
   const u32 o = owners ? owners[lo] : lo;
@@ -139,23 +133,25 @@ __device__ __forceinline__ Lane chunk_setup(const TreeJ& t, const Chunk& ch, Wav
     const u64 m = __ballot(ln.valid && ln.cp < d);
     if (ln.l == 0) w->opener[d] = m;
   }
-  // nodes open before the chunk: their first leaf, one search per depth
-  const u64 cf = __shfl(ln.c, 0, 64);
-  if (ln.l < CODE_DIGITS && ch.k > 0) {
-    const int d = (int)ln.l + 1;
-    const u64 x = code_prefix(cf, d);
-    u32 lo = 0, hi = ch.k * JW;
-    while (lo < hi) {
-      const u32 mid = (lo + hi) >> 1;
-      if ((t.ck[base + mid] & CODE_MASK) < x) lo = mid + 1;
-      else hi = mid;
-    }
-    w->carry[d] = t.pfx[base + lo] ^ ch.p0;
-  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return ln;
+}
+
+// After a chunk: the start of each depth's node open at its end (its last
+// opener at that depth, else the node open before it) for the owner's next chunk.
+__device__ __forceinline__ void chunk_carry(WaveLds* w, u32 lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();  // (the chunk's reads of carry first)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane < CODE_DIGITS) {
+    const u64 m = w->opener[lane + 1];
+    if (m) w->carry[lane + 1] = w->p[63 - __clzll(m)];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // the prefix before the first leaf of leaf ln's node at depth d
@@ -214,118 +210,115 @@ __device__ __forceinline__ u32 wave_excl_sum(u32 v, u32* total) {
   return x - v;
 }
 
-// chunks per requested owner (an empty or out-of-range owner: one, its `{}`)
-__global__ void k_jp_chunks(TreeJ t, const u32* __restrict__ owners, u32 n, u64* __restrict__ nch,
-                            u32* __restrict__ bad) {
-  for (u32 j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    const u32 o = owners ? owners[j] : j;
-    if (o >= t.n_owners) atomicOr(bad, 1u);
-    const u64 L = o < t.n_owners ? t.end[o] - t.off[o] : 0;
-    nch[j] = L ? (L + JW - 1) / JW : 1;
-  }
-}
-
-// the text of a chunk: `{` before the owner's first piece, its pieces, the
-// root's tail after the last (an empty tree: `{}`)
+// A wave per requested owner, its chunks in order (the node starts carried
+// from chunk to chunk in LDS).  k_jp_len: each owner's text length (an empty
+// or out-of-range owner: `{}`, the latter flagged in *bad).
 __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_len(TreeJ t, const u32* __restrict__ owners, u32 n,
-                                                          const u64* __restrict__ cbase, u64 nchunks,
-                                                          u64* __restrict__ clen) {
+                                                          u64* __restrict__ len, u32* __restrict__ bad) {
   __shared__ WaveLds lds[JW_WAVES];
   WaveLds* w = &lds[threadIdx.x / JW];
-  for (u64 c = (u64)blockIdx.x * JW_WAVES + threadIdx.x / JW; c < nchunks; c += (u64)gridDim.x * JW_WAVES) {
-    const Chunk ch = chunk_of(t, owners, cbase, n, c);
-    if (ch.L == 0) {
-      if ((threadIdx.x & 63) == 0) clen[c] = 2;
+  const u32 lane = threadIdx.x & 63;
+  for (u32 j = blockIdx.x * JW_WAVES + threadIdx.x / JW; j < n; j += gridDim.x * JW_WAVES) {
+    const u32 o = owners ? owners[j] : j;
+    if (o >= t.n_owners && lane == 0) atomicOr(bad, 1u);
+    const u64 a = o < t.n_owners ? t.off[o] : 0;
+    const u32 L = o < t.n_owners ? (u32)(t.end[o] - a) : 0u;
+    if (L == 0) {
+      if (lane == 0) len[j] = 2;
       continue;
     }
-    const Lane ln = chunk_setup(t, ch, w);
-    u32 tot;
-    wave_excl_sum(leaf_piece(w, ln, [](u32, char) {}), &tot);
-    if (ln.l == 0) {
-      const bool last = (u64)(ch.k + 1) * JW >= ch.L;
-      clen[c] = tot + (ch.k == 0 ? 1u : 0u) + (last ? root_tail_len(t.pfx[ch.a + ch.L] ^ ch.p0) : 0u);
+    const int32_t p0 = t.pfx[a];
+    u64 total = 1;
+    for (u32 k = 0; (u64)k * JW < L; ++k) {
+      const Chunk ch{j, L, a, k, p0, true};
+      const Lane ln = chunk_setup(t, ch, w);
+      u32 tot;
+      wave_excl_sum(leaf_piece(w, ln, [](u32, char) {}), &tot);
+      total += tot;
+      chunk_carry(w, lane);
     }
-    __builtin_amdgcn_wave_barrier();  // (the wave's LDS is rewritten by its next chunk)
+    if (lane == 0) len[j] = total + root_tail_len(t.pfx[a + L] ^ p0);
   }
 }
 
-__global__ void k_jp_owner_len(u32 n, const u64* __restrict__ cbase, const u64* __restrict__ cpos,
-                               u64* __restrict__ len) {
-  for (u32 j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
-    len[j] = cpos[cbase[j + 1]] - cpos[cbase[j]];
-}
-
+// k_jp_emit: owner j's text at out + off[j], a chunk at a time (staged in LDS)
 __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_emit(TreeJ t, const u32* __restrict__ owners, u32 n,
-                                                           const u64* __restrict__ cbase, u64 nchunks,
-                                                           const u64* __restrict__ cpos, const u64* __restrict__ off,
-                                                           char* __restrict__ out) {
+                                                           const u64* __restrict__ off, char* __restrict__ out) {
   __shared__ WaveLds lds[JW_WAVES];
   __shared__ __attribute__((aligned(16))) unsigned char stage[JW_WAVES][JW_STAGE + 16];
   const u32 wv = threadIdx.x / JW, lane = threadIdx.x & 63;
   WaveLds* w = &lds[wv];
   unsigned char* sg = stage[wv];
-  for (u64 c = (u64)blockIdx.x * JW_WAVES + wv; c < nchunks; c += (u64)gridDim.x * JW_WAVES) {
-    const Chunk ch = chunk_of(t, owners, cbase, n, c);
-    char* dst = out + off[ch.j] + (cpos[c] - cpos[cbase[ch.j]]);
-    if (ch.L == 0) {
+  for (u32 j = blockIdx.x * JW_WAVES + wv; j < n; j += gridDim.x * JW_WAVES) {
+    const u32 o = owners ? owners[j] : j;
+    const u64 a = o < t.n_owners ? t.off[o] : 0;
+    const u32 L = o < t.n_owners ? (u32)(t.end[o] - a) : 0u;
+    char* dst0 = out + off[j];
+    if (L == 0) {
       if (lane == 0) {
-        dst[0] = '{';
-        dst[1] = '}';
+        dst0[0] = '{';
+        dst0[1] = '}';
       }
       continue;
     }
-    const Lane ln = chunk_setup(t, ch, w);
-    const u32 my = leaf_piece(w, ln, [](u32, char) {});
-    u32 tot;
-    const u32 head = ch.k == 0 ? 1u : 0u;
-    const u32 pos = head + wave_excl_sum(my, &tot);
-    const bool last = (u64)(ch.k + 1) * JW >= ch.L;
-    const int32_t R = last ? (t.pfx[ch.a + ch.L] ^ ch.p0) : 0;
-    const u32 total = head + tot + (last ? root_tail_len(R) : 0u);
-    auto tail = [&](auto put) {  // `,"hash":R}` at head + tot
-      const char* h = ",\"hash\":";
-      u32 q = head + tot;
-      for (int k = 0; k < 8; ++k) put(q + k, h[k]);
-      const u32 len = dec_len(R);
-      u32 x = R < 0 ? 0u - (u32)R : (u32)R;
-      for (u32 k = len; k-- > (R < 0 ? 1u : 0u);) {
-        put(q + 8 + k, (char)('0' + x % 10u));
-        x /= 10u;
+    const int32_t p0 = t.pfx[a];
+    u64 run = 0;  // the owner's bytes written
+    for (u32 k = 0; (u64)k * JW < L; ++k) {
+      const Chunk ch{j, L, a, k, p0, true};
+      char* dst = dst0 + run;
+      const Lane ln = chunk_setup(t, ch, w);
+      const u32 my = leaf_piece(w, ln, [](u32, char) {});
+      u32 tot;
+      const u32 head = ch.k == 0 ? 1u : 0u;
+      const u32 pos = head + wave_excl_sum(my, &tot);
+      const bool last = (u64)(ch.k + 1) * JW >= ch.L;
+      const int32_t R = last ? (t.pfx[ch.a + ch.L] ^ ch.p0) : 0;
+      const u32 total = head + tot + (last ? root_tail_len(R) : 0u);
+      auto tail = [&](auto put) {  // `,"hash":R}` at head + tot
+        const char* h = ",\"hash\":";
+        u32 q = head + tot;
+        for (int k = 0; k < 8; ++k) put(q + k, h[k]);
+        const u32 len = dec_len(R);
+        u32 x = R < 0 ? 0u - (u32)R : (u32)R;
+        for (u32 k = len; k-- > (R < 0 ? 1u : 0u);) {
+          put(q + 8 + k, (char)('0' + x % 10u));
+          x /= 10u;
+        }
+        if (R < 0) put(q + 8, '-');
+        put(q + 8 + len, '}');
+      };
+      if (total <= JW_STAGE) {
+        // staged at the destination's offset mod 16: the copy out is whole 16-B
+        // LDS reads and stores between the ends
+        const u32 s0 = (u32)((uintptr_t)dst & 15u);
+        unsigned char* sgo = sg + s0;
+        leaf_piece(w, ln, [&](u32 k, char b) { sgo[pos + k] = (unsigned char)b; });
+        if (lane == 0) {
+          if (head) sgo[0] = '{';
+          if (last) tail([&](u32 k, char b) { sgo[k] = (unsigned char)b; });
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        char* d16 = dst - s0;  // 16-B aligned
+        const u32 end = s0 + total;
+        const u32 first = std::min<u32>(end, 16u);  // bytes [s0, first) of the first 16
+        if (lane >= s0 && lane < first) d16[lane] = (char)sg[lane];
+        const u32 full = end >> 4;  // 16-B blocks [1, full) whole; the last block's bytes below `end`
+        for (u32 q = 1 + lane; q < full; q += JW)
+          reinterpret_cast<uint4*>(d16)[q] = reinterpret_cast<const uint4*>(sg)[q];
+        const u32 t0 = std::max<u32>(16u, full << 4);
+        if (t0 + lane < end) d16[t0 + lane] = (char)sg[t0 + lane];
+      } else {  // (a chunk of very deep, sparse leaves: its bytes straight out)
+        leaf_piece(w, ln, [&](u32 k, char b) { dst[pos + k] = b; });
+        if (lane == 0) {
+          if (head) dst[0] = '{';
+          if (last) tail([&](u32 k, char b) { dst[k] = b; });
+        }
       }
-      if (R < 0) put(q + 8, '-');
-      put(q + 8 + len, '}');
-    };
-    if (total <= JW_STAGE) {
-      // staged at the destination's offset mod 16: the copy out is whole 16-B
-      // LDS reads and stores between the ends
-      const u32 s0 = (u32)((uintptr_t)dst & 15u);
-      unsigned char* sgo = sg + s0;
-      leaf_piece(w, ln, [&](u32 k, char b) { sgo[pos + k] = (unsigned char)b; });
-      if (lane == 0) {
-        if (head) sgo[0] = '{';
-        if (last) tail([&](u32 k, char b) { sgo[k] = (unsigned char)b; });
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      char* d16 = dst - s0;  // 16-B aligned
-      const u32 end = s0 + total;
-      const u32 first = std::min<u32>(end, 16u);  // bytes [s0, first) of the first 16
-      if (lane >= s0 && lane < first) d16[lane] = (char)sg[lane];
-      const u32 full = end >> 4;  // 16-B blocks [1, full) whole; the last block's bytes below `end`
-      for (u32 q = 1 + lane; q < full; q += JW)
-        reinterpret_cast<uint4*>(d16)[q] = reinterpret_cast<const uint4*>(sg)[q];
-      const u32 t0 = std::max<u32>(16u, full << 4);
-      if (t0 + lane < end) d16[t0 + lane] = (char)sg[t0 + lane];
-    } else {  // (a chunk of very deep, sparse leaves: its bytes straight out)
-      leaf_piece(w, ln, [&](u32 k, char b) { dst[pos + k] = b; });
-      if (lane == 0) {
-        if (head) dst[0] = '{';
-        if (last) tail([&](u32 k, char b) { dst[k] = b; });
-      }
+      run += total;
+      chunk_carry(w, lane);  // (also: the stage is rewritten by the next chunk)
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();  // (the stage and the wave's LDS are rewritten by its next chunk)
   }
 }
 
@@ -336,40 +329,20 @@ __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_emit(TreeJ t, const u32* _
 // each text straight into its response).  The plan's arrays live in S.
 int evm::json_plan(evm_ctx* ctx, Scratch& S, const evm_tree* t, const uint32_t* owners, uint32_t n, uint64_t* len,
                    uint32_t* bad, JsonPlan* plan) {
+  (void)S;
   const TreeJ tv{t->off, t->end, t->ck, t->pfx, t->n_owners};
-  u64* nch = S.alloc<u64>((size_t)n + 1);
-  u64* cbase = S.alloc<u64>((size_t)n + 1);
-  if (!nch || !cbase) return EVM_ENOMEM;
-  if (n) KLAUNCH(k_jp_chunks, dim3(grid_for(n, 256)), dim3(256), tv, owners, n, nch, bad);
-  int st = scan_exclusive<u64, OpAdd>(ctx, S, nch, n, cbase, cbase + n);
-  if (st) return st;
-  u64 nchunks = 0;
-  {
-    LandList l;
-    l.add(cbase + n, &nchunks, sizeof(u64));
-    if ((st = land_words(ctx, l))) return st;
-  }
-  u64* clen = S.alloc<u64>(nchunks + 1);
-  u64* cpos = S.alloc<u64>(nchunks + 1);
-  if (!clen || !cpos) return EVM_ENOMEM;
-  const u32 grid = (u32)std::min<u64>((nchunks + JW_WAVES - 1) / JW_WAVES, (u64)ctx->n_cu * 16);
-  if (nchunks)
-    KLAUNCH(k_jp_len, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (const u64*)cbase, nchunks,
-            clen);
-  if ((st = scan_exclusive<u64, OpAdd>(ctx, S, clen, nchunks, cpos, cpos + nchunks))) return st;
-  if (n) KLAUNCH(k_jp_owner_len, dim3(grid_for(n, 256)), dim3(256), n, (const u64*)cbase, (const u64*)cpos, (u64*)len);
-  plan->cbase = reinterpret_cast<uint64_t*>(cbase);
-  plan->cpos = reinterpret_cast<uint64_t*>(cpos);
-  plan->nchunks = nchunks;
+  const u32 grid = (u32)std::min<u64>((n + JW_WAVES - 1) / JW_WAVES, (u64)ctx->n_cu * 32);
+  if (n) KLAUNCH(k_jp_len, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (u64*)len, bad);
+  plan->n = n;
   return hip_ok(hipGetLastError());
 }
 int evm::json_emit(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, const JsonPlan& plan,
                    const uint64_t* off, char* out) {
+  (void)plan;
   const TreeJ tv{t->off, t->end, t->ck, t->pfx, t->n_owners};
-  const u32 grid = (u32)std::min<u64>((plan.nchunks + JW_WAVES - 1) / JW_WAVES, (u64)ctx->n_cu * 16);
-  if (plan.nchunks)
-    KLAUNCH(k_jp_emit, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (const u64*)plan.cbase,
-            (u64)plan.nchunks, (const u64*)plan.cpos, (const u64*)off, out);
+  const u32 grid = (u32)std::min<u64>((n + JW_WAVES - 1) / JW_WAVES, (u64)ctx->n_cu * 32);
+  if (n)
+    KLAUNCH(k_jp_emit, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (const u64*)off, out);
   return hip_ok(hipGetLastError());
 }
 
