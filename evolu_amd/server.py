@@ -163,7 +163,17 @@ class SyncServer:
         self.eng = eng
         self.store = eng.store_new(capacity)
         self.capacity = capacity
-        self.slot: Dict[str, int] = {}
+        self._slot_d: Dict[str, int] = {}
+        # the device rounds' userIds (sync_device): equal-length ASCII ids as
+        # 24-B keys by slot on the device, their 64-bit hashes sorted for the
+        # lookups; slots >= _host_upto are not in the host dict yet (`slot`
+        # adds them when a host path asks).  None: the device keys do not
+        # cover every slot -- the rounds map userIds through the host dict.
+        self._dkeys = None
+        self._dlen = 0
+        self._dhash = None
+        self._dslot = None
+        self._host_upto = 0
         self.next_id = 0
         # the message log, by id: segments of ids [base, base + n) -- the
         # timestamp rows (N, 48), content offsets (N + 1) and contents of a
@@ -180,13 +190,83 @@ class SyncServer:
     def close(self):
         self.store.free()
 
+    @property
+    def slot(self) -> Dict[str, int]:
+        """userId -> owner slot (every user seen so far)."""
+        if self._dkeys is not None and self._host_upto < self._dkeys.shape[0]:
+            S, L = self._dkeys.shape[0], self._dlen
+            b = self._dkeys[self._host_upto:, :L].cpu().numpy()
+            big = b.tobytes().decode("ascii")
+            self._slot_d.update(zip((big[i:i + L] for i in range(0, len(big), L)), range(self._host_upto, S)))
+            self._host_upto = S
+        return self._slot_d
+
+    @slot.setter
+    def slot(self, d: Dict[str, int]):
+        self._slot_d = d
+        self._dkeys = self._dhash = self._dslot = None
+        self._host_upto = len(d)
+
     def _slot(self, user: str) -> int:
-        s = self.slot.get(user)
+        d = self.slot
+        s = d.get(user)
         if s is None:
-            if len(self.slot) >= self.capacity:
+            if len(d) >= self.capacity:
                 raise _lib.EngineError(_lib.EVM_ECAPACITY, "SyncServer: more users than owner slots")
-            s = self.slot[user] = len(self.slot)
+            s = d[user] = len(d)
+            self._dkeys = self._dhash = self._dslot = None  # (a slot the device keys do not hold)
+            self._host_upto = len(d)
         return s
+
+    def _device_slots(self, packed, ulen: np.ndarray, n: int):
+        """The slots of a device round's users from the device keys: packed
+        (device uint8) holds the n userIds back to back.  -> int64 numpy
+        slots, or None when the host dict must decide (ids of several lengths,
+        longer than 24 bytes or not ASCII; a user twice; a hash shared by two
+        keys; the device keys not covering every slot)."""
+        import torch
+
+        L = int(ulen[0]) if n else 0
+        if not n or not 0 < L <= 24 or not (ulen == L).all():
+            return None
+        fresh = not self._slot_d and self._dkeys is None
+        if not fresh and (self._dkeys is None or self._dlen != L):
+            return None
+        dev = packed.device
+        k = packed[:n * L].view(n, L)
+        if bool((k >= 0x80).any()):
+            return None
+        keys = torch.zeros((n, 24), dtype=torch.uint8, device=dev)
+        keys[:, :L] = k
+        w = keys.view(torch.int64)  # (n, 3)
+        h = (w[:, 0] * -7046029254386353131) ^ (w[:, 1] * -4658895280553007687) ^ (w[:, 2] * 7640891576956012809)
+        if torch.unique(h).numel() != n:
+            return None  # (a user twice, or two of them sharing a hash: the host dict decides)
+        S = 0 if fresh else self._dkeys.shape[0]
+        if fresh:
+            found = torch.zeros(n, dtype=torch.bool, device=dev)
+            old = torch.zeros(n, dtype=torch.int64, device=dev)
+        else:
+            i = torch.searchsorted(self._dhash, h).clamp_(max=max(S - 1, 0))
+            hit = self._dhash[i] == h
+            old = self._dslot[i]
+            found = hit & (self._dkeys[old] == keys).all(1)
+            if bool((hit & ~found).any()):
+                return None  # (a hash shared by two keys)
+        new = ~found
+        n_new = int(new.sum())
+        if S + n_new > self.capacity:
+            raise _lib.EngineError(_lib.EVM_ECAPACITY, "SyncServer: more users than owner slots")
+        rank = torch.cumsum(new.to(torch.int64), 0) - 1 + S  # (new users: slots in request order)
+        slots = torch.where(found, old, rank)
+        if n_new:
+            nk = keys[new]
+            self._dkeys = nk if fresh else torch.cat([self._dkeys, nk])
+            hh = h[new] if fresh else torch.cat([self._dhash, h[new]])
+            ss = slots[new] if fresh else torch.cat([self._dslot, slots[new]])
+            order = torch.argsort(hh)
+            self._dhash, self._dslot, self._dlen = hh[order], ss[order], L
+        return slots.cpu().numpy()
 
     def _log(self, base: int, ts, coff, content, rowmap=None):
         self._base.append(base)
@@ -293,14 +373,18 @@ class SyncServer:
         src_d, len_d, dst_d = up(src), up(lens), up(dst[:-1])
         check(lib.evm_gather_spans_dev(eng.h, P(arena), P(src_d), P(len_d), P(dst_d), 2 * n, P(packed)),
               "evm_gather_spans_dev")
-        pk = packed.cpu().numpy()
         ub = int(dst[n])
-        nodes16 = pk[ub:ub + 16 * n].reshape(n, 16)
-        if not np.isin(nodes16, np.frombuffer(b"0123456789abcdefABCDEF", dtype=np.uint8)).all():
+        nodes_d = packed[ub:ub + 16 * n].view(n, 16)
+        hexd = torch.zeros(256, dtype=torch.bool, device=dev)
+        hexd[torch.frombuffer(bytearray(b"0123456789abcdefABCDEF"), dtype=torch.uint8).to(dev).long()] = True
+        if not bool(hexd[nodes_d.long()].all()):
             return self._device_fallback(arena, off, T, t_call)
         t1 = time.perf_counter()
-        users = _decode_spans(pk[:ub], dst[:n + 1], ulen)
-        if not self.slot and n <= self.capacity:
+        slots = self._device_slots(packed, ulen, n)
+        if slots is not None:
+            pass  # (the device keys: no userId decoded on the host)
+        elif not self.slot and n <= self.capacity:
+            users = _decode_spans(packed[:ub].cpu().numpy(), dst[:n + 1], ulen)
             # a new server's first round: every user new, slots in request order
             self.slot = dict(zip(users, range(n)))
             if len(self.slot) != n:
@@ -308,6 +392,7 @@ class SyncServer:
                 return self._device_fallback(arena, off, T, t_call)  # (an owner twice: rounds)
             slots = np.arange(n, dtype=np.int64)
         else:
+            users = _decode_spans(packed[:ub].cpu().numpy(), dst[:n + 1], ulen)
             get = self.slot.get
             new = [u for u in users if get(u) is None]  # (new users take slots in request order)
             if new:
@@ -315,6 +400,7 @@ class SyncServer:
                 if len(self.slot) + len(new) > self.capacity:
                     raise _lib.EngineError(_lib.EVM_ECAPACITY, "SyncServer: more users than owner slots")
                 self.slot.update(zip(new, range(len(self.slot), len(self.slot) + len(new))))
+                self.slot = self._slot_d  # (slots the device keys do not hold)
             slots = np.fromiter(map(get, users), dtype=np.int64, count=n)
             if np.unique(slots).size != n:
                 return self._device_fallback(arena, off, T, t_call)  # (an owner twice: rounds)
@@ -325,7 +411,7 @@ class SyncServer:
         con_base = np.zeros(n + 1, dtype=np.uint64)
         np.cumsum(cbytes, out=con_base[1:])
         N, CB = int(msg_base[n]), int(con_base[n])
-        ts = torch.zeros((max(N, 1), 48), dtype=torch.uint8, device=dev)
+        ts = torch.empty((max(N, 1), 48), dtype=torch.uint8, device=dev)  # (every row written by the split)
         coff = torch.empty(N + 1, dtype=torch.int64, device=dev)
         coff[N] = CB
         content = torch.empty(max(CB, 1), dtype=torch.uint8, device=dev)
@@ -370,13 +456,13 @@ class SyncServer:
         if len(ans):
             t0 = time.perf_counter()
             sl = slots[ans]
-            node = np.full((O, 16), ord("0"), dtype=np.uint8)
-            node[sl] = nodes16[ans]
-            active = np.zeros(O, dtype=np.uint8)
-            active[sl] = 1
-            diff, soff, sid = self.store.select(client, eng.dev(node), eng.dev(active))
-            client.free()
             sl_d = torch.from_numpy(sl).to(dev)
+            node = torch.full((O, 16), ord("0"), dtype=torch.uint8, device=dev)
+            node[sl_d] = nodes_d[torch.from_numpy(ans).to(dev)]
+            active = torch.zeros(O, dtype=torch.uint8, device=dev)
+            active[sl_d] = 1
+            diff, soff, sid = self.store.select(client, node, active)
+            client.free()
             rng_err_d = (diff[sl_d] == _lib.DIFF_RANGE_ERROR).to(torch.uint8)
             T["select"] += time.perf_counter() - t0
             t0 = time.perf_counter()

@@ -3,7 +3,10 @@ the userId decode (the same strings the host path's per-body decode makes),
 the message log's segments moving between host and device tensors, and the
 DeviceResponses view."""
 import numpy as np
+import pytest
 import torch
+
+from evolu_amd import _lib as L
 
 from evolu_amd.server import DeviceResponses, RangeError, _decode_spans, _Seg
 
@@ -52,3 +55,49 @@ def test_device_responses_view():
     assert r.to_host() == [b"AAA", None, b"BBBB", b"CC"]
     r2 = DeviceResponses(buf, off, [True, err, True, True])
     assert r2.to_host()[1] is err and len(r2) == 4
+
+
+class _Srv:
+    """SyncServer's user-directory state without an engine (the method and the
+    property run on CPU tensors here)."""
+    def __init__(self, capacity=100):
+        from evolu_amd.server import SyncServer
+        self._slot_d, self._dkeys, self._dlen, self._dhash, self._dslot, self._host_upto = {}, None, 0, None, None, 0
+        self.capacity = capacity
+        self.cls = SyncServer
+
+    def slots(self, users):
+        b = b"".join(u.encode() for u in users)
+        packed = torch.from_numpy(np.frombuffer(b or b"\0", dtype=np.uint8).copy())
+        ulen = np.array([len(u.encode()) for u in users], dtype=np.uint64)
+        return self.cls._device_slots(self, packed, ulen, len(users))
+
+    @property
+    def slot(self):
+        from evolu_amd.server import SyncServer
+        return SyncServer.slot.fget(self)
+
+
+def test_device_user_directory_assigns_the_dict_paths_slots():
+    s = _Srv()
+    r1 = ["%021x" % k for k in (5, 3, 9, 1)]
+    assert s.slots(r1).tolist() == [0, 1, 2, 3]  # (a new server: request order)
+    r2 = ["%021x" % k for k in (7, 9, 11, 5)]
+    assert s.slots(r2).tolist() == [4, 2, 5, 0]  # (known users keep theirs; new ones in request order)
+    assert s._host_upto == 0
+    d = s.slot  # (the host dict, on demand)
+    assert d == {u: i for i, u in enumerate(r1 + ["%021x" % 7, "%021x" % 11])} and s._host_upto == 6
+    assert s.slots(["%021x" % 13]).tolist() == [6]
+    assert s.slot["%021x" % 13] == 6
+    # the host dict decides: a user twice, several lengths, non-ASCII, longer than 24 bytes
+    assert s.slots(["%021x" % 20, "%021x" % 20]) is None
+    assert s.slots(["%021x" % 21, "%020x" % 22]) is None
+    assert s.slots(["é" * 10 + "a"]) is None
+    assert _Srv().slots(["x" * 25]) is None
+    # ids of another length than the directory's: the host dict decides
+    assert s.slots(["%020x" % 23]) is None
+    # capacity
+    s2 = _Srv(capacity=2)
+    assert s2.slots(["a" * 21, "b" * 21]).tolist() == [0, 1]
+    with pytest.raises(L.EngineError):
+        s2.slots(["c" * 21])
