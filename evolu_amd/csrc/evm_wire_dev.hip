@@ -79,12 +79,49 @@ struct Win {
   }
 };
 
+// The same reads through a window in LDS: NC 16-B chunks per lane (a refill
+// issues NC independent loads -- a long walk takes a few messages per
+// refill; the per-lane windows 4*65*.. bytes apart so a wave's reads spread
+// over the banks).  The window lives at lds[lane * LW_STRIDE ..].
+constexpr int LW_NC = 16;
+constexpr u32 LW_STRIDE = LW_NC * 4 + 1;  // dwords per lane
+struct LWin {
+  u32* lds;
+  const uint8_t* w;
+  const uint8_t* lim;
+  __device__ __forceinline__ void init(const uint8_t* end, u32* mine) {
+    lim = reinterpret_cast<const uint8_t*>(((uintptr_t)end + 15) & ~(uintptr_t)15);
+    w = nullptr;
+    lds = mine;
+  }
+  __device__ __forceinline__ void refill(const uint8_t* p) {
+    w = reinterpret_cast<const uint8_t*>((uintptr_t)p & ~(uintptr_t)15);
+    uint4 v[LW_NC];
+#pragma unroll
+    for (int c = 0; c < LW_NC; ++c)
+      v[c] = w + 16 * c < lim ? *reinterpret_cast<const uint4*>(w + 16 * c) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int c = 0; c < LW_NC; ++c) {
+      lds[4 * c] = v[c].x;
+      lds[4 * c + 1] = v[c].y;
+      lds[4 * c + 2] = v[c].z;
+      lds[4 * c + 3] = v[c].w;
+    }
+  }
+  __device__ __forceinline__ uint8_t get(const uint8_t* p) {
+    if (p < w || p >= w + 16 * LW_NC) refill(p);
+    const u32 k = (u32)(p - w);
+    return (uint8_t)(lds[k >> 2] >> ((k & 3u) * 8u));
+  }
+};
+
 // evm_proto.cpp's Reader on device bytes (the same checks, in the same order)
-struct DReader {
+template <class W>
+struct DReaderT {
   const uint8_t* p;
   const uint8_t* e;
   bool ok;
-  Win* win;
+  W* win;
   __device__ __forceinline__ bool more() const { return ok && p < e; }
   __device__ __forceinline__ u64 varint() {
     u64 v = 0;
@@ -136,6 +173,8 @@ struct DReader {
   }
 };
 
+using DReader = DReaderT<Win>;
+
 struct DMsg {
   const uint8_t* ts;
   u64 ts_len;
@@ -143,8 +182,9 @@ struct DMsg {
   u64 content_len;
 };
 
-__device__ __forceinline__ bool d_read_msg(const uint8_t* q, u64 n, DMsg* m, Win* win) {
-  DReader r{q, q + n, true, win};
+template <class W>
+__device__ __forceinline__ bool d_read_msg(const uint8_t* q, u64 n, DMsg* m, W* win) {
+  DReaderT<W> r{q, q + n, true, win};
   *m = DMsg{nullptr, 0, nullptr, 0};
   while (r.more()) {
     const u64 tag = r.varint();
@@ -162,9 +202,9 @@ __device__ __forceinline__ bool d_read_msg(const uint8_t* q, u64 n, DMsg* m, Win
 }
 
 // evm_proto.cpp's walk(): on_msg(index, msg, its field's tag) per message
-template <typename F>
-__device__ __forceinline__ int d_walk(int kind, const uint8_t* buf, u64 len, evm_pb_sync* info, Win* win, F on_msg) {
-  DReader r{buf, buf + len, true, win};
+template <class W, typename F>
+__device__ __forceinline__ int d_walk(int kind, const uint8_t* buf, u64 len, evm_pb_sync* info, W* win, F on_msg) {
+  DReaderT<W> r{buf, buf + len, true, win};
   evm_pb_sync s{0, 0, 0, 0, 0, 0, 0, 0, 0};
   const u32 tree_field = kind == EVM_PB_SYNC_REQUEST ? 4u : 2u;
   while (r.more()) {
@@ -213,11 +253,12 @@ __device__ __forceinline__ int d_walk(int kind, const uint8_t* buf, u64 len, evm
 constexpr u64 PB_MIN_MSG = 50;
 __global__ void k_pb_scan(int kind, const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
                           evm_pb_sync* __restrict__ info, int32_t* __restrict__ status, u64* __restrict__ slots) {
+  __shared__ u32 lw[64 * LW_STRIDE];  // (a 64-thread block)
   for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
     const u64 a = off[k], b = off[k + 1];
     evm_pb_sync s{0, 0, 0, 0, 0, 0, 0, 0, 0};
-    Win win;
-    win.init(arena + b);
+    LWin win;
+    win.init(arena + b, lw + threadIdx.x * LW_STRIDE);
     const u64 s0 = a / PB_MIN_MSG, room = b / PB_MIN_MSG - s0;
     int st = b < a ? EVM_EINVAL : d_walk(kind, arena + a, b - a, &s, &win, [&](u64 i, const DMsg&, const uint8_t* at) {
       if (slots && i < room) slots[s0 + i] = (u64)(at - arena);
