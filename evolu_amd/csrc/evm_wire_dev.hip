@@ -464,7 +464,7 @@ struct JText {
 
 // The common text first: JSON.stringify's own form, `{` then tokens --
 // OPEN `"d":{` (a child, digits ascending), HASH `"hash":N}` (closes the
-// node; a `,` follows unless it is the root's) -- read a wave per tree, 1 KB
+// node; a `,` follows unless it is the root's) -- read a wave per tree, 3 KB
 // per step.  A token starts at every `"` after `{` or `,` and nowhere else in
 // that form, so the lanes find them in their 16 bytes independently; each
 // token checks that its successor starts right after it (through a `,` after
@@ -484,7 +484,7 @@ constexpr int32_t JP_SLOW = -1;
 constexpr u64 JP_KEY_MASK = 0xFFFFFF00FFull, JP_KEY = 0x7B3A220022ull;          // `"?":{`
 constexpr u64 JP_HASH_MASK = 0x00FFFFFFFFFFFFFFull, JP_HASH = 0x003A226873616822ull;  // `"hash":`
 constexpr int JV_WAVES = 4;
-constexpr u32 JV_STEP = 2048;                // text bytes per step: 32 per lane
+constexpr u32 JV_STEP = 3072;                // text bytes per step: 48 per lane (~4 chunks of 64 tokens in config 3's trees)
 constexpr u32 JV_BUF = 16 + JV_STEP + 48;    // the chunk before (a token's `{` / `,`), the step, lookahead
 constexpr u32 JV_TOK = JV_STEP / 2;          // token starts in a step (>= 2 bytes apart: `,"` in a malformed text)
 constexpr u32 JV_HASH = 3, JV_END = 4, JV_BAD = 5, JV_ROOT = 6, JV_NONE = 7;  // token kinds (0-2: OPEN digit)
@@ -667,46 +667,49 @@ __global__ __launch_bounds__(64 * JV_WAVES) void k_json_wave(const uint8_t* __re
       bool bad = false;
       // the step's 32 bytes per lane and the 48 after the step (lanes 0-2), loaded
       // one step ahead
-      uint4 v0 = chunk(A + 32 * lane), v1 = chunk(A + 32 * lane + 16), la = make_uint4(0, 0, 0, 0);
+      uint4 v0 = chunk(A + 48 * lane), v1 = chunk(A + 48 * lane + 16), v2 = chunk(A + 48 * lane + 32),
+            la = make_uint4(0, 0, 0, 0);
       if (lane < 3) la = chunk(A + JV_STEP + 16 * lane);
-      uint4 last1 = make_uint4(0, 0, 0, 0);  // (lane 63: the step before's last 16 bytes)
+      uint4 last2 = make_uint4(0, 0, 0, 0);  // (lane 63: the step before's last 16 bytes)
       for (u64 P0 = 0; P0 < E && !bad; P0 += JV_STEP) {
         const uint8_t* S1 = A + P0 + JV_STEP;
-        const uint4 n0 = chunk(S1 + 32 * lane), n1 = chunk(S1 + 32 * lane + 16);
+        const uint4 n0 = chunk(S1 + 48 * lane), n1 = chunk(S1 + 48 * lane + 16), n2 = chunk(S1 + 48 * lane + 32);
         uint4 nla = make_uint4(0, 0, 0, 0);
         if (lane < 3) nla = chunk(S1 + JV_STEP + 16 * lane);
         // stage the step's bytes, the chunk before them and the lookahead in LDS
         uint4* b4 = reinterpret_cast<uint4*>(w->buf);
-        b4[1 + 2 * lane] = v0;
-        b4[2 + 2 * lane] = v1;
-        if (lane < 3) b4[1 + 2 * 64 + lane] = la;
-        if (lane == 63) b4[0] = last1;
+        b4[1 + 3 * lane] = v0;
+        b4[2 + 3 * lane] = v1;
+        b4[3 + 3 * lane] = v2;
+        if (lane < 3) b4[1 + 3 * 64 + lane] = la;
+        if (lane == 63) b4[0] = last2;
         wave_sync();
-        // token starts in this lane's 32 bytes: `"` after `{` or `,`, within [s0 + 1, E)
-        const u32 prev = w->buf[3 + 8 * lane] >> 24;
+        // token starts in this lane's 48 bytes: `"` after `{` or `,`, within [s0 + 1, E)
+        const u32 prev = w->buf[3 + 12 * lane] >> 24;
         auto oc4 = [](u32 x) { return bytes_eq(x, 0x7B7B7B7Bu) | bytes_eq(x, 0x2C2C2C2Cu); };
         auto q4 = [](u32 x) { return bytes_eq(x, 0x22222222u); };
-        const u32 q = q4(v0.x) | q4(v0.y) << 4 | q4(v0.z) << 8 | q4(v0.w) << 12 | q4(v1.x) << 16 | q4(v1.y) << 20 |
-                      q4(v1.z) << 24 | q4(v1.w) << 28;
-        const u32 oc = oc4(v0.x) | oc4(v0.y) << 4 | oc4(v0.z) << 8 | oc4(v0.w) << 12 | oc4(v1.x) << 16 |
-                       oc4(v1.y) << 20 | oc4(v1.z) << 24 | oc4(v1.w) << 28;
-        u32 starts = q & ((oc << 1) | (prev == '{' || prev == ',' ? 1u : 0u));
-        const u64 pos0 = P0 + 32 * (u64)lane;
+        auto q16 = [&](uint4 v) { return q4(v.x) | q4(v.y) << 4 | q4(v.z) << 8 | q4(v.w) << 12; };
+        auto oc16 = [&](uint4 v) { return oc4(v.x) | oc4(v.y) << 4 | oc4(v.z) << 8 | oc4(v.w) << 12; };
+        const u64 q = (u64)q16(v0) | (u64)q16(v1) << 16 | (u64)q16(v2) << 32;
+        const u64 oc = (u64)oc16(v0) | (u64)oc16(v1) << 16 | (u64)oc16(v2) << 32;
+        u64 starts = q & ((oc << 1) | (prev == '{' || prev == ',' ? 1ull : 0ull)) & 0xFFFFFFFFFFFFull;
+        const u64 pos0 = P0 + 48 * (u64)lane;
         const int64_t lo = (int64_t)(s0 + 1) - (int64_t)pos0, hi = (int64_t)E - (int64_t)pos0;
-        if (lo > 0) starts &= lo >= 32 ? 0u : ~((1u << lo) - 1u);
-        if (hi < 32) starts &= hi <= 0 ? 0u : (1u << hi) - 1u;
-        last1 = v1;
+        if (lo > 0) starts &= lo >= 48 ? 0ull : ~((1ull << lo) - 1ull);
+        if (hi < 48) starts &= hi <= 0 ? 0ull : (1ull << hi) - 1ull;
+        last2 = v2;
         v0 = n0;
         v1 = n1;
+        v2 = n2;
         la = nla;
-        const u32 nt = __popc(starts);
+        const u32 nt = __popcll(starts);
         u32 tb = wave_scan(JvCount{nt}, lane, [](JvCount y, JvCount x) { return JvCount{x.n + y.n}; }).n;
         const u32 T = __builtin_amdgcn_readlane(tb, 63);
         tb -= nt;
         while (starts) {
-          const u32 j = __ffs(starts) - 1;
+          const u32 j = __ffsll((unsigned long long)starts) - 1;
           starts &= starts - 1;
-          w->pos[tb++] = (uint16_t)(16 + 32 * lane + j);
+          w->pos[tb++] = (uint16_t)(16 + 48 * lane + j);
         }
         wave_sync();
         // the tokens, 64 at a time, one per lane
