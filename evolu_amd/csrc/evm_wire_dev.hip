@@ -492,6 +492,7 @@ constexpr u64 CODE_ALL = (1ull << (2 * CODE_DIGITS)) - 1ull;
 
 struct alignas(16) JvLds {
   u32 buf[JV_BUF / 4];
+  unsigned long long bal[CODE_DIGITS];  // a chunk's OPEN lanes by depth
   uint16_t pos[JV_TOK];      // the step's token starts (buffer bytes), in text order
   int32_t stk[CODE_DIGITS];  // the leaves' XOR before the last OPEN at each depth (earlier chunks)
 };
@@ -501,6 +502,10 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// 0x80 in each zero byte of x; the four bytes' top bits as bits 0-3
+__device__ __forceinline__ u32 zero_bytes(u32 x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu); }
+__device__ __forceinline__ u32 gather4(u32 t) { return ((((t >> 7) & 0x01010101u) * 0x00204081u) >> 21) & 0xFu; }
 
 // bit k: byte k of w equals c (c4 = c in every byte)
 __device__ __forceinline__ u32 bytes_eq(u32 w, u32 c4) {
@@ -549,7 +554,7 @@ __device__ __forceinline__ T wave_scan(T x, int lane, Comb comb) {
   return x;
 }
 // (the scanned values: a count; depth change and leaf XOR; the code operation
-// "keep the digits above depth a, then set B"; a min and a max)
+// "keep the digits above depth a, then set B")
 struct JvCount {
   u32 n;
   template <int CTRL>
@@ -569,12 +574,6 @@ struct JvOp {
   template <int CTRL>
   __device__ __forceinline__ JvOp shift() const { return JvOp{(int)dpp<CTRL>((u32)a), dpp64<CTRL>(B)}; }
   __device__ __forceinline__ JvOp at(int l) const { return JvOp{(int)rl((u32)a, l), ((u64)rl((u32)(B >> 32), l) << 32) | rl((u32)B, l)}; }
-};
-struct JvRange {
-  int mn, mx;
-  template <int CTRL>
-  __device__ __forceinline__ JvRange shift() const { return JvRange{(int)dpp<CTRL>((u32)mn), (int)dpp<CTRL>((u32)mx)}; }
-  __device__ __forceinline__ JvRange at(int l) const { return JvRange{(int)rl((u32)mn, l), (int)rl((u32)mx, l)}; }
 };
 
 // The token at buffer byte pb (text position p, the text ends at E): its kind
@@ -686,8 +685,8 @@ __global__ __launch_bounds__(64 * JV_WAVES) void k_json_wave(const uint8_t* __re
         wave_sync();
         // token starts in this lane's 48 bytes: `"` after `{` or `,`, within [s0 + 1, E)
         const u32 prev = w->buf[3 + 12 * lane] >> 24;
-        auto oc4 = [](u32 x) { return bytes_eq(x, 0x7B7B7B7Bu) | bytes_eq(x, 0x2C2C2C2Cu); };
-        auto q4 = [](u32 x) { return bytes_eq(x, 0x22222222u); };
+        auto oc4 = [](u32 x) { return gather4(zero_bytes(x ^ 0x7B7B7B7Bu) | zero_bytes(x ^ 0x2C2C2C2Cu)); };
+        auto q4 = [](u32 x) { return gather4(zero_bytes(x ^ 0x22222222u)); };
         auto q16 = [&](uint4 v) { return q4(v.x) | q4(v.y) << 4 | q4(v.z) << 8 | q4(v.w) << 12; };
         auto oc16 = [&](uint4 v) { return oc4(v.x) | oc4(v.y) << 4 | oc4(v.z) << 8 | oc4(v.w) << 12; };
         const u64 q = (u64)q16(v0) | (u64)q16(v1) << 16 | (u64)q16(v2) << 32;
@@ -757,19 +756,14 @@ __global__ __launch_bounds__(64 * JV_WAVES) void k_json_wave(const uint8_t* __re
           // an internal node's open: the last OPEN one depth up (in this chunk: a
           // ballot per depth present; before it: the depth's entry in stk)
           const int need = hash && !leaf && db >= 1 ? db - 1 : -1;
-          u64 mneed = 0, mown = 0;
-          const u64 opens = __ballot(open && db < CODE_DIGITS);
-          if (opens) {
-            const bool o2 = open && db < CODE_DIGITS;
-            const JvRange r = wave_scan(JvRange{o2 ? db : 64, o2 ? db : -1}, lane,
-                                        [](JvRange y, JvRange x) { return JvRange{min(x.mn, y.mn), max(x.mx, y.mx)}; });
-            const int dmin = __builtin_amdgcn_readlane(r.mn, 63), dmax = __builtin_amdgcn_readlane(r.mx, 63);
-            for (int d = dmin; d <= dmax; ++d) {
-              const u64 b = __ballot(open && db == d);
-              mneed = need == d ? b : mneed;
-              mown = open && db == d ? b : mown;
-            }
-          }
+          // (the chunk's OPEN lanes per depth: one LDS OR per lane, not a ballot per depth)
+          const bool o2 = open && db < CODE_DIGITS;
+          if (lane < CODE_DIGITS) w->bal[lane] = 0;
+          wave_sync();
+          if (o2) atomicOr(&w->bal[db], 1ull << lane);
+          wave_sync();
+          const u64 mneed = need >= 0 ? w->bal[need] : 0ull;
+          const u64 mown = o2 ? w->bal[db] : 0ull;
           const u64 mm = mneed & lt;
           const int32_t po_lane = __shfl(pb, mm ? 63 - __clzll(mm) : lane, 64);
           if (hash && !leaf) {
