@@ -374,7 +374,8 @@ int tree_compact(evm_ctx* ctx, const evm_tree* t);
 // *bad |= 1 for an owner out of range) and the plan the emit follows (arrays
 // in S); the texts written at out + off[j]
 struct JsonPlan {
-  uint32_t n = 0;  // (the texts are placed by the caller from the lengths)
+  uint32_t n = 0;             // (the texts are placed by the caller from the lengths)
+  uint16_t* plen = nullptr;   // each leaf's piece length, by leaf slot (in the caller's Scratch)
 };
 int json_plan(evm_ctx* ctx, Scratch& S, const evm_tree* t, const uint32_t* owners, uint32_t n, uint64_t* len,
               uint32_t* bad, JsonPlan* plan);

@@ -214,7 +214,8 @@ __device__ __forceinline__ u32 wave_excl_sum(u32 v, u32* total) {
 // from chunk to chunk in LDS).  k_jp_len: each owner's text length (an empty
 // or out-of-range owner: `{}`, the latter flagged in *bad).
 __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_len(TreeJ t, const u32* __restrict__ owners, u32 n,
-                                                          u64* __restrict__ len, u32* __restrict__ bad) {
+                                                          u64* __restrict__ len, u32* __restrict__ bad,
+                                                          uint16_t* __restrict__ plen) {
   __shared__ WaveLds lds[JW_WAVES];
   WaveLds* w = &lds[threadIdx.x / JW];
   const u32 lane = threadIdx.x & 63;
@@ -233,7 +234,9 @@ __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_len(TreeJ t, const u32* __
       const Chunk ch{j, L, a, k, p0, true};
       const Lane ln = chunk_setup(t, ch, w);
       u32 tot;
-      wave_excl_sum(leaf_piece(w, ln, [](u32, char) {}), &tot);
+      const u32 my = leaf_piece(w, ln, [](u32, char) {});
+      if (plen && ln.valid) plen[ch.a + ln.i] = (uint16_t)my;  // (k_jp_emit reads it: no second length pass)
+      wave_excl_sum(my, &tot);
       total += tot;
       chunk_carry(w, lane);
     }
@@ -243,7 +246,8 @@ __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_len(TreeJ t, const u32* __
 
 // k_jp_emit: owner j's text at out + off[j], a chunk at a time (staged in LDS)
 __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_emit(TreeJ t, const u32* __restrict__ owners, u32 n,
-                                                           const u64* __restrict__ off, char* __restrict__ out) {
+                                                           const u64* __restrict__ off, char* __restrict__ out,
+                                                           const uint16_t* __restrict__ plen) {
   __shared__ WaveLds lds[JW_WAVES];
   __shared__ __attribute__((aligned(16))) unsigned char stage[JW_WAVES][JW_STAGE + 16];
   const u32 wv = threadIdx.x / JW, lane = threadIdx.x & 63;
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_emit(TreeJ t, const u32* _
       const Chunk ch{j, L, a, k, p0, true};
       char* dst = dst0 + run;
       const Lane ln = chunk_setup(t, ch, w);
-      const u32 my = leaf_piece(w, ln, [](u32, char) {});
+      const u32 my = plen ? (ln.valid ? (u32)plen[ch.a + ln.i] : 0u) : leaf_piece(w, ln, [](u32, char) {});
       u32 tot;
       const u32 head = ch.k == 0 ? 1u : 0u;
       const u32 pos = head + wave_excl_sum(my, &tot);
@@ -329,20 +333,23 @@ __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_emit(TreeJ t, const u32* _
 // each text straight into its response).  The plan's arrays live in S.
 int evm::json_plan(evm_ctx* ctx, Scratch& S, const evm_tree* t, const uint32_t* owners, uint32_t n, uint64_t* len,
                    uint32_t* bad, JsonPlan* plan) {
-  (void)S;
   const TreeJ tv{t->off, t->end, t->ck, t->pfx, t->n_owners};
   const u32 grid = (u32)std::min<u64>((n + JW_WAVES - 1) / JW_WAVES, (u64)ctx->n_cu * 32);
-  if (n) KLAUNCH(k_jp_len, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (u64*)len, bad);
+  // each leaf's piece length, by leaf slot, for the emit
+  plan->plen = S.alloc<uint16_t>((size_t)(t->gapped ? t->cap : t->n_leaves) + 1);
+  if (!plan->plen) return EVM_ENOMEM;
+  if (n)
+    KLAUNCH(k_jp_len, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (u64*)len, bad, plan->plen);
   plan->n = n;
   return hip_ok(hipGetLastError());
 }
 int evm::json_emit(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t n, const JsonPlan& plan,
                    const uint64_t* off, char* out) {
-  (void)plan;
   const TreeJ tv{t->off, t->end, t->ck, t->pfx, t->n_owners};
   const u32 grid = (u32)std::min<u64>((n + JW_WAVES - 1) / JW_WAVES, (u64)ctx->n_cu * 32);
   if (n)
-    KLAUNCH(k_jp_emit, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (const u64*)off, out);
+    KLAUNCH(k_jp_emit, dim3(std::max<u32>(grid, 1)), dim3(JW * JW_WAVES), tv, owners, n, (const u64*)off, out,
+            (const uint16_t*)plan.plen);
   return hip_ok(hipGetLastError());
 }
 
