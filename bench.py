@@ -158,7 +158,7 @@ def parse():
     ap.add_argument("--dom-events", type=int, default=1,
                     help="1: HIP events around the dominant kernel inside the timed region (the roofline's "
                          "duration); 0: none in the timed region, the duration from an identical pass after it")
-    ap.add_argument("--traffic-dir", default=os.path.join(ROOT, "profiles"),
+    ap.add_argument("--traffic-dir", default=os.path.join(ROOT, "profiles", "r06"),
                     help="PMC-derived HBM bytes per launch per kernel, traffic_<workload>.json per workload "
                          "(written by tools/pmc_traffic.py from tools/gpu_prof.sh's passes)")
     return ap.parse_args()
@@ -364,7 +364,23 @@ def quiet_stdout():
     os.dup2(2, 1)
 
 
+def _traffic_ratios(o):
+    """Every roofline block with a PMC traffic figure also states it as a
+    multiple of its algorithmic bytes (traffic well above 1x = re-reads)."""
+    if isinstance(o, dict):
+        t, a = o.get("traffic"), o.get("alg_bytes_per_launch")
+        if "traffic" in o and "alg_bytes_per_launch" in o:
+            o["traffic_ratio"] = (t / a) if t and a else None
+            o["traffic_src"] = os.path.relpath(TRAFFIC_DIR, ROOT)
+        for v in o.values():
+            _traffic_ratios(v)
+    elif isinstance(o, list):
+        for v in o:
+            _traffic_ratios(v)
+
+
 def emit(obj):
+    _traffic_ratios(obj)
     line = (json.dumps(obj) + "\n").encode()
     if _STDOUT is None:
         sys.stdout.write(line.decode())
@@ -925,7 +941,7 @@ C4_SEED = 0xE7010004  # seed = 0xE7010000 + config number
 
 
 def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10, warmup=2, sample=1000,
-                 seed=C4_SEED, verbose=False, dist_ingest=True):
+                 seed=C4_SEED, verbose=False, dist_ingest=True, src_wire_steps=3):
     """BASELINE config 4 on one rank: the sync server (index.ts:138-202,
     addMessages + getMessages) over owners_per_gpu x world owners of
     per_owner messages each, sharded by murmur3(userId) mod world.
@@ -1087,6 +1103,43 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
         ref.free()
         client_s.free()
     parity = comm.min(1 if ok else 0) == 1
+    # ---- the ingest kernel of the rows that crossed a link: at N > 1,
+    # (N - 1) / N of every rank's rows arrive as 24-B records and K5 reads
+    # them where they landed (k_svo_a<..., SRC_WIRE>); at world 1 the keep-input
+    # route never moves a row, so these steps route WITHOUT keep-input (every
+    # row a record) to time that kernel at the leg's full size
+    src_wire = None
+    if dist_ingest and src_wire_steps:
+        wname = "(k_svo_a<1024, SRC_WIRE>)"
+        ws_ms = []
+        eng.prof_enable(True)
+        eng.prof_only(wname)
+        eng.prof_reset()
+        comm.barrier()
+        for _ in range(src_wire_steps + 1):
+            torch.cuda.synchronize(dev)
+            w0 = time.perf_counter()
+            srv.dd.route(ts_in, owner_in, need_src=False, keep_input=False)
+            srv.new_store()
+            srv.dd.ingest(srv.store, id_base, flags)
+            torch.cuda.synchronize(dev)
+            ws_ms.append((time.perf_counter() - w0) * 1e3)
+            if len(ws_ms) == 1:
+                eng.prof_reset()  # (the first is a warm-up)
+        pw = eng.prof_report()
+        eng.prof_enable(False)
+        eng.prof_only(None)
+        if wname in pw:
+            w_tot, w_n = pw[wname]
+            w_avg = w_tot / w_n / 1e3
+            per_msg, per_leaf = SERVER_ALG[wname]
+            w_alg = per_msg * n_r + per_leaf * srv.store.tree().n_leaves
+            src_wire = {"kernel": wname, "kernel_ms_avg": w_avg * 1e3, "alg_bytes_per_launch": w_alg,
+                        "frac": w_alg / w_avg / HBM_PEAK, "rows": int(n_r),
+                        "route_ingest_ms_per_step": sum(ws_ms[1:]) / max(1, len(ws_ms) - 1),
+                        "traffic": traffic_of(wname, "config4"),
+                        "note": "route without EVM_ROUTE_KEEP_INPUT: every row a 24-B record, as (N-1)/N of the "
+                                "rows are at N GPUs; K5 reads them in place"}
     n = owners_per_gpu * P  # per GPU (weak scaling)
     ms = elapsed / steps * 1e3
     tot_ms, launches = prof_dom[dom]
@@ -1122,7 +1175,7 @@ def config4_rank(eng, dd, comm, owners_per_gpu=125_000, per_owner=1000, steps=10
         "route": {"ms_per_step": route_avg, "bytes_per_msg": ROUTE_BYTES, "remote_bytes_per_gpu": remote * ROUTE_BYTES,
                   "xgmi_frac": (remote * ROUTE_BYTES / (route_avg / 1e3) / ((world - 1) * XGMI_LINK))
                   if world > 1 else None},
-        "parity_checked": parity, "self_check_rank%d" % rank: detail, "setup_s": setup_s,
+        "parity_checked": parity, "self_check_rank%d" % rank: detail, "setup_s": setup_s, "src_wire": src_wire,
     }
     srv.close()
     client.free()
@@ -2036,9 +2089,8 @@ def e2e_device(eng, arena, off, host_out, O, pick, device_ms):
         if res.result[k] is not True:
             same = False
             continue
-        got = res.buf[int(res.off[k]):int(res.off[k + 1])].cpu().numpy().tobytes()
-        same = same and got == bytes(host_out[k])
-    resp_bytes = int(res.buf.numel()) if res.buf is not None else 0
+        same = same and res.get(k) == bytes(host_out[k])
+    resp_bytes = int(res.nbytes)
     srv.close()
     return {"ms": wall * 1e3, "ratio_to_device_step": wall * 1e3 / device_ms if device_ms else None,
             "ms_by_part": {k: v * 1e3 for k, v in timing.items()}, "responses": ok, "response_bytes": resp_bytes,

@@ -22,6 +22,10 @@ EVM_ENOMEM = 7
 EVM_ECAPACITY = 8
 EVM_EDIST = 9
 EVM_ESTATE = 10
+EVM_EROUNDS = 11
+EVM_EHANDOVER = 12
+SYNC_HOST = 0
+SYNC_DEVICE = 1
 DIST_ID_BYTES = 128
 
 META_CASEMASK = 0x0000FFFF
@@ -40,7 +44,6 @@ OPT_CLIENT_PATH = 1
 OPT_SERVER_PATH = 2
 OPT_OVERLAP = 3
 OPT_RADIX = 4
-OPT_TEST_FAIL = 5
 OPT_DIFF_GRID = 6
 OPT_SELECT_PATH = 7
 
@@ -69,6 +72,7 @@ SIGNATURES = {
     "evm_get_stream": (_vp, [_vp]),
     "evm_sync": (_i, [_vp]),
     "evm_set_option": (_i, [_vp, _i, C.c_int64]),
+    "evm_test_fault": (_i, [_vp, _i]),  # include/evm_test.h (EVM_TEST_HOOKS=1 only)
     "evm_prof_enable": (_i, [_vp, _i]),
     "evm_prof_reset": (_i, [_vp]),
     "evm_cross_cell_check": (_i, [_vp, _vp, _sz, _sz, _vp, C.c_uint32, C.POINTER(C.c_int32)]),
@@ -117,6 +121,19 @@ SIGNATURES = {
     "evm_tree_from_json_dev": (_i, [_vp, _u32, _vp, _vp, _vp, _vp, C.POINTER(_vp)]),
     "evm_pb_encode_responses_dev": (_i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _sz, _vp, _vp, _vp,
                                          _sz, _vp, C.POINTER(C.c_uint64)]),
+    "evm_sync_create": (_i, [_vp, _vp, C.POINTER(_vp)]),
+    "evm_sync_destroy": (_i, [_vp]),
+    "evm_sync_round": (_i, [_vp, _vp, _vp, _u32, _i, _vp, _vp, C.POINTER(C.c_uint64)]),
+    "evm_sync_fetch": (_i, [_vp, _vp]),
+    "evm_sync_responses_dev": (_vp, [_vp]),
+    "evm_sync_users": (_i, [_vp, _vp, _vp, _u32, _i, _vp]),
+    "evm_sync_user_flag": (_i, [_vp, _u32, _i]),
+    "evm_sync_user_count": (_i, [_vp, C.POINTER(_u32), C.POINTER(C.c_uint64)]),
+    "evm_sync_user_keys": (_i, [_vp, _vp, _vp]),
+    "evm_sync_log_add": (_i, [_vp, _vp, _sz, C.c_uint64, _vp, _vp, C.POINTER(C.c_uint64)]),
+    "evm_sync_log_read": (_i, [_vp, _vp, C.c_uint64, _vp, _vp, _vp]),
+    "evm_sync_next_id": (C.c_uint64, [_vp]),
+    "evm_sync_timing": (_i, [_vp, _vp]),
     "evm_store_since": (_i, [_vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_server_select": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "evm_store_select_after": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),

@@ -13,7 +13,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("EVM_ARCH", "gfx950")
 
 SOURCES = ["evm_engine.hip", "evm_client.hip", "evm_server.hip", "evm_clock.hip", "evm_dist.hip", "evm_json.cpp", "evm_json_dev.hip", "evm_wire_dev.hip",
-           "evm_proto.cpp"]
+           "evm_proto.cpp", "evm_sync.hip"]
 HEADERS = ["evm_device.hpp", "evm_pack.hpp", "evm_prims.hpp", "evm_internal.hpp"]
 
 

@@ -1039,6 +1039,9 @@ const char* evm_strerror(int s) {
     case EVM_ENOMEM: return "device out of memory";
     case EVM_ECAPACITY: return "output buffer too small";
     case EVM_EDIST: return "RCCL unavailable or a collective failed";
+    case EVM_ESTATE: return "a store invariant broke in a merge; nothing committed";
+    case EVM_EROUNDS: return "a userId in two requests of one call: split the call into rounds";
+    case EVM_EHANDOVER: return "request not modelled here: the caller's reference path runs it";
   }
   return "unknown status";
 }
@@ -1083,6 +1086,7 @@ void evm_destroy(evm_ctx* ctx) {
   for (hipEvent_t e : ctx->prof_pool) (void)hipEventDestroy(e);
   block_cache_clear(ctx);
   evm_pending_pool_clear(ctx);
+  evm_host_stage_free(ctx);
   if (ctx->xtab) (void)hipFree(ctx->xtab);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
@@ -1142,15 +1146,22 @@ int evm_set_option(evm_ctx* ctx, int option, int64_t value) {
     ctx->diff_grid = (int)value;
     return EVM_OK;
   }
-  if (option == EVM_OPT_TEST_FAIL && value >= 0 && value <= 2) {
-    ctx->test_fail = (int)value;
-    return EVM_OK;
-  }
   if (option == EVM_OPT_SERVER_PATH && value >= 0 && value <= 4) {
     ctx->server_path = (int)value;
     return EVM_OK;
   }
   return EVM_EINVAL;
+}
+
+// include/evm_test.h: fault injection for the atomicity tests, outside the
+// product ABI (evm.h) and refused unless the process runs with
+// EVM_TEST_HOOKS=1 -- no product caller can switch a check off by accident.
+int evm_test_fault(evm_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 2) return EVM_EINVAL;
+  const char* e = getenv("EVM_TEST_HOOKS");
+  if (!e || strcmp(e, "1") != 0) return EVM_EINVAL;
+  ctx->test_fail = mode;
+  return EVM_OK;
 }
 
 int evm_prof_enable(evm_ctx* ctx, int on) {

@@ -16,6 +16,9 @@ struct Info;
 }
 
 struct evm_pending;
+namespace evm {
+struct HostStage;
+}
 
 struct evm_ctx {
   int device;
@@ -29,7 +32,7 @@ struct evm_ctx {
   int client_path = 0;  // EVM_OPT_CLIENT_PATH
   int server_path = 0;  // EVM_OPT_SERVER_PATH
   int overlap = 1;      // EVM_OPT_OVERLAP: independent checks on a second stream
-  int test_fail = 0;       // EVM_OPT_TEST_FAIL (tests only)
+  int test_fail = 0;       // evm_test_fault (include/evm_test.h; tests only)
   int radix_onesweep = 1;  // EVM_OPT_RADIX: 1 one-sweep radix passes (look-back), 0 histogram + scan + scatter
   int diff_grid = 0;       // EVM_OPT_DIFF_GRID: k_diff workgroups per CU (0: one lane group per owner)
   int select_path = 0;     // EVM_OPT_SELECT_PATH: 0 one-pass keep + rank + emit, 1 keep / scan / emit passes
@@ -54,6 +57,7 @@ struct evm_ctx {
   // a steady-state loop of ingests / applies makes no allocation calls
   std::vector<std::pair<void*, size_t>> blocks;
   std::vector<evm_pending*> pend_pool;  // finished evm_apply_batch_async handles (pinned slot + event kept)
+  evm::HostStage* stage = nullptr;  // pinned chunks + copy stream for host <-> device staging (evm_sync.hip)
 };
 
 // One MerkleTree per owner, as sorted unique leaves keyed by
@@ -329,6 +333,7 @@ void block_free(evm_ctx* ctx, void* p, size_t bytes);
 void block_cache_clear(evm_ctx* ctx);
 }  // namespace evm
 void evm_pending_pool_clear(evm_ctx* ctx);  // evm_client.hip
+void evm_host_stage_free(evm_ctx* ctx);     // evm_sync.hip
 namespace evm {
 
 // shared launchers (evm_engine.hip)

@@ -258,6 +258,7 @@ int evm_pb_encode(int kind, const char* ts, size_t stride, const uint32_t* ts_le
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -307,8 +308,7 @@ int evm_pb_split_batch(int kind, const uint8_t* arena, const uint64_t* off, uint
                        uint32_t* ts_len, uint64_t* ts_off, uint64_t* content_off, uint8_t* content) {
   if (n && (!arena || !off || !status || !msg_base || !content_base || !ts || !content_off)) return EVM_EINVAL;
   if (stride < 46) return EVM_EINVAL;
-  int bad = EVM_OK;
-  std::vector<int> errs((size_t)std::max(1, host_threads(n)), EVM_OK);
+  std::atomic<int> err{EVM_OK};  // the first error any thread meets
   parallel_for(n, [&](size_t a, size_t b) {
     std::vector<uint64_t> co;
     for (size_t k = a; k < b; ++k) {
@@ -322,7 +322,8 @@ int evm_pb_split_batch(int kind, const uint8_t* arena, const uint64_t* off, uint
       const int st = evm_pb_split(kind, body, len, ts + m0 * stride, stride, ts_len ? ts_len + m0 : nullptr,
                                   ts_off ? ts_off + m0 : nullptr, co.data(), content ? content + c0 : nullptr);
       if (st) {
-        errs[0] = st;  // (a body that changed between the passes)
+        int none = EVM_OK;
+        err.compare_exchange_strong(none, st);  // (a body that changed between the passes)
         continue;
       }
       for (uint64_t i = 0; i < s.n_messages; ++i) {
@@ -334,8 +335,7 @@ int evm_pb_split_batch(int kind, const uint8_t* arena, const uint64_t* off, uint
       content_off[m0 + s.n_messages] = c0 + co[s.n_messages];
     }
   });
-  for (int e : errs) bad = bad ? bad : e;
-  return bad;
+  return err.load();
 }
 
 // SyncResponse bodies (index.ts:235-245) for n requests: request r's

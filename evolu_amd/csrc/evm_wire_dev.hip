@@ -795,12 +795,6 @@ __global__ __launch_bounds__(64 * JV_WAVES) void k_json_wave(const uint8_t* __re
           const int last = (int)min<u32>(T - c, 64u) - 1;
           lastk = __builtin_amdgcn_readlane(k, last);
           lastcode = ((u64)rl((u32)(cb >> 32), last) << 32) | rl((u32)cb, last);
-#ifdef JV_DEBUG
-          if (lane == 0)
-            printf("P0 %llu c %u T %u depth %d code %llx P %d lastk %u lastcode %llx cnt %llu bl %d\n",
-                   (unsigned long long)P0, c, T, depth, (unsigned long long)code, P, lastk,
-                   (unsigned long long)lastcode, (unsigned long long)cnt, (int)(__ballot(bl) != 0));
-#endif
           if (__ballot(bl)) {
             bad = true;
             break;

@@ -27,6 +27,10 @@
  *                         "timestamp"), batched over owners
  *   evm_tree_to_json /
  *   evm_tree_from_json .. types.ts:80-84 merkleTreeToString / FromString
+ *   evm_sync_round ...... apps/server/src/index.ts:204-251 the whole sync
+ *                         request handler (parseBody, getMerkleTree,
+ *                         addMessages, getMessages, toBinary), batched over
+ *                         the requests of one round, bodies in and out
  */
 #ifndef EVM_H
 #define EVM_H
@@ -50,7 +54,10 @@ enum evm_status {
   EVM_ENOMEM = 7,     /* device allocation failed */
   EVM_ECAPACITY = 8,  /* output buffer too small */
   EVM_EDIST = 9,      /* RCCL missing or a collective failed (evm_dist_*) */
-  EVM_ESTATE = 10     /* a store invariant broke in a merge (stored and new keys not disjoint); nothing committed */
+  EVM_ESTATE = 10,    /* a store invariant broke in a merge (stored and new keys not disjoint); nothing committed */
+  EVM_EROUNDS = 11,   /* evm_sync_round: a userId in two requests of one call; nothing applied (split the call) */
+  EVM_EHANDOVER = 12  /* evm_sync_round, per request: not modelled here (a nodeId that is not 16 hex chars, or a
+                         user handed to the caller); nothing of it applied -- the caller's reference path runs it */
 };
 
 /* ---- packed timestamp record (32 bytes, device) -------------------------
@@ -120,9 +127,6 @@ int evm_sync(evm_ctx* ctx);
                                  records instead of parsing the rows itself (A/B) */
 #define EVM_OPT_RADIX 4       /* radix sorts: 1 (default) one-sweep passes with decoupled look-back; 2 the same with \
                                  10-bit digits when that saves a pass; 0 histogram + scan + scatter per pass */
-#define EVM_OPT_TEST_FAIL 5   /* tests only: 1 = the sort-path phase of a split ingest fails (EVM_ENOMEM); \
-                                 2 = K5 skips its check against the stored rows (the merge's guard then \
-                                 returns EVM_ESTATE) */
 #define EVM_OPT_DIFF_GRID 6   /* evm_merkle_diff / select: k_diff workgroups per CU (0: one lane group per owner) */
 #define EVM_OPT_SELECT_PATH 7 /* getMessages selection with a requester: 0 (default) keep + rank + emit in one pass \
                                  (look-back over candidate tiles), 1 keep / scan / emit passes (A/B) */
@@ -478,6 +482,74 @@ int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, 
                                 const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
                                 size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
                                 uint8_t* out, size_t cap, uint64_t* out_off, uint64_t* total);
+
+/* ------------------------------------------------------------ sync server
+ * The server's request handler, apps/server/src/index.ts:204-251 (parseBody
+ * :108-116, getMerkleTree :118-134, addMessages :136-171, getMessages
+ * :173-202, SyncResponse.toBinary :233-241), for n SyncRequest bodies in one
+ * call, run on the device end to end: the bodies decoded where they lie, the
+ * userId -> owner slot directory a device hash table (new users take slots in
+ * request order), one addMessages over every request (the reference's
+ * per-request transactions: a request with a row outside the native domain
+ * commits nothing), the client trees parsed, one getMessages, the responses
+ * built in device memory.  The server owns the directory and the message log
+ * (the rows and contents getMessages answers with); the store is the
+ * caller's (evm_store_new with n_owners = the user capacity).
+ *
+ * A userId with a byte >= 0x80 is the caller's too (EVM_EHANDOVER: protobuf-ts
+ * decodes it as UTF-8, and an invalid sequence decodes lossily).
+ *
+ * evm_sync_round: bodies arena[off[k] .. off[k + 1]) (off: HOST, n + 1
+ * entries); where = EVM_SYNC_HOST (arena in host memory: staged through
+ * pinned buffers to the device) or EVM_SYNC_DEVICE (arena in device memory,
+ * readable in whole 16-B chunks).  Call status: EVM_OK, EVM_EROUNDS (a userId
+ * in two requests: nothing applied -- the caller splits the call into rounds
+ * of one request per user, in order), EVM_ECAPACITY (more users than the
+ * store's owners: nothing applied), or an error.  Per request (host
+ * result[n]): EVM_OK (response bytes [resp_off[k], resp_off[k + 1]) of the
+ * round's response arena), EVM_EINVAL (SyncRequest.fromBinary threw -> 500),
+ * EVM_ETREE (merkleTreeFromString threw -> 500; its rows are committed, as
+ * the reference's addMessages ran first), EVM_ERANGE (diffMerkleTrees threw
+ * RangeError -> 500; rows committed), EVM_ENONCANON (a timestamp outside
+ * the native domain: nothing of the request stored -- the caller's reference
+ * path decides: RangeError of toISOString, or a lenient spelling V8
+ * accepts), EVM_EHANDOVER (see the status).  resp_off: host n + 1;
+ * *resp_bytes: the arena's size.  evm_sync_fetch copies the arena to host
+ * memory; evm_sync_responses_dev returns it in device memory (valid until
+ * the next round).
+ *
+ * The rest serves a caller that runs some requests on its own path (the
+ * reference's, for EVM_ENONCANON / EVM_EHANDOVER) against the same store:
+ * evm_sync_users looks up (insert != 0: and adds, in order) users given in
+ * host memory -> slots; evm_sync_user_flag hands a user over (1: every later
+ * request of it answers EVM_EHANDOVER) or takes it back (0); evm_sync_log_add
+ * appends rows ingested outside a round to the message log (host arrays:
+ * ts rows of `stride` bytes, content_off n + 1 from 0, contents) and returns
+ * their first message id (ids are consecutive, shared with the rounds);
+ * evm_sync_log_read reads messages back by id (host: ts 46 B each,
+ * content_off n + 1, contents; content NULL: sizes only). */
+#define EVM_SYNC_HOST 0
+#define EVM_SYNC_DEVICE 1
+typedef struct evm_sync_server evm_sync_server;
+int evm_sync_create(evm_ctx* ctx, evm_store* store, evm_sync_server** out);
+int evm_sync_destroy(evm_sync_server* s);
+int evm_sync_round(evm_sync_server* s, const uint8_t* arena, const uint64_t* off, uint32_t n, int where,
+                   int32_t* result, uint64_t* resp_off, uint64_t* resp_bytes);
+int evm_sync_fetch(evm_sync_server* s, uint8_t* out);
+const uint8_t* evm_sync_responses_dev(const evm_sync_server* s);
+int evm_sync_users(evm_sync_server* s, const uint8_t* ids, const uint64_t* id_off, uint32_t n, int insert,
+                   uint32_t* slots);
+int evm_sync_user_flag(evm_sync_server* s, uint32_t slot, int flag);
+int evm_sync_user_count(const evm_sync_server* s, uint32_t* n_users, uint64_t* key_bytes);
+int evm_sync_user_keys(evm_sync_server* s, uint8_t* keys, uint64_t* key_off);
+int evm_sync_log_add(evm_sync_server* s, const char* ts, size_t stride, uint64_t n, const uint64_t* content_off,
+                     const uint8_t* content, uint64_t* first_id);
+int evm_sync_log_read(evm_sync_server* s, const uint64_t* ids, uint64_t n, char* ts, uint64_t* content_off,
+                      uint8_t* content);
+uint64_t evm_sync_next_id(const evm_sync_server* s);
+/* the last round's wall time by part, ms[8]: staging in (host rounds), decode,
+ * users, addMessages, client trees, getMessages, encode, staging out (fetch) */
+int evm_sync_timing(const evm_sync_server* s, double* ms);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU owner sharding (evm_dist.hip).  One process per

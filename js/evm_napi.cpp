@@ -1249,6 +1249,92 @@ napi_value DistSplitApply(napi_env env, napi_callback_info info) {
   return res;
 }
 
+// ---------------------------------------------------------------- sync server (index.ts:204-251)
+// syncCreate(ctx, store) -> server handle (the user directory + message log over the store)
+napi_value SyncCreate(napi_env env, napi_callback_info info) {
+  napi_value a[2];
+  if (!get_args(env, info, 2, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_sync_server* s = nullptr;
+  const int st = evm_sync_create(cx->c, (evm_store*)ext(env, a[1]), &s);
+  if (st) return throw_status(env, st, "evm_sync_create");
+  return make_ext(env, s);
+}
+
+napi_value SyncDestroy(napi_env env, napi_callback_info info) {
+  napi_value a[2];
+  if (!get_args(env, info, 2, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_sync_destroy((evm_sync_server*)ext(env, a[1]));
+  return nullptr;
+}
+
+// syncRound(ctx, server, bodies Uint8Array, offsets Float64Array(n + 1))
+//   -> { status, results: Int32Array(n), offsets: Float64Array(n + 1), responses: Uint8Array }
+// status EVM_EROUNDS (a userId twice: nothing applied) leaves the rest empty.
+napi_value SyncRound(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  if (!get_args(env, info, 4, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_sync_server* srv = (evm_sync_server*)ext(env, a[1]);
+  void *body, *offd;
+  size_t bl, ol;
+  if (!bytes_of(env, a[2], &body, &bl) || !bytes_of(env, a[3], &offd, &ol)) return nullptr;
+  const size_t n1 = ol / 8;
+  if (n1 < 1) return throw_status(env, EVM_EINVAL, "syncRound: offsets");
+  const uint32_t n = (uint32_t)(n1 - 1);
+  std::vector<uint64_t> off(n1);
+  for (size_t k = 0; k < n1; ++k) off[k] = (uint64_t)static_cast<const double*>(offd)[k];
+  if (off[n] > bl) return throw_status(env, EVM_EINVAL, "syncRound: offsets past the bodies");
+  std::vector<int32_t> res(n);
+  std::vector<uint64_t> roff(n1);
+  uint64_t total = 0;
+  const int st = evm_sync_round(srv, (const uint8_t*)body, off.data(), n, EVM_SYNC_HOST, res.data(), roff.data(),
+                                &total);
+  if (st != EVM_OK && st != EVM_EROUNDS) return throw_status(env, st, "evm_sync_round");
+  napi_value out, v;
+  napi_create_object(env, &out);
+  napi_create_int32(env, st, &v);
+  napi_set_named_property(env, out, "status", v);
+  if (st == EVM_EROUNDS) return out;
+  void* p;
+  napi_value vr = typed(env, napi_int32_array, n, 4, &p);
+  if (n) memcpy(p, res.data(), 4 * (size_t)n);
+  napi_set_named_property(env, out, "results", vr);
+  napi_value vo = typed(env, napi_float64_array, n1, 8, &p);
+  for (size_t k = 0; k < n1; ++k) static_cast<double*>(p)[k] = (double)roff[k];
+  napi_set_named_property(env, out, "offsets", vo);
+  napi_value vb = typed(env, napi_uint8_array, (size_t)total, 1, &p);
+  if (total) {
+    const int fs = evm_sync_fetch(srv, (uint8_t*)p);
+    if (fs) return throw_status(env, fs, "evm_sync_fetch");
+  }
+  napi_set_named_property(env, out, "responses", vb);
+  return out;
+}
+
+// syncUserFlag(ctx, server, userId string, flag): hand a user to the caller's path (1) or back (0)
+napi_value SyncUserFlag(napi_env env, napi_callback_info info) {
+  napi_value a[4];
+  if (!get_args(env, info, 4, a)) return nullptr;
+  Ctx* cx = ctx_of(env, a[0]);
+  std::lock_guard<std::mutex> lock(cx->m);
+  evm_sync_server* srv = (evm_sync_server*)ext(env, a[1]);
+  size_t len = 0;
+  napi_get_value_string_utf8(env, a[2], nullptr, 0, &len);
+  std::string u(len + 1, '\0');
+  napi_get_value_string_utf8(env, a[2], &u[0], len + 1, &len);
+  const uint64_t uo[2] = {0, (uint64_t)len};
+  uint32_t slot = 0;
+  int st = evm_sync_users(srv, (const uint8_t*)u.data(), uo, 1, 1, &slot);
+  if (!st) st = evm_sync_user_flag(srv, slot, (int)u32(env, a[3]));
+  if (st) return throw_status(env, st, "syncUserFlag");
+  return nullptr;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   const struct {
     const char* name;
@@ -1266,7 +1352,8 @@ napi_value Init(napi_env env, napi_value exports) {
              {"distHubNew", DistHubNew},     {"distHubFree", DistHubFree},   {"distHubAbort", DistHubAbort},
              {"distInitLoopback", DistInitLoopback}, {"distDirectory", DistDirectory},
              {"distHotOwners", DistHotOwners}, {"distSplit", DistSplit},   {"distSelectSplit", DistSelectSplit},
-             {"distSplitApply", DistSplitApply}};
+             {"distSplitApply", DistSplitApply}, {"syncCreate", SyncCreate}, {"syncDestroy", SyncDestroy},
+             {"syncRound", SyncRound},       {"syncUserFlag", SyncUserFlag}};
   for (const auto& f : fns) {
     napi_value v;
     napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.fn, nullptr, &v);

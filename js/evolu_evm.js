@@ -289,6 +289,71 @@ class Server {
   }
 }
 
+// apps/server/src/index.ts:218-248, the whole POST handler for a batch of
+// request bodies: one native round (evm_sync_round) -- parseBody, the userId
+// directory, addMessages, getMessages and SyncResponse.toBinary on the device.
+// sync(bodies: Uint8Array[]) -> per body the response bytes (Uint8Array), 500
+// (the handler's res.status(500): a body that does not parse, a client tree
+// merkleTreeFromString rejects, a RangeError of the diff), or null: not
+// applied here -- a timestamp outside the engine's domain, a nodeId that is not
+// 16 hex chars, a non-ASCII userId, or a user handed over (handOver): the
+// reference's handler runs it.  A user with two requests in one call gets them
+// in rounds, in order (the k-th request of every user in round k).
+const EVM_EROUNDS = 11;
+const SYNC_ANSWERED = 0;
+const SYNC_500 = new Set([1 /* EVM_EINVAL */, 4 /* EVM_ERANGE */, 5 /* EVM_ETREE */]);
+class SyncServer {
+  constructor(engine, nUsers) {
+    this.engine = engine;
+    this.store = addon.storeNew(engine.ctx, nUsers);
+    this.h = addon.syncCreate(engine.ctx, this.store);
+  }
+  close() {
+    addon.syncDestroy(this.engine.ctx, this.h);
+    addon.storeFree(this.engine.ctx, this.store);
+  }
+  handOver(userId, flag = true) {
+    addon.syncUserFlag(this.engine.ctx, this.h, userId, flag ? 1 : 0);
+  }
+  sync(bodies) {
+    const out = new Array(bodies.length).fill(null);
+    if (!this._round(bodies, bodies.map((_, i) => i), out)) {
+      const seen = new Map();
+      const rounds = [];
+      bodies.forEach((b, i) => {
+        let u = null;
+        try {
+          u = SyncRequest.fromBinary(b).userId;
+        } catch (e) {
+          u = null;  // (answered 500 by the round)
+        }
+        const k = u === null ? 0 : (seen.get(u) || 0);
+        if (u !== null) seen.set(u, k + 1);
+        while (rounds.length <= k) rounds.push([]);
+        rounds[k].push(i);
+      });
+      for (const idx of rounds) this._round(idx.map((i) => bodies[i]), idx, out);
+    }
+    return out;
+  }
+  _round(bodies, idx, out) {
+    const off = new Float64Array(bodies.length + 1);
+    bodies.forEach((b, i) => { off[i + 1] = off[i] + b.length; });
+    const arena = new Uint8Array(off[bodies.length]);
+    bodies.forEach((b, i) => arena.set(b, off[i]));
+    const r = addon.syncRound(this.engine.ctx, this.h, arena, off);
+    if (process.env.EVM_SYNC_TRACE) console.error("syncRound", bodies.length, r.status, r.results && Array.from(r.results));
+    if (r.status === EVM_EROUNDS) return false;
+    for (let k = 0; k < bodies.length; k++) {
+      const code = r.results[k];
+      if (code === SYNC_ANSWERED) out[idx[k]] = r.responses.slice(r.offsets[k], r.offsets[k + 1]);
+      else if (SYNC_500.has(code)) out[idx[k]] = 500;
+      else out[idx[k]] = null;
+    }
+    return true;
+  }
+}
+
 // Multi-GPU owner sharding (evm_dist_*): one Engine + Dist per GPU process;
 // rank 0 makes the id (Dist.uniqueId()) and hands it to the other processes.
 // Owners live on rank owner % world, or -- after directory(userIds) -- on rank
@@ -421,4 +486,5 @@ class Dist {
   }
 }
 
-module.exports = { Engine, Server, Dist, SyncRequest, SyncResponse, encodeTimestamps, MSG_UPS, MSG_XOR, MSG_INS };
+module.exports = { Engine, Server, SyncServer, Dist, SyncRequest, SyncResponse, encodeTimestamps, MSG_UPS, MSG_XOR,
+  MSG_INS };

@@ -276,3 +276,38 @@ def test_js_dist_split_loopback(tmp_path, world):
     for x in res:  # Dist.addRouted (evm_dist_ingest) == Server.addMessages over the routed rows
         ri = x["routedIngest"]
         assert ri["status"] == 0 and ri["sameFlags"] and ri["sameTrees"] and ri["n"] == len(x["server"]["rows"])
+
+
+@pytest.mark.skipif(shutil.which("node") is None or not os.path.exists("/usr/include/node/node_api.h"),
+                    reason="node / N-API headers not present")
+def test_js_sync_server_round_equals_server_db(tmp_path):
+    """The whole POST handler through the addon (js/evolu_evm.js SyncServer ->
+    evm_sync_round): calls of SyncRequest bodies -- several requests of one
+    user in one call (rounds), a body that does not parse, an absent client
+    tree -- against the oracle's ServerDb.sync (index.ts:204-251) of the same
+    bodies in the same order: the same response bytes, 500 where it throws."""
+    import base64
+
+    from tests.test_gpu_wire import REQ, _expected, _requests
+
+    _build_addon()
+    bodies = _requests(9, n_users=10, n_req=40)
+    rng = random.Random(4)
+    node = W.node_id(rng)
+    ts = W.hlc_timestamps(rng, 6, [node])
+    bodies.insert(7, b"\x0a\x05ab")  # truncated: parseBody throws
+    bodies.insert(13, REQ(messages=[dict(timestamp=t, content=b"q") for t in ts], userId="no-tree",
+                          nodeId=node).SerializeToString())  # merkleTree absent: JSON.parse("") throws
+    calls = [bodies[:17], bodies[17:30], bodies[30:]]
+    f = tmp_path / "sync.json"
+    f.write_text(json.dumps({"users": 16, "calls": [[base64.b64encode(b).decode() for b in c] for c in calls]}))
+    run = subprocess.run(["node", os.path.join(ROOT, "js", "test_sync.js"), str(f)], check=True,
+                         capture_output=True, text=True, timeout=300, env=dict(os.environ, EVM_SYNC_TRACE="1"))
+    got = json.loads(run.stdout.strip().splitlines()[-1])
+    want = _expected(bodies)
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        if w in ("500", "ParseBodyError"):
+            assert g == 500, (i, run.stderr[-3000:])
+        else:
+            assert g is not None and base64.b64decode(g) == w, (i, run.stderr[-3000:])

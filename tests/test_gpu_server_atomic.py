@@ -11,12 +11,23 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def eng():
+    import os
+
     from evolu_amd.engine import Engine
 
+    os.environ["EVM_TEST_HOOKS"] = "1"  # include/evm_test.h: the fault hook answers only with it set
     e = Engine(0)
     yield e
-    e.set_option(5, 0)
+    _fault(e, 0)
     e.close()
+    del os.environ["EVM_TEST_HOOKS"]
+
+
+def _fault(eng, mode):
+    """include/evm_test.h evm_test_fault (test-only, outside the product ABI)."""
+    from evolu_amd import _lib as L
+
+    L.check(L.load().evm_test_fault(eng.h, mode), "evm_test_fault")
 
 
 def _snapshot(store):
@@ -45,9 +56,9 @@ def test_split_ingest_rolls_back_on_phase2_failure(eng):
     store.ingest(eng.dev(ts_a), eng.dev(own_a), 0)
     before = _snapshot(store)
     flags = eng.dev(np.full(len(ts_b), 0x55, dtype=np.uint8))
-    eng.set_option(L.OPT_TEST_FAIL, 1)
+    _fault(eng, 1)
     _, st = store.ingest(eng.dev(ts_b), eng.dev(own_b), len(ts_a), flags=flags, raise_on_error=False)
-    eng.set_option(L.OPT_TEST_FAIL, 0)
+    _fault(eng, 0)
     eng.set_option(L.OPT_SERVER_PATH, 0)
     assert st == L.EVM_ENOMEM
     after = _snapshot(store)
@@ -94,7 +105,7 @@ def test_steady_state_makes_no_allocations(eng):
 def test_merge_guard_refuses_overlapping_keys(eng):
     """The merge (k_svo_b) places rows assuming the segment's stored and new
     keys are disjoint.  With K5's check against the stored rows switched off
-    (EVM_OPT_TEST_FAIL 2) a redelivered stored timestamp reaches the merge as
+    (evm_test_fault 2, include/evm_test.h) a redelivered stored timestamp reaches the merge as
     a new row: the guard must return EVM_ESTATE -- not fault, not commit --
     leave the store as it was and report nothing inserted; the same batch
     then ingests normally."""
@@ -118,9 +129,9 @@ def test_merge_guard_refuses_overlapping_keys(eng):
     for path in (0, 3):  # segments of one owner; the LDS path without segments
         eng.set_option(L.OPT_SERVER_PATH, path)
         flags = eng.dev(np.full(len(ts_b), 0x55, dtype=np.uint8))
-        eng.set_option(L.OPT_TEST_FAIL, 2)
+        _fault(eng, 2)
         _, st = store.ingest(eng.dev(ts_b), eng.dev(own_b), 10_000_000, flags=flags, raise_on_error=False)
-        eng.set_option(L.OPT_TEST_FAIL, 0)
+        _fault(eng, 0)
         assert st == L.EVM_ESTATE
         assert int(flags.cpu().numpy().astype(np.int64).sum()) == 0, "no message reported as inserted"
         for x, y in zip(before, _snapshot(store)):
@@ -139,3 +150,18 @@ def test_merge_guard_refuses_overlapping_keys(eng):
         assert np.array_equal(x, y)
     store.free()
     ref.free()
+
+
+def test_fault_hook_refused_without_test_env(eng):
+    """The fault hook is not on the product ABI: without EVM_TEST_HOOKS=1 it
+    refuses (EVM_EINVAL) and the context keeps its checks."""
+    import os
+
+    from evolu_amd import _lib as L
+
+    del os.environ["EVM_TEST_HOOKS"]
+    try:
+        assert L.load().evm_test_fault(eng.h, 2) == L.EVM_EINVAL
+    finally:
+        os.environ["EVM_TEST_HOOKS"] = "1"
+    assert L.load().evm_test_fault(eng.h, 0) == L.EVM_OK

@@ -189,10 +189,10 @@ def test_node_id_not_hex_is_handed_over_unapplied(eng):
 
 
 def test_fast_path_equals_per_request_path(eng):
-    """sync() runs a call's common requests as whole-call arrays (batch
-    decode, one ingest per round, one tree parse, one selection, the trees'
-    JSON in one device launch, batch encode); sync_per_request() runs every
-    request through the per-request path.  Same bytes, same errors, over
+    """sync() runs a call as native rounds (evm_sync_round: the bodies
+    staged to the device, decoded, ingested, their trees parsed, selected and
+    encoded there); sync_per_request() runs every request through the
+    per-request path.  Same bytes, same errors, over
     several rounds per user, a truncated body, a client tree that does not
     parse, a nodeId that is not 16 hex chars, an invalid date (500) and a
     lenient timestamp."""
@@ -216,7 +216,7 @@ def test_fast_path_equals_per_request_path(eng):
     a = SyncServer(eng, 32)
     b = SyncServer(eng, 32)
     ga, gb = a.sync(bodies), b.sync_per_request(bodies)
-    assert set(a.timing) >= {"decode", "ingest", "trees", "select", "json", "encode", "per_request"}
+    assert set(a.timing) >= {"h2d", "decode", "users", "ingest", "trees", "select", "encode", "d2h", "per_request"}
     for i, (x, y) in enumerate(zip(ga, gb)):
         if isinstance(x, (bytes, type(None))):
             assert x == y, i

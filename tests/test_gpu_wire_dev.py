@@ -280,7 +280,7 @@ def test_sync_device_equals_sync_and_the_reference(eng):
     assert all(r is True for r in res.result)
     got = res.to_host()
     assert got == want == b.sync(bodies)
-    assert set(a.timing) >= {"decode", "ingest", "trees", "select", "encode"}
+    assert set(a.timing) >= {"decode", "users", "ingest", "trees", "select", "encode"}
     # a second round of the same users: new messages, the client trees of round one
     arena2, off2 = _e2e(eng, 24, 40, 57)
     bodies2 = [arena2[int(off2[k]):int(off2[k + 1])].tobytes() for k in range(len(off2) - 1)]
@@ -343,13 +343,44 @@ def test_sync_device_mixed_with_host_calls_and_per_request_cases(eng):
     g3 = r3.to_host()
     _same(g3, b.sync(call3))
     assert isinstance(g3[0], RangeError)
-    # calls the device path hands to sync() whole
-    for call in ([b"\x0a\x05ab"] + call2[:2],
-                 [call2[0], call2[0]],
-                 [REQ(userId="nh", nodeId="xyz", merkleTree="{}").SerializeToString()] + call2[:1]):
+    # an unparsable body and a nodeId that is not hex: answered inside the
+    # device round; a userId twice: the call cut into rounds on the host
+    for call, whole in (([b"\x0a\x05ab"] + call2[:2], False),
+                        ([call2[0], call2[0]], True),
+                        ([REQ(userId="nh", nodeId="xyz", merkleTree="{}").SerializeToString()] + call2[:1], False)):
         ar, of = _arena(call)
         _same(a.sync_device(eng.dev(ar), of).to_host(), b.sync(call))
-        assert "device_fallback" in a.timing
+        assert ("device_fallback" in a.timing) == whole
     assert a.store.n_messages == b.store.n_messages
     a.close()
     b.close()
+
+
+def test_absent_or_empty_merkle_tree_is_a_500_on_both_paths(eng):
+    """index.ts:187 JSON.parse(request.merkleTree): an empty or absent field
+    (proto3 decodes it as "") throws -> that request answers 500 after its
+    addMessages committed -- on the device round exactly as on the host
+    path and the per-request path."""
+    from evolu_amd import _lib as L
+    from evolu_amd.server import SyncServer
+
+    rng = random.Random(11)
+    node = W.node_id(rng)
+    ts = W.hlc_timestamps(rng, 12, [node])
+    msgs = lambda a, b: [dict(timestamp=t, content=b"c") for t in ts[a:b]]  # noqa: E731
+    call = [REQ(messages=msgs(0, 4), userId="empty", nodeId=node, merkleTree="").SerializeToString(),
+            REQ(messages=msgs(4, 8), userId="absent", nodeId=node).SerializeToString(),
+            REQ(messages=msgs(8, 12), userId="fine", nodeId=node, merkleTree="{}").SerializeToString()]
+    a, b, c = SyncServer(eng, 8), SyncServer(eng, 8), SyncServer(eng, 8)
+    ar, of = _arena(call)
+    got = a.sync_device(eng.dev(ar), of).to_host()
+    host = b.sync(call)
+    per = c.sync_per_request(call)
+    for g in (got, host, per):
+        assert isinstance(g[0], L.EngineError) and isinstance(g[1], L.EngineError)
+        assert isinstance(g[2], bytes)
+    assert got[2] == host[2] == per[2]
+    # the rows were committed all the same (addMessages ran before getMessages)
+    assert a.store.n_messages == b.store.n_messages == c.store.n_messages == 12
+    for s_ in (a, b, c):
+        s_.close()

@@ -1,5 +1,5 @@
 """CPU checks of the C ABI library: it loads, and exports every symbol
-include/evm.h declares (no compute calls -- there is no GPU here)."""
+include/*.h declares (no compute calls -- there is no GPU here)."""
 import ctypes
 import os
 import re
@@ -10,7 +10,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    text = open(os.path.join(ROOT, "include", "evm.h")).read()
+    import glob
+
+    text = "".join(open(h).read() for h in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(evm_[a-z0-9_]+)\s*\(", text)))
 

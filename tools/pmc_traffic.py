@@ -60,30 +60,52 @@ def short(name):
         return base
     if base == "k_svo_a" and targs:
         # KLAUNCH names the template launch by its source text: "(k_svo_a<1024, true>)"
+        # (template <CAP, SRC, THREADS = SVO_THREADS, LEAF = false>)
         args = [a.strip().rstrip("u") for a in targs[1:-1].split(",")]
         args = ["SVO_CAP" if a == "4096" else a for a in args]
         if len(args) >= 2:  # the source is an int template argument: 0 records, 1 rows, 2 received records
             args[1] = {"0": "false", "1": "true", "2": "SRC_WIRE"}.get(args[1], args[1])
+        if len(args) == 4 and args[3] == "false":  # the default LEAF is not in the launch text
+            args = args[:3]
+        if len(args) == 4:  # the LEAF build names its workgroup size by the constant
+            args[2] = "SVO_THREADS" if args[2] == "256" else args[2]
         if len(args) == 3 and args[2] == "256":  # the default workgroup size is not in the launch text
             args = args[:2]
         return "(k_svo_a<%s>)" % ", ".join(args)
     return base
 
 
+def full_size(vals):
+    """The launches of the leg's own size: a bench leg also launches its
+    kernels on miniatures (warm-up shapes, self-checks on sampled owners), so
+    the figure per launch is the mean over the launches within 2x of the
+    largest -- never a miniature standing in for a full-size launch."""
+    if not vals:
+        return None, 0
+    top = max(vals)
+    big = [v for v in vals if v >= 0.5 * top]
+    return sum(big) / len(big), len(big)
+
+
 def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
-    out = {}
+    acc = {}
     for name in set(fetch) | set(write):
         k = short(name)
         if not k:
             continue
-        f = fetch.get(name, [])
-        w = write.get(name, [])
-        fb = 2.0 * 1024.0 * (sum(f) / len(f)) if f else None
-        wb = 1024.0 * (sum(w) / len(w)) if w else None
-        out[k] = {"fetch_bytes": fb, "write_bytes": wb,
-                  "bytes": (fb or 0.0) + (wb or 0.0), "launches": max(len(f), len(w))}
+        f, w = acc.setdefault(k, ([], []))
+        f.extend(fetch.get(name, []))
+        w.extend(write.get(name, []))
+    out = {}
+    for k, (f, w) in acc.items():
+        fm, fn = full_size(f)
+        wm, wn = full_size(w)
+        fb = 2.0 * 1024.0 * fm if fm is not None else None
+        wb = 1024.0 * wm if wm is not None else None
+        out[k] = {"fetch_bytes": fb, "write_bytes": wb, "bytes": (fb or 0.0) + (wb or 0.0),
+                  "launches": max(fn, wn), "all_launches": max(len(f), len(w))}
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
 
 
