@@ -781,22 +781,22 @@ int round_dev(evm_sync_server* sv, const uint8_t* arena, const u64* off_h, u32 n
   }
   const evm_tree* tree = evm_store_tree(sv->store);
   uint64_t total = 0;
-  st = evm_pb_encode_responses_dev(ctx, na, tree, owners, U64C(sel_off), U64C(sel_id), skip, ns, sbase.data(), srow.data(),
-                                   sts.data(), 48, scoff.data(), scon.data(), nullptr, 0, U64P(rout), &total);
-  if (st) return st;
-  if (total + 16 > sv->resp_bytes) {
-    if (sv->resp) block_free(ctx, sv->resp, sv->resp_bytes);
-    sv->resp = nullptr;
-    size_t bytes = total + 16;
-    sv->resp = static_cast<uint8_t*>(block_alloc(ctx, &bytes));
-    if (!sv->resp) {
-      sv->resp_bytes = 0;
-      return EVM_ENOMEM;
-    }
-    sv->resp_bytes = bytes;
-  }
-  st = evm_pb_encode_responses_dev(ctx, na, tree, owners, U64C(sel_off), U64C(sel_id), skip, ns, sbase.data(), srow.data(),
-                                   sts.data(), 48, scoff.data(), scon.data(), sv->resp, sv->resp_bytes, U64P(rout), &total);
+  int ast = EVM_OK;
+  st = encode_responses_dev(
+      ctx, na, tree, owners, U64C(sel_off), U64C(sel_id), skip, ns, sbase.data(), srow.data(), sts.data(), 48,
+      scoff.data(), scon.data(),
+      [&](uint64_t need) -> uint8_t* {  // (the round's response arena, from the context's block cache)
+        if (need + 16 > sv->resp_bytes) {
+          if (sv->resp) block_free(ctx, sv->resp, sv->resp_bytes);
+          size_t bytes = need + 16;
+          sv->resp = static_cast<uint8_t*>(block_alloc(ctx, &bytes));
+          sv->resp_bytes = sv->resp ? bytes : 0;
+          if (!sv->resp) ast = EVM_ENOMEM;
+        }
+        return sv->resp;
+      },
+      U64P(rout), &total);
+  if (!st) st = ast;
   if (st) return st;
   std::vector<u64> ro((size_t)na + 1);
   std::vector<uint8_t> hskip(na);

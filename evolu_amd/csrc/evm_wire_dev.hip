@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <functional>
 #include <vector>
 
 #include "evm_device.hpp"
@@ -1274,11 +1275,15 @@ int evm_tree_from_json_dev(evm_ctx* ctx, uint32_t n_owners, const uint8_t* json,
   return EVM_OK;
 }
 
-int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, const uint32_t* owners,
-                                const uint64_t* osel_off, const uint64_t* osel_id, const uint8_t* skip, uint32_t n_seg,
-                                const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
-                                size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
-                                uint8_t* out, size_t cap, uint64_t* out_off, uint64_t* total) {
+}  // extern "C"
+
+// SyncResponse bodies in one pass over the plan: the sizes, then `out(total)`
+// (the caller's buffer of >= total bytes, or null: sizes only), then the bytes.
+int evm::encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, const uint32_t* owners,
+                              const uint64_t* osel_off, const uint64_t* osel_id, const uint8_t* skip, uint32_t n_seg,
+                              const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
+                              size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
+                              const std::function<uint8_t*(uint64_t)>& out_for, uint64_t* out_off, uint64_t* total) {
   if (!ctx || !tree || !total || (n && (!owners || !osel_off || !out_off)) || stride < 46 ||
       (n_seg && (!seg_base || !seg_ts || !seg_coff || !seg_content)))
     return EVM_EINVAL;
@@ -1349,8 +1354,8 @@ int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, 
   }
   if (hb) return EVM_EINVAL;  // (an owner out of range, or an id in no segment)
   *total = hs[1];
+  uint8_t* out = out_for(hs[1]);
   if (!out) return EVM_OK;
-  if (hs[1] > cap) return EVM_ECAPACITY;
   if (n)
     KLAUNCH(k_resp_tree_hdr, dim3(grid_for(n, 256)), dim3(256), n, (const u64*)sel_off, (const u64*)mpos,
             (const u64*)jlen, (const u64*)doff, out, jdst);
@@ -1362,4 +1367,22 @@ int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, 
   return hip_ok(hipGetLastError());
 }
 
-}  // extern "C"
+extern "C" int evm_pb_encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, const uint32_t* owners,
+                                           const uint64_t* osel_off, const uint64_t* osel_id, const uint8_t* skip,
+                                           uint32_t n_seg, const uint64_t* seg_base, const uint64_t* const* seg_row,
+                                           const char* const* seg_ts, size_t stride,
+                                           const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
+                                           uint8_t* out, size_t cap, uint64_t* out_off, uint64_t* total) {
+  bool small = false;
+  const int st = evm::encode_responses_dev(
+      ctx, n, tree, owners, osel_off, osel_id, skip, n_seg, seg_base, seg_row, seg_ts, stride, seg_coff, seg_content,
+      [&](uint64_t need) -> uint8_t* {
+        if (out && need > cap) {
+          small = true;
+          return nullptr;
+        }
+        return out;
+      },
+      out_off, total);
+  return st ? st : small ? EVM_ECAPACITY : EVM_OK;
+}

@@ -331,17 +331,23 @@ class SyncServer:
                 sub_a, sub_o = _sub_arena(arena, off, idx)
                 done = self._host_round(sub_a, sub_o, idx, out, views, T)
                 assert done, "a round with one request per user"
-        T["other"] = time.perf_counter() - t_call - sum(v for v in T.values())
+        T["other"] = time.perf_counter() - t_call - sum(v for k, v in T.items() if not k.endswith("_call"))
         return out
 
     def _host_round(self, arena, off, idx, out, views, T) -> bool:
         """One native round over host bodies, results into out[idx[k]];
         False (nothing applied) when a user sends two of the requests."""
+        import time
+
+        t0 = time.perf_counter()
         res, roff, total = self._round_native(arena, off, _lib.SYNC_HOST)
         if res is None:
             return False
+        T["round_call"] = T.get("round_call", 0.0) + time.perf_counter() - t0
         self._add_timing(T)
+        t0 = time.perf_counter()
         resp = self._fetch(total) if total else None
+        T["fetch_call"] = T.get("fetch_call", 0.0) + time.perf_counter() - t0
         T["d2h"] += self._part_ms(7) / 1e3
         rb = memoryview(resp) if views and resp is not None else resp
         ro = roff.tolist()

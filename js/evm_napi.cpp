@@ -707,7 +707,8 @@ napi_value PbDecode(napi_env env, napi_callback_info info) {
   napi_value tl = typed(env, napi_uint32_array, n, 4, &tlp);
   napi_value content = typed(env, napi_uint8_array, si.content_bytes, 1, &cp);
   std::vector<uint64_t> off(n + 1), toff(n);
-  st = evm_pb_split(kind, (const uint8_t*)body, bl, (char*)tsp, 48, (uint32_t*)tlp, toff.data(), off.data(),
+  char none[48];  // (a body without messages: a zero-length typed array may have no data pointer)
+  st = evm_pb_split(kind, (const uint8_t*)body, bl, n ? (char*)tsp : none, 48, (uint32_t*)tlp, toff.data(), off.data(),
                     (uint8_t*)cp);
   if (st) return throw_status(env, st, "evm_pb_split");
   double* op;

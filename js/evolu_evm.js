@@ -332,7 +332,9 @@ class SyncServer {
         while (rounds.length <= k) rounds.push([]);
         rounds[k].push(i);
       });
-      for (const idx of rounds) this._round(idx.map((i) => bodies[i]), idx, out);
+      for (const idx of rounds) {
+        if (!this._round(idx.map((i) => bodies[i]), idx, out)) throw new Error("syncRound: a userId twice in a round");
+      }
     }
     return out;
   }
@@ -342,7 +344,6 @@ class SyncServer {
     const arena = new Uint8Array(off[bodies.length]);
     bodies.forEach((b, i) => arena.set(b, off[i]));
     const r = addon.syncRound(this.engine.ctx, this.h, arena, off);
-    if (process.env.EVM_SYNC_TRACE) console.error("syncRound", bodies.length, r.status, r.results && Array.from(r.results));
     if (r.status === EVM_EROUNDS) return false;
     for (let k = 0; k < bodies.length; k++) {
       const code = r.results[k];
