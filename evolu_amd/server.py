@@ -47,6 +47,7 @@ user as stale.
 from __future__ import annotations
 
 import ctypes as C
+from collections.abc import Sequence as _SequenceABC
 from typing import Dict, List, Optional, Sequence, Set, Union
 
 import numpy as np
@@ -151,6 +152,39 @@ def _sub_arena(arena: np.ndarray, off: np.ndarray, idx: np.ndarray):
     np.cumsum(ln, out=sub_o[1:])
     sub_a = np.concatenate([arena[int(off[i]):int(off[i + 1])] for i in idx.tolist()] or [np.zeros(0, np.uint8)])
     return np.ascontiguousarray(sub_a if len(sub_a) else np.zeros(1, np.uint8)), sub_o
+
+
+class Responses(_SequenceABC):
+    """sync_arena(views=True)'s answer: result k is response k's bytes as a
+    memoryview into one host response arena (made when read), or what sync()
+    returns for it (an exception object, a HandedOver, None)."""
+
+    def __init__(self, n: int):
+        self.n = n
+        self.arena = None  # memoryview of the response arena, off: uint64 [n + 1] (every request answered)
+        self.off = None
+        self.items: Optional[List[Result]] = None  # (or each result on its own)
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            return [self[i] for i in range(*k.indices(self.n))]
+        if k < 0:
+            k += self.n
+        if not 0 <= k < self.n:
+            raise IndexError(k)
+        if self.items is not None:
+            return self.items[k]
+        if self.arena is not None:
+            return self.arena[int(self.off[k]):int(self.off[k + 1])]
+        return None
+
+    def __setitem__(self, k, v):
+        if self.items is None:
+            self.items = [self[i] for i in range(self.n)]
+        self.items[k] = v
 
 
 class DeviceResponses:
@@ -321,7 +355,7 @@ class SyncServer:
         t_call = time.perf_counter()
         T = self.timing = dict.fromkeys(TIMING_PARTS + ("per_request", "other"), 0.0)
         n = len(off) - 1
-        out: List[Result] = [None] * n
+        out = Responses(n) if views else [None] * n
         if n == 0:
             return out
         if not self._host_round(arena, off, np.arange(n), out, views, T):
@@ -350,14 +384,11 @@ class SyncServer:
         T["fetch_call"] = T.get("fetch_call", 0.0) + time.perf_counter() - t0
         T["d2h"] += self._part_ms(7) / 1e3
         rb = memoryview(resp) if views and resp is not None else resp
-        ro = roff.tolist()
         ok = self._ok
-        if ok is not None and len(idx) == len(out) and ok.all():  # (the common case: every request answered)
-            if views:
-                out[:] = [rb[a:b] for a, b in zip(ro[:-1], ro[1:])]
-            else:
-                out[:] = [rb[a:b].tobytes() for a, b in zip(ro[:-1], ro[1:])]
+        if views and isinstance(out, Responses) and ok is not None and len(idx) == len(out) and ok.all():
+            out.arena, out.off = rb, roff  # (the common case: every request answered, views made on access)
             return True
+        ro = roff.tolist()
         for k, i in enumerate(idx.tolist()):
             r = res[k]
             if r is True:

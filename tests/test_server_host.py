@@ -55,3 +55,20 @@ def test_device_responses_view():
     # a call answered on the host path (no device arena)
     r3 = DeviceResponses(None, np.zeros(3, dtype=np.uint64), [b"x", None])
     assert r3.to_host() == [b"x", None]
+
+
+def test_responses_sequence_views_and_overrides():
+    """sync_arena(views=True)'s answer: memoryviews into one arena, made on
+    access; a per-request result set on it overrides that entry."""
+    from evolu_amd.server import Responses
+
+    r = Responses(3)
+    r.arena = memoryview(b"aabbbc")
+    r.off = np.array([0, 2, 5, 6], dtype=np.uint64)
+    assert [bytes(x) for x in r] == [b"aa", b"bbb", b"c"] and len(r) == 3
+    assert isinstance(r[0], memoryview) and bytes(r[-1]) == b"c"
+    err = RangeError("x")
+    r[1] = err
+    assert r[1] is err and bytes(r[2]) == b"c" and [bytes(x) for x in r[0:1]] == [b"aa"]
+    with pytest.raises(IndexError):
+        r[3]
