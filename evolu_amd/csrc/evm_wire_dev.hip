@@ -333,46 +333,75 @@ __global__ void k_pb_rows(const uint8_t* __restrict__ arena, const u64* __restri
 // k_pb_rows from the scan's slots: a wave per body, a lane per message
 __global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
                                                      const int32_t* __restrict__ status, const u64* __restrict__ msg_base,
-                                                     const u64* __restrict__ slots, const u32* __restrict__ owner_of,
-                                                     char* __restrict__ ts, u64 stride, u64* __restrict__ cat,
-                                                     u64* __restrict__ clen, u32* __restrict__ owner, u32* __restrict__ bad) {
+                                                     const u64* __restrict__ content_base, const u64* __restrict__ slots,
+                                                     const u32* __restrict__ owner_of, char* __restrict__ ts, u64 stride,
+                                                     u64* __restrict__ content_off, uint8_t* __restrict__ content,
+                                                     u32* __restrict__ owner, u32* __restrict__ bad) {
   const u32 lane = threadIdx.x & 63;
   for (u32 k = blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += gridDim.x * 4) {
     if (status[k]) continue;
     const u64 a = off[k], b = off[k + 1], m0 = msg_base[k], mn = msg_base[k + 1] - m0;
     const u64 s0 = a / PB_MIN_MSG;
     const u32 ow = owner_of ? owner_of[k] : 0u;
+    u64 cpos = content_base[k];  // the body's contents go here, message after message
     if (mn > b / PB_MIN_MSG - s0) {  // (a message shorter than 50 bytes: its timestamp is not 46)
       if (lane == 0) atomicOr(bad, 1u);
       for (u64 i = lane; i < mn; i += 64) {  // (its rows empty, no content: the call fails)
         u64* row = reinterpret_cast<u64*>(ts + (m0 + i) * stride);
         for (u64 j = 0; j < stride; j += 8) row[j >> 3] = ~0ull;
-        cat[m0 + i] = 0;
-        clen[m0 + i] = 0;
+        content_off[m0 + i] = cpos;
         if (owner) owner[m0 + i] = ow;
       }
       continue;
     }
-    for (u64 i = lane; i < mn; i += 64) {
-      const uint8_t* f = arena + slots[s0 + i];
-      Win win;
-      win.init(arena + b);
-      DReader r{f, arena + b, true, &win};
-      r.varint();  // (the field's tag: 1, length-delimited -- the scan read it)
-      const uint8_t* q;
-      u64 len;
-      r.bytes(&q, &len);
-      DMsg msg;
-      d_read_msg(q, len, &msg, &win);
-      const u64 m = m0 + i;
-      u64* row = reinterpret_cast<u64*>(ts + m * stride);
-      const bool std46 = msg.ts_len == 46;
-      for (int j = 0; j < 5; ++j) row[j] = std46 ? win.get8(msg.ts + 8 * j) : ~0ull;
-      row[5] = (std46 ? win.get8(msg.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
-      for (u64 j = 48; j < stride; j += 8) row[j >> 3] = 0ull;
-      cat[m] = msg.content ? (u64)(msg.content - arena) : 0ull;
-      clen[m] = msg.content_len;
-      if (owner) owner[m] = ow;
+    // 64 messages at a time, a lane each (mn is wave-uniform: every lane runs
+    // every chunk, so the contents' prefix sum is a wave scan)
+    for (u64 i0 = 0; i0 < mn; i0 += 64) {
+      const u64 i = i0 + lane;
+      u64 cl = 0;
+      const uint8_t* csrc = nullptr;
+      if (i < mn) {
+        const uint8_t* f = arena + slots[s0 + i];
+        Win win;
+        win.init(arena + b);
+        DReader r{f, arena + b, true, &win};
+        r.varint();  // (the field's tag: 1, length-delimited -- the scan read it)
+        const uint8_t* q;
+        u64 len;
+        r.bytes(&q, &len);
+        DMsg msg;
+        d_read_msg(q, len, &msg, &win);
+        const u64 m = m0 + i;
+        u64* row = reinterpret_cast<u64*>(ts + m * stride);
+        const bool std46 = msg.ts_len == 46;
+        for (int j = 0; j < 5; ++j) row[j] = std46 ? win.get8(msg.ts + 8 * j) : ~0ull;
+        row[5] = (std46 ? win.get8(msg.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
+        for (u64 j = 48; j < stride; j += 8) row[j >> 3] = 0ull;
+        csrc = msg.content;
+        cl = msg.content ? msg.content_len : 0;
+        if (owner) owner[m] = ow;
+      }
+      // this message's content offset: the body's base + the contents before it
+      u64 x = cl;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const u64 y = __shfl_up(x, d, 64);
+        if ((int)lane >= d) x += y;
+      }
+      const u64 dst = cpos + x - cl;
+      cpos += __shfl(x, 63, 64);
+      if (i < mn) {
+        content_off[m0 + i] = dst;
+        // the content, 16 bytes at a time with every load issued before the stores
+        for (u64 j0 = 0; j0 < cl; j0 += 16) {
+          uint8_t v[16];
+#pragma unroll
+          for (int t = 0; t < 16; ++t) v[t] = j0 + t < cl ? csrc[j0 + t] : 0;
+#pragma unroll
+          for (int t = 0; t < 16; ++t)
+            if (j0 + t < cl) content[dst + j0 + t] = v[t];
+        }
+      }
     }
   }
 }
@@ -382,7 +411,16 @@ __global__ void k_pb_content(const uint8_t* __restrict__ arena, const u64* __res
   for (u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x; m < N; m += (u64)gridDim.x * blockDim.x) {
     const u64 d = content_off[m], len = content_off[m + 1] - d;
     const uint8_t* src = arena + cat[m];
-    for (u64 j = 0; j < len; ++j) content[d + j] = src[j];
+    // 16 bytes at a time, every load issued before the stores (a byte loop
+    // waited out one load latency per byte: 2.2 ms for config 3's round)
+    for (u64 j0 = 0; j0 < len; j0 += 16) {
+      uint8_t b[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) b[k] = j0 + k < len ? src[j0 + k] : 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (j0 + k < len) content[d + j0 + k] = b[k];
+    }
   }
 }
 
@@ -1180,7 +1218,6 @@ int evm_pb_split_index_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const u
       stride < 48 || stride % 16 || (kind != EVM_PB_SYNC_REQUEST && kind != EVM_PB_SYNC_RESPONSE))
     return EVM_EINVAL;
   if (!n) return EVM_OK;
-  (void)content_base;  // (the content offsets come from one scan over every message's length)
   Scratch S(ctx);
   int st;
   u64 N = 0;
@@ -1190,14 +1227,20 @@ int evm_pb_split_index_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const u
     if ((st = land_words(ctx, l))) return st;
   }
   u32* bad = S.alloc<u32>(1);
-  u64* cat = S.alloc<u64>(N + 1);
-  u64* clen = S.alloc<u64>(N + 1);
-  if (!bad || !cat || !clen) return EVM_ENOMEM;
+  if (!bad) return EVM_ENOMEM;
   HIPR(hipMemsetAsync(bad, 0, sizeof(u32), ctx->stream));
+  u64* co = reinterpret_cast<u64*>(content_off);
   if (slots) {
+    // rows, contents and their offsets in one pass (the bodies' content bases
+    // from the caller): no offsets array for a second kernel, no scan
     KLAUNCH(k_pb_rows_idx, dim3(grid_for(n, 4, 1 << 16)), dim3(256), arena, (const u64*)off, n, status,
-            (const u64*)msg_base, (const u64*)slots, owner_of, ts, (u64)stride, cat, clen, owner, bad);
+            (const u64*)msg_base, (const u64*)content_base, (const u64*)slots, owner_of, ts, (u64)stride, co, content,
+            owner, bad);
+    HIPR(hipMemcpyAsync(co + N, content_base + n, sizeof(u64), hipMemcpyDeviceToDevice, ctx->stream));
   } else {
+    u64* cat = S.alloc<u64>(N + 1);
+    u64* clen = S.alloc<u64>(N + 1);
+    if (!cat || !clen) return EVM_ENOMEM;
     u64* mat = S.alloc<u64>(N + 1);
     u32* mlen = S.alloc<u32>(N + 1);
     if (!mat || !mlen) return EVM_ENOMEM;
@@ -1206,11 +1249,10 @@ int evm_pb_split_index_dev(evm_ctx* ctx, int kind, const uint8_t* arena, const u
     if (N)
       KLAUNCH(k_pb_rows, dim3(grid_for(N, 256, 1 << 16)), dim3(256), arena, (const u64*)mat, (const u32*)mlen, N, ts,
               (u64)stride, cat, clen);
+    if ((st = scan_exclusive<u64, OpAdd>(ctx, S, clen, N, co, co + N))) return st;
+    if (N) KLAUNCH(k_pb_content, dim3(grid_for(N, 256, 1 << 16)), dim3(256), arena, (const u64*)cat, (const u64*)co, N,
+                   content);
   }
-  u64* co = reinterpret_cast<u64*>(content_off);
-  if ((st = scan_exclusive<u64, OpAdd>(ctx, S, clen, N, co, co + N))) return st;
-  if (N) KLAUNCH(k_pb_content, dim3(grid_for(N, 256, 1 << 16)), dim3(256), arena, (const u64*)cat, (const u64*)co, N,
-                 content);
   u32 hb = 0;
   {
     LandList l;

@@ -35,14 +35,22 @@ print("bodies ready: %d bytes" % int(off[-1]), flush=True)
 a_d = torch.from_numpy(arena).to(dev)
 pick = np.linspace(0, len(off) - 2, 8).round().astype(np.int64)
 ref = None
-for rep in range(2):
+for rep in range(3):
     srv = SyncServer(eng, owners)
+    if rep == 2:  # (a profiled round: the kernels' times)
+        eng.prof_enable(True)
+        eng.prof_reset()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = srv.sync_device(a_d, off)
     torch.cuda.synchronize()
-    print("device round %.1f ms" % ((time.perf_counter() - t0) * 1e3),
-          {k: round(v * 1e3, 2) for k, v in srv.timing.items()}, flush=True)
+    if rep == 2:
+        prof = eng.prof_report()
+        eng.prof_enable(False)
+        print("kernels ms", {k: round(v[0], 3) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])[:14]})
+    else:
+        print("device round %.1f ms" % ((time.perf_counter() - t0) * 1e3),
+              {k: round(v * 1e3, 2) for k, v in srv.timing.items()}, flush=True)
     ref = [res.get(int(k)) for k in pick]
     srv.close()
 del a_d
