@@ -142,6 +142,7 @@ def parse():
                          "GPU 0 through evm_dist_hub (not a multi-GPU measurement)")
     ap.add_argument("--extra", type=int, default=1, help="N=1 client run: add the config-1 and config-3 legs")
     ap.add_argument("--e2e", type=int, default=1, help="config 3 leg: add the end-to-end SyncServer round")
+    ap.add_argument("--reingest", type=int, default=1, help="config 3 leg: add the reingest rounds (a growing store)")
     ap.add_argument("--shape", choices=["auto", "config2", "config4c"], default="auto",
                     help="client workload: config2 = one owner per GPU, no exchange; config4c = owners_per_rank "
                          "owners per GPU, every rank's batch holds messages of all the job's owners and routes them "
@@ -2224,7 +2225,8 @@ def server_run(a, rank, world, local, owners, per_owner, zipf, request, cpu=Fals
         for k in ("metric", "n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
             out.pop(k)
     if zipf <= 0:
-        out["reingest"] = reingest(eng, a, ts_r, lown, owners, per_owner, request, flags)
+        if getattr(a, "reingest", 1):
+            out["reingest"] = reingest(eng, a, ts_r, lown, owners, per_owner, request, flags)
         if getattr(a, "e2e", 1) and request >= per_owner:
             out["e2e"] = e2e_leg(eng, ts_np, owner_np, client, ms)
     eng.close()

@@ -710,6 +710,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   auto rl_get = [&](u32 i) -> u32 { return s_rl[i] & RLM; };
   __shared__ u64 s_red[2 * (THREADS / 64)];
   __shared__ u32 tmp[THREADS / 64 + 1];
+  __shared__ u64 tmp64[THREADS / 64 + 1];
   __shared__ uint16_t s_b3[243];  // base-3 digits of 0..242 (the leaves' key codes)
   const u32 s = list ? list[blockIdx.x] : blockIdx.x;  // pass 2: only the segments pass 1 deferred
   const u32 o = seg_owner(sv, s);
@@ -1084,13 +1085,21 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     }
     __syncthreads();
   }
-  // first occurrences not yet stored; thread t owns sorted positions t*PER ..
+  // first occurrences not yet stored; thread t owns sorted positions t, t +
+  // THREADS, ... (row r = the positions r * THREADS ..): each row's stores
+  // below are one coalesced run per wave, and the LDS reads are conflict-free
+  // (ownership of t * PER .. made every store instruction a 32-B-strided
+  // partial-line write: the row stores cost K5 a quarter of its time)
   u64 mt[PER], mh[PER];
   u32 ml[PER], mb[PER], mhash[PER];
-  u32 insm = 0, c = 0;
+  u32 insm = 0;
+  constexpr int NPK = (PER + 3) / 4;  // per-row counts packed 4 to a u64 (16 bits each: <= THREADS)
+  u64 cpk[NPK];
+#pragma unroll
+  for (int j = 0; j < NPK; ++j) cpk[j] = 0;
 #pragma unroll
   for (int r = 0; r < PER; ++r) {
-    const u32 p = threadIdx.x * PER + r;
+    const u32 p = threadIdx.x + r * THREADS;
     mt[r] = mh[r] = 0;
     ml[r] = mb[r] = mhash[r] = 0;
     if (p < m) {
@@ -1109,7 +1118,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       }
       if (ins) {
         insm |= 1u << r;
-        ++c;
+        cpk[r >> 2] += 1ull << (16 * (r & 3));
       }
     }
   }
@@ -1117,8 +1126,22 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   // divisions of the offsets from a whole-minute base (spans < 2^32 ms)
   const u64 base_min = (tmin >> 16) / 60000ull, base_ms = base_min * 60000ull;
   const bool narrow = ((tmax >> 16) - base_ms) >> 32 == 0;
-  u32 M;
-  u32 q = block_inclusive_scan<u32>(c, tmp, OpAdd<u32>(), &M) - c;  // (its barriers free the LDS arrays)
+  // each row's inserted rows before this thread's (packed block scans; their
+  // barriers free the LDS arrays), then the rows' bases from the totals
+  u32 qr[PER];
+  u32 M = 0;
+#pragma unroll
+  for (int j = 0; j < NPK; ++j) {
+    u64 tot;
+    const u64 ex = block_inclusive_scan<u64>(cpk[j], tmp64, OpAdd<u64>(), &tot) - cpk[j];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      if (4 * j + f < PER) {
+        qr[4 * j + f] = M + (u32)((ex >> (16 * f)) & 0xFFFFull);
+        M += (u32)((tot >> (16 * f)) & 0xFFFFull);
+      }
+    }
+  }
   u32* s_min = reinterpret_cast<u32*>(s_k);  // inserted rows, sorted: minute
   u32* s_hq = s_min + CAP;                   //                        hash
   u32* s_lx = reinterpret_cast<u32*>(s_rh);  // per leaf: XOR
@@ -1126,7 +1149,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
   for (u32 t = threadIdx.x; t < CAP; t += THREADS) s_lx[t] = 0;
 #pragma unroll
   for (int r = 0; r < PER; ++r) {
-    const u32 p = threadIdx.x * PER + r;
+    const u32 p = threadIdx.x + r * THREADS;
     if (p < m) {
       const bool ins = (insm >> r) & 1u;
       const u32 ob = orig ? orig[mb[r]] : mb[r];  // the message's index in the caller's batch
@@ -1134,6 +1157,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
       // only the duplicates (the minority) need a random 1-B store
       if (!ins || !flags_preset) flags[ob] = ins ? (uint8_t)EVM_MSG_INS : (uint8_t)0;
       if (ins) {
+        const u32 q = qr[r];
         const u64 w = a + q;
         n_tc[w] = mt[r];
         n_hi[w] = mh[r];
@@ -1143,28 +1167,46 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
         s_min[q] = narrow ? (u32)base_min + (u32)((mt[r] >> 16) - base_ms) / 60000u
                           : (u32)((mt[r] >> 16) / 60000ull);  // == rec.minute on the native domain
         s_hq[q] = mhash[r];
-        ++q;
       }
     }
   }
   __syncthreads();
-  // leaves: runs of one minute among the inserted rows (sorted by millis)
-  u32 hm = 0, hc = 0;
+  // leaves: runs of one minute among the inserted rows (sorted by millis);
+  // every row's leaf = the run heads at or before it (packed scans again)
+  u32 hm = 0;
+  u64 hpk[NPK];
+#pragma unroll
+  for (int j = 0; j < NPK; ++j) hpk[j] = 0;
 #pragma unroll
   for (int r = 0; r < PER; ++r) {
-    const u32 p = threadIdx.x * PER + r;
+    const u32 p = threadIdx.x + r * THREADS;
     if (p < M && (p == 0 || s_min[p] != s_min[p - 1])) {
       hm |= 1u << r;
-      ++hc;
+      hpk[r >> 2] += 1ull << (16 * (r & 3));
     }
   }
-  u32 NL;
-  int lid = (int)(block_inclusive_scan<u32>(hc, tmp, OpAdd<u32>(), &NL) - hc) - 1;
+  u32 lidr[PER];
+  u32 NL = 0;
+#pragma unroll
+  for (int j = 0; j < NPK; ++j) {
+    u64 tot;
+    const u64 inc = block_inclusive_scan<u64>(hpk[j], tmp64, OpAdd<u64>(), &tot);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      if (4 * j + f < PER) {
+        lidr[4 * j + f] = NL + (u32)((inc >> (16 * f)) & 0xFFFFull) - 1u;  // (the row's head count at or before it)
+        NL += (u32)((tot >> (16 * f)) & 0xFFFFull);
+      }
+    }
+  }
 #pragma unroll
   for (int r = 0; r < PER; ++r) {
-    const u32 p = threadIdx.x * PER + r;
+    const u32 p = threadIdx.x + r * THREADS;
     if (p < M) {
-      if ((hm >> r) & 1u) s_lm[++lid] = s_min[p];
+      // (a row's leaf: the last head at or before it -- in an earlier row of
+      // positions when no head in this row precedes it)
+      u32 lid = lidr[r];
+      if ((hm >> r) & 1u) s_lm[lid] = s_min[p];
       atomicXor(&s_lx[lid], s_hq[p]);
     }
   }
@@ -1209,7 +1251,9 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     }
     l_ck[lb0 + l] = code;
     l_xr[lb0 + l] = (int32_t)s_lx[l];
-    l_dup[lb0 + l] = dup ? 1 : 0;
+    // (a gapped tree -- the empty store's, g_off -- is final here: no merge or
+    // copy reads the marks, and no leaf of an empty tree is a duplicate)
+    if (!g_off) l_dup[lb0 + l] = dup ? 1 : 0;
     dups += dup ? 1u : 0u;
     lx ^= s_lx[l];
   }
