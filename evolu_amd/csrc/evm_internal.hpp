@@ -379,6 +379,15 @@ int tree_compact(evm_ctx* ctx, const evm_tree* t);
 // evm_json_dev.hip: per requested owner its tree JSON's length (device len[n];
 // *bad |= 1 for an owner out of range) and the plan the emit follows (arrays
 // in S); the texts written at out + off[j]
+// A client tree text of len bytes has at most len / 14 nodes (`"0":{"hash":0}`
+// is the shortest non-root node): its leaf slots in a parsed tree, with the
+// owner's prefix slot.
+constexpr u32 JP_MIN_NODE = 14;
+__host__ __device__ inline u64 json_slot_bound(u64 len) { return len / JP_MIN_NODE + 2; }
+int json_tree_slots(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* len, u64** slots);
+int json_tree_parse(evm_ctx* ctx, u32 n_owners, const uint8_t* json, const u64* at, const u64* len, const u64* slots,
+                    int32_t* status, evm_tree* t, u64* nl);
+
 struct JsonPlan {
   uint32_t n = 0;             // (the texts are placed by the caller from the lengths)
   uint16_t* plen = nullptr;   // each leaf's piece length, by leaf slot (in the caller's Scratch)

@@ -225,18 +225,16 @@ __global__ void k_fill_u32(u32* p, size_t n, u32 v) {
 enum : uint8_t { RC_ACTIVE = 0, RC_OUT = 1, RC_REJECTED = 2, RC_ETREE = 3, RC_UNSORTED = 4 };
 
 // at/len of each included request's client tree (by slot; the kernel that
-// parses reads the texts where they lie), the owners the ingest rejected
+// parses reads the texts where they lie).  It runs beside the ingest, so the
+// owners the ingest rejects are parsed too and turned away by k_sync_reject.
 __global__ void k_sync_trees(const u64* __restrict__ off, const evm_pb_sync* __restrict__ info, u32 n,
-                             const uint8_t* __restrict__ incl, const u32* __restrict__ slot,
-                             const uint8_t* __restrict__ ostat, u64* __restrict__ at, u64* __restrict__ len,
-                             uint8_t* __restrict__ rc) {
+                             const uint8_t* __restrict__ incl, const u32* __restrict__ slot, u64* __restrict__ at,
+                             u64* __restrict__ len, uint8_t* __restrict__ rc) {
   for (u32 r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
     uint8_t c = RC_OUT;
     if (incl[r]) {
       const u32 s = slot[r];
-      if (ostat[s]) {
-        c = RC_REJECTED;
-      } else if (info[r].tree_len == 0) {
+      if (info[r].tree_len == 0) {
         c = RC_ETREE;  // JSON.parse("") throws (an absent merkleTree decodes as "")
       } else {
         at[s] = off[r] + info[r].tree_off;
@@ -246,6 +244,14 @@ __global__ void k_sync_trees(const u64* __restrict__ off, const evm_pb_sync* __r
     }
     rc[r] = c;
   }
+}
+
+// the owners the ingest rejected (a row outside the domain: the request's
+// transaction rolled back) answer nothing, whatever their trees
+__global__ void k_sync_reject(u32 n, const uint8_t* __restrict__ incl, const u32* __restrict__ slot,
+                              const uint8_t* __restrict__ ostat, uint8_t* __restrict__ rc) {
+  for (u32 r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x)
+    if (incl[r] && ostat[slot[r]]) rc[r] = RC_REJECTED;
 }
 
 // the parse's verdict per request; the requester's nodeId and the active
@@ -465,6 +471,10 @@ struct evm_sync_server {
   size_t hbuf_bytes = 0;
   // the last round's wall time by part (ms): h2d, decode, users, ingest, trees, select, encode, d2h
   double part_ms[8] = {};
+  // the round's second stream: the client trees are parsed there while the
+  // messages are split and ingested on the context's stream
+  hipStream_t ps = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace {
@@ -639,6 +649,60 @@ int round_dev(evm_sync_server* sv, const uint8_t* arena, const u64* off_h, u32 n
   HIPR(hipMemcpyAsync(cb_d, cbase.data(), sizeof(u64) * ((size_t)n + 1), hipMemcpyHostToDevice, ctx->stream));
   HIPR(hipMemcpyAsync(incl_d, incl.data(), n, hipMemcpyHostToDevice, ctx->stream));
   HIPR(hipMemsetAsync(ostat, 0, O, ctx->stream));
+  // ---- getMerkleTree's client side, forked: the requests' trees parsed where
+  // they lie, on the round's second stream (its scratch from S, the tree sized
+  // on the host from the texts' lengths: nothing on it waits for the host)
+  u64* at = S.alloc<u64>(O);
+  u64* ln = S.alloc<u64>(O);
+  int32_t* tst = S.alloc<int32_t>(O);
+  uint8_t* rc = S.alloc<uint8_t>(n);
+  uint8_t* node = S.alloc<uint8_t>((size_t)O * 16);
+  uint8_t* active = S.alloc<uint8_t>(O);
+  u64* nl = S.alloc<u64>(1);
+  if (!at || !ln || !tst || !rc || !node || !active || !nl) return EVM_ENOMEM;
+  u64 tcap = 2ull * O;  // (json_slot_bound summed over the owners: an owner without a text takes 2)
+  for (u32 r = 0; r < n; ++r)
+    if (incl[r]) tcap += json_slot_bound(info[r].tree_len) - 2;
+  evm_tree* client = nullptr;
+  struct Fork {  // the parse stream joined (and the tree freed on a failure) on every path out
+    evm_sync_server* sv;
+    evm_tree** client;
+    bool open = false, keep = false;
+    void join() {
+      if (open) (void)hipStreamWaitEvent(sv->ctx->stream, sv->ev_join, 0);
+      open = false;
+    }
+    ~Fork() {
+      if (open) (void)hipStreamSynchronize(sv->ps);
+      join();
+      if (!keep && *client) {
+        (void)hipStreamSynchronize(sv->ctx->stream);
+        evm_tree_free(sv->ctx, *client);
+        *client = nullptr;
+      }
+    }
+  } fork{sv, &client};
+  {
+    HIPR(hipEventRecord(sv->ev_fork, ctx->stream));
+    HIPR(hipStreamWaitEvent(sv->ps, sv->ev_fork, 0));
+    fork.open = true;
+    const hipStream_t main = ctx->stream;
+    ctx->stream = sv->ps;  // (launches only until it is restored: no host sync on either stream)
+    u64* slots = nullptr;
+    int pst2 = hip_ok(hipMemsetAsync(at, 0, sizeof(u64) * O, ctx->stream));
+    if (!pst2) pst2 = hip_ok(hipMemsetAsync(ln, 0, sizeof(u64) * O, ctx->stream));
+    if (!pst2) pst2 = hip_ok(hipMemsetAsync(node, '0', (size_t)O * 16, ctx->stream));
+    if (!pst2) pst2 = hip_ok(hipMemsetAsync(active, 0, O, ctx->stream));
+    if (!pst2) {
+      KLAUNCH(k_sync_trees, dim3(grid_for(n, 256)), dim3(256), off_d, info_d, n, incl_d, slot_d, at, ln, rc);
+      pst2 = json_tree_slots(ctx, S, O, ln, &slots);
+    }
+    if (!pst2) pst2 = tree_alloc_gapped(ctx, O, std::max<u64>(tcap, 1), &client);
+    if (!pst2) pst2 = json_tree_parse(ctx, O, arena, at, ln, slots, tst, client, nl);
+    if (!pst2) pst2 = hip_ok(hipEventRecord(sv->ev_join, ctx->stream));
+    ctx->stream = main;
+    if (pst2) return pst2;
+  }
   // ---- the rows and contents of the round (a new log segment) + addMessages
   if (N) {
     SyncSeg g;
@@ -658,26 +722,20 @@ int round_dev(evm_sync_server* sv, const uint8_t* arena, const u64* off_h, u32 n
     sv->segs.push_back(g);
     sv->next_id += N;
   }
-  HIPR(hipStreamSynchronize(ctx->stream));
   stamp(3);
-  // ---- getMerkleTree's client side: the requests' trees, parsed where they lie
-  u64* at = S.alloc<u64>(O);
-  u64* ln = S.alloc<u64>(O);
-  int32_t* tst = S.alloc<int32_t>(O);
-  uint8_t* rc = S.alloc<uint8_t>(n);
-  uint8_t* node = S.alloc<uint8_t>((size_t)O * 16);
-  uint8_t* active = S.alloc<uint8_t>(O);
-  if (!at || !ln || !tst || !rc || !node || !active) return EVM_ENOMEM;
-  HIPR(hipMemsetAsync(at, 0, sizeof(u64) * O, ctx->stream));
-  HIPR(hipMemsetAsync(ln, 0, sizeof(u64) * O, ctx->stream));
-  HIPR(hipMemsetAsync(node, '0', (size_t)O * 16, ctx->stream));
-  HIPR(hipMemsetAsync(active, 0, O, ctx->stream));
-  KLAUNCH(k_sync_trees, dim3(grid_for(n, 256)), dim3(256), off_d, info_d, n, incl_d, slot_d, ostat, at, ln, rc);
-  evm_tree* client = nullptr;
-  if ((st = evm_tree_from_json_dev(ctx, O, arena, U64C(at), U64C(ln), tst, &client))) return st;
+  // ---- the parse joined: the ingest's rejections, the parse's verdicts
+  fork.join();
+  KLAUNCH(k_sync_reject, dim3(grid_for(n, 256)), dim3(256), n, incl_d, slot_d, ostat, rc);
   KLAUNCH(k_sync_active, dim3(grid_for(n, 256)), dim3(256), arena, off_d, info_d, n, slot_d, tst, rc, node, active);
   HIPR(hipMemcpyAsync(hrc, rc, n, hipMemcpyDeviceToHost, ctx->stream));
+  u64 hnl = 0;
+  HIPR(hipMemcpyAsync(&hnl, nl, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
+  client->n_leaves = hnl;
+  auto free_client = [&]() {
+    if (client) evm_tree_free(ctx, client);
+    client = nullptr;
+  };
   // texts whose keys are out of order (valid JSON JSON.stringify never
   // writes): the host parser reads them, merged into the device's trees
   std::vector<u32> uns;
@@ -709,13 +767,13 @@ int round_dev(evm_sync_server* sv, const uint8_t* arena, const u64* off_h, u32 n
     }
     evm_tree* ht = nullptr;
     if ((st = evm_tree_from_json(ctx, O, ptr.data(), lens.data(), &ht))) {
-      evm_tree_free(ctx, client);
+      free_client();
       return st;
     }
     evm_tree* merged = nullptr;
     st = evm_tree_merge(ctx, client, ht, &merged);
     evm_tree_free(ctx, ht);
-    evm_tree_free(ctx, client);
+    free_client();
     if (st) return st;
     client = merged;
     for (size_t j = 0; j < uns.size(); ++j) {
@@ -754,13 +812,13 @@ int round_dev(evm_sync_server* sv, const uint8_t* arena, const u64* off_h, u32 n
   uint8_t* skip = S.alloc<uint8_t>(na);
   u64* rout = S.alloc<u64>((size_t)na + 1);
   if (!diff || !sel_off || !sel_id || !ans_d || !owners || !skip || !rout) {
-    evm_tree_free(ctx, client);
+    free_client();
     return EVM_ENOMEM;
   }
   uint64_t n_sel = 0;
   st = evm_server_select(ctx, sv->store, client, reinterpret_cast<const char*>(node), active, diff, U64P(sel_off),
                          U64P(sel_id), nst + 1, &n_sel);
-  evm_tree_free(ctx, client);
+  free_client();
   if (st) return st;
   HIPR(hipStreamSynchronize(ctx->stream));
   stamp(5);
@@ -837,7 +895,10 @@ int evm_sync_create(evm_ctx* ctx, evm_store* store, evm_sync_server** out) {
             hipMalloc(reinterpret_cast<void**>(&s->koff), sizeof(u64) * std::max<u32>(O, 1)) == hipSuccess &&
             hipMalloc(reinterpret_cast<void**>(&s->klen), sizeof(u32) * std::max<u32>(O, 1)) == hipSuccess &&
             hipMalloc(reinterpret_cast<void**>(&s->claim), sizeof(u32) * std::max<u32>(O, 1)) == hipSuccess &&
-            hipMalloc(reinterpret_cast<void**>(&s->flag), std::max<u32>(O, 1)) == hipSuccess;
+            hipMalloc(reinterpret_cast<void**>(&s->flag), std::max<u32>(O, 1)) == hipSuccess &&
+            hipStreamCreateWithFlags(&s->ps, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) == hipSuccess;
   if (ok) {
     hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(tsz, 256)), dim3(256), 0, ctx->stream, s->table, (size_t)tsz,
                        DIR_EMPTY);
@@ -868,6 +929,9 @@ int evm_sync_destroy(evm_sync_server* s) {
   if (s->kbytes) (void)hipFree(s->kbytes);
   if (s->hbuf) (void)hipHostFree(s->hbuf);
   (void)hipStreamSynchronize(ctx->stream);
+  if (s->ps) (void)hipStreamDestroy(s->ps);
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
   delete s;
   return EVM_OK;
 }

@@ -84,7 +84,10 @@ struct Win {
 // issues NC independent loads -- a long walk takes a few messages per
 // refill; the per-lane windows 4*65*.. bytes apart so a wave's reads spread
 // over the banks).  The window lives at lds[lane * LW_STRIDE ..].
-constexpr int LW_NC = 16;
+#ifndef EVM_LW_NC
+#define EVM_LW_NC 16
+#endif
+constexpr int LW_NC = EVM_LW_NC;
 constexpr u32 LW_STRIDE = LW_NC * 4 + 1;  // dwords per lane
 struct LWin {
   u32* lds;
@@ -202,46 +205,50 @@ __device__ __forceinline__ bool d_read_msg(const uint8_t* q, u64 n, DMsg* m, W* 
   return r.ok;
 }
 
-// evm_proto.cpp's walk(): on_msg(index, msg, its field's tag) per message
+// One top-level field of a body at r.p (the loop body of evm_proto.cpp's
+// walk()): EVM_OK or EVM_EINVAL; on_msg(index, msg, its field's tag) per message
+template <class W, typename F>
+__device__ __forceinline__ int d_field(int kind, DReaderT<W>& r, const uint8_t* buf, evm_pb_sync& s, F on_msg) {
+  const u32 tree_field = kind == EVM_PB_SYNC_REQUEST ? 4u : 2u;
+  const uint8_t* at = r.p;
+  const u64 tag = r.varint();
+  if (!r.ok) return EVM_EINVAL;
+  const u32 field = (u32)(tag >> 3), wt = (u32)(tag & 7);
+  if (field == 0) return EVM_EINVAL;
+  const bool is_str = field == 1 || field == tree_field || (kind == EVM_PB_SYNC_REQUEST && (field == 2 || field == 3));
+  if (!is_str) return r.skip(wt) ? EVM_OK : EVM_EINVAL;
+  if (wt != 2) return EVM_EINVAL;
+  const uint8_t* q;
+  u64 n;
+  if (!r.bytes(&q, &n)) return EVM_EINVAL;
+  const u64 off = (u64)(q - buf);
+  if (field == 1) {
+    DMsg m;
+    if (!d_read_msg(q, n, &m, r.win)) return EVM_EINVAL;
+    if (m.ts_len != 46) ++s.nonstd_ts;
+    s.content_bytes += m.content_len;
+    on_msg(s.n_messages, m, at);
+    ++s.n_messages;
+  } else if (field == tree_field) {
+    s.tree_off = off;
+    s.tree_len = n;
+  } else if (field == 2) {
+    s.user_off = off;
+    s.user_len = n;
+  } else {
+    s.node_off = off;
+    s.node_len = n;
+  }
+  return EVM_OK;
+}
+
+// evm_proto.cpp's walk() over a whole body
 template <class W, typename F>
 __device__ __forceinline__ int d_walk(int kind, const uint8_t* buf, u64 len, evm_pb_sync* info, W* win, F on_msg) {
   DReaderT<W> r{buf, buf + len, true, win};
   evm_pb_sync s{0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const u32 tree_field = kind == EVM_PB_SYNC_REQUEST ? 4u : 2u;
-  while (r.more()) {
-    const uint8_t* at = r.p;
-    const u64 tag = r.varint();
-    if (!r.ok) return EVM_EINVAL;
-    const u32 field = (u32)(tag >> 3), wt = (u32)(tag & 7);
-    if (field == 0) return EVM_EINVAL;
-    const bool is_str = field == 1 || field == tree_field || (kind == EVM_PB_SYNC_REQUEST && (field == 2 || field == 3));
-    if (!is_str) {
-      if (!r.skip(wt)) return EVM_EINVAL;
-      continue;
-    }
-    if (wt != 2) return EVM_EINVAL;
-    const uint8_t* q;
-    u64 n;
-    if (!r.bytes(&q, &n)) return EVM_EINVAL;
-    const u64 off = (u64)(q - buf);
-    if (field == 1) {
-      DMsg m;
-      if (!d_read_msg(q, n, &m, win)) return EVM_EINVAL;
-      if (m.ts_len != 46) ++s.nonstd_ts;
-      s.content_bytes += m.content_len;
-      on_msg(s.n_messages, m, at);
-      ++s.n_messages;
-    } else if (field == tree_field) {
-      s.tree_off = off;
-      s.tree_len = n;
-    } else if (field == 2) {
-      s.user_off = off;
-      s.user_len = n;
-    } else {
-      s.node_off = off;
-      s.node_len = n;
-    }
-  }
+  while (r.more())
+    if (d_field(kind, r, buf, s, on_msg)) return EVM_EINVAL;
   if (!r.ok) return EVM_EINVAL;
   if (info) *info = s;
   return EVM_OK;
@@ -330,14 +337,33 @@ __global__ void k_pb_rows(const uint8_t* __restrict__ arena, const u64* __restri
   }
 }
 
-// k_pb_rows from the scan's slots: a wave per body, a lane per message
+// bytes in global memory: a pointer read from LDS would be flat, and a flat
+// load makes every later store wait for it and for every store before it
+typedef __attribute__((address_space(1))) uint8_t gu8;
+
+// s_waitcnt vmcnt(0) on the common path: the loads above it are complete.
+// (Each store below sits in its own exec-masked block; without a wait every
+// block could have been skipped, so each one waited again -- for the stores
+// before it as well.)
+__device__ __forceinline__ void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// k_pb_rows from the scan's slots: a wave per body, a lane per message; the
+// 64 rows staged in LDS and stored as one contiguous run (a lane writing its
+// own row made every store a 48-B-strided partial-line write), each content
+// copied by its lane in unaligned 16-B pieces (bytes: 6.9 ms for config 3's
+// round, 16-B pieces 4.9 ms; the wave copying the 64 contents one after
+// another, a byte per lane, 7.5-8 ms)
+constexpr u32 PB_ROW_WORDS = 6;  // a row's 46 timestamp bytes as 8-B words (the rest of the stride is 0)
 __global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
                                                      const int32_t* __restrict__ status, const u64* __restrict__ msg_base,
                                                      const u64* __restrict__ content_base, const u64* __restrict__ slots,
                                                      const u32* __restrict__ owner_of, char* __restrict__ ts, u64 stride,
                                                      u64* __restrict__ content_off, uint8_t* __restrict__ content,
                                                      u32* __restrict__ owner, u32* __restrict__ bad) {
+  __shared__ u64 srow[4][64 * PB_ROW_WORDS];
   const u32 lane = threadIdx.x & 63;
+  u64* sr = srow[threadIdx.x >> 6];
+  const u32 SW = (u32)(stride / 8);  // (stride: a multiple of 16, >= 48)
   for (u32 k = blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += gridDim.x * 4) {
     if (status[k]) continue;
     const u64 a = off[k], b = off[k + 1], m0 = msg_base[k], mn = msg_base[k + 1] - m0;
@@ -358,6 +384,7 @@ __global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__
     // every chunk, so the contents' prefix sum is a wave scan)
     for (u64 i0 = 0; i0 < mn; i0 += 64) {
       const u64 i = i0 + lane;
+      const u32 cnt = (u32)min<u64>(64, mn - i0);
       u64 cl = 0;
       const uint8_t* csrc = nullptr;
       if (i < mn) {
@@ -371,15 +398,13 @@ __global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__
         r.bytes(&q, &len);
         DMsg msg;
         d_read_msg(q, len, &msg, &win);
-        const u64 m = m0 + i;
-        u64* row = reinterpret_cast<u64*>(ts + m * stride);
         const bool std46 = msg.ts_len == 46;
-        for (int j = 0; j < 5; ++j) row[j] = std46 ? win.get8(msg.ts + 8 * j) : ~0ull;
-        row[5] = (std46 ? win.get8(msg.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
-        for (u64 j = 48; j < stride; j += 8) row[j >> 3] = 0ull;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) sr[lane * PB_ROW_WORDS + j] = std46 ? win.get8(msg.ts + 8 * j) : ~0ull;
+        sr[lane * PB_ROW_WORDS + 5] = (std46 ? win.get8(msg.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
         csrc = msg.content;
         cl = msg.content ? msg.content_len : 0;
-        if (owner) owner[m] = ow;
+        if (owner) owner[m0 + i] = ow;
       }
       // this message's content offset: the body's base + the contents before it
       u64 x = cl;
@@ -390,18 +415,41 @@ __global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__
       }
       const u64 dst = cpos + x - cl;
       cpos += __shfl(x, 63, 64);
-      if (i < mn) {
-        content_off[m0 + i] = dst;
-        // the content, 16 bytes at a time with every load issued before the stores
-        for (u64 j0 = 0; j0 < cl; j0 += 16) {
-          uint8_t v[16];
-#pragma unroll
-          for (int t = 0; t < 16; ++t) v[t] = j0 + t < cl ? csrc[j0 + t] : 0;
-#pragma unroll
-          for (int t = 0; t < 16; ++t)
-            if (j0 + t < cl) content[dst + j0 + t] = v[t];
-        }
+      if (i < mn) content_off[m0 + i] = dst;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the chunk's rows are one contiguous run of cnt * SW words
+      u64* rows = reinterpret_cast<u64*>(ts + (m0 + i0) * stride);
+      for (u32 w = lane; w < cnt * SW; w += 64) {
+        const u32 r = SW == PB_ROW_WORDS ? w / PB_ROW_WORDS : w / SW, f = w - r * SW;
+        rows[w] = f < PB_ROW_WORDS ? sr[r * PB_ROW_WORDS + f] : 0ull;
       }
+      if (i < mn) {
+        // whole 16-B pieces by unaligned 16-B loads and stores (inside this
+        // message's bytes: no other lane's), four in flight; the tail by bytes
+        typedef uint4 __attribute__((aligned(1))) u4u;
+        const u64 n16 = cl >> 4;
+        u64 j = 0;
+        for (; j + 4 <= n16; j += 4) {
+          uint4 pc[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) pc[t] = *reinterpret_cast<const u4u*>(csrc + 16 * (j + t));
+#pragma unroll
+          for (int t = 0; t < 4; ++t) *reinterpret_cast<u4u*>(content + dst + 16 * (j + t)) = pc[t];
+        }
+        for (; j < n16; ++j) *reinterpret_cast<u4u*>(content + dst + 16 * j) = *reinterpret_cast<const u4u*>(csrc + 16 * j);
+        const u64 t0 = n16 * 16;
+        uint8_t v[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) v[t] = t0 + t < cl ? csrc[t0 + t] : 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+          if (t0 + t < cl) content[dst + t0 + t] = v[t];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // (sr is rewritten by the next chunk)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
 }
@@ -437,8 +485,7 @@ __global__ void k_gather_spans(const uint8_t* __restrict__ src, const u64* __res
 // thread per owner; the frames of a block's threads live in LDS.
 constexpr int JP_THREADS = 64;
 constexpr int JP_LEVELS = CODE_DIGITS + 1;
-constexpr u32 JP_MIN_NODE = 14;
-constexpr u64 CODE_MASK40 = (1ull << 40) - 1;  // `"0":{"hash":0}`: the fewest bytes of a non-root node
+constexpr u64 CODE_MASK40 = (1ull << 40) - 1;
 
 __device__ __forceinline__ bool jws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 
@@ -998,7 +1045,7 @@ __global__ __launch_bounds__(JP_THREADS) void k_json_parse(const uint8_t* __rest
 // leaf slots per owner: the bound on its nodes + 1 (the root's prefix slot)
 __global__ void k_json_bound(const u64* __restrict__ jlen, u32 n, u64* __restrict__ slots) {
   for (u32 o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x)
-    slots[o] = jlen[o] / JP_MIN_NODE + 2;
+    slots[o] = json_slot_bound(jlen[o]);
 }
 
 // -------------------------------------------------------------- responses
@@ -1163,27 +1210,50 @@ __global__ __launch_bounds__(256) void k_resp_msgs(u32 n, const u64* __restrict_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int j = 0; j < 64; ++j) {
-      const RespMsg& q = meta[wv][j];
-      const u32 len = q.len;
-      if (!len) continue;  // (wave-uniform)
-      const u32 ts_end = q.hdr + 46;
-      for (u32 k = lane; k < len; k += 64) {
-        uint8_t b;
-        if (k < q.hdr) b = q.h[k];
-        else if (k < ts_end) b = (uint8_t)q.t[k - q.hdr];
-        else {
-          // content field: tag, varint length, bytes
-          const u32 e = k - ts_end;
-          const u32 vl = vlen(q.cl);
-          if (e == 0) b = (uint8_t)(2u << 3 | 2u);
-          else if (e <= vl) {
-            u64 v = q.cl;
-            for (u32 z = 1; z < e; ++z) v >>= 7;
-            b = (uint8_t)((v & 0x7f) | (e < vl ? 0x80 : 0));
-          } else b = q.c[e - 1 - vl];
-        }
-        q.d[k] = b;
+    // RG messages x RU passes of 64 bytes loaded before any is stored (a
+    // message at a time waited out a load latency per 64 bytes)
+    constexpr int RG = 4, RU = 3;
+    for (int j0 = 0; j0 < 64; j0 += RG) {
+      u32 lmax = 0;
+#pragma unroll
+      for (int g = 0; g < RG; ++g) lmax = max(lmax, meta[wv][j0 + g].len);
+      for (u32 b0 = 0; b0 < lmax; b0 += 64 * RU) {
+        // first the loaded bytes (timestamp, content: one load each, no other
+        // write to its register while it is in flight), then the headers'
+        // bytes and the stores
+        uint8_t v[RG][RU];
+#pragma unroll
+        for (int g = 0; g < RG; ++g)
+#pragma unroll
+          for (int u = 0; u < RU; ++u) {
+            const RespMsg& q = meta[wv][j0 + g];
+            const u32 k = b0 + 64 * u + lane, ts_end = q.hdr + 46, vl = vlen(q.cl);
+            const gu8* p = nullptr;
+            if (k < q.len && k >= q.hdr) p = k < ts_end ? (const gu8*)(uintptr_t)q.t + (k - q.hdr)
+                                           : k > ts_end + vl ? (const gu8*)(uintptr_t)q.c + (k - ts_end - 1 - vl) : nullptr;
+            v[g][u] = p ? *p : (uint8_t)0;
+          }
+        vm_wait_all();
+#pragma unroll
+        for (int g = 0; g < RG; ++g)
+#pragma unroll
+          for (int u = 0; u < RU; ++u) {
+            const RespMsg& q = meta[wv][j0 + g];
+            const u32 k = b0 + 64 * u + lane, ts_end = q.hdr + 46;
+            if (k >= q.len) continue;
+            uint8_t b = v[g][u];
+            if (k < q.hdr) b = q.h[k];
+            else if (k >= ts_end) {  // the content field's tag and varint length
+              const u32 e = k - ts_end, vl = vlen(q.cl);
+              if (e == 0) b = (uint8_t)(2u << 3 | 2u);
+              else if (e <= vl) {
+                u64 x = q.cl;
+                for (u32 z = 1; z < e; ++z) x >>= 7;
+                b = (uint8_t)((x & 0x7f) | (e < vl ? 0x80 : 0));
+              }
+            }
+            ((gu8*)(uintptr_t)q.d)[k] = b;
+          }
       }
     }
     __builtin_amdgcn_wave_barrier();  // (meta is rewritten by the next round)
@@ -1191,6 +1261,33 @@ __global__ __launch_bounds__(256) void k_resp_msgs(u32 n, const u64* __restrict_
 }
 
 }  // namespace
+
+// Each owner's leaf slots (the bound on its nodes + 1: json_slot_bound) and
+// their exclusive scan, *slots[O] = the total -- launches only (S owns slots).
+int evm::json_tree_slots(evm_ctx* ctx, Scratch& S, u32 n_owners, const u64* len, u64** slots) {
+  u64* bnd = S.alloc<u64>((size_t)n_owners + 1);
+  u64* sl = S.alloc<u64>((size_t)n_owners + 1);
+  if (!bnd || !sl) return EVM_ENOMEM;
+  if (n_owners) KLAUNCH(k_json_bound, dim3(grid_for(n_owners, 256)), dim3(256), len, n_owners, bnd);
+  *slots = sl;
+  return scan_exclusive<u64, OpAdd>(ctx, S, bnd, n_owners, sl, sl + n_owners);
+}
+
+// The owners' texts into t (gapped, cap >= the slots' total): the wave parser,
+// then the exact one for the texts it left; *nl = the leaves (launches only:
+// the caller reads *nl into t->n_leaves once the stream has run).
+int evm::json_tree_parse(evm_ctx* ctx, u32 n_owners, const uint8_t* json, const u64* at, const u64* len,
+                         const u64* slots, int32_t* status, evm_tree* t, u64* nl) {
+  HIPR(hipMemsetAsync(nl, 0, sizeof(u64), ctx->stream));
+  HIPR(hipMemsetAsync(t->off + n_owners, 0, sizeof(u64), ctx->stream));
+  if (n_owners)
+    KLAUNCH(k_json_wave, dim3((n_owners + JV_WAVES - 1) / JV_WAVES), dim3(64 * JV_WAVES), json, at, len, n_owners,
+            slots, (u64*)t->off, (u64*)t->end, (u64*)t->ck, t->xr, t->pfx, status, nl);
+  if (n_owners)
+    KLAUNCH(k_json_parse, dim3((n_owners + JP_THREADS - 1) / JP_THREADS), dim3(JP_THREADS), json, at, len, n_owners,
+            slots, (u64*)t->off, (u64*)t->end, (u64*)t->ck, t->xr, t->pfx, status, nl);
+  return hip_ok(hipGetLastError());
+}
 
 extern "C" {
 
@@ -1283,30 +1380,20 @@ int evm_tree_from_json_dev(evm_ctx* ctx, uint32_t n_owners, const uint8_t* json,
   if (!ctx || !out || !status || (n_owners && (!json || !at || !len))) return EVM_EINVAL;
   *out = nullptr;
   Scratch S(ctx);
-  u64* bnd = S.alloc<u64>((size_t)n_owners + 1);
-  u64* slots = S.alloc<u64>((size_t)n_owners + 1);
+  u64* slots = nullptr;
   u64* nl = S.alloc<u64>(1);
-  if (!bnd || !slots || !nl) return EVM_ENOMEM;
-  HIPR(hipMemsetAsync(nl, 0, sizeof(u64), ctx->stream));
-  if (n_owners) KLAUNCH(k_json_bound, dim3(grid_for(n_owners, 256)), dim3(256), (const u64*)len, n_owners, bnd);
-  int st = scan_exclusive<u64, OpAdd>(ctx, S, bnd, n_owners, slots, slots + n_owners);
+  if (!nl) return EVM_ENOMEM;
+  int st = json_tree_slots(ctx, S, n_owners, reinterpret_cast<const u64*>(len), &slots);
   if (st) return st;
   u64 cap = 0;
   HIPR(hipMemcpyAsync(&cap, slots + n_owners, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
   HIPR(hipStreamSynchronize(ctx->stream));
   evm_tree* t = nullptr;
   if ((st = tree_alloc_gapped(ctx, n_owners, std::max<u64>(cap, 1), &t))) return st;
-  HIPR(hipMemsetAsync(t->off + n_owners, 0, sizeof(u64), ctx->stream));
-  if (n_owners)
-    KLAUNCH(k_json_wave, dim3((n_owners + JV_WAVES - 1) / JV_WAVES), dim3(64 * JV_WAVES), json, (const u64*)at,
-            (const u64*)len, n_owners, (const u64*)slots, (u64*)t->off, (u64*)t->end, (u64*)t->ck, t->xr, t->pfx,
-            status, nl);
-  if (n_owners)
-    KLAUNCH(k_json_parse, dim3((n_owners + JP_THREADS - 1) / JP_THREADS), dim3(JP_THREADS), json, (const u64*)at,
-            (const u64*)len, n_owners, (const u64*)slots, (u64*)t->off, (u64*)t->end, (u64*)t->ck, t->xr, t->pfx,
-            status, nl);
+  st = json_tree_parse(ctx, n_owners, json, reinterpret_cast<const u64*>(at), reinterpret_cast<const u64*>(len), slots,
+                       status, t, nl);
   u64 hl = 0;
-  st = hip_ok(hipMemcpyAsync(&hl, nl, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
+  if (!st) st = hip_ok(hipMemcpyAsync(&hl, nl, sizeof(u64), hipMemcpyDeviceToHost, ctx->stream));
   if (!st) st = hip_ok(hipStreamSynchronize(ctx->stream));
   if (st) {
     tree_destroy(ctx, t);

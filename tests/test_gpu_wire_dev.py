@@ -384,3 +384,125 @@ def test_absent_or_empty_merkle_tree_is_a_500_on_both_paths(eng):
     assert a.store.n_messages == b.store.n_messages == c.store.n_messages == 12
     for s_ in (a, b, c):
         s_.close()
+
+
+# ---- large bodies with bytes that look like message fields inside contents
+# and tree texts, repeated and unknown fields, errors deep inside
+def _vi(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _ld(field, payload):  # a length-delimited field
+    return _vi(field << 3 | 2) + _vi(len(payload)) + payload
+
+
+FAKE = b"\x0a\x30\x0a\x2e"  # a message field's first bytes (tag, length, its timestamp's tag and length)
+
+
+def _msg(rng, ts_len=46, clen=None, plant=True):
+    ts = bytes(rng.choice(b"0123456789-:T.Z") for _ in range(ts_len))
+    n = rng.choice([0, 5, 40, 120, 300]) if clen is None else clen
+    c = bytearray(rng.getrandbits(8) for _ in range(n))
+    if plant and n >= 8:  # false starts inside the content
+        for _ in range(rng.randint(1, 3)):
+            at = rng.randrange(0, n - 4)
+            c[at:at + 4] = FAKE
+    body = _ld(1, ts) + (_ld(2, bytes(c)) if n or rng.random() < 0.5 else b"")
+    return _ld(1, body)
+
+
+def _field_places(body):
+    """The top-level message fields' offsets (a plain protobuf walk; None if it fails)."""
+    p, out = 0, []
+    while p < len(body):
+        at, tag, sh = p, 0, 0
+        while True:
+            b = body[p]
+            p += 1
+            tag |= (b & 0x7F) << sh
+            sh += 7
+            if not b & 0x80:
+                break
+        f, wt = tag >> 3, tag & 7
+        if wt == 2:
+            ln, sh = 0, 0
+            while True:
+                b = body[p]
+                p += 1
+                ln |= (b & 0x7F) << sh
+                sh += 7
+                if not b & 0x80:
+                    break
+            if f == 1:
+                out.append(at)
+            p += ln
+        elif wt == 0:
+            while body[p] & 0x80:
+                p += 1
+            p += 1
+        elif wt == 1:
+            p += 8
+        elif wt == 5:
+            p += 4
+        else:
+            return None
+    return out if p == len(body) else None
+
+
+def _large_bodies(seed):
+    rng = random.Random(seed)
+    user, node = _ld(2, b"u" * 21), _ld(3, b"0123456789abcdef")
+    tree_text = b'{"1":{"hash":5},' + FAKE * 4000 + b'"hash":5}'
+    B = []
+    B.append(b"".join(_msg(rng) for _ in range(2000)) + user + node + _ld(4, b'{"hash":1}'))  # the usual order
+    B.append(_ld(4, tree_text) + b"".join(_msg(rng) for _ in range(600)) + user)  # a long text first
+    mid = [_msg(rng) for _ in range(900)]
+    B.append(b"".join(mid[:400]) + _ld(4, tree_text) + b"".join(mid[400:]) + _ld(4, b"{}") + node)  # repeated: the last wins
+    B.append(b"".join(_msg(rng, clen=0, plant=False) for _ in range(5000)))  # 50-B messages: every slot used
+    B.append(b"".join(_msg(rng, ts_len=45) for _ in range(700)))  # timestamps that are not 46 bytes
+    x = b"".join(_msg(rng) for _ in range(800))
+    B.append(x[:-3])  # truncated at the end
+    B.append(x[:len(x) // 2] + b"\x00" + x[len(x) // 2:])  # (a field 0 mid-body, unless it lands inside a message)
+    y = b"".join(_msg(rng) + (b"\x48\x07" if i % 7 == 0 else b"") + (b"\x51" + bytes(8) if i % 11 == 0 else b"")
+                 + (b"\x5d" + bytes(4) if i % 13 == 0 else b"") for i in range(900))
+    B.append(y)  # unknown varint / fixed64 / fixed32 fields among the messages
+    B.append(y[:len(y) // 3] + b"\x0b" + y[len(y) // 3:])  # a group: rejected
+    B.append(b"".join(_msg(rng, plant=False) for _ in range(80)))
+    return B
+
+
+def test_scan_of_large_adversarial_bodies_equals_the_host_codec(eng):
+    from evolu_amd import _lib as L
+    from evolu_amd import wire
+
+    lib = L.load()
+    bodies = _large_bodies(11)
+    arena, off = _arena(bodies)
+    n = len(bodies)
+    hinfo = (wire._Sync * n)()
+    hst = np.zeros(n, dtype=np.int32)
+    L.check(lib.evm_pb_scan_batch(L.PB_SYNC_REQUEST, C.c_void_p(arena.ctypes.data), C.c_void_p(off.ctypes.data), n,
+                                  hinfo, C.c_void_p(hst.ctypes.data)), "scan")
+    hi = np.ctypeslib.as_array(hinfo).view(np.uint64).reshape(n, 9)
+    assert hst[0] == 0 and hst[5] != 0 and hst[8] != 0 and hi[4, 8] == 700 and hi[2, 7] == 2  # (the fixture's cases)
+    a_d, off_d = eng.dev(arena), eng.dev(off.view(np.int64))
+    info_d = torch.empty((n, 9), dtype=torch.int64, device=a_d.device)
+    st_d = torch.empty(n, dtype=torch.int32, device=a_d.device)
+    slots = torch.full((int(off[-1]) // 50 + 1,), -1, dtype=torch.int64, device=a_d.device)
+    L.check(lib.evm_pb_scan_index_dev(eng.h, L.PB_SYNC_REQUEST, _P(a_d), _P(off_d), n, _P(info_d), _P(st_d), _P(slots)),
+            "scan_index_dev")
+    assert (st_d.cpu().numpy() == hst).all()
+    assert (info_d.cpu().numpy().view(np.uint64) == hi).all()
+    sl = slots.cpu().numpy()
+    for k in np.flatnonzero(hst == 0):
+        want = _field_places(bodies[k])
+        assert want is not None and len(want) == int(hi[k, 0])
+        s0 = int(off[k]) // 50
+        room = int(off[k + 1]) // 50 - s0
+        got = sl[s0: s0 + min(len(want), room)] - int(off[k])
+        assert (got == np.array(want[:room], dtype=np.int64)).all(), k

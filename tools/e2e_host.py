@@ -1,7 +1,7 @@
 """Config-3 rounds through the native sync server (evm_sync_round) on
 bench.py's bodies: device-resident rounds and host-bodies rounds (pinned H2D
 -> round -> pinned D2H), two of each on fresh servers, timed by part.
-`python tools/e2e_host.py` (E2E_OWNERS to shrink)."""
+`python tools/e2e_host.py` (E2E_OWNERS to shrink, E2E_HOST=0: device rounds only)."""
 import os
 import sys
 import time
@@ -55,7 +55,7 @@ for rep in range(3):
     srv.close()
 del a_d
 torch.cuda.empty_cache()
-for rep in range(2):
+for rep in range(int(os.environ.get("E2E_HOST", 2))):
     srv = SyncServer(eng, owners)
     t0 = time.perf_counter()
     out = srv.sync_arena(arena, off)
