@@ -199,6 +199,84 @@ __device__ __forceinline__ u32 leaf_piece(const WaveLds* w, const Lane& ln, Put 
   return n;
 }
 
+// n (<= 8) bytes of v (the first in the low byte) at p in LDS, written in
+// at most three stores of exactly those bytes (LDS takes unaligned 2-, 4- and
+// 8-byte accesses; a neighbour lane's bytes next to them are not touched)
+typedef uint64_t __attribute__((aligned(1))) lu64;
+typedef uint32_t __attribute__((aligned(1))) lu32;
+typedef uint16_t __attribute__((aligned(1))) lu16;
+__device__ __forceinline__ void lds_put(unsigned char* p, u64 v, u32 n) {
+  if (n == 8) {
+    *reinterpret_cast<lu64*>(p) = v;
+    return;
+  }
+  if (n & 4) {
+    *reinterpret_cast<lu32*>(p) = (u32)v;
+    p += 4;
+    v >>= 32;
+  }
+  if (n & 2) {
+    *reinterpret_cast<lu16*>(p) = (uint16_t)v;
+    p += 2;
+    v >>= 16;
+  }
+  if (n & 1) *p = (unsigned char)v;
+}
+// n (1..8) decimal digits of v, zero-padded, the first in the low byte
+__device__ __forceinline__ u64 dec_chars(u32 v, u32 n) {
+  u64 s = 0;
+#pragma unroll
+  for (u32 k = 0; k < 8; ++k)
+    if (k < n) {
+      s = (s << 8) | (u64)('0' + v % 10u);
+      v /= 10u;
+    }
+  return s;
+}
+
+// leaf_piece's bytes into the LDS stage at p, a few bytes per store
+__device__ __forceinline__ void leaf_piece_wide(const WaveLds* w, const Lane& ln, unsigned char* p) {
+  if (!ln.valid) return;
+  const u64 c = ln.c;
+  const int D = ln.D, cp = ln.cp, cn = ln.cn;
+  if (ln.i && ln.prevD > cp) *p++ = ',';
+  for (int k = cp + 1; k <= D; ++k) {
+    const u32 dg = (u32)(c >> (2 * (CODE_DIGITS - k))) & 3u;  // digit + 1
+    lds_put(p, 0x7B3A220022ull | (u64)('0' + dg - 1) << 8, 5);  // `"d":{`
+    p += 5;
+  }
+  for (int d = D; d > cn; --d) {
+    const int32_t h = ln.pn ^ node_start(w, ln, d);
+    if (d < D) {
+      lds_put(p, 0x3A2268736168222Cull, 8);  // `,"hash":`
+      p += 8;
+    } else {
+      lds_put(p, 0x3A22687361682200ull >> 8, 7);  // `"hash":`
+      p += 7;
+    }
+    const u32 x = h < 0 ? 0u - (u32)h : (u32)h;
+    if (h < 0) *p++ = '-';
+    if (x >= 100000000u) {
+      const u32 hi = x / 100000000u, lo = x - hi * 100000000u, nh = hi >= 10u ? 2u : 1u;
+      lds_put(p, dec_chars(hi, nh), nh);
+      p += nh;
+      lds_put(p, dec_chars(lo, 8u), 8);
+      p += 8;
+      *p++ = '}';
+    } else {
+      const u32 nd = dec_len((int32_t)x);
+      const u64 ds = dec_chars(x, nd);
+      if (nd < 8) {
+        lds_put(p, ds | (u64)'}' << (8 * nd), nd + 1);
+      } else {
+        lds_put(p, ds, 8);
+        p[8] = '}';
+      }
+      p += nd + 1;
+    }
+  }
+}
+
 __device__ __forceinline__ u32 wave_excl_sum(u32 v, u32* total) {
   u32 x = v;
 #pragma unroll
@@ -296,7 +374,7 @@ __global__ __launch_bounds__(JW * JW_WAVES) void k_jp_emit(TreeJ t, const u32* _
         // LDS reads and stores between the ends
         const u32 s0 = (u32)((uintptr_t)dst & 15u);
         unsigned char* sgo = sg + s0;
-        leaf_piece(w, ln, [&](u32 k, char b) { sgo[pos + k] = (unsigned char)b; });
+        leaf_piece_wide(w, ln, sgo + pos);  // (a byte per store: encode 9.3 -> 8.8 ms on config 3's round)
         if (lane == 0) {
           if (head) sgo[0] = '{';
           if (last) tail([&](u32 k, char b) { sgo[k] = (unsigned char)b; });

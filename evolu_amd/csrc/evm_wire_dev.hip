@@ -1489,11 +1489,19 @@ int evm::encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, co
   if (n)
     KLAUNCH(k_resp_tree_hdr, dim3(grid_for(n, 256)), dim3(256), n, (const u64*)sel_off, (const u64*)mpos,
             (const u64*)jlen, (const u64*)doff, out, jdst);
+  // the messages' bytes (memory-bound) on the second stream beside the tree
+  // texts (VALU-bound): disjoint bytes of the responses, joined on the way out
+  SideFork side(ctx);
+  if (NS) {
+    const hipStream_t ms = side.stream();
+    evm::ProfScope ps_(ctx, "k_resp_msgs", ms);
+    hipLaunchKernelGGL(k_resp_msgs, dim3(grid_for((NS + 63) / 64, 4)), dim3(256), 0, ms, n, (const u64*)sel_off,
+                       (const u64*)sel_id, NS, (const DSeg*)dseg, n_seg, (u64)stride, (const u64*)mpos,
+                       (const u64*)doff, out);
+  }
   if ((st = json_emit(ctx, tree, owners, n, jplan, reinterpret_cast<const uint64_t*>(jdst), reinterpret_cast<char*>(out))))
     return st;
-  if (NS)
-    KLAUNCH(k_resp_msgs, dim3(grid_for((NS + 63) / 64, 4)), dim3(256), n, (const u64*)sel_off, (const u64*)sel_id, NS,
-            (const DSeg*)dseg, n_seg, (u64)stride, (const u64*)mpos, (const u64*)doff, out);
+  side.join();
   return hip_ok(hipGetLastError());
 }
 

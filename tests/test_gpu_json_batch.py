@@ -122,3 +122,34 @@ def test_owner_out_of_range_is_refused(eng):
         t.to_json_batch(eng.dev(np.array([1, 4], dtype=np.uint32)))
     assert e.value.status == L.EVM_EINVAL
     assert torch.cuda.is_available()
+
+
+def _i32(x):
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >= 1 << 31 else x
+
+
+def test_hashes_of_every_length_and_sign(eng):
+    """The emitter writes a node's hash as its decimal digits in pieces of up
+    to eight bytes: every length 1..10, both signs, 0 and -2**31, at every
+    depth and in every position (first child, later child, the root)."""
+    vals = [0, -1, 9, 10, -99, 12345678, -12345678, 99999999, 100000000, -100000000, 123456789,
+            2147483647, -2147483648, 1000000000, -999999999, 7, 4096]
+    rng = random.Random(5)
+    texts = []
+    for k in range(40):
+        # a small trie: a few depth-1 children, each with leaves below
+        def node(depth):
+            if depth == 0 or rng.random() < 0.3:
+                return rng.choice(vals), None
+            kids = sorted(rng.sample("012", rng.randint(1, 3)))
+            parts, x = [], 0
+            for d in kids:
+                h, body = node(depth - 1)
+                x ^= h
+                parts.append('"%s":%s' % (d, body if body else '{"hash":%d}' % h))
+            return _i32(x), "{" + ",".join(parts) + ',"hash":%d}' % _i32(x)
+        h, body = node(rng.randint(1, 4))
+        texts.append(body if body else '{"0":{"hash":%d},"hash":%d}' % (h, h))
+    tt = eng.tree_from_json(texts)
+    assert _texts(tt) == texts
