@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <functional>
+#include <type_traits>
 #include <vector>
 
 #include "evm_device.hpp"
@@ -347,13 +348,41 @@ typedef __attribute__((address_space(1))) uint8_t gu8;
 // before it as well.)
 __device__ __forceinline__ void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
-// k_pb_rows from the scan's slots: a wave per body, a lane per message; the
-// 64 rows staged in LDS and stored as one contiguous run (a lane writing its
-// own row made every store a 48-B-strided partial-line write), each content
-// copied by its lane in unaligned 16-B pieces (bytes: 6.9 ms for config 3's
-// round, 16-B pieces 4.9 ms; the wave copying the 64 contents one after
-// another, a byte per lane, 7.5-8 ms)
 constexpr u32 PB_ROW_WORDS = 6;  // a row's 46 timestamp bytes as 8-B words (the rest of the stride is 0)
+// Reads of a span of device bytes staged in LDS ([A, Z), A 16-B aligned),
+// anything outside it from global memory
+typedef uint64_t __attribute__((aligned(1))) ulu64;
+typedef uint4 __attribute__((aligned(1))) u4u;
+typedef __attribute__((address_space(3))) const unsigned char lds_u8;
+typedef __attribute__((address_space(3))) const ulu64 lds_u64;
+struct SWin {
+  lds_u8* st;
+  const uint8_t* A;
+  const uint8_t* Z;
+  __device__ __forceinline__ uint8_t get(const uint8_t* p) const { return p >= A && p < Z ? st[p - A] : *p; }
+  __device__ __forceinline__ u64 get8(const uint8_t* p) const {
+    if (p >= A && p + 8 <= Z) return *reinterpret_cast<lds_u64*>(st + (p - A));
+    u64 v = 0;
+    for (int k = 0; k < 8; ++k) v |= (u64)get(p + k) << (8 * k);
+    return v;
+  }
+};
+__device__ __forceinline__ u64 readlane64(u64 x, int l) {
+  return ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(x >> 32), l) << 32) |
+         (u32)__builtin_amdgcn_readlane((int)(u32)x, l);
+}
+constexpr u32 PB_STAGE = 8192;  // bytes of a chunk's 64 messages staged in LDS per wave (more: read in place)
+
+// k_pb_rows from the scan's slots: a wave per body, a lane per message.  Each
+// 64 messages' bytes are loaded into LDS by the wave (coalesced 16-B loads;
+// each lane reading its own message through a register window fetched ~1.7x
+// the bytes) and parsed there; the 64 rows are staged in LDS and stored as one
+// contiguous run (a lane writing its own row made every store a
+// 48-B-strided partial-line write); each content is copied by its lane in
+// unaligned 16-B pieces (a byte loop: 6.9 ms for config 3's round, 16-B
+// pieces 4.9 ms; the wave copying the 64 contents one after another, a byte
+// per lane, 7.5-8 ms)
+
 __global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__ arena, const u64* __restrict__ off, u32 n,
                                                      const int32_t* __restrict__ status, const u64* __restrict__ msg_base,
                                                      const u64* __restrict__ content_base, const u64* __restrict__ slots,
@@ -361,8 +390,10 @@ __global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__
                                                      u64* __restrict__ content_off, uint8_t* __restrict__ content,
                                                      u32* __restrict__ owner, u32* __restrict__ bad) {
   __shared__ u64 srow[4][64 * PB_ROW_WORDS];
+  __shared__ uint4 sstage[4][PB_STAGE / 16];
   const u32 lane = threadIdx.x & 63;
   u64* sr = srow[threadIdx.x >> 6];
+  uint4* stg = sstage[threadIdx.x >> 6];
   const u32 SW = (u32)(stride / 8);  // (stride: a multiple of 16, >= 48)
   for (u32 k = blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += gridDim.x * 4) {
     if (status[k]) continue;
@@ -385,23 +416,51 @@ __global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__
     for (u64 i0 = 0; i0 < mn; i0 += 64) {
       const u64 i = i0 + lane;
       const u32 cnt = (u32)min<u64>(64, mn - i0);
+      const u64 fpos = i < mn ? slots[s0 + i] : 0;
+      // the chunk's bytes: its first message field up to the next chunk's
+      // first (the body's last chunk: to its last message's end), loaded
+      // into LDS by the wave with coalesced 16-B loads -- each lane reading
+      // its own message through a window fetched ~1.7x the bytes
+      u64 E;
+      if (i0 + 64 < mn) {
+        E = slots[s0 + i0 + 64];
+      } else {
+        u64 e = 0;
+        if (lane == cnt - 1) {
+          Win w2;
+          w2.init(arena + b);
+          DReader r{arena + fpos, arena + b, true, &w2};
+          r.varint();
+          const u64 len = r.varint();
+          e = (u64)(r.p - arena) + len;
+        }
+        E = readlane64(e, (int)cnt - 1);
+      }
+      const u64 A0 = readlane64(fpos, 0) & ~15ull;
+      const bool staged = E >= A0 && E - A0 <= PB_STAGE;  // (wave-uniform)
+      if (staged) {
+        const u32 nq = (u32)((E - A0 + 15) >> 4);
+        for (u32 q = lane; q < nq; q += 64) stg[q] = *reinterpret_cast<const uint4*>(arena + A0 + 16ull * q);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      // (an unstaged chunk -- a content of kilobytes -- reads its bytes one by one)
+      SWin sw{(lds_u8*)stg, arena + A0, arena + (staged ? E : A0)};
       u64 cl = 0;
       const uint8_t* csrc = nullptr;
       if (i < mn) {
-        const uint8_t* f = arena + slots[s0 + i];
-        Win win;
-        win.init(arena + b);
-        DReader r{f, arena + b, true, &win};
+        DReaderT<SWin> r{arena + fpos, arena + b, true, &sw};
         r.varint();  // (the field's tag: 1, length-delimited -- the scan read it)
         const uint8_t* q;
         u64 len;
         r.bytes(&q, &len);
         DMsg msg;
-        d_read_msg(q, len, &msg, &win);
+        d_read_msg(q, len, &msg, &sw);
         const bool std46 = msg.ts_len == 46;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) sr[lane * PB_ROW_WORDS + j] = std46 ? win.get8(msg.ts + 8 * j) : ~0ull;
-        sr[lane * PB_ROW_WORDS + 5] = (std46 ? win.get8(msg.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
+        for (int j = 0; j < 5; ++j) sr[lane * PB_ROW_WORDS + j] = std46 ? sw.get8(msg.ts + 8 * j) : ~0ull;
+        sr[lane * PB_ROW_WORDS + 5] = (std46 ? sw.get8(msg.ts + 40) : ~0ull) & 0x0000FFFFFFFFFFFFull;
         csrc = msg.content;
         cl = msg.content ? msg.content_len : 0;
         if (owner) owner[m0 + i] = ow;
@@ -426,29 +485,26 @@ __global__ __launch_bounds__(256) void k_pb_rows_idx(const uint8_t* __restrict__
         rows[w] = f < PB_ROW_WORDS ? sr[r * PB_ROW_WORDS + f] : 0ull;
       }
       if (i < mn) {
-        // whole 16-B pieces by unaligned 16-B loads and stores (inside this
-        // message's bytes: no other lane's), four in flight; the tail by bytes
-        typedef uint4 __attribute__((aligned(1))) u4u;
+        // whole 16-B pieces by unaligned 16-B loads (from the staged copy when
+        // the content lies in it) and stores (inside this message's bytes: no
+        // other lane's), four in flight; the tail by bytes
         const u64 n16 = cl >> 4;
-        u64 j = 0;
-        for (; j + 4 <= n16; j += 4) {
-          uint4 pc[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) pc[t] = *reinterpret_cast<const u4u*>(csrc + 16 * (j + t));
-#pragma unroll
-          for (int t = 0; t < 4; ++t) *reinterpret_cast<u4u*>(content + dst + 16 * (j + t)) = pc[t];
-        }
-        for (; j < n16; ++j) *reinterpret_cast<u4u*>(content + dst + 16 * j) = *reinterpret_cast<const u4u*>(csrc + 16 * j);
         const u64 t0 = n16 * 16;
-        uint8_t v[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) v[t] = t0 + t < cl ? csrc[t0 + t] : 0;
-#pragma unroll
-        for (int t = 0; t < 16; ++t)
-          if (t0 + t < cl) content[dst + t0 + t] = v[t];
+        if (csrc >= sw.A && csrc + cl <= sw.Z) {  // (from the staged copy)
+          typedef unsigned int v4u __attribute__((ext_vector_type(4), aligned(1)));
+          typedef __attribute__((address_space(3))) const v4u lds_v4;
+          lds_u8* src = sw.st + (csrc - sw.A);
+          for (u64 j = 0; j < n16; ++j)
+            *reinterpret_cast<v4u*>(content + dst + 16 * j) = *reinterpret_cast<lds_v4*>(src + 16 * j);
+          for (u64 t = t0; t < cl; ++t) content[dst + t] = src[t];
+        } else {  // (a chunk too long for the stage: in place)
+          for (u64 j = 0; j < n16; ++j)
+            *reinterpret_cast<u4u*>(content + dst + 16 * j) = *reinterpret_cast<const u4u*>(csrc + 16 * j);
+          for (u64 t = t0; t < cl; ++t) content[dst + t] = csrc[t];
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();  // (sr is rewritten by the next chunk)
+      __builtin_amdgcn_wave_barrier();  // (sr and the stage are rewritten by the next chunk)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
