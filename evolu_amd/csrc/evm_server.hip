@@ -798,7 +798,20 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
     // received (tc, node, case mask): the string is rebuilt in registers for
     // murmur3 (a canonical timestamp is a function of them)
     u32 bad = 0;
+    // received records double-buffered: record k + 1's loads in flight while
+    // record k's string is rebuilt and hashed
+    u64 ntc = 0, nnode = 0;
+    u32 ncm = 0;
+    auto load_w = [&](int k) {
+      const u32 t = threadIdx.x + k * THREADS;
+      if (t < m && !wire_self_row(wsrc, bi[k])) wire_load(wsrc, bi[k], &ntc, &nnode, &ncm);
+    };
+    load_w(0);
+#pragma unroll
     for (int k = 0; k < PER; ++k) {
+      const u64 wtc = ntc, wnode = nnode;
+      const u32 cm = ncm;
+      if (k + 1 < PER) load_w(k + 1);
       const u32 t = threadIdx.x + k * THREADS;
       if (t < m && wire_self_row(wsrc, bi[k])) {
         // a keep-input route's own row: the caller's string, parsed here
@@ -812,10 +825,7 @@ __global__ __launch_bounds__(THREADS) void k_svo_a(
         tc[k] = p.tc;
         tmin = min(tmin, p.tc);
         tmax = max(tmax, p.tc);
-      } else if (t < m) {
-        u64 wtc, wnode;
-        u32 cm;
-        wire_load(wsrc, bi[k], &wtc, &wnode, &cm);  // (all PER loads up front: 86 -> more VGPRs, 15 % slower)
+      } else if (t < m) {  // (all PER loads up front instead: 86 -> more VGPRs, 15 % slower)
         u32 w[12];
         format_ts46(wtc, wnode, cm & EVM_META_CASEMASK, w);
         bad |= (cm & EVM_META_VALID) ? 0u : 1u;

@@ -9,6 +9,8 @@ import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 p=d.get('pipeline',{})
 print('%s %.3f ms frac %.3f' % (sys.argv[2], d['ms_per_step'], p.get('pipeline_hbm_frac',0)))
 print('   '+' '.join('%s=%.3f' % (k, v) for k,v in list(p.get('kernels_ms_per_step',{}).items())[:8]))
+sw=d.get('src_wire')
+if sw: print('   src_wire K5 %.3f ms' % sw['kernel_ms_avg'])
 r=d.get('reingest')
 if r: print('   reingest %.3f ms ' % r['ms_per_ingest_median'] + ' '.join('%s=%.3f' % (k,v) for k,v in list(r['kernels_ms'].items())[:4]))
 " "$1" "$2"; }
