@@ -85,8 +85,10 @@ struct Win {
 // issues NC independent loads -- a long walk takes a few messages per
 // refill; the per-lane windows 4*65*.. bytes apart so a wave's reads spread
 // over the banks).  The window lives at lds[lane * LW_STRIDE ..].
+// (12 chunks, a 192-B window: config 3's scan 3.3 ms; 8: 3.7, 10: 3.6, 14: 3.4,
+// 16: 4.1-4.3, 24: 8.0, 32: 31.6 -- same box, alternating builds)
 #ifndef EVM_LW_NC
-#define EVM_LW_NC 16
+#define EVM_LW_NC 12
 #endif
 constexpr int LW_NC = EVM_LW_NC;
 constexpr u32 LW_STRIDE = LW_NC * 4 + 1;  // dwords per lane
