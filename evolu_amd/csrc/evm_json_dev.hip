@@ -222,16 +222,17 @@ __device__ __forceinline__ void lds_put(unsigned char* p, u64 v, u32 n) {
   }
   if (n & 1) *p = (unsigned char)v;
 }
-// n (1..8) decimal digits of v, zero-padded, the first in the low byte
+// the last n (1..8) decimal digits of v < 10^8, the first in the low byte:
+// four 2-digit pairs from two divisions by 10^4 and 10^2 (no digit loop)
 __device__ __forceinline__ u64 dec_chars(u32 v, u32 n) {
-  u64 s = 0;
-#pragma unroll
-  for (u32 k = 0; k < 8; ++k)
-    if (k < n) {
-      s = (s << 8) | (u64)('0' + v % 10u);
-      v /= 10u;
-    }
-  return s;
+  const u32 hi = v / 10000u, lo = v - hi * 10000u;
+  const u32 h1 = hi / 100u, h2 = hi - h1 * 100u, l1 = lo / 100u, l2 = lo - l1 * 100u;
+  auto two = [](u32 d) -> u64 {
+    const u32 t = d / 10u;
+    return (u64)((t | ((d - t * 10u) << 8)) + 0x3030u);
+  };
+  const u64 s = two(h1) | two(h2) << 16 | two(l1) << 32 | two(l2) << 48;
+  return s >> (8 * (8 - n));
 }
 
 // leaf_piece's bytes into the LDS stage at p, a few bytes per store
