@@ -399,12 +399,17 @@ int json_emit(evm_ctx* ctx, const evm_tree* t, const uint32_t* owners, uint32_t 
 int fold_into_tree(evm_ctx* ctx, Scratch& S, const evm_tree* in, u32 n_owners, u64* ck, u32* h, size_t m,
                    const Info& host_info, evm_tree** out);
 // evm_pb_encode_responses_dev in one pass: out_for(total) gives the output
-// buffer (null: sizes only) once the sizes are known (evm_wire_dev.hip)
+// buffer (null: sizes only) once the sizes are known (evm_wire_dev.hip).
+// pre: the tree texts' plan made by the caller (json_plan over the same
+// owners: lengths pre_jlen[n], its out-of-range flag pre_bad), already on or
+// joined to the context's stream
 int encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, const uint32_t* owners,
                          const uint64_t* osel_off, const uint64_t* osel_id, const uint8_t* skip, uint32_t n_seg,
                          const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
                          size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
-                         const std::function<uint8_t*(uint64_t)>& out_for, uint64_t* out_off, uint64_t* total);
+                         const std::function<uint8_t*(uint64_t)>& out_for, uint64_t* out_off, uint64_t* total,
+                         const JsonPlan* pre = nullptr, const uint64_t* pre_jlen = nullptr,
+                         const uint32_t* pre_bad = nullptr);
 
 // A route's received packed records, read where they lie (evm_dist_ingest):
 // the parsed form of each 46-B timestamp -- tc, node, case mask |

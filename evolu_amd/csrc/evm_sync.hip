@@ -278,14 +278,15 @@ __global__ void k_sync_active(const uint8_t* __restrict__ arena, const u64* __re
   }
 }
 
-// answered requests (request order): their owner slots, and RangeError skips
+// answered requests (request order): their owner slots; their RangeError skips
+__global__ void k_sync_owners(const u32* __restrict__ ans, u32 na, const u32* __restrict__ slot,
+                              u32* __restrict__ owners) {
+  for (u32 j = blockIdx.x * blockDim.x + threadIdx.x; j < na; j += gridDim.x * blockDim.x) owners[j] = slot[ans[j]];
+}
 __global__ void k_sync_answer(const u32* __restrict__ ans, u32 na, const u32* __restrict__ slot,
-                              const int64_t* __restrict__ diff, u32* __restrict__ owners, uint8_t* __restrict__ skip) {
-  for (u32 j = blockIdx.x * blockDim.x + threadIdx.x; j < na; j += gridDim.x * blockDim.x) {
-    const u32 s = slot[ans[j]];
-    owners[j] = s;
-    skip[j] = diff[s] == EVM_DIFF_RANGE_ERROR ? 1 : 0;
-  }
+                              const int64_t* __restrict__ diff, uint8_t* __restrict__ skip) {
+  for (u32 j = blockIdx.x * blockDim.x + threadIdx.x; j < na; j += gridDim.x * blockDim.x)
+    skip[j] = diff[slot[ans[j]]] == EVM_DIFF_RANGE_ERROR ? 1 : 0;
 }
 
 // evm_sync_log_read: per id its segment row -> the 46-B timestamp and the
@@ -811,9 +812,32 @@ int round_dev(evm_sync_server* sv, const uint8_t* arena, const u64* off_h, u32 n
   u32* owners = S.alloc<u32>(na);
   uint8_t* skip = S.alloc<uint8_t>(na);
   u64* rout = S.alloc<u64>((size_t)na + 1);
-  if (!diff || !sel_off || !sel_id || !ans_d || !owners || !skip || !rout) {
+  u64* jlen = S.alloc<u64>((size_t)na + 1);
+  u32* jbad = S.alloc<u32>(1);
+  if (!diff || !sel_off || !sel_id || !ans_d || !owners || !skip || !rout || !jlen || !jbad) {
     free_client();
     return EVM_ENOMEM;
+  }
+  const evm_tree* tree = evm_store_tree(sv->store);
+  // the answered owners, then their tree texts' lengths (k_jp_len) on the
+  // second stream while getMessages runs: both only read the store's tree
+  JsonPlan jplan;
+  if (na) {
+    HIPR(hipMemcpyAsync(ans_d, ans.data(), sizeof(u32) * na, hipMemcpyHostToDevice, ctx->stream));
+    KLAUNCH(k_sync_owners, dim3(grid_for(na, 256)), dim3(256), ans_d, na, slot_d, owners);
+    HIPR(hipMemsetAsync(jbad, 0, sizeof(u32), ctx->stream));
+    HIPR(hipEventRecord(sv->ev_fork, ctx->stream));
+    HIPR(hipStreamWaitEvent(sv->ps, sv->ev_fork, 0));
+    fork.open = true;
+    const hipStream_t main = ctx->stream;
+    ctx->stream = sv->ps;  // (launches only)
+    int pst2 = json_plan(ctx, S, tree, owners, na, reinterpret_cast<uint64_t*>(jlen), jbad, &jplan);
+    if (!pst2) pst2 = hip_ok(hipEventRecord(sv->ev_join, ctx->stream));
+    ctx->stream = main;
+    if (pst2) {
+      free_client();
+      return pst2;
+    }
   }
   uint64_t n_sel = 0;
   st = evm_server_select(ctx, sv->store, client, reinterpret_cast<const char*>(node), active, diff, U64P(sel_off),
@@ -823,8 +847,8 @@ int round_dev(evm_sync_server* sv, const uint8_t* arena, const u64* off_h, u32 n
   HIPR(hipStreamSynchronize(ctx->stream));
   stamp(5);
   if (!na) return EVM_OK;
-  HIPR(hipMemcpyAsync(ans_d, ans.data(), sizeof(u32) * na, hipMemcpyHostToDevice, ctx->stream));
-  KLAUNCH(k_sync_answer, dim3(grid_for(na, 256)), dim3(256), ans_d, na, slot_d, diff, owners, skip);
+  fork.join();
+  KLAUNCH(k_sync_answer, dim3(grid_for(na, 256)), dim3(256), ans_d, na, slot_d, diff, skip);
   // ---- SyncResponse.toBinary: sizes, then the bytes into the round's arena
   const u32 ns = (u32)sv->segs.size();
   std::vector<uint64_t> sbase(ns);
@@ -837,7 +861,6 @@ int round_dev(evm_sync_server* sv, const uint8_t* arena, const u64* off_h, u32 n
     scoff[k] = U64C(sv->segs[k].coff);
     scon[k] = sv->segs[k].content;
   }
-  const evm_tree* tree = evm_store_tree(sv->store);
   uint64_t total = 0;
   int ast = EVM_OK;
   st = encode_responses_dev(
@@ -853,7 +876,7 @@ int round_dev(evm_sync_server* sv, const uint8_t* arena, const u64* off_h, u32 n
         }
         return sv->resp;
       },
-      U64P(rout), &total);
+      U64P(rout), &total, &jplan, reinterpret_cast<const uint64_t*>(jlen), jbad);
   if (!st) st = ast;
   if (st) return st;
   std::vector<u64> ro((size_t)na + 1);

@@ -1470,7 +1470,8 @@ int evm::encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, co
                               const uint64_t* osel_off, const uint64_t* osel_id, const uint8_t* skip, uint32_t n_seg,
                               const uint64_t* seg_base, const uint64_t* const* seg_row, const char* const* seg_ts,
                               size_t stride, const uint64_t* const* seg_coff, const uint8_t* const* seg_content,
-                              const std::function<uint8_t*(uint64_t)>& out_for, uint64_t* out_off, uint64_t* total) {
+                              const std::function<uint8_t*(uint64_t)>& out_for, uint64_t* out_off, uint64_t* total,
+                              const JsonPlan* pre, const uint64_t* pre_jlen, const uint32_t* pre_bad) {
   if (!ctx || !tree || !total || (n && (!owners || !osel_off || !out_off)) || stride < 46 ||
       (n_seg && (!seg_base || !seg_ts || !seg_coff || !seg_content)))
     return EVM_EINVAL;
@@ -1522,8 +1523,12 @@ int evm::encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, co
   // (the emitter reads a gapped tree as it lies -- an empty store's ingest
   // leaves one: no compaction pass, 1.2 ms of config 3's round)
   JsonPlan jplan;
-  st = json_plan(ctx, S, tree, owners, n, reinterpret_cast<uint64_t*>(jlen), bad, &jplan);
-  if (st) return st;
+  if (pre) {
+    jplan = *pre;
+    jlen = reinterpret_cast<u64*>(const_cast<uint64_t*>(pre_jlen));
+  } else if ((st = json_plan(ctx, S, tree, owners, n, reinterpret_cast<uint64_t*>(jlen), bad, &jplan))) {
+    return st;
+  }
   if (NS)
     KLAUNCH(k_resp_msg_size, dim3(grid_for(NS, 256)), dim3(256), (const u64*)sel_id, NS, (const DSeg*)dseg, n_seg,
             (u64)stride, msz, bad);
@@ -1533,14 +1538,15 @@ int evm::encode_responses_dev(evm_ctx* ctx, uint32_t n, const evm_tree* tree, co
             rlen);
   u64* doff = reinterpret_cast<u64*>(out_off);
   if ((st = scan_exclusive<u64, OpAdd>(ctx, S, rlen, n, doff, doff + n))) return st;
-  u32 hb = 0;
+  u32 hb = 0, hpb = 0;
   {
     LandList l;
     l.add(doff + n, &hs[1], sizeof(u64));
     l.add(bad, &hb, sizeof(u32));
+    if (pre_bad) l.add(pre_bad, &hpb, sizeof(u32));
     if ((st = land_words(ctx, l))) return st;
   }
-  if (hb) return EVM_EINVAL;  // (an owner out of range, or an id in no segment)
+  if (hb || hpb) return EVM_EINVAL;  // (an owner out of range, or an id in no segment)
   *total = hs[1];
   uint8_t* out = out_for(hs[1]);
   if (!out) return EVM_OK;
