@@ -1981,6 +1981,26 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_scan(StoreView st, u32 n
   if (threadIdx.x == 0) range[0] = cand_owner(cpos, 0, n_owners, j0);
   if (threadIdx.x == 1) range[1] = cand_owner(cpos, 0, n_owners, j1) + 1;
   __syncthreads();
+  // the tile's owners' candidate starts staged in LDS: each candidate's owner
+  // search runs there instead of as a chain of dependent global loads (a
+  // tile spanning more owners than it has candidates searches in place)
+  __shared__ u32 s_cpos[SEL_TILE + 1];
+  const u32 r0 = range[0], nr = range[1] - range[0];
+  const bool staged = nr <= SEL_TILE;
+  if (staged)
+    for (u32 x = threadIdx.x; x <= nr; x += SEL_THREADS) s_cpos[x] = cpos[r0 + x];
+  __syncthreads();
+  auto owner_of = [&](u32 j) -> u32 {
+    if (!staged) return cand_owner(cpos, r0, range[1], j);
+    u32 lo = 0, hi = nr;  // invariant: s_cpos[lo] <= j < s_cpos[hi]
+    while (lo + 1 < hi) {
+      const u32 mid = (lo + hi) >> 1;
+      if (s_cpos[mid] <= j) lo = mid;
+      else hi = mid;
+    }
+    return r0 + lo;
+  };
+  auto start_of = [&](u32 o) -> u32 { return staged ? s_cpos[o - r0] : cpos[o]; };
   const u64 lt = lanemask_lt();
   u32 own[SEL_ITEMS], rk[SEL_ITEMS];
   u64 kk[SEL_ITEMS];
@@ -1992,8 +2012,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_scan(StoreView st, u32 n
     own[r] = 0;
     kk[r] = 0;
     if (j <= j1) {
-      const u32 o = cand_owner(cpos, range[0], range[1], j);
-      const size_t k = first[o] + (j - cpos[o]);
+      const u32 o = owner_of(j);
+      const size_t k = first[o] + (j - start_of(o));
       own[r] = o;
       kk[r] = k;
       keep = node_hex_of(st.hi[k], st.lo[k]) != req[o];
@@ -2032,7 +2052,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sv_sel_scan(StoreView st, u32 n
     const u32 j = j0 + r * SEL_THREADS + threadIdx.x;
     if (j > j1) continue;
     const u64 q = excl + before[r] + rk[r];
-    if (j == cpos[own[r]]) kst[j] = (u32)q;  // the owner's first candidate: its selection offset
+    if (j == start_of(own[r])) kst[j] = (u32)q;  // the owner's first candidate: its selection offset
     if (!((keepm >> r) & 1u) || q >= cap) continue;
     const size_t k = kk[r];
     sel_id[q] = id[k];
