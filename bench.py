@@ -1940,17 +1940,21 @@ def reingest(eng, a, ts1, own1, owners, per_owner, request, flags):
     for k in range(3):
         t_d, o_d, _ = gen.source(0xE7040000 + k, owners, per_owner, 1, 0, ts2.device)
         rounds.append((t_d, o_d))
-    st = eng.store_new(owners)
-    st.ingest(ts1, own1, 0, flags=flags)
-    round_ms = []
-    for k, (tsk, owk) in enumerate(rounds):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        st.ingest(tsk, owk, (k + 1) << 40, flags=f2)
-        torch.cuda.synchronize()
-        round_ms.append((time.perf_counter() - t0) * 1e3)
-    stored_rounds = int(st.n_messages)
-    st.free()
+    # (twice: the first pass grows the memory pool to the largest store, as a
+    # server's earlier rounds would have -- a timed round that first has to
+    # map ~13 GB of new device memory measured the driver, up to 250 ms)
+    for rep in range(2):
+        st = eng.store_new(owners)
+        st.ingest(ts1, own1, 0, flags=flags)
+        round_ms = []
+        for k, (tsk, owk) in enumerate(rounds):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            st.ingest(tsk, owk, (k + 1) << 40, flags=f2)
+            torch.cuda.synchronize()
+            round_ms.append((time.perf_counter() - t0) * 1e3)
+        stored_rounds = int(st.n_messages)
+        st.free()
     del rounds
     return {"workload": "a second round of %d msgs (%d owners, new timestamps) into a store holding %d rows: "
                         "addMessages with the stored rows and trees merged" % (n, owners, ts1.shape[0]),
